@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Headline benchmark: tokens/sec of the Llama-3-8B training task (BASELINE.json metric).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched under
+``torch.distributed.run`` with one rank per GPU (RCCL over xGMI).  W untimed warmup steps, then
+exactly K timed steps bracketed by barrier + ``torch.cuda.synchronize()``; the elapsed time is the
+MAX over ranks; rank 0 prints one JSON line.  Every timed step is a full training step: forward,
+backward, ZeRO-1 reduce-scatter, fused AdamW, all-gather.
+
+Weak scaling: each GPU processes ``--micro-batch`` × ``--seq-len`` tokens per step.
+Data: synthetic random token ids; weights: random init (no network, no checkpoints).
+
+The orchestration half of the metric (p50 cold start of a task via ``dstack apply``) is measured
+by ``bench_coldstart.py``; when ``--coldstart`` is given (N=1 only, default off) its p50 is
+included in the JSON line as ``cold_start_p50_s``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "p50 job cold-start (s) + tokens/sec of 8-GPU Llama-3-8B task via dstack apply"
+BASELINE_VALUE = None  # BASELINE.json "published": {} — the reference publishes no number
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--seq-len", type=int, default=8192)
+    ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--coldstart", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    cold = None
+    if args.coldstart and world == 1:
+        from bench_coldstart import measure_cold_start
+
+        cold = measure_cold_start(runs=5)
+
+    from dstack_amd.workloads.train_llama import run
+
+    env, tr, res = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup, log_every=0)
+    if env.rank == 0:
+        import torch
+
+        out = {
+            "metric": METRIC,
+            "value": round(res["tokens_per_s"], 2),
+            "unit": "tokens/s",
+            "n_gpus": env.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(res["ms_per_step"], 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (res["tokens_per_s"] / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform random token ids), random-init weights",
+            "config": {
+                "model": "Llama-3-8B" if args.model == "llama-3-8b" else args.model,
+                "global_batch": args.micro_batch * env.world,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{env.world}" + ("-zero1" if env.world > 1 else ""),
+                "optimizer": "AdamW (fp32 master, fused HIP kernel)",
+            },
+            "tflops_per_gpu": round(res["tflops_per_gpu"], 1),
+            "final_loss": res["final_loss"],
+            "ops": os.environ.get("DSTACK_AMD_OPS", "hip"),
+            "attn": os.environ.get("DSTACK_AMD_ATTN", "hip"),
+            "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu",
+        }
+        if cold is not None:
+            out["cold_start_p50_s"] = cold["p50_s"]
+        print(json.dumps(out), flush=True)
+    if env.distributed:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

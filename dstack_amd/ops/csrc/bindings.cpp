@@ -1,0 +1,208 @@
+// PyTorch bindings for the dstack_amd HIP kernels. The kernels themselves (elementwise.hip,
+// flash_attn.hip) are plain HIP translation units with C launchers; this file only validates
+// tensors, allocates outputs and forwards the current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+hipError_t dsa_rmsnorm_fwd(const void*, const void*, const void*, void*, void*, float*, int, int, float,
+                           hipStream_t);
+int dsa_rmsnorm_bwd_grid(int rows);
+hipError_t dsa_rmsnorm_bwd(const void*, const void*, const void*, const float*, const void*, void*, float*,
+                           float*, int, int, hipStream_t);
+hipError_t dsa_swiglu_fwd(const void*, void*, int, int, hipStream_t);
+hipError_t dsa_swiglu_bwd(const void*, const void*, void*, int, int, hipStream_t);
+hipError_t dsa_rope_qkv(const void*, void*, const float*, const float*, int, int, int, int, int, int,
+                        hipStream_t);
+hipError_t dsa_ce_fwd(const void*, const int64_t*, float*, float*, int, int, hipStream_t);
+hipError_t dsa_ce_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, hipStream_t);
+hipError_t dsa_adamw(void*, const void*, float*, float*, float*, size_t, float, float, float, float, float,
+                     float, float, float, hipStream_t);
+hipError_t dsa_fa_fwd(const void*, void*, float*, int, int, int, int, int, float, int, hipStream_t);
+size_t dsa_fa_bwd_workspace(int, int, int);
+hipError_t dsa_fa_bwd(const void*, const void*, const void*, const float*, void*, void*, int, int, int, int,
+                      int, float, int, hipStream_t);
+}
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "dstack_amd kernel ", what, " failed: ", hipGetErrorString(e));
+}
+
+void check_bf16(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a ROCm tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+std::vector<torch::Tensor> rms_norm_fwd(torch::Tensor x, torch::Tensor w, double eps) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  const int rows = x.size(0), D = x.size(1);
+  auto y = torch::empty_like(x);
+  auto rstd = torch::empty({rows}, x.options().dtype(torch::kFloat32));
+  check(dsa_rmsnorm_fwd(x.data_ptr(), nullptr, w.data_ptr(), nullptr, y.data_ptr(), rstd.data_ptr<float>(),
+                        rows, D, (float)eps, stream()),
+        "rms_norm_fwd");
+  return {y, rstd};
+}
+
+std::vector<torch::Tensor> add_rms_norm_fwd(torch::Tensor x, torch::Tensor delta, torch::Tensor w, double eps) {
+  check_bf16(x, "x");
+  check_bf16(delta, "delta");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.sizes() == delta.sizes(), "x/delta shape mismatch");
+  const int rows = x.size(0), D = x.size(1);
+  auto h = torch::empty_like(x);
+  auto y = torch::empty_like(x);
+  auto rstd = torch::empty({rows}, x.options().dtype(torch::kFloat32));
+  check(dsa_rmsnorm_fwd(x.data_ptr(), delta.data_ptr(), w.data_ptr(), h.data_ptr(), y.data_ptr(),
+                        rstd.data_ptr<float>(), rows, D, (float)eps, stream()),
+        "add_rms_norm_fwd");
+  return {h, y, rstd};
+}
+
+std::vector<torch::Tensor> rms_norm_bwd(torch::Tensor dy, torch::Tensor h, torch::Tensor w, torch::Tensor rstd,
+                                        c10::optional<torch::Tensor> dres) {
+  check_bf16(dy, "dy");
+  check_bf16(h, "h");
+  check_bf16(w, "w");
+  const int rows = h.size(0), D = h.size(1);
+  const void* dres_ptr = nullptr;
+  if (dres.has_value()) {
+    check_bf16(*dres, "dres");
+    dres_ptr = dres->data_ptr();
+  }
+  auto dx = torch::empty_like(h);
+  const int grid = dsa_rmsnorm_bwd_grid(rows);
+  auto part = torch::empty({grid, D}, h.options().dtype(torch::kFloat32));
+  auto dw = torch::empty({D}, h.options().dtype(torch::kFloat32));
+  check(dsa_rmsnorm_bwd(dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dres_ptr,
+                        dx.data_ptr(), part.data_ptr<float>(), dw.data_ptr<float>(), rows, D, stream()),
+        "rms_norm_bwd");
+  return {dx, dw};
+}
+
+torch::Tensor swiglu_fwd(torch::Tensor gu) {
+  check_bf16(gu, "gu");
+  const int F = gu.size(-1) / 2;
+  const int rows = gu.numel() / gu.size(-1);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto out = torch::empty(sizes, gu.options());
+  check(dsa_swiglu_fwd(gu.data_ptr(), out.data_ptr(), rows, F, stream()), "swiglu_fwd");
+  return out;
+}
+
+torch::Tensor swiglu_bwd(torch::Tensor da, torch::Tensor gu) {
+  check_bf16(da, "da");
+  check_bf16(gu, "gu");
+  const int F = gu.size(-1) / 2;
+  const int rows = gu.numel() / gu.size(-1);
+  auto dgu = torch::empty_like(gu);
+  check(dsa_swiglu_bwd(da.data_ptr(), gu.data_ptr(), dgu.data_ptr(), rows, F, stream()), "swiglu_bwd");
+  return dgu;
+}
+
+torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, int64_t n_rot, int64_t head_dim,
+                       bool inverse) {
+  check_bf16(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, S, NH*D]");
+  TORCH_CHECK(cos.scalar_type() == torch::kFloat32 && sin.scalar_type() == torch::kFloat32, "cos/sin fp32");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous(), "cos/sin contiguous");
+  const int B = qkv.size(0), S = qkv.size(1);
+  const int NH = qkv.size(2) / head_dim;
+  TORCH_CHECK(cos.size(0) >= S && cos.size(1) == head_dim / 2, "rope table shape");
+  auto out = torch::empty_like(qkv);
+  check(dsa_rope_qkv(qkv.data_ptr(), out.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), B * S, S, NH,
+                     (int)n_rot, (int)head_dim, inverse ? 1 : 0, stream()),
+        "rope_qkv");
+  return out;
+}
+
+std::vector<torch::Tensor> cross_entropy_fwd(torch::Tensor logits, torch::Tensor target) {
+  check_bf16(logits, "logits");
+  TORCH_CHECK(target.scalar_type() == torch::kInt64 && target.is_contiguous(), "target int64");
+  const int rows = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V % 8 == 0, "vocab must be a multiple of 8");
+  auto loss = torch::empty({rows}, logits.options().dtype(torch::kFloat32));
+  auto lse = torch::empty({rows}, logits.options().dtype(torch::kFloat32));
+  check(dsa_ce_fwd(logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(),
+                   rows, V, stream()),
+        "cross_entropy_fwd");
+  return {loss, lse};
+}
+
+torch::Tensor cross_entropy_bwd(torch::Tensor logits, torch::Tensor target, torch::Tensor lse, torch::Tensor scale,
+                                bool inplace) {
+  check_bf16(logits, "logits");
+  const int rows = logits.size(0), V = logits.size(1);
+  auto out = inplace ? logits : torch::empty_like(logits);
+  check(dsa_ce_bwd(logits.data_ptr(), target.data_ptr<int64_t>(), lse.data_ptr<float>(), scale.data_ptr<float>(),
+                   out.data_ptr(), rows, V, stream()),
+        "cross_entropy_bwd");
+  return out;
+}
+
+void adamw(torch::Tensor param, torch::Tensor grad, torch::Tensor master, torch::Tensor m, torch::Tensor v,
+           double lr, double b1, double b2, double eps, double wd, double bc1, double bc2, double gscale) {
+  check_bf16(param, "param");
+  check_bf16(grad, "grad");
+  for (auto* t : {&master, &m, &v}) {
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->is_contiguous(), "adam state must be fp32 contiguous");
+    TORCH_CHECK(t->numel() == param.numel(), "adam state numel mismatch");
+  }
+  check(dsa_adamw(param.data_ptr(), grad.data_ptr(), master.data_ptr<float>(), m.data_ptr<float>(),
+                  v.data_ptr<float>(), param.numel(), lr, b1, b2, eps, wd, bc1, bc2, gscale, stream()),
+        "adamw");
+}
+
+std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor qkv, int64_t H, int64_t KVH, bool causal) {
+  check_bf16(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, S, (H+2KVH)*D]");
+  const int B = qkv.size(0), S = qkv.size(1);
+  const int D = qkv.size(2) / (H + 2 * KVH);
+  auto out = torch::empty({B, S, H * D}, qkv.options());
+  auto lse = torch::empty({B, H, S}, qkv.options().dtype(torch::kFloat32));
+  check(dsa_fa_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), B, S, H, KVH, D, 1.0f / std::sqrt((float)D),
+                   causal ? 1 : 0, stream()),
+        "flash_attn_fwd");
+  return {out, lse};
+}
+
+torch::Tensor flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H,
+                             int64_t KVH, bool causal) {
+  check_bf16(dout, "dout");
+  check_bf16(qkv, "qkv");
+  check_bf16(out, "out");
+  const int B = qkv.size(0), S = qkv.size(1);
+  const int D = qkv.size(2) / (H + 2 * KVH);
+  auto dqkv = torch::empty_like(qkv);
+  auto ws = torch::empty({(int64_t)dsa_fa_bwd_workspace(B, S, H)}, qkv.options().dtype(torch::kUInt8));
+  check(dsa_fa_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), dqkv.data_ptr(),
+                   ws.data_ptr(), B, S, H, KVH, D, 1.0f / std::sqrt((float)D), causal ? 1 : 0, stream()),
+        "flash_attn_bwd");
+  return dqkv;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "dstack_amd HIP/CDNA4 kernels (gfx950)";
+  m.def("rms_norm_fwd", &rms_norm_fwd);
+  m.def("add_rms_norm_fwd", &add_rms_norm_fwd);
+  m.def("rms_norm_bwd", &rms_norm_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope_qkv", &rope_qkv);
+  m.def("cross_entropy_fwd", &cross_entropy_fwd);
+  m.def("cross_entropy_bwd", &cross_entropy_bwd);
+  m.def("adamw", &adamw);
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
+}

@@ -1,0 +1,506 @@
+// Memory-bound fused ops for the Llama training step on MI355X (gfx950).
+//
+// Every kernel moves bf16 as 16-byte vectors (8 x bf16 per lane, one dwordx4 per lane per access,
+// 1 KiB per wave-instruction) and reduces rows inside ONE 64-lane wave with __shfl_xor, so no LDS
+// and no __syncthreads sit on the critical path. Grids are sized to keep >=4 waves per SIMD
+// resident across all 256 CUs.
+#include "common.h"
+
+using namespace dsa;
+
+// ------------------------------------------------------------------------------------------------
+// RMSNorm forward (optionally fused with the residual add h = x + delta).
+// One wave per row; the row stays in registers between the reduction and the normalisation.
+// ------------------------------------------------------------------------------------------------
+template <int NCH, bool ADD>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ delta,
+                                                          const bf16_t* __restrict__ w,
+                                                          bf16_t* __restrict__ h_out,
+                                                          bf16_t* __restrict__ y,
+                                                          float* __restrict__ rstd_out, int rows,
+                                                          int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = D >> 3;
+  const size_t base = (size_t)row * D;
+  float v[NCH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      us8 a = *reinterpret_cast<const us8*>(x + base + ch * 8);
+      unpack8(a, v[c]);
+      if constexpr (ADD) {
+        float d[8];
+        unpack8(*reinterpret_cast<const us8*>(delta + base + ch * 8), d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] = bf2f(f2bf(v[c][i] + d[i]));  // h is stored in bf16
+        *reinterpret_cast<us8*>(h_out + base + ch * 8) = pack8(v[c]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      float wv[8], o[8];
+      unpack8(*reinterpret_cast<const us8*>(w + ch * 8), wv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = v[c][i] * r * wv[i];
+      *reinterpret_cast<us8*>(y + base + ch * 8) = pack8(o);
+    }
+  }
+  if (lane == 0) rstd_out[row] = r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// RMSNorm backward: dx = r*g - h*r^3*mean(g*h) (+ dres), g = dy*w ;  dw partials per block.
+// Grid-strided over rows so each wave accumulates its dw contribution in registers; the block's
+// waves combine through LDS and write one fp32 partial row per block, reduced by colsum below.
+// ------------------------------------------------------------------------------------------------
+template <int NCH, bool RES>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                          const bf16_t* __restrict__ h,
+                                                          const bf16_t* __restrict__ w,
+                                                          const float* __restrict__ rstd,
+                                                          const bf16_t* __restrict__ dres,
+                                                          bf16_t* __restrict__ dx,
+                                                          float* __restrict__ dw_part, int rows,
+                                                          int D) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  const int nch = D >> 3;
+  float wv[NCH][8];
+  float dwa[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = lane + c * 64;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dwa[c][i] = 0.f;
+    if (ch < nch) unpack8(*reinterpret_cast<const us8*>(w + ch * 8), wv[c]);
+  }
+  for (int row = blockIdx.x * nw + wid; row < rows; row += gridDim.x * nw) {
+    const size_t base = (size_t)row * D;
+    const float r = rstd[row];
+    float hv[NCH][8], g[NCH][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        float d[8];
+        unpack8(*reinterpret_cast<const us8*>(dy + base + ch * 8), d);
+        unpack8(*reinterpret_cast<const us8*>(h + base + ch * 8), hv[c]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          g[c][i] = d[i] * wv[c][i];
+          dot += g[c][i] * hv[c][i];
+          dwa[c][i] += d[i] * hv[c][i] * r;
+        }
+      }
+    }
+    dot = wave_sum(dot);
+    const float k = dot * r * r * r / (float)D;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        float o[8];
+        if constexpr (RES) {
+          unpack8(*reinterpret_cast<const us8*>(dres + base + ch * 8), o);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += r * g[c][i] - hv[c][i] * k;
+        *reinterpret_cast<us8*>(dx + base + ch * 8) = pack8(o);
+      }
+    }
+  }
+  // combine the waves' dw partials: wave 0 writes, others add (LDS holds D floats)
+  for (int wv_i = 0; wv_i < nw; ++wv_i) {
+    if (wid == wv_i) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nch) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if (wv_i == 0)
+              lds[ch * 8 + i] = dwa[c][i];
+            else
+              lds[ch * 8 + i] += dwa[c][i];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < D; i += blockDim.x) dw_part[(size_t)blockIdx.x * D + i] = lds[i];
+}
+
+// column sums of a [P, D] fp32 matrix -> out[D] (fp32)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part,
+                                                     float* __restrict__ out, int P, int D) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= D) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(size_t)p * D + col];
+  out[col] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// SwiGLU on [T, 2F] = [gate | up]  ->  [T, F]
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
+
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu,
+                                                         bf16_t* __restrict__ out, int rows,
+                                                         int F) {
+  const int nch = F >> 3;
+  const size_t total = (size_t)rows * nch;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t row = i / nch, ch = i % nch;
+    float g[8], u[8], o[8];
+    unpack8(*reinterpret_cast<const us8*>(gu + row * 2 * F + ch * 8), g);
+    unpack8(*reinterpret_cast<const us8*>(gu + row * 2 * F + F + ch * 8), u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = silu_f(g[k]) * u[k];
+    *reinterpret_cast<us8*>(out + row * F + ch * 8) = pack8(o);
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ da,
+                                                         const bf16_t* __restrict__ gu,
+                                                         bf16_t* __restrict__ dgu, int rows,
+                                                         int F) {
+  const int nch = F >> 3;
+  const size_t total = (size_t)rows * nch;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t row = i / nch, ch = i % nch;
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(*reinterpret_cast<const us8*>(gu + row * 2 * F + ch * 8), g);
+    unpack8(*reinterpret_cast<const us8*>(gu + row * 2 * F + F + ch * 8), u);
+    unpack8(*reinterpret_cast<const us8*>(da + row * F + ch * 8), d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float s = 1.f / (1.f + __expf(-g[k]));
+      du[k] = d[k] * g[k] * s;
+      dg[k] = d[k] * u[k] * s * (1.f + g[k] * (1.f - s));
+    }
+    *reinterpret_cast<us8*>(dgu + row * 2 * F + ch * 8) = pack8(dg);
+    *reinterpret_cast<us8*>(dgu + row * 2 * F + F + ch * 8) = pack8(du);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// RoPE (rotate-half) over the first n_rot heads of a fused qkv row [NH*D]; other heads copied.
+// cos/sin tables [S, D/2] fp32 are precomputed on the host (no on-device trig).
+// Each lane owns 8 consecutive pairs (i, i + D/2) of one head.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rope_qkv_kernel(const bf16_t* __restrict__ in,
+                                                       bf16_t* __restrict__ out,
+                                                       const float* __restrict__ cosT,
+                                                       const float* __restrict__ sinT, int rows,
+                                                       int S, int NH, int n_rot, int D,
+                                                       float sign) {
+  const int half = D >> 1;
+  const int cph = half >> 3;  // 8-pair chunks per head
+  const size_t per_row = (size_t)NH * cph;
+  const size_t total = (size_t)rows * per_row;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t row = i / per_row;
+    const int rem = (int)(i % per_row);
+    const int head = rem / cph, c = rem % cph;
+    const size_t off = row * (size_t)NH * D + (size_t)head * D + c * 8;
+    us8 a = *reinterpret_cast<const us8*>(in + off);
+    us8 b = *reinterpret_cast<const us8*>(in + off + half);
+    if (head < n_rot) {
+      const int pos = (int)(row % S);
+      const f4* cp = reinterpret_cast<const f4*>(cosT + (size_t)pos * half + c * 8);
+      const f4* sp = reinterpret_cast<const f4*>(sinT + (size_t)pos * half + c * 8);
+      const f4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+      const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      float x1[8], x2[8], o1[8], o2[8];
+      unpack8(a, x1);
+      unpack8(b, x2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float s = sign * sn[k];
+        o1[k] = x1[k] * cs[k] - x2[k] * s;
+        o2[k] = x2[k] * cs[k] + x1[k] * s;
+      }
+      a = pack8(o1);
+      b = pack8(o2);
+    }
+    *reinterpret_cast<us8*>(out + off) = a;
+    *reinterpret_cast<us8*>(out + off + half) = b;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Softmax cross-entropy over a [T, V] bf16 logits matrix. One 256-thread block per row.
+// fwd: online (max, sum-exp) per lane -> block combine -> lse, loss = lse - logit[target].
+// bwd: dlogit = scale * (exp(logit - lse) - onehot), written in place over the logits.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mn));
+  m = mn;
+}
+
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ logits,
+                                                     const int64_t* __restrict__ target,
+                                                     float* __restrict__ loss,
+                                                     float* __restrict__ lse_out, int V) {
+  __shared__ float sm[8], ss[8];
+  const size_t row = blockIdx.x;
+  const bf16_t* L = logits + row * (size_t)V;
+  float m = -INFINITY, s = 0.f;
+  const int nch = V >> 3;
+  for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {
+    float v[8];
+    unpack8(*reinterpret_cast<const us8*>(L + ch * 8), v);
+    float lm = v[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) lm = fmaxf(lm, v[k]);
+    float ls = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ls += __expf(v[k] - lm);
+    online_merge(m, s, lm, ls);
+  }
+  for (int i = (nch << 3) + threadIdx.x; i < V; i += blockDim.x) online_merge(m, s, bf2f(L[i]), 1.f);
+  // wave combine
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    online_merge(m, s, m2, s2);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[wid] = m;
+    ss[wid] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) online_merge(m, s, sm[w], ss[w]);
+    const float lse = m + __logf(s);
+    lse_out[row] = lse;
+    const int64_t t = target[row];
+    loss[row] = (t >= 0 && t < V) ? lse - bf2f(L[t]) : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ logits,
+                                                     const int64_t* __restrict__ target,
+                                                     const float* __restrict__ lse,
+                                                     const float* __restrict__ scale_ptr,
+                                                     bf16_t* __restrict__ dlogits, int V) {
+  const size_t row = blockIdx.x;
+  const float l = lse[row];
+  const float scale = scale_ptr[0];
+  const int64_t t = target[row];
+  const bf16_t* L = logits + row * (size_t)V;
+  bf16_t* G = dlogits + row * (size_t)V;
+  const int nch = V >> 3;
+  for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {
+    float v[8];
+    unpack8(*reinterpret_cast<const us8*>(L + ch * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = __expf(v[k] - l);
+      if (ch * 8 + k == t) v[k] -= 1.f;
+      v[k] *= scale;
+    }
+    *reinterpret_cast<us8*>(G + ch * 8) = pack8(v);
+  }
+  for (int i = (nch << 3) + threadIdx.x; i < V; i += blockDim.x) {
+    float p = __expf(bf2f(L[i]) - l);
+    if (i == t) p -= 1.f;
+    G[i] = f2bf(p * scale);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused AdamW over flat shards: bf16 param/grad, fp32 master/m/v (decoupled weight decay).
+// 8 elements per lane per iteration: one dwordx4 for param/grad, two for each fp32 stream.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adamw_kernel(bf16_t* __restrict__ param,
+                                                    const bf16_t* __restrict__ grad,
+                                                    float* __restrict__ master,
+                                                    float* __restrict__ mom,
+                                                    float* __restrict__ var, size_t n, float lr,
+                                                    float b1, float b2, float eps, float wd,
+                                                    float bc1, float bc2, float gscale) {
+  const size_t nv = n >> 3;
+  const float step_size = lr / bc1;
+  const float inv_bc2_sqrt = rsqrtf(bc2);
+  const float decay = 1.f - lr * wd;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float g[8];
+    unpack8(*reinterpret_cast<const us8*>(grad + i * 8), g);
+    f4* mp = reinterpret_cast<f4*>(master + i * 8);
+    f4* m1 = reinterpret_cast<f4*>(mom + i * 8);
+    f4* m2 = reinterpret_cast<f4*>(var + i * 8);
+    f4 p0 = mp[0], p1 = mp[1], a0 = m1[0], a1 = m1[1], v0 = m2[0], v1 = m2[1];
+    float p[8] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
+    float a[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gg = g[k] * gscale;
+      a[k] = b1 * a[k] + (1.f - b1) * gg;
+      v[k] = b2 * v[k] + (1.f - b2) * gg * gg;
+      const float denom = sqrtf(v[k]) * inv_bc2_sqrt + eps;
+      p[k] = p[k] * decay - step_size * a[k] / denom;
+    }
+    mp[0] = f4{p[0], p[1], p[2], p[3]};
+    mp[1] = f4{p[4], p[5], p[6], p[7]};
+    m1[0] = f4{a[0], a[1], a[2], a[3]};
+    m1[1] = f4{a[4], a[5], a[6], a[7]};
+    m2[0] = f4{v[0], v[1], v[2], v[3]};
+    m2[1] = f4{v[4], v[5], v[6], v[7]};
+    *reinterpret_cast<us8*>(param + i * 8) = pack8(p);
+  }
+  // scalar tail (n % 8)
+  for (size_t i = (nv << 3) + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const float gg = bf2f(grad[i]) * gscale;
+    const float a = b1 * mom[i] + (1.f - b1) * gg;
+    const float v = b2 * var[i] + (1.f - b2) * gg * gg;
+    const float p = master[i] * decay - step_size * a / (sqrtf(v) * inv_bc2_sqrt + eps);
+    mom[i] = a;
+    var[i] = v;
+    master[i] = p;
+    param[i] = f2bf(p);
+  }
+}
+
+// ================================================================================================
+// host launchers (raw pointers + stream; the torch binding lives in bindings.cpp)
+// ================================================================================================
+static inline int grid_for(size_t work, int block, int cap = 256 * 16) {
+  size_t g = (work + block - 1) / block;
+  if (g > (size_t)cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+#define NCH_DISPATCH(D, ...)                       \
+  do {                                             \
+    const int _n = ((D) / 8 + 63) / 64;            \
+    if (_n <= 1) { constexpr int NCH = 1; __VA_ARGS__; }        \
+    else if (_n <= 2) { constexpr int NCH = 2; __VA_ARGS__; }   \
+    else if (_n <= 4) { constexpr int NCH = 4; __VA_ARGS__; }   \
+    else if (_n <= 8) { constexpr int NCH = 8; __VA_ARGS__; }   \
+    else if (_n <= 16) { constexpr int NCH = 16; __VA_ARGS__; } \
+    else return hipErrorInvalidValue;              \
+  } while (0)
+
+extern "C" hipError_t dsa_rmsnorm_fwd(const void* x, const void* delta, const void* w, void* h_out,
+                                      void* y, float* rstd, int rows, int D, float eps,
+                                      hipStream_t st) {
+  if (D % 8) return hipErrorInvalidValue;
+  const int block = 256, rpb = block / 64;
+  const int grid = (rows + rpb - 1) / rpb;
+  if (delta) {
+    NCH_DISPATCH(D, rmsnorm_fwd_kernel<NCH, true><<<grid, block, 0, st>>>(
+        (const bf16_t*)x, (const bf16_t*)delta, (const bf16_t*)w, (bf16_t*)h_out, (bf16_t*)y, rstd,
+        rows, D, eps));
+  } else {
+    NCH_DISPATCH(D, rmsnorm_fwd_kernel<NCH, false><<<grid, block, 0, st>>>(
+        (const bf16_t*)x, nullptr, (const bf16_t*)w, nullptr, (bf16_t*)y, rstd, rows, D, eps));
+  }
+  return hipGetLastError();
+}
+
+// dw_part must hold grid*D floats where grid = dsa_rmsnorm_bwd_grid(rows)
+extern "C" int dsa_rmsnorm_bwd_grid(int rows) {
+  int g = (rows + 3) / 4;
+  return g > 1024 ? 1024 : (g < 1 ? 1 : g);
+}
+
+extern "C" hipError_t dsa_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* rstd,
+                                      const void* dres, void* dx, float* dw_part, float* dw,
+                                      int rows, int D, hipStream_t st) {
+  if (D % 8) return hipErrorInvalidValue;
+  const int block = 256;
+  const int grid = dsa_rmsnorm_bwd_grid(rows);
+  const size_t lds = (size_t)D * sizeof(float);
+  if (dres) {
+    NCH_DISPATCH(D, rmsnorm_bwd_kernel<NCH, true><<<grid, block, lds, st>>>(
+        (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)w, rstd, (const bf16_t*)dres,
+        (bf16_t*)dx, dw_part, rows, D));
+  } else {
+    NCH_DISPATCH(D, rmsnorm_bwd_kernel<NCH, false><<<grid, block, lds, st>>>(
+        (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)w, rstd, nullptr, (bf16_t*)dx, dw_part,
+        rows, D));
+  }
+  DSA_CHECK(hipGetLastError());
+  colsum_kernel<<<(D + 255) / 256, 256, 0, st>>>(dw_part, dw, grid, D);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_swiglu_fwd(const void* gu, void* out, int rows, int F, hipStream_t st) {
+  if (F % 8) return hipErrorInvalidValue;
+  const size_t work = (size_t)rows * (F / 8);
+  swiglu_fwd_kernel<<<grid_for(work, 256), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)out, rows, F);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_swiglu_bwd(const void* da, const void* gu, void* dgu, int rows, int F,
+                                     hipStream_t st) {
+  if (F % 8) return hipErrorInvalidValue;
+  const size_t work = (size_t)rows * (F / 8);
+  swiglu_bwd_kernel<<<grid_for(work, 256), 256, 0, st>>>((const bf16_t*)da, (const bf16_t*)gu,
+                                                         (bf16_t*)dgu, rows, F);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_rope_qkv(const void* in, void* out, const float* cosT, const float* sinT,
+                                   int rows, int S, int NH, int n_rot, int D, int inverse,
+                                   hipStream_t st) {
+  if (D % 16) return hipErrorInvalidValue;
+  const size_t work = (size_t)rows * NH * (D / 16);
+  rope_qkv_kernel<<<grid_for(work, 256), 256, 0, st>>>((const bf16_t*)in, (bf16_t*)out, cosT, sinT,
+                                                       rows, S, NH, n_rot, D,
+                                                       inverse ? -1.f : 1.f);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_ce_fwd(const void* logits, const int64_t* target, float* loss, float* lse,
+                                 int rows, int V, hipStream_t st) {
+  ce_fwd_kernel<<<rows, 256, 0, st>>>((const bf16_t*)logits, target, loss, lse, V);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_ce_bwd(const void* logits, const int64_t* target, const float* lse,
+                                 const float* scale, void* dlogits, int rows, int V,
+                                 hipStream_t st) {
+  ce_bwd_kernel<<<rows, 256, 0, st>>>((const bf16_t*)logits, target, lse, scale, (bf16_t*)dlogits,
+                                      V);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_adamw(void* param, const void* grad, float* master, float* m, float* v,
+                                size_t n, float lr, float b1, float b2, float eps, float wd,
+                                float bc1, float bc2, float gscale, hipStream_t st) {
+  adamw_kernel<<<grid_for(n / 8 + 1, 256, 256 * 8), 256, 0, st>>>(
+      (bf16_t*)param, (const bf16_t*)grad, master, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
+  return hipGetLastError();
+}

@@ -1,0 +1,560 @@
+// Causal GQA flash attention (forward + backward) for CDNA4 / gfx950, head_dim 128, bf16.
+//
+// Layout: the kernels read q, k and v straight out of the fused projection output
+// qkv[B, S, (H + 2*KVH) * 128] (row stride = (H + 2*KVH)*128 elements), so the model never
+// transposes or splits qkv.  Output o is [B, S, H*128]; lse/delta are fp32 [B, H, S] in the log2
+// domain of the scaled scores.
+//
+// Structure (one workgroup = 4 waves, each wave owns 32 rows of the 32x32x16 bf16 MFMA):
+//  * K/V (and Q/dO in the dK/dV pass) tiles are staged HBM -> LDS by global_load_lds (LDS-DMA,
+//    16 B/lane, no staging VGPRs) into a 2-deep ring; the next tile's DMA is in flight while the
+//    current tile computes, one barrier per tile.
+//  * LDS image: 256-byte rows with a 16-byte-chunk XOR  ch ^ (((row&3)<<2)|((row>>2)&3)) — conflict-
+//    free both for ds_read_b128 row reads (MFMA operands with d contiguous) and for
+//    ds_read_b64_tr_b16 transposed reads (operands with the key/query index contiguous).  LDS-DMA
+//    writes lane-linearly, so the swizzle is applied to the per-lane SOURCE address.
+//  * "key on the row" orientation: forward computes S^T = K·Q^T so a lane owns one query and the
+//    softmax row max / sum are in-register (+1 xor-32 shuffle); the S^T accumulator is directly the
+//    B operand of O^T += V^T·P^T (no LDS round trip for P).  The backward dK/dV pass uses
+//    "key on the lane" (S = Q·K^T) so P and dS feed dV^T/dK^T directly; the dQ pass uses the
+//    forward orientation and feeds dS^T as the A operand of dQ = dS·K.  dQ is computed by its own
+//    q-major pass instead of cross-workgroup atomics (deterministic, no atomic-rate floor).
+#include "common.h"
+
+using namespace dsa;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS3(T, p) ((__attribute__((address_space(3))) T*)(p))
+#define GLB1(T, p) ((__attribute__((address_space(1))) T*)(p))
+
+namespace {
+
+constexpr int HD = 128;          // head dim
+constexpr int TILE_BYTES = 64 * 256;  // 64 rows x 128 bf16
+
+__device__ __forceinline__ int swz(int row, int ch) {
+  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 lds_row(const char* base, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(base + swz(row, ch));
+}
+
+// A-operand fragment of X^T where X is a [rows][128] tile in LDS read by columns:
+// element j of lane-half h = X[16*ks + 8*(j>>2) + 4*h + (j&3)][col0 + (lane&31)]  (the k order of
+// an MFMA accumulator used as the other operand).  Two ds_read_b64_tr_b16 per fragment.
+__device__ __forceinline__ bf16x8 lds_tr(const char* base, int row_base, int col0, int lane) {
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int r0 = row_base + 4 * (g >> 1) + q4;
+  const int c0 = (col0 >> 3) + 2 * (g & 1) + (p4 >> 1);
+  const int sub = 8 * (p4 & 1);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(bf16x4, base + swz(r0, c0) + sub));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(bf16x4, base + swz(r0 + 8, c0) + sub));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Issue LDS-DMA of a [64 x 128] bf16 tile (rows row0.., row stride `stride` elements) into the
+// swizzled LDS image at `lds`.  4 waves x 4 wave-instructions of 1 KiB (4 rows each).
+__device__ __forceinline__ void dma_tile64(const bf16_t* g, long stride, char* lds, int wave,
+                                           int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    const int row = piece * 4 + (lane >> 4);
+    const int pc = lane & 15;
+    const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    const bf16_t* src = g + (long)row * stride + ch * 8;
+    __builtin_amdgcn_global_load_lds(GLB1(void, src), LDS3(void, lds + piece * 1024), 16, 0, 0);
+  }
+}
+
+// 64 contiguous floats -> LDS (one wave-instruction, 4 B/lane)
+__device__ __forceinline__ void dma_f32x64(const float* g, char* lds, int lane) {
+  __builtin_amdgcn_global_load_lds(GLB1(void, g + lane), LDS3(void, lds), 4, 0, 0);
+}
+
+__device__ __forceinline__ void wait_dma_and_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+__device__ __forceinline__ bf16x8 to_bf16x8(const f32x16& acc, int base) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(acc[base + j]);
+  return r;
+}
+
+}  // namespace
+
+// ================================================================================================
+// Forward
+// ================================================================================================
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
+                                                        bf16_t* __restrict__ out,
+                                                        float* __restrict__ lse, int B, int S,
+                                                        int H, int KVH, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
+  const int NH = H + 2 * KVH;
+  const long rs = (long)NH * HD;  // row stride
+  const int nqb = S / 128;
+  const int bid = blockIdx.x;
+  const int qb = CAUSAL ? nqb - 1 - bid / (B * H) : bid / (B * H);  // heaviest blocks first
+  const int bh = bid % (B * H);
+  const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
+  const bf16_t* base = qkv + (long)b * S * rs;
+  const bf16_t* qp = base + hh * HD;
+  const bf16_t* kp = base + (H + kvh) * HD;
+  const bf16_t* vp = base + (H + KVH + kvh) * HD;
+  const int q0 = qb * 128, qw0 = q0 + 32 * w, myq = qw0 + l32;
+
+  bf16x8 qf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+    qf[ks] = *reinterpret_cast<const bf16x8*>(qp + (long)myq * rs + 16 * ks + 8 * hf);
+
+  f32x16 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m = -INFINITY, lsum = 0.f;
+  const int nkv = CAUSAL ? (q0 + 128) / 64 : S / 64;
+
+  dma_tile64(kp, rs, smem, w, lane);
+  dma_tile64(vp, rs, smem + TILE_BYTES, w, lane);
+  wait_dma_and_barrier();
+
+  for (int it = 0; it < nkv; ++it) {
+    const char* kl = smem + (it & 1) * 2 * TILE_BYTES;
+    const char* vl = kl + TILE_BYTES;
+    if (it + 1 < nkv) {
+      char* nk = smem + ((it + 1) & 1) * 2 * TILE_BYTES;
+      dma_tile64(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
+      dma_tile64(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
+    }
+    const int kv0 = it * 64;
+    if (!CAUSAL || kv0 <= qw0 + 31) {
+      f32x16 st[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[t][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) st[t] = mfma(lds_row(kl, 32 * t + l32, 2 * ks + hf), qf[ks], st[t]);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float s = st[t][r] * scale_log2;
+          if (CAUSAL) {
+            const int key = kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            if (key > myq) s = -INFINITY;
+          }
+          st[t][r] = s;
+          mx = fmaxf(mx, s);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float alpha = exp2f(m - mn);
+      m = mn;
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(st[t][r] - mn);
+          st[t][r] = p;
+          ps += p;
+        }
+      lsum = lsum * alpha + ps;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      bf16x8 pb[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) pb[s4] = to_bf16x8(st[s4 >> 1], 8 * (s4 & 1));
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) o[d] = mfma(lds_tr(vl, 16 * s4, 32 * d, lane), pb[s4], o[d]);
+    }
+    wait_dma_and_barrier();
+  }
+
+  lsum += __shfl_xor(lsum, 32, 64);
+  const float inv = 1.f / lsum;
+  bf16_t* op = out + ((long)b * S + myq) * H * HD + hh * HD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int dd = 32 * d + 8 * rr + 4 * hf;
+      typedef unsigned short us4 __attribute__((ext_vector_type(4)));
+      us4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = f2bf(o[d][4 * rr + i] * inv);
+      *reinterpret_cast<us4*>(op + dd) = v;
+    }
+  if (hf == 0) lse[((long)b * H + hh) * S + myq] = m + log2f(lsum);
+}
+
+// ================================================================================================
+// Backward preprocess: delta = rowsum(dO * O) (fp32, [B, H, S]); 16 lanes per (b, s, h) row.
+// ================================================================================================
+__global__ __launch_bounds__(256) void fa_bwd_delta_kernel(const bf16_t* __restrict__ o,
+                                                           const bf16_t* __restrict__ dout,
+                                                           float* __restrict__ delta, int B, int S,
+                                                           int H) {
+  const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int sub = threadIdx.x & 15;
+  const long rows = (long)B * S * H;
+  float acc = 0.f;
+  if (row < rows) {
+    float a[8], g[8];
+    unpack8(*reinterpret_cast<const us8*>(o + row * HD + sub * 8), a);
+    unpack8(*reinterpret_cast<const us8*>(dout + row * HD + sub * 8), g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += a[i] * g[i];
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (row < rows && sub == 0) {
+    const long bs = row / H;
+    const int hh = (int)(row % H);
+    const long b = bs / S, s = bs % S;
+    delta[(b * H + hh) * S + s] = acc;
+  }
+}
+
+// ================================================================================================
+// Backward dK/dV pass: workgroup = 128 keys of one (b, q-head); wave w owns keys kb0 + 32w.
+// Loops over 64-row q tiles from the diagonal to S; writes fp32 per-q-head partials
+// dkp/dvp [B, S, H, 128] that fa_bwd_reduce_kv sums over the GQA group.
+// ================================================================================================
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
+    int H, int KVH, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // per stage: Q tile (16K) | dO tile (16K) | lse (256 B) | delta (256 B)
+  constexpr int STAGE = 2 * TILE_BYTES + 512;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
+  const int NH = H + 2 * KVH;
+  const long rs = (long)NH * HD;
+  const long ors = (long)H * HD;
+  const int bid = blockIdx.x;
+  const int kb = bid / (B * H);  // small kb = most q tiles: heaviest first
+  const int bh = bid % (B * H);
+  const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
+  const bf16_t* base = qkv + (long)b * S * rs;
+  const bf16_t* qp = base + hh * HD;
+  const bf16_t* kp = base + (H + kvh) * HD;
+  const bf16_t* vp = base + (H + KVH + kvh) * HD;
+  const bf16_t* dop = dout + (long)b * S * ors + hh * HD;
+  const float* lp = lse + ((long)b * H + hh) * S;
+  const float* dp = delta + ((long)b * H + hh) * S;
+  const int kb0 = kb * 128, kw0 = kb0 + 32 * w, mykey = kw0 + l32;
+
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    kf[ks] = *reinterpret_cast<const bf16x8*>(kp + (long)mykey * rs + 16 * ks + 8 * hf);
+    vf[ks] = *reinterpret_cast<const bf16x8*>(vp + (long)mykey * rs + 16 * ks + 8 * hf);
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dk[d][r] = 0.f;
+      dv[d][r] = 0.f;
+    }
+
+  const int qt_begin = CAUSAL ? kb0 / 64 : 0;
+  const int nqt = S / 64;
+  auto issue = [&](int qt, char* st) {
+    dma_tile64(qp + (long)qt * 64 * rs, rs, st, w, lane);
+    dma_tile64(dop + (long)qt * 64 * ors, ors, st + TILE_BYTES, w, lane);
+    if (w == 0) dma_f32x64(lp + qt * 64, st + 2 * TILE_BYTES, lane);
+    if (w == 1) dma_f32x64(dp + qt * 64, st + 2 * TILE_BYTES + 256, lane);
+  };
+  issue(qt_begin, smem);
+  wait_dma_and_barrier();
+
+  for (int qt = qt_begin; qt < nqt; ++qt) {
+    const int stage = (qt - qt_begin) & 1;
+    const char* ql = smem + stage * STAGE;
+    const char* dol = ql + TILE_BYTES;
+    const float* ll = reinterpret_cast<const float*>(ql + 2 * TILE_BYTES);
+    const float* dl = ll + 64;
+    if (qt + 1 < nqt) issue(qt + 1, smem + (stage ^ 1) * STAGE);
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qlo = qt * 64 + 32 * qs;
+      if (CAUSAL && qlo + 31 < kw0) continue;  // every query of this sub-tile precedes my keys
+      f32x16 s, dpv;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] = 0.f;
+        dpv[r] = 0.f;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        s = mfma(lds_row(ql, 32 * qs + l32, 2 * ks + hf), kf[ks], s);
+        dpv = mfma(lds_row(dol, 32 * qs + l32, 2 * ks + hf), vf[ks], dpv);
+      }
+      // rows of s/dpv: q = qlo + (r&3) + 8*(r>>2) + 4*hf ; column (lane) = mykey
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int qi = 32 * qs + 8 * rr + 4 * hf;
+        const f4 L = *reinterpret_cast<const f4*>(ll + qi);
+        const f4 Dl = *reinterpret_cast<const f4*>(dl + qi);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rr + i;
+          float p = exp2f(s[r] * scale_log2 - L[i]);
+          if (CAUSAL && mykey > qt * 64 + qi + i) p = 0.f;
+          s[r] = p;
+          dpv[r] = p * (dpv[r] - Dl[i]);
+        }
+      }
+      bf16x8 pb[2], dsb[2];
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        pb[k2] = to_bf16x8(s, 8 * k2);
+        dsb[k2] = to_bf16x8(dpv, 8 * k2);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+          dv[d] = mfma(lds_tr(dol, 32 * qs + 16 * k2, 32 * d, lane), pb[k2], dv[d]);
+          dk[d] = mfma(lds_tr(ql, 32 * qs + 16 * k2, 32 * d, lane), dsb[k2], dk[d]);
+        }
+    }
+    wait_dma_and_barrier();
+  }
+  // dk^T/dv^T accumulators: column (lane) = key, rows = d
+  const float sm = scale_log2 * 0.6931471805599453f;  // softmax scale = scale_log2 * ln2
+  float* dkr = dkp + (((long)b * S + mykey) * H + hh) * HD;
+  float* dvr = dvp + (((long)b * S + mykey) * H + hh) * HD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int dd = 32 * d + 8 * rr + 4 * hf;
+      *reinterpret_cast<f4*>(dkr + dd) =
+          f4{dk[d][4 * rr] * sm, dk[d][4 * rr + 1] * sm, dk[d][4 * rr + 2] * sm, dk[d][4 * rr + 3] * sm};
+      *reinterpret_cast<f4*>(dvr + dd) = f4{dv[d][4 * rr], dv[d][4 * rr + 1], dv[d][4 * rr + 2], dv[d][4 * rr + 3]};
+    }
+}
+
+// sum the per-q-head fp32 partials over each GQA group -> bf16 dk/dv inside dqkv
+__global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __restrict__ dkp,
+                                                               const float* __restrict__ dvp,
+                                                               bf16_t* __restrict__ dqkv, int B,
+                                                               int S, int H, int KVH) {
+  const int G = H / KVH;
+  const long total = (long)B * S * KVH * (HD / 8);
+  const long NHD = (long)(H + 2 * KVH) * HD;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % (HD / 8));
+    const long r = i / (HD / 8);
+    const int kvh = (int)(r % KVH);
+    const long bs = r / KVH;
+    float ak[8] = {0, 0, 0, 0, 0, 0, 0, 0}, av[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int g = 0; g < G; ++g) {
+      const long src = (bs * H + kvh * G + g) * HD + c * 8;
+      const f4* pk = reinterpret_cast<const f4*>(dkp + src);
+      const f4* pv = reinterpret_cast<const f4*>(dvp + src);
+      const f4 k0 = pk[0], k1 = pk[1], v0 = pv[0], v1 = pv[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ak[j] += k0[j];
+        ak[4 + j] += k1[j];
+        av[j] += v0[j];
+        av[4 + j] += v1[j];
+      }
+    }
+    bf16_t* row = dqkv + bs * NHD;
+    *reinterpret_cast<us8*>(row + (H + kvh) * HD + c * 8) = pack8(ak);
+    *reinterpret_cast<us8*>(row + (H + KVH + kvh) * HD + c * 8) = pack8(av);
+  }
+}
+
+// ================================================================================================
+// Backward dQ pass: workgroup = 128 queries of one (b, q-head); loops over 64-key K/V tiles.
+// ================================================================================================
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
+                                                           const bf16_t* __restrict__ dout,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta,
+                                                           bf16_t* __restrict__ dqkv, int B, int S,
+                                                           int H, int KVH, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
+  const int NH = H + 2 * KVH;
+  const long rs = (long)NH * HD;
+  const long ors = (long)H * HD;
+  const int nqb = S / 128;
+  const int bid = blockIdx.x;
+  const int qb = CAUSAL ? nqb - 1 - bid / (B * H) : bid / (B * H);
+  const int bh = bid % (B * H);
+  const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
+  const bf16_t* base = qkv + (long)b * S * rs;
+  const bf16_t* qp = base + hh * HD;
+  const bf16_t* kp = base + (H + kvh) * HD;
+  const bf16_t* vp = base + (H + KVH + kvh) * HD;
+  const bf16_t* dop = dout + (long)b * S * ors + hh * HD;
+  const int q0 = qb * 128, qw0 = q0 + 32 * w, myq = qw0 + l32;
+
+  bf16x8 qf[8], df[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    qf[ks] = *reinterpret_cast<const bf16x8*>(qp + (long)myq * rs + 16 * ks + 8 * hf);
+    df[ks] = *reinterpret_cast<const bf16x8*>(dop + (long)myq * ors + 16 * ks + 8 * hf);
+  }
+  const float L = lse[((long)b * H + hh) * S + myq];
+  const float Dl = delta[((long)b * H + hh) * S + myq];
+  f32x16 dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+  const int nkv = CAUSAL ? (q0 + 128) / 64 : S / 64;
+
+  dma_tile64(kp, rs, smem, w, lane);
+  dma_tile64(vp, rs, smem + TILE_BYTES, w, lane);
+  wait_dma_and_barrier();
+  for (int it = 0; it < nkv; ++it) {
+    const char* kl = smem + (it & 1) * 2 * TILE_BYTES;
+    const char* vl = kl + TILE_BYTES;
+    if (it + 1 < nkv) {
+      char* nk = smem + ((it + 1) & 1) * 2 * TILE_BYTES;
+      dma_tile64(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
+      dma_tile64(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
+    }
+    const int kv0 = it * 64;
+    if (!CAUSAL || kv0 <= qw0 + 31) {
+      f32x16 st[2], dpt[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          st[t][r] = 0.f;
+          dpt[t][r] = 0.f;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          st[t] = mfma(lds_row(kl, 32 * t + l32, 2 * ks + hf), qf[ks], st[t]);
+          dpt[t] = mfma(lds_row(vl, 32 * t + l32, 2 * ks + hf), df[ks], dpt[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = exp2f(st[t][r] * scale_log2 - L);
+          if (CAUSAL) {
+            const int key = kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            if (key > myq) p = 0.f;
+          }
+          dpt[t][r] = p * (dpt[t][r] - Dl);
+        }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const bf16x8 a = to_bf16x8(dpt[s4 >> 1], 8 * (s4 & 1));
+#pragma unroll
+        for (int d = 0; d < 4; ++d) dq[d] = mfma(a, lds_tr(kl, 16 * s4, 32 * d, lane), dq[d]);
+      }
+    }
+    wait_dma_and_barrier();
+  }
+  // dq accumulator: column (lane) = d within block, rows q = (r&3) + 8*(r>>2) + 4*hf (wave-local)
+  const float sm = scale_log2 * 0.6931471805599453f;
+  bf16_t* dqb = dqkv + ((long)b * S + qw0) * rs + hh * HD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qq = (r & 3) + 8 * (r >> 2) + 4 * hf;
+      dqb[(long)qq * rs + 32 * d + l32] = f2bf(dq[d][r] * sm);
+    }
+}
+
+// ================================================================================================
+// launchers
+// ================================================================================================
+static inline bool fa_shape_ok(int S, int H, int KVH, int D) {
+  return D == HD && S % 128 == 0 && S > 0 && KVH > 0 && H % KVH == 0;
+}
+
+extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, int S, int H, int KVH,
+                                 int D, float scale, int causal, hipStream_t st) {
+  if (!fa_shape_ok(S, H, KVH, D)) return hipErrorInvalidValue;
+  const float sl2 = scale * 1.4426950408889634f;
+  const int grid = B * H * (S / 128);
+  const size_t lds = 4 * TILE_BYTES;
+  if (causal)
+    fa_fwd_kernel<true><<<grid, 256, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+  else
+    fa_fwd_kernel<false><<<grid, 256, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+  return hipGetLastError();
+}
+
+// workspace: delta (B*H*S fp32) + dkp + dvp (2 * B*S*H*128 fp32)
+extern "C" size_t dsa_fa_bwd_workspace(int B, int S, int H) {
+  return (size_t)B * H * S * 4 + 2 * (size_t)B * S * H * HD * 4;
+}
+
+extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
+                                 void* dqkv, void* workspace, int B, int S, int H, int KVH, int D,
+                                 float scale, int causal, hipStream_t st) {
+  if (!fa_shape_ok(S, H, KVH, D)) return hipErrorInvalidValue;
+  const float sl2 = scale * 1.4426950408889634f;
+  float* delta = (float*)workspace;
+  float* dkp = delta + (size_t)B * H * S;
+  float* dvp = dkp + (size_t)B * S * H * HD;
+  const long rows = (long)B * S * H;
+  fa_bwd_delta_kernel<<<(int)((rows + 15) / 16), 256, 0, st>>>((const bf16_t*)out, (const bf16_t*)dout,
+                                                               delta, B, S, H);
+  DSA_CHECK(hipGetLastError());
+  const int grid = B * H * (S / 128);
+  const size_t lds_kv = 2 * (2 * TILE_BYTES + 512);
+  const size_t lds_q = 4 * TILE_BYTES;
+  if (causal) {
+    fa_bwd_dkdv_kernel<true><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
+                                                        delta, dkp, dvp, B, S, H, KVH, sl2);
+    DSA_CHECK(hipGetLastError());
+    fa_bwd_dq_kernel<true><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta,
+                                                     (bf16_t*)dqkv, B, S, H, KVH, sl2);
+  } else {
+    fa_bwd_dkdv_kernel<false><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
+                                                         delta, dkp, dvp, B, S, H, KVH, sl2);
+    DSA_CHECK(hipGetLastError());
+    fa_bwd_dq_kernel<false><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
+                                                      delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+  }
+  DSA_CHECK(hipGetLastError());
+  const long work = (long)B * S * KVH * (HD / 8);
+  int g = (int)((work + 255) / 256);
+  if (g > 4096) g = 4096;
+  fa_bwd_reduce_kv_kernel<<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH);
+  return hipGetLastError();
+}

@@ -1,0 +1,206 @@
+"""Autograd wrappers around the HIP kernels (``_C``) with CPU reference fallbacks."""
+
+from __future__ import annotations
+
+import os
+
+import torch
+
+from dstack_amd.ops import _ext
+from dstack_amd.ops import reference as ref
+
+
+def _2d(t: torch.Tensor) -> torch.Tensor:
+    return t.reshape(-1, t.shape[-1])
+
+
+# ----------------------------------------------------------------------------------------------
+# RMSNorm (+ fused residual add)
+# ----------------------------------------------------------------------------------------------
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        C = _ext.require()
+        y, rstd = C.rms_norm_fwd(_2d(x), w, eps)
+        ctx.save_for_backward(x, w, rstd)
+        return y.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        x, w, rstd = ctx.saved_tensors
+        dx, dw = C.rms_norm_bwd(_2d(dy.contiguous()), _2d(x), w, rstd, None)
+        return dx.view_as(x), dw.to(w.dtype), None
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """h = x + delta ; y = rmsnorm(h) * w.  Returns (h, y); one HBM pass instead of two."""
+
+    @staticmethod
+    def forward(ctx, x, delta, w, eps):
+        C = _ext.require()
+        h, y, rstd = C.add_rms_norm_fwd(_2d(x), _2d(delta), w, eps)
+        ctx.save_for_backward(h, w, rstd)
+        return h.view_as(x), y.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        C = _ext.require()
+        h, w, rstd = ctx.saved_tensors
+        if dh is not None:
+            dh = _2d(dh.contiguous())
+        dx, dw = C.rms_norm_bwd(_2d(dy.contiguous()), h, w, rstd, dh)
+        dx = dx.view(dy.shape)
+        return dx, dx, dw.to(w.dtype), None
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    if _ext.use_hip(x):
+        return _RMSNorm.apply(x.contiguous(), w, eps)
+    return ref.rms_norm(x, w, eps)
+
+
+def add_rms_norm(x: torch.Tensor, delta: torch.Tensor, w: torch.Tensor, eps: float = 1e-5):
+    if _ext.use_hip(x):
+        return _AddRMSNorm.apply(x.contiguous(), delta.contiguous(), w, eps)
+    return ref.add_rms_norm(x, delta, w, eps)
+
+
+# ----------------------------------------------------------------------------------------------
+# SwiGLU on the fused [gate | up] projection output
+# ----------------------------------------------------------------------------------------------
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        C = _ext.require()
+        ctx.save_for_backward(gu)
+        return C.swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, da):
+        C = _ext.require()
+        (gu,) = ctx.saved_tensors
+        return C.swiglu_bwd(da.contiguous(), gu)
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    if _ext.use_hip(gu):
+        return _SwiGLU.apply(gu.contiguous())
+    return ref.swiglu(gu)
+
+
+# ----------------------------------------------------------------------------------------------
+# RoPE applied to the q and k heads of a fused qkv activation [B, S, (H + 2*KV) * D]
+# ----------------------------------------------------------------------------------------------
+class _RopeQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, n_rot_heads, head_dim):
+        C = _ext.require()
+        ctx.save_for_backward(cos, sin)
+        ctx.meta = (n_rot_heads, head_dim)
+        return C.rope_qkv(qkv, cos, sin, n_rot_heads, head_dim, False)
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = _ext.require()
+        cos, sin = ctx.saved_tensors
+        n_rot_heads, head_dim = ctx.meta
+        return C.rope_qkv(dout.contiguous(), cos, sin, n_rot_heads, head_dim, True), None, None, None, None
+
+
+def rope(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_rot_heads: int, head_dim: int):
+    """Rotate the first ``n_rot_heads`` heads (q and k) of ``qkv`` [B, S, NH*D]; v passes through."""
+    if _ext.use_hip(qkv):
+        return _RopeQKV.apply(qkv.contiguous(), cos, sin, n_rot_heads, head_dim)
+    b, s, _ = qkv.shape
+    x = qkv.view(b, s, -1, head_dim)
+    rot = ref.apply_rope(x[:, :, :n_rot_heads], cos, sin)
+    return torch.cat([rot, x[:, :, n_rot_heads:]], dim=2).reshape(b, s, -1)
+
+
+# ----------------------------------------------------------------------------------------------
+# Attention (causal, GQA) straight from the fused qkv activation [B, S, (H + 2*KV) * D]
+# ----------------------------------------------------------------------------------------------
+class _FlashAttnQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, n_heads, n_kv_heads, causal):
+        C = _ext.require()
+        o, lse = C.flash_attn_fwd(qkv, n_heads, n_kv_heads, causal)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.meta = (n_heads, n_kv_heads, causal)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        C = _ext.require()
+        qkv, o, lse = ctx.saved_tensors
+        n_heads, n_kv_heads, causal = ctx.meta
+        dqkv = C.flash_attn_bwd(do.contiguous(), qkv, o, lse, n_heads, n_kv_heads, causal)
+        return dqkv, None, None, None
+
+
+def _attn_impl() -> str:
+    return os.environ.get("DSTACK_AMD_ATTN", "hip").lower()
+
+
+def split_qkv(qkv: torch.Tensor, n_heads: int, n_kv_heads: int):
+    b, s, _ = qkv.shape
+    x = qkv.view(b, s, n_heads + 2 * n_kv_heads, -1)
+    return x[:, :, :n_heads], x[:, :, n_heads : n_heads + n_kv_heads], x[:, :, n_heads + n_kv_heads :]
+
+
+def attention(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, causal: bool = True) -> torch.Tensor:
+    """Causal GQA attention on the fused projection output; returns [B, S, H*D]."""
+    b, s, _ = qkv.shape
+    if _ext.use_hip(qkv) and _attn_impl() == "hip":
+        return _FlashAttnQKV.apply(qkv.contiguous(), n_heads, n_kv_heads, causal)
+    q, k, v = split_qkv(qkv, n_heads, n_kv_heads)
+    if q.is_cuda:
+        # library attention (PyTorch-ROCm SDPA) — opt-in A/B baseline only (DSTACK_AMD_ATTN=sdpa)
+        o = torch.nn.functional.scaled_dot_product_attention(
+            q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=causal, enable_gqa=True
+        ).transpose(1, 2)
+    else:
+        o = ref.attention(q, k, v, causal)
+    return o.reshape(b, s, -1)
+
+
+# ----------------------------------------------------------------------------------------------
+# Fused softmax cross-entropy over the vocab (never materialises fp32 logits)
+# ----------------------------------------------------------------------------------------------
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target):
+        C = _ext.require()
+        loss_rows, lse = C.cross_entropy_fwd(logits, target)
+        ctx.save_for_backward(logits, target, lse)
+        return loss_rows.mean()
+
+    @staticmethod
+    def backward(ctx, dloss):
+        C = _ext.require()
+        logits, target, lse = ctx.saved_tensors
+        scale = dloss / logits.shape[0]
+        # gradient is written in place over the logits buffer (logits are dead after this)
+        dlogits = C.cross_entropy_bwd(logits, target, lse, scale.float().reshape(1), True)
+        return dlogits, None
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """Mean token cross-entropy; ``logits`` [T, V] bf16, ``target`` [T] int64."""
+    if _ext.use_hip(logits):
+        return _CrossEntropy.apply(logits.contiguous(), target.contiguous())
+    return ref.cross_entropy(logits, target)
+
+
+# ----------------------------------------------------------------------------------------------
+# Fused AdamW over flat buffers (bf16 param/grad, fp32 master/m/v)
+# ----------------------------------------------------------------------------------------------
+def adamw_(param, grad, master, m, v, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    if _ext.use_hip(param):
+        C = _ext.require()
+        bc1 = 1.0 - beta1**step
+        bc2 = 1.0 - beta2**step
+        C.adamw(param, grad, master, m, v, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale)
+        return
+    ref.adamw_(param, grad, master, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale)

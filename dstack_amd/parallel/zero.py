@@ -1,0 +1,195 @@
+"""ZeRO-1 data parallelism over RCCL with flat, bucketed parameter/gradient storage.
+
+Design (MI355X-first, not a DDP translation):
+
+* **One flat bf16 parameter buffer and one flat bf16 gradient buffer.** Every ``nn.Parameter`` is a
+  view into them, laid out in *reverse* registration order so that the parameters whose gradients
+  are produced first in backward are contiguous. A bucket is a contiguous slice of both buffers,
+  padded to a multiple of ``world_size * 64`` elements, so reduce-scatter/all-gather run on
+  buffers in place with no packing copies.
+* **Gradient reduce-scatter overlapped with backward.** A post-accumulate-grad hook counts down the
+  parameters of each bucket; when a bucket is complete it is reduce-scattered
+  asynchronously on RCCL's stream while autograd keeps computing earlier layers (SUM; the
+  1/world of the average is folded into the AdamW kernel's grad scale).
+* **Sharded fp32 optimizer state.** Rank r owns shard r of every bucket: fp32 master weights, Adam
+  m and v (12 B/param / world_size). With 288 GB HBM3E per GPU, a single GPU holds the full 8B
+  model state (≈128 GB); with 8 GPUs the optimizer state shrinks to ≈12 GB per GPU.
+* **Fused AdamW** (``ops.adamw_``, one HIP kernel per bucket shard) then an all-gather of the
+  updated bf16 shards back into the flat parameter buffer.
+* Bucket size defaults to 256 Mi elements (512 MB bf16): xGMI rings are per-link bound (≈153 GB/s
+  per link), so few large collectives amortise RCCL launch latency; backward of one Llama-3-8B
+  layer produces ≈436 MB of gradients, so a bucket completes roughly every layer.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from dstack_amd import ops
+
+ALIGN = 64
+
+
+@dataclass
+class Bucket:
+    index: int
+    start: int  # offset in the flat buffers
+    numel: int  # padded
+    params: list = field(default_factory=list)
+    pending: int = 0
+    work: object = None
+
+    def shard_range(self, rank: int, world: int):
+        n = self.numel // world
+        return self.start + rank * n, n
+
+
+class ZeroOptimizer:
+    def __init__(
+        self,
+        model: nn.Module,
+        lr: float = 3e-4,
+        betas=(0.9, 0.95),
+        eps: float = 1e-8,
+        weight_decay: float = 0.1,
+        bucket_numel: int = 256 * 1024 * 1024,
+        group: dist.ProcessGroup | None = None,
+        overlap: bool = True,
+    ):
+        self.model = model
+        self.lr = lr
+        self.beta1, self.beta2 = betas
+        self.eps = eps
+        self.weight_decay = weight_decay
+        self.group = group
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.distributed else 1
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        self.overlap = overlap and self.world > 1
+        self.step_count = 0
+
+        params = [p for p in model.parameters() if p.requires_grad]
+        device = params[0].device
+        dtype = params[0].dtype
+        # ---- bucket layout (reverse registration order ≈ gradient production order) ----
+        self.buckets: list[Bucket] = []
+        pad_to = self.world * ALIGN
+        cur = Bucket(0, 0, 0)
+        off = 0
+        layout = []
+        for p in reversed(params):
+            n = p.numel()
+            if cur.params and cur.numel + n > bucket_numel:
+                cur.numel = _round_up(cur.numel, pad_to)
+                off = cur.start + cur.numel
+                self.buckets.append(cur)
+                cur = Bucket(len(self.buckets), off, 0)
+            layout.append((p, cur.start + cur.numel))
+            cur.params.append(p)
+            cur.numel += n
+        cur.numel = _round_up(cur.numel, pad_to)
+        self.buckets.append(cur)
+        self.total_numel = cur.start + cur.numel
+
+        self.flat_param = torch.zeros(self.total_numel, dtype=dtype, device=device)
+        self.flat_grad = torch.zeros(self.total_numel, dtype=dtype, device=device)
+        self._bucket_of = {}
+        for p, o in layout:
+            n = p.numel()
+            self.flat_param[o : o + n].copy_(p.detach().reshape(-1))
+            p.data = self.flat_param[o : o + n].view_as(p)
+            p.grad = self.flat_grad[o : o + n].view_as(p)
+        for b in self.buckets:
+            for p in b.params:
+                self._bucket_of[p] = b
+
+        # ---- sharded fp32 state ----
+        self.master, self.exp_avg, self.exp_avg_sq = [], [], []
+        for b in self.buckets:
+            s, n = b.shard_range(self.rank, self.world)
+            self.master.append(self.flat_param[s : s + n].float())
+            self.exp_avg.append(torch.zeros(n, dtype=torch.float32, device=device))
+            self.exp_avg_sq.append(torch.zeros(n, dtype=torch.float32, device=device))
+
+        self._hooks = []
+        if self.overlap:
+            for p in params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
+        self._arm()
+
+    # ------------------------------------------------------------------------------------------
+    def _arm(self):
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.work = None
+
+    def _on_grad_ready(self, p: torch.Tensor):
+        b = self._bucket_of[p]
+        b.pending -= 1
+        if b.pending == 0:
+            self._reduce_bucket(b, async_op=True)
+
+    def _reduce_bucket(self, b: Bucket, async_op: bool):
+        if self.world == 1:
+            return
+        s, n = b.shard_range(self.rank, self.world)
+        full = self.flat_grad[b.start : b.start + b.numel]
+        out = self.flat_grad[s : s + n]
+        b.work = dist.reduce_scatter_tensor(
+            out, full, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op
+        )
+
+    def zero_grad(self):
+        self.flat_grad.zero_()
+        self._arm()
+
+    @torch.no_grad()
+    def step(self):
+        self.step_count += 1
+        if self.world > 1:
+            for b in self.buckets:
+                if b.work is None:  # not overlapped (or a param received no grad)
+                    self._reduce_bucket(b, async_op=False)
+                else:
+                    b.work.wait()
+        for i, b in enumerate(self.buckets):
+            s, n = b.shard_range(self.rank, self.world)
+            ops.adamw_(
+                self.flat_param[s : s + n],
+                self.flat_grad[s : s + n],
+                self.master[i],
+                self.exp_avg[i],
+                self.exp_avg_sq[i],
+                lr=self.lr,
+                beta1=self.beta1,
+                beta2=self.beta2,
+                eps=self.eps,
+                weight_decay=self.weight_decay,
+                step=self.step_count,
+                grad_scale=1.0 / self.world,  # the 1/world of the average is fused into AdamW
+            )
+        if self.world > 1:
+            works = []
+            for b in self.buckets:
+                s, n = b.shard_range(self.rank, self.world)
+                works.append(
+                    dist.all_gather_into_tensor(
+                        self.flat_param[b.start : b.start + b.numel],
+                        self.flat_param[s : s + n],
+                        group=self.group,
+                        async_op=True,
+                    )
+                )
+            for w in works:
+                w.wait()
+
+    def state_bytes(self) -> int:
+        return sum(t.numel() * 4 for t in self.master + self.exp_avg + self.exp_avg_sq)
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m

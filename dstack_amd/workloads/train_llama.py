@@ -1,0 +1,153 @@
+"""Llama-3 pre-training step on MI355X: one process per GPU, ZeRO-1 DP over RCCL/xGMI.
+
+This is the workload behind the headline benchmark ("tokens/sec of an 8-GPU Llama-3-8B task via
+dstack apply", BASELINE.json). It is launched either directly by ``bench.py`` or by a
+``type: task`` run (``examples/llama3-8b-train.dstack.yml``) whose runner exports the rendezvous
+env (``DSTACK_MASTER_NODE_IP``, ``DSTACK_NODE_RANK``, …, plus ``MASTER_ADDR``/``RANK``/…).
+
+Data is synthetic (uniform random token ids) and weights are random-init: there is no network.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from dstack_amd.models.llama import CONFIGS, Llama
+from dstack_amd.parallel.zero import ZeroOptimizer
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+
+def init_distributed(backend: str | None = None) -> DistEnv:
+    """Reads torchrun's env (or the dstack runner's RCCL rendezvous env) and joins the group."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    env = DistEnv(rank, world, local_rank)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"  # "nccl" is RCCL on ROCm
+        kwargs = {}
+        if backend == "nccl":
+            kwargs["device_id"] = torch.device("cuda", local_rank)
+        dist.init_process_group(backend=backend, **kwargs)
+    return env
+
+
+class Trainer:
+    def __init__(self, model_name: str, seq_len: int, micro_batch: int, device, lr: float = 3e-4,
+                 seed: int = 0, bucket_numel: int = 256 * 1024 * 1024):
+        self.cfg = CONFIGS[model_name]
+        self.seq_len = seq_len
+        self.micro_batch = micro_batch
+        self.device = device
+        dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+        with torch.device(device):
+            model = Llama(self.cfg)
+        model.to(dtype)
+        model.init_weights(seed=seed)
+        self.model = model
+        self.opt = ZeroOptimizer(model, lr=lr, bucket_numel=bucket_numel)
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        g = torch.Generator(device=device).manual_seed(1234 + rank)
+        n = micro_batch * (seq_len + 1)
+        self.data = torch.randint(0, self.cfg.vocab_size, (4, n), device=device, generator=g)
+        self._i = 0
+
+    def batch(self):
+        row = self.data[self._i % self.data.shape[0]].view(self.micro_batch, self.seq_len + 1)
+        self._i += 1
+        return row[:, :-1], row[:, 1:]
+
+    def step(self) -> torch.Tensor:
+        tokens, targets = self.batch()
+        self.opt.zero_grad()
+        loss = self.model.loss(tokens, targets)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
+
+    @property
+    def tokens_per_step(self) -> int:
+        return self.micro_batch * self.seq_len
+
+
+def _sync(env: DistEnv):
+    if env.distributed:
+        dist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1):
+    env = init_distributed()
+    device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    t0 = time.time()
+    tr = Trainer(model, seq_len, micro_batch, device)
+    if env.rank == 0:
+        print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
+              f"init={time.time()-t0:.1f}s", flush=True)
+    for i in range(warmup):
+        loss = tr.step()
+        if env.rank == 0:
+            print(f"[train] warmup {i} loss={loss.item():.4f}", flush=True)
+    _sync(env)
+    t_start = time.perf_counter()
+    losses = []
+    for i in range(steps):
+        losses.append(tr.step())
+        if log_every and env.rank == 0 and (i + 1) % log_every == 0:
+            print(f"[train] step {i} loss={losses[-1].item():.4f}", flush=True)
+    _sync(env)
+    elapsed = time.perf_counter() - t_start
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if env.distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    tok_s = tr.tokens_per_step * env.world * steps / elapsed
+    result = {
+        "tokens_per_s": tok_s,
+        "ms_per_step": elapsed / steps * 1e3,
+        "world": env.world,
+        "flops_per_token": tr.cfg.flops_per_token(seq_len),
+        "final_loss": losses[-1].item() if losses else None,
+    }
+    result["tflops_per_gpu"] = tok_s / env.world * result["flops_per_token"] / 1e12
+    if env.rank == 0:
+        print("[train] result " + json.dumps(result), flush=True)
+    return env, tr, result
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--seq-len", type=int, default=8192)
+    ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    args = ap.parse_args(argv)
+    env, _, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup)
+    if env.distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference (``ops.reference``)."""
+
+import math
+
+import pytest
+import torch
+
+from dstack_amd import ops
+from dstack_amd.ops import _ext
+from dstack_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(*shape, device, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator(device=device).manual_seed(seed)
+    return (torch.randn(*shape, device=device, generator=g) * scale).to(dtype)
+
+
+def _close(a, b, atol, rtol=0.0):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"max abs err {err} > {tol}"
+
+
+def test_extension_loaded(gpu):
+    assert _ext.available(), "HIP extension must be built for GPU runs"
+
+
+@pytest.mark.parametrize("D", [256, 4096, 8192])
+def test_rms_norm(gpu, D):
+    x = _rand(512, D, device=gpu).requires_grad_()
+    w = (1 + 0.1 * _rand(D, device=gpu, seed=1)).requires_grad_()
+    y = ops.rms_norm(x, w, 1e-5)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    yr = ref.rms_norm(xr, wr, 1e-5)
+    _close(y, yr, 2e-2, 1e-2)
+    dy = _rand(512, D, device=gpu, seed=2)
+    y.backward(dy)
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 3e-2, 1e-2)
+    _close(w.grad, wr.grad, 0.5, 2e-2)
+
+
+def test_add_rms_norm(gpu):
+    D = 4096
+    x = _rand(256, D, device=gpu).requires_grad_()
+    d = _rand(256, D, device=gpu, seed=3).requires_grad_()
+    w = (1 + 0.1 * _rand(D, device=gpu, seed=1)).requires_grad_()
+    h, y = ops.add_rms_norm(x, d, w, 1e-5)
+    xr, dr, wr = (t.detach().float().requires_grad_() for t in (x, d, w))
+    hr = xr + dr
+    yr = ref.rms_norm(hr, wr, 1e-5)
+    _close(h, hr, 2e-2, 1e-2)
+    _close(y, yr, 3e-2, 1e-2)
+    gh, gy = _rand(256, D, device=gpu, seed=4), _rand(256, D, device=gpu, seed=5)
+    (h.float() * gh.float()).sum().add((y.float() * gy.float()).sum()).backward()
+    (hr * gh.float()).sum().add((yr * gy.float()).sum()).backward()
+    _close(x.grad, xr.grad, 5e-2, 1e-2)
+    _close(d.grad, dr.grad, 5e-2, 1e-2)
+
+
+def test_swiglu(gpu):
+    gu = _rand(1024, 2 * 1792, device=gpu).requires_grad_()
+    a = ops.swiglu(gu)
+    gr = gu.detach().float().requires_grad_()
+    ar = ref.swiglu(gr)
+    _close(a, ar, 2e-2, 1e-2)
+    da = _rand(1024, 1792, device=gpu, seed=7)
+    a.backward(da)
+    ar.backward(da.float())
+    _close(gu.grad, gr.grad, 3e-2, 1e-2)
+
+
+def test_rope(gpu):
+    B, S, H, KV, D = 2, 256, 8, 2, 128
+    qkv = _rand(B, S, (H + 2 * KV) * D, device=gpu).requires_grad_()
+    cos, sin = ref.rope_cos_sin(S, D, 500000.0, gpu)
+    out = ops.rope(qkv, cos, sin, H + KV, D)
+    x = qkv.detach().float().view(B, S, H + 2 * KV, D)
+    exp = torch.cat([ref.apply_rope(x[:, :, : H + KV], cos, sin), x[:, :, H + KV :]], 2).reshape(B, S, -1)
+    _close(out, exp, 2e-2, 1e-2)
+    g = _rand(B, S, (H + 2 * KV) * D, device=gpu, seed=9)
+    out.backward(g)
+    xr = qkv.detach().float().view(B, S, H + 2 * KV, D).requires_grad_()
+    er = torch.cat([ref.apply_rope(xr[:, :, : H + KV], cos, sin), xr[:, :, H + KV :]], 2).reshape(B, S, -1)
+    er.backward(g.float())
+    _close(qkv.grad, xr.grad.reshape(B, S, -1), 2e-2, 1e-2)
+
+
+@pytest.mark.parametrize("V", [1024, 128256])
+def test_cross_entropy(gpu, V):
+    T = 256
+    logits = _rand(T, V, device=gpu, scale=3.0).requires_grad_()
+    tgt = torch.randint(0, V, (T,), device=gpu)
+    loss = ops.cross_entropy(logits.clone(), tgt)
+    lr_ = logits.detach().float().requires_grad_()
+    lref = ref.cross_entropy(lr_, tgt)
+    assert abs(loss.item() - lref.item()) < 2e-3 * max(1.0, abs(lref.item()))
+    l2 = ops.cross_entropy(logits, tgt)
+    l2.backward()
+    lref.backward()
+    _close(logits.grad, lr_.grad, 2e-4, 2e-2)
+
+
+def test_adamw(gpu):
+    n = 1 << 20 | 5  # exercise the scalar tail
+    p = _rand(n, device=gpu)
+    g = _rand(n, device=gpu, seed=11, scale=0.01)
+    master = p.float()
+    m = torch.zeros(n, device=gpu)
+    v = torch.zeros(n, device=gpu)
+    p2, master2, m2, v2 = p.clone(), master.clone(), m.clone(), v.clone()
+    for step in (1, 2, 3):
+        ops.adamw_(p, g, master, m, v, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=step,
+                   grad_scale=0.5)
+        ref.adamw_(p2, g, master2, m2, v2, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.5)
+    _close(master, master2, 1e-5, 1e-5)
+    _close(m, m2, 1e-7, 1e-5)
+    _close(p, p2, 1e-2)
+
+
+@pytest.mark.parametrize("S,H,KV", [(128, 4, 1), (256, 8, 2), (512, 4, 4), (1024, 32, 8)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention(gpu, S, H, KV, causal):
+    B, D = 2, 128
+    qkv = _rand(B, S, (H + 2 * KV) * D, device=gpu).requires_grad_()
+    o = ops.attention(qkv, H, KV, causal=causal)
+    xr = qkv.detach().float().requires_grad_()
+    q, k, v = ops.functional.split_qkv(xr, H, KV)
+    orf = ref.attention(q, k, v, causal).reshape(B, S, -1)
+    _close(o, orf, 2e-2, 2e-2)
+    do = _rand(B, S, H * D, device=gpu, seed=13)
+    o.backward(do)
+    orf.backward(do.float())
+    g, gr = qkv.grad.view(B, S, H + 2 * KV, D), xr.grad.view(B, S, H + 2 * KV, D)
+    for name, sl in (("dq", slice(0, H)), ("dk", slice(H, H + KV)), ("dv", slice(H + KV, H + 2 * KV))):
+        a, b = g[:, :, sl].float(), gr[:, :, sl]
+        err = (a - b).abs().max().item()
+        scale = b.abs().max().item()
+        assert err <= 3e-2 * scale + 2e-2, f"{name}: err {err} (ref max {scale})"
+
+
+def test_flash_attention_lse_rescale_branch(gpu):
+    """Force the online-softmax rescale: a spike key late in the sequence for every query."""
+    B, S, H, KV, D = 1, 512, 2, 1, 128
+    qkv = _rand(B, S, (H + 2 * KV) * D, device=gpu, scale=0.5)
+    x = qkv.view(B, S, H + 2 * KV, D)
+    x[:, 300, H] = x[:, 300, 0].mean(0) * 0 + 4.0  # key 300 aligned with an all-positive direction
+    x[:, :, :H] = x[:, :, :H].abs()
+    qkv = x.reshape(B, S, -1).contiguous()
+    o = ops.attention(qkv, H, KV, causal=True)
+    q, k, v = ops.functional.split_qkv(qkv.float(), H, KV)
+    orf = ref.attention(q, k, v, True).reshape(B, S, -1)
+    _close(o, orf, 3e-2, 2e-2)
+
+
+def test_llama_tiny_step_matches_reference(gpu, monkeypatch):
+    """One fwd+bwd of the tiny Llama through the HIP path vs the fp32 reference path."""
+    from dstack_amd.models.llama import CONFIGS, Llama
+    import dataclasses
+
+    cfg = dataclasses.replace(CONFIGS["llama-tiny"], dim=512, n_heads=4, n_kv_heads=2)
+    torch.manual_seed(0)
+    with torch.device(gpu):
+        m = Llama(cfg)
+    m.init_weights()
+    mb = m.to(torch.bfloat16)
+    tok = torch.randint(0, cfg.vocab_size, (2, 129), device=gpu)
+    loss = mb.loss(tok[:, :-1], tok[:, 1:])
+    loss.backward()
+    grads = {n: p.grad.float().clone() for n, p in mb.named_parameters()}
+    mb.zero_grad()
+    monkeypatch.setenv("DSTACK_AMD_OPS", "torch")
+    loss_ref = mb.loss(tok[:, :-1], tok[:, 1:])
+    loss_ref.backward()
+    assert abs(loss.item() - loss_ref.item()) < 2e-2
+    for n, p in mb.named_parameters():
+        a, b = grads[n], p.grad.float()
+        rel = (a - b).norm() / (b.norm() + 1e-12)
+        assert rel < 0.08, f"{n}: rel grad err {rel}"
