@@ -62,8 +62,10 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 
 // ------------------------------------------------------------------------------------------------
 // RMSNorm backward: dx = r*g - h*r^3*mean(g*h) (+ dres), g = dy*w ;  dw partials per block.
-// Grid-strided over rows so each wave accumulates its dw contribution in registers; the block's
-// waves combine through LDS and write one fp32 partial row per block, reduced by colsum below.
+// One 256-thread block per row (grid-strided over rows): each thread owns NCH chunks of 8
+// columns, so its dw contribution stays in NCH*8 registers for the whole launch; the row dot is a
+// wave shuffle + a 4-entry LDS combine.  Each block writes one fp32 dw partial row; colsum_kernel
+// reduces the [grid, D] partials.
 // ------------------------------------------------------------------------------------------------
 template <int NCH, bool RES>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restrict__ dy,
@@ -74,28 +76,28 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restri
                                                           bf16_t* __restrict__ dx,
                                                           float* __restrict__ dw_part, int rows,
                                                           int D) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ float red[2][4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
   const int nch = D >> 3;
   float wv[NCH][8];
   float dwa[NCH][8];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int ch = lane + c * 64;
+    const int ch = threadIdx.x + c * 256;
 #pragma unroll
     for (int i = 0; i < 8; ++i) dwa[c][i] = 0.f;
     if (ch < nch) unpack8(*reinterpret_cast<const us8*>(w + ch * 8), wv[c]);
   }
-  for (int row = blockIdx.x * nw + wid; row < rows; row += gridDim.x * nw) {
+  int parity = 0;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x, parity ^= 1) {
     const size_t base = (size_t)row * D;
     const float r = rstd[row];
     float hv[NCH][8], g[NCH][8];
     float dot = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int ch = lane + c * 64;
+      const int ch = threadIdx.x + c * 256;
       if (ch < nch) {
         float d[8];
         unpack8(*reinterpret_cast<const us8*>(dy + base + ch * 8), d);
@@ -109,10 +111,13 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restri
       }
     }
     dot = wave_sum(dot);
+    if (lane == 0) red[parity][wid] = dot;  // double-buffered: one barrier per row
+    __syncthreads();
+    dot = red[parity][0] + red[parity][1] + red[parity][2] + red[parity][3];
     const float k = dot * r * r * r / (float)D;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int ch = lane + c * 64;
+      const int ch = threadIdx.x + c * 256;
       if (ch < nch) {
         float o[8];
         if constexpr (RES) {
@@ -127,36 +132,30 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restri
       }
     }
   }
-  // combine the waves' dw partials: wave 0 writes, others add (LDS holds D floats)
-  for (int wv_i = 0; wv_i < nw; ++wv_i) {
-    if (wid == wv_i) {
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int ch = lane + c * 64;
-        if (ch < nch) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if (wv_i == 0)
-              lds[ch * 8 + i] = dwa[c][i];
-            else
-              lds[ch * 8 + i] += dwa[c][i];
-          }
-        }
-      }
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = threadIdx.x + c * 256;
+    if (ch < nch) {
+      f4* dst = reinterpret_cast<f4*>(dw_part + (size_t)blockIdx.x * D + ch * 8);
+      dst[0] = f4{dwa[c][0], dwa[c][1], dwa[c][2], dwa[c][3]};
+      dst[1] = f4{dwa[c][4], dwa[c][5], dwa[c][6], dwa[c][7]};
     }
-    __syncthreads();
   }
-  for (int i = threadIdx.x; i < D; i += blockDim.x) dw_part[(size_t)blockIdx.x * D + i] = lds[i];
 }
 
-// column sums of a [P, D] fp32 matrix -> out[D] (fp32)
+// column sums of a [P, D] fp32 matrix -> out[D]: block = 64 columns x 4 row-groups, coalesced
+// 256-byte row segments per wave, LDS combine of the 4 row-groups.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part,
                                                      float* __restrict__ out, int P, int D) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= D) return;
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * D + col];
-  out[col] = s;
+  if (col < D)
+    for (int p = rg; p < P; p += 4) s += part[(size_t)p * D + col];
+  red[rg][c] = s;
+  __syncthreads();
+  if (rg == 0 && col < D) out[col] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -412,6 +411,16 @@ static inline int grid_for(size_t work, int block, int cap = 256 * 16) {
     else return hipErrorInvalidValue;              \
   } while (0)
 
+// chunks-per-thread dispatch for block-per-row kernels (256 threads x 8 columns per chunk)
+#define NCH_DISPATCH_BLK(D, ...)                   \
+  do {                                             \
+    const int _n = ((D) / 8 + 255) / 256;          \
+    if (_n <= 1) { constexpr int NCH = 1; __VA_ARGS__; }      \
+    else if (_n <= 2) { constexpr int NCH = 2; __VA_ARGS__; } \
+    else if (_n <= 4) { constexpr int NCH = 4; __VA_ARGS__; } \
+    else return hipErrorInvalidValue;              \
+  } while (0)
+
 extern "C" hipError_t dsa_rmsnorm_fwd(const void* x, const void* delta, const void* w, void* h_out,
                                       void* y, float* rstd, int rows, int D, float eps,
                                       hipStream_t st) {
@@ -431,7 +440,7 @@ extern "C" hipError_t dsa_rmsnorm_fwd(const void* x, const void* delta, const vo
 
 // dw_part must hold grid*D floats where grid = dsa_rmsnorm_bwd_grid(rows)
 extern "C" int dsa_rmsnorm_bwd_grid(int rows) {
-  int g = (rows + 3) / 4;
+  int g = rows;
   return g > 1024 ? 1024 : (g < 1 ? 1 : g);
 }
 
@@ -441,18 +450,18 @@ extern "C" hipError_t dsa_rmsnorm_bwd(const void* dy, const void* h, const void*
   if (D % 8) return hipErrorInvalidValue;
   const int block = 256;
   const int grid = dsa_rmsnorm_bwd_grid(rows);
-  const size_t lds = (size_t)D * sizeof(float);
+  const size_t lds = 0;
   if (dres) {
-    NCH_DISPATCH(D, rmsnorm_bwd_kernel<NCH, true><<<grid, block, lds, st>>>(
+    NCH_DISPATCH_BLK(D, rmsnorm_bwd_kernel<NCH, true><<<grid, block, lds, st>>>(
         (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)w, rstd, (const bf16_t*)dres,
         (bf16_t*)dx, dw_part, rows, D));
   } else {
-    NCH_DISPATCH(D, rmsnorm_bwd_kernel<NCH, false><<<grid, block, lds, st>>>(
+    NCH_DISPATCH_BLK(D, rmsnorm_bwd_kernel<NCH, false><<<grid, block, lds, st>>>(
         (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)w, rstd, nullptr, (bf16_t*)dx, dw_part,
         rows, D));
   }
   DSA_CHECK(hipGetLastError());
-  colsum_kernel<<<(D + 255) / 256, 256, 0, st>>>(dw_part, dw, grid, D);
+  colsum_kernel<<<(D + 63) / 64, 256, 0, st>>>(dw_part, dw, grid, D);
   return hipGetLastError();
 }
 

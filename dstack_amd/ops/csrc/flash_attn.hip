@@ -35,6 +35,9 @@ namespace {
 
 constexpr int HD = 128;          // head dim
 constexpr int TILE_BYTES = 64 * 256;  // 64 rows x 128 bf16
+#ifndef DKDV_WAVES_PER_SIMD
+#define DKDV_WAVES_PER_SIMD 1  // dK/dV + K/V fragments need ~300 registers: 1 wave/SIMD, no spills
+#endif
 
 __device__ __forceinline__ int swz(int row, int ch) {
   return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(256) void fa_bwd_delta_kernel(const bf16_t* __restr
 // dkp/dvp [B, S, H, 128] that fa_bwd_reduce_kv sums over the GQA group.
 // ================================================================================================
 template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
+__global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
     int H, int KVH, float scale_log2) {

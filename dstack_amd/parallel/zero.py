@@ -71,6 +71,7 @@ class ZeroOptimizer:
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.overlap = overlap and self.world > 1
         self.step_count = 0
+        self.sync_grads = True  # False while accumulating non-final micro-batches
 
         params = [p for p in model.parameters() if p.requires_grad]
         device = params[0].device
@@ -128,6 +129,8 @@ class ZeroOptimizer:
             b.work = None
 
     def _on_grad_ready(self, p: torch.Tensor):
+        if not self.sync_grads:
+            return
         b = self._bucket_of[p]
         b.pending -= 1
         if b.pending == 0:

@@ -54,10 +54,11 @@ def init_distributed(backend: str | None = None) -> DistEnv:
 
 class Trainer:
     def __init__(self, model_name: str, seq_len: int, micro_batch: int, device, lr: float = 3e-4,
-                 seed: int = 0, bucket_numel: int = 256 * 1024 * 1024):
+                 seed: int = 0, bucket_numel: int = 256 * 1024 * 1024, grad_accum: int = 1):
         self.cfg = CONFIGS[model_name]
         self.seq_len = seq_len
         self.micro_batch = micro_batch
+        self.grad_accum = grad_accum
         self.device = device
         dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
         with torch.device(device):
@@ -78,16 +79,22 @@ class Trainer:
         return row[:, :-1], row[:, 1:]
 
     def step(self) -> torch.Tensor:
-        tokens, targets = self.batch()
+        """One optimizer step = ``grad_accum`` micro-batches; the gradient reduce-scatter is armed
+        only for the last micro-batch so it overlaps that backward."""
         self.opt.zero_grad()
-        loss = self.model.loss(tokens, targets)
-        loss.backward()
+        total = None
+        for i in range(self.grad_accum):
+            tokens, targets = self.batch()
+            self.opt.sync_grads = i == self.grad_accum - 1
+            loss = self.model.loss(tokens, targets)
+            (loss / self.grad_accum if self.grad_accum > 1 else loss).backward()
+            total = loss.detach() if total is None else total + loss.detach()
         self.opt.step()
-        return loss.detach()
+        return total / self.grad_accum
 
     @property
     def tokens_per_step(self) -> int:
-        return self.micro_batch * self.seq_len
+        return self.micro_batch * self.seq_len * self.grad_accum
 
 
 def _sync(env: DistEnv):
@@ -97,11 +104,12 @@ def _sync(env: DistEnv):
         torch.cuda.synchronize()
 
 
-def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1):
+def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1,
+        grad_accum: int = 1):
     env = init_distributed()
     device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     t0 = time.time()
-    tr = Trainer(model, seq_len, micro_batch, device)
+    tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum)
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
               f"init={time.time()-t0:.1f}s", flush=True)
@@ -129,6 +137,7 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         "world": env.world,
         "flops_per_token": tr.cfg.flops_per_token(seq_len),
         "final_loss": losses[-1].item() if losses else None,
+        "max_mem_gb": torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else None,
     }
     result["tflops_per_gpu"] = tok_s / env.world * result["flops_per_token"] / 1e12
     if env.rank == 0:
@@ -143,8 +152,10 @@ def main(argv=None):
     ap.add_argument("--micro-batch", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--grad-accum", type=int, default=1)
     args = ap.parse_args(argv)
-    env, _, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup)
+    env, _, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup,
+                    grad_accum=args.grad_accum)
     if env.distributed:
         dist.destroy_process_group()
 
