@@ -1,0 +1,58 @@
+"""Server settings from the environment (reference: ``S/settings.py:1-73``)."""
+
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+
+def _env_bool(name: str, default: bool = False) -> bool:
+    v = os.getenv(name)
+    if v is None:
+        return default
+    return v.strip().lower() in ("1", "true", "yes", "on")
+
+
+DSTACK_DIR_PATH = Path(os.getenv("DSTACK_DIR", Path.home() / ".dstack"))
+SERVER_DIR_PATH = Path(os.getenv("DSTACK_SERVER_DIR", DSTACK_DIR_PATH / "server"))
+SERVER_CONFIG_FILE_PATH = SERVER_DIR_PATH / "config.yml"
+SERVER_DATA_DIR_PATH = SERVER_DIR_PATH / "data"
+
+DATABASE_URL = os.getenv("DSTACK_DATABASE_URL", f"sqlite:///{SERVER_DATA_DIR_PATH}/sqlite.db")
+DB_POOL_SIZE = int(os.getenv("DSTACK_DB_POOL_SIZE", "20"))
+
+SERVER_HOST = os.getenv("DSTACK_SERVER_HOST", "127.0.0.1")
+SERVER_PORT = int(os.getenv("DSTACK_SERVER_PORT", "3000"))
+SERVER_URL = os.getenv("DSTACK_SERVER_URL", f"http://{SERVER_HOST}:{SERVER_PORT}")
+SERVER_ADMIN_TOKEN = os.getenv("DSTACK_SERVER_ADMIN_TOKEN")
+SERVER_LOG_LEVEL = os.getenv("DSTACK_SERVER_LOG_LEVEL", "INFO").upper()
+SERVER_LOG_FORMAT = os.getenv("DSTACK_SERVER_LOG_FORMAT", "standard")  # standard | json | rich
+
+SERVER_METRICS_TTL_SECONDS = int(os.getenv("DSTACK_SERVER_METRICS_TTL_SECONDS", "3600"))
+SERVER_METRICS_COLLECT_INTERVAL = float(os.getenv("DSTACK_SERVER_METRICS_COLLECT_INTERVAL", "10"))
+SERVER_BACKGROUND_PROCESSING_ENABLED = not _env_bool("DSTACK_SERVER_BACKGROUND_PROCESSING_DISABLED")
+# Event-driven scheduling: background tasks are woken on state changes; the interval is only the
+# fallback poll. Set to 0 to reproduce the reference's pure-polling behaviour.
+SERVER_EVENT_DRIVEN = not _env_bool("DSTACK_SERVER_POLLING_ONLY")
+
+SERVER_CLOUDWATCH_LOG_GROUP = os.getenv("DSTACK_SERVER_CLOUDWATCH_LOG_GROUP")
+SERVER_S3_BUCKET = os.getenv("DSTACK_SERVER_S3_BUCKET")
+SENTRY_DSN = os.getenv("DSTACK_SENTRY_DSN")
+SENTRY_TRACES_SAMPLE_RATE = float(os.getenv("DSTACK_SENTRY_TRACES_SAMPLE_RATE", "0.1"))
+
+DEFAULT_PROJECT_NAME = "main"
+LOCAL_BACKEND_ENABLED = _env_bool("DSTACK_LOCAL_BACKEND_ENABLED", True)
+# where the local backend finds the native agents
+SHIM_BINARY_PATH = os.getenv("DSTACK_SHIM_BINARY_PATH")
+RUNNER_BINARY_PATH = os.getenv("DSTACK_RUNNER_BINARY_PATH")
+RUNNER_DOWNLOAD_URL = os.getenv("DSTACK_RUNNER_DOWNLOAD_URL")
+SHIM_DOWNLOAD_URL = os.getenv("DSTACK_SHIM_DOWNLOAD_URL")
+
+SERVICE_CLIENT_MAX_BODY_SIZE = int(os.getenv("DSTACK_SERVICE_CLIENT_MAX_BODY_SIZE", str(64 * 1024 * 1024)))
+ACME_SERVER = os.getenv("DSTACK_ACME_SERVER")
+ACME_EAB_KID = os.getenv("DSTACK_ACME_EAB_KID")
+ACME_EAB_HMAC_KEY = os.getenv("DSTACK_ACME_EAB_HMAC_KEY")
+
+MAX_OFFERS_TRIED = int(os.getenv("DSTACK_SERVER_MAX_OFFERS_TRIED", "15"))
+MAX_PLAN_OFFERS = 50
+DEFAULT_RUNNER_TIMEOUT = 600

@@ -1,0 +1,690 @@
+// Implementation of net.h (see header).
+#include "net.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/sha.h>
+#include <poll.h>
+#include <signal.h>
+#include <stdarg.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/time.h>
+#include <sys/un.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+namespace dsa {
+
+// ---------------------------------------------------------------------------------------------
+// logging
+// ---------------------------------------------------------------------------------------------
+static std::atomic<int> g_log_level{LOG_INFO};
+static std::mutex g_log_mu;
+
+void set_log_level(int level) { g_log_level = level; }
+int log_level() { return g_log_level; }
+
+void logf(int level, const char* fmt, ...) {
+  if (level > g_log_level) return;
+  static const char* names[] = {"", "", "ERROR", "WARN", "INFO", "DEBUG", "TRACE"};
+  char ts[64];
+  struct timeval tv;
+  gettimeofday(&tv, nullptr);
+  struct tm tmv;
+  gmtime_r(&tv.tv_sec, &tmv);
+  snprintf(ts, sizeof ts, "%04d-%02d-%02dT%02d:%02d:%02d.%03ldZ", tmv.tm_year + 1900, tmv.tm_mon + 1,
+           tmv.tm_mday, tmv.tm_hour, tmv.tm_min, tmv.tm_sec, (long)(tv.tv_usec / 1000));
+  char msg[4096];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(msg, sizeof msg, fmt, ap);
+  va_end(ap);
+  std::lock_guard<std::mutex> lk(g_log_mu);
+  fprintf(stderr, "%s %-5s %s\n", ts, names[level < 7 ? level : 6], msg);
+  fflush(stderr);
+}
+
+// ---------------------------------------------------------------------------------------------
+// utils
+// ---------------------------------------------------------------------------------------------
+static const char* B64 = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+
+std::string base64_encode(const std::string& in) {
+  std::string out;
+  out.reserve((in.size() + 2) / 3 * 4);
+  size_t i = 0;
+  while (i + 2 < in.size()) {
+    uint32_t v = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8) | (uint8_t)in[i + 2];
+    out.push_back(B64[(v >> 18) & 63]);
+    out.push_back(B64[(v >> 12) & 63]);
+    out.push_back(B64[(v >> 6) & 63]);
+    out.push_back(B64[v & 63]);
+    i += 3;
+  }
+  if (i + 1 == in.size()) {
+    uint32_t v = ((uint8_t)in[i] << 16);
+    out.push_back(B64[(v >> 18) & 63]);
+    out.push_back(B64[(v >> 12) & 63]);
+    out += "==";
+  } else if (i + 2 == in.size()) {
+    uint32_t v = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8);
+    out.push_back(B64[(v >> 18) & 63]);
+    out.push_back(B64[(v >> 12) & 63]);
+    out.push_back(B64[(v >> 6) & 63]);
+    out.push_back('=');
+  }
+  return out;
+}
+
+std::string base64_decode(const std::string& in) {
+  int T[256];
+  for (int k = 0; k < 256; ++k) T[k] = -1;
+  for (int k = 0; k < 64; ++k) T[(uint8_t)B64[k]] = k;
+  T[(uint8_t)'-'] = 62;
+  T[(uint8_t)'_'] = 63;
+  std::string out;
+  uint32_t v = 0;
+  int bits = -8;
+  for (unsigned char c : in) {
+    if (T[c] < 0) continue;
+    v = (v << 6) | T[c];
+    bits += 6;
+    if (bits >= 0) {
+      out.push_back((char)((v >> bits) & 0xFF));
+      bits -= 8;
+    }
+  }
+  return out;
+}
+
+int64_t now_micros() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+int64_t now_millis() { return now_micros() / 1000; }
+
+std::string url_decode(const std::string& s) {
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size()) {
+      out.push_back((char)std::stoi(s.substr(i + 1, 2), nullptr, 16));
+      i += 2;
+    } else if (s[i] == '+') {
+      out.push_back(' ');
+    } else {
+      out.push_back(s[i]);
+    }
+  }
+  return out;
+}
+
+std::string to_lower(std::string s) {
+  for (auto& c : s) c = (char)tolower((unsigned char)c);
+  return s;
+}
+
+std::vector<std::string> split(const std::string& s, char sep) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (char c : s) {
+    if (c == sep) {
+      out.push_back(cur);
+      cur.clear();
+    } else {
+      cur.push_back(c);
+    }
+  }
+  out.push_back(cur);
+  return out;
+}
+
+std::string trim(const std::string& s) {
+  size_t a = s.find_first_not_of(" \t\r\n");
+  if (a == std::string::npos) return "";
+  size_t b = s.find_last_not_of(" \t\r\n");
+  return s.substr(a, b - a + 1);
+}
+
+bool read_file(const std::string& path, std::string& out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  out = ss.str();
+  return true;
+}
+
+bool write_file(const std::string& path, const std::string& data, int mode) {
+  std::string tmp = path + ".tmp";
+  {
+    std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+    if (!f) return false;
+    f << data;
+  }
+  chmod(tmp.c_str(), mode);
+  return rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+bool mkdirs(const std::string& path, int mode) {
+  if (path.empty()) return false;
+  std::string cur;
+  for (auto& part : split(path, '/')) {
+    if (part.empty()) {
+      if (cur.empty()) cur = "/";
+      continue;
+    }
+    if (!cur.empty() && cur.back() != '/') cur.push_back('/');
+    cur += part;
+    if (mkdir(cur.c_str(), mode) != 0 && errno != EEXIST) return false;
+  }
+  return true;
+}
+
+bool path_exists(const std::string& path) {
+  struct stat st;
+  return stat(path.c_str(), &st) == 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// request / response helpers
+// ---------------------------------------------------------------------------------------------
+std::string HttpRequest::header(const std::string& k, const std::string& def) const {
+  auto it = headers.find(to_lower(k));
+  return it == headers.end() ? def : it->second;
+}
+std::string HttpRequest::q(const std::string& k, const std::string& def) const {
+  auto it = query.find(k);
+  return it == query.end() ? def : it->second;
+}
+Json HttpRequest::json() const { return body.empty() ? Json::object() : Json::parse(body); }
+
+HttpResponse HttpResponse::json(const Json& j, int status) {
+  HttpResponse r;
+  r.status = status;
+  r.headers["Content-Type"] = "application/json";
+  r.body = j.dump();
+  return r;
+}
+HttpResponse HttpResponse::text(const std::string& t, int status) {
+  HttpResponse r;
+  r.status = status;
+  r.headers["Content-Type"] = "text/plain";
+  r.body = t;
+  return r;
+}
+HttpResponse HttpResponse::error(int status, const std::string& msg) {
+  Json j = Json::object();
+  j.set("error", msg);
+  return json(j, status);
+}
+
+static const char* status_text(int s) {
+  switch (s) {
+    case 101: return "Switching Protocols";
+    case 200: return "OK";
+    case 201: return "Created";
+    case 204: return "No Content";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 403: return "Forbidden";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 409: return "Conflict";
+    case 413: return "Payload Too Large";
+    case 500: return "Internal Server Error";
+    case 503: return "Service Unavailable";
+    default: return "Status";
+  }
+}
+
+static bool send_all(int fd, const char* p, size_t n) {
+  while (n > 0) {
+    ssize_t w = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
+// buffered reader over a socket
+struct SockReader {
+  int fd;
+  std::string buf;
+  size_t pos = 0;
+  int timeout_ms;
+  bool fill() {
+    if (pos > 0 && pos == buf.size()) {
+      buf.clear();
+      pos = 0;
+    }
+    struct pollfd p{fd, POLLIN, 0};
+    int r = ::poll(&p, 1, timeout_ms);
+    if (r <= 0) return false;
+    char tmp[65536];
+    ssize_t n = ::recv(fd, tmp, sizeof tmp, 0);
+    if (n <= 0) return false;
+    buf.append(tmp, (size_t)n);
+    return true;
+  }
+  bool read_line(std::string& line) {
+    while (true) {
+      size_t e = buf.find("\r\n", pos);
+      if (e != std::string::npos) {
+        line = buf.substr(pos, e - pos);
+        pos = e + 2;
+        return true;
+      }
+      if (buf.size() - pos > 1 << 20) return false;
+      if (!fill()) return false;
+    }
+  }
+  bool read_n(size_t n, std::string& out) {
+    while (buf.size() - pos < n)
+      if (!fill()) return false;
+    out = buf.substr(pos, n);
+    pos += n;
+    return true;
+  }
+  bool read_some(std::string& out) {
+    if (buf.size() == pos && !fill()) return false;
+    out = buf.substr(pos);
+    pos = buf.size();
+    return true;
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// WebSocket (server side, RFC 6455; unmasked frames from server)
+// ---------------------------------------------------------------------------------------------
+bool WsConn::send_frame(int opcode, const std::string& data) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (closed_) return false;
+  std::string h;
+  h.push_back((char)(0x80 | opcode));
+  size_t n = data.size();
+  if (n < 126) {
+    h.push_back((char)n);
+  } else if (n < 65536) {
+    h.push_back((char)126);
+    h.push_back((char)((n >> 8) & 0xFF));
+    h.push_back((char)(n & 0xFF));
+  } else {
+    h.push_back((char)127);
+    for (int k = 7; k >= 0; --k) h.push_back((char)((n >> (8 * k)) & 0xFF));
+  }
+  if (!send_all(fd_, h.data(), h.size()) || !send_all(fd_, data.data(), data.size())) {
+    closed_ = true;
+    return false;
+  }
+  return true;
+}
+
+void WsConn::close(int code) {
+  std::string payload;
+  payload.push_back((char)((code >> 8) & 0xFF));
+  payload.push_back((char)(code & 0xFF));
+  send_frame(0x8, payload);
+  std::lock_guard<std::mutex> lk(mu_);
+  closed_ = true;
+}
+
+bool WsConn::poll_peer(int timeout_ms) {
+  if (closed_) return false;
+  struct pollfd p{fd_, POLLIN, 0};
+  int r = ::poll(&p, 1, timeout_ms);
+  if (r <= 0) return true;  // nothing from the peer
+  char buf[4096];
+  ssize_t n = ::recv(fd_, buf, sizeof buf, MSG_DONTWAIT);
+  if (n <= 0) {
+    closed_ = true;
+    return false;
+  }
+  // a close frame from the client (opcode 8) ends the stream; other frames are ignored
+  if ((buf[0] & 0x0F) == 0x8) {
+    closed_ = true;
+    return false;
+  }
+  return true;
+}
+
+static std::string ws_accept_key(const std::string& key) {
+  std::string s = key + "258EAFA5-E914-47DA-95CA-C5AB0DC85B11";
+  unsigned char dig[SHA_DIGEST_LENGTH];
+  SHA1((const unsigned char*)s.data(), s.size(), dig);
+  return base64_encode(std::string((const char*)dig, SHA_DIGEST_LENGTH));
+}
+
+// ---------------------------------------------------------------------------------------------
+// server
+// ---------------------------------------------------------------------------------------------
+HttpServer::~HttpServer() { stop(); }
+
+static std::vector<std::string> path_parts(const std::string& p) {
+  std::vector<std::string> out;
+  for (auto& s : split(p, '/'))
+    if (!s.empty()) out.push_back(s);
+  return out;
+}
+
+void HttpServer::route(const std::string& method, const std::string& pattern, HttpHandler h) {
+  routes_.push_back(Route{method, path_parts(pattern), std::move(h), nullptr});
+}
+
+void HttpServer::websocket(const std::string& pattern, WsHandler h) {
+  routes_.push_back(Route{"WS", path_parts(pattern), nullptr, std::move(h)});
+}
+
+bool HttpServer::match(const Route& r, const std::string& path, std::map<std::string, std::string>& params) const {
+  auto parts = path_parts(path);
+  if (parts.size() != r.parts.size()) return false;
+  for (size_t k = 0; k < parts.size(); ++k) {
+    const auto& rp = r.parts[k];
+    if (rp.size() > 2 && rp.front() == '{' && rp.back() == '}') {
+      params[rp.substr(1, rp.size() - 2)] = url_decode(parts[k]);
+    } else if (rp != parts[k]) {
+      return false;
+    }
+  }
+  return true;
+}
+
+int HttpServer::start() {
+  signal(SIGPIPE, SIG_IGN);
+  listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+  if (listen_fd_ < 0) return -1;
+  int one = 1;
+  setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  struct sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons((uint16_t)port_);
+  if (inet_pton(AF_INET, host_.c_str(), &addr.sin_addr) != 1) addr.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (::bind(listen_fd_, (struct sockaddr*)&addr, sizeof addr) != 0) {
+    LOGE("bind %s:%d failed: %s", host_.c_str(), port_, strerror(errno));
+    ::close(listen_fd_);
+    listen_fd_ = -1;
+    return -1;
+  }
+  if (::listen(listen_fd_, 128) != 0) return -1;
+  socklen_t len = sizeof addr;
+  getsockname(listen_fd_, (struct sockaddr*)&addr, &len);
+  port_ = ntohs(addr.sin_port);
+  running_ = true;
+  return port_;
+}
+
+void HttpServer::serve_forever() {
+  while (running_) {
+    struct pollfd p{listen_fd_, POLLIN, 0};
+    int r = ::poll(&p, 1, 200);
+    if (r <= 0) continue;
+    struct sockaddr_in caddr{};
+    socklen_t clen = sizeof caddr;
+    int fd = ::accept(listen_fd_, (struct sockaddr*)&caddr, &clen);
+    if (fd < 0) continue;
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    char ip[64];
+    inet_ntop(AF_INET, &caddr.sin_addr, ip, sizeof ip);
+    std::thread(&HttpServer::handle_conn, this, fd, std::string(ip)).detach();
+  }
+}
+
+void HttpServer::stop() {
+  running_ = false;
+  if (listen_fd_ >= 0) {
+    ::shutdown(listen_fd_, SHUT_RDWR);
+    ::close(listen_fd_);
+    listen_fd_ = -1;
+  }
+}
+
+static void parse_query(const std::string& qs, std::map<std::string, std::string>& out) {
+  for (auto& kv : split(qs, '&')) {
+    if (kv.empty()) continue;
+    auto eq = kv.find('=');
+    if (eq == std::string::npos)
+      out[url_decode(kv)] = "";
+    else
+      out[url_decode(kv.substr(0, eq))] = url_decode(kv.substr(eq + 1));
+  }
+}
+
+void HttpServer::handle_conn(int fd, std::string remote) {
+  SockReader rd{fd, {}, 0, 120000};
+  while (running_) {
+    std::string line;
+    if (!rd.read_line(line)) break;
+    if (line.empty()) continue;
+    HttpRequest req;
+    req.remote_addr = remote;
+    auto sp1 = line.find(' '), sp2 = line.rfind(' ');
+    if (sp1 == std::string::npos || sp2 == sp1) break;
+    req.method = line.substr(0, sp1);
+    std::string target = line.substr(sp1 + 1, sp2 - sp1 - 1);
+    auto qm = target.find('?');
+    req.path = qm == std::string::npos ? target : target.substr(0, qm);
+    if (qm != std::string::npos) parse_query(target.substr(qm + 1), req.query);
+    bool bad = false;
+    while (true) {
+      if (!rd.read_line(line)) {
+        bad = true;
+        break;
+      }
+      if (line.empty()) break;
+      auto c = line.find(':');
+      if (c != std::string::npos) req.headers[to_lower(trim(line.substr(0, c)))] = trim(line.substr(c + 1));
+    }
+    if (bad) break;
+    size_t clen = 0;
+    if (req.headers.count("content-length")) clen = (size_t)std::stoull(req.headers["content-length"]);
+    if (clen > (size_t)512 << 20) {
+      auto r = HttpResponse::error(413, "body too large");
+      std::string out = "HTTP/1.1 413 Payload Too Large\r\nContent-Length: " + std::to_string(r.body.size()) +
+                        "\r\nConnection: close\r\n\r\n" + r.body;
+      send_all(fd, out.data(), out.size());
+      break;
+    }
+    if (clen > 0 && !rd.read_n(clen, req.body)) break;
+    bool keep_alive = to_lower(req.header("connection")) != "close";
+
+    // WebSocket upgrade
+    if (to_lower(req.header("upgrade")) == "websocket") {
+      for (auto& r : routes_) {
+        if (r.method != "WS") continue;
+        std::map<std::string, std::string> params;
+        if (!match(r, req.path, params)) continue;
+        req.params = params;
+        std::string resp = "HTTP/1.1 101 Switching Protocols\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+                           "Sec-WebSocket-Accept: " +
+                           ws_accept_key(req.header("sec-websocket-key")) + "\r\n\r\n";
+        send_all(fd, resp.data(), resp.size());
+        WsConn ws(fd);
+        try {
+          r.ws(req, ws);
+        } catch (const std::exception& e) {
+          LOGW("websocket handler error: %s", e.what());
+        }
+        if (!ws.closed()) ws.close();
+        ::close(fd);
+        return;
+      }
+    }
+
+    HttpResponse resp;
+    bool found = false, method_mismatch = false;
+    for (auto& r : routes_) {
+      if (r.method == "WS") continue;
+      std::map<std::string, std::string> params;
+      if (!match(r, req.path, params)) continue;
+      if (r.method != req.method) {
+        method_mismatch = true;
+        continue;
+      }
+      found = true;
+      req.params = params;
+      try {
+        resp = r.handler(req);
+      } catch (const std::exception& e) {
+        resp = HttpResponse::error(500, e.what());
+      }
+      break;
+    }
+    if (!found) resp = method_mismatch ? HttpResponse::error(405, "method not allowed") : HttpResponse::error(404, "not found");
+    LOGD("%s %s -> %d", req.method.c_str(), req.path.c_str(), resp.status);
+    std::string out = "HTTP/1.1 " + std::to_string(resp.status) + " " + status_text(resp.status) + "\r\n";
+    for (auto& h : resp.headers) out += h.first + ": " + h.second + "\r\n";
+    out += "Content-Length: " + std::to_string(resp.body.size()) + "\r\n";
+    out += keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
+    out += resp.body;
+    if (!send_all(fd, out.data(), out.size()) || !keep_alive) break;
+  }
+  ::close(fd);
+}
+
+// ---------------------------------------------------------------------------------------------
+// client
+// ---------------------------------------------------------------------------------------------
+static int connect_tcp(const std::string& host, int port, int timeout_ms, std::string& err) {
+  struct addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res) {
+    err = "resolve failed: " + host;
+    return -1;
+  }
+  int fd = -1;
+  for (auto* ai = res; ai; ai = ai->ai_next) {
+    fd = ::socket(ai->ai_family, ai->ai_socktype, ai->ai_protocol);
+    if (fd < 0) continue;
+    int fl = fcntl(fd, F_GETFL, 0);
+    fcntl(fd, F_SETFL, fl | O_NONBLOCK);
+    int r = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
+    if (r != 0 && errno == EINPROGRESS) {
+      struct pollfd p{fd, POLLOUT, 0};
+      if (::poll(&p, 1, timeout_ms) == 1) {
+        int so = 0;
+        socklen_t sl = sizeof so;
+        getsockopt(fd, SOL_SOCKET, SO_ERROR, &so, &sl);
+        r = so == 0 ? 0 : -1;
+      } else {
+        r = -1;
+      }
+    }
+    if (r == 0) {
+      fcntl(fd, F_SETFL, fl);
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      break;
+    }
+    ::close(fd);
+    fd = -1;
+  }
+  freeaddrinfo(res);
+  if (fd < 0) err = "connect failed: " + host + ":" + std::to_string(port);
+  return fd;
+}
+
+static int connect_unix(const std::string& path, std::string& err) {
+  int fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
+  struct sockaddr_un addr{};
+  addr.sun_family = AF_UNIX;
+  strncpy(addr.sun_path, path.c_str(), sizeof(addr.sun_path) - 1);
+  if (::connect(fd, (struct sockaddr*)&addr, sizeof addr) != 0) {
+    err = "connect unix socket failed: " + path;
+    ::close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+HttpClientResponse http_request(const HttpClientRequest& req) {
+  HttpClientResponse resp;
+  int fd = req.unix_socket.empty() ? connect_tcp(req.host, req.port, req.timeout_ms, resp.error)
+                                   : connect_unix(req.unix_socket, resp.error);
+  if (fd < 0) return resp;
+  std::string out = req.method + " " + req.path + " HTTP/1.1\r\n";
+  out += "Host: " + (req.unix_socket.empty() ? req.host : std::string("docker")) + "\r\n";
+  bool has_ct = false;
+  for (auto& h : req.headers) {
+    out += h.first + ": " + h.second + "\r\n";
+    if (to_lower(h.first) == "content-type") has_ct = true;
+  }
+  if (!req.body.empty() && !has_ct) out += "Content-Type: application/json\r\n";
+  out += "Content-Length: " + std::to_string(req.body.size()) + "\r\nConnection: close\r\n\r\n";
+  out += req.body;
+  if (!send_all(fd, out.data(), out.size())) {
+    resp.error = "send failed";
+    ::close(fd);
+    return resp;
+  }
+  SockReader rd{fd, {}, 0, req.timeout_ms};
+  std::string line;
+  if (!rd.read_line(line)) {
+    resp.error = "no response";
+    ::close(fd);
+    return resp;
+  }
+  auto sp = line.find(' ');
+  resp.status = sp == std::string::npos ? 0 : atoi(line.c_str() + sp + 1);
+  while (rd.read_line(line) && !line.empty()) {
+    auto c = line.find(':');
+    if (c != std::string::npos) resp.headers[to_lower(trim(line.substr(0, c)))] = trim(line.substr(c + 1));
+  }
+  auto emit = [&](const std::string& chunk) -> bool {
+    if (req.on_chunk) return req.on_chunk(chunk);
+    resp.body += chunk;
+    return true;
+  };
+  if (to_lower(resp.headers["transfer-encoding"]).find("chunked") != std::string::npos) {
+    while (rd.read_line(line)) {
+      size_t n = strtoul(line.c_str(), nullptr, 16);
+      if (n == 0) break;
+      std::string chunk;
+      if (!rd.read_n(n, chunk)) break;
+      if (!emit(chunk)) break;
+      rd.read_line(line);  // CRLF after chunk
+    }
+  } else if (resp.headers.count("content-length")) {
+    size_t n = (size_t)std::stoull(resp.headers["content-length"]);
+    std::string body;
+    if (n > 0 && rd.read_n(n, body)) emit(body);
+  } else if (resp.status != 204 && resp.status != 101) {
+    std::string chunk;
+    while (rd.read_some(chunk))
+      if (!emit(chunk)) break;
+  }
+  ::close(fd);
+  return resp;
+}
+
+HttpClientResponse http_get_url(const std::string& url, int timeout_ms) {
+  HttpClientRequest req;
+  req.timeout_ms = timeout_ms;
+  std::string u = url;
+  if (u.rfind("http://", 0) == 0) u = u.substr(7);
+  auto slash = u.find('/');
+  std::string hostport = slash == std::string::npos ? u : u.substr(0, slash);
+  req.path = slash == std::string::npos ? "/" : u.substr(slash);
+  auto colon = hostport.find(':');
+  req.host = colon == std::string::npos ? hostport : hostport.substr(0, colon);
+  req.port = colon == std::string::npos ? 80 : atoi(hostport.c_str() + colon + 1);
+  return http_request(req);
+}
+
+}  // namespace dsa

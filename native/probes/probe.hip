@@ -1,0 +1,276 @@
+// dstack-probe: per-GPU health probes for MI355X hosts (hand-written HIP, gfx950).
+//
+//   dstack-probe [--quick] [--json] [--hbm] [--mfma] [--xgmi] [--rccl] [--device N]
+//
+// * HBM:  streaming copy over 2 x 1 GiB buffers, 16-byte (dwordx4) loads/stores, grid-stride,
+//         grid = 8 blocks/CU -> achieved TB/s (MI355X measured ceiling ~6.3 TB/s, spec 8).
+// * MFMA: register-resident bf16 (v_mfma_f32_32x32x16_bf16) and fp8 (32x32x16_fp8_fp8) loops,
+//         4 independent accumulators per wave, 4 waves per CU on every CU -> dense TFLOPS and the
+//         implied clock; a throttled or faulty GPU shows up as a low number.
+// * xGMI: hipMemcpyPeerAsync of 256 MiB for every ordered GPU pair -> GB/s matrix (a healthy
+//         MI355X link moves ~100+ GB/s one-way; PCIe-routed pairs are far slower).
+// * RCCL: all-reduce bf16 sweep across all visible GPUs (see rccl_probe.cpp).
+// Results are one JSON document; exit status 1 if any GPU falls below the health thresholds.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                                    \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess) {                                                                      \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);     \
+      exit(2);                                                                                   \
+    }                                                                                            \
+  } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void copy_kernel(const f4* __restrict__ src, f4* __restrict__ dst, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = __builtin_nontemporal_load(src + i);
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(f4* __restrict__ dst, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = f4{1.f, 2.f, 3.f, (float)(i & 1023)};
+}
+
+// bf16 MFMA loop: 4 independent 32x32 accumulators per wave; operands derived from the lane id so
+// the compiler cannot constant-fold; the checksum store keeps everything live.
+__global__ __launch_bounds__(256) void mfma_bf16_kernel(float* out, int iters) {
+  const int lane = threadIdx.x & 63;
+  bf16x8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (__bf16)(0.001f * (float)((lane + j) & 7));
+    b[j] = (__bf16)(0.002f * (float)((lane * 3 + j) & 7));
+  }
+  f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c3, 0, 0, 0);
+  }
+  float s = 0.f;
+  for (int r = 0; r < 16; ++r) s += c0[r] + c1[r] + c2[r] + c3[r];
+  if (s == 1234.5f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;  // never true; keeps MFMAs live
+}
+
+__global__ __launch_bounds__(256) void mfma_fp8_kernel(float* out, int iters) {
+  const int lane = threadIdx.x & 63;
+  long a = 0x3830282018100800L + lane, b = 0x3931292119110901L + lane * 7;
+  f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c3, 0, 0, 0);
+  }
+  float s = 0.f;
+  for (int r = 0; r < 16; ++r) s += c0[r] + c1[r] + c2[r] + c3[r];
+  if (s == 1234.5f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+static float time_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return ms;
+}
+
+static double hbm_probe(int dev, bool quick) {
+  CK(hipSetDevice(dev));
+  hipDeviceProp_t p;
+  CK(hipGetDeviceProperties(&p, dev));
+  size_t bytes = (quick ? 256ull : 1024ull) << 20;
+  size_t n = bytes / sizeof(f4);
+  f4 *a, *b;
+  CK(hipMalloc(&a, bytes));
+  CK(hipMalloc(&b, bytes));
+  int grid = p.multiProcessorCount * 8;
+  fill_kernel<<<grid, 256>>>(a, n);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  copy_kernel<<<grid, 256>>>(a, b, n);  // warm
+  const int reps = quick ? 5 : 20;
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) copy_kernel<<<grid, 256>>>(r & 1 ? b : a, r & 1 ? a : b, n);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  double tb_s = 2.0 * bytes * reps / (time_ms(e0, e1) * 1e-3) / 1e12;
+  CK(hipFree(a));
+  CK(hipFree(b));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return tb_s;
+}
+
+static double mfma_probe(int dev, bool quick, bool fp8) {
+  CK(hipSetDevice(dev));
+  hipDeviceProp_t p;
+  CK(hipGetDeviceProperties(&p, dev));
+  float* out;
+  CK(hipMalloc(&out, (size_t)p.multiProcessorCount * 256 * 4 * sizeof(float)));
+  const int iters = quick ? 20000 : 100000;
+  const int blocks = p.multiProcessorCount * 2;  // 2 blocks x 4 waves per CU = 2 waves per SIMD
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto launch = [&](int it) {
+    if (fp8)
+      mfma_fp8_kernel<<<blocks, 256>>>(out, it);
+    else
+      mfma_bf16_kernel<<<blocks, 256>>>(out, it);
+  };
+  launch(1000);
+  CK(hipEventRecord(e0));
+  launch(iters);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  // 32x32x16 MFMA = 2*32*32*16 FLOP; 4 per iteration per wave; 4 waves per block
+  double flops = 2.0 * 32 * 32 * 16 * 4.0 * iters * 4.0 * blocks;
+  double tflops = flops / (time_ms(e0, e1) * 1e-3) / 1e12;
+  CK(hipFree(out));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return tflops;
+}
+
+static std::vector<std::vector<double>> xgmi_probe(int ndev, bool quick) {
+  std::vector<std::vector<double>> m((size_t)ndev, std::vector<double>((size_t)ndev, 0.0));
+  size_t bytes = (quick ? 64ull : 256ull) << 20;
+  std::vector<void*> buf((size_t)ndev);
+  for (int d = 0; d < ndev; ++d) {
+    CK(hipSetDevice(d));
+    CK(hipMalloc(&buf[(size_t)d], bytes));
+    for (int e = 0; e < ndev; ++e) {
+      if (e == d) continue;
+      int can = 0;
+      CK(hipDeviceCanAccessPeer(&can, d, e));
+      if (can) (void)hipDeviceEnablePeerAccess(e, 0);
+    }
+  }
+  (void)hipGetLastError();
+  for (int s = 0; s < ndev; ++s)
+    for (int d = 0; d < ndev; ++d) {
+      if (s == d) continue;
+      CK(hipSetDevice(s));
+      hipStream_t st;
+      CK(hipStreamCreate(&st));
+      hipEvent_t e0, e1;
+      CK(hipEventCreate(&e0));
+      CK(hipEventCreate(&e1));
+      CK(hipMemcpyPeerAsync(buf[(size_t)d], d, buf[(size_t)s], s, bytes, st));
+      const int reps = quick ? 3 : 10;
+      CK(hipEventRecord(e0, st));
+      for (int r = 0; r < reps; ++r) CK(hipMemcpyPeerAsync(buf[(size_t)d], d, buf[(size_t)s], s, bytes, st));
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      m[(size_t)s][(size_t)d] = (double)bytes * reps / (time_ms(e0, e1) * 1e-3) / 1e9;
+      CK(hipEventDestroy(e0));
+      CK(hipEventDestroy(e1));
+      CK(hipStreamDestroy(st));
+    }
+  for (int d = 0; d < ndev; ++d) {
+    CK(hipSetDevice(d));
+    CK(hipFree(buf[(size_t)d]));
+  }
+  return m;
+}
+
+// rccl_probe.cpp
+std::string rccl_allreduce_probe(int ndev, bool quick, double* best_busbw);
+
+int main(int argc, char** argv) {
+  bool quick = false, json = false, want_hbm = false, want_mfma = false, want_xgmi = false, want_rccl = false;
+  int only_dev = -1;
+  double min_hbm = 2.0, min_mfma = 500.0;  // TB/s, TFLOPS: well below a healthy MI355X
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--quick") quick = true;
+    else if (a == "--json") json = true;
+    else if (a == "--hbm") want_hbm = true;
+    else if (a == "--mfma") want_mfma = true;
+    else if (a == "--xgmi") want_xgmi = true;
+    else if (a == "--rccl") want_rccl = true;
+    else if (a == "--device" && i + 1 < argc) only_dev = atoi(argv[++i]);
+    else if (a == "--min-hbm-tbs" && i + 1 < argc) min_hbm = atof(argv[++i]);
+    else if (a == "--min-mfma-tflops" && i + 1 < argc) min_mfma = atof(argv[++i]);
+    else {
+      fprintf(stderr, "usage: dstack-probe [--quick] [--json] [--hbm] [--mfma] [--xgmi] [--rccl] [--device N]\n");
+      return 2;
+    }
+  }
+  if (!want_hbm && !want_mfma && !want_xgmi && !want_rccl) want_hbm = want_mfma = want_xgmi = true;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    printf("{\"healthy\": false, \"message\": \"no HIP devices\"}\n");
+    return 1;
+  }
+  std::string out = "{";
+  bool healthy = true;
+  std::vector<int> devs;
+  for (int d = 0; d < ndev; ++d)
+    if (only_dev < 0 || d == only_dev) devs.push_back(d);
+  char buf[256];
+  if (want_hbm) {
+    out += "\"hbm_tb_s\": [";
+    for (size_t k = 0; k < devs.size(); ++k) {
+      double v = hbm_probe(devs[k], quick);
+      if (v < min_hbm) healthy = false;
+      snprintf(buf, sizeof buf, "%s%.3f", k ? ", " : "", v);
+      out += buf;
+    }
+    out += "], ";
+  }
+  if (want_mfma) {
+    out += "\"mfma_bf16_tflops\": [";
+    for (size_t k = 0; k < devs.size(); ++k) {
+      double v = mfma_probe(devs[k], quick, false);
+      if (v < min_mfma) healthy = false;
+      snprintf(buf, sizeof buf, "%s%.1f", k ? ", " : "", v);
+      out += buf;
+    }
+    out += "], \"mfma_fp8_tflops\": [";
+    for (size_t k = 0; k < devs.size(); ++k) {
+      snprintf(buf, sizeof buf, "%s%.1f", k ? ", " : "", mfma_probe(devs[k], quick, true));
+      out += buf;
+    }
+    out += "], ";
+  }
+  if (want_xgmi && ndev > 1 && only_dev < 0) {
+    auto m = xgmi_probe(ndev, quick);
+    out += "\"xgmi_gb_s\": [";
+    for (int s = 0; s < ndev; ++s) {
+      out += s ? ", [" : "[";
+      for (int d = 0; d < ndev; ++d) {
+        snprintf(buf, sizeof buf, "%s%.1f", d ? ", " : "", m[(size_t)s][(size_t)d]);
+        out += buf;
+      }
+      out += "]";
+    }
+    out += "], ";
+  }
+  if (want_rccl && ndev > 1 && only_dev < 0) {
+    double best = 0;
+    out += "\"rccl\": " + rccl_allreduce_probe(ndev, quick, &best) + ", ";
+    snprintf(buf, sizeof buf, "\"rccl_busbw_gb_s\": %.1f, ", best);
+    out += buf;
+  }
+  snprintf(buf, sizeof buf, "\"devices\": %d, \"healthy\": %s}", (int)devs.size(), healthy ? "true" : "false");
+  out += buf;
+  if (json)
+    printf("%s\n", out.c_str());
+  else
+    printf("dstack-probe: %s\n", out.c_str());
+  return healthy ? 0 : 1;
+}

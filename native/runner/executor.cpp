@@ -1,0 +1,609 @@
+// dstack-runner executor implementation (see executor.h).
+#include "executor.h"
+
+#include <arpa/inet.h>
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <grp.h>
+#include <ifaddrs.h>
+#include <net/if.h>
+#include <poll.h>
+#include <pty.h>
+#include <pwd.h>
+#include <signal.h>
+#include <stdarg.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <sstream>
+
+#include "../common/net.h"
+
+extern char** environ;
+
+namespace dsa {
+
+const char* exec_state_name(ExecState s) {
+  switch (s) {
+    case ExecState::WaitSubmit: return "wait_submit";
+    case ExecState::WaitCode: return "wait_code";
+    case ExecState::WaitRun: return "wait_run";
+    case ExecState::ServeLogs: return "serve_logs";
+    case ExecState::WaitLogsFinished: return "wait_logs_finished";
+  }
+  return "unknown";
+}
+
+// ------------------------------------------------------------------------------------------------
+// LogHistory
+// ------------------------------------------------------------------------------------------------
+void LogHistory::append(const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    int64_t ts = now_millis();
+    if (ts <= last_) ts = last_ + 1;  // strictly increasing surrogate timestamps (timestamp.go)
+    last_ = ts;
+    events_.push_back(LogEvent{ts, msg});
+  }
+  cv_.notify_all();
+}
+
+std::vector<LogEvent> LogHistory::after(int64_t ts, size_t limit) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = std::upper_bound(events_.begin(), events_.end(), ts,
+                             [](int64_t t, const LogEvent& e) { return t < e.timestamp; });
+  std::vector<LogEvent> out;
+  for (; it != events_.end() && out.size() < limit; ++it) out.push_back(*it);
+  return out;
+}
+
+int64_t LogHistory::last_timestamp() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return last_;
+}
+
+size_t LogHistory::size() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return events_.size();
+}
+
+bool LogHistory::wait_after(int64_t ts, int timeout_ms) const {
+  std::unique_lock<std::mutex> lk(mu_);
+  return cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return last_ > ts; });
+}
+
+// ------------------------------------------------------------------------------------------------
+// env interpolation: ${VAR} -> value, $$ -> $
+// ------------------------------------------------------------------------------------------------
+std::string interpolate_env(const std::string& s, const std::vector<std::pair<std::string, std::string>>& env,
+                            std::string* err) {
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] != '$') {
+      out.push_back(s[i]);
+      continue;
+    }
+    if (i + 1 < s.size() && s[i + 1] == '$') {
+      out.push_back('$');
+      ++i;
+      continue;
+    }
+    if (i + 1 < s.size() && s[i + 1] == '{') {
+      size_t e = s.find('}', i + 2);
+      if (e == std::string::npos) {
+        if (err) *err = "unterminated ${ in: " + s;
+        return s;
+      }
+      std::string name = s.substr(i + 2, e - i - 2);
+      std::string val;
+      for (auto it = env.rbegin(); it != env.rend(); ++it)
+        if (it->first == name) {
+          val = it->second;
+          break;
+        }
+      out += val;
+      i = e;
+      continue;
+    }
+    out.push_back('$');
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Executor
+// ------------------------------------------------------------------------------------------------
+Executor::Executor(RunnerOptions opts) : opts_(std::move(opts)) {
+  mkdirs(opts_.temp_dir);
+  code_path_ = opts_.temp_dir + "/code";
+}
+
+Executor::~Executor() {
+  stop();
+  if (worker_.joinable()) worker_.join();
+}
+
+void Executor::rlog(const char* fmt, ...) {
+  char buf[4096];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  LOGI("%s", buf);
+  runner_logs_.append(std::string(buf) + "\n");
+}
+
+void Executor::add_state(const std::string& state, const std::string& reason, const std::string& msg,
+                         int exit_status) {
+  std::lock_guard<std::mutex> lk(states_mu_);
+  int64_t ts = now_millis();
+  if (!states_.empty() && ts <= states_.back().timestamp) ts = states_.back().timestamp + 1;
+  states_.push_back(JobStateEvent{state, ts, reason, msg, exit_status});
+}
+
+std::string Executor::submit(const Json& body) {
+  if (state_ != ExecState::WaitSubmit) return std::string("submit not allowed in state ") + exec_state_name(state_);
+  if (!body.get("job_spec").is_object()) return "job_spec is required";
+  submit_body_ = body;
+  state_ = ExecState::WaitCode;
+  rlog("job submitted: %s", body["run_spec"]["run_name"].str(body["run_name"].str("?")).c_str());
+  return "";
+}
+
+std::string Executor::upload_code(const std::string& blob) {
+  if (state_ != ExecState::WaitCode) return std::string("upload_code not allowed in state ") + exec_state_name(state_);
+  if (!write_file(code_path_, blob)) return "cannot write code blob";
+  state_ = ExecState::WaitRun;
+  rlog("code uploaded: %zu bytes", blob.size());
+  return "";
+}
+
+std::string Executor::run() {
+  if (state_ != ExecState::WaitRun) return std::string("run not allowed in state ") + exec_state_name(state_);
+  state_ = ExecState::ServeLogs;
+  worker_ = std::thread(&Executor::run_thread, this);
+  return "";
+}
+
+void Executor::stop() {
+  stop_requested_ = true;
+  int pg = child_pgid_;
+  if (pg > 0) {
+    kill(-pg, SIGINT);  // graceful first; exec_job escalates to SIGKILL after 10 s
+  }
+}
+
+void Executor::wait_finished() {
+  std::unique_lock<std::mutex> lk(fin_mu_);
+  fin_cv_.wait(lk, [&] { return finished_.load(); });
+}
+
+void Executor::mark_pulled(int64_t ts) const {
+  (void)ts;
+  if (finished_) pulled_after_finish_ = true;
+}
+
+Json Executor::pull(int64_t since) const {
+  Json out = Json::object();
+  Json states = Json::array();
+  {
+    std::lock_guard<std::mutex> lk(states_mu_);
+    for (auto& s : states_) {
+      if (s.timestamp <= since) continue;
+      Json j = Json::object();
+      j.set("state", s.state);
+      j.set("timestamp", (long long)s.timestamp);
+      j.set("termination_reason", s.termination_reason);
+      j.set("termination_message", s.termination_message);
+      if (s.exit_status >= 0) j.set("exit_status", s.exit_status);
+      states.push_back(j);
+    }
+  }
+  auto enc = [](const std::vector<LogEvent>& evs) {
+    Json a = Json::array();
+    for (auto& e : evs) {
+      Json j = Json::object();
+      j.set("timestamp", (long long)e.timestamp);
+      j.set("message", base64_encode(e.message));
+      a.push_back(j);
+    }
+    return a;
+  };
+  const size_t limit = 5000;
+  auto jl = job_logs_.after(since, limit);
+  auto rl = runner_logs_.after(since, limit);
+  int64_t last = since;
+  for (auto& e : jl) last = std::max(last, e.timestamp);
+  for (auto& e : rl) last = std::max(last, e.timestamp);
+  {
+    std::lock_guard<std::mutex> lk(states_mu_);
+    for (auto& s : states_) last = std::max(last, s.timestamp);
+  }
+  out.set("job_states", states);
+  out.set("job_logs", enc(jl));
+  out.set("runner_logs", enc(rl));
+  out.set("last_updated", (long long)last);
+  out.set("has_more", jl.size() >= limit || rl.size() >= limit);
+  return out;
+}
+
+static std::string iface_for_ip(const std::string& ip) {
+  struct ifaddrs* ifa = nullptr;
+  if (getifaddrs(&ifa) != 0) return "";
+  std::string name;
+  for (auto* p = ifa; p; p = p->ifa_next) {
+    if (!p->ifa_addr || p->ifa_addr->sa_family != AF_INET) continue;
+    char buf[64];
+    inet_ntop(AF_INET, &((struct sockaddr_in*)p->ifa_addr)->sin_addr, buf, sizeof buf);
+    if (ip == buf) {
+      name = p->ifa_name;
+      break;
+    }
+  }
+  freeifaddrs(ifa);
+  return name;
+}
+
+std::vector<std::pair<std::string, std::string>> Executor::build_env() const {
+  std::vector<std::pair<std::string, std::string>> env;
+  auto set = [&](const std::string& k, const std::string& v) {
+    for (auto& kv : env)
+      if (kv.first == k) {
+        kv.second = v;
+        return;
+      }
+    env.emplace_back(k, v);
+  };
+  auto has = [&](const std::string& k) {
+    for (auto& kv : env)
+      if (kv.first == k) return true;
+    return false;
+  };
+  for (char** e = environ; e && *e; ++e) {
+    std::string s = *e;
+    auto eq = s.find('=');
+    if (eq != std::string::npos) env.emplace_back(s.substr(0, eq), s.substr(eq + 1));
+  }
+  const Json& js = submit_body_["job_spec"];
+  const Json& ci = submit_body_["cluster_info"];
+  const Json& rs = submit_body_["run_spec"];
+  std::string run_name = rs["run_name"].str(submit_body_["run_name"].str());
+  std::string repo_id = rs["repo_id"].str(submit_body_["repo_id"].str());
+  std::vector<std::string> ips;
+  for (auto& ip : ci["job_ips"].items()) ips.push_back(ip.str());
+  int node_rank = (int)js["job_num"].as_int(0);
+  int nodes = ips.empty() ? (int)js["jobs_per_replica"].as_int(1) : (int)ips.size();
+  int gpus_per_node = (int)ci["gpus_per_job"].as_int(0);
+  std::string master = ci["master_job_ip"].str(ips.empty() ? "127.0.0.1" : ips[0]);
+  std::string ips_joined;
+  for (size_t k = 0; k < ips.size(); ++k) ips_joined += (k ? "\n" : "") + ips[k];
+  // dstack rendezvous contract (executor.go:213-230)
+  set("DSTACK_RUN_NAME", run_name);
+  set("DSTACK_REPO_ID", repo_id);
+  set("RUN_NAME", run_name);
+  set("REPO_ID", repo_id);
+  set("DSTACK_NODES_IPS", ips_joined);
+  set("DSTACK_MASTER_NODE_IP", master);
+  set("DSTACK_NODE_RANK", std::to_string(node_rank));
+  set("DSTACK_NODES_NUM", std::to_string(nodes));
+  set("DSTACK_GPUS_PER_NODE", std::to_string(gpus_per_node));
+  set("DSTACK_GPUS_NUM", std::to_string(nodes * gpus_per_node));
+  // MI355X additions: torch rendezvous defaults (torchrun reads PET_* as its CLI defaults) ...
+  if (!has("MASTER_ADDR")) set("MASTER_ADDR", master);
+  if (!has("MASTER_PORT")) set("MASTER_PORT", "29500");
+  set("PET_NNODES", std::to_string(nodes));
+  set("PET_NODE_RANK", std::to_string(node_rank));
+  set("PET_MASTER_ADDR", master);
+  set("PET_MASTER_PORT", "29500");
+  if (gpus_per_node > 0) set("PET_NPROC_PER_NODE", std::to_string(gpus_per_node));
+  // ... and RCCL over xGMI (intra-node) + RoCE/IB (inter-node)
+  if (gpus_per_node > 0 && !has("HIP_VISIBLE_DEVICES")) {
+    std::string v;
+    for (int g = 0; g < gpus_per_node; ++g) v += (g ? "," : "") + std::to_string(g);
+    set("HIP_VISIBLE_DEVICES", v);
+  }
+  if (!has("HSA_FORCE_FINE_GRAIN_PCIE")) set("HSA_FORCE_FINE_GRAIN_PCIE", "1");
+  if (!has("HSA_ENABLE_IPC_MODE_LEGACY")) set("HSA_ENABLE_IPC_MODE_LEGACY", "0");
+  if (nodes > 1 && !has("NCCL_SOCKET_IFNAME")) {
+    std::string my_ip = node_rank < (int)ips.size() ? ips[node_rank] : "";
+    std::string ifname = my_ip.empty() ? "" : iface_for_ip(my_ip);
+    if (!ifname.empty()) set("NCCL_SOCKET_IFNAME", ifname);
+  }
+  // secrets (os env < dstack env < secrets < job env)
+  for (auto& kv : submit_body_["secrets"].members()) set(kv.first, kv.second.str());
+  std::vector<std::pair<std::string, std::string>> jobenv;
+  for (auto& kv : js["env"].members()) {
+    std::string err;
+    set(kv.first, interpolate_env(kv.second.str(), env, &err));
+  }
+  set("HOME", opts_.home_dir);
+  return env;
+}
+
+static int run_cmd(const std::vector<std::string>& argv, const std::string& cwd, std::string* output) {
+  int pipefd[2];
+  if (pipe(pipefd) != 0) return -1;
+  pid_t pid = fork();
+  if (pid == 0) {
+    dup2(pipefd[1], 1);
+    dup2(pipefd[1], 2);
+    close(pipefd[0]);
+    close(pipefd[1]);
+    if (!cwd.empty() && chdir(cwd.c_str()) != 0) _exit(127);
+    std::vector<char*> a;
+    for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
+    a.push_back(nullptr);
+    execvp(a[0], a.data());
+    _exit(127);
+  }
+  close(pipefd[1]);
+  char buf[4096];
+  ssize_t n;
+  while ((n = read(pipefd[0], buf, sizeof buf)) > 0)
+    if (output) output->append(buf, (size_t)n);
+  close(pipefd[0]);
+  int st = 0;
+  waitpid(pid, &st, 0);
+  return WIFEXITED(st) ? WEXITSTATUS(st) : -1;
+}
+
+bool Executor::setup_repo(std::string& err) {
+  const Json& rs = submit_body_["run_spec"];
+  const Json& repo = rs["repo_data"].is_object() ? rs["repo_data"] : submit_body_["repo_data"];
+  std::string type = repo["repo_type"].str("virtual");
+  mkdirs(opts_.working_dir);
+  std::string blob;
+  read_file(code_path_, blob);
+  if (type == "remote") {
+    const Json& creds = submit_body_["repo_credentials"];
+    std::string url = creds["clone_url"].str();
+    if (url.empty()) {
+      std::string host = repo["repo_host_name"].str(), name = repo["repo_name"].str();
+      url = "https://" + host + "/" + name + ".git";
+    }
+    std::string token = creds["oauth_token"].str();
+    if (!token.empty() && url.rfind("https://", 0) == 0) url = "https://" + token + "@" + url.substr(8);
+    std::string key = creds["private_key"].str();
+    if (!key.empty()) {
+      std::string kp = opts_.temp_dir + "/repo_key";
+      write_file(kp, key, 0600);
+      setenv("GIT_SSH_COMMAND", ("ssh -i " + kp + " -o StrictHostKeyChecking=no").c_str(), 1);
+    }
+    std::vector<std::string> clone = {"git", "clone"};
+    bool single = submit_body_["job_spec"]["single_branch"].as_bool(false);
+    std::string branch = repo["repo_branch"].str();
+    if (single && !branch.empty()) clone.insert(clone.end(), {"--single-branch", "--branch", branch});
+    clone.push_back(url);
+    clone.push_back(opts_.working_dir);
+    std::string out;
+    if (!path_exists(opts_.working_dir + "/.git")) {
+      rlog("cloning repo %s", repo["repo_name"].str().c_str());
+      if (run_cmd(clone, "", &out) != 0) {
+        err = "git clone failed: " + out;
+        return false;
+      }
+    }
+    std::string hash = repo["repo_hash"].str();
+    if (!hash.empty() && run_cmd({"git", "checkout", hash}, opts_.working_dir, &out) != 0) {
+      err = "git checkout failed: " + out;
+      return false;
+    }
+    if (!blob.empty()) {
+      if (run_cmd({"git", "apply", "--whitespace=nowarn", code_path_}, opts_.working_dir, &out) != 0) {
+        err = "git apply failed: " + out;
+        return false;
+      }
+    }
+    return true;
+  }
+  // local / virtual: tar.gz blob
+  if (!blob.empty()) {
+    std::string out;
+    if (run_cmd({"tar", "-xzf", code_path_, "-C", opts_.working_dir}, "", &out) != 0) {
+      err = "code extraction failed: " + out;
+      return false;
+    }
+  }
+  return true;
+}
+
+bool Executor::run_probe() {
+  if (opts_.probe_binary.empty() || !path_exists(opts_.probe_binary)) return true;
+  std::string out;
+  int rc = run_cmd({opts_.probe_binary, "--quick", "--json"}, "", &out);
+  job_logs_.append("[dstack] GPU health probe: " + out + (out.empty() || out.back() != '\n' ? "\n" : ""));
+  return rc == 0;
+}
+
+int Executor::exec_job(std::string& reason, std::string& msg) {
+  const Json& js = submit_body_["job_spec"];
+  std::vector<std::string> argv;
+  for (auto& c : js["commands"].items()) argv.push_back(c.str());
+  if (argv.empty()) {
+    reason = "executor_error";
+    msg = "empty command";
+    return -1;
+  }
+  auto env = build_env();
+  // DSTACK_ROCPROF=1: wrap the job in rocprofv3 kernel-trace statistics; the summary is appended
+  // to the job log when the job ends (rocprof counters surfaced in run logs)
+  std::string rocprof_dir;
+  for (auto& kv : env)
+    if (kv.first == "DSTACK_ROCPROF" && (kv.second == "1" || kv.second == "true")) rocprof_dir = opts_.temp_dir + "/rocprof";
+  if (!rocprof_dir.empty()) {
+    mkdirs(rocprof_dir);
+    std::vector<std::string> wrapped = {"rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv",
+                                        "-d", rocprof_dir, "-o", "job", "--"};
+    wrapped.insert(wrapped.end(), argv.begin(), argv.end());
+    argv = wrapped;
+  }
+  std::string wd = opts_.working_dir;
+  std::string jwd = js["working_dir"].str();
+  if (!jwd.empty()) wd = jwd[0] == '/' ? jwd : wd + "/" + jwd;
+  mkdirs(wd);
+  std::vector<std::string> envs;
+  for (auto& kv : env) envs.push_back(kv.first + "=" + kv.second);
+  if (opts_.write_ssh_env) {
+    std::string ssh_dir = opts_.home_dir + "/.ssh";
+    mkdirs(ssh_dir, 0700);
+    std::string content;
+    for (auto& e : envs)
+      if (e.find('\n') == std::string::npos) content += e + "\n";
+    write_file(ssh_dir + "/environment", content, 0600);
+  }
+  int uid = -1, gid = -1;
+  const Json& user = js["user"];
+  if (user.is_object()) {
+    if (user["uid"].is_number()) uid = (int)user["uid"].as_int();
+    if (user["gid"].is_number()) gid = (int)user["gid"].as_int();
+    if (uid < 0 && user["username"].is_string()) {
+      struct passwd* pw = getpwnam(user["username"].str().c_str());
+      if (pw) {
+        uid = (int)pw->pw_uid;
+        if (gid < 0) gid = (int)pw->pw_gid;
+      }
+    }
+  }
+  int master = -1;
+  struct winsize ws{};
+  ws.ws_row = 50;
+  ws.ws_col = 200;
+  pid_t pid = forkpty(&master, nullptr, nullptr, &ws);
+  if (pid < 0) {
+    reason = "executor_error";
+    msg = std::string("forkpty failed: ") + strerror(errno);
+    return -1;
+  }
+  if (pid == 0) {
+    if (chdir(wd.c_str()) != 0) _exit(126);
+    if (getuid() == 0 && uid >= 0) {
+      if (gid >= 0 && setgid((gid_t)gid) != 0) _exit(126);
+      setgroups(0, nullptr);
+      if (setuid((uid_t)uid) != 0) _exit(126);
+    }
+    std::vector<char*> a, e;
+    for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
+    a.push_back(nullptr);
+    for (auto& s : envs) e.push_back(const_cast<char*>(s.c_str()));
+    e.push_back(nullptr);
+    execvpe(a[0], a.data(), e.data());
+    fprintf(stderr, "exec %s failed: %s\n", a[0], strerror(errno));
+    _exit(127);
+  }
+  child_pgid_ = pid;  // forkpty() makes the child a session (and process group) leader
+  add_state("running");
+  rlog("job started: pid=%d cwd=%s", pid, wd.c_str());
+  int64_t max_duration = js["max_duration"].as_int(0);
+  int64_t t0 = now_millis(), stop_at = 0;
+  bool timed_out = false;
+  char buf[65536];
+  int status = 0;
+  bool exited = false;
+  while (true) {
+    struct pollfd p{master, POLLIN, 0};
+    int r = poll(&p, 1, 200);
+    if (r > 0 && (p.revents & POLLIN)) {
+      ssize_t n = read(master, buf, sizeof buf);
+      if (n > 0) job_logs_.append(std::string(buf, (size_t)n));
+    }
+    if (!exited) {
+      pid_t w = waitpid(pid, &status, WNOHANG);
+      if (w == pid) exited = true;
+    }
+    if (exited) {
+      // drain remaining pty output
+      while (true) {
+        struct pollfd q{master, POLLIN, 0};
+        if (poll(&q, 1, 50) <= 0) break;
+        ssize_t n = read(master, buf, sizeof buf);
+        if (n <= 0) break;
+        job_logs_.append(std::string(buf, (size_t)n));
+      }
+      break;
+    }
+    int64_t now = now_millis();
+    if (max_duration > 0 && !timed_out && now - t0 > max_duration * 1000) {
+      timed_out = true;
+      rlog("max_duration exceeded: stopping job");
+      kill(-pid, SIGINT);
+      stop_at = now;
+    }
+    if (stop_requested_ && stop_at == 0) stop_at = now;
+    if (stop_at > 0 && now - stop_at > 10000) kill(-pid, SIGKILL);  // killDelay (executor.go:74)
+  }
+  close(master);
+  child_pgid_ = 0;
+  int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+  if (!rocprof_dir.empty()) {
+    // surface the kernel statistics in the job log
+    DIR* d = opendir(rocprof_dir.c_str());
+    std::string stats_path;
+    if (d) {
+      while (auto* e = readdir(d)) {
+        std::string n = e->d_name;
+        if (n.find("kernel_stats.csv") != std::string::npos) stats_path = rocprof_dir + "/" + n;
+      }
+      closedir(d);
+    }
+    std::string csv;
+    if (!stats_path.empty() && read_file(stats_path, csv)) {
+      std::istringstream ss(csv);
+      std::string line, out = "\n[dstack] rocprofv3 kernel statistics (top 15):\n";
+      int k = 0;
+      while (std::getline(ss, line) && k < 16) {
+        out += "  " + line.substr(0, 240) + "\n";
+        ++k;
+      }
+      job_logs_.append(out);
+    }
+  }
+  if (timed_out) {
+    reason = "max_duration_exceeded";
+    return code;
+  }
+  if (stop_requested_) {
+    reason = "terminated_by_user";
+    return code;
+  }
+  if (code != 0) {
+    reason = "container_exited_with_error";
+    msg = "exit status " + std::to_string(code);
+  }
+  return code;
+}
+
+void Executor::run_thread() {
+  std::string err;
+  rlog("setting up repo");
+  if (!setup_repo(err)) {
+    rlog("repo setup failed: %s", err.c_str());
+    add_state("failed", "executor_error", err);
+  } else if (submit_body_["job_spec"]["gpu_probe"].as_bool(false) && !run_probe()) {
+    add_state("failed", "gpu_health_check_failed", "GPU health probe failed");
+  } else if (stop_requested_) {
+    add_state("terminated", "terminated_by_user");
+  } else {
+    std::string reason, msg;
+    int code = exec_job(reason, msg);
+    if (reason == "max_duration_exceeded" || reason == "terminated_by_user")
+      add_state("terminated", reason, msg, code);
+    else if (!reason.empty())
+      add_state("failed", reason, msg, code);
+    else
+      add_state("done", "done_by_runner", "", code);
+    rlog("job finished: exit_status=%d %s", code, reason.c_str());
+  }
+  state_ = ExecState::WaitLogsFinished;
+  {
+    std::lock_guard<std::mutex> lk(fin_mu_);
+    finished_ = true;
+  }
+  fin_cv_.notify_all();
+}
+
+}  // namespace dsa

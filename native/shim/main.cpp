@@ -1,0 +1,277 @@
+// dstack-shim entry point + REST API (reference: runner/cmd/shim/main.go:25-205,
+// runner/internal/shim/api/{server.go:33-55,handlers.go:13-123}).
+//
+//   dstack-shim [--log-level N] [--shim-home DIR] [--shim-http-port 10998] [--host 0.0.0.0]
+//               [--runner-binary-path PATH] [--runner-download-url URL] [--probe-binary PATH]
+//               [--runner-http-port 10999] [--runner-ssh-port 10022] [--driver docker|process|auto]
+//               [--privileged] [--service]
+#include <signal.h>
+#include <stdlib.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <thread>
+
+#include "../common/amdgpu.h"
+#include "../common/net.h"
+#include "shim.h"
+
+namespace dsa {
+
+static const char* SHIM_VERSION = "0.1.0-mi355x";
+
+Shim::Shim(ShimOptions o, std::unique_ptr<TaskDriver> driver) : opts_(std::move(o)), driver_(std::move(driver)) {
+  auto gpus = discover_amd_gpus();
+  std::vector<int> numa;
+  for (auto& g : gpus) numa.push_back(g.numa_node);
+  auto& smi = AmdSmi::instance();
+  gpus_.init((int)gpus.size(), smi.available() ? smi.xgmi_matrix() : std::vector<std::vector<int>>{}, numa);
+  LOGI("shim: driver=%s gpus=%zu", driver_->name(), gpus.size());
+}
+
+void Shim::restore() {
+  for (auto& t : driver_->restore()) {
+    gpus_.lock(t.gpus);
+    storage_.add(t);
+    LOGI("restored task %s (%s)", t.config.id.c_str(), task_status_name(t.status));
+    if (t.status == TaskStatus::Running) {
+      std::string id = t.config.id;
+      std::thread([this, id] {
+        Task cur;
+        if (!storage_.get(id, cur)) return;
+        driver_->wait(cur);
+        storage_.set_status(id, TaskStatus::Terminated, "container_exited", "");
+        gpus_.release(cur.gpus);
+      }).detach();
+    }
+  }
+}
+
+Json Shim::host_info() {
+  std::lock_guard<std::mutex> lk(hi_mu_);
+  if (host_info_.is_null()) host_info_ = collect_host_info(opts_.home);
+  return host_info_;
+}
+
+Json Shim::submit(const Json& cfg, int& http_status) {
+  TaskConfig c = TaskConfig::from_json(cfg);
+  if (c.id.empty()) {
+    http_status = 400;
+    return Json("task id is required");
+  }
+  Task t;
+  t.config = c;
+  t.created_ms = now_millis();
+  t.timings["submitted"] = t.created_ms;
+  if (!storage_.add(t)) {
+    http_status = 409;
+    return Json("task already exists");
+  }
+  http_status = 200;
+  std::thread(&Shim::run_task, this, c.id).detach();
+  return t.to_json();
+}
+
+void Shim::run_task(std::string id) {
+  Task t;
+  if (!storage_.get(id, t)) return;
+  storage_.set_status(id, TaskStatus::Preparing);
+  // GPU grant: explicit indices (server-side xGMI placement) or a count resolved here
+  std::vector<int> granted;
+  if (!t.config.gpu_indices.empty()) {
+    if (!gpus_.lock(t.config.gpu_indices)) {
+      storage_.set_status(id, TaskStatus::Terminated, "creating_container_error", "requested GPUs are busy");
+      return;
+    }
+    granted = t.config.gpu_indices;
+  } else if (t.config.gpu != 0) {
+    granted = gpus_.acquire(t.config.gpu);
+    if (granted.empty() || (t.config.gpu > 0 && (int)granted.size() != t.config.gpu)) {
+      gpus_.release(granted);
+      storage_.set_status(id, TaskStatus::Terminated, "creating_container_error", "not enough free GPUs");
+      return;
+    }
+  }
+  if (!storage_.get(id, t)) return;
+  t.gpus = granted;
+  storage_.update(t);
+  if (!t.config.host_ssh_keys.empty() && !t.config.host_ssh_user.empty())
+    add_authorized_keys(t.config.host_ssh_user, t.config.host_ssh_keys);
+  storage_.set_status(id, TaskStatus::Pulling);
+  storage_.set_status(id, TaskStatus::Creating);
+  if (!storage_.get(id, t)) return;
+  std::string reason, msg;
+  bool ok = driver_->run(t, reason, msg);
+  Task cur;
+  if (storage_.get(id, cur)) {
+    t.status = cur.status;
+    t.timings.insert(cur.timings.begin(), cur.timings.end());
+    storage_.update(t);
+  }
+  if (!ok) {
+    LOGW("task %s failed to start: %s", id.c_str(), msg.c_str());
+    gpus_.release(granted);
+    storage_.set_status(id, TaskStatus::Terminated, reason, msg);
+    return;
+  }
+  storage_.set_status(id, TaskStatus::Running);
+  LOGI("task %s running (runner port %d, gpus %zu)", id.c_str(), t.runner_port, granted.size());
+  driver_->wait(t);
+  gpus_.release(granted);
+  storage_.set_status(id, TaskStatus::Terminated, "done_by_runner", "");
+  if (!t.config.host_ssh_keys.empty() && !t.config.host_ssh_user.empty())
+    remove_authorized_keys(t.config.host_ssh_user, t.config.host_ssh_keys);
+}
+
+bool Shim::get(const std::string& id, Json& out) const {
+  Task t;
+  if (!storage_.get(id, t)) return false;
+  out = t.to_json();
+  return true;
+}
+
+Json Shim::list() const {
+  Json j = Json::object();
+  Json ids = Json::array();
+  for (auto& id : storage_.ids()) ids.push_back(id);
+  j.set("ids", ids);
+  return j;
+}
+
+bool Shim::terminate(const std::string& id, const std::string& reason, const std::string& msg, int timeout_s) {
+  Task t;
+  if (!storage_.get(id, t)) return false;
+  if (t.status == TaskStatus::Terminated) return true;
+  driver_->terminate(t, timeout_s);
+  storage_.set_status(id, TaskStatus::Terminated, reason.empty() ? "terminated_by_server" : reason, msg);
+  return true;
+}
+
+bool Shim::remove(const std::string& id, std::string& err) {
+  Task t;
+  if (!storage_.get(id, t)) {
+    err = "not found";
+    return false;
+  }
+  if (t.status != TaskStatus::Terminated) {
+    err = "task is not terminated";
+    return false;
+  }
+  driver_->remove(t);
+  storage_.remove(id);
+  return true;
+}
+
+}  // namespace dsa
+
+using namespace dsa;
+
+int main(int argc, char** argv) {
+  ShimOptions o;
+  const char* home = getenv("HOME");
+  o.home = std::string(home ? home : "/root") + "/.dstack-shim";
+  int port = 10998;
+  std::string host = "0.0.0.0";
+  bool service = false;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "missing value for %s\n", a.c_str());
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--log-level") set_log_level(atoi(next().c_str()));
+    else if (a == "--shim-home") o.home = next();
+    else if (a == "--shim-http-port") port = atoi(next().c_str());
+    else if (a == "--host") host = next();
+    else if (a == "--runner-binary-path") o.runner_binary = next();
+    else if (a == "--runner-download-url") o.runner_download_url = next();
+    else if (a == "--probe-binary") o.probe_binary = next();
+    else if (a == "--runner-http-port") o.runner_http_port = atoi(next().c_str());
+    else if (a == "--runner-ssh-port") o.runner_ssh_port = atoi(next().c_str());
+    else if (a == "--driver") o.driver = next();
+    else if (a == "--privileged") o.privileged = true;
+    else if (a == "--service") service = true;
+    else if (a == "--version") {
+      printf("%s\n", SHIM_VERSION);
+      return 0;
+    } else if (a == "--host-info") {  // print host_info.json and exit (used by SSH-fleet deploy)
+      printf("%s\n", collect_host_info("/").dump().c_str());
+      return 0;
+    } else {
+      fprintf(stderr, "unknown flag %s\n", a.c_str());
+      return 2;
+    }
+  }
+  // env fallbacks (main.go:40-124)
+  if (const char* v = getenv("DSTACK_SHIM_HTTP_PORT")) port = atoi(v);
+  if (const char* v = getenv("DSTACK_RUNNER_BINARY_PATH"); v && o.runner_binary.empty()) o.runner_binary = v;
+  if (const char* v = getenv("DSTACK_RUNNER_DOWNLOAD_URL"); v && o.runner_download_url.empty()) o.runner_download_url = v;
+  signal(SIGPIPE, SIG_IGN);
+  mkdirs(o.home);
+  if (o.runner_binary.empty()) o.runner_binary = o.home + "/dstack-runner";
+  if (!path_exists(o.runner_binary) && !o.runner_download_url.empty()) {  // runner.go:18-109
+    LOGI("downloading runner from %s", o.runner_download_url.c_str());
+    auto r = http_get_url(o.runner_download_url, 10 * 60 * 1000);
+    if (!r.ok() || !write_file(o.runner_binary, r.body, 0755)) {
+      LOGE("runner download failed: %d %s", r.status, r.error.c_str());
+      return 1;
+    }
+  }
+  bool use_docker = o.driver == "docker" || (o.driver == "auto" && docker_available(o.docker_socket));
+  Shim shim(o, use_docker ? make_docker_driver(o) : make_process_driver(o));
+  shim.restore();
+  if (service) write_file(o.home + "/host_info.json", shim.host_info().dump());
+
+  HttpServer srv(host, port);
+  srv.route("GET", "/api/healthcheck", [&](HttpRequest&) {
+    Json j = Json::object();
+    j.set("service", "dstack-shim");
+    j.set("version", SHIM_VERSION);
+    j.set("driver", shim.driver_name());
+    j.set("gpus_free", shim.gpu_lock().free_count());
+    j.set("gpus_total", shim.gpu_lock().total());
+    return HttpResponse::json(j);
+  });
+  srv.route("GET", "/api/host_info", [&](HttpRequest&) { return HttpResponse::json(shim.host_info()); });
+  srv.route("GET", "/api/tasks", [&](HttpRequest&) { return HttpResponse::json(shim.list()); });
+  srv.route("GET", "/api/tasks/{id}", [&](HttpRequest& r) {
+    Json j;
+    if (!shim.get(r.params["id"], j)) return HttpResponse::error(404, "task not found");
+    return HttpResponse::json(j);
+  });
+  srv.route("POST", "/api/tasks", [&](HttpRequest& r) {
+    Json body;
+    try {
+      body = r.json();
+    } catch (const std::exception& e) {
+      return HttpResponse::error(400, e.what());
+    }
+    int st = 200;
+    Json out = shim.submit(body, st);
+    return st == 200 ? HttpResponse::json(out) : HttpResponse::error(st, out.str());
+  });
+  srv.route("POST", "/api/tasks/{id}/terminate", [&](HttpRequest& r) {
+    Json body = r.body.empty() ? Json::object() : Json::parse(r.body);
+    if (!shim.terminate(r.params["id"], body["termination_reason"].str(), body["termination_message"].str(),
+                        (int)body["timeout"].as_int(10)))
+      return HttpResponse::error(404, "task not found");
+    Json j;
+    shim.get(r.params["id"], j);
+    return HttpResponse::json(j);
+  });
+  srv.route("POST", "/api/tasks/{id}/remove", [&](HttpRequest& r) {
+    std::string err;
+    if (!shim.remove(r.params["id"], err)) return HttpResponse::error(err == "not found" ? 404 : 409, err);
+    return HttpResponse::json(Json::object());
+  });
+  if (srv.start() < 0) return 1;
+  LOGI("dstack-shim %s listening on %s:%d (driver %s)", SHIM_VERSION, host.c_str(), srv.port(), shim.driver_name());
+  // print the bound port for supervisors that start us with --shim-http-port 0
+  printf("DSTACK_SHIM_PORT=%d\n", srv.port());
+  fflush(stdout);
+  srv.serve_forever();
+  return 0;
+}

@@ -1,0 +1,170 @@
+// Process task driver: runs the dstack-runner as a child process of the shim, without Docker.
+// Used by the local backend, by bare-metal SSH hosts without a container runtime and by the
+// CPU-only tests.  GPU isolation: the granted GPUs are exported as HIP_VISIBLE_DEVICES (host
+// numbering), so ROCm in the job sees exactly those devices.
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <thread>
+
+#include "../common/net.h"
+#include "shim.h"
+
+extern char** environ;
+
+namespace dsa {
+
+static int free_tcp_port() {
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  struct sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  a.sin_port = 0;
+  if (::bind(fd, (struct sockaddr*)&a, sizeof a) != 0) {
+    ::close(fd);
+    return 0;
+  }
+  socklen_t l = sizeof a;
+  getsockname(fd, (struct sockaddr*)&a, &l);
+  int p = ntohs(a.sin_port);
+  ::close(fd);
+  return p;
+}
+
+class ProcessDriver : public TaskDriver {
+ public:
+  explicit ProcessDriver(ShimOptions o) : o_(std::move(o)) {}
+  const char* name() const override { return "process"; }
+
+  bool run(Task& t, std::string& reason, std::string& msg) override {
+    if (o_.runner_binary.empty() || !path_exists(o_.runner_binary)) {
+      reason = "creating_container_error";
+      msg = "dstack-runner binary not found: " + o_.runner_binary;
+      return false;
+    }
+    std::string dir = o_.home + "/tasks/" + t.config.id;
+    mkdirs(dir + "/tmp");
+    mkdirs(dir + "/home");
+    mkdirs(dir + "/workflow");
+    // instance mounts: expose host paths inside the task dir (symlinks) for parity with docker
+    for (auto& m : t.config.instance_mounts.items()) {
+      std::string ip = m["instance_path"].str(), p = m["path"].str();
+      if (!ip.empty() && !p.empty()) {
+        std::string link = dir + "/mounts" + p;
+        mkdirs(link.substr(0, link.rfind('/')));
+        if (symlink(ip.c_str(), link.c_str()) != 0) LOGW("mount link %s failed", link.c_str());
+      }
+    }
+    int port = free_tcp_port();
+    if (port == 0) {
+      reason = "creating_container_error";
+      msg = "no free port for the runner";
+      return false;
+    }
+    std::vector<std::string> envs;
+    for (char** e = environ; e && *e; ++e) {
+      std::string s = *e;
+      if (s.rfind("HIP_VISIBLE_DEVICES=", 0) == 0 || s.rfind("ROCR_VISIBLE_DEVICES=", 0) == 0 ||
+          s.rfind("CUDA_VISIBLE_DEVICES=", 0) == 0)
+        continue;
+      envs.push_back(s);
+    }
+    for (auto& kv : t.config.env) envs.push_back(kv.first + "=" + kv.second);
+    if (!t.gpus.empty()) {
+      std::string v;
+      for (size_t k = 0; k < t.gpus.size(); ++k) v += (k ? "," : "") + std::to_string(t.gpus[k]);
+      envs.push_back("HIP_VISIBLE_DEVICES=" + v);
+      envs.push_back("DSTACK_GPU_INDICES=" + v);
+    } else if (t.config.gpu == 0) {
+      envs.push_back("HIP_VISIBLE_DEVICES=-1");  // no GPU granted: hide all devices
+    }
+    std::vector<std::string> argv = {o_.runner_binary, "--log-level", std::to_string(log_level()), "start",
+                                     "--http-port", std::to_string(port), "--temp-dir", dir + "/tmp",
+                                     "--home-dir", dir + "/home", "--working-dir", dir + "/workflow"};
+    if (!o_.probe_binary.empty()) {
+      argv.push_back("--probe");
+      argv.push_back(o_.probe_binary);
+    }
+    std::string log_path = dir + "/runner.log";
+    pid_t pid = fork();
+    if (pid < 0) {
+      reason = "creating_container_error";
+      msg = strerror(errno);
+      return false;
+    }
+    if (pid == 0) {
+      setsid();
+      int fd = open(log_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+      if (fd >= 0) {
+        dup2(fd, 1);
+        dup2(fd, 2);
+        close(fd);
+      }
+      std::vector<char*> a, e;
+      for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
+      a.push_back(nullptr);
+      for (auto& s : envs) e.push_back(const_cast<char*>(s.c_str()));
+      e.push_back(nullptr);
+      execve(a[0], a.data(), e.data());
+      _exit(127);
+    }
+    t.pid = pid;
+    t.runner_port = port;
+    t.container_name = "process-" + std::to_string(pid);
+    t.ports = {PortMapping{o_.runner_http_port, port}};
+    // wait until the runner accepts connections so the server's first call succeeds
+    for (int k = 0; k < 500; ++k) {
+      HttpClientRequest r;
+      r.port = port;
+      r.path = "/api/healthcheck";
+      r.timeout_ms = 200;
+      if (http_request(r).ok()) break;
+      int st;
+      if (waitpid(pid, &st, WNOHANG) == pid) {
+        reason = "creating_container_error";
+        msg = "runner exited during startup (see " + log_path + ")";
+        t.pid = 0;
+        return false;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    return true;
+  }
+
+  void wait(Task& t) override {
+    if (t.pid <= 0) return;
+    int st = 0;
+    waitpid(t.pid, &st, 0);
+  }
+
+  void terminate(Task& t, int timeout_s) override {
+    if (t.pid <= 0) return;
+    kill(-t.pid, SIGTERM);
+    for (int k = 0; k < timeout_s * 10; ++k) {
+      if (kill(t.pid, 0) != 0) return;
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+    kill(-t.pid, SIGKILL);
+  }
+
+  void remove(Task& t) override {
+    std::string dir = o_.home + "/tasks/" + t.config.id;
+    std::string cmd = "rm -rf '" + dir + "'";
+    if (system(cmd.c_str()) != 0) LOGW("cannot remove %s", dir.c_str());
+  }
+
+ private:
+  ShimOptions o_;
+};
+
+std::unique_ptr<TaskDriver> make_process_driver(const ShimOptions& o) {
+  return std::unique_ptr<TaskDriver>(new ProcessDriver(o));
+}
+
+}  // namespace dsa
