@@ -1,0 +1,312 @@
+"""High-level Python API (reference: ``api/_public/__init__.py:17-95``, ``api/_public/runs.py:53-700``,
+``api/_public/repos.py``).
+
+``Client.from_config()`` -> ``client.runs.apply_configuration(conf, repo)`` -> ``Run`` with
+``logs()`` / ``wait()`` / ``attach()`` / ``stop()``.  Logs are read from the server's log storage
+(``/logs/poll``) while detached and, once attached, streamed straight from the runner's
+``/logs_ws`` websocket through the SSH forward (lower latency for ``dstack apply``).
+"""
+
+from __future__ import annotations
+
+import base64
+import io
+import os
+import threading
+import time
+from typing import Dict, Iterator, List, Optional
+
+from dstack_amd.api.server import APIClient, client_from_env_or_config
+from dstack_amd.core.errors import ClientError, ConfigurationError
+from dstack_amd.core.models.configurations import AnyRunConfiguration, ServiceConfiguration
+from dstack_amd.core.models.fleets import Fleet, FleetConfiguration, FleetSpec
+from dstack_amd.core.models.profiles import Profile
+from dstack_amd.core.models.repos import Repo, VirtualRepo
+from dstack_amd.core.models.runs import JobStatus, Run as RunModel, RunPlan, RunSpec, RunStatus
+from dstack_amd.core.models.volumes import Volume, VolumeConfiguration
+
+
+class Run:
+    def __init__(self, api: APIClient, project: str, run: RunModel, ssh_identity_file: Optional[str] = None):
+        self._api = api
+        self._project = project
+        self._run = run
+        self._ssh_identity_file = ssh_identity_file
+        self._attach = None
+
+    # ---- properties ---------------------------------------------------------------------------
+    @property
+    def name(self) -> str:
+        return self._run.run_spec.run_name
+
+    @property
+    def status(self) -> RunStatus:
+        return self._run.status
+
+    @property
+    def model(self) -> RunModel:
+        return self._run
+
+    @property
+    def hostname(self) -> Optional[str]:
+        jpd = self._latest_submission().job_provisioning_data if self._run.jobs else None
+        return jpd.hostname if jpd else None
+
+    @property
+    def backend(self):
+        jpd = self._latest_submission().job_provisioning_data if self._run.jobs else None
+        return jpd.backend if jpd else None
+
+    @property
+    def ports(self) -> Optional[Dict[int, int]]:
+        return self._attach.ports if self._attach else None
+
+    @property
+    def service_url(self) -> Optional[str]:
+        if not isinstance(self._run.run_spec.configuration, ServiceConfiguration):
+            return None
+        if self._run.service is not None:
+            url = self._run.service.url
+            return url if url.startswith("http") else self._api.base_url + url
+        return f"{self._api.base_url}/proxy/services/{self._project}/{self.name}/"
+
+    def _latest_submission(self, replica_num: int = 0, job_num: int = 0):
+        for j in self._run.jobs:
+            if j.job_spec.replica_num == replica_num and j.job_spec.job_num == job_num:
+                return j.job_submissions[-1]
+        return self._run.jobs[0].job_submissions[-1]
+
+    # ---- lifecycle ----------------------------------------------------------------------------
+    def refresh(self) -> "Run":
+        self._run = self._api.runs.get(self._project, self.name)
+        return self
+
+    def stop(self, abort: bool = False):
+        self._api.runs.stop(self._project, [self.name], abort)
+
+    def wait(self, statuses=None, timeout: Optional[float] = None, poll: float = 0.25) -> RunStatus:
+        """Block until the run reaches one of ``statuses`` (default: finished)."""
+        deadline = None if timeout is None else time.time() + timeout
+        while True:
+            self.refresh()
+            st = self.status
+            if (statuses is None and st.is_finished()) or (statuses is not None and st in statuses):
+                return st
+            if deadline is not None and time.time() > deadline:
+                raise TimeoutError(f"run {self.name} still {st.value} after {timeout}s")
+            time.sleep(poll)
+
+    def logs(self, start_time=None, diagnose: bool = False, replica_num: int = 0, job_num: int = 0,
+             follow: bool = False, poll: float = 0.5) -> Iterator[bytes]:
+        """Yield the job's log chunks; with ``follow`` keep yielding until the run finishes."""
+        next_token = None
+        while True:
+            if not self._run.jobs:
+                if not follow:
+                    return
+                time.sleep(poll)
+                self.refresh()
+                continue
+            sub = self._latest_submission(replica_num, job_num)
+            while True:
+                resp = self._api.logs.poll(self._project, self.name, sub.id, start_time=start_time,
+                                           diagnose=diagnose, next_token=next_token)
+                for ev in resp.logs:
+                    yield base64.b64decode(ev.message)
+                if resp.next_token and resp.logs:
+                    next_token = resp.next_token
+                    continue
+                break
+            if not follow:
+                return
+            finished = self._run.status.is_finished()
+            if finished:
+                return
+            time.sleep(poll)
+            self.refresh()
+            if self._run.status.is_finished():
+                finished = True  # one more drain pass after termination
+
+    def attach(self, ssh_identity_file: Optional[str] = None, bind_address: str = "127.0.0.1",
+               ports_overrides: Optional[Dict[int, int]] = None) -> bool:
+        """Forward the job's ports to localhost (and for remote hosts open an SSH master)."""
+        from dstack_amd.core.services.ssh.attach import RunAttach
+
+        self.refresh()
+        sub = self._latest_submission()
+        if sub.status not in (JobStatus.RUNNING,):
+            return False
+        self._attach = RunAttach(self._run, sub, ssh_identity_file or self._ssh_identity_file,
+                                 bind_address=bind_address, ports_overrides=ports_overrides or {})
+        self._attach.open()
+        return True
+
+    def detach(self):
+        if self._attach is not None:
+            self._attach.close()
+            self._attach = None
+
+    def __repr__(self) -> str:
+        return f"<Run '{self.name}' {self.status.value}>"
+
+
+class RunCollection:
+    def __init__(self, api: APIClient, project: str, client: "Client"):
+        self._api = api
+        self._project = project
+        self._client = client
+
+    def _upload(self, repo: Repo) -> Optional[str]:
+        buf = io.BytesIO()
+        h = repo.write_code_file(buf)
+        data = buf.getvalue()
+        if not data:
+            return h
+        return self._api.repos.upload_code(self._project, repo.repo_id, data)
+
+    def get_plan(self, configuration: AnyRunConfiguration, repo: Optional[Repo] = None,
+                 configuration_path: Optional[str] = None, profile: Optional[Profile] = None,
+                 run_name: Optional[str] = None, ssh_identity_file: Optional[str] = None,
+                 max_offers: Optional[int] = None) -> RunPlan:
+        repo = repo or VirtualRepo()
+        self._client.repos.init(repo)
+        code_hash = self._upload(repo)
+        pub = ""
+        key = ssh_identity_file or self._client.ssh_identity_file
+        if key and os.path.exists(str(key) + ".pub"):
+            with open(str(key) + ".pub") as f:
+                pub = f.read().strip()
+        spec = RunSpec(run_name=run_name or getattr(configuration, "name", None), repo_id=repo.repo_id,
+                       repo_data=repo.run_repo_data, repo_code_hash=code_hash,
+                       working_dir=getattr(configuration, "working_dir", None),
+                       configuration_path=configuration_path, configuration=configuration, profile=profile,
+                       ssh_key_pub=pub)
+        return self._api.runs.get_plan(self._project, spec, max_offers)
+
+    def exec_plan(self, plan: RunPlan, repo: Optional[Repo] = None, force: bool = False) -> Run:
+        run = self._api.runs.apply_plan(self._project, plan, force=force)
+        return Run(self._api, self._project, run, self._client.ssh_identity_file)
+
+    def apply_configuration(self, configuration: AnyRunConfiguration, repo: Optional[Repo] = None,
+                            configuration_path: Optional[str] = None, profile: Optional[Profile] = None,
+                            run_name: Optional[str] = None, force: bool = False) -> Run:
+        plan = self.get_plan(configuration, repo, configuration_path, profile, run_name)
+        return self.exec_plan(plan, repo, force=force)
+
+    def submit(self, configuration: AnyRunConfiguration, repo: Optional[Repo] = None,
+               run_name: Optional[str] = None, profile: Optional[Profile] = None) -> Run:
+        repo = repo or VirtualRepo()
+        self._client.repos.init(repo)
+        code_hash = self._upload(repo)
+        spec = RunSpec(run_name=run_name or getattr(configuration, "name", None), repo_id=repo.repo_id,
+                       repo_data=repo.run_repo_data, repo_code_hash=code_hash, configuration=configuration,
+                       profile=profile)
+        return Run(self._api, self._project, self._api.runs.submit(self._project, spec),
+                   self._client.ssh_identity_file)
+
+    def list(self, all: bool = False, limit: int = 100) -> List[Run]:
+        runs = self._api.runs.list(self._project, only_active=not all, limit=limit)
+        return [Run(self._api, self._project, r, self._client.ssh_identity_file) for r in runs]
+
+    def get(self, run_name: str) -> Optional[Run]:
+        try:
+            return Run(self._api, self._project, self._api.runs.get(self._project, run_name),
+                       self._client.ssh_identity_file)
+        except ClientError:
+            return None
+        except Exception as e:  # noqa: BLE001
+            if "not" in str(e).lower() and "exist" in str(e).lower():
+                return None
+            raise
+
+
+class RepoCollection:
+    def __init__(self, api: APIClient, project: str):
+        self._api = api
+        self._project = project
+        self._inited: set = set()
+
+    def init(self, repo: Repo, git_identity_file: Optional[str] = None, oauth_token: Optional[str] = None):
+        if repo.repo_id in self._inited:
+            return
+        creds = None
+        if git_identity_file or oauth_token:
+            creds = {"protocol": "ssh" if git_identity_file else "https", "oauth_token": oauth_token,
+                     "private_key": open(git_identity_file).read() if git_identity_file else None}
+        info = repo.get_repo_info().model_dump(mode="json")
+        self._api.repos.init(self._project, repo.repo_id, info, creds)
+        self._inited.add(repo.repo_id)
+
+    def is_initialized(self, repo: Repo) -> bool:
+        try:
+            self._api.repos.get(self._project, repo.repo_id)
+            return True
+        except Exception:  # noqa: BLE001
+            return False
+
+
+class FleetCollection:
+    def __init__(self, api: APIClient, project: str):
+        self._api, self._project = api, project
+
+    def apply_configuration(self, configuration: FleetConfiguration) -> Fleet:
+        spec = FleetSpec(configuration=configuration)
+        return self._api.fleets.create(self._project, spec)
+
+    def list(self) -> List[Fleet]:
+        return self._api.fleets.list(self._project)
+
+    def get(self, name: str) -> Fleet:
+        return self._api.fleets.get(self._project, name)
+
+    def delete(self, name: str):
+        self._api.fleets.delete(self._project, [name])
+
+
+class VolumeCollection:
+    def __init__(self, api: APIClient, project: str):
+        self._api, self._project = api, project
+
+    def create(self, configuration: VolumeConfiguration) -> Volume:
+        return self._api.volumes.create(self._project, configuration)
+
+    def list(self) -> List[Volume]:
+        return self._api.volumes.list(self._project)
+
+    def get(self, name: str) -> Volume:
+        return self._api.volumes.get(self._project, name)
+
+    def delete(self, name: str):
+        self._api.volumes.delete(self._project, [name])
+
+
+class Client:
+    def __init__(self, api_client: APIClient, project_name: str, ssh_identity_file: Optional[str] = None):
+        self.api = api_client
+        self.project = project_name
+        self.ssh_identity_file = ssh_identity_file
+        self.repos = RepoCollection(api_client, project_name)
+        self.runs = RunCollection(api_client, project_name, self)
+        self.fleets = FleetCollection(api_client, project_name)
+        self.volumes = VolumeCollection(api_client, project_name)
+
+    @staticmethod
+    def from_config(project_name: Optional[str] = None, server_url: Optional[str] = None,
+                    user_token: Optional[str] = None, ssh_identity_file: Optional[str] = None) -> "Client":
+        if server_url and user_token:
+            api, project = APIClient(server_url, user_token), project_name or "main"
+        elif server_url or user_token:
+            raise ConfigurationError("server_url and user_token must be given together")
+        else:
+            api, project = client_from_env_or_config(project_name)
+        if ssh_identity_file is None:
+            try:
+                from dstack_amd.core.services.configs import ConfigManager
+
+                ssh_identity_file = str(ConfigManager().ensure_ssh_key())
+            except Exception:  # noqa: BLE001 - ssh-keygen missing: attach just won't work
+                ssh_identity_file = None
+        return Client(api, project, ssh_identity_file)
+
+
+_ = threading

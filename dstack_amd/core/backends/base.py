@@ -1,0 +1,225 @@
+"""Backend Compute interface and shared bootstrap helpers (reference:
+``C/backends/base/compute.py:45-451``, ``C/backends/base/offers.py:18-175``)."""
+
+from __future__ import annotations
+
+import threading
+import time
+from abc import ABC, abstractmethod
+from typing import Dict, List, Optional, Tuple
+
+from dstack_amd.core.errors import BackendError, ComputeError
+from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.gateways import GatewayComputeConfiguration, GatewayProvisioningData
+from dstack_amd.core.models.instances import (
+    InstanceAvailability,
+    InstanceConfiguration,
+    InstanceOffer,
+    InstanceOfferWithAvailability,
+)
+from dstack_amd.core.models.placement import PlacementGroup, PlacementGroupProvisioningData
+from dstack_amd.core.models.resources import ResourcesSpec
+from dstack_amd.core.models.runs import Job, JobProvisioningData, Requirements, Run
+from dstack_amd.core.models.volumes import Volume, VolumeAttachmentData, VolumeProvisioningData
+
+DSTACK_SHIM_HTTP_PORT = 10998
+DSTACK_RUNNER_HTTP_PORT = 10999
+DSTACK_RUNNER_SSH_PORT = 10022
+OFFERS_CACHE_TTL = 30.0
+
+
+class Compute(ABC):
+    TYPE: BackendType
+
+    def __init__(self):
+        self._offers_cache: Dict[str, Tuple[float, List[InstanceOfferWithAvailability]]] = {}
+        self._offers_lock = threading.Lock()
+
+    # ---- offers ----------------------------------------------------------------------------
+    @abstractmethod
+    def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
+        ...
+
+    def get_offers_cached(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
+        key = requirements.model_dump_json() if requirements else ""
+        with self._offers_lock:
+            hit = self._offers_cache.get(key)
+            if hit and time.monotonic() - hit[0] < OFFERS_CACHE_TTL:
+                return hit[1]
+        offers = self.get_offers(requirements)
+        with self._offers_lock:
+            self._offers_cache[key] = (time.monotonic(), offers)
+        return offers
+
+    # ---- instances ---------------------------------------------------------------------------
+    def run_job(self, run: Run, job: Job, instance_offer: InstanceOfferWithAvailability,
+                project_ssh_public_key: str, project_ssh_private_key: str,
+                volumes: List[Volume]) -> JobProvisioningData:
+        """Provision an instance for one job (default: create_instance with a job-derived config)."""
+        from dstack_amd.core.models.instances import SSHKey
+
+        cfg = InstanceConfiguration(
+            project_name=run.project_name, instance_name=f"{run.run_spec.run_name}-{job.job_spec.job_num}",
+            user=run.user, ssh_keys=[SSHKey(public=project_ssh_public_key.strip())], volumes=volumes,
+        )
+        return self.create_instance(instance_offer, cfg)
+
+    def create_instance(self, instance_offer: InstanceOfferWithAvailability,
+                        instance_config: InstanceConfiguration) -> JobProvisioningData:
+        raise NotImplementedError(f"{self.TYPE.value} cannot create instances")
+
+    @abstractmethod
+    def terminate_instance(self, instance_id: str, region: str, backend_data: Optional[str] = None) -> None:
+        ...
+
+    def update_provisioning_data(self, provisioning_data: JobProvisioningData, project_ssh_public_key: str,
+                                 project_ssh_private_key: str) -> None:
+        """Fill hostname/internal_ip once the cloud reports them (no-op when already set)."""
+
+    # ---- placement groups --------------------------------------------------------------------
+    def create_placement_group(self, placement_group: PlacementGroup) -> PlacementGroupProvisioningData:
+        raise NotImplementedError()
+
+    def delete_placement_group(self, placement_group: PlacementGroup) -> None:
+        raise NotImplementedError()
+
+    # ---- gateways ----------------------------------------------------------------------------
+    def create_gateway(self, configuration: GatewayComputeConfiguration) -> GatewayProvisioningData:
+        raise NotImplementedError()
+
+    def terminate_gateway(self, instance_id: str, configuration: GatewayComputeConfiguration,
+                          backend_data: Optional[str] = None) -> None:
+        raise NotImplementedError()
+
+    # ---- volumes -----------------------------------------------------------------------------
+    def register_volume(self, volume: Volume) -> VolumeProvisioningData:
+        raise NotImplementedError()
+
+    def create_volume(self, volume: Volume) -> VolumeProvisioningData:
+        raise NotImplementedError()
+
+    def delete_volume(self, volume: Volume) -> None:
+        raise NotImplementedError()
+
+    def attach_volume(self, volume: Volume, instance_id: str) -> VolumeAttachmentData:
+        raise NotImplementedError()
+
+    def detach_volume(self, volume: Volume, instance_id: str, force: bool = False) -> None:
+        raise NotImplementedError()
+
+    def is_volume_detached(self, volume: Volume, instance_id: str) -> bool:
+        return True
+
+
+def offer_matches(offer: InstanceOffer, req: Optional[Requirements]) -> bool:
+    """Catalog matching (reference ``match_requirements``)."""
+    if req is None:
+        return True
+    r: ResourcesSpec = req.resources
+    res = offer.instance.resources
+    if not r.cpu.contains(res.cpus):
+        return False
+    if not r.memory.contains(res.memory_mib / 1024):
+        return False
+    if r.disk and r.disk.size.max is not None and res.disk.size_mib / 1024 < r.disk.size.min:
+        return False
+    if req.spot is not None and res.spot != req.spot:
+        return False
+    if req.max_price is not None and offer.price > req.max_price:
+        return False
+    g = r.gpu
+    if g is None or (g.count.max == 0):
+        return not res.gpus if (g is not None and g.count.max == 0) else True
+    if not g.count.contains(len(res.gpus)):
+        return False
+    if not res.gpus:
+        return g.count.min == 0
+    gpu = res.gpus[0]
+    if g.vendor is not None and gpu.vendor is not None and gpu.vendor != g.vendor:
+        return False
+    if g.name and gpu.name.lower() not in {n.lower() for n in g.name}:
+        return False
+    if g.memory is not None and not g.memory.contains(gpu.memory_mib / 1024):
+        return False
+    if g.total_memory is not None and not g.total_memory.contains(gpu.memory_mib / 1024 * len(res.gpus)):
+        return False
+    return True
+
+
+def choose_disk_size_mib(req: Optional[Requirements], default_gb: int = 100) -> int:
+    if req is None or req.resources.disk is None:
+        return default_gb * 1024
+    size = req.resources.disk.size
+    gb = size.min if size.min is not None else default_gb
+    return int(gb * 1024)
+
+
+def with_availability(offers: List[InstanceOffer], availability=InstanceAvailability.AVAILABLE):
+    return [InstanceOfferWithAvailability(**o.model_dump(), availability=availability) for o in offers]
+
+
+# ---------------------------------------------------------------------------------------------
+# bootstrap scripts (cloud-init / SSH deploy)
+# ---------------------------------------------------------------------------------------------
+def get_shim_env(authorized_keys: List[str], runner_url: str = "", shim_http_port: int = DSTACK_SHIM_HTTP_PORT,
+                 driver: str = "auto") -> Dict[str, str]:
+    return {
+        "DSTACK_SHIM_HTTP_PORT": str(shim_http_port),
+        "DSTACK_RUNNER_HTTP_PORT": str(DSTACK_RUNNER_HTTP_PORT),
+        "DSTACK_RUNNER_SSH_PORT": str(DSTACK_RUNNER_SSH_PORT),
+        "DSTACK_RUNNER_DOWNLOAD_URL": runner_url,
+        "DSTACK_SHIM_DRIVER": driver,
+        "DSTACK_PUBLIC_SSH_KEY": "\n".join(authorized_keys),
+    }
+
+
+def get_shim_commands(authorized_keys: List[str], shim_url: str, runner_url: str, is_privileged: bool = False,
+                      driver: str = "auto") -> List[str]:
+    """Commands a fresh VM runs (cloud-init) to fetch and start the shim (compute.py:216-309)."""
+    env = get_shim_env(authorized_keys, runner_url, driver=driver)
+    exports = " ".join(f"{k}='{v}'" for k, v in env.items() if k != "DSTACK_PUBLIC_SSH_KEY")
+    return [
+        "mkdir -p /root/.dstack-shim",
+        f"curl -fsSL -o /usr/local/bin/dstack-shim '{shim_url}' && chmod +x /usr/local/bin/dstack-shim",
+        f"curl -fsSL -o /root/.dstack-shim/dstack-runner '{runner_url}' && chmod +x /root/.dstack-shim/dstack-runner",
+        f"{exports} nohup /usr/local/bin/dstack-shim --service --driver {driver}"
+        + (" --privileged" if is_privileged else "")
+        + " > /root/.dstack-shim/shim.log 2>&1 &",
+    ]
+
+
+def get_user_data(authorized_keys: List[str], shim_url: str, runner_url: str) -> str:
+    cmds = get_shim_commands(authorized_keys, shim_url, runner_url)
+    keys = "\n".join(f"  - {k}" for k in authorized_keys)
+    runcmd = "\n".join(f"  - {json_quote(c)}" for c in cmds)
+    return f"#cloud-config\nssh_authorized_keys:\n{keys}\nruncmd:\n{runcmd}\n"
+
+
+def json_quote(s: str) -> str:
+    import json
+
+    return json.dumps(s)
+
+
+def get_docker_commands(authorized_keys: List[str], runner_url: str) -> List[str]:
+    """Container-only backends (runpod/vastai/k8s): install sshd and start the runner directly
+    (compute.py:334-387)."""
+    keys = "\\n".join(authorized_keys)
+    return [
+        "export DEBIAN_FRONTEND=noninteractive",
+        "(command -v sshd || (apt-get update -qq && apt-get install -yqq openssh-server)) >/dev/null 2>&1",
+        "mkdir -p ~/.ssh /run/sshd && chmod 700 ~/.ssh",
+        f"printf '{keys}\\n' >> ~/.ssh/authorized_keys && chmod 600 ~/.ssh/authorized_keys",
+        f"$(command -v sshd) -p {DSTACK_RUNNER_SSH_PORT} -o PermitUserEnvironment=yes",
+        f"curl -fsSL -o /usr/local/bin/dstack-runner '{runner_url}' && chmod +x /usr/local/bin/dstack-runner",
+        f"/usr/local/bin/dstack-runner start --http-port {DSTACK_RUNNER_HTTP_PORT} --temp-dir /tmp/runner "
+        "--home-dir /root --working-dir /workflow --ssh-env",
+    ]
+
+
+def raise_compute_error(msg: str):
+    raise ComputeError(msg)
+
+
+class BackendUnavailable(BackendError):
+    pass

@@ -139,3 +139,15 @@ class SSHPortInUseError(SSHError):
 
 class RunnerError(DstackError):
     """The in-container agent (dstack-runner) or host agent (dstack-shim) failed a request."""
+
+
+class ClientError(DstackError):
+    """Client-side failure talking to the server (reference: ``core/errors.py`` ``ClientError``)."""
+
+
+class URLNotFoundError(ClientError):
+    pass
+
+
+class MethodNotAllowedError(ClientError):
+    pass

@@ -1,0 +1,178 @@
+"""FastAPI application (reference: ``S/app.py:67-271``).
+
+Lifespan: migrations -> encryption keys -> admin user + default project + ``config.yml`` -> local
+backend shim -> reconcilers (event-driven scheduler) -> prints the admin token.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import time
+from contextlib import asynccontextmanager
+from typing import Optional
+
+from fastapi import FastAPI, Request
+from fastapi.exceptions import RequestValidationError
+from fastapi.responses import JSONResponse
+
+from dstack_amd import __version__
+from dstack_amd.core.errors import (
+    ForbiddenError,
+    ResourceNotExistsError,
+    ServerClientError,
+    UnauthorizedError,
+)
+from dstack_amd.server import settings
+from dstack_amd.server.db import get_db, migrate, session_scope
+
+logger = logging.getLogger("dstack_amd.server")
+
+
+def configure_logging(level: Optional[str] = None):
+    lvl = getattr(logging, (level or settings.SERVER_LOG_LEVEL).upper(), logging.INFO)
+    fmt = "%(asctime)s %(levelname)s %(name)s: %(message)s"
+    if settings.SERVER_LOG_FORMAT == "json":
+        fmt = '{"ts": "%(asctime)s", "level": "%(levelname)s", "logger": "%(name)s", "msg": "%(message)s"}'
+    logging.basicConfig(level=lvl, format=fmt)
+    logging.getLogger("httpx").setLevel(logging.WARNING)
+
+
+def init_server_state(admin_token: Optional[str] = None):
+    """Idempotent bootstrap shared by the app lifespan and tests."""
+    from dstack_amd.server.services.config import ServerConfigManager
+    from dstack_amd.server.services.pools import get_or_create_default_pool
+    from dstack_amd.server.services.projects import get_or_create_default_project
+    from dstack_amd.server.services.users import get_or_create_admin_user
+
+    migrate()
+    cm = ServerConfigManager()
+    cm.load_config()
+    cm.apply_encryption()
+    with session_scope() as s:
+        admin = get_or_create_admin_user(s, admin_token or settings.SERVER_ADMIN_TOKEN)
+        project = get_or_create_default_project(s, admin, settings.DEFAULT_PROJECT_NAME)
+        get_or_create_default_pool(s, project)
+        cm.apply_config(s, admin)
+        token = admin.token
+    return token
+
+
+def create_app(start_background: bool = True) -> FastAPI:
+    @asynccontextmanager
+    async def lifespan(app: FastAPI):
+        from starlette.concurrency import run_in_threadpool
+
+        token = await run_in_threadpool(init_server_state)
+        app.state.admin_token = token
+        sched = None
+        if start_background and settings.SERVER_BACKGROUND_PROCESSING_ENABLED:
+            from dstack_amd.server.background import start_background_tasks
+
+            sched = start_background_tasks()
+        url = settings.SERVER_URL
+        print(f"The admin token is {token}", flush=True)
+        print(f"The dstack-amd server {__version__} is running at {url}", flush=True)
+        _write_client_config(url, token)
+        yield
+        if sched is not None:
+            sched.shutdown()
+        from dstack_amd.core.backends.local import LocalShim
+
+        if LocalShim._instance is not None:
+            LocalShim._instance.stop()
+
+    app = FastAPI(title="dstack-amd", version=__version__, lifespan=lifespan, docs_url="/api/docs",
+                  openapi_url="/api/openapi.json")
+    register_routes(app)
+    return app
+
+
+def _write_client_config(url: str, token: str):
+    """Make the local CLI usable right after `dstack server` (``update_default_project``)."""
+    if os.environ.get("DSTACK_SERVER_NO_CLIENT_CONFIG"):
+        return
+    try:
+        from dstack_amd.core.services.configs import ConfigManager
+
+        cm = ConfigManager()
+        cm.configure_project(settings.DEFAULT_PROJECT_NAME, url, token, default=True)
+        cm.save()
+    except Exception as e:  # noqa: BLE001
+        logger.debug("client config not written: %s", e)
+
+
+def _error(status: int, msg: str, code: str) -> JSONResponse:
+    return JSONResponse(status_code=status, content={"detail": [{"msg": msg, "code": code}]})
+
+
+def register_routes(app: FastAPI):
+    from dstack_amd.server.routers import core, proxy, runs
+
+    for r in (core.server_router, core.users_router, core.projects_router, core.backends_router,
+              core.project_backends_router, core.secrets_router, core.repos_router, runs.runs_root,
+              runs.runs_router, runs.fleets_root, runs.fleets_router, runs.instances_root, runs.volumes_root,
+              runs.volumes_router, runs.gateways_router, runs.logs_router, runs.metrics_router, runs.pools_root,
+              runs.pool_router, proxy.router):
+        app.include_router(r)
+
+    @app.exception_handler(UnauthorizedError)
+    async def _unauth(request: Request, exc: UnauthorizedError):
+        return _error(401, exc.msg, exc.code)
+
+    @app.exception_handler(ForbiddenError)
+    async def _forbidden(request: Request, exc: ForbiddenError):
+        return _error(403, exc.msg, exc.code)
+
+    @app.exception_handler(ResourceNotExistsError)
+    async def _notfound(request: Request, exc: ResourceNotExistsError):
+        return _error(400, exc.msg, exc.code)
+
+    @app.exception_handler(ServerClientError)
+    async def _client_error(request: Request, exc: ServerClientError):
+        return _error(400, exc.msg, exc.code)
+
+    @app.exception_handler(RequestValidationError)
+    async def _validation(request: Request, exc: RequestValidationError):
+        return JSONResponse(status_code=422, content={"detail": jsonable_errors(exc.errors())})
+
+    @app.middleware("http")
+    async def log_request(request: Request, call_next):
+        start = time.perf_counter()
+        client_version = request.headers.get("x-api-version")
+        if client_version and not _compatible(client_version):
+            return _error(400, f"The client version {client_version} is incompatible with the server {__version__}",
+                          "error")
+        response = await call_next(request)
+        logger.debug("%s %s %s %.1f ms", request.method, request.url.path, response.status_code,
+                     (time.perf_counter() - start) * 1e3)
+        return response
+
+    @app.get("/healthcheck")
+    def healthcheck():
+        return {"status": "running"}
+
+    @app.get("/api/server/scheduler_stats")
+    def scheduler_stats():
+        from dstack_amd.server.background.scheduler import get_scheduler
+
+        return get_scheduler().stats()
+
+
+def jsonable_errors(errors):
+    out = []
+    for e in errors:
+        out.append({k: (str(v) if k == "ctx" else v) for k, v in e.items() if k != "input"})
+    return out
+
+
+def _compatible(client_version: str) -> bool:
+    if client_version in ("latest", "0.0.0") or __version__.startswith("0.0"):
+        return True
+    try:
+        return client_version.split(".")[0] == __version__.split(".")[0]
+    except Exception:  # noqa: BLE001
+        return True
+
+
+_ = get_db

@@ -1,0 +1,230 @@
+"""Instance lifecycle (reference: ``S/background/tasks/process_instances.py:112-965``).
+
+PENDING: SSH-fleet hosts are deployed (shim + runner over ssh/scp, host_info with the amdsmi/xGMI
+topology); cloud-fleet instances are created through the backends.  PROVISIONING: wait for the
+hostname, then the shim healthcheck -> IDLE.  IDLE/BUSY: shim healthcheck (unreachable hosts are
+terminated after 20 min), idle-duration expiry -> TERMINATING.  TERMINATING: backend terminate.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+from datetime import timedelta
+from typing import Optional
+
+from sqlalchemy import select
+from sqlalchemy.orm import Session
+
+from dstack_amd.core.backends.remote import deploy_ssh_instance, host_info_to_instance_type, remote_backend_data, split_blocks
+from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.instances import (
+    InstanceAvailability,
+    InstanceConfiguration,
+    InstanceOfferWithAvailability,
+    InstanceStatus,
+    RemoteConnectionInfo,
+    SSHKey,
+)
+from dstack_amd.core.models.profiles import Profile
+from dstack_amd.core.models.runs import JobProvisioningData, Requirements
+from dstack_amd.server.background import scheduler
+from dstack_amd.server.background.common import claim_and_process
+from dstack_amd.server.models import InstanceModel
+from dstack_amd.server.services import backends as backends_services
+from dstack_amd.server.services import offers as offers_services
+from dstack_amd.server.services import pools as pools_services
+from dstack_amd.server.services.runner.client import get_shim_client
+from dstack_amd.utils.common import get_current_datetime, get_ip_from_network
+
+logger = logging.getLogger(__name__)
+
+TERMINATION_DEADLINE_OFFSET = timedelta(minutes=20)
+PROVISIONING_DEADLINE = timedelta(minutes=20)
+SSH_DEPLOY_RETRY = timedelta(seconds=30)
+
+
+def process_instances(batch: int = 5) -> bool:
+    def select_ids(s: Session):
+        return s.execute(select(InstanceModel.id).where(InstanceModel.status != InstanceStatus.TERMINATED.value)
+                         .where(InstanceModel.deleted == False)  # noqa: E712
+                         .order_by(InstanceModel.last_processed_at).limit(batch * 4)).scalars()
+
+    return claim_and_process("instances", select_ids, _process_instance, batch)
+
+
+def _process_instance(s: Session, inst_id):
+    inst = s.get(InstanceModel, inst_id)
+    if inst is None:
+        return
+    st = InstanceStatus(inst.status)
+    if st == InstanceStatus.PENDING:
+        if inst.remote_connection_info:
+            _add_remote(s, inst)
+        else:
+            _create_instance(s, inst)
+    elif st == InstanceStatus.PROVISIONING:
+        _check_provisioning(s, inst)
+    elif st in (InstanceStatus.IDLE, InstanceStatus.BUSY):
+        _check_instance(s, inst)
+    elif st == InstanceStatus.TERMINATING:
+        _terminate(s, inst)
+    inst.last_processed_at = get_current_datetime()
+
+
+def _add_remote(s: Session, inst: InstanceModel):
+    if inst.last_retry_at and get_current_datetime() - inst.last_retry_at < SSH_DEPLOY_RETRY:
+        return
+    inst.last_retry_at = get_current_datetime()
+    rci = RemoteConnectionInfo.model_validate_json(inst.remote_connection_info)
+    project = inst.project
+    key = next((k.private for k in rci.ssh_keys if k.private), None) or project.ssh_private_key
+    try:
+        host_info = deploy_ssh_instance(rci, project.ssh_public_key, key)
+    except Exception as e:  # noqa: BLE001
+        logger.warning("instance %s: SSH deploy failed: %s", inst.name, e)
+        inst.termination_reason = f"deploy failed: {e}"[:4000]
+        if get_current_datetime() - inst.created_at > TERMINATION_DEADLINE_OFFSET:
+            inst.status = InstanceStatus.TERMINATED.value
+        return
+    itype, topo = host_info_to_instance_type(host_info)
+    bd = json.loads(inst.backend_data or "{}")
+    internal_ip = bd.get("internal_ip") or get_ip_from_network(bd.get("network"), host_info.get("addresses") or [])
+    if internal_ip is None and bd.get("network"):
+        inst.termination_reason = f"no address in network {bd.get('network')}"
+        inst.status = InstanceStatus.TERMINATED.value
+        return
+    total_blocks = split_blocks(topo, bd.get("blocks", 1))
+    jpd = JobProvisioningData(
+        backend=BackendType.REMOTE, instance_type=itype, instance_id=inst.name, hostname=rci.host,
+        internal_ip=internal_ip or rci.host, region="remote", price=0.0, username=rci.ssh_user, ssh_port=rci.port,
+        dockerized=True, backend_data=remote_backend_data(direct=bool(bd.get("direct"))),
+    )
+    offer = InstanceOfferWithAvailability(backend=BackendType.REMOTE, instance=itype, region="remote", price=0.0,
+                                          availability=InstanceAvailability.AVAILABLE, total_blocks=total_blocks)
+    inst.job_provisioning_data = jpd.model_dump_json()
+    inst.offer = offer.model_dump_json()
+    inst.host_topology = topo.model_dump_json()
+    inst.total_blocks = total_blocks
+    inst.status = InstanceStatus.IDLE.value
+    inst.started_at = get_current_datetime()
+    inst.termination_reason = None
+    scheduler.wake(scheduler.SUBMITTED_JOBS)
+
+
+def _create_instance(s: Session, inst: InstanceModel):
+    project = inst.project
+    profile = Profile.model_validate_json(inst.profile) if inst.profile else Profile(name="default")
+    req = Requirements.model_validate_json(inst.requirements) if inst.requirements else None
+    if req is None:
+        inst.status = InstanceStatus.TERMINATED.value
+        inst.termination_reason = "no requirements"
+        return
+    offers = offers_services.get_offers_by_requirements(s, project, profile, req, exclude_not_available=True)
+    cfg = InstanceConfiguration(project_name=project.name, instance_name=inst.name, user="",
+                                ssh_keys=[SSHKey(public=project.ssh_public_key.strip())])
+    for compute, offer in offers[:15]:
+        if offer.backend == BackendType.REMOTE:
+            continue
+        try:
+            jpd = compute.create_instance(offer, cfg)
+        except Exception as e:  # noqa: BLE001
+            logger.info("instance %s: %s/%s failed: %s", inst.name, offer.backend.value, offer.instance.name, e)
+            continue
+        inst.backend = jpd.backend.value
+        inst.region = jpd.region
+        inst.price = jpd.price
+        inst.offer = offer.model_dump_json()
+        inst.job_provisioning_data = jpd.model_dump_json()
+        inst.total_blocks = 1
+        inst.backend_data = jpd.backend_data
+        inst.status = (InstanceStatus.IDLE if jpd.backend == BackendType.LOCAL else InstanceStatus.PROVISIONING).value
+        inst.started_at = get_current_datetime()
+        if jpd.backend == BackendType.LOCAL:
+            from dstack_amd.core.backends.local import LocalShim
+
+            _, topo = host_info_to_instance_type(LocalShim.get().host_info)
+            inst.host_topology = topo.model_dump_json()
+        return
+    inst.termination_reason = "no offers / no capacity"
+    if get_current_datetime() - inst.created_at > timedelta(hours=24):
+        inst.status = InstanceStatus.TERMINATED.value
+
+
+def _check_provisioning(s: Session, inst: InstanceModel):
+    jpd = pools_services.instance_jpd(inst)
+    if jpd is None:
+        return
+    if not jpd.hostname:
+        try:
+            compute = backends_services.get_project_backend(s, inst.project, jpd.backend)
+            compute.update_provisioning_data(jpd, inst.project.ssh_public_key, inst.project.ssh_private_key)
+            inst.job_provisioning_data = jpd.model_dump_json()
+        except Exception as e:  # noqa: BLE001
+            logger.debug("update_provisioning_data: %s", e)
+    if jpd.hostname and _shim_healthy(inst, jpd):
+        inst.status = (InstanceStatus.BUSY if (inst.busy_blocks or 0) > 0 else InstanceStatus.IDLE).value
+        scheduler.wake(scheduler.RUNNING_JOBS, scheduler.SUBMITTED_JOBS)
+        return
+    if get_current_datetime() - inst.created_at > PROVISIONING_DEADLINE:
+        inst.status = InstanceStatus.TERMINATING.value
+        inst.termination_reason = "provisioning timeout"
+
+
+def _shim_healthy(inst: InstanceModel, jpd: JobProvisioningData) -> bool:
+    try:
+        return get_shim_client(jpd, inst.project.ssh_private_key).healthcheck() is not None
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def _check_instance(s: Session, inst: InstanceModel):
+    jpd = pools_services.instance_jpd(inst)
+    if jpd is None:
+        return
+    now = get_current_datetime()
+    healthy = _shim_healthy(inst, jpd) if jpd.dockerized else True
+    if healthy:
+        inst.unreachable = False
+        inst.termination_deadline = None
+        inst.health_status = None
+    else:
+        inst.unreachable = True
+        inst.health_status = "shim unreachable"
+        if inst.termination_deadline is None:
+            inst.termination_deadline = now + TERMINATION_DEADLINE_OFFSET
+        elif now > inst.termination_deadline and jpd.backend != BackendType.REMOTE:
+            inst.status = InstanceStatus.TERMINATING.value
+            inst.termination_reason = "unreachable"
+            return
+    if inst.status == InstanceStatus.IDLE.value and (inst.busy_blocks or 0) == 0:
+        idle_limit = inst.termination_idle_time
+        if idle_limit is not None and idle_limit >= 0 and inst.termination_policy != "dont-destroy":
+            since = inst.last_job_processed_at or inst.started_at or inst.created_at
+            if now - since > timedelta(seconds=idle_limit):
+                inst.status = InstanceStatus.TERMINATING.value
+                inst.termination_reason = "idle timeout"
+                scheduler.wake(scheduler.INSTANCES)
+
+
+def _terminate(s: Session, inst: InstanceModel):
+    jpd = pools_services.instance_jpd(inst)
+    if jpd is not None and jpd.backend not in (BackendType.REMOTE, BackendType.LOCAL):
+        try:
+            compute = backends_services.get_project_backend(s, inst.project, jpd.backend)
+            compute.terminate_instance(jpd.instance_id, jpd.region, jpd.backend_data)
+        except Exception as e:  # noqa: BLE001
+            now = get_current_datetime()
+            inst.first_termination_retry_at = inst.first_termination_retry_at or now
+            inst.last_termination_retry_at = now
+            if now - inst.first_termination_retry_at < timedelta(minutes=15):
+                logger.warning("instance %s: terminate failed (will retry): %s", inst.name, e)
+                return
+    inst.status = InstanceStatus.TERMINATED.value
+    inst.finished_at = get_current_datetime()
+    inst.deleted = True
+    inst.deleted_at = get_current_datetime()
+    scheduler.wake(scheduler.FLEETS)
+
+
+_ = Optional

@@ -1,0 +1,295 @@
+"""REST routers: runs, fleets, instances, volumes, gateways, logs, metrics (reference:
+``S/routers/{runs,fleets,instances,volumes,gateways,logs,metrics,pools}.py``)."""
+
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+from fastapi import APIRouter, Depends, Query
+from sqlalchemy import select
+from sqlalchemy.orm import Session
+
+from dstack_amd.core.errors import ResourceNotExistsError, ServerClientError
+from dstack_amd.core.models.fleets import Fleet, FleetPlan, Instance
+from dstack_amd.core.models.gateways import Gateway, GatewayPlan, GatewaySpec
+from dstack_amd.core.models.logs import JobMetrics, JobSubmissionLogs
+from dstack_amd.core.models.runs import Run, RunPlan
+from dstack_amd.core.models.volumes import Volume, VolumePlan, VolumeSpec
+from dstack_amd.server import schemas
+from dstack_amd.server.deps import get_session
+from dstack_amd.server.models import JobModel, ProjectModel, UserModel
+from dstack_amd.server.security.permissions import authenticated, project_admin, project_manager, project_member
+from dstack_amd.server.services import fleets as fleets_services
+from dstack_amd.server.services import gateways as gateways_services
+from dstack_amd.server.services import logs as logs_services
+from dstack_amd.server.services import metrics as metrics_services
+from dstack_amd.server.services import pools as pools_services
+from dstack_amd.server.services import projects as projects_services
+from dstack_amd.server.services import runs as runs_services
+from dstack_amd.server.services import volumes as volumes_services
+
+UP = Tuple[UserModel, ProjectModel]
+
+runs_root = APIRouter(prefix="/api/runs", tags=["runs"])
+runs_router = APIRouter(prefix="/api/project/{project_name}/runs", tags=["runs"])
+fleets_root = APIRouter(prefix="/api/fleets", tags=["fleets"])
+fleets_router = APIRouter(prefix="/api/project/{project_name}/fleets", tags=["fleets"])
+instances_root = APIRouter(prefix="/api/instances", tags=["instances"])
+volumes_root = APIRouter(prefix="/api/volumes", tags=["volumes"])
+volumes_router = APIRouter(prefix="/api/project/{project_name}/volumes", tags=["volumes"])
+gateways_router = APIRouter(prefix="/api/project/{project_name}/gateways", tags=["gateways"])
+logs_router = APIRouter(prefix="/api/project/{project_name}/logs", tags=["logs"])
+metrics_router = APIRouter(prefix="/api/project/{project_name}/metrics", tags=["metrics"])
+pools_root = APIRouter(prefix="/api/pools", tags=["pools"])
+pool_router = APIRouter(prefix="/api/project/{project_name}/pool", tags=["pools"])
+
+
+# ---- runs -----------------------------------------------------------------------------------
+@runs_root.post("/list")
+def list_runs(body: schemas.ListRunsRequest, user: UserModel = Depends(authenticated),
+              s: Session = Depends(get_session)) -> List[Run]:
+    return runs_services.list_user_runs(s, user, body.project_name, body.repo_id, body.only_active, body.limit,
+                                        body.prev_submitted_at, body.ascending)
+
+
+@runs_router.post("/get")
+def get_run(body: schemas.GetRunRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> Run:
+    r = runs_services.get_run(s, up[1], body.run_name, body.id)
+    if r is None:
+        raise ResourceNotExistsError("Run not found")
+    return r
+
+
+@runs_router.post("/get_plan")
+def get_run_plan(body: schemas.GetRunPlanRequest, up: UP = Depends(project_member),
+                 s: Session = Depends(get_session)) -> RunPlan:
+    return runs_services.get_plan(s, up[1], up[0], body.run_spec, body.max_offers or 50)
+
+
+@runs_router.post("/apply")
+def apply_plan(body: schemas.ApplyRunPlanRequest, up: UP = Depends(project_member),
+               s: Session = Depends(get_session)) -> Run:
+    return runs_services.apply_plan(s, up[1], up[0], body.plan.run_spec, body.plan.current_resource, body.force)
+
+
+@runs_router.post("/submit")
+def submit_run(body: schemas.SubmitRunRequest, up: UP = Depends(project_member),
+               s: Session = Depends(get_session)) -> Run:
+    return runs_services.submit_run(s, up[1], up[0], body.run_spec)
+
+
+@runs_router.post("/stop")
+def stop_runs(body: schemas.StopRunsRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+    runs_services.stop_runs(s, up[1], body.runs_names, body.abort)
+    return {}
+
+
+@runs_router.post("/delete")
+def delete_runs(body: schemas.DeleteRunsRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+    runs_services.delete_runs(s, up[1], body.runs_names)
+    return {}
+
+
+# ---- fleets ---------------------------------------------------------------------------------
+@fleets_root.post("/list")
+def list_all_fleets(body: Optional[schemas.ListFleetsRequest] = None, user: UserModel = Depends(authenticated),
+                    s: Session = Depends(get_session)) -> List[Fleet]:
+    out = []
+    for p in projects_services.list_user_projects(s, user):
+        if body and body.project_name and p.name != body.project_name:
+            continue
+        out += [fleets_services.fleet_model_to_fleet(f) for f in fleets_services.list_project_fleets(s, p)]
+    return out
+
+
+@fleets_router.post("/list")
+def list_fleets(up: UP = Depends(project_member), s: Session = Depends(get_session)) -> List[Fleet]:
+    return [fleets_services.fleet_model_to_fleet(f) for f in fleets_services.list_project_fleets(s, up[1])]
+
+
+@fleets_router.post("/get")
+def get_fleet(body: schemas.GetFleetRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> Fleet:
+    f = fleets_services.get_fleet_by_name(s, up[1], body.name) if body.name else None
+    if f is None:
+        raise ResourceNotExistsError("Fleet not found")
+    return fleets_services.fleet_model_to_fleet(f)
+
+
+@fleets_router.post("/get_plan")
+def get_fleet_plan(body: schemas.GetFleetPlanRequest, up: UP = Depends(project_member),
+                   s: Session = Depends(get_session)) -> FleetPlan:
+    return fleets_services.get_plan(s, up[1], up[0], body.spec)
+
+
+@fleets_router.post("/create")
+def create_fleet(body: schemas.CreateFleetRequest, up: UP = Depends(project_manager),
+                 s: Session = Depends(get_session)) -> Fleet:
+    return fleets_services.create_fleet(s, up[1], up[0], body.spec)
+
+
+@fleets_router.post("/delete")
+def delete_fleets(body: schemas.DeleteFleetsRequest, up: UP = Depends(project_manager),
+                  s: Session = Depends(get_session)):
+    fleets_services.delete_fleets(s, up[1], body.names)
+    return {}
+
+
+@fleets_router.post("/delete_instances")
+def delete_fleet_instances(body: schemas.DeleteFleetInstancesRequest, up: UP = Depends(project_manager),
+                           s: Session = Depends(get_session)):
+    fleets_services.delete_fleet_instances(s, up[1], body.name, body.instance_nums)
+    return {}
+
+
+# ---- instances / legacy pools ---------------------------------------------------------------
+@instances_root.post("/list")
+def list_instances(body: Optional[schemas.ListInstancesRequest] = None, user: UserModel = Depends(authenticated),
+                   s: Session = Depends(get_session)) -> List[Instance]:
+    out = []
+    for p in projects_services.list_user_projects(s, user):
+        if body and body.project_names and p.name not in body.project_names:
+            continue
+        for inst in pools_services.list_project_instances(s, p, include_terminated=not (body and body.only_active)):
+            if body and body.fleet_ids and inst.fleet_id not in body.fleet_ids:
+                continue
+            out.append(pools_services.instance_model_to_instance(inst))
+    return out[: (body.limit if body else 1000)]
+
+
+@pools_root.post("/list_instances")
+def pools_list_instances(user: UserModel = Depends(authenticated), s: Session = Depends(get_session)) -> List[Instance]:
+    return list_instances(None, user, s)
+
+
+@pool_router.post("/list")
+def pool_list(up: UP = Depends(project_member), s: Session = Depends(get_session)):
+    pool = pools_services.get_or_create_default_pool(s, up[1])
+    insts = pools_services.list_project_instances(s, up[1])
+    return [{"name": pool.name, "default": True, "created_at": pool.created_at, "total_instances": len(insts),
+             "available_instances": sum(1 for i in insts if i.status == "idle")}]
+
+
+@pool_router.post("/show")
+def pool_show(up: UP = Depends(project_member), s: Session = Depends(get_session)):
+    pool = pools_services.get_or_create_default_pool(s, up[1])
+    return {"name": pool.name, "instances": [pools_services.instance_model_to_instance(i)
+                                              for i in pools_services.list_project_instances(s, up[1])]}
+
+
+# ---- volumes --------------------------------------------------------------------------------
+@volumes_root.post("/list")
+def list_all_volumes(body: Optional[schemas.ListVolumesRequest] = None, user: UserModel = Depends(authenticated),
+                     s: Session = Depends(get_session)) -> List[Volume]:
+    out = []
+    for p in projects_services.list_user_projects(s, user):
+        if body and body.project_name and p.name != body.project_name:
+            continue
+        out += [volumes_services.volume_model_to_volume(v) for v in volumes_services.list_project_volumes(s, p)]
+    return out
+
+
+@volumes_router.post("/list")
+def list_volumes(up: UP = Depends(project_member), s: Session = Depends(get_session)) -> List[Volume]:
+    return [volumes_services.volume_model_to_volume(v) for v in volumes_services.list_project_volumes(s, up[1])]
+
+
+@volumes_router.post("/get")
+def get_volume(body: schemas.GetVolumeRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> Volume:
+    v = volumes_services.get_volume_by_name(s, up[1], body.name)
+    if v is None:
+        raise ResourceNotExistsError("Volume not found")
+    return volumes_services.volume_model_to_volume(v)
+
+
+@volumes_router.post("/get_plan")
+def get_volume_plan(body: dict, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> VolumePlan:
+    return volumes_services.get_plan(s, up[1], up[0], VolumeSpec.model_validate(body["spec"]))
+
+
+@volumes_router.post("/create")
+def create_volume(body: schemas.CreateVolumeRequest, up: UP = Depends(project_member),
+                  s: Session = Depends(get_session)) -> Volume:
+    return volumes_services.create_volume(s, up[1], up[0], body.configuration)
+
+
+@volumes_router.post("/delete")
+def delete_volumes(body: schemas.DeleteVolumesRequest, up: UP = Depends(project_member),
+                   s: Session = Depends(get_session)):
+    volumes_services.delete_volumes(s, up[1], body.names)
+    return {}
+
+
+# ---- gateways -------------------------------------------------------------------------------
+@gateways_router.post("/list")
+def list_gateways(up: UP = Depends(project_member), s: Session = Depends(get_session)) -> List[Gateway]:
+    return [gateways_services.gateway_model_to_gateway(g) for g in gateways_services.list_project_gateways(s, up[1])]
+
+
+@gateways_router.post("/get")
+def get_gateway(body: schemas.GetGatewayRequest, up: UP = Depends(project_member),
+                s: Session = Depends(get_session)) -> Gateway:
+    g = gateways_services.get_gateway_by_name(s, up[1], body.name)
+    if g is None:
+        raise ResourceNotExistsError("Gateway not found")
+    return gateways_services.gateway_model_to_gateway(g)
+
+
+@gateways_router.post("/get_plan")
+def get_gateway_plan(body: dict, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> GatewayPlan:
+    return gateways_services.get_plan(s, up[1], up[0], GatewaySpec.model_validate(body["spec"]))
+
+
+@gateways_router.post("/create")
+def create_gateway(body: schemas.CreateGatewayRequest, up: UP = Depends(project_admin),
+                   s: Session = Depends(get_session)) -> Gateway:
+    return gateways_services.create_gateway(s, up[1], body.configuration)
+
+
+@gateways_router.post("/delete")
+def delete_gateways(body: schemas.DeleteGatewaysRequest, up: UP = Depends(project_admin),
+                    s: Session = Depends(get_session)):
+    gateways_services.delete_gateways(s, up[1], body.names)
+    return {}
+
+
+@gateways_router.post("/set_default")
+def set_default_gateway(body: schemas.SetDefaultGatewayRequest, up: UP = Depends(project_admin),
+                        s: Session = Depends(get_session)):
+    gateways_services.set_default_gateway(s, up[1], body.name)
+    return {}
+
+
+@gateways_router.post("/set_wildcard_domain")
+def set_wildcard_domain(body: schemas.SetWildcardDomainRequest, up: UP = Depends(project_admin),
+                        s: Session = Depends(get_session)) -> Gateway:
+    return gateways_services.set_wildcard_domain(s, up[1], body.name, body.wildcard_domain)
+
+
+# ---- logs / metrics -------------------------------------------------------------------------
+@logs_router.post("/poll")
+def poll_logs(body: schemas.PollLogsRequest, up: UP = Depends(project_member)) -> JobSubmissionLogs:
+    from datetime import datetime
+
+    start = body.start_time
+    if body.next_token:
+        try:
+            start = datetime.fromisoformat(body.next_token)
+        except ValueError:
+            raise ServerClientError("invalid next_token")
+    return logs_services.get_default_log_storage().poll_logs(
+        up[1].name, body.run_name, str(body.job_submission_id), start, body.end_time, body.descending, body.limit,
+        body.diagnose)
+
+
+@metrics_router.get("/job/{run_name}")
+def get_job_metrics(run_name: str, replica_num: int = Query(0), job_num: int = Query(0), limit: int = Query(2),
+                    up: UP = Depends(project_member), s: Session = Depends(get_session)) -> JobMetrics:
+    run = runs_services.get_run_by_name_or_error(s, up[1], run_name)
+    jobs = [j for j in run.jobs if j.replica_num == replica_num and j.job_num == job_num]
+    if not jobs:
+        raise ResourceNotExistsError("Job not found")
+    job = max(jobs, key=lambda j: j.submission_num)
+    return metrics_services.get_job_metrics(s, job, limit)
+
+
+_ = (select, JobModel)

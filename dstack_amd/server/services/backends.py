@@ -1,0 +1,166 @@
+"""Backend registry, configurators and offer fan-out (reference:
+``S/services/backends/__init__.py:36-451``, ``S/services/backends/configurators/*``).
+
+A project's backends are rows of ``backends`` (type + JSON config + encrypted auth).  The ``local``
+backend is implicit (enabled by ``DSTACK_LOCAL_BACKEND_ENABLED``); the ``remote`` backend (SSH
+fleets) needs no configuration.  Cloud backends are configured with credentials; their offers
+come from the built-in catalog (``core/backends/catalog.py``).
+"""
+
+from __future__ import annotations
+
+import concurrent.futures as cf
+import json
+import threading
+import time
+import uuid
+from typing import Dict, List, Optional, Tuple
+
+from sqlalchemy import select
+from sqlalchemy.orm import Session
+
+from dstack_amd.core.backends.base import Compute
+from dstack_amd.core.errors import BackendNotAvailable, ResourceExistsError, ResourceNotExistsError, ServerClientError
+from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.instances import InstanceAvailability, InstanceOfferWithAvailability
+from dstack_amd.core.models.runs import Requirements
+from dstack_amd.server import settings
+from dstack_amd.server.models import BackendModel, ProjectModel
+
+
+def _make_compute(backend_type: BackendType, config: dict, auth: dict) -> Compute:
+    if backend_type == BackendType.LOCAL:
+        from dstack_amd.core.backends.local import LocalCompute
+
+        return LocalCompute()
+    if backend_type == BackendType.REMOTE:
+        from dstack_amd.core.backends.remote import RemoteCompute
+
+        return RemoteCompute()
+    from dstack_amd.core.backends.catalog import CatalogCompute
+
+    return CatalogCompute(backend_type, config, auth)
+
+
+CONFIGURABLE_BACKENDS = [b for b in BackendType if b not in (BackendType.LOCAL, BackendType.REMOTE)]
+
+_cache: Dict[Tuple[uuid.UUID, str, str], Compute] = {}
+_cache_lock = threading.Lock()
+
+
+def list_backend_types() -> List[str]:
+    return [b.value for b in BackendType]
+
+
+def get_project_backends(s: Session, project: ProjectModel) -> List[Tuple[BackendType, Compute]]:
+    out: List[Tuple[BackendType, Compute]] = []
+    rows = list(s.execute(select(BackendModel).where(BackendModel.project_id == project.id)).scalars())
+    for row in rows:
+        key = (project.id, row.type, row.config + "|" + (row.auth or ""))
+        with _cache_lock:
+            comp = _cache.get(key)
+            if comp is None:
+                comp = _make_compute(BackendType(row.type), json.loads(row.config or "{}"), json.loads(row.auth or "{}"))
+                _cache[key] = comp
+        out.append((BackendType(row.type), comp))
+    if settings.LOCAL_BACKEND_ENABLED and not any(t == BackendType.LOCAL for t, _ in out):
+        out.append((BackendType.LOCAL, get_local_compute()))
+    return out
+
+
+_local: Optional[Compute] = None
+_remote: Optional[Compute] = None
+
+
+def get_local_compute() -> Compute:
+    global _local
+    if _local is None:
+        from dstack_amd.core.backends.local import LocalCompute
+
+        _local = LocalCompute()
+    return _local
+
+
+def get_remote_compute() -> Compute:
+    global _remote
+    if _remote is None:
+        from dstack_amd.core.backends.remote import RemoteCompute
+
+        _remote = RemoteCompute()
+    return _remote
+
+
+def get_project_backend(s: Session, project: ProjectModel, backend_type: BackendType) -> Compute:
+    if backend_type == BackendType.REMOTE:
+        return get_remote_compute()
+    for t, c in get_project_backends(s, project):
+        if t == backend_type:
+            return c
+    raise BackendNotAvailable(f"Backend {backend_type.value} is not configured for project {project.name}")
+
+
+def create_backend(s: Session, project: ProjectModel, config: dict) -> BackendModel:
+    btype = BackendType(config.get("type"))
+    if btype in (BackendType.LOCAL, BackendType.REMOTE):
+        raise ServerClientError(f"{btype.value} backend needs no configuration")
+    existing = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
+                                                    BackendModel.type == btype.value)).scalar_one_or_none()
+    if existing is not None:
+        raise ResourceExistsError(f"Backend {btype.value} exists")
+    cfg = {k: v for k, v in config.items() if k not in ("type", "creds")}
+    row = BackendModel(id=uuid.uuid4(), project_id=project.id, type=btype.value, config=json.dumps(cfg),
+                       auth=json.dumps(config.get("creds") or {}))
+    s.add(row)
+    s.flush()
+    return row
+
+
+def update_backend(s: Session, project: ProjectModel, config: dict) -> BackendModel:
+    btype = BackendType(config.get("type"))
+    row = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
+                                               BackendModel.type == btype.value)).scalar_one_or_none()
+    if row is None:
+        raise ResourceNotExistsError(f"Backend {btype.value} not found")
+    row.config = json.dumps({k: v for k, v in config.items() if k not in ("type", "creds")})
+    if config.get("creds") is not None:
+        row.auth = json.dumps(config["creds"])
+    return row
+
+
+def delete_backends(s: Session, project: ProjectModel, names: List[str]):
+    for n in names:
+        row = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
+                                                   BackendModel.type == n)).scalar_one_or_none()
+        if row is not None:
+            s.delete(row)
+
+
+def backend_config_info(s: Session, project: ProjectModel, name: str) -> dict:
+    row = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
+                                               BackendModel.type == name)).scalar_one_or_none()
+    if row is None:
+        raise ResourceNotExistsError()
+    return {"type": row.type, **json.loads(row.config or "{}")}
+
+
+def get_instance_offers(
+    backends: List[Tuple[BackendType, Compute]], requirements: Requirements, exclude_not_available: bool = False,
+) -> List[Tuple[Compute, InstanceOfferWithAvailability]]:
+    """Query every backend concurrently, merge by price; unavailable offers last
+    (``get_instance_offers`` ``S/services/backends/__init__.py:417-451``)."""
+    results: List[Tuple[Compute, InstanceOfferWithAvailability]] = []
+    if not backends:
+        return results
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(backends))) as ex:
+        futs = {ex.submit(c.get_offers_cached, requirements): c for _, c in backends}
+        for fut in cf.as_completed(futs):
+            comp = futs[fut]
+            try:
+                offers = fut.result()
+            except Exception:  # noqa: BLE001 - a broken backend must not break planning
+                continue
+            results.extend((comp, o) for o in offers)
+    if exclude_not_available:
+        results = [r for r in results if r[1].availability.is_available()]
+    results.sort(key=lambda r: (not r[1].availability.is_available(), r[1].price))
+    return results

@@ -1,0 +1,188 @@
+"""Fleets (reference: ``S/services/fleets.py:236-793``): plan, create (cloud: ``nodes`` pending
+instances, optionally in a placement group; SSH: one instance per host), delete, list."""
+
+from __future__ import annotations
+
+import json
+import uuid
+from typing import List, Optional
+
+from sqlalchemy import select
+from sqlalchemy.orm import Session
+
+from dstack_amd.core.errors import ResourceExistsError, ResourceNotExistsError, ServerClientError
+from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.common import Duration
+from dstack_amd.core.models.envs import Env
+from dstack_amd.core.models.fleets import (
+    Fleet,
+    FleetConfiguration,
+    FleetPlan,
+    FleetSpec,
+    FleetStatus,
+    InstanceGroupPlacement,
+    SSHHostParams,
+)
+from dstack_amd.core.models.instances import InstanceStatus, RemoteConnectionInfo, SSHKey
+from dstack_amd.core.models.profiles import DEFAULT_FLEET_TERMINATION_IDLE_TIME, Profile
+from dstack_amd.core.models.resources import ResourcesSpec
+from dstack_amd.core.models.runs import Requirements, get_policy_map
+from dstack_amd.core.models.profiles import SpotPolicy
+from dstack_amd.server.background import scheduler
+from dstack_amd.server.models import FleetModel, InstanceModel, ProjectModel, UserModel
+from dstack_amd.server.services import offers as offers_services
+from dstack_amd.server.services import pools as pools_services
+from dstack_amd.server.services.locking import get_locker
+from dstack_amd.utils.common import generate_name, get_current_datetime
+
+
+def fleet_model_to_fleet(f: FleetModel, include_terminated: bool = False) -> Fleet:
+    instances = [pools_services.instance_model_to_instance(i) for i in sorted(f.instances, key=lambda i: i.instance_num)
+                 if include_terminated or i.status != InstanceStatus.TERMINATED.value]
+    return Fleet(id=f.id, name=f.name, project_name=f.project.name, spec=FleetSpec.model_validate_json(f.spec),
+                 created_at=f.created_at, status=FleetStatus(f.status), status_message=f.status_message,
+                 instances=instances)
+
+
+def list_project_fleets(s: Session, project: ProjectModel) -> List[FleetModel]:
+    return list(s.execute(select(FleetModel).where(FleetModel.project_id == project.id, FleetModel.deleted == False)  # noqa
+                          .order_by(FleetModel.created_at)).scalars())
+
+
+def get_fleet_by_name(s: Session, project: ProjectModel, name: str) -> Optional[FleetModel]:
+    return s.execute(select(FleetModel).where(FleetModel.project_id == project.id, FleetModel.name == name,
+                                              FleetModel.deleted == False)).scalar_one_or_none()  # noqa
+
+
+def _requirements(conf: FleetConfiguration, profile: Profile) -> Requirements:
+    return Requirements(resources=conf.resources or ResourcesSpec(), max_price=profile.max_price,
+                        spot=get_policy_map(profile.spot_policy, SpotPolicy.ONDEMAND), reservation=profile.reservation)
+
+
+def get_plan(s: Session, project: ProjectModel, user: UserModel, spec: FleetSpec) -> FleetPlan:
+    current = None
+    if spec.configuration.name:
+        f = get_fleet_by_name(s, project, spec.configuration.name)
+        current = fleet_model_to_fleet(f) if f else None
+    offers = []
+    if spec.configuration.ssh_config is None:
+        profile = spec.merged_profile
+        offers = [o for _, o in offers_services.get_offers_by_requirements(
+            s, project, profile, _requirements(spec.configuration, profile),
+            multinode=spec.configuration.placement == InstanceGroupPlacement.CLUSTER,
+            blocks=spec.configuration.blocks,
+        )]
+    return FleetPlan(project_name=project.name, user=user.name, spec=spec, current_resource=current,
+                     offers=offers[:50], total_offers=len(offers), max_offer_price=max((o.price for o in offers),
+                                                                                       default=None))
+
+
+def _idle_seconds(conf: FleetConfiguration) -> int:
+    v = conf.idle_duration
+    if v is None:
+        return DEFAULT_FLEET_TERMINATION_IDLE_TIME
+    return int(v)
+
+
+def create_fleet(s: Session, project: ProjectModel, user: UserModel, spec: FleetSpec) -> Fleet:
+    conf = spec.configuration
+    with get_locker().advisory_lock(f"fleet_names_{project.id}"):
+        if conf.name is None:
+            conf.name = generate_name()
+        if get_fleet_by_name(s, project, conf.name) is not None:
+            raise ResourceExistsError(f"Fleet {conf.name} exists")
+        fleet = FleetModel(id=uuid.uuid4(), name=conf.name, project_id=project.id, status=FleetStatus.ACTIVE.value,
+                           spec=spec.model_dump_json(), created_at=get_current_datetime(),
+                           last_processed_at=get_current_datetime())
+        s.add(fleet)
+        s.flush()
+        pool = pools_services.get_or_create_default_pool(s, project)
+        profile = spec.merged_profile
+        if conf.ssh_config is not None:
+            for i, host in enumerate(conf.ssh_config.hosts):
+                h = host if isinstance(host, SSHHostParams) else SSHHostParams(hostname=host)
+                user_name = h.user or conf.ssh_config.user or "root"
+                port = h.port or conf.ssh_config.port or 22
+                key = h.ssh_key or conf.ssh_config.ssh_key
+                if key is None:
+                    ident = h.identity_file or conf.ssh_config.identity_file
+                    if ident:
+                        import os
+
+                        with open(os.path.expanduser(ident)) as fh:
+                            key = SSHKey(public="", private=fh.read())
+                if key is None:
+                    raise ServerClientError(f"No SSH key for host {h.hostname}")
+                rci = RemoteConnectionInfo(host=h.hostname, port=port, ssh_user=user_name, ssh_keys=[key],
+                                           env=conf.env)
+                pools_services.create_instance_model(
+                    s, project, pool, name=f"{conf.name}-{i}", status=InstanceStatus.PENDING, fleet=fleet,
+                    instance_num=i, backend=BackendType.REMOTE.value, region="remote", price=0.0,
+                    remote_connection_info=rci.model_dump_json(),
+                    termination_idle_time=-1, termination_policy="dont-destroy",
+                    total_blocks=None if h.blocks == "auto" else int(h.blocks),
+                    backend_data=json.dumps({"blocks": h.blocks, "internal_ip": h.internal_ip,
+                                             "network": conf.ssh_config.network}),
+                )
+        else:
+            nodes = conf.nodes.min or 0
+            for i in range(nodes):
+                pools_services.create_instance_model(
+                    s, project, pool, name=f"{conf.name}-{i}", status=InstanceStatus.PENDING, fleet=fleet,
+                    instance_num=i, profile=profile.model_dump_json(),
+                    requirements=_requirements(conf, profile).model_dump_json(),
+                    termination_idle_time=_idle_seconds(conf),
+                    termination_policy="destroy-after-idle" if _idle_seconds(conf) >= 0 else "dont-destroy",
+                    backend_data=json.dumps({"blocks": conf.blocks,
+                                             "placement": conf.placement.value if conf.placement else None}),
+                )
+        s.flush()
+        s.refresh(fleet)
+    scheduler.wake(scheduler.INSTANCES)
+    return fleet_model_to_fleet(fleet)
+
+
+def create_autocreated_fleet(s: Session, project: ProjectModel, run_name: str, profile: Profile,
+                             multinode: bool) -> FleetModel:
+    conf = FleetConfiguration(name=f"{run_name}-fleet-{uuid.uuid4().hex[:4]}", nodes=1,
+                              placement=InstanceGroupPlacement.CLUSTER if multinode else None)
+    spec = FleetSpec(configuration=conf, profile=profile, autocreated=True)
+    fleet = FleetModel(id=uuid.uuid4(), name=conf.name, project_id=project.id, status=FleetStatus.ACTIVE.value,
+                       spec=spec.model_dump_json())
+    s.add(fleet)
+    s.flush()
+    return fleet
+
+
+def delete_fleets(s: Session, project: ProjectModel, names: List[str]):
+    for name in names:
+        f = get_fleet_by_name(s, project, name)
+        if f is None:
+            raise ResourceNotExistsError(f"Fleet {name} not found")
+        busy = [i for i in f.instances if i.status == InstanceStatus.BUSY.value]
+        if busy:
+            raise ServerClientError(f"Fleet {name} has busy instances; stop the runs first")
+        for inst in f.instances:
+            if inst.status not in (InstanceStatus.TERMINATING.value, InstanceStatus.TERMINATED.value):
+                inst.status = InstanceStatus.TERMINATING.value
+                inst.termination_reason = "fleet deleted"
+        f.status = FleetStatus.TERMINATING.value
+    s.flush()
+    scheduler.wake(scheduler.INSTANCES, scheduler.FLEETS)
+
+
+def delete_fleet_instances(s: Session, project: ProjectModel, name: str, instance_nums: List[int]):
+    f = get_fleet_by_name(s, project, name)
+    if f is None:
+        raise ResourceNotExistsError(f"Fleet {name} not found")
+    for inst in f.instances:
+        if inst.instance_num in instance_nums:
+            if inst.status == InstanceStatus.BUSY.value:
+                raise ServerClientError(f"Instance {inst.name} is busy")
+            inst.status = InstanceStatus.TERMINATING.value
+            inst.termination_reason = "deleted by user"
+    s.flush()
+    scheduler.wake(scheduler.INSTANCES)
+
+
+_ = (Duration, Env, InstanceModel)

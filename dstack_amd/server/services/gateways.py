@@ -1,0 +1,212 @@
+"""Gateways (reference: ``S/services/gateways/__init__.py:88-559``, ``client.py:16-190``).
+
+A gateway is a host running ``dstack_amd.proxy.gateway`` (nginx + stats + OpenAI model proxy).
+The server talks to its REST API (``/api/registry/...``, ``/api/stats``) — over an SSH tunnel for
+cloud gateways, or directly for ``local``/on-prem gateways (``backend_data.direct``).
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import uuid
+from typing import List, Optional
+
+import httpx
+from sqlalchemy import select
+from sqlalchemy.orm import Session
+
+from dstack_amd.core.errors import GatewayError, ResourceExistsError, ResourceNotExistsError, ServerClientError
+from dstack_amd.core.models.backends import BACKENDS_WITH_GATEWAY_SUPPORT, BackendType
+from dstack_amd.core.models.gateways import (
+    Gateway,
+    GatewayConfiguration,
+    GatewayPlan,
+    GatewaySpec,
+    GatewayStatus,
+)
+from dstack_amd.core.models.runs import RunSpec
+from dstack_amd.server.background import scheduler
+from dstack_amd.server.models import BackendModel, GatewayComputeModel, GatewayModel, JobModel, ProjectModel, RunModel, UserModel
+from dstack_amd.server.services import jobs as jobs_services
+from dstack_amd.utils.common import generate_name, generate_rsa_key_pair, get_current_datetime
+
+logger = logging.getLogger(__name__)
+
+
+def gateway_model_to_gateway(g: GatewayModel) -> Gateway:
+    conf = GatewayConfiguration.model_validate_json(g.configuration) if g.configuration else \
+        GatewayConfiguration(backend=BackendType(g.backend.type), region=g.region)
+    comp = g.gateway_compute
+    return Gateway(name=g.name, configuration=conf, created_at=g.created_at, status=GatewayStatus(g.status),
+                   status_message=g.status_message, hostname=comp.hostname if comp else None,
+                   ip_address=comp.ip_address if comp else None, instance_id=comp.instance_id if comp else None,
+                   backend=conf.backend, region=g.region, default=g.project.default_gateway_id == g.id,
+                   wildcard_domain=g.wildcard_domain)
+
+
+def list_project_gateways(s: Session, project: ProjectModel) -> List[GatewayModel]:
+    return list(s.execute(select(GatewayModel).where(GatewayModel.project_id == project.id)).scalars())
+
+
+def get_gateway_by_name(s: Session, project: ProjectModel, name: str) -> Optional[GatewayModel]:
+    return s.execute(select(GatewayModel).where(GatewayModel.project_id == project.id,
+                                                GatewayModel.name == name)).scalar_one_or_none()
+
+
+def get_plan(s: Session, project: ProjectModel, user: UserModel, spec: GatewaySpec) -> GatewayPlan:
+    cur = get_gateway_by_name(s, project, spec.configuration.name) if spec.configuration.name else None
+    return GatewayPlan(project_name=project.name, user=user.name, spec=spec,
+                       current_resource=gateway_model_to_gateway(cur) if cur else None)
+
+
+def create_gateway(s: Session, project: ProjectModel, conf: GatewayConfiguration) -> Gateway:
+    if conf.backend not in BACKENDS_WITH_GATEWAY_SUPPORT:
+        raise ServerClientError(f"Backend {conf.backend.value} does not support gateways")
+    if conf.name is None:
+        conf.name = generate_name()
+    if get_gateway_by_name(s, project, conf.name) is not None:
+        raise ResourceExistsError(f"Gateway {conf.name} exists")
+    backend = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
+                                                   BackendModel.type == conf.backend.value)).scalar_one_or_none()
+    if backend is None:
+        if conf.backend != BackendType.LOCAL:
+            raise ServerClientError(f"Backend {conf.backend.value} is not configured")
+        backend = BackendModel(id=uuid.uuid4(), project_id=project.id, type="local", config="{}", auth="{}")
+        s.add(backend)
+        s.flush()
+    g = GatewayModel(id=uuid.uuid4(), name=conf.name, region=conf.region, project_id=project.id,
+                     backend_id=backend.id, configuration=conf.model_dump_json(), status=GatewayStatus.SUBMITTED.value,
+                     wildcard_domain=conf.domain, created_at=get_current_datetime(),
+                     last_processed_at=get_current_datetime())
+    s.add(g)
+    s.flush()
+    if conf.default or project.default_gateway_id is None:
+        project.default_gateway_id = g.id
+    scheduler.wake(scheduler.GATEWAYS)
+    s.refresh(g)
+    return gateway_model_to_gateway(g)
+
+
+def delete_gateways(s: Session, project: ProjectModel, names: List[str]):
+    for n in names:
+        g = get_gateway_by_name(s, project, n)
+        if g is None:
+            raise ResourceNotExistsError(f"Gateway {n} not found")
+        if project.default_gateway_id == g.id:
+            project.default_gateway_id = None
+        if g.gateway_compute:
+            g.gateway_compute.active = False
+            g.gateway_compute.deleted = True
+        s.delete(g)
+
+
+def set_default_gateway(s: Session, project: ProjectModel, name: str):
+    g = get_gateway_by_name(s, project, name)
+    if g is None:
+        raise ResourceNotExistsError()
+    project.default_gateway_id = g.id
+
+
+def set_wildcard_domain(s: Session, project: ProjectModel, name: str, domain: Optional[str]) -> Gateway:
+    g = get_gateway_by_name(s, project, name)
+    if g is None:
+        raise ResourceNotExistsError()
+    g.wildcard_domain = domain
+    return gateway_model_to_gateway(g)
+
+
+# ---------------------------------------------------------------------------------------------
+# gateway API client
+# ---------------------------------------------------------------------------------------------
+def _gateway_url(g: GatewayModel) -> Optional[str]:
+    comp = g.gateway_compute
+    if comp is None:
+        return None
+    data = json.loads(comp.backend_data or "{}")
+    return data.get("api_url") or f"http://{comp.ip_address}:8000"
+
+
+def _call(g: GatewayModel, method: str, path: str, body: Optional[dict] = None) -> dict:
+    url = _gateway_url(g)
+    if url is None:
+        raise GatewayError(f"gateway {g.name} is not provisioned")
+    r = httpx.request(method, url + path, json=body, timeout=30)
+    if r.status_code >= 400:
+        raise GatewayError(f"gateway {g.name}: {r.status_code} {r.text}")
+    return r.json() if r.content else {}
+
+
+def gateway_register_service(s: Session, run: RunModel):
+    g = s.get(GatewayModel, run.gateway_id)
+    spec = RunSpec.model_validate_json(run.run_spec)
+    conf = spec.configuration
+    body = {"run_name": run.run_name, "domain": f"{run.run_name}.{g.wildcard_domain}", "https": conf.https,
+            "auth": conf.auth, "client_max_body_size": 64 * 2**20,
+            "options": {"openai": {"model": conf.model.model_dump()}} if conf.model else {}}
+    _call(g, "POST", f"/api/registry/{run.project.name}/services/register", body)
+
+
+def gateway_register_replica(s: Session, run: RunModel, job: JobModel):
+    g = s.get(GatewayModel, run.gateway_id)
+    jpd = jobs_services.job_jpd(job)
+    spec = RunSpec.model_validate_json(run.run_spec)
+    body = {"job_id": str(job.id), "app_port": spec.configuration.port.container_port,
+            "ssh_host": f"{jpd.username}@{jpd.hostname}", "ssh_port": jpd.ssh_port or 22,
+            "internal_ip": jpd.internal_ip}
+    try:
+        _call(g, "POST", f"/api/registry/{run.project.name}/services/{run.run_name}/replicas/register", body)
+    except GatewayError as e:
+        logger.warning("register replica: %s", e)
+
+
+def gateway_unregister_replica(s: Session, run: RunModel, job: JobModel):
+    g = s.get(GatewayModel, run.gateway_id)
+    if g is None:
+        return
+    try:
+        _call(g, "POST", f"/api/registry/{run.project.name}/services/{run.run_name}/replicas/{job.id}/unregister")
+    except GatewayError as e:
+        logger.info("unregister replica: %s", e)
+
+
+def gateway_stats(g: GatewayModel) -> dict:
+    return _call(g, "GET", "/api/stats/collect")
+
+
+def provision_gateway(s: Session, g: GatewayModel):
+    """SUBMITTED -> RUNNING.  ``local`` gateways run in-process on the server host; cloud gateways
+    need the backend's ``create_gateway`` (cloud API)."""
+    conf = GatewayConfiguration.model_validate_json(g.configuration)
+    if conf.backend == BackendType.LOCAL:
+        private, public = generate_rsa_key_pair("dstack-gateway")
+        comp = GatewayComputeModel(id=uuid.uuid4(), instance_id="local", ip_address="127.0.0.1", hostname="localhost",
+                                   region="local", backend_id=g.backend_id, ssh_private_key=private,
+                                   ssh_public_key=public, configuration=conf.model_dump_json(),
+                                   backend_data=json.dumps({"api_url": None}))
+        s.add(comp)
+        s.flush()
+        g.gateway_compute_id = comp.id
+        g.status = GatewayStatus.RUNNING.value
+        return
+    from dstack_amd.server.services import backends as backends_services
+
+    try:
+        compute = backends_services.get_project_backend(s, g.project, conf.backend)
+        from dstack_amd.core.models.gateways import GatewayComputeConfiguration
+
+        private, public = generate_rsa_key_pair("dstack-gateway")
+        gpd = compute.create_gateway(GatewayComputeConfiguration(
+            project_name=g.project.name, instance_name=g.name, backend=conf.backend, region=conf.region,
+            public_ip=conf.public_ip, ssh_key_pub=public, certificate=conf.certificate))
+    except Exception as e:  # noqa: BLE001
+        g.status = GatewayStatus.FAILED.value
+        g.status_message = str(e)[:1000]
+        return
+    comp = GatewayComputeModel(id=uuid.uuid4(), instance_id=gpd.instance_id, ip_address=gpd.ip_address,
+                               hostname=gpd.hostname, region=gpd.region, backend_id=g.backend_id,
+                               ssh_private_key=private, ssh_public_key=public, backend_data=gpd.backend_data)
+    s.add(comp)
+    s.flush()
+    g.gateway_compute_id = comp.id
+    g.status = GatewayStatus.PROVISIONING.value

@@ -1,0 +1,159 @@
+"""RunSpec -> JobSpec[] (reference: ``S/services/jobs/configurators/{base,task,dev,service}.py``).
+
+* commands: ``/bin/bash -c "<setup && commands>"`` (or the configured entrypoint);
+* default image: a ROCm PyTorch image when AMD GPUs are requested (MI355X-first), else a base
+  Ubuntu/Python image; images are irrelevant for the ``process`` shim driver;
+* max_duration defaults: task/service off, dev-environment 6 h; stop_duration 300 s;
+* tasks expand into ``nodes`` jobs per replica; services into one job per replica;
+* ``${{ dstack.node_rank }}`` is interpolated into volume names/paths per job;
+* the MI355X health probe is requested for jobs that take AMD GPUs on a fresh instance.
+"""
+
+from __future__ import annotations
+
+import shlex
+from typing import Dict, List, Optional
+
+from dstack_amd.core.models.configurations import (
+    DevEnvironmentConfiguration,
+    PortMapping,
+    ServiceConfiguration,
+    TaskConfiguration,
+)
+from dstack_amd.core.models.profiles import DEFAULT_STOP_DURATION, ProfileRetry, RetryEvent, SpotPolicy
+from dstack_amd.core.models.resources import AcceleratorVendor
+from dstack_amd.core.models.runs import AppSpec, JobSpec, Requirements, Retry, RunSpec, get_policy_map
+from dstack_amd.core.models.unix import UnixUser
+from dstack_amd.core.models.volumes import InstanceMountPoint, VolumeMountPoint
+from dstack_amd.utils.interpolator import VariablesInterpolator
+
+DEFAULT_MAX_DURATION_DEV = 6 * 3600
+DEFAULT_AMD_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.7.1"
+DEFAULT_CPU_IMAGE = "python:{python}-slim"
+
+
+def get_default_python_version() -> str:
+    return "3.10"
+
+
+def get_default_image(conf) -> str:
+    gpu = conf.resources.gpu
+    wants_gpu = gpu is not None and gpu.count.max != 0
+    if wants_gpu and gpu.vendor in (None, AcceleratorVendor.AMD):
+        return DEFAULT_AMD_IMAGE
+    py = conf.python.value if conf.python else get_default_python_version()
+    return DEFAULT_CPU_IMAGE.format(python=py)
+
+
+def _retry(run_spec: RunSpec) -> Optional[Retry]:
+    prof = run_spec.merged_profile
+    r = prof.retry
+    if r is None and prof.retry_policy is not None and prof.retry_policy.retry:
+        return Retry(on_events=[RetryEvent.NO_CAPACITY, RetryEvent.INTERRUPTION, RetryEvent.ERROR],
+                     duration=int(prof.retry_policy.duration or 3600))
+    if r is None or r is False:
+        return None
+    if r is True:
+        return Retry(on_events=[RetryEvent.NO_CAPACITY, RetryEvent.INTERRUPTION, RetryEvent.ERROR], duration=3600)
+    assert isinstance(r, ProfileRetry)
+    return Retry(on_events=r.on_events, duration=int(r.duration or 3600))
+
+
+def _duration(v, default: Optional[int]) -> Optional[int]:
+    if v == "off":
+        return None
+    if v is None:
+        return default
+    return int(v)
+
+
+def _shell_commands(conf) -> List[str]:
+    cmds: List[str] = list(conf.setup)
+    if isinstance(conf, DevEnvironmentConfiguration):
+        cmds += list(conf.init)
+        cmds += [
+            "echo ''",
+            "echo 'To connect: ssh $DSTACK_RUN_NAME  (or open VS Code with the Remote-SSH extension)'",
+            "sleep infinity",
+        ]
+    else:
+        cmds += list(conf.commands)
+    return cmds
+
+
+def _build_commands(conf, image_entrypoint: Optional[List[str]] = None) -> List[str]:
+    shell = _shell_commands(conf)
+    if conf.entrypoint is not None:
+        return shlex.split(conf.entrypoint) + shell
+    if shell:
+        return ["/bin/bash", "-c", " && ".join(shell)]
+    return list(image_entrypoint or [])
+
+
+def _app_specs(conf) -> List[AppSpec]:
+    specs = []
+    ports: List[PortMapping] = getattr(conf, "ports", []) or []
+    for i, p in enumerate(ports):
+        specs.append(AppSpec(port=p.container_port, map_to_port=p.local_port, app_name=f"app{i}"))
+    return specs
+
+
+def interpolate_job_volumes(volumes, job_num: int):
+    it = VariablesInterpolator({"dstack": {"job_num": str(job_num), "node_rank": str(job_num)}})
+    out = []
+    for v in volumes:
+        if isinstance(v, VolumeMountPoint):
+            names = v.name if isinstance(v.name, list) else [v.name]
+            names = [it.interpolate(n) for n in names]
+            out.append(VolumeMountPoint(name=names if isinstance(v.name, list) else names[0],
+                                        path=it.interpolate(v.path)))
+        elif isinstance(v, InstanceMountPoint):
+            out.append(InstanceMountPoint(instance_path=it.interpolate(v.instance_path), path=it.interpolate(v.path),
+                                          optional=v.optional))
+    return out
+
+
+def get_job_specs_from_run_spec(run_spec: RunSpec, replica_num: int = 0,
+                                secrets: Optional[Dict[str, str]] = None) -> List[JobSpec]:
+    conf = run_spec.configuration
+    prof = run_spec.merged_profile
+    nodes = conf.nodes if isinstance(conf, TaskConfiguration) else 1
+    spot = get_policy_map(prof.spot_policy, SpotPolicy.ONDEMAND if not isinstance(conf, TaskConfiguration)
+                          else SpotPolicy.ONDEMAND)
+    requirements = Requirements(resources=conf.resources, max_price=prof.max_price, spot=spot,
+                                reservation=prof.reservation)
+    if isinstance(conf, DevEnvironmentConfiguration):
+        max_duration = _duration(prof.max_duration, DEFAULT_MAX_DURATION_DEV)
+    else:
+        max_duration = _duration(prof.max_duration, None)
+    stop_duration = _duration(prof.stop_duration, DEFAULT_STOP_DURATION)
+    env: Dict[str, str] = {}
+    ns = {"secrets": dict(secrets or {}), "env": {}}
+    it = VariablesInterpolator(ns, skip=["run"])
+    for k, v in conf.env.items():
+        if hasattr(v, "key"):  # unresolved sentinel: the client did not provide it
+            continue
+        env[k] = it.interpolate(str(v), return_missing=True)[0]
+    image = conf.image or get_default_image(conf)
+    user = UnixUser.parse(conf.user) if conf.user else None
+    gpu_wanted = conf.resources.gpu is not None and (conf.resources.gpu.count.max or 0) > 0
+    specs = []
+    for job_num in range(nodes):
+        job_name = f"{run_spec.run_name}-{job_num}-{replica_num}"
+        specs.append(JobSpec(
+            replica_num=replica_num, job_num=job_num, job_name=job_name, jobs_per_replica=nodes,
+            app_specs=_app_specs(conf), user=user, commands=_build_commands(conf), env=env,
+            home_dir=conf.home_dir, image_name=image, privileged=conf.privileged,
+            single_branch=conf.single_branch if conf.single_branch is not None
+            else not isinstance(conf, DevEnvironmentConfiguration),
+            max_duration=max_duration, stop_duration=stop_duration, registry_auth=conf.registry_auth,
+            requirements=requirements, retry=_retry(run_spec),
+            volumes=[v.model_dump(mode="json") for v in interpolate_job_volumes(conf.volumes, job_num)],
+            working_dir=conf.working_dir or run_spec.working_dir,
+            gpu_probe=gpu_wanted and env.get("DSTACK_GPU_PROBE", "0") == "1",
+        ))
+    return specs
+
+
+def service_port(conf: ServiceConfiguration) -> int:
+    return conf.port.container_port

@@ -1,0 +1,348 @@
+"""Runs service (reference: ``S/services/runs.py:273-1020``): plan, apply, submit, stop, delete,
+model conversion, terminating-run handling, replica scaling and retry."""
+
+from __future__ import annotations
+
+import json
+import logging
+import re
+import uuid
+from datetime import datetime
+from typing import List, Optional
+
+from sqlalchemy import select
+from sqlalchemy.orm import Session
+
+from dstack_amd.core.errors import ResourceNotExistsError, ServerClientError
+from dstack_amd.core.models.common import ApplyAction
+from dstack_amd.core.models.configurations import ServiceConfiguration, TaskConfiguration
+from dstack_amd.core.models.profiles import CreationPolicy
+from dstack_amd.core.models.runs import (
+    Job,
+    JobPlan,
+    JobStatus,
+    JobTerminationReason,
+    Run,
+    RunPlan,
+    RunSpec,
+    RunStatus,
+    RunTerminationReason,
+    ServiceSpec,
+)
+from dstack_amd.server import settings
+from dstack_amd.server.background import scheduler
+from dstack_amd.server.models import JobModel, ProjectModel, RunModel, UserModel
+from dstack_amd.server.services import jobs as jobs_services
+from dstack_amd.server.services import offers as offers_services
+from dstack_amd.server.services import pools as pools_services
+from dstack_amd.server.services import repos as repos_services
+from dstack_amd.server.services.locking import get_locker
+from dstack_amd.utils.common import generate_name, get_current_datetime
+
+logger = logging.getLogger(__name__)
+
+_RUN_NAME_RE = re.compile(r"^[a-z][a-z0-9-]{1,40}$")
+
+
+def run_model_to_run(run: RunModel, include_jobs: bool = True, return_in_api: bool = False) -> Run:
+    jobs: List[Job] = []
+    if include_jobs:
+        by_job: dict = {}
+        for j in sorted(run.jobs, key=lambda j: (j.replica_num, j.job_num, j.submission_num)):
+            key = (j.replica_num, j.job_num)
+            if key not in by_job:
+                by_job[key] = Job(job_spec=jobs_services.job_spec(j), job_submissions=[])
+            by_job[key].job_spec = jobs_services.job_spec(j)
+            by_job[key].job_submissions.append(jobs_services.job_model_to_job_submission(j))
+        jobs = list(by_job.values())
+    latest = None
+    if run.jobs:
+        latest_job = max(run.jobs, key=lambda j: (j.submitted_at, j.submission_num))
+        latest = jobs_services.job_model_to_job_submission(latest_job)
+    spec = RunSpec.model_validate_json(run.run_spec)
+    cost = 0.0
+    for j in run.jobs:
+        jpd = jobs_services.job_jpd(j)
+        if jpd is None:
+            continue
+        end = j.finished_at or get_current_datetime()
+        cost += jpd.price * max(0.0, (end - j.submitted_at).total_seconds()) / 3600
+    return Run(
+        id=run.id, project_name=run.project.name, user=run.user.name, submitted_at=run.submitted_at,
+        last_processed_at=run.last_processed_at, status=RunStatus(run.status),
+        termination_reason=RunTerminationReason(run.termination_reason) if run.termination_reason else None,
+        run_spec=spec, jobs=jobs, latest_job_submission=latest, cost=round(cost, 4),
+        service=ServiceSpec.model_validate_json(run.service_spec) if run.service_spec else None,
+        deleted=run.deleted,
+    )
+
+
+def list_user_runs(s: Session, user: UserModel, project_name: Optional[str] = None, repo_id: Optional[str] = None,
+                   only_active: bool = False, limit: int = 100, prev_submitted_at: Optional[datetime] = None,
+                   ascending: bool = False) -> List[Run]:
+    from dstack_amd.server.services.projects import list_user_projects
+
+    projects = list_user_projects(s, user)
+    if project_name:
+        projects = [p for p in projects if p.name == project_name]
+    if not projects:
+        return []
+    q = select(RunModel).where(RunModel.project_id.in_([p.id for p in projects]), RunModel.deleted == False)  # noqa
+    if only_active:
+        q = q.where(RunModel.status.notin_([st.value for st in RunStatus.finished_statuses()]))
+    if prev_submitted_at is not None:
+        q = q.where(RunModel.submitted_at > prev_submitted_at if ascending else RunModel.submitted_at < prev_submitted_at)
+    q = q.order_by(RunModel.submitted_at.asc() if ascending else RunModel.submitted_at.desc()).limit(limit)
+    rows = list(s.execute(q).scalars())
+    if repo_id:
+        rows = [r for r in rows if r.repo and r.repo.name == repo_id]
+    return [run_model_to_run(r) for r in rows]
+
+
+def get_run_model(s: Session, project: ProjectModel, run_name: Optional[str] = None,
+                  run_id: Optional[uuid.UUID] = None) -> Optional[RunModel]:
+    q = select(RunModel).where(RunModel.project_id == project.id)
+    if run_id is not None:
+        q = q.where(RunModel.id == run_id)
+    else:
+        q = q.where(RunModel.run_name == run_name, RunModel.deleted == False)  # noqa: E712
+    return s.execute(q.order_by(RunModel.submitted_at.desc())).scalars().first()
+
+
+def get_run(s: Session, project: ProjectModel, run_name: Optional[str] = None,
+            run_id: Optional[uuid.UUID] = None) -> Optional[Run]:
+    r = get_run_model(s, project, run_name, run_id)
+    return run_model_to_run(r) if r else None
+
+
+def _validate_run_spec(run_spec: RunSpec):
+    if run_spec.run_name is not None and not _RUN_NAME_RE.match(run_spec.run_name):
+        raise ServerClientError("Run name must be 2-41 chars of a-z, 0-9 and -, starting with a letter")
+
+
+def get_plan(s: Session, project: ProjectModel, user: UserModel, run_spec: RunSpec, max_offers: int = 50) -> RunPlan:
+    _validate_run_spec(run_spec)
+    effective = run_spec.model_copy(deep=True)
+    if effective.run_name is None:
+        effective.run_name = "dry-run"
+    current = None
+    action = ApplyAction.CREATE
+    if run_spec.run_name:
+        cur = get_run_model(s, project, run_spec.run_name)
+        if cur is not None and not RunStatus(cur.status).is_finished():
+            current = run_model_to_run(cur)
+            action = ApplyAction.UPDATE
+    profile = effective.merged_profile
+    job_plans = []
+    pool = pools_services.get_or_create_default_pool(s, project)
+    instances = pools_services.list_project_instances(s, project)
+    for spec in jobs_services.get_jobs_from_run_spec(effective, replica_num=0):
+        multinode = spec.jobs_per_replica > 1
+        pool_offers = [o for _, o in pools_services.filter_pool_instances(instances, profile, spec.requirements,
+                                                                          multinode=multinode)]
+        offers = pool_offers[:]
+        if profile.creation_policy != CreationPolicy.REUSE:
+            backend_offers = offers_services.get_offers_by_requirements(
+                s, project, profile, spec.requirements, multinode=multinode, privileged=spec.privileged,
+            )
+            offers += [o for _, o in backend_offers]
+        job_plans.append(JobPlan(job_spec=spec, offers=offers[:max_offers], total_offers=len(offers),
+                                 max_price=max((o.price for o in offers), default=None)))
+    run_spec.run_name = run_spec.run_name  # plan keeps the user's (possibly None) name
+    _ = pool
+    return RunPlan(project_name=project.name, user=user.name, run_spec=run_spec, job_plans=job_plans,
+                   current_resource=current, action=action)
+
+
+def submit_run(s: Session, project: ProjectModel, user: UserModel, run_spec: RunSpec) -> Run:
+    _validate_run_spec(run_spec)
+    with get_locker().advisory_lock(f"run_names_{project.id}"):
+        if run_spec.run_name is None:
+            for _ in range(20):
+                name = generate_name()
+                if get_run_model(s, project, name) is None:
+                    run_spec.run_name = name
+                    break
+        else:
+            existing = get_run_model(s, project, run_spec.run_name)
+            if existing is not None:
+                if not RunStatus(existing.status).is_finished():
+                    raise ServerClientError(f"Run {run_spec.run_name} is already active")
+                existing.deleted = True
+        repo = (repos_services.get_repo(s, project, run_spec.repo_id) if run_spec.repo_id else None) or \
+            repos_services.get_or_create_virtual_repo(s, project, run_spec.repo_id or "none")
+        now = get_current_datetime()
+        conf = run_spec.configuration
+        replicas = conf.replicas.min if isinstance(conf, ServiceConfiguration) else 1
+        run = RunModel(id=uuid.uuid4(), project_id=project.id, user_id=user.id, repo_id=repo.id,
+                       run_name=run_spec.run_name, submitted_at=now, last_processed_at=now,
+                       status=RunStatus.SUBMITTED.value, run_spec=run_spec.model_dump_json(),
+                       desired_replica_count=replicas)
+        s.add(run)
+        s.flush()
+        secrets = jobs_services.get_job_secrets(s, project)
+        for replica_num in range(replicas):
+            for spec in jobs_services.get_jobs_from_run_spec(run_spec, replica_num, secrets):
+                s.add(jobs_services.new_job_model(run, spec))
+        if isinstance(conf, ServiceConfiguration):
+            from dstack_amd.server.services.services import register_service
+
+            register_service(s, run)
+        s.flush()
+        s.refresh(run)
+    scheduler.wake(scheduler.SUBMITTED_JOBS, scheduler.RUNS)
+    return run_model_to_run(run)
+
+
+def apply_plan(s: Session, project: ProjectModel, user: UserModel, run_spec: RunSpec,
+               current_resource: Optional[Run] = None, force: bool = False) -> Run:
+    """Create, or update in place when only replica/scaling params changed (``apply_plan``)."""
+    if run_spec.run_name:
+        cur = get_run_model(s, project, run_spec.run_name)
+        if cur is not None and not RunStatus(cur.status).is_finished():
+            cur_spec = RunSpec.model_validate_json(cur.run_spec)
+            if not force and current_resource is not None and current_resource.id != cur.id:
+                raise ServerClientError("The run changed since the plan was made; re-plan or use --force")
+            if _updatable(cur_spec, run_spec):
+                cur.run_spec = run_spec.model_dump_json()
+                conf = run_spec.configuration
+                if isinstance(conf, ServiceConfiguration):
+                    cur.desired_replica_count = max(conf.replicas.min, min(conf.replicas.max, cur.desired_replica_count))
+                s.flush()
+                scheduler.wake(scheduler.RUNS)
+                return run_model_to_run(cur)
+            stop_runs(s, project, [cur.run_name], abort=False)
+            s.flush()
+            raise ServerClientError(f"Run {cur.run_name} cannot be updated in place; it is being stopped — apply "
+                                    "again once it has terminated")
+    return submit_run(s, project, user, run_spec)
+
+
+_UPDATABLE = {"replicas", "scaling"}
+
+
+def _updatable(old: RunSpec, new: RunSpec) -> bool:
+    a = old.configuration.model_dump(mode="json")
+    b = new.configuration.model_dump(mode="json")
+    diff = {k for k in set(a) | set(b) if a.get(k) != b.get(k)}
+    return diff <= _UPDATABLE
+
+
+def stop_runs(s: Session, project: ProjectModel, runs_names: List[str], abort: bool):
+    reason = RunTerminationReason.ABORTED_BY_USER if abort else RunTerminationReason.STOPPED_BY_USER
+    for name in runs_names:
+        run = get_run_model(s, project, name)
+        if run is None:
+            continue
+        if RunStatus(run.status).is_finished():
+            continue
+        run.status = RunStatus.TERMINATING.value
+        run.termination_reason = reason.value
+        run.last_processed_at = get_current_datetime()
+    s.flush()
+    scheduler.wake(scheduler.RUNS)
+
+
+def delete_runs(s: Session, project: ProjectModel, runs_names: List[str]):
+    for name in runs_names:
+        run = get_run_model(s, project, name)
+        if run is None:
+            continue
+        if not RunStatus(run.status).is_finished():
+            raise ServerClientError(f"Run {name} is not finished; stop it first")
+        run.deleted = True
+
+
+def process_terminating_run(s: Session, run: RunModel):
+    """Stop every unfinished job of a TERMINATING run; finish the run once all jobs are done
+    (``S/services/runs.py:876-922``)."""
+    reason = RunTerminationReason(run.termination_reason)
+    job_reason = reason.to_job_termination_reason()
+    unfinished = False
+    for job in run.jobs:
+        st = JobStatus(job.status)
+        if st.is_finished():
+            continue
+        unfinished = True
+        if st == JobStatus.TERMINATING:
+            continue
+        if st == JobStatus.RUNNING and job_reason != JobTerminationReason.ABORTED_BY_USER:
+            jobs_services.stop_runner(s, job)
+            jobs_services.terminate_job(job, job_reason, delay=True)
+        else:
+            jobs_services.terminate_job(job, job_reason, delay=False)
+    if not unfinished:
+        run.status = reason.to_status().value
+        if isinstance(RunSpec.model_validate_json(run.run_spec).configuration, ServiceConfiguration):
+            from dstack_amd.server.services.services import unregister_service
+
+            unregister_service(s, run)
+    scheduler.wake(scheduler.TERMINATING_JOBS)
+
+
+def scale_run_replicas(s: Session, run: RunModel, replicas_diff: int):
+    """Add replicas (new job models) or terminate the newest ones (``scale_run_replicas``)."""
+    if replicas_diff == 0:
+        return
+    spec = RunSpec.model_validate_json(run.run_spec)
+    groups = jobs_services.group_jobs_by_replica_latest(run.jobs)
+    active = {r: js for r, js in groups.items() if not all(JobStatus(j.status).is_finished() for j in js)}
+    if replicas_diff < 0:
+        for r in sorted(active, reverse=True)[: -replicas_diff]:
+            for j in active[r]:
+                if j.status == JobStatus.RUNNING.value:
+                    jobs_services.stop_runner(s, j)
+                jobs_services.terminate_job(j, JobTerminationReason.SCALED_DOWN)
+        scheduler.wake(scheduler.TERMINATING_JOBS)
+        return
+    secrets = jobs_services.get_job_secrets(s, run.project)
+    next_replica = max(groups.keys(), default=-1) + 1
+    # reuse finished replica slots first
+    finished = sorted(r for r in groups if r not in active)
+    for _ in range(replicas_diff):
+        if finished:
+            r = finished.pop(0)
+            sub = max(j.submission_num for j in groups[r]) + 1
+        else:
+            r, sub = next_replica, 0
+            next_replica += 1
+        for js in jobs_services.get_jobs_from_run_spec(spec, r, secrets):
+            s.add(jobs_services.new_job_model(run, js, submission_num=sub))
+    s.flush()
+    scheduler.wake(scheduler.SUBMITTED_JOBS)
+
+
+def retry_run_replica_jobs(s: Session, run: RunModel, latest_jobs: List[JobModel], only_failed: bool):
+    """New submissions for a replica's jobs (``retry_run_replica_jobs``)."""
+    spec = RunSpec.model_validate_json(run.run_spec)
+    secrets = jobs_services.get_job_secrets(s, run.project)
+    for old in latest_jobs:
+        if only_failed and JobStatus(old.status) not in (JobStatus.FAILED, JobStatus.TERMINATED, JobStatus.ABORTED):
+            continue
+        for js in jobs_services.get_jobs_from_run_spec(spec, old.replica_num, secrets):
+            if js.job_num == old.job_num:
+                s.add(jobs_services.new_job_model(run, js, submission_num=old.submission_num + 1))
+    s.flush()
+    scheduler.wake(scheduler.SUBMITTED_JOBS)
+
+
+def is_multinode(run_spec: RunSpec) -> bool:
+    c = run_spec.configuration
+    return isinstance(c, TaskConfiguration) and c.nodes > 1
+
+
+def get_run_by_name_or_error(s: Session, project: ProjectModel, name: str) -> RunModel:
+    r = get_run_model(s, project, name)
+    if r is None:
+        raise ResourceNotExistsError(f"Run {name} not found")
+    return r
+
+
+def settings_snapshot() -> dict:
+    return {"event_driven": settings.SERVER_EVENT_DRIVEN}
+
+
+__all__ = [
+    "get_plan", "apply_plan", "submit_run", "stop_runs", "delete_runs", "list_user_runs", "get_run",
+    "run_model_to_run", "process_terminating_run", "scale_run_replicas", "retry_run_replica_jobs", "json",
+]
