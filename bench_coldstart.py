@@ -38,12 +38,19 @@ def measure_cold_start(runs: int = 5, timeout: float = 120.0, command: str = "ec
             sub_ts = t.get("submitted", t0)
             sample = {
                 "status": sub.status.value,
+                "termination_reason": sub.termination_reason.value if sub.termination_reason else None,
+                "message": sub.termination_reason_message,
                 "submit_to_provisioned": _d(t, "provisioned", sub_ts) or _d(t, "assigned", sub_ts),
                 "submit_to_running": _d(t, "running", sub_ts),
                 "submit_to_first_log": _d(t, "first_log", sub_ts),
                 "client_wall_to_done": time.time() - t0,
             }
             samples.append(sample)
+            if sample["submit_to_first_log"] is None:
+                print(f"coldstart run {i} failed: {sample}", file=sys.stderr)
+                print(srv.log()[-4000:], file=sys.stderr)
+                for chunk in run.logs(diagnose=True):
+                    sys.stderr.write(chunk.decode(errors="replace"))
     ok = [s for s in samples if s["submit_to_first_log"] is not None]
     p50 = statistics.median([s["submit_to_first_log"] for s in ok]) if ok else None
     return {

@@ -196,6 +196,8 @@ class ServiceConfiguration(ProfileParams, _WithCommands, BaseRunConfiguration):
             v = IntRange(min=int(lo or 0), max=int(hi) if hi else None)
         elif isinstance(v, (int, float)) and not isinstance(v, bool):
             v = IntRange(min=int(v), max=int(v))
+        elif isinstance(v, str):
+            v = IntRange(min=int(v.strip()), max=int(v.strip()))
         elif isinstance(v, dict):
             v = IntRange(min=v.get("min", 0), max=v.get("max"))
         if v.max is None:

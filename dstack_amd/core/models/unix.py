@@ -17,9 +17,14 @@ class UnixUser(CoreModel):
     def parse(cls, v: str) -> "UnixUser":
         if not v:
             raise ValueError("empty user")
-        user, _, group = v.partition(":")
-        if not user:
+        parts = v.split(":")
+        if len(parts) > 2:
+            raise ValueError(f"invalid user: {v} (expected user[:group])")
+        user, group = parts[0], (parts[1] if len(parts) == 2 else None)
+        if not user or (group is not None and not group):
             raise ValueError(f"invalid user: {v}")
+        if user.startswith("-") or (group or "").startswith("-"):
+            raise ValueError(f"negative uid/gid: {v}")
         kw: dict = {}
         if user.isdigit():
             kw["uid"] = int(user)
@@ -30,8 +35,6 @@ class UnixUser(CoreModel):
                 kw["gid"] = int(group)
             else:
                 kw["groupname"] = group
-        elif _ := None:
-            pass
         return cls(**kw)
 
     def __str__(self) -> str:

@@ -65,9 +65,9 @@ CONFIGS = {
     "llama-3.2-1b": LlamaConfig(
         name="llama-3.2-1b", dim=2048, n_layers=16, n_heads=32, n_kv_heads=8, ffn_dim=8192
     ),
-    # tiny config used by CPU unit tests and the GPU smoke test
+    # tiny config used by CPU unit tests and the GPU smoke test (head_dim 128: the flash kernel's tile)
     "llama-tiny": LlamaConfig(
-        name="llama-tiny", dim=256, n_layers=2, n_heads=4, n_kv_heads=2, ffn_dim=512, vocab_size=1024,
+        name="llama-tiny", dim=512, n_layers=2, n_heads=4, n_kv_heads=2, ffn_dim=1024, vocab_size=1024,
         max_seq_len=256,
     ),
 }

@@ -153,6 +153,10 @@ def attention(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, causal: bool = T
     """Causal GQA attention on the fused projection output; returns [B, S, H*D]."""
     b, s, _ = qkv.shape
     if _ext.use_hip(qkv) and _attn_impl() == "hip":
+        d = qkv.shape[-1] // (n_heads + 2 * n_kv_heads)
+        if d != 128 or s % 128 != 0:
+            raise ValueError(f"HIP flash attention needs head_dim 128 and seq_len % 128 == 0 (got head_dim {d}, "
+                             f"seq_len {s}); set DSTACK_AMD_ATTN=sdpa for other shapes")
         return _FlashAttnQKV.apply(qkv.contiguous(), n_heads, n_kv_heads, causal)
     q, k, v = split_qkv(qkv, n_heads, n_kv_heads)
     if q.is_cuda:

@@ -78,6 +78,22 @@ bool LogHistory::wait_after(int64_t ts, int timeout_ms) const {
 }
 
 // ------------------------------------------------------------------------------------------------
+// PATH lookup done in the parent (execvpe may allocate in the child)
+std::string resolve_in_path(const std::string& prog, const std::string& path_var) {
+  if (prog.find('/') != std::string::npos) return prog;
+  size_t start = 0;
+  while (start <= path_var.size()) {
+    size_t end = path_var.find(':', start);
+    if (end == std::string::npos) end = path_var.size();
+    std::string dir = path_var.substr(start, end - start);
+    if (dir.empty()) dir = ".";
+    std::string cand = dir + "/" + prog;
+    if (access(cand.c_str(), X_OK) == 0) return cand;
+    start = end + 1;
+  }
+  return prog;
+}
+
 // env interpolation: ${VAR} -> value, $$ -> $
 // ------------------------------------------------------------------------------------------------
 std::string interpolate_env(const std::string& s, const std::vector<std::pair<std::string, std::string>>& env,
@@ -469,15 +485,60 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
       }
     }
   }
+  // materialise argv/envp (and the resolved executable) before fork(): the runner is
+  // multi-threaded (HTTP server), so the child may only make async-signal-safe calls until exec
+  std::vector<char*> a, e;
+  for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
+  a.push_back(nullptr);
+  for (auto& s : envs) e.push_back(const_cast<char*>(s.c_str()));
+  e.push_back(nullptr);
+  std::string path_var = getenv("PATH") ? getenv("PATH") : "/usr/local/bin:/usr/bin:/bin";
+  for (auto& kv : env)
+    if (kv.first == "PATH") path_var = kv.second;
+  std::string exe = resolve_in_path(argv[0], path_var);
   int master = -1;
   struct winsize ws{};
   ws.ws_row = 50;
   ws.ws_col = 200;
-  pid_t pid = forkpty(&master, nullptr, nullptr, &ws);
+  // a pty gives the job line-buffered output and a controlling terminal; sandboxes without
+  // /dev/ptmx (e.g. unprivileged CI boxes) fall back to a pipe for stdout+stderr
+  bool use_pty = true;
+  int pipefd[2] = {-1, -1};
+  const char* no_pty = getenv("DSTACK_RUNNER_NO_PTY");
+  pid_t pid = -1;
+  if (no_pty && *no_pty && *no_pty != '0')
+    errno = ENOTSUP;
+  else
+    pid = forkpty(&master, nullptr, nullptr, &ws);
   if (pid < 0) {
-    reason = "executor_error";
-    msg = std::string("forkpty failed: ") + strerror(errno);
-    return -1;
+    int pty_errno = errno;
+    use_pty = false;
+    if (pipe(pipefd) != 0) {
+      reason = "executor_error";
+      msg = std::string("forkpty failed: ") + strerror(pty_errno) + "; pipe failed: " + strerror(errno);
+      return -1;
+    }
+    rlog("forkpty unavailable (%s): using a pipe", strerror(pty_errno));
+    pid = fork();
+    if (pid < 0) {
+      reason = "executor_error";
+      msg = std::string("fork failed: ") + strerror(errno);
+      close(pipefd[0]);
+      close(pipefd[1]);
+      return -1;
+    }
+    if (pid == 0) {
+      setsid();
+      int devnull = open("/dev/null", O_RDONLY);
+      if (devnull >= 0) dup2(devnull, 0);
+      dup2(pipefd[1], 1);
+      dup2(pipefd[1], 2);
+      close(pipefd[0]);
+      close(pipefd[1]);
+    } else {
+      close(pipefd[1]);
+      master = pipefd[0];
+    }
   }
   if (pid == 0) {
     if (chdir(wd.c_str()) != 0) _exit(126);
@@ -486,16 +547,13 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
       setgroups(0, nullptr);
       if (setuid((uid_t)uid) != 0) _exit(126);
     }
-    std::vector<char*> a, e;
-    for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
-    a.push_back(nullptr);
-    for (auto& s : envs) e.push_back(const_cast<char*>(s.c_str()));
-    e.push_back(nullptr);
-    execvpe(a[0], a.data(), e.data());
-    fprintf(stderr, "exec %s failed: %s\n", a[0], strerror(errno));
+    execve(exe.c_str(), a.data(), e.data());
+    static const char kMsg[] = "dstack-runner: exec failed\n";
+    if (write(2, kMsg, sizeof kMsg - 1) < 0) _exit(127);
     _exit(127);
   }
-  child_pgid_ = pid;  // forkpty() makes the child a session (and process group) leader
+  child_pgid_ = pid;  // forkpty()/setsid() make the child a session (and process group) leader
+  (void)use_pty;
   add_state("running");
   rlog("job started: pid=%d cwd=%s", pid, wd.c_str());
   int64_t max_duration = js["max_duration"].as_int(0);

@@ -57,6 +57,7 @@ struct RunnerOptions {
 
 class Executor {
  public:
+  std::atomic<int>* child_pgid_ptr() { return &child_pgid_; }
   explicit Executor(RunnerOptions opts);
   ~Executor();
 

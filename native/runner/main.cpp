@@ -68,6 +68,17 @@ int main(int argc, char** argv) {
   }
   signal(SIGPIPE, SIG_IGN);
   Executor ex(opts);
+  // the job runs in its own session: forward termination to its process group
+  static std::atomic<int>* g_job_pgid = nullptr;
+  g_job_pgid = ex.child_pgid_ptr();
+  struct sigaction sa{};
+  sa.sa_handler = [](int sig) {
+    int pg = g_job_pgid ? g_job_pgid->load() : 0;
+    if (pg > 0) kill(-pg, SIGKILL);
+    _exit(128 + sig);
+  };
+  sigaction(SIGTERM, &sa, nullptr);
+  sigaction(SIGINT, &sa, nullptr);
   HttpServer srv("0.0.0.0", http_port);
   std::atomic<bool> stop_server{false};
 

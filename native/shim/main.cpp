@@ -210,6 +210,13 @@ int main(int argc, char** argv) {
   if (const char* v = getenv("DSTACK_RUNNER_BINARY_PATH"); v && o.runner_binary.empty()) o.runner_binary = v;
   if (const char* v = getenv("DSTACK_RUNNER_DOWNLOAD_URL"); v && o.runner_download_url.empty()) o.runner_download_url = v;
   signal(SIGPIPE, SIG_IGN);
+  struct sigaction sa{};
+  sa.sa_handler = [](int sig) {
+    kill_registered_children(SIGTERM);
+    _exit(sig == SIGTERM ? 0 : 128 + sig);
+  };
+  sigaction(SIGTERM, &sa, nullptr);
+  sigaction(SIGINT, &sa, nullptr);
   mkdirs(o.home);
   if (o.runner_binary.empty()) o.runner_binary = o.home + "/dstack-runner";
   if (!path_exists(o.runner_binary) && !o.runner_download_url.empty()) {  // runner.go:18-109

@@ -6,6 +6,8 @@
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <signal.h>
+
+#include <atomic>
 #include <sys/socket.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -35,6 +37,31 @@ static int free_tcp_port() {
   int p = ntohs(a.sin_port);
   ::close(fd);
   return p;
+}
+
+// Process-group ids of runner children, readable from a signal handler: when the shim is stopped,
+// process-driver tasks (plain child processes, unlike containers) must not outlive it.
+static std::atomic<int> g_child_pgids[512];
+
+void register_child_pgid(int pgid) {
+  for (auto& slot : g_child_pgids) {
+    int expected = 0;
+    if (slot.compare_exchange_strong(expected, pgid)) return;
+  }
+}
+
+void unregister_child_pgid(int pgid) {
+  for (auto& slot : g_child_pgids) {
+    int expected = pgid;
+    if (slot.compare_exchange_strong(expected, 0)) return;
+  }
+}
+
+void kill_registered_children(int sig) {  // async-signal-safe
+  for (auto& slot : g_child_pgids) {
+    int pg = slot.load();
+    if (pg > 0) kill(-pg, sig);
+  }
 }
 
 class ProcessDriver : public TaskDriver {
@@ -92,6 +119,13 @@ class ProcessDriver : public TaskDriver {
       argv.push_back(o_.probe_binary);
     }
     std::string log_path = dir + "/runner.log";
+    // everything the child needs is materialised before fork(): the shim is multi-threaded, so
+    // the child may only make async-signal-safe calls (no malloc) until execve
+    std::vector<char*> a, e;
+    for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
+    a.push_back(nullptr);
+    for (auto& s : envs) e.push_back(const_cast<char*>(s.c_str()));
+    e.push_back(nullptr);
     pid_t pid = fork();
     if (pid < 0) {
       reason = "creating_container_error";
@@ -106,14 +140,10 @@ class ProcessDriver : public TaskDriver {
         dup2(fd, 2);
         close(fd);
       }
-      std::vector<char*> a, e;
-      for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
-      a.push_back(nullptr);
-      for (auto& s : envs) e.push_back(const_cast<char*>(s.c_str()));
-      e.push_back(nullptr);
       execve(a[0], a.data(), e.data());
       _exit(127);
     }
+    register_child_pgid(pid);
     t.pid = pid;
     t.runner_port = port;
     t.container_name = "process-" + std::to_string(pid);
@@ -127,6 +157,7 @@ class ProcessDriver : public TaskDriver {
       if (http_request(r).ok()) break;
       int st;
       if (waitpid(pid, &st, WNOHANG) == pid) {
+        unregister_child_pgid(pid);
         reason = "creating_container_error";
         msg = "runner exited during startup (see " + log_path + ")";
         t.pid = 0;
@@ -141,6 +172,7 @@ class ProcessDriver : public TaskDriver {
     if (t.pid <= 0) return;
     int st = 0;
     waitpid(t.pid, &st, 0);
+    unregister_child_pgid(t.pid);
   }
 
   void terminate(Task& t, int timeout_s) override {

@@ -133,6 +133,10 @@ class TaskDriver {
 
 std::unique_ptr<TaskDriver> make_docker_driver(const ShimOptions& o);
 std::unique_ptr<TaskDriver> make_process_driver(const ShimOptions& o);
+// process-driver children (killed on shim shutdown; see process.cpp)
+void register_child_pgid(int pgid);
+void unregister_child_pgid(int pgid);
+void kill_registered_children(int sig);
 bool docker_available(const std::string& socket_path);
 
 // shell bootstrap that starts sshd + the runner inside a container (docker.go:873-911)

@@ -1,0 +1,224 @@
+"""REST API tests against an in-memory server (reference test strategy: ``src/tests/_internal/
+server/routers/test_*.py`` — TestClient + real DB, background tasks driven explicitly)."""
+
+import pytest
+
+from tests.conftest import ADMIN_TOKEN
+
+
+def _task(name="t1", **kw):
+    conf = {"type": "task", "commands": ["echo hi"]}
+    conf.update(kw)
+    return {"run_spec": {"run_name": name, "repo_id": "virt", "repo_data": {"repo_type": "virtual"},
+                         "configuration": conf, "ssh_key_pub": ""}}
+
+
+def _init_virtual_repo(client):
+    r = client.post("/api/project/main/repos/init", json={"repo_id": "virt", "repo_info": {"repo_type": "virtual"}})
+    assert r.status_code == 200, r.text
+
+
+# ---- server / auth ----------------------------------------------------------------------------
+def test_server_info(client):
+    r = client.post("/api/server/get_info")
+    assert r.status_code == 200
+    assert r.json()["server_version"]
+
+
+def test_healthcheck(client):
+    assert client.get("/healthcheck").json() == {"status": "running"}
+
+
+def test_requires_token(client):
+    r = client.post("/api/users/get_my_user", headers={"Authorization": "Bearer nope"})
+    assert r.status_code in (401, 403)
+    r = client.post("/api/projects/list", headers={"Authorization": ""})
+    assert r.status_code in (401, 403)
+
+
+def test_incompatible_client_version(client):
+    r = client.post("/api/server/get_info", headers={"X-API-VERSION": "99.0.0"})
+    assert r.status_code == 400
+
+
+# ---- users ------------------------------------------------------------------------------------
+def test_users_crud(client):
+    me = client.post("/api/users/get_my_user").json()
+    assert me["username"] == "admin" and me["creds"]["token"] == ADMIN_TOKEN
+    r = client.post("/api/users/create", json={"username": "alice", "global_role": "user"})
+    assert r.status_code == 200, r.text
+    alice_token = r.json()["creds"]["token"]
+    names = {u["username"] for u in client.post("/api/users/list").json()}
+    assert {"admin", "alice"} <= names
+    # a non-admin only sees itself and cannot create users
+    r = client.post("/api/users/list", headers={"Authorization": f"Bearer {alice_token}"})
+    assert [u["username"] for u in r.json()] == ["alice"]
+    r = client.post("/api/users/create", json={"username": "bob"}, headers={"Authorization": f"Bearer {alice_token}"})
+    assert r.status_code == 403
+    r = client.post("/api/users/refresh_token", json={"username": "alice"})
+    assert r.json()["creds"]["token"] != alice_token
+    client.post("/api/users/delete", json={"users": ["alice"]})
+    assert "alice" not in {u["username"] for u in client.post("/api/users/list").json()}
+
+
+def test_duplicate_user_rejected(client):
+    assert client.post("/api/users/create", json={"username": "carol"}).status_code == 200
+    r = client.post("/api/users/create", json={"username": "carol"})
+    assert r.status_code == 400
+    assert r.json()["detail"][0]["code"] == "resource_exists"
+
+
+# ---- projects ---------------------------------------------------------------------------------
+def test_projects_and_members(client):
+    assert [p["project_name"] for p in client.post("/api/projects/list").json()] == ["main"]
+    r = client.post("/api/projects/create", json={"project_name": "research"})
+    assert r.status_code == 200, r.text
+    u = client.post("/api/users/create", json={"username": "dan"}).json()
+    dan = {"Authorization": f"Bearer {u['creds']['token']}"}
+    assert client.post("/api/projects/research/get", headers=dan).status_code == 403
+    r = client.post("/api/projects/research/set_members",
+                    json={"members": [{"username": "admin", "project_role": "admin"},
+                                      {"username": "dan", "project_role": "user"}]})
+    assert r.status_code == 200, r.text
+    assert client.post("/api/projects/research/get", headers=dan).status_code == 200
+    assert [p["project_name"] for p in client.post("/api/projects/list", headers=dan).json()] == ["research"]
+    # a plain member cannot manage members
+    r = client.post("/api/projects/research/set_members", json={"members": []}, headers=dan)
+    assert r.status_code == 403
+    client.post("/api/projects/delete", json={"projects_names": ["research"]})
+    assert [p["project_name"] for p in client.post("/api/projects/list").json()] == ["main"]
+
+
+def test_invalid_project_name(client):
+    assert client.post("/api/projects/create", json={"project_name": "bad name!"}).status_code in (400, 422)
+
+
+# ---- secrets ----------------------------------------------------------------------------------
+def test_secrets(client):
+    r = client.post("/api/project/main/secrets/add", json={"name": "HF_TOKEN", "value": "s3cr3t"})
+    assert r.status_code == 200, r.text
+    assert client.post("/api/project/main/secrets/get", json={"name": "HF_TOKEN"}).json()["value"] == "s3cr3t"
+    listed = client.post("/api/project/main/secrets/list").json()
+    assert [s["name"] for s in listed] == ["HF_TOKEN"]
+    client.post("/api/project/main/secrets/delete", json={"secrets_names": ["HF_TOKEN"]})
+    assert client.post("/api/project/main/secrets/list").json() == []
+
+
+# ---- repos ------------------------------------------------------------------------------------
+def test_repos_and_code_upload(client):
+    _init_virtual_repo(client)
+    repos = client.post("/api/project/main/repos/list").json()
+    assert [r["repo_id"] for r in repos] == ["virt"]
+    r = client.post("/api/project/main/repos/upload_code?repo_id=virt", content=b"tar-bytes",
+                    headers={"content-type": "application/octet-stream"})
+    assert r.status_code == 200 and len(r.json()["blob_hash"]) == 64
+    client.post("/api/project/main/repos/delete", json={"repos_ids": ["virt"]})
+    assert client.post("/api/project/main/repos/list").json() == []
+
+
+# ---- backends ---------------------------------------------------------------------------------
+def test_backend_types(client):
+    types = client.post("/api/backends/list_types").json()
+    assert "local" in types and "remote" in types
+
+
+# ---- runs -------------------------------------------------------------------------------------
+def test_run_plan_submit_stop_delete(client):
+    _init_virtual_repo(client)
+    plan = client.post("/api/project/main/runs/get_plan", json=_task("r1"))
+    assert plan.status_code == 200, plan.text
+    body = plan.json()
+    assert body["job_plans"][0]["job_spec"]["commands"][-1].endswith("echo hi")
+    r = client.post("/api/project/main/runs/submit", json=_task("r1"))
+    assert r.status_code == 200, r.text
+    assert r.json()["status"] == "submitted"
+    # duplicate active run name rejected
+    assert client.post("/api/project/main/runs/submit", json=_task("r1")).status_code == 400
+    runs = client.post("/api/runs/list", json={}).json()
+    assert [x["run_spec"]["run_name"] for x in runs] == ["r1"]
+    got = client.post("/api/project/main/runs/get", json={"run_name": "r1"}).json()
+    assert got["jobs"][0]["job_submissions"][0]["status"] == "submitted"
+    assert client.post("/api/project/main/runs/stop", json={"runs_names": ["r1"], "abort": True}).status_code == 200
+    got = client.post("/api/project/main/runs/get", json={"run_name": "r1"}).json()
+    assert got["status"] == "terminating"
+    # cannot delete an active run
+    assert client.post("/api/project/main/runs/delete", json={"runs_names": ["r1"]}).status_code == 400
+
+
+def test_run_generated_name(client):
+    _init_virtual_repo(client)
+    r = client.post("/api/project/main/runs/submit", json=_task(None))
+    assert r.status_code == 200, r.text
+    assert r.json()["run_spec"]["run_name"]
+
+
+def test_invalid_configuration_rejected(client):
+    _init_virtual_repo(client)
+    spec = _task("bad")
+    spec["run_spec"]["configuration"]["unknown_field"] = 1
+    assert client.post("/api/project/main/runs/submit", json=spec).status_code == 422
+
+
+def test_multinode_task_creates_jobs(client):
+    _init_virtual_repo(client)
+    r = client.post("/api/project/main/runs/submit", json=_task("mn", nodes=2))
+    assert r.status_code == 200, r.text
+    jobs = r.json()["jobs"]
+    assert sorted(j["job_spec"]["job_num"] for j in jobs) == [0, 1]
+    assert all(j["job_spec"]["jobs_per_replica"] == 2 for j in jobs)
+
+
+def test_service_replicas(client):
+    _init_virtual_repo(client)
+    conf = {"type": "service", "commands": ["python -m http.server 8000"], "port": 8000, "replicas": 2}
+    spec = {"run_spec": {"run_name": "svc", "repo_id": "virt", "repo_data": {"repo_type": "virtual"},
+                         "configuration": conf, "ssh_key_pub": ""}}
+    r = client.post("/api/project/main/runs/submit", json=spec)
+    assert r.status_code == 200, r.text
+    assert sorted(j["job_spec"]["replica_num"] for j in r.json()["jobs"]) == [0, 1]
+
+
+# ---- fleets / instances / volumes / gateways ---------------------------------------------------
+def test_ssh_fleet_create_and_delete(client):
+    spec = {"spec": {"configuration": {"type": "fleet", "name": "onprem",
+                                       "ssh_config": {"user": "ubuntu", "identity_file": "/dev/null",
+                                                      "hosts": ["10.0.0.1", "10.0.0.2"]}},
+                     "profile": {"name": "default"}}}
+    r = client.post("/api/project/main/fleets/get_plan", json=spec)
+    assert r.status_code == 200, r.text
+    r = client.post("/api/project/main/fleets/create", json=spec)
+    assert r.status_code == 200, r.text
+    fleet = r.json()
+    assert fleet["name"] == "onprem" and len(fleet["instances"]) == 2
+    names = [f["name"] for f in client.post("/api/project/main/fleets/list").json()]
+    assert names == ["onprem"]
+    inst = client.post("/api/instances/list", json={}).json()
+    assert len(inst) == 2
+    assert client.post("/api/project/main/fleets/delete", json={"names": ["onprem"]}).status_code == 200
+
+
+def test_volumes_list_empty(client):
+    assert client.post("/api/project/main/volumes/list").json() == []
+    assert client.post("/api/volumes/list", json={}).json() == []
+
+
+def test_gateways_list_empty(client):
+    assert client.post("/api/project/main/gateways/list").json() == []
+
+
+def test_pool_list(client):
+    r = client.post("/api/project/main/pool/list")
+    assert r.status_code == 200
+
+
+def test_logs_poll_unknown_submission(client):
+    import uuid
+
+    r = client.post("/api/project/main/logs/poll", json={"run_name": "nope", "job_submission_id": str(uuid.uuid4())})
+    assert r.status_code == 200
+    assert r.json()["logs"] == []
+
+
+@pytest.mark.parametrize("path", ["/api/project/nope/runs/get", "/api/project/nope/fleets/list"])
+def test_unknown_project(client, path):
+    assert client.post(path, json={"run_name": "x"}).status_code in (403, 404, 400)
