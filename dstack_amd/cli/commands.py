@@ -1,0 +1,512 @@
+"""``dstack`` sub-commands (reference: ``cli/commands/{apply,attach,config,delete,fleet,gateway,init,
+logs,pool,ps,server,stats,stop,volume}.py``)."""
+
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+from dstack_amd.cli.utils import (
+    confirm_ask,
+    console,
+    fleets_table,
+    gateways_table,
+    print_table,
+    runs_table,
+    volumes_table,
+)
+from dstack_amd.core.errors import CLIError
+
+
+def _client(args):
+    from dstack_amd.api import Client
+
+    return Client.from_config(project_name=getattr(args, "project", None))
+
+
+def add_project_arg(p: argparse.ArgumentParser):
+    p.add_argument("--project", metavar="NAME", help="Project name (default: the default project)")
+
+
+# ---- server -----------------------------------------------------------------------------------
+def register_server(sub):
+    p = sub.add_parser("server", help="Start the dstack-amd server")
+    p.add_argument("--host", default=os.getenv("DSTACK_SERVER_HOST", "127.0.0.1"))
+    p.add_argument("-p", "--port", type=int, default=int(os.getenv("DSTACK_SERVER_PORT", "3000")))
+    p.add_argument("-l", "--log-level", default=os.getenv("DSTACK_SERVER_LOG_LEVEL", "INFO"))
+    p.add_argument("--token", default=os.getenv("DSTACK_SERVER_ADMIN_TOKEN"), help="Admin token")
+    p.add_argument("-y", "--yes", action="store_true")
+    p.set_defaults(func=cmd_server)
+
+
+def cmd_server(args) -> int:
+    from dstack_amd.server.main import run
+
+    run(args.host, args.port, args.log_level, args.token)
+    return 0
+
+
+# ---- config / init ----------------------------------------------------------------------------
+def register_config(sub):
+    p = sub.add_parser("config", help="Configure a server project in ~/.dstack/config.yml")
+    p.add_argument("--project", help="Project name")
+    p.add_argument("--url", help="Server URL")
+    p.add_argument("--token", help="User token")
+    p.add_argument("--default", action="store_true", help="Make the project the default")
+    p.add_argument("--remove", action="store_true", help="Remove the project configuration")
+    p.add_argument("-y", "--yes", action="store_true")
+    p.add_argument("-n", "--no", action="store_true")
+    p.set_defaults(func=cmd_config)
+
+
+def cmd_config(args) -> int:
+    from dstack_amd.api.server import APIClient
+    from dstack_amd.core.services.configs import ConfigManager
+
+    cm = ConfigManager()
+    if args.remove:
+        if not args.project:
+            raise CLIError("--project is required with --remove")
+        if args.yes or confirm_ask(f"Remove the project [code]{args.project}[/] configuration?"):
+            cm.delete_project(args.project)
+            cm.save()
+            console.print(f"Project [code]{args.project}[/] configuration removed")
+        return 0
+    if not (args.project and args.url and args.token):
+        for p in cm.config.projects:
+            console.print(f"{p.name}\t{p.url}{'  (default)' if p.default else ''}")
+        if not cm.config.projects:
+            console.print("No projects configured. Use: dstack config --url URL --project NAME --token TOKEN")
+        return 0
+    # validate the token against the server before saving
+    api = APIClient(args.url, args.token)
+    try:
+        api.projects.get(args.project)
+    except Exception as e:  # noqa: BLE001
+        raise CLIError(f"Cannot access project {args.project} at {args.url}: {e}") from e
+    default = args.default or not cm.config.projects
+    if not default and not args.no and not args.yes:
+        default = confirm_ask(f"Set [code]{args.project}[/] as the default project?", default=False)
+    cm.configure_project(args.project, args.url, args.token, default=default)
+    cm.save()
+    console.print(f"Configuration updated at {cm.config_filepath}")
+    return 0
+
+
+def register_init(sub):
+    p = sub.add_parser("init", help="Initialise the current directory as a repo for runs")
+    add_project_arg(p)
+    p.add_argument("-t", "--token", help="Git OAuth token for private repos")
+    p.add_argument("--git-identity", dest="git_identity_file", help="SSH key for private git repos")
+    p.add_argument("--ssh-identity", dest="ssh_identity_file", help="SSH key for dstack attach")
+    p.add_argument("--local", action="store_true", help="Upload the working tree instead of using git")
+    p.set_defaults(func=cmd_init)
+
+
+def cmd_init(args) -> int:
+    from dstack_amd.core.models.repos import LocalRepo, RemoteRepo, RepoError
+    from dstack_amd.core.services.configs import ConfigManager
+
+    client = _client(args)
+    cwd = os.getcwd()
+    repo = None
+    if not args.local:
+        try:
+            repo = RemoteRepo(cwd)
+        except RepoError:
+            repo = None
+    if repo is None:
+        repo = LocalRepo(cwd)
+    client.repos.init(repo, git_identity_file=args.git_identity_file, oauth_token=args.token)
+    cm = ConfigManager()
+    key = args.ssh_identity_file or str(cm.ensure_ssh_key())
+    cm.save_repo_config(cwd, repo.repo_id, "local" if isinstance(repo, LocalRepo) else "remote", key)
+    console.print("OK")
+    return 0
+
+
+# ---- apply / delete ---------------------------------------------------------------------------
+def register_apply(sub):
+    from dstack_amd.cli.configurators import RunConfigurator, register_repo_args
+
+    p = sub.add_parser("apply", help="Apply a configuration (run, fleet, gateway, volume)")
+    add_project_arg(p)
+    p.add_argument("-f", "--file", dest="configuration_file", help="Configuration file (default: .dstack.yml)")
+    p.add_argument("-y", "--yes", action="store_true", help="Do not ask for confirmation")
+    p.add_argument("--force", action="store_true", help="Re-create the resource even if unchanged")
+    p.add_argument("-d", "--detach", action="store_true", help="Exit right after submitting")
+    register_repo_args(p)
+    RunConfigurator.register_args(p)
+    p.set_defaults(func=cmd_apply)
+
+
+def cmd_apply(args) -> int:
+    from dstack_amd.cli.configurators import configurator_for, find_default_configuration, load_configuration
+
+    path = args.configuration_file or find_default_configuration(os.getcwd())
+    if path is None:
+        raise CLIError("No configuration file given (-f) and no .dstack.yml in the current directory")
+    conf = load_configuration(path)
+    client = _client(args)
+    return configurator_for(conf.type).apply(client, conf, path, args)
+
+
+def register_delete(sub):
+    p = sub.add_parser("delete", help="Delete the resources of a configuration (fleet, gateway, volume)")
+    add_project_arg(p)
+    p.add_argument("-f", "--file", dest="configuration_file", required=True)
+    p.add_argument("-y", "--yes", action="store_true")
+    p.set_defaults(func=cmd_delete)
+
+
+def cmd_delete(args) -> int:
+    from dstack_amd.cli.configurators import configurator_for, load_configuration
+
+    conf = load_configuration(args.configuration_file)
+    if conf.type in ("task", "service", "dev-environment"):
+        raise CLIError("Use `dstack stop` for runs")
+    return configurator_for(conf.type).delete(_client(args), conf, args)
+
+
+# ---- ps / logs / stop / attach / stats --------------------------------------------------------
+def register_ps(sub):
+    p = sub.add_parser("ps", help="List runs")
+    add_project_arg(p)
+    p.add_argument("-a", "--all", action="store_true", help="Show finished runs too")
+    p.add_argument("-v", "--verbose", action="store_true")
+    p.add_argument("-w", "--watch", action="store_true", help="Refresh every second")
+    p.add_argument("-n", "--last", type=int, default=None, help="Show the last N runs")
+    p.set_defaults(func=cmd_ps)
+
+
+def cmd_ps(args) -> int:
+    client = _client(args)
+
+    def table():
+        runs = [r.model for r in client.runs.list(all=args.all, limit=args.last or 100)]
+        if not args.all and not runs:
+            runs = [r.model for r in client.runs.list(all=True, limit=1)]
+        return runs_table(runs, verbose=args.verbose)
+
+    if not args.watch:
+        print_table(table())
+        return 0
+    from rich.live import Live
+
+    try:
+        with Live(table(), console=console, refresh_per_second=2) as live:
+            while True:
+                time.sleep(1)
+                live.update(table())
+    except KeyboardInterrupt:
+        return 0
+
+
+def register_logs(sub):
+    p = sub.add_parser("logs", help="Show run logs")
+    add_project_arg(p)
+    p.add_argument("run_name")
+    p.add_argument("-d", "--diagnose", action="store_true", help="Show runner logs (diagnostics)")
+    p.add_argument("-a", "--attach", action="store_true", help="Follow the logs")
+    p.add_argument("--replica", type=int, default=0)
+    p.add_argument("--job", type=int, default=0)
+    p.add_argument("--ssh-identity", dest="ssh_identity_file")
+    p.set_defaults(func=cmd_logs)
+
+
+def cmd_logs(args) -> int:
+    client = _client(args)
+    run = client.runs.get(args.run_name)
+    if run is None:
+        raise CLIError(f"Run {args.run_name} not found")
+    try:
+        for chunk in run.logs(diagnose=args.diagnose, replica_num=args.replica, job_num=args.job,
+                              follow=args.attach):
+            sys.stdout.buffer.write(chunk)
+            sys.stdout.flush()
+    except KeyboardInterrupt:
+        pass
+    return 0
+
+
+def register_stop(sub):
+    p = sub.add_parser("stop", help="Stop a run")
+    add_project_arg(p)
+    p.add_argument("run_name")
+    p.add_argument("-x", "--abort", action="store_true", help="Abort without graceful shutdown")
+    p.add_argument("-y", "--yes", action="store_true")
+    p.set_defaults(func=cmd_stop)
+
+
+def cmd_stop(args) -> int:
+    client = _client(args)
+    run = client.runs.get(args.run_name)
+    if run is None:
+        raise CLIError(f"Run {args.run_name} not found")
+    verb = "abort" if args.abort else "stop"
+    if not args.yes and not confirm_ask(f"Are you sure you want to {verb} the run [code]{args.run_name}[/]?"):
+        return 0
+    run.stop(abort=args.abort)
+    console.print(f"Run [code]{args.run_name}[/] {'aborted' if args.abort else 'is stopping'}")
+    return 0
+
+
+def register_attach(sub):
+    p = sub.add_parser("attach", help="Attach to a run: forward ports, optionally stream logs")
+    add_project_arg(p)
+    p.add_argument("run_name")
+    p.add_argument("--ssh-identity", dest="ssh_identity_file")
+    p.add_argument("--logs", action="store_true", help="Stream the run logs")
+    p.add_argument("--host", dest="bind_address", default="127.0.0.1", help="Local address to bind")
+    p.add_argument("-p", "--port", action="append", default=[], dest="ports", metavar="LOCAL:CONTAINER")
+    p.add_argument("--replica", type=int, default=0)
+    p.add_argument("--job", type=int, default=0)
+    p.set_defaults(func=cmd_attach)
+
+
+def cmd_attach(args) -> int:
+    client = _client(args)
+    run = client.runs.get(args.run_name)
+    if run is None:
+        raise CLIError(f"Run {args.run_name} not found")
+    overrides = {}
+    for p in args.ports:
+        local, _, container = p.partition(":")
+        if not container:
+            raise CLIError(f"invalid port mapping {p}: use LOCAL:CONTAINER")
+        overrides[int(container)] = int(local)
+    if not run.attach(ssh_identity_file=args.ssh_identity_file, bind_address=args.bind_address,
+                      ports_overrides=overrides):
+        raise CLIError(f"Run {args.run_name} is not running")
+    for cport, lport in (run.ports or {}).items():
+        console.print(f"Forwarded port {cport} -> {args.bind_address}:{lport}")
+    try:
+        if args.logs:
+            for chunk in run.logs(follow=True):
+                sys.stdout.buffer.write(chunk)
+                sys.stdout.flush()
+        else:
+            console.print("Attached. Press Ctrl-C to detach.")
+            while not run.refresh().status.is_finished():
+                time.sleep(2)
+    except KeyboardInterrupt:
+        pass
+    finally:
+        run.detach()
+    return 0
+
+
+def register_stats(sub):
+    p = sub.add_parser("stats", help="Show run resource metrics (CPU, memory, GPU)")
+    add_project_arg(p)
+    p.add_argument("run_name")
+    p.add_argument("-w", "--watch", action="store_true")
+    p.set_defaults(func=cmd_stats)
+
+
+def cmd_stats(args) -> int:
+    from rich.table import Table
+
+    client = _client(args)
+    run = client.runs.get(args.run_name)
+    if run is None:
+        raise CLIError(f"Run {args.run_name} not found")
+
+    def table():
+        t = Table(box=None, header_style="bold")
+        for col in ("NAME", "CPU", "MEMORY", "GPU"):
+            t.add_column(col)
+        for job in run.refresh().model.jobs:
+            m = client.api.metrics.get_job_metrics(client.project, args.run_name, job.job_spec.replica_num,
+                                                  job.job_spec.job_num)
+            vals = {x.name: (x.values[-1] if x.values else None) for x in m.metrics}
+            cpu = vals.get("cpu_usage_percent")
+            mem = vals.get("memory_working_set_bytes")
+            mem_total = vals.get("memory_total_bytes")
+            gpus = []
+            for i in range(int(vals.get("gpus_detected_num") or 0)):
+                util, used = vals.get(f"gpu_util_percent_gpu{i}"), vals.get(f"gpu_memory_usage_bytes_gpu{i}")
+                gpus.append(f"#{i} {_gb(used)} {util if util is not None else '-'}% util")
+            t.add_row(job.job_spec.job_name, f"{cpu}%" if cpu is not None else "-",
+                      f"{_gb(mem)}/{_gb(mem_total)}" if mem_total else _gb(mem), "\n".join(gpus) or "-")
+        return t
+
+    if not args.watch:
+        print_table(table())
+        return 0
+    from rich.live import Live
+
+    try:
+        with Live(table(), console=console, refresh_per_second=1) as live:
+            while True:
+                time.sleep(2)
+                live.update(table())
+    except KeyboardInterrupt:
+        return 0
+
+
+def _gb(v) -> str:
+    return "-" if v is None else f"{v / 2**30:.1f}GB"
+
+
+# ---- fleet / volume / gateway / pool ----------------------------------------------------------
+def register_fleet(sub):
+    p = sub.add_parser("fleet", help="Manage fleets")
+    add_project_arg(p)
+    p.add_argument("-v", "--verbose", action="store_true")
+    p.set_defaults(func=cmd_fleet_list)
+    s = p.add_subparsers(dest="fleet_cmd")
+    lp = s.add_parser("list")
+    lp.add_argument("-v", "--verbose", action="store_true")
+    add_project_arg(lp)
+    lp.set_defaults(func=cmd_fleet_list)
+    dp = s.add_parser("delete")
+    add_project_arg(dp)
+    dp.add_argument("name")
+    dp.add_argument("-i", "--instance", type=int, action="append", dest="instance_nums")
+    dp.add_argument("-y", "--yes", action="store_true")
+    dp.set_defaults(func=cmd_fleet_delete)
+
+
+def cmd_fleet_list(args) -> int:
+    client = _client(args)
+    print_table(fleets_table(client.api.fleets.list(client.project), verbose=getattr(args, "verbose", False)))
+    return 0
+
+
+def cmd_fleet_delete(args) -> int:
+    client = _client(args)
+    if args.instance_nums:
+        if args.yes or confirm_ask(f"Delete instances {args.instance_nums} of fleet [code]{args.name}[/]?"):
+            client.api.fleets.delete_instances(client.project, args.name, args.instance_nums)
+            console.print("Instances deleted")
+        return 0
+    if args.yes or confirm_ask(f"Delete the fleet [code]{args.name}[/]?"):
+        client.api.fleets.delete(client.project, [args.name])
+        console.print(f"Fleet [code]{args.name}[/] deleted")
+    return 0
+
+
+def register_volume(sub):
+    p = sub.add_parser("volume", help="Manage volumes")
+    add_project_arg(p)
+    p.set_defaults(func=cmd_volume_list, verbose=False)
+    s = p.add_subparsers(dest="volume_cmd")
+    lp = s.add_parser("list")
+    add_project_arg(lp)
+    lp.add_argument("-v", "--verbose", action="store_true")
+    lp.set_defaults(func=cmd_volume_list)
+    dp = s.add_parser("delete")
+    add_project_arg(dp)
+    dp.add_argument("name")
+    dp.add_argument("-y", "--yes", action="store_true")
+    dp.set_defaults(func=cmd_volume_delete)
+
+
+def cmd_volume_list(args) -> int:
+    client = _client(args)
+    print_table(volumes_table(client.api.volumes.list(client.project)))
+    return 0
+
+
+def cmd_volume_delete(args) -> int:
+    client = _client(args)
+    if args.yes or confirm_ask(f"Delete the volume [code]{args.name}[/]?"):
+        client.api.volumes.delete(client.project, [args.name])
+        console.print(f"Volume [code]{args.name}[/] deleted")
+    return 0
+
+
+def register_gateway(sub):
+    p = sub.add_parser("gateway", help="Manage gateways")
+    add_project_arg(p)
+    p.set_defaults(func=cmd_gateway_list)
+    s = p.add_subparsers(dest="gateway_cmd")
+    lp = s.add_parser("list")
+    add_project_arg(lp)
+    lp.add_argument("-v", "--verbose", action="store_true")
+    lp.set_defaults(func=cmd_gateway_list)
+    cp = s.add_parser("create")
+    add_project_arg(cp)
+    cp.add_argument("--backend", required=True)
+    cp.add_argument("--region", required=True)
+    cp.add_argument("--set-default", action="store_true")
+    cp.add_argument("--name")
+    cp.add_argument("--domain", required=True)
+    cp.set_defaults(func=cmd_gateway_create)
+    dp = s.add_parser("delete")
+    add_project_arg(dp)
+    dp.add_argument("name")
+    dp.add_argument("-y", "--yes", action="store_true")
+    dp.set_defaults(func=cmd_gateway_delete)
+    up = s.add_parser("update")
+    add_project_arg(up)
+    up.add_argument("name")
+    up.add_argument("--set-default", action="store_true")
+    up.add_argument("--domain")
+    up.set_defaults(func=cmd_gateway_update)
+
+
+def cmd_gateway_list(args) -> int:
+    client = _client(args)
+    print_table(gateways_table(client.api.gateways.list(client.project)))
+    return 0
+
+
+def cmd_gateway_create(args) -> int:
+    from dstack_amd.core.models.gateways import GatewayConfiguration
+
+    client = _client(args)
+    conf = GatewayConfiguration(name=args.name, backend=args.backend, region=args.region, domain=args.domain,
+                                default=args.set_default)
+    gw = client.api.gateways.create(client.project, conf)
+    print_table(gateways_table([gw]))
+    return 0
+
+
+def cmd_gateway_delete(args) -> int:
+    client = _client(args)
+    if args.yes or confirm_ask(f"Delete the gateway [code]{args.name}[/]?"):
+        client.api.gateways.delete(client.project, [args.name])
+        console.print(f"Gateway [code]{args.name}[/] deleted")
+    return 0
+
+
+def cmd_gateway_update(args) -> int:
+    client = _client(args)
+    if args.set_default:
+        client.api.gateways.set_default(client.project, args.name)
+    if args.domain is not None:
+        client.api.gateways.set_wildcard_domain(client.project, args.name, args.domain)
+    print_table(gateways_table([client.api.gateways.get(client.project, args.name)]))
+    return 0
+
+
+def register_pool(sub):
+    p = sub.add_parser("pool", help="(Deprecated: use fleets) list pool instances")
+    add_project_arg(p)
+    p.set_defaults(func=cmd_pool)
+
+
+def cmd_pool(args) -> int:
+    from rich.table import Table
+
+    client = _client(args)
+    t = Table(box=None, header_style="bold")
+    for col in ("INSTANCE", "BACKEND", "RESOURCES", "PRICE", "STATUS", "CREATED"):
+        t.add_column(col)
+    from dstack_amd.cli.utils import pretty_date
+
+    for inst in client.api.instances.list([client.project]):
+        t.add_row(inst.name, f"{inst.backend.value if inst.backend else ''} ({inst.region or ''})",
+                  inst.instance_type.resources.pretty_format() if inst.instance_type else "",
+                  f"${inst.price:.4g}" if inst.price is not None else "", inst.status.value, pretty_date(inst.created))
+    print_table(t)
+    return 0
+
+
+REGISTRARS = [register_server, register_config, register_init, register_apply, register_delete, register_ps,
+              register_logs, register_stop, register_attach, register_stats, register_fleet, register_volume,
+              register_gateway, register_pool]

@@ -1,0 +1,160 @@
+"""End-to-end on CPU: real server subprocess + local backend (native ``dstack-shim`` process driver
++ ``dstack-runner``) driven through the public API and the ``dstack`` CLI (reference analogue:
+the manual ``dstack apply`` flow of SURVEY §3.2; the reference has no automated e2e test)."""
+
+import os
+import subprocess
+import sys
+import textwrap
+import time
+
+import httpx
+import pytest
+
+from dstack_amd.native_bin import runner_path, shim_path
+
+pytestmark = pytest.mark.skipif(not (shim_path() and runner_path()), reason="native agents not built")
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def server():
+    from dstack_amd.server.testing import ServerProcess
+
+    srv = ServerProcess().start()
+    yield srv
+    srv.stop()
+
+
+@pytest.fixture
+def client(server):
+    return server.client()
+
+
+def _logs(run) -> str:
+    return b"".join(run.logs()).decode(errors="replace")
+
+
+def test_task_runs_and_streams_logs(client):
+    from dstack_amd.api import Task
+
+    run = client.runs.submit(Task(commands=["echo hello-$DSTACK_RUN_NAME", "echo rank=$DSTACK_NODE_RANK"],
+                                  name="e2e-hello"))
+    assert run.wait(timeout=60).value == "done"
+    out = _logs(run)
+    assert "hello-e2e-hello" in out and "rank=0" in out
+    sub = run.model.jobs[0].job_submissions[-1]
+    assert sub.exit_status == 0
+    t = sub.timings
+    assert t["submitted"] <= t["running"] <= t["first_log"] + 1e-3
+    assert t["first_log"] - t["submitted"] < 10.0
+
+
+def test_task_failure_exit_code(client):
+    from dstack_amd.api import Task
+
+    run = client.runs.submit(Task(commands=["echo about-to-fail", "exit 7"], name="e2e-fail"))
+    assert run.wait(timeout=60).value == "failed"
+    sub = run.model.jobs[0].job_submissions[-1]
+    assert sub.exit_status == 7
+    assert sub.termination_reason.value == "container_exited_with_error"
+    assert "about-to-fail" in _logs(run)
+
+
+def test_env_and_secrets_interpolation(client, server):
+    from dstack_amd.api import Task
+
+    client.api.secrets.create_or_update("main", "MY_SECRET", "s3cr3t-value")
+    run = client.runs.submit(Task(commands=["echo A=$A S=$S"], env={"A": "1", "S": "${{ secrets.MY_SECRET }}"},
+                                  name="e2e-env"))
+    assert run.wait(timeout=60).value == "done"
+    assert "A=1 S=s3cr3t-value" in _logs(run)
+
+
+def test_stop_long_running(client):
+    from dstack_amd.api import Task
+
+    run = client.runs.submit(Task(commands=["echo started", "sleep 300"], name="e2e-stop"))
+    deadline = time.time() + 30
+    while "started" not in _logs(run) and time.time() < deadline:
+        time.sleep(0.2)
+    run.stop(abort=False)
+    st = run.wait(timeout=60)
+    assert st.value in ("terminated", "aborted", "done")
+    assert run.model.jobs[0].job_submissions[-1].termination_reason.value in (
+        "terminated_by_user", "aborted_by_user")
+
+
+def test_local_repo_code_upload(client, tmp_path):
+    from dstack_amd.api import Task
+    from dstack_amd.core.models.repos import LocalRepo
+
+    (tmp_path / "train.py").write_text("print('training-script-ran', 6 * 7)\n")
+    (tmp_path / ".gitignore").write_text("ignored.txt\n")
+    (tmp_path / "ignored.txt").write_text("nope")
+    run = client.runs.submit(Task(commands=["python3 train.py", "ls"], name="e2e-repo"), repo=LocalRepo(str(tmp_path)))
+    assert run.wait(timeout=60).value == "done"
+    out = _logs(run)
+    assert "training-script-ran 42" in out
+    assert "ignored.txt" not in out
+
+
+def test_service_through_in_server_proxy(client, server):
+    from dstack_amd.api import Service
+
+    port = 18000 + os.getpid() % 1000
+    conf = Service(commands=[f"python3 -m http.server {port}"], port=port, name="e2e-svc", auth=False)
+    run = client.runs.submit(conf)
+    url = f"{server.url}/proxy/services/main/e2e-svc/"
+    deadline = time.time() + 60
+    body = None
+    while time.time() < deadline:
+        try:
+            r = httpx.get(url, timeout=2)
+            if r.status_code == 200:
+                body = r.text
+                break
+        except httpx.HTTPError:
+            pass
+        time.sleep(0.3)
+    run.stop(abort=True)
+    run.wait(timeout=60)
+    assert body is not None and "Directory listing" in body
+
+
+def test_multinode_task_rendezvous_env(client):
+    from dstack_amd.api import Task
+
+    cmd = "echo node=$DSTACK_NODE_RANK/$DSTACK_NODES_NUM master=$DSTACK_MASTER_NODE_IP world=$WORLD_SIZE"
+    run = client.runs.submit(Task(commands=[cmd], nodes=2, name="e2e-multinode"))
+    assert run.wait(timeout=90).value == "done"
+    outs = sorted(b"".join(run.logs(job_num=j)).decode() for j in (0, 1))
+    assert any("node=0/2" in o for o in outs) and any("node=1/2" in o for o in outs)
+    assert all("master=" in o and "master= " not in o for o in outs)
+
+
+def test_cli_apply_ps_logs(server, tmp_path):
+    (tmp_path / ".dstack.yml").write_text(textwrap.dedent("""
+        type: task
+        name: e2e-cli
+        commands:
+          - echo cli-says-$DSTACK_RUN_NAME
+          - cat data.txt
+        """))
+    (tmp_path / "data.txt").write_text("uploaded-data\n")
+    env = dict(os.environ, DSTACK_SERVER_URL=server.url, DSTACK_TOKEN=server.token,
+               DSTACK_DIR=str(tmp_path / "home"), PYTHONPATH=REPO)
+    dstack = [sys.executable, "-m", "dstack_amd"]
+    r = subprocess.run(dstack + ["apply", "-y"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "cli-says-e2e-cli" in r.stdout and "uploaded-data" in r.stdout
+    r = subprocess.run(dstack + ["ps", "-a"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=60)
+    assert "e2e-cli" in r.stdout
+    r = subprocess.run(dstack + ["logs", "e2e-cli"], cwd=tmp_path, env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert "uploaded-data" in r.stdout
+    (tmp_path / "fail.dstack.yml").write_text("type: task\nname: e2e-cli-fail\ncommands: [\"exit 5\"]\n")
+    r = subprocess.run(dstack + ["apply", "-y", "-f", "fail.dstack.yml"], cwd=tmp_path, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 5, r.stdout + r.stderr
