@@ -99,6 +99,7 @@ def main():
             "final_loss": res["final_loss"],
             "max_mem_gb": res["max_mem_gb"],
             "ops": os.environ.get("DSTACK_AMD_OPS", "hip"),
+            "gemm_tuning": res.get("gemm_tuning"),
             "attn": os.environ.get("DSTACK_AMD_ATTN", "hip"),
             "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu",
         }

@@ -108,11 +108,14 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         grad_accum: int = 1):
     env = init_distributed()
     device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    from dstack_amd.ops import gemm_tuning
+
+    gemm_mode = gemm_tuning.setup(device_index=env.local_rank if device.type == "cuda" else 0)
     t0 = time.time()
     tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum)
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
-              f"init={time.time()-t0:.1f}s", flush=True)
+              f"init={time.time()-t0:.1f}s gemm_tuning={gemm_mode}", flush=True)
     for i in range(warmup):
         loss = tr.step()
         if env.rank == 0:
@@ -140,6 +143,7 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         "max_mem_gb": torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else None,
     }
     result["tflops_per_gpu"] = tok_s / env.world * result["flops_per_token"] / 1e12
+    result["gemm_tuning"] = gemm_mode
     if env.rank == 0:
         print("[train] result " + json.dumps(result), flush=True)
     return env, tr, result
