@@ -81,6 +81,9 @@ def create_app(start_background: bool = True) -> FastAPI:
 
         if LocalShim._instance is not None:
             LocalShim._instance.stop()
+        from dstack_amd.server.services.gateways import LocalGatewayProcess
+
+        LocalGatewayProcess.stop_all()
 
     app = FastAPI(title="dstack-amd", version=__version__, lifespan=lifespan, docs_url="/api/docs",
                   openapi_url="/api/openapi.json")

@@ -45,20 +45,25 @@ def process_gateways_connections() -> bool:
     from dstack_amd.server.services.gateways import gateway_stats
     from dstack_amd.server.services.services import get_request_stats
 
+    from dstack_amd.server.models import RunModel
+
     with session_scope() as s:
         for g in s.execute(select(GatewayModel).where(GatewayModel.status == GatewayStatus.RUNNING.value)).scalars():
-            comp = g.gateway_compute
-            if comp is None or comp.instance_id == "local":
+            if g.gateway_compute is None:
                 continue
             try:
                 stats = gateway_stats(g)
             except Exception as e:  # noqa: BLE001
                 logger.debug("gateway %s stats: %s", g.name, e)
                 continue
-            for svc in stats.get("services", []):
-                run_id = svc.get("run_id")
-                for ts, dur in svc.get("requests", []):
-                    get_request_stats().record(run_id, dur, ts)
+            for item in stats if isinstance(stats, list) else []:
+                run = s.execute(select(RunModel).where(RunModel.project_id == g.project_id,
+                                                       RunModel.run_name == item.get("run_name"),
+                                                       RunModel.deleted == False)  # noqa: E712
+                                .order_by(RunModel.submitted_at.desc())).scalars().first()
+                w = (item.get("stats") or {}).get("60")
+                if run is not None and w is not None:
+                    get_request_stats().set_external(run.id, w["requests"] / 60.0, w["request_time"])
     return False
 
 

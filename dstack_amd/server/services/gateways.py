@@ -98,6 +98,9 @@ def delete_gateways(s: Session, project: ProjectModel, names: List[str]):
         if g.gateway_compute:
             g.gateway_compute.active = False
             g.gateway_compute.deleted = True
+        local = LocalGatewayProcess._instances.pop(f"{project.name}/{g.name}", None)
+        if local is not None:
+            local.stop()
         s.delete(g)
 
 
@@ -124,7 +127,60 @@ def _gateway_url(g: GatewayModel) -> Optional[str]:
     if comp is None:
         return None
     data = json.loads(comp.backend_data or "{}")
-    return data.get("api_url") or f"http://{comp.ip_address}:8000"
+    if data.get("api_url"):
+        return data["api_url"]  # local / trusted-LAN gateway
+    # cloud gateway: the control API listens on the gateway's loopback; reach it over SSH
+    from dstack_amd.core.services.ssh.tunnel import SSHTarget, get_tunnel_pool
+
+    target = SSHTarget(comp.ip_address, data.get("ssh_user", "ubuntu"), int(data.get("ssh_port", 22)))
+    local = get_tunnel_pool().forward(target, comp.ssh_private_key, int(data.get("control_port", 8000)))
+    return f"http://127.0.0.1:{local}"
+
+
+class LocalGatewayProcess:
+    """A gateway for the ``local`` backend: ``dstack_amd.proxy.gateway.main`` on the server host
+    (built-in data plane unless nginx is installed)."""
+
+    _instances: dict = {}
+
+    def __init__(self, name: str, state_dir: str, server_url: str):
+        import subprocess
+        import sys
+
+        from dstack_amd.server.testing import free_port
+
+        self.control_port, self.http_port = free_port(), free_port()
+        self.proc = subprocess.Popen(
+            [sys.executable, "-m", "dstack_amd.proxy.gateway.main", "--state-dir", state_dir, "--control-port",
+             str(self.control_port), "--http-port", str(self.http_port), "--server-url", server_url,
+             "--data-plane", "builtin"], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+            start_new_session=True)
+        for _ in range(300):
+            try:
+                if httpx.get(f"http://127.0.0.1:{self.control_port}/api/healthcheck", timeout=1).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                pass
+            if self.proc.poll() is not None:
+                raise GatewayError("local gateway exited during startup")
+            import time
+
+            time.sleep(0.1)
+        LocalGatewayProcess._instances[name] = self
+
+    def stop(self):
+        if self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(10)
+            except Exception:  # noqa: BLE001
+                self.proc.kill()
+
+    @classmethod
+    def stop_all(cls):
+        for gw in list(cls._instances.values()):
+            gw.stop()
+        cls._instances.clear()
 
 
 def _call(g: GatewayModel, method: str, path: str, body: Optional[dict] = None) -> dict:
@@ -145,15 +201,32 @@ def gateway_register_service(s: Session, run: RunModel):
             "auth": conf.auth, "client_max_body_size": 64 * 2**20,
             "options": {"openai": {"model": conf.model.model_dump()}} if conf.model else {}}
     _call(g, "POST", f"/api/registry/{run.project.name}/services/register", body)
+    if conf.model is not None:
+        _call(g, "POST", f"/api/registry/{run.project.name}/entrypoints/register",
+              {"domain": f"gateway.{g.wildcard_domain}", "https": conf.https})
+
+
+def gateway_unregister_service(s: Session, run: RunModel):
+    g = s.get(GatewayModel, run.gateway_id) if run.gateway_id else None
+    if g is None:
+        return
+    try:
+        _call(g, "POST", f"/api/registry/{run.project.name}/services/{run.run_name}/unregister")
+    except GatewayError as e:
+        logger.info("unregister service: %s", e)
 
 
 def gateway_register_replica(s: Session, run: RunModel, job: JobModel):
     g = s.get(GatewayModel, run.gateway_id)
     jpd = jobs_services.job_jpd(job)
     spec = RunSpec.model_validate_json(run.run_spec)
-    body = {"job_id": str(job.id), "app_port": spec.configuration.port.container_port,
-            "ssh_host": f"{jpd.username}@{jpd.hostname}", "ssh_port": jpd.ssh_port or 22,
-            "internal_ip": jpd.internal_ip}
+    jrd = jobs_services.job_jrd(job)
+    port = spec.configuration.port.container_port
+    if jrd is not None and jrd.ports:
+        port = int(jrd.ports.get(port, jrd.ports.get(str(port), port)))
+    direct = jpd.backend == BackendType.LOCAL or bool(json.loads(jpd.backend_data or "{}").get("direct"))
+    body = {"job_id": str(job.id), "app_port": port, "ssh_host": f"{jpd.username}@{jpd.hostname}",
+            "ssh_port": jpd.ssh_port or 22, "internal_ip": jpd.internal_ip or jpd.hostname, "direct": direct}
     try:
         _call(g, "POST", f"/api/registry/{run.project.name}/services/{run.run_name}/replicas/register", body)
     except GatewayError as e:
@@ -179,11 +252,23 @@ def provision_gateway(s: Session, g: GatewayModel):
     need the backend's ``create_gateway`` (cloud API)."""
     conf = GatewayConfiguration.model_validate_json(g.configuration)
     if conf.backend == BackendType.LOCAL:
+        from dstack_amd.server import settings
+
         private, public = generate_rsa_key_pair("dstack-gateway")
-        comp = GatewayComputeModel(id=uuid.uuid4(), instance_id="local", ip_address="127.0.0.1", hostname="localhost",
-                                   region="local", backend_id=g.backend_id, ssh_private_key=private,
-                                   ssh_public_key=public, configuration=conf.model_dump_json(),
-                                   backend_data=json.dumps({"api_url": None}))
+        try:
+            proc = LocalGatewayProcess(f"{g.project.name}/{g.name}",
+                                       str(settings.SERVER_DIR_PATH / "gateways" / g.project.name / g.name),
+                                       settings.SERVER_URL)
+        except GatewayError as e:
+            g.status = GatewayStatus.FAILED.value
+            g.status_message = str(e)
+            return
+        comp = GatewayComputeModel(id=uuid.uuid4(), instance_id="local", ip_address="127.0.0.1",
+                                   hostname=f"127.0.0.1:{proc.http_port}", region="local", backend_id=g.backend_id,
+                                   ssh_private_key=private, ssh_public_key=public,
+                                   configuration=conf.model_dump_json(),
+                                   backend_data=json.dumps({"api_url": f"http://127.0.0.1:{proc.control_port}",
+                                                            "http_port": proc.http_port}))
         s.add(comp)
         s.flush()
         g.gateway_compute_id = comp.id

@@ -58,6 +58,9 @@ def register_service(s: Session, run: RunModel):
                                      type=conf.model.type)
         run.gateway_id = gateway.id
         svc = ServiceSpec(url=url, model=model, options={"gateway": gateway.name})
+        from dstack_amd.server.services.gateways import gateway_register_service
+
+        gateway_register_service(s, run)
     else:
         if conf.scaling is not None and conf.scaling.metric == "rps" and gateway is None and \
                 conf.replicas.min != conf.replicas.max:
@@ -74,6 +77,10 @@ def register_service(s: Session, run: RunModel):
 
 def unregister_service(s: Session, run: RunModel):
     get_request_stats().forget(run.id)
+    if run.gateway_id is not None:
+        from dstack_amd.server.services.gateways import gateway_unregister_service
+
+        gateway_unregister_service(s, run)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -87,6 +94,7 @@ class RequestStats:
     def __init__(self):
         self._lock = threading.Lock()
         self._events: Dict[object, Deque[Tuple[float, float]]] = defaultdict(deque)
+        self._external: Dict[object, Tuple[float, float, float]] = {}
 
     def record(self, service_id, duration_s: float = 0.0, ts: Optional[float] = None):
         ts = ts or time.time()
@@ -96,14 +104,22 @@ class RequestStats:
             while q and q[0][0] < ts - self.WINDOW:
                 q.popleft()
 
+    def set_external(self, service_id, rps: float, mean_request_time: float):
+        """Aggregates reported by a gateway (its nginx/data plane saw the requests, not us)."""
+        with self._lock:
+            self._external[service_id] = (time.time(), rps, mean_request_time)
+
+    def _external_fresh(self, service_id):
+        e = self._external.get(service_id)
+        return e if e is not None and time.time() - e[0] < 120 else None
+
     def rps(self, service_id, window: float = 60.0) -> float:
         now = time.time()
         with self._lock:
             q = self._events.get(service_id)
-            if not q:
-                return 0.0
-            n = sum(1 for t, _ in q if t >= now - window)
-        return n / window
+            n = sum(1 for t, _ in q if t >= now - window) if q else 0
+            ext = self._external_fresh(service_id)
+        return n / window + (ext[1] if ext else 0.0)
 
     def mean_request_time(self, service_id, window: float = 60.0) -> float:
         now = time.time()
@@ -114,6 +130,7 @@ class RequestStats:
     def forget(self, service_id):
         with self._lock:
             self._events.pop(service_id, None)
+            self._external.pop(service_id, None)
 
 
 _stats = RequestStats()

@@ -158,3 +158,41 @@ def test_cli_apply_ps_logs(server, tmp_path):
     r = subprocess.run(dstack + ["apply", "-y", "-f", "fail.dstack.yml"], cwd=tmp_path, env=env, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 5, r.stdout + r.stderr
+
+
+def test_service_through_local_gateway(tmp_path):
+    """Gateway on the server host (built-in data plane): service registered on the gateway,
+    replica upstream registered when the job runs, Host-routed request reaches the replica."""
+    from dstack_amd.api import Service
+    from dstack_amd.core.models.gateways import GatewayConfiguration
+    from dstack_amd.server.testing import ServerProcess, free_port
+
+    with ServerProcess() as srv:
+        c = srv.client()
+        gw = c.api.gateways.create("main", GatewayConfiguration(name="gw", backend="local", region="local",
+                                                                domain="apps.test", default=True))
+        deadline = time.time() + 30
+        while gw.status.value != "running" and time.time() < deadline:
+            time.sleep(0.2)
+            gw = c.api.gateways.get("main", "gw")
+        assert gw.status.value == "running", gw.status_message
+        port = free_port()
+        run = c.runs.submit(Service(commands=[f"python3 -m http.server {port}"], port=port, name="gwsvc", https=False,
+                                    auth=False))
+        assert run.model.service.url == "http://gwsvc.apps.test"
+        data_plane = f"http://{gw.hostname}/"
+        body = None
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            try:
+                r = httpx.get(data_plane, headers={"host": "gwsvc.apps.test"}, timeout=2)
+                if r.status_code == 200:
+                    body = r.text
+                    break
+            except httpx.HTTPError:
+                pass
+            time.sleep(0.3)
+        run.stop(abort=True)
+        run.wait(timeout=60)
+        c.api.gateways.delete("main", ["gw"])
+        assert body is not None and "Directory listing" in body
