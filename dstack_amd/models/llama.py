@@ -95,13 +95,13 @@ class DecoderLayer(nn.Module):
             h = ops.rms_norm(x, self.attn_norm, cfg.norm_eps)
         else:
             x, h = ops.add_rms_norm(x, delta, self.attn_norm, cfg.norm_eps)
-        qkv = h @ self.wqkv.t()
+        qkv = ops.linear(h, self.wqkv)
         qkv = ops.rope(qkv, cos, sin, cfg.n_heads + cfg.n_kv_heads, hd)
         o = ops.attention(qkv, cfg.n_heads, cfg.n_kv_heads, causal=True)
-        attn_out = o @ self.wo.t()
+        attn_out = ops.linear(o, self.wo)
         x, h = ops.add_rms_norm(x, attn_out, self.ffn_norm, cfg.norm_eps)
-        a = ops.swiglu(h @ self.wgu.t())
-        return x, a @ self.wdown.t()
+        a = ops.swiglu(ops.linear(h, self.wgu))
+        return x, ops.linear(a, self.wdown)
 
 
 class Llama(nn.Module):
@@ -141,7 +141,7 @@ class Llama(nn.Module):
         for layer in self.layers:
             x, delta = layer(x, delta, cos, sin)
         _, h = ops.add_rms_norm(x, delta, self.norm, self.cfg.norm_eps)
-        return h.reshape(b * s, -1) @ self.lm_head.t()
+        return ops.linear(h.reshape(b * s, -1), self.lm_head)
 
     def loss(self, tokens: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         logits = self.forward(tokens)

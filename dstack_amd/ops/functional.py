@@ -172,6 +172,35 @@ def attention(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, causal: bool = T
 # ----------------------------------------------------------------------------------------------
 # Fused softmax cross-entropy over the vocab (never materialises fp32 logits)
 # ----------------------------------------------------------------------------------------------
+class _Linear(torch.autograd.Function):
+    """``y = x @ w.T`` whose weight gradient is written by the GEMM itself into the optimizer's
+    flat gradient buffer (``w._dsa_grad_sink``): the first micro-batch uses beta=0 (no memset of
+    the buffer), later ones accumulate with beta=1 in the hipBLASLt epilogue — no separate
+    AccumulateGrad add kernel, no zero-fill, one pass over the gradient instead of three."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        gx = g @ w if ctx.needs_input_grad[0] else None
+        if not ctx.needs_input_grad[1]:
+            return gx, None
+        g2, x2 = g.reshape(-1, g.shape[-1]), x.reshape(-1, x.shape[-1])
+        sink = getattr(w, "_dsa_grad_sink", None)
+        if sink is None:
+            return gx, g2.t() @ x2
+        sink(w, g2, x2)
+        return gx, None
+
+
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return _Linear.apply(x, w)
+
+
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target):

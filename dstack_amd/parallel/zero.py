@@ -116,10 +116,22 @@ class ZeroOptimizer:
             self.exp_avg.append(torch.zeros(n, dtype=torch.float32, device=device))
             self.exp_avg_sq.append(torch.zeros(n, dtype=torch.float32, device=device))
 
+        # padding between buckets' real params is never written by backward: zero it once per step
+        self._pads = []
+        for b in self.buckets:
+            used = sum(p.numel() for p in b.params)
+            if used < b.numel:
+                self._pads.append((b.start + used, b.numel - used))
+        self._backend = dist.get_backend(group) if self.distributed else None
         self._hooks = []
-        if self.overlap:
-            for p in params:
+        for p in params:
+            if p.dim() == 2:
+                # GEMM-produced weight gradients are written straight into flat_grad (ops.linear)
+                p._dsa_grad_sink = self._direct_grad
+                p._dsa_fresh = True
+            if self.overlap:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
+        self._direct_ok = set()
         self._arm()
 
     # ------------------------------------------------------------------------------------------
@@ -127,6 +139,17 @@ class ZeroOptimizer:
         for b in self.buckets:
             b.pending = len(b.params)
             b.work = None
+
+    def _direct_grad(self, p: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
+        """Weight gradient sink for ``ops.linear``: dW = g^T x into the flat buffer."""
+        if p._dsa_fresh:
+            torch.mm(g2.t(), x2, out=p.grad)
+            p._dsa_fresh = False
+        else:
+            p.grad.addmm_(g2.t(), x2)
+        self._direct_ok.add(p)
+        if self.overlap:
+            self._on_grad_ready(p)
 
     def _on_grad_ready(self, p: torch.Tensor):
         if not self.sync_grads:
@@ -142,12 +165,26 @@ class ZeroOptimizer:
         s, n = b.shard_range(self.rank, self.world)
         full = self.flat_grad[b.start : b.start + b.numel]
         out = self.flat_grad[s : s + n]
+        if self._backend == "gloo":  # CPU tests: gloo has no reduce-scatter
+            b.work = dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            return
+        # in place: RCCL reduce-scatters when recvbuff == sendbuff + rank * recvcount
         b.work = dist.reduce_scatter_tensor(
             out, full, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op
         )
 
     def zero_grad(self):
-        self.flat_grad.zero_()
+        """Zero only what backward accumulates into through autograd (norm weights, embedding)
+        and the bucket padding; GEMM weight gradients are overwritten by the first micro-batch."""
+        for b in self.buckets:
+            for p in b.params:
+                if p in self._direct_ok:
+                    p._dsa_fresh = True
+                else:
+                    p.grad.zero_()
+        for off, n in self._pads:
+            self.flat_grad[off : off + n].zero_()
+        self._direct_ok = set()
         self._arm()
 
     @torch.no_grad()
@@ -179,14 +216,14 @@ class ZeroOptimizer:
             works = []
             for b in self.buckets:
                 s, n = b.shard_range(self.rank, self.world)
-                works.append(
-                    dist.all_gather_into_tensor(
-                        self.flat_param[b.start : b.start + b.numel],
-                        self.flat_param[s : s + n],
-                        group=self.group,
-                        async_op=True,
-                    )
-                )
+                full = self.flat_param[b.start : b.start + b.numel]
+                if self._backend == "gloo":
+                    chunks = list(full.chunk(self.world))
+                    works.append(dist.all_gather(chunks, chunks[self.rank].clone(), group=self.group, async_op=True))
+                    continue
+                # in place: sendbuff == recvbuff + rank * sendcount
+                works.append(dist.all_gather_into_tensor(full, self.flat_param[s : s + n], group=self.group,
+                                                         async_op=True))
             for w in works:
                 w.wait()
 

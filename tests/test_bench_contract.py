@@ -1,0 +1,50 @@
+"""``bench.py`` driver contract on CPU: one JSON line from rank 0 with the BASELINE metric, for
+N=1 and for N=2 ranks under ``torch.distributed.run`` (gloo, 127.0.0.1 rendezvous)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--model", "llama-tiny", "--seq-len", "64", "--steps", "2", "--warmup", "1", "--grad-accum", "2",
+        "--no-coldstart"]
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _json_lines(out: str):
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+def _env():
+    return dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=REPO)
+
+
+def test_bench_single_process_json():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", *ARGS], cwd=REPO, env=_env(), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    assert d["metric"].startswith("p50 job cold-start")
+    assert d["config"]["global_batch"] == 2 and d["config"]["seq_len"] == 64
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_gloo():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2", *ARGS]
+    r = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    d = lines[0]
+    assert d["n_gpus"] == 2
+    assert d["config"]["parallelism"] == "dp2-zero1"
+    assert d["config"]["global_batch"] == 4
