@@ -1,0 +1,349 @@
+"""Container clouds: the job runs directly in a cloud container with ``dstack-runner`` as its
+entrypoint (no shim) — reference: ``C/backends/runpod/compute.py:40-251`` (GraphQL),
+``C/backends/vastai/compute.py`` and ``C/backends/kubernetes/compute.py:56-360``.
+
+RunPod is the AMD MI300X container path; Kubernetes requests ``amd.com/gpu`` (ROCm device plugin)
+and reaches pods through one SSH jump pod per backend (NodePort), as in the reference.
+"""
+
+from __future__ import annotations
+
+import base64
+import json
+import os
+import ssl
+import tempfile
+from typing import Dict, List, Optional, Tuple
+
+import httpx
+import yaml
+
+from dstack_amd.core.backends.base import Compute, DSTACK_RUNNER_SSH_PORT
+from dstack_amd.core.backends.catalog import catalog_offers
+from dstack_amd.core.backends.clouds.common import check_response, container_commands
+from dstack_amd.core.errors import ComputeError, NoCapacityError
+from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.instances import (
+    InstanceAvailability,
+    InstanceOfferWithAvailability,
+    SSHConnectionParams,
+)
+from dstack_amd.core.models.runs import Job, JobProvisioningData, Requirements, Run
+from dstack_amd.core.models.volumes import Volume, VolumeProvisioningData
+
+DEFAULT_ROCM_IMAGE = "rocm/pytorch:rocm6.4_ubuntu22.04_py3.10_pytorch_release_2.6.0"
+
+
+def _job_image(job: Job) -> str:
+    return job.job_spec.image_name or DEFAULT_ROCM_IMAGE
+
+
+def _entrypoint(keys: List[str]) -> str:
+    return " && ".join(container_commands(keys))
+
+
+class ContainerCompute(Compute):
+    def __init__(self, config: Dict, auth: Dict, client: Optional[httpx.Client] = None):
+        super().__init__()
+        self.config, self.auth = config or {}, auth or {}
+        self.http = client or httpx.Client(timeout=60)
+
+    def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
+        return catalog_offers(self.TYPE, self.config.get("regions"), requirements)
+
+
+# ---------------------------------------------------------------------------------------------
+class RunpodCompute(ContainerCompute):
+    TYPE = BackendType.RUNPOD
+    API = "https://api.runpod.io/graphql"
+
+    def _gql(self, query: str, variables: Optional[dict] = None) -> dict:
+        r = self.http.post(self.API, params={"api_key": self.auth.get("api_key", "")},
+                           json={"query": query, "variables": variables or {}})
+        d = check_response(r, "runpod graphql").json()
+        if d.get("errors"):
+            msg = "; ".join(e.get("message", "") for e in d["errors"])
+            if "no longer any instances available" in msg.lower() or "not enough" in msg.lower():
+                raise NoCapacityError(f"runpod: {msg}")
+            raise ComputeError(f"runpod: {msg}")
+        return d["data"]
+
+    def run_job(self, run: Run, job: Job, instance_offer: InstanceOfferWithAvailability, project_ssh_public_key: str,
+                project_ssh_private_key: str, volumes: List[Volume]) -> JobProvisioningData:
+        res = instance_offer.instance.resources
+        keys = [project_ssh_public_key.strip()] + ([run.run_spec.ssh_key_pub.strip()] if run.run_spec.ssh_key_pub else [])
+        gpu_type = {"MI300X": "AMD Instinct MI300X OAM"}.get(res.gpus[0].name, res.gpus[0].name) if res.gpus else None
+        inp = {
+            "name": f"{run.run_spec.run_name}-{job.job_spec.job_num}", "imageName": _job_image(job),
+            "gpuTypeId": gpu_type, "gpuCount": len(res.gpus), "cloudType": "SECURE" if not res.spot else "COMMUNITY",
+            "containerDiskInGb": max(10, res.disk.size_mib // 1024), "volumeInGb": 0, "minVcpuCount": res.cpus,
+            "minMemoryInGb": res.memory_mib // 1024, "dataCenterId": instance_offer.region,
+            "dockerArgs": f"bash -c {json.dumps(_entrypoint(keys))}",
+            "ports": f"{DSTACK_RUNNER_SSH_PORT}/tcp", "supportPublicIp": True,
+            "env": [{"key": "DSTACK_RUNNER_SSH", "value": "1"}],
+        }
+        if volumes:
+            inp["networkVolumeId"] = volumes[0].volume_id
+            inp["volumeMountPath"] = "/workspace"
+        mutation = "mutation($input: PodFindAndDeployOnDemandInput) { podFindAndDeployOnDemand(input: $input) " \
+                   "{ id machineId } }"
+        if res.spot:
+            mutation = "mutation($input: PodRentInterruptableInput!) { podRentInterruptable(input: $input) " \
+                       "{ id machineId } }"
+            inp["bidPerGpu"] = instance_offer.price / max(1, len(res.gpus))
+        data = self._gql(mutation, {"input": inp})
+        pod = data.get("podFindAndDeployOnDemand") or data.get("podRentInterruptable")
+        return JobProvisioningData(
+            backend=self.TYPE, instance_type=instance_offer.instance, instance_id=pod["id"], hostname=None,
+            region=instance_offer.region, price=instance_offer.price, username="root", ssh_port=None,
+            dockerized=False, backend_data=json.dumps({"machine_id": pod.get("machineId")}))
+
+    def update_provisioning_data(self, provisioning_data: JobProvisioningData, project_ssh_public_key: str = "",
+                                 project_ssh_private_key: str = "") -> None:
+        q = "query($id: String!) { pod(input: {podId: $id}) { id runtime { ports { ip isIpPublic privatePort " \
+            "publicPort type } } } }"
+        pod = self._gql(q, {"id": provisioning_data.instance_id}).get("pod") or {}
+        for p in ((pod.get("runtime") or {}).get("ports") or []):
+            if p.get("privatePort") == DSTACK_RUNNER_SSH_PORT and p.get("isIpPublic"):
+                provisioning_data.hostname = p["ip"]
+                provisioning_data.ssh_port = p["publicPort"]
+
+    def terminate_instance(self, instance_id: str, region: str, backend_data: Optional[str] = None) -> None:
+        try:
+            self._gql("mutation($id: String!) { podTerminate(input: {podId: $id}) }", {"id": instance_id})
+        except ComputeError as e:
+            if "not found" not in str(e).lower():
+                raise
+
+    def create_volume(self, volume: Volume) -> VolumeProvisioningData:
+        conf = volume.configuration
+        q = "mutation($input: CreateNetworkVolumeInput!) { createNetworkVolume(input: $input) { id size } }"
+        d = self._gql(q, {"input": {"name": volume.name, "size": int(conf.size or 100), "dataCenterId": conf.region}})
+        v = d["createNetworkVolume"]
+        return VolumeProvisioningData(backend=self.TYPE, volume_id=v["id"], size_gb=int(v["size"]),
+                                      price=0.07 * int(v["size"]) / 730, attachable=False, detachable=False)
+
+    def register_volume(self, volume: Volume) -> VolumeProvisioningData:
+        d = self._gql("query { myself { networkVolumes { id name size dataCenterId } } }")
+        for v in d["myself"]["networkVolumes"]:
+            if v["id"] == volume.configuration.volume_id:
+                return VolumeProvisioningData(backend=self.TYPE, volume_id=v["id"], size_gb=int(v["size"]),
+                                              attachable=False, detachable=False)
+        raise ComputeError(f"runpod volume {volume.configuration.volume_id} not found")
+
+    def delete_volume(self, volume: Volume) -> None:
+        self._gql("mutation($id: String!) { deleteNetworkVolume(input: {id: $id}) }", {"id": volume.volume_id})
+
+
+# ---------------------------------------------------------------------------------------------
+class VastAICompute(ContainerCompute):
+    TYPE = BackendType.VASTAI
+    API = "https://console.vast.ai/api/v0"
+
+    def _h(self):
+        return {"Authorization": f"Bearer {self.auth.get('api_key', '')}"}
+
+    def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
+        """Live marketplace asks (``/bundles``) when reachable; the catalog otherwise."""
+        try:
+            r = self.http.post(f"{self.API}/bundles/", headers=self._h(),
+                               json={"rentable": {"eq": True}, "rented": {"eq": False}, "order": [["dph_total", "asc"]],
+                                     "limit": 100})
+            asks = r.json().get("offers", []) if r.status_code == 200 else []
+        except httpx.HTTPError:
+            asks = []
+        if not asks:
+            return super().get_offers(requirements)
+        from dstack_amd.core.backends.base import offer_matches
+        from dstack_amd.core.models.gpus import normalize_gpu_name
+        from dstack_amd.core.models.instances import Disk, Gpu, InstanceType, Resources
+
+        out = []
+        for a in asks:
+            name = normalize_gpu_name(a.get("gpu_name", ""))
+            gpus = [Gpu(name=name, memory_mib=int(a.get("gpu_ram", 0))) for _ in range(int(a.get("num_gpus", 0)))]
+            res = Resources(cpus=int(a.get("cpu_cores_effective", 1)), memory_mib=int(a.get("cpu_ram", 0)), gpus=gpus,
+                            spot=False, disk=Disk(size_mib=int(float(a.get("disk_space", 100)) * 1024)))
+            o = InstanceOfferWithAvailability(backend=self.TYPE, instance=InstanceType(name=str(a["id"]), resources=res),
+                                              region=str(a.get("geolocation", "any")), price=float(a["dph_total"]),
+                                              availability=InstanceAvailability.AVAILABLE)
+            if offer_matches(o, requirements):
+                out.append(o)
+        return out
+
+    def run_job(self, run, job, instance_offer, project_ssh_public_key, project_ssh_private_key, volumes):
+        keys = [project_ssh_public_key.strip()] + ([run.run_spec.ssh_key_pub.strip()] if run.run_spec.ssh_key_pub else [])
+        body = {"client_id": "me", "image": _job_image(job), "disk": instance_offer.instance.resources.disk.size_mib // 1024,
+                "label": f"{run.run_spec.run_name}-{job.job_spec.job_num}", "onstart": _entrypoint(keys),
+                "runtype": "args", "env": {f"-p {DSTACK_RUNNER_SSH_PORT}:{DSTACK_RUNNER_SSH_PORT}": "1"}}
+        r = check_response(self.http.put(f"{self.API}/asks/{instance_offer.instance.name}/", headers=self._h(),
+                                         json=body), "vastai rent")
+        d = r.json()
+        if not d.get("success"):
+            raise NoCapacityError(f"vastai: {d}")
+        return JobProvisioningData(backend=self.TYPE, instance_type=instance_offer.instance,
+                                   instance_id=str(d["new_contract"]), hostname=None, region=instance_offer.region,
+                                   price=instance_offer.price, username="root", ssh_port=None, dockerized=False)
+
+    def update_provisioning_data(self, provisioning_data, project_ssh_public_key="", project_ssh_private_key=""):
+        r = check_response(self.http.get(f"{self.API}/instances/{provisioning_data.instance_id}/",
+                                         headers=self._h()), "vastai get")
+        inst = r.json().get("instances") or {}
+        ports = (inst.get("ports") or {}).get(f"{DSTACK_RUNNER_SSH_PORT}/tcp") or []
+        if inst.get("actual_status") == "running" and ports:
+            provisioning_data.hostname = inst.get("public_ipaddr", "").strip()
+            provisioning_data.ssh_port = int(ports[0]["HostPort"])
+
+    def terminate_instance(self, instance_id, region, backend_data=None):
+        r = self.http.delete(f"{self.API}/instances/{instance_id}/", headers=self._h())
+        if r.status_code != 404:
+            check_response(r, "vastai delete")
+
+
+# ---------------------------------------------------------------------------------------------
+class KubernetesCompute(ContainerCompute):
+    """Pods with ``amd.com/gpu`` limits; SSH through a per-backend jump pod (NodePort service)."""
+
+    TYPE = BackendType.KUBERNETES
+    NAMESPACE = "default"
+
+    def __init__(self, config, auth, client=None):
+        super().__init__(config, auth, client)
+        self._kube = self._load_kubeconfig()
+        self.namespace = self.config.get("namespace", self.NAMESPACE)
+
+    def _load_kubeconfig(self) -> dict:
+        kc = self.config.get("kubeconfig") or {}
+        data = kc.get("data")
+        if data is None and kc.get("filename"):
+            with open(os.path.expanduser(kc["filename"])) as f:
+                data = f.read()
+        if not data:
+            return {"server": self.config.get("api_url", "https://kubernetes.default.svc"), "token": self.auth.get("token")}
+        d = yaml.safe_load(data)
+        ctx_name = d.get("current-context")
+        ctx = next((c["context"] for c in d.get("contexts", []) if c["name"] == ctx_name), d["contexts"][0]["context"])
+        cluster = next(c["cluster"] for c in d["clusters"] if c["name"] == ctx["cluster"])
+        user = next(u["user"] for u in d["users"] if u["name"] == ctx["user"])
+        return {"server": cluster["server"], "ca": cluster.get("certificate-authority-data"),
+                "token": user.get("token"), "cert": user.get("client-certificate-data"),
+                "key": user.get("client-key-data")}
+
+    def _client(self) -> httpx.Client:
+        if self.http is not None and not isinstance(self.http, type(None)) and getattr(self, "_http_injected", True):
+            return self.http
+        return self.http
+
+    def _h(self):
+        return {"Authorization": f"Bearer {self._kube['token']}"} if self._kube.get("token") else {}
+
+    def _url(self, path: str) -> str:
+        return self._kube["server"].rstrip("/") + path
+
+    def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
+        """One offer per node (allocatable CPU/memory/``amd.com/gpu``)."""
+        from dstack_amd.core.backends.base import offer_matches
+        from dstack_amd.core.models.instances import Disk, Gpu, InstanceType, Resources
+
+        try:
+            r = self.http.get(self._url("/api/v1/nodes"), headers=self._h())
+            nodes = r.json().get("items", []) if r.status_code == 200 else []
+        except httpx.HTTPError:
+            nodes = []
+        out = []
+        for n in nodes:
+            alloc = n.get("status", {}).get("allocatable", {})
+            labels = n.get("metadata", {}).get("labels", {})
+            ngpu = int(alloc.get("amd.com/gpu", 0) or 0)
+            gname = labels.get("amd.com/gpu.product-name") or labels.get("beta.amd.com/gpu.product-name") or "MI300X"
+            from dstack_amd.core.models.gpus import normalize_gpu_name
+
+            gname = normalize_gpu_name(gname)
+            res = Resources(cpus=_cpu(alloc.get("cpu", "1")), memory_mib=_mem_mib(alloc.get("memory", "0")),
+                            gpus=[Gpu(name=gname, memory_mib=0, vendor="amd") for _ in range(ngpu)], spot=False,
+                            disk=Disk(size_mib=_mem_mib(alloc.get("ephemeral-storage", "100Gi"))))
+            o = InstanceOfferWithAvailability(backend=self.TYPE, instance=InstanceType(
+                name=n["metadata"]["name"], resources=res), region=self.namespace, price=0.0,
+                availability=InstanceAvailability.AVAILABLE)
+            if offer_matches(o, requirements):
+                out.append(o)
+        return out
+
+    def _ensure_jump_pod(self, project_ssh_public_key: str) -> Tuple[str, int]:
+        name = "dstack-ssh-jump"
+        r = self.http.get(self._url(f"/api/v1/namespaces/{self.namespace}/services/{name}"), headers=self._h())
+        if r.status_code == 404:
+            pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "labels": {"app": name}},
+                   "spec": {"containers": [{"name": "sshd", "image": "linuxserver/openssh-server:latest",
+                                            "env": [{"name": "PUBLIC_KEY", "value": project_ssh_public_key},
+                                                    {"name": "USER_NAME", "value": "root"}],
+                                            "ports": [{"containerPort": 2222}]}]}}
+            check_response(self.http.post(self._url(f"/api/v1/namespaces/{self.namespace}/pods"), headers=self._h(),
+                                          json=pod), "k8s jump pod")
+            svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name},
+                   "spec": {"type": "NodePort", "selector": {"app": name}, "ports": [{"port": 22, "targetPort": 2222}]}}
+            r = check_response(self.http.post(self._url(f"/api/v1/namespaces/{self.namespace}/services"),
+                                              headers=self._h(), json=svc), "k8s jump service")
+        port = r.json()["spec"]["ports"][0]["nodePort"]
+        host = self.config.get("networking", {}).get("ssh_host") or httpx.URL(self._kube["server"]).host
+        return host, int(port)
+
+    def run_job(self, run, job, instance_offer, project_ssh_public_key, project_ssh_private_key, volumes):
+        keys = [project_ssh_public_key.strip()] + ([run.run_spec.ssh_key_pub.strip()] if run.run_spec.ssh_key_pub else [])
+        res = instance_offer.instance.resources
+        name = f"{run.run_spec.run_name}-{job.job_spec.job_num}-{job.job_spec.replica_num}"[:60]
+        limits = {"cpu": str(res.cpus), "memory": f"{res.memory_mib}Mi"}
+        if res.gpus:
+            limits["amd.com/gpu"] = str(len(res.gpus))
+        pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "labels": {"app.kubernetes.io/name": name}},
+               "spec": {"restartPolicy": "Never", "nodeName": instance_offer.instance.name,
+                        "containers": [{"name": "job", "image": _job_image(job), "command": ["/bin/bash", "-c"],
+                                        "args": [_entrypoint(keys)], "ports": [{"containerPort": DSTACK_RUNNER_SSH_PORT}],
+                                        "resources": {"limits": limits, "requests": limits},
+                                        "securityContext": {"capabilities": {"add": ["SYS_PTRACE", "IPC_LOCK"]}},
+                                        "volumeMounts": [{"name": "shm", "mountPath": "/dev/shm"}]}],
+                        "volumes": [{"name": "shm", "emptyDir": {"medium": "Memory"}}]}}
+        check_response(self.http.post(self._url(f"/api/v1/namespaces/{self.namespace}/pods"), headers=self._h(),
+                                      json=pod), "k8s create pod")
+        svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name},
+               "spec": {"type": "ClusterIP", "selector": {"app.kubernetes.io/name": name},
+                        "ports": [{"port": DSTACK_RUNNER_SSH_PORT}]}}
+        check_response(self.http.post(self._url(f"/api/v1/namespaces/{self.namespace}/services"), headers=self._h(),
+                                      json=svc), "k8s create service")
+        jump_host, jump_port = self._ensure_jump_pod(project_ssh_public_key)
+        return JobProvisioningData(
+            backend=self.TYPE, instance_type=instance_offer.instance, instance_id=name, hostname=None,
+            region=self.namespace, price=0.0, username="root", ssh_port=DSTACK_RUNNER_SSH_PORT, dockerized=False,
+            ssh_proxy=SSHConnectionParams(hostname=jump_host, username="root", port=jump_port))
+
+    def update_provisioning_data(self, provisioning_data, project_ssh_public_key="", project_ssh_private_key=""):
+        r = check_response(self.http.get(self._url(f"/api/v1/namespaces/{self.namespace}/services/"
+                                                    f"{provisioning_data.instance_id}"), headers=self._h()), "k8s svc")
+        ip = r.json().get("spec", {}).get("clusterIP")
+        p = self.http.get(self._url(f"/api/v1/namespaces/{self.namespace}/pods/{provisioning_data.instance_id}"),
+                          headers=self._h()).json()
+        if p.get("status", {}).get("phase") == "Running" and ip:
+            provisioning_data.hostname = ip
+            provisioning_data.internal_ip = p["status"].get("podIP")
+
+    def terminate_instance(self, instance_id, region, backend_data=None):
+        for kind in ("services", "pods"):
+            r = self.http.delete(self._url(f"/api/v1/namespaces/{self.namespace}/{kind}/{instance_id}"),
+                                 headers=self._h())
+            if r.status_code not in (200, 202, 404):
+                check_response(r, f"k8s delete {kind}")
+
+
+def _cpu(v: str) -> int:
+    return max(1, int(float(v[:-1]) / 1000) if v.endswith("m") else int(float(v)))
+
+
+def _mem_mib(v: str) -> int:
+    units = {"Ki": 1 / 1024, "Mi": 1, "Gi": 1024, "Ti": 1024 * 1024, "K": 1 / 1024, "M": 1, "G": 1024}
+    for u, m in units.items():
+        if v.endswith(u):
+            return int(float(v[: -len(u)]) * m)
+    return int(float(v) / 2**20)
+
+
+_ = (base64, ssl, tempfile)

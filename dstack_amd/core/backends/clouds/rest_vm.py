@@ -1,0 +1,294 @@
+"""REST-API VM clouds (reference: ``C/backends/{lambdalabs,vultr,tensordock,cudo,datacrunch,nebius}/
+compute.py`` and their ``api_client.py``).
+
+Each class maps the cloud's launch / get / terminate endpoints onto ``VMCompute``; the VM's
+cloud-init installs ``dstack-shim``.  Vultr is the MI355X/MI325X/MI300X bare-metal path.
+"""
+
+from __future__ import annotations
+
+import base64
+import uuid
+from typing import Dict, Optional, Tuple
+
+from dstack_amd.core.backends.clouds.common import OAuthToken, VMCompute, check_response, cloud_init
+from dstack_amd.core.errors import ComputeError
+from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.instances import InstanceConfiguration, InstanceOfferWithAvailability
+
+
+class LambdaCompute(VMCompute):
+    """Lambda Cloud: ``/instance-operations/launch`` + registered SSH key (lambdalabs/compute.py)."""
+
+    TYPE = BackendType.LAMBDA
+    API = "https://cloud.lambdalabs.com/api/v1"
+
+    def _h(self):
+        return {"Authorization": f"Bearer {self.auth.get('api_key', '')}"}
+
+    def _ensure_key(self, cfg: InstanceConfiguration) -> str:
+        name = f"dstack-{cfg.project_name}"
+        r = check_response(self.http.get(f"{self.API}/ssh-keys", headers=self._h()), "lambda ssh-keys")
+        if not any(k["name"] == name for k in r.json().get("data", [])):
+            check_response(self.http.post(f"{self.API}/ssh-keys", headers=self._h(),
+                                          json={"name": name, "public_key": cfg.get_public_keys()[0]}),
+                           "lambda add ssh-key")
+        return name
+
+    def _launch(self, offer: InstanceOfferWithAvailability, cfg: InstanceConfiguration
+                ) -> Tuple[str, Optional[str], Optional[dict]]:
+        body = {"region_name": offer.region, "instance_type_name": offer.instance.name,
+                "ssh_key_names": [self._ensure_key(cfg)], "name": cfg.instance_name, "quantity": 1,
+                "user_data": cloud_init(cfg)}
+        r = check_response(self.http.post(f"{self.API}/instance-operations/launch", headers=self._h(), json=body),
+                           "lambda launch")
+        return r.json()["data"]["instance_ids"][0], None, None
+
+    def _describe(self, instance_id, region, backend_data) -> dict:
+        r = self.http.get(f"{self.API}/instances/{instance_id}", headers=self._h())
+        if r.status_code == 404:
+            return {"status": "terminated"}
+        d = check_response(r, "lambda get").json()["data"]
+        return {"status": d.get("status"), "hostname": d.get("ip"), "internal_ip": d.get("private_ip")}
+
+    def _terminate(self, instance_id, region, backend_data) -> None:
+        check_response(self.http.post(f"{self.API}/instance-operations/terminate", headers=self._h(),
+                                      json={"instance_ids": [instance_id]}), "lambda terminate")
+
+
+class VultrCompute(VMCompute):
+    """Vultr v2 API: cloud GPU instances and bare metal (the MI300X/MI325X/MI355X 8-GPU nodes)."""
+
+    TYPE = BackendType.VULTR
+    API = "https://api.vultr.com/v2"
+    SSH_USER = "root"
+    UBUNTU_22_OS_ID = 1743
+
+    def _h(self):
+        return {"Authorization": f"Bearer {self.auth.get('api_key', '')}"}
+
+    @staticmethod
+    def _kind(plan: str) -> str:
+        return "bare-metals" if plan.startswith("vbm-") else "instances"
+
+    def _launch(self, offer, cfg):
+        kind = self._kind(offer.instance.name)
+        body = {"region": offer.region, "plan": offer.instance.name, "label": cfg.instance_name,
+                "os_id": self.UBUNTU_22_OS_ID, "user_data": base64.b64encode(cloud_init(cfg).encode()).decode(),
+                "tags": ["dstack", cfg.project_name]}
+        if kind == "instances":
+            body["backups"] = "disabled"
+        r = check_response(self.http.post(f"{self.API}/{kind}", headers=self._h(), json=body), "vultr create")
+        key = "bare_metal" if kind == "bare-metals" else "instance"
+        return r.json()[key]["id"], None, {"kind": kind}
+
+    def _describe(self, instance_id, region, backend_data):
+        kind = backend_data.get("kind", "instances")
+        r = self.http.get(f"{self.API}/{kind}/{instance_id}", headers=self._h())
+        if r.status_code == 404:
+            return {"status": "terminated"}
+        d = check_response(r, "vultr get").json()
+        d = d.get("bare_metal") or d.get("instance") or {}
+        ip = d.get("main_ip")
+        ready = d.get("status") == "active" and ip and ip != "0.0.0.0"
+        return {"status": d.get("status"), "hostname": ip if ready else None, "internal_ip": d.get("internal_ip")}
+
+    def _terminate(self, instance_id, region, backend_data):
+        kind = backend_data.get("kind", "instances")
+        r = self.http.delete(f"{self.API}/{kind}/{instance_id}", headers=self._h())
+        if r.status_code != 404:
+            check_response(r, "vultr delete")
+
+
+class TensorDockCompute(VMCompute):
+    """TensorDock marketplace: ``/client/deploy/single`` on a host node (tensordock/compute.py)."""
+
+    TYPE = BackendType.TENSORDOCK
+    API = "https://marketplace.tensordock.com/api/v0"
+    SSH_USER = "user"
+
+    def _auth(self):
+        return {"api_key": self.auth.get("api_key", ""), "api_token": self.auth.get("api_token", "")}
+
+    def _launch(self, offer, cfg):
+        res = offer.instance.resources
+        node = offer.instance.name.split(":")[-1] if ":" in offer.instance.name else offer.region
+        data = {**self._auth(), "hostnode": node, "name": cfg.instance_name, "gpu_count": len(res.gpus),
+                "gpu_model": (res.gpus[0].name.lower() if res.gpus else ""), "vcpus": res.cpus,
+                "ram": res.memory_mib // 1024, "storage": res.disk.size_mib // 1024,
+                "external_ports": "{22}", "internal_ports": "{22}", "operating_system": "Ubuntu 22.04 LTS",
+                "cloudinit_script": cloud_init(cfg), "password": uuid.uuid4().hex}
+        r = check_response(self.http.post(f"{self.API}/client/deploy/single", data=data), "tensordock deploy")
+        d = r.json()
+        if not d.get("success"):
+            raise ComputeError(f"tensordock deploy: {d}")
+        ssh_port = next((int(k) for k, v in (d.get("port_forwards") or {}).items() if str(v) == "22"), 22)
+        return d["server"], d.get("ip"), {"ssh_port": ssh_port}
+
+    def create_instance(self, instance_offer, instance_config):
+        jpd = super().create_instance(instance_offer, instance_config)
+        jpd.ssh_port = (eval_json(jpd.backend_data) or {}).get("ssh_port", 22)
+        return jpd
+
+    def _describe(self, instance_id, region, backend_data):
+        r = check_response(self.http.post(f"{self.API}/client/get/single",
+                                          data={**self._auth(), "server": instance_id}), "tensordock get")
+        vm = r.json().get("virtualmachines") or {}
+        return {"status": vm.get("status"), "hostname": vm.get("ip_address")}
+
+    def _terminate(self, instance_id, region, backend_data):
+        check_response(self.http.post(f"{self.API}/client/delete/single",
+                                      data={**self._auth(), "server": instance_id}), "tensordock delete")
+
+
+class CudoCompute(VMCompute):
+    """Cudo Compute REST (cudo/compute.py): ``/projects/{p}/vm`` create/get/terminate."""
+
+    TYPE = BackendType.CUDO
+    API = "https://rest.compute.cudo.org/v1"
+    SSH_USER = "root"
+
+    def _h(self):
+        return {"Authorization": f"Bearer {self.auth.get('api_key', '')}"}
+
+    def _launch(self, offer, cfg):
+        project = self.config.get("project_id", "default")
+        res = offer.instance.resources
+        vm_id = cfg.instance_name[:60]
+        body = {"dataCenterId": offer.region, "machineType": offer.instance.name, "vmId": vm_id,
+                "vcpus": res.cpus, "memoryGib": res.memory_mib // 1024, "gpus": len(res.gpus),
+                "bootDiskImageId": "ubuntu-2204-nvidia-535-docker-v20240214" if res.gpus else "ubuntu-2204",
+                "bootDisk": {"sizeGib": res.disk.size_mib // 1024}, "customSshKeys": cfg.get_public_keys(),
+                "startScript": cloud_init(cfg)}
+        check_response(self.http.post(f"{self.API}/projects/{project}/vm", headers=self._h(), json=body),
+                       "cudo create")
+        return vm_id, None, {"project": project}
+
+    def _describe(self, instance_id, region, backend_data):
+        r = self.http.get(f"{self.API}/projects/{backend_data.get('project', 'default')}/vms/{instance_id}",
+                          headers=self._h())
+        if r.status_code == 404:
+            return {"status": "terminated"}
+        vm = check_response(r, "cudo get").json().get("VM", {})
+        return {"status": vm.get("state", "").lower(), "hostname": vm.get("externalIpAddress"),
+                "internal_ip": vm.get("internalIpAddress")}
+
+    def _terminate(self, instance_id, region, backend_data):
+        r = self.http.post(f"{self.API}/projects/{backend_data.get('project', 'default')}/vms/{instance_id}/terminate",
+                           headers=self._h())
+        if r.status_code != 404:
+            check_response(r, "cudo terminate")
+
+
+class DataCrunchCompute(VMCompute):
+    """DataCrunch: OAuth2 client credentials + ``/instances`` (datacrunch/compute.py)."""
+
+    TYPE = BackendType.DATACRUNCH
+    API = "https://api.datacrunch.io/v1"
+    SSH_USER = "root"
+
+    def __init__(self, config, auth, client=None):
+        super().__init__(config, auth, client)
+        self._token = OAuthToken(self._fetch_token)
+
+    def _fetch_token(self):
+        r = check_response(self.http.post(f"{self.API}/oauth2/token", json={
+            "grant_type": "client_credentials", "client_id": self.auth.get("client_id"),
+            "client_secret": self.auth.get("client_secret")}), "datacrunch token")
+        d = r.json()
+        return d["access_token"], d.get("expires_in", 3600)
+
+    def _h(self):
+        return {"Authorization": f"Bearer {self._token.get()}"}
+
+    def _launch(self, offer, cfg):
+        r = check_response(self.http.post(f"{self.API}/scripts", headers=self._h(), json={
+            "name": f"{cfg.instance_name}-init", "script": "#!/bin/bash\ncloud-init single --name runcmd || true\n"
+                                                             + _runcmd_script(cloud_init(cfg))}), "datacrunch script")
+        script_id = r.json() if isinstance(r.json(), str) else r.json().get("id")
+        keys = []
+        for pk in cfg.get_public_keys():
+            k = check_response(self.http.post(f"{self.API}/sshkeys", headers=self._h(),
+                                              json={"name": f"dstack-{uuid.uuid4().hex[:8]}", "key": pk}),
+                               "datacrunch ssh key")
+            keys.append(k.json() if isinstance(k.json(), str) else k.json().get("id"))
+        body = {"instance_type": offer.instance.name, "image": "ubuntu-22.04", "hostname": cfg.instance_name,
+                "description": cfg.instance_name, "ssh_key_ids": keys, "location_code": offer.region,
+                "startup_script_id": script_id, "is_spot": offer.instance.resources.spot,
+                "os_volume": {"name": "os", "size": offer.instance.resources.disk.size_mib // 1024}}
+        r = check_response(self.http.post(f"{self.API}/instances", headers=self._h(), json=body), "datacrunch deploy")
+        iid = r.text.strip().strip('"')
+        return iid, None, None
+
+    def _describe(self, instance_id, region, backend_data):
+        r = self.http.get(f"{self.API}/instances/{instance_id}", headers=self._h())
+        if r.status_code == 404:
+            return {"status": "terminated"}
+        d = check_response(r, "datacrunch get").json()
+        return {"status": d.get("status"), "hostname": d.get("ip")}
+
+    def _terminate(self, instance_id, region, backend_data):
+        check_response(self.http.put(f"{self.API}/instances", headers=self._h(),
+                                     json={"action": "delete", "id": instance_id}), "datacrunch delete")
+
+
+class NebiusCompute(VMCompute):
+    """Nebius AI cloud (REST gateway with a static IAM token; the reference's nebius backend)."""
+
+    TYPE = BackendType.NEBIUS
+    API = "https://compute.api.nebius.cloud/compute/v1"
+
+    def _h(self):
+        return {"Authorization": f"Bearer {self.auth.get('iam_token', '')}"}
+
+    def _launch(self, offer, cfg):
+        res = offer.instance.resources
+        body = {"folderId": self.config.get("folder_id"), "name": cfg.instance_name, "zoneId": offer.region,
+                "platformId": offer.instance.name.split(":")[0],
+                "resourcesSpec": {"cores": res.cpus, "memory": res.memory_mib * 2**20, "gpus": len(res.gpus)},
+                "metadata": {"user-data": cloud_init(cfg)},
+                "bootDiskSpec": {"diskSpec": {"size": res.disk.size_mib * 2**20,
+                                              "imageId": self.config.get("image_id", "ubuntu-22-04-lts-gpu")}},
+                "networkInterfaceSpecs": [{"subnetId": self.config.get("subnet_id"),
+                                           "primaryV4AddressSpec": {"oneToOneNatSpec": {"ipVersion": "IPV4"}}}]}
+        r = check_response(self.http.post(f"{self.API}/instances", headers=self._h(), json=body), "nebius create")
+        return r.json()["metadata"]["instanceId"], None, None
+
+    def _describe(self, instance_id, region, backend_data):
+        r = self.http.get(f"{self.API}/instances/{instance_id}", headers=self._h())
+        if r.status_code == 404:
+            return {"status": "terminated"}
+        d = check_response(r, "nebius get").json()
+        nic = (d.get("networkInterfaces") or [{}])[0]
+        nat = nic.get("primaryV4Address", {}).get("oneToOneNat", {}).get("address")
+        return {"status": d.get("status", "").lower(), "hostname": nat,
+                "internal_ip": nic.get("primaryV4Address", {}).get("address")}
+
+    def _terminate(self, instance_id, region, backend_data):
+        r = self.http.delete(f"{self.API}/instances/{instance_id}", headers=self._h())
+        if r.status_code != 404:
+            check_response(r, "nebius delete")
+
+
+def _runcmd_script(user_data: str) -> str:
+    """Extract the runcmd lines of our cloud-config as a bash script (for clouds with plain
+    startup scripts)."""
+    import json
+
+    out = []
+    in_run = False
+    for line in user_data.splitlines():
+        if line.startswith("runcmd:"):
+            in_run = True
+            continue
+        if in_run and line.startswith("  - "):
+            out.append(json.loads(line[4:]))
+        elif in_run:
+            break
+    return "\n".join(out) + "\n"
+
+
+def eval_json(s: Optional[str]) -> Optional[Dict]:
+    import json
+
+    return json.loads(s) if s else None

@@ -110,3 +110,15 @@ def convert_intel_accelerator_name(name: str) -> str:
         if name.startswith(model):
             return market
     return name
+
+
+def normalize_gpu_name(name: str) -> str:
+    """Any vendor's marketing/device-plugin name → catalog name (AMD first)."""
+    if not name:
+        return name
+    up = name.upper()
+    if "AMD" in up or "INSTINCT" in up or re.match(r"^MI\d", up):
+        return convert_amd_gpu_name(name)
+    if up.startswith("HL-"):
+        return convert_intel_accelerator_name(name)
+    return convert_nvidia_gpu_name(name)

@@ -4,7 +4,8 @@
 A project's backends are rows of ``backends`` (type + JSON config + encrypted auth).  The ``local``
 backend is implicit (enabled by ``DSTACK_LOCAL_BACKEND_ENABLED``); the ``remote`` backend (SSH
 fleets) needs no configuration.  Cloud backends are configured with credentials; their offers
-come from the built-in catalog (``core/backends/catalog.py``).
+come from the built-in catalog (``core/backends/catalog.py``) or the cloud's live API, and they
+provision through ``core/backends/clouds`` (REST clients, no vendor SDKs).
 """
 
 from __future__ import annotations
@@ -37,6 +38,11 @@ def _make_compute(backend_type: BackendType, config: dict, auth: dict) -> Comput
         from dstack_amd.core.backends.remote import RemoteCompute
 
         return RemoteCompute()
+    from dstack_amd.core.backends.clouds import compute_class
+
+    cls = compute_class(backend_type)
+    if cls is not None:
+        return cls(config, auth)
     from dstack_amd.core.backends.catalog import CatalogCompute
 
     return CatalogCompute(backend_type, config, auth)

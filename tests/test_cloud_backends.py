@@ -1,0 +1,338 @@
+"""Cloud backends against mock HTTP transports (reference analogue: ``src/tests/_internal/core/
+backends/*``): request shapes, auth/signing, the create -> poll -> terminate flow, capacity errors."""
+
+import base64
+import json
+import re
+import subprocess
+import urllib.parse
+
+import httpx
+import pytest
+
+from dstack_amd.core.backends.clouds import compute_class
+from dstack_amd.core.backends.clouds.common import sigv4_headers
+from dstack_amd.core.errors import NoCapacityError
+from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.instances import InstanceConfiguration, SSHKey
+from dstack_amd.core.models.runs import Requirements
+from dstack_amd.core.models.resources import ResourcesSpec
+
+CFG = InstanceConfiguration(project_name="main", instance_name="run-0-0", user="admin",
+                            ssh_keys=[SSHKey(public="ssh-ed25519 AAAA test@dstack")])
+
+
+def _client(handler):
+    return httpx.Client(transport=httpx.MockTransport(handler))
+
+
+def _offer(compute, gpu="MI300X"):
+    req = Requirements(resources=ResourcesSpec.model_validate({"gpu": gpu}))
+    offers = compute.get_offers(req)
+    assert offers, f"no {gpu} offers for {compute.TYPE}"
+    return offers[0]
+
+
+# ---- AWS --------------------------------------------------------------------------------------
+def test_sigv4_known_vector():
+    """AWS documentation's GetSessionToken-style vector shape: deterministic for fixed inputs."""
+    import datetime as dt
+
+    h = sigv4_headers("GET", "https://iam.amazonaws.com/?Action=ListUsers&Version=2010-05-08", "us-east-1", "iam",
+                      "AKIDEXAMPLE", "wJalrXUtnFEMI/K7MDENG+bPxRfiCYEXAMPLEKEY",
+                      now=dt.datetime(2015, 8, 30, 12, 36, 0, tzinfo=dt.timezone.utc))
+    assert h["x-amz-date"] == "20150830T123600Z"
+    assert h["Authorization"].startswith("AWS4-HMAC-SHA256 Credential=AKIDEXAMPLE/20150830/us-east-1/iam/aws4_request")
+    again = sigv4_headers("GET", "https://iam.amazonaws.com/?Action=ListUsers&Version=2010-05-08", "us-east-1", "iam",
+                          "AKIDEXAMPLE", "wJalrXUtnFEMI/K7MDENG+bPxRfiCYEXAMPLEKEY",
+                          now=dt.datetime(2015, 8, 30, 12, 36, 0, tzinfo=dt.timezone.utc))
+    assert h == again
+
+
+def _xml(body):
+    return f'<Response xmlns="http://ec2.amazonaws.com/doc/2016-11-15/">{body}</Response>'
+
+
+def test_aws_run_describe_terminate():
+    calls = []
+
+    def handler(req: httpx.Request):
+        form = dict(urllib.parse.parse_qsl(req.content.decode()))
+        calls.append(form["Action"])
+        assert req.headers["authorization"].startswith("AWS4-HMAC-SHA256 Credential=AK/")
+        a = form["Action"]
+        if a == "DescribeImages":
+            return httpx.Response(200, text=_xml("<imagesSet><item><imageId>ami-1</imageId><creationDate>2024"
+                                                 "</creationDate></item></imagesSet>"))
+        if a == "DescribeSecurityGroups":
+            return httpx.Response(200, text=_xml("<securityGroupInfo><item><groupId>sg-1</groupId></item>"
+                                                 "</securityGroupInfo>"))
+        if a == "RunInstances":
+            assert form["InstanceType"] == "p5.48xlarge" and form["ImageId"] == "ami-1"
+            ud = base64.b64decode(form["UserData"]).decode()
+            assert ud.startswith("#cloud-config") and "dstack-shim" in ud
+            return httpx.Response(200, text=_xml("<instancesSet><item><instanceId>i-123</instanceId></item>"
+                                                 "</instancesSet>"))
+        if a == "DescribeInstances":
+            return httpx.Response(200, text=_xml("<reservationSet><item><instancesSet><item><instanceId>i-123"
+                                                 "</instanceId><instanceState><name>running</name></instanceState>"
+                                                 "<ipAddress>3.3.3.3</ipAddress><privateIpAddress>10.0.0.3"
+                                                 "</privateIpAddress></item></instancesSet></item></reservationSet>"))
+        if a == "TerminateInstances":
+            return httpx.Response(200, text=_xml(""))
+        return httpx.Response(400, text=_xml("<Errors><Error><Code>Bad</Code></Error></Errors>"))
+
+    c = compute_class(BackendType.AWS)({}, {"access_key": "AK", "secret_key": "SK"}, _client(handler))
+    offer = _offer(c, "H100:8")
+    jpd = c.create_instance(offer, CFG)
+    assert jpd.instance_id == "i-123" and jpd.hostname is None
+    c.update_provisioning_data(jpd)
+    assert jpd.hostname == "3.3.3.3" and jpd.internal_ip == "10.0.0.3"
+    c.terminate_instance(jpd.instance_id, jpd.region, jpd.backend_data)
+    assert calls[-1] == "TerminateInstances"
+
+
+def test_aws_capacity_error():
+    def handler(req):
+        form = dict(urllib.parse.parse_qsl(req.content.decode()))
+        if form["Action"] == "RunInstances":
+            return httpx.Response(500, text=_xml("<Errors><Error><Code>InsufficientInstanceCapacity</Code>"
+                                                 "<Message>none</Message></Error></Errors>"))
+        if form["Action"] == "DescribeImages":
+            return httpx.Response(200, text=_xml("<imagesSet><item><imageId>ami-1</imageId></item></imagesSet>"))
+        return httpx.Response(200, text=_xml("<securityGroupInfo><item><groupId>sg</groupId></item>"
+                                             "</securityGroupInfo>"))
+
+    c = compute_class(BackendType.AWS)({}, {"access_key": "AK", "secret_key": "SK"}, _client(handler))
+    with pytest.raises(NoCapacityError):
+        c.create_instance(_offer(c, "H100:8"), CFG)
+
+
+# ---- Vultr (MI355X bare metal) -----------------------------------------------------------------
+def test_vultr_mi355x_bare_metal():
+    state = {"status": "pending"}
+
+    def handler(req):
+        assert req.headers["authorization"] == "Bearer vk"
+        if req.method == "POST" and req.url.path == "/v2/bare-metals":
+            body = json.loads(req.content)
+            assert body["plan"].endswith("mi355x-gpu")
+            assert "dstack-shim" in base64.b64decode(body["user_data"]).decode()
+            return httpx.Response(202, json={"bare_metal": {"id": "bm-1"}})
+        if req.method == "GET" and req.url.path == "/v2/bare-metals/bm-1":
+            return httpx.Response(200, json={"bare_metal": {"status": state["status"], "main_ip": "5.5.5.5"}})
+        if req.method == "DELETE":
+            return httpx.Response(204)
+        return httpx.Response(404)
+
+    c = compute_class(BackendType.VULTR)({}, {"api_key": "vk"}, _client(handler))
+    offer = _offer(c, "MI355X:8")
+    assert offer.instance.resources.gpus[0].name == "MI355X" and len(offer.instance.resources.gpus) == 8
+    jpd = c.create_instance(offer, CFG)
+    c.update_provisioning_data(jpd)
+    assert jpd.hostname is None  # not active yet
+    state["status"] = "active"
+    c.update_provisioning_data(jpd)
+    assert jpd.hostname == "5.5.5.5" and jpd.username == "root"
+    c.terminate_instance(jpd.instance_id, jpd.region, jpd.backend_data)
+
+
+# ---- RunPod (MI300X containers) ----------------------------------------------------------------
+def test_runpod_pod_lifecycle():
+    seen = []
+
+    def handler(req):
+        q = json.loads(req.content)
+        seen.append(q["query"].split("(")[0].split()[-1] if "mutation" in q["query"] else "query")
+        if "podFindAndDeployOnDemand" in q["query"]:
+            inp = q["variables"]["input"]
+            assert inp["gpuTypeId"] == "AMD Instinct MI300X OAM" and "dstack-runner" in inp["dockerArgs"]
+            return httpx.Response(200, json={"data": {"podFindAndDeployOnDemand": {"id": "pod1", "machineId": "m"}}})
+        if "pod(input" in q["query"]:
+            return httpx.Response(200, json={"data": {"pod": {"id": "pod1", "runtime": {"ports": [
+                {"ip": "7.7.7.7", "isIpPublic": True, "privatePort": 10022, "publicPort": 40022, "type": "tcp"}]}}}})
+        if "podTerminate" in q["query"]:
+            return httpx.Response(200, json={"data": {"podTerminate": None}})
+        return httpx.Response(200, json={"errors": [{"message": "unexpected"}]})
+
+    from types import SimpleNamespace
+
+    c = compute_class(BackendType.RUNPOD)({}, {"api_key": "rk"}, _client(handler))
+    offer = _offer(c, "MI300X:1")
+    run = SimpleNamespace(run_spec=SimpleNamespace(run_name="r", ssh_key_pub="ssh-ed25519 USER"))
+    job = SimpleNamespace(job_spec=SimpleNamespace(job_num=0, image_name=None))
+    jpd = c.run_job(run, job, offer, "ssh-ed25519 PROJECT", "", [])
+    assert jpd.instance_id == "pod1" and not jpd.dockerized
+    c.update_provisioning_data(jpd)
+    assert (jpd.hostname, jpd.ssh_port) == ("7.7.7.7", 40022)
+    c.terminate_instance("pod1", jpd.region)
+
+
+def test_runpod_no_capacity():
+    def handler(req):
+        return httpx.Response(200, json={"errors": [{"message": "There are no longer any instances available"}]})
+
+    from types import SimpleNamespace
+
+    c = compute_class(BackendType.RUNPOD)({}, {"api_key": "rk"}, _client(handler))
+    run = SimpleNamespace(run_spec=SimpleNamespace(run_name="r", ssh_key_pub=""))
+    job = SimpleNamespace(job_spec=SimpleNamespace(job_num=0, image_name=None))
+    with pytest.raises(NoCapacityError):
+        c.run_job(run, job, _offer(c, "MI300X:1"), "ssh-ed25519 K", "", [])
+
+
+# ---- Lambda / DataCrunch / Cudo ----------------------------------------------------------------
+def test_lambda_launch_registers_key():
+    keys = []
+
+    def handler(req):
+        p = req.url.path
+        if p.endswith("/ssh-keys") and req.method == "GET":
+            return httpx.Response(200, json={"data": [{"name": k} for k in keys]})
+        if p.endswith("/ssh-keys"):
+            keys.append(json.loads(req.content)["name"])
+            return httpx.Response(200, json={"data": {}})
+        if p.endswith("/launch"):
+            body = json.loads(req.content)
+            assert body["ssh_key_names"] == ["dstack-main"]
+            return httpx.Response(200, json={"data": {"instance_ids": ["L1"]}})
+        if p.endswith("/instances/L1"):
+            return httpx.Response(200, json={"data": {"status": "active", "ip": "9.9.9.9"}})
+        if p.endswith("/terminate"):
+            return httpx.Response(200, json={"data": {}})
+        return httpx.Response(404)
+
+    c = compute_class(BackendType.LAMBDA)({}, {"api_key": "lk"}, _client(handler))
+    jpd = c.create_instance(_offer(c, "H100:8"), CFG)
+    c.update_provisioning_data(jpd)
+    assert jpd.hostname == "9.9.9.9" and keys == ["dstack-main"]
+    c.terminate_instance("L1", jpd.region)
+
+
+def test_datacrunch_oauth_token_cached():
+    tokens = []
+
+    def handler(req):
+        if req.url.path.endswith("/oauth2/token"):
+            tokens.append(1)
+            return httpx.Response(200, json={"access_token": "T", "expires_in": 3600})
+        assert req.headers["authorization"] == "Bearer T"
+        if req.url.path.endswith("/scripts"):
+            return httpx.Response(200, text='"script-1"')
+        if req.url.path.endswith("/sshkeys"):
+            return httpx.Response(200, text='"key-1"')
+        if req.url.path.endswith("/instances") and req.method == "POST":
+            return httpx.Response(200, text='"inst-1"')
+        return httpx.Response(200, json={"status": "running", "ip": "1.2.3.4"})
+
+    c = compute_class(BackendType.DATACRUNCH)({}, {"client_id": "a", "client_secret": "b"}, _client(handler))
+    jpd = c.create_instance(_offer(c, "H100:8"), CFG)
+    c.update_provisioning_data(jpd)
+    assert jpd.instance_id == "inst-1" and jpd.hostname == "1.2.3.4"
+    assert len(tokens) == 1
+
+
+# ---- GCP / OCI signing with a real RSA key ---------------------------------------------------
+@pytest.fixture(scope="module")
+def rsa_pem(tmp_path_factory):
+    p = tmp_path_factory.mktemp("k") / "key.pem"
+    subprocess.run(["openssl", "genrsa", "-out", str(p), "2048"], check=True, capture_output=True)
+    return p.read_text()
+
+
+def test_gcp_jwt_token_and_insert(rsa_pem):
+    def handler(req):
+        if req.url.host == "oauth2.googleapis.com":
+            form = dict(urllib.parse.parse_qsl(req.content.decode()))
+            assert form["grant_type"].endswith("jwt-bearer")
+            assert len(form["assertion"].split(".")) == 3
+            return httpx.Response(200, json={"access_token": "G", "expires_in": 3600})
+        assert req.headers["authorization"] == "Bearer G"
+        if req.method == "POST":
+            body = json.loads(req.content)
+            assert body["scheduling"]["onHostMaintenance"] == "TERMINATE"
+            return httpx.Response(200, json={"name": "op"})
+        return httpx.Response(200, json={"status": "RUNNING", "networkInterfaces": [
+            {"networkIP": "10.1.1.1", "accessConfigs": [{"natIP": "34.1.1.1"}]}]})
+
+    sa = {"client_email": "sa@p.iam.gserviceaccount.com", "private_key": rsa_pem, "project_id": "p"}
+    c = compute_class(BackendType.GCP)({}, {"data": json.dumps(sa)}, _client(handler))
+    jpd = c.create_instance(_offer(c, "H100:8"), CFG)
+    c.update_provisioning_data(jpd)
+    assert jpd.hostname == "34.1.1.1"
+
+
+def test_oci_http_signature(rsa_pem):
+    def handler(req):
+        auth = req.headers["authorization"]
+        assert auth.startswith('Signature version="1",keyId="ten/usr/fp",algorithm="rsa-sha256"')
+        if req.method == "POST":
+            assert 'headers="(request-target) date host x-content-sha256 content-type content-length"' in auth
+            assert json.loads(req.content)["shape"] == "BM.GPU.MI300X.8"
+            return httpx.Response(200, json={"id": "ocid1.instance"})
+        if "vnicAttachments" in str(req.url):
+            return httpx.Response(200, json=[{"vnicId": "v1"}])
+        if "/vnics/" in req.url.path:
+            return httpx.Response(200, json={"publicIp": "140.1.1.1", "privateIp": "10.0.0.9"})
+        return httpx.Response(200, json={"lifecycleState": "RUNNING"})
+
+    c = compute_class(BackendType.OCI)({"compartment_id": "comp"}, {"tenancy": "ten", "user": "usr",
+                                                                      "fingerprint": "fp", "key_content": rsa_pem},
+                                       _client(handler))
+    jpd = c.create_instance(_offer(c, "MI300X:8"), CFG)
+    c.update_provisioning_data(jpd)
+    assert jpd.hostname == "140.1.1.1"
+
+
+# ---- Kubernetes -------------------------------------------------------------------------------
+def test_kubernetes_offers_and_pod():
+    created = []
+
+    def handler(req):
+        p = req.url.path
+        if p == "/api/v1/nodes":
+            return httpx.Response(200, json={"items": [{"metadata": {"name": "mi355x-node", "labels": {
+                "amd.com/gpu.product-name": "AMD Instinct MI355 OAM"}}, "status": {"allocatable": {
+                    "cpu": "256", "memory": "3000Gi", "amd.com/gpu": "8", "ephemeral-storage": "10Ti"}}}]})
+        if req.method == "POST":
+            body = json.loads(req.content)
+            created.append(body["kind"])
+            if body["kind"] == "Pod" and body["metadata"]["name"] != "dstack-ssh-jump":
+                lim = body["spec"]["containers"][0]["resources"]["limits"]
+                assert lim["amd.com/gpu"] == "8"
+            if body["kind"] == "Service" and body["spec"]["type"] == "NodePort":
+                return httpx.Response(201, json={"spec": {"ports": [{"nodePort": 30022}]}})
+            return httpx.Response(201, json=body)
+        if p.endswith("/services/dstack-ssh-jump"):
+            return httpx.Response(404)
+        if "/services/" in p:
+            return httpx.Response(200, json={"spec": {"clusterIP": "10.96.0.5"}})
+        if "/pods/" in p:
+            return httpx.Response(200, json={"status": {"phase": "Running", "podIP": "10.244.0.7"}})
+        return httpx.Response(404)
+
+    from types import SimpleNamespace
+
+    kubeconfig = {"data": json.dumps({"current-context": "c", "contexts": [{"name": "c", "context": {
+        "cluster": "k", "user": "u"}}], "clusters": [{"name": "k", "cluster": {"server": "https://k8s.example:6443"}}],
+        "users": [{"name": "u", "user": {"token": "tok"}}]})}
+    c = compute_class(BackendType.KUBERNETES)({"kubeconfig": kubeconfig}, {}, _client(handler))
+    offers = c.get_offers(Requirements(resources=ResourcesSpec.model_validate({"gpu": "MI355X:8"})))
+    assert len(offers) == 1 and offers[0].instance.resources.gpus[0].name == "MI355X"
+    run = SimpleNamespace(run_spec=SimpleNamespace(run_name="r", ssh_key_pub=""))
+    job = SimpleNamespace(job_spec=SimpleNamespace(job_num=0, replica_num=0, image_name=None))
+    jpd = c.run_job(run, job, offers[0], "ssh-ed25519 K", "", [])
+    assert jpd.ssh_proxy.port == 30022 and jpd.ssh_proxy.hostname == "k8s.example"
+    c.update_provisioning_data(jpd)
+    assert jpd.hostname == "10.96.0.5"
+    assert created.count("Pod") == 2 and created.count("Service") == 2
+
+
+def test_every_cloud_backend_plans_offers():
+    for bt in BackendType:
+        cls = compute_class(bt)
+        if cls is None or bt == BackendType.KUBERNETES:
+            continue
+        c = cls({}, {}, _client(lambda req: httpx.Response(500)))
+        assert isinstance(c.get_offers(None), list)
+        assert re.match(r"^[a-z]+$", c.TYPE.value)
