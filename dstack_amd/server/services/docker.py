@@ -1,0 +1,126 @@
+"""Docker registry introspection (reference: ``S/services/docker.py:74-101``, python-dxf; cached
+80 s in ``S/services/jobs/configurators/base.py:282-289``).
+
+Reads an image's config (``User``, ``Entrypoint``, ``Cmd``, ``Env``) through the registry HTTP API
+v2: bearer-token challenge (Docker Hub, GHCR, NGC, ECR-compatible), manifest list / OCI index ->
+``linux/amd64`` manifest -> config blob.  Used when a configuration gives an ``image`` but no
+``commands`` (run the image's own entrypoint) and to resolve the container user.
+"""
+
+from __future__ import annotations
+
+import threading
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import httpx
+
+MANIFEST_TYPES = ", ".join([
+    "application/vnd.docker.distribution.manifest.list.v2+json",
+    "application/vnd.oci.image.index.v1+json",
+    "application/vnd.docker.distribution.manifest.v2+json",
+    "application/vnd.oci.image.manifest.v1+json",
+])
+CACHE_TTL = 80.0
+
+
+@dataclass
+class ImageRef:
+    registry: str
+    repository: str
+    reference: str  # tag or digest
+
+
+@dataclass
+class ImageConfig:
+    user: Optional[str]
+    entrypoint: Optional[List[str]]
+    cmd: Optional[List[str]]
+    env: List[str]
+
+
+def parse_image_name(image: str) -> ImageRef:
+    """``ubuntu`` -> docker.io/library/ubuntu:latest; ``ghcr.io/o/r:t``; ``reg:5000/r@sha256:..``"""
+    name, digest = (image.split("@", 1) + [None])[:2]
+    first, _, rest = name.partition("/")
+    if rest and ("." in first or ":" in first or first == "localhost"):
+        registry, path = first, rest
+    else:
+        registry, path = "registry-1.docker.io", name
+        if "/" not in path:
+            path = f"library/{path}"
+    tag = "latest"
+    if ":" in path.rsplit("/", 1)[-1]:
+        path, tag = path.rsplit(":", 1)
+    if registry == "docker.io":
+        registry = "registry-1.docker.io"
+    return ImageRef(registry, path, digest or tag)
+
+
+class RegistryClient:
+    def __init__(self, client: Optional[httpx.Client] = None):
+        self.http = client or httpx.Client(timeout=30, follow_redirects=True)
+        self._cache: Dict[Tuple[str, Optional[str]], Tuple[float, ImageConfig]] = {}
+        self._lock = threading.Lock()
+
+    def _token(self, challenge: str, auth: Optional[Tuple[str, str]]) -> Optional[str]:
+        params = dict(p.split("=", 1) for p in challenge[len("Bearer "):].replace('"', "").split(","))
+        realm = params.pop("realm")
+        r = self.http.get(realm, params=params, auth=auth)
+        if r.status_code != 200:
+            return None
+        d = r.json()
+        return d.get("token") or d.get("access_token")
+
+    def _get(self, url: str, headers: dict, auth, state: dict) -> httpx.Response:
+        if state.get("token"):
+            headers = {**headers, "Authorization": f"Bearer {state['token']}"}
+        r = self.http.get(url, headers=headers, auth=auth if not state.get("token") else None)
+        if r.status_code == 401 and r.headers.get("www-authenticate", "").startswith("Bearer "):
+            state["token"] = self._token(r.headers["www-authenticate"], auth)
+            if state["token"]:
+                r = self.http.get(url, headers={**headers, "Authorization": f"Bearer {state['token']}"})
+        return r
+
+    def get_image_config(self, image: str, username: Optional[str] = None,
+                         password: Optional[str] = None) -> ImageConfig:
+        key = (image, username)
+        with self._lock:
+            hit = self._cache.get(key)
+            if hit and time.time() - hit[0] < CACHE_TTL:
+                return hit[1]
+        ref = parse_image_name(image)
+        base = f"https://{ref.registry}/v2/{ref.repository}"
+        auth = (username, password) if username and password else None
+        state: dict = {}
+        r = self._get(f"{base}/manifests/{ref.reference}", {"Accept": MANIFEST_TYPES}, auth, state)
+        if r.status_code != 200:
+            raise LookupError(f"{image}: manifest {r.status_code}")
+        m = r.json()
+        if "manifests" in m:  # index: pick linux/amd64
+            chosen = next((x for x in m["manifests"] if x.get("platform", {}).get("os") == "linux"
+                           and x.get("platform", {}).get("architecture") == "amd64"), m["manifests"][0])
+            r = self._get(f"{base}/manifests/{chosen['digest']}", {"Accept": MANIFEST_TYPES}, auth, state)
+            if r.status_code != 200:
+                raise LookupError(f"{image}: platform manifest {r.status_code}")
+            m = r.json()
+        r = self._get(f"{base}/blobs/{m['config']['digest']}", {}, auth, state)
+        if r.status_code != 200:
+            raise LookupError(f"{image}: config blob {r.status_code}")
+        c = r.json().get("config") or {}
+        cfg = ImageConfig(user=c.get("User") or None, entrypoint=c.get("Entrypoint"), cmd=c.get("Cmd"),
+                          env=c.get("Env") or [])
+        with self._lock:
+            self._cache[key] = (time.time(), cfg)
+        return cfg
+
+
+_client: Optional[RegistryClient] = None
+
+
+def get_image_config(image: str, username: Optional[str] = None, password: Optional[str] = None) -> ImageConfig:
+    global _client
+    if _client is None:
+        _client = RegistryClient()
+    return _client.get_image_config(image, username, password)

@@ -136,13 +136,25 @@ def get_job_specs_from_run_spec(run_spec: RunSpec, replica_num: int = 0,
         env[k] = it.interpolate(str(v), return_missing=True)[0]
     image = conf.image or get_default_image(conf)
     user = UnixUser.parse(conf.user) if conf.user else None
+    image_entrypoint = None
+    if conf.image and (not _shell_commands(conf) or user is None) and conf.entrypoint is None:
+        # a custom image without commands runs its own ENTRYPOINT + CMD; its USER is the default user
+        cfg = _image_config(conf)
+        if cfg is not None:
+            if not _shell_commands(conf):
+                image_entrypoint = (cfg.entrypoint or []) + (cfg.cmd or [])
+            if user is None and cfg.user:
+                try:
+                    user = UnixUser.parse(cfg.user)
+                except ValueError:
+                    user = None
     gpu_wanted = conf.resources.gpu is not None and (conf.resources.gpu.count.max or 0) > 0
     specs = []
     for job_num in range(nodes):
         job_name = f"{run_spec.run_name}-{job_num}-{replica_num}"
         specs.append(JobSpec(
             replica_num=replica_num, job_num=job_num, job_name=job_name, jobs_per_replica=nodes,
-            app_specs=_app_specs(conf), user=user, commands=_build_commands(conf), env=env,
+            app_specs=_app_specs(conf), user=user, commands=_build_commands(conf, image_entrypoint), env=env,
             home_dir=conf.home_dir, image_name=image, privileged=conf.privileged,
             single_branch=conf.single_branch if conf.single_branch is not None
             else not isinstance(conf, DevEnvironmentConfiguration),
@@ -153,6 +165,17 @@ def get_job_specs_from_run_spec(run_spec: RunSpec, replica_num: int = 0,
             gpu_probe=gpu_wanted and env.get("DSTACK_GPU_PROBE", "0") == "1",
         ))
     return specs
+
+
+def _image_config(conf):
+    """Registry lookup (cached 80 s); offline / private-without-creds images just skip it."""
+    from dstack_amd.server.services.docker import get_image_config
+
+    ra = conf.registry_auth
+    try:
+        return get_image_config(conf.image, ra.username if ra else None, ra.password if ra else None)
+    except Exception:  # noqa: BLE001 - network/registry errors must not block submission
+        return None
 
 
 def service_port(conf: ServiceConfiguration) -> int:

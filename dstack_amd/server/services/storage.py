@@ -1,8 +1,9 @@
 """Optional object storage for code blobs (reference: ``S/services/storage.py:13-74``, S3).
 
-``DSTACK_SERVER_S3_BUCKET`` would enable S3 in the reference; boto3 is not available in this
-image, so the MI355X build ships a filesystem store (``DSTACK_SERVER_CODE_STORE_DIR``) with the
-same interface; when neither is set, blobs stay in the database."""
+* ``DSTACK_SERVER_S3_BUCKET``: S3 over its REST API with SigV4 (no boto3), key
+  ``data/projects/{project}/codes/{repo_id}/{blob_hash}`` as in the reference;
+* ``DSTACK_SERVER_CODE_STORE_DIR``: the same layout on a (shared) filesystem;
+* neither: blobs stay in the database."""
 
 from __future__ import annotations
 
@@ -30,6 +31,46 @@ class FileStorage:
         return p.read_bytes() if p.exists() else b""
 
 
-def get_default_storage() -> Optional[FileStorage]:
+class S3Storage:
+    def __init__(self, bucket: str, region: Optional[str] = None, client=None, endpoint: Optional[str] = None):
+        import httpx
+
+        self.bucket = bucket
+        self.region = region or os.getenv("DSTACK_SERVER_S3_BUCKET_REGION") or os.getenv("AWS_REGION", "us-east-1")
+        self.endpoint = endpoint or f"https://{bucket}.s3.{self.region}.amazonaws.com"
+        self.http = client or httpx.Client(timeout=60)
+        self.access_key = os.getenv("AWS_ACCESS_KEY_ID", "")
+        self.secret_key = os.getenv("AWS_SECRET_ACCESS_KEY", "")
+        self.token = os.getenv("AWS_SESSION_TOKEN")
+
+    @staticmethod
+    def _key(project: str, repo_id: str, blob_hash: str) -> str:
+        return f"data/projects/{project}/codes/{repo_id}/{blob_hash}"
+
+    def _req(self, method: str, key: str, body: bytes = b""):
+        from dstack_amd.core.backends.clouds.common import sigv4_headers
+
+        url = f"{self.endpoint}/{key}"
+        h = sigv4_headers(method, url, self.region, "s3", self.access_key, self.secret_key, body, self.token)
+        return self.http.request(method, url, content=body or None, headers=h)
+
+    def upload_code(self, project: str, repo_id: str, blob_hash: str, blob: bytes):
+        r = self._req("PUT", self._key(project, repo_id, blob_hash), blob)
+        if r.status_code >= 300:
+            raise RuntimeError(f"S3 put failed: {r.status_code} {r.text[:200]}")
+
+    def get_code(self, project: str, repo_id: str, blob_hash: str) -> bytes:
+        r = self._req("GET", self._key(project, repo_id, blob_hash))
+        if r.status_code == 404:
+            return b""
+        if r.status_code >= 300:
+            raise RuntimeError(f"S3 get failed: {r.status_code} {r.text[:200]}")
+        return r.content
+
+
+def get_default_storage():
+    bucket = os.getenv("DSTACK_SERVER_S3_BUCKET")
+    if bucket:
+        return S3Storage(bucket)
     d = os.getenv("DSTACK_SERVER_CODE_STORE_DIR")
     return FileStorage(d) if d else None

@@ -336,3 +336,36 @@ def test_every_cloud_backend_plans_offers():
         c = cls({}, {}, _client(lambda req: httpx.Response(500)))
         assert isinstance(c.get_offers(None), list)
         assert re.match(r"^[a-z]+$", c.TYPE.value)
+
+
+# ---- Docker registry introspection -------------------------------------------------------------
+def test_registry_image_config_with_token_challenge():
+    from dstack_amd.server.services.docker import RegistryClient, parse_image_name
+
+    assert parse_image_name("ubuntu").repository == "library/ubuntu"
+    assert parse_image_name("rocm/pytorch:latest").reference == "latest"
+    r = parse_image_name("ghcr.io/org/img@sha256:abc")
+    assert (r.registry, r.repository, r.reference) == ("ghcr.io", "org/img", "sha256:abc")
+
+    def handler(req):
+        if req.url.host == "auth.docker.io":
+            assert req.url.params["scope"] == "repository:rocm/vllm:pull"
+            return httpx.Response(200, json={"token": "T"})
+        if req.headers.get("authorization") != "Bearer T":
+            return httpx.Response(401, headers={"www-authenticate": 'Bearer realm="https://auth.docker.io/token",'
+                                                                     'service="registry.docker.io",'
+                                                                     'scope="repository:rocm/vllm:pull"'})
+        if req.url.path.endswith("/manifests/latest"):
+            return httpx.Response(200, json={"manifests": [
+                {"digest": "sha256:arm", "platform": {"os": "linux", "architecture": "arm64"}},
+                {"digest": "sha256:amd", "platform": {"os": "linux", "architecture": "amd64"}}]})
+        if req.url.path.endswith("/manifests/sha256:amd"):
+            return httpx.Response(200, json={"config": {"digest": "sha256:cfg"}})
+        if req.url.path.endswith("/blobs/sha256:cfg"):
+            return httpx.Response(200, json={"config": {"User": "1000:1000", "Entrypoint": ["python3", "-m", "vllm"],
+                                                        "Cmd": ["serve"], "Env": ["PATH=/usr/bin"]}})
+        return httpx.Response(404)
+
+    rc = RegistryClient(_client(handler))
+    cfg = rc.get_image_config("rocm/vllm")
+    assert cfg.user == "1000:1000" and cfg.entrypoint == ["python3", "-m", "vllm"] and cfg.cmd == ["serve"]
