@@ -155,6 +155,17 @@ def register_routes(app: FastAPI):
     def healthcheck():
         return {"status": "running"}
 
+    from pathlib import Path
+
+    from fastapi.responses import HTMLResponse
+
+    ui_index = Path(__file__).parent / "ui" / "index.html"
+
+    @app.get("/", include_in_schema=False)
+    def ui():
+        """Web UI (single page over the REST API)."""
+        return HTMLResponse(ui_index.read_text() if ui_index.exists() else "<h3>dstack-amd</h3>")
+
     @app.get("/api/server/scheduler_stats")
     def scheduler_stats():
         from dstack_amd.server.background.scheduler import get_scheduler

@@ -222,3 +222,8 @@ def test_logs_poll_unknown_submission(client):
 @pytest.mark.parametrize("path", ["/api/project/nope/runs/get", "/api/project/nope/fleets/list"])
 def test_unknown_project(client, path):
     assert client.post(path, json={"run_name": "x"}).status_code in (403, 404, 400)
+
+
+def test_web_ui_served(client):
+    r = client.get("/")
+    assert r.status_code == 200 and "dstack-amd" in r.text and "/api/runs/list" in r.text
