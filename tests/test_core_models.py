@@ -230,3 +230,16 @@ def test_interpolator_missing_and_errors():
         _interp().interpolate("${{ run.args ")
     with pytest.raises(InterpolatorError):
         _interp().interpolate("${{ run.ar-gs }}")
+
+
+def _own_examples():
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples")
+    return sorted(os.path.join(d, f) for d, _, fs in os.walk(root) for f in fs if f.endswith(".dstack.yml"))
+
+
+@pytest.mark.parametrize("path", _own_examples())
+def test_own_example_configurations(path):
+    with open(path) as f:
+        data = yaml.safe_load(f)
+    conf = parse_apply_configuration(data)
+    assert conf.type == data["type"]
