@@ -1,0 +1,186 @@
+// Unit tests for the native agents (reference analogue: runner/internal/**/*_test.go).
+// Build + run: make -C native test
+#include <unistd.h>
+
+#include <cstdio>
+#include <functional>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../common/amdgpu.h"
+#include "../common/json.h"
+#include "../common/net.h"
+#include "../runner/executor.h"
+#include "../shim/shim.h"
+
+using namespace dsa;
+
+static int g_failed = 0, g_run = 0;
+#define CHECK(cond)                                                          \
+  do {                                                                       \
+    if (!(cond)) {                                                           \
+      fprintf(stderr, "  FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond);     \
+      ++g_failed;                                                            \
+    }                                                                        \
+  } while (0)
+
+static void run(const char* name, const std::function<void()>& fn) {
+  int before = g_failed;
+  ++g_run;
+  fn();
+  fprintf(stderr, "%s %s\n", g_failed == before ? "ok  " : "FAIL", name);
+}
+
+int main() {
+  set_log_level(0);
+
+  run("json roundtrip", [] {
+    Json j = Json::parse(R"({"a":1,"b":[true,null,"x\né"],"c":{"d":-2.5e3}})");
+    CHECK(j["a"].as_int() == 1);
+    CHECK(j["b"][(size_t)0].as_bool());
+    CHECK(j["b"][(size_t)2].str() == "x\n\xc3\xa9");
+    CHECK(j["c"]["d"].as_double() == -2500.0);
+    Json k = Json::parse(j.dump());
+    CHECK(k.dump() == j.dump());
+    bool threw = false;
+    try {
+      Json::parse("{\"a\":");
+    } catch (const std::exception&) {
+      threw = true;
+    }
+    CHECK(threw);
+  });
+
+  run("base64", [] {
+    for (std::string s : {std::string(""), std::string("f"), std::string("fo"), std::string("foo"),
+                          std::string("\x00\xff\x10 binary", 10)})
+      CHECK(base64_decode(base64_encode(s)) == s);
+    CHECK(base64_encode("hello") == "aGVsbG8=");
+  });
+
+  run("log history: strictly increasing timestamps + after()", [] {
+    LogHistory h;
+    for (int i = 0; i < 5000; ++i) h.append("line " + std::to_string(i) + "\n");
+    auto all = h.after(0);
+    CHECK(all.size() == 5000);
+    bool increasing = true;
+    for (size_t i = 1; i < all.size(); ++i) increasing &= all[i].timestamp > all[i - 1].timestamp;
+    CHECK(increasing);
+    auto tail = h.after(all[4000].timestamp);
+    CHECK(tail.size() == 999);
+    CHECK(tail.front().message == "line 4001\n");
+    CHECK(h.after(all.back().timestamp).empty());
+  });
+
+  run("log history: wait_after wakes on append", [] {
+    LogHistory h;
+    int64_t t0 = h.last_timestamp();
+    std::thread w([&] {
+      usleep(20000);
+      h.append("x");
+    });
+    CHECK(h.wait_after(t0, 2000));
+    w.join();
+  });
+
+  run("env interpolation", [] {
+    std::vector<std::pair<std::string, std::string>> env = {{"A", "1"}, {"B", "two"}};
+    std::string err;
+    CHECK(interpolate_env("x${A}y${B}", env, &err) == "x1ytwo");
+    CHECK(interpolate_env("$${A}", env, &err) == "${A}");
+    CHECK(interpolate_env("plain $A", env, &err) == "plain $A");
+    err.clear();
+    CHECK(interpolate_env("[${MISSING}]", env, &err) == "[]");  // unset -> empty, as in a shell
+    CHECK(err.empty());
+    interpolate_env("${UNTERMINATED", env, &err);
+    CHECK(!err.empty());
+  });
+
+  run("task status transitions", [] {
+    CHECK(task_transition_allowed(TaskStatus::Pending, TaskStatus::Preparing));
+    CHECK(task_transition_allowed(TaskStatus::Running, TaskStatus::Terminated));
+    CHECK(!task_transition_allowed(TaskStatus::Terminated, TaskStatus::Running));
+    TaskStorage st;
+    Task t;
+    t.config.id = "t1";
+    CHECK(st.add(t));
+    CHECK(!st.add(t));  // duplicate id
+    CHECK(st.set_status("t1", TaskStatus::Preparing));
+    CHECK(!st.set_status("t1", TaskStatus::Pending));  // backwards
+    Task out;
+    CHECK(st.get("t1", out) && out.status == TaskStatus::Preparing);
+    CHECK(st.remove("t1") && !st.get("t1", out));
+  });
+
+  // 8 GPUs in two fully connected quads {0-3} {4-7} joined by one link pair (2<->6)
+  std::vector<std::vector<int>> xgmi(8, std::vector<int>(8, 0));
+  for (int a = 0; a < 8; ++a)
+    for (int b = 0; b < 8; ++b)
+      if (a != b && (a / 4) == (b / 4)) xgmi[a][b] = 1;
+  xgmi[2][6] = xgmi[6][2] = 1;
+  std::vector<int> numa = {0, 0, 0, 0, 1, 1, 1, 1};
+
+  run("xGMI placement prefers a fully connected set", [&] {
+    auto g = pick_gpus_xgmi({0, 1, 2, 3, 4, 5, 6, 7}, 4, xgmi, numa);
+    CHECK(g.size() == 4);
+    std::set<int> s(g.begin(), g.end());
+    bool quad = s == std::set<int>{0, 1, 2, 3} || s == std::set<int>{4, 5, 6, 7};
+    CHECK(quad);
+    auto h = pick_gpus_xgmi({1, 2, 4, 5, 6}, 2, xgmi, numa);
+    CHECK(h.size() == 2 && xgmi[h[0]][h[1]] == 1);
+    CHECK(pick_gpus_xgmi({0, 1}, 3, xgmi, numa).empty());
+  });
+
+  run("gpu lock acquire/release/lock", [&] {
+    GpuLock gl;
+    gl.init(8, xgmi, numa);
+    auto a = gl.acquire(4);
+    CHECK(a.size() == 4 && gl.free_count() == 4);
+    auto b = gl.acquire(4);
+    CHECK(b.size() == 4 && gl.free_count() == 0);
+    CHECK(gl.acquire(1).empty());
+    gl.release(a);
+    CHECK(gl.free_count() == 4);
+    CHECK(!gl.lock({b[0]}));  // already busy
+    CHECK(gl.lock(a));
+    gl.release(a);
+    gl.release(b);
+    CHECK(gl.acquire(-1).size() == 8);
+  });
+
+  run("amd catalog names", [] {
+    CHECK(amd_catalog_name("AMD Instinct MI355 OAM") == "MI355X");
+    CHECK(amd_catalog_name("AMD Instinct MI300X OAM") == "MI300X");
+    CHECK(amd_catalog_name("AMD Instinct MI325X") == "MI325X");
+  });
+
+  run("http server + client roundtrip", [] {
+    HttpServer srv("127.0.0.1", 0);
+    srv.route("POST", "/echo/{name}", [](HttpRequest& r) {
+      Json j = Json::object();
+      j.set("name", r.params["name"]);
+      j.set("body", r.body);
+      return HttpResponse::json(j);
+    });
+    CHECK(srv.start() > 0);
+    std::thread th([&] { srv.serve_forever(); });
+    HttpClientRequest req;
+    req.method = "POST";
+    req.port = srv.port();
+    req.path = "/echo/abc";
+    req.body = "payload";
+    auto resp = http_request(req);
+    CHECK(resp.ok());
+    Json j = Json::parse(resp.body);
+    CHECK(j["name"].str() == "abc" && j["body"].str() == "payload");
+    req.path = "/missing";
+    CHECK(http_request(req).status == 404);
+    srv.stop();
+    th.join();
+  });
+
+  fprintf(stderr, "%d/%d test groups passed\n", g_run - (g_failed ? 1 : 0), g_run);
+  return g_failed ? 1 : 0;
+}

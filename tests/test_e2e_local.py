@@ -196,3 +196,10 @@ def test_service_through_local_gateway(tmp_path):
         run.wait(timeout=60)
         c.api.gateways.delete("main", ["gw"])
         assert body is not None and "Directory listing" in body
+
+
+def test_native_unit_tests():
+    """C++ unit tests of the agents (JSON, log history, xGMI placement, GPU lock, HTTP)."""
+    r = subprocess.run(["make", "-C", os.path.join(REPO, "native"), "test"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
