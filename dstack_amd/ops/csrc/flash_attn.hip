@@ -43,6 +43,10 @@ __device__ __forceinline__ int swz(int row, int ch) {
   return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
+// v_exp_f32 directly: exp2f() adds a denormal range-reduction (cmp/cndmask/add/ldexp) around it;
+// softmax probabilities below 2^-126 are irrelevant, so the bare instruction is exact enough
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -156,37 +160,43 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16_t* __restrict
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) st[t] = mfma(lds_row(kl, 32 * t + l32, 2 * ks + hf), qf[ks], st[t]);
       }
+      // only the tile(s) crossing this wave's diagonal need the causal mask (wave-uniform test)
+      if (CAUSAL && kv0 + 63 > qw0) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            if (key > myq) st[t][r] = -INFINITY;
+          }
+      }
+      // max on the raw scores (scale > 0 commutes with max); p = 2^(s*scale - m) as one fma + exp
       float mx = -INFINITY;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float s = st[t][r] * scale_log2;
-          if (CAUSAL) {
-            const int key = kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hf;
-            if (key > myq) s = -INFINITY;
-          }
-          st[t][r] = s;
-          mx = fmaxf(mx, s);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[t][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
       const float mn = fmaxf(m, mx);
-      const float alpha = exp2f(m - mn);
+      const float alpha = fexp2(m - mn);
       m = mn;
       float ps = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(st[t][r] - mn);
+          const float p = fexp2(fmaf(st[t][r], scale_log2, -mn));
           st[t][r] = p;
           ps += p;
         }
       lsum = lsum * alpha + ps;
+      // rescale O only when some lane's running max moved (after the first tiles it rarely does)
+      if (__any(alpha != 1.f)) {
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
+        for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      }
       bf16x8 pb[4];
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) pb[s4] = to_bf16x8(st[s4 >> 1], 8 * (s4 & 1));
@@ -322,6 +332,7 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
         dpv = mfma(lds_row(dol, 32 * qs + l32, 2 * ks + hf), vf[ks], dpv);
       }
       // rows of s/dpv: q = qlo + (r&3) + 8*(r>>2) + 4*hf ; column (lane) = mykey
+      const bool diag = CAUSAL && qlo < kw0 + 31;  // sub-tile straddles this wave's keys
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int qi = 32 * qs + 8 * rr + 4 * hf;
@@ -330,8 +341,8 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * rr + i;
-          float p = exp2f(s[r] * scale_log2 - L[i]);
-          if (CAUSAL && mykey > qt * 64 + qi + i) p = 0.f;
+          float p = fexp2(fmaf(s[r], scale_log2, -L[i]));
+          if (diag && mykey > qt * 64 + qi + i) p = 0.f;
           s[r] = p;
           dpv[r] = p * (dpv[r] - Dl[i]);
         }
@@ -469,12 +480,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(const bf16_t* __restr
           dpt[t] = mfma(lds_row(vl, 32 * t + l32, 2 * ks + hf), df[ks], dpt[t]);
         }
       }
+      const bool diag = CAUSAL && kv0 + 63 > qw0;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(st[t][r] * scale_log2 - L);
-          if (CAUSAL) {
+          float p = fexp2(fmaf(st[t][r], scale_log2, -L));
+          if (diag) {
             const int key = kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hf;
             if (key > myq) p = 0.f;
           }
