@@ -113,6 +113,9 @@ class Llama(nn.Module):
         self.norm = nn.Parameter(torch.ones(cfg.dim))
         self.lm_head = nn.Parameter(torch.empty(cfg.vocab_size, cfg.dim))
         self._rope_cache: dict = {}
+        # set by ZeroOptimizer.install_prefetch_hooks: blocks until the all-gather of the given
+        # (updated) parameters has landed, so embedding/head wait only when they are used
+        self.param_waiter = None
 
     @torch.no_grad()
     def init_weights(self, std: float = 0.02, seed: int = 0):
@@ -136,10 +139,14 @@ class Llama(nn.Module):
         """Returns logits [B*S, V] (bf16 when the weights are bf16)."""
         b, s = tokens.shape
         cos, sin = self.rope_tables(s, tokens.device)
+        if self.param_waiter is not None:
+            self.param_waiter([self.embed])
         x = torch.nn.functional.embedding(tokens, self.embed)
         delta = None
         for layer in self.layers:
             x, delta = layer(x, delta, cos, sin)
+        if self.param_waiter is not None:
+            self.param_waiter([self.norm, self.lm_head])
         _, h = ops.add_rms_norm(x, delta, self.norm, self.cfg.norm_eps)
         return ops.linear(h.reshape(b * s, -1), self.lm_head)
 

@@ -42,6 +42,7 @@ class Bucket:
     params: list = field(default_factory=list)
     pending: int = 0
     work: object = None
+    ag_work: object = None
 
     def shard_range(self, rank: int, world: int):
         n = self.numel // world
@@ -132,6 +133,7 @@ class ZeroOptimizer:
             if self.overlap:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self._direct_ok = set()
+        self._prefetch = False
         self._arm()
 
     # ------------------------------------------------------------------------------------------
@@ -190,6 +192,7 @@ class ZeroOptimizer:
     @torch.no_grad()
     def step(self):
         self.step_count += 1
+        self.wait_params()  # no forward ran since the last step: finish its all-gathers first
         if self.world > 1:
             for b in self.buckets:
                 if b.work is None:  # not overlapped (or a param received no grad)
@@ -213,19 +216,49 @@ class ZeroOptimizer:
                 grad_scale=1.0 / self.world,  # the 1/world of the average is fused into AdamW
             )
         if self.world > 1:
-            works = []
-            for b in self.buckets:
+            # gather the updated shards in forward order (buckets are stored in backward order);
+            # with prefetch hooks installed the next forward waits per bucket, so the all-gather
+            # of later layers overlaps the compute of earlier ones
+            for b in reversed(self.buckets):
                 s, n = b.shard_range(self.rank, self.world)
                 full = self.flat_param[b.start : b.start + b.numel]
                 if self._backend == "gloo":
                     chunks = list(full.chunk(self.world))
-                    works.append(dist.all_gather(chunks, chunks[self.rank].clone(), group=self.group, async_op=True))
+                    b.ag_work = dist.all_gather(chunks, chunks[self.rank].clone(), group=self.group, async_op=True)
                     continue
                 # in place: sendbuff == recvbuff + rank * sendcount
-                works.append(dist.all_gather_into_tensor(full, self.flat_param[s : s + n], group=self.group,
-                                                         async_op=True))
-            for w in works:
-                w.wait()
+                b.ag_work = dist.all_gather_into_tensor(full, self.flat_param[s : s + n], group=self.group,
+                                                        async_op=True)
+            if not self._prefetch:
+                self.wait_params()
+
+    def wait_params(self, buckets=None):
+        """Block until the all-gathered parameters of ``buckets`` (default: all) have landed."""
+        for b in buckets if buckets is not None else self.buckets:
+            if b.ag_work is not None:
+                b.ag_work.wait()
+                b.ag_work = None
+
+    def install_prefetch_hooks(self, model: nn.Module):
+        """Overlap the parameter all-gather with the next forward: each module waits only for
+        the buckets holding its own parameters (forward pre-hook); anything not covered by a
+        hook is waited for before backward / the next optimizer step."""
+        if self.world == 1:
+            return
+        self._prefetch = True
+        for mod in model.modules():
+            if hasattr(mod, "param_waiter"):
+                # the module waits itself, right before each of its parameters is used
+                mod.param_waiter = lambda params: self.wait_params(self._buckets_of(params))
+                continue
+            own = [p for p in mod.parameters(recurse=False) if p.requires_grad]
+            if not own:
+                continue
+            buckets = self._buckets_of(own)
+            self._hooks.append(mod.register_forward_pre_hook(lambda m, a, _b=buckets: self.wait_params(_b)))
+
+    def _buckets_of(self, params):
+        return [self.buckets[i] for i in sorted({self._bucket_of[p].index for p in params})]
 
     def state_bytes(self) -> int:
         return sum(t.numel() * 4 for t in self.master + self.exp_avg + self.exp_avg_sq)

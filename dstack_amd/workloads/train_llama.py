@@ -67,6 +67,7 @@ class Trainer:
         model.init_weights(seed=seed)
         self.model = model
         self.opt = ZeroOptimizer(model, lr=lr, bucket_numel=bucket_numel)
+        self.opt.install_prefetch_hooks(model)
         rank = dist.get_rank() if dist.is_initialized() else 0
         g = torch.Generator(device=device).manual_seed(1234 + rank)
         n = micro_batch * (seq_len + 1)

@@ -55,8 +55,10 @@ def _reference_steps(model, steps_batches, grad_accum):
     return model
 
 
-def _zero_steps(model, steps_batches, grad_accum, bucket_numel=1 << 20, eps=EPS):
+def _zero_steps(model, steps_batches, grad_accum, bucket_numel=1 << 20, eps=EPS, prefetch=False):
     opt = ZeroOptimizer(model, lr=LR, betas=BETAS, eps=eps, weight_decay=WD, bucket_numel=bucket_numel)
+    if prefetch:
+        opt.install_prefetch_hooks(model)
     for micro in steps_batches:
         opt.zero_grad()
         for i, b in enumerate(micro):
@@ -64,6 +66,7 @@ def _zero_steps(model, steps_batches, grad_accum, bucket_numel=1 << 20, eps=EPS)
             loss = model.loss(b[:, :-1], b[:, 1:])
             (loss / grad_accum).backward()
         opt.step()
+    opt.wait_params()  # prefetch mode leaves the last all-gather in flight for the next forward
     return model, opt
 
 
@@ -88,7 +91,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, prefetch=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(2)
@@ -96,14 +99,16 @@ def _worker(rank, world, port, out_dir):
     steps = [_batches(2, 2 * world, seed=s) for s in range(2)]
     # each rank takes its slice of every micro-batch
     mine = [[b[rank * 2:(rank + 1) * 2] for b in micro] for micro in steps]
-    model, _ = _zero_steps(base, mine, grad_accum=2, bucket_numel=1 << 19, eps=EPS_DIST)
+    model, _ = _zero_steps(base, mine, grad_accum=2, bucket_numel=1 << 19, eps=EPS_DIST, prefetch=prefetch)
     torch.save({k: v.detach() for k, v in model.state_dict().items()}, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.destroy_process_group()
 
 
-def test_zero_gloo_world2_matches_single_process(tmp_path):
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_zero_gloo_world2_matches_single_process(tmp_path, prefetch):
     world = 2
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), prefetch), nprocs=world,
+                       start_method="spawn")
     states = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     # every rank ends with identical parameters (all-gather of the updated shards)
     for k in states[0]:
