@@ -100,8 +100,9 @@ def deploy_ssh_instance(rci: RemoteConnectionInfo, project_public_key: str, priv
                 raise ProvisioningError(f"copy {name} failed: {cp.stderr.decode(errors='ignore')}")
             pool.run(target, private_key, f"mv -f {REMOTE_SHIM_DIR}/{name}.new {REMOTE_SHIM_DIR}/{name} && "
                                           f"chmod +x {REMOTE_SHIM_DIR}/{name}")
-    env_lines = "\n".join(f"{k}={v}" for k, v in rci.env.items()) if len(rci.env) else ""
-    env_lines += f"\nDSTACK_SHIM_HTTP_PORT={DSTACK_SHIM_HTTP_PORT}\n"
+    env = dict(rci.env.items()) if len(rci.env) else {}
+    env.setdefault("DSTACK_SHIM_HTTP_PORT", str(DSTACK_SHIM_HTTP_PORT))
+    env_lines = "".join(f"{k}={v}\n" for k, v in env.items())
     pool.run(target, private_key, f"cat > {REMOTE_SHIM_DIR}/shim.env", input=env_lines.encode())
     probe_flag = f"--probe-binary $HOME/.dstack-shim/dstack-probe" if probe else ""
     if has_systemd and rci.ssh_user == "root":
@@ -110,10 +111,13 @@ def deploy_ssh_instance(rci: RemoteConnectionInfo, project_public_key: str, priv
         pool.run(target, private_key, "systemctl daemon-reload && systemctl enable dstack-shim && "
                                       "systemctl restart dstack-shim")
     else:
+        # restart the previous shim by its pid file (never by process name: other users' or
+        # other installations' agents may run on the same host)
         pool.run(target, private_key,
-                 f"cd {REMOTE_SHIM_DIR} && (pkill -x dstack-shim || true) && set -a && . ./shim.env && set +a && "
-                 f"nohup ./dstack-shim --service --shim-home $HOME/.dstack-shim --runner-binary-path "
-                 f"$HOME/.dstack-shim/dstack-runner {probe_flag} > shim.log 2>&1 < /dev/null &")
+                 f"cd {REMOTE_SHIM_DIR} && rm -f host_info.json && "
+                 f"([ -f shim.pid ] && kill $(cat shim.pid) 2>/dev/null; true) && set -a && . ./shim.env && set +a && "
+                 f"(nohup ./dstack-shim --service --shim-home $HOME/.dstack-shim --runner-binary-path "
+                 f"$HOME/.dstack-shim/dstack-runner {probe_flag} > shim.log 2>&1 < /dev/null & echo $! > shim.pid)")
     deadline = time.monotonic() + min(timeout, 180)
     host_info = None
     while time.monotonic() < deadline:  # poll host_info.json (provisioning.py:175-202)

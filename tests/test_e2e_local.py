@@ -203,3 +203,57 @@ def test_native_unit_tests():
     r = subprocess.run(["make", "-C", os.path.join(REPO, "native"), "test"], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+class _LocalPool:
+    """Stands in for the SSH TunnelPool: runs the deploy commands on this host under a temp HOME."""
+
+    def __init__(self, home):
+        self.home = home
+
+    def run(self, target, private_key, command, timeout=600, input=None):
+        env = dict(os.environ, HOME=str(self.home))
+        return subprocess.run(["bash", "-c", command], env=env, input=input, capture_output=True, timeout=timeout)
+
+    def copy(self, target, private_key, local_path, remote_path, timeout=600):
+        import shutil
+
+        dst = os.path.join(self.home, remote_path)
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
+        shutil.copy(local_path, dst)
+        return subprocess.CompletedProcess([], 0, b"", b"")
+
+
+def test_ssh_fleet_deploy_flow(tmp_path, monkeypatch):
+    """deploy_ssh_instance end to end minus the ssh transport: agents copied, shim.env written,
+    shim started (pid file), host_info read back and turned into an instance type."""
+    import signal
+
+    from dstack_amd.core.backends import remote
+    from dstack_amd.core.models.instances import RemoteConnectionInfo, SSHKey
+    from dstack_amd.server.testing import free_port
+
+    home = tmp_path / "home"
+    home.mkdir()
+    monkeypatch.setattr(remote, "get_tunnel_pool", lambda: _LocalPool(home))
+    port = free_port()
+    rci = RemoteConnectionInfo(host="10.0.0.5", port=22, ssh_user="ubuntu",
+                               ssh_keys=[SSHKey(public="ssh-ed25519 AAAA k")],
+                               env={"DSTACK_SHIM_HTTP_PORT": str(port)})
+    try:
+        info = remote.deploy_ssh_instance(rci, "ssh-ed25519 AAAA project", "unused-private-key", timeout=60)
+        shim_dir = home / ".dstack-shim"
+        assert (shim_dir / "dstack-shim").exists() and (shim_dir / "dstack-runner").exists()
+        assert f"DSTACK_SHIM_HTTP_PORT={port}" in (shim_dir / "shim.env").read_text()
+        assert "ssh-ed25519 AAAA project" in (home / ".ssh" / "authorized_keys").read_text()
+        itype, topo = remote.host_info_to_instance_type(info)
+        assert itype.resources.cpus >= 1 and itype.resources.memory_mib > 0
+        r = httpx.get(f"http://127.0.0.1:{port}/api/healthcheck", timeout=5)
+        assert r.json()["service"] == "dstack-shim"
+    finally:
+        pid_file = home / ".dstack-shim" / "shim.pid"
+        if pid_file.exists():
+            try:
+                os.kill(int(pid_file.read_text().strip()), signal.SIGTERM)
+            except (ProcessLookupError, ValueError):
+                pass
