@@ -21,6 +21,8 @@
 //    q-major pass instead of cross-workgroup atomics (deterministic, no atomic-rate floor).
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace dsa;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -258,14 +260,16 @@ __global__ __launch_bounds__(256) void fa_bwd_delta_kernel(const bf16_t* __restr
 // Loops over 64-row q tiles from the diagonal to S; writes fp32 per-q-head partials
 // dkp/dvp [B, S, H, 128] that fa_bwd_reduce_kv sums over the GQA group.
 // ================================================================================================
-template <bool CAUSAL>
+template <bool CAUSAL, int NQS>
 __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
     int H, int KVH, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // per stage: Q tile (16K) | dO tile (16K) | lse (256 B) | delta (256 B)
-  constexpr int STAGE = 2 * TILE_BYTES + 512;
+  // a stage holds QT = 32*NQS query rows: Q (QT x 256 B) | dO (QT x 256 B) | lse (QT x 4) | delta
+  constexpr int QT = 32 * NQS;
+  constexpr int QB = QT * 256;
+  constexpr int STAGE = 2 * QB + 8 * QT;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
   const int NH = H + 2 * KVH;
   const long rs = (long)NH * HD;
@@ -298,13 +302,16 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
       dv[d][r] = 0.f;
     }
 
-  const int qt_begin = CAUSAL ? kb0 / 64 : 0;
-  const int nqt = S / 64;
+  const int qt_begin = CAUSAL ? kb0 / QT : 0;
+  const int nqt = S / QT;
   auto issue = [&](int qt, char* st) {
-    dma_tile64(qp + (long)qt * 64 * rs, rs, st, w, lane);
-    dma_tile64(dop + (long)qt * 64 * ors, ors, st + TILE_BYTES, w, lane);
-    if (w == 0) dma_f32x64(lp + qt * 64, st + 2 * TILE_BYTES, lane);
-    if (w == 1) dma_f32x64(dp + qt * 64, st + 2 * TILE_BYTES + 256, lane);
+#pragma unroll
+    for (int h64 = 0; h64 < QT / 64; ++h64) {
+      dma_tile64(qp + ((long)qt * QT + 64 * h64) * rs, rs, st + h64 * TILE_BYTES, w, lane);
+      dma_tile64(dop + ((long)qt * QT + 64 * h64) * ors, ors, st + QB + h64 * TILE_BYTES, w, lane);
+      if (w == 0) dma_f32x64(lp + qt * QT + 64 * h64, st + 2 * QB + 256 * h64, lane);
+      if (w == 1) dma_f32x64(dp + qt * QT + 64 * h64, st + 2 * QB + 4 * QT + 256 * h64, lane);
+    }
   };
   issue(qt_begin, smem);
   wait_dma_and_barrier();
@@ -312,17 +319,21 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
   for (int qt = qt_begin; qt < nqt; ++qt) {
     const int stage = (qt - qt_begin) & 1;
     const char* ql = smem + stage * STAGE;
-    const char* dol = ql + TILE_BYTES;
-    const float* ll = reinterpret_cast<const float*>(ql + 2 * TILE_BYTES);
-    const float* dl = ll + 64;
+    const char* dol = ql + QB;
+    const float* ll = reinterpret_cast<const float*>(ql + 2 * QB);
+    const float* dl = ll + QT;
     if (qt + 1 < nqt) issue(qt + 1, smem + (stage ^ 1) * STAGE);
-    // Both 32-query sub-tiles as straight-line code (no per-sub-tile branch): the scheduler can
-    // overlap one sub-tile's exp/VALU work with the other's MFMAs.  A wave skips a whole tile only
+    // Pairs of 32-query sub-tiles as straight-line code (no per-sub-tile branch): the scheduler
+    // can overlap one sub-tile's exp/VALU work with the other's MFMAs.  A wave skips a pair only
     // when every query precedes its keys; partially visible sub-tiles are masked (p = 0).
-    if (!CAUSAL || qt * 64 + 63 >= kw0) {
+#pragma unroll
+    for (int pr = 0; pr < NQS / 2; ++pr) {
+      const int q0p = qt * QT + 64 * pr;  // first query of the pair
+      if (CAUSAL && q0p + 63 < kw0) continue;
       f32x16 s[2], dpv[2];
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
+        const int row = 64 * pr + 32 * qs + l32;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           s[qs][r] = 0.f;
@@ -330,27 +341,27 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
         }
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
-          s[qs] = mfma(lds_row(ql, 32 * qs + l32, 2 * ks + hf), kf[ks], s[qs]);
-          dpv[qs] = mfma(lds_row(dol, 32 * qs + l32, 2 * ks + hf), vf[ks], dpv[qs]);
+          s[qs] = mfma(lds_row(ql, row, 2 * ks + hf), kf[ks], s[qs]);
+          dpv[qs] = mfma(lds_row(dol, row, 2 * ks + hf), vf[ks], dpv[qs]);
         }
       }
       bf16x8 pb[2][2], dsb[2][2];
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
-        // rows of s/dpv: q = qt*64 + 32*qs + (r&3) + 8*(r>>2) + 4*hf ; column (lane) = mykey
-        const bool diag = CAUSAL && qt * 64 + 32 * qs < kw0 + 31;
+        // rows of s/dpv: q = q0p + 32*qs + (r&3) + 8*(r>>2) + 4*hf ; column (lane) = mykey
+        const bool diag = CAUSAL && q0p + 32 * qs < kw0 + 31;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int qi = 32 * qs + 8 * rr + 4 * hf;
+          const int qi = 64 * pr + 32 * qs + 8 * rr + 4 * hf;
           const f4 L = *reinterpret_cast<const f4*>(ll + qi);
           const f4 Dl = *reinterpret_cast<const f4*>(dl + qi);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int r = 4 * rr + i;
-            float pr = fexp2(fmaf(s[qs][r], scale_log2, -L[i]));
-            if (diag && mykey > qt * 64 + qi + i) pr = 0.f;
-            s[qs][r] = pr;
-            dpv[qs][r] = pr * (dpv[qs][r] - Dl[i]);
+            float pv = fexp2(fmaf(s[qs][r], scale_log2, -L[i]));
+            if (diag && mykey > qt * QT + qi + i) pv = 0.f;
+            s[qs][r] = pv;
+            dpv[qs][r] = pv * (dpv[qs][r] - Dl[i]);
           }
         }
 #pragma unroll
@@ -365,8 +376,9 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
         for (int d = 0; d < 4; ++d)
 #pragma unroll
           for (int k2 = 0; k2 < 2; ++k2) {
-            dv[d] = mfma(lds_tr(dol, 32 * qs + 16 * k2, 32 * d, lane), pb[qs][k2], dv[d]);
-            dk[d] = mfma(lds_tr(ql, 32 * qs + 16 * k2, 32 * d, lane), dsb[qs][k2], dk[d]);
+            const int r0 = 64 * pr + 32 * qs + 16 * k2;
+            dv[d] = mfma(lds_tr(dol, r0, 32 * d, lane), pb[qs][k2], dv[d]);
+            dk[d] = mfma(lds_tr(ql, r0, 32 * d, lane), dsb[qs][k2], dk[d]);
           }
     }
     wait_dma_and_barrier();
@@ -559,21 +571,29 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
                                                                delta, B, S, H);
   DSA_CHECK(hipGetLastError());
   const int grid = B * H * (S / 128);
-  const size_t lds_kv = 2 * (2 * TILE_BYTES + 512);
+  // dK/dV q-tile per pipeline stage: 64 rows (default) or 128 (DSTACK_AMD_FA_DKDV_QT=128: half
+  // the barriers, 130 KiB of LDS)
+  static const int dkdv_qt = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DKDV_QT");
+    return (v && atoi(v) == 128) ? 128 : 64;
+  }();
+  const size_t lds_kv = 2 * (2 * (size_t)dkdv_qt * 256 + 8 * (size_t)dkdv_qt);
   const size_t lds_q = 4 * TILE_BYTES;
+#define DSA_DKDV(C, N)                                                                               \
+  fa_bwd_dkdv_kernel<C, N><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, \
+                                                      delta, dkp, dvp, B, S, H, KVH, sl2)
   if (causal) {
-    fa_bwd_dkdv_kernel<true><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
-                                                        delta, dkp, dvp, B, S, H, KVH, sl2);
+    if (dkdv_qt == 128) DSA_DKDV(true, 4); else DSA_DKDV(true, 2);
     DSA_CHECK(hipGetLastError());
     fa_bwd_dq_kernel<true><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta,
                                                      (bf16_t*)dqkv, B, S, H, KVH, sl2);
   } else {
-    fa_bwd_dkdv_kernel<false><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
-                                                         delta, dkp, dvp, B, S, H, KVH, sl2);
+    if (dkdv_qt == 128) DSA_DKDV(false, 4); else DSA_DKDV(false, 2);
     DSA_CHECK(hipGetLastError());
     fa_bwd_dq_kernel<false><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
                                                       delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
   }
+#undef DSA_DKDV
   DSA_CHECK(hipGetLastError());
   const long work = (long)B * S * KVH * (HD / 8);
   int g = (int)((work + 255) / 256);
