@@ -43,6 +43,7 @@ class Bucket:
     pending: int = 0
     work: object = None
     ag_work: object = None
+    updated: bool = False  # AdamW already ran for this step (optimizer-in-backward)
 
     def shard_range(self, rank: int, world: int):
         n = self.numel // world
@@ -60,6 +61,7 @@ class ZeroOptimizer:
         bucket_numel: int = 256 * 1024 * 1024,
         group: dist.ProcessGroup | None = None,
         overlap: bool = True,
+        overlap_update: bool = True,
     ):
         self.model = model
         self.lr = lr
@@ -72,6 +74,9 @@ class ZeroOptimizer:
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.overlap = overlap and self.world > 1
         self.step_count = 0
+        # optimizer-in-backward: a bucket whose final gradients are complete is reduce-scattered,
+        # updated (AdamW on its shard) and all-gathered on a side stream while backward keeps
+        # computing earlier layers (HBM-bound AdamW beside MFMA-bound GEMMs)
         self.sync_grads = True  # False while accumulating non-final micro-batches
 
         params = [p for p in model.parameters() if p.requires_grad]
@@ -124,13 +129,17 @@ class ZeroOptimizer:
             if used < b.numel:
                 self._pads.append((b.start + used, b.numel - used))
         self._backend = dist.get_backend(group) if self.distributed else None
+        self._side = None
+        if overlap_update and device.type == "cuda":
+            self._side = torch.cuda.Stream(device=device)
+        self._hooks_on = self.overlap or self._side is not None
         self._hooks = []
         for p in params:
             if p.dim() == 2:
                 # GEMM-produced weight gradients are written straight into flat_grad (ops.linear)
                 p._dsa_grad_sink = self._direct_grad
                 p._dsa_fresh = True
-            if self.overlap:
+            if self._hooks_on:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self._direct_ok = set()
         self._prefetch = False
@@ -141,6 +150,7 @@ class ZeroOptimizer:
         for b in self.buckets:
             b.pending = len(b.params)
             b.work = None
+            b.updated = False
 
     def _direct_grad(self, p: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
         """Weight gradient sink for ``ops.linear``: dW = g^T x into the flat buffer."""
@@ -150,7 +160,7 @@ class ZeroOptimizer:
         else:
             p.grad.addmm_(g2.t(), x2)
         self._direct_ok.add(p)
-        if self.overlap:
+        if self._hooks_on:
             self._on_grad_ready(p)
 
     def _on_grad_ready(self, p: torch.Tensor):
@@ -159,7 +169,45 @@ class ZeroOptimizer:
         b = self._bucket_of[p]
         b.pending -= 1
         if b.pending == 0:
-            self._reduce_bucket(b, async_op=True)
+            if self.overlap:
+                self._reduce_bucket(b, async_op=True)
+            if self._side is not None:
+                self._update_bucket_async(b)
+
+    def _adamw(self, b: Bucket, step: int):
+        s, n = b.shard_range(self.rank, self.world)
+        i = b.index
+        ops.adamw_(self.flat_param[s : s + n], self.flat_grad[s : s + n], self.master[i], self.exp_avg[i],
+                   self.exp_avg_sq[i], lr=self.lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
+                   weight_decay=self.weight_decay, step=step,
+                   grad_scale=1.0 / self.world)  # the 1/world of the average is fused into AdamW
+
+    def _all_gather(self, b: Bucket):
+        s, n = b.shard_range(self.rank, self.world)
+        full = self.flat_param[b.start : b.start + b.numel]
+        if self._backend == "gloo":
+            chunks = list(full.chunk(self.world))
+            b.ag_work = dist.all_gather(chunks, chunks[self.rank].clone(), group=self.group, async_op=True)
+            return
+        # in place: sendbuff == recvbuff + rank * sendcount
+        b.ag_work = dist.all_gather_into_tensor(full, self.flat_param[s : s + n], group=self.group, async_op=True)
+
+    @torch.no_grad()
+    def _update_bucket_async(self, b: Bucket):
+        """Called from backward as soon as bucket ``b`` holds its final gradients.  Ordering:
+        compute stream (grads written, and the bucket's weights already read by its dgrad GEMMs,
+        which ops.linear issues before the weight-gradient sink) -> [reduce-scatter] -> side
+        stream: AdamW -> [all-gather].  ``step()`` joins the side stream."""
+        side = self._side
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            if b.work is not None:
+                b.work.wait()  # the side stream waits for the reduce-scatter
+                b.work = None
+            self._adamw(b, self.step_count + 1)
+            if self.world > 1:
+                self._all_gather(b)
+        b.updated = True
 
     def _reduce_bucket(self, b: Bucket, async_op: bool):
         if self.world == 1:
@@ -191,46 +239,30 @@ class ZeroOptimizer:
 
     @torch.no_grad()
     def step(self):
-        self.step_count += 1
         self.wait_params()  # no forward ran since the last step: finish its all-gathers first
+        self.step_count += 1
+        pending = [b for b in self.buckets if not b.updated]
         if self.world > 1:
-            for b in self.buckets:
+            for b in pending:
                 if b.work is None:  # not overlapped (or a param received no grad)
                     self._reduce_bucket(b, async_op=False)
                 else:
                     b.work.wait()
-        for i, b in enumerate(self.buckets):
-            s, n = b.shard_range(self.rank, self.world)
-            ops.adamw_(
-                self.flat_param[s : s + n],
-                self.flat_grad[s : s + n],
-                self.master[i],
-                self.exp_avg[i],
-                self.exp_avg_sq[i],
-                lr=self.lr,
-                beta1=self.beta1,
-                beta2=self.beta2,
-                eps=self.eps,
-                weight_decay=self.weight_decay,
-                step=self.step_count,
-                grad_scale=1.0 / self.world,  # the 1/world of the average is fused into AdamW
-            )
+                    b.work = None
+        for b in pending:
+            self._adamw(b, self.step_count)
         if self.world > 1:
             # gather the updated shards in forward order (buckets are stored in backward order);
             # with prefetch hooks installed the next forward waits per bucket, so the all-gather
             # of later layers overlaps the compute of earlier ones
-            for b in reversed(self.buckets):
-                s, n = b.shard_range(self.rank, self.world)
-                full = self.flat_param[b.start : b.start + b.numel]
-                if self._backend == "gloo":
-                    chunks = list(full.chunk(self.world))
-                    b.ag_work = dist.all_gather(chunks, chunks[self.rank].clone(), group=self.group, async_op=True)
-                    continue
-                # in place: sendbuff == recvbuff + rank * sendcount
-                b.ag_work = dist.all_gather_into_tensor(full, self.flat_param[s : s + n], group=self.group,
-                                                        async_op=True)
-            if not self._prefetch:
-                self.wait_params()
+            for b in reversed(pending):
+                self._all_gather(b)
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
+        for b in self.buckets:
+            b.updated = False
+        if self.world > 1 and not self._prefetch:
+            self.wait_params()
 
     def wait_params(self, buckets=None):
         """Block until the all-gathered parameters of ``buckets`` (default: all) have landed."""

@@ -181,3 +181,40 @@ def test_llama_tiny_step_matches_reference(gpu, monkeypatch):
         a, b = grads[n], p.grad.float()
         rel = (a - b).norm() / (b.norm() + 1e-12)
         assert rel < 0.08, f"{n}: rel grad err {rel}"
+
+
+def _train_tiny(gpu, overlap_update, steps=3, grad_accum=2):
+    from dstack_amd.models.llama import CONFIGS, Llama
+    from dstack_amd.parallel.zero import ZeroOptimizer
+
+    cfg = CONFIGS["llama-tiny"]
+    torch.manual_seed(0)
+    with torch.device(gpu):
+        m = Llama(cfg)
+    m.init_weights(seed=1)
+    m = m.to(torch.bfloat16)
+    opt = ZeroOptimizer(m, lr=1e-3, bucket_numel=1 << 20, overlap_update=overlap_update)
+    g = torch.Generator(device=gpu).manual_seed(7)
+    losses = []
+    for _ in range(steps):
+        opt.zero_grad()
+        for i in range(grad_accum):
+            tok = torch.randint(0, cfg.vocab_size, (2, 257), device=gpu, generator=g)
+            opt.sync_grads = i == grad_accum - 1
+            loss = m.loss(tok[:, :-1], tok[:, 1:])
+            (loss / grad_accum).backward()
+        opt.step()
+        losses.append(loss.item())
+    torch.cuda.synchronize()
+    return m, opt, losses
+
+
+def test_optimizer_in_backward_matches_plain_step(gpu):
+    """AdamW launched per bucket on a side stream during backward == AdamW after backward."""
+    m1, o1, l1 = _train_tiny(gpu, overlap_update=True)
+    m2, o2, l2 = _train_tiny(gpu, overlap_update=False)
+    assert o1._side is not None and o2._side is None
+    assert l1 == l2
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), n
+    assert l1[-1] < l1[0]  # it trains
