@@ -130,6 +130,10 @@ class ZeroOptimizer:
                 self._pads.append((b.start + used, b.numel - used))
         self._backend = dist.get_backend(group) if self.distributed else None
         self._side = None
+        import os
+
+        if os.environ.get("DSTACK_AMD_OPT_OVERLAP") is not None:
+            overlap_update = os.environ["DSTACK_AMD_OPT_OVERLAP"] not in ("0", "false", "")
         if overlap_update and device.type == "cuda":
             self._side = torch.cuda.Stream(device=device)
         self._hooks_on = self.overlap or self._side is not None
