@@ -58,6 +58,21 @@ def init_server_state(admin_token: Optional[str] = None):
     return token
 
 
+def init_sentry():
+    """Optional error/trace reporting (reference ``S/app.py:67-76``): active when
+    ``DSTACK_SENTRY_DSN`` is set and the ``sentry_sdk`` package is installed."""
+    if not settings.SENTRY_DSN:
+        return False
+    try:
+        import sentry_sdk
+    except ImportError:
+        logger.warning("DSTACK_SENTRY_DSN is set but sentry_sdk is not installed")
+        return False
+    sentry_sdk.init(dsn=settings.SENTRY_DSN, traces_sample_rate=settings.SENTRY_TRACES_SAMPLE_RATE,
+                    release=__version__)
+    return True
+
+
 def create_app(start_background: bool = True) -> FastAPI:
     @asynccontextmanager
     async def lifespan(app: FastAPI):
@@ -85,6 +100,7 @@ def create_app(start_background: bool = True) -> FastAPI:
 
         LocalGatewayProcess.stop_all()
 
+    init_sentry()
     app = FastAPI(title="dstack-amd", version=__version__, lifespan=lifespan, docs_url="/api/docs",
                   openapi_url="/api/openapi.json")
     register_routes(app)
@@ -165,6 +181,18 @@ def register_routes(app: FastAPI):
     def ui():
         """Web UI (single page over the REST API)."""
         return HTMLResponse(ui_index.read_text() if ui_index.exists() else "<h3>dstack-amd</h3>")
+
+    @app.get("/metrics", include_in_schema=False)
+    def prometheus_metrics():
+        """Prometheus exposition (DSTACK_ENABLE_PROMETHEUS_METRICS=0 disables it)."""
+        from fastapi.responses import PlainTextResponse
+
+        if os.environ.get("DSTACK_ENABLE_PROMETHEUS_METRICS", "1") in ("0", "false"):
+            return PlainTextResponse("", status_code=404)
+        from dstack_amd.server.services.prometheus import render
+
+        with session_scope() as s:
+            return PlainTextResponse(render(s), media_type="text/plain; version=0.0.4")
 
     @app.get("/api/server/scheduler_stats")
     def scheduler_stats():

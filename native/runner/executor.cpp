@@ -74,7 +74,10 @@ size_t LogHistory::size() const {
 
 bool LogHistory::wait_after(int64_t ts, int timeout_ms) const {
   std::unique_lock<std::mutex> lk(mu_);
-  return cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return last_ > ts; });
+  // system_clock deadline: libstdc++ maps it to pthread_cond_timedwait (steady-clock waits use
+  // pthread_cond_clockwait, which ThreadSanitizer does not intercept -> false "double lock")
+  const auto deadline = std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms);
+  return cv_.wait_until(lk, deadline, [&] { return last_ > ts; });
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -227,3 +227,12 @@ def test_unknown_project(client, path):
 def test_web_ui_served(client):
     r = client.get("/")
     assert r.status_code == 200 and "dstack-amd" in r.text and "/api/runs/list" in r.text
+
+
+def test_prometheus_metrics(client):
+    _init_virtual_repo(client)
+    client.post("/api/project/main/runs/submit", json=_task("prom1"))
+    r = client.get("/metrics")
+    assert r.status_code == 200
+    assert 'dstack_runs{project="main",status="submitted"} 1' in r.text
+    assert "# TYPE dstack_job_gpu_util_percent gauge" in r.text
