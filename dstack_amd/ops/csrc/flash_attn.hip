@@ -22,6 +22,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <string>
 
 using namespace dsa;
 
@@ -388,6 +389,157 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
     }
 }
 
+// ================================================================================================
+// Backward dK/dV pass, 8-wave variant: workgroup = 128 keys of one (b, q-head), 512 threads.
+// Wave w owns keys kb0 + 32*(w&3) and the (w>>2)-th 32-query half of every 64-query tile, so a
+// key group's dK/dV is accumulated by two waves that are reduced through LDS at the end.  K and V
+// of the block stay resident in LDS (B operands re-read per MFMA instead of living in 64 VGPRs),
+// which brings a wave under 256 registers: 2 waves per SIMD hide each other's LDS/exp latency.
+// LDS: K|V (64 KiB) + 2-stage Q/dO/lse/delta ring (65 KiB) = 129 KiB -> one workgroup per CU.
+// ================================================================================================
+template <bool CAUSAL>
+__global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
+    int H, int KVH, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KV_BYTES = 2 * 128 * 256;            // K (128 rows) | V (128 rows)
+  constexpr int STAGE = 2 * TILE_BYTES + 512;        // Q (64) | dO (64) | lse | delta
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
+  const int g = w & 3, qh = w >> 2, w4 = w & 3;
+  const int NH = H + 2 * KVH;
+  const long rs = (long)NH * HD;
+  const long ors = (long)H * HD;
+  const int bid = blockIdx.x;
+  const int kb = bid / (B * H);  // small kb = most q tiles: heaviest first
+  const int bh = bid % (B * H);
+  const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
+  const bf16_t* base = qkv + (long)b * S * rs;
+  const bf16_t* qp = base + hh * HD;
+  const bf16_t* kp = base + (H + kvh) * HD;
+  const bf16_t* vp = base + (H + KVH + kvh) * HD;
+  const bf16_t* dop = dout + (long)b * S * ors + hh * HD;
+  const float* lp = lse + ((long)b * H + hh) * S;
+  const float* dp = delta + ((long)b * H + hh) * S;
+  const int kb0 = kb * 128, kw0 = kb0 + 32 * g, mykey = kw0 + l32;
+  char* kl = smem;
+  char* vl = smem + 128 * 256;
+  char* ring = smem + KV_BYTES;
+
+  // K/V of the block: waves 0-3 stage K, waves 4-7 stage V (two 64-row halves each)
+  {
+    const bf16_t* src = qh == 0 ? kp : vp;
+    char* dst = qh == 0 ? kl : vl;
+    dma_tile64(src + (long)kb0 * rs, rs, dst, w4, lane);
+    dma_tile64(src + (long)(kb0 + 64) * rs, rs, dst + TILE_BYTES, w4, lane);
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dk[d][r] = 0.f;
+      dv[d][r] = 0.f;
+    }
+  const int qt_begin = CAUSAL ? kb0 / 64 : 0;
+  const int nqt = S / 64;
+  auto issue = [&](int qt, char* st) {
+    if (qh == 0)
+      dma_tile64(qp + (long)qt * 64 * rs, rs, st, w4, lane);
+    else
+      dma_tile64(dop + (long)qt * 64 * ors, ors, st + TILE_BYTES, w4, lane);
+    if (w == 0) dma_f32x64(lp + qt * 64, st + 2 * TILE_BYTES, lane);
+    if (w == 4) dma_f32x64(dp + qt * 64, st + 2 * TILE_BYTES + 256, lane);
+  };
+  issue(qt_begin, ring);
+  wait_dma_and_barrier();
+
+  for (int qt = qt_begin; qt < nqt; ++qt) {
+    const int stage = (qt - qt_begin) & 1;
+    const char* ql = ring + stage * STAGE;
+    const char* dol = ql + TILE_BYTES;
+    const float* ll = reinterpret_cast<const float*>(ql + 2 * TILE_BYTES);
+    const float* dl = ll + 64;
+    if (qt + 1 < nqt) issue(qt + 1, ring + (stage ^ 1) * STAGE);
+    const int qlo = qt * 64 + 32 * qh;
+    if (!CAUSAL || qlo + 31 >= kw0) {  // some query of my half-tile sees my keys
+      f32x16 sc, dpv;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sc[r] = 0.f;
+        dpv[r] = 0.f;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        sc = mfma(lds_row(ql, 32 * qh + l32, 2 * ks + hf), lds_row(kl, 32 * g + l32, 2 * ks + hf), sc);
+        dpv = mfma(lds_row(dol, 32 * qh + l32, 2 * ks + hf), lds_row(vl, 32 * g + l32, 2 * ks + hf), dpv);
+      }
+      const bool diag = CAUSAL && qlo < kw0 + 31;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int qi = 32 * qh + 8 * rr + 4 * hf;
+        const f4 L = *reinterpret_cast<const f4*>(ll + qi);
+        const f4 Dl = *reinterpret_cast<const f4*>(dl + qi);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rr + i;
+          float pv = fexp2(fmaf(sc[r], scale_log2, -L[i]));
+          if (diag && mykey > qt * 64 + qi + i) pv = 0.f;
+          sc[r] = pv;
+          dpv[r] = pv * (dpv[r] - Dl[i]);
+        }
+      }
+      bf16x8 pb[2], dsb[2];
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        pb[k2] = to_bf16x8(sc, 8 * k2);
+        dsb[k2] = to_bf16x8(dpv, 8 * k2);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+          dv[d] = mfma(lds_tr(dol, 32 * qh + 16 * k2, 32 * d, lane), pb[k2], dv[d]);
+          dk[d] = mfma(lds_tr(ql, 32 * qh + 16 * k2, 32 * d, lane), dsb[k2], dk[d]);
+        }
+    }
+    wait_dma_and_barrier();
+  }
+  // reduce the two q-halves of every key group through LDS (the K/V + ring space is free now):
+  // layout [g][dk|dv][d][r][lane] floats -> lane-contiguous, conflict-free
+  float* red = reinterpret_cast<float*>(smem);
+  if (qh == 1) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        red[(((g * 2 + 0) * 4 + d) * 16 + r) * 64 + lane] = dk[d][r];
+        red[(((g * 2 + 1) * 4 + d) * 16 + r) * 64 + lane] = dv[d][r];
+      }
+  }
+  __syncthreads();
+  if (qh == 0) {
+    const float sm = scale_log2 * 0.6931471805599453f;  // softmax scale = scale_log2 * ln2
+    float* dkr = dkp + (((long)b * S + mykey) * H + hh) * HD;
+    float* dvr = dvp + (((long)b * S + mykey) * H + hh) * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int dd = 32 * d + 8 * rr + 4 * hf;
+        f4 ok, ov;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rr + i;
+          ok[i] = (dk[d][r] + red[(((g * 2 + 0) * 4 + d) * 16 + r) * 64 + lane]) * sm;
+          ov[i] = dv[d][r] + red[(((g * 2 + 1) * 4 + d) * 16 + r) * 64 + lane];
+        }
+        *reinterpret_cast<f4*>(dkr + dd) = ok;
+        *reinterpret_cast<f4*>(dvr + dd) = ov;
+      }
+  }
+}
+
 // sum the per-q-head fp32 partials over each GQA group -> bf16 dk/dv inside dqkv
 __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __restrict__ dkp,
                                                                const float* __restrict__ dvp,
@@ -569,9 +721,21 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   }();
   const size_t lds_kv = 2 * (2 * (size_t)dkdv_qt * 256 + 8 * (size_t)dkdv_qt);
   const size_t lds_q = 4 * TILE_BYTES;
-#define DSA_DKDV(C, N)                                                                               \
-  fa_bwd_dkdv_kernel<C, N><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, \
-                                                      delta, dkp, dvp, B, S, H, KVH, sl2)
+  // dK/dV kernel: the 8-wave K/V-resident variant is the default (2.10 vs 2.53 ms for the whole
+  // backward at S=8192, same box); DSTACK_AMD_FA_DKDV=4w selects the 4-wave register-resident one
+  static const bool dkdv8 = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DKDV");
+    return !(v && std::string(v) == "4w");
+  }();
+#define DSA_DKDV(C, N)                                                                                 \
+  do {                                                                                                 \
+    if (dkdv8)                                                                                         \
+      fa_bwd_dkdv8_kernel<C><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(          \
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
+    else                                                                                               \
+      fa_bwd_dkdv_kernel<C, N><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, \
+                                                          delta, dkp, dvp, B, S, H, KVH, sl2);         \
+  } while (0)
   if (causal) {
     if (dkdv_qt == 128) DSA_DKDV(true, 4); else DSA_DKDV(true, 2);
     DSA_CHECK(hipGetLastError());

@@ -224,3 +224,30 @@ def test_optimizer_in_backward_matches_plain_step(gpu):
         rel = ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
         assert rel < 1e-2, f"{n}: {rel}"
     assert l1[-1] < l1[0]  # it trains
+
+
+def test_flash_attention_dkdv_variants_agree(gpu, tmp_path):
+    """The 8-wave (default) and 4-wave (DSTACK_AMD_FA_DKDV=4w) dK/dV kernels give the same
+    gradients; the switch is read once per process, so the 4-wave run is a child process."""
+    import os
+    import subprocess
+    import sys
+
+    B, S, H, KV, D = 1, 1024, 8, 2, 128
+    script = (
+        "import sys, torch\n"
+        "from dstack_amd import ops\n"
+        "g = torch.Generator(device='cuda').manual_seed(0)\n"
+        f"x = torch.randn({B}, {S}, {(H + 2 * KV) * D}, device='cuda', generator=g).bfloat16().requires_grad_()\n"
+        f"do = torch.randn({B}, {S}, {H * D}, device='cuda', generator=g).bfloat16()\n"
+        f"ops.attention(x, {H}, {KV}, causal=True).backward(do)\n"
+        "torch.save(x.grad.cpu(), sys.argv[1])\n"
+    )
+    env = dict(os.environ)
+    for variant in ("4w", "8w"):
+        env["DSTACK_AMD_FA_DKDV"] = variant
+        subprocess.run([sys.executable, "-c", script, str(tmp_path / f"{variant}.pt")], env=env, check=True,
+                       timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    a = torch.load(tmp_path / "4w.pt", weights_only=True).float()
+    b = torch.load(tmp_path / "8w.pt", weights_only=True).float()
+    assert ((a - b).norm() / b.norm()).item() < 2e-3
