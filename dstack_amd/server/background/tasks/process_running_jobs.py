@@ -19,7 +19,7 @@ from sqlalchemy import select
 from sqlalchemy.orm import Session
 
 from dstack_amd.core.backends.base import DSTACK_RUNNER_HTTP_PORT
-from dstack_amd.core.errors import RunnerError, SSHError
+from dstack_amd.core.errors import RunnerError, ServerClientError, SSHError
 from dstack_amd.core.models.configurations import ServiceConfiguration
 from dstack_amd.core.models.instances import InstanceStatus
 from dstack_amd.core.models.runs import (
@@ -93,7 +93,31 @@ def _cluster_info(run: RunModel, job: JobModel) -> Optional[ClusterInfo]:
     return ClusterInfo(job_ips=ips, master_job_ip=ips[0], gpus_per_job=gpus)
 
 
-def _task_body(run: RunModel, job: JobModel) -> dict:
+def _attach_volumes(s: Session, run: RunModel, job: JobModel) -> bool:
+    """Attach the job's network volumes once its instance is up (``JobRuntimeData.volume_names``
+    records them); a volume error fails the job with ``VOLUME_ERROR``."""
+    from dstack_amd.server.services.jobs import volumes as job_volumes
+
+    spec = jobs_services.job_spec(job)
+    jrd = jobs_services.job_jrd(job)
+    if jrd is None or jrd.volume_names is not None or not job_volumes.volume_mount_points(spec):
+        return True
+    inst = s.get(InstanceModel, job.instance_id) if job.instance_id is not None else None
+    if inst is None:
+        return True
+    try:
+        vols = job_volumes.get_job_configured_volumes(s, run.project, spec)
+        job_volumes.check_can_attach_job_volumes(vols)
+        jrd.volume_names = job_volumes.attach_job_volumes(s, job, inst, vols)
+    except ServerClientError as e:
+        jobs_services.terminate_job(job, JobTerminationReason.VOLUME_ERROR, str(e), delay=False)
+        scheduler.wake(scheduler.TERMINATING_JOBS)
+        return False
+    job.job_runtime_data = jrd.model_dump_json()
+    return True
+
+
+def _task_body(run: RunModel, job: JobModel, s: Optional[Session] = None) -> dict:
     spec = jobs_services.job_spec(job)
     jrd = jobs_services.job_jrd(job)
     run_spec = RunSpec.model_validate_json(run.run_spec)
@@ -122,7 +146,7 @@ def _task_body(run: RunModel, job: JobModel) -> dict:
         "cpu": jrd.cpu if jrd and jrd.cpu else 0, "memory": int((jrd.memory or 0) * 2**30) if jrd else 0,
         "shm_size": int(shm * 2**30) if shm else 0,
         "network_mode": jrd.network_mode.value if jrd else "host",
-        "volumes": [], "volume_mounts": volume_mounts, "instance_mounts": instance_mounts,
+        "volumes": _volume_specs(s, job, jrd), "volume_mounts": volume_mounts, "instance_mounts": instance_mounts,
         "container_ssh_keys": keys, "ports": ports,
         "host_ssh_user": "", "host_ssh_keys": [],
     }
@@ -130,6 +154,14 @@ def _task_body(run: RunModel, job: JobModel) -> dict:
         body["registry_username"] = spec.registry_auth.username
         body["registry_password"] = spec.registry_auth.password
     return body
+
+
+def _volume_specs(s: Optional[Session], job: JobModel, jrd) -> list:
+    if s is None or jrd is None or not jrd.volume_names:
+        return []
+    from dstack_amd.server.services.jobs.volumes import shim_volume_specs
+
+    return shim_volume_specs(s, job, jrd.volume_names)
 
 
 def _process_provisioning(s: Session, run: RunModel, job: JobModel):
@@ -147,9 +179,11 @@ def _process_provisioning(s: Session, run: RunModel, job: JobModel):
         job.status = JobStatus.PULLING.value  # container backends: the runner *is* the container
         jobs_services.mark_timing(job, "pulling")
         return
+    if not _attach_volumes(s, run, job):
+        return
     try:
         shim = get_shim_client(jpd, project.ssh_private_key)
-        shim.submit_task(_task_body(run, job))
+        shim.submit_task(_task_body(run, job, s))
     except (SSHError, RunnerError, Exception) as e:  # noqa: BLE001
         logger.info("%s: shim not reachable yet: %s", job.job_name, e)
         if get_current_datetime() - job.submitted_at > PROVISIONING_TIMEOUT:

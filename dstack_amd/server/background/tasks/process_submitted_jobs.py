@@ -17,7 +17,7 @@ from typing import List, Optional
 from sqlalchemy import select
 from sqlalchemy.orm import Session
 
-from dstack_amd.core.errors import BackendError, ComputeError, NoCapacityError
+from dstack_amd.core.errors import BackendError, ComputeError, NoCapacityError, ServerClientError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.common import NetworkMode
 from dstack_amd.core.models.instances import InstanceOfferWithAvailability, InstanceStatus
@@ -40,6 +40,7 @@ from dstack_amd.server.services import jobs as jobs_services
 from dstack_amd.server.services import offers as offers_services
 from dstack_amd.server.services import pools as pools_services
 from dstack_amd.server.services import runs as runs_services
+from dstack_amd.server.services.jobs import volumes as job_volumes
 from dstack_amd.server.services.locking import lockset
 from dstack_amd.server.services.topology import busy_set, pick_gpus
 from dstack_amd.utils.common import get_current_datetime
@@ -74,8 +75,16 @@ def _process_job(s: Session, job_id):
             return  # wait for the master job to be provisioned
         master_jpd = jobs_services.job_jpd(master)
     fleet = s.get(FleetModel, run.fleet_id) if run.fleet_id else None
+    # network volumes pin the job to their backend/region (attached in process_running_jobs)
+    try:
+        volumes = job_volumes.get_job_configured_volumes(s, run.project, spec)
+        job_volumes.check_can_attach_job_volumes(volumes)
+    except ServerClientError as e:
+        jobs_services.terminate_job(job, JobTerminationReason.VOLUME_ERROR, str(e), delay=False)
+        scheduler.wake(scheduler.TERMINATING_JOBS, scheduler.RUNS)
+        return
     # ---- 1) reuse a pool instance ----
-    if _assign_pool_instance(s, run, job, spec, profile, fleet, multinode, master_jpd):
+    if _assign_pool_instance(s, run, job, spec, profile, fleet, multinode, master_jpd, volumes):
         scheduler.wake(scheduler.RUNNING_JOBS, scheduler.RUNS)
         return
     if profile.creation_policy == CreationPolicy.REUSE or (fleet is not None and not _fleet_autocreated(fleet)):
@@ -88,6 +97,7 @@ def _process_job(s: Session, job_id):
         instance_mounts=any("instance_path" in v for v in (spec.volumes or [])),
     )
     offers = [(c, o) for c, o in offers if o.backend != BackendType.REMOTE]
+    offers = job_volumes.filter_offers_by_volumes(offers, volumes)
     if not offers:
         _no_capacity(job, "No offers match the requirements")
         return
@@ -141,10 +151,11 @@ def _gpu_request(spec, offer: InstanceOfferWithAvailability) -> int:
 
 
 def _assign_pool_instance(s: Session, run: RunModel, job: JobModel, spec, profile, fleet, multinode: bool,
-                          master_jpd) -> bool:
+                          master_jpd, volumes=()) -> bool:
     instances = pools_services.list_project_instances(s, run.project)
     cands = pools_services.filter_pool_instances(instances, profile, spec.requirements, fleet=fleet,
                                                  multinode=multinode, master_jpd=master_jpd)
+    cands = [(i, sh) for i, sh in cands if job_volumes.instance_matches_volumes(i, volumes)]
     if not cands:
         return False
     ls = lockset("instances")

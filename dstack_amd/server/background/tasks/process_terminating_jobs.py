@@ -5,6 +5,7 @@ volumes, release the instance's blocks/GPUs."""
 from __future__ import annotations
 
 import logging
+from datetime import timedelta
 
 from sqlalchemy import select
 from sqlalchemy.orm import Session
@@ -30,6 +31,16 @@ def process_terminating_jobs(batch: int = 5) -> bool:
 
     more = claim_and_process("jobs", select_ids, _process_job, batch)
     return more
+
+
+def _detach_volumes(s: Session, job: JobModel) -> bool:
+    from dstack_amd.server.services.jobs.volumes import detach_job_volumes
+
+    try:
+        return detach_job_volumes(s, job, job.instance_id, job.remove_at)
+    except Exception as e:  # noqa: BLE001 - a broken backend must not wedge termination forever
+        logger.warning("%s: volume detach failed: %s", job.job_name, e)
+        return job.remove_at is not None and get_current_datetime() - job.remove_at > timedelta(minutes=10)
 
 
 def _process_job(s: Session, job_id):
@@ -62,6 +73,9 @@ def _process_job(s: Session, job_id):
         from dstack_amd.server.services.services import unregister_replica
 
         unregister_replica(s, run, job)
+    if not _detach_volumes(s, job):
+        job.last_processed_at = get_current_datetime()
+        return  # retried on the next pass (soft detach in progress; forced after stop_duration)
     jobs_services.release_instance(s, job)
     job.volumes_detached_at = get_current_datetime()
     job.status = reason.to_status().value

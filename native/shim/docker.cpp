@@ -119,6 +119,11 @@ class DockerDriver : public TaskDriver {
   }
 
   bool run(Task& t, std::string& reason, std::string& msg) override {
+    std::map<std::string, std::string> vol_paths;
+    if (!prepare_volumes(t, o_.volumes_root, vol_paths, msg)) {
+      reason = "volume_error";
+      return false;
+    }
     if (!pull(t, msg)) {
       reason = "creating_container_error";
       return false;
@@ -150,8 +155,11 @@ class DockerDriver : public TaskDriver {
     if (!o_.probe_binary.empty()) binds.push_back(o_.probe_binary + ":/usr/local/bin/dstack-probe:ro");
     for (auto& m : t.config.instance_mounts.items())
       binds.push_back(m["instance_path"].str() + ":" + m["path"].str());
-    for (auto& m : t.config.volume_mounts.items())
-      binds.push_back("/dstack-volumes/" + m["name"].str() + ":" + m["path"].str());
+    for (auto& m : t.config.volume_mounts.items()) {
+      auto it = vol_paths.find(m["name"].str());
+      std::string host = it != vol_paths.end() ? it->second : o_.volumes_root + "/" + m["name"].str();
+      binds.push_back(host + ":" + m["path"].str());
+    }
     hc.set("Binds", binds);
     hc.set("NetworkMode", t.config.network_mode);
     hc.set("Privileged", t.config.privileged || o_.privileged);
@@ -261,8 +269,8 @@ class DockerDriver : public TaskDriver {
   }
 
   void remove(Task& t) override {
-    if (t.container_id.empty()) return;
-    call("DELETE", "/containers/" + t.container_id + "?force=1&v=1");
+    if (!t.container_id.empty()) call("DELETE", "/containers/" + t.container_id + "?force=1&v=1");
+    unmount_volumes(t, o_.volumes_root);
   }
 
   std::vector<Task> restore() override {

@@ -192,6 +192,7 @@ int main(int argc, char** argv) {
     else if (a == "--runner-http-port") o.runner_http_port = atoi(next().c_str());
     else if (a == "--runner-ssh-port") o.runner_ssh_port = atoi(next().c_str());
     else if (a == "--driver") o.driver = next();
+    else if (a == "--volumes-root") o.volumes_root = next();
     else if (a == "--privileged") o.privileged = true;
     else if (a == "--service") service = true;
     else if (a == "--version") {

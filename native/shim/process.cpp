@@ -79,6 +79,20 @@ class ProcessDriver : public TaskDriver {
     mkdirs(dir + "/tmp");
     mkdirs(dir + "/home");
     mkdirs(dir + "/workflow");
+    // network volumes: mounted on the host, then linked into the task dir like instance mounts
+    std::map<std::string, std::string> vol_paths;
+    if (!prepare_volumes(t, o_.volumes_root, vol_paths, msg)) {
+      reason = "volume_error";
+      return false;
+    }
+    for (auto& m : t.config.volume_mounts.items()) {
+      auto it = vol_paths.find(m["name"].str());
+      std::string p = m["path"].str();
+      if (it == vol_paths.end() || p.empty()) continue;
+      std::string link = dir + "/mounts" + p;
+      mkdirs(link.substr(0, link.rfind('/')));
+      if (symlink(it->second.c_str(), link.c_str()) != 0) LOGW("volume link %s failed", link.c_str());
+    }
     // instance mounts: expose host paths inside the task dir (symlinks) for parity with docker
     for (auto& m : t.config.instance_mounts.items()) {
       std::string ip = m["instance_path"].str(), p = m["path"].str();
@@ -187,8 +201,9 @@ class ProcessDriver : public TaskDriver {
 
   void remove(Task& t) override {
     std::string dir = o_.home + "/tasks/" + t.config.id;
-    std::string cmd = "rm -rf '" + dir + "'";
-    if (system(cmd.c_str()) != 0) LOGW("cannot remove %s", dir.c_str());
+    std::string out;
+    if (run_capture({"rm", "-rf", "--", dir}, out) != 0) LOGW("cannot remove %s", dir.c_str());
+    unmount_volumes(t, o_.volumes_root);
   }
 
  private:

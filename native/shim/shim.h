@@ -115,6 +115,7 @@ struct ShimOptions {
   std::string docker_socket = "/var/run/docker.sock";
   std::string driver = "auto";  // docker | process | auto
   int pull_timeout_s = 20 * 60;
+  std::string volumes_root = "/dstack-volumes";
 };
 
 class TaskDriver {
@@ -138,6 +139,17 @@ void register_child_pgid(int pgid);
 void unregister_child_pgid(int pgid);
 void kill_registered_children(int sig);
 bool docker_available(const std::string& socket_path);
+
+// ---- network volumes (volumes.cpp) --------------------------------------------------------------
+int run_capture(const std::vector<std::string>& argv, std::string& out);
+std::string aws_device_from_lsblk(const std::string& lsblk_json, const std::string& volume_id);
+std::string aws_xvd_name(const std::string& device_name);
+std::string resolve_volume_device(const Json& v);
+// mount (formatting new volumes) and return the host path to bind for the volume
+bool prepare_volume(const Json& v, const std::string& root, std::string& host_path, std::string& err);
+bool prepare_volumes(Task& t, const std::string& root, std::map<std::string, std::string>& paths,
+                     std::string& err);
+bool unmount_volumes(const Task& t, const std::string& root);
 
 // shell bootstrap that starts sshd + the runner inside a container (docker.go:873-911)
 std::string container_bootstrap_script(const ShimOptions& o, const std::vector<std::string>& keys);

@@ -4,6 +4,7 @@
 
 #include <cstdio>
 #include <functional>
+#include <map>
 #include <set>
 #include <string>
 #include <thread>
@@ -179,6 +180,47 @@ int main() {
     CHECK(http_request(req).status == 404);
     srv.stop();
     th.join();
+  });
+
+  run("volumes: aws nvme serial / xvd mapping / local dirs / refcounted unmount", [] {
+    const std::string lsblk = R"({"blockdevices":[
+      {"name":"nvme0n1","serial":"vol0aaaa","type":"disk","children":[{"name":"nvme0n1p1","serial":null,"type":"part"}]},
+      {"name":"nvme1n1","serial":"vol0123456789abcdef  ","type":"disk"}]})";
+    CHECK(aws_device_from_lsblk(lsblk, "vol-0123456789abcdef") == "/dev/nvme1n1");
+    CHECK(aws_device_from_lsblk(lsblk, "vol-0aaaa") == "/dev/nvme0n1p1");
+    CHECK(aws_device_from_lsblk(lsblk, "vol-missing").empty());
+    CHECK(aws_device_from_lsblk("not json", "vol-0aaaa").empty());
+    CHECK(aws_xvd_name("/dev/sdf") == "/dev/xvdf");
+    CHECK(aws_xvd_name("/dev/nvme1n1") == "/dev/nvme1n1");
+    std::string out;
+    CHECK(run_capture({"echo", "hi"}, out) == 0 && out == "hi\n");
+    CHECK(run_capture({"/nonexistent-binary-xyz"}, out) != 0);
+    char tmpl[] = "/tmp/dsa-vol-XXXXXX";
+    std::string root = mkdtemp(tmpl);
+    Task t;
+    Json v = Json::object();
+    v.set("backend", "local");
+    v.set("name", "data");
+    v.set("volume_id", root + "/hostdir");
+    t.config.volumes.push_back(v);
+    std::map<std::string, std::string> paths;
+    std::string err;
+    CHECK(prepare_volumes(t, root, paths, err));
+    CHECK(paths["data"] == root + "/hostdir" && path_exists(root + "/hostdir"));
+    CHECK(prepare_volumes(t, root, paths, err));  // second user of the same volume
+    CHECK(unmount_volumes(t, root));
+    CHECK(unmount_volumes(t, root));
+    Json bad = Json::object();
+    bad.set("backend", "aws");
+    bad.set("name", "../etc");
+    std::string hp;
+    CHECK(!prepare_volume(bad, root, hp, err) && err.find("invalid") != std::string::npos);
+    Json missing = Json::object();
+    missing.set("backend", "gcp");
+    missing.set("name", "nodisk");
+    missing.set("device_name", "dstack-nodisk-xyz");
+    CHECK(!prepare_volume(missing, root, hp, err) && err.find("not found") != std::string::npos);
+    run_capture({"rm", "-rf", "--", root}, out);
   });
 
   fprintf(stderr, "%d/%d test groups passed\n", g_run - (g_failed ? 1 : 0), g_run);
