@@ -14,5 +14,6 @@ from dstack_amd.ops.functional import (  # noqa: F401
     rms_norm,
     rope,
     swiglu,
+    weight_grad,
 )
 from dstack_amd.ops import _ext  # noqa: F401

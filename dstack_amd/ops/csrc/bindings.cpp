@@ -23,6 +23,8 @@ hipError_t dsa_fa_fwd(const void*, void*, float*, int, int, int, int, int, float
 size_t dsa_fa_bwd_workspace(int, int, int);
 hipError_t dsa_fa_bwd(const void*, const void*, const void*, const float*, void*, void*, int, int, int, int,
                       int, float, int, hipStream_t);
+bool dsa_gemm_tn_supported(int, int, int);
+hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 }
 
 namespace {
@@ -190,6 +192,22 @@ torch::Tensor flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tenso
   return dqkv;
 }
 
+bool gemm_tn_supported(int64_t P, int64_t Q, int64_t T) { return dsa_gemm_tn_supported(P, Q, T); }
+
+// out[P][Q] (+)= a^T b ; a = [T][P], b = [T][Q] (weight gradient dW = dY^T X)
+void gemm_tn(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool accumulate) {
+  for (auto* t : {&a, &b, &out}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kBFloat16 && t->dim() == 2, "gemm_tn: 2-D bf16 tensors");
+    TORCH_CHECK(t->stride(1) == 1, "gemm_tn: rows must be contiguous");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_tn: 16-byte aligned base");
+  }
+  const int64_t T = a.size(0), P = a.size(1), Q = b.size(1);
+  TORCH_CHECK(b.size(0) == T && out.size(0) == P && out.size(1) == Q, "gemm_tn: shape mismatch");
+  check(dsa_gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), P, Q, T, a.stride(0), b.stride(0), out.stride(0),
+                    accumulate ? 1 : 0, stream()),
+        "gemm_tn");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -205,4 +223,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw", &adamw);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("gemm_tn", &gemm_tn);
+  m.def("gemm_tn_supported", &gemm_tn_supported);
 }

@@ -19,89 +19,19 @@
 //    "key on the lane" (S = Q·K^T) so P and dS feed dV^T/dK^T directly; the dQ pass uses the
 //    forward orientation and feeds dS^T as the A operand of dQ = dS·K.  dQ is computed by its own
 //    q-major pass instead of cross-workgroup atomics (deterministic, no atomic-rate floor).
-#include "common.h"
+#include "mfma_tiles.h"
 
 #include <cstdlib>
 #include <string>
 
 using namespace dsa;
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-#define LDS3(T, p) ((__attribute__((address_space(3))) T*)(p))
-#define GLB1(T, p) ((__attribute__((address_space(1))) T*)(p))
-
 namespace {
 
 constexpr int HD = 128;          // head dim
-constexpr int TILE_BYTES = 64 * 256;  // 64 rows x 128 bf16
 #ifndef DKDV_WAVES_PER_SIMD
 #define DKDV_WAVES_PER_SIMD 1  // dK/dV + K/V fragments need ~300 registers: 1 wave/SIMD, no spills
 #endif
-
-__device__ __forceinline__ int swz(int row, int ch) {
-  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
-}
-
-// v_exp_f32 directly: exp2f() adds a denormal range-reduction (cmp/cndmask/add/ldexp) around it;
-// softmax probabilities below 2^-126 are irrelevant, so the bare instruction is exact enough
-__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
-
-__device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ bf16x8 lds_row(const char* base, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(base + swz(row, ch));
-}
-
-// A-operand fragment of X^T where X is a [rows][128] tile in LDS read by columns:
-// element j of lane-half h = X[16*ks + 8*(j>>2) + 4*h + (j&3)][col0 + (lane&31)]  (the k order of
-// an MFMA accumulator used as the other operand).  Two ds_read_b64_tr_b16 per fragment.
-__device__ __forceinline__ bf16x8 lds_tr(const char* base, int row_base, int col0, int lane) {
-  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-  const int r0 = row_base + 4 * (g >> 1) + q4;
-  const int c0 = (col0 >> 3) + 2 * (g & 1) + (p4 >> 1);
-  const int sub = 8 * (p4 & 1);
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(bf16x4, base + swz(r0, c0) + sub));
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(bf16x4, base + swz(r0 + 8, c0) + sub));
-  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
-// Issue LDS-DMA of a [64 x 128] bf16 tile (rows row0.., row stride `stride` elements) into the
-// swizzled LDS image at `lds`.  4 waves x 4 wave-instructions of 1 KiB (4 rows each).
-__device__ __forceinline__ void dma_tile64(const bf16_t* g, long stride, char* lds, int wave,
-                                           int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wave * 4 + i;
-    const int row = piece * 4 + (lane >> 4);
-    const int pc = lane & 15;
-    const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
-    const bf16_t* src = g + (long)row * stride + ch * 8;
-    __builtin_amdgcn_global_load_lds(GLB1(void, src), LDS3(void, lds + piece * 1024), 16, 0, 0);
-  }
-}
-
-// 64 contiguous floats -> LDS (one wave-instruction, 4 B/lane)
-__device__ __forceinline__ void dma_f32x64(const float* g, char* lds, int lane) {
-  __builtin_amdgcn_global_load_lds(GLB1(void, g + lane), LDS3(void, lds), 4, 0, 0);
-}
-
-__device__ __forceinline__ void wait_dma_and_barrier() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
-__device__ __forceinline__ bf16x8 to_bf16x8(const f32x16& acc, int base) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(acc[base + j]);
-  return r;
-}
 
 }  // namespace
 

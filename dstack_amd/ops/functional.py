@@ -201,6 +201,20 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return _Linear.apply(x, w)
 
 
+def weight_grad(g: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    """``out (+)= g^T x`` for g [T, P], x [T, Q] (dW of a linear layer) with the HIP gemm_tn kernel
+    (csrc/gemm.hip) when the shape is tiled by it, else torch.  At parity with hipBLASLt on the
+    Llama shapes (profiles/gemm_wgrad_r1.txt), so the training path keeps the library GEMM."""
+    if _ext.use_hip(g):
+        C = _ext.require()
+        if C.gemm_tn_supported(g.shape[1], x.shape[1], g.shape[0]) and g.stride(1) == 1 and x.stride(1) == 1:
+            C.gemm_tn(g, x, out, accumulate)
+            return out
+    if accumulate:
+        return out.addmm_(g.t(), x)
+    return torch.mm(g.t(), x, out=out)
+
+
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target):

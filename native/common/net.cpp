@@ -373,7 +373,11 @@ static std::string ws_accept_key(const std::string& key) {
 // ---------------------------------------------------------------------------------------------
 // server
 // ---------------------------------------------------------------------------------------------
-HttpServer::~HttpServer() { stop(); }
+HttpServer::~HttpServer() {
+  stop();
+  const int fd = listen_fd_.exchange(-1);
+  if (fd >= 0) ::close(fd);
+}
 
 static std::vector<std::string> path_parts(const std::string& p) {
   std::vector<std::string> out;
@@ -406,36 +410,43 @@ bool HttpServer::match(const Route& r, const std::string& path, std::map<std::st
 
 int HttpServer::start() {
   signal(SIGPIPE, SIG_IGN);
-  listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
-  if (listen_fd_ < 0) return -1;
+  const int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+  if (lfd < 0) return -1;
   int one = 1;
-  setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
   struct sockaddr_in addr{};
   addr.sin_family = AF_INET;
   addr.sin_port = htons((uint16_t)port_);
   if (inet_pton(AF_INET, host_.c_str(), &addr.sin_addr) != 1) addr.sin_addr.s_addr = htonl(INADDR_ANY);
-  if (::bind(listen_fd_, (struct sockaddr*)&addr, sizeof addr) != 0) {
+  if (::bind(lfd, (struct sockaddr*)&addr, sizeof addr) != 0) {
     LOGE("bind %s:%d failed: %s", host_.c_str(), port_, strerror(errno));
-    ::close(listen_fd_);
-    listen_fd_ = -1;
+    ::close(lfd);
     return -1;
   }
-  if (::listen(listen_fd_, 128) != 0) return -1;
+  if (::listen(lfd, 128) != 0) {
+    ::close(lfd);
+    return -1;
+  }
   socklen_t len = sizeof addr;
-  getsockname(listen_fd_, (struct sockaddr*)&addr, &len);
+  getsockname(lfd, (struct sockaddr*)&addr, &len);
   port_ = ntohs(addr.sin_port);
+  listen_fd_ = lfd;
   running_ = true;
   return port_;
 }
 
+// The listening socket is owned by serve_forever() while it runs: stop() only flips running_ and
+// shuts the socket down (waking poll/accept); the fd is closed by the serving thread on its way out
+// (or by the destructor when it never served), so no thread closes an fd another is polling.
 void HttpServer::serve_forever() {
+  const int lfd = listen_fd_;
   while (running_) {
-    struct pollfd p{listen_fd_, POLLIN, 0};
+    struct pollfd p{lfd, POLLIN, 0};
     int r = ::poll(&p, 1, 200);
     if (r <= 0) continue;
     struct sockaddr_in caddr{};
     socklen_t clen = sizeof caddr;
-    int fd = ::accept(listen_fd_, (struct sockaddr*)&caddr, &clen);
+    int fd = ::accept(lfd, (struct sockaddr*)&caddr, &clen);
     if (fd < 0) continue;
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
@@ -443,15 +454,14 @@ void HttpServer::serve_forever() {
     inet_ntop(AF_INET, &caddr.sin_addr, ip, sizeof ip);
     std::thread(&HttpServer::handle_conn, this, fd, std::string(ip)).detach();
   }
+  int expected = lfd;
+  if (listen_fd_.compare_exchange_strong(expected, -1)) ::close(lfd);
 }
 
 void HttpServer::stop() {
   running_ = false;
-  if (listen_fd_ >= 0) {
-    ::shutdown(listen_fd_, SHUT_RDWR);
-    ::close(listen_fd_);
-    listen_fd_ = -1;
-  }
+  const int fd = listen_fd_;
+  if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
 }
 
 static void parse_query(const std::string& qs, std::map<std::string, std::string>& out) {

@@ -116,7 +116,7 @@ class HttpServer {
   void handle_conn(int fd, std::string remote);
   std::string host_;
   int port_;
-  int listen_fd_ = -1;
+  std::atomic<int> listen_fd_{-1};
   std::atomic<bool> running_{false};
   std::vector<Route> routes_;
 };

@@ -251,3 +251,31 @@ def test_flash_attention_dkdv_variants_agree(gpu, tmp_path):
     a = torch.load(tmp_path / "4w.pt", weights_only=True).float()
     b = torch.load(tmp_path / "8w.pt", weights_only=True).float()
     assert ((a - b).norm() / b.norm()).item() < 2e-3
+
+
+@pytest.mark.parametrize("T,P,Q", [(64, 256, 256), (512, 768, 512), (1024, 512, 1280)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_weight_grad_gemm_tn(gpu, T, P, Q, accumulate):
+    """HIP gemm_tn (dW = g^T x) against an fp32 matmul, incl. accumulation into bf16."""
+    C = _ext.require()
+    assert C.gemm_tn_supported(P, Q, T)
+    g = _rand(T, P, device=gpu, seed=3)
+    x = _rand(T, Q, device=gpu, seed=4)
+    base = _rand(P, Q, device=gpu, seed=5)
+    out = base.clone()
+    ops.weight_grad(g, x, out, accumulate=accumulate)
+    refv = g.float().t() @ x.float() + (base.float() if accumulate else 0)
+    err = ((out.float() - refv).norm() / refv.norm()).item()
+    assert err < 4e-3, err
+
+
+def test_weight_grad_strided_rows(gpu):
+    """Row-strided views (a column slice of a wider buffer) are consumed in place."""
+    T, P, Q = 256, 512, 256
+    gw = _rand(T, P + 128, device=gpu, seed=6)
+    xw = _rand(T, Q + 64, device=gpu, seed=7)
+    g, x = gw[:, 64:64 + P], xw[:, :Q]
+    out = torch.empty(P, Q, device=gpu, dtype=torch.bfloat16)
+    ops.weight_grad(g, x, out)
+    refv = g.float().t() @ x.float()
+    assert ((out.float() - refv).norm() / refv.norm()).item() < 4e-3
