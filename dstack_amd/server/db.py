@@ -1,9 +1,13 @@
-"""Database layer: SQLAlchemy 2.0 ORM over SQLite (WAL) — reference: ``S/db.py:16-106``.
+"""Database layer: SQLAlchemy 2.0 ORM over SQLite (WAL) or Postgres — reference: ``S/db.py:16-106``.
 
 The MI355X build runs the control plane synchronously: request handlers and reconciler tasks run
 in worker threads, each with its own short ``Session``.  SQLite is opened in WAL mode with a 30 s
 busy timeout and foreign keys on; schema evolution uses the versioned migrations in
-``server/migrations.py`` (no alembic in this image).
+``server/migrations.py`` (no alembic in this image).  With ``DSTACK_DATABASE_URL=postgresql://...``
+several server replicas share the database: reconcilers claim rows with ``FOR UPDATE SKIP LOCKED``
+and named operations/migrations take ``pg_advisory_xact_lock`` (``services/locking.py``).  The
+Postgres driver (psycopg) is not part of this image, so that path is covered by SQL-compilation
+tests only.
 """
 
 from __future__ import annotations
@@ -28,8 +32,10 @@ class Database:
             kwargs["connect_args"] = {"check_same_thread": False, "timeout": 30}
             if url in ("sqlite://", "sqlite:///:memory:"):
                 kwargs["poolclass"] = StaticPool
-        else:
+        else:  # postgresql(+psycopg)://: several server replicas may share the database
             kwargs["pool_size"] = settings.DB_POOL_SIZE
+            kwargs["max_overflow"] = settings.DB_MAX_OVERFLOW
+            kwargs["pool_pre_ping"] = True
         self.engine: Engine = create_engine(url, **kwargs)
         if url.startswith("sqlite"):
             event.listen(self.engine, "connect", _sqlite_pragmas)

@@ -46,9 +46,18 @@ def current_version(conn) -> int:
     return int(row or 0)
 
 
+MIGRATIONS_LOCK_NAME = "dstack_migrations"
+
+
 def run_migrations(db) -> int:
+    """Apply pending migrations.  Server replicas sharing a Postgres database serialise on a
+    transaction-scoped advisory lock (reference ``S/db.py:75-82``: alembic under an advisory lock)."""
+    from dstack_amd.server.services.locking import ADVISORY_XACT_LOCK_SQL, advisory_key
+
     with _lock:
         with db.engine.begin() as conn:
+            if conn.dialect.name == "postgresql":
+                conn.execute(text(ADVISORY_XACT_LOCK_SQL), {"k": advisory_key(MIGRATIONS_LOCK_NAME)})
             v = current_version(conn)
             for i, mig in enumerate(MIGRATIONS, start=1):
                 if i <= v:

@@ -32,7 +32,7 @@ from dstack_amd.server.background import scheduler
 from dstack_amd.server.models import FleetModel, InstanceModel, ProjectModel, UserModel
 from dstack_amd.server.services import offers as offers_services
 from dstack_amd.server.services import pools as pools_services
-from dstack_amd.server.services.locking import get_locker
+from dstack_amd.server.services.locking import db_advisory_lock
 from dstack_amd.utils.common import generate_name, get_current_datetime
 
 
@@ -86,7 +86,7 @@ def _idle_seconds(conf: FleetConfiguration) -> int:
 
 def create_fleet(s: Session, project: ProjectModel, user: UserModel, spec: FleetSpec) -> Fleet:
     conf = spec.configuration
-    with get_locker().advisory_lock(f"fleet_names_{project.id}"):
+    with db_advisory_lock(s, f"fleet_names_{project.id}"):
         if conf.name is None:
             conf.name = generate_name()
         if get_fleet_by_name(s, project, conf.name) is not None:

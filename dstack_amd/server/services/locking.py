@@ -1,18 +1,26 @@
-"""In-process locksets for the control plane (reference: ``S/services/locking.py:13-81``,
+"""Locking for the control plane (reference: ``S/services/locking.py:13-81``,
 ``contributing/LOCKING.md``).
 
-With SQLite the server is a single process, so every background task claims the rows it processes
-by adding their ids to a named in-memory lockset; rows already in the set are skipped by other
-workers.  ``advisory_lock`` serialises whole operations (e.g. run-name allocation per project).
+* In-process locksets: every background task claims the rows it processes by adding their ids to
+  a named lockset; rows already in the set are skipped by the server's other worker threads.
+* Postgres (several server replicas on one database): on top of the lockset, the row itself is
+  claimed inside the processing transaction with ``SELECT ... FOR UPDATE SKIP LOCKED``
+  (``claim_row``) so another replica skips it, and named operations take a transaction-scoped
+  ``pg_advisory_xact_lock`` (``db_advisory_lock``).  With SQLite (one server process) both reduce
+  to the in-process primitives.
 """
 
 from __future__ import annotations
 
 import contextlib
+import hashlib
 import threading
 import time
 from collections import defaultdict
-from typing import Dict, Hashable, Iterable, Iterator, List, Set
+from typing import Dict, Hashable, Iterable, Iterator, List, Optional, Set
+
+from sqlalchemy import select, text
+from sqlalchemy.orm import Session
 
 
 class Lockset:
@@ -89,3 +97,39 @@ def get_locker() -> ResourceLocker:
 
 def lockset(namespace: str) -> Lockset:
     return _locker.get_lockset(namespace)
+
+
+def _is_postgres(s: Session) -> bool:
+    return s.get_bind().dialect.name == "postgresql"
+
+
+def claim_row_stmt(model, row_id):
+    """The row-claim query: the row's id if no other transaction holds it, else no row."""
+    return select(model.id).where(model.id == row_id).with_for_update(skip_locked=True)
+
+
+def claim_row(s: Session, model, row_id) -> bool:
+    """Claim ``row_id`` of ``model`` for the rest of ``s``'s transaction.  Postgres: row lock with
+    SKIP LOCKED (False = another replica is processing it); SQLite: always True (the in-process
+    lockset already excluded the server's other threads)."""
+    if not _is_postgres(s):
+        return True
+    return s.execute(claim_row_stmt(model, row_id)).scalar_one_or_none() is not None
+
+
+def advisory_key(name: str) -> int:
+    """Stable signed 64-bit key for ``pg_advisory_*`` (Python's hash() is salted per process)."""
+    return int.from_bytes(hashlib.blake2b(name.encode(), digest_size=8).digest(), "big", signed=True)
+
+
+ADVISORY_XACT_LOCK_SQL = "SELECT pg_advisory_xact_lock(:k)"
+
+
+@contextlib.contextmanager
+def db_advisory_lock(s: Optional[Session], name: str) -> Iterator[None]:
+    """Serialise a named operation across threads (always) and server replicas (Postgres: held
+    until ``s``'s transaction ends)."""
+    with _locker.advisory_lock(name):
+        if s is not None and _is_postgres(s):
+            s.execute(text(ADVISORY_XACT_LOCK_SQL), {"k": advisory_key(name)})
+        yield

@@ -36,7 +36,7 @@ from dstack_amd.server.services import jobs as jobs_services
 from dstack_amd.server.services import offers as offers_services
 from dstack_amd.server.services import pools as pools_services
 from dstack_amd.server.services import repos as repos_services
-from dstack_amd.server.services.locking import get_locker
+from dstack_amd.server.services.locking import db_advisory_lock
 from dstack_amd.utils.common import generate_name, get_current_datetime
 
 logger = logging.getLogger(__name__)
@@ -156,7 +156,7 @@ def get_plan(s: Session, project: ProjectModel, user: UserModel, run_spec: RunSp
 
 def submit_run(s: Session, project: ProjectModel, user: UserModel, run_spec: RunSpec) -> Run:
     _validate_run_spec(run_spec)
-    with get_locker().advisory_lock(f"run_names_{project.id}"):
+    with db_advisory_lock(s, f"run_names_{project.id}"):
         if run_spec.run_name is None:
             for _ in range(20):
                 name = generate_name()

@@ -20,6 +20,7 @@ SERVER_DATA_DIR_PATH = SERVER_DIR_PATH / "data"
 
 DATABASE_URL = os.getenv("DSTACK_DATABASE_URL", f"sqlite:///{SERVER_DATA_DIR_PATH}/sqlite.db")
 DB_POOL_SIZE = int(os.getenv("DSTACK_DB_POOL_SIZE", "20"))
+DB_MAX_OVERFLOW = int(os.getenv("DSTACK_DB_MAX_OVERFLOW", "20"))
 
 SERVER_HOST = os.getenv("DSTACK_SERVER_HOST", "127.0.0.1")
 SERVER_PORT = int(os.getenv("DSTACK_SERVER_PORT", "3000"))
