@@ -12,6 +12,8 @@ int dsa_rmsnorm_bwd_grid(int rows);
 hipError_t dsa_rmsnorm_bwd(const void*, const void*, const void*, const float*, const void*, void*, float*,
                            float*, int, int, hipStream_t);
 hipError_t dsa_swiglu_fwd(const void*, void*, int, int, hipStream_t);
+bool dsa_transpose2d_supported(int, int);
+hipError_t dsa_transpose2d(const void*, void*, int, int, hipStream_t);
 hipError_t dsa_swiglu_bwd(const void*, const void*, void*, int, int, hipStream_t);
 hipError_t dsa_rope_qkv(const void*, void*, const float*, const float*, int, int, int, int, int, int,
                         hipStream_t);
@@ -88,6 +90,19 @@ std::vector<torch::Tensor> rms_norm_bwd(torch::Tensor dy, torch::Tensor h, torch
                         dx.data_ptr(), part.data_ptr<float>(), dw.data_ptr<float>(), rows, D, stream()),
         "rms_norm_bwd");
   return {dx, dw};
+}
+
+bool transpose2d_supported(int64_t R, int64_t C) { return dsa_transpose2d_supported((int)R, (int)C); }
+
+// out[C, R] = x[R, C]^T for a row-contiguous 2-D bf16 x (row stride may exceed C)
+torch::Tensor transpose2d(torch::Tensor x) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) == x.size(1), "transpose2d: contiguous 2-D input");
+  const int R = (int)x.size(0), C = (int)x.size(1);
+  TORCH_CHECK(dsa_transpose2d_supported(R, C), "transpose2d: shape not tiled (R % 128, C % 64)");
+  auto out = torch::empty({C, R}, x.options());
+  check(dsa_transpose2d(x.data_ptr(), out.data_ptr(), R, C, stream()), "transpose2d");
+  return out;
 }
 
 torch::Tensor swiglu_fwd(torch::Tensor gu) {
@@ -216,6 +231,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_rms_norm_fwd", &add_rms_norm_fwd);
   m.def("rms_norm_bwd", &rms_norm_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("transpose2d", &transpose2d);
+  m.def("transpose2d_supported", &transpose2d_supported);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_qkv", &rope_qkv);
   m.def("cross_entropy_fwd", &cross_entropy_fwd);

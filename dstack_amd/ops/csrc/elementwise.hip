@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 // RMSNorm backward: dx = r*g - h*r^3*mean(g*h) (+ dres), g = dy*w ;  dw partials per block.
 // One 256-thread block per row (grid-strided over rows): each thread owns NCH chunks of 8
 // columns, so its dw contribution stays in NCH*8 registers for the whole launch; the row dot is a
-// wave shuffle + a 4-entry LDS combine.  Each block writes one fp32 dw partial row; colsum_kernel
+// wave shuffle + a 4-entry LDS combine.  Each block writes one fp32 dw partial row; colsum (two passes)
 // reduces the [grid, D] partials.
 // ------------------------------------------------------------------------------------------------
 template <int NCH, bool RES>
@@ -143,19 +143,59 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restri
   }
 }
 
-// column sums of a [P, D] fp32 matrix -> out[D]: block = 64 columns x 4 row-groups, coalesced
-// 256-byte row segments per wave, LDS combine of the 4 row-groups.
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part,
-                                                     float* __restrict__ out, int P, int D) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + c;
-  float s = 0.f;
+// column sums of a [P, D] fp32 matrix -> out[D], two deterministic passes that fill the chip
+// (the old single pass ran D/64 = 64 workgroups for D=4096: 69 us for 16 MB, r1f profile).
+//  pass 1: grid (D/256) x RS; a wave reads 256 columns as float4, the 4 waves of a block split
+//          the block's row range, LDS combine, and the block's partial overwrites the FIRST row
+//          of its own range (only this block reads that range, and it has finished reading).
+//  pass 2: one wave per 256 columns sums the RS partial rows.
+constexpr int COLSUM_RS = 16;
+__global__ __launch_bounds__(256) void colsum_pass1_kernel(float* __restrict__ part, int P, int D,
+                                                           int rpb) {
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = (blockIdx.x * 64 + lane) * 4;
+  const int r0 = blockIdx.y * rpb, r1 = min(P, r0 + rpb);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < D)
-    for (int p = rg; p < P; p += 4) s += part[(size_t)p * D + col];
-  red[rg][c] = s;
+    for (int r = r0 + wv; r < r1; r += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)r * D + col);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  red[wv][lane] = s;
   __syncthreads();
-  if (rg == 0 && col < D) out[col] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  if (wv == 0 && col < D && r0 < r1) {
+    float4 a = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 b = red[k][lane];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    *reinterpret_cast<float4*>(part + (size_t)r0 * D + col) = a;
+  }
+}
+
+__global__ __launch_bounds__(64) void colsum_pass2_kernel(const float* __restrict__ part,
+                                                          float* __restrict__ out, int P, int D,
+                                                          int rpb) {
+  const int col = (blockIdx.x * 64 + threadIdx.x) * 4;
+  if (col >= D) return;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+  for (int r = 0; r < P; r += rpb) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (size_t)r * D + col);
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  *reinterpret_cast<float4*>(out + col) = a;
+}
+
+static hipError_t colsum(float* part, float* out, int P, int D, hipStream_t st) {
+  const int rpb = (P + COLSUM_RS - 1) / COLSUM_RS;
+  const int cb = (D + 255) / 256;
+  colsum_pass1_kernel<<<dim3(cb, COLSUM_RS), 256, 0, st>>>(part, P, D, rpb);
+  DSA_CHECK(hipGetLastError());
+  colsum_pass2_kernel<<<cb, 64, 0, st>>>(part, out, P, D, rpb);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -421,6 +461,46 @@ static inline int grid_for(size_t work, int block, int cap = 256 * 16) {
     else return hipErrorInvalidValue;              \
   } while (0)
 
+// ------------------------------------------------------------------------------------------------
+// 2-D bf16 transpose out[C, R] = in[R, C]^T (reduction-contiguous operands for the weight-gradient
+// GEMMs: hipBLASLt runs dW = g^T x at ~1.1 PFLOP/s when both operands are token-major and at
+// 1.35-1.56 PFLOP/s when they are token-contiguous, tools/bench_wgrad_layouts.py).
+// Tile 128 rows x 64 columns per 256-thread workgroup: 16-byte coalesced row loads into a padded
+// LDS tile (row pitch 72 elements, so the column reads below are bank-conflict free), then each
+// thread gathers 32 consecutive rows of one column and writes them as 4 x 16 B.
+// ------------------------------------------------------------------------------------------------
+constexpr int TR_R = 128, TR_C = 64, TR_P = TR_C + 8;
+__global__ __launch_bounds__(256) void transpose2d_kernel(const bf16_t* __restrict__ in,
+                                                          bf16_t* __restrict__ out, int R, int C) {
+  __shared__ __attribute__((aligned(16))) unsigned short tile[TR_R * TR_P];
+  const int c0 = blockIdx.x * TR_C, r0 = blockIdx.y * TR_R;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 128 rows x 8 chunks of 8 columns = 1024 chunks / 256 threads
+    const int idx = i * 256 + t, r = idx >> 3, ch = idx & 7;
+    const us8 v = *reinterpret_cast<const us8*>(in + (size_t)(r0 + r) * C + c0 + ch * 8);
+    *reinterpret_cast<us8*>(tile + r * TR_P + ch * 8) = v;
+  }
+  __syncthreads();
+  const int c = t & 63, rg = t >> 6;
+  us8 o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[j][k] = tile[(rg * 32 + j * 8 + k) * TR_P + c];
+  bf16_t* dst = out + (size_t)(c0 + c) * R + r0 + rg * 32;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) *reinterpret_cast<us8*>(dst + j * 8) = o[j];
+}
+
+extern "C" bool dsa_transpose2d_supported(int R, int C) { return R % TR_R == 0 && C % TR_C == 0; }
+
+extern "C" hipError_t dsa_transpose2d(const void* in, void* out, int R, int C, hipStream_t st) {
+  if (!dsa_transpose2d_supported(R, C)) return hipErrorInvalidValue;
+  transpose2d_kernel<<<dim3(C / TR_C, R / TR_R), 256, 0, st>>>((const bf16_t*)in, (bf16_t*)out, R, C);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t dsa_rmsnorm_fwd(const void* x, const void* delta, const void* w, void* h_out,
                                       void* y, float* rstd, int rows, int D, float eps,
                                       hipStream_t st) {
@@ -461,8 +541,7 @@ extern "C" hipError_t dsa_rmsnorm_bwd(const void* dy, const void* h, const void*
         rows, D));
   }
   DSA_CHECK(hipGetLastError());
-  colsum_kernel<<<(D + 63) / 64, 256, 0, st>>>(dw_part, dw, grid, D);
-  return hipGetLastError();
+  return colsum(dw_part, dw, grid, D, st);
 }
 
 extern "C" hipError_t dsa_swiglu_fwd(const void* gu, void* out, int rows, int F, hipStream_t st) {

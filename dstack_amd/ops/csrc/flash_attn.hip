@@ -186,6 +186,44 @@ __global__ __launch_bounds__(256) void fa_bwd_delta_kernel(const bf16_t* __restr
   }
 }
 
+// Tiled delta: workgroup = 32 consecutive positions x 8 heads of one batch row.  Reads are 2 KiB
+// contiguous per position (8 heads x 128 d); the [B, H, S] result is staged in LDS and written
+// as full 128-byte lines per head.  The row-per-16-lanes kernel above scatters 4-byte stores
+// with stride S, and adjacent positions land on different XCDs' L2s: partial-line write-backs
+// made it 558 us at S=8192 (measured, r1f profile) for 134 MB of reads.
+__global__ __launch_bounds__(256) void fa_bwd_delta_tiled_kernel(const bf16_t* __restrict__ o,
+                                                                 const bf16_t* __restrict__ dout,
+                                                                 float* __restrict__ delta, int B,
+                                                                 int S, int H) {
+  constexpr int ST = 32, HT = 8;
+  __shared__ float red[HT][ST + 1];
+  const int nht = H / HT, nst = S / ST;
+  int bid = blockIdx.x;
+  const int ht = bid % nht;
+  bid /= nht;
+  const int st = bid % nst, b = bid / nst;
+  const int sub = threadIdx.x & 15, r = threadIdx.x >> 4;
+  const long base = ((long)b * S + (long)st * ST) * H + ht * HT;
+#pragma unroll 4
+  for (int it = 0; it < ST * HT / 16; ++it) {
+    const int idx = it * 16 + r;
+    const int s = idx / HT, h = idx % HT;
+    const long row = base + (long)s * H + h;
+    float a[8], g[8];
+    unpack8(*reinterpret_cast<const us8*>(o + row * HD + sub * 8), a);
+    unpack8(*reinterpret_cast<const us8*>(dout + row * HD + sub * 8), g);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += a[i] * g[i];
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (sub == 0) red[h][s] = acc;
+  }
+  __syncthreads();
+  const int h = threadIdx.x / ST, s = threadIdx.x % ST;  // 256 threads = HT x ST outputs
+  delta[((long)b * H + ht * HT + h) * S + (long)st * ST + s] = red[h][s];
+}
+
 // ================================================================================================
 // Backward dK/dV pass: workgroup = 128 keys of one (b, q-head); wave w owns keys kb0 + 32w.
 // Loops over 64-row q tiles from the diagonal to S; writes fp32 per-q-head partials
@@ -639,8 +677,12 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   float* dkp = delta + (size_t)B * H * S;
   float* dvp = dkp + (size_t)B * S * H * HD;
   const long rows = (long)B * S * H;
-  fa_bwd_delta_kernel<<<(int)((rows + 15) / 16), 256, 0, st>>>((const bf16_t*)out, (const bf16_t*)dout,
-                                                               delta, B, S, H);
+  if (H % 8 == 0 && S % 32 == 0)
+    fa_bwd_delta_tiled_kernel<<<B * (S / 32) * (H / 8), 256, 0, st>>>(
+        (const bf16_t*)out, (const bf16_t*)dout, delta, B, S, H);
+  else
+    fa_bwd_delta_kernel<<<(int)((rows + 15) / 16), 256, 0, st>>>((const bf16_t*)out,
+                                                                 (const bf16_t*)dout, delta, B, S, H);
   DSA_CHECK(hipGetLastError());
   const int grid = B * H * (S / 128);
   // dK/dV q-tile per pipeline stage: 64 rows (default) or 128 (DSTACK_AMD_FA_DKDV_QT=128: half

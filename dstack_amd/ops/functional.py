@@ -176,7 +176,8 @@ class _Linear(torch.autograd.Function):
     """``y = x @ w.T`` whose weight gradient is written by the GEMM itself into the optimizer's
     flat gradient buffer (``w._dsa_grad_sink``): the first micro-batch uses beta=0 (no memset of
     the buffer), later ones accumulate with beta=1 in the hipBLASLt epilogue — no separate
-    AccumulateGrad add kernel, no zero-fill, one pass over the gradient instead of three."""
+    AccumulateGrad add kernel, no zero-fill, one pass over the gradient instead of three.
+    The dW GEMM's operands are re-laid out token-contiguous first (``wgrad_operands``)."""
 
     @staticmethod
     def forward(ctx, x, w):
@@ -189,12 +190,38 @@ class _Linear(torch.autograd.Function):
         gx = g @ w if ctx.needs_input_grad[0] else None
         if not ctx.needs_input_grad[1]:
             return gx, None
-        g2, x2 = g.reshape(-1, g.shape[-1]), x.reshape(-1, x.shape[-1])
+        a, b = wgrad_operands(g.reshape(-1, g.shape[-1]), x.reshape(-1, x.shape[-1]))
         sink = getattr(w, "_dsa_grad_sink", None)
         if sink is None:
-            return gx, g2.t() @ x2
-        sink(w, g2, x2)
+            return gx, a @ b
+        sink(w, a, b)
         return gx, None
+
+
+def _wgrad_mode() -> str:
+    return os.environ.get("DSTACK_AMD_WGRAD", "auto").lower()
+
+
+def wgrad_operands(g2: torch.Tensor, x2: torch.Tensor):
+    """Operands (a [P, T], b [T, Q]) with dW = a @ b for g2 [T, P], x2 [T, Q].
+
+    hipBLASLt runs dW = g^T x at ~1.0-1.1 PFLOP/s on MI355X when both operands are token-major
+    (the reduction dimension is the strided one for both) and at 1.3-1.56 PFLOP/s when they are
+    token-contiguous (tools/bench_wgrad_layouts.py, profiles/wgrad_layouts_r1.txt).  So x is
+    transposed by the HIP transpose kernel (T x Q, a few % of the GEMM's time) and g too when it
+    is no larger than x (down/o projections; the gate_up and lm_head gradients are 3.5-31x larger
+    than their inputs and stay token-major).  ``DSTACK_AMD_WGRAD=strided`` keeps the old layout."""
+    a, b = g2.t(), x2
+    if not (_ext.use_hip(x2) and _wgrad_mode() == "auto"):
+        return a, b
+    C = _ext.require()
+    T, P = g2.shape
+    Q = x2.shape[1]
+    if x2.is_contiguous() and C.transpose2d_supported(T, Q):
+        b = C.transpose2d(x2).t()
+    if P <= Q and g2.is_contiguous() and C.transpose2d_supported(T, P):
+        a = C.transpose2d(g2)
+    return a, b
 
 
 def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

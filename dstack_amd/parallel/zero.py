@@ -156,13 +156,14 @@ class ZeroOptimizer:
             b.work = None
             b.updated = False
 
-    def _direct_grad(self, p: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
-        """Weight gradient sink for ``ops.linear``: dW = g^T x into the flat buffer."""
+    def _direct_grad(self, p: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+        """Weight gradient sink for ``ops.linear``: dW = a @ b (a = g^T [P, T], b = x [T, Q], as
+        views in whichever layout ``ops.functional.wgrad_operands`` chose) into the flat buffer."""
         if p._dsa_fresh:
-            torch.mm(g2.t(), x2, out=p.grad)
+            torch.mm(a, b, out=p.grad)
             p._dsa_fresh = False
         else:
-            p.grad.addmm_(g2.t(), x2)
+            p.grad.addmm_(a, b)
         self._direct_ok.add(p)
         if self._hooks_on:
             self._on_grad_ready(p)

@@ -279,3 +279,29 @@ def test_weight_grad_strided_rows(gpu):
     ops.weight_grad(g, x, out)
     refv = g.float().t() @ x.float()
     assert ((out.float() - refv).norm() / refv.norm()).item() < 4e-3
+
+
+@pytest.mark.parametrize("R,C", [(128, 64), (256, 4096), (8192, 192)])
+def test_transpose2d(gpu, R, C):
+    Cx = _ext.require()
+    x = _rand(R, C, device=gpu, seed=8)
+    assert torch.equal(Cx.transpose2d(x), x.t().contiguous())
+
+
+@pytest.mark.parametrize("T,P,Q", [(256, 128, 512), (512, 1024, 256), (384, 200, 256)])
+def test_linear_wgrad_layouts_agree(gpu, T, P, Q, monkeypatch):
+    """dW through the token-contiguous operands (transposed x and, when P <= Q, g) equals the
+    token-major GEMM; a shape the transpose kernel does not tile (P=200) keeps g token-major."""
+    x = _rand(T, Q, device=gpu, seed=9).requires_grad_()
+    w = _rand(P, Q, device=gpu, seed=10, scale=0.05).requires_grad_()
+    g = _rand(T, P, device=gpu, seed=11)
+    grads = {}
+    for mode in ("auto", "strided"):
+        monkeypatch.setenv("DSTACK_AMD_WGRAD", mode)
+        x.grad = w.grad = None
+        ops.linear(x, w).backward(g)
+        grads[mode] = (x.grad.clone(), w.grad.clone())
+    refw = g.float().t() @ x.detach().float()
+    for mode, (_, gw) in grads.items():
+        assert ((gw.float() - refw).norm() / refw.norm()).item() < 4e-3, mode
+    assert torch.equal(grads["auto"][0], grads["strided"][0])
