@@ -20,7 +20,7 @@ hipError_t dsa_rope_qkv(const void*, void*, const float*, const float*, int, int
 hipError_t dsa_ce_fwd(const void*, const int64_t*, float*, float*, int, int, hipStream_t);
 hipError_t dsa_ce_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, hipStream_t);
 hipError_t dsa_adamw(void*, const void*, float*, float*, float*, size_t, float, float, float, float, float,
-                     float, float, float, hipStream_t);
+                     float, float, float, int, hipStream_t);
 hipError_t dsa_fa_fwd(const void*, void*, float*, int, int, int, int, int, float, int, hipStream_t);
 size_t dsa_fa_bwd_workspace(int, int, int);
 hipError_t dsa_fa_bwd(const void*, const void*, const void*, const float*, void*, void*, int, int, int, int,
@@ -167,7 +167,8 @@ torch::Tensor cross_entropy_bwd(torch::Tensor logits, torch::Tensor target, torc
 }
 
 void adamw(torch::Tensor param, torch::Tensor grad, torch::Tensor master, torch::Tensor m, torch::Tensor v,
-           double lr, double b1, double b2, double eps, double wd, double bc1, double bc2, double gscale) {
+           double lr, double b1, double b2, double eps, double wd, double bc1, double bc2, double gscale,
+           int64_t max_blocks) {
   check_bf16(param, "param");
   check_bf16(grad, "grad");
   for (auto* t : {&master, &m, &v}) {
@@ -175,7 +176,8 @@ void adamw(torch::Tensor param, torch::Tensor grad, torch::Tensor master, torch:
     TORCH_CHECK(t->numel() == param.numel(), "adam state numel mismatch");
   }
   check(dsa_adamw(param.data_ptr(), grad.data_ptr(), master.data_ptr<float>(), m.data_ptr<float>(),
-                  v.data_ptr<float>(), param.numel(), lr, b1, b2, eps, wd, bc1, bc2, gscale, stream()),
+                  v.data_ptr<float>(), param.numel(), lr, b1, b2, eps, wd, bc1, bc2, gscale, (int)max_blocks,
+                  stream()),
         "adamw");
 }
 

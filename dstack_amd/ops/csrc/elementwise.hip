@@ -4,7 +4,7 @@
 // 1 KiB per wave-instruction) and reduces rows inside ONE 64-lane wave with __shfl_xor, so no LDS
 // and no __syncthreads sit on the critical path. Grids are sized to keep >=4 waves per SIMD
 // resident across all 256 CUs.
-#include "common.h"
+#include "mfma_tiles.h"
 
 using namespace dsa;
 
@@ -465,32 +465,41 @@ static inline int grid_for(size_t work, int block, int cap = 256 * 16) {
 // 2-D bf16 transpose out[C, R] = in[R, C]^T (reduction-contiguous operands for the weight-gradient
 // GEMMs: hipBLASLt runs dW = g^T x at ~1.1 PFLOP/s when both operands are token-major and at
 // 1.35-1.56 PFLOP/s when they are token-contiguous, tools/bench_wgrad_layouts.py).
-// Tile 128 rows x 64 columns per 256-thread workgroup: 16-byte coalesced row loads into a padded
-// LDS tile (row pitch 72 elements, so the column reads below are bank-conflict free), then each
-// thread gathers 32 consecutive rows of one column and writes them as 4 x 16 B.
+// Tile 128 rows x 64 columns per 256-thread workgroup: 16-byte coalesced row loads into LDS, then
+// ds_read_b64_tr_b16 (gfx950's transposed LDS read: a 16-lane group gets a 4-row x 16-column block
+// column-major, lane i = column i) twice per lane gives 8 consecutive rows of one column = one
+// 16-byte store of an output row.  LDS row pitch 96 elements (48 dwords): the 4 rows of a block
+// start on banks 0/48/32/16, so a 32-lane half (2 blocks x 4 rows x 16 B) covers all 64 banks once.
+// (The first version gathered 2-byte LDS reads: 45-49 us per 64 MB, 2.7 TB/s, r1j profile.)
 // ------------------------------------------------------------------------------------------------
-constexpr int TR_R = 128, TR_C = 64, TR_P = TR_C + 8;
+constexpr int TR_R = 128, TR_C = 64, TR_P = 96;
 __global__ __launch_bounds__(256) void transpose2d_kernel(const bf16_t* __restrict__ in,
                                                           bf16_t* __restrict__ out, int R, int C) {
-  __shared__ __attribute__((aligned(16))) unsigned short tile[TR_R * TR_P];
+  __shared__ __attribute__((aligned(16))) bf16_t tile[TR_R * TR_P];
   const int c0 = blockIdx.x * TR_C, r0 = blockIdx.y * TR_R;
   const int t = threadIdx.x;
+  us8 v[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {  // 128 rows x 8 chunks of 8 columns = 1024 chunks / 256 threads
     const int idx = i * 256 + t, r = idx >> 3, ch = idx & 7;
-    const us8 v = *reinterpret_cast<const us8*>(in + (size_t)(r0 + r) * C + c0 + ch * 8);
-    *reinterpret_cast<us8*>(tile + r * TR_P + ch * 8) = v;
+    v[i] = *reinterpret_cast<const us8*>(in + (size_t)(r0 + r) * C + c0 + ch * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t, r = idx >> 3, ch = idx & 7;
+    *reinterpret_cast<us8*>(tile + r * TR_P + ch * 8) = v[i];
   }
   __syncthreads();
-  const int c = t & 63, rg = t >> 6;
-  us8 o[4];
+  const int G = t >> 4, lane16 = t & 15, q = (t >> 2) & 3, p = t & 3;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) o[j][k] = tile[(rg * 32 + j * 8 + k) * TR_P + c];
-  bf16_t* dst = out + (size_t)(c0 + c) * R + r0 + rg * 32;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) *reinterpret_cast<us8*>(dst + j * 8) = o[j];
+  for (int pass = 0; pass < 4; ++pass) {  // 4 column blocks x 16 row chunks of 8 = 64 units
+    const int u = pass * 16 + G, cb = u & 3, rk = u >> 2;
+    const bf16_t* src = tile + (rk * 8 + q) * TR_P + cb * 16 + 4 * p;
+    const dsa::bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, src));
+    const dsa::bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, src + 4 * TR_P));
+    const dsa::bf16x8 o = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<dsa::bf16x8*>(out + (size_t)(c0 + cb * 16 + lane16) * R + r0 + rk * 8) = o;
+  }
 }
 
 extern "C" bool dsa_transpose2d_supported(int R, int C) { return R % TR_R == 0 && C % TR_C == 0; }
@@ -587,8 +596,14 @@ extern "C" hipError_t dsa_ce_bwd(const void* logits, const int64_t* target, cons
 
 extern "C" hipError_t dsa_adamw(void* param, const void* grad, float* master, float* m, float* v,
                                 size_t n, float lr, float b1, float b2, float eps, float wd,
-                                float bc1, float bc2, float gscale, hipStream_t st) {
-  adamw_kernel<<<grid_for(n / 8 + 1, 256, 256 * 8), 256, 0, st>>>(
+                                float bc1, float bc2, float gscale, int max_blocks, hipStream_t st) {
+  // max_blocks > 0 caps the grid (persistent grid-stride): the optimizer-in-backward path runs
+  // AdamW on a side stream beside MFMA-bound kernels, where a full-chip grid takes every CU's
+  // slots and just serialises the two (r1g trace: dK/dV 1.13 -> 2.3 ms while AdamW ran).  Measured
+  // same box (tools/run_r1l.sh, ms/step): full grid 799, 64 blocks 807, 32 843, 16 956, no
+  // overlap 802 -- per-CU HBM bandwidth is too low for a small persistent grid, so 0 stays default
+  const int cap = max_blocks > 0 ? max_blocks : 256 * 8;
+  adamw_kernel<<<grid_for(n / 8 + 1, 256, cap), 256, 0, st>>>(
       (bf16_t*)param, (const bf16_t*)grad, master, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
   return hipGetLastError();
 }

@@ -270,11 +270,14 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------------------------
 # Fused AdamW over flat buffers (bf16 param/grad, fp32 master/m/v)
 # ----------------------------------------------------------------------------------------------
-def adamw_(param, grad, master, m, v, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+def adamw_(param, grad, master, m, v, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0,
+           max_blocks=0):
+    """``max_blocks`` > 0 caps the HIP kernel's (grid-stride) grid, e.g. to leave most CUs to the
+    compute stream when the update runs beside backward."""
     if _ext.use_hip(param):
         C = _ext.require()
         bc1 = 1.0 - beta1**step
         bc2 = 1.0 - beta2**step
-        C.adamw(param, grad, master, m, v, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale)
+        C.adamw(param, grad, master, m, v, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale, max_blocks)
         return
     ref.adamw_(param, grad, master, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale)

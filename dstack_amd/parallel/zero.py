@@ -136,6 +136,9 @@ class ZeroOptimizer:
             overlap_update = os.environ["DSTACK_AMD_OPT_OVERLAP"] not in ("0", "false", "")
         if overlap_update and device.type == "cuda":
             self._side = torch.cuda.Stream(device=device)
+        # AdamW beside backward runs on a capped grid (persistent workgroups on a few CUs) so the
+        # compute kernels keep the rest of the chip; 0 = full grid
+        self._side_blocks = int(os.environ.get("DSTACK_AMD_ADAMW_SIDE_BLOCKS", "0"))
         self._hooks_on = self.overlap or self._side is not None
         self._hooks = []
         for p in params:
@@ -179,13 +182,14 @@ class ZeroOptimizer:
             if self._side is not None:
                 self._update_bucket_async(b)
 
-    def _adamw(self, b: Bucket, step: int):
+    def _adamw(self, b: Bucket, step: int, max_blocks: int = 0):
         s, n = b.shard_range(self.rank, self.world)
         i = b.index
         ops.adamw_(self.flat_param[s : s + n], self.flat_grad[s : s + n], self.master[i], self.exp_avg[i],
                    self.exp_avg_sq[i], lr=self.lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
                    weight_decay=self.weight_decay, step=step,
-                   grad_scale=1.0 / self.world)  # the 1/world of the average is fused into AdamW
+                   grad_scale=1.0 / self.world,  # the 1/world of the average is fused into AdamW
+                   max_blocks=max_blocks)
 
     def _all_gather(self, b: Bucket):
         s, n = b.shard_range(self.rank, self.world)
@@ -209,7 +213,7 @@ class ZeroOptimizer:
             if b.work is not None:
                 b.work.wait()  # the side stream waits for the reduce-scatter
                 b.work = None
-            self._adamw(b, self.step_count + 1)
+            self._adamw(b, self.step_count + 1, self._side_blocks)
             if self.world > 1:
                 self._all_gather(b)
         b.updated = True
