@@ -163,17 +163,66 @@ def pools_list_instances(user: UserModel = Depends(authenticated), s: Session = 
 
 @pool_router.post("/list")
 def pool_list(up: UP = Depends(project_member), s: Session = Depends(get_session)):
-    pool = pools_services.get_or_create_default_pool(s, up[1])
-    insts = pools_services.list_project_instances(s, up[1])
-    return [{"name": pool.name, "default": True, "created_at": pool.created_at, "total_instances": len(insts),
-             "available_instances": sum(1 for i in insts if i.status == "idle")}]
+    return pools_services.list_project_pools(s, up[1])
 
 
 @pool_router.post("/show")
-def pool_show(up: UP = Depends(project_member), s: Session = Depends(get_session)):
-    pool = pools_services.get_or_create_default_pool(s, up[1])
-    return {"name": pool.name, "instances": [pools_services.instance_model_to_instance(i)
-                                              for i in pools_services.list_project_instances(s, up[1])]}
+def pool_show(body: Optional[schemas.ShowPoolRequest] = None, up: UP = Depends(project_member),
+              s: Session = Depends(get_session)):
+    return pools_services.show_pool_instances(s, up[1], body.name if body else None)
+
+
+@pool_router.post("/create")
+def pool_create(body: schemas.CreatePoolRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+    pools_services.create_pool(s, up[1], body.name)
+    return None
+
+
+@pool_router.post("/set_default")
+def pool_set_default(body: schemas.SetDefaultPoolRequest, up: UP = Depends(project_member),
+                     s: Session = Depends(get_session)):
+    pools_services.set_default_pool(s, up[1], body.pool_name)
+    return None
+
+
+@pool_router.post("/delete")
+def pool_delete(body: schemas.DeletePoolRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+    pools_services.delete_pool(s, up[1], body.name)
+    return None
+
+
+@pool_router.post("/remove")
+def pool_remove_instance(body: schemas.RemoveInstanceRequest, up: UP = Depends(project_member),
+                         s: Session = Depends(get_session)):
+    pools_services.remove_instance(s, up[1], body.pool_name, body.instance_name, body.force)
+    return None
+
+
+@pool_router.post("/add_remote")
+def pool_add_remote(body: schemas.AddRemoteInstanceRequest, up: UP = Depends(project_member),
+                    s: Session = Depends(get_session)) -> Instance:
+    if not body.host.strip() or not body.ssh_user.strip() or not body.ssh_keys:
+        raise ServerClientError("Host, user or ssh keys are empty")
+    return pools_services.add_remote(s, up[1], body.pool_name, body.instance_name, body.instance_network,
+                                     body.region, body.host, body.port or 22, body.ssh_user, body.ssh_keys)
+
+
+# legacy: get_offers / create_instance live under runs in the reference (routers/runs.py:183-219)
+@runs_router.post("/get_offers")
+def runs_get_offers(body: schemas.GetOffersRequest, up: UP = Depends(project_member),
+                    s: Session = Depends(get_session)):
+    from dstack_amd.core.models.runs import PoolInstanceOffers
+    from dstack_amd.server.services import offers as offers_services
+
+    pool = pools_services.get_or_create_pool_by_name(s, up[1], body.profile.pool_name)
+    offers = offers_services.get_offers_by_requirements(s, up[1], body.profile, body.requirements)
+    return PoolInstanceOffers(pool_name=pool.name, instances=[o for _, o in offers])
+
+
+@runs_router.post("/create_instance")
+def runs_create_instance(body: schemas.CreateInstanceRequest, up: UP = Depends(project_member),
+                         s: Session = Depends(get_session)) -> Instance:
+    return fleets_services.create_instance(s, up[1], up[0], body.profile, body.requirements)
 
 
 # ---- volumes --------------------------------------------------------------------------------

@@ -11,7 +11,9 @@ from pydantic import ConfigDict
 from dstack_amd.core.models.common import CoreModel
 from dstack_amd.core.models.fleets import FleetSpec
 from dstack_amd.core.models.gateways import GatewayConfiguration
-from dstack_amd.core.models.runs import ApplyRunPlanInput, Run, RunSpec
+from dstack_amd.core.models.instances import SSHKey
+from dstack_amd.core.models.profiles import Profile
+from dstack_amd.core.models.runs import ApplyRunPlanInput, Requirements, Run, RunSpec
 from dstack_amd.core.models.users import GlobalRole, ProjectRole
 from dstack_amd.core.models.volumes import VolumeConfiguration
 
@@ -226,3 +228,48 @@ class ListVolumesRequest(_Req):
 
 
 _ = Run
+
+
+# ---- legacy pools (reference: S/schemas/pools.py, S/schemas/runs.py AddRemoteInstanceRequest) ----
+class CreatePoolRequest(_Req):
+    name: str
+
+
+class SetDefaultPoolRequest(_Req):
+    pool_name: str
+
+
+class DeletePoolRequest(_Req):
+    name: str
+    force: bool = False
+
+
+class ShowPoolRequest(_Req):
+    name: Optional[str] = None
+
+
+class RemoveInstanceRequest(_Req):
+    pool_name: str
+    instance_name: str
+    force: bool = False
+
+
+class AddRemoteInstanceRequest(_Req):
+    pool_name: Optional[str] = None
+    instance_name: Optional[str] = None
+    instance_network: Optional[str] = None
+    region: Optional[str] = None
+    host: str
+    port: Optional[int] = None
+    ssh_user: str
+    ssh_keys: List[SSHKey]
+
+
+class GetOffersRequest(_Req):
+    profile: Profile
+    requirements: Requirements
+
+
+class CreateInstanceRequest(_Req):
+    profile: Profile
+    requirements: Requirements

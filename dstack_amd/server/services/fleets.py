@@ -186,3 +186,26 @@ def delete_fleet_instances(s: Session, project: ProjectModel, name: str, instanc
 
 
 _ = (Duration, Env, InstanceModel)
+
+
+def create_instance(s: Session, project: ProjectModel, user: UserModel, profile: Profile,
+                    requirements: Requirements) -> Instance:
+    """Legacy ``runs/create_instance`` (reference: ``S/services/fleets.py`` create_instance): one
+    PENDING cloud instance in an auto-created fleet; the instance reconciler provisions it from
+    the offers matching ``requirements``."""
+    offers = offers_services.get_offers_by_requirements(s, project, profile, requirements,
+                                                        exclude_not_available=True)
+    if not offers:
+        raise ServerClientError("No offers found for the requirements")
+    pool = pools_services.get_or_create_pool_by_name(s, project, profile.pool_name)
+    name = f"{profile.name or 'instance'}-{uuid.uuid4().hex[:6]}"
+    fleet = create_autocreated_fleet(s, project, name, profile, multinode=False)
+    inst = pools_services.create_instance_model(
+        s, project, pool, name=f"{fleet.name}-0", status=InstanceStatus.PENDING, fleet=fleet, instance_num=0,
+        profile=profile.model_dump_json(), requirements=requirements.model_dump_json(),
+        termination_idle_time=DEFAULT_FLEET_TERMINATION_IDLE_TIME, termination_policy="destroy-after-idle",
+        backend_data=json.dumps({"blocks": 1, "placement": None}),
+    )
+    s.flush()
+    scheduler.wake(scheduler.INSTANCES)
+    return pools_services.instance_model_to_instance(inst)

@@ -163,3 +163,149 @@ def create_instance_model(s: Session, project: ProjectModel, pool: PoolModel, na
     s.add(inst)
     s.flush()
     return inst
+
+
+# ---- legacy pool API (reference: S/services/pools.py:64-380, routers/pools.py; deprecated there) --
+def get_pool(s: Session, project: ProjectModel, name: str) -> Optional[PoolModel]:
+    return s.execute(select(PoolModel).where(PoolModel.project_id == project.id, PoolModel.name == name,
+                                             PoolModel.deleted == False)).scalar_one_or_none()  # noqa: E712
+
+
+def get_or_create_pool_by_name(s: Session, project: ProjectModel, name: Optional[str]) -> PoolModel:
+    if name is None:
+        if project.default_pool_id is not None:
+            pool = s.get(PoolModel, project.default_pool_id)
+            if pool is not None and not pool.deleted:
+                return pool
+        return get_or_create_default_pool(s, project)
+    pool = get_pool(s, project, name)
+    if pool is None:
+        pool = create_pool(s, project, name)
+    return pool
+
+
+def _pool_instances(pool: PoolModel) -> List[InstanceModel]:
+    return [i for i in pool.instances if not i.deleted]
+
+
+def pool_model_to_pool(project: ProjectModel, pool: PoolModel):
+    from dstack_amd.core.models.fleets import Pool
+
+    insts = _pool_instances(pool)
+    avail = sum(1 for i in insts if i.status in (InstanceStatus.IDLE.value, InstanceStatus.BUSY.value))
+    return Pool(name=pool.name, default=project.default_pool_id == pool.id, created_at=pool.created_at,
+                total_instances=len(insts), available_instances=avail)
+
+
+def list_project_pools(s: Session, project: ProjectModel):
+    pools = list(s.execute(select(PoolModel).where(PoolModel.project_id == project.id,
+                                                   PoolModel.deleted == False)).scalars())  # noqa: E712
+    if not pools:
+        pools = [get_or_create_default_pool(s, project)]
+    return [pool_model_to_pool(project, p) for p in pools]
+
+
+def create_pool(s: Session, project: ProjectModel, name: str) -> PoolModel:
+    from dstack_amd.core.errors import ResourceExistsError
+
+    if get_pool(s, project, name) is not None:
+        raise ResourceExistsError(f"Pool {name} exists")
+    pool = PoolModel(id=uuid.uuid4(), name=name, project_id=project.id)
+    s.add(pool)
+    s.flush()
+    if project.default_pool_id is None:
+        project.default_pool_id = pool.id
+    return pool
+
+
+def set_default_pool(s: Session, project: ProjectModel, name: str):
+    from dstack_amd.core.errors import ResourceNotExistsError
+
+    pool = get_pool(s, project, name)
+    if pool is None:
+        raise ResourceNotExistsError("Pool not found")
+    project.default_pool_id = pool.id
+
+
+def delete_pool(s: Session, project: ProjectModel, name: str):
+    from dstack_amd.core.errors import ResourceNotExistsError, ServerClientError
+
+    pool = get_pool(s, project, name)
+    if pool is None:
+        raise ResourceNotExistsError("Pool not found")
+    if any(i.status != InstanceStatus.TERMINATED.value for i in _pool_instances(pool)):
+        raise ServerClientError("Cannot delete pool with running instances")
+    pool.deleted = True
+    pool.deleted_at = get_current_datetime()
+    if project.default_pool_id == pool.id:
+        project.default_pool_id = None
+
+
+def remove_instance(s: Session, project: ProjectModel, pool_name: str, instance_name: str, force: bool):
+    """Mark a pool instance for termination (an instance running jobs only with ``force``)."""
+    from dstack_amd.core.errors import ResourceNotExistsError
+    from dstack_amd.server.background import scheduler
+
+    pool = get_pool(s, project, pool_name)
+    if pool is None:
+        raise ResourceNotExistsError("Pool not found")
+    done = False
+    for inst in _pool_instances(pool):
+        if inst.name == instance_name and (force or not inst.jobs):
+            inst.status = InstanceStatus.TERMINATING.value
+            done = True
+    if not done:
+        raise ResourceNotExistsError("Could not find instance to terminate")
+    scheduler.wake(scheduler.INSTANCES)
+
+
+def show_pool_instances(s: Session, project: ProjectModel, name: Optional[str]):
+    from dstack_amd.core.errors import ResourceNotExistsError
+    from dstack_amd.core.models.fleets import PoolInstances
+
+    if name is not None:
+        pool = get_pool(s, project, name)
+        if pool is None:
+            raise ResourceNotExistsError("Pool not found")
+    else:
+        pool = get_or_create_pool_by_name(s, project, None)
+    return PoolInstances(name=pool.name, instances=[instance_model_to_instance(i) for i in _pool_instances(pool)])
+
+
+def add_remote(s: Session, project: ProjectModel, pool_name: Optional[str], instance_name: Optional[str],
+               instance_network: Optional[str], region: Optional[str], host: str, port: int, ssh_user: str,
+               ssh_keys) -> Instance:
+    """Register an SSH host as a pool instance (PENDING -> the instance reconciler deploys the shim
+    and reads back host_info, exactly as for SSH-fleet hosts).  Idempotent per host/port/user."""
+    import ipaddress
+
+    from dstack_amd.core.errors import ServerClientError
+    from dstack_amd.core.models.instances import RemoteConnectionInfo
+    from dstack_amd.server.background import scheduler
+
+    if instance_network is not None:
+        try:
+            instance_network = str(ipaddress.IPv4Interface(instance_network).network)
+        except ValueError:
+            raise ServerClientError("Failed to parse network value")
+    insts = s.execute(select(InstanceModel).where(InstanceModel.project_id == project.id,
+                                                  InstanceModel.deleted == False)).scalars()  # noqa: E712
+    for inst in insts:
+        if inst.remote_connection_info:
+            rci = RemoteConnectionInfo.model_validate_json(inst.remote_connection_info)
+            if rci.host == host and rci.port == port and rci.ssh_user == ssh_user:
+                return instance_model_to_instance(inst)
+    pool = get_or_create_pool_by_name(s, project, pool_name)
+    if instance_name is None:
+        n = sum(1 for _ in _pool_instances(pool))
+        instance_name = f"{pool.name}-{n}"
+    rci = RemoteConnectionInfo(host=host, port=port, ssh_user=ssh_user, ssh_keys=ssh_keys)
+    inst = create_instance_model(
+        s, project, pool, name=instance_name, status=InstanceStatus.PENDING, backend=BackendType.REMOTE.value,
+        region=region or "remote", price=0.0, remote_connection_info=rci.model_dump_json(),
+        termination_idle_time=-1, termination_policy="dont-destroy",
+        backend_data=json.dumps({"blocks": 1, "internal_ip": None, "network": instance_network}),
+    )
+    s.flush()
+    scheduler.wake(scheduler.INSTANCES)
+    return instance_model_to_instance(inst)

@@ -236,3 +236,46 @@ def test_prometheus_metrics(client):
     assert r.status_code == 200
     assert 'dstack_runs{project="main",status="submitted"} 1' in r.text
     assert "# TYPE dstack_job_gpu_util_percent gauge" in r.text
+
+
+# ---- legacy pool API (reference routers/pools.py, routers/runs.py:183-219, deprecated) ----------
+def test_legacy_pools_crud(client):
+    r = client.post("/api/project/main/pool/create", json={"name": "p2"})
+    assert r.status_code == 200, r.text
+    assert client.post("/api/project/main/pool/create", json={"name": "p2"}).status_code == 400
+    names = {p["name"] for p in client.post("/api/project/main/pool/list").json()}
+    assert "p2" in names
+    assert client.post("/api/project/main/pool/set_default", json={"pool_name": "p2"}).status_code == 200
+    pools = {p["name"]: p for p in client.post("/api/project/main/pool/list").json()}
+    assert pools["p2"]["default"] is True
+    assert client.post("/api/project/main/pool/set_default", json={"pool_name": "nope"}).status_code == 400
+    r = client.post("/api/project/main/pool/add_remote", json={
+        "pool_name": "p2", "host": "10.0.0.7", "port": 22, "ssh_user": "ubuntu",
+        "ssh_keys": [{"public": "ssh-ed25519 AAAA", "private": "-----BEGIN KEY-----"}],
+        "instance_network": "10.0.0.0/24"})
+    assert r.status_code == 200, r.text
+    inst = r.json()
+    assert inst["status"] == "pending" and inst["backend"] == "remote"
+    # idempotent per host/port/user
+    again = client.post("/api/project/main/pool/add_remote", json={
+        "pool_name": "p2", "host": "10.0.0.7", "port": 22, "ssh_user": "ubuntu",
+        "ssh_keys": [{"public": "ssh-ed25519 AAAA"}]}).json()
+    assert again["id"] == inst["id"]
+    shown = client.post("/api/project/main/pool/show", json={"name": "p2"}).json()
+    assert [i["name"] for i in shown["instances"]] == [inst["name"]]
+    # a pool with live instances cannot be deleted; remove the instance first
+    assert client.post("/api/project/main/pool/delete", json={"name": "p2"}).status_code == 400
+    r = client.post("/api/project/main/pool/remove", json={"pool_name": "p2", "instance_name": inst["name"]})
+    assert r.status_code == 200, r.text
+    shown = client.post("/api/project/main/pool/show", json={"name": "p2"}).json()
+    assert shown["instances"][0]["status"] == "terminating"
+    bad = client.post("/api/project/main/pool/add_remote", json={"host": " ", "ssh_user": "u", "ssh_keys": []})
+    assert bad.status_code == 400
+
+
+def test_legacy_get_offers(client):
+    r = client.post("/api/project/main/runs/get_offers", json={
+        "profile": {"name": "default"}, "requirements": {"resources": {"cpu": "1..", "memory": "0.1GB.."}}})
+    assert r.status_code == 200, r.text
+    body = r.json()
+    assert body["pool_name"] and isinstance(body["instances"], list)
