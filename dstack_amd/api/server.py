@@ -17,11 +17,13 @@ from pydantic import BaseModel, TypeAdapter
 
 from dstack_amd import __version__
 from dstack_amd.core.errors import ClientError, ServerClientError, URLNotFoundError
-from dstack_amd.core.models.fleets import Fleet, FleetPlan, FleetSpec, Instance
+from dstack_amd.core.models.fleets import Fleet, FleetPlan, FleetSpec, Instance, Pool, PoolInstances
+from dstack_amd.core.models.instances import SSHKey
+from dstack_amd.core.models.profiles import Profile
 from dstack_amd.core.models.gateways import Gateway, GatewayConfiguration
 from dstack_amd.core.models.logs import JobMetrics, JobSubmissionLogs
 from dstack_amd.core.models.repos import RepoHead
-from dstack_amd.core.models.runs import ApplyRunPlanInput, Run, RunPlan, RunSpec
+from dstack_amd.core.models.runs import ApplyRunPlanInput, PoolInstanceOffers, Requirements, Run, RunPlan, RunSpec
 from dstack_amd.core.models.users import Project, ServerInfo, User, UserWithCreds
 from dstack_amd.core.models.volumes import Volume, VolumeConfiguration
 
@@ -329,11 +331,43 @@ class _Gateways(_Group):
 
 
 class _Pool(_Group):
-    def list(self, project_name: str) -> list:
-        return self._c.post(f"/api/project/{project_name}/pool/list")
+    """Legacy pool API (deprecated in the reference in favour of fleets; kept for old clients)."""
 
-    def show(self, project_name: str) -> dict:
-        return self._c.post(f"/api/project/{project_name}/pool/show")
+    def list(self, project_name: str) -> List[Pool]:
+        return self._c.post(f"/api/project/{project_name}/pool/list", model=List[Pool])
+
+    def show(self, project_name: str, pool_name: Optional[str] = None) -> PoolInstances:
+        return self._c.post(f"/api/project/{project_name}/pool/show", {"name": pool_name}, model=PoolInstances)
+
+    def create(self, project_name: str, pool_name: str):
+        self._c.post(f"/api/project/{project_name}/pool/create", {"name": pool_name})
+
+    def delete(self, project_name: str, pool_name: str, force: bool = False):
+        self._c.post(f"/api/project/{project_name}/pool/delete", {"name": pool_name, "force": force})
+
+    def set_default(self, project_name: str, pool_name: str):
+        self._c.post(f"/api/project/{project_name}/pool/set_default", {"pool_name": pool_name})
+
+    def remove(self, project_name: str, pool_name: str, instance_name: str, force: bool = False):
+        self._c.post(f"/api/project/{project_name}/pool/remove",
+                     {"pool_name": pool_name, "instance_name": instance_name, "force": force})
+
+    def add_remote(self, project_name: str, host: str, port: int, ssh_user: str, ssh_keys: List[SSHKey],
+                   pool_name: Optional[str] = None, instance_name: Optional[str] = None,
+                   region: Optional[str] = None, instance_network: Optional[str] = None) -> Instance:
+        return self._c.post(f"/api/project/{project_name}/pool/add_remote", {
+            "pool_name": pool_name, "instance_name": instance_name, "instance_network": instance_network,
+            "region": region, "host": host, "port": port, "ssh_user": ssh_user,
+            "ssh_keys": [_dump(k) for k in ssh_keys]}, model=Instance)
+
+    def get_offers(self, project_name: str, profile: Profile, requirements: Requirements) -> PoolInstanceOffers:
+        return self._c.post(f"/api/project/{project_name}/runs/get_offers",
+                            {"profile": _dump(profile), "requirements": _dump(requirements)},
+                            model=PoolInstanceOffers)
+
+    def create_instance(self, project_name: str, profile: Profile, requirements: Requirements) -> Instance:
+        return self._c.post(f"/api/project/{project_name}/runs/create_instance",
+                            {"profile": _dump(profile), "requirements": _dump(requirements)}, model=Instance)
 
 
 def client_from_env_or_config(project: Optional[str] = None) -> "tuple[APIClient, str]":

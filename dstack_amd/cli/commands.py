@@ -485,28 +485,226 @@ def cmd_gateway_update(args) -> int:
 
 
 def register_pool(sub):
-    p = sub.add_parser("pool", help="(Deprecated: use fleets) list pool instances")
+    """``dstack pool`` (reference: cli/commands/pool.py; deprecated there in favour of fleets)."""
+    p = sub.add_parser("pool", help="(Deprecated: use fleets) manage pools and pool instances")
     add_project_arg(p)
-    p.set_defaults(func=cmd_pool)
+    s = p.add_subparsers(dest="pool_cmd")
+    lp = s.add_parser("list", help="List pools")
+    lp.add_argument("-v", "--verbose", action="store_true")
+    lp.set_defaults(func=cmd_pool_list)
+    cp = s.add_parser("create", help="Create a pool")
+    cp.add_argument("-n", "--name", dest="pool_name", required=True)
+    cp.set_defaults(func=cmd_pool_create)
+    dp = s.add_parser("delete", help="Delete a pool")
+    dp.add_argument("-n", "--name", dest="pool_name", required=True)
+    dp.set_defaults(func=cmd_pool_delete)
+    pp = s.add_parser("ps", help="Show pool instances")
+    pp.add_argument("--pool", dest="pool_name")
+    pp.add_argument("-w", "--watch", action="store_true")
+    pp.set_defaults(func=cmd_pool_ps)
+    ap = s.add_parser("add", help="Add a cloud instance to the pool")
+    ap.add_argument("-y", "--yes", action="store_true")
+    ap.add_argument("--max-offers", type=int, default=3)
+    ap.add_argument("--gpu", help="GPU requirement, e.g. MI355X:8")
+    ap.add_argument("--cpu", help="CPU requirement, e.g. 32..")
+    ap.add_argument("--memory", help="Memory requirement, e.g. 256GB..")
+    ap.add_argument("--disk", help="Disk requirement, e.g. 500GB..")
+    ap.add_argument("--pool", dest="pool_name")
+    ap.add_argument("--max-price", type=float)
+    ap.add_argument("-b", "--backend", action="append", dest="backends")
+    ap.add_argument("-r", "--region", action="append", dest="regions")
+    ap.add_argument("--spot-policy", dest="spot_policy")
+    ap.set_defaults(func=cmd_pool_add)
+    rp = s.add_parser("rm", aliases=["remove"], help="Remove an instance from the pool")
+    rp.add_argument("instance_name")
+    rp.add_argument("--pool", dest="pool_name")
+    rp.add_argument("--force", action="store_true")
+    rp.add_argument("-y", "--yes", action="store_true")
+    rp.set_defaults(func=cmd_pool_rm)
+    sp = s.add_parser("set-default", help="Set the project's default pool")
+    sp.add_argument("--pool", dest="pool_name", required=True)
+    sp.set_defaults(func=cmd_pool_set_default)
+    hp = s.add_parser("add-ssh", help="Add an SSH host (e.g. an on-prem MI355X node) to the pool")
+    hp.add_argument("destination", help="[user@]host")
+    hp.add_argument("-i", dest="ssh_identity_file", required=True, metavar="SSH_PRIVATE_KEY")
+    hp.add_argument("-p", dest="ssh_port", type=int)
+    hp.add_argument("-l", dest="login_name")
+    hp.add_argument("--region")
+    hp.add_argument("--pool", dest="pool_name")
+    hp.add_argument("--name", dest="instance_name")
+    hp.add_argument("--network", help="Network for multinode setups, <ip>/<mask>")
+    hp.set_defaults(func=cmd_pool_add_ssh)
+    p.set_defaults(func=cmd_pool_ps, pool_name=None, watch=False)
 
 
-def cmd_pool(args) -> int:
+def _instances_table(instances):
     from rich.table import Table
 
-    client = _client(args)
+    from dstack_amd.cli.utils import pretty_date
+
     t = Table(box=None, header_style="bold")
     for col in ("INSTANCE", "BACKEND", "RESOURCES", "PRICE", "STATUS", "CREATED"):
         t.add_column(col)
-    from dstack_amd.cli.utils import pretty_date
-
-    for inst in client.api.instances.list([client.project]):
+    for inst in instances:
         t.add_row(inst.name, f"{inst.backend.value if inst.backend else ''} ({inst.region or ''})",
                   inst.instance_type.resources.pretty_format() if inst.instance_type else "",
                   f"${inst.price:.4g}" if inst.price is not None else "", inst.status.value, pretty_date(inst.created))
+    return t
+
+
+def cmd_pool_list(args) -> int:
+    from rich.table import Table
+
+    from dstack_amd.cli.utils import pretty_date
+
+    client = _client(args)
+    t = Table(box=None, header_style="bold")
+    for col in ("NAME", "DEFAULT", "INSTANCES", "AVAILABLE", "CREATED"):
+        t.add_column(col)
+    for pool in client.api.pool.list(client.project):
+        t.add_row(pool.name, "yes" if pool.default else "", str(pool.total_instances), str(pool.available_instances),
+                  pretty_date(pool.created_at))
     print_table(t)
     return 0
 
 
+def cmd_pool_create(args) -> int:
+    client = _client(args)
+    client.api.pool.create(client.project, args.pool_name)
+    console.print(f"Pool {args.pool_name!r} created")
+    return 0
+
+
+def cmd_pool_delete(args) -> int:
+    client = _client(args)
+    client.api.pool.delete(client.project, args.pool_name, False)
+    console.print(f"Pool {args.pool_name!r} removed")
+    return 0
+
+
+def cmd_pool_ps(args) -> int:
+    import time
+
+    client = _client(args)
+    while True:
+        pool = client.api.pool.show(client.project, args.pool_name)
+        console.print(f" Pool name  {pool.name}\n")
+        print_table(_instances_table(pool.instances))
+        if not args.watch:
+            return 0
+        time.sleep(2)
+
+
+def cmd_pool_rm(args) -> int:
+    client = _client(args)
+    pool = client.api.pool.show(client.project, args.pool_name)
+    if not any(i.name == args.instance_name for i in pool.instances):
+        raise CLIError(f"Instance {args.instance_name!r} not found in pool {pool.name!r}")
+    if args.yes or confirm_ask(f"Remove instance [code]{args.instance_name}[/]?"):
+        client.api.pool.remove(client.project, pool.name, args.instance_name, args.force)
+        console.print(f"Instance {args.instance_name!r} removed")
+    return 0
+
+
+def cmd_pool_set_default(args) -> int:
+    client = _client(args)
+    client.api.pool.set_default(client.project, args.pool_name)
+    return 0
+
+
+def _pool_requirements(args):
+    from dstack_amd.core.models.profiles import Profile, SpotPolicy
+    from dstack_amd.core.models.resources import ResourcesSpec
+    from dstack_amd.core.models.runs import Requirements, get_policy_map
+
+    res = {}
+    for k in ("gpu", "cpu", "memory", "disk"):
+        if getattr(args, k, None):
+            res[k] = getattr(args, k)
+    spot = SpotPolicy(args.spot_policy) if args.spot_policy else None
+    profile = Profile(name="pool-add", backends=args.backends, regions=args.regions, max_price=args.max_price,
+                      spot_policy=spot, pool_name=args.pool_name)
+    req = Requirements(resources=ResourcesSpec.model_validate(res), max_price=args.max_price,
+                       spot=get_policy_map(spot, SpotPolicy.ONDEMAND))
+    return profile, req
+
+
+def cmd_pool_add(args) -> int:
+    from rich.table import Table
+
+    client = _client(args)
+    profile, req = _pool_requirements(args)
+    offers = client.api.pool.get_offers(client.project, profile, req)
+    if not offers.instances:
+        raise CLIError("No offers match the requirements")
+    t = Table(box=None, header_style="bold")
+    for col in ("#", "BACKEND", "REGION", "INSTANCE", "RESOURCES", "PRICE"):
+        t.add_column(col)
+    for i, o in enumerate(offers.instances[: args.max_offers], 1):
+        t.add_row(str(i), o.backend.value, o.region, o.instance.name, o.instance.resources.pretty_format(),
+                  f"${o.price:.4g}")
+    print_table(t)
+    if not (args.yes or confirm_ask(f"Add an instance to pool [code]{offers.pool_name}[/]?")):
+        return 0
+    inst = client.api.pool.create_instance(client.project, profile, req)
+    print_table(_instances_table([inst]))
+    return 0
+
+
+def cmd_pool_add_ssh(args) -> int:
+    from dstack_amd.core.models.instances import SSHKey
+
+    client = _client(args)
+    user, _, host = args.destination.rpartition("@")
+    user = args.login_name or user or "root"
+    key_path = os.path.expanduser(args.ssh_identity_file)
+    with open(key_path) as f:
+        private = f.read()
+    public = ""
+    if os.path.exists(key_path + ".pub"):
+        with open(key_path + ".pub") as f:
+            public = f.read().strip()
+    inst = client.api.pool.add_remote(client.project, host=host, port=args.ssh_port or 22, ssh_user=user,
+                                      ssh_keys=[SSHKey(public=public, private=private)], pool_name=args.pool_name,
+                                      instance_name=args.instance_name, region=args.region,
+                                      instance_network=args.network)
+    print_table(_instances_table([inst]))
+    return 0
+
+
+# ---- run (deprecated alias of apply for run configurations; reference cli/commands/run.py) ------
+def register_run(sub):
+    from dstack_amd.cli.configurators import RunConfigurator, register_repo_args
+
+    p = sub.add_parser("run", help="(Deprecated: use apply) run a configuration")
+    add_project_arg(p)
+    p.add_argument("working_dir")
+    p.add_argument("-f", "--file", dest="configuration_file", help="Configuration file (default: .dstack.yml)")
+    p.add_argument("-y", "--yes", action="store_true", help="Do not ask for confirmation")
+    p.add_argument("-d", "--detach", action="store_true", help="Exit right after submitting")
+    p.add_argument("--force", action="store_true", help=argparse.SUPPRESS)
+    register_repo_args(p)
+    RunConfigurator.register_args(p)
+    p.set_defaults(func=cmd_run)
+
+
+def cmd_run(args) -> int:
+    from dstack_amd.cli.configurators import configurator_for, find_default_configuration, load_configuration
+
+    console.print("[yellow]dstack run is deprecated in favor of dstack apply[/]")
+    base = os.path.abspath(args.working_dir)
+    path = args.configuration_file or find_default_configuration(base)
+    if path is None:
+        raise CLIError(f"No configuration file given (-f) and no .dstack.yml in {base}")
+    conf = load_configuration(path)
+    if conf.type not in ("task", "service", "dev-environment"):
+        raise CLIError(f"dstack run only runs task/service/dev-environment configurations, got {conf.type}")
+    if getattr(args, "repo", None) is None:
+        args.repo = base
+    client = _client(args)
+    return configurator_for(conf.type).apply(client, conf, path, args)
+
+
 REGISTRARS = [register_server, register_config, register_init, register_apply, register_delete, register_ps,
               register_logs, register_stop, register_attach, register_stats, register_fleet, register_volume,
-              register_gateway, register_pool]
+              register_gateway, register_pool, register_run]

@@ -259,3 +259,34 @@ def test_ssh_fleet_deploy_flow(tmp_path, monkeypatch):
                 os.kill(int(pid_file.read_text().strip()), signal.SIGTERM)
             except (ProcessLookupError, ValueError):
                 pass
+
+
+def test_cli_deprecated_run_and_pool(server, tmp_path):
+    """``dstack run DIR`` (deprecated alias of apply) and the ``dstack pool`` subcommands."""
+    proj = tmp_path / "proj"
+    proj.mkdir()
+    (proj / ".dstack.yml").write_text("type: task\nname: e2e-run\ncommands: [\"echo via-run\"]\n")
+    env = dict(os.environ, DSTACK_SERVER_URL=server.url, DSTACK_TOKEN=server.token,
+               DSTACK_DIR=str(tmp_path / "home"), PYTHONPATH=REPO)
+    dstack = [sys.executable, "-m", "dstack_amd"]
+    r = subprocess.run(dstack + ["run", str(proj), "-y"], cwd=tmp_path, env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "via-run" in r.stdout and "deprecated" in r.stdout
+    r = subprocess.run(dstack + ["pool", "create", "-n", "cli-pool"], env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    r = subprocess.run(dstack + ["pool", "list"], env=env, capture_output=True, text=True, timeout=60)
+    assert "cli-pool" in r.stdout, r.stdout + r.stderr
+    key = tmp_path / "id_test"
+    key.write_text("-----BEGIN OPENSSH PRIVATE KEY-----\nx\n-----END OPENSSH PRIVATE KEY-----\n")
+    (tmp_path / "id_test.pub").write_text("ssh-ed25519 AAAATEST test\n")
+    r = subprocess.run(dstack + ["pool", "add-ssh", "ubuntu@192.0.2.10", "-i", str(key), "--pool", "cli-pool",
+                                 "--name", "onprem-0"], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    r = subprocess.run(dstack + ["pool", "ps", "--pool", "cli-pool"], env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert "onprem-0" in r.stdout, r.stdout + r.stderr
+    r = subprocess.run(dstack + ["pool", "rm", "onprem-0", "--pool", "cli-pool", "-y", "--force"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
