@@ -13,6 +13,7 @@ hipError_t dsa_rmsnorm_bwd(const void*, const void*, const void*, const float*, 
                            float*, int, int, hipStream_t);
 hipError_t dsa_swiglu_fwd(const void*, void*, int, int, hipStream_t);
 bool dsa_transpose2d_supported(int, int);
+hipError_t dsa_swiglu_fwd_t(const void*, void*, void*, int, int, hipStream_t);
 hipError_t dsa_transpose2d(const void*, void*, int, int, hipStream_t);
 hipError_t dsa_swiglu_bwd(const void*, const void*, void*, int, int, hipStream_t);
 hipError_t dsa_rope_qkv(const void*, void*, const float*, const float*, int, int, int, int, int, int,
@@ -114,6 +115,20 @@ torch::Tensor swiglu_fwd(torch::Tensor gu) {
   auto out = torch::empty(sizes, gu.options());
   check(dsa_swiglu_fwd(gu.data_ptr(), out.data_ptr(), rows, F, stream()), "swiglu_fwd");
   return out;
+}
+
+// (a, aT): a = silu(gate) * up [..., F] and its transpose aT [F, T] (T = rows)
+std::vector<torch::Tensor> swiglu_fwd_t(torch::Tensor gu) {
+  check_bf16(gu, "gu");
+  const int F = gu.size(-1) / 2;
+  const int T = gu.numel() / gu.size(-1);
+  TORCH_CHECK(T % 128 == 0 && F % 64 == 0, "swiglu_fwd_t: rows % 128 and F % 64 must be 0");
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto out = torch::empty(sizes, gu.options());
+  auto outT = torch::empty({F, T}, gu.options());
+  check(dsa_swiglu_fwd_t(gu.data_ptr(), out.data_ptr(), outT.data_ptr(), T, F, stream()), "swiglu_fwd_t");
+  return {out, outT};
 }
 
 torch::Tensor swiglu_bwd(torch::Tensor da, torch::Tensor gu) {
@@ -234,6 +249,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rms_norm_bwd", &rms_norm_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("transpose2d", &transpose2d);
+  m.def("swiglu_fwd_t", &swiglu_fwd_t);
   m.def("transpose2d_supported", &transpose2d_supported);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_qkv", &rope_qkv);

@@ -502,6 +502,56 @@ __global__ __launch_bounds__(256) void transpose2d_kernel(const bf16_t* __restri
   }
 }
 
+// SwiGLU forward that also writes the transposed output aT[F, T] (the down projection's
+// token-contiguous weight-gradient operand, so backward needs no separate transpose of a: the
+// extra 2 B/element write replaces a 4 B/element transpose pass).  Same 128 x 64 tiling and
+// ds_read_b64_tr_b16 gather as transpose2d_kernel.
+__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restrict__ gu,
+                                                           bf16_t* __restrict__ out,
+                                                           bf16_t* __restrict__ outT, int T, int F) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[TR_R * TR_P];
+  const int c0 = blockIdx.x * TR_C, r0 = blockIdx.y * TR_R;
+  const int t = threadIdx.x;
+  us8 gv[4], uv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t, r = idx >> 3, ch = idx & 7;
+    const bf16_t* src = gu + (size_t)(r0 + r) * 2 * F + c0 + ch * 8;
+    gv[i] = *reinterpret_cast<const us8*>(src);
+    uv[i] = *reinterpret_cast<const us8*>(src + F);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t, r = idx >> 3, ch = idx & 7;
+    float g[8], u[8], o[8];
+    unpack8(gv[i], g);
+    unpack8(uv[i], u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = silu_f(g[k]) * u[k];
+    const us8 a = pack8(o);
+    *reinterpret_cast<us8*>(out + (size_t)(r0 + r) * F + c0 + ch * 8) = a;
+    *reinterpret_cast<us8*>(tile + r * TR_P + ch * 8) = a;
+  }
+  __syncthreads();
+  const int G = t >> 4, lane16 = t & 15, q = (t >> 2) & 3, p = t & 3;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int u = pass * 16 + G, cb = u & 3, rk = u >> 2;
+    const bf16_t* src = tile + (rk * 8 + q) * TR_P + cb * 16 + 4 * p;
+    const dsa::bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, src));
+    const dsa::bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, src + 4 * TR_P));
+    const dsa::bf16x8 o = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<dsa::bf16x8*>(outT + (size_t)(c0 + cb * 16 + lane16) * T + r0 + rk * 8) = o;
+  }
+}
+
+extern "C" hipError_t dsa_swiglu_fwd_t(const void* gu, void* out, void* outT, int T, int F, hipStream_t st) {
+  if (T % TR_R || F % TR_C) return hipErrorInvalidValue;
+  swiglu_fwd_t_kernel<<<dim3(F / TR_C, T / TR_R), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)out,
+                                                                (bf16_t*)outT, T, F);
+  return hipGetLastError();
+}
+
 extern "C" bool dsa_transpose2d_supported(int R, int C) { return R % TR_R == 0 && C % TR_C == 0; }
 
 extern "C" hipError_t dsa_transpose2d(const void* in, void* out, int R, int C, hipStream_t st) {

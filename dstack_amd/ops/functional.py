@@ -71,21 +71,36 @@ def add_rms_norm(x: torch.Tensor, delta: torch.Tensor, w: torch.Tensor, eps: flo
 # ----------------------------------------------------------------------------------------------
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, with_t):
         C = _ext.require()
         ctx.save_for_backward(gu)
-        return C.swiglu_fwd(gu)
+        if with_t:
+            a, aT = C.swiglu_fwd_t(gu)
+            ctx.mark_non_differentiable(aT)
+            return a, aT
+        return C.swiglu_fwd(gu), None
 
     @staticmethod
-    def backward(ctx, da):
+    def backward(ctx, da, _daT):
         C = _ext.require()
         (gu,) = ctx.saved_tensors
-        return C.swiglu_bwd(da.contiguous(), gu)
+        return C.swiglu_bwd(da.contiguous(), gu), None
 
 
 def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    """silu(gate) * up of the fused [gate | up] projection.  On the HIP path with token-contiguous
+    weight gradients (``DSTACK_AMD_WGRAD=auto``) the kernel also writes the transposed output,
+    attached as ``a._dsa_t`` [F, T]: ``linear`` then saves only that copy for the down projection's
+    weight gradient (memory-neutral) and backward skips the transpose of ``a``."""
     if _ext.use_hip(gu):
-        return _SwiGLU.apply(gu.contiguous())
+        gu = gu.contiguous()
+        T = gu.numel() // gu.shape[-1]
+        F = gu.shape[-1] // 2
+        with_t = _wgrad_mode() == "auto" and T % 128 == 0 and F % 64 == 0
+        a, aT = _SwiGLU.apply(gu, with_t)
+        if aT is not None:
+            a._dsa_t = aT
+        return a
     return ref.swiglu(gu)
 
 
@@ -177,20 +192,27 @@ class _Linear(torch.autograd.Function):
     flat gradient buffer (``w._dsa_grad_sink``): the first micro-batch uses beta=0 (no memset of
     the buffer), later ones accumulate with beta=1 in the hipBLASLt epilogue — no separate
     AccumulateGrad add kernel, no zero-fill, one pass over the gradient instead of three.
-    The dW GEMM's operands are re-laid out token-contiguous first (``wgrad_operands``)."""
+    The dW GEMM's operands are re-laid out token-contiguous first (``wgrad_operands``); when the
+    producer of ``x`` already wrote ``x^T`` (``x._dsa_t``, e.g. SwiGLU) only that copy is saved."""
 
     @staticmethod
     def forward(ctx, x, w):
-        ctx.save_for_backward(x, w)
+        xT = getattr(x, "_dsa_t", None)
+        ctx.x_is_t = xT is not None
+        ctx.save_for_backward(xT if ctx.x_is_t else x, w)
         return x @ w.t()
 
     @staticmethod
     def backward(ctx, g):
-        x, w = ctx.saved_tensors
+        xs, w = ctx.saved_tensors
         gx = g @ w if ctx.needs_input_grad[0] else None
         if not ctx.needs_input_grad[1]:
             return gx, None
-        a, b = wgrad_operands(g.reshape(-1, g.shape[-1]), x.reshape(-1, x.shape[-1]))
+        g2 = g.reshape(-1, g.shape[-1])
+        if ctx.x_is_t:
+            a, b = wgrad_operands(g2, None, xT=xs)
+        else:
+            a, b = wgrad_operands(g2, xs.reshape(-1, xs.shape[-1]))
         sink = getattr(w, "_dsa_grad_sink", None)
         if sink is None:
             return gx, a @ b
@@ -202,8 +224,9 @@ def _wgrad_mode() -> str:
     return os.environ.get("DSTACK_AMD_WGRAD", "auto").lower()
 
 
-def wgrad_operands(g2: torch.Tensor, x2: torch.Tensor):
-    """Operands (a [P, T], b [T, Q]) with dW = a @ b for g2 [T, P], x2 [T, Q].
+def wgrad_operands(g2: torch.Tensor, x2, xT=None):
+    """Operands (a [P, T], b [T, Q]) with dW = a @ b for g2 [T, P] and x2 [T, Q] (or its transpose
+    ``xT`` [Q, T] when the producer already wrote it).
 
     hipBLASLt runs dW = g^T x at ~1.0-1.1 PFLOP/s on MI355X when both operands are token-major
     (the reduction dimension is the strided one for both) and at 1.3-1.56 PFLOP/s when they are
@@ -211,13 +234,14 @@ def wgrad_operands(g2: torch.Tensor, x2: torch.Tensor):
     transposed by the HIP transpose kernel (T x Q, a few % of the GEMM's time) and g too when it
     is no larger than x (down/o projections; the gate_up and lm_head gradients are 3.5-31x larger
     than their inputs and stay token-major).  ``DSTACK_AMD_WGRAD=strided`` keeps the old layout."""
-    a, b = g2.t(), x2
-    if not (_ext.use_hip(x2) and _wgrad_mode() == "auto"):
+    T, P = g2.shape
+    Q = xT.shape[0] if xT is not None else x2.shape[1]
+    a = g2.t()
+    b = xT.t() if xT is not None else x2
+    if not (_ext.use_hip(g2) and _wgrad_mode() == "auto"):
         return a, b
     C = _ext.require()
-    T, P = g2.shape
-    Q = x2.shape[1]
-    if x2.is_contiguous() and C.transpose2d_supported(T, Q):
+    if xT is None and x2.is_contiguous() and C.transpose2d_supported(T, Q):
         b = C.transpose2d(x2).t()
     if P <= Q and g2.is_contiguous() and C.transpose2d_supported(T, P):
         a = C.transpose2d(g2)

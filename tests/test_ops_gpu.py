@@ -305,3 +305,31 @@ def test_linear_wgrad_layouts_agree(gpu, T, P, Q, monkeypatch):
     for mode, (_, gw) in grads.items():
         assert ((gw.float() - refw).norm() / refw.norm()).item() < 4e-3, mode
     assert torch.equal(grads["auto"][0], grads["strided"][0])
+
+
+def test_swiglu_fwd_t_matches(gpu):
+    Cx = _ext.require()
+    gu = _rand(256, 2 * 192, device=gpu, seed=12)
+    a, aT = Cx.swiglu_fwd_t(gu)
+    assert torch.equal(a, Cx.swiglu_fwd(gu))
+    assert torch.equal(aT, a.t().contiguous())
+
+
+def test_swiglu_down_chain_wgrad_modes_agree(gpu, monkeypatch):
+    """swiglu -> linear(down): the fused transposed SwiGLU output feeding the down projection's
+    weight gradient gives the same gradients as the token-major path."""
+    T, F, D = 256, 192, 128
+    gu = _rand(T, 2 * F, device=gpu, seed=13).requires_grad_()
+    w = _rand(D, F, device=gpu, seed=14, scale=0.05).requires_grad_()
+    g = _rand(T, D, device=gpu, seed=15)
+    res = {}
+    for mode in ("auto", "strided"):
+        monkeypatch.setenv("DSTACK_AMD_WGRAD", mode)
+        gu.grad = w.grad = None
+        a = ops.swiglu(gu)
+        assert hasattr(a, "_dsa_t") == (mode == "auto")
+        ops.linear(a, w).backward(g)
+        res[mode] = (gu.grad.clone(), w.grad.clone())
+    assert torch.equal(res["auto"][0], res["strided"][0])
+    ra, rs = res["auto"][1].float(), res["strided"][1].float()
+    assert ((ra - rs).norm() / rs.norm()).item() < 4e-3
