@@ -1,0 +1,57 @@
+"""The headline metric end to end on a GPU host: a dstack-amd server (local backend = native
+dstack-shim process driver + dstack-runner on this host) receives the Llama-3-8B training task
+through the public API (what ``dstack apply`` does), the shim grants a GPU (HIP_VISIBLE_DEVICES),
+the runner starts ``bench.py`` as the job, and the tokens/s line is read back from the job's logs.
+
+Prints one JSON line: cold start of THIS task (submit -> running / first log), the job's own bench
+result, and the wall time from submit to done.  The parent never touches the GPU (it only runs the
+server and reads logs), so the job process is the only GPU user."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from dstack_amd.api import GPU, Resources, Task
+    from dstack_amd.server.testing import ServerProcess
+
+    steps = os.environ.get("E2E_STEPS", "5")
+    cmd = (f"echo HIP_VISIBLE_DEVICES=$HIP_VISIBLE_DEVICES && cd {ROOT} && "
+           f"python bench.py --steps {steps} --warmup 2 --no-coldstart")
+    with ServerProcess() as srv:
+        client = srv.client()
+        conf = Task(name="llama3-8b-e2e", commands=[cmd], resources=Resources(gpu=GPU(count=1)))
+        t0 = time.time()
+        run = client.runs.submit(conf)
+        run.wait(timeout=float(os.environ.get("E2E_TIMEOUT", "600")), poll=0.5)
+        wall = time.time() - t0
+        logs = b"".join(run.logs()).decode(errors="replace")
+        sub = run.model.jobs[0].job_submissions[-1]
+        t = sub.timings or {}
+        ts = t.get("submitted", t0)
+        bench = None
+        for line in logs.splitlines():
+            if line.startswith("{") and '"metric"' in line:
+                bench = json.loads(line)
+        out = {
+            "status": sub.status.value,
+            "exit_status": sub.exit_status,
+            "gpu_env": [ln for ln in logs.splitlines() if ln.startswith("HIP_VISIBLE_DEVICES")][:1],
+            "submit_to_running_s": (t["running"] - ts) if "running" in t else None,
+            "submit_to_first_log_s": (t["first_log"] - ts) if "first_log" in t else None,
+            "submit_to_done_s": wall,
+            "job_bench": bench,
+        }
+        if bench is None:
+            out["log_tail"] = logs[-3000:]
+            out["server_log_tail"] = srv.log()[-3000:]
+        print(json.dumps(out), flush=True)
+        return 0 if bench is not None else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
