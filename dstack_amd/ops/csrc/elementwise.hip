@@ -433,7 +433,17 @@ __global__ __launch_bounds__(256) void adamw_kernel(bf16_t* __restrict__ param,
 // ================================================================================================
 // host launchers (raw pointers + stream; the torch binding lives in bindings.cpp)
 // ================================================================================================
-static inline int grid_for(size_t work, int block, int cap = 256 * 16) {
+// Grid for a grid-stride elementwise kernel: uncapped by default, i.e. one work item per thread:
+// blocks are then dispatched in address order and the chip streams memory front to back (a plain
+// copy measured 6.18 TB/s that way vs 4.2-4.8 TB/s with 8-32 resident blocks per CU striding
+// across the buffer, tools/diag/hbm_variants.hip; same box: SwiGLU fwd 139 -> 123 us, bwd 225 ->
+// 209 us, AdamW 6.22 -> 6.49 TB/s, profiles/grid_cap_r1q.txt).  DSTACK_AMD_GRID_CAP=N caps it.
+static inline int grid_for(size_t work, int block, int cap = 0x7fffffff) {
+  static const long env_cap = [] {
+    const char* v = getenv("DSTACK_AMD_GRID_CAP");
+    return v ? atol(v) : -1L;
+  }();
+  if (env_cap >= 0) cap = env_cap == 0 ? 0x7fffffff : (int)env_cap;
   size_t g = (work + block - 1) / block;
   if (g > (size_t)cap) g = cap;
   if (g < 1) g = 1;
@@ -652,7 +662,7 @@ extern "C" hipError_t dsa_adamw(void* param, const void* grad, float* master, fl
   // slots and just serialises the two (r1g trace: dK/dV 1.13 -> 2.3 ms while AdamW ran).  Measured
   // same box (tools/run_r1l.sh, ms/step): full grid 799, 64 blocks 807, 32 843, 16 956, no
   // overlap 802 -- per-CU HBM bandwidth is too low for a small persistent grid, so 0 stays default
-  const int cap = max_blocks > 0 ? max_blocks : 256 * 8;
+  const int cap = max_blocks > 0 ? max_blocks : 0x7fffffff;  // (DSTACK_AMD_GRID_CAP overrides)
   adamw_kernel<<<grid_for(n / 8 + 1, 256, cap), 256, 0, st>>>(
       (bf16_t*)param, (const bf16_t*)grad, master, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
   return hipGetLastError();

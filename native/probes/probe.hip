@@ -2,9 +2,9 @@
 //
 //   dstack-probe [--quick] [--json] [--hbm] [--mfma] [--xgmi] [--rccl] [--device N]
 //
-// * HBM:  streaming copy over 2 x 1 GiB buffers, 16-byte (dwordx4) loads/stores, grid-stride,
-//         grid = 8 blocks/CU -> achieved TB/s (MI355X measured ceiling ~6.3 TB/s, spec 8).
-// * MFMA: register-resident bf16 (v_mfma_f32_32x32x16_bf16) and fp8 (32x32x16_fp8_fp8) loops,
+// * HBM:  streaming copy over 2 x 1 GiB buffers, 16-byte (dwordx4) loads/stores, one element per
+//         thread over a full grid -> achieved TB/s (MI355X measured ceiling ~6.3 TB/s, spec 8).
+// * MFMA: register-resident bf16 (v_mfma_f32_32x32x16_bf16) and fp8 (block-scaled 32x32x64 f8f6f4) loops,
 //         4 independent accumulators per wave, 4 waves per CU on every CU -> dense TFLOPS and the
 //         implied clock; a throttled or faulty GPU shows up as a low number.
 // * xGMI: hipMemcpyPeerAsync of 256 MiB for every ordered GPU pair -> GB/s matrix (a healthy
@@ -33,9 +33,13 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------------------------------------
+// One 16-byte element per thread over a full grid (n/256 blocks): blocks are dispatched in address
+// order, so the chip streams memory front to back.  Measured on MI355X (tools/diag/hbm_variants.hip,
+// 1 GiB copy): 6.18 TB/s, vs 4.2-4.8 TB/s for grid-stride loops (8-32 blocks/CU, 1 or 4 loads in
+// flight, nt loads) whose every iteration jumps across the whole buffer.
 __global__ __launch_bounds__(256) void copy_kernel(const f4* __restrict__ src, f4* __restrict__ dst, size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    dst[i] = __builtin_nontemporal_load(src + i);
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(256) void fill_kernel(f4* __restrict__ dst, size_t n) {
@@ -64,15 +68,23 @@ __global__ __launch_bounds__(256) void mfma_bf16_kernel(float* out, int iters) {
   if (s == 1234.5f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;  // never true; keeps MFMAs live
 }
 
+// fp8 at the CDNA4 rate: the block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 operands, unit
+// E8M0 scales) runs a 32x32x64 product in twice the cycles of the bf16 32x32x16, i.e. 2x the bf16
+// rate; the non-scaled 32x32x16_fp8_fp8 only matches bf16 (measured 2427 TF, profiles/probe_r1.json)
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 __global__ __launch_bounds__(256) void mfma_fp8_kernel(float* out, int iters) {
   const int lane = threadIdx.x & 63;
-  long a = 0x3830282018100800L + lane, b = 0x3931292119110901L + lane * 7;
+  i32x8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = 0x38302820 + ((lane + j) & 7);
+    b[j] = 0x39312921 + ((lane * 7 + j) & 7);
+  }
   f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
   for (int i = 0; i < iters; ++i) {
-    c0 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c1, 0, 0, 0);
-    c2 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c2, 0, 0, 0);
-    c3 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c3, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c0, 0, 0, 0, 127, 0, 127);
+    c1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c1, 0, 0, 0, 127, 0, 127);
+    c2 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c2, 0, 0, 0, 127, 0, 127);
+    c3 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c3, 0, 0, 0, 127, 0, 127);
   }
   float s = 0.f;
   for (int r = 0; r < 16; ++r) s += c0[r] + c1[r] + c2[r] + c3[r];
@@ -100,10 +112,11 @@ static double hbm_probe(int dev, bool quick) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  copy_kernel<<<grid, 256>>>(a, b, n);  // warm
+  const int cgrid = (int)((n + 255) / 256);
+  copy_kernel<<<cgrid, 256>>>(a, b, n);  // warm
   const int reps = quick ? 5 : 20;
   CK(hipEventRecord(e0));
-  for (int r = 0; r < reps; ++r) copy_kernel<<<grid, 256>>>(r & 1 ? b : a, r & 1 ? a : b, n);
+  for (int r = 0; r < reps; ++r) copy_kernel<<<cgrid, 256>>>(r & 1 ? b : a, r & 1 ? a : b, n);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   double tb_s = 2.0 * bytes * reps / (time_ms(e0, e1) * 1e-3) / 1e12;
@@ -136,8 +149,9 @@ static double mfma_probe(int dev, bool quick, bool fp8) {
   launch(iters);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
-  // 32x32x16 MFMA = 2*32*32*16 FLOP; 4 per iteration per wave; 4 waves per block
-  double flops = 2.0 * 32 * 32 * 16 * 4.0 * iters * 4.0 * blocks;
+  // bf16 32x32x16 MFMA = 2*32*32*16 FLOP, fp8 32x32x64 = 2*32*32*64; 4 per iteration per wave;
+  // 4 waves per block
+  double flops = 2.0 * 32 * 32 * (fp8 ? 64 : 16) * 4.0 * iters * 4.0 * blocks;
   double tflops = flops / (time_ms(e0, e1) * 1e-3) / 1e12;
   CK(hipFree(out));
   CK(hipEventDestroy(e0));

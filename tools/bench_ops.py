@@ -39,7 +39,7 @@ res["ce_bwd_ms"] = timeit(lambda: C.cross_entropy_bwd(logits, tgt, lse, sc, Fals
 n = 512 * 1024 * 1024
 p = torch.zeros(n, device=dev, dtype=torch.bfloat16); g = torch.zeros_like(p)
 mst = torch.zeros(n, device=dev); m = torch.zeros(n, device=dev); v = torch.zeros(n, device=dev)
-t = timeit(lambda: C.adamw(p, g, mst, m, v, 1e-3, .9, .95, 1e-8, .1, .5, .5, 1.0), iters=5)
+t = timeit(lambda: C.adamw(p, g, mst, m, v, 1e-3, .9, .95, 1e-8, .1, .5, .5, 1.0, 0), iters=5)
 res["adamw_512M_ms"] = t; res["adamw_TBps"] = n * 30 / t / 1e9
 del p, g, mst, m, v
 for name in ["rmsnorm_fwd", "swiglu_fwd", "swiglu_bwd", "rope", "ce_fwd", "ce_bwd"]:
