@@ -478,11 +478,37 @@ static inline int grid_for(size_t work, int block, int cap = 0x7fffffff) {
 // Tile 128 rows x 64 columns per 256-thread workgroup: 16-byte coalesced row loads into LDS, then
 // ds_read_b64_tr_b16 (gfx950's transposed LDS read: a 16-lane group gets a 4-row x 16-column block
 // column-major, lane i = column i) twice per lane gives 8 consecutive rows of one column = one
-// 16-byte store of an output row.  LDS row pitch 96 elements (48 dwords): the 4 rows of a block
-// start on banks 0/48/32/16, so a 32-lane half (2 blocks x 4 rows x 16 B) covers all 64 banks once.
-// (The first version gathered 2-byte LDS reads: 45-49 us per 64 MB, 2.7 TB/s, r1j profile.)
+// 16-byte store into an output row.
+//  * Store coalescing: wave w owns output rows c0+16w .. +15 (column block w of the tile) and its 4
+//    lane groups take 4 consecutive 8-row chunks, so one store instruction writes 16 output rows x
+//    64 contiguous bytes (the first version spread an instruction over 64 rows x 16 B).
+//  * LDS banks: row pitch 96 elements (48 dwords: rows 0-3 of a block start on banks 0/48/32/16) and
+//    the two 32-byte halves of a row's 64-byte column span swapped on rows with bit 3 set, so a
+//    32-lane half (two groups = rows 8 apart, same columns) covers all 64 banks once.
+// (2-byte LDS gathers: 45-49 us per 64 MB = 2.7 TB/s, r1j profile; 64-row stores: 3.7 TB/s, r1k.)
 // ------------------------------------------------------------------------------------------------
 constexpr int TR_R = 128, TR_C = 64, TR_P = 96;
+
+// element offset in the LDS tile of (row r, column c); c's 16-column block is swizzled by row bit 3
+__device__ __forceinline__ int tr_off(int r, int c) { return r * TR_P + (c ^ (((r >> 3) & 1) << 4)); }
+
+// write the [TR_R][TR_C] LDS tile transposed: out[(c0 + c) * ld + r0 + r]
+__device__ __forceinline__ void tr_store_tile(const bf16_t* tile, bf16_t* out, size_t ld, int c0, int r0,
+                                              int t) {
+  const int w = t >> 6, j = (t >> 4) & 3, lane16 = t & 15, q = (t >> 2) & 3, p = t & 3;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int rk = pass * 4 + j;  // 8-row chunk
+    const int row = rk * 8 + q;
+    const bf16_t* lo_p = tile + tr_off(row, w * 16 + 4 * p);
+    const bf16_t* hi_p = tile + tr_off(row + 4, w * 16 + 4 * p);
+    const dsa::bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, lo_p));
+    const dsa::bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, hi_p));
+    const dsa::bf16x8 o = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<dsa::bf16x8*>(out + (size_t)(c0 + w * 16 + lane16) * ld + r0 + rk * 8) = o;
+  }
+}
+
 __global__ __launch_bounds__(256) void transpose2d_kernel(const bf16_t* __restrict__ in,
                                                           bf16_t* __restrict__ out, int R, int C) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[TR_R * TR_P];
@@ -497,25 +523,16 @@ __global__ __launch_bounds__(256) void transpose2d_kernel(const bf16_t* __restri
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int idx = i * 256 + t, r = idx >> 3, ch = idx & 7;
-    *reinterpret_cast<us8*>(tile + r * TR_P + ch * 8) = v[i];
+    *reinterpret_cast<us8*>(tile + tr_off(r, ch * 8)) = v[i];
   }
   __syncthreads();
-  const int G = t >> 4, lane16 = t & 15, q = (t >> 2) & 3, p = t & 3;
-#pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {  // 4 column blocks x 16 row chunks of 8 = 64 units
-    const int u = pass * 16 + G, cb = u & 3, rk = u >> 2;
-    const bf16_t* src = tile + (rk * 8 + q) * TR_P + cb * 16 + 4 * p;
-    const dsa::bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, src));
-    const dsa::bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, src + 4 * TR_P));
-    const dsa::bf16x8 o = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    *reinterpret_cast<dsa::bf16x8*>(out + (size_t)(c0 + cb * 16 + lane16) * R + r0 + rk * 8) = o;
-  }
+  tr_store_tile(tile, out, (size_t)R, c0, r0, t);
 }
 
 // SwiGLU forward that also writes the transposed output aT[F, T] (the down projection's
 // token-contiguous weight-gradient operand, so backward needs no separate transpose of a: the
 // extra 2 B/element write replaces a 4 B/element transpose pass).  Same 128 x 64 tiling and
-// ds_read_b64_tr_b16 gather as transpose2d_kernel.
+// transposed store as transpose2d_kernel.
 __global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restrict__ gu,
                                                            bf16_t* __restrict__ out,
                                                            bf16_t* __restrict__ outT, int T, int F) {
@@ -540,19 +557,10 @@ __global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restr
     for (int k = 0; k < 8; ++k) o[k] = silu_f(g[k]) * u[k];
     const us8 a = pack8(o);
     *reinterpret_cast<us8*>(out + (size_t)(r0 + r) * F + c0 + ch * 8) = a;
-    *reinterpret_cast<us8*>(tile + r * TR_P + ch * 8) = a;
+    *reinterpret_cast<us8*>(tile + tr_off(r, ch * 8)) = a;
   }
   __syncthreads();
-  const int G = t >> 4, lane16 = t & 15, q = (t >> 2) & 3, p = t & 3;
-#pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
-    const int u = pass * 16 + G, cb = u & 3, rk = u >> 2;
-    const bf16_t* src = tile + (rk * 8 + q) * TR_P + cb * 16 + 4 * p;
-    const dsa::bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, src));
-    const dsa::bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(dsa::bf16x4, src + 4 * TR_P));
-    const dsa::bf16x8 o = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    *reinterpret_cast<dsa::bf16x8*>(outT + (size_t)(c0 + cb * 16 + lane16) * T + r0 + rk * 8) = o;
-  }
+  tr_store_tile(tile, outT, (size_t)T, c0, r0, t);
 }
 
 extern "C" hipError_t dsa_swiglu_fwd_t(const void* gu, void* out, void* outT, int T, int F, hipStream_t st) {
