@@ -38,16 +38,20 @@ constexpr int HD = 128;          // head dim
 // ================================================================================================
 // Forward
 // ================================================================================================
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
+// NW waves per workgroup, 32 query rows each (QB = 32 * NW rows per workgroup); every wave of the
+// workgroup shares the K/V tiles.  NW = 4 (2 workgroups per CU) or 8 (1 per CU: half the K/V
+// LDS-DMA traffic per query row; the default when S % 256 == 0).
+template <bool CAUSAL, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
                                                         float* __restrict__ lse, int B, int S,
                                                         int H, int KVH, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int QB = 32 * NW;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
   const int NH = H + 2 * KVH;
   const long rs = (long)NH * HD;  // row stride
-  const int nqb = S / 128;
+  const int nqb = S / QB;
   const int bid = blockIdx.x;
   const int qb = CAUSAL ? nqb - 1 - bid / (B * H) : bid / (B * H);  // heaviest blocks first
   const int bh = bid % (B * H);
@@ -56,7 +60,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16_t* __restrict
   const bf16_t* qp = base + hh * HD;
   const bf16_t* kp = base + (H + kvh) * HD;
   const bf16_t* vp = base + (H + KVH + kvh) * HD;
-  const int q0 = qb * 128, qw0 = q0 + 32 * w, myq = qw0 + l32;
+  const int q0 = qb * QB, qw0 = q0 + 32 * w, myq = qw0 + l32;
 
   bf16x8 qf[8];
 #pragma unroll
@@ -69,10 +73,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16_t* __restrict
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
   float m = -INFINITY, lsum = 0.f;
-  const int nkv = CAUSAL ? (q0 + 128) / 64 : S / 64;
+  const int nkv = CAUSAL ? (q0 + QB) / 64 : S / 64;
 
-  dma_tile64(kp, rs, smem, w, lane);
-  dma_tile64(vp, rs, smem + TILE_BYTES, w, lane);
+  dma_tile64_n<NW>(kp, rs, smem, w, lane);
+  dma_tile64_n<NW>(vp, rs, smem + TILE_BYTES, w, lane);
   wait_dma_and_barrier();
 
   for (int it = 0; it < nkv; ++it) {
@@ -80,8 +84,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16_t* __restrict
     const char* vl = kl + TILE_BYTES;
     if (it + 1 < nkv) {
       char* nk = smem + ((it + 1) & 1) * 2 * TILE_BYTES;
-      dma_tile64(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
-      dma_tile64(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
+      dma_tile64_n<NW>(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
+      dma_tile64_n<NW>(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
     }
     const int kv0 = it * 64;
     if (!CAUSAL || kv0 <= qw0 + 31) {
@@ -654,8 +658,22 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
                                  int D, float scale, int causal, hipStream_t st) {
   if (!fa_shape_ok(S, H, KVH, D)) return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
-  const int grid = B * H * (S / 128);
   const size_t lds = 4 * TILE_BYTES;
+  // 8 waves (one 256-row workgroup per CU) by default: 0.710 vs 0.720 ms at S=8192, three
+  // interleaved same-box runs (tools/run_r1s.sh); DSTACK_AMD_FA_FWD_WAVES=4 selects the 4-wave form
+  static const int waves = [] {
+    const char* v = getenv("DSTACK_AMD_FA_FWD_WAVES");
+    return (v && atoi(v) == 4) ? 4 : 8;
+  }();
+  if (waves == 8 && S % 256 == 0) {
+    const int grid = B * H * (S / 256);
+    if (causal)
+      fa_fwd_kernel<true, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+    else
+      fa_fwd_kernel<false, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+    return hipGetLastError();
+  }
+  const int grid = B * H * (S / 128);
   if (causal)
     fa_fwd_kernel<true><<<grid, 256, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
   else

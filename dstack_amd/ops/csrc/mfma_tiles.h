@@ -66,6 +66,21 @@ __device__ __forceinline__ void dma_tile64(const bf16_t* g, long stride, char* l
   }
 }
 
+// Same tile, issued by NW waves (16 / NW wave-instructions each).
+template <int NW>
+__device__ __forceinline__ void dma_tile64_n(const bf16_t* g, long stride, char* lds, int wave, int lane) {
+  static_assert(16 % NW == 0, "16 pieces split over NW waves");
+#pragma unroll
+  for (int i = 0; i < 16 / NW; ++i) {
+    const int piece = wave * (16 / NW) + i;
+    const int row = piece * 4 + (lane >> 4);
+    const int pc = lane & 15;
+    const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    const bf16_t* src = g + (long)row * stride + ch * 8;
+    __builtin_amdgcn_global_load_lds(GLB1(void, src), LDS3(void, lds + piece * 1024), 16, 0, 0);
+  }
+}
+
 // 64 contiguous floats -> LDS (one wave-instruction, 4 B/lane)
 __device__ __forceinline__ void dma_f32x64(const float* g, char* lds, int lane) {
   __builtin_amdgcn_global_load_lds(GLB1(void, g + lane), LDS3(void, lds), 4, 0, 0);
