@@ -548,8 +548,8 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __re
 // ================================================================================================
 // Backward dQ pass: workgroup = 128 queries of one (b, q-head); loops over 64-key K/V tiles.
 // ================================================================================================
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
+template <bool CAUSAL, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
                                                            const bf16_t* __restrict__ dout,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta,
@@ -560,7 +560,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(const bf16_t* __restr
   const int NH = H + 2 * KVH;
   const long rs = (long)NH * HD;
   const long ors = (long)H * HD;
-  const int nqb = S / 128;
+  constexpr int QB = 32 * NW;
+  const int nqb = S / QB;
   const int bid = blockIdx.x;
   const int qb = CAUSAL ? nqb - 1 - bid / (B * H) : bid / (B * H);
   const int bh = bid % (B * H);
@@ -570,7 +571,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(const bf16_t* __restr
   const bf16_t* kp = base + (H + kvh) * HD;
   const bf16_t* vp = base + (H + KVH + kvh) * HD;
   const bf16_t* dop = dout + (long)b * S * ors + hh * HD;
-  const int q0 = qb * 128, qw0 = q0 + 32 * w, myq = qw0 + l32;
+  const int q0 = qb * QB, qw0 = q0 + 32 * w, myq = qw0 + l32;
 
   bf16x8 qf[8], df[8];
 #pragma unroll
@@ -585,18 +586,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(const bf16_t* __restr
   for (int d = 0; d < 4; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
-  const int nkv = CAUSAL ? (q0 + 128) / 64 : S / 64;
+  const int nkv = CAUSAL ? (q0 + QB) / 64 : S / 64;
 
-  dma_tile64(kp, rs, smem, w, lane);
-  dma_tile64(vp, rs, smem + TILE_BYTES, w, lane);
+  dma_tile64_n<NW>(kp, rs, smem, w, lane);
+  dma_tile64_n<NW>(vp, rs, smem + TILE_BYTES, w, lane);
   wait_dma_and_barrier();
   for (int it = 0; it < nkv; ++it) {
     const char* kl = smem + (it & 1) * 2 * TILE_BYTES;
     const char* vl = kl + TILE_BYTES;
     if (it + 1 < nkv) {
       char* nk = smem + ((it + 1) & 1) * 2 * TILE_BYTES;
-      dma_tile64(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
-      dma_tile64(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
+      dma_tile64_n<NW>(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
+      dma_tile64_n<NW>(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
     }
     const int kv0 = it * 64;
     if (!CAUSAL || kv0 <= qw0 + 31) {
@@ -606,7 +607,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(const bf16_t* __restr
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           st[t][r] = 0.f;
-          dpt[t][r] = 0.f;
+          dpt[t][r] = NW == 8 ? -Dl : 0.f;  // 8 waves: -delta seeds dP (see the launch note)
         }
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(const bf16_t* __restr
             const int key = kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hf;
             if (key > myq) p = 0.f;
           }
-          dpt[t][r] = p * (dpt[t][r] - Dl);
+          dpt[t][r] = NW == 8 ? p * dpt[t][r] : p * (dpt[t][r] - Dl);
         }
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
@@ -717,6 +718,15 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     const char* v = getenv("DSTACK_AMD_FA_DKDV");
     return !(v && std::string(v) == "4w");
   }();
+  // dQ pass: 8 waves / 256 query rows per workgroup when S % 256 == 0 (DSTACK_AMD_FA_DQ_WAVES=4|8).
+  // Whole backward at S=8192, same box, 3 interleaved runs each (tools/run_r1t.sh): 4 waves 2.06-2.08
+  // ms; 8 waves 2.04-2.07; 8 waves with the dP accumulator seeded with -delta ('row constant')
+  // 2.00-2.05 -- the seeding is kept for 8 waves only: with 4 waves it measured 2.14-2.17 ms.
+  static const int dq_waves_env = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DQ_WAVES");
+    return (v && atoi(v) == 4) ? 4 : 8;
+  }();
+  const int dq_waves = (dq_waves_env == 8 && S % 256 == 0) ? 8 : 4;
 #define DSA_DKDV(C, N)                                                                                 \
   do {                                                                                                 \
     if (dkdv8)                                                                                         \
@@ -729,13 +739,21 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   if (causal) {
     if (dkdv_qt == 128) DSA_DKDV(true, 4); else DSA_DKDV(true, 2);
     DSA_CHECK(hipGetLastError());
-    fa_bwd_dq_kernel<true><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta,
-                                                     (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    if (dq_waves == 8)
+      fa_bwd_dq_kernel<true, 8><<<B * H * (S / 256), 512, lds_q, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    else
+      fa_bwd_dq_kernel<true><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta,
+                                                       (bf16_t*)dqkv, B, S, H, KVH, sl2);
   } else {
     if (dkdv_qt == 128) DSA_DKDV(false, 4); else DSA_DKDV(false, 2);
     DSA_CHECK(hipGetLastError());
-    fa_bwd_dq_kernel<false><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
-                                                      delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    if (dq_waves == 8)
+      fa_bwd_dq_kernel<false, 8><<<B * H * (S / 256), 512, lds_q, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    else
+      fa_bwd_dq_kernel<false><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
+                                                        delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
   }
 #undef DSA_DKDV
   DSA_CHECK(hipGetLastError());
