@@ -226,9 +226,11 @@ def test_optimizer_in_backward_matches_plain_step(gpu):
     assert l1[-1] < l1[0]  # it trains
 
 
-def test_flash_attention_dkdv_variants_agree(gpu, tmp_path):
-    """The 8-wave (default) and 4-wave (DSTACK_AMD_FA_DKDV=4w) dK/dV kernels give the same
-    gradients; the switch is read once per process, so the 4-wave run is a child process."""
+def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
+    """Every kernel variant gives the same output and gradients as the defaults (8-wave forward,
+    8-wave dK/dV, 8-wave dQ): the 4-wave dK/dV (DSTACK_AMD_FA_DKDV=4w) and the 4-wave forward and
+    dQ passes (DSTACK_AMD_FA_FWD_WAVES=4, DSTACK_AMD_FA_DQ_WAVES=4).  The switches are read once per
+    process, so each variant runs in a child process."""
     import os
     import subprocess
     import sys
@@ -240,17 +242,26 @@ def test_flash_attention_dkdv_variants_agree(gpu, tmp_path):
         "g = torch.Generator(device='cuda').manual_seed(0)\n"
         f"x = torch.randn({B}, {S}, {(H + 2 * KV) * D}, device='cuda', generator=g).bfloat16().requires_grad_()\n"
         f"do = torch.randn({B}, {S}, {H * D}, device='cuda', generator=g).bfloat16()\n"
-        f"ops.attention(x, {H}, {KV}, causal=True).backward(do)\n"
-        "torch.save(x.grad.cpu(), sys.argv[1])\n"
+        f"o = ops.attention(x, {H}, {KV}, causal=True)\n"
+        "o.backward(do)\n"
+        "torch.save({'o': o.detach().cpu(), 'g': x.grad.cpu()}, sys.argv[1])\n"
     )
-    env = dict(os.environ)
-    for variant in ("4w", "8w"):
-        env["DSTACK_AMD_FA_DKDV"] = variant
-        subprocess.run([sys.executable, "-c", script, str(tmp_path / f"{variant}.pt")], env=env, check=True,
+    variants = {"default": {}, "dkdv4": {"DSTACK_AMD_FA_DKDV": "4w"},
+                "fwd4_dq4": {"DSTACK_AMD_FA_FWD_WAVES": "4", "DSTACK_AMD_FA_DQ_WAVES": "4"}}
+    out = {}
+    for name, extra in variants.items():
+        env = dict(os.environ)
+        for k in ("DSTACK_AMD_FA_DKDV", "DSTACK_AMD_FA_FWD_WAVES", "DSTACK_AMD_FA_DQ_WAVES"):
+            env.pop(k, None)
+        env.update(extra)
+        subprocess.run([sys.executable, "-c", script, str(tmp_path / f"{name}.pt")], env=env, check=True,
                        timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    a = torch.load(tmp_path / "4w.pt", weights_only=True).float()
-    b = torch.load(tmp_path / "8w.pt", weights_only=True).float()
-    assert ((a - b).norm() / b.norm()).item() < 2e-3
+        out[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
+    ref_o, ref_g = out["default"]["o"].float(), out["default"]["g"].float()
+    for name in ("dkdv4", "fwd4_dq4"):
+        o, g = out[name]["o"].float(), out[name]["g"].float()
+        assert ((o - ref_o).norm() / ref_o.norm()).item() < 2e-3, name
+        assert ((g - ref_g).norm() / ref_g.norm()).item() < 2e-3, name
 
 
 @pytest.mark.parametrize("T,P,Q", [(64, 256, 256), (512, 768, 512), (1024, 512, 1280)])

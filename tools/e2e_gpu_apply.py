@@ -20,8 +20,14 @@ def main():
     from dstack_amd.server.testing import ServerProcess
 
     steps = os.environ.get("E2E_STEPS", "5")
-    cmd = (f"echo HIP_VISIBLE_DEVICES=$HIP_VISIBLE_DEVICES && cd {ROOT} && "
-           f"python bench.py --steps {steps} --warmup 2 --no-coldstart")
+    launch = "python"
+    if os.environ.get("E2E_TORCHRUN") == "1":
+        # the examples/llama3-8b-train command: torchrun over the rendezvous env the runner exports
+        launch = ("torchrun --nproc-per-node=$DSTACK_GPUS_PER_NODE --master-addr=$DSTACK_MASTER_NODE_IP "
+                  "--master-port=29511")
+    cmd = (f"echo HIP_VISIBLE_DEVICES=$HIP_VISIBLE_DEVICES DSTACK_GPUS_NUM=$DSTACK_GPUS_NUM "
+           f"MASTER_ADDR=$DSTACK_MASTER_NODE_IP && cd {ROOT} && "
+           f"{launch} bench.py --gpus $DSTACK_GPUS_NUM --steps {steps} --warmup 2 --no-coldstart")
     with ServerProcess() as srv:
         client = srv.client()
         conf = Task(name="llama3-8b-e2e", commands=[cmd], resources=Resources(gpu=GPU(count=1)))
@@ -40,7 +46,7 @@ def main():
         out = {
             "status": sub.status.value,
             "exit_status": sub.exit_status,
-            "gpu_env": [ln for ln in logs.splitlines() if ln.startswith("HIP_VISIBLE_DEVICES")][:1],
+            "job_env": [ln for ln in logs.splitlines() if ln.startswith("HIP_VISIBLE_DEVICES")][:1],
             "submit_to_running_s": (t["running"] - ts) if "running" in t else None,
             "submit_to_first_log_s": (t["first_log"] - ts) if "first_log" in t else None,
             "submit_to_done_s": wall,
