@@ -668,7 +668,7 @@ extern "C" hipError_t dsa_adamw(void* param, const void* grad, float* master, fl
   // max_blocks > 0 caps the grid (persistent grid-stride): the optimizer-in-backward path runs
   // AdamW on a side stream beside MFMA-bound kernels, where a full-chip grid takes every CU's
   // slots and just serialises the two (r1g trace: dK/dV 1.13 -> 2.3 ms while AdamW ran).  Measured
-  // same box (tools/run_r1l.sh, ms/step): full grid 799, 64 blocks 807, 32 843, 16 956, no
+  // same box (tools/gpu_sessions/run_r1l.sh, ms/step): full grid 799, 64 blocks 807, 32 843, 16 956, no
   // overlap 802 -- per-CU HBM bandwidth is too low for a small persistent grid, so 0 stays default
   const int cap = max_blocks > 0 ? max_blocks : 0x7fffffff;  // (DSTACK_AMD_GRID_CAP overrides)
   adamw_kernel<<<grid_for(n / 8 + 1, 256, cap), 256, 0, st>>>(

@@ -661,7 +661,7 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
   const float sl2 = scale * 1.4426950408889634f;
   const size_t lds = 4 * TILE_BYTES;
   // 8 waves (one 256-row workgroup per CU) by default: 0.710 vs 0.720 ms at S=8192, three
-  // interleaved same-box runs (tools/run_r1s.sh); DSTACK_AMD_FA_FWD_WAVES=4 selects the 4-wave form
+  // interleaved same-box runs (tools/gpu_sessions/run_r1s.sh); DSTACK_AMD_FA_FWD_WAVES=4 selects the 4-wave form
   static const int waves = [] {
     const char* v = getenv("DSTACK_AMD_FA_FWD_WAVES");
     return (v && atoi(v) == 4) ? 4 : 8;
@@ -719,7 +719,7 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     return !(v && std::string(v) == "4w");
   }();
   // dQ pass: 8 waves / 256 query rows per workgroup when S % 256 == 0 (DSTACK_AMD_FA_DQ_WAVES=4|8).
-  // Whole backward at S=8192, same box, 3 interleaved runs each (tools/run_r1t.sh): 4 waves 2.06-2.08
+  // Whole backward at S=8192, same box, 3 interleaved runs each (tools/gpu_sessions/run_r1t.sh): 4 waves 2.06-2.08
   // ms; 8 waves 2.04-2.07; 8 waves with the dP accumulator seeded with -delta ('row constant')
   // 2.00-2.05 -- the seeding is kept for 8 waves only: with 4 waves it measured 2.14-2.17 ms.
   static const int dq_waves_env = [] {
