@@ -28,12 +28,26 @@ def main():
     cmd = (f"echo HIP_VISIBLE_DEVICES=$HIP_VISIBLE_DEVICES DSTACK_GPUS_NUM=$DSTACK_GPUS_NUM "
            f"MASTER_ADDR=$DSTACK_MASTER_NODE_IP && cd {ROOT} && "
            f"{launch} bench.py --gpus $DSTACK_GPUS_NUM --steps {steps} --warmup 2 --no-coldstart")
-    with ServerProcess() as srv:
+    # hardware metrics: the server polls the runner's /api/metrics (cgroup + amdsmi) every 2 s here
+    with ServerProcess(env={"DSTACK_SERVER_METRICS_COLLECT_INTERVAL": "2"}) as srv:
         client = srv.client()
         conf = Task(name="llama3-8b-e2e", commands=[cmd], resources=Resources(gpu=GPU(count=1)))
         t0 = time.time()
         run = client.runs.submit(conf)
-        run.wait(timeout=float(os.environ.get("E2E_TIMEOUT", "600")), poll=0.5)
+        deadline = t0 + float(os.environ.get("E2E_TIMEOUT", "600"))
+        samples = []
+        while time.time() < deadline:
+            run.refresh()
+            if run.status.is_finished():
+                break
+            try:
+                jm = client.api.metrics.get_job_metrics("main", run.name, limit=1)
+                cur = {m.name: m.values[-1] for m in jm.metrics if m.values}
+                if cur:
+                    samples.append({k: v for k, v in cur.items() if "gpu" in k or k.startswith("memory")})
+            except Exception:  # noqa: BLE001 - metrics appear once the job runs
+                pass
+            time.sleep(1.0)
         wall = time.time() - t0
         logs = b"".join(run.logs()).decode(errors="replace")
         sub = run.model.jobs[0].job_submissions[-1]
@@ -51,6 +65,8 @@ def main():
             "submit_to_first_log_s": (t["first_log"] - ts) if "first_log" in t else None,
             "submit_to_done_s": wall,
             "job_bench": bench,
+            "hw_metrics_samples": len(samples),
+            "hw_metrics_peak": {k: max(x.get(k, 0) for x in samples) for k in (samples[-1] if samples else {})},
         }
         if bench is None:
             out["log_tail"] = logs[-3000:]
