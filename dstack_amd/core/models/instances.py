@@ -196,6 +196,7 @@ class InstanceHealth(CoreModel):
     healthy: bool = True
     hbm_tb_s: Optional[List[float]] = None
     mfma_bf16_tflops: Optional[List[float]] = None
+    mfma_fp8_tflops: Optional[List[float]] = None
     xgmi_gb_s: Optional[List[List[float]]] = None
     rccl_busbw_gb_s: Optional[float] = None
     message: str = ""

@@ -289,6 +289,8 @@ def _process_running(s: Session, run: RunModel, job: JobModel):
         _runner_unreachable(job, str(e))
         return
     job.remove_at = None  # runner reachable again: clear the unreachable marker
+    if resp.get("gpu_probe") and job.instance is not None:
+        _record_gpu_probe(job, resp["gpu_probe"])
     if resp.get("job_logs") or resp.get("runner_logs"):
         logs_services.write_job_logs(run.project.name, run.run_name, str(job.id), resp)
         if resp.get("job_logs"):
@@ -312,6 +314,28 @@ def _process_running(s: Session, run: RunModel, job: JobModel):
         jobs_services.terminate_job(job, reason, last.get("termination_message") or None, delay=False)
         jobs_services.mark_timing(job, "finished")
         scheduler.wake(scheduler.TERMINATING_JOBS, scheduler.RUNS)
+
+
+def _record_gpu_probe(job: JobModel, doc: dict):
+    """The runner ran dstack-probe (HBM/MFMA HIP kernels) before the job: keep the result as the
+    instance's health so `fleet`/`instances` show it and the scheduler can avoid a bad host."""
+    from dstack_amd.core.models.instances import InstanceHealth
+
+    inst = job.instance
+    try:
+        health = InstanceHealth(
+            healthy=bool(doc.get("healthy", True)), hbm_tb_s=doc.get("hbm_tb_s"),
+            mfma_bf16_tflops=doc.get("mfma_bf16_tflops"),
+            mfma_fp8_tflops=doc.get("mfma_fp8_tflops"), xgmi_gb_s=doc.get("xgmi_gb_s"),
+            rccl_busbw_gb_s=doc.get("rccl_busbw_gb_s"),
+            message="" if doc.get("healthy", True) else "GPU health probe below thresholds",
+        )
+    except Exception:  # noqa: BLE001 - a malformed probe document must not break the job
+        return
+    data = health.model_dump_json()
+    if inst.health_data != data:
+        inst.health_data = data
+        inst.health_status = None if health.healthy else health.message
 
 
 def _runner_unreachable(job: JobModel, err: str):

@@ -244,6 +244,15 @@ Json Executor::pull(int64_t since) const {
     for (auto& s : states_) last = std::max(last, s.timestamp);
   }
   out.set("job_states", states);
+  {
+    std::lock_guard<std::mutex> lk(states_mu_);
+    if (!probe_json_.empty()) {
+      try {
+        out.set("gpu_probe", Json::parse(probe_json_));
+      } catch (...) {
+      }
+    }
+  }
   out.set("job_logs", enc(jl));
   out.set("runner_logs", enc(rl));
   out.set("last_updated", (long long)last);
@@ -436,6 +445,17 @@ bool Executor::run_probe() {
   std::string out;
   int rc = run_cmd({opts_.probe_binary, "--quick", "--json"}, "", &out);
   job_logs_.append("[dstack] GPU health probe: " + out + (out.empty() || out.back() != '\n' ? "\n" : ""));
+  // the last JSON line is the probe document; the server copies it into the instance's health
+  std::string doc;
+  size_t end = out.find_last_not_of(" \r\n");
+  if (end != std::string::npos) {
+    size_t begin = out.rfind('\n', end);
+    doc = out.substr(begin == std::string::npos ? 0 : begin + 1, end - (begin == std::string::npos ? 0 : begin + 1) + 1);
+  }
+  if (!doc.empty() && doc[0] == '{') {
+    std::lock_guard<std::mutex> lk(states_mu_);
+    probe_json_ = doc;
+  }
   return rc == 0;
 }
 

@@ -272,3 +272,32 @@ def test_retry_decision(db, reason, retry_events, expect_retry):
         s.flush()
         run = s.get(RunModel, rid)
         assert (pr._retry_duration(run, j) is not None) == expect_retry
+
+
+def test_gpu_probe_result_recorded_as_instance_health(db):
+    """The runner's dstack-probe document (pull response ``gpu_probe``) becomes the instance's
+    health; a probe below thresholds marks the instance unhealthy."""
+    from dstack_amd.server.background.tasks import process_running_jobs as prj
+
+    with session_scope() as s:
+        iid = _instance(s)
+        rid = _submit(s, {"type": "task", "commands": ["x"]})
+        j = _job(s, rid)
+        j.status = JobStatus.RUNNING.value
+        j.instance_id = iid
+        j.job_provisioning_data = _jpd().model_dump_json()
+        jid = j.id
+    for doc, healthy in (({"hbm_tb_s": [6.05], "mfma_bf16_tflops": [2103.8], "healthy": True}, True),
+                         ({"hbm_tb_s": [1.1], "mfma_bf16_tflops": [310.0], "healthy": False}, False)):
+        runner = mock.Mock()
+        runner.pull.return_value = {"job_states": [], "job_logs": [], "runner_logs": [], "last_updated": 1,
+                                    "gpu_probe": doc}
+        with mock.patch.object(prj, "get_runner_client", return_value=runner), session_scope() as s:
+            j = s.get(JobModel, jid)
+            prj._process_running(s, j.run, j)
+        with session_scope() as s:
+            inst = pools_services.instance_model_to_instance(s.get(InstanceModel, iid))
+            assert inst.health is not None
+            assert inst.health["healthy"] is healthy
+            assert inst.health["hbm_tb_s"] == doc["hbm_tb_s"]
+            assert (s.get(InstanceModel, iid).health_status is None) is healthy

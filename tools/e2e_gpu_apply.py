@@ -29,9 +29,16 @@ def main():
            f"MASTER_ADDR=$DSTACK_MASTER_NODE_IP && cd {ROOT} && "
            f"{launch} bench.py --gpus $DSTACK_GPUS_NUM --steps {steps} --warmup 2 --no-coldstart")
     # hardware metrics: the server polls the runner's /api/metrics (cgroup + amdsmi) every 2 s here
-    with ServerProcess(env={"DSTACK_SERVER_METRICS_COLLECT_INTERVAL": "2"}) as srv:
+    # E2E_PROBE=1: the shim hands dstack-probe to the runner, which runs the HIP health probes
+    # (HBM, bf16/fp8 MFMA) before the job; the result becomes the instance's health
+    probe = os.environ.get("E2E_PROBE") == "1"
+    srv_env = {"DSTACK_SERVER_METRICS_COLLECT_INTERVAL": "2"}
+    if probe:
+        srv_env["DSTACK_LOCAL_GPU_PROBE"] = "1"
+    with ServerProcess(env=srv_env) as srv:
         client = srv.client()
-        conf = Task(name="llama3-8b-e2e", commands=[cmd], resources=Resources(gpu=GPU(count=1)))
+        conf = Task(name="llama3-8b-e2e", commands=[cmd], resources=Resources(gpu=GPU(count=1)),
+                    env={"DSTACK_GPU_PROBE": "1"} if probe else {})
         t0 = time.time()
         run = client.runs.submit(conf)
         deadline = t0 + float(os.environ.get("E2E_TIMEOUT", "600"))
@@ -68,6 +75,10 @@ def main():
             "hw_metrics_samples": len(samples),
             "hw_metrics_peak": {k: max(x.get(k, 0) for x in samples) for k in (samples[-1] if samples else {})},
         }
+        if probe:
+            insts = client.api.instances.list(["main"])
+            out["instance_health"] = [i.health for i in insts]
+            out["probe_log"] = [ln for ln in logs.splitlines() if "GPU health probe" in ln][:1]
         if bench is None:
             out["log_tail"] = logs[-3000:]
             out["server_log_tail"] = srv.log()[-3000:]
