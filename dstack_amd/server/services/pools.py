@@ -127,6 +127,8 @@ def filter_pool_instances(
     for inst in instances:
         if inst.status not in (InstanceStatus.IDLE.value, InstanceStatus.BUSY.value) or inst.unreachable:
             continue
+        if inst.health_data and not json.loads(inst.health_data).get("healthy", True):
+            continue  # its GPUs failed the HIP health probe (HBM/MFMA below thresholds)
         if fleet is not None and inst.fleet_id != fleet.id:
             continue
         if profile.backends and inst.backend and BackendType(inst.backend) not in profile.backends:

@@ -301,3 +301,19 @@ def test_gpu_probe_result_recorded_as_instance_health(db):
             assert inst.health["healthy"] is healthy
             assert inst.health["hbm_tb_s"] == doc["hbm_tb_s"]
             assert (s.get(InstanceModel, iid).health_status is None) is healthy
+
+
+def test_unhealthy_instance_not_reused(db):
+    """An instance whose GPU probe failed is skipped when pool instances are matched to a job."""
+    from dstack_amd.core.models.instances import InstanceHealth
+    from dstack_amd.core.models.profiles import Profile
+    from dstack_amd.core.models.resources import ResourcesSpec
+    from dstack_amd.core.models.runs import Requirements
+
+    with session_scope() as s:
+        iid = _instance(s)
+        inst = s.get(InstanceModel, iid)
+        req = Requirements(resources=ResourcesSpec.model_validate({"gpu": "MI355X:8"}))
+        assert [i.id for i, _ in pools_services.filter_pool_instances([inst], Profile(name="p"), req)] == [iid]
+        inst.health_data = InstanceHealth(healthy=False, hbm_tb_s=[0.9]).model_dump_json()
+        assert pools_services.filter_pool_instances([inst], Profile(name="p"), req) == []
