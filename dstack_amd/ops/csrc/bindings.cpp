@@ -10,7 +10,7 @@ hipError_t dsa_rmsnorm_fwd(const void*, const void*, const void*, void*, void*, 
                            hipStream_t);
 int dsa_rmsnorm_bwd_grid(int rows);
 hipError_t dsa_rmsnorm_bwd(const void*, const void*, const void*, const float*, const void*, void*, float*,
-                           float*, int, int, hipStream_t);
+                           float*, void*, int, int, int, hipStream_t);
 hipError_t dsa_swiglu_fwd(const void*, void*, int, int, hipStream_t);
 bool dsa_transpose2d_supported(int, int);
 hipError_t dsa_swiglu_fwd_t(const void*, void*, void*, int, int, hipStream_t);
@@ -72,8 +72,11 @@ std::vector<torch::Tensor> add_rms_norm_fwd(torch::Tensor x, torch::Tensor delta
   return {h, y, rstd};
 }
 
+// dw_out (bf16 [D], optional): write the weight gradient there (accumulating when `accumulate`)
+// instead of returning an fp32 dw -- the optimizer's flat-buffer view of the norm weight's grad
 std::vector<torch::Tensor> rms_norm_bwd(torch::Tensor dy, torch::Tensor h, torch::Tensor w, torch::Tensor rstd,
-                                        c10::optional<torch::Tensor> dres) {
+                                        c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> dw_out,
+                                        bool accumulate) {
   check_bf16(dy, "dy");
   check_bf16(h, "h");
   check_bf16(w, "w");
@@ -83,12 +86,19 @@ std::vector<torch::Tensor> rms_norm_bwd(torch::Tensor dy, torch::Tensor h, torch
     check_bf16(*dres, "dres");
     dres_ptr = dres->data_ptr();
   }
+  void* dw_out_ptr = nullptr;
+  if (dw_out.has_value()) {
+    check_bf16(*dw_out, "dw_out");
+    TORCH_CHECK(dw_out->numel() == D, "dw_out must hold D elements");
+    dw_out_ptr = dw_out->data_ptr();
+  }
   auto dx = torch::empty_like(h);
   const int grid = dsa_rmsnorm_bwd_grid(rows);
   auto part = torch::empty({grid, D}, h.options().dtype(torch::kFloat32));
-  auto dw = torch::empty({D}, h.options().dtype(torch::kFloat32));
+  auto dw = dw_out_ptr ? torch::Tensor() : torch::empty({D}, h.options().dtype(torch::kFloat32));
   check(dsa_rmsnorm_bwd(dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dres_ptr,
-                        dx.data_ptr(), part.data_ptr<float>(), dw.data_ptr<float>(), rows, D, stream()),
+                        dx.data_ptr(), part.data_ptr<float>(), dw_out_ptr ? nullptr : dw.data_ptr<float>(),
+                        dw_out_ptr, accumulate ? 1 : 0, rows, D, stream()),
         "rms_norm_bwd");
   return {dx, dw};
 }
@@ -246,7 +256,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dstack_amd HIP/CDNA4 kernels (gfx950)";
   m.def("rms_norm_fwd", &rms_norm_fwd);
   m.def("add_rms_norm_fwd", &add_rms_norm_fwd);
-  m.def("rms_norm_bwd", &rms_norm_bwd);
+  m.def("rms_norm_bwd", &rms_norm_bwd, py::arg("dy"), py::arg("h"), py::arg("w"), py::arg("rstd"),
+        py::arg("dres") = py::none(), py::arg("dw_out") = py::none(), py::arg("accumulate") = false);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("transpose2d", &transpose2d);
   m.def("swiglu_fwd_t", &swiglu_fwd_t);

@@ -175,9 +175,13 @@ __global__ __launch_bounds__(256) void colsum_pass1_kernel(float* __restrict__ p
   }
 }
 
+// out (fp32) = column sums, or -- when out_bf16 is given -- out_bf16 = (accumulate ? out_bf16 : 0)
+// + column sums: the norm weight's gradient lands directly in the optimizer's flat bf16 buffer
+// (no fp32 -> bf16 copy kernel and no AccumulateGrad add kernel per norm per micro-batch)
 __global__ __launch_bounds__(64) void colsum_pass2_kernel(const float* __restrict__ part,
-                                                          float* __restrict__ out, int P, int D,
-                                                          int rpb) {
+                                                          float* __restrict__ out,
+                                                          bf16_t* __restrict__ out_bf16, int accumulate,
+                                                          int P, int D, int rpb) {
   const int col = (blockIdx.x * 64 + threadIdx.x) * 4;
   if (col >= D) return;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -186,15 +190,24 @@ __global__ __launch_bounds__(64) void colsum_pass2_kernel(const float* __restric
     const float4 v = *reinterpret_cast<const float4*>(part + (size_t)r * D + col);
     a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
   }
-  *reinterpret_cast<float4*>(out + col) = a;
+  if (out_bf16 == nullptr) {
+    *reinterpret_cast<float4*>(out + col) = a;
+    return;
+  }
+  bf16_t* o = out_bf16 + col;
+  if (accumulate) {
+    a.x += bf2f(o[0]); a.y += bf2f(o[1]); a.z += bf2f(o[2]); a.w += bf2f(o[3]);
+  }
+  o[0] = f2bf(a.x); o[1] = f2bf(a.y); o[2] = f2bf(a.z); o[3] = f2bf(a.w);
 }
 
-static hipError_t colsum(float* part, float* out, int P, int D, hipStream_t st) {
+static hipError_t colsum(float* part, float* out, bf16_t* out_bf16, int accumulate, int P, int D,
+                         hipStream_t st) {
   const int rpb = (P + COLSUM_RS - 1) / COLSUM_RS;
   const int cb = (D + 255) / 256;
   colsum_pass1_kernel<<<dim3(cb, COLSUM_RS), 256, 0, st>>>(part, P, D, rpb);
   DSA_CHECK(hipGetLastError());
-  colsum_pass2_kernel<<<cb, 64, 0, st>>>(part, out, P, D, rpb);
+  colsum_pass2_kernel<<<cb, 64, 0, st>>>(part, out, out_bf16, accumulate, P, D, rpb);
   return hipGetLastError();
 }
 
@@ -601,9 +614,11 @@ extern "C" int dsa_rmsnorm_bwd_grid(int rows) {
   return g > 1024 ? 1024 : (g < 1 ? 1 : g);
 }
 
+// dw_bf16 != null: the weight gradient goes to dw_bf16 (bf16, accumulated into when `accumulate`)
+// instead of the fp32 dw
 extern "C" hipError_t dsa_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* rstd,
                                       const void* dres, void* dx, float* dw_part, float* dw,
-                                      int rows, int D, hipStream_t st) {
+                                      void* dw_bf16, int accumulate, int rows, int D, hipStream_t st) {
   if (D % 8) return hipErrorInvalidValue;
   const int block = 256;
   const int grid = dsa_rmsnorm_bwd_grid(rows);
@@ -618,7 +633,7 @@ extern "C" hipError_t dsa_rmsnorm_bwd(const void* dy, const void* h, const void*
         rows, D));
   }
   DSA_CHECK(hipGetLastError());
-  return colsum(dw_part, dw, grid, D, st);
+  return colsum(dw_part, dw, (bf16_t*)dw_bf16, accumulate, grid, D, st);
 }
 
 extern "C" hipError_t dsa_swiglu_fwd(const void* gu, void* out, int rows, int F, hipStream_t st) {

@@ -29,7 +29,13 @@ class _RMSNorm(torch.autograd.Function):
     def backward(ctx, dy):
         C = _ext.require()
         x, w, rstd = ctx.saved_tensors
-        dx, dw = C.rms_norm_bwd(_2d(dy.contiguous()), _2d(x), w, rstd, None)
+        dy2 = _2d(dy.contiguous())
+        writer = getattr(w, "_dsa_grad_writer", None)
+        if writer is not None and w.dtype == torch.bfloat16:
+            out = {}
+            writer(w, lambda dst, acc: out.setdefault("dx", C.rms_norm_bwd(dy2, _2d(x), w, rstd, None, dst, acc)[0]))
+            return out["dx"].view_as(x), None, None
+        dx, dw = C.rms_norm_bwd(dy2, _2d(x), w, rstd, None)
         return dx.view_as(x), dw.to(w.dtype), None
 
 
@@ -49,7 +55,15 @@ class _AddRMSNorm(torch.autograd.Function):
         h, w, rstd = ctx.saved_tensors
         if dh is not None:
             dh = _2d(dh.contiguous())
-        dx, dw = C.rms_norm_bwd(_2d(dy.contiguous()), h, w, rstd, dh)
+        dy2 = _2d(dy.contiguous())
+        writer = getattr(w, "_dsa_grad_writer", None)
+        if writer is not None and w.dtype == torch.bfloat16:
+            # the weight gradient is written by the kernel into the optimizer's flat buffer
+            out = {}
+            writer(w, lambda dst, acc: out.setdefault("dx", C.rms_norm_bwd(dy2, h, w, rstd, dh, dst, acc)[0]))
+            dx = out["dx"].view(dy.shape)
+            return dx, dx, None, None
+        dx, dw = C.rms_norm_bwd(dy2, h, w, rstd, dh)
         dx = dx.view(dy.shape)
         return dx, dx, dw.to(w.dtype), None
 

@@ -146,6 +146,12 @@ class ZeroOptimizer:
                 # GEMM-produced weight gradients are written straight into flat_grad (ops.linear)
                 p._dsa_grad_sink = self._direct_grad
                 p._dsa_fresh = True
+            if p.dim() == 1:
+                # norm weights: RMSNorm backward's column-sum kernel writes into flat_grad too
+                # (ops.functional).  The embedding keeps PyTorch's backward: it sums repeated token
+                # rows in fp32, which a bf16 atomic scatter into the flat buffer would not.
+                p._dsa_grad_writer = self._direct_write
+                p._dsa_fresh = True
             if self._hooks_on:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self._direct_ok = set()
@@ -158,6 +164,8 @@ class ZeroOptimizer:
             b.pending = len(b.params)
             b.work = None
             b.updated = False
+        # parameters already counted down in this step's synchronising backward (see _on_grad_ready)
+        self._reported = set()
 
     def _direct_grad(self, p: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
         """Weight gradient sink for ``ops.linear``: dW = a @ b (a = g^T [P, T], b = x [T, Q], as
@@ -171,9 +179,28 @@ class ZeroOptimizer:
         if self._hooks_on:
             self._on_grad_ready(p)
 
+    def _direct_write(self, p: torch.Tensor, write):
+        """Gradient writer for kernels that produce a parameter's gradient themselves:
+        ``write(dst, accumulate)`` fills (first micro-batch) or adds into ``p.grad``."""
+        write(p.grad, not p._dsa_fresh)
+        p._dsa_fresh = False
+        self._direct_ok.add(p)
+        if self._hooks_on:
+            self._on_grad_ready(p)
+
     def _on_grad_ready(self, p: torch.Tensor):
+        """Count ``p`` down in its bucket; the bucket's reduce-scatter / AdamW start at zero.
+
+        A parameter whose gradient a kernel writes directly (GEMM sink, norm writer) reports from
+        inside its op's backward, and PyTorch then STILL runs its post-accumulate-grad hook (the
+        op returned None for it: the hook fires with an undefined gradient).  Without the
+        ``_reported`` set that second report counted the bucket down twice, so it could be
+        reduce-scattered / updated before its last parameter's gradient had landed."""
         if not self.sync_grads:
             return
+        if p in self._reported:
+            return
+        self._reported.add(p)
         b = self._bucket_of[p]
         b.pending -= 1
         if b.pending == 0:

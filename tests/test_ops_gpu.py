@@ -214,12 +214,18 @@ def test_optimizer_in_backward_matches_plain_step(gpu):
     within the run-to-run variation of the plain path itself (library GEMMs may pick
     stream-K kernels whose partial-tile fix-up order is not fixed)."""
     m1, o1, l1 = _train_tiny(gpu, overlap_update=True)
+    _, _, l1b = _train_tiny(gpu, overlap_update=True)
     m2, o2, l2 = _train_tiny(gpu, overlap_update=False)
     m3, _, l3 = _train_tiny(gpu, overlap_update=False)
     assert o1._side is not None and o2._side is None
-    noise = max(abs(a - b) for a, b in zip(l2, l3))
+    # run-to-run noise of either path (library GEMMs may pick stream-K kernels whose fix-up order
+    # follows kernel timing, which the overlapped AdamW shifts); the two paths compute the same
+    # update, so beyond that noise only 0.01 % of the loss is allowed (a bucket updated before its
+    # last gradient landed -- the double-counting bug fixed in ZeroOptimizer._on_grad_ready --
+    # moved the loss by 0.06 % after 3 steps)
+    noise = max(max(abs(a - b) for a, b in zip(l2, l3)), max(abs(a - b) for a, b in zip(l1, l1b)))
     diff = max(abs(a - b) for a, b in zip(l1, l2))
-    assert diff <= 10 * noise + 2e-3, (l1, l2, l3)
+    assert diff <= 10 * noise + 1e-4 * abs(l2[-1]), (l1, l1b, l2, l3)
     for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
         rel = ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
         assert rel < 1e-2, f"{n}: {rel}"
@@ -344,3 +350,20 @@ def test_swiglu_down_chain_wgrad_modes_agree(gpu, monkeypatch):
     assert torch.equal(res["auto"][0], res["strided"][0])
     ra, rs = res["auto"][1].float(), res["strided"][1].float()
     assert ((ra - rs).norm() / rs.norm()).item() < 4e-3
+
+
+def test_rms_norm_bwd_writes_weight_grad_in_place(gpu):
+    """rms_norm_bwd(dw_out=..., accumulate) writes/accumulates the bf16 weight gradient in place."""
+    Cx = _ext.require()
+    T, D = 256, 512
+    x = _rand(T, D, device=gpu, seed=18)
+    w = _rand(D, device=gpu, seed=19) + 1
+    dy = _rand(T, D, device=gpu, seed=20)
+    _, rstd = Cx.rms_norm_fwd(x, w, 1e-5)
+    dx_ref, dw_ref = Cx.rms_norm_bwd(dy, x, w, rstd)
+    out = torch.full((D,), 7.0, device=gpu, dtype=torch.bfloat16)
+    dx, _ = Cx.rms_norm_bwd(dy, x, w, rstd, None, out, False)
+    assert torch.equal(dx, dx_ref)
+    _close(out, dw_ref, 5e-2, 1e-2)
+    Cx.rms_norm_bwd(dy, x, w, rstd, None, out, True)
+    _close(out, 2 * dw_ref, 1e-1, 1e-2)

@@ -130,3 +130,38 @@ def test_zero_bucket_layout_is_padded_and_reverse_ordered(bucket_numel):
     first = opt.buckets[0].params[0]
     assert first is list(model.parameters())[-1]  # last-registered param first (backward order)
     assert opt.total_numel >= sum(p.numel() for p in model.parameters())
+
+
+def test_bucket_completes_once_after_all_its_gradients():
+    """Every bucket is counted down exactly once per parameter in the synchronising backward and
+    completes only after all of its parameters' gradients were produced -- also for parameters whose
+    gradient a kernel writes directly (PyTorch still runs their post-accumulate-grad hook, with an
+    undefined gradient, after the op already reported them)."""
+    model = _model()
+    opt = ZeroOptimizer(model, lr=LR, bucket_numel=1 << 18)
+    assert len(opt.buckets) > 2
+    seen, completions = set(), []
+    orig = ZeroOptimizer._on_grad_ready
+
+    def on_ready(p):
+        if opt.sync_grads and p.grad is not None:
+            seen.add(p)
+        before = opt._bucket_of[p].pending
+        orig(opt, p)
+        b = opt._bucket_of[p]
+        if before == 1 and b.pending == 0:
+            completions.append((b.index, {id(q) for q in seen}))
+
+    opt._on_grad_ready = on_ready
+    opt._hooks_on = True
+    for p in model.parameters():
+        p.register_post_accumulate_grad_hook(on_ready)
+    batches = _batches(2, 2, seed=3)
+    opt.zero_grad()
+    for i, b in enumerate(batches):
+        opt.sync_grads = i == len(batches) - 1
+        model.loss(b[:, :-1], b[:, 1:]).backward()
+    assert sorted(i for i, _ in completions) == list(range(len(opt.buckets)))  # each exactly once
+    for i, seen_ids in completions:
+        assert {id(p) for p in opt.buckets[i].params} <= seen_ids, f"bucket {i} completed early"
+    assert all(b.pending == 0 for b in opt.buckets)

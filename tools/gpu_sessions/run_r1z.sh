@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_r1z.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/gpu_tests_r1z.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_r1z.log
+bash tools/prof_tag.sh r1z
