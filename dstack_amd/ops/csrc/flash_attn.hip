@@ -41,7 +41,11 @@ constexpr int HD = 128;          // head dim
 // NW waves per workgroup, 32 query rows each (QB = 32 * NW rows per workgroup); every wave of the
 // workgroup shares the K/V tiles.  NW = 4 (2 workgroups per CU) or 8 (1 per CU: half the K/V
 // LDS-DMA traffic per query row; the default when S % 256 == 0).
-template <bool CAUSAL, int NW = 4>
+// PF: the S^T = K·Q^T phase keeps 4 K-fragment reads in flight and alternates the two accumulator
+// chains, instead of one read -> lgkmcnt(0) -> MFMA per step (which exposes the LDS latency on
+// every MFMA of the phase): 0.702 vs 0.713 ms at S=8192 over three interleaved same-box runs
+// (tools/gpu_sessions/run_r1ze.sh); DSTACK_AMD_FA_FWD_PF=0 selects the old form.
+template <bool CAUSAL, int NW = 4, bool PF = true>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
                                                         float* __restrict__ lse, int B, int S,
@@ -91,11 +95,34 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
     if (!CAUSAL || kv0 <= qw0 + 31) {
       f32x16 st[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[t][r] = 0.f;
+      if constexpr (PF) {
+        // step i: key tile t = i & 1, k-slice ks = i >> 1; fragment i + 4 is read while i computes
+        bf16x8 kf[4];
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) st[t] = mfma(lds_row(kl, 32 * t + l32, 2 * ks + hf), qf[ks], st[t]);
+        for (int i = 0; i < 4; ++i) kf[i] = lds_row(kl, 32 * (i & 1) + l32, 2 * (i >> 1) + hf);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const bf16x8 a = kf[i & 3];
+          if (i + 4 < 16) kf[i & 3] = lds_row(kl, 32 * ((i + 4) & 1) + l32, 2 * ((i + 4) >> 1) + hf);
+          st[i & 1] = mfma(a, qf[i >> 1], st[i & 1]);
+        }
+        // pin the interleave (the scheduler otherwise sinks each read below the MFMAs that free
+        // its register, leaving one read pair in flight): 4 reads, then (MFMA, read) x 12, 4 MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      } else {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int ks = 0; ks < 8; ++ks) st[t] = mfma(lds_row(kl, 32 * t + l32, 2 * ks + hf), qf[ks], st[t]);
       }
       // only the tile(s) crossing this wave's diagonal need the causal mask (wave-uniform test)
       if (CAUSAL && kv0 + 63 > qw0) {
@@ -666,10 +693,16 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     const char* v = getenv("DSTACK_AMD_FA_FWD_WAVES");
     return (v && atoi(v) == 4) ? 4 : 8;
   }();
+  static const bool pf = [] {
+    const char* v = getenv("DSTACK_AMD_FA_FWD_PF");
+    return !(v && atoi(v) == 0);
+  }();
   if (waves == 8 && S % 256 == 0) {
     const int grid = B * H * (S / 256);
-    if (causal)
+    if (causal && pf)
       fa_fwd_kernel<true, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+    else if (causal)
+      fa_fwd_kernel<true, 8, false><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
     else
       fa_fwd_kernel<false, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
     return hipGetLastError();
