@@ -274,6 +274,31 @@ class ZeroOptimizer:
         self._arm()
 
     @torch.no_grad()
+    # ---- checkpointing (reference: none -- dstack leaves ML checkpoints to the job) ----
+    def shard_state(self) -> dict:
+        """This rank's fp32 AdamW state (master weights, first and second moments) by bucket."""
+        out = {}
+        for i in range(len(self.buckets)):
+            out[f"master.{i}"] = self.master[i]
+            out[f"exp_avg.{i}"] = self.exp_avg[i]
+            out[f"exp_avg_sq.{i}"] = self.exp_avg_sq[i]
+        return out
+
+    def load_state(self, flat_param: torch.Tensor, shard: dict, step_count: int):
+        """Restore from :meth:`shard_state` of the same rank in a job of the same world size and
+        the full bf16 parameter buffer."""
+        if flat_param.numel() != self.total_numel:
+            raise ValueError(f"checkpoint has {flat_param.numel()} parameters, this model {self.total_numel}")
+        self.flat_param.copy_(flat_param.to(self.flat_param.device, self.flat_param.dtype))
+        for i in range(len(self.buckets)):
+            for name, dst in (("master", self.master), ("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
+                src = shard[f"{name}.{i}"]
+                if src.numel() != dst[i].numel():
+                    raise ValueError(f"{name}.{i}: shard of {src.numel()} elements, expected {dst[i].numel()} "
+                                     "(checkpoints restore only into the same world size)")
+                dst[i].copy_(src.to(dst[i].device))
+        self.step_count = step_count
+
     def step(self):
         self.wait_params()  # no forward ran since the last step: finish its all-gathers first
         self.step_count += 1

@@ -93,9 +93,54 @@ class Trainer:
         self.opt.step()
         return total / self.grad_accum
 
+    # ---- checkpoints: safetensors, one optimizer shard per rank, written to a directory that is
+    # usually a dstack volume (the reference leaves checkpointing to the job) ----
+    def save_checkpoint(self, path: str):
+        from safetensors.torch import save_file
+
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        os.makedirs(path, exist_ok=True)
+        meta = os.path.join(path, "meta.json")
+        if rank == 0 and os.path.exists(meta):
+            os.remove(meta)  # incomplete until rewritten below
+        shard = {k: v.detach().cpu().contiguous() for k, v in self.opt.shard_state().items()}
+        _atomic_save(save_file, shard, os.path.join(path, f"optim-rank{rank:05d}-of-{world:05d}.safetensors"))
+        if rank == 0:
+            _atomic_save(save_file, {"flat_param": self.opt.flat_param.detach().cpu()},
+                         os.path.join(path, "params.safetensors"))
+        if dist.is_initialized():
+            dist.barrier()
+        if rank == 0:
+            with open(meta + ".tmp", "w") as f:
+                json.dump({"step": self.opt.step_count, "world": world, "data_index": self._i,
+                           "total_numel": self.opt.total_numel, "model": self.cfg.name}, f)
+            os.replace(meta + ".tmp", meta)
+
+    def load_checkpoint(self, path: str) -> int:
+        """Restore a checkpoint written by :meth:`save_checkpoint`; returns its step."""
+        from safetensors.torch import load_file
+
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        with open(os.path.join(path, "meta.json")) as f:
+            meta = json.load(f)
+        if meta["world"] != world:
+            raise ValueError(f"checkpoint written by {meta['world']} ranks, this job has {world}")
+        params = load_file(os.path.join(path, "params.safetensors"))["flat_param"]
+        shard = load_file(os.path.join(path, f"optim-rank{rank:05d}-of-{world:05d}.safetensors"))
+        self.opt.load_state(params, shard, meta["step"])
+        self._i = meta["data_index"]
+        return meta["step"]
+
     @property
     def tokens_per_step(self) -> int:
         return self.micro_batch * self.seq_len * self.grad_accum
+
+
+def _atomic_save(save_file, tensors: dict, dst: str):
+    save_file(tensors, dst + ".tmp")
+    os.replace(dst + ".tmp", dst)
 
 
 def _sync(env: DistEnv):
@@ -106,7 +151,7 @@ def _sync(env: DistEnv):
 
 
 def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1,
-        grad_accum: int = 1):
+        grad_accum: int = 1, checkpoint_dir: str | None = None, save_every: int = 0):
     env = init_distributed()
     device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     from dstack_amd.ops import gemm_tuning
@@ -117,6 +162,10 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
               f"init={time.time()-t0:.1f}s gemm_tuning={gemm_mode}", flush=True)
+    if checkpoint_dir and os.path.exists(os.path.join(checkpoint_dir, "meta.json")):
+        resumed = tr.load_checkpoint(checkpoint_dir)
+        if env.rank == 0:
+            print(f"[train] resumed from {checkpoint_dir} at step {resumed}", flush=True)
     for i in range(warmup):
         loss = tr.step()
         if env.rank == 0:
@@ -128,6 +177,8 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         losses.append(tr.step())
         if log_every and env.rank == 0 and (i + 1) % log_every == 0:
             print(f"[train] step {i} loss={losses[-1].item():.4f}", flush=True)
+        if checkpoint_dir and save_every and (i + 1) % save_every == 0:
+            tr.save_checkpoint(checkpoint_dir)  # inside the timed loop only when asked for
     _sync(env)
     elapsed = time.perf_counter() - t_start
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -158,9 +209,14 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--checkpoint-dir", default=None,
+                    help="resume from here if it holds a checkpoint (e.g. a dstack volume mount)")
+    ap.add_argument("--save-every", type=int, default=0, help="save a checkpoint every N timed steps")
     args = ap.parse_args(argv)
-    env, _, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup,
-                    grad_accum=args.grad_accum)
+    env, tr, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup,
+                     grad_accum=args.grad_accum, checkpoint_dir=args.checkpoint_dir, save_every=args.save_every)
+    if args.checkpoint_dir:
+        tr.save_checkpoint(args.checkpoint_dir)
     if env.distributed:
         dist.destroy_process_group()
 
