@@ -273,7 +273,6 @@ class ZeroOptimizer:
         self._direct_ok = set()
         self._arm()
 
-    @torch.no_grad()
     # ---- checkpointing (reference: none -- dstack leaves ML checkpoints to the job) ----
     def shard_state(self) -> dict:
         """This rank's fp32 AdamW state (master weights, first and second moments) by bucket."""
@@ -284,6 +283,7 @@ class ZeroOptimizer:
             out[f"exp_avg_sq.{i}"] = self.exp_avg_sq[i]
         return out
 
+    @torch.no_grad()
     def load_state(self, flat_param: torch.Tensor, shard: dict, step_count: int):
         """Restore from :meth:`shard_state` of the same rank in a job of the same world size and
         the full bf16 parameter buffer."""
@@ -299,6 +299,7 @@ class ZeroOptimizer:
                 dst[i].copy_(src.to(dst[i].device))
         self.step_count = step_count
 
+    @torch.no_grad()
     def step(self):
         self.wait_params()  # no forward ran since the last step: finish its all-gathers first
         self.step_count += 1

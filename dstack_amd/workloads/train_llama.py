@@ -13,6 +13,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import time
 from dataclasses import dataclass
 
@@ -94,41 +95,101 @@ class Trainer:
         return total / self.grad_accum
 
     # ---- checkpoints: safetensors, one optimizer shard per rank, written to a directory that is
-    # usually a dstack volume (the reference leaves checkpointing to the job) ----
-    def save_checkpoint(self, path: str):
+    # usually a dstack volume (the reference leaves checkpointing to the job).
+    #
+    # Layout: ``<dir>/step-<N>/`` holds ``optim-rank<r>-of-<w>.safetensors`` (every rank),
+    # ``params.safetensors`` and ``meta.json`` (local rank 0 of every node, so node-local volumes
+    # such as ``${{ dstack.node_rank }}`` ones work too); ``<dir>/latest`` names the newest complete
+    # step directory and is replaced atomically only after every rank has finished writing, so a
+    # save cut short is never loaded.  Older step directories beyond ``keep`` are pruned. ----
+    def save_checkpoint(self, path: str, keep: int = 2):
         from safetensors.torch import save_file
 
-        rank = dist.get_rank() if dist.is_initialized() else 0
-        world = dist.get_world_size() if dist.is_initialized() else 1
-        os.makedirs(path, exist_ok=True)
-        meta = os.path.join(path, "meta.json")
-        if rank == 0 and os.path.exists(meta):
-            os.remove(meta)  # incomplete until rewritten below
+        rank, world, local_rank = _ranks()
+        # the all-gathers of the last step may still be in flight (prefetch hooks defer the wait
+        # to the next forward): the saved bf16 params must be the fully gathered buffer
+        self.opt.wait_params()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        step = self.opt.step_count
+        sdir = os.path.join(path, f"step-{step:08d}")
+        os.makedirs(sdir, exist_ok=True)
         shard = {k: v.detach().cpu().contiguous() for k, v in self.opt.shard_state().items()}
-        _atomic_save(save_file, shard, os.path.join(path, f"optim-rank{rank:05d}-of-{world:05d}.safetensors"))
-        if rank == 0:
+        _atomic_save(save_file, shard, os.path.join(sdir, f"optim-rank{rank:05d}-of-{world:05d}.safetensors"), rank)
+        if local_rank == 0:
             _atomic_save(save_file, {"flat_param": self.opt.flat_param.detach().cpu()},
-                         os.path.join(path, "params.safetensors"))
+                         os.path.join(sdir, "params.safetensors"), rank)
+            _atomic_write(os.path.join(sdir, "meta.json"),
+                          json.dumps({"step": step, "world": world, "data_index": self._i,
+                                      "total_numel": self.opt.total_numel, "model": self.cfg.name}), rank)
+        if dist.is_initialized():
+            dist.barrier()  # every shard of this step is on disk before ``latest`` points at it
+        if local_rank == 0:
+            _atomic_write(os.path.join(path, "latest"), os.path.basename(sdir), rank)
+            olds = sorted(d for d in os.listdir(path) if d.startswith("step-") and d != os.path.basename(sdir))
+            for d in olds[: max(0, len(olds) - (keep - 1))]:
+                shutil.rmtree(os.path.join(path, d), ignore_errors=True)
         if dist.is_initialized():
             dist.barrier()
-        if rank == 0:
-            with open(meta + ".tmp", "w") as f:
-                json.dump({"step": self.opt.step_count, "world": world, "data_index": self._i,
-                           "total_numel": self.opt.total_numel, "model": self.cfg.name}, f)
-            os.replace(meta + ".tmp", meta)
 
-    def load_checkpoint(self, path: str) -> int:
+    @staticmethod
+    def checkpoint_step(path: str | None) -> int | None:
+        """The step of the newest complete checkpoint under ``path`` (None if there is none)."""
+        if not path:
+            return None
+        try:
+            with open(os.path.join(path, "latest")) as f:
+                name = f.read().strip()
+            with open(os.path.join(path, name, "meta.json")) as f:
+                return int(json.load(f)["step"])
+        except (OSError, ValueError, KeyError):
+            return None
+
+    def resume_step(self, path: str | None) -> int | None:
+        """Collective: rank 0 decides whether to resume (and from which step) and broadcasts it;
+        every rank then checks that it can read that step's files, so a directory that is not
+        shared across nodes (or a node that lost its volume) fails on every rank at once instead
+        of leaving some ranks resumed and others hanging in a collective."""
+        step = self.checkpoint_step(path)
+        if not dist.is_initialized():
+            return step
+        dev = self.device if self._backend_is_nccl() else torch.device("cpu")
+        t = torch.tensor([-1 if step is None else step], dtype=torch.int64, device=dev)
+        dist.broadcast(t, src=0)
+        step = None if t.item() < 0 else int(t.item())
+        if step is None:
+            return None
+        rank, world, _ = _ranks()
+        sdir = os.path.join(path, f"step-{step:08d}")
+        ok = all(os.path.exists(os.path.join(sdir, f)) for f in
+                 ("meta.json", "params.safetensors", f"optim-rank{rank:05d}-of-{world:05d}.safetensors"))
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.SUM)
+        if flag.item():
+            raise RuntimeError(f"{int(flag.item())} rank(s) cannot read checkpoint step {step} under {path}: "
+                               "--checkpoint-dir must be shared by the ranks of a node (one volume per node, "
+                               "or one network volume for all nodes)")
+        return step
+
+    def _backend_is_nccl(self) -> bool:
+        return dist.is_initialized() and dist.get_backend() == "nccl"
+
+    def load_checkpoint(self, path: str, step: int | None = None) -> int:
         """Restore a checkpoint written by :meth:`save_checkpoint`; returns its step."""
         from safetensors.torch import load_file
 
-        rank = dist.get_rank() if dist.is_initialized() else 0
-        world = dist.get_world_size() if dist.is_initialized() else 1
-        with open(os.path.join(path, "meta.json")) as f:
+        rank, world, _ = _ranks()
+        if step is None:
+            step = self.checkpoint_step(path)
+            if step is None:
+                raise FileNotFoundError(f"no complete checkpoint under {path}")
+        sdir = os.path.join(path, f"step-{step:08d}")
+        with open(os.path.join(sdir, "meta.json")) as f:
             meta = json.load(f)
         if meta["world"] != world:
             raise ValueError(f"checkpoint written by {meta['world']} ranks, this job has {world}")
-        params = load_file(os.path.join(path, "params.safetensors"))["flat_param"]
-        shard = load_file(os.path.join(path, f"optim-rank{rank:05d}-of-{world:05d}.safetensors"))
+        params = load_file(os.path.join(sdir, "params.safetensors"))["flat_param"]
+        shard = load_file(os.path.join(sdir, f"optim-rank{rank:05d}-of-{world:05d}.safetensors"))
         self.opt.load_state(params, shard, meta["step"])
         self._i = meta["data_index"]
         return meta["step"]
@@ -138,9 +199,25 @@ class Trainer:
         return self.micro_batch * self.seq_len * self.grad_accum
 
 
-def _atomic_save(save_file, tensors: dict, dst: str):
-    save_file(tensors, dst + ".tmp")
-    os.replace(dst + ".tmp", dst)
+def _ranks() -> tuple[int, int, int]:
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", dist.get_rank()))
+    return 0, 1, 0
+
+
+def _atomic_save(save_file, tensors: dict, dst: str, rank: int = 0):
+    tmp = f"{dst}.tmp{rank}"  # per-writer temp name: ranks of different nodes may share a volume
+    save_file(tensors, tmp)
+    os.replace(tmp, dst)
+
+
+def _atomic_write(dst: str, text: str, rank: int = 0):
+    tmp = f"{dst}.tmp{rank}"
+    with open(tmp, "w") as f:
+        f.write(text)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, dst)
 
 
 def _sync(env: DistEnv):
@@ -162,33 +239,46 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
               f"init={time.time()-t0:.1f}s gemm_tuning={gemm_mode}", flush=True)
-    if checkpoint_dir and os.path.exists(os.path.join(checkpoint_dir, "meta.json")):
-        resumed = tr.load_checkpoint(checkpoint_dir)
-        if env.rank == 0:
-            print(f"[train] resumed from {checkpoint_dir} at step {resumed}", flush=True)
+    if checkpoint_dir:
+        # --steps is the job's total number of optimizer steps: a resumed job (retry after an
+        # interruption) trains only the remainder and skips the warmup; saves fall on global
+        # step numbers (opt.step_count % save_every == 0)
+        resumed = tr.resume_step(checkpoint_dir)
+        if resumed is not None:
+            tr.load_checkpoint(checkpoint_dir, resumed)
+            warmup = 0
+            if env.rank == 0:
+                print(f"[train] resumed from {checkpoint_dir} at step {resumed}", flush=True)
+        warmup = max(0, min(warmup, steps - tr.opt.step_count))
+        steps = max(0, steps - tr.opt.step_count - warmup)
+
+    def _maybe_save():
+        if checkpoint_dir and save_every and tr.opt.step_count % save_every == 0:
+            tr.save_checkpoint(checkpoint_dir)
+
     for i in range(warmup):
         loss = tr.step()
         if env.rank == 0:
             print(f"[train] warmup {i} loss={loss.item():.4f}", flush=True)
+        _maybe_save()
     _sync(env)
     t_start = time.perf_counter()
     losses = []
     for i in range(steps):
         losses.append(tr.step())
         if log_every and env.rank == 0 and (i + 1) % log_every == 0:
-            print(f"[train] step {i} loss={losses[-1].item():.4f}", flush=True)
-        if checkpoint_dir and save_every and (i + 1) % save_every == 0:
-            tr.save_checkpoint(checkpoint_dir)  # inside the timed loop only when asked for
+            print(f"[train] step {tr.opt.step_count} loss={losses[-1].item():.4f}", flush=True)
+        _maybe_save()  # inside the timed loop only when asked for
     _sync(env)
     elapsed = time.perf_counter() - t_start
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if env.distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
-    tok_s = tr.tokens_per_step * env.world * steps / elapsed
+    tok_s = tr.tokens_per_step * env.world * steps / elapsed if steps else 0.0
     result = {
         "tokens_per_s": tok_s,
-        "ms_per_step": elapsed / steps * 1e3,
+        "ms_per_step": elapsed / steps * 1e3 if steps else 0.0,
         "world": env.world,
         "flops_per_token": tr.cfg.flops_per_token(seq_len),
         "final_loss": losses[-1].item() if losses else None,
@@ -206,17 +296,19 @@ def main(argv=None):
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--seq-len", type=int, default=8192)
     ap.add_argument("--micro-batch", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=10,
+                    help="timed steps; with --checkpoint-dir the job's total optimizer steps (warmup included)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--checkpoint-dir", default=None,
                     help="resume from here if it holds a checkpoint (e.g. a dstack volume mount)")
-    ap.add_argument("--save-every", type=int, default=0, help="save a checkpoint every N timed steps")
+    ap.add_argument("--save-every", type=int, default=0,
+                    help="save a checkpoint whenever the optimizer step count is a multiple of N")
     args = ap.parse_args(argv)
     env, tr, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup,
                      grad_accum=args.grad_accum, checkpoint_dir=args.checkpoint_dir, save_every=args.save_every)
-    if args.checkpoint_dir:
-        tr.save_checkpoint(args.checkpoint_dir)
+    if args.checkpoint_dir and not (args.save_every and tr.opt.step_count % args.save_every == 0):
+        tr.save_checkpoint(args.checkpoint_dir)  # (a step that is a multiple of save_every is saved)
     if env.distributed:
         dist.destroy_process_group()
 
