@@ -26,6 +26,13 @@ hipError_t dsa_fa_fwd(const void*, void*, float*, int, int, int, int, int, float
 size_t dsa_fa_bwd_workspace(int, int, int);
 hipError_t dsa_fa_bwd(const void*, const void*, const void*, const float*, void*, void*, int, int, int, int,
                       int, float, int, hipStream_t);
+int dsa_paged_page_size();
+hipError_t dsa_rope_cache_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int,
+                                int, hipStream_t);
+hipError_t dsa_paged_decode(const void*, long, const void*, const void*, const int*, int, const int*, void*, float*,
+                            float*, int, int, int, int, int, float, hipStream_t);
+hipError_t dsa_sample(const void*, long, int, int, const float*, const int64_t*, const int*, int*, float*,
+                      hipStream_t);
 bool dsa_gemm_tn_supported(int, int, int);
 hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 }
@@ -250,6 +257,88 @@ void gemm_tn(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool accumulat
         "gemm_tn");
 }
 
+// ---- serving: paged KV cache (k [P][KVH][64][128], v [P][KVH][128][64]) ----
+void check_i32(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kInt32 && t.is_contiguous(), name,
+              " must be a contiguous int32 ROCm tensor");
+}
+
+void check_cache(const torch::Tensor& k, const torch::Tensor& v, int64_t KVH) {
+  check_bf16(k, "k_cache");
+  check_bf16(v, "v_cache");
+  const int64_t P = dsa_paged_page_size();
+  TORCH_CHECK(k.dim() == 4 && k.size(1) == KVH && k.size(2) == P && k.size(3) == 128,
+              "k_cache must be [pages, KVH, 64, 128]");
+  TORCH_CHECK(v.dim() == 4 && v.size(0) == k.size(0) && v.size(1) == KVH && v.size(2) == 128 && v.size(3) == P,
+              "v_cache must be [pages, KVH, 128, 64]");
+}
+
+// rotates q/k of qkv [T, (H+2KVH)*128] in place and writes k, v of each token to its cache slot
+void rope_cache_write(torch::Tensor qkv, torch::Tensor positions, torch::Tensor slots, torch::Tensor cos,
+                      torch::Tensor sin, torch::Tensor k_cache, torch::Tensor v_cache, int64_t H, int64_t KVH) {
+  check_bf16(qkv, "qkv");
+  check_i32(positions, "positions");
+  check_i32(slots, "slots");
+  check_cache(k_cache, v_cache, KVH);
+  const int64_t T = positions.numel();
+  TORCH_CHECK(slots.numel() == T && qkv.numel() == T * (H + 2 * KVH) * 128, "rope_cache_write: shape mismatch");
+  TORCH_CHECK(cos.scalar_type() == torch::kFloat32 && sin.scalar_type() == torch::kFloat32 && cos.is_contiguous() &&
+                  sin.is_contiguous() && cos.size(1) == 64 && sin.sizes() == cos.sizes(),
+              "rope tables must be fp32 [max_pos, 64]");
+  check(dsa_rope_cache_write(qkv.data_ptr(), positions.data_ptr<int>(), slots.data_ptr<int>(), cos.data_ptr<float>(),
+                             sin.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(), (int)T, (int)H, (int)KVH,
+                             stream()),
+        "rope_cache_write");
+}
+
+// q: [B, >= H*128] rows (e.g. the fused qkv output; its row stride is passed); out [B, H*128] bf16.
+// o_part / lse_part: fp32 workspaces of >= B*H*nsplit*128 and B*H*nsplit elements (unused when nsplit == 1)
+void paged_decode(torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor block_tables,
+                  torch::Tensor ctx_lens, torch::Tensor out, torch::Tensor o_part, torch::Tensor lse_part, int64_t H,
+                  int64_t KVH, int64_t nsplit, int64_t pages_per_split, double scale) {
+  TORCH_CHECK(q.is_cuda() && q.scalar_type() == torch::kBFloat16 && q.dim() == 2 && q.stride(1) == 1 &&
+                  q.size(1) >= H * 128 && q.stride(0) % 8 == 0,
+              "q must be bf16 [B, >= H*128] with contiguous rows");
+  check_cache(k_cache, v_cache, KVH);
+  check_i32(block_tables, "block_tables");
+  check_i32(ctx_lens, "ctx_lens");
+  check_bf16(out, "out");
+  const int64_t B = q.size(0);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) == B && ctx_lens.numel() == B, "batch mismatch");
+  TORCH_CHECK(nsplit * pages_per_split >= block_tables.size(1), "splits do not cover the block table");
+  TORCH_CHECK(out.numel() == B * H * 128, "out must be [B, H*128]");
+  if (nsplit > 1) {
+    TORCH_CHECK(o_part.scalar_type() == torch::kFloat32 && o_part.numel() >= B * H * nsplit * 128 &&
+                    lse_part.scalar_type() == torch::kFloat32 && lse_part.numel() >= B * H * nsplit,
+                "paged_decode: split workspaces too small");
+  }
+  check(dsa_paged_decode(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                         block_tables.data_ptr<int>(), (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
+                         out.data_ptr(), nsplit > 1 ? o_part.data_ptr<float>() : nullptr,
+                         nsplit > 1 ? lse_part.data_ptr<float>() : nullptr, (int)B, (int)H, (int)KVH, (int)nsplit,
+                         (int)pages_per_split, (float)scale, stream()),
+        "paged_decode");
+}
+
+// tokens (int32 [rows]) and log-probs (fp32 [rows]) written in place; temps fp32, seeds int64, steps int32
+void sample(torch::Tensor logits, torch::Tensor temps, torch::Tensor seeds, torch::Tensor steps, torch::Tensor tokens,
+            torch::Tensor logprobs) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == torch::kBFloat16 && logits.dim() == 2 &&
+                  logits.stride(1) == 1,
+              "logits must be bf16 [rows, V] with contiguous rows");
+  const int64_t rows = logits.size(0);
+  TORCH_CHECK(temps.scalar_type() == torch::kFloat32 && temps.numel() == rows && temps.is_contiguous(), "temps");
+  TORCH_CHECK(seeds.scalar_type() == torch::kInt64 && seeds.numel() == rows && seeds.is_contiguous(), "seeds");
+  check_i32(steps, "steps");
+  check_i32(tokens, "tokens");
+  TORCH_CHECK(steps.numel() == rows && tokens.numel() == rows, "sample: rows mismatch");
+  TORCH_CHECK(logprobs.scalar_type() == torch::kFloat32 && logprobs.numel() == rows, "logprobs fp32 [rows]");
+  check(dsa_sample(logits.data_ptr(), logits.stride(0), (int)rows, (int)logits.size(1), temps.data_ptr<float>(),
+                   seeds.data_ptr<int64_t>(), steps.data_ptr<int>(), tokens.data_ptr<int>(), logprobs.data_ptr<float>(),
+                   stream()),
+        "sample");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -271,4 +360,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("gemm_tn", &gemm_tn);
   m.def("gemm_tn_supported", &gemm_tn_supported);
+  m.def("paged_page_size", &dsa_paged_page_size);
+  m.def("rope_cache_write", &rope_cache_write);
+  m.def("paged_decode", &paged_decode);
+  m.def("sample", &sample);
 }

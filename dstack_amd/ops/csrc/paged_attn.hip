@@ -1,0 +1,408 @@
+// Serving kernels for CDNA4 / gfx950: paged KV cache writes, paged decode attention (GQA,
+// split-KV "flash decoding") and fused sampling.  Used by dstack_amd.serving (the MI355X-native
+// inference engine behind `type: service` runs); the reference orchestrator ships no model code
+// and delegates serving to vLLM/TGI containers (reference examples/deployment/vllm, tgi).
+//
+// KV cache layout, one pair of tensors per layer (PAGE = 64 tokens, head_dim 128):
+//   k_cache [num_pages][KVH][PAGE][128]   token-major: one 256-B row per key
+//   v_cache [num_pages][KVH][128][PAGE]   dim-major:   each V column is a 128-B run of 64 keys
+// so every MFMA operand of the decode kernel is one 16-byte load straight from HBM (no LDS):
+//
+//  * S^T = K · Q^T with v_mfma_f32_16x16x32_bf16: A = 16 keys x 32 dims (lane = key row, 16 B of
+//    its 256-B row), B = Q^T (lane = query column: the <=16 query heads that share one KV head,
+//    GQA), so one lane holds 4 keys' scores of ONE query -> the softmax max/sum are 16 in-register
+//    ops plus two xor-shuffles (lanes q, q+16, q+32, q+48).
+//  * The 4 key tiles of a page are ordered so that the S^T accumulators, packed to bf16, are
+//    directly the B operand of O^T += V^T · P^T with the keys in natural order (element j of lane
+//    group g = key 32m + 8g + j), and the V^T operand is one 16-B load of the dim-major V page.
+//  * O^T's layout puts the query on the lane, so the online-softmax rescale is lane-local.
+//  * Split-KV: grid = (splits, KVH, batch); each one-wave workgroup walks `pages_per_split` pages,
+//    writes a normalised partial O and its log2-sum-exp, and a combine kernel merges the splits
+//    (skipped when there is one split).  The grid is a function of the batch size and the
+//    maximum context only, so the decode step can be captured once per batch bucket in a
+//    hipGraph.
+#include "common.h"
+
+using namespace dsa;
+
+namespace {
+
+constexpr int PAGE = 64;
+constexpr int HDIM = 128;
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// RoPE on q and k of the fused projection output (in place) + K/V scatter into the paged cache.
+// qkv [T][(H + 2*KVH) * 128]; token t sits at position positions[t] and cache slot slots[t]
+// (= page * PAGE + offset; < 0: padding token, not cached).  One thread = 8 rotation pairs.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rope_cache_write_kernel(bf16_t* __restrict__ qkv,
+                                                               const int* __restrict__ positions,
+                                                               const int* __restrict__ slots,
+                                                               const float* __restrict__ cosT,
+                                                               const float* __restrict__ sinT,
+                                                               bf16_t* __restrict__ k_cache,
+                                                               bf16_t* __restrict__ v_cache, int T,
+                                                               int H, int KVH) {
+  constexpr int half = HDIM / 2, cph = half / 8;  // 8 chunks of 8 pairs per head
+  const int NH = H + 2 * KVH;
+  const size_t total = (size_t)T * NH * cph;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i / ((size_t)NH * cph));
+    const int rem = (int)(i % ((size_t)NH * cph));
+    const int head = rem / cph, c = rem % cph;
+    bf16_t* row = qkv + (size_t)t * NH * HDIM + (size_t)head * HDIM;
+    us8 a = *reinterpret_cast<const us8*>(row + c * 8);
+    us8 b = *reinterpret_cast<const us8*>(row + half + c * 8);
+    if (head < H + KVH) {  // q and k heads rotate
+      const int pos = positions[t];
+      const f4* cp = reinterpret_cast<const f4*>(cosT + (size_t)pos * half + c * 8);
+      const f4* sp = reinterpret_cast<const f4*>(sinT + (size_t)pos * half + c * 8);
+      const f4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+      const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      float x1[8], x2[8], o1[8], o2[8];
+      unpack8(a, x1);
+      unpack8(b, x2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o1[k] = x1[k] * cs[k] - x2[k] * sn[k];
+        o2[k] = x2[k] * cs[k] + x1[k] * sn[k];
+      }
+      a = pack8(o1);
+      b = pack8(o2);
+      *reinterpret_cast<us8*>(row + c * 8) = a;
+      *reinterpret_cast<us8*>(row + half + c * 8) = b;
+    }
+    const int slot = slots[t];
+    if (head < H || slot < 0) continue;
+    const int page = slot / PAGE, off = slot % PAGE;
+    if (head < H + KVH) {
+      bf16_t* dst = k_cache + (((size_t)page * KVH + (head - H)) * PAGE + off) * HDIM;
+      *reinterpret_cast<us8*>(dst + c * 8) = a;
+      *reinterpret_cast<us8*>(dst + half + c * 8) = b;
+    } else {
+      bf16_t* dst = v_cache + ((size_t)page * KVH + (head - H - KVH)) * HDIM * PAGE + off;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        dst[(size_t)(c * 8 + k) * PAGE] = a[k];
+        dst[(size_t)(half + c * 8 + k) * PAGE] = b[k];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Paged decode attention.  One wave = (batch row b, kv head, split).  q row b is at q + b*q_stride
+// with its H heads contiguous (128 elements each): the fused qkv output is read in place.
+// G = query heads per KV head (1..16).  Output: DIRECT -> out[b][h*128 + d] bf16 (one split);
+// otherwise o_part[b][h][split][128] fp32 (normalised) + lse_part[b][h][split] (log2 domain).
+// ------------------------------------------------------------------------------------------------
+template <bool DIRECT>
+__global__ __launch_bounds__(64) void paged_decode_kernel(
+    const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ ctx_lens, bf16_t* __restrict__ out, float* __restrict__ o_part,
+    float* __restrict__ lse_part, int H, int KVH, int G, int nsplit, int pages_per_split,
+    float scale_log2) {
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x, qc = lane & 15, g = lane >> 4;
+  const int ctx = ctx_lens[b];
+  const int n_pages = (ctx + PAGE - 1) / PAGE;
+  const int p0 = split * pages_per_split;
+  const int p1 = min(p0 + pages_per_split, n_pages);
+  const int h = kvh * G + qc;
+  const bool qvalid = qc < G;
+
+  float m = -INFINITY, l = 0.f;
+  f32x4_t acc[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) acc[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (p0 < p1) {
+    // Q^T operand: lane (qc, g) holds q[h][32kk + 8g .. +8] for k-step kk
+    bf16x8_t qf[4];
+    const bf16_t* qrow = q + (long)b * q_stride + (long)(qvalid ? h : kvh * G) * HDIM;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      qf[kk] = ld8(qrow + 32 * kk + 8 * g);
+      if (!qvalid) qf[kk] = bf16x8_t{};
+    }
+    const int* bt = block_tables + (long)b * bt_stride;
+    const int r = lane & 15;
+    for (int p = p0; p < p1; ++p) {
+      const long page = bt[p];
+      const bf16_t* kb = k_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
+      const bf16_t* vb = v_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
+      // issue every load of the page (K: 16 x 16 B, V: 16 x 16 B per lane) before any MFMA
+      bf16x8_t kf[4][4], vf[2][8];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int key = 32 * (t >> 1) + 8 * (r >> 2) + 4 * (t & 1) + (r & 3);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) kf[t][kk] = ld8(kb + key * HDIM + 32 * kk + 8 * g);
+      }
+#pragma unroll
+      for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+        for (int n = 0; n < 8; ++n) vf[mm][n] = ld8(vb + (16 * n + r) * PAGE + 32 * mm + 8 * g);
+      // S^T tiles: lane holds keys 32(t>>1) + 8g + 4(t&1) + i, i = 0..3, of query qc
+      f32x4_t s[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) s[t] = mfma16(kf[t][kk], qf[kk], s[t]);
+      }
+      const int base = p * PAGE;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = base + 32 * (t >> 1) + 8 * g + 4 * (t & 1) + i;
+          const float v = key < ctx ? s[t][i] * scale_log2 : -INFINITY;
+          s[t][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float alpha = fexp2(m - mn);
+      m = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = fexp2(s[t][i] - mn);
+          s[t][i] = e;
+          ls += e;
+        }
+      l = l * alpha + ls;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) acc[n] *= alpha;
+      // P^T operand of PV step mm: element j of lane group g = key 32mm + 8g + j
+#pragma unroll
+      for (int mm = 0; mm < 2; ++mm) {
+        bf16x8_t pf;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pf[i] = (__bf16)s[2 * mm][i];
+          pf[4 + i] = (__bf16)s[2 * mm + 1][i];
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) acc[n] = mfma16(vf[mm][n], pf, acc[n]);
+      }
+    }
+  }
+  // O^T accumulator: lane (qc, g) holds O[h][16n + 4g + i]
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qvalid) return;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (DIRECT) {
+    bf16_t* o = out + (long)b * H * HDIM + (long)h * HDIM;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      typedef unsigned short us4 __attribute__((ext_vector_type(4)));
+      us4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = f2bf(acc[n][i] * inv);
+      *reinterpret_cast<us4*>(o + 16 * n + 4 * g) = v;
+    }
+  } else {
+    const long idx = ((long)b * H + h) * nsplit + split;
+    float* o = o_part + idx * HDIM;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) *reinterpret_cast<f32x4_t*>(o + 16 * n + 4 * g) = acc[n] * inv;
+    if (g == 0) lse_part[idx] = l > 0.f ? m + __log2f(l) : -INFINITY;
+  }
+}
+
+// merge the split partials: out[b][h*128 + d] = sum_s 2^(lse_s - M) o_s / sum_s 2^(lse_s - M)
+__global__ __launch_bounds__(128) void paged_combine_kernel(const float* __restrict__ o_part,
+                                                            const float* __restrict__ lse_part,
+                                                            bf16_t* __restrict__ out, int H,
+                                                            int nsplit) {
+  const long bh = blockIdx.x;
+  const int d = threadIdx.x;
+  const float* lse = lse_part + bh * nsplit;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, lse[s]);
+  float num = 0.f, den = 0.f;
+  if (M > -INFINITY) {
+    for (int s = 0; s < nsplit; ++s) {
+      const float w = lse[s] > -INFINITY ? fexp2(lse[s] - M) : 0.f;
+      num += w * o_part[(bh * nsplit + s) * HDIM + d];
+      den += w;
+    }
+  }
+  out[bh * HDIM + d] = f2bf(den > 0.f ? num / den : 0.f);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sampling: one workgroup per row of logits [rows][V] (bf16, row stride `stride`).
+// temperature <= 0 -> greedy argmax; otherwise Gumbel-max over logits / T (exactly a draw from
+// softmax(logits / T)) with a counter-based hash of (seed, step, index).  Also returns the chosen
+// token's log-probability under softmax(logits / T) (greedy: T = 1), from an online max/sum in the
+// same pass.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void sample_kernel(const bf16_t* __restrict__ logits, long stride,
+                                                     int V, const float* __restrict__ temps,
+                                                     const int64_t* __restrict__ seeds,
+                                                     const int* __restrict__ steps,
+                                                     int* __restrict__ tokens,
+                                                     float* __restrict__ logprobs) {
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* x = logits + (long)row * stride;
+  const float T = temps[row];
+  const bool greedy = !(T > 0.f);
+  const float invT = greedy ? 1.f : 1.f / T;
+  const uint64_t key = mix64((uint64_t)seeds[row] * 0x9e3779b97f4a7c15ULL + (uint64_t)steps[row]);
+  float best = -INFINITY, mx = -INFINITY, sum = 0.f, bestx = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int i0 = tid * 8; i0 < V; i0 += 256 * 8) {
+    float v[8];
+    if (i0 + 8 <= V && (stride % 8) == 0) {
+      unpack8(*reinterpret_cast<const us8*>(x + i0), v);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = i0 + k < V ? bf2f(x[i0 + k]) : -INFINITY;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + k;
+      if (i >= V) break;
+      const float z = v[k] * invT;
+      if (z == -INFINITY) continue;  // masked logit (e.g. a banned token)
+      // online log-sum-exp of z
+      if (z > mx) {
+        sum = sum * __expf(mx - z) + 1.f;
+        mx = z;
+      } else {
+        sum += __expf(z - mx);
+      }
+      float score = z;
+      if (!greedy) {
+        const uint64_t hsh = mix64(key ^ ((uint64_t)i * 0xd1b54a32d192ed03ULL));
+        const float u = ((float)(hsh >> 40) + 0.5f) * (1.0f / 16777216.0f);
+        score = z - __logf(-__logf(u));
+      }
+      if (score > best || (score == best && i < bi)) {
+        best = score;
+        bi = i;
+        bestx = z;
+      }
+    }
+  }
+  // wave reduction of (best, bi, bestx) and (mx, sum)
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    const float ox = __shfl_xor(bestx, o, 64);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+      bestx = ox;
+    }
+    const float om = __shfl_xor(mx, o, 64), os = __shfl_xor(sum, o, 64);
+    const float nm = fmaxf(mx, om);
+    sum = (mx > -INFINITY ? sum * __expf(mx - nm) : 0.f) + (om > -INFINITY ? os * __expf(om - nm) : 0.f);
+    mx = nm;
+  }
+  __shared__ float sb[4], sx[4], sm[4], ss[4];
+  __shared__ int si[4];
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    sb[w] = best;
+    si[w] = bi;
+    sx[w] = bestx;
+    sm[w] = mx;
+    ss[w] = sum;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int k = 1; k < 4; ++k) {
+      if (sb[k] > best || (sb[k] == best && si[k] < bi)) {
+        best = sb[k];
+        bi = si[k];
+        bestx = sx[k];
+      }
+      const float nm = fmaxf(mx, sm[k]);
+      sum = (mx > -INFINITY ? sum * __expf(mx - nm) : 0.f) + (sm[k] > -INFINITY ? ss[k] * __expf(sm[k] - nm) : 0.f);
+      mx = nm;
+    }
+    tokens[row] = bi;
+    if (logprobs) logprobs[row] = bestx - (mx + __logf(sum));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+extern "C" int dsa_paged_page_size() { return PAGE; }
+
+extern "C" hipError_t dsa_rope_cache_write(void* qkv, const int* positions, const int* slots,
+                                           const float* cosT, const float* sinT, void* k_cache,
+                                           void* v_cache, int T, int H, int KVH, hipStream_t st) {
+  if (T <= 0) return hipSuccess;
+  const size_t work = (size_t)T * (H + 2 * KVH) * (HDIM / 16);
+  size_t grid = (work + 255) / 256;
+  if (grid > 65535 * 4) grid = 65535 * 4;
+  rope_cache_write_kernel<<<(unsigned)grid, 256, 0, st>>>((bf16_t*)qkv, positions, slots, cosT, sinT,
+                                                          (bf16_t*)k_cache, (bf16_t*)v_cache, T, H, KVH);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_paged_decode(const void* q, long q_stride, const void* k_cache,
+                                       const void* v_cache, const int* block_tables, int bt_stride,
+                                       const int* ctx_lens, void* out, float* o_part,
+                                       float* lse_part, int B, int H, int KVH, int nsplit,
+                                       int pages_per_split, float scale, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (KVH <= 0 || H % KVH || H / KVH > 16 || nsplit < 1 || pages_per_split < 1) return hipErrorInvalidValue;
+  const int G = H / KVH;
+  const float sl2 = scale * 1.4426950408889634f;
+  const dim3 grid(nsplit, KVH, B);
+  if (nsplit == 1) {
+    paged_decode_kernel<true><<<grid, 64, 0, st>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache,
+                                                  (const bf16_t*)v_cache, block_tables, bt_stride,
+                                                  ctx_lens, (bf16_t*)out, nullptr, nullptr, H, KVH, G,
+                                                  nsplit, pages_per_split, sl2);
+    return hipGetLastError();
+  }
+  paged_decode_kernel<false><<<grid, 64, 0, st>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache,
+                                                 (const bf16_t*)v_cache, block_tables, bt_stride,
+                                                 ctx_lens, nullptr, o_part, lse_part, H, KVH, G,
+                                                 nsplit, pages_per_split, sl2);
+  DSA_CHECK(hipGetLastError());
+  paged_combine_kernel<<<B * H, 128, 0, st>>>(o_part, lse_part, (bf16_t*)out, H, nsplit);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_sample(const void* logits, long stride, int rows, int V, const float* temps,
+                                 const int64_t* seeds, const int* steps, int* tokens, float* logprobs,
+                                 hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  sample_kernel<<<rows, 256, 0, st>>>((const bf16_t*)logits, stride, V, temps, seeds, steps, tokens,
+                                      logprobs);
+  return hipGetLastError();
+}

@@ -1,0 +1,157 @@
+"""Serving ops: paged KV cache writes, paged decode attention and sampling.
+
+HIP kernels in ``csrc/paged_attn.hip`` for ROCm tensors; the PyTorch functions here are the CPU
+path of the engine and the fp32 references the GPU tests compare against.
+
+Cache layout (per layer): ``k_cache [pages, KVH, PAGE, 128]`` token-major and
+``v_cache [pages, KVH, 128, PAGE]`` dim-major (see the kernel file for why), ``PAGE = 64``.
+A token's cache slot is ``page * PAGE + offset``.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from dstack_amd.ops import _ext
+
+PAGE = 64
+HEAD_DIM = 128
+
+
+def alloc_cache(num_pages: int, n_kv_heads: int, dtype=torch.bfloat16, device=None):
+    k = torch.zeros(num_pages, n_kv_heads, PAGE, HEAD_DIM, dtype=dtype, device=device)
+    v = torch.zeros(num_pages, n_kv_heads, HEAD_DIM, PAGE, dtype=dtype, device=device)
+    return k, v
+
+
+# ----------------------------------------------------------------------------------------------
+# RoPE + cache write
+# ----------------------------------------------------------------------------------------------
+def rope_cache_write(qkv: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cos: torch.Tensor,
+                     sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n_heads: int,
+                     n_kv_heads: int) -> torch.Tensor:
+    """Rotate q and k of ``qkv`` [T, (H + 2*KVH) * 128] in place (token t at ``positions[t]``) and
+    store k/v of every token with ``slots[t] >= 0`` in the cache.  Returns ``qkv``."""
+    if _ext.use_hip(qkv):
+        _ext.require().rope_cache_write(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads)
+        return qkv
+    return rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads)
+
+
+def rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads):
+    T = positions.numel()
+    x = qkv.view(T, n_heads + 2 * n_kv_heads, HEAD_DIM)
+    rot = x[:, : n_heads + n_kv_heads].float()
+    c = cos[positions.long()].unsqueeze(1)
+    s = sin[positions.long()].unsqueeze(1)
+    x1, x2 = rot[..., : HEAD_DIM // 2], rot[..., HEAD_DIM // 2 :]
+    x[:, : n_heads + n_kv_heads] = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(qkv.dtype)
+    keep = slots >= 0
+    if keep.any():
+        sl = slots[keep].long()
+        page, off = sl // PAGE, sl % PAGE
+        k = x[keep][:, n_heads : n_heads + n_kv_heads]  # [n, KVH, D]
+        v = x[keep][:, n_heads + n_kv_heads :]
+        k_cache[page, :, off, :] = k.to(k_cache.dtype)
+        v_cache[page, :, :, off] = v.to(v_cache.dtype)
+    return qkv
+
+
+# ----------------------------------------------------------------------------------------------
+# Paged decode attention
+# ----------------------------------------------------------------------------------------------
+def split_plan(batch: int, n_kv_heads: int, table_width: int, target_waves: int = 4096):
+    """(nsplit, pages_per_split): enough one-wave workgroups to fill 256 CUs at any context, a
+    function of the batch bucket and the block-table width only (graph-capturable)."""
+    want = max(1, math.ceil(target_waves / max(1, batch * n_kv_heads)))
+    nsplit = max(1, min(want, table_width))
+    pps = math.ceil(table_width / nsplit)
+    return math.ceil(table_width / pps), pps
+
+
+class DecodeWorkspace:
+    """Preallocated split-KV partials for a batch bucket (hipGraph-safe: no allocation per step)."""
+
+    def __init__(self, batch: int, n_heads: int, n_kv_heads: int, table_width: int, device):
+        self.nsplit, self.pps = split_plan(batch, n_kv_heads, table_width)
+        n = batch * n_heads * self.nsplit if self.nsplit > 1 else 1
+        self.o_part = torch.empty(n * HEAD_DIM, dtype=torch.float32, device=device)
+        self.lse_part = torch.empty(n, dtype=torch.float32, device=device)
+
+
+def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                 ctx_lens: torch.Tensor, n_heads: int, n_kv_heads: int, out: torch.Tensor | None = None,
+                 ws: DecodeWorkspace | None = None) -> torch.Tensor:
+    """Attention of one new query token per sequence over its cached keys/values.
+
+    ``q`` [B, >= H*128] (rows may be the fused qkv output: only the first H*128 columns are read),
+    ``block_tables`` [B, W] int32 page ids, ``ctx_lens`` [B] int32.  Returns [B, H*128]."""
+    B = q.shape[0]
+    if out is None:
+        out = torch.empty(B, n_heads * HEAD_DIM, dtype=q.dtype, device=q.device)
+    if _ext.use_hip(q):
+        if ws is None:
+            ws = DecodeWorkspace(B, n_heads, n_kv_heads, block_tables.shape[1], q.device)
+        _ext.require().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o_part, ws.lse_part,
+                                    n_heads, n_kv_heads, ws.nsplit, ws.pps, 1.0 / math.sqrt(HEAD_DIM))
+        return out
+    out.copy_(paged_decode_ref(q, k_cache, v_cache, block_tables, ctx_lens, n_heads, n_kv_heads).to(out.dtype))
+    return out
+
+
+def paged_decode_ref(q, k_cache, v_cache, block_tables, ctx_lens, n_heads, n_kv_heads):
+    """fp32 reference: gathers each sequence's pages and runs plain softmax attention."""
+    B = q.shape[0]
+    G = n_heads // n_kv_heads
+    out = torch.empty(B, n_heads * HEAD_DIM, dtype=torch.float32, device=q.device)
+    for b in range(B):
+        n = int(ctx_lens[b])
+        pages = block_tables[b, : (n + PAGE - 1) // PAGE].long()
+        k = k_cache[pages].float().permute(1, 0, 2, 3).reshape(n_kv_heads, -1, HEAD_DIM)[:, :n]  # [KVH, n, D]
+        v = v_cache[pages].float().permute(1, 0, 3, 2).reshape(n_kv_heads, -1, HEAD_DIM)[:, :n]
+        qb = q[b, : n_heads * HEAD_DIM].float().view(n_kv_heads, G, HEAD_DIM)
+        s = torch.einsum("hgd,hnd->hgn", qb, k) / math.sqrt(HEAD_DIM)
+        p = torch.softmax(s, dim=-1)
+        out[b] = torch.einsum("hgn,hnd->hgd", p, v).reshape(-1)
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# Sampling
+# ----------------------------------------------------------------------------------------------
+def sample(logits: torch.Tensor, temps: torch.Tensor, seeds: torch.Tensor, steps: torch.Tensor,
+           tokens: torch.Tensor | None = None, logprobs: torch.Tensor | None = None):
+    """Per row: greedy argmax when ``temps[r] <= 0``, else an exact draw from softmax(logits/T)
+    (Gumbel-max with a counter-based hash of (seed, step, token)).  Returns (tokens int32,
+    logprobs fp32: log-probability of the chosen token under softmax(logits / T))."""
+    R = logits.shape[0]
+    if tokens is None:
+        tokens = torch.empty(R, dtype=torch.int32, device=logits.device)
+    if logprobs is None:
+        logprobs = torch.empty(R, dtype=torch.float32, device=logits.device)
+    if _ext.use_hip(logits):
+        _ext.require().sample(logits, temps, seeds, steps, tokens, logprobs)
+        return tokens, logprobs
+    t, lp = sample_ref(logits, temps, seeds, steps)
+    tokens.copy_(t)
+    logprobs.copy_(lp)
+    return tokens, logprobs
+
+
+def sample_ref(logits, temps, seeds, steps):
+    x = logits.float()
+    t = temps.float().clamp_min(0)
+    scale = torch.where(t > 0, 1.0 / torch.where(t > 0, t, torch.ones_like(t)), torch.ones_like(t))
+    z = x * scale[:, None]
+    lse = torch.logsumexp(z, dim=-1)
+    score = z.clone()
+    for r in range(x.shape[0]):
+        if t[r] > 0:
+            g = torch.Generator(device="cpu").manual_seed(int(seeds[r]) * 1000003 + int(steps[r]))
+            u = torch.rand(x.shape[1], generator=g).clamp(1e-7, 1 - 1e-7).to(x.device)
+            score[r] = z[r] - torch.log(-torch.log(u))
+    tok = score.argmax(dim=-1)
+    lp = z.gather(1, tok[:, None]).squeeze(1) - lse
+    return tok.to(torch.int32), lp

@@ -1,0 +1,350 @@
+"""Llama-family inference model for the serving engine: paged KV cache, prefill + decode.
+
+MI355X-first layout (contrast: the reference runs vLLM/TGI containers for services,
+``examples/deployment/vllm/.dstack.yml``):
+
+* one GPU holds the whole model whenever it fits — Llama-3-70B bf16 is 141 GB of the 288 GB HBM3E,
+  leaving ~110 GB of KV cache (≈340k tokens) — so a replica is one process on one GPU (no tensor
+  parallel all-reduces on the decode path); services scale by replicas;
+* fused projections (``wqkv``, ``wgu``) as in the training model, so a decode step is 4 GEMMs per
+  layer (hipBLASLt; skinny M = batch) plus HIP kernels for everything else: fused add+RMSNorm,
+  RoPE fused with the paged-cache scatter, MFMA paged decode attention reading q straight from the
+  qkv projection output, SwiGLU, and a fused sampler;
+* prefill runs the training flash-attention forward kernel on each prompt (padded to 128 rows;
+  causal masking makes the padding inert) and computes the LM head only for the last token;
+* ``decode`` takes only static-shape tensors, so the engine captures it in one hipGraph per batch
+  bucket (launch-bound small batches).
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from dstack_amd.models.llama import CONFIGS, LlamaConfig
+from dstack_amd.ops import _ext
+from dstack_amd.ops import reference as ref
+from dstack_amd.ops import serving as sops
+
+
+@dataclass
+class RopeScaling:
+    """Llama-3.1 "llama3" RoPE frequency scaling (HF ``rope_scaling``)."""
+
+    factor: float = 8.0
+    low_freq_factor: float = 1.0
+    high_freq_factor: float = 4.0
+    original_max_position_embeddings: int = 8192
+
+
+def rope_tables(max_pos: int, head_dim: int, theta: float, scaling: RopeScaling | None, device):
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling is not None:
+        low_wl = scaling.original_max_position_embeddings / scaling.low_freq_factor
+        high_wl = scaling.original_max_position_embeddings / scaling.high_freq_factor
+        wl = 2 * math.pi / inv
+        smooth = (scaling.original_max_position_embeddings / wl - scaling.low_freq_factor) / (
+            scaling.high_freq_factor - scaling.low_freq_factor)
+        scaled = torch.where(wl > low_wl, inv / scaling.factor, inv)
+        mid = (wl <= low_wl) & (wl >= high_wl)
+        inv = torch.where(mid, (1 - smooth) * inv / scaling.factor + smooth * inv, scaled)
+    ang = torch.outer(torch.arange(max_pos, dtype=torch.float64), inv)
+    return ang.cos().float().contiguous().to(device), ang.sin().float().contiguous().to(device)
+
+
+@dataclass
+class ModelSpec:
+    cfg: LlamaConfig
+    rope_scaling: RopeScaling | None = None
+    tie_embeddings: bool = False
+    bos_token_id: int | None = None
+    eos_token_ids: tuple = ()
+    path: str | None = None  # HF checkpoint directory (None: random init)
+
+
+def load_spec(model: str) -> ModelSpec:
+    """``model`` is a built-in config name (``llama-3-8b``, ``llama-3-70b``, …: random weights) or an
+    HF Llama checkpoint directory (``config.json`` + ``*.safetensors``)."""
+    if model in CONFIGS:
+        return ModelSpec(CONFIGS[model], eos_token_ids=())
+    cfg_path = os.path.join(model, "config.json")
+    if not os.path.exists(cfg_path):
+        raise ValueError(f"unknown model {model!r}: neither a built-in config ({', '.join(CONFIGS)}) "
+                         "nor a directory with config.json")
+    with open(cfg_path) as f:
+        hf = json.load(f)
+    arch = (hf.get("architectures") or ["LlamaForCausalLM"])[0]
+    if hf.get("model_type", "llama") not in ("llama",) and "Llama" not in arch:
+        raise ValueError(f"unsupported architecture {arch} (Llama family only)")
+    heads = hf["num_attention_heads"]
+    dim = hf["hidden_size"]
+    head_dim = hf.get("head_dim") or dim // heads
+    if head_dim != 128 or dim != heads * head_dim:
+        raise ValueError(f"head_dim must be 128 with hidden_size = heads * head_dim (got {head_dim})")
+    # rope: ``rope_theta`` + ``rope_scaling`` (transformers 4.x) or ``rope_parameters`` (5.x)
+    rp = hf.get("rope_parameters") or {}
+    theta = hf.get("rope_theta", rp.get("rope_theta", 10000.0))
+    cfg = LlamaConfig(
+        name=os.path.basename(os.path.normpath(model)), dim=dim, n_layers=hf["num_hidden_layers"], n_heads=heads,
+        n_kv_heads=hf.get("num_key_value_heads", heads), ffn_dim=hf["intermediate_size"],
+        vocab_size=hf["vocab_size"], rope_theta=float(theta),
+        norm_eps=float(hf.get("rms_norm_eps", 1e-5)), max_seq_len=int(hf.get("max_position_embeddings", 8192)),
+    )
+    rs = hf.get("rope_scaling") or (rp if rp.get("rope_type", "default") != "default" else None)
+    scaling = None
+    if rs and (rs.get("rope_type") or rs.get("type")) == "default":
+        rs = None
+    if rs and (rs.get("rope_type") or rs.get("type")) == "llama3":
+        scaling = RopeScaling(float(rs["factor"]), float(rs.get("low_freq_factor", 1.0)),
+                              float(rs.get("high_freq_factor", 4.0)),
+                              int(rs.get("original_max_position_embeddings", 8192)))
+    elif rs:
+        raise ValueError(f"unsupported rope_scaling {rs}")
+    eos = hf.get("eos_token_id")
+    eos_ids = tuple(eos) if isinstance(eos, list) else ((eos,) if eos is not None else ())
+    return ModelSpec(cfg, scaling, bool(hf.get("tie_word_embeddings", False)), hf.get("bos_token_id"), eos_ids,
+                     path=model)
+
+
+class ServingLlama:
+    """Weights + paged KV cache of one Llama model on one device."""
+
+    def __init__(self, spec: ModelSpec, device, dtype=None, max_model_len: int | None = None):
+        self.spec = spec
+        self.cfg = cfg = spec.cfg
+        self.device = torch.device(device)
+        self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        if cfg.head_dim != sops.HEAD_DIM:
+            raise ValueError("serving kernels need head_dim 128")
+        self.max_model_len = max_model_len or cfg.max_seq_len
+        self.H, self.KVH, self.D = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+        self.NH = self.H + 2 * self.KVH
+        self.hip = self.device.type == "cuda" and not _ext.force_torch()
+        if self.hip:
+            _ext.require()
+        self.cos, self.sin = rope_tables(self.max_model_len + sops.PAGE, self.D, cfg.rope_theta, spec.rope_scaling,
+                                         self.device)
+        self.layers: list[dict] = []
+        self.k_cache: list[torch.Tensor] = []
+        self.v_cache: list[torch.Tensor] = []
+        self.num_pages = 0
+
+    # ------------------------------------------------------------------------------------------
+    # weights
+    # ------------------------------------------------------------------------------------------
+    def _empty(self, *shape):
+        return torch.empty(*shape, dtype=self.dtype, device=self.device)
+
+    def allocate_weights(self):
+        cfg = self.cfg
+        d, f, hd = cfg.dim, cfg.ffn_dim, cfg.head_dim
+        self.embed = self._empty(cfg.vocab_size, d)
+        self.norm = self._empty(d)
+        self.lm_head = self.embed if self.spec.tie_embeddings else self._empty(cfg.vocab_size, d)
+        self.layers = [
+            dict(attn_norm=self._empty(d), wqkv=self._empty(self.NH * hd, d), wo=self._empty(d, self.H * hd),
+                 ffn_norm=self._empty(d), wgu=self._empty(2 * f, d), wdown=self._empty(d, f))
+            for _ in range(cfg.n_layers)
+        ]
+
+    @torch.no_grad()
+    def init_random(self, seed: int = 0, std: float = 0.02):
+        """Random-init weights of the architecture (benchmarks: no network, no checkpoints)."""
+        self.allocate_weights()
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        out_std = std / math.sqrt(2 * self.cfg.n_layers)
+        for t in (self.embed, self.lm_head):
+            t.normal_(0.0, std, generator=g)
+        self.norm.fill_(1.0)
+        for L in self.layers:
+            L["attn_norm"].fill_(1.0)
+            L["ffn_norm"].fill_(1.0)
+            L["wqkv"].normal_(0.0, std, generator=g)
+            L["wgu"].normal_(0.0, std, generator=g)
+            L["wo"].normal_(0.0, out_std, generator=g)
+            L["wdown"].normal_(0.0, out_std, generator=g)
+        return self
+
+    @torch.no_grad()
+    def load_hf(self, path: str | None = None):
+        """Load an HF Llama safetensors checkpoint (q/k/v and gate/up fused on load)."""
+        from safetensors import safe_open
+
+        path = path or self.spec.path
+        self.allocate_weights()
+        files = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
+        if not files:
+            raise FileNotFoundError(f"no *.safetensors in {path}")
+        H, KVH, hd, f = self.H, self.KVH, self.D, self.cfg.ffn_dim
+        seen = set()
+
+        def put(dst, src):
+            dst.copy_(src.to(self.device, self.dtype))
+
+        for fn in files:
+            with safe_open(os.path.join(path, fn), framework="pt") as st:
+                for name in st.keys():
+                    t = st.get_tensor(name)
+                    seen.add(name)
+                    if name == "model.embed_tokens.weight":
+                        put(self.embed, t)
+                    elif name == "model.norm.weight":
+                        put(self.norm, t)
+                    elif name == "lm_head.weight":
+                        if not self.spec.tie_embeddings:
+                            put(self.lm_head, t)
+                    elif name.startswith("model.layers."):
+                        parts = name.split(".")
+                        L = self.layers[int(parts[2])]
+                        key = ".".join(parts[3:])
+                        if key == "input_layernorm.weight":
+                            put(L["attn_norm"], t)
+                        elif key == "post_attention_layernorm.weight":
+                            put(L["ffn_norm"], t)
+                        elif key == "self_attn.q_proj.weight":
+                            put(L["wqkv"][: H * hd], t)
+                        elif key == "self_attn.k_proj.weight":
+                            put(L["wqkv"][H * hd : (H + KVH) * hd], t)
+                        elif key == "self_attn.v_proj.weight":
+                            put(L["wqkv"][(H + KVH) * hd :], t)
+                        elif key == "self_attn.o_proj.weight":
+                            put(L["wo"], t)
+                        elif key == "mlp.gate_proj.weight":
+                            put(L["wgu"][:f], t)
+                        elif key == "mlp.up_proj.weight":
+                            put(L["wgu"][f:], t)
+                        elif key == "mlp.down_proj.weight":
+                            put(L["wdown"], t)
+                        elif "rotary_emb" not in key:
+                            raise ValueError(f"unexpected tensor {name}")
+                    else:
+                        raise ValueError(f"unexpected tensor {name}")
+        expected = {"model.embed_tokens.weight", "model.norm.weight"}
+        if not self.spec.tie_embeddings:
+            expected.add("lm_head.weight")
+        for i in range(self.cfg.n_layers):
+            expected |= {f"model.layers.{i}.{k}.weight" for k in (
+                "input_layernorm", "post_attention_layernorm", "self_attn.q_proj", "self_attn.k_proj",
+                "self_attn.v_proj", "self_attn.o_proj", "mlp.gate_proj", "mlp.up_proj", "mlp.down_proj")}
+        missing = expected - seen
+        if missing:
+            raise ValueError(f"checkpoint {path} is missing {len(missing)} tensors, e.g. {sorted(missing)[:3]}")
+        return self
+
+    def weight_bytes(self) -> int:
+        ts = [self.embed, self.norm] + ([] if self.lm_head is self.embed else [self.lm_head])
+        ts += [t for L in self.layers for t in L.values()]
+        return sum(t.numel() * t.element_size() for t in ts)
+
+    # ------------------------------------------------------------------------------------------
+    # KV cache
+    # ------------------------------------------------------------------------------------------
+    def kv_bytes_per_page(self) -> int:
+        return 2 * self.cfg.n_layers * self.KVH * sops.PAGE * self.D * torch.empty(0, dtype=self.dtype).element_size()
+
+    def allocate_kv(self, num_pages: int | None = None, gpu_memory_utilization: float = 0.90,
+                    reserve_bytes: int = 8 << 30):
+        """``num_pages`` pages of every layer's cache; by default as many as fit in
+        ``gpu_memory_utilization`` of HBM after the weights and a workspace reserve."""
+        if num_pages is None:
+            if self.device.type != "cuda":
+                num_pages = max(4, (self.max_model_len // sops.PAGE + 1) * 4)
+            else:
+                free, total = torch.cuda.mem_get_info(self.device)
+                used = total - free
+                budget = total * gpu_memory_utilization - used - reserve_bytes
+                num_pages = int(budget // self.kv_bytes_per_page())
+                if num_pages < self.max_model_len // sops.PAGE + 1:
+                    raise RuntimeError(f"not enough HBM for the KV cache of one {self.max_model_len}-token sequence")
+        self.num_pages = num_pages
+        self.k_cache, self.v_cache = [], []
+        for _ in range(self.cfg.n_layers):
+            k, v = sops.alloc_cache(num_pages, self.KVH, self.dtype, self.device)
+            self.k_cache.append(k)
+            self.v_cache.append(v)
+        return num_pages
+
+    # ------------------------------------------------------------------------------------------
+    # fused ops (HIP on the GPU, fp32 references on the CPU)
+    # ------------------------------------------------------------------------------------------
+    def _rms(self, x, w):
+        if self.hip:
+            return _ext.require().rms_norm_fwd(x, w, self.cfg.norm_eps)[0]
+        return ref.rms_norm(x, w, self.cfg.norm_eps)
+
+    def _add_rms(self, x, delta, w):
+        if self.hip:
+            h, y, _ = _ext.require().add_rms_norm_fwd(x, delta, w, self.cfg.norm_eps)
+            return h, y
+        return ref.add_rms_norm(x, delta, w, self.cfg.norm_eps)
+
+    def _swiglu(self, gu):
+        if self.hip:
+            return _ext.require().swiglu_fwd(gu)
+        return ref.swiglu(gu)
+
+    def _mlp_and_attn_out(self, L, x, o):
+        """(x + o @ wo^T) -> norm -> SwiGLU MLP; returns (new residual, mlp output)."""
+        x, h = self._add_rms(x, o @ L["wo"].t(), L["ffn_norm"])
+        return x, self._swiglu(h @ L["wgu"].t()) @ L["wdown"].t()
+
+    # ------------------------------------------------------------------------------------------
+    # forward passes
+    # ------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def prefill(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, offsets, lens):
+        """Prompts packed into 128-row-aligned segments of one token buffer (``offsets[i]`` is the
+        first row of prompt i, ``lens[i]`` its length; padding rows have slot -1).  Writes every
+        prompt token's K/V into the cache and returns the logits of each prompt's last token
+        [n, vocab]."""
+        H, KVH = self.H, self.KVH
+        rows = tokens.numel()
+        x = F.embedding(tokens, self.embed)
+        delta = None
+        bounds = []
+        for i in range(len(lens)):
+            nxt = offsets[i + 1] if i + 1 < len(lens) else rows
+            bounds.append((int(offsets[i]), int(nxt) - int(offsets[i])))
+        for li, L in enumerate(self.layers):
+            if delta is None:
+                h = self._rms(x, L["attn_norm"])
+            else:
+                x, h = self._add_rms(x, delta, L["attn_norm"])
+            qkv = h @ L["wqkv"].t()
+            sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH)
+            o = torch.empty(rows, H * self.D, dtype=x.dtype, device=x.device)
+            for off, n in bounds:
+                seg = qkv[off : off + n].view(1, n, -1)
+                if self.hip:
+                    o[off : off + n] = _ext.require().flash_attn_fwd(seg, H, KVH, True)[0].view(n, -1)
+                else:
+                    q, k, v = seg.view(1, n, self.NH, self.D).split([H, KVH, KVH], dim=2)
+                    o[off : off + n] = ref.attention(q, k, v, causal=True).reshape(n, -1)
+            x, delta = self._mlp_and_attn_out(L, x, o)
+        last = torch.tensor([int(offsets[i]) + int(lens[i]) - 1 for i in range(len(lens))], device=x.device)
+        x, h = self._add_rms(x[last], delta[last], self.norm)
+        return h @ self.lm_head.t()
+
+    @torch.no_grad()
+    def decode(self, tokens, positions, slots, block_tables, ctx_lens, ws=None):
+        """One new token per sequence (all inputs [B] / [B, W] device tensors, static shapes):
+        returns logits [B, vocab].  Rows with ``ctx_lens == 0`` (graph padding) are inert."""
+        H, KVH = self.H, self.KVH
+        x = F.embedding(tokens, self.embed)
+        delta = None
+        for li, L in enumerate(self.layers):
+            if delta is None:
+                h = self._rms(x, L["attn_norm"])
+            else:
+                x, h = self._add_rms(x, delta, L["attn_norm"])
+            qkv = h @ L["wqkv"].t()
+            sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH)
+            o = sops.paged_decode(qkv, self.k_cache[li], self.v_cache[li], block_tables, ctx_lens, H, KVH, ws=ws)
+            x, delta = self._mlp_and_attn_out(L, x, o)
+        _, h = self._add_rms(x, delta, self.norm)
+        return h @ self.lm_head.t()
