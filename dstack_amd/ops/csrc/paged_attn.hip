@@ -143,22 +143,36 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
     }
     const int* bt = block_tables + (long)b * bt_stride;
     const int r = lane & 15;
-    for (int p = p0; p < p1; ++p) {
-      const long page = bt[p];
+    // K row offsets of the 4 S^T tiles (key 32(t>>1) + 8(r>>2) + 4(t&1) + (r&3)) and the V^T
+    // fragment offset are lane constants; one page = 16 K + 16 V 16-byte loads per lane.
+    // Two-stage software pipeline, pinned with sched_barrier (left alone, hipcc interleaved
+    // load -> wait -> MFMA with <= 3 loads in flight, which made the kernel latency-bound at
+    // ~1.8 TB/s): V(p) is in flight during S(p) = K(p) Q^T, and K(p+1) during softmax + P V(p).
+    int koff[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) koff[t] = (32 * (t >> 1) + 8 * (r >> 2) + 4 * (t & 1) + (r & 3)) * HDIM + 8 * g;
+    const int voff = r * PAGE + 8 * g;
+    bf16x8_t kf[4][4], vf[2][8];
+    auto load_k = [&](long page) {
       const bf16_t* kb = k_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) kf[t][kk] = ld8(kb + koff[t] + 32 * kk);
+    };
+    auto load_v = [&](long page) {
       const bf16_t* vb = v_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
-      // issue every load of the page (K: 16 x 16 B, V: 16 x 16 B per lane) before any MFMA
-      bf16x8_t kf[4][4], vf[2][8];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int key = 32 * (t >> 1) + 8 * (r >> 2) + 4 * (t & 1) + (r & 3);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) kf[t][kk] = ld8(kb + key * HDIM + 32 * kk + 8 * g);
-      }
 #pragma unroll
       for (int mm = 0; mm < 2; ++mm)
 #pragma unroll
-        for (int n = 0; n < 8; ++n) vf[mm][n] = ld8(vb + (16 * n + r) * PAGE + 32 * mm + 8 * g);
+        for (int n = 0; n < 8; ++n) vf[mm][n] = ld8(vb + voff + 16 * n * PAGE + 32 * mm);
+    };
+    long page = bt[p0];
+    load_k(page);
+    for (int p = p0; p < p1; ++p) {
+      const long next = p + 1 < p1 ? bt[p + 1] : page;
+      load_v(page);
+      __builtin_amdgcn_sched_barrier(0);
       // S^T tiles: lane holds keys 32(t>>1) + 8g + 4(t&1) + i, i = 0..3, of query qc
       f32x4_t s[4];
 #pragma unroll
@@ -167,6 +181,10 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) s[t] = mfma16(kf[t][kk], qf[kk], s[t]);
       }
+      __builtin_amdgcn_sched_barrier(0);
+      load_k(next);  // unconditional (last page: a redundant reload) so vmcnt counting stays static
+      __builtin_amdgcn_sched_barrier(0);
+      page = next;
       const int base = p * PAGE;
       float mx = -INFINITY;
 #pragma unroll
@@ -207,6 +225,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
 #pragma unroll
         for (int n = 0; n < 8; ++n) acc[n] = mfma16(vf[mm][n], pf, acc[n]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   // O^T accumulator: lane (qc, g) holds O[h][16n + 4g + i]

@@ -19,12 +19,16 @@ from typing import Optional
 TUNED_DIR = Path(__file__).resolve().parent / "tuned"
 
 
-def results_path(arch: str = "gfx950") -> Path:
+def results_path(arch: str = "gfx950", kind: str = "train") -> Path:
+    """``kind`` = ``train`` (Llama training projections) or ``serving`` (the decode GEMMs of the
+    serving engine: M = every hipGraph batch bucket, N/K = the fused projections and LM head)."""
     override = os.environ.get("DSTACK_AMD_GEMM_TUNING_FILE")
-    return Path(override) if override else TUNED_DIR / f"gemm_tunableop_{arch}.csv"
+    if override:
+        return Path(override)
+    return TUNED_DIR / (f"gemm_tunableop_{arch}.csv" if kind == "train" else f"gemm_tunableop_{kind}_{arch}.csv")
 
 
-def setup(mode: Optional[str] = None, device_index: int = 0) -> str:
+def setup(mode: Optional[str] = None, device_index: int = 0, kind: str = "train") -> str:
     """Configure TunableOp before the first GEMM.  Returns the effective mode."""
     import torch
 
@@ -32,7 +36,7 @@ def setup(mode: Optional[str] = None, device_index: int = 0) -> str:
         return "off"
     mode = (mode or os.environ.get("DSTACK_AMD_GEMM_TUNING") or "use").lower()
     arch = torch.cuda.get_device_properties(device_index).gcnArchName.split(":")[0]
-    path = results_path(arch)
+    path = results_path(arch, kind)
     tunable = torch.cuda.tunable
     if mode == "off":
         tunable.enable(False)

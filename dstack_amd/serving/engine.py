@@ -78,6 +78,11 @@ class LLMEngine:
 
         self.model = model
         self.device = model.device
+        if self.device.type == "cuda":
+            from dstack_amd.ops import gemm_tuning
+
+            # hipBLASLt solutions tuned offline for the decode GEMMs (tools/tune_serving_gemms.py)
+            self.gemm_tuning = gemm_tuning.setup(device_index=self.device.index or 0, kind="serving")
         if not model.k_cache:
             model.allocate_kv(num_pages, gpu_memory_utilization=gpu_memory_utilization)
         self.max_batch = max_batch

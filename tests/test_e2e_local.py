@@ -123,6 +123,41 @@ def test_service_through_in_server_proxy(client, server):
     assert body is not None and "Directory listing" in body
 
 
+def test_llm_service_through_model_proxy(client, server):
+    """A ``type: service`` replica running the serving engine (tiny random Llama on the CPU) behind
+    the in-server OpenAI model proxy: chat completion request -> proxy -> replica -> engine."""
+    from dstack_amd.api import Service
+    from dstack_amd.core.models.services import OpenAIChatModel
+
+    port = 19000 + os.getpid() % 1000
+    cmd = (f"{sys.executable} -m dstack_amd.serving --model llama-tiny --served-model-name tiny-llama "
+           f"--max-model-len 256 --max-batch 4 --port {port} --host 127.0.0.1")
+    conf = Service(commands=[f"cd {REPO} && {cmd}"], port=port, name="e2e-llm", auth=False,
+                   model=OpenAIChatModel(name="tiny-llama", format="openai"))
+    run = client.runs.submit(conf)
+    url = f"{server.url}/proxy/models/main/chat/completions"
+    body = None
+    deadline = time.time() + 120
+    try:
+        while time.time() < deadline:
+            try:
+                r = httpx.post(url, json={"model": "tiny-llama", "max_tokens": 4, "temperature": 0,
+                                          "messages": [{"role": "user", "content": "hello"}]},
+                               headers={"Authorization": f"Bearer {server.token}"}, timeout=10)
+                if r.status_code == 200:
+                    body = r.json()
+                    break
+            except httpx.HTTPError:
+                pass
+            time.sleep(0.5)
+    finally:
+        run.stop(abort=True)
+        run.wait(timeout=60)
+    assert body is not None, _logs(run)[-2000:]
+    assert body["choices"][0]["message"]["role"] == "assistant"
+    assert 1 <= body["usage"]["completion_tokens"] <= 4
+
+
 def test_multinode_task_rendezvous_env(client):
     from dstack_amd.api import Task
 

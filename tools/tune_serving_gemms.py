@@ -1,0 +1,63 @@
+"""Tune (``--mode tune``) or time (``--mode use``/``off``) the decode-step GEMMs of the serving
+engine: y[M, N] = x[M, K] @ W[N, K]^T for every hipGraph batch bucket M and every projection of
+the given models.  Decode GEMMs are weight-streaming (M <= 256 rows against GBs of weights), so the
+figure of merit is weight bytes / time (TB/s) against HBM3E.  Tune mode writes
+``dstack_amd/ops/tuned/gemm_tunableop_serving_gfx950.csv`` (or $DSTACK_AMD_GEMM_TUNING_FILE).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--models", default="llama-3-8b,llama-3-70b")
+    ap.add_argument("--mode", default="use", choices=["tune", "use", "off"])
+    ap.add_argument("--buckets", default="")
+    ap.add_argument("--max-batch", type=int, default=256)
+    args = ap.parse_args()
+    import torch
+
+    from dstack_amd.models.llama import CONFIGS
+    from dstack_amd.ops import gemm_tuning
+    from dstack_amd.serving.engine import _buckets
+
+    mode = gemm_tuning.setup(args.mode, kind="serving")
+    buckets = [int(b) for b in args.buckets.split(",")] if args.buckets else _buckets(args.max_batch)
+    dev = torch.device("cuda")
+    out = []
+    for name in args.models.split(","):
+        c = CONFIGS[name]
+        nh = c.n_heads + 2 * c.n_kv_heads
+        shapes = {"wqkv": (nh * c.head_dim, c.dim), "wo": (c.dim, c.n_heads * c.head_dim),
+                  "wgu": (2 * c.ffn_dim, c.dim), "wdown": (c.dim, c.ffn_dim), "lm_head": (c.vocab_size, c.dim)}
+        for wname, (N, K) in shapes.items():
+            w = torch.randn(N, K, device=dev).to(torch.bfloat16)
+            for M in buckets:
+                x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+                for _ in range(3):
+                    y = x @ w.t()
+                torch.cuda.synchronize()
+                it = 20
+                t0 = time.perf_counter()
+                for _ in range(it):
+                    y = x @ w.t()
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t0) / it
+                tbs = (N * K + M * K + M * N) * 2 / dt / 1e12
+                out.append({"model": name, "w": wname, "M": M, "N": N, "K": K, "us": round(dt * 1e6, 1),
+                            "TBps": round(tbs, 2)})
+                print(json.dumps(out[-1]), flush=True)
+                del y
+    print(json.dumps({"mode": mode, "file": str(gemm_tuning.results_path(kind="serving"))}))
+
+
+if __name__ == "__main__":
+    main()
