@@ -118,7 +118,11 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
     const int* __restrict__ ctx_lens, bf16_t* __restrict__ out, float* __restrict__ o_part,
     float* __restrict__ lse_part, int H, int KVH, int G, int nsplit, int pages_per_split,
     float scale_log2) {
-  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  // grid (B * KVH, nsplit): consecutive workgroups are different (sequence, KV head) pairs of the
+  // SAME split, so the populated splits are dealt round-robin over all 8 XCDs.  (With the split
+  // as the fastest index, split s landed on XCD s % 8: at 8 splits and short contexts every
+  // populated wave ran on one XCD, 5.5x slower, tools/bench_paged_decode.py.)
+  const int kvh = blockIdx.x % KVH, b = blockIdx.x / KVH, split = blockIdx.y;
   const int lane = threadIdx.x, qc = lane & 15, g = lane >> 4;
   const int ctx = ctx_lens[b];
   const int n_pages = (ctx + PAGE - 1) / PAGE;
@@ -245,10 +249,12 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
     }
   } else {
     const long idx = ((long)b * H + h) * nsplit + split;
-    float* o = o_part + idx * HDIM;
-#pragma unroll
-    for (int n = 0; n < 8; ++n) *reinterpret_cast<f32x4_t*>(o + 16 * n + 4 * g) = acc[n] * inv;
     if (g == 0) lse_part[idx] = l > 0.f ? m + __log2f(l) : -INFINITY;
+    if (l > 0.f) {  // an empty split writes only its -inf lse; the combine never reads its o
+      float* o = o_part + idx * HDIM;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) *reinterpret_cast<f32x4_t*>(o + 16 * n + 4 * g) = acc[n] * inv;
+    }
   }
 }
 
@@ -265,7 +271,8 @@ __global__ __launch_bounds__(128) void paged_combine_kernel(const float* __restr
   float num = 0.f, den = 0.f;
   if (M > -INFINITY) {
     for (int s = 0; s < nsplit; ++s) {
-      const float w = lse[s] > -INFINITY ? fexp2(lse[s] - M) : 0.f;
+      if (lse[s] == -INFINITY) continue;
+      const float w = fexp2(lse[s] - M);
       num += w * o_part[(bh * nsplit + s) * HDIM + d];
       den += w;
     }
@@ -400,7 +407,7 @@ extern "C" hipError_t dsa_paged_decode(const void* q, long q_stride, const void*
   if (KVH <= 0 || H % KVH || H / KVH > 16 || nsplit < 1 || pages_per_split < 1) return hipErrorInvalidValue;
   const int G = H / KVH;
   const float sl2 = scale * 1.4426950408889634f;
-  const dim3 grid(nsplit, KVH, B);
+  const dim3 grid(B * KVH, nsplit);
   if (nsplit == 1) {
     paged_decode_kernel<true><<<grid, 64, 0, st>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache,
                                                   (const bf16_t*)v_cache, block_tables, bt_stride,

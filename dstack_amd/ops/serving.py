@@ -62,7 +62,7 @@ def rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_he
 # ----------------------------------------------------------------------------------------------
 # Paged decode attention
 # ----------------------------------------------------------------------------------------------
-def split_plan(batch: int, n_kv_heads: int, table_width: int, target_waves: int = 4096):
+def split_plan(batch: int, n_kv_heads: int, table_width: int, target_waves: int = 2048):
     """(nsplit, pages_per_split): enough one-wave workgroups to fill 256 CUs at any context, a
     function of the batch bucket and the block-table width only (graph-capturable)."""
     want = max(1, math.ceil(target_waves / max(1, batch * n_kv_heads)))
@@ -74,8 +74,9 @@ def split_plan(batch: int, n_kv_heads: int, table_width: int, target_waves: int 
 class DecodeWorkspace:
     """Preallocated split-KV partials for a batch bucket (hipGraph-safe: no allocation per step)."""
 
-    def __init__(self, batch: int, n_heads: int, n_kv_heads: int, table_width: int, device):
-        self.nsplit, self.pps = split_plan(batch, n_kv_heads, table_width)
+    def __init__(self, batch: int, n_heads: int, n_kv_heads: int, table_width: int, device,
+                 target_waves: int = 2048):
+        self.nsplit, self.pps = split_plan(batch, n_kv_heads, table_width, target_waves)
         n = batch * n_heads * self.nsplit if self.nsplit > 1 else 1
         self.o_part = torch.empty(n * HEAD_DIM, dtype=torch.float32, device=device)
         self.lse_part = torch.empty(n, dtype=torch.float32, device=device)

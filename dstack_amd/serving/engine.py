@@ -14,6 +14,11 @@ Offline use::
 Online use: ``start()`` runs the loop in a background thread; ``add_request`` takes an ``on_event``
 callback that receives ``(request, token_id, finished)`` from that thread (the HTTP server turns it
 into an asyncio queue).
+
+Tensor parallel (``ServingLlama(tp_group=...)``, one process per GPU under torchrun): rank 0 is the
+leader — scheduler, requests, sampling, HTTP — and broadcasts every step's inputs (one packed int64
+tensor) to the followers, which run ``follow()``: the same model step on their shard, joining the
+step's all-reduces and the logits all-gather.
 """
 
 from __future__ import annotations
@@ -25,6 +30,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from dstack_amd.ops import serving as sops
 from dstack_amd.serving.model import ServingLlama, load_spec
@@ -78,6 +84,10 @@ class LLMEngine:
 
         self.model = model
         self.device = model.device
+        self.tp, self.tp_group = model.tp, model.tp_group
+        self.leader = model.tp_rank == 0
+        if self.tp > 1:
+            self._src = dist.get_global_rank(self.tp_group, 0)
         if self.device.type == "cuda":
             from dstack_amd.ops import gemm_tuning
 
@@ -98,17 +108,19 @@ class LLMEngine:
         self._wake = threading.Event()
         self._thread = None
         self._stop = False
-        self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
+        # (tensor parallel: eager steps, so every rank issues the same RCCL collectives in order)
+        self.use_graphs = (self.device.type == "cuda" and self.tp == 1) if use_graphs is None else use_graphs
         self.buckets = _buckets(max_batch)
         self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self._alloc_static()
         self.stats = dict(prefill_tokens=0, decode_tokens=0, steps=0, preemptions=0, prefill_s=0.0, decode_s=0.0)
 
     @classmethod
-    def from_model(cls, model: str, device=None, max_model_len: int | None = None, seed: int = 0, **kw):
+    def from_model(cls, model: str, device=None, max_model_len: int | None = None, seed: int = 0, tp_group=None,
+                   **kw):
         spec = load_spec(model)
         device = device or ("cuda" if torch.cuda.is_available() else "cpu")
-        m = ServingLlama(spec, device, max_model_len=max_model_len)
+        m = ServingLlama(spec, device, max_model_len=max_model_len, tp_group=tp_group)
         if spec.path:
             m.load_hf()
         else:
@@ -226,6 +238,8 @@ class LLMEngine:
             toks = np.zeros(plan["rows"], dtype=np.int64)
             for r, off, n in zip(reqs, plan["offsets"], plan["lens"]):
                 toks[off : off + n] = r.all_ids[:n]
+            if self.tp > 1:
+                self._bcast_prefill(toks, plan["positions"], plan["slots"], plan["offsets"], plan["lens"])
             dev = self.device
             logits = self.model.prefill(torch.from_numpy(toks).to(dev), torch.from_numpy(plan["positions"]).to(dev),
                                         torch.from_numpy(plan["slots"]).to(dev), plan["offsets"], plan["lens"])
@@ -296,6 +310,8 @@ class LLMEngine:
                 self.s_ctx[n:b].zero_()
                 self.s_temps[n:b].zero_()
             filtered = any(r.params.top_p < 1.0 or r.params.top_k > 0 for r in reqs)
+            if self.tp > 1:
+                self._bcast_decode(b)
             if self._graphs and b in self._graphs:
                 self._graphs[b].replay()
                 logits = self._graph_logits[b]
@@ -306,6 +322,63 @@ class LLMEngine:
                 sops.sample(logits, self.s_temps[:n], self.s_seeds[:n], self.s_steps[:n], self.s_out_tok[:n],
                             self.s_out_lp[:n])
             return self.s_out_tok[:n].tolist(), self.s_out_lp[:n].tolist()
+
+    # ------------------------------------------------------------------------------------------
+    # tensor parallel: the leader broadcasts each step's inputs, followers replay them
+    # ------------------------------------------------------------------------------------------
+    _STOP, _PREFILL, _DECODE = 0, 1, 2
+
+    def _bcast(self, header, payload=None):
+        hdr = torch.tensor(header + [0] * (4 - len(header)), dtype=torch.int64, device=self.device)
+        dist.broadcast(hdr, src=self._src, group=self.tp_group)
+        if payload is not None:
+            dist.broadcast(payload, src=self._src, group=self.tp_group)
+
+    def _bcast_prefill(self, toks, positions, slots, offsets, lens):
+        parts = [np.asarray(a, dtype=np.int64) for a in (toks, positions, slots, offsets, lens)]
+        payload = torch.from_numpy(np.concatenate(parts)).to(self.device)
+        self._bcast([self._PREFILL, len(lens), len(toks)], payload)
+
+    def _bcast_decode(self, b: int):
+        payload = torch.cat([self.s_tokens[:b], self.s_pos[:b].long(), self.s_slots[:b].long(), self.s_ctx[:b].long(),
+                             self.s_tables[:b].long().flatten()])
+        self._bcast([self._DECODE, b, b, self.width], payload)
+
+    @torch.no_grad()
+    def follow(self):
+        """Follower rank loop: run the leader's steps on this rank's shard until it stops."""
+        assert self.tp > 1 and not self.leader
+        dev = self.device
+        while True:
+            hdr = torch.empty(4, dtype=torch.int64, device=dev)
+            dist.broadcast(hdr, src=self._src, group=self.tp_group)
+            kind, n, rows, width = hdr.tolist()
+            if kind == self._STOP:
+                return
+            if kind == self._PREFILL:
+                payload = torch.empty(3 * rows + 2 * n, dtype=torch.int64, device=dev)
+                dist.broadcast(payload, src=self._src, group=self.tp_group)
+                toks, pos, slots, offsets, lens = payload.split([rows, rows, rows, n, n])
+                self.model.prefill(toks, pos.int(), slots.int(), offsets.tolist(), lens.tolist())
+            else:
+                b = n
+                payload = torch.empty(4 * b + b * width, dtype=torch.int64, device=dev)
+                dist.broadcast(payload, src=self._src, group=self.tp_group)
+                toks, pos, slots, ctx, tables = payload.split([b, b, b, b, b * width])
+                self.s_tokens[:b].copy_(toks)
+                self.s_pos[:b].copy_(pos)
+                self.s_slots[:b].copy_(slots)
+                self.s_ctx[:b].copy_(ctx)
+                self.s_tables[:b].copy_(tables.view(b, width))
+                self.model.decode(self.s_tokens[:b], self.s_pos[:b], self.s_slots[:b], self.s_tables[:b],
+                                  self.s_ctx[:b], ws=self._ws[b])
+
+    def shutdown(self):
+        """Leader: release the followers (tensor parallel) and stop the loop thread."""
+        self.stop()
+        if self.tp > 1 and self.leader and not getattr(self, "_released", False):
+            self._released = True
+            self._bcast([self._STOP])
 
     # ------------------------------------------------------------------------------------------
     def generate(self, prompts, params: SamplingParams | list | None = None) -> list[Request]:

@@ -13,7 +13,11 @@ MI355X-first layout (contrast: the reference runs vLLM/TGI containers for servic
 * prefill runs the training flash-attention forward kernel on each prompt (padded to 128 rows;
   causal masking makes the padding inert) and computes the LM head only for the last token;
 * ``decode`` takes only static-shape tensors, so the engine captures it in one hipGraph per batch
-  bucket (launch-bound small batches).
+  bucket (launch-bound small batches);
+* models that do not fit one GPU (Llama-3.1-405B: 810 GB bf16 = 102 GB per GPU at TP 8) run
+  tensor-parallel over RCCL/xGMI (``tp_group``): attention heads (q and kv), the FFN and the vocab
+  are sharded Megatron-style, so a layer costs two all-reduces of [tokens, dim] (after ``wo`` and
+  ``wdown``) and the logits one all-gather; each rank holds the KV cache of its own KV heads.
 """
 
 from __future__ import annotations
@@ -21,9 +25,11 @@ from __future__ import annotations
 import json
 import math
 import os
+import zlib
 from dataclasses import dataclass
 
 import torch
+import torch.distributed as dist
 import torch.nn.functional as F
 
 from dstack_amd.models.llama import CONFIGS, LlamaConfig
@@ -112,9 +118,10 @@ def load_spec(model: str) -> ModelSpec:
 
 
 class ServingLlama:
-    """Weights + paged KV cache of one Llama model on one device."""
+    """Weights + paged KV cache of one Llama model on one device (or of one tensor-parallel shard:
+    ``H``/``KVH``/``F``/``V`` below are then this rank's local head / FFN / vocab counts)."""
 
-    def __init__(self, spec: ModelSpec, device, dtype=None, max_model_len: int | None = None):
+    def __init__(self, spec: ModelSpec, device, dtype=None, max_model_len: int | None = None, tp_group=None):
         self.spec = spec
         self.cfg = cfg = spec.cfg
         self.device = torch.device(device)
@@ -122,7 +129,15 @@ class ServingLlama:
         if cfg.head_dim != sops.HEAD_DIM:
             raise ValueError("serving kernels need head_dim 128")
         self.max_model_len = max_model_len or cfg.max_seq_len
-        self.H, self.KVH, self.D = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+        self.tp_group = tp_group
+        self.tp = dist.get_world_size(tp_group) if tp_group is not None else 1
+        self.tp_rank = dist.get_rank(tp_group) if tp_group is not None else 0
+        tp = self.tp
+        if cfg.n_heads % tp or cfg.n_kv_heads % tp or cfg.ffn_dim % tp or cfg.vocab_size % tp:
+            raise ValueError(f"tensor parallel {tp} must divide heads {cfg.n_heads}, kv heads {cfg.n_kv_heads}, "
+                             f"ffn {cfg.ffn_dim} and vocab {cfg.vocab_size}")
+        self.H, self.KVH, self.D = cfg.n_heads // tp, cfg.n_kv_heads // tp, cfg.head_dim
+        self.F, self.V = cfg.ffn_dim // tp, cfg.vocab_size // tp
         self.NH = self.H + 2 * self.KVH
         self.hip = self.device.type == "cuda" and not _ext.force_torch()
         if self.hip:
@@ -142,32 +157,63 @@ class ServingLlama:
 
     def allocate_weights(self):
         cfg = self.cfg
-        d, f, hd = cfg.dim, cfg.ffn_dim, cfg.head_dim
-        self.embed = self._empty(cfg.vocab_size, d)
+        d, hd = cfg.dim, cfg.head_dim
+        self.embed = self._empty(cfg.vocab_size, d)  # replicated (an index lookup)
         self.norm = self._empty(d)
-        self.lm_head = self.embed if self.spec.tie_embeddings else self._empty(cfg.vocab_size, d)
+        if self.spec.tie_embeddings:
+            self.lm_head = self.embed[self.tp_rank * self.V : (self.tp_rank + 1) * self.V]
+        else:
+            self.lm_head = self._empty(self.V, d)
         self.layers = [
             dict(attn_norm=self._empty(d), wqkv=self._empty(self.NH * hd, d), wo=self._empty(d, self.H * hd),
-                 ffn_norm=self._empty(d), wgu=self._empty(2 * f, d), wdown=self._empty(d, f))
+                 ffn_norm=self._empty(d), wgu=self._empty(2 * self.F, d), wdown=self._empty(d, self.F))
             for _ in range(cfg.n_layers)
         ]
 
+    # ---- tensor-parallel sharding of full (unsharded) tensors ----
+    def _shard(self, kind: str, t: torch.Tensor) -> torch.Tensor:
+        """This rank's slice of a full weight: ``q``/``k``/``v`` rows by head, ``wo``/``wdown`` columns,
+        ``gate``/``up`` rows by FFN unit, ``vocab`` rows (LM head)."""
+        if self.tp == 1:
+            return t
+        r, hd = self.tp_rank, self.D
+        rows = {"q": self.H * hd, "k": self.KVH * hd, "v": self.KVH * hd, "gate": self.F, "up": self.F,
+                "vocab": self.V}
+        if kind in rows:
+            n = rows[kind]
+            return t[r * n : (r + 1) * n]
+        n = self.H * hd if kind == "wo" else self.F
+        return t[:, r * n : (r + 1) * n]
+
     @torch.no_grad()
     def init_random(self, seed: int = 0, std: float = 0.02):
-        """Random-init weights of the architecture (benchmarks: no network, no checkpoints)."""
+        """Random-init weights of the architecture (benchmarks: no network, no checkpoints).  Every
+        full tensor is drawn from its own generator (seed, name) and then sharded, so a
+        tensor-parallel model holds exactly the slices of the single-GPU one."""
         self.allocate_weights()
-        g = torch.Generator(device=self.device).manual_seed(seed)
-        out_std = std / math.sqrt(2 * self.cfg.n_layers)
-        for t in (self.embed, self.lm_head):
-            t.normal_(0.0, std, generator=g)
+        cfg = self.cfg
+        out_std = std / math.sqrt(2 * cfg.n_layers)
+        hd = cfg.head_dim
+
+        def draw(name, shape, sd):
+            g = torch.Generator(device=self.device).manual_seed(zlib.crc32(f"{seed}:{name}".encode()))
+            return torch.empty(*shape, dtype=self.dtype, device=self.device).normal_(0.0, sd, generator=g)
+
+        self.embed.copy_(draw("embed", self.embed.shape, std))
+        if not self.spec.tie_embeddings:
+            self.lm_head.copy_(self._shard("vocab", draw("lm_head", (cfg.vocab_size, cfg.dim), std)))
         self.norm.fill_(1.0)
-        for L in self.layers:
+        for i, L in enumerate(self.layers):
             L["attn_norm"].fill_(1.0)
             L["ffn_norm"].fill_(1.0)
-            L["wqkv"].normal_(0.0, std, generator=g)
-            L["wgu"].normal_(0.0, std, generator=g)
-            L["wo"].normal_(0.0, out_std, generator=g)
-            L["wdown"].normal_(0.0, out_std, generator=g)
+            full = draw(f"{i}.wqkv", ((cfg.n_heads + 2 * cfg.n_kv_heads) * hd, cfg.dim), std)
+            q, k, v = full.split([cfg.n_heads * hd, cfg.n_kv_heads * hd, cfg.n_kv_heads * hd])
+            L["wqkv"].copy_(torch.cat([self._shard("q", q), self._shard("k", k), self._shard("v", v)]))
+            full = draw(f"{i}.wgu", (2 * cfg.ffn_dim, cfg.dim), std)
+            L["wgu"].copy_(torch.cat([self._shard("gate", full[: cfg.ffn_dim]), self._shard("up", full[cfg.ffn_dim :])]))
+            L["wo"].copy_(self._shard("wo", draw(f"{i}.wo", (cfg.dim, cfg.n_heads * hd), out_std)))
+            L["wdown"].copy_(self._shard("wdown", draw(f"{i}.wdown", (cfg.dim, cfg.ffn_dim), out_std)))
+            del full, q, k, v
         return self
 
     @torch.no_grad()
@@ -180,10 +226,12 @@ class ServingLlama:
         files = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
         if not files:
             raise FileNotFoundError(f"no *.safetensors in {path}")
-        H, KVH, hd, f = self.H, self.KVH, self.D, self.cfg.ffn_dim
+        H, KVH, hd, f = self.H, self.KVH, self.D, self.F  # local (per tensor-parallel rank)
         seen = set()
 
-        def put(dst, src):
+        def put(dst, src, kind=None):
+            if kind is not None:
+                src = self._shard(kind, src)
             dst.copy_(src.to(self.device, self.dtype))
 
         for fn in files:
@@ -197,7 +245,7 @@ class ServingLlama:
                         put(self.norm, t)
                     elif name == "lm_head.weight":
                         if not self.spec.tie_embeddings:
-                            put(self.lm_head, t)
+                            put(self.lm_head, t, "vocab")
                     elif name.startswith("model.layers."):
                         parts = name.split(".")
                         L = self.layers[int(parts[2])]
@@ -207,19 +255,19 @@ class ServingLlama:
                         elif key == "post_attention_layernorm.weight":
                             put(L["ffn_norm"], t)
                         elif key == "self_attn.q_proj.weight":
-                            put(L["wqkv"][: H * hd], t)
+                            put(L["wqkv"][: H * hd], t, "q")
                         elif key == "self_attn.k_proj.weight":
-                            put(L["wqkv"][H * hd : (H + KVH) * hd], t)
+                            put(L["wqkv"][H * hd : (H + KVH) * hd], t, "k")
                         elif key == "self_attn.v_proj.weight":
-                            put(L["wqkv"][(H + KVH) * hd :], t)
+                            put(L["wqkv"][(H + KVH) * hd :], t, "v")
                         elif key == "self_attn.o_proj.weight":
-                            put(L["wo"], t)
+                            put(L["wo"], t, "wo")
                         elif key == "mlp.gate_proj.weight":
-                            put(L["wgu"][:f], t)
+                            put(L["wgu"][:f], t, "gate")
                         elif key == "mlp.up_proj.weight":
-                            put(L["wgu"][f:], t)
+                            put(L["wgu"][f:], t, "up")
                         elif key == "mlp.down_proj.weight":
-                            put(L["wdown"], t)
+                            put(L["wdown"], t, "wdown")
                         elif "rotary_emb" not in key:
                             raise ValueError(f"unexpected tensor {name}")
                     else:
@@ -237,7 +285,7 @@ class ServingLlama:
         return self
 
     def weight_bytes(self) -> int:
-        ts = [self.embed, self.norm] + ([] if self.lm_head is self.embed else [self.lm_head])
+        ts = [self.embed, self.norm] + ([] if self.spec.tie_embeddings else [self.lm_head])
         ts += [t for L in self.layers for t in L.values()]
         return sum(t.numel() * t.element_size() for t in ts)
 
@@ -259,8 +307,12 @@ class ServingLlama:
                 used = total - free
                 budget = total * gpu_memory_utilization - used - reserve_bytes
                 num_pages = int(budget // self.kv_bytes_per_page())
-                if num_pages < self.max_model_len // sops.PAGE + 1:
-                    raise RuntimeError(f"not enough HBM for the KV cache of one {self.max_model_len}-token sequence")
+            if self.tp > 1:  # every rank must hold the pages the leader's scheduler hands out
+                t = torch.tensor([num_pages], dtype=torch.int64, device=self.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.tp_group)
+                num_pages = int(t.item())
+            if self.device.type == "cuda" and num_pages < self.max_model_len // sops.PAGE + 1:
+                raise RuntimeError(f"not enough HBM for the KV cache of one {self.max_model_len}-token sequence")
         self.num_pages = num_pages
         self.k_cache, self.v_cache = [], []
         for _ in range(self.cfg.n_layers):
@@ -288,10 +340,24 @@ class ServingLlama:
             return _ext.require().swiglu_fwd(gu)
         return ref.swiglu(gu)
 
+    def _reduce(self, t):
+        """Sum the row-parallel partial outputs of the tensor-parallel ranks (RCCL all-reduce)."""
+        if self.tp > 1:
+            dist.all_reduce(t, group=self.tp_group)
+        return t
+
+    def _logits(self, h):
+        logits = h @ self.lm_head.t()
+        if self.tp == 1:
+            return logits
+        parts = [torch.empty_like(logits) for _ in range(self.tp)]
+        dist.all_gather(parts, logits.contiguous(), group=self.tp_group)
+        return torch.cat(parts, dim=-1)
+
     def _mlp_and_attn_out(self, L, x, o):
         """(x + o @ wo^T) -> norm -> SwiGLU MLP; returns (new residual, mlp output)."""
-        x, h = self._add_rms(x, o @ L["wo"].t(), L["ffn_norm"])
-        return x, self._swiglu(h @ L["wgu"].t()) @ L["wdown"].t()
+        x, h = self._add_rms(x, self._reduce(o @ L["wo"].t()), L["ffn_norm"])
+        return x, self._reduce(self._swiglu(h @ L["wgu"].t()) @ L["wdown"].t())
 
     # ------------------------------------------------------------------------------------------
     # forward passes
@@ -328,7 +394,7 @@ class ServingLlama:
             x, delta = self._mlp_and_attn_out(L, x, o)
         last = torch.tensor([int(offsets[i]) + int(lens[i]) - 1 for i in range(len(lens))], device=x.device)
         x, h = self._add_rms(x[last], delta[last], self.norm)
-        return h @ self.lm_head.t()
+        return self._logits(h)
 
     @torch.no_grad()
     def decode(self, tokens, positions, slots, block_tables, ctx_lens, ws=None):
@@ -347,4 +413,4 @@ class ServingLlama:
             o = sops.paged_decode(qkv, self.k_cache[li], self.v_cache[li], block_tables, ctx_lens, H, KVH, ws=ws)
             x, delta = self._mlp_and_attn_out(L, x, o)
         _, h = self._add_rms(x, delta, self.norm)
-        return h @ self.lm_head.t()
+        return self._logits(h)

@@ -28,16 +28,17 @@ def test_extension_loaded(gpu):
     assert _ext.available(), "HIP extension must be built for GPU runs"
 
 
+@pytest.mark.parametrize("rows", [512, 4096])  # block-per-row (<= 1024 rows) and wave-per-row kernels
 @pytest.mark.parametrize("D", [256, 4096, 8192])
-def test_rms_norm(gpu, D):
-    x = _rand(512, D, device=gpu).requires_grad_()
+def test_rms_norm(gpu, D, rows):
+    x = _rand(rows, D, device=gpu).requires_grad_()
     w = (1 + 0.1 * _rand(D, device=gpu, seed=1)).requires_grad_()
     y = ops.rms_norm(x, w, 1e-5)
     xr = x.detach().float().requires_grad_()
     wr = w.detach().float().requires_grad_()
     yr = ref.rms_norm(xr, wr, 1e-5)
     _close(y, yr, 2e-2, 1e-2)
-    dy = _rand(512, D, device=gpu, seed=2)
+    dy = _rand(rows, D, device=gpu, seed=2)
     y.backward(dy)
     yr.backward(dy.float())
     _close(x.grad, xr.grad, 3e-2, 1e-2)

@@ -174,6 +174,72 @@ def test_engine_preemption_keeps_greedy_outputs():
 
 
 # ------------------------------------------------------------------------------------------------
+# tensor parallel (gloo, 2 ranks on the CPU): same tokens as the single-process engine
+# ------------------------------------------------------------------------------------------------
+def _tp_worker(rank, world, port, model, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = LLMEngine.from_model(model, device="cpu", max_model_len=256, max_batch=4, num_pages=24,
+                                   tp_group=dist.group.WORLD)
+        if rank == 0:
+            prompts = [[1, 5, 9, 33, 7, 100, 2, 45, 61], [1, 300, 301, 302], list(range(3, 140))]
+            outs = eng.generate(prompts, SamplingParams(max_tokens=10, temperature=0, ignore_eos=True))
+            seeded = eng.generate([[4, 5, 6]], SamplingParams(max_tokens=6, temperature=0.9, seed=3, ignore_eos=True))
+            eng.shutdown()
+            q.put([r.output_ids for r in outs] + [seeded[0].output_ids])
+        else:
+            eng.follow()
+    finally:
+        dist.destroy_process_group()
+
+
+def _hf_tiny_tp(tmp_path):
+    transformers = pytest.importorskip("transformers")
+    cfg = transformers.LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2,
+                                   num_attention_heads=4, num_key_value_heads=2, vocab_size=512,
+                                   max_position_embeddings=1024, rope_theta=500000.0, head_dim=128)
+    torch.manual_seed(1)
+    m = transformers.LlamaForCausalLM(cfg)
+    with torch.no_grad():
+        for p in m.parameters():
+            if p.dim() == 2:
+                p.normal_(0, 0.06)
+    m.save_pretrained(str(tmp_path / "hftp"))
+    return str(tmp_path / "hftp")
+
+
+@pytest.mark.parametrize("source", ["random", "hf"])
+def test_tensor_parallel_matches_single_process(tmp_path, source):
+    import torch.multiprocessing as mp
+
+    from dstack_amd.server.testing import free_port
+
+    model = "llama-tiny" if source == "random" else _hf_tiny_tp(tmp_path)
+    single = LLMEngine.from_model(model, device="cpu", max_model_len=256, max_batch=4, num_pages=24)
+    prompts = [[1, 5, 9, 33, 7, 100, 2, 45, 61], [1, 300, 301, 302], list(range(3, 140))]
+    want = [r.output_ids for r in single.generate(prompts, SamplingParams(max_tokens=10, temperature=0,
+                                                                          ignore_eos=True))]
+    want.append(single.generate([[4, 5, 6]], SamplingParams(max_tokens=6, temperature=0.9, seed=3,
+                                                            ignore_eos=True))[0].output_ids)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, model, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == want
+
+
+# ------------------------------------------------------------------------------------------------
 # ops references
 # ------------------------------------------------------------------------------------------------
 def test_paged_decode_ref_matches_dense_attention():
