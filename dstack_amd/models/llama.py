@@ -141,7 +141,7 @@ class Llama(nn.Module):
         cos, sin = self.rope_tables(s, tokens.device)
         if self.param_waiter is not None:
             self.param_waiter([self.embed])
-        x = torch.nn.functional.embedding(tokens, self.embed)
+        x = ops.embedding(tokens, self.embed)
         delta = None
         for layer in self.layers:
             x, delta = layer(x, delta, cos, sin)

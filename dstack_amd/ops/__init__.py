@@ -10,6 +10,7 @@ from dstack_amd.ops.functional import (  # noqa: F401
     add_rms_norm,
     attention,
     cross_entropy,
+    embedding,
     linear,
     rms_norm,
     rope,

@@ -16,12 +16,14 @@ bool dsa_transpose2d_supported(int, int);
 hipError_t dsa_swiglu_fwd_t(const void*, void*, void*, int, int, hipStream_t);
 hipError_t dsa_transpose2d(const void*, void*, int, int, hipStream_t);
 hipError_t dsa_swiglu_bwd(const void*, const void*, void*, int, int, hipStream_t);
+hipError_t dsa_swiglu_bwd_t(const void*, const void*, void*, void*, int, int, hipStream_t);
 hipError_t dsa_rope_qkv(const void*, void*, const float*, const float*, int, int, int, int, int, int,
                         hipStream_t);
 hipError_t dsa_ce_fwd(const void*, const int64_t*, float*, float*, int, int, hipStream_t);
 hipError_t dsa_ce_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, hipStream_t);
 hipError_t dsa_adamw(void*, const void*, float*, float*, float*, size_t, float, float, float, float, float,
                      float, float, float, int, hipStream_t);
+hipError_t dsa_embedding_bwd(const void*, const int64_t*, const int64_t*, void*, int, int, int, hipStream_t);
 hipError_t dsa_fa_fwd(const void*, void*, float*, int, int, int, int, int, float, int, hipStream_t);
 size_t dsa_fa_bwd_workspace(int, int, int);
 hipError_t dsa_fa_bwd(const void*, const void*, const void*, const float*, void*, void*, int, int, int, int,
@@ -158,6 +160,21 @@ torch::Tensor swiglu_bwd(torch::Tensor da, torch::Tensor gu) {
   return dgu;
 }
 
+// returns {dgu [.., 2F], dgu^T [2F, T]}
+std::vector<torch::Tensor> swiglu_bwd_t(torch::Tensor da, torch::Tensor gu) {
+  check_bf16(da, "da");
+  check_bf16(gu, "gu");
+  const int F = gu.size(-1) / 2;
+  const int T = gu.numel() / gu.size(-1);
+  TORCH_CHECK(T % 128 == 0 && F % 64 == 0, "swiglu_bwd_t: rows % 128 and F % 64 must be 0");
+  TORCH_CHECK(da.numel() == (int64_t)T * F, "swiglu_bwd_t: da must be [T, F]");
+  auto dgu = torch::empty_like(gu);
+  auto dguT = torch::empty({2 * F, T}, gu.options());
+  check(dsa_swiglu_bwd_t(da.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), T, F, stream()),
+        "swiglu_bwd_t");
+  return {dgu, dguT};
+}
+
 torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, int64_t n_rot, int64_t head_dim,
                        bool inverse) {
   check_bf16(qkv, "qkv");
@@ -196,6 +213,23 @@ torch::Tensor cross_entropy_bwd(torch::Tensor logits, torch::Tensor target, torc
                    out.data_ptr(), rows, V, stream()),
         "cross_entropy_bwd");
   return out;
+}
+
+// grad (bf16 [V, D]) (+)= scatter-sum of dy rows by token id; the ids come stably sorted with their
+// original positions (torch.sort(stable=True)).  accumulate=false clears the whole table first.
+void embedding_bwd(torch::Tensor dy, torch::Tensor sorted_tok, torch::Tensor order, torch::Tensor grad,
+                   bool accumulate) {
+  check_bf16(dy, "dy");
+  check_bf16(grad, "grad");
+  TORCH_CHECK(dy.dim() == 2 && grad.dim() == 2 && dy.size(1) == grad.size(1), "embedding_bwd: dy [T, D], grad [V, D]");
+  for (auto* t : {&sorted_tok, &order}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt64 && t->is_contiguous() && t->numel() == dy.size(0),
+                "embedding_bwd: sorted ids / order must be int64 [T]");
+  }
+  if (!accumulate) check(hipMemsetAsync(grad.data_ptr(), 0, grad.numel() * 2, stream()), "embedding_bwd memset");
+  check(dsa_embedding_bwd(dy.data_ptr(), sorted_tok.data_ptr<int64_t>(), order.data_ptr<int64_t>(), grad.data_ptr(),
+                          (int)dy.size(0), (int)dy.size(1), accumulate ? 1 : 0, stream()),
+        "embedding_bwd");
 }
 
 void adamw(torch::Tensor param, torch::Tensor grad, torch::Tensor master, torch::Tensor m, torch::Tensor v,
@@ -352,10 +386,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_fwd_t", &swiglu_fwd_t);
   m.def("transpose2d_supported", &transpose2d_supported);
   m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_bwd_t", &swiglu_bwd_t);
   m.def("rope_qkv", &rope_qkv);
   m.def("cross_entropy_fwd", &cross_entropy_fwd);
   m.def("cross_entropy_bwd", &cross_entropy_bwd);
   m.def("adamw", &adamw);
+  m.def("embedding_bwd", &embedding_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("gemm_tn", &gemm_tn);

@@ -629,6 +629,60 @@ __global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restr
   tr_store_tile(tile, outT, (size_t)T, c0, r0, t);
 }
 
+// SwiGLU backward that also writes dgu^T [2F, T]: the gate/up projection's weight gradient
+// dW = dgu^T h then runs with both operands token-contiguous (TN) instead of token-major (TT),
+// for one extra 2 B/element write of the [T, 2F] gradient.  Same 128 x 64 tiling and transposed
+// store as transpose2d_kernel; the gate and up halves go through two LDS tiles.
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restrict__ da,
+                                                           const bf16_t* __restrict__ gu,
+                                                           bf16_t* __restrict__ dgu,
+                                                           bf16_t* __restrict__ dguT, int T, int F) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile_g[TR_R * TR_P];
+  __shared__ __attribute__((aligned(16))) bf16_t tile_u[TR_R * TR_P];
+  const int c0 = blockIdx.x * TR_C, r0 = blockIdx.y * TR_R;
+  const int t = threadIdx.x;
+  us8 gv[4], uv[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t, r = idx >> 3, ch = idx & 7;
+    const bf16_t* src = gu + (size_t)(r0 + r) * 2 * F + c0 + ch * 8;
+    gv[i] = *reinterpret_cast<const us8*>(src);
+    uv[i] = *reinterpret_cast<const us8*>(src + F);
+    dv[i] = *reinterpret_cast<const us8*>(da + (size_t)(r0 + r) * F + c0 + ch * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t, r = idx >> 3, ch = idx & 7;
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(gv[i], g);
+    unpack8(uv[i], u);
+    unpack8(dv[i], d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float s = 1.f / (1.f + __expf(-g[k]));
+      du[k] = d[k] * g[k] * s;
+      dg[k] = d[k] * u[k] * s * (1.f + g[k] * (1.f - s));
+    }
+    const us8 a = pack8(dg), b = pack8(du);
+    bf16_t* dst = dgu + (size_t)(r0 + r) * 2 * F + c0 + ch * 8;
+    *reinterpret_cast<us8*>(dst) = a;
+    *reinterpret_cast<us8*>(dst + F) = b;
+    *reinterpret_cast<us8*>(tile_g + tr_off(r, ch * 8)) = a;
+    *reinterpret_cast<us8*>(tile_u + tr_off(r, ch * 8)) = b;
+  }
+  __syncthreads();
+  tr_store_tile(tile_g, dguT, (size_t)T, c0, r0, t);
+  tr_store_tile(tile_u, dguT, (size_t)T, F + c0, r0, t);
+}
+
+extern "C" hipError_t dsa_swiglu_bwd_t(const void* da, const void* gu, void* dgu, void* dguT, int T, int F,
+                                       hipStream_t st) {
+  if (T % TR_R || F % TR_C) return hipErrorInvalidValue;
+  swiglu_bwd_t_kernel<<<dim3(F / TR_C, T / TR_R), 256, 0, st>>>((const bf16_t*)da, (const bf16_t*)gu,
+                                                                (bf16_t*)dgu, (bf16_t*)dguT, T, F);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t dsa_swiglu_fwd_t(const void* gu, void* out, void* outT, int T, int F, hipStream_t st) {
   if (T % TR_R || F % TR_C) return hipErrorInvalidValue;
   swiglu_fwd_t_kernel<<<dim3(F / TR_C, T / TR_R), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)out,
@@ -737,6 +791,50 @@ extern "C" hipError_t dsa_ce_bwd(const void* logits, const int64_t* target, cons
                                  hipStream_t st) {
   ce_bwd_kernel<<<rows, 256, 0, st>>>((const bf16_t*)logits, target, lse, scale, (bf16_t*)dlogits,
                                       V);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Embedding backward, deterministic with fp32 sums: the token ids are stably sorted on the host side
+// (sorted_tok, order).  Workgroup j looks at sorted position j; only the first position of a run
+// of equal ids does work: it sums the run's dy rows in fp32 (in stable order) and writes the bf16
+// gradient row (or adds it to the row already there).  Only the touched rows are read/written,
+// ~T*D*6 bytes, instead of PyTorch's dense [V, D] zero-fill + scatter + add per micro-batch
+// (~1.9 ms per 8192-token micro-batch of Llama-3-8B, r2g trace).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                        const int64_t* __restrict__ sorted_tok,
+                                                        const int64_t* __restrict__ order,
+                                                        bf16_t* __restrict__ grad, int T, int D,
+                                                        int accumulate) {
+  const int j = blockIdx.x;
+  const int64_t tok = sorted_tok[j];
+  if (j > 0 && sorted_tok[j - 1] == tok) return;  // not the first of its run (workgroup-uniform)
+  int end = j + 1;
+  while (end < T && sorted_tok[end] == tok) ++end;
+  bf16_t* g = grad + tok * (int64_t)D;
+  for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = j; k < end; ++k) {
+      float v[8];
+      unpack8(*reinterpret_cast<const us8*>(dy + order[k] * (int64_t)D + c), v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += v[i];
+    }
+    if (accumulate) {
+      float o[8];
+      unpack8(*reinterpret_cast<const us8*>(g + c), o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += o[i];
+    }
+    *reinterpret_cast<us8*>(g + c) = pack8(acc);
+  }
+}
+
+extern "C" hipError_t dsa_embedding_bwd(const void* dy, const int64_t* sorted_tok, const int64_t* order,
+                                        void* grad, int T, int D, int accumulate, hipStream_t st) {
+  if (D % 8 || T <= 0) return hipErrorInvalidValue;
+  embed_bwd_kernel<<<T, 256, 0, st>>>((const bf16_t*)dy, sorted_tok, order, (bf16_t*)grad, T, D, accumulate);
   return hipGetLastError();
 }
 

@@ -45,6 +45,8 @@ class _AddRMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, delta, w, eps):
         C = _ext.require()
+        # an unused residual output (the final norm) gets dh=None, not a materialised zero tensor
+        ctx.set_materialize_grads(False)
         h, y, rstd = C.add_rms_norm_fwd(_2d(x), _2d(delta), w, eps)
         ctx.save_for_backward(h, w, rstd)
         return h.view_as(x), y.view_as(x)
@@ -88,6 +90,10 @@ class _SwiGLU(torch.autograd.Function):
     def forward(ctx, gu, with_t):
         C = _ext.require()
         ctx.save_for_backward(gu)
+        # aT is non-differentiable: without this autograd zero-fills a [F, T] gradient for it in
+        # every backward (a 235 MB fill per layer and micro-batch of Llama-3-8B, r2g trace)
+        ctx.set_materialize_grads(False)
+        ctx.with_t = with_t
         if with_t:
             a, aT = C.swiglu_fwd_t(gu)
             ctx.mark_non_differentiable(aT)
@@ -98,6 +104,11 @@ class _SwiGLU(torch.autograd.Function):
     def backward(ctx, da, _daT):
         C = _ext.require()
         (gu,) = ctx.saved_tensors
+        if ctx.with_t and os.environ.get("DSTACK_AMD_SWIGLU_BWD_T", "1") != "0":
+            # also write dgu^T: the gate/up weight gradient then takes token-contiguous operands
+            dgu, dguT = C.swiglu_bwd_t(da.contiguous(), gu)
+            dgu._dsa_t = dguT
+            return dgu, None
         return C.swiglu_bwd(da.contiguous(), gu), None
 
 
@@ -145,6 +156,38 @@ def rope(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_rot_heads: i
     x = qkv.view(b, s, -1, head_dim)
     rot = ref.apply_rope(x[:, :, :n_rot_heads], cos, sin)
     return torch.cat([rot, x[:, :, n_rot_heads:]], dim=2).reshape(b, s, -1)
+
+
+# ----------------------------------------------------------------------------------------------
+# Token embedding whose backward scatter-sums straight into the optimizer's flat gradient buffer
+# ----------------------------------------------------------------------------------------------
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tokens, w):
+        ctx.save_for_backward(tokens, w)
+        return torch.nn.functional.embedding(tokens, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        tokens, w = ctx.saved_tensors
+        dy2 = _2d(dy.contiguous())
+        sorted_tok, order = torch.sort(tokens.reshape(-1), stable=True)
+        writer = getattr(w, "_dsa_grad_writer", None)
+        if writer is not None:
+            writer(w, lambda dst, acc: C.embedding_bwd(dy2, sorted_tok, order, dst, acc))
+            return None, None
+        dw = torch.empty_like(w)
+        C.embedding_bwd(dy2, sorted_tok, order, dw, False)
+        return None, dw
+
+
+def embedding(tokens: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``w[tokens]``; the HIP backward sums repeated ids in fp32 in a fixed order (deterministic) and
+    touches only the rows of the batch's ids (csrc/elementwise.hip ``embed_bwd_kernel``)."""
+    if _ext.use_hip(w) and w.dtype == torch.bfloat16 and w.shape[1] % 8 == 0:
+        return _Embedding.apply(tokens, w)
+    return torch.nn.functional.embedding(tokens, w)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -223,10 +266,11 @@ class _Linear(torch.autograd.Function):
         if not ctx.needs_input_grad[1]:
             return gx, None
         g2 = g.reshape(-1, g.shape[-1])
+        gT = getattr(g, "_dsa_t", None)
         if ctx.x_is_t:
-            a, b = wgrad_operands(g2, None, xT=xs)
+            a, b = wgrad_operands(g2, None, xT=xs, gT=gT)
         else:
-            a, b = wgrad_operands(g2, xs.reshape(-1, xs.shape[-1]))
+            a, b = wgrad_operands(g2, xs.reshape(-1, xs.shape[-1]), gT=gT)
         sink = getattr(w, "_dsa_grad_sink", None)
         if sink is None:
             return gx, a @ b
@@ -238,16 +282,18 @@ def _wgrad_mode() -> str:
     return os.environ.get("DSTACK_AMD_WGRAD", "auto").lower()
 
 
-def wgrad_operands(g2: torch.Tensor, x2, xT=None):
+def wgrad_operands(g2: torch.Tensor, x2, xT=None, gT=None):
     """Operands (a [P, T], b [T, Q]) with dW = a @ b for g2 [T, P] and x2 [T, Q] (or its transpose
-    ``xT`` [Q, T] when the producer already wrote it).
+    ``xT`` [Q, T] when the producer already wrote it; likewise ``gT`` [P, T] for g2).
 
     hipBLASLt runs dW = g^T x at ~1.0-1.1 PFLOP/s on MI355X when both operands are token-major
     (the reduction dimension is the strided one for both) and at 1.3-1.56 PFLOP/s when they are
     token-contiguous (tools/bench_wgrad_layouts.py, profiles/wgrad_layouts_r1.txt).  So x is
     transposed by the HIP transpose kernel (T x Q, a few % of the GEMM's time) and g too when it
-    is no larger than x (down/o projections; the gate_up and lm_head gradients are 3.5-31x larger
-    than their inputs and stay token-major).  ``DSTACK_AMD_WGRAD=strided`` keeps the old layout."""
+    is no larger than x (down/o projections).  A larger g (the gate_up gradient, 3.5x its input)
+    is used transposed only when its producer already wrote g^T (``gT``: SwiGLU backward);
+    the lm_head gradient (31x) stays token-major.  ``DSTACK_AMD_WGRAD=strided`` keeps the old
+    layout."""
     T, P = g2.shape
     Q = xT.shape[0] if xT is not None else x2.shape[1]
     a = g2.t()
@@ -257,7 +303,9 @@ def wgrad_operands(g2: torch.Tensor, x2, xT=None):
     C = _ext.require()
     if xT is None and x2.is_contiguous() and C.transpose2d_supported(T, Q):
         b = C.transpose2d(x2).t()
-    if P <= Q and g2.is_contiguous() and C.transpose2d_supported(T, P):
+    if gT is not None and tuple(gT.shape) == (P, T):
+        a = gT
+    elif P <= Q and g2.is_contiguous() and C.transpose2d_supported(T, P):
         a = C.transpose2d(g2)
     return a, b
 

@@ -128,7 +128,6 @@ class ZeroOptimizer:
             used = sum(p.numel() for p in b.params)
             if used < b.numel:
                 self._pads.append((b.start + used, b.numel - used))
-        self._backend = dist.get_backend(group) if self.distributed else None
         self._side = None
         import os
 
@@ -146,12 +145,11 @@ class ZeroOptimizer:
                 # GEMM-produced weight gradients are written straight into flat_grad (ops.linear)
                 p._dsa_grad_sink = self._direct_grad
                 p._dsa_fresh = True
-            if p.dim() == 1:
-                # norm weights: RMSNorm backward's column-sum kernel writes into flat_grad too
-                # (ops.functional).  The embedding keeps PyTorch's backward: it sums repeated token
-                # rows in fp32, which a bf16 atomic scatter into the flat buffer would not.
-                p._dsa_grad_writer = self._direct_write
-                p._dsa_fresh = True
+            # norm weights (RMSNorm backward's column-sum kernel) and the token embedding (sorted,
+            # fp32 segment-sum scatter kernel) write their gradients into flat_grad themselves too
+            # (ops.functional); a 2-D weight used by ops.linear only ever uses the sink above
+            p._dsa_grad_writer = self._direct_write
+            p._dsa_fresh = True
             if self._hooks_on:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self._direct_ok = set()
@@ -221,11 +219,8 @@ class ZeroOptimizer:
     def _all_gather(self, b: Bucket):
         s, n = b.shard_range(self.rank, self.world)
         full = self.flat_param[b.start : b.start + b.numel]
-        if self._backend == "gloo":
-            chunks = list(full.chunk(self.world))
-            b.ag_work = dist.all_gather(chunks, chunks[self.rank].clone(), group=self.group, async_op=True)
-            return
-        # in place: sendbuff == recvbuff + rank * sendcount
+        # in place: sendbuff == recvbuff + rank * sendcount (the same call on RCCL and, in the CPU
+        # tests, on gloo, so the multi-rank tests run the code path the GPUs run)
         b.ag_work = dist.all_gather_into_tensor(full, self.flat_param[s : s + n], group=self.group, async_op=True)
 
     @torch.no_grad()
@@ -251,9 +246,6 @@ class ZeroOptimizer:
         s, n = b.shard_range(self.rank, self.world)
         full = self.flat_grad[b.start : b.start + b.numel]
         out = self.flat_grad[s : s + n]
-        if self._backend == "gloo":  # CPU tests: gloo has no reduce-scatter
-            b.work = dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
-            return
         # in place: RCCL reduce-scatters when recvbuff == sendbuff + rank * recvcount
         b.work = dist.reduce_scatter_tensor(
             out, full, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op
