@@ -262,7 +262,10 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         xs, w = ctx.saved_tensors
-        gx = g @ w if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            wt = _transposed_weight(w)
+            gx = g @ (wt.t() if wt is not None else w)
         if not ctx.needs_input_grad[1]:
             return gx, None
         g2 = g.reshape(-1, g.shape[-1])
@@ -276,6 +279,30 @@ class _Linear(torch.autograd.Function):
             return gx, a @ b
         sink(w, a, b)
         return gx, None
+
+
+def _transposed_weight(w: torch.Tensor):
+    """W^T [K, N] of a weight W [N, K] whose optimizer publishes a weight generation
+    (``w._dsa_wgen()``, bumped whenever the weights change: ZeroOptimizer.step / load_state).
+
+    The input gradient g @ W reduces over N, which is W's strided dimension: hipBLASLt runs that
+    "NN" GEMM at 1.22-1.40 PFLOP/s in the Llama-3-8B step, against 1.55-1.60 for the forward's
+    layout, where the reduction dimension is contiguous in both operands.  g @ (W^T)^T is that
+    layout.  The transpose is made once per weight generation, in the first micro-batch's
+    backward (~225 us per layer, HIP transpose kernel) and reused by every later micro-batch;
+    ``DSTACK_AMD_DGRAD_WT=0`` keeps the NN GEMM."""
+    gen = getattr(w, "_dsa_wgen", None)
+    if gen is None or w.dim() != 2 or not _ext.use_hip(w) or os.environ.get("DSTACK_AMD_DGRAD_WT", "1") == "0":
+        return None
+    C = _ext.require()
+    if not (w.is_contiguous() and C.transpose2d_supported(w.shape[0], w.shape[1])):
+        return None
+    cur = gen()
+    cached = getattr(w, "_dsa_wt", None)
+    if cached is None or cached[0] != cur:
+        w._dsa_wt = None  # drop the stale copy before allocating the new one
+        w._dsa_wt = (cur, C.transpose2d(w.detach()))
+    return w._dsa_wt[1]
 
 
 def _wgrad_mode() -> str:

@@ -145,6 +145,8 @@ class ZeroOptimizer:
                 # GEMM-produced weight gradients are written straight into flat_grad (ops.linear)
                 p._dsa_grad_sink = self._direct_grad
                 p._dsa_fresh = True
+                # weight generation: ops.linear caches W^T for the input-gradient GEMM per generation
+                p._dsa_wgen = self._weight_generation
             # norm weights (RMSNorm backward's column-sum kernel) and the token embedding (sorted,
             # fp32 segment-sum scatter kernel) write their gradients into flat_grad themselves too
             # (ops.functional); a 2-D weight used by ops.linear only ever uses the sink above
@@ -154,7 +156,12 @@ class ZeroOptimizer:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self._direct_ok = set()
         self._prefetch = False
+        self._wgen = 0
         self._arm()
+
+    def _weight_generation(self) -> int:
+        """Changes whenever the parameters are rewritten (optimizer step, checkpoint load)."""
+        return self._wgen
 
     # ------------------------------------------------------------------------------------------
     def _arm(self):
@@ -290,11 +297,13 @@ class ZeroOptimizer:
                                      "(checkpoints restore only into the same world size)")
                 dst[i].copy_(src.to(dst[i].device))
         self.step_count = step_count
+        self._wgen += 1
 
     @torch.no_grad()
     def step(self):
         self.wait_params()  # no forward ran since the last step: finish its all-gathers first
         self.step_count += 1
+        self._wgen += 1
         pending = [b for b in self.buckets if not b.updated]
         if self.world > 1:
             for b in pending:

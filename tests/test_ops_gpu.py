@@ -443,3 +443,27 @@ def test_gate_up_chain_wgrad_modes_agree(gpu, monkeypatch):
     assert torch.equal(res["auto"][0], res["strided"][0])
     ra, rs = res["auto"][1].float(), res["strided"][1].float()
     assert ((ra - rs).norm() / rs.norm()).item() < 4e-3
+
+
+def test_linear_dgrad_uses_transposed_weight_per_generation(gpu, monkeypatch):
+    """With a weight generation published (ZeroOptimizer), linear's input gradient runs on a cached
+    W^T; the cache is rebuilt when the generation changes, so an updated weight is never stale."""
+    T, N, K = 256, 384, 256
+    gen = [0]
+    w = _rand(N, K, device=gpu, seed=26, scale=0.05).requires_grad_()
+    w._dsa_wgen = lambda: gen[0]
+    x = _rand(T, K, device=gpu, seed=27).requires_grad_()
+    g = _rand(T, N, device=gpu, seed=28)
+    ops.linear(x, w).backward(g)
+    assert w._dsa_wt[0] == 0 and torch.equal(w._dsa_wt[1], w.detach().t().contiguous())
+    _close(x.grad, g.float() @ w.detach().float(), 0.05, 1e-2)
+    with torch.no_grad():
+        w.mul_(-2.0)
+    gen[0] = 1
+    x.grad = None
+    ops.linear(x, w).backward(g)
+    assert w._dsa_wt[0] == 1
+    _close(x.grad, g.float() @ w.detach().float(), 0.05, 1e-2)
+    monkeypatch.setenv("DSTACK_AMD_DGRAD_WT", "0")
+    gx_nn = torch.autograd.grad(ops.linear(x, w), x, g)[0]
+    _close(x.grad, gx_nn, 0.05, 1e-2)
