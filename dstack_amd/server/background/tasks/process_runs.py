@@ -54,6 +54,8 @@ def _process_run(s: Session, run_id):
     if run is None:
         return
     s.refresh(run)
+    if RunStatus(run.status).is_finished():
+        return  # finished between selection and claim (another pass finished it): nothing to do
     if run.status == RunStatus.TERMINATING.value:
         runs_services.process_terminating_run(s, run)
     elif run.status == RunStatus.PENDING.value:
