@@ -206,16 +206,30 @@ class RunConfigurator:
             plan = client.runs.get_plan(conf, repo, configuration_path=conf_path, profile=profile, run_name=run_name,
                                         max_offers=args.max_offers)
         print_table(plan_table(plan, args.max_offers))
+        stop_first = None
         if plan.current_resource is not None and not plan.current_resource.status.is_finished():
-            action = "update" if plan.action and plan.action.value == "update" else "re-create"
-            if not args.yes and not confirm_ask(f"Active run [code]{plan.run_spec.run_name}[/] already exists. "
-                                                f"{action.capitalize()} it?"):
+            if plan.action and plan.action.value == "update":
+                question = f"Active run [code]{plan.run_spec.run_name}[/] already exists. Update it?"
+            else:  # not updatable in place: stop it, wait, then submit the new spec
+                stop_first = plan.run_spec.run_name
+                question = f"Active run [code]{stop_first}[/] already exists and cannot be updated in place. " \
+                           "Stop and override the run?"
+            if not args.yes and not confirm_ask(question):
                 console.print("\nExiting...")
                 return 0
         elif not args.yes and not confirm_ask("Submit the run?" if plan.job_plans[0].offers else
                                               "No offers right now. Submit anyway (waits for capacity)?"):
             console.print("\nExiting...")
             return 0
+        if stop_first is not None:
+            with console.status("Stopping run..."):
+                old = client.runs.get(stop_first)
+                if old is not None:
+                    old.stop(abort=False)
+                while old is not None and not old.status.is_finished():
+                    time.sleep(1)
+                    old = client.runs.get(stop_first)
+            plan.current_resource = None
         with console.status("Submitting run..."):
             run = client.runs.exec_plan(plan, repo, force=args.force)
         name = run.name

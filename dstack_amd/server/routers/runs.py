@@ -49,7 +49,7 @@ pool_router = APIRouter(prefix="/api/project/{project_name}/pool", tags=["pools"
 def list_runs(body: schemas.ListRunsRequest, user: UserModel = Depends(authenticated),
               s: Session = Depends(get_session)) -> List[Run]:
     return runs_services.list_user_runs(s, user, body.project_name, body.repo_id, body.only_active, body.limit,
-                                        body.prev_submitted_at, body.ascending)
+                                        body.prev_submitted_at, body.ascending, body.username, body.prev_run_id)
 
 
 @runs_router.post("/get")

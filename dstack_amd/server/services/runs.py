@@ -79,24 +79,46 @@ def run_model_to_run(run: RunModel, include_jobs: bool = True, return_in_api: bo
 
 def list_user_runs(s: Session, user: UserModel, project_name: Optional[str] = None, repo_id: Optional[str] = None,
                    only_active: bool = False, limit: int = 100, prev_submitted_at: Optional[datetime] = None,
-                   ascending: bool = False) -> List[Run]:
-    from dstack_amd.server.services.projects import list_user_projects
+                   ascending: bool = False, username: Optional[str] = None,
+                   prev_run_id: Optional[uuid.UUID] = None) -> List[Run]:
+    """Runs of the projects the user sees (all for a global admin), newest first, as keyset pages:
+    the next page starts after (``prev_submitted_at``, ``prev_run_id``) of the previous page's last
+    run (reference ``S/services/runs.py:list_user_runs``).  ``repo_id`` needs ``project_name``;
+    ``username`` keeps one user's runs."""
+    from sqlalchemy import and_, or_
 
+    from dstack_amd.server.services.projects import list_user_projects
+    from dstack_amd.server.services.users import get_user_by_name
+
+    if project_name is None and repo_id is not None:
+        return []
     projects = list_user_projects(s, user)
     if project_name:
         projects = [p for p in projects if p.name == project_name]
     if not projects:
         return []
     q = select(RunModel).where(RunModel.project_id.in_([p.id for p in projects]), RunModel.deleted == False)  # noqa
+    if repo_id is not None:
+        q = q.where(RunModel.repo_id == repos_services.get_repo_or_error(s, projects[0], repo_id).id)
+    if username is not None:
+        runs_user = get_user_by_name(s, username)
+        if runs_user is None:
+            raise ResourceNotExistsError("User not found")
+        q = q.where(RunModel.user_id == runs_user.id)
     if only_active:
         q = q.where(RunModel.status.notin_([st.value for st in RunStatus.finished_statuses()]))
     if prev_submitted_at is not None:
-        q = q.where(RunModel.submitted_at > prev_submitted_at if ascending else RunModel.submitted_at < prev_submitted_at)
-    q = q.order_by(RunModel.submitted_at.asc() if ascending else RunModel.submitted_at.desc()).limit(limit)
-    rows = list(s.execute(q).scalars())
-    if repo_id:
-        rows = [r for r in rows if r.repo and r.repo.name == repo_id]
-    return [run_model_to_run(r) for r in rows]
+        after = RunModel.submitted_at > prev_submitted_at if ascending else RunModel.submitted_at < prev_submitted_at
+        if prev_run_id is None:
+            q = q.where(after)
+        else:
+            tie = RunModel.id > prev_run_id if ascending else RunModel.id < prev_run_id
+            q = q.where(or_(after, and_(RunModel.submitted_at == prev_submitted_at, tie)))
+    if ascending:
+        q = q.order_by(RunModel.submitted_at.asc(), RunModel.id.asc())
+    else:
+        q = q.order_by(RunModel.submitted_at.desc(), RunModel.id.desc())
+    return [run_model_to_run(r) for r in s.execute(q.limit(limit)).scalars()]
 
 
 def get_run_model(s: Session, project: ProjectModel, run_name: Optional[str] = None,
@@ -131,7 +153,10 @@ def get_plan(s: Session, project: ProjectModel, user: UserModel, run_spec: RunSp
         cur = get_run_model(s, project, run_spec.run_name)
         if cur is not None and not RunStatus(cur.status).is_finished():
             current = run_model_to_run(cur)
-            action = ApplyAction.UPDATE
+            # UPDATE only when the change can be applied to the live run (replicas / scaling);
+            # anything else is a CREATE the client must stop the active run for first
+            if _updatable(RunSpec.model_validate_json(cur.run_spec), run_spec):
+                action = ApplyAction.UPDATE
     profile = effective.merged_profile
     job_plans = []
     pool = pools_services.get_or_create_default_pool(s, project)
@@ -203,18 +228,16 @@ def apply_plan(s: Session, project: ProjectModel, user: UserModel, run_spec: Run
             cur_spec = RunSpec.model_validate_json(cur.run_spec)
             if not force and current_resource is not None and current_resource.id != cur.id:
                 raise ServerClientError("The run changed since the plan was made; re-plan or use --force")
-            if _updatable(cur_spec, run_spec):
-                cur.run_spec = run_spec.model_dump_json()
-                conf = run_spec.configuration
-                if isinstance(conf, ServiceConfiguration):
-                    cur.desired_replica_count = max(conf.replicas.min, min(conf.replicas.max, cur.desired_replica_count))
-                s.flush()
-                scheduler.wake(scheduler.RUNS)
-                return run_model_to_run(cur)
-            stop_runs(s, project, [cur.run_name], abort=False)
+            if not _updatable(cur_spec, run_spec):
+                # the client stops the run and waits for it to finish before re-applying
+                raise ServerClientError("Cannot override active run. Stop the run first.")
+            cur.run_spec = run_spec.model_dump_json()
+            conf = run_spec.configuration
+            if isinstance(conf, ServiceConfiguration):
+                cur.desired_replica_count = max(conf.replicas.min, min(conf.replicas.max, cur.desired_replica_count))
             s.flush()
-            raise ServerClientError(f"Run {cur.run_name} cannot be updated in place; it is being stopped — apply "
-                                    "again once it has terminated")
+            scheduler.wake(scheduler.RUNS)
+            return run_model_to_run(cur)
     return submit_run(s, project, user, run_spec)
 
 
