@@ -239,7 +239,7 @@ class NebiusCompute(VMCompute):
     API = "https://compute.api.nebius.cloud/compute/v1"
 
     def _h(self):
-        return {"Authorization": f"Bearer {self.auth.get('iam_token', '')}"}
+        return {"Authorization": f"Bearer {self.auth.get('iam_token') or self.auth.get('token', '')}"}
 
     def _launch(self, offer, cfg):
         res = offer.instance.resources

@@ -1,0 +1,277 @@
+"""Per-backend configuration contract: what ``projects[].backends[]`` in the server's ``config.yml``
+and the ``/api/project/{p}/backends/create|update(_yaml)`` endpoints accept (reference:
+``C/models/backends/{aws,azure,gcp,oci,lambdalabs,vultr,tensordock,cudo,datacrunch,nebius,runpod,
+vastai,kubernetes}.py`` — the same YAML keys and credential types, so a reference server config
+loads unchanged).
+
+Every backend is one model discriminated by ``type``; credentials are a nested union discriminated
+by ``creds.type``.  ``split_backend_config`` validates a raw mapping and returns (config without
+secrets, secrets) — the server stores the two in separate columns, the secrets encrypted, and never
+returns the secrets from ``config_info``/``get_yaml``.
+"""
+
+from __future__ import annotations
+
+from typing import Annotated, Dict, List, Literal, Optional, Tuple, Union
+
+from pydantic import Field, ValidationError
+
+from dstack_amd.core.errors import ServerClientError
+from dstack_amd.core.models.common import CoreModel
+
+
+class _Input(CoreModel):
+    model_config = {"extra": "forbid"}
+
+
+# ---- credential types -----------------------------------------------------------------------------
+class AccessKeyCreds(_Input):
+    type: Literal["access_key"] = "access_key"
+    access_key: str
+    secret_key: str
+    session_token: Optional[str] = None
+
+
+class DefaultCreds(_Input):
+    """Use the environment's credentials (instance role, CLI config, env vars)."""
+
+    type: Literal["default"] = "default"
+
+
+class ClientCreds(_Input):  # Azure service principal
+    type: Literal["client"] = "client"
+    client_id: str
+    client_secret: str
+    tenant_id: Optional[str] = None
+
+
+class ServiceAccountCreds(_Input):  # GCP / Nebius service-account key file (contents in ``data``)
+    type: Literal["service_account"] = "service_account"
+    filename: Optional[str] = None
+    data: str
+
+
+class OCIClientCreds(_Input):
+    type: Literal["client"] = "client"
+    user: str
+    tenancy: str
+    key_file: Optional[str] = None
+    key_content: Optional[str] = None
+    pass_phrase: Optional[str] = None
+    fingerprint: str
+    region: str
+
+
+class OCIDefaultCreds(_Input):
+    type: Literal["default"] = "default"
+    file: str = "~/.oci/config"
+    profile: str = "DEFAULT"
+
+
+class APIKeyCreds(_Input):
+    type: Literal["api_key"] = "api_key"
+    api_key: str
+
+
+class TensorDockCreds(_Input):
+    type: Literal["api_key"] = "api_key"
+    api_key: str
+    api_token: str
+
+
+class DataCrunchCreds(_Input):
+    type: Literal["api_key"] = "api_key"
+    client_id: str
+    client_secret: str
+
+
+class IAMTokenCreds(_Input):
+    """A pre-issued Nebius IAM token (addition to the reference's service-account creds)."""
+
+    type: Literal["iam_token"] = "iam_token"
+    iam_token: str
+
+
+# ---- backend configs ---------------------------------------------------------------------------
+class AWSOSImage(_Input):
+    name: str
+    owner: str = "self"
+    user: str = "ubuntu"
+
+
+class AWSOSImages(_Input):
+    cpu: Optional[AWSOSImage] = None
+    amd: Optional[AWSOSImage] = None  # ROCm image for AMD Instinct instances
+    nvidia: Optional[AWSOSImage] = None
+
+
+class AWSConfig(_Input):
+    type: Literal["aws"] = "aws"
+    regions: Optional[List[str]] = None
+    vpc_name: Optional[str] = None
+    vpc_ids: Optional[Dict[str, str]] = None
+    subnet_ids: Optional[Dict[str, str]] = None
+    default_vpcs: Optional[bool] = None
+    public_ips: Optional[bool] = None
+    tags: Optional[Dict[str, str]] = None
+    os_images: Optional[AWSOSImages] = None
+    creds: Annotated[Union[AccessKeyCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
+
+
+class AzureConfig(_Input):
+    type: Literal["azure"] = "azure"
+    tenant_id: str
+    subscription_id: str
+    locations: Optional[List[str]] = None
+    regions: Optional[List[str]] = None
+    vpc_ids: Optional[Dict[str, str]] = None
+    resource_groups: Optional[Dict[str, str]] = None
+    subnet_id: Optional[str] = None
+    public_ips: Optional[bool] = None
+    tags: Optional[Dict[str, str]] = None
+    creds: Annotated[Union[ClientCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
+
+
+class GCPConfig(_Input):
+    type: Literal["gcp"] = "gcp"
+    project_id: str
+    regions: Optional[List[str]] = None
+    zones: Optional[Dict[str, str]] = None
+    vpc_name: Optional[str] = None
+    vpc_project_id: Optional[str] = None
+    public_ips: Optional[bool] = None
+    nat_check: Optional[bool] = None
+    vm_service_account: Optional[str] = None
+    tags: Optional[Dict[str, str]] = None
+    creds: Annotated[Union[ServiceAccountCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
+
+
+class OCIConfig(_Input):
+    type: Literal["oci"] = "oci"
+    regions: Optional[List[str]] = None
+    compartment_id: Optional[str] = None
+    subnet_ids: Optional[Dict[str, str]] = None
+    images: Optional[Dict[str, str]] = None
+    availability_domains: Optional[Dict[str, str]] = None
+    creds: Annotated[Union[OCIClientCreds, OCIDefaultCreds], Field(discriminator="type")] = OCIDefaultCreds()
+
+
+class LambdaConfig(_Input):
+    type: Literal["lambda"] = "lambda"
+    regions: Optional[List[str]] = None
+    creds: APIKeyCreds
+
+
+class VultrConfig(_Input):
+    type: Literal["vultr"] = "vultr"
+    regions: Optional[List[str]] = None
+    creds: APIKeyCreds
+
+
+class TensorDockConfig(_Input):
+    type: Literal["tensordock"] = "tensordock"
+    regions: Optional[List[str]] = None
+    creds: TensorDockCreds
+
+
+class CudoConfig(_Input):
+    type: Literal["cudo"] = "cudo"
+    project_id: str
+    regions: Optional[List[str]] = None
+    creds: APIKeyCreds
+
+
+class DataCrunchConfig(_Input):
+    type: Literal["datacrunch"] = "datacrunch"
+    regions: Optional[List[str]] = None
+    creds: DataCrunchCreds
+
+
+class NebiusConfig(_Input):
+    type: Literal["nebius"] = "nebius"
+    cloud_id: Optional[str] = None
+    folder_id: str
+    network_id: Optional[str] = None
+    subnet_id: Optional[str] = None
+    image_id: Optional[str] = None
+    regions: Optional[List[str]] = None
+    creds: Annotated[Union[ServiceAccountCreds, IAMTokenCreds], Field(discriminator="type")]
+
+
+class RunpodConfig(_Input):
+    type: Literal["runpod"] = "runpod"
+    regions: Optional[List[str]] = None
+    creds: APIKeyCreds
+
+
+class VastAIConfig(_Input):
+    type: Literal["vastai"] = "vastai"
+    regions: Optional[List[str]] = None
+    creds: APIKeyCreds
+
+
+class KubernetesNetworking(_Input):
+    ssh_host: Optional[str] = None
+    ssh_port: Optional[int] = None
+
+
+class Kubeconfig(_Input):
+    filename: Optional[str] = None
+    data: str
+
+
+class KubernetesConfig(_Input):
+    type: Literal["kubernetes"] = "kubernetes"
+    namespace: Optional[str] = None
+    api_url: Optional[str] = None
+    networking: KubernetesNetworking = KubernetesNetworking()
+    kubeconfig: Kubeconfig  # the cluster credentials (stored with the secrets)
+
+
+class DstackConfig(_Input):
+    type: Literal["dstack"] = "dstack"
+    base_backends: List[str] = []
+
+
+AnyBackendConfig = Annotated[
+    Union[AWSConfig, AzureConfig, GCPConfig, OCIConfig, LambdaConfig, VultrConfig, TensorDockConfig, CudoConfig,
+          DataCrunchConfig, NebiusConfig, RunpodConfig, VastAIConfig, KubernetesConfig, DstackConfig],
+    Field(discriminator="type"),
+]
+
+
+class _Wrapper(CoreModel):
+    config: AnyBackendConfig
+
+
+# secret-bearing keys per backend type (everything else is plain configuration)
+_SECRET_KEYS = {"kubernetes": ("kubeconfig",)}
+
+
+def parse_backend_config(raw: dict):
+    """Validate a backend mapping; a bad one raises ``ServerClientError`` naming the fields."""
+    if not isinstance(raw, dict) or "type" not in raw:
+        raise ServerClientError("Backend config must be a mapping with a 'type'")
+    try:
+        return _Wrapper.model_validate({"config": raw}).config
+    except ValidationError as e:
+        errs = "; ".join(f"{'.'.join(str(x) for x in err['loc'][2:]) or 'config'}: {err['msg']}"
+                         for err in e.errors())
+        raise ServerClientError(f"Invalid {raw.get('type')} backend config: {errs}") from None
+
+
+def split_backend_config(raw: dict) -> Tuple[str, dict, dict]:
+    """(type, config without secrets, secrets) of a validated backend mapping."""
+    model = parse_backend_config(raw)
+    data = model.model_dump(mode="json", exclude_none=True)
+    btype = data.pop("type")
+    secret_keys = _SECRET_KEYS.get(btype, ("creds",))
+    secrets = {}
+    for k in secret_keys:
+        if k in data:
+            v = data.pop(k)
+            if k == "creds":
+                secrets.update(v)
+            else:
+                secrets[k] = v
+    return btype, data, secrets

@@ -135,7 +135,10 @@ def list_backend_types() -> List[str]:
 
 @backends_router.post("/config_values")
 def backend_config_values(body: dict) -> dict:
-    return {"type": body.get("type"), "regions": {"values": []}}
+    """Choices for a backend form (reference ``/api/backends/config_values``): the regions the
+    catalog knows for the type, with the requested ones (or all) selected; credentials are
+    validated when the backend is created."""
+    return backends_services.backend_config_values(body)
 
 
 @project_backends_router.post("/create")

@@ -22,6 +22,7 @@ from sqlalchemy.orm import Session
 
 from dstack_amd.core.backends.base import Compute
 from dstack_amd.core.errors import BackendNotAvailable, ResourceExistsError, ResourceNotExistsError, ServerClientError
+from dstack_amd.core.models.backend_configs import split_backend_config
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.instances import InstanceAvailability, InstanceOfferWithAvailability
 from dstack_amd.core.models.runs import Requirements
@@ -41,6 +42,8 @@ def _make_compute(backend_type: BackendType, config: dict, auth: dict) -> Comput
     from dstack_amd.core.backends.clouds import compute_class
 
     cls = compute_class(backend_type)
+    if backend_type == BackendType.KUBERNETES and auth.get("kubeconfig") and not config.get("kubeconfig"):
+        config = {**config, "kubeconfig": auth["kubeconfig"]}  # stored with the secrets
     if cls is not None:
         return cls(config, auth)
     from dstack_amd.core.backends.catalog import CatalogCompute
@@ -106,31 +109,49 @@ def get_project_backend(s: Session, project: ProjectModel, backend_type: Backend
 
 
 def create_backend(s: Session, project: ProjectModel, config: dict) -> BackendModel:
-    btype = BackendType(config.get("type"))
-    if btype in (BackendType.LOCAL, BackendType.REMOTE):
-        raise ServerClientError(f"{btype.value} backend needs no configuration")
+    """Validate ``config`` against the backend's model (``core/models/backend_configs.py``) and
+    store it: plain settings in ``config``, credentials in the encrypted ``auth`` column."""
+    btype = _configurable_type(config)
     existing = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
                                                     BackendModel.type == btype.value)).scalar_one_or_none()
     if existing is not None:
         raise ResourceExistsError(f"Backend {btype.value} exists")
-    cfg = {k: v for k, v in config.items() if k not in ("type", "creds")}
+    _, cfg, secrets = split_backend_config(config)
     row = BackendModel(id=uuid.uuid4(), project_id=project.id, type=btype.value, config=json.dumps(cfg),
-                       auth=json.dumps(config.get("creds") or {}))
+                       auth=json.dumps(secrets))
     s.add(row)
     s.flush()
     return row
 
 
 def update_backend(s: Session, project: ProjectModel, config: dict) -> BackendModel:
-    btype = BackendType(config.get("type"))
+    """Replace a backend's settings; credentials omitted from ``config`` keep their stored value."""
+    btype = _configurable_type(config)
     row = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
                                                BackendModel.type == btype.value)).scalar_one_or_none()
     if row is None:
         raise ResourceNotExistsError(f"Backend {btype.value} not found")
-    row.config = json.dumps({k: v for k, v in config.items() if k not in ("type", "creds")})
-    if config.get("creds") is not None:
-        row.auth = json.dumps(config["creds"])
+    merged = dict(config)
+    old_secrets = json.loads(row.auth or "{}")
+    if merged.get("creds") is None and btype != BackendType.KUBERNETES and old_secrets:
+        merged["creds"] = old_secrets
+    if btype == BackendType.KUBERNETES and merged.get("kubeconfig") is None and old_secrets.get("kubeconfig"):
+        merged["kubeconfig"] = old_secrets["kubeconfig"]
+    _, cfg, secrets = split_backend_config(merged)
+    row.config = json.dumps(cfg)
+    row.auth = json.dumps(secrets)
     return row
+
+
+def _configurable_type(config: dict) -> BackendType:
+    try:
+        btype = BackendType(config.get("type"))
+    except ValueError:
+        raise ServerClientError(f"Unknown backend type {config.get('type')!r}; one of: "
+                                f"{', '.join(b.value for b in CONFIGURABLE_BACKENDS)}") from None
+    if btype in (BackendType.LOCAL, BackendType.REMOTE):
+        raise ServerClientError(f"{btype.value} backend needs no configuration")
+    return btype
 
 
 def delete_backends(s: Session, project: ProjectModel, names: List[str]):
@@ -139,6 +160,18 @@ def delete_backends(s: Session, project: ProjectModel, names: List[str]):
                                                    BackendModel.type == n)).scalar_one_or_none()
         if row is not None:
             s.delete(row)
+
+
+def backend_config_values(body: dict) -> dict:
+    from dstack_amd.core.backends.catalog import CATALOG
+
+    btype = _configurable_type(body)
+    regions = sorted({r for it in CATALOG if it.backend == btype for r in it.regions})
+    wanted = body.get("regions") or body.get("locations")
+    selected = [r for r in regions if not wanted or r in wanted]
+    return {"type": btype.value, "default_creds": btype in (BackendType.AWS, BackendType.AZURE, BackendType.GCP,
+                                                             BackendType.OCI),
+            "regions": {"selected": selected, "values": [{"value": r, "label": r} for r in regions]}}
 
 
 def backend_config_info(s: Session, project: ProjectModel, name: str) -> dict:
