@@ -318,6 +318,7 @@ class FleetConfigurator:
 
         if conf.name is None:
             conf.name = Path(conf_path).stem.replace(".dstack", "").replace("_", "-") or "fleet"
+        _resolve_ssh_keys(conf)
         spec = FleetSpec(configuration=conf, configuration_path=conf_path)
         plan = client.api.fleets.get_plan(client.project, spec)
         if plan.current_resource is not None:
@@ -349,6 +350,35 @@ class FleetConfigurator:
         client.api.fleets.delete(client.project, [conf.name])
         console.print(f"Fleet [code]{conf.name}[/] deleted")
         return 0
+
+
+def _read_ssh_key(identity_file: str):
+    """``identity_file`` -> SSHKey with the private key's contents (and the ``.pub`` next to it)."""
+    from dstack_amd.core.models.fleets import SSHKey
+
+    path = os.path.expanduser(identity_file)
+    try:
+        with open(path) as f:
+            private = f.read()
+    except OSError as e:
+        raise ConfigurationError(f"Cannot read identity_file {identity_file}: {e}") from e
+    public = ""
+    if os.path.exists(path + ".pub"):
+        with open(path + ".pub") as f:
+            public = f.read().strip()
+    return SSHKey(public=public, private=private)
+
+
+def _resolve_ssh_keys(conf):
+    """The fleet's ``identity_file``s are read HERE, on the client; the server gets key contents."""
+    sc = getattr(conf, "ssh_config", None)
+    if sc is None:
+        return
+    if sc.ssh_key is None and sc.identity_file:
+        sc.ssh_key = _read_ssh_key(sc.identity_file)
+    for h in sc.hosts:
+        if not isinstance(h, str) and h.ssh_key is None and h.identity_file:
+            h.ssh_key = _read_ssh_key(h.identity_file)
 
 
 class GatewayConfigurator:

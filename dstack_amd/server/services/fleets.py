@@ -4,6 +4,7 @@ instances, optionally in a placement group; SSH: one instance per host), delete,
 from __future__ import annotations
 
 import json
+import re
 import uuid
 from typing import List, Optional
 
@@ -84,8 +85,51 @@ def _idle_seconds(conf: FleetConfiguration) -> int:
     return int(v)
 
 
+_NAME_RE = re.compile(r"^[a-z][a-z0-9-]{1,40}$")
+_KEY_HEADER = re.compile(r"-----BEGIN (RSA |EC |OPENSSH )?PRIVATE KEY-----")
+
+
+def _validate_fleet_spec(spec: FleetSpec):
+    """Reject specs the reconcilers could never act on (reference ``_validate_fleet_spec``): a fleet
+    needs ``nodes`` or ``ssh_config``; every SSH host needs a user and a usable private key (the
+    CLI resolves ``identity_file`` into ``ssh_key`` on the client: the server never reads a path
+    it was sent); ``internal_ip`` is given for all hosts or none, and not together with
+    ``network``."""
+    conf = spec.configuration
+    if conf.name is not None and not _NAME_RE.match(conf.name):
+        raise ServerClientError("Fleet name must be 2-41 chars of a-z, 0-9 and -, starting with a letter")
+    if conf.ssh_config is None and conf.nodes is None:
+        raise ServerClientError("No ssh_config or nodes specified")
+    sc = conf.ssh_config
+    if sc is None:
+        return
+    with_ip = 0
+    for host in sc.hosts:
+        h = host if isinstance(host, SSHHostParams) else SSHHostParams(hostname=host)
+        key = h.ssh_key or sc.ssh_key
+        if key is None:
+            raise ServerClientError(f"No ssh key specified for host {h.hostname}")
+        _validate_private_key(key)
+        if (h.user or sc.user) is None:
+            raise ServerClientError(f"No ssh user specified for host {h.hostname}")
+        with_ip += h.internal_ip is not None
+    if with_ip not in (0, len(sc.hosts)):
+        raise ServerClientError("internal_ip must be specified for all hosts")
+    if with_ip and sc.network is not None:
+        raise ServerClientError("internal_ip is mutually exclusive with network")
+
+
+def _validate_private_key(key: SSHKey):
+    if not key.private:
+        raise ServerClientError("Private key not provided")
+    if not _KEY_HEADER.search(key.private) or "ENCRYPTED" in key.private:
+        raise ServerClientError("Unsupported key type. The key type should be RSA, ECDSA, or Ed25519 and should "
+                                "not be encrypted with passphrase.")
+
+
 def create_fleet(s: Session, project: ProjectModel, user: UserModel, spec: FleetSpec) -> Fleet:
     conf = spec.configuration
+    _validate_fleet_spec(spec)
     with db_advisory_lock(s, f"fleet_names_{project.id}"):
         if conf.name is None:
             conf.name = generate_name()
@@ -101,18 +145,9 @@ def create_fleet(s: Session, project: ProjectModel, user: UserModel, spec: Fleet
         if conf.ssh_config is not None:
             for i, host in enumerate(conf.ssh_config.hosts):
                 h = host if isinstance(host, SSHHostParams) else SSHHostParams(hostname=host)
-                user_name = h.user or conf.ssh_config.user or "root"
+                user_name = h.user or conf.ssh_config.user
                 port = h.port or conf.ssh_config.port or 22
                 key = h.ssh_key or conf.ssh_config.ssh_key
-                if key is None:
-                    ident = h.identity_file or conf.ssh_config.identity_file
-                    if ident:
-                        import os
-
-                        with open(os.path.expanduser(ident)) as fh:
-                            key = SSHKey(public="", private=fh.read())
-                if key is None:
-                    raise ServerClientError(f"No SSH key for host {h.hostname}")
                 rci = RemoteConnectionInfo(host=h.hostname, port=port, ssh_user=user_name, ssh_keys=[key],
                                            env=conf.env)
                 pools_services.create_instance_model(

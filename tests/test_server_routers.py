@@ -180,8 +180,10 @@ def test_service_replicas(client):
 
 # ---- fleets / instances / volumes / gateways ---------------------------------------------------
 def test_ssh_fleet_create_and_delete(client):
+    key = {"public": "ssh-ed25519 AAAA", "private": "-----BEGIN OPENSSH PRIVATE KEY-----\nx\n"
+                                                   "-----END OPENSSH PRIVATE KEY-----\n"}
     spec = {"spec": {"configuration": {"type": "fleet", "name": "onprem",
-                                       "ssh_config": {"user": "ubuntu", "identity_file": "/dev/null",
+                                       "ssh_config": {"user": "ubuntu", "ssh_key": key,
                                                       "hosts": ["10.0.0.1", "10.0.0.2"]}},
                      "profile": {"name": "default"}}}
     r = client.post("/api/project/main/fleets/get_plan", json=spec)
