@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import json
 import logging
+import uuid
 from datetime import timedelta
 from typing import Optional
 
@@ -17,7 +18,8 @@ from sqlalchemy import select
 from sqlalchemy.orm import Session
 
 from dstack_amd.core.backends.remote import deploy_ssh_instance, host_info_to_instance_type, remote_backend_data, split_blocks
-from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.backends import BACKENDS_WITH_CREATE_INSTANCE_SUPPORT, BACKENDS_WITH_PLACEMENT_GROUPS_SUPPORT, BackendType
+from dstack_amd.core.models.fleets import InstanceGroupPlacement
 from dstack_amd.core.models.instances import (
     InstanceAvailability,
     InstanceConfiguration,
@@ -26,7 +28,7 @@ from dstack_amd.core.models.instances import (
     RemoteConnectionInfo,
     SSHKey,
 )
-from dstack_amd.core.models.profiles import Profile
+from dstack_amd.core.models.profiles import Profile, RetryEvent
 from dstack_amd.core.models.runs import JobProvisioningData, Requirements
 from dstack_amd.server.background import scheduler
 from dstack_amd.server.background.common import claim_and_process
@@ -112,7 +114,22 @@ def _add_remote(s: Session, inst: InstanceModel):
     scheduler.wake(scheduler.SUBMITTED_JOBS)
 
 
+NO_CAPACITY_RETRY = timedelta(minutes=1)
+MAX_OFFERS_TRIED = 15
+
+
 def _create_instance(s: Session, inst: InstanceModel):
+    """Provision a cloud-fleet instance (reference ``_create_instance``, process_instances.py:431-605).
+
+    * ``placement: cluster`` fleets: instances after the first wait until it is provisioned, then
+      take offers only from its backend and region (same availability zone, and an AWS placement
+      group created once per fleet/backend/region), so the nodes share a network fabric;
+    * no offers / every offer failed: with ``retry.on_events: [no-capacity]`` try again every
+      minute until the retry duration expires, otherwise the instance is terminated;
+    * ``blocks`` of the fleet split the new instance's GPUs for shared use."""
+    now = get_current_datetime()
+    if inst.last_retry_at is not None and now - inst.last_retry_at < NO_CAPACITY_RETRY:
+        return
     project = inst.project
     profile = Profile.model_validate_json(inst.profile) if inst.profile else Profile(name="default")
     req = Requirements.model_validate_json(inst.requirements) if inst.requirements else None
@@ -120,12 +137,43 @@ def _create_instance(s: Session, inst: InstanceModel):
         inst.status = InstanceStatus.TERMINATED.value
         inst.termination_reason = "no requirements"
         return
-    offers = offers_services.get_offers_by_requirements(s, project, profile, req, exclude_not_available=True)
+    bd = json.loads(inst.backend_data or "{}")
+    cluster = bd.get("placement") == InstanceGroupPlacement.CLUSTER.value
+    master_jpd: Optional[JobProvisioningData] = None
+    if cluster and inst.fleet is not None:
+        master = min(inst.fleet.instances, key=lambda i: (i.instance_num, i.created_at))
+        if master.id != inst.id:
+            if master.job_provisioning_data is None:
+                if master.status != InstanceStatus.TERMINATED.value:
+                    return  # wait for the first node: the others follow it
+            else:
+                master_jpd = JobProvisioningData.model_validate_json(master.job_provisioning_data)
+    from dstack_amd.server.services.jobs.configurators import retry_from_profile
+
+    retry = retry_from_profile(profile)
+    should_retry = retry is not None and RetryEvent.NO_CAPACITY in retry.on_events
+    if retry is not None and now > inst.created_at + timedelta(seconds=retry.duration):
+        inst.status = InstanceStatus.TERMINATED.value
+        inst.termination_reason = "Retry duration expired"
+        return
+    blocks = bd.get("blocks", 1) or 1
+    offers = offers_services.get_offers_by_requirements(
+        s, project, profile, req, exclude_not_available=True, multinode=cluster,
+        master_job_provisioning_data=master_jpd, blocks=blocks)
+    offers = [(c, o) for c, o in offers
+              if o.backend in BACKENDS_WITH_CREATE_INSTANCE_SUPPORT and o.backend != BackendType.REMOTE]
     cfg = InstanceConfiguration(project_name=project.name, instance_name=inst.name, user="",
-                                ssh_keys=[SSHKey(public=project.ssh_public_key.strip())])
-    for compute, offer in offers[:15]:
-        if offer.backend == BackendType.REMOTE:
-            continue
+                                ssh_keys=[SSHKey(public=project.ssh_public_key.strip())],
+                                availability_zone=master_jpd.availability_zone if master_jpd else None,
+                                reservation=profile.reservation)
+    for compute, offer in offers[:MAX_OFFERS_TRIED]:
+        if cluster and inst.fleet is not None and offer.backend in BACKENDS_WITH_PLACEMENT_GROUPS_SUPPORT:
+            try:
+                cfg.placement_group_name = _fleet_placement_group(s, inst, compute, offer)
+            except Exception as e:  # noqa: BLE001
+                logger.info("instance %s: placement group in %s/%s failed: %s", inst.name, offer.backend.value,
+                            offer.region, e)
+                continue
         try:
             jpd = compute.create_instance(offer, cfg)
         except Exception as e:  # noqa: BLE001
@@ -136,19 +184,42 @@ def _create_instance(s: Session, inst: InstanceModel):
         inst.price = jpd.price
         inst.offer = offer.model_dump_json()
         inst.job_provisioning_data = jpd.model_dump_json()
-        inst.total_blocks = 1
+        n_gpus = len(offer.instance.resources.gpus)
+        inst.total_blocks = (max(1, n_gpus) if blocks == "auto" else int(blocks))
         inst.backend_data = jpd.backend_data
         inst.status = (InstanceStatus.IDLE if jpd.backend == BackendType.LOCAL else InstanceStatus.PROVISIONING).value
-        inst.started_at = get_current_datetime()
+        inst.started_at = now
+        inst.termination_reason = None
         if jpd.backend == BackendType.LOCAL:
             from dstack_amd.core.backends.local import LocalShim
 
             _, topo = host_info_to_instance_type(LocalShim.get().host_info)
             inst.host_topology = topo.model_dump_json()
         return
-    inst.termination_reason = "no offers / no capacity"
-    if get_current_datetime() - inst.created_at > timedelta(hours=24):
+    inst.last_retry_at = now
+    inst.termination_reason = "no offers / no capacity" if not offers else "all offers failed"
+    if not should_retry:
         inst.status = InstanceStatus.TERMINATED.value
+
+
+def _fleet_placement_group(s: Session, inst: InstanceModel, compute, offer) -> str:
+    """The fleet's cluster placement group in the offer's backend/region (created on first use)."""
+    from dstack_amd.core.models.placement import PlacementGroup, PlacementGroupConfiguration
+    from dstack_amd.server.models import PlacementGroupModel
+
+    for pg in s.execute(select(PlacementGroupModel).where(PlacementGroupModel.fleet_id == inst.fleet_id,
+                                                          PlacementGroupModel.deleted == False)).scalars():  # noqa
+        c = PlacementGroupConfiguration.model_validate_json(pg.configuration)
+        if c.backend == offer.backend and c.region == offer.region:
+            return pg.name
+    conf = PlacementGroupConfiguration(backend=offer.backend, region=offer.region)
+    name = f"{inst.project.name}-{inst.fleet.name}-{uuid.uuid4().hex[:8]}-pg"
+    pgpd = compute.create_placement_group(PlacementGroup(name=name, project_name=inst.project.name,
+                                                         configuration=conf))
+    s.add(PlacementGroupModel(id=uuid.uuid4(), name=name, project_id=inst.project_id, fleet_id=inst.fleet_id,
+                              configuration=conf.model_dump_json(), provisioning_data=pgpd.model_dump_json()))
+    s.flush()
+    return name
 
 
 def _check_provisioning(s: Session, inst: InstanceModel):
@@ -227,4 +298,3 @@ def _terminate(s: Session, inst: InstanceModel):
     scheduler.wake(scheduler.FLEETS)
 
 
-_ = Optional

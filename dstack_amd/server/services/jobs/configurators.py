@@ -46,7 +46,11 @@ def get_default_image(conf) -> str:
 
 
 def _retry(run_spec: RunSpec) -> Optional[Retry]:
-    prof = run_spec.merged_profile
+    return retry_from_profile(run_spec.merged_profile)
+
+
+def retry_from_profile(prof) -> Optional[Retry]:
+    """``retry`` (or the deprecated ``retry_policy``) of a profile as (events, duration seconds)."""
     r = prof.retry
     if r is None and prof.retry_policy is not None and prof.retry_policy.retry:
         return Retry(on_events=[RetryEvent.NO_CAPACITY, RetryEvent.INTERRUPTION, RetryEvent.ERROR],

@@ -64,5 +64,5 @@ def _divisible(offer: InstanceOfferWithAvailability, blocks) -> bool:
 
 
 def _with_blocks(offer: InstanceOfferWithAvailability, blocks) -> InstanceOfferWithAvailability:
-    total = len(offer.instance.resources.gpus) or 1 if blocks == "auto" else blocks
+    total = (len(offer.instance.resources.gpus) or 1) if blocks == "auto" else blocks
     return offer.model_copy(update={"total_blocks": total})

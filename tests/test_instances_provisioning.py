@@ -1,0 +1,197 @@
+"""Cloud-fleet instance provisioning in ``process_instances`` (reference: ``src/tests/_internal/server/
+background/tasks/test_process_instances.py``): ``placement: cluster`` fleets provision the first
+node, then the rest in its backend/region/availability zone inside one placement group; no-capacity
+retries every minute until ``retry.duration`` runs out; without retry the instance is terminated;
+``blocks`` split a new instance's GPUs; offers from backends that cannot create instances are
+skipped."""
+
+from __future__ import annotations
+
+import json
+from datetime import timedelta
+from typing import List
+from unittest import mock
+
+import pytest
+
+from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.instances import (
+    Disk,
+    Gpu,
+    InstanceAvailability,
+    InstanceOfferWithAvailability,
+    InstanceStatus,
+    InstanceType,
+    Resources,
+)
+from dstack_amd.core.models.placement import PlacementGroupProvisioningData
+from dstack_amd.core.models.runs import JobProvisioningData
+from dstack_amd.server.background.tasks import process_instances as pi
+from dstack_amd.server.db import session_scope
+from dstack_amd.server.models import FleetModel, InstanceModel, PlacementGroupModel, ProjectModel, UserModel
+from dstack_amd.server.services import fleets as fleets_services
+from dstack_amd.utils.common import get_current_datetime
+
+
+def _offer(backend=BackendType.AWS, region="us-east-1", gpus=8, price=10.0):
+    it = InstanceType(name="p-mi355x", resources=Resources(cpus=128, memory_mib=2048 * 1024,
+                                                           gpus=[Gpu(name="MI355X", memory_mib=288 * 1024)] * gpus,
+                                                           disk=Disk(size_mib=1024 * 1024)))
+    return InstanceOfferWithAvailability(backend=backend, instance=it, region=region, price=price,
+                                         availability=InstanceAvailability.AVAILABLE)
+
+
+class FakeCompute:
+    def __init__(self, fail: bool = False):
+        self.created: List[tuple] = []
+        self.pgs: List[str] = []
+        self.fail = fail
+
+    def create_instance(self, offer, cfg):
+        if self.fail:
+            raise RuntimeError("InsufficientInstanceCapacity")
+        self.created.append((offer.backend, offer.region, cfg.availability_zone, cfg.placement_group_name))
+        return JobProvisioningData(backend=offer.backend, instance_type=offer.instance, instance_id=f"i-{len(self.created)}",
+                                   hostname=None, internal_ip=None, region=offer.region, price=offer.price,
+                                   username="ubuntu", ssh_port=22, dockerized=True,
+                                   availability_zone=f"{offer.region}a")
+
+    def create_placement_group(self, pg):
+        self.pgs.append(pg.name)
+        return PlacementGroupProvisioningData(backend=pg.configuration.backend)
+
+
+def _fleet(s, conf: dict):
+    from dstack_amd.core.models.fleets import FleetSpec
+
+    project = s.query(ProjectModel).filter_by(name="main").one()
+    user = s.query(UserModel).filter_by(name="admin").one()
+    spec = FleetSpec.model_validate({"configuration": {"type": "fleet", **conf}, "profile": {"name": "default"}})
+    return fleets_services.create_fleet(s, project, user, spec)
+
+
+def _instances(s, fleet_name):
+    f = s.query(FleetModel).filter_by(name=fleet_name).one()
+    return sorted(f.instances, key=lambda i: i.instance_num)
+
+
+def _process(iid, offers_fn, at=None):
+    patches = [mock.patch.object(pi.offers_services, "get_offers_by_requirements", side_effect=offers_fn)]
+    if at is not None:
+        patches.append(mock.patch.object(pi, "get_current_datetime", return_value=at))
+    for p in patches:
+        p.start()
+    try:
+        with session_scope() as s:
+            pi._process_instance(s, iid)
+    finally:
+        for p in patches:
+            p.stop()
+
+
+def test_cluster_fleet_follows_first_node(db):
+    comp = FakeCompute()
+    calls = []
+
+    def offers(s, project, profile, req, **kw):
+        calls.append(kw)
+        mj = kw.get("master_job_provisioning_data")
+        if mj is not None:
+            return [(comp, _offer(mj.backend, mj.region))]
+        return [(comp, _offer(BackendType.AWS, "us-west-2", price=9.0)), (comp, _offer(BackendType.AWS, "us-east-1"))]
+
+    with session_scope() as s:
+        _fleet(s, {"name": "clu", "nodes": 3, "placement": "cluster", "resources": {"gpu": "MI355X:8"}})
+        ids = [i.id for i in _instances(s, "clu")]
+    _process(ids[1], offers)  # a follower before the first node: waits, no offers queried
+    assert calls == [] and comp.created == []
+    _process(ids[0], offers)
+    assert comp.created[0][:2] == (BackendType.AWS, "us-west-2") and calls[0]["multinode"]
+    for iid in ids[1:]:
+        _process(iid, offers)
+    assert [c[:3] for c in comp.created[1:]] == [(BackendType.AWS, "us-west-2", "us-west-2a")] * 2
+    # one placement group for the fleet in that backend/region, used by every node
+    assert len(comp.pgs) == 1 and {c[3] for c in comp.created} == {comp.pgs[0]}
+    with session_scope() as s:
+        assert s.query(PlacementGroupModel).count() == 1
+        assert {i.status for i in _instances(s, "clu")} == {InstanceStatus.PROVISIONING.value}
+
+
+def test_no_capacity_retried_every_minute_until_duration(db):
+    comp = FakeCompute(fail=True)
+    with session_scope() as s:
+        _fleet(s, {"name": "retry", "nodes": 1, "retry": {"on_events": ["no-capacity"], "duration": "10m"}})
+        (inst,) = _instances(s, "retry")
+        iid, created = inst.id, inst.created_at
+    offers = lambda *a, **k: [(comp, _offer())]  # noqa: E731
+    _process(iid, offers)
+    with session_scope() as s:
+        i = s.get(InstanceModel, iid)
+        assert i.status == InstanceStatus.PENDING.value and i.last_retry_at is not None
+        assert i.termination_reason == "all offers failed"
+    # within the minute: not retried; after it: retried
+    with mock.patch.object(comp, "create_instance", side_effect=RuntimeError("x")) as ci:
+        _process(iid, offers, at=created + timedelta(seconds=20))
+        assert ci.call_count == 0
+        _process(iid, offers, at=created + timedelta(minutes=2))
+        assert ci.call_count == 1
+    _process(iid, offers, at=created + timedelta(minutes=11))
+    with session_scope() as s:
+        i = s.get(InstanceModel, iid)
+        assert i.status == InstanceStatus.TERMINATED.value and i.termination_reason == "Retry duration expired"
+
+
+def test_no_offers_without_retry_terminates(db):
+    with session_scope() as s:
+        _fleet(s, {"name": "noretry", "nodes": 1})
+        (inst,) = _instances(s, "noretry")
+        iid = inst.id
+    _process(iid, lambda *a, **k: [])
+    with session_scope() as s:
+        i = s.get(InstanceModel, iid)
+        assert i.status == InstanceStatus.TERMINATED.value and "no offers" in i.termination_reason
+
+
+@pytest.mark.parametrize("blocks,expect", [(1, 1), (4, 4), ("auto", 8)])
+def test_fleet_blocks_split_new_instance(db, blocks, expect):
+    comp = FakeCompute()
+    seen = {}
+
+    def offers(s, project, profile, req, **kw):
+        seen["blocks"] = kw.get("blocks")
+        return [(comp, _offer())]
+
+    with session_scope() as s:
+        _fleet(s, {"name": "blk", "nodes": 1, "blocks": blocks})
+        (inst,) = _instances(s, "blk")
+        iid = inst.id
+    _process(iid, offers)
+    assert seen["blocks"] == blocks
+    with session_scope() as s:
+        assert s.get(InstanceModel, iid).total_blocks == expect
+
+
+def test_offers_of_backends_without_create_instance_skipped(db):
+    comp = FakeCompute()
+    with session_scope() as s:
+        _fleet(s, {"name": "skip", "nodes": 1})
+        (inst,) = _instances(s, "skip")
+        iid = inst.id
+    _process(iid, lambda *a, **k: [(comp, _offer(BackendType.RUNPOD, "EU-RO-1", gpus=1, price=1.0)),
+                                   (comp, _offer(BackendType.VULTR, "ewr"))])
+    assert [c[0] for c in comp.created] == [BackendType.VULTR]
+
+
+def test_blocks_offer_helper_keeps_int_blocks():
+    from dstack_amd.server.services.offers import _with_blocks
+
+    assert _with_blocks(_offer(gpus=8), 2).total_blocks == 2
+    assert _with_blocks(_offer(gpus=8), "auto").total_blocks == 8
+    assert _with_blocks(_offer(gpus=0), "auto").total_blocks == 1
+
+
+def test_fleet_backend_data_records_placement(db):
+    with session_scope() as s:
+        _fleet(s, {"name": "bd", "nodes": 2, "placement": "cluster"})
+        assert all(json.loads(i.backend_data)["placement"] == "cluster" for i in _instances(s, "bd"))
+    _ = get_current_datetime
