@@ -319,14 +319,20 @@ def set_wildcard_domain(body: schemas.SetWildcardDomainRequest, up: UP = Depends
 def poll_logs(body: schemas.PollLogsRequest, up: UP = Depends(project_member)) -> JobSubmissionLogs:
     from datetime import datetime
 
-    start = body.start_time
+    start, end = body.start_time, body.end_time
     if body.next_token:
         try:
-            start = datetime.fromisoformat(body.next_token)
+            token = datetime.fromisoformat(body.next_token)
         except ValueError:
             raise ServerClientError("invalid next_token")
+        # the token is the last returned event's timestamp: the next page continues past it in the
+        # direction of the listing
+        if body.descending:
+            end = token
+        else:
+            start = token
     return logs_services.get_default_log_storage().poll_logs(
-        up[1].name, body.run_name, str(body.job_submission_id), start, body.end_time, body.descending, body.limit,
+        up[1].name, body.run_name, str(body.job_submission_id), start, end, body.descending, body.limit,
         body.diagnose)
 
 

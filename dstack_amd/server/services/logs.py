@@ -95,7 +95,8 @@ class FileLogStorage(LogStorage):
             with self._lock:
                 ts_list, offs, end = self._index(p)
             lo = bisect.bisect_right(ts_list, _aware(start_time).timestamp()) if start_time is not None else 0
-            hi = bisect.bisect_right(ts_list, _aware(end_time).timestamp()) if end_time is not None else len(ts_list)
+            # (start_time, end_time) is exclusive at both ends: callers page with the last timestamp
+            hi = bisect.bisect_left(ts_list, _aware(end_time).timestamp()) if end_time is not None else len(ts_list)
             if descending:
                 lo = max(lo, hi - limit)
             else:

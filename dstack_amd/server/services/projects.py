@@ -47,6 +47,11 @@ def list_user_projects(s: Session, user: UserModel) -> List[ProjectModel]:
 
 
 def create_project(s: Session, user: UserModel, project_name: str) -> ProjectModel:
+    if user.global_role != GlobalRole.ADMIN.value:
+        owned = s.execute(select(ProjectModel).where(ProjectModel.owner_id == user.id,
+                                                     ProjectModel.deleted == False)).scalars().all()  # noqa: E712
+        if len(owned) >= (user.projects_quota or 0):
+            raise ServerClientError("User project quota exceeded")
     if get_project_by_name(s, project_name, include_deleted=True) is not None:
         raise ResourceExistsError(f"Project {project_name} exists")
     if not project_name.replace("-", "").replace("_", "").isalnum():
@@ -75,6 +80,14 @@ def set_members(s: Session, actor: UserModel, project: ProjectModel, members: Li
     role = get_member_role(project, actor)
     if actor.global_role != GlobalRole.ADMIN.value and role not in (ProjectRole.ADMIN, ProjectRole.MANAGER):
         raise ForbiddenError()
+    if actor.global_role != GlobalRole.ADMIN.value and role == ProjectRole.MANAGER:
+        # a manager manages users and managers, never the project's admins
+        want = {(m["username"], ProjectRole(m["project_role"])) for m in members
+                if ProjectRole(m["project_role"]) == ProjectRole.ADMIN}
+        have = {(m.user.name, ProjectRole.ADMIN) for m in project.members
+                if ProjectRole(m.project_role) == ProjectRole.ADMIN}
+        if want != have:
+            raise ForbiddenError("Access denied: changing project admins")
     for m in list(project.members):
         s.delete(m)
     s.flush()
