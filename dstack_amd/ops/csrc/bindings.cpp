@@ -36,6 +36,8 @@ hipError_t dsa_paged_decode(const void*, long, const void*, const void*, const i
 hipError_t dsa_sample(const void*, long, int, int, const float*, const int64_t*, const int*, int*, float*,
                       hipStream_t);
 bool dsa_gemm_tn_supported(int, int, int);
+bool dsa_gemv_supported(int, int);
+hipError_t dsa_gemv(const void*, long, const void*, void*, long, int, int, int, hipStream_t);
 hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 }
 
@@ -277,6 +279,23 @@ torch::Tensor flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tenso
 
 bool gemm_tn_supported(int64_t P, int64_t Q, int64_t T) { return dsa_gemm_tn_supported(P, Q, T); }
 
+bool gemv_supported(int64_t M, int64_t K) { return dsa_gemv_supported((int)M, (int)K); }
+
+// y [M, N] = x [M, K] @ w[N, K]^T for M <= 4 (decode projections, csrc/gemv.hip)
+torch::Tensor gemv(torch::Tensor x, torch::Tensor w) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.stride(1) == 1,
+              "gemv: x must be bf16 [M, K] with contiguous rows");
+  check_bf16(w, "w");
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == x.size(1), "gemv: w must be [N, K]");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "gemv: x alignment");
+  const int64_t M = x.size(0), N = w.size(0), K = x.size(1);
+  TORCH_CHECK(dsa_gemv_supported((int)M, (int)K), "gemv: M <= 4 and K % 512 == 0");
+  auto y = torch::empty({M, N}, x.options());
+  check(dsa_gemv(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), N, (int)M, (int)N, (int)K, stream()),
+        "gemv");
+  return y;
+}
+
 // out[P][Q] (+)= a^T b ; a = [T][P], b = [T][Q] (weight gradient dW = dY^T X)
 void gemm_tn(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool accumulate) {
   for (auto* t : {&a, &b, &out}) {
@@ -396,6 +415,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("gemm_tn", &gemm_tn);
   m.def("gemm_tn_supported", &gemm_tn_supported);
+  m.def("gemv", &gemv);
+  m.def("gemv_supported", &gemv_supported);
   m.def("paged_page_size", &dsa_paged_page_size);
   m.def("rope_cache_write", &rope_cache_write);
   m.def("paged_decode", &paged_decode);

@@ -259,25 +259,58 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
 }
 
 // merge the split partials: out[b][h*128 + d] = sum_s 2^(lse_s - M) o_s / sum_s 2^(lse_s - M)
-__global__ __launch_bounds__(128) void paged_combine_kernel(const float* __restrict__ o_part,
+// One 256-thread workgroup per (b, h): 8 groups of 32 lanes take every 8th split, a lane owns 4
+// d values (one 16-byte load of a 512-byte partial row per split), and the groups meet in LDS.
+// (The first form walked all splits serially with one thread per d: at batch 1 and 32k context,
+// ~256 splits, it was latency-bound at 85 us per layer -- 6.8 ms of a 33 ms 70B decode step,
+// profiles/decode_batch1_32k_r2p.txt.)
+__global__ __launch_bounds__(256) void paged_combine_kernel(const float* __restrict__ o_part,
                                                             const float* __restrict__ lse_part,
                                                             bf16_t* __restrict__ out, int H,
                                                             int nsplit) {
+  __shared__ float red_max[4];
+  __shared__ float red_den[8];
+  __shared__ f4 red_num[8][32];
   const long bh = blockIdx.x;
-  const int d = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = tid >> 5, l32 = tid & 31;
   const float* lse = lse_part + bh * nsplit;
   float M = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, lse[s]);
-  float num = 0.f, den = 0.f;
+  for (int s = tid; s < nsplit; s += 256) M = fmaxf(M, lse[s]);
+  M = wave_max(M);
+  if (lane == 0) red_max[wave] = M;
+  __syncthreads();
+  M = fmaxf(fmaxf(red_max[0], red_max[1]), fmaxf(red_max[2], red_max[3]));
+  f4 num = {0.f, 0.f, 0.f, 0.f};
+  float den = 0.f;
   if (M > -INFINITY) {
-    for (int s = 0; s < nsplit; ++s) {
-      if (lse[s] == -INFINITY) continue;
-      const float w = fexp2(lse[s] - M);
-      num += w * o_part[(bh * nsplit + s) * HDIM + d];
+    const f4* op = reinterpret_cast<const f4*>(o_part + bh * (long)nsplit * HDIM) + l32;
+#pragma unroll 4
+    for (int s = g; s < nsplit; s += 8) {
+      const float ls = lse[s];
+      const float w = ls == -INFINITY ? 0.f : fexp2(ls - M);
+      const f4 o = op[(long)s * (HDIM / 4)];
+      num += w * o;
       den += w;
     }
   }
-  out[bh * HDIM + d] = f2bf(den > 0.f ? num / den : 0.f);
+  red_num[g][l32] = num;
+  if (l32 == 0) red_den[g] = den;
+  __syncthreads();
+  if (tid < 32) {
+    f4 n = red_num[0][tid];
+    float dsum = red_den[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      n += red_num[k][tid];
+      dsum += red_den[k];
+    }
+    const float inv = dsum > 0.f ? 1.f / dsum : 0.f;
+    typedef unsigned short us4 __attribute__((ext_vector_type(4)));
+    us4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = f2bf(n[i] * inv);
+    *reinterpret_cast<us4*>(out + bh * HDIM + 4 * tid) = v;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -420,7 +453,7 @@ extern "C" hipError_t dsa_paged_decode(const void* q, long q_stride, const void*
                                                  ctx_lens, nullptr, o_part, lse_part, H, KVH, G,
                                                  nsplit, pages_per_split, sl2);
   DSA_CHECK(hipGetLastError());
-  paged_combine_kernel<<<B * H, 128, 0, st>>>(o_part, lse_part, (bf16_t*)out, H, nsplit);
+  paged_combine_kernel<<<B * H, 256, 0, st>>>(o_part, lse_part, (bf16_t*)out, H, nsplit);
   return hipGetLastError();
 }
 

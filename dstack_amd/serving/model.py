@@ -142,6 +142,8 @@ class ServingLlama:
         self.hip = self.device.type == "cuda" and not _ext.force_torch()
         if self.hip:
             _ext.require()
+        # DSTACK_AMD_GEMV=0: small decode batches on hipBLASLt too (A/B switch)
+        self.gemv = os.environ.get("DSTACK_AMD_GEMV", "1") != "0"
         self.cos, self.sin = rope_tables(self.max_model_len + sops.PAGE, self.D, cfg.rope_theta, spec.rope_scaling,
                                          self.device)
         self.layers: list[dict] = []
@@ -340,6 +342,17 @@ class ServingLlama:
             return _ext.require().swiglu_fwd(gu)
         return ref.swiglu(gu)
 
+    def _mm(self, x, w):
+        """``x @ w.T``: a batch-1 decode step streams the weights through the HIP GEMV kernel
+        (``csrc/gemv.hip``: 6.1-6.8 TB/s on the 70B projections vs hipBLASLt's 5.5-6.2, where it
+        wins; at 2-4 rows hipBLASLt is faster, profiles/bench_gemv_r2o.log); larger batches and
+        prefill use hipBLASLt."""
+        if self.hip and self.gemv and x.shape[0] == 1:
+            C = _ext.require()
+            if C.gemv_supported(x.shape[0], x.shape[1]) and x.stride(-1) == 1:
+                return C.gemv(x, w)
+        return x @ w.t()
+
     def _reduce(self, t):
         """Sum the row-parallel partial outputs of the tensor-parallel ranks (RCCL all-reduce)."""
         if self.tp > 1:
@@ -347,7 +360,7 @@ class ServingLlama:
         return t
 
     def _logits(self, h):
-        logits = h @ self.lm_head.t()
+        logits = self._mm(h, self.lm_head)
         if self.tp == 1:
             return logits
         parts = [torch.empty_like(logits) for _ in range(self.tp)]
@@ -356,8 +369,8 @@ class ServingLlama:
 
     def _mlp_and_attn_out(self, L, x, o):
         """(x + o @ wo^T) -> norm -> SwiGLU MLP; returns (new residual, mlp output)."""
-        x, h = self._add_rms(x, self._reduce(o @ L["wo"].t()), L["ffn_norm"])
-        return x, self._reduce(self._swiglu(h @ L["wgu"].t()) @ L["wdown"].t())
+        x, h = self._add_rms(x, self._reduce(self._mm(o, L["wo"])), L["ffn_norm"])
+        return x, self._reduce(self._mm(self._swiglu(self._mm(h, L["wgu"])), L["wdown"]))
 
     # ------------------------------------------------------------------------------------------
     # forward passes
@@ -408,7 +421,7 @@ class ServingLlama:
                 h = self._rms(x, L["attn_norm"])
             else:
                 x, h = self._add_rms(x, delta, L["attn_norm"])
-            qkv = h @ L["wqkv"].t()
+            qkv = self._mm(h, L["wqkv"])
             sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH)
             o = sops.paged_decode(qkv, self.k_cache[li], self.v_cache[li], block_tables, ctx_lens, H, KVH, ws=ws)
             x, delta = self._mlp_and_attn_out(L, x, o)

@@ -455,3 +455,22 @@ def test_gpu_engine_matches_cpu_and_graphs(gpu, tmp_path):
         for p, o in zip(prompts, out_g):
             ref = hf(torch.tensor([p])).logits[0, -1]
             assert ref[o[0]] >= ref.max() - 0.02 * (ref.max() - ref.min())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K", [(1024, 4096), (4100, 14336), (257, 3584)])
+def test_gemv_matches_fp32(gpu, M, N, K):
+    """Decode-projection GEMV kernel vs an fp32 matmul (row counts not divisible by 4, a K that
+    is not a multiple of the 4-step unroll, x with a padded row stride)."""
+    from dstack_amd.ops import _ext
+
+    C = _ext.require()
+    g = torch.Generator(device=gpu).manual_seed(M * 7 + N)
+    xs = torch.randn(M, K + 64, device=gpu, generator=g).to(torch.bfloat16)
+    x = xs[:, :K]
+    w = (torch.randn(N, K, device=gpu, generator=g) * 0.02).to(torch.bfloat16)
+    y = C.gemv(x, w)
+    ref = x.float() @ w.float().t()
+    err = ((y.float() - ref).norm() / ref.norm()).item()
+    assert y.shape == (M, N) and err < 5e-3, err
