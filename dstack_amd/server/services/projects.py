@@ -2,6 +2,7 @@
 
 from __future__ import annotations
 
+import json
 import uuid
 from typing import List, Optional
 
@@ -20,7 +21,8 @@ def project_model_to_project(p: ProjectModel, include_backends: bool = True) -> 
     members = [Member(user=user_model_to_user(m.user), project_role=ProjectRole(m.project_role)) for m in p.members]
     backends = []
     if include_backends:
-        backends = [BackendInfo(name=BackendType(b.type)) for b in p.backends]
+        # settings only: credentials live in the encrypted auth column and are never returned
+        backends = [BackendInfo(name=BackendType(b.type), config=json.loads(b.config or "{}")) for b in p.backends]
     return Project(project_id=p.id, project_name=p.name, owner=user_model_to_user(p.owner), created_at=p.created_at,
                    backends=backends, members=members)
 

@@ -229,6 +229,10 @@ def test_unknown_project(client, path):
 def test_web_ui_served(client):
     r = client.get("/")
     assert r.status_code == 200 and "dstack-amd" in r.text and "/api/runs/list" in r.text
+    # management views over the same API: instances, members editor, backends from YAML, metrics charts
+    for needle in ("/api/instances/list", "set_members", "backends/${x}", "create_yaml", "metrics/job/", "prev_run_id",
+                   "fleets/delete_instances", "users/refresh_token"):
+        assert needle in r.text, needle
 
 
 def test_prometheus_metrics(client):
