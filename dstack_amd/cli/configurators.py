@@ -71,37 +71,41 @@ def load_profile(repo_dir: str, name: Optional[str]) -> Optional[Profile]:
 
 
 def apply_profile_args(args, profile: Profile):
+    """CLI profile flags onto ``profile``; the changed fields are re-validated through the model
+    (``1h`` → seconds, backend names → enum, retry mapping → ``ProfileRetry``)."""
+    upd = {}
     if args.max_price is not None:
-        profile.max_price = args.max_price
+        upd["max_price"] = args.max_price
     if args.max_duration is not None:
-        profile.max_duration = args.max_duration
+        upd["max_duration"] = args.max_duration
     if args.backends:
-        profile.backends = args.backends
+        upd["backends"] = args.backends
     if args.regions:
-        profile.regions = args.regions
+        upd["regions"] = args.regions
     if args.instance_types:
-        profile.instance_types = args.instance_types
+        upd["instance_types"] = args.instance_types
     if args.pool_name:
-        profile.pool_name = args.pool_name
+        upd["pool_name"] = args.pool_name
     if args.creation_policy_reuse:
-        profile.creation_policy = CreationPolicy.REUSE
+        upd["creation_policy"] = CreationPolicy.REUSE
     if args.dont_destroy:
-        profile.termination_policy = TerminationPolicy.DONT_DESTROY
+        upd["termination_policy"] = TerminationPolicy.DONT_DESTROY
     if args.idle_duration is not None:
-        profile.idle_duration = args.idle_duration
+        upd["idle_duration"] = args.idle_duration
     if args.instance_name:
-        profile.instance_name = args.instance_name
-        profile.creation_policy = CreationPolicy.REUSE
+        upd["instance_name"] = args.instance_name
+        upd["creation_policy"] = CreationPolicy.REUSE
     if args.spot_policy is not None:
-        profile.spot_policy = args.spot_policy
+        upd["spot_policy"] = args.spot_policy
+    events = ["no-capacity", "interruption", "error"]
     if args.retry_policy is not None:
-        if args.retry_policy:
-            profile.retry = {"on_events": ["no-capacity", "interruption", "error"],
-                             "duration": args.retry_duration}
-        else:
-            profile.retry = False
+        upd["retry"] = {"on_events": events, "duration": args.retry_duration} if args.retry_policy else False
     elif args.retry_duration:
-        profile.retry = {"on_events": ["no-capacity", "interruption", "error"], "duration": args.retry_duration}
+        upd["retry"] = {"on_events": events, "duration": args.retry_duration}
+    if upd:
+        merged = type(profile).model_validate({**profile.model_dump(), **upd})
+        for k in upd:
+            setattr(profile, k, getattr(merged, k))
 
 
 # ---- repo selection (cli/services/repos.py) ---------------------------------------------------
@@ -158,6 +162,75 @@ def find_default_configuration(cwd: str) -> Optional[str]:
     return None
 
 
+# ---- run configuration overrides --------------------------------------------------------------
+def apply_env_args(conf, env_args: List[str]) -> None:
+    """``-e KEY=VALUE`` sets, ``-e KEY`` copies the local value (error if unset); ``env: [KEY]``
+    entries of the configuration without a value are filled from the local environment too."""
+    if env_args:
+        env = Env(conf.env)
+        for e in env_args:
+            if "=" in e:
+                k, v = e.split("=", 1)
+                env[k] = v
+            elif e in os.environ:
+                env[e] = os.environ[e]
+            else:
+                raise ConfigurationError(f"{e} is not set in the local environment")
+        conf.env = env
+    try:
+        conf.env = Env(conf.env).resolve(os.environ)
+    except (KeyError, ValueError) as e:
+        raise ConfigurationError(f"Environment variable not set locally: {e}") from e
+
+
+def merge_ports(conf_ports, arg_ports: List[PortMapping]) -> List[PortMapping]:
+    """``-p`` mappings replace the configuration's mapping of the same container port; two ``-p``
+    for one container port, or one local port used twice, is an error."""
+    by_container: Dict[int, PortMapping] = {}
+    for p in arg_ports:
+        if p.container_port in by_container:
+            raise ConfigurationError(f"Container port {p.container_port} is mapped more than once")
+        by_container[p.container_port] = p
+    merged = {p.container_port: p for p in conf_ports}
+    merged.update(by_container)
+    local = [p.local_port for p in merged.values() if p.local_port is not None]
+    dup = {x for x in local if local.count(x) > 1}
+    if dup:
+        raise ConfigurationError(f"Local port(s) {sorted(dup)} are mapped more than once")
+    return list(merged.values())
+
+
+def interpolate_registry_auth(conf) -> None:
+    """``registry_auth`` may reference the run's env: ``password: ${{ env.REGISTRY_TOKEN }}``."""
+    auth = getattr(conf, "registry_auth", None)
+    if auth is None:
+        return
+    from dstack_amd.utils.interpolator import InterpolatorError, VariablesInterpolator
+
+    it = VariablesInterpolator({"env": {k: str(v) for k, v in dict(Env(conf.env)).items()}}, skip=["secrets"])
+    try:
+        conf.registry_auth = type(auth)(username=it.interpolate_or_error(auth.username),
+                                        password=it.interpolate_or_error(auth.password))
+    except InterpolatorError as e:
+        raise ConfigurationError(f"registry_auth: {e}") from e
+
+
+def validate_gpu_vendor_and_image(conf) -> None:
+    """Infer ``resources.gpu.vendor`` from the names when they agree on one vendor (done by the
+    GPU spec model) and require ``image`` for a non-AMD GPU: the default image here is the ROCm
+    base image, so only AMD GPUs can run without one (the reference's rule is the mirror image: a
+    CUDA default image, ``image`` required for AMD)."""
+    gpu = conf.resources.gpu if conf.resources is not None else None
+    if gpu is None or getattr(conf, "image", None):
+        return
+    if gpu.count.max == 0:
+        return
+    vendor = gpu.vendor.value if gpu.vendor is not None else None
+    if vendor is not None and vendor != "amd":
+        raise ConfigurationError(f"`image` is required if `resources.gpu.vendor` is `{vendor}` "
+                                 "(the default image is ROCm-only)")
+
+
 # ---- run configurator -------------------------------------------------------------------------
 class RunConfigurator:
     TYPES = ("task", "service", "dev-environment")
@@ -174,30 +247,23 @@ class RunConfigurator:
         g.add_argument("-p", "--port", action="append", default=[], dest="ports", metavar="[LOCAL:]CONTAINER")
         register_profile_args(parser)
 
-    def apply(self, client: Client, conf, conf_path: str, args) -> int:
-        if args.env:
-            env = Env(conf.env)
-            for e in args.env:
-                if "=" in e:
-                    k, v = e.split("=", 1)
-                    env[k] = v
-                elif e in os.environ:
-                    env[e] = os.environ[e]
-                else:
-                    raise CLIError(f"{e} is not set in the local environment")
-            conf.env = env
-        try:  # `env: [HF_TOKEN]` takes the value from the local environment
-            conf.env = Env(conf.env).resolve(os.environ)
-        except (KeyError, ValueError) as e:
-            raise CLIError(f"Environment variable not set locally: {e}") from e
-        if args.gpu:
-            conf.resources.gpu = args.gpu
-            conf.resources = type(conf.resources).model_validate(conf.resources.model_dump())
-        if args.disk:
-            conf.resources.disk = args.disk
-            conf.resources = type(conf.resources).model_validate(conf.resources.model_dump())
+    @staticmethod
+    def apply_args(conf, args) -> None:
+        """CLI overrides onto the configuration (reference: ``BaseRunConfigurator.apply_args``,
+        ``cli/services/configurators/run.py``): ``-e`` adds/overrides env vars, ``-p`` replaces the
+        mapping of the same container port, ``--gpu``/``--disk`` replace the requirement; then
+        ``${{ env.X }}`` in ``registry_auth`` is resolved and the GPU vendor / image pair checked."""
+        apply_env_args(conf, args.env)
+        res = {k: v for k, v in (("gpu", args.gpu), ("disk", args.disk)) if v}
+        if res:
+            conf.resources = type(conf.resources).model_validate({**conf.resources.model_dump(), **res})
         if args.ports and hasattr(conf, "ports"):
-            conf.ports = list(conf.ports) + [PortMapping.parse(p) for p in args.ports]
+            conf.ports = merge_ports(conf.ports, [PortMapping.parse(p) for p in args.ports])
+        interpolate_registry_auth(conf)
+        validate_gpu_vendor_and_image(conf)
+
+    def apply(self, client: Client, conf, conf_path: str, args) -> int:
+        self.apply_args(conf, args)
         repo = get_repo(args, os.path.dirname(os.path.abspath(conf_path)))
         profile = load_profile(repo.repo_dir or os.getcwd(), args.profile) or Profile(name="default")
         apply_profile_args(args, profile)
@@ -311,11 +377,18 @@ class FleetConfigurator:
 
     @staticmethod
     def register_args(parser):
-        pass
+        parser.add_argument_group("Fleet Options").add_argument(
+            "-e", "--env", action="append", default=[], metavar="KEY[=VALUE]",
+            help="Environment variable for the fleet's hosts (repeatable)")
+
+    @staticmethod
+    def apply_args(conf, args) -> None:
+        apply_env_args(conf, getattr(args, "env", None) or [])
 
     def apply(self, client: Client, conf, conf_path: str, args) -> int:
         from dstack_amd.core.models.fleets import FleetSpec
 
+        self.apply_args(conf, args)
         if conf.name is None:
             conf.name = Path(conf_path).stem.replace(".dstack", "").replace("_", "-") or "fleet"
         _resolve_ssh_keys(conf)

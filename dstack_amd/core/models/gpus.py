@@ -61,10 +61,20 @@ def gpu_info(name: str) -> Optional[GPUInfo]:
     return GPUS.get(name) or GPUS.get(name.upper())
 
 
+# NVIDIA model names without catalog facts: enough to tell the vendor of a ``resources.gpu`` name
+_NVIDIA_NAMES = frozenset(n.upper() for n in (
+    "B200", "GB200", "H200", "H100", "H100NVL", "H800", "GH200", "A100", "A800", "A40", "A30", "A10", "A10G",
+    "A16", "A2", "A4000", "A4500", "A5000", "A6000", "A1000", "A2000", "RTX6000", "RTX4000", "RTX5000",
+    "RTXA6000", "RTXA5000", "RTXA4000", "L40", "L40S", "L4", "L20", "T4", "V100", "P100", "P40", "P4", "K80",
+    "RTX3090", "RTX4090", "RTX3080", "RTX4080"))
+
+
 def vendor_of(name: str) -> Optional[AcceleratorVendor]:
     info = gpu_info(name)
     if info:
         return info.vendor
+    if name.upper().replace("-", "") in _NVIDIA_NAMES:
+        return _NV
     if re.match(r"^MI\d", name, re.I):
         return _AMD
     if re.match(r"^(v\d|tpu)", name, re.I):

@@ -49,7 +49,7 @@ template <bool CAUSAL, int NW = 4, bool PF = true>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
                                                         float* __restrict__ lse, int B, int S,
-                                                        int H, int KVH, float scale_log2) {
+                                                        int H, int KVH, float scale_log2, float thr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int QB = 32 * NW;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
@@ -141,7 +141,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[t][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
-      const float mn = fmaxf(m, mx);
+      // deferred max: keep the running max until a tile exceeds it by more than thr (log2 units),
+      // so P stays <= 2^thr and O / lsum are rescaled only on those tiles (thr = 0: exact max)
+      const float mn = (mx > m + thr) ? mx : m;
       const float alpha = fexp2(m - mn);
       m = mn;
       float ps = 0.f;
@@ -687,6 +689,12 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
   if (!fa_shape_ok(S, H, KVH, D)) return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
   const size_t lds = 4 * TILE_BYTES;
+  // deferred-max threshold (log2 units; 0 = rescale on every new max): 8 takes the S=8192 causal
+  // forward from 0.700 to 0.660 ms, same fp32-reference error (tools/gpu_sessions/run_r2r.sh)
+  static const float thr = [] {
+    const char* v = getenv("DSTACK_AMD_FA_RESCALE_THR");
+    return v ? (float)atof(v) : 8.f;
+  }();
   // 8 waves (one 256-row workgroup per CU) by default: 0.710 vs 0.720 ms at S=8192, three
   // interleaved same-box runs (tools/gpu_sessions/run_r1s.sh); DSTACK_AMD_FA_FWD_WAVES=4 selects the 4-wave form
   static const int waves = [] {
@@ -700,18 +708,18 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
   if (waves == 8 && S % 256 == 0) {
     const int grid = B * H * (S / 256);
     if (causal && pf)
-      fa_fwd_kernel<true, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+      fa_fwd_kernel<true, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2, thr);
     else if (causal)
-      fa_fwd_kernel<true, 8, false><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+      fa_fwd_kernel<true, 8, false><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2, thr);
     else
-      fa_fwd_kernel<false, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+      fa_fwd_kernel<false, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2, thr);
     return hipGetLastError();
   }
   const int grid = B * H * (S / 128);
   if (causal)
-    fa_fwd_kernel<true><<<grid, 256, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+    fa_fwd_kernel<true><<<grid, 256, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2, thr);
   else
-    fa_fwd_kernel<false><<<grid, 256, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2);
+    fa_fwd_kernel<false><<<grid, 256, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2, thr);
   return hipGetLastError();
 }
 
