@@ -1,6 +1,15 @@
 """Public Python API (reference: ``src/dstack/api/__init__.py``)."""
 
-from dstack_amd.api._public import Client, FleetCollection, RepoCollection, Run, RunCollection, VolumeCollection
+from dstack_amd.api._public import (
+    Backend,
+    BackendCollection,
+    Client,
+    FleetCollection,
+    RepoCollection,
+    Run,
+    RunCollection,
+    VolumeCollection,
+)
 from dstack_amd.api.server import APIClient
 from dstack_amd.core.errors import ClientError
 from dstack_amd.core.models.backends import BackendType
@@ -18,7 +27,7 @@ from dstack_amd.core.models.services import OpenAIChatModel, ScalingSpec as Scal
 from dstack_amd.core.services.ssh.ports import PortUsedError
 
 __all__ = [
-    "APIClient", "BackendType", "Client", "ClientError", "ComputeCapability", "DevEnvironment", "Disk",
+    "APIClient", "Backend", "BackendCollection", "BackendType", "Client", "ClientError", "ComputeCapability", "DevEnvironment", "Disk",
     "FleetCollection", "GPU", "LocalRepo", "Memory", "OpenAIChatModel", "PortUsedError", "Range", "RegistryAuth",
     "RemoteRepo", "RepoCollection", "Resources", "Run", "RunCollection", "RunStatus", "Scaling", "Service", "Task",
     "TGIChatModel", "VirtualRepo", "VolumeCollection",

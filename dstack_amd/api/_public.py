@@ -17,7 +17,7 @@ import time
 from typing import Dict, Iterator, List, Optional
 
 from dstack_amd.api.server import APIClient, client_from_env_or_config
-from dstack_amd.core.errors import ClientError, ConfigurationError
+from dstack_amd.core.errors import ClientError, ConfigurationError, ResourceNotExistsError
 from dstack_amd.core.models.configurations import AnyRunConfiguration, ServiceConfiguration
 from dstack_amd.core.models.fleets import Fleet, FleetConfiguration, FleetSpec
 from dstack_amd.core.models.profiles import Profile
@@ -212,12 +212,8 @@ class RunCollection:
         try:
             return Run(self._api, self._project, self._api.runs.get(self._project, run_name),
                        self._client.ssh_identity_file)
-        except ClientError:
+        except (ClientError, ResourceNotExistsError):
             return None
-        except Exception as e:  # noqa: BLE001
-            if "not" in str(e).lower() and "exist" in str(e).lower():
-                return None
-            raise
 
 
 class RepoCollection:
@@ -280,6 +276,42 @@ class VolumeCollection:
         self._api.volumes.delete(self._project, [name])
 
 
+class Backend:
+    """A backend configured in the project (reference: ``dstack/api/_public/backends.py``)."""
+
+    def __init__(self, api: APIClient, info):
+        self._api = api
+        self._info = info
+
+    @property
+    def name(self) -> str:
+        return self._info.name.value if hasattr(self._info.name, "value") else str(self._info.name)
+
+    @property
+    def config(self) -> dict:
+        """Settings without credentials."""
+        return dict(self._info.config)
+
+    def __repr__(self) -> str:
+        return f"<Backend '{self.name}'>"
+
+
+class BackendCollection:
+    def __init__(self, api: APIClient, project: str):
+        self._api, self._project = api, project
+
+    def list(self) -> List[Backend]:
+        return [Backend(self._api, b) for b in self._api.projects.get(self._project).backends]
+
+    def create(self, config: dict) -> Backend:
+        """``config`` is a ``projects[].backends[]`` mapping of the server config (type, creds, ...)."""
+        self._api.backends.create(self._project, config)
+        return next(b for b in self.list() if b.name == config["type"])
+
+    def delete(self, names: List[str]):
+        self._api.backends.delete(self._project, names)
+
+
 class Client:
     def __init__(self, api_client: APIClient, project_name: str, ssh_identity_file: Optional[str] = None):
         self.api = api_client
@@ -289,6 +321,7 @@ class Client:
         self.runs = RunCollection(api_client, project_name, self)
         self.fleets = FleetCollection(api_client, project_name)
         self.volumes = VolumeCollection(api_client, project_name)
+        self.backends = BackendCollection(api_client, project_name)
 
     @staticmethod
     def from_config(project_name: Optional[str] = None, server_url: Optional[str] = None,

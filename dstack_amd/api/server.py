@@ -16,7 +16,14 @@ import httpx
 from pydantic import BaseModel, TypeAdapter
 
 from dstack_amd import __version__
-from dstack_amd.core.errors import ClientError, ServerClientError, URLNotFoundError
+from dstack_amd.core.errors import (
+    ClientError,
+    ResourceExistsError,
+    ResourceNotExistsError,
+    ServerClientError,
+    ServerClientErrorCode,
+    URLNotFoundError,
+)
 from dstack_amd.core.models.fleets import Fleet, FleetPlan, FleetSpec, Instance, Pool, PoolInstances
 from dstack_amd.core.models.instances import SSHKey
 from dstack_amd.core.models.profiles import Profile
@@ -108,8 +115,11 @@ def _server_error(r: httpx.Response) -> ServerClientError:
         for d in detail:
             loc = d.get("loc")
             msgs.append(f"{'.'.join(str(x) for x in loc[1:])}: {d['msg']}" if loc else d.get("msg", ""))
-        e = ServerClientError("; ".join(msgs))
-        e.code = detail[0].get("code", "error")
+        code = detail[0].get("code", "error")
+        cls = {ServerClientErrorCode.RESOURCE_NOT_EXISTS: ResourceNotExistsError,
+               ServerClientErrorCode.RESOURCE_EXISTS: ResourceExistsError}.get(code, ServerClientError)
+        e = cls("; ".join(msgs))
+        e.code = code
         return e
     e = ServerClientError(str(detail))
     return e
@@ -171,6 +181,15 @@ class _Projects(_Group):
 class _Backends(_Group):
     def list_types(self) -> List[str]:
         return self._c.post("/api/backends/list_types")
+
+    def create(self, project_name: str, config: dict) -> dict:
+        return self._c.post(f"/api/project/{project_name}/backends/create", config)
+
+    def update(self, project_name: str, config: dict) -> dict:
+        return self._c.post(f"/api/project/{project_name}/backends/update", config)
+
+    def config_info(self, project_name: str, backend_name: str) -> dict:
+        return self._c.post(f"/api/project/{project_name}/backends/{backend_name}/config_info")
 
     def create_yaml(self, project_name: str, config_yaml: str):
         self._c.post(f"/api/project/{project_name}/backends/create_yaml", {"config_yaml": config_yaml})

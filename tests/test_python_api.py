@@ -1,0 +1,85 @@
+"""The public Python API (``dstack_amd.api``: ``Client`` and its collections, reference
+``src/dstack/api/_public/*``) against the in-process server: backends, fleets, volumes, runs
+(plan, submit, list, get, stop) and the users/projects endpoints of ``APIClient``."""
+
+from __future__ import annotations
+
+import pytest
+
+from dstack_amd.api import APIClient, Client, GPU, Resources, Task, VirtualRepo
+from dstack_amd.core.errors import ServerClientError
+
+
+@pytest.fixture
+def api(client):
+    a = APIClient("http://testserver", client.headers["Authorization"].split()[1])
+    a._http = client  # the FastAPI TestClient is an httpx.Client: same request path, no socket
+    return a
+
+
+@pytest.fixture
+def dc(api):
+    return Client(api, "main")
+
+
+def test_backends_collection(dc):
+    assert [b.name for b in dc.backends.list()] == [] or all(b.name for b in dc.backends.list())
+    b = dc.backends.create({"type": "vultr", "creds": {"type": "api_key", "api_key": "secret-key"}})
+    assert b.name == "vultr" and "creds" not in b.config
+    assert "secret-key" not in repr(dc.backends.list()) + str([x.config for x in dc.backends.list()])
+    with pytest.raises(ServerClientError):
+        dc.backends.create({"type": "vultr", "creds": {"type": "api_key", "api_key": "k2"}})  # exists
+    dc.backends.delete(["vultr"])
+    assert "vultr" not in [x.name for x in dc.backends.list()]
+
+
+def test_fleet_and_volume_collections(dc):
+    from dstack_amd.core.models.fleets import FleetConfiguration
+    from dstack_amd.core.models.volumes import VolumeConfiguration
+
+    key = {"public": "ssh-ed25519 AAAA", "private": "-----BEGIN OPENSSH PRIVATE KEY-----\nx\n"
+                                                   "-----END OPENSSH PRIVATE KEY-----\n"}
+    conf = FleetConfiguration.model_validate({"type": "fleet", "name": "onprem", "ssh_config": {
+        "user": "ubuntu", "ssh_key": key, "hosts": ["10.0.0.1", "10.0.0.2"]}})
+    fleet = dc.fleets.apply_configuration(conf)
+    assert fleet.name == "onprem" and len(fleet.instances) == 2
+    assert [f.name for f in dc.fleets.list()] == ["onprem"]
+    assert dc.fleets.get("onprem").id == fleet.id
+    dc.fleets.delete("onprem")
+
+    vol = dc.volumes.create(VolumeConfiguration.model_validate(
+        {"type": "volume", "name": "data", "backend": "local", "region": "local", "size": "100GB"}))
+    assert vol.name == "data" and [v.name for v in dc.volumes.list()] == ["data"]
+    assert dc.volumes.get("data").id == vol.id
+    dc.volumes.delete("data")
+
+
+def test_runs_plan_submit_list_stop(dc):
+    task = Task(commands=["echo hi"], resources=Resources(gpu=GPU(name=["MI355X"], count=8)))
+    plan = dc.runs.get_plan(task, VirtualRepo(), run_name="api-run")
+    assert plan.run_spec.run_name == "api-run"
+    assert plan.run_spec.configuration.resources.gpu.vendor.value == "amd"
+    run = dc.runs.exec_plan(plan, VirtualRepo())
+    assert run.name == "api-run" and run.status.value == "submitted"
+    assert [r.name for r in dc.runs.list()] == ["api-run"]
+    got = dc.runs.get("api-run")
+    assert got is not None and got.model.id == run.model.id
+    assert dc.runs.get("nope") is None
+    got.stop()
+    assert dc.runs.get("api-run").status.value in ("terminating", "terminated", "done", "aborted")
+
+
+def test_users_and_projects_via_api_client(api):
+    me = api.users.get_my_user()
+    assert me.username == "admin" and me.global_role.value == "admin"
+    u = api.users.create("alice", global_role="user")
+    assert u.username == "alice"
+    p = api.projects.create("team")
+    assert p.project_name == "team"
+    p = api.projects.set_members("team", [{"username": "alice", "project_role": "manager"},
+                                          {"username": "admin", "project_role": "admin"}])
+    assert {m.user.username: m.project_role.value for m in p.members} == {"alice": "manager", "admin": "admin"}
+    api.projects.delete(["team"])
+    assert "team" not in [x.project_name for x in api.projects.list()]
+    api.users.delete(["alice"])
+    assert "alice" not in [x.username for x in api.users.list()]
