@@ -132,7 +132,7 @@ def _task_body(run: RunModel, job: JobModel, s: Optional[Session] = None) -> dic
         if isinstance(mp, VolumeMountPoint):
             volume_mounts.append({"name": mp.name if isinstance(mp.name, str) else mp.name[0], "path": mp.path})
         elif isinstance(mp, InstanceMountPoint):
-            instance_mounts.append({"instance_path": mp.instance_path, "path": mp.path})
+            instance_mounts.append({"instance_path": mp.instance_path, "path": mp.path, "optional": mp.optional})
     ports = [a.port for a in (spec.app_specs or [])]
     if isinstance(conf, ServiceConfiguration):
         ports.append(conf.port.container_port)

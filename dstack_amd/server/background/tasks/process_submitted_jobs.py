@@ -87,14 +87,17 @@ def _process_job(s: Session, job_id):
     if _assign_pool_instance(s, run, job, spec, profile, fleet, multinode, master_jpd, volumes):
         scheduler.wake(scheduler.RUNNING_JOBS, scheduler.RUNS)
         return
-    if profile.creation_policy == CreationPolicy.REUSE or (fleet is not None and not _fleet_autocreated(fleet)):
+    if profile.creation_policy == CreationPolicy.REUSE:
         _no_capacity(job, "No idle instance matches the requirements (creation_policy: reuse)")
+        return
+    if fleet is not None and not _fleet_can_grow(fleet):
+        _no_capacity(job, f"No idle instance in fleet {fleet.name} matches the requirements")
         return
     # ---- 2) provision a new instance ----
     offers = offers_services.get_offers_by_requirements(
         s, run.project, profile, spec.requirements, exclude_not_available=True, multinode=multinode,
         master_job_provisioning_data=master_jpd, privileged=spec.privileged,
-        instance_mounts=any("instance_path" in v for v in (spec.volumes or [])),
+        instance_mounts=_has_required_instance_mounts(spec),
     )
     offers = [(c, o) for c, o in offers if o.backend != BackendType.REMOTE]
     offers = job_volumes.filter_offers_by_volumes(offers, volumes)
@@ -121,11 +124,30 @@ def _master_job(run: RunModel, job: JobModel) -> Optional[JobModel]:
     return max(cands, key=lambda j: j.submission_num) if cands else None
 
 
-def _fleet_autocreated(fleet: FleetModel) -> bool:
+def _has_required_instance_mounts(spec) -> bool:
+    """Non-optional instance mounts need a VM backend (a host path to bind); optional ones do not
+    restrict the offers (reference: ``check_run_spec_has_instance_mounts``)."""
+    from dstack_amd.core.models.volumes import InstanceMountPoint
+
+    return any(isinstance(mp, InstanceMountPoint) and not mp.optional for mp in spec.mount_points())
+
+
+def _fleet_can_grow(fleet: FleetModel) -> bool:
+    """A run bound to a fleet gets a new instance in it when the fleet is autocreated, or a cloud
+    fleet below its ``nodes.max`` (SSH fleets have exactly their hosts)."""
     try:
-        return bool(json.loads(fleet.spec).get("autocreated"))
+        spec = json.loads(fleet.spec)
     except ValueError:
         return False
+    if spec.get("autocreated"):
+        return True
+    conf = spec.get("configuration") or {}
+    if conf.get("ssh_config"):
+        return False
+    nodes = conf.get("nodes") or {}
+    nmax = nodes.get("max") if isinstance(nodes, dict) else nodes
+    active = [i for i in fleet.instances if not i.deleted and i.status != InstanceStatus.TERMINATED.value]
+    return nmax is None or len(active) < int(nmax)
 
 
 def _no_capacity(job: JobModel, msg: str):

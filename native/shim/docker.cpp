@@ -153,8 +153,11 @@ class DockerDriver : public TaskDriver {
     Json binds = Json::array();
     binds.push_back(o_.runner_binary + ":/usr/local/bin/dstack-runner:ro");
     if (!o_.probe_binary.empty()) binds.push_back(o_.probe_binary + ":/usr/local/bin/dstack-probe:ro");
-    for (auto& m : t.config.instance_mounts.items())
+    for (auto& m : t.config.instance_mounts.items()) {
+      // optional mounts are skipped when the host path does not exist (e.g. a cache dir)
+      if (m["optional"].as_bool() && access(m["instance_path"].str().c_str(), F_OK) != 0) continue;
       binds.push_back(m["instance_path"].str() + ":" + m["path"].str());
+    }
     for (auto& m : t.config.volume_mounts.items()) {
       auto it = vol_paths.find(m["name"].str());
       std::string host = it != vol_paths.end() ? it->second : o_.volumes_root + "/" + m["name"].str();

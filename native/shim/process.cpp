@@ -96,6 +96,7 @@ class ProcessDriver : public TaskDriver {
     // instance mounts: expose host paths inside the task dir (symlinks) for parity with docker
     for (auto& m : t.config.instance_mounts.items()) {
       std::string ip = m["instance_path"].str(), p = m["path"].str();
+      if (m["optional"].as_bool() && access(ip.c_str(), F_OK) != 0) continue;
       if (!ip.empty() && !p.empty()) {
         std::string link = dir + "/mounts" + p;
         mkdirs(link.substr(0, link.rfind('/')));
