@@ -20,6 +20,7 @@ from sqlalchemy.orm import Session
 
 from dstack_amd.core.backends.base import DSTACK_RUNNER_HTTP_PORT
 from dstack_amd.core.errors import RunnerError, ServerClientError, SSHError
+from dstack_amd.core.models.common import NetworkMode
 from dstack_amd.core.models.configurations import ServiceConfiguration
 from dstack_amd.core.models.instances import InstanceStatus
 from dstack_amd.core.models.runs import (
@@ -206,6 +207,7 @@ def _process_pulling(s: Session, run: RunModel, job: JobModel):
                 task = shim.get_task(str(job.id))
             except Exception as e:  # noqa: BLE001
                 logger.info("%s: shim get_task failed: %s", job.job_name, e)
+                _runner_unreachable(job, f"shim: {e}")  # host gone while pulling: interrupted after a grace
                 return
             if task is None:
                 job.status = JobStatus.PROVISIONING.value  # shim lost the task (restart): resubmit
@@ -225,11 +227,14 @@ def _process_pulling(s: Session, run: RunModel, job: JobModel):
             return
         if task["status"] != "running":
             return
-        jobs_services.mark_timing(job, "container_running")
+        job.remove_at = None
         jrd = jobs_services.job_jrd(job)
         ports = {int(p["container"]): int(p["host"]) for p in task.get("ports") or []}
         if task.get("runner_port"):
             ports[DSTACK_RUNNER_HTTP_PORT] = int(task["runner_port"])
+        if jrd is not None and jrd.network_mode == NetworkMode.BRIDGE and DSTACK_RUNNER_HTTP_PORT not in ports:
+            return  # bridge network: the runner is reachable only through its published port; not mapped yet
+        jobs_services.mark_timing(job, "container_running")
         if jrd is not None:
             jrd.ports = ports or None
             if task.get("gpus") is not None and not jrd.gpu_indices:

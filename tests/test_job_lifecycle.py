@@ -47,13 +47,15 @@ _ips = itertools.count(11)
 class FakeShim:
     """dstack-shim task API: submit_task / get_task / terminate_task / remove_task."""
 
-    def __init__(self, host: str, fail_create: Optional[str] = None):
+    def __init__(self, host: str, fail_create: Optional[str] = None, ports_ready: bool = True):
         self.host = host
         self.tasks: Dict[str, dict] = {}
         self.submitted: List[dict] = []
         self.terminated: List[tuple] = []
         self.removed: List[str] = []
         self.fail_create = fail_create
+        self.ports_ready = ports_ready  # bridge network: docker has published the container ports
+        self.down = False  # the host stopped answering
 
     def healthcheck(self):
         return {"service": "dstack-shim"}
@@ -61,14 +63,30 @@ class FakeShim:
     def submit_task(self, body: dict):
         self.submitted.append(body)
         task = {"id": body["id"], "status": "running", "ports": [], "runner_port": None,
-                "gpus": body.get("gpu_indices")}
+                "gpus": body.get("gpu_indices"), "network_mode": body.get("network_mode")}
+        self._publish(task, body.get("ports") or [])
         if self.fail_create:
             task.update(status="terminated", termination_reason="creating_container_error",
                         termination_message=self.fail_create)
         self.tasks[body["id"]] = task
 
+    def _publish(self, task: dict, ports: List[int]):
+        """Like the real shim: host network -> the runner on its own port; bridge -> every
+        container port (runner 10999, sshd 10022, the app's) published on a host port."""
+        if task["network_mode"] != "bridge":
+            task.update(runner_port=10999, ports=[{"container": 10999, "host": 10999}])
+        elif self.ports_ready:
+            cports = [10999, 10022] + list(ports)
+            task["ports"] = [{"container": c, "host": 32000 + i} for i, c in enumerate(cports)]
+            task["runner_port"] = 32000
+
     def get_task(self, task_id: str):
-        return self.tasks.get(task_id)
+        if self.down:
+            raise ConnectionError("ssh: connect to host: Connection timed out")
+        task = self.tasks.get(task_id)
+        if task is not None and not task["ports"] and task["status"] == "running":
+            self._publish(task, [])
+        return task
 
     def terminate_task(self, task_id, reason, message, timeout=10):
         self.terminated.append((task_id, reason))
@@ -463,3 +481,56 @@ def test_blocks_share_one_host_disjoint_gpus(db, blocks, gpus_per_job, jobs):
             picked.append(tuple(jobs_services.job_jrd(job).gpu_indices))
     flat = [g for p in picked for g in p]
     assert len(flat) == len(set(flat)) == jobs * gpus_per_job
+
+
+def test_bridge_job_waits_for_published_runner_port(db):
+    """Blocks put a job on a bridge network: the runner is reachable only through the host port
+    docker publishes for it, so the job stays PULLING (runner not contacted) until the shim
+    reports that mapping (reference: ``test_pulling_shim_port_mapping_not_ready``)."""
+    agents = Agents()
+    with session_scope() as s:
+        iid, ip = _remote_instance(s, "node-b", blocks=2)
+        rid = _submit(s, {"type": "task", "commands": ["true"], "resources": {"gpu": "MI355X:4"}})
+    agents.shims[ip] = FakeShim(ip, ports_ready=False)
+    with agents.patch():
+        _tick(rid)
+        with session_scope() as s:
+            (job,) = _jobs(s, rid)
+            assert job.status == JobStatus.PULLING.value
+        assert ip not in agents.runners  # runner never contacted without its port
+        agents.shims[ip].ports_ready = True
+        _tick(rid)
+        with session_scope() as s:
+            (job,) = _jobs(s, rid)
+            assert job.status == JobStatus.RUNNING.value
+            from dstack_amd.server.services import jobs as jobs_services
+
+            assert jobs_services.job_jrd(job).ports[10999] == 32000
+
+
+def test_host_lost_while_pulling_interrupts_job(db):
+    """The shim stops answering while the job is PULLING: after the unreachable grace the job is
+    interrupted with no capacity (reference: ``test_pulling_shim_failed``), so retry can resubmit."""
+    from datetime import timedelta
+
+    from dstack_amd.server import settings
+
+    agents = Agents()
+    with session_scope() as s:
+        iid, ip = _remote_instance(s, "node-c", blocks=2)
+        rid = _submit(s, {"type": "task", "commands": ["true"], "resources": {"gpu": "MI355X:4"}})
+    agents.shims[ip] = FakeShim(ip, ports_ready=False)
+    with agents.patch():
+        _tick(rid)
+        agents.shims[ip].down = True
+        _tick(rid)
+        with session_scope() as s:
+            (job,) = _jobs(s, rid)
+            assert job.status == JobStatus.PULLING.value  # inside the grace period
+        later = get_current_datetime() + timedelta(seconds=settings.DEFAULT_RUNNER_TIMEOUT)
+        with mock.patch.object(prj, "get_current_datetime", return_value=later):
+            _tick(rid)
+        with session_scope() as s:
+            (job,) = _jobs(s, rid)
+            assert job.status in (JobStatus.TERMINATING.value, JobStatus.FAILED.value)
+            assert job.termination_reason == JobTerminationReason.INTERRUPTED_BY_NO_CAPACITY.value
