@@ -1,0 +1,165 @@
+"""Run status aggregation in ``process_runs`` (reference: ``src/tests/_internal/server/background/
+tasks/test_process_runs.py``): the run status from its replicas' latest job submissions (FAILED >
+RUNNING > PROVISIONING > SUBMITTED > DONE), retry to PENDING on no-capacity / interruption, the
+retry-duration limit, PENDING -> SUBMITTED after the resubmission delay, and multi-replica services
+where one replica's failure is retried without leaving RUNNING."""
+
+from __future__ import annotations
+
+from datetime import timedelta
+from typing import List
+from unittest import mock
+
+import pytest
+
+from dstack_amd.core.models.runs import JobStatus, JobTerminationReason, RunSpec, RunStatus, RunTerminationReason
+from dstack_amd.server.background.tasks import process_runs as pr
+from dstack_amd.server.db import session_scope
+from dstack_amd.server.models import JobModel, ProjectModel, RunModel, UserModel
+from dstack_amd.server.services import runs as runs_services
+from dstack_amd.utils.common import get_current_datetime
+
+RETRY = {"on_events": ["no-capacity", "interruption", "error"], "duration": "1h"}
+JPD = ('{"backend": "aws", "instance_type": {"name": "i", "resources": {"cpus": 4, "memory_mib": 8192, '
+       '"gpus": [], "spot": false}}, "instance_id": "i-1", "hostname": "1.1.1.1", "region": "us", "price": 1.0, '
+       '"username": "ubuntu", "ssh_port": 22, "dockerized": true}')
+
+
+def _run(conf: dict, status: RunStatus = RunStatus.SUBMITTED, retry=None) -> str:
+    with session_scope() as s:
+        project = s.query(ProjectModel).filter_by(name="main").one()
+        user = s.query(UserModel).filter_by(name="admin").one()
+        profile = {"name": "default"}
+        if retry is not None:
+            profile["retry"] = retry
+        spec = RunSpec.model_validate({"run_name": "rr", "repo_id": "virt", "repo_data": {"repo_type": "virtual"},
+                                       "configuration": conf, "profile": profile})
+        run_id = runs_services.submit_run(s, project, user, spec).id
+        s.get(RunModel, run_id).status = status.value
+        return run_id
+
+
+def _task(**kw):
+    return {"type": "task", "commands": ["true"], **kw}
+
+
+def _service(replicas=2):
+    return {"type": "service", "commands": ["serve"], "port": 8000, "replicas": replicas}
+
+
+def _set_jobs(run_id, *states):
+    """states[i] = (JobStatus, termination reason or None, provisioned?) for replica i's job."""
+    with session_scope() as s:
+        jobs: List[JobModel] = sorted(s.query(JobModel).filter_by(run_id=run_id), key=lambda j: j.replica_num)
+        for j, st in zip(jobs, states):
+            status, reason, provisioned = (st + (None, None))[:3] if isinstance(st, tuple) else (st, None, None)
+            j.status = status.value
+            j.termination_reason = reason.value if reason else None
+            if provisioned or status in (JobStatus.PROVISIONING, JobStatus.PULLING, JobStatus.RUNNING):
+                j.job_provisioning_data = JPD
+            if status.is_finished():
+                j.finished_at = get_current_datetime()
+
+
+def _process(run_id, at=None):
+    with mock.patch.object(pr, "get_current_datetime", return_value=at or get_current_datetime()):
+        with session_scope() as s:
+            pr._process_run(s, run_id)
+    with session_scope() as s:
+        run = s.get(RunModel, run_id)
+        return RunStatus(run.status), run.termination_reason, sorted(
+            (j.replica_num, j.submission_num, j.status) for j in run.jobs)
+
+
+@pytest.mark.parametrize("job_status,run_status", [
+    (JobStatus.SUBMITTED, RunStatus.SUBMITTED),
+    (JobStatus.PROVISIONING, RunStatus.PROVISIONING),
+    (JobStatus.PULLING, RunStatus.PROVISIONING),  # keep provisioning while the image pulls
+    (JobStatus.RUNNING, RunStatus.RUNNING),
+])
+def test_single_job_status_maps_to_run(db, job_status, run_status):
+    rid = _run(_task())
+    _set_jobs(rid, job_status)
+    assert _process(rid)[0] == run_status
+
+
+def test_running_to_done(db):
+    rid = _run(_task(), RunStatus.RUNNING)
+    _set_jobs(rid, (JobStatus.DONE, JobTerminationReason.DONE_BY_RUNNER, True))
+    st, reason, _ = _process(rid)
+    assert st == RunStatus.TERMINATING and reason == RunTerminationReason.ALL_JOBS_DONE.value
+
+
+def test_failed_job_without_retry_terminates_run(db):
+    rid = _run(_task(), RunStatus.RUNNING)
+    _set_jobs(rid, (JobStatus.FAILED, JobTerminationReason.CONTAINER_EXITED_WITH_ERROR, True))
+    st, reason, _ = _process(rid)
+    assert st == RunStatus.TERMINATING and reason == RunTerminationReason.JOB_FAILED.value
+
+
+def test_retry_running_to_pending_then_submitted(db):
+    rid = _run(_task(), RunStatus.RUNNING, retry=RETRY)
+    _set_jobs(rid, (JobStatus.FAILED, JobTerminationReason.INTERRUPTED_BY_NO_CAPACITY, True))
+    st, _, jobs = _process(rid)
+    assert st == RunStatus.PENDING and len(jobs) == 1
+    # resubmitted only after the retry delay
+    assert _process(rid)[0] == RunStatus.PENDING
+    st, _, jobs = _process(rid, at=get_current_datetime() + pr.RETRY_DELAY + timedelta(seconds=1))
+    assert st == RunStatus.SUBMITTED
+    assert jobs == [(0, 0, JobStatus.FAILED.value), (0, 1, JobStatus.SUBMITTED.value)]
+
+
+def test_retry_limit_exceeded(db):
+    rid = _run(_task(), RunStatus.RUNNING, retry={**RETRY, "duration": "10m"})
+    _set_jobs(rid, (JobStatus.FAILED, JobTerminationReason.INTERRUPTED_BY_NO_CAPACITY, True))
+    st, reason, _ = _process(rid, at=get_current_datetime() + timedelta(hours=1))
+    assert st == RunStatus.TERMINATING and reason == RunTerminationReason.RETRY_LIMIT_EXCEEDED.value
+
+
+def test_no_capacity_not_retried_without_event(db):
+    rid = _run(_task(), RunStatus.SUBMITTED, retry={"on_events": ["error"], "duration": "1h"})
+    _set_jobs(rid, (JobStatus.FAILED, JobTerminationReason.FAILED_TO_START_DUE_TO_NO_CAPACITY))
+    assert _process(rid)[0] == RunStatus.TERMINATING
+
+
+# ---- multi-replica services ----------------------------------------------------------------------
+@pytest.mark.parametrize("states,run_status", [
+    ((JobStatus.SUBMITTED, JobStatus.PROVISIONING), RunStatus.PROVISIONING),  # provisioning if any
+    ((JobStatus.PROVISIONING, JobStatus.RUNNING), RunStatus.RUNNING),  # running if any
+])
+def test_service_replicas_any_rule(db, states, run_status):
+    rid = _run(_service())
+    _set_jobs(rid, *states)
+    assert _process(rid)[0] == run_status
+
+
+def test_service_all_replicas_no_capacity_to_pending(db):
+    rid = _run(_service(), RunStatus.SUBMITTED, retry=RETRY)
+    _set_jobs(rid, (JobStatus.FAILED, JobTerminationReason.FAILED_TO_START_DUE_TO_NO_CAPACITY),
+              (JobStatus.FAILED, JobTerminationReason.FAILED_TO_START_DUE_TO_NO_CAPACITY))
+    assert _process(rid)[0] == RunStatus.PENDING
+
+
+def test_service_some_no_capacity_keeps_running_and_retries_replica(db):
+    rid = _run(_service(), RunStatus.RUNNING, retry=RETRY)
+    _set_jobs(rid, JobStatus.RUNNING, (JobStatus.FAILED, JobTerminationReason.FAILED_TO_START_DUE_TO_NO_CAPACITY))
+    st, _, jobs = _process(rid)
+    assert st == RunStatus.RUNNING
+    assert (1, 1, JobStatus.SUBMITTED.value) in jobs  # the failed replica got a new submission
+
+
+def test_service_some_failed_without_retry_terminates(db):
+    rid = _run(_service(), RunStatus.RUNNING)
+    _set_jobs(rid, JobStatus.RUNNING, (JobStatus.FAILED, JobTerminationReason.CONTAINER_EXITED_WITH_ERROR, True))
+    st, reason, _ = _process(rid)
+    assert st == RunStatus.TERMINATING and reason == RunTerminationReason.JOB_FAILED.value
+
+
+def test_pending_service_resubmits_every_replica(db):
+    rid = _run(_service(), RunStatus.PENDING, retry=RETRY)
+    _set_jobs(rid, (JobStatus.FAILED, JobTerminationReason.FAILED_TO_START_DUE_TO_NO_CAPACITY),
+              (JobStatus.FAILED, JobTerminationReason.FAILED_TO_START_DUE_TO_NO_CAPACITY))
+    st, _, jobs = _process(rid, at=get_current_datetime() + pr.RETRY_DELAY + timedelta(seconds=1))
+    assert st == RunStatus.SUBMITTED
+    assert [(r, n, js) for r, n, js in jobs if js == JobStatus.SUBMITTED.value] == [
+        (0, 1, JobStatus.SUBMITTED.value), (1, 1, JobStatus.SUBMITTED.value)]
