@@ -38,6 +38,10 @@ hipError_t dsa_sample(const void*, long, int, int, const float*, const int64_t*,
 bool dsa_gemm_tn_supported(int, int, int);
 bool dsa_gemv_supported(int, int);
 hipError_t dsa_gemv(const void*, long, const void*, void*, long, int, int, int, hipStream_t);
+bool dsa_quant_fp8_supported(int);
+hipError_t dsa_quant_fp8_rows(const void*, long, void*, long, float*, int, int, hipStream_t);
+bool dsa_gemv_fp8_supported(int, int);
+hipError_t dsa_gemv_fp8(const void*, long, const void*, const float*, void*, long, int, int, int, hipStream_t);
 hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 }
 
@@ -296,6 +300,42 @@ torch::Tensor gemv(torch::Tensor x, torch::Tensor w) {
   return y;
 }
 
+// FP8 (e4m3) rows: q [M, K] uint8 (view as float8_e4m3fn) and s [M] fp32, x[m] ~= q[m] * s[m]
+std::vector<torch::Tensor> quant_fp8_rows(torch::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.stride(1) == 1,
+              "quant_fp8_rows: x must be bf16 [M, K] with contiguous rows");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "quant_fp8_rows: alignment");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(dsa_quant_fp8_supported((int)K), "quant_fp8_rows: K % 8 == 0");
+  auto q = torch::empty({M, K}, x.options().dtype(torch::kUInt8));
+  auto sc = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  if (M > 0)
+    check(dsa_quant_fp8_rows(x.data_ptr(), x.stride(0), q.data_ptr(), K, sc.data_ptr<float>(), (int)M, (int)K,
+                             stream()),
+          "quant_fp8_rows");
+  return {q, sc};
+}
+
+bool gemv_fp8_supported(int64_t M, int64_t K) { return dsa_gemv_fp8_supported((int)M, (int)K); }
+
+// y [M, N] = (x [M, K] @ q[N, K]^T) * s[N] for M <= 4, q e4m3 bytes (decode, csrc/fp8.hip)
+torch::Tensor gemv_fp8(torch::Tensor x, torch::Tensor q, torch::Tensor sc) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.stride(1) == 1,
+              "gemv_fp8: x must be bf16 [M, K] with contiguous rows");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "gemv_fp8: x alignment");
+  TORCH_CHECK(q.is_cuda() && q.element_size() == 1 && q.dim() == 2 && q.is_contiguous() && q.size(1) == x.size(1),
+              "gemv_fp8: q must be contiguous 1-byte [N, K]");
+  TORCH_CHECK(sc.is_cuda() && sc.scalar_type() == torch::kFloat32 && sc.numel() == q.size(0) && sc.is_contiguous(),
+              "gemv_fp8: s must be fp32 [N]");
+  const int64_t M = x.size(0), N = q.size(0), K = x.size(1);
+  TORCH_CHECK(dsa_gemv_fp8_supported((int)M, (int)K), "gemv_fp8: M <= 4 and K % 1024 == 0");
+  auto y = torch::empty({M, N}, x.options());
+  check(dsa_gemv_fp8(x.data_ptr(), x.stride(0), q.data_ptr(), sc.data_ptr<float>(), y.data_ptr(), N, (int)M,
+                     (int)N, (int)K, stream()),
+        "gemv_fp8");
+  return y;
+}
+
 // out[P][Q] (+)= a^T b ; a = [T][P], b = [T][Q] (weight gradient dW = dY^T X)
 void gemm_tn(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool accumulate) {
   for (auto* t : {&a, &b, &out}) {
@@ -413,6 +453,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("quant_fp8_rows", &quant_fp8_rows);
+  m.def("gemv_fp8", &gemv_fp8);
+  m.def("gemv_fp8_supported", &gemv_fp8_supported);
   m.def("gemm_tn", &gemm_tn);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemv", &gemv);

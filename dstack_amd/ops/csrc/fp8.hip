@@ -1,0 +1,153 @@
+// FP8 (OCP e4m3, the gfx950 v_cvt_pk_fp8_f32 / v_cvt_pk_f32_fp8 format) serving kernels.
+//
+// Weight-only bytes dominate a decode step (a 70B model streams 140 GB of bf16 weights per step):
+// e4m3 weights with one fp32 scale per output row halve that and let hipBLASLt run the larger
+// batches on the fp8 MFMA rate.  Two kernels:
+//  * quant_rows: x [M][K] bf16 -> q [M][K] e4m3 + s [M] fp32 with s = max|x_row| / 448 (dynamic
+//    per-token activation scales; also used once per weight at load time, per output row).
+//  * gemv_fp8: y[m][n] = s_w[n] * sum_k x[m][k] * q[n][k] for M <= 4 rows — the batch-1 decode
+//    weight stream at half the bytes of csrc/gemv.hip.  One wave per output row, 16 weights (16 B)
+//    per lane per load, U loads in flight, XCD-banded rows, fp32 accumulation.
+#include "common.h"
+
+using namespace dsa;
+
+namespace {
+
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+constexpr float E4M3_MAX = 448.f;
+
+// 4 fp8 (one dword) -> 4 floats
+__device__ __forceinline__ void fp8x4_to_f32(unsigned int v, float* o) {
+  auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(v, false);  // bytes 0, 1
+  auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(v, true);   // bytes 2, 3
+  o[0] = lo[0];
+  o[1] = lo[1];
+  o[2] = hi[0];
+  o[3] = hi[1];
+}
+
+// 4 floats (already scaled into range) -> one dword of fp8, saturating at +-448
+__device__ __forceinline__ unsigned int f32x4_to_fp8(float a, float b, float c, float d) {
+  a = __builtin_amdgcn_fmed3f(a, E4M3_MAX, -E4M3_MAX);
+  b = __builtin_amdgcn_fmed3f(b, E4M3_MAX, -E4M3_MAX);
+  c = __builtin_amdgcn_fmed3f(c, E4M3_MAX, -E4M3_MAX);
+  d = __builtin_amdgcn_fmed3f(d, E4M3_MAX, -E4M3_MAX);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (unsigned int)w;
+}
+
+// one 256-thread workgroup per row; K % 8 == 0
+__global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restrict__ x, long ldx,
+                                                         unsigned char* __restrict__ q, long ldq,
+                                                         float* __restrict__ s, int K) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* xr = x + (long)row * ldx;
+  float amax = 0.f;
+  for (int k = tid * 8; k < K; k += 256 * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const us8*>(xr + k), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  }
+  amax = wave_max(amax);
+  if ((tid & 63) == 0) red[tid >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float scale = fmaxf(amax, 1e-12f) / E4M3_MAX;
+  const float inv = 1.f / scale;
+  if (tid == 0) s[row] = scale;
+  unsigned char* qr = q + (long)row * ldq;
+  for (int k = tid * 8; k < K; k += 256 * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const us8*>(xr + k), v);
+    unsigned int w0 = f32x4_to_fp8(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+    unsigned int w1 = f32x4_to_fp8(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv);
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+  }
+}
+
+template <int M, int U>
+__global__ __launch_bounds__(256) void gemv_fp8_kernel(const bf16_t* __restrict__ x, long ldx,
+                                                       const unsigned char* __restrict__ W,
+                                                       const float* __restrict__ sw, bf16_t* __restrict__ y,
+                                                       long ldy, int N, int K) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int per = nwg >> 3, rem = nwg & 7, xcd = b & 7, idx = b >> 3;
+  const int wg = (nwg >= 8) ? xcd * per + (xcd < rem ? xcd : rem) + idx : b;
+  const int row = wg * 4 + wave;
+  if (row >= N) return;  // wave-uniform
+  const unsigned char* wr = W + (long)row * K;
+  float acc[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) acc[m] = 0.f;
+  // lane l covers columns 16 l .. 16 l + 15 of every 1024-column step
+  for (int k0 = lane * 16; k0 < K; k0 += 1024 * U) {
+    u4 wv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k0 + 1024 * u < K) wv[u] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(wr + k0 + 1024 * u));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 1024 * u;
+      if (k >= K) break;
+      float w16[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fp8x4_to_f32(wv[u][j], w16 + 4 * j);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float x8[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          unpack8(*reinterpret_cast<const us8*>(x + m * ldx + k + 8 * h), x8);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[m] = fmaf(w16[8 * h + i], x8[i], acc[m]);
+        }
+      }
+    }
+  }
+  const float scale = sw[row];
+#pragma unroll
+  for (int m = 0; m < M; ++m) acc[m] = wave_sum(acc[m]);
+  if (lane < M) {
+    float v = acc[0];
+#pragma unroll
+    for (int m = 1; m < M; ++m)
+      if (lane == m) v = acc[m];
+    y[lane * ldy + row] = f2bf(v * scale);
+  }
+}
+
+}  // namespace
+
+extern "C" bool dsa_quant_fp8_supported(int K) { return K > 0 && K % 8 == 0; }
+
+extern "C" hipError_t dsa_quant_fp8_rows(const void* x, long ldx, void* q, long ldq, float* s, int M, int K,
+                                         hipStream_t st) {
+  if (!dsa_quant_fp8_supported(K) || M <= 0) return hipErrorInvalidValue;
+  quant_rows_kernel<<<M, 256, 0, st>>>((const bf16_t*)x, ldx, (unsigned char*)q, ldq, s, K);
+  return hipGetLastError();
+}
+
+extern "C" bool dsa_gemv_fp8_supported(int M, int K) { return M >= 1 && M <= 4 && K % 1024 == 0 && K > 0; }
+
+extern "C" hipError_t dsa_gemv_fp8(const void* x, long ldx, const void* W, const float* sw, void* y, long ldy,
+                                   int M, int N, int K, hipStream_t st) {
+  if (!dsa_gemv_fp8_supported(M, K) || N <= 0) return hipErrorInvalidValue;
+  const int grid = (N + 3) / 4;
+#define DSA_GEMV8(MM)                                                                                 \
+  gemv_fp8_kernel<MM, 4><<<grid, 256, 0, st>>>((const bf16_t*)x, ldx, (const unsigned char*)W, sw,   \
+                                               (bf16_t*)y, ldy, N, K)
+  switch (M) {
+    case 1: DSA_GEMV8(1); break;
+    case 2: DSA_GEMV8(2); break;
+    case 3: DSA_GEMV8(3); break;
+    default: DSA_GEMV8(4); break;
+  }
+#undef DSA_GEMV8
+  return hipGetLastError();
+}

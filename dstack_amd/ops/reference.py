@@ -64,6 +64,24 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = 
     return (p @ vf).transpose(1, 2).to(q.dtype)
 
 
+E4M3_MAX = 448.0
+
+
+def quant_fp8_rows(x: torch.Tensor):
+    """Per-row e4m3 quantization (csrc/fp8.hip ``quant_rows``): q [M, K] float8_e4m3fn, s [M] fp32
+    with s = max|x_row| / 448, x ~= q * s."""
+    xf = x.float()
+    s = xf.abs().amax(dim=1).clamp_min(1e-12) / E4M3_MAX
+    q = (xf / s[:, None]).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn)
+    return q, s
+
+
+def fp8_linear(x: torch.Tensor, q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """x @ (q * s)^T with x quantized per row first: the math of the fp8 serving GEMMs, in fp32."""
+    xq, xs = quant_fp8_rows(x)
+    return ((xq.float() * xs[:, None]) @ (q.float() * s[:, None]).t()).to(x.dtype)
+
+
 def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     return F.cross_entropy(logits.float(), target, reduction="mean")
 

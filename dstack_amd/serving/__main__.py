@@ -23,6 +23,8 @@ def main(argv=None):
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.90)
     ap.add_argument("--no-graphs", action="store_true", help="run decode steps eagerly (no hipGraph capture)")
     ap.add_argument("--seed", type=int, default=0, help="random-init seed for built-in configs")
+    ap.add_argument("--quantization", choices=["fp8"], default=None,
+                    help="fp8: e4m3 projection weights with per-channel scales, per-token activation scales")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(message)s")
     log = logging.getLogger("dstack_amd.serving")
@@ -38,7 +40,7 @@ def main(argv=None):
     t0 = time.time()
     eng = LLMEngine.from_model(args.model, max_model_len=args.max_model_len, seed=args.seed, max_batch=args.max_batch,
                                max_prefill_tokens=args.max_prefill_tokens, use_graphs=not args.no_graphs and None,
-                               gpu_memory_utilization=args.gpu_memory_utilization)
+                               gpu_memory_utilization=args.gpu_memory_utilization, quantization=args.quantization)
     eng.capture_graphs()
     m = eng.model
     log.info("model %s: %.1f GB weights, %d KV pages (%d tokens), max_model_len %d, %d graph buckets, ready in %.1fs",

@@ -117,14 +117,16 @@ class LLMEngine:
 
     @classmethod
     def from_model(cls, model: str, device=None, max_model_len: int | None = None, seed: int = 0, tp_group=None,
-                   **kw):
+                   quantization: str | None = None, **kw):
         spec = load_spec(model)
         device = device or ("cuda" if torch.cuda.is_available() else "cpu")
-        m = ServingLlama(spec, device, max_model_len=max_model_len, tp_group=tp_group)
+        m = ServingLlama(spec, device, max_model_len=max_model_len, tp_group=tp_group, quantization=quantization)
         if spec.path:
             m.load_hf()
         else:
             m.init_random(seed)
+        if quantization == "fp8":
+            m.quantize_fp8()  # before the KV cache is sized: the freed bf16 bytes become KV pages
         return cls(m, eos_token_ids=spec.eos_token_ids, **kw)
 
     # ------------------------------------------------------------------------------------------

@@ -38,6 +38,23 @@ from dstack_amd.ops import reference as ref
 from dstack_amd.ops import serving as sops
 
 
+class Fp8Weight:
+    """A linear weight stored as e4m3 bytes ``q`` [N, K] (uint8 storage, float8_e4m3fn values) with
+    one fp32 scale per output row ``s`` [N]: W ~= q * s[:, None]."""
+
+    __slots__ = ("q", "s")
+
+    def __init__(self, q: torch.Tensor, s: torch.Tensor):
+        self.q, self.s = q, s
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    def nbytes(self) -> int:
+        return self.q.numel() + self.s.numel() * 4
+
+
 @dataclass
 class RopeScaling:
     """Llama-3.1 "llama3" RoPE frequency scaling (HF ``rope_scaling``)."""
@@ -121,7 +138,11 @@ class ServingLlama:
     """Weights + paged KV cache of one Llama model on one device (or of one tensor-parallel shard:
     ``H``/``KVH``/``F``/``V`` below are then this rank's local head / FFN / vocab counts)."""
 
-    def __init__(self, spec: ModelSpec, device, dtype=None, max_model_len: int | None = None, tp_group=None):
+    def __init__(self, spec: ModelSpec, device, dtype=None, max_model_len: int | None = None, tp_group=None,
+                 quantization: str | None = None):
+        if quantization not in (None, "fp8"):
+            raise ValueError(f"unsupported quantization {quantization!r} (supported: fp8)")
+        self.quantization = quantization
         self.spec = spec
         self.cfg = cfg = spec.cfg
         self.device = torch.device(device)
@@ -286,10 +307,37 @@ class ServingLlama:
             raise ValueError(f"checkpoint {path} is missing {len(missing)} tensors, e.g. {sorted(missing)[:3]}")
         return self
 
+    # projections that fp8 quantization converts (the LM head, embedding and norms stay bf16)
+    FP8_KEYS = ("wqkv", "wo", "wgu", "wdown")
+
+    @torch.no_grad()
+    def quantize_fp8(self):
+        """Convert every layer's projections to e4m3 with per-output-row scales (dynamic per-token
+        activation scales at run time), freeing the bf16 copies: halves the weight bytes a decode
+        step streams and runs the larger GEMMs on the fp8 MFMA rate."""
+        for L in self.layers:
+            for k in self.FP8_KEYS:
+                w = L[k]
+                if isinstance(w, Fp8Weight):
+                    continue
+                if self.hip:
+                    q, sc = _ext.require().quant_fp8_rows(w)
+                else:
+                    q8, sc = ref.quant_fp8_rows(w)
+                    q = q8.view(torch.uint8)
+                L[k] = Fp8Weight(q, sc)
+                del w
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+        return self
+
     def weight_bytes(self) -> int:
         ts = [self.embed, self.norm] + ([] if self.spec.tie_embeddings else [self.lm_head])
-        ts += [t for L in self.layers for t in L.values()]
-        return sum(t.numel() * t.element_size() for t in ts)
+        n = sum(t.numel() * t.element_size() for t in ts)
+        for L in self.layers:
+            for t in L.values():
+                n += t.nbytes() if isinstance(t, Fp8Weight) else t.numel() * t.element_size()
+        return n
 
     # ------------------------------------------------------------------------------------------
     # KV cache
@@ -347,11 +395,32 @@ class ServingLlama:
         (``csrc/gemv.hip``: 6.1-6.8 TB/s on the 70B projections vs hipBLASLt's 5.5-6.2, where it
         wins; at 2-4 rows hipBLASLt is faster, profiles/bench_gemv_r2o.log); larger batches and
         prefill use hipBLASLt."""
+        if isinstance(w, Fp8Weight):
+            return self._mm_fp8(x, w)
         if self.hip and self.gemv and x.shape[0] == 1:
             C = _ext.require()
             if C.gemv_supported(x.shape[0], x.shape[1]) and x.stride(-1) == 1:
                 return C.gemv(x, w)
         return x @ w.t()
+
+    def _mm_fp8(self, x, w: Fp8Weight):
+        """``x @ (q * s)^T``: up to 4 rows on the fp8 HIP GEMV (half the weight bytes of the bf16
+        one); more rows are quantized per token (HIP) and multiplied by hipBLASLt's fp8 GEMM with
+        row-wise scales (``torch._scaled_mm``)."""
+        if not self.hip:
+            return ref.fp8_linear(x, w.q.view(torch.float8_e4m3fn), w.s)
+        C = _ext.require()
+        x = x if x.stride(-1) == 1 and x.stride(0) % 8 == 0 else x.contiguous()
+        M = x.shape[0]
+        if self.gemv and C.gemv_fp8_supported(M, x.shape[1]):
+            return C.gemv_fp8(x, w.q, w.s)
+        pad = -M % 16  # hipBLASLt's fp8 GEMM wants every dimension a multiple of 16
+        if pad:
+            x = torch.nn.functional.pad(x, (0, 0, 0, pad))
+        xq, xs = C.quant_fp8_rows(x)
+        y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), w.q.view(torch.float8_e4m3fn).t(),
+                             scale_a=xs.view(-1, 1), scale_b=w.s.view(1, -1), out_dtype=x.dtype)
+        return y[:M] if pad else y
 
     def _reduce(self, t):
         """Sum the row-parallel partial outputs of the tensor-parallel ranks (RCCL all-reduce)."""
@@ -394,7 +463,7 @@ class ServingLlama:
                 h = self._rms(x, L["attn_norm"])
             else:
                 x, h = self._add_rms(x, delta, L["attn_norm"])
-            qkv = h @ L["wqkv"].t()
+            qkv = self._mm(h, L["wqkv"]) if isinstance(L["wqkv"], Fp8Weight) else h @ L["wqkv"].t()
             sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH)
             o = torch.empty(rows, H * self.D, dtype=x.dtype, device=x.device)
             for off, n in bounds:

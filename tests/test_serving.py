@@ -474,3 +474,105 @@ def test_gemv_matches_fp32(gpu, M, N, K):
     ref = x.float() @ w.float().t()
     err = ((y.float() - ref).norm() / ref.norm()).item()
     assert y.shape == (M, N) and err < 5e-3, err
+
+
+# ------------------------------------------------------------------------------------------------
+# fp8 (e4m3) projection weights
+# ------------------------------------------------------------------------------------------------
+def test_fp8_reference_quantization_roundtrip():
+    from dstack_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    x = torch.randn(5, 256) * torch.tensor([0.01, 1.0, 30.0, 1e3, 1e-3])[:, None]
+    q, s = ref.quant_fp8_rows(x)
+    assert q.dtype == torch.float8_e4m3fn and s.shape == (5,)
+    assert (q.float().abs().amax(dim=1) == 448).all()  # every row uses the full e4m3 range
+    back = q.float() * s[:, None]
+    assert ((back - x).norm(dim=1) / x.norm(dim=1)).max() < 0.04  # 3 mantissa bits
+
+
+def test_fp8_engine_close_to_bf16_engine():
+    """The fp8 model's prefill logits track the unquantized model's (per-channel weight scales,
+    per-token activation scales), and it frees about half of the projection bytes."""
+    kw = dict(device="cpu", max_model_len=256, max_batch=4, num_pages=16)
+    base = LLMEngine.from_model("llama-tiny", **kw)
+    q8 = LLMEngine.from_model("llama-tiny", quantization="fp8", **kw)
+    assert q8.model.weight_bytes() < 0.75 * base.model.weight_bytes()
+    assert all(type(L["wgu"]).__name__ == "Fp8Weight" for L in q8.model.layers)
+    prompt = torch.tensor(list(range(1, 129)))
+    pos = torch.arange(128, dtype=torch.int32)
+    slots = torch.arange(128, dtype=torch.int32)
+    a = base.model.prefill(prompt, pos, slots, [0], [128])
+    b = q8.model.prefill(prompt, pos, slots, [0], [128])
+    cos = torch.nn.functional.cosine_similarity(a.float(), b.float(), dim=-1).item()
+    assert cos > 0.99, cos
+    sp = SamplingParams(max_tokens=8, temperature=0, ignore_eos=True)
+    out = q8.generate([[1, 2, 3, 4, 5]], sp)
+    assert len(out[0].output_ids) == 8
+
+
+def test_fp8_rejects_unknown_quantization():
+    from dstack_amd.serving.model import ServingLlama, load_spec
+
+    with pytest.raises(ValueError, match="quantization"):
+        ServingLlama(load_spec("llama-tiny"), "cpu", quantization="int3")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K", [(1, 4096), (7, 8192), (256, 4096)])
+def test_gpu_quant_fp8_rows_matches_torch(gpu, M, K):
+    """HIP per-row e4m3 quantization: scales equal max|x|/448 and the bytes decode to the same
+    values as torch's float8_e4m3fn cast (round to nearest even) up to ties."""
+    from dstack_amd.ops import _ext, reference as ref
+
+    C = _ext.require()
+    g = torch.Generator(device=gpu).manual_seed(M)
+    x = (torch.randn(M, K, device=gpu, generator=g) * torch.rand(M, 1, device=gpu, generator=g) * 10).bfloat16()
+    q, s = C.quant_fp8_rows(x)
+    qr, sr = ref.quant_fp8_rows(x)
+    torch.testing.assert_close(s, sr, rtol=1e-6, atol=0)
+    got = q.view(torch.float8_e4m3fn).float()
+    want = qr.float()
+    assert (got != want).float().mean().item() < 1e-3
+    assert ((got * s[:, None] - x.float()).norm() / x.float().norm()).item() < 0.04
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("N,K", [(1024, 4096), (4101, 14336)])
+def test_gpu_gemv_fp8_matches_fp32(gpu, M, N, K):
+    """fp8-weight GEMV vs the fp32 product of the dequantized weights (rows not divisible by 4,
+    padded x rows)."""
+    from dstack_amd.ops import _ext
+
+    C = _ext.require()
+    g = torch.Generator(device=gpu).manual_seed(M * 11 + N)
+    xs = torch.randn(M, K + 64, device=gpu, generator=g).to(torch.bfloat16)
+    x = xs[:, :K]
+    w = (torch.randn(N, K, device=gpu, generator=g) * 0.02).to(torch.bfloat16)
+    q, s = C.quant_fp8_rows(w)
+    y = C.gemv_fp8(x, q, s)
+    ref = x.float() @ (q.view(torch.float8_e4m3fn).float() * s[:, None]).t()
+    err = ((y.float() - ref).norm() / ref.norm()).item()
+    assert y.shape == (M, N) and err < 5e-3, err
+
+
+@pytest.mark.gpu
+def test_gpu_fp8_engine_tracks_bf16(gpu):
+    """fp8 serving model on the HIP path (GEMV for batch 1, hipBLASLt fp8 GEMM with row-wise scales
+    for prefill and larger batches): prefill logits close to the bf16 model's, generation runs
+    with hipGraphs."""
+    kw = dict(device="cuda", max_model_len=512, max_batch=8, num_pages=64)
+    base = LLMEngine.from_model("llama-tiny", **kw)
+    q8 = LLMEngine.from_model("llama-tiny", quantization="fp8", **kw)
+    prompt = torch.arange(1, 257, device=gpu)
+    pos = torch.arange(256, dtype=torch.int32, device=gpu)
+    slots = torch.arange(256, dtype=torch.int32, device=gpu)
+    a = base.model.prefill(prompt, pos, slots, [0], [256])
+    b = q8.model.prefill(prompt, pos, slots, [0], [256])
+    cos = torch.nn.functional.cosine_similarity(a.float(), b.float(), dim=-1).item()
+    assert cos > 0.99, cos
+    q8.capture_graphs()
+    sp = SamplingParams(max_tokens=16, temperature=0, ignore_eos=True)
+    outs = q8.generate([[1, 2, 3, 4, 5], list(range(7, 90))], sp)
+    assert all(len(o.output_ids) == 16 for o in outs)

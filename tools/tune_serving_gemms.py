@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--mode", default="use", choices=["tune", "use", "off"])
     ap.add_argument("--buckets", default="")
     ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: the e4m3 projections of --quantization fp8 (torch._scaled_mm, row-wise scales; "
+                         "M padded to 16 as the model does; the LM head stays bf16)")
     args = ap.parse_args()
     import torch
 
@@ -38,21 +41,36 @@ def main():
         nh = c.n_heads + 2 * c.n_kv_heads
         shapes = {"wqkv": (nh * c.head_dim, c.dim), "wo": (c.dim, c.n_heads * c.head_dim),
                   "wgu": (2 * c.ffn_dim, c.dim), "wdown": (c.dim, c.ffn_dim), "lm_head": (c.vocab_size, c.dim)}
+        fp8 = args.dtype == "fp8"
+        f8 = torch.float8_e4m3fn
         for wname, (N, K) in shapes.items():
+            if fp8 and wname == "lm_head":
+                continue
             w = torch.randn(N, K, device=dev).to(torch.bfloat16)
-            for M in buckets:
+            if fp8:
+                w8, sw = w.to(f8), torch.rand(1, N, device=dev) + 0.5
+            for M in sorted({(m + 15) // 16 * 16 for m in buckets} if fp8 else buckets):
                 x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+                if fp8:
+                    x8, sx = x.to(f8), torch.rand(M, 1, device=dev) + 0.5
+
+                    def mm():
+                        return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw, out_dtype=torch.bfloat16)
+                else:
+                    def mm():
+                        return x @ w.t()
                 for _ in range(3):
-                    y = x @ w.t()
+                    y = mm()
                 torch.cuda.synchronize()
                 it = 20
                 t0 = time.perf_counter()
                 for _ in range(it):
-                    y = x @ w.t()
+                    y = mm()
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) / it
-                tbs = (N * K + M * K + M * N) * 2 / dt / 1e12
-                out.append({"model": name, "w": wname, "M": M, "N": N, "K": K, "us": round(dt * 1e6, 1),
+                tbs = (N * K * (1 if fp8 else 2) + (M * K + M * N) * 2) / dt / 1e12
+                out.append({"model": name, "w": wname, "dtype": args.dtype, "M": M, "N": N, "K": K,
+                            "us": round(dt * 1e6, 1),
                             "TBps": round(tbs, 2)})
                 print(json.dumps(out[-1]), flush=True)
                 del y
