@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--quantization", choices=["fp8"], default=None)
+    ap.add_argument("--kv-cache-dtype", choices=["auto", "fp8"], default="auto")
     args = ap.parse_args()
 
     import numpy as np
@@ -55,7 +56,7 @@ def main():
     t0 = time.perf_counter()
     eng = LLMEngine.from_model(args.model, max_model_len=max_len, max_batch=1 if args.latency else args.max_batch,
                                max_prefill_tokens=args.max_prefill_tokens, use_graphs=not args.no_graphs and None,
-                               quantization=args.quantization)
+                               quantization=args.quantization, kv_cache_dtype=args.kv_cache_dtype)
     t_load = time.perf_counter() - t0
     t0 = time.perf_counter()
     eng.capture_graphs()
@@ -94,7 +95,8 @@ def main():
         "value": round(_pct(e2e, 50), 4) if args.latency else round(out_tokens / elapsed, 1),
         "unit": "s" if args.latency else "tokens/s",
         "higher_is_better": not args.latency,
-        "model": args.model, "dtype": str(m.dtype).replace("torch.", ""), "quantization": args.quantization, "n_gpus": 1,
+        "model": args.model, "dtype": str(m.dtype).replace("torch.", ""), "quantization": args.quantization,
+        "kv_cache_dtype": args.kv_cache_dtype, "n_gpus": 1,
         "data": "synthetic prompts (uniform random token ids), random-init weights",
         "num_prompts": n, "input_len": args.input_len, "output_len": args.output_len,
         "max_batch": eng.max_batch, "elapsed_s": round(elapsed, 3),

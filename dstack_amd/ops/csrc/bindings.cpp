@@ -30,9 +30,9 @@ hipError_t dsa_fa_bwd(const void*, const void*, const void*, const float*, void*
                       int, float, int, hipStream_t);
 int dsa_paged_page_size();
 hipError_t dsa_rope_cache_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int,
-                                int, hipStream_t);
+                                int, int, float, float, hipStream_t);
 hipError_t dsa_paged_decode(const void*, long, const void*, const void*, const int*, int, const int*, void*, float*,
-                            float*, int, int, int, int, int, float, hipStream_t);
+                            float*, int, int, int, int, int, float, int, float, float, hipStream_t);
 hipError_t dsa_sample(const void*, long, int, int, const float*, const int64_t*, const int*, int*, float*,
                       hipStream_t);
 bool dsa_gemm_tn_supported(int, int, int);
@@ -356,23 +356,34 @@ void check_i32(const torch::Tensor& t, const char* name) {
               " must be a contiguous int32 ROCm tensor");
 }
 
-void check_cache(const torch::Tensor& k, const torch::Tensor& v, int64_t KVH) {
-  check_bf16(k, "k_cache");
-  check_bf16(v, "v_cache");
+// returns true for an fp8 (e4m3) cache, false for bf16
+bool check_cache(const torch::Tensor& k, const torch::Tensor& v, int64_t KVH) {
+  const bool fp8 = k.scalar_type() == torch::kFloat8_e4m3fn;
+  if (fp8) {
+    TORCH_CHECK(k.is_cuda() && k.is_contiguous() && v.is_cuda() && v.is_contiguous() &&
+                    v.scalar_type() == torch::kFloat8_e4m3fn,
+                "fp8 k_cache / v_cache must both be contiguous float8_e4m3fn");
+  } else {
+    check_bf16(k, "k_cache");
+    check_bf16(v, "v_cache");
+  }
   const int64_t P = dsa_paged_page_size();
   TORCH_CHECK(k.dim() == 4 && k.size(1) == KVH && k.size(2) == P && k.size(3) == 128,
               "k_cache must be [pages, KVH, 64, 128]");
   TORCH_CHECK(v.dim() == 4 && v.size(0) == k.size(0) && v.size(1) == KVH && v.size(2) == 128 && v.size(3) == P,
               "v_cache must be [pages, KVH, 128, 64]");
+  return fp8;
 }
 
 // rotates q/k of qkv [T, (H+2KVH)*128] in place and writes k, v of each token to its cache slot
 void rope_cache_write(torch::Tensor qkv, torch::Tensor positions, torch::Tensor slots, torch::Tensor cos,
-                      torch::Tensor sin, torch::Tensor k_cache, torch::Tensor v_cache, int64_t H, int64_t KVH) {
+                      torch::Tensor sin, torch::Tensor k_cache, torch::Tensor v_cache, int64_t H, int64_t KVH,
+                      double k_scale, double v_scale) {
   check_bf16(qkv, "qkv");
   check_i32(positions, "positions");
   check_i32(slots, "slots");
-  check_cache(k_cache, v_cache, KVH);
+  const bool fp8 = check_cache(k_cache, v_cache, KVH);
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "kv cache scales must be positive");
   const int64_t T = positions.numel();
   TORCH_CHECK(slots.numel() == T && qkv.numel() == T * (H + 2 * KVH) * 128, "rope_cache_write: shape mismatch");
   TORCH_CHECK(cos.scalar_type() == torch::kFloat32 && sin.scalar_type() == torch::kFloat32 && cos.is_contiguous() &&
@@ -380,7 +391,7 @@ void rope_cache_write(torch::Tensor qkv, torch::Tensor positions, torch::Tensor 
               "rope tables must be fp32 [max_pos, 64]");
   check(dsa_rope_cache_write(qkv.data_ptr(), positions.data_ptr<int>(), slots.data_ptr<int>(), cos.data_ptr<float>(),
                              sin.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(), (int)T, (int)H, (int)KVH,
-                             stream()),
+                             fp8 ? 1 : 0, (float)k_scale, (float)v_scale, stream()),
         "rope_cache_write");
 }
 
@@ -388,11 +399,12 @@ void rope_cache_write(torch::Tensor qkv, torch::Tensor positions, torch::Tensor 
 // o_part / lse_part: fp32 workspaces of >= B*H*nsplit*128 and B*H*nsplit elements (unused when nsplit == 1)
 void paged_decode(torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor block_tables,
                   torch::Tensor ctx_lens, torch::Tensor out, torch::Tensor o_part, torch::Tensor lse_part, int64_t H,
-                  int64_t KVH, int64_t nsplit, int64_t pages_per_split, double scale) {
+                  int64_t KVH, int64_t nsplit, int64_t pages_per_split, double scale, double k_scale,
+                  double v_scale) {
   TORCH_CHECK(q.is_cuda() && q.scalar_type() == torch::kBFloat16 && q.dim() == 2 && q.stride(1) == 1 &&
                   q.size(1) >= H * 128 && q.stride(0) % 8 == 0,
               "q must be bf16 [B, >= H*128] with contiguous rows");
-  check_cache(k_cache, v_cache, KVH);
+  const bool fp8 = check_cache(k_cache, v_cache, KVH);
   check_i32(block_tables, "block_tables");
   check_i32(ctx_lens, "ctx_lens");
   check_bf16(out, "out");
@@ -409,7 +421,7 @@ void paged_decode(torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
                          block_tables.data_ptr<int>(), (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
                          out.data_ptr(), nsplit > 1 ? o_part.data_ptr<float>() : nullptr,
                          nsplit > 1 ? lse_part.data_ptr<float>() : nullptr, (int)B, (int)H, (int)KVH, (int)nsplit,
-                         (int)pages_per_split, (float)scale, stream()),
+                         (int)pages_per_split, (float)scale, fp8 ? 1 : 0, (float)k_scale, (float)v_scale, stream()),
         "paged_decode");
 }
 

@@ -23,6 +23,8 @@
 //    hipGraph.
 #include "common.h"
 
+#include <type_traits>
+
 using namespace dsa;
 
 namespace {
@@ -41,6 +43,30 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
 
+typedef unsigned int u2_t __attribute__((ext_vector_type(2)));
+
+// 8 e4m3 cache bytes (held raw while in flight: half the registers of bf16) -> the same bf16x8
+// MFMA operand the bf16 cache gives, converted right before the MFMA that reads it
+__device__ __forceinline__ bf16x8_t fp8x8_to_bf16(const u2_t w) {
+  bf16x8_t r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(w[h], false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(w[h], true);
+    r[4 * h + 0] = (__bf16)lo[0];
+    r[4 * h + 1] = (__bf16)lo[1];
+    r[4 * h + 2] = (__bf16)hi[0];
+    r[4 * h + 3] = (__bf16)hi[1];
+  }
+  return r;
+}
+
+// one float -> one e4m3 byte (saturating at +-448)
+__device__ __forceinline__ unsigned char to_fp8(float x) {
+  x = __builtin_amdgcn_fmed3f(x, 448.f, -448.f);
+  return (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32(x, x, 0, false) & 0xff);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -48,14 +74,16 @@ __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_c
 // qkv [T][(H + 2*KVH) * 128]; token t sits at position positions[t] and cache slot slots[t]
 // (= page * PAGE + offset; < 0: padding token, not cached).  One thread = 8 rotation pairs.
 // ------------------------------------------------------------------------------------------------
+// FP8: the cache holds e4m3 bytes of k / k_scale and v / v_scale (same layout, 1 byte per value).
+template <bool FP8>
 __global__ __launch_bounds__(256) void rope_cache_write_kernel(bf16_t* __restrict__ qkv,
                                                                const int* __restrict__ positions,
                                                                const int* __restrict__ slots,
                                                                const float* __restrict__ cosT,
                                                                const float* __restrict__ sinT,
-                                                               bf16_t* __restrict__ k_cache,
-                                                               bf16_t* __restrict__ v_cache, int T,
-                                                               int H, int KVH) {
+                                                               void* __restrict__ k_cache,
+                                                               void* __restrict__ v_cache, int T,
+                                                               int H, int KVH, float inv_ks, float inv_vs) {
   constexpr int half = HDIM / 2, cph = half / 8;  // 8 chunks of 8 pairs per head
   const int NH = H + 2 * KVH;
   const size_t total = (size_t)T * NH * cph;
@@ -90,12 +118,46 @@ __global__ __launch_bounds__(256) void rope_cache_write_kernel(bf16_t* __restric
     const int slot = slots[t];
     if (head < H || slot < 0) continue;
     const int page = slot / PAGE, off = slot % PAGE;
-    if (head < H + KVH) {
-      bf16_t* dst = k_cache + (((size_t)page * KVH + (head - H)) * PAGE + off) * HDIM;
+    if constexpr (FP8) {
+      typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+      if (head < H + KVH) {
+        unsigned char* dst = (unsigned char*)k_cache + (((size_t)page * KVH + (head - H)) * PAGE + off) * HDIM;
+        float x[8], y[8];
+        unpack8(a, x);
+        unpack8(b, y);
+        u2 wa, wb;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          int w = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(x[4 * h2] * inv_ks, 448.f, -448.f),
+                                                  __builtin_amdgcn_fmed3f(x[4 * h2 + 1] * inv_ks, 448.f, -448.f), 0,
+                                                  false);
+          wa[h2] = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(x[4 * h2 + 2] * inv_ks, 448.f, -448.f),
+                                                   __builtin_amdgcn_fmed3f(x[4 * h2 + 3] * inv_ks, 448.f, -448.f), w,
+                                                   true);
+          w = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(y[4 * h2] * inv_ks, 448.f, -448.f),
+                                              __builtin_amdgcn_fmed3f(y[4 * h2 + 1] * inv_ks, 448.f, -448.f), 0,
+                                              false);
+          wb[h2] = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(y[4 * h2 + 2] * inv_ks, 448.f, -448.f),
+                                                   __builtin_amdgcn_fmed3f(y[4 * h2 + 3] * inv_ks, 448.f, -448.f), w,
+                                                   true);
+        }
+        *reinterpret_cast<u2*>(dst + c * 8) = wa;
+        *reinterpret_cast<u2*>(dst + half + c * 8) = wb;
+      } else {
+        unsigned char* dst =
+            (unsigned char*)v_cache + ((size_t)page * KVH + (head - H - KVH)) * HDIM * PAGE + off;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          dst[(size_t)(c * 8 + k) * PAGE] = to_fp8(bf2f(a[k]) * inv_vs);
+          dst[(size_t)(half + c * 8 + k) * PAGE] = to_fp8(bf2f(b[k]) * inv_vs);
+        }
+      }
+    } else if (head < H + KVH) {
+      bf16_t* dst = (bf16_t*)k_cache + (((size_t)page * KVH + (head - H)) * PAGE + off) * HDIM;
       *reinterpret_cast<us8*>(dst + c * 8) = a;
       *reinterpret_cast<us8*>(dst + half + c * 8) = b;
     } else {
-      bf16_t* dst = v_cache + ((size_t)page * KVH + (head - H - KVH)) * HDIM * PAGE + off;
+      bf16_t* dst = (bf16_t*)v_cache + ((size_t)page * KVH + (head - H - KVH)) * HDIM * PAGE + off;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         dst[(size_t)(c * 8 + k) * PAGE] = a[k];
@@ -111,13 +173,15 @@ __global__ __launch_bounds__(256) void rope_cache_write_kernel(bf16_t* __restric
 // G = query heads per KV head (1..16).  Output: DIRECT -> out[b][h*128 + d] bf16 (one split);
 // otherwise o_part[b][h][split][128] fp32 (normalised) + lse_part[b][h][split] (log2 domain).
 // ------------------------------------------------------------------------------------------------
-template <bool DIRECT>
+// FP8: e4m3 cache (half the bytes of the HBM-bound page stream), converted to the same bf16
+// operands in registers; k_scale is folded into scale_log2 by the host, v_scale into the output.
+template <bool DIRECT, bool FP8>
 __global__ __launch_bounds__(64) void paged_decode_kernel(
-    const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
-    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const bf16_t* __restrict__ q, long q_stride, const void* __restrict__ k_cache,
+    const void* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, bf16_t* __restrict__ out, float* __restrict__ o_part,
     float* __restrict__ lse_part, int H, int KVH, int G, int nsplit, int pages_per_split,
-    float scale_log2) {
+    float scale_log2, float v_scale) {
   // grid (B * KVH, nsplit): consecutive workgroups are different (sequence, KV head) pairs of the
   // SAME split, so the populated splits are dealt round-robin over all 8 XCDs.  (With the split
   // as the fastest index, split s landed on XCD s % 8: at 8 splits and short contexts every
@@ -156,20 +220,44 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
 #pragma unroll
     for (int t = 0; t < 4; ++t) koff[t] = (32 * (t >> 1) + 8 * (r >> 2) + 4 * (t & 1) + (r & 3)) * HDIM + 8 * g;
     const int voff = r * PAGE + 8 * g;
-    bf16x8_t kf[4][4], vf[2][8];
+    // operands in flight: bf16x8 (16 B) per lane, or the raw 8 e4m3 bytes of an fp8 cache
+    using OpT = typename std::conditional<FP8, u2_t, bf16x8_t>::type;
+    OpT kf[4][4], vf[2][8];
+    auto op = [](const OpT& v) -> bf16x8_t {
+      if constexpr (FP8)
+        return fp8x8_to_bf16(v);
+      else
+        return v;
+    };
     auto load_k = [&](long page) {
-      const bf16_t* kb = k_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
+      if constexpr (FP8) {
+        const unsigned char* kb = (const unsigned char*)k_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) kf[t][kk] = ld8(kb + koff[t] + 32 * kk);
+          for (int kk = 0; kk < 4; ++kk) kf[t][kk] = *reinterpret_cast<const u2_t*>(kb + koff[t] + 32 * kk);
+      } else {
+        const bf16_t* kb = (const bf16_t*)k_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) kf[t][kk] = ld8(kb + koff[t] + 32 * kk);
+      }
     };
     auto load_v = [&](long page) {
-      const bf16_t* vb = v_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
+      if constexpr (FP8) {
+        const unsigned char* vb = (const unsigned char*)v_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
 #pragma unroll
-      for (int mm = 0; mm < 2; ++mm)
+        for (int mm = 0; mm < 2; ++mm)
 #pragma unroll
-        for (int n = 0; n < 8; ++n) vf[mm][n] = ld8(vb + voff + 16 * n * PAGE + 32 * mm);
+          for (int n = 0; n < 8; ++n) vf[mm][n] = *reinterpret_cast<const u2_t*>(vb + voff + 16 * n * PAGE + 32 * mm);
+      } else {
+        const bf16_t* vb = (const bf16_t*)v_cache + (page * KVH + kvh) * (long)(PAGE * HDIM);
+#pragma unroll
+        for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+          for (int n = 0; n < 8; ++n) vf[mm][n] = ld8(vb + voff + 16 * n * PAGE + 32 * mm);
+      }
     };
     long page = bt[p0];
     load_k(page);
@@ -183,7 +271,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
       for (int t = 0; t < 4; ++t) {
         s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) s[t] = mfma16(kf[t][kk], qf[kk], s[t]);
+        for (int kk = 0; kk < 4; ++kk) s[t] = mfma16(op(kf[t][kk]), qf[kk], s[t]);
       }
       __builtin_amdgcn_sched_barrier(0);
       load_k(next);  // unconditional (last page: a redundant reload) so vmcnt counting stays static
@@ -227,7 +315,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
           pf[4 + i] = (__bf16)s[2 * mm + 1][i];
         }
 #pragma unroll
-        for (int n = 0; n < 8; ++n) acc[n] = mfma16(vf[mm][n], pf, acc[n]);
+        for (int n = 0; n < 8; ++n) acc[n] = mfma16(op(vf[mm][n]), pf, acc[n]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -236,7 +324,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   if (!qvalid) return;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
+  const float inv = l > 0.f ? v_scale / l : 0.f;
   if (DIRECT) {
     bf16_t* o = out + (long)b * H * HDIM + (long)h * HDIM;
 #pragma unroll
@@ -287,7 +375,8 @@ __global__ __launch_bounds__(256) void paged_combine_kernel(const float* __restr
 #pragma unroll 4
     for (int s = g; s < nsplit; s += 8) {
       const float ls = lse[s];
-      const float w = ls == -INFINITY ? 0.f : fexp2(ls - M);
+      if (ls == -INFINITY) continue;  // empty split: its o row was never written (0 * garbage = NaN)
+      const float w = fexp2(ls - M);
       const f4 o = op[(long)s * (HDIM / 4)];
       num += w * o;
       den += w;
@@ -421,13 +510,19 @@ extern "C" int dsa_paged_page_size() { return PAGE; }
 
 extern "C" hipError_t dsa_rope_cache_write(void* qkv, const int* positions, const int* slots,
                                            const float* cosT, const float* sinT, void* k_cache,
-                                           void* v_cache, int T, int H, int KVH, hipStream_t st) {
+                                           void* v_cache, int T, int H, int KVH, int fp8, float k_scale,
+                                           float v_scale, hipStream_t st) {
   if (T <= 0) return hipSuccess;
   const size_t work = (size_t)T * (H + 2 * KVH) * (HDIM / 16);
   size_t grid = (work + 255) / 256;
   if (grid > 65535 * 4) grid = 65535 * 4;
-  rope_cache_write_kernel<<<(unsigned)grid, 256, 0, st>>>((bf16_t*)qkv, positions, slots, cosT, sinT,
-                                                          (bf16_t*)k_cache, (bf16_t*)v_cache, T, H, KVH);
+  if (fp8)
+    rope_cache_write_kernel<true><<<(unsigned)grid, 256, 0, st>>>((bf16_t*)qkv, positions, slots, cosT, sinT,
+                                                                  k_cache, v_cache, T, H, KVH, 1.f / k_scale,
+                                                                  1.f / v_scale);
+  else
+    rope_cache_write_kernel<false><<<(unsigned)grid, 256, 0, st>>>((bf16_t*)qkv, positions, slots, cosT, sinT,
+                                                                   k_cache, v_cache, T, H, KVH, 1.f, 1.f);
   return hipGetLastError();
 }
 
@@ -435,23 +530,25 @@ extern "C" hipError_t dsa_paged_decode(const void* q, long q_stride, const void*
                                        const void* v_cache, const int* block_tables, int bt_stride,
                                        const int* ctx_lens, void* out, float* o_part,
                                        float* lse_part, int B, int H, int KVH, int nsplit,
-                                       int pages_per_split, float scale, hipStream_t st) {
+                                       int pages_per_split, float scale, int fp8, float k_scale,
+                                       float v_scale, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   if (KVH <= 0 || H % KVH || H / KVH > 16 || nsplit < 1 || pages_per_split < 1) return hipErrorInvalidValue;
   const int G = H / KVH;
-  const float sl2 = scale * 1.4426950408889634f;
+  const float sl2 = scale * 1.4426950408889634f * (fp8 ? k_scale : 1.f);
+  const float vs = fp8 ? v_scale : 1.f;
   const dim3 grid(B * KVH, nsplit);
+#define DSA_PAGED(D, F8)                                                                               \
+  paged_decode_kernel<D, F8><<<grid, 64, 0, st>>>((const bf16_t*)q, q_stride, k_cache, v_cache, block_tables, \
+                                                  bt_stride, ctx_lens, D ? (bf16_t*)out : nullptr,             \
+                                                  D ? nullptr : o_part, D ? nullptr : lse_part, H, KVH, G,     \
+                                                  nsplit, pages_per_split, sl2, vs)
   if (nsplit == 1) {
-    paged_decode_kernel<true><<<grid, 64, 0, st>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache,
-                                                  (const bf16_t*)v_cache, block_tables, bt_stride,
-                                                  ctx_lens, (bf16_t*)out, nullptr, nullptr, H, KVH, G,
-                                                  nsplit, pages_per_split, sl2);
+    if (fp8) DSA_PAGED(true, true); else DSA_PAGED(true, false);
     return hipGetLastError();
   }
-  paged_decode_kernel<false><<<grid, 64, 0, st>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache,
-                                                 (const bf16_t*)v_cache, block_tables, bt_stride,
-                                                 ctx_lens, nullptr, o_part, lse_part, H, KVH, G,
-                                                 nsplit, pages_per_split, sl2);
+  if (fp8) DSA_PAGED(false, true); else DSA_PAGED(false, false);
+#undef DSA_PAGED
   DSA_CHECK(hipGetLastError());
   paged_combine_kernel<<<B * H, 256, 0, st>>>(o_part, lse_part, (bf16_t*)out, H, nsplit);
   return hipGetLastError();

@@ -21,9 +21,15 @@ HEAD_DIM = 128
 
 
 def alloc_cache(num_pages: int, n_kv_heads: int, dtype=torch.bfloat16, device=None):
+    """``dtype`` bf16 (or fp32 on the CPU) or ``torch.float8_e4m3fn`` (an fp8 cache holds
+    k / k_scale and v / v_scale: half the bytes a decode step streams, twice the tokens)."""
     k = torch.zeros(num_pages, n_kv_heads, PAGE, HEAD_DIM, dtype=dtype, device=device)
     v = torch.zeros(num_pages, n_kv_heads, HEAD_DIM, PAGE, dtype=dtype, device=device)
     return k, v
+
+
+def _is_fp8(cache: torch.Tensor) -> bool:
+    return cache.dtype == torch.float8_e4m3fn
 
 
 # ----------------------------------------------------------------------------------------------
@@ -31,16 +37,19 @@ def alloc_cache(num_pages: int, n_kv_heads: int, dtype=torch.bfloat16, device=No
 # ----------------------------------------------------------------------------------------------
 def rope_cache_write(qkv: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cos: torch.Tensor,
                      sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n_heads: int,
-                     n_kv_heads: int) -> torch.Tensor:
+                     n_kv_heads: int, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
     """Rotate q and k of ``qkv`` [T, (H + 2*KVH) * 128] in place (token t at ``positions[t]``) and
     store k/v of every token with ``slots[t] >= 0`` in the cache.  Returns ``qkv``."""
     if _ext.use_hip(qkv):
-        _ext.require().rope_cache_write(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads)
+        _ext.require().rope_cache_write(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads,
+                                        k_scale, v_scale)
         return qkv
-    return rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads)
+    return rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads,
+                                k_scale, v_scale)
 
 
-def rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads):
+def rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads,
+                         k_scale: float = 1.0, v_scale: float = 1.0):
     T = positions.numel()
     x = qkv.view(T, n_heads + 2 * n_kv_heads, HEAD_DIM)
     rot = x[:, : n_heads + n_kv_heads].float()
@@ -54,6 +63,9 @@ def rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_he
         page, off = sl // PAGE, sl % PAGE
         k = x[keep][:, n_heads : n_heads + n_kv_heads]  # [n, KVH, D]
         v = x[keep][:, n_heads + n_kv_heads :]
+        if _is_fp8(k_cache):
+            k = (k.float() / k_scale).clamp(-448, 448)
+            v = (v.float() / v_scale).clamp(-448, 448)
         k_cache[page, :, off, :] = k.to(k_cache.dtype)
         v_cache[page, :, :, off] = v.to(v_cache.dtype)
     return qkv
@@ -84,7 +96,7 @@ class DecodeWorkspace:
 
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                  ctx_lens: torch.Tensor, n_heads: int, n_kv_heads: int, out: torch.Tensor | None = None,
-                 ws: DecodeWorkspace | None = None) -> torch.Tensor:
+                 ws: DecodeWorkspace | None = None, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
     """Attention of one new query token per sequence over its cached keys/values.
 
     ``q`` [B, >= H*128] (rows may be the fused qkv output: only the first H*128 columns are read),
@@ -96,13 +108,16 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
         if ws is None:
             ws = DecodeWorkspace(B, n_heads, n_kv_heads, block_tables.shape[1], q.device)
         _ext.require().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o_part, ws.lse_part,
-                                    n_heads, n_kv_heads, ws.nsplit, ws.pps, 1.0 / math.sqrt(HEAD_DIM))
+                                    n_heads, n_kv_heads, ws.nsplit, ws.pps, 1.0 / math.sqrt(HEAD_DIM), k_scale,
+                                    v_scale)
         return out
-    out.copy_(paged_decode_ref(q, k_cache, v_cache, block_tables, ctx_lens, n_heads, n_kv_heads).to(out.dtype))
+    out.copy_(paged_decode_ref(q, k_cache, v_cache, block_tables, ctx_lens, n_heads, n_kv_heads, k_scale,
+                               v_scale).to(out.dtype))
     return out
 
 
-def paged_decode_ref(q, k_cache, v_cache, block_tables, ctx_lens, n_heads, n_kv_heads):
+def paged_decode_ref(q, k_cache, v_cache, block_tables, ctx_lens, n_heads, n_kv_heads, k_scale: float = 1.0,
+                     v_scale: float = 1.0):
     """fp32 reference: gathers each sequence's pages and runs plain softmax attention."""
     B = q.shape[0]
     G = n_heads // n_kv_heads
@@ -110,8 +125,9 @@ def paged_decode_ref(q, k_cache, v_cache, block_tables, ctx_lens, n_heads, n_kv_
     for b in range(B):
         n = int(ctx_lens[b])
         pages = block_tables[b, : (n + PAGE - 1) // PAGE].long()
-        k = k_cache[pages].float().permute(1, 0, 2, 3).reshape(n_kv_heads, -1, HEAD_DIM)[:, :n]  # [KVH, n, D]
-        v = v_cache[pages].float().permute(1, 0, 3, 2).reshape(n_kv_heads, -1, HEAD_DIM)[:, :n]
+        ks, vs = (k_scale, v_scale) if _is_fp8(k_cache) else (1.0, 1.0)
+        k = k_cache[pages].float().permute(1, 0, 2, 3).reshape(n_kv_heads, -1, HEAD_DIM)[:, :n] * ks  # [KVH, n, D]
+        v = v_cache[pages].float().permute(1, 0, 3, 2).reshape(n_kv_heads, -1, HEAD_DIM)[:, :n] * vs
         qb = q[b, : n_heads * HEAD_DIM].float().view(n_kv_heads, G, HEAD_DIM)
         s = torch.einsum("hgd,hnd->hgn", qb, k) / math.sqrt(HEAD_DIM)
         p = torch.softmax(s, dim=-1)

@@ -25,6 +25,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0, help="random-init seed for built-in configs")
     ap.add_argument("--quantization", choices=["fp8"], default=None,
                     help="fp8: e4m3 projection weights with per-channel scales, per-token activation scales")
+    ap.add_argument("--kv-cache-dtype", choices=["auto", "fp8"], default="auto",
+                    help="fp8: e4m3 paged KV cache (half the bytes per decode step, twice the tokens)")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(message)s")
     log = logging.getLogger("dstack_amd.serving")
@@ -40,7 +42,8 @@ def main(argv=None):
     t0 = time.time()
     eng = LLMEngine.from_model(args.model, max_model_len=args.max_model_len, seed=args.seed, max_batch=args.max_batch,
                                max_prefill_tokens=args.max_prefill_tokens, use_graphs=not args.no_graphs and None,
-                               gpu_memory_utilization=args.gpu_memory_utilization, quantization=args.quantization)
+                               gpu_memory_utilization=args.gpu_memory_utilization, quantization=args.quantization,
+                               kv_cache_dtype=args.kv_cache_dtype)
     eng.capture_graphs()
     m = eng.model
     log.info("model %s: %.1f GB weights, %d KV pages (%d tokens), max_model_len %d, %d graph buckets, ready in %.1fs",

@@ -117,10 +117,11 @@ class LLMEngine:
 
     @classmethod
     def from_model(cls, model: str, device=None, max_model_len: int | None = None, seed: int = 0, tp_group=None,
-                   quantization: str | None = None, **kw):
+                   quantization: str | None = None, kv_cache_dtype: str = "auto", **kw):
         spec = load_spec(model)
         device = device or ("cuda" if torch.cuda.is_available() else "cpu")
-        m = ServingLlama(spec, device, max_model_len=max_model_len, tp_group=tp_group, quantization=quantization)
+        m = ServingLlama(spec, device, max_model_len=max_model_len, tp_group=tp_group, quantization=quantization,
+                         kv_cache_dtype=kv_cache_dtype)
         if spec.path:
             m.load_hf()
         else:

@@ -139,10 +139,16 @@ class ServingLlama:
     ``H``/``KVH``/``F``/``V`` below are then this rank's local head / FFN / vocab counts)."""
 
     def __init__(self, spec: ModelSpec, device, dtype=None, max_model_len: int | None = None, tp_group=None,
-                 quantization: str | None = None):
+                 quantization: str | None = None, kv_cache_dtype: str = "auto"):
         if quantization not in (None, "fp8"):
             raise ValueError(f"unsupported quantization {quantization!r} (supported: fp8)")
+        if kv_cache_dtype not in ("auto", "fp8"):
+            raise ValueError(f"unsupported kv_cache_dtype {kv_cache_dtype!r} (supported: auto, fp8)")
         self.quantization = quantization
+        self.kv_cache_dtype = kv_cache_dtype
+        # fp8 cache: e4m3 bytes of k / k_scale, v / v_scale (1.0: K and V of Llama layers stay far
+        # inside e4m3's +-448 range)
+        self.k_scale = self.v_scale = 1.0
         self.spec = spec
         self.cfg = cfg = spec.cfg
         self.device = torch.device(device)
@@ -342,8 +348,13 @@ class ServingLlama:
     # ------------------------------------------------------------------------------------------
     # KV cache
     # ------------------------------------------------------------------------------------------
+    @property
+    def cache_dtype(self):
+        return torch.float8_e4m3fn if self.kv_cache_dtype == "fp8" else self.dtype
+
     def kv_bytes_per_page(self) -> int:
-        return 2 * self.cfg.n_layers * self.KVH * sops.PAGE * self.D * torch.empty(0, dtype=self.dtype).element_size()
+        esize = torch.empty(0, dtype=self.cache_dtype).element_size()
+        return 2 * self.cfg.n_layers * self.KVH * sops.PAGE * self.D * esize
 
     def allocate_kv(self, num_pages: int | None = None, gpu_memory_utilization: float = 0.90,
                     reserve_bytes: int = 8 << 30):
@@ -366,7 +377,7 @@ class ServingLlama:
         self.num_pages = num_pages
         self.k_cache, self.v_cache = [], []
         for _ in range(self.cfg.n_layers):
-            k, v = sops.alloc_cache(num_pages, self.KVH, self.dtype, self.device)
+            k, v = sops.alloc_cache(num_pages, self.KVH, self.cache_dtype, self.device)
             self.k_cache.append(k)
             self.v_cache.append(v)
         return num_pages
@@ -464,7 +475,8 @@ class ServingLlama:
             else:
                 x, h = self._add_rms(x, delta, L["attn_norm"])
             qkv = self._mm(h, L["wqkv"]) if isinstance(L["wqkv"], Fp8Weight) else h @ L["wqkv"].t()
-            sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH)
+            sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH,
+                                  self.k_scale, self.v_scale)
             o = torch.empty(rows, H * self.D, dtype=x.dtype, device=x.device)
             for off, n in bounds:
                 seg = qkv[off : off + n].view(1, n, -1)
@@ -491,8 +503,10 @@ class ServingLlama:
             else:
                 x, h = self._add_rms(x, delta, L["attn_norm"])
             qkv = self._mm(h, L["wqkv"])
-            sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH)
-            o = sops.paged_decode(qkv, self.k_cache[li], self.v_cache[li], block_tables, ctx_lens, H, KVH, ws=ws)
+            sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH,
+                                  self.k_scale, self.v_scale)
+            o = sops.paged_decode(qkv, self.k_cache[li], self.v_cache[li], block_tables, ctx_lens, H, KVH, ws=ws,
+                                  k_scale=self.k_scale, v_scale=self.v_scale)
             x, delta = self._mlp_and_attn_out(L, x, o)
         _, h = self._add_rms(x, delta, self.norm)
         return self._logits(h)

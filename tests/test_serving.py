@@ -576,3 +576,111 @@ def test_gpu_fp8_engine_tracks_bf16(gpu):
     sp = SamplingParams(max_tokens=16, temperature=0, ignore_eos=True)
     outs = q8.generate([[1, 2, 3, 4, 5], list(range(7, 90))], sp)
     assert all(len(o.output_ids) == 16 for o in outs)
+
+
+# ------------------------------------------------------------------------------------------------
+# fp8 (e4m3) KV cache
+# ------------------------------------------------------------------------------------------------
+def test_fp8_kv_cache_engine_close_to_bf16():
+    """An fp8 KV cache holds twice the tokens per byte; greedy decoding on it tracks the bf16
+    cache (first decode logits close; the CPU path dequantizes in the fp32 reference)."""
+    kw = dict(device="cpu", max_model_len=256, max_batch=4, num_pages=16)
+    base = LLMEngine.from_model("llama-tiny", **kw)
+    f8 = LLMEngine.from_model("llama-tiny", kv_cache_dtype="fp8", **kw)
+    assert f8.model.k_cache[0].dtype == torch.float8_e4m3fn
+    assert f8.model.kv_bytes_per_page() * 4 == base.model.kv_bytes_per_page()  # fp32 CPU cache vs 1 byte
+    sp = SamplingParams(max_tokens=12, temperature=0, ignore_eos=True)
+    prompts = [[1, 5, 9, 33, 7, 100, 2, 45, 61], list(range(3, 90))]
+    a = [r.output_ids for r in base.generate(prompts, sp)]
+    b = [r.output_ids for r in f8.generate(prompts, sp)]
+    agree = sum(x == y for p, q in zip(a, b) for x, y in zip(p, q)) / sum(len(p) for p in a)
+    assert agree > 0.8, (a, b)
+    with pytest.raises(ValueError, match="kv_cache_dtype"):
+        LLMEngine.from_model("llama-tiny", kv_cache_dtype="int4", **kw)
+
+
+@pytest.mark.gpu
+def test_gpu_paged_decode_empty_splits_ignore_workspace(gpu):
+    """Splits past a sequence's context write only their -inf lse; the combine must not read their
+    (uninitialised) partial rows: a NaN-filled workspace leaves the output finite and exact."""
+    torch.manual_seed(0)
+    dev, H, KVH, B, W = "cuda", 8, 2, 1, 8
+    k_cache, v_cache = sops.alloc_cache(16, KVH, torch.bfloat16, dev)
+    k_cache.normal_()
+    v_cache.normal_()
+    table = torch.arange(W, dtype=torch.int32, device=dev).view(1, W)
+    ctx = torch.tensor([201], dtype=torch.int32, device=dev)  # 4 of 8 single-page splits populated
+    qkv = torch.randn(B, (H + 2 * KVH) * 128, device=dev).to(torch.bfloat16)
+    ws = sops.DecodeWorkspace(B, H, KVH, W, dev)
+    assert ws.nsplit == 8
+    ws.o_part.fill_(float("nan"))
+    got = sops.paged_decode(qkv, k_cache, v_cache, table, ctx, H, KVH, ws=ws)
+    want = sops.paged_decode_ref(qkv, k_cache, v_cache, table, ctx, H, KVH)
+    assert torch.isfinite(got).all()
+    torch.testing.assert_close(got.float(), want, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,KVH", [(32, 8), (64, 8)])
+def test_gpu_paged_decode_fp8_cache(gpu, H, KVH):
+    """Paged decode over an e4m3 cache (with non-unit k/v scales folded into the kernel) vs the
+    fp32 reference over the dequantized cache, split and single-split."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    pages, B, W = 80, 5, 40
+    k_cache, v_cache = sops.alloc_cache(pages, KVH, torch.float8_e4m3fn, dev)
+    k_cache.copy_(torch.randn(k_cache.shape, device=dev).clamp(-4, 4).to(torch.float8_e4m3fn))
+    v_cache.copy_(torch.randn(v_cache.shape, device=dev).clamp(-4, 4).to(torch.float8_e4m3fn))
+    perm = torch.randint(0, pages, (B, W), device=dev, dtype=torch.int32)
+    ctx = torch.tensor([1, 63, 64, 1000, 2560], dtype=torch.int32, device=dev)
+    qkv = torch.randn(B, (H + 2 * KVH) * 128, device=dev).to(torch.bfloat16)
+    ks, vs = 0.5, 2.0
+    want = sops.paged_decode_ref(qkv, k_cache, v_cache, perm, ctx, H, KVH, ks, vs)
+    for one in (False, True):
+        ws = sops.DecodeWorkspace(B, H, KVH, W, dev)
+        if one:
+            ws.nsplit, ws.pps = 1, W
+        got = sops.paged_decode(qkv, k_cache, v_cache, perm, ctx, H, KVH, ws=ws, k_scale=ks, v_scale=vs)
+        torch.testing.assert_close(got.float(), want, atol=4e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_rope_cache_write_fp8(gpu):
+    """RoPE + scatter into an e4m3 cache: the bytes equal the reference's cast of k / k_scale and
+    v / v_scale (up to rounding ties of the bf16-rotated k)."""
+    torch.manual_seed(0)
+    dev, H, KVH, T = "cuda", 32, 8, 70
+    cos, sin = sops_rope(dev)
+    qkv = torch.randn(T, (H + 2 * KVH) * 128, device=dev).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=dev, dtype=torch.int32)
+    slots = torch.randperm(10 * 64, device=dev)[:T].int()
+    slots[5] = -1
+    kc, vc = sops.alloc_cache(10, KVH, torch.float8_e4m3fn, dev)
+    kr, vr = sops.alloc_cache(10, KVH, torch.float8_e4m3fn, dev)
+    got = sops.rope_cache_write(qkv.clone(), pos, slots, cos, sin, kc, vc, H, KVH, 0.5, 2.0)
+    want = sops.rope_cache_write_ref(qkv.clone(), pos, slots, cos, sin, kr, vr, H, KVH, 0.5, 2.0)
+    torch.testing.assert_close(got, want)  # q / k rotation is unchanged
+    assert (kc.float() != kr.float()).float().mean().item() < 1e-3
+    assert torch.equal(vc.float(), vr.float())
+
+
+@pytest.mark.gpu
+def test_gpu_fp8_kv_decode_logits_track_bf16(gpu):
+    """One decode step over a 200-token context held in an fp8 cache gives logits close to the
+    same step over the bf16 cache (same weights), on the HIP path."""
+    kw = dict(device="cuda", max_model_len=512, max_batch=8, num_pages=64)
+    outs = []
+    for kv in ("auto", "fp8"):
+        m = LLMEngine.from_model("llama-tiny", kv_cache_dtype=kv, **kw).model
+        n = 256  # prefill rows (128-aligned); the first 200 are the prompt
+        toks = torch.arange(1, n + 1, device=gpu) % 500
+        pos = torch.arange(n, dtype=torch.int32, device=gpu)
+        slots = torch.where(pos < 200, pos, torch.full_like(pos, -1))
+        m.prefill(toks, pos, slots, [0], [200])
+        table = torch.arange(8, dtype=torch.int32, device=gpu).view(1, 8)
+        logits = m.decode(torch.tensor([7], device=gpu), torch.tensor([200], dtype=torch.int32, device=gpu),
+                          torch.tensor([200], dtype=torch.int32, device=gpu), table,
+                          torch.tensor([201], dtype=torch.int32, device=gpu))
+        outs.append(logits.float())
+    cos = torch.nn.functional.cosine_similarity(outs[0], outs[1], dim=-1).item()
+    assert cos > 0.99, cos
