@@ -1,4 +1,4 @@
-"""Decode-projection GEMV (csrc/gemv.hip) vs hipBLASLt (torch.mm with the shipped serving TunableOp
+"""Decode-projection GEMV (csrc/gemv.hip; fp8 weights: csrc/fp8.hip) vs hipBLASLt (torch.mm with the shipped serving TunableOp
 selections) at M = 1/2/4 on the Llama-3-70B / 8B projection shapes: weight-stream TB/s."""
 import json
 import os
@@ -38,6 +38,11 @@ def main():
             err = ((C.gemv(x, w).float() - (x @ w.t()).float()).norm() / (x @ w.t()).float().norm()).item()
             out[f"{name}.M{M}"] = {"gemv_ms": tg, "gemv_TBps": N * K * 2 / tg / 1e9, "lib_ms": tl,
                                    "lib_TBps": N * K * 2 / tl / 1e9, "rel_err": err}
+            if C.gemv_fp8_supported(M, K):  # e4m3 weights: half the bytes (--quantization fp8)
+                q, sc = C.quant_fp8_rows(w)
+                t8 = timeit(lambda: C.gemv_fp8(x, q, sc))
+                out[f"{name}.M{M}"].update(fp8_ms=t8, fp8_TBps=N * K / t8 / 1e9)
+                del q, sc
             print(name, M, json.dumps(out[f"{name}.M{M}"]), flush=True)
         del w
         torch.cuda.empty_cache()
