@@ -235,11 +235,17 @@ def _check_provisioning(s: Session, inst: InstanceModel):
             logger.debug("update_provisioning_data: %s", e)
     if jpd.hostname and _shim_healthy(inst, jpd):
         inst.status = (InstanceStatus.BUSY if (inst.busy_blocks or 0) > 0 else InstanceStatus.IDLE).value
+        inst.termination_deadline = None
+        inst.health_status = None
+        inst.unreachable = False
         scheduler.wake(scheduler.RUNNING_JOBS, scheduler.SUBMITTED_JOBS)
         return
-    if get_current_datetime() - inst.created_at > PROVISIONING_DEADLINE:
+    now = get_current_datetime()
+    inst.health_status = "waiting for the cloud to report the host" if not jpd.hostname else "shim not reachable yet"
+    if now - (inst.started_at or inst.created_at) > PROVISIONING_DEADLINE:
         inst.status = InstanceStatus.TERMINATING.value
         inst.termination_reason = "provisioning timeout"
+        inst.termination_deadline = inst.termination_deadline or now
 
 
 def _shim_healthy(inst: InstanceModel, jpd: JobProvisioningData) -> bool:

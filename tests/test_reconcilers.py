@@ -148,6 +148,53 @@ def test_provisioning_instance_becomes_idle_when_shim_answers(db):
         assert s.get(InstanceModel, iid).status == "idle"
 
 
+@pytest.mark.parametrize("busy_blocks,want", [(0, "idle"), (1, "busy")])
+def test_provisioning_ready_clears_health_and_deadline(db, busy_blocks, want):
+    """(reference: ``test_check_shim_transitions_provisioning_on_ready`` / ``_on_busy``) a host that
+    had health problems while provisioning comes up clean; a job already assigned makes it BUSY."""
+    from datetime import timedelta
+
+    from dstack_amd.server.background.tasks import process_instances as pi
+
+    with session_scope() as s:
+        iid = _instance(s, status=InstanceStatus.PROVISIONING)
+        inst = s.get(InstanceModel, iid)
+        inst.health_status = "ssh connect problem"
+        inst.termination_deadline = get_current_datetime() + timedelta(days=1)
+        inst.busy_blocks = busy_blocks
+    ok = mock.Mock()
+    ok.healthcheck.return_value = {"service": "dstack-shim"}
+    with mock.patch.object(pi, "get_shim_client", return_value=ok), session_scope() as s:
+        pi._process_instance(s, iid)
+    with session_scope() as s:
+        inst = s.get(InstanceModel, iid)
+        assert (inst.status, inst.health_status, inst.termination_deadline) == (want, None, None)
+
+
+def test_provisioning_unreachable_times_out(db):
+    """(reference: ``test_check_shim_transitions_provisioning_on_terminating``) the shim never
+    answers: the health status says so, and past the provisioning deadline the host terminates."""
+    from dstack_amd.server.background.tasks import process_instances as pi
+
+    with session_scope() as s:
+        iid = _instance(s, status=InstanceStatus.PROVISIONING)
+        s.get(InstanceModel, iid).started_at = get_current_datetime() - pi.PROVISIONING_DEADLINE / 2
+    down = mock.Mock()
+    down.healthcheck.side_effect = ConnectionError("ssh: connect to host: timed out")
+    with mock.patch.object(pi, "get_shim_client", return_value=down), session_scope() as s:
+        pi._process_instance(s, iid)
+    with session_scope() as s:
+        inst = s.get(InstanceModel, iid)
+        assert inst.status == "provisioning" and inst.health_status
+        inst.started_at = get_current_datetime() - pi.PROVISIONING_DEADLINE * 2
+    with mock.patch.object(pi, "get_shim_client", return_value=down), session_scope() as s:
+        pi._process_instance(s, iid)
+    with session_scope() as s:
+        inst = s.get(InstanceModel, iid)
+        assert inst.status == "terminating" and inst.termination_reason == "provisioning timeout"
+        assert inst.termination_deadline is not None
+
+
 # ---- submitted jobs / runs --------------------------------------------------------------------
 def _submit(s, conf: dict, name="r1"):
     from dstack_amd.server.services import runs as runs_services
