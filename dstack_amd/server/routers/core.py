@@ -47,7 +47,7 @@ def get_server_info() -> ServerInfo:
 
 # ---- users ----------------------------------------------------------------------------------
 @users_router.post("/list")
-def list_users(user: UserModel = Depends(authenticated), s: Session = Depends(get_session)) -> List[User]:
+def list_users(user: UserModel = Depends(authenticated), s: Session = Depends(get_session, scope="function")) -> List[User]:
     if user.global_role != GlobalRole.ADMIN.value:
         return [users_services.user_model_to_user(user)]
     return [users_services.user_model_to_user(u) for u in users_services.list_users(s)]
@@ -60,7 +60,7 @@ def get_my_user(user: UserModel = Depends(authenticated)) -> UserWithCreds:
 
 @users_router.post("/get_user")
 def get_user(body: schemas.GetUserRequest, user: UserModel = Depends(authenticated),
-             s: Session = Depends(get_session)) -> UserWithCreds:
+             s: Session = Depends(get_session, scope="function")) -> UserWithCreds:
     if user.global_role != GlobalRole.ADMIN.value and user.name != body.username:
         raise ForbiddenError()
     u = users_services.get_user_by_name(s, body.username)
@@ -71,46 +71,46 @@ def get_user(body: schemas.GetUserRequest, user: UserModel = Depends(authenticat
 
 @users_router.post("/create")
 def create_user(body: schemas.CreateUserRequest, user: UserModel = Depends(global_admin),
-                s: Session = Depends(get_session)) -> UserWithCreds:
+                s: Session = Depends(get_session, scope="function")) -> UserWithCreds:
     u = users_services.create_user(s, body.username, body.global_role, body.email, active=body.active)
     return users_services.user_model_to_user_with_creds(u)
 
 
 @users_router.post("/update")
 def update_user(body: schemas.UpdateUserRequest, user: UserModel = Depends(global_admin),
-                s: Session = Depends(get_session)) -> User:
+                s: Session = Depends(get_session, scope="function")) -> User:
     return users_services.user_model_to_user(
         users_services.update_user(s, body.username, body.global_role, body.email, body.active))
 
 
 @users_router.post("/refresh_token")
 def refresh_token(body: schemas.RefreshTokenRequest, user: UserModel = Depends(authenticated),
-                  s: Session = Depends(get_session)) -> UserWithCreds:
+                  s: Session = Depends(get_session, scope="function")) -> UserWithCreds:
     return users_services.user_model_to_user_with_creds(users_services.refresh_token(s, user, body.username))
 
 
 @users_router.post("/delete")
 def delete_users(body: schemas.DeleteUsersRequest, user: UserModel = Depends(global_admin),
-                 s: Session = Depends(get_session)):
+                 s: Session = Depends(get_session, scope="function")):
     users_services.delete_users(s, user, body.users)
     return {}
 
 
 # ---- projects -------------------------------------------------------------------------------
 @projects_router.post("/list")
-def list_projects(user: UserModel = Depends(authenticated), s: Session = Depends(get_session)) -> List[Project]:
+def list_projects(user: UserModel = Depends(authenticated), s: Session = Depends(get_session, scope="function")) -> List[Project]:
     return [projects_services.project_model_to_project(p) for p in projects_services.list_user_projects(s, user)]
 
 
 @projects_router.post("/create")
 def create_project(body: schemas.CreateProjectRequest, user: UserModel = Depends(authenticated),
-                   s: Session = Depends(get_session)) -> Project:
+                   s: Session = Depends(get_session, scope="function")) -> Project:
     return projects_services.project_model_to_project(projects_services.create_project(s, user, body.project_name))
 
 
 @projects_router.post("/delete")
 def delete_projects(body: schemas.DeleteProjectsRequest, user: UserModel = Depends(authenticated),
-                    s: Session = Depends(get_session)):
+                    s: Session = Depends(get_session, scope="function")):
     projects_services.delete_projects(s, user, body.projects_names)
     return {}
 
@@ -122,7 +122,7 @@ def get_project(up: UP = Depends(project_member)) -> Project:
 
 @projects_router.post("/{project_name}/set_members")
 def set_members(body: schemas.SetProjectMembersRequest, up: UP = Depends(project_manager),
-                s: Session = Depends(get_session)) -> Project:
+                s: Session = Depends(get_session, scope="function")) -> Project:
     projects_services.set_members(s, up[0], up[1], [m.model_dump(mode="json") for m in body.members])
     return projects_services.project_model_to_project(up[1])
 
@@ -142,32 +142,32 @@ def backend_config_values(body: dict) -> dict:
 
 
 @project_backends_router.post("/create")
-def create_backend(body: dict, up: UP = Depends(project_admin), s: Session = Depends(get_session)) -> dict:
+def create_backend(body: dict, up: UP = Depends(project_admin), s: Session = Depends(get_session, scope="function")) -> dict:
     backends_services.create_backend(s, up[1], body)
     return body
 
 
 @project_backends_router.post("/update")
-def update_backend(body: dict, up: UP = Depends(project_admin), s: Session = Depends(get_session)) -> dict:
+def update_backend(body: dict, up: UP = Depends(project_admin), s: Session = Depends(get_session, scope="function")) -> dict:
     backends_services.update_backend(s, up[1], body)
     return body
 
 
 @project_backends_router.post("/delete")
 def delete_backends(body: schemas.DeleteBackendsRequest, up: UP = Depends(project_admin),
-                    s: Session = Depends(get_session)):
+                    s: Session = Depends(get_session, scope="function")):
     backends_services.delete_backends(s, up[1], body.backends_names)
     return {}
 
 
 @project_backends_router.post("/{backend_name}/config_info")
-def backend_config_info(backend_name: str, up: UP = Depends(project_admin), s: Session = Depends(get_session)) -> dict:
+def backend_config_info(backend_name: str, up: UP = Depends(project_admin), s: Session = Depends(get_session, scope="function")) -> dict:
     return backends_services.backend_config_info(s, up[1], backend_name)
 
 
 @project_backends_router.post("/create_yaml")
 def create_backend_yaml(body: schemas.CreateBackendYAMLRequest, up: UP = Depends(project_admin),
-                        s: Session = Depends(get_session)):
+                        s: Session = Depends(get_session, scope="function")):
     cfg = yaml.safe_load(body.config_yaml) or {}
     if not isinstance(cfg, dict):
         raise ServerClientError("backend YAML must be a mapping")
@@ -177,62 +177,62 @@ def create_backend_yaml(body: schemas.CreateBackendYAMLRequest, up: UP = Depends
 
 @project_backends_router.post("/update_yaml")
 def update_backend_yaml(body: schemas.CreateBackendYAMLRequest, up: UP = Depends(project_admin),
-                        s: Session = Depends(get_session)):
+                        s: Session = Depends(get_session, scope="function")):
     backends_services.update_backend(s, up[1], yaml.safe_load(body.config_yaml) or {})
     return {}
 
 
 @project_backends_router.post("/{backend_name}/get_yaml")
-def get_backend_yaml(backend_name: str, up: UP = Depends(project_admin), s: Session = Depends(get_session)) -> dict:
+def get_backend_yaml(backend_name: str, up: UP = Depends(project_admin), s: Session = Depends(get_session, scope="function")) -> dict:
     return {"name": backend_name,
             "config_yaml": yaml.safe_dump(backends_services.backend_config_info(s, up[1], backend_name))}
 
 
 # ---- secrets --------------------------------------------------------------------------------
 @secrets_router.post("/list")
-def list_secrets(up: UP = Depends(project_manager), s: Session = Depends(get_session)):
+def list_secrets(up: UP = Depends(project_manager), s: Session = Depends(get_session, scope="function")):
     return secrets_services.list_secrets(s, up[1])
 
 
 @secrets_router.post("/get")
-def get_secret(body: schemas.GetSecretRequest, up: UP = Depends(project_manager), s: Session = Depends(get_session)):
+def get_secret(body: schemas.GetSecretRequest, up: UP = Depends(project_manager), s: Session = Depends(get_session, scope="function")):
     return secrets_services.get_secret(s, up[1], body.name)
 
 
 @secrets_router.post("/add")
-def add_secret(body: schemas.AddSecretRequest, up: UP = Depends(project_manager), s: Session = Depends(get_session)):
+def add_secret(body: schemas.AddSecretRequest, up: UP = Depends(project_manager), s: Session = Depends(get_session, scope="function")):
     return secrets_services.add_secret(s, up[1], body.name, body.value)
 
 
 @secrets_router.post("/delete")
 def delete_secrets(body: schemas.DeleteSecretsRequest, up: UP = Depends(project_manager),
-                   s: Session = Depends(get_session)):
+                   s: Session = Depends(get_session, scope="function")):
     secrets_services.delete_secrets(s, up[1], body.secrets_names)
     return {}
 
 
 # ---- repos ----------------------------------------------------------------------------------
 @repos_router.post("/list")
-def list_repos(up: UP = Depends(project_member), s: Session = Depends(get_session)) -> List[RepoHead]:
+def list_repos(up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> List[RepoHead]:
     return repos_services.list_repos(s, up[1])
 
 
 @repos_router.post("/get")
-def get_repo(body: schemas.GetRepoRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+def get_repo(body: schemas.GetRepoRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")):
     r = repos_services.get_repo_or_error(s, up[1], body.repo_id)
     creds = repos_services.get_repo_creds(s, r, up[0].id) if body.include_creds else None
     return repos_services.repo_model_to_head(r, creds)
 
 
 @repos_router.post("/init")
-def init_repo(body: schemas.InitRepoRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+def init_repo(body: schemas.InitRepoRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")):
     repos_services.init_repo(s, up[1], up[0], body.repo_id, body.repo_info, body.repo_creds)
     return {}
 
 
 @repos_router.post("/delete")
 def delete_repos(body: schemas.DeleteReposRequest, up: UP = Depends(project_manager),
-                 s: Session = Depends(get_session)):
+                 s: Session = Depends(get_session, scope="function")):
     repos_services.delete_repos(s, up[1], body.repos_ids)
     return {}
 

@@ -47,13 +47,13 @@ pool_router = APIRouter(prefix="/api/project/{project_name}/pool", tags=["pools"
 # ---- runs -----------------------------------------------------------------------------------
 @runs_root.post("/list")
 def list_runs(body: schemas.ListRunsRequest, user: UserModel = Depends(authenticated),
-              s: Session = Depends(get_session)) -> List[Run]:
+              s: Session = Depends(get_session, scope="function")) -> List[Run]:
     return runs_services.list_user_runs(s, user, body.project_name, body.repo_id, body.only_active, body.limit,
                                         body.prev_submitted_at, body.ascending, body.username, body.prev_run_id)
 
 
 @runs_router.post("/get")
-def get_run(body: schemas.GetRunRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> Run:
+def get_run(body: schemas.GetRunRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> Run:
     r = runs_services.get_run(s, up[1], body.run_name, body.id)
     if r is None:
         raise ResourceNotExistsError("Run not found")
@@ -62,30 +62,30 @@ def get_run(body: schemas.GetRunRequest, up: UP = Depends(project_member), s: Se
 
 @runs_router.post("/get_plan")
 def get_run_plan(body: schemas.GetRunPlanRequest, up: UP = Depends(project_member),
-                 s: Session = Depends(get_session)) -> RunPlan:
+                 s: Session = Depends(get_session, scope="function")) -> RunPlan:
     return runs_services.get_plan(s, up[1], up[0], body.run_spec, body.max_offers or 50)
 
 
 @runs_router.post("/apply")
 def apply_plan(body: schemas.ApplyRunPlanRequest, up: UP = Depends(project_member),
-               s: Session = Depends(get_session)) -> Run:
+               s: Session = Depends(get_session, scope="function")) -> Run:
     return runs_services.apply_plan(s, up[1], up[0], body.plan.run_spec, body.plan.current_resource, body.force)
 
 
 @runs_router.post("/submit")
 def submit_run(body: schemas.SubmitRunRequest, up: UP = Depends(project_member),
-               s: Session = Depends(get_session)) -> Run:
+               s: Session = Depends(get_session, scope="function")) -> Run:
     return runs_services.submit_run(s, up[1], up[0], body.run_spec)
 
 
 @runs_router.post("/stop")
-def stop_runs(body: schemas.StopRunsRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+def stop_runs(body: schemas.StopRunsRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")):
     runs_services.stop_runs(s, up[1], body.runs_names, body.abort)
     return {}
 
 
 @runs_router.post("/delete")
-def delete_runs(body: schemas.DeleteRunsRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+def delete_runs(body: schemas.DeleteRunsRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")):
     runs_services.delete_runs(s, up[1], body.runs_names)
     return {}
 
@@ -93,7 +93,7 @@ def delete_runs(body: schemas.DeleteRunsRequest, up: UP = Depends(project_member
 # ---- fleets ---------------------------------------------------------------------------------
 @fleets_root.post("/list")
 def list_all_fleets(body: Optional[schemas.ListFleetsRequest] = None, user: UserModel = Depends(authenticated),
-                    s: Session = Depends(get_session)) -> List[Fleet]:
+                    s: Session = Depends(get_session, scope="function")) -> List[Fleet]:
     out = []
     for p in projects_services.list_user_projects(s, user):
         if body and body.project_name and p.name != body.project_name:
@@ -103,12 +103,12 @@ def list_all_fleets(body: Optional[schemas.ListFleetsRequest] = None, user: User
 
 
 @fleets_router.post("/list")
-def list_fleets(up: UP = Depends(project_member), s: Session = Depends(get_session)) -> List[Fleet]:
+def list_fleets(up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> List[Fleet]:
     return [fleets_services.fleet_model_to_fleet(f) for f in fleets_services.list_project_fleets(s, up[1])]
 
 
 @fleets_router.post("/get")
-def get_fleet(body: schemas.GetFleetRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> Fleet:
+def get_fleet(body: schemas.GetFleetRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> Fleet:
     f = fleets_services.get_fleet_by_name(s, up[1], body.name) if body.name else None
     if f is None:
         raise ResourceNotExistsError("Fleet not found")
@@ -117,26 +117,26 @@ def get_fleet(body: schemas.GetFleetRequest, up: UP = Depends(project_member), s
 
 @fleets_router.post("/get_plan")
 def get_fleet_plan(body: schemas.GetFleetPlanRequest, up: UP = Depends(project_member),
-                   s: Session = Depends(get_session)) -> FleetPlan:
+                   s: Session = Depends(get_session, scope="function")) -> FleetPlan:
     return fleets_services.get_plan(s, up[1], up[0], body.spec)
 
 
 @fleets_router.post("/create")
 def create_fleet(body: schemas.CreateFleetRequest, up: UP = Depends(project_manager),
-                 s: Session = Depends(get_session)) -> Fleet:
+                 s: Session = Depends(get_session, scope="function")) -> Fleet:
     return fleets_services.create_fleet(s, up[1], up[0], body.spec)
 
 
 @fleets_router.post("/delete")
 def delete_fleets(body: schemas.DeleteFleetsRequest, up: UP = Depends(project_manager),
-                  s: Session = Depends(get_session)):
+                  s: Session = Depends(get_session, scope="function")):
     fleets_services.delete_fleets(s, up[1], body.names)
     return {}
 
 
 @fleets_router.post("/delete_instances")
 def delete_fleet_instances(body: schemas.DeleteFleetInstancesRequest, up: UP = Depends(project_manager),
-                           s: Session = Depends(get_session)):
+                           s: Session = Depends(get_session, scope="function")):
     fleets_services.delete_fleet_instances(s, up[1], body.name, body.instance_nums)
     return {}
 
@@ -144,7 +144,7 @@ def delete_fleet_instances(body: schemas.DeleteFleetInstancesRequest, up: UP = D
 # ---- instances / legacy pools ---------------------------------------------------------------
 @instances_root.post("/list")
 def list_instances(body: Optional[schemas.ListInstancesRequest] = None, user: UserModel = Depends(authenticated),
-                   s: Session = Depends(get_session)) -> List[Instance]:
+                   s: Session = Depends(get_session, scope="function")) -> List[Instance]:
     out = []
     for p in projects_services.list_user_projects(s, user):
         if body and body.project_names and p.name not in body.project_names:
@@ -157,50 +157,50 @@ def list_instances(body: Optional[schemas.ListInstancesRequest] = None, user: Us
 
 
 @pools_root.post("/list_instances")
-def pools_list_instances(user: UserModel = Depends(authenticated), s: Session = Depends(get_session)) -> List[Instance]:
+def pools_list_instances(user: UserModel = Depends(authenticated), s: Session = Depends(get_session, scope="function")) -> List[Instance]:
     return list_instances(None, user, s)
 
 
 @pool_router.post("/list")
-def pool_list(up: UP = Depends(project_member), s: Session = Depends(get_session)):
+def pool_list(up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")):
     return pools_services.list_project_pools(s, up[1])
 
 
 @pool_router.post("/show")
 def pool_show(body: Optional[schemas.ShowPoolRequest] = None, up: UP = Depends(project_member),
-              s: Session = Depends(get_session)):
+              s: Session = Depends(get_session, scope="function")):
     return pools_services.show_pool_instances(s, up[1], body.name if body else None)
 
 
 @pool_router.post("/create")
-def pool_create(body: schemas.CreatePoolRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+def pool_create(body: schemas.CreatePoolRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")):
     pools_services.create_pool(s, up[1], body.name)
     return None
 
 
 @pool_router.post("/set_default")
 def pool_set_default(body: schemas.SetDefaultPoolRequest, up: UP = Depends(project_member),
-                     s: Session = Depends(get_session)):
+                     s: Session = Depends(get_session, scope="function")):
     pools_services.set_default_pool(s, up[1], body.pool_name)
     return None
 
 
 @pool_router.post("/delete")
-def pool_delete(body: schemas.DeletePoolRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)):
+def pool_delete(body: schemas.DeletePoolRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")):
     pools_services.delete_pool(s, up[1], body.name)
     return None
 
 
 @pool_router.post("/remove")
 def pool_remove_instance(body: schemas.RemoveInstanceRequest, up: UP = Depends(project_member),
-                         s: Session = Depends(get_session)):
+                         s: Session = Depends(get_session, scope="function")):
     pools_services.remove_instance(s, up[1], body.pool_name, body.instance_name, body.force)
     return None
 
 
 @pool_router.post("/add_remote")
 def pool_add_remote(body: schemas.AddRemoteInstanceRequest, up: UP = Depends(project_member),
-                    s: Session = Depends(get_session)) -> Instance:
+                    s: Session = Depends(get_session, scope="function")) -> Instance:
     if not body.host.strip() or not body.ssh_user.strip() or not body.ssh_keys:
         raise ServerClientError("Host, user or ssh keys are empty")
     return pools_services.add_remote(s, up[1], body.pool_name, body.instance_name, body.instance_network,
@@ -210,7 +210,7 @@ def pool_add_remote(body: schemas.AddRemoteInstanceRequest, up: UP = Depends(pro
 # legacy: get_offers / create_instance live under runs in the reference (routers/runs.py:183-219)
 @runs_router.post("/get_offers")
 def runs_get_offers(body: schemas.GetOffersRequest, up: UP = Depends(project_member),
-                    s: Session = Depends(get_session)):
+                    s: Session = Depends(get_session, scope="function")):
     from dstack_amd.core.models.runs import PoolInstanceOffers
     from dstack_amd.server.services import offers as offers_services
 
@@ -221,14 +221,14 @@ def runs_get_offers(body: schemas.GetOffersRequest, up: UP = Depends(project_mem
 
 @runs_router.post("/create_instance")
 def runs_create_instance(body: schemas.CreateInstanceRequest, up: UP = Depends(project_member),
-                         s: Session = Depends(get_session)) -> Instance:
+                         s: Session = Depends(get_session, scope="function")) -> Instance:
     return fleets_services.create_instance(s, up[1], up[0], body.profile, body.requirements)
 
 
 # ---- volumes --------------------------------------------------------------------------------
 @volumes_root.post("/list")
 def list_all_volumes(body: Optional[schemas.ListVolumesRequest] = None, user: UserModel = Depends(authenticated),
-                     s: Session = Depends(get_session)) -> List[Volume]:
+                     s: Session = Depends(get_session, scope="function")) -> List[Volume]:
     out = []
     for p in projects_services.list_user_projects(s, user):
         if body and body.project_name and p.name != body.project_name:
@@ -238,12 +238,12 @@ def list_all_volumes(body: Optional[schemas.ListVolumesRequest] = None, user: Us
 
 
 @volumes_router.post("/list")
-def list_volumes(up: UP = Depends(project_member), s: Session = Depends(get_session)) -> List[Volume]:
+def list_volumes(up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> List[Volume]:
     return [volumes_services.volume_model_to_volume(v) for v in volumes_services.list_project_volumes(s, up[1])]
 
 
 @volumes_router.post("/get")
-def get_volume(body: schemas.GetVolumeRequest, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> Volume:
+def get_volume(body: schemas.GetVolumeRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> Volume:
     v = volumes_services.get_volume_by_name(s, up[1], body.name)
     if v is None:
         raise ResourceNotExistsError("Volume not found")
@@ -251,32 +251,32 @@ def get_volume(body: schemas.GetVolumeRequest, up: UP = Depends(project_member),
 
 
 @volumes_router.post("/get_plan")
-def get_volume_plan(body: dict, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> VolumePlan:
+def get_volume_plan(body: dict, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> VolumePlan:
     return volumes_services.get_plan(s, up[1], up[0], VolumeSpec.model_validate(body["spec"]))
 
 
 @volumes_router.post("/create")
 def create_volume(body: schemas.CreateVolumeRequest, up: UP = Depends(project_member),
-                  s: Session = Depends(get_session)) -> Volume:
+                  s: Session = Depends(get_session, scope="function")) -> Volume:
     return volumes_services.create_volume(s, up[1], up[0], body.configuration)
 
 
 @volumes_router.post("/delete")
 def delete_volumes(body: schemas.DeleteVolumesRequest, up: UP = Depends(project_member),
-                   s: Session = Depends(get_session)):
+                   s: Session = Depends(get_session, scope="function")):
     volumes_services.delete_volumes(s, up[1], body.names)
     return {}
 
 
 # ---- gateways -------------------------------------------------------------------------------
 @gateways_router.post("/list")
-def list_gateways(up: UP = Depends(project_member), s: Session = Depends(get_session)) -> List[Gateway]:
+def list_gateways(up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> List[Gateway]:
     return [gateways_services.gateway_model_to_gateway(g) for g in gateways_services.list_project_gateways(s, up[1])]
 
 
 @gateways_router.post("/get")
 def get_gateway(body: schemas.GetGatewayRequest, up: UP = Depends(project_member),
-                s: Session = Depends(get_session)) -> Gateway:
+                s: Session = Depends(get_session, scope="function")) -> Gateway:
     g = gateways_services.get_gateway_by_name(s, up[1], body.name)
     if g is None:
         raise ResourceNotExistsError("Gateway not found")
@@ -284,33 +284,33 @@ def get_gateway(body: schemas.GetGatewayRequest, up: UP = Depends(project_member
 
 
 @gateways_router.post("/get_plan")
-def get_gateway_plan(body: dict, up: UP = Depends(project_member), s: Session = Depends(get_session)) -> GatewayPlan:
+def get_gateway_plan(body: dict, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> GatewayPlan:
     return gateways_services.get_plan(s, up[1], up[0], GatewaySpec.model_validate(body["spec"]))
 
 
 @gateways_router.post("/create")
 def create_gateway(body: schemas.CreateGatewayRequest, up: UP = Depends(project_admin),
-                   s: Session = Depends(get_session)) -> Gateway:
+                   s: Session = Depends(get_session, scope="function")) -> Gateway:
     return gateways_services.create_gateway(s, up[1], body.configuration)
 
 
 @gateways_router.post("/delete")
 def delete_gateways(body: schemas.DeleteGatewaysRequest, up: UP = Depends(project_admin),
-                    s: Session = Depends(get_session)):
+                    s: Session = Depends(get_session, scope="function")):
     gateways_services.delete_gateways(s, up[1], body.names)
     return {}
 
 
 @gateways_router.post("/set_default")
 def set_default_gateway(body: schemas.SetDefaultGatewayRequest, up: UP = Depends(project_admin),
-                        s: Session = Depends(get_session)):
+                        s: Session = Depends(get_session, scope="function")):
     gateways_services.set_default_gateway(s, up[1], body.name)
     return {}
 
 
 @gateways_router.post("/set_wildcard_domain")
 def set_wildcard_domain(body: schemas.SetWildcardDomainRequest, up: UP = Depends(project_admin),
-                        s: Session = Depends(get_session)) -> Gateway:
+                        s: Session = Depends(get_session, scope="function")) -> Gateway:
     return gateways_services.set_wildcard_domain(s, up[1], body.name, body.wildcard_domain)
 
 
@@ -338,7 +338,7 @@ def poll_logs(body: schemas.PollLogsRequest, up: UP = Depends(project_member)) -
 
 @metrics_router.get("/job/{run_name}")
 def get_job_metrics(run_name: str, replica_num: int = Query(0), job_num: int = Query(0), limit: int = Query(2),
-                    up: UP = Depends(project_member), s: Session = Depends(get_session)) -> JobMetrics:
+                    up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> JobMetrics:
     run = runs_services.get_run_by_name_or_error(s, up[1], run_name)
     jobs = [j for j in run.jobs if j.replica_num == replica_num and j.job_num == job_num]
     if not jobs:

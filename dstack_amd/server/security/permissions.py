@@ -24,7 +24,7 @@ def _token(request: Request) -> str:
     return auth[7:].strip()
 
 
-def authenticated(request: Request, s: Session = Depends(get_session)) -> UserModel:
+def authenticated(request: Request, s: Session = Depends(get_session, scope="function")) -> UserModel:
     user = get_user_by_token(s, _token(request))
     if user is None or not user.active:
         raise UnauthorizedError()
@@ -50,15 +50,15 @@ def _project_access(project_name: str, user: UserModel, s: Session, roles) -> Tu
 
 
 def project_member(project_name: str, user: UserModel = Depends(authenticated),
-                   s: Session = Depends(get_session)) -> Tuple[UserModel, ProjectModel]:
+                   s: Session = Depends(get_session, scope="function")) -> Tuple[UserModel, ProjectModel]:
     return _project_access(project_name, user, s, (ProjectRole.ADMIN, ProjectRole.MANAGER, ProjectRole.USER))
 
 
 def project_manager(project_name: str, user: UserModel = Depends(authenticated),
-                    s: Session = Depends(get_session)) -> Tuple[UserModel, ProjectModel]:
+                    s: Session = Depends(get_session, scope="function")) -> Tuple[UserModel, ProjectModel]:
     return _project_access(project_name, user, s, (ProjectRole.ADMIN, ProjectRole.MANAGER))
 
 
 def project_admin(project_name: str, user: UserModel = Depends(authenticated),
-                  s: Session = Depends(get_session)) -> Tuple[UserModel, ProjectModel]:
+                  s: Session = Depends(get_session, scope="function")) -> Tuple[UserModel, ProjectModel]:
     return _project_access(project_name, user, s, (ProjectRole.ADMIN,))

@@ -101,6 +101,9 @@ def delete_gateways(s: Session, project: ProjectModel, names: List[str]):
         local = LocalGatewayProcess._instances.pop(f"{project.name}/{g.name}", None)
         if local is not None:
             local.stop()
+        # runs keep their history without the gateway (the reference's ON DELETE SET NULL)
+        s.query(RunModel).filter(RunModel.gateway_id == g.id).update({RunModel.gateway_id: None},
+                                                                       synchronize_session="fetch")
         s.delete(g)
 
 

@@ -597,10 +597,15 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
       if (w == pid) exited = true;
     }
     if (exited) {
-      // drain remaining pty output
-      while (true) {
+      // Drain the pty until read() reports the slave side closed (EIO).  The kernel moves what the
+      // child wrote into the master's buffer from a worker, which under load can run well after
+      // the exit, so "no POLLIN within a few ms" is not the end of the output; read() after
+      // POLLHUP flushes that pending input first.  Bounded: a descendant that keeps the pty open
+      // ends the drain after 1 s of silence (5 s at most).
+      const int64_t drain_end = now_millis() + 5000;
+      while (now_millis() < drain_end) {
         struct pollfd q{master, POLLIN, 0};
-        if (poll(&q, 1, 50) <= 0) break;
+        if (poll(&q, 1, 1000) <= 0) break;
         ssize_t n = read(master, buf, sizeof buf);
         if (n <= 0) break;
         job_logs_.append(std::string(buf, (size_t)n));
