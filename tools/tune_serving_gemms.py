@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--models", default="llama-3-8b,llama-3-70b")
     ap.add_argument("--mode", default="use", choices=["tune", "use", "off"])
     ap.add_argument("--buckets", default="")
+    ap.add_argument("--prefill-m", default="", help="extra row counts, e.g. 16384,32000 (prefill steps)")
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: the e4m3 projections of --quantization fp8 (torch._scaled_mm, row-wise scales; "
@@ -34,6 +35,7 @@ def main():
 
     mode = gemm_tuning.setup(args.mode, kind="serving")
     buckets = [int(b) for b in args.buckets.split(",")] if args.buckets else _buckets(args.max_batch)
+    buckets += [int(m) for m in args.prefill_m.split(",") if m]
     dev = torch.device("cuda")
     out = []
     for name in args.models.split(","):
