@@ -6,9 +6,12 @@
 //  * quant_rows: x [M][K] bf16 -> q [M][K] e4m3 + s [M] fp32 with s = max|x_row| / 448 (dynamic
 //    per-token activation scales; also used once per weight at load time, per output row).
 //  * gemv_fp8: y[m][n] = s_w[n] * sum_k x[m][k] * q[n][k] for M <= 4 rows — the batch-1 decode
-//    weight stream at half the bytes of csrc/gemv.hip.  One wave per output row, 16 weights (16 B)
-//    per lane per load, U loads in flight, XCD-banded rows, fp32 accumulation.
+//    weight stream at half the bytes of csrc/gemv.hip.  One wave per 1, 2 or 4 output rows (the
+//    x slice loaded once per step serves all of them), 16 weights (16 B) per lane per load,
+//    XCD-banded rows, fp32 accumulation.
 #include "common.h"
+
+#include <cstdlib>
 
 using namespace dsa;
 
@@ -122,6 +125,78 @@ __global__ __launch_bounds__(256) void gemv_fp8_kernel(const bf16_t* __restrict_
   }
 }
 
+// R output rows per wave: the x slice a lane loads (16 bf16 = 32 B) is reused for R rows of
+// weights (R x 16 B), so a step issues 2 + R loads for 16 R weight bytes instead of 3 loads for
+// 16 (the one-row form loads twice as many x bytes as weight bytes).
+template <int M, int R, int U>
+__global__ __launch_bounds__(256) void gemv_fp8_rows_kernel(const bf16_t* __restrict__ x, long ldx,
+                                                            const unsigned char* __restrict__ W,
+                                                            const float* __restrict__ sw, bf16_t* __restrict__ y,
+                                                            long ldy, int N, int K) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int per = nwg >> 3, rem = nwg & 7, xcd = b & 7, idx = b >> 3;
+  const int wg = (nwg >= 8) ? xcd * per + (xcd < rem ? xcd : rem) + idx : b;
+  const int row0 = (wg * 4 + wave) * R;
+  if (row0 >= N) return;  // wave-uniform
+  const int nr = min(R, N - row0);
+  float acc[R][M];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+  for (int k0 = lane * 16; k0 < K; k0 += 1024 * U) {
+    u4 wv[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (k0 + 1024 * u < K && r < nr)
+          wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(W + (long)(row0 + r) * K + k0 + 1024 * u));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 1024 * u;
+      if (k >= K) break;
+      float xs[M][16];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const us8 a = *reinterpret_cast<const us8*>(x + m * ldx + k);
+        const us8 c = *reinterpret_cast<const us8*>(x + m * ldx + k + 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xs[m][i] = bf2f(a[i]);
+          xs[m][8 + i] = bf2f(c[i]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r >= nr) break;
+        float w16[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fp8x4_to_f32(wv[u][r][j], w16 + 4 * j);
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[r][m] = fmaf(w16[i], xs[m][i], acc[r][m]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (r >= nr) break;
+    const float scale = sw[row0 + r];
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+    if (lane < M) {
+      float v = acc[r][0];
+#pragma unroll
+      for (int m = 1; m < M; ++m)
+        if (lane == m) v = acc[r][m];
+      y[lane * ldy + row0 + r] = f2bf(v * scale);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" bool dsa_quant_fp8_supported(int K) { return K > 0 && K % 8 == 0; }
@@ -138,6 +213,36 @@ extern "C" bool dsa_gemv_fp8_supported(int M, int K) { return M >= 1 && M <= 4 &
 extern "C" hipError_t dsa_gemv_fp8(const void* x, long ldx, const void* W, const float* sw, void* y, long ldy,
                                    int M, int N, int K, hipStream_t st) {
   if (!dsa_gemv_fp8_supported(M, K) || N <= 0) return hipErrorInvalidValue;
+  // rows per wave (x reuse): the most of 4 / 2 / 1 that still leaves >= 1024 workgroups (4 per CU).
+  // Per Llama-3-70B layer at batch 1: 159 us with one row per wave, 143 us with 4 everywhere,
+  // 142.5 us with this choice (profiles/bench_gemv_fp8_rows_r3f.txt).  DSTACK_AMD_GEMV_FP8_R forces 1 / 2 / 4.
+  static const int forced = [] {
+    const char* v = getenv("DSTACK_AMD_GEMV_FP8_R");
+    return v ? atoi(v) : 0;
+  }();
+  int rows = forced;
+  if (rows != 1 && rows != 2 && rows != 4) rows = N / 16 >= 1024 ? 4 : (N / 8 >= 1024 ? 2 : 1);
+  if (rows == 4 || rows == 2) {
+    const int R = rows, grid = (N + 4 * R - 1) / (4 * R);
+#define DSA_GEMV8R(MM, RR)                                                                                   \
+  gemv_fp8_rows_kernel<MM, RR, 2><<<grid, 256, 0, st>>>((const bf16_t*)x, ldx, (const unsigned char*)W, sw, \
+                                                        (bf16_t*)y, ldy, N, K)
+#define DSA_GEMV8R_M(RR)                \
+  switch (M) {                          \
+    case 1: DSA_GEMV8R(1, RR); break;   \
+    case 2: DSA_GEMV8R(2, RR); break;   \
+    case 3: DSA_GEMV8R(3, RR); break;   \
+    default: DSA_GEMV8R(4, RR); break;  \
+  }
+    if (R == 4) {
+      DSA_GEMV8R_M(4)
+    } else {
+      DSA_GEMV8R_M(2)
+    }
+#undef DSA_GEMV8R_M
+#undef DSA_GEMV8R
+    return hipGetLastError();
+  }
   const int grid = (N + 3) / 4;
 #define DSA_GEMV8(MM)                                                                                 \
   gemv_fp8_kernel<MM, 4><<<grid, 256, 0, st>>>((const bf16_t*)x, ldx, (const unsigned char*)W, sw,   \
