@@ -39,6 +39,9 @@ bool dsa_gemm_tn_supported(int, int, int);
 bool dsa_gemv_supported(int, int);
 hipError_t dsa_gemv(const void*, long, const void*, void*, long, int, int, int, hipStream_t);
 bool dsa_quant_fp8_supported(int);
+bool dsa_rmsnorm_fwd_fp8_supported(int, int);
+hipError_t dsa_rmsnorm_fwd_fp8(const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
+                               hipStream_t);
 hipError_t dsa_quant_fp8_rows(const void*, long, void*, long, float*, int, int, hipStream_t);
 bool dsa_gemv_fp8_supported(int, int);
 hipError_t dsa_gemv_fp8(const void*, long, const void*, const float*, void*, long, int, int, int, hipStream_t);
@@ -85,6 +88,32 @@ std::vector<torch::Tensor> add_rms_norm_fwd(torch::Tensor x, torch::Tensor delta
                         rstd.data_ptr<float>(), rows, D, (float)eps, stream()),
         "add_rms_norm_fwd");
   return {h, y, rstd};
+}
+
+bool rms_norm_fp8_supported(int64_t rows, int64_t D) { return dsa_rmsnorm_fwd_fp8_supported((int)rows, (int)D); }
+
+// (x + delta) -> RMSNorm -> e4m3 [rows, D] (uint8) + per-row scales; returns {h (x + delta, or an
+// empty tensor without delta), q, s}.  Serving decode (rows <= 1024).
+std::vector<torch::Tensor> rms_norm_fp8(torch::Tensor x, c10::optional<torch::Tensor> delta, torch::Tensor w,
+                                        double eps) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  const int rows = x.size(0), D = x.size(1);
+  TORCH_CHECK(dsa_rmsnorm_fwd_fp8_supported(rows, D), "rms_norm_fp8: rows <= 1024, D % 8 == 0, D <= 8192");
+  torch::Tensor h;
+  if (delta.has_value()) {
+    check_bf16(*delta, "delta");
+    TORCH_CHECK(delta->sizes() == x.sizes(), "x/delta shape mismatch");
+    h = torch::empty_like(x);
+  }
+  auto q = torch::empty({rows, D}, x.options().dtype(torch::kUInt8));
+  auto qs = torch::empty({rows}, x.options().dtype(torch::kFloat32));
+  auto rstd = torch::empty({rows}, x.options().dtype(torch::kFloat32));
+  check(dsa_rmsnorm_fwd_fp8(x.data_ptr(), delta.has_value() ? delta->data_ptr() : nullptr, w.data_ptr(),
+                            delta.has_value() ? h.data_ptr() : nullptr, q.data_ptr(), qs.data_ptr<float>(),
+                            rstd.data_ptr<float>(), rows, D, (float)eps, stream()),
+        "rms_norm_fp8");
+  return {delta.has_value() ? h : torch::Tensor(), q, qs};
 }
 
 // dw_out (bf16 [D], optional): write the weight gradient there (accumulating when `accumulate`)
@@ -466,6 +495,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("quant_fp8_rows", &quant_fp8_rows);
+  m.def("rms_norm_fp8", &rms_norm_fp8);
+  m.def("rms_norm_fp8_supported", &rms_norm_fp8_supported);
   m.def("gemv_fp8", &gemv_fp8);
   m.def("gemv_fp8_supported", &gemv_fp8_supported);
   m.def("gemm_tn", &gemm_tn);

@@ -64,15 +64,20 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 // 1 wave per CU at batch 256 (latency-bound: 17 us for 256 x 8192, 1 TB/s); a 256-thread block per
 // row gives every lane 1-4 chunks, issues the weight loads before the reduction, and combines the
 // 4 wave sums through LDS.
-template <int NCH, bool ADD>
+// Q (fp8 serving): instead of the bf16 y, write y as e4m3 bytes with one per-row scale
+// (max|y| / 448) to q_out / qs_out — the activation quantization of the next fp8 GEMM fused in.
+template <int NCH, bool ADD, bool Q = false>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_rowblock_kernel(const bf16_t* __restrict__ x,
                                                                    const bf16_t* __restrict__ delta,
                                                                    const bf16_t* __restrict__ w,
                                                                    bf16_t* __restrict__ h_out,
                                                                    bf16_t* __restrict__ y,
                                                                    float* __restrict__ rstd_out,
-                                                                   int D, float eps) {
+                                                                   int D, float eps,
+                                                                   unsigned char* __restrict__ q_out = nullptr,
+                                                                   float* __restrict__ qs_out = nullptr) {
   __shared__ float part[4];
+  __shared__ float pmax[4];
   const int tid = threadIdx.x, row = blockIdx.x;
   const int nch = D >> 3;
   const size_t base = (size_t)row * D;
@@ -100,14 +105,53 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_rowblock_kernel(const bf16_t*
   __syncthreads();
   ss = part[0] + part[1] + part[2] + part[3];
   const float r = rsqrtf(ss / (float)D + eps);
+  if constexpr (Q) {
+    // y in registers, the row's absmax across the block, then e4m3 bytes (8 per chunk)
+    float amax = 0.f;
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int ch = tid + c * 256;
-    if (ch < nch) {
-      float o[8];
+    for (int c = 0; c < NCH; ++c) {
+      const int ch = tid + c * 256;
+      if (ch < nch) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = v[c][i] * r * wv[c][i];
-      *reinterpret_cast<us8*>(y + base + ch * 8) = pack8(o);
+        for (int i = 0; i < 8; ++i) {
+          v[c][i] = bf2f(f2bf(v[c][i] * r * wv[c][i]));  // the bf16 value the unfused path quantizes
+          amax = fmaxf(amax, fabsf(v[c][i]));
+        }
+      }
+    }
+    amax = wave_max(amax);
+    if ((tid & 63) == 0) pmax[tid >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(pmax[0], pmax[1]), fmaxf(pmax[2], pmax[3]));
+    const float scale = fmaxf(amax, 1e-12f) / 448.f, inv = 1.f / scale;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int ch = tid + c * 256;
+      if (ch < nch) {
+        typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        u2 wq;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const float* o = v[c] + 4 * h2;
+          int wd = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(o[0] * inv, 448.f, -448.f),
+                                                   __builtin_amdgcn_fmed3f(o[1] * inv, 448.f, -448.f), 0, false);
+          wq[h2] = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(o[2] * inv, 448.f, -448.f),
+                                                   __builtin_amdgcn_fmed3f(o[3] * inv, 448.f, -448.f), wd, true);
+        }
+        *reinterpret_cast<u2*>(q_out + base + ch * 8) = wq;
+      }
+    }
+    if (tid == 0) qs_out[row] = scale;
+  } else {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int ch = tid + c * 256;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = v[c][i] * r * wv[c][i];
+        *reinterpret_cast<us8*>(y + base + ch * 8) = pack8(o);
+      }
     }
   }
   if (tid == 0) rstd_out[row] = r;
@@ -721,6 +765,23 @@ extern "C" hipError_t dsa_rmsnorm_fwd(const void* x, const void* delta, const vo
   } else {
     NCH_DISPATCH(D, rmsnorm_fwd_kernel<NCH, false><<<grid, block, 0, st>>>(
         (const bf16_t*)x, nullptr, (const bf16_t*)w, nullptr, (bf16_t*)y, rstd, rows, D, eps));
+  }
+  return hipGetLastError();
+}
+
+// (add +) RMSNorm whose output goes straight to e4m3 with per-row scales (fp8 serving, rows <= 1024)
+extern "C" bool dsa_rmsnorm_fwd_fp8_supported(int rows, int D) { return rows > 0 && rows <= 1024 && D % 8 == 0 && D <= 8192; }
+
+extern "C" hipError_t dsa_rmsnorm_fwd_fp8(const void* x, const void* delta, const void* w, void* h_out, void* q,
+                                          float* qs, float* rstd, int rows, int D, float eps, hipStream_t st) {
+  if (!dsa_rmsnorm_fwd_fp8_supported(rows, D)) return hipErrorInvalidValue;
+  if (delta) {
+    NCH_DISPATCH_BLK(D, rmsnorm_fwd_rowblock_kernel<NCH, true, true><<<rows, 256, 0, st>>>(
+        (const bf16_t*)x, (const bf16_t*)delta, (const bf16_t*)w, (bf16_t*)h_out, nullptr, rstd, D, eps,
+        (unsigned char*)q, qs));
+  } else {
+    NCH_DISPATCH_BLK(D, rmsnorm_fwd_rowblock_kernel<NCH, false, true><<<rows, 256, 0, st>>>(
+        (const bf16_t*)x, nullptr, (const bf16_t*)w, nullptr, nullptr, rstd, D, eps, (unsigned char*)q, qs));
   }
   return hipGetLastError();
 }

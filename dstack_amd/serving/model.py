@@ -55,6 +55,16 @@ class Fp8Weight:
         return self.q.numel() + self.s.numel() * 4
 
 
+class Fp8Act:
+    """Activations already in e4m3 with per-row scales (``q`` uint8 [M, K], ``s`` fp32 [M]),
+    produced by the fused add+RMSNorm->fp8 kernel for the next fp8 GEMM."""
+
+    __slots__ = ("q", "s")
+
+    def __init__(self, q: torch.Tensor, s: torch.Tensor):
+        self.q, self.s = q, s
+
+
 @dataclass
 class RopeScaling:
     """Llama-3.1 "llama3" RoPE frequency scaling (HF ``rope_scaling``)."""
@@ -171,6 +181,8 @@ class ServingLlama:
             _ext.require()
         # DSTACK_AMD_GEMV=0: small decode batches on hipBLASLt too (A/B switch)
         self.gemv = os.environ.get("DSTACK_AMD_GEMV", "1") != "0"
+        # fp8: norms feeding an fp8 GEMM write e4m3 directly (DSTACK_AMD_FP8_FUSE_NORM=0: separate quant)
+        self.fuse_norm_quant = os.environ.get("DSTACK_AMD_FP8_FUSE_NORM", "1") != "0"
         self.cos, self.sin = rope_tables(self.max_model_len + sops.PAGE, self.D, cfg.rope_theta, spec.rope_scaling,
                                          self.device)
         self.layers: list[dict] = []
@@ -385,13 +397,25 @@ class ServingLlama:
     # ------------------------------------------------------------------------------------------
     # fused ops (HIP on the GPU, fp32 references on the CPU)
     # ------------------------------------------------------------------------------------------
-    def _rms(self, x, w):
+    def _fuse_fp8(self, x, w) -> bool:
+        """Whether the norm feeding ``w`` should emit e4m3 directly: an fp8 weight multiplied by
+        hipBLASLt (more than the GEMV's 4 rows) and a row count the fused kernel covers."""
+        return (self.hip and isinstance(w, Fp8Weight) and x.shape[0] > 4 and self.fuse_norm_quant
+                and _ext.require().rms_norm_fp8_supported(x.shape[0], x.shape[1]))
+
+    def _rms(self, x, w, next_w=None):
         if self.hip:
+            if next_w is not None and self._fuse_fp8(x, next_w):
+                _, q, s = _ext.require().rms_norm_fp8(x, None, w, self.cfg.norm_eps)
+                return Fp8Act(q, s)
             return _ext.require().rms_norm_fwd(x, w, self.cfg.norm_eps)[0]
         return ref.rms_norm(x, w, self.cfg.norm_eps)
 
-    def _add_rms(self, x, delta, w):
+    def _add_rms(self, x, delta, w, next_w=None):
         if self.hip:
+            if next_w is not None and self._fuse_fp8(x, next_w):
+                h, q, s = _ext.require().rms_norm_fp8(x, delta, w, self.cfg.norm_eps)
+                return h, Fp8Act(q, s)
             h, y, _ = _ext.require().add_rms_norm_fwd(x, delta, w, self.cfg.norm_eps)
             return h, y
         return ref.add_rms_norm(x, delta, w, self.cfg.norm_eps)
@@ -406,7 +430,7 @@ class ServingLlama:
         (``csrc/gemv.hip``: 6.1-6.8 TB/s on the 70B projections vs hipBLASLt's 5.5-6.2, where it
         wins; at 2-4 rows hipBLASLt is faster, profiles/bench_gemv_r2o.log); larger batches and
         prefill use hipBLASLt."""
-        if isinstance(w, Fp8Weight):
+        if isinstance(w, Fp8Weight) or isinstance(x, Fp8Act):
             return self._mm_fp8(x, w)
         if self.hip and self.gemv and x.shape[0] == 1:
             C = _ext.require()
@@ -418,19 +442,24 @@ class ServingLlama:
         """``x @ (q * s)^T``: up to 4 rows on the fp8 HIP GEMV (half the weight bytes of the bf16
         one); more rows are quantized per token (HIP) and multiplied by hipBLASLt's fp8 GEMM with
         row-wise scales (``torch._scaled_mm``)."""
-        if not self.hip:
-            return ref.fp8_linear(x, w.q.view(torch.float8_e4m3fn), w.s)
-        C = _ext.require()
-        x = x if x.stride(-1) == 1 and x.stride(0) % 8 == 0 else x.contiguous()
-        M = x.shape[0]
-        if self.gemv and C.gemv_fp8_supported(M, x.shape[1]):
-            return C.gemv_fp8(x, w.q, w.s)
+        if isinstance(x, Fp8Act):  # quantized by the fused norm
+            xq, xs = x.q, x.s
+            M = xq.shape[0]
+        else:
+            if not self.hip:
+                return ref.fp8_linear(x, w.q.view(torch.float8_e4m3fn), w.s)
+            C = _ext.require()
+            x = x if x.stride(-1) == 1 and x.stride(0) % 8 == 0 else x.contiguous()
+            M = x.shape[0]
+            if self.gemv and C.gemv_fp8_supported(M, x.shape[1]):
+                return C.gemv_fp8(x, w.q, w.s)
+            xq, xs = C.quant_fp8_rows(x)
         pad = -M % 16  # hipBLASLt's fp8 GEMM wants every dimension a multiple of 16
-        if pad:
-            x = torch.nn.functional.pad(x, (0, 0, 0, pad))
-        xq, xs = C.quant_fp8_rows(x)
+        if pad:  # zero rows (e4m3 0x00 = 0.0) with unit scales
+            xq = torch.nn.functional.pad(xq, (0, 0, 0, pad))
+            xs = torch.nn.functional.pad(xs, (0, pad), value=1.0)
         y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), w.q.view(torch.float8_e4m3fn).t(),
-                             scale_a=xs.view(-1, 1), scale_b=w.s.view(1, -1), out_dtype=x.dtype)
+                             scale_a=xs.view(-1, 1), scale_b=w.s.view(1, -1), out_dtype=self.dtype)
         return y[:M] if pad else y
 
     def _reduce(self, t):
@@ -449,7 +478,7 @@ class ServingLlama:
 
     def _mlp_and_attn_out(self, L, x, o):
         """(x + o @ wo^T) -> norm -> SwiGLU MLP; returns (new residual, mlp output)."""
-        x, h = self._add_rms(x, self._reduce(self._mm(o, L["wo"])), L["ffn_norm"])
+        x, h = self._add_rms(x, self._reduce(self._mm(o, L["wo"])), L["ffn_norm"], next_w=L["wgu"])
         return x, self._reduce(self._mm(self._swiglu(self._mm(h, L["wgu"])), L["wdown"]))
 
     # ------------------------------------------------------------------------------------------
@@ -471,9 +500,9 @@ class ServingLlama:
             bounds.append((int(offsets[i]), int(nxt) - int(offsets[i])))
         for li, L in enumerate(self.layers):
             if delta is None:
-                h = self._rms(x, L["attn_norm"])
+                h = self._rms(x, L["attn_norm"], next_w=L["wqkv"])
             else:
-                x, h = self._add_rms(x, delta, L["attn_norm"])
+                x, h = self._add_rms(x, delta, L["attn_norm"], next_w=L["wqkv"])
             qkv = self._mm(h, L["wqkv"]) if isinstance(L["wqkv"], Fp8Weight) else h @ L["wqkv"].t()
             sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH,
                                   self.k_scale, self.v_scale)
@@ -499,9 +528,9 @@ class ServingLlama:
         delta = None
         for li, L in enumerate(self.layers):
             if delta is None:
-                h = self._rms(x, L["attn_norm"])
+                h = self._rms(x, L["attn_norm"], next_w=L["wqkv"])
             else:
-                x, h = self._add_rms(x, delta, L["attn_norm"])
+                x, h = self._add_rms(x, delta, L["attn_norm"], next_w=L["wqkv"])
             qkv = self._mm(h, L["wqkv"])
             sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH,
                                   self.k_scale, self.v_scale)

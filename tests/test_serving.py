@@ -684,3 +684,26 @@ def test_gpu_fp8_kv_decode_logits_track_bf16(gpu):
         outs.append(logits.float())
     cos = torch.nn.functional.cosine_similarity(outs[0], outs[1], dim=-1).item()
     assert cos > 0.99, cos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_delta", [False, True])
+def test_gpu_rms_norm_fp8_matches_unfused(gpu, with_delta):
+    """The fused (add +) RMSNorm -> e4m3 kernel equals RMSNorm followed by the row quantizer."""
+    from dstack_amd.ops import _ext
+
+    C = _ext.require()
+    g = torch.Generator(device=gpu).manual_seed(3)
+    x = torch.randn(37, 8192, device=gpu, generator=g).bfloat16()
+    d = torch.randn(37, 8192, device=gpu, generator=g).bfloat16()
+    w = (torch.rand(8192, device=gpu, generator=g) + 0.5).bfloat16()
+    if with_delta:
+        h_ref, y_ref, _ = C.add_rms_norm_fwd(x, d, w, 1e-5)
+        h, q, s = C.rms_norm_fp8(x, d, w, 1e-5)
+        assert torch.equal(h, h_ref)
+    else:
+        y_ref = C.rms_norm_fwd(x, w, 1e-5)[0]
+        _, q, s = C.rms_norm_fp8(x, None, w, 1e-5)
+    q_ref, s_ref = C.quant_fp8_rows(y_ref)
+    torch.testing.assert_close(s, s_ref, rtol=1e-6, atol=0)
+    assert (q != q_ref).float().mean().item() < 1e-3
