@@ -2,6 +2,7 @@
 // Objects keep insertion order (small vectors), numbers are stored as double or int64.
 #pragma once
 #include <cmath>
+#include <cstring>
 #include <cstdint>
 #include <cstdio>
 #include <map>
@@ -159,9 +160,11 @@ class Json {
           out += "null";
           break;
         }
-        char buf[32];
+        char buf[40];
         snprintf(buf, sizeof buf, "%.17g", d_);
         out += buf;
+        // keep it a double on re-parse ("-0" or "3" would come back as an integer)
+        if (!strpbrk(buf, ".eE")) out += ".0";
         break;
       }
       case String: escape(s_, out); break;
@@ -332,15 +335,31 @@ class Json {
       i += 4;
       return Json();
     }
+    // RFC 8259 number: -? (0 | [1-9][0-9]*) (. [0-9]+)? ([eE] [+-]? [0-9]+)?
     size_t st = i;
     bool is_float = false;
-    if (i < s.size() && (s[i] == '-' || s[i] == '+')) ++i;
-    while (i < s.size() && ((s[i] >= '0' && s[i] <= '9') || s[i] == '.' || s[i] == 'e' || s[i] == 'E' ||
-                            s[i] == '-' || s[i] == '+')) {
-      if (s[i] == '.' || s[i] == 'e' || s[i] == 'E') is_float = true;
+    auto digits = [&]() {
+      size_t d0 = i;
+      while (i < s.size() && s[i] >= '0' && s[i] <= '9') ++i;
+      return i - d0;
+    };
+    if (i < s.size() && s[i] == '-') ++i;
+    if (i >= s.size() || s[i] < '0' || s[i] > '9') throw std::runtime_error("json: unexpected character");
+    if (s[i] == '0')
       ++i;
+    else
+      digits();
+    if (i < s.size() && s[i] == '.') {
+      ++i;
+      is_float = true;
+      if (digits() == 0) throw std::runtime_error("json: digits expected after '.'");
     }
-    if (st == i) throw std::runtime_error("json: unexpected character");
+    if (i < s.size() && (s[i] == 'e' || s[i] == 'E')) {
+      ++i;
+      is_float = true;
+      if (i < s.size() && (s[i] == '+' || s[i] == '-')) ++i;
+      if (digits() == 0) throw std::runtime_error("json: digits expected in the exponent");
+    }
     std::string num = s.substr(st, i - st);
     if (!is_float) {
       try {

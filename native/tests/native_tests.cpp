@@ -54,6 +54,57 @@ int main() {
     CHECK(threw);
   });
 
+  run("json fuzz", [] {
+    // the agents parse JSON from the network with a hand-written parser.  Feed it
+    // random bytes, truncations and byte flips of valid documents and deep nesting: every input
+    // must either parse (and round-trip) or throw -- never crash, hang or read out of bounds
+    // (the test-asan target runs this under AddressSanitizer).
+    uint64_t st = 0x9e3779b97f4a7c15ULL;
+    auto rnd = [&st]() {
+      st ^= st << 13;
+      st ^= st >> 7;
+      st ^= st << 17;
+      return st;
+    };
+    const std::vector<std::string> seeds = {
+        R"({"a":1,"b":[true,null,"x\u00e9\n"],"c":{"d":-2.5e3,"e":""}})",
+        R"([{"job_spec":{"commands":["echo hi"],"env":{"A":"1"}},"cluster_info":{"job_ips":["10.0.0.1"]}}])",
+        R"({"id":"t","status":"running","ports":[{"container":10999,"host":32000}],"gpus":[0,1]})",
+        "\"\\ud83d\\ude00 surrogate pair\"", "-0.0e-5", "[]", "{}", "123456789012345678901"};
+    const std::string alphabet = "{}[]:,\"\\/ -+.0123456789eEtrufalsn\x00\x7f\xc3\xa9\xff";
+    int parsed = 0, threw = 0;
+    auto attempt = [&](const std::string& in) {
+      try {
+        Json j = Json::parse(in);
+        Json k = Json::parse(j.dump());  // whatever parses must round-trip
+        CHECK(k.dump() == j.dump());
+        ++parsed;
+      } catch (const std::exception&) {
+        ++threw;
+      }
+    };
+    for (int it = 0; it < 20000; ++it) {
+      std::string in;
+      const int mode = (int)(rnd() % 4);
+      if (mode == 0) {  // random bytes from a JSON-ish alphabet
+        const size_t n = rnd() % 64;
+        for (size_t i = 0; i < n; ++i) in.push_back(alphabet[rnd() % alphabet.size()]);
+      } else {
+        in = seeds[rnd() % seeds.size()];
+        if (mode == 1 && !in.empty()) in.resize(rnd() % in.size());  // truncation
+        if (mode == 2)  // byte flips
+          for (int f = 0; f < 3 && !in.empty(); ++f) in[rnd() % in.size()] = (char)(rnd() & 0xff);
+        if (mode == 3 && !in.empty())  // insertions
+          in.insert(rnd() % in.size(), 1, alphabet[rnd() % alphabet.size()]);
+      }
+      attempt(in);
+    }
+    // deep nesting is bounded (no stack overflow): either parsed or rejected
+    attempt(std::string(100000, '[') + std::string(100000, ']'));
+    attempt(std::string(100000, '['));
+    CHECK(parsed > 0 && threw > 0);
+  });
+
   run("base64", [] {
     for (std::string s : {std::string(""), std::string("f"), std::string("fo"), std::string("foo"),
                           std::string("\x00\xff\x10 binary", 10)})
