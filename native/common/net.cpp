@@ -116,10 +116,17 @@ int64_t now_micros() {
 int64_t now_millis() { return now_micros() / 1000; }
 
 std::string url_decode(const std::string& s) {
+  auto hex = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  };
   std::string out;
   for (size_t i = 0; i < s.size(); ++i) {
-    if (s[i] == '%' && i + 2 < s.size()) {
-      out.push_back((char)std::stoi(s.substr(i + 1, 2), nullptr, 16));
+    // a '%' not followed by two hex digits is kept literally instead of throwing from a request thread
+    if (s[i] == '%' && i + 2 < s.size() && hex(s[i + 1]) >= 0 && hex(s[i + 2]) >= 0) {
+      out.push_back((char)(hex(s[i + 1]) * 16 + hex(s[i + 2])));
       i += 2;
     } else if (s[i] == '+') {
       out.push_back(' ');
@@ -242,7 +249,9 @@ static const char* status_text(int s) {
     case 404: return "Not Found";
     case 405: return "Method Not Allowed";
     case 409: return "Conflict";
+    case 411: return "Length Required";
     case 413: return "Payload Too Large";
+    case 431: return "Request Header Fields Too Large";
     case 500: return "Internal Server Error";
     case 503: return "Service Unavailable";
     default: return "Status";
@@ -475,7 +484,44 @@ static void parse_query(const std::string& qs, std::map<std::string, std::string
   }
 }
 
+// Content-Length is 1*DIGIT (RFC 9110 §8.6); anything else (sign, spaces, hex, overflow) is
+// rejected rather than handed to stoull, whose exceptions would end the agent from a worker thread.
+static bool parse_content_length(const std::string& v, size_t& out) {
+  if (v.empty() || v.size() > 18) return false;
+  size_t n = 0;
+  for (char c : v) {
+    if (c < '0' || c > '9') return false;
+    n = n * 10 + (size_t)(c - '0');
+  }
+  out = n;
+  return true;
+}
+
+static constexpr size_t kMaxHeaderBytes = 64 << 10;
+static constexpr size_t kMaxHeaders = 128;
+static constexpr size_t kMaxBody = (size_t)512 << 20;
+
+static void send_error_and_close(int fd, int status, const char* msg) {
+  auto r = HttpResponse::error(status, msg);
+  std::string out = "HTTP/1.1 " + std::to_string(status) + " " + status_text(status) +
+                    "\r\nContent-Length: " + std::to_string(r.body.size()) + "\r\nConnection: close\r\n\r\n" + r.body;
+  send_all(fd, out.data(), out.size());
+}
+
 void HttpServer::handle_conn(int fd, std::string remote) {
+  // A connection thread is detached: nothing may escape it, or std::terminate takes the whole
+  // shim/runner down because of one bad client.
+  try {
+    serve_conn(fd, remote);
+  } catch (const std::exception& e) {
+    LOGW("connection from %s dropped: %s", remote.c_str(), e.what());
+  } catch (...) {
+    LOGW("connection from %s dropped", remote.c_str());
+  }
+  ::close(fd);
+}
+
+void HttpServer::serve_conn(int fd, const std::string& remote) {
   SockReader rd{fd, {}, 0, 120000};
   while (running_) {
     std::string line;
@@ -490,24 +536,39 @@ void HttpServer::handle_conn(int fd, std::string remote) {
     auto qm = target.find('?');
     req.path = qm == std::string::npos ? target : target.substr(0, qm);
     if (qm != std::string::npos) parse_query(target.substr(qm + 1), req.query);
-    bool bad = false;
+    bool bad = false, too_big = false;
+    size_t header_bytes = 0, n_headers = 0;
     while (true) {
       if (!rd.read_line(line)) {
         bad = true;
         break;
       }
       if (line.empty()) break;
+      header_bytes += line.size() + 2;
+      if (++n_headers > kMaxHeaders || header_bytes > kMaxHeaderBytes) {
+        too_big = true;
+        break;
+      }
       auto c = line.find(':');
       if (c != std::string::npos) req.headers[to_lower(trim(line.substr(0, c)))] = trim(line.substr(c + 1));
     }
+    if (too_big) {
+      send_error_and_close(fd, 431, "request headers too large");
+      break;
+    }
     if (bad) break;
+    // Only Content-Length framed bodies: a chunked body would otherwise be read as the next request.
+    if (!req.header("transfer-encoding").empty()) {
+      send_error_and_close(fd, 411, "Transfer-Encoding not supported; send Content-Length");
+      break;
+    }
     size_t clen = 0;
-    if (req.headers.count("content-length")) clen = (size_t)std::stoull(req.headers["content-length"]);
-    if (clen > (size_t)512 << 20) {
-      auto r = HttpResponse::error(413, "body too large");
-      std::string out = "HTTP/1.1 413 Payload Too Large\r\nContent-Length: " + std::to_string(r.body.size()) +
-                        "\r\nConnection: close\r\n\r\n" + r.body;
-      send_all(fd, out.data(), out.size());
+    if (req.headers.count("content-length") && !parse_content_length(req.headers["content-length"], clen)) {
+      send_error_and_close(fd, 400, "invalid Content-Length");
+      break;
+    }
+    if (clen > kMaxBody) {
+      send_error_and_close(fd, 413, "body too large");
       break;
     }
     if (clen > 0 && !rd.read_n(clen, req.body)) break;
@@ -531,7 +592,6 @@ void HttpServer::handle_conn(int fd, std::string remote) {
           LOGW("websocket handler error: %s", e.what());
         }
         if (!ws.closed()) ws.close();
-        ::close(fd);
         return;
       }
     }
@@ -564,7 +624,6 @@ void HttpServer::handle_conn(int fd, std::string remote) {
     out += resp.body;
     if (!send_all(fd, out.data(), out.size()) || !keep_alive) break;
   }
-  ::close(fd);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -663,23 +722,36 @@ HttpClientResponse http_request(const HttpClientRequest& req) {
   };
   if (to_lower(resp.headers["transfer-encoding"]).find("chunked") != std::string::npos) {
     while (rd.read_line(line)) {
-      size_t n = strtoul(line.c_str(), nullptr, 16);
+      char* end = nullptr;
+      unsigned long long n = strtoull(line.c_str(), &end, 16);
+      if (end == line.c_str()) {  // not a chunk-size line
+        resp.error = "malformed chunked body";
+        break;
+      }
       if (n == 0) break;
+      if (n > kMaxBody) {
+        resp.error = "chunk too large";
+        break;
+      }
       std::string chunk;
-      if (!rd.read_n(n, chunk)) break;
+      if (!rd.read_n((size_t)n, chunk)) break;
       if (!emit(chunk)) break;
       rd.read_line(line);  // CRLF after chunk
     }
   } else if (resp.headers.count("content-length")) {
-    size_t n = (size_t)std::stoull(resp.headers["content-length"]);
+    size_t n = 0;
     std::string body;
-    if (n > 0 && rd.read_n(n, body)) emit(body);
+    if (!parse_content_length(resp.headers["content-length"], n) || n > kMaxBody)
+      resp.error = "invalid Content-Length";
+    else if (n > 0 && rd.read_n(n, body))
+      emit(body);
   } else if (resp.status != 204 && resp.status != 101) {
     std::string chunk;
     while (rd.read_some(chunk))
       if (!emit(chunk)) break;
   }
   ::close(fd);
+  if (!resp.error.empty()) resp.status = 0;  // body framing broken: treat as a transport error
   return resp;
 }
 

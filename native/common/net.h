@@ -114,6 +114,7 @@ class HttpServer {
   };
   bool match(const Route& r, const std::string& path, std::map<std::string, std::string>& params) const;
   void handle_conn(int fd, std::string remote);
+  void serve_conn(int fd, const std::string& remote);
   std::string host_;
   int port_;
   std::atomic<int> listen_fd_{-1};

@@ -1,8 +1,13 @@
 // Unit tests for the native agents (reference analogue: runner/internal/**/*_test.go).
 // Build + run: make -C native test
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
 #include <unistd.h>
 
 #include <cstdio>
+#include <random>
 #include <functional>
 #include <map>
 #include <set>
@@ -26,6 +31,41 @@ static int g_failed = 0, g_run = 0;
       ++g_failed;                                                            \
     }                                                                        \
   } while (0)
+
+// Send raw bytes to 127.0.0.1:port, half-close, and return everything the server wrote back
+// before closing (bounded by a 5 s poll so a server that never answers fails the check).
+static std::string raw_exchange(int port, const std::string& data) {
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  struct sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+  if (::connect(fd, (struct sockaddr*)&a, sizeof a) != 0) {
+    ::close(fd);
+    return "<connect failed>";
+  }
+  size_t off = 0;
+  while (off < data.size()) {
+    ssize_t w = ::send(fd, data.data() + off, data.size() - off, MSG_NOSIGNAL);
+    if (w <= 0) break;
+    off += (size_t)w;
+  }
+  ::shutdown(fd, SHUT_WR);
+  std::string out;
+  char buf[4096];
+  while (true) {
+    struct pollfd p{fd, POLLIN, 0};
+    if (::poll(&p, 1, 5000) <= 0) {
+      out += "<timeout>";
+      break;
+    }
+    ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+    if (n <= 0) break;
+    out.append(buf, (size_t)n);
+  }
+  ::close(fd);
+  return out;
+}
 
 static void run(const char* name, const std::function<void()>& fn) {
   int before = g_failed;
@@ -231,6 +271,101 @@ int main() {
     CHECK(http_request(req).status == 404);
     srv.stop();
     th.join();
+  });
+
+  run("http server: malformed requests get an error or a close, never a crash", [] {
+    HttpServer srv("127.0.0.1", 0);
+    srv.route("POST", "/echo", [](HttpRequest& r) {
+      Json j = Json::object();
+      j.set("body", r.body);
+      return HttpResponse::json(j);
+    });
+    CHECK(srv.start() > 0);
+    std::thread th([&] { srv.serve_forever(); });
+    const int port = srv.port();
+    CHECK(url_decode("a%41%zz%4") == "aA%zz%4" && url_decode("x+y%2f") == "x y/");
+    auto status_of = [](const std::string& resp) { return resp.rfind("HTTP/1.1 ", 0) == 0 ? atoi(resp.c_str() + 9) : 0; };
+    CHECK(status_of(raw_exchange(port, "POST /echo HTTP/1.1\r\nContent-Length: abc\r\n\r\n")) == 400);
+    CHECK(status_of(raw_exchange(port, "POST /echo HTTP/1.1\r\nContent-Length: -1\r\n\r\n")) == 400);
+    CHECK(status_of(raw_exchange(port, "POST /echo HTTP/1.1\r\nContent-Length: 99999999999999999999999\r\n\r\n")) == 400);
+    CHECK(status_of(raw_exchange(port, "POST /echo HTTP/1.1\r\nContent-Length: 999999999999\r\n\r\n")) == 413);
+    CHECK(status_of(raw_exchange(port, "POST /echo HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n")) == 411);
+    std::string many = "GET /echo HTTP/1.1\r\n";
+    for (int k = 0; k < 200; ++k) many += "X-H" + std::to_string(k) + ": v\r\n";
+    CHECK(status_of(raw_exchange(port, many + "\r\n")) == 431);
+    CHECK(status_of(raw_exchange(port, "GET /echo HTTP/1.1\r\nX: " + std::string(100000, 'a') + "\r\n\r\n")) == 431);
+    // truncated: the server gets EOF mid-request and just closes
+    CHECK(raw_exchange(port, "POST /echo HTTP/1.1\r\nContent-Length: 10\r\n\r\nabc").empty());
+    CHECK(raw_exchange(port, "POST /echo HTTP/1.1\r\nHost: x").empty());
+    CHECK(raw_exchange(port, "garbage-without-spaces\r\n\r\n").empty());
+    // random bytes, and random byte flips of a valid request
+    std::mt19937 rng(7);
+    const std::string valid = "POST /echo?x=%zz&y HTTP/1.1\r\nContent-Length: 4\r\nConnection: close\r\n\r\nbody";
+    for (int it = 0; it < 300; ++it) {
+      std::string s;
+      if (it % 2) {
+        s.resize(rng() % 200);
+        for (auto& c : s) c = (char)(rng() % 256);
+      } else {
+        s = valid;
+        for (int f = 0; f < 1 + (int)(rng() % 4); ++f) s[rng() % s.size()] = (char)(rng() % 256);
+      }
+      std::string r = raw_exchange(port, s);
+      CHECK(r.find("<timeout>") == std::string::npos);
+    }
+    // still serving after all of that
+    CHECK(status_of(raw_exchange(port, valid)) == 200);
+    HttpClientRequest req;
+    req.method = "POST";
+    req.port = port;
+    req.path = "/echo";
+    req.body = "ok";
+    CHECK(http_request(req).ok());
+    srv.stop();
+    th.join();
+  });
+
+  run("http client: malformed responses are transport errors", [] {
+    // a one-shot server written with raw sockets that answers with a fixed byte string
+    auto serve_once = [](const std::string& reply, int& port_out) {
+      int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+      struct sockaddr_in a{};
+      a.sin_family = AF_INET;
+      inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+      ::bind(lfd, (struct sockaddr*)&a, sizeof a);
+      ::listen(lfd, 1);
+      socklen_t len = sizeof a;
+      getsockname(lfd, (struct sockaddr*)&a, &len);
+      port_out = ntohs(a.sin_port);
+      return std::thread([lfd, reply] {
+        int fd = ::accept(lfd, nullptr, nullptr);
+        char buf[4096];
+        ::recv(fd, buf, sizeof buf, 0);
+        ::send(fd, reply.data(), reply.size(), MSG_NOSIGNAL);
+        ::shutdown(fd, SHUT_WR);
+        ::close(fd);
+        ::close(lfd);
+      });
+    };
+    auto get = [&](const std::string& reply) {
+      int port = 0;
+      std::thread t = serve_once(reply, port);
+      HttpClientRequest req;
+      req.port = port;
+      req.timeout_ms = 5000;
+      auto r = http_request(req);
+      t.join();
+      return r;
+    };
+    CHECK(get("HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\nok").body == "ok");
+    auto bad_len = get("HTTP/1.1 200 OK\r\nContent-Length: x1\r\n\r\nok");
+    CHECK(!bad_len.ok() && !bad_len.error.empty());
+    auto bad_chunk = get("HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\nok\r\n0\r\n\r\n");
+    CHECK(!bad_chunk.ok() && bad_chunk.error == "malformed chunked body");
+    auto huge_chunk = get("HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nffffffffffff\r\nok\r\n");
+    CHECK(!huge_chunk.ok() && huge_chunk.error == "chunk too large");
+    auto good_chunk = get("HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n2\r\nok\r\n1;ext=1\r\n!\r\n0\r\n\r\n");
+    CHECK(good_chunk.ok() && good_chunk.body == "ok!");
   });
 
   run("volumes: aws nvme serial / xvd mapping / local dirs / refcounted unmount", [] {
