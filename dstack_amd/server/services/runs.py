@@ -36,7 +36,7 @@ from dstack_amd.server.services import jobs as jobs_services
 from dstack_amd.server.services import offers as offers_services
 from dstack_amd.server.services import pools as pools_services
 from dstack_amd.server.services import repos as repos_services
-from dstack_amd.server.services.locking import db_advisory_lock
+from dstack_amd.server.services.locking import db_advisory_lock, lockset
 from dstack_amd.utils.common import generate_name, get_current_datetime
 
 logger = logging.getLogger(__name__)
@@ -252,17 +252,23 @@ def _updatable(old: RunSpec, new: RunSpec) -> bool:
 
 
 def stop_runs(s: Session, project: ProjectModel, runs_names: List[str], abort: bool):
+    """Mark the runs TERMINATING (``S/services/runs.py:stop_runs``).
+
+    The runs are held in the background processor's ``runs`` lockset (and row-locked on Postgres)
+    and the change is committed before they are released: otherwise a ``process_runs`` pass that
+    loaded a run just before the stop (e.g. while it was provisioning) writes its own status
+    transition back over TERMINATING, and the run keeps running with a termination reason set."""
     reason = RunTerminationReason.ABORTED_BY_USER if abort else RunTerminationReason.STOPPED_BY_USER
-    for name in runs_names:
-        run = get_run_model(s, project, name)
-        if run is None:
-            continue
-        if RunStatus(run.status).is_finished():
-            continue
-        run.status = RunStatus.TERMINATING.value
-        run.termination_reason = reason.value
-        run.last_processed_at = get_current_datetime()
-    s.flush()
+    runs = [r for r in (get_run_model(s, project, name) for name in runs_names) if r is not None]
+    with lockset("runs").hold([r.id for r in runs], timeout=60.0):
+        for run in runs:
+            s.refresh(run, with_for_update=True)  # the state the last background pass committed
+            if RunStatus(run.status).is_finished():
+                continue
+            run.status = RunStatus.TERMINATING.value
+            run.termination_reason = reason.value
+            run.last_processed_at = get_current_datetime()
+        s.commit()
     scheduler.wake(scheduler.RUNS)
 
 

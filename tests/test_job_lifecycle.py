@@ -428,6 +428,42 @@ def test_graceful_stop_stops_runner_then_terminates(db):
         assert s.get(InstanceModel, iid).status == InstanceStatus.IDLE.value
 
 
+def test_stop_is_not_overwritten_by_a_concurrent_run_pass(db):
+    """A ``process_runs`` pass that loaded the run before the stop and commits a status transition
+    after it must not write over TERMINATING: stop_runs waits for the pass to release the run."""
+    import threading
+    import time
+
+    from dstack_amd.server.services.locking import lockset
+
+    with session_scope() as s:
+        rid = _submit(s, {"type": "task", "commands": ["sleep infinity"]})
+        s.get(RunModel, rid).status = RunStatus.PROVISIONING.value
+    loaded, done = threading.Event(), threading.Event()
+
+    def background_pass():  # what claim_and_process + _process_active do, stretched out in time
+        with lockset("runs").hold([rid]):
+            with session_scope() as s:
+                run = s.get(RunModel, rid)
+                assert run.status == RunStatus.PROVISIONING.value
+                loaded.set()
+                time.sleep(0.3)  # the stop request arrives meanwhile
+                run.status = RunStatus.RUNNING.value
+        done.set()
+
+    t = threading.Thread(target=background_pass)
+    t.start()
+    assert loaded.wait(5)
+    with session_scope() as s:
+        runs_services.stop_runs(s, s.get(RunModel, rid).project, ["run1"], abort=False)
+    assert done.is_set()  # the stop waited for the pass instead of racing it
+    t.join(5)
+    with session_scope() as s:
+        run = s.get(RunModel, rid)
+        assert run.status == RunStatus.TERMINATING.value
+        assert run.termination_reason == "stopped_by_user"
+
+
 def test_abort_skips_graceful_stop(db):
     agents = Agents(final_state=None)
     with session_scope() as s:
