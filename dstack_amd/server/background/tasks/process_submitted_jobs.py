@@ -41,7 +41,7 @@ from dstack_amd.server.services import offers as offers_services
 from dstack_amd.server.services import pools as pools_services
 from dstack_amd.server.services import runs as runs_services
 from dstack_amd.server.services.jobs import volumes as job_volumes
-from dstack_amd.server.services.locking import lockset
+from dstack_amd.server.services.locking import lockset, release_at_transaction_end
 from dstack_amd.server.services.topology import busy_set, pick_gpus
 from dstack_amd.utils.common import get_current_datetime
 
@@ -184,6 +184,7 @@ def _assign_pool_instance(s: Session, run: RunModel, job: JobModel, spec, profil
     for inst, shared in cands:
         if not ls.try_add_many([inst.id]):
             continue
+        assigned = False
         try:
             s.refresh(inst)
             shared = pools_services.get_instance_shared_offer(inst, spec.requirements)
@@ -211,9 +212,13 @@ def _assign_pool_instance(s: Session, run: RunModel, job: JobModel, spec, profil
             if run.fleet_id is None:
                 run.fleet_id = inst.fleet_id
             s.flush()
+            assigned = True
             return True
         finally:
-            ls.remove_many([inst.id])
+            if assigned:  # BUSY must be committed before another thread may re-read the instance
+                release_at_transaction_end(s, ls, [inst.id])
+            else:
+                ls.remove_many([inst.id])
     return False
 
 

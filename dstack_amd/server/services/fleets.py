@@ -3,13 +3,14 @@ instances, optionally in a placement group; SSH: one instance per host), delete,
 
 from __future__ import annotations
 
+import contextlib
 import json
 import re
 import uuid
 from typing import List, Optional
 
 from sqlalchemy import select
-from sqlalchemy.orm import Session
+from sqlalchemy.orm import Session, object_session
 
 from dstack_amd.core.errors import ResourceExistsError, ResourceNotExistsError, ServerClientError
 from dstack_amd.core.models.backends import BackendType
@@ -33,7 +34,7 @@ from dstack_amd.server.background import scheduler
 from dstack_amd.server.models import FleetModel, InstanceModel, ProjectModel, UserModel
 from dstack_amd.server.services import offers as offers_services
 from dstack_amd.server.services import pools as pools_services
-from dstack_amd.server.services.locking import db_advisory_lock
+from dstack_amd.server.services.locking import db_advisory_lock, lockset
 from dstack_amd.utils.common import generate_name, get_current_datetime
 
 
@@ -190,19 +191,28 @@ def create_autocreated_fleet(s: Session, project: ProjectModel, run_name: str, p
 
 
 def delete_fleets(s: Session, project: ProjectModel, names: List[str]):
+    """Fleets and their instances are held in the background processors' locksets while their
+    state is re-read, checked and changed, and committed before release: a job assigned to an
+    instance (IDLE -> BUSY) or an instance pass (PROVISIONING -> IDLE) racing the delete can then
+    neither slip past the busy check nor write over TERMINATING."""
+    fleets = []
     for name in names:
         f = get_fleet_by_name(s, project, name)
         if f is None:
             raise ResourceNotExistsError(f"Fleet {name} not found")
-        busy = [i for i in f.instances if i.status == InstanceStatus.BUSY.value]
-        if busy:
-            raise ServerClientError(f"Fleet {name} has busy instances; stop the runs first")
-        for inst in f.instances:
-            if inst.status not in (InstanceStatus.TERMINATING.value, InstanceStatus.TERMINATED.value):
-                inst.status = InstanceStatus.TERMINATING.value
-                inst.termination_reason = "fleet deleted"
-        f.status = FleetStatus.TERMINATING.value
-    s.flush()
+        fleets.append(f)
+    with _held(fleets, [i for f in fleets for i in f.instances]):
+        for f in fleets:
+            busy = [i for i in f.instances if i.status == InstanceStatus.BUSY.value]
+            if busy:
+                raise ServerClientError(f"Fleet {f.name} has busy instances; stop the runs first")
+        for f in fleets:
+            for inst in f.instances:
+                if inst.status not in (InstanceStatus.TERMINATING.value, InstanceStatus.TERMINATED.value):
+                    inst.status = InstanceStatus.TERMINATING.value
+                    inst.termination_reason = "fleet deleted"
+            f.status = FleetStatus.TERMINATING.value
+        s.commit()
     scheduler.wake(scheduler.INSTANCES, scheduler.FLEETS)
 
 
@@ -210,17 +220,28 @@ def delete_fleet_instances(s: Session, project: ProjectModel, name: str, instanc
     f = get_fleet_by_name(s, project, name)
     if f is None:
         raise ResourceNotExistsError(f"Fleet {name} not found")
-    for inst in f.instances:
-        if inst.instance_num in instance_nums:
+    targets = [i for i in f.instances if i.instance_num in instance_nums]
+    with _held([], targets):
+        for inst in targets:
             if inst.status == InstanceStatus.BUSY.value:
                 raise ServerClientError(f"Instance {inst.name} is busy")
+        for inst in targets:
             inst.status = InstanceStatus.TERMINATING.value
             inst.termination_reason = "deleted by user"
-    s.flush()
+        s.commit()
     scheduler.wake(scheduler.INSTANCES)
 
 
-_ = (Duration, Env, InstanceModel)
+@contextlib.contextmanager
+def _held(fleets, instances, timeout: float = 60.0):
+    """Hold fleets and instances in their background locksets and re-read them (row-locked on
+    Postgres) so the block sees the state the last background pass committed."""
+    with lockset("fleets").hold([f.id for f in fleets], timeout), \
+            lockset("instances").hold([i.id for i in instances], timeout):
+        for obj in [*fleets, *instances]:
+            sess = object_session(obj)
+            sess.refresh(obj, with_for_update=True)
+        yield
 
 
 def create_instance(s: Session, project: ProjectModel, user: UserModel, profile: Profile,

@@ -70,6 +70,26 @@ class Lockset:
             self.remove_many(keys)
 
 
+def release_at_transaction_end(s: Session, ls: Lockset, keys: Iterable[Hashable]):
+    """Keep ``keys`` (already held in ``ls``) until ``s``'s transaction commits or rolls back.
+
+    A status change made under an in-process lock must be committed before the lock is released:
+    released at flush time, another thread can re-read the still-committed old row and write its
+    own transition over the change when it commits after it."""
+    keys = list(keys)
+    from sqlalchemy import event
+
+    released = []
+
+    def _release(_session):
+        if not released:  # whichever of the two events comes first; a later one must not
+            released.append(True)  # release keys another thread has claimed since
+            ls.remove_many(keys)
+
+    event.listen(s, "after_commit", _release, once=True)
+    event.listen(s, "after_rollback", _release, once=True)
+
+
 class ResourceLocker:
     def __init__(self):
         self._locksets: Dict[str, Lockset] = defaultdict(Lockset)

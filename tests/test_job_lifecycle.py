@@ -464,6 +464,50 @@ def test_stop_is_not_overwritten_by_a_concurrent_run_pass(db):
         assert run.termination_reason == "stopped_by_user"
 
 
+def test_fleet_delete_waits_for_a_concurrent_job_assignment(db):
+    """An instance being assigned to a job (IDLE -> BUSY, committed after the assignment's flush)
+    must not be terminated by a fleet delete that read it as IDLE: the delete waits and refuses."""
+    import threading
+    import time
+    import uuid
+
+    from dstack_amd.core.errors import ServerClientError
+    from dstack_amd.server.models import FleetModel
+    from dstack_amd.server.services import fleets as fleets_services
+    from dstack_amd.server.services.locking import lockset, release_at_transaction_end
+
+    with session_scope() as s:
+        iid, _ = _remote_instance(s, "node-race")
+        project = s.query(ProjectModel).filter_by(name="main").one()
+        fleet = FleetModel(id=uuid.uuid4(), name="f-race", project_id=project.id, status="active", spec="{}")
+        s.add(fleet)
+        s.flush()
+        s.get(InstanceModel, iid).fleet_id = fleet.id
+    loaded = threading.Event()
+
+    def assignment():  # _assign_pool_instance: lock, mark BUSY, flush; the job pass commits later
+        ls = lockset("instances")
+        assert ls.try_add_many([iid])
+        with session_scope() as s:
+            s.get(InstanceModel, iid).status = InstanceStatus.BUSY.value
+            s.flush()
+            release_at_transaction_end(s, ls, [iid])
+            loaded.set()
+            time.sleep(0.3)
+            assert iid in ls  # still held between flush and commit
+        assert iid not in ls  # released by the commit
+
+    t = threading.Thread(target=assignment)
+    t.start()
+    assert loaded.wait(5)
+    with pytest.raises(ServerClientError, match="busy"):
+        with session_scope() as s:
+            fleets_services.delete_fleets(s, s.query(ProjectModel).filter_by(name="main").one(), ["f-race"])
+    t.join(5)
+    with session_scope() as s:
+        assert s.get(InstanceModel, iid).status == InstanceStatus.BUSY.value
+
+
 def test_abort_skips_graceful_stop(db):
     agents = Agents(final_state=None)
     with session_scope() as s:
