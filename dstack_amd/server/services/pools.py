@@ -251,13 +251,21 @@ def remove_instance(s: Session, project: ProjectModel, pool_name: str, instance_
     pool = get_pool(s, project, pool_name)
     if pool is None:
         raise ResourceNotExistsError("Pool not found")
+    from dstack_amd.server.services.locking import lockset
+
+    named = [i for i in _pool_instances(pool) if i.name == instance_name]
     done = False
-    for inst in _pool_instances(pool):
-        if inst.name == instance_name and (force or not inst.jobs):
-            inst.status = InstanceStatus.TERMINATING.value
-            done = True
-    if not done:
-        raise ResourceNotExistsError("Could not find instance to terminate")
+    # held in the instances lockset and committed inside, like the fleet deletes: a job assigned
+    # to the instance meanwhile (its lock is kept until that assignment commits) is seen here
+    with lockset("instances").hold([i.id for i in named], timeout=60.0):
+        for inst in named:
+            s.refresh(inst, with_for_update=True)
+            if force or not inst.jobs:
+                inst.status = InstanceStatus.TERMINATING.value
+                done = True
+        if not done:
+            raise ResourceNotExistsError("Could not find instance to terminate")
+        s.commit()
     scheduler.wake(scheduler.INSTANCES)
 
 
