@@ -125,6 +125,33 @@ def _attached_instance_ids(s: Session, v: VolumeModel) -> List:
                           .where(volumes_attachments.c.volume_id == v.id)).scalars())
 
 
+def _hold_volume(s: Session, v: VolumeModel, timeout: float = 10.0):
+    """Hold ``v`` in the volumes lockset until ``s`` commits, then re-read it: a concurrent
+    ``delete_volumes`` (which holds the same lock and commits inside) either finishes first, and the
+    attach sees ``deleted``, or waits and sees the attachment."""
+    import time
+
+    from dstack_amd.server.services.locking import lockset, release_at_transaction_end
+
+    held = s.info.get("held_volumes")
+    if held is None:  # volumes this transaction holds; forgotten when it ends (the locks go too)
+        from sqlalchemy import event
+
+        held = s.info["held_volumes"] = set()
+        for name in ("after_commit", "after_rollback"):
+            event.listen(s, name, lambda _s: s.info.pop("held_volumes", None), once=True)
+    if v.id not in held:
+        ls = lockset("volumes")
+        deadline = time.monotonic() + timeout
+        while not ls.add_all_or_nothing([v.id]):
+            if time.monotonic() > deadline:
+                raise ServerClientError(f"Volume {v.name} is busy")
+            time.sleep(0.005)
+        held.add(v.id)
+        release_at_transaction_end(s, ls, [v.id])
+    s.refresh(v, with_for_update=True)
+
+
 def attach_job_volumes(s: Session, job: JobModel, inst: InstanceModel,
                        volumes: Sequence[Sequence[VolumeModel]]) -> List[str]:
     """Attach the matching alternative of every mount point to ``inst``; returns the attached
@@ -141,6 +168,9 @@ def attach_job_volumes(s: Session, job: JobModel, inst: InstanceModel,
         v = next((x for x in cands if _backend_region(x) == (backend, inst.region)), None)
         if v is None:
             raise ServerClientError(f"No volume among {[x.name for x in cands]} in {backend.value}/{inst.region}")
+        _hold_volume(s, v)
+        if v.deleted:
+            raise ServerClientError(f"Volume {v.name} was deleted")
         attached = _attached_instance_ids(s, v)
         if inst.id in attached:
             names.append(v.name)

@@ -74,10 +74,26 @@ def create_volume(s: Session, project: ProjectModel, user: UserModel, conf: Volu
 
 
 def delete_volumes(s: Session, project: ProjectModel, names: List[str]):
+    """Held in the volumes lockset and committed inside, so a job attaching a volume concurrently
+    (``jobs.volumes.attach_job_volumes``, same lock) cannot slip past the attachment check."""
+    from dstack_amd.server.services.locking import lockset
+
+    vols = []
     for n in names:
         v = get_volume_by_name(s, project, n)
         if v is None:
             raise ResourceNotExistsError(f"Volume {n} not found")
+        vols.append(v)
+    with lockset("volumes").hold([v.id for v in vols], timeout=60.0):
+        for v in vols:
+            s.refresh(v, with_for_update=True)
+        _delete_volumes_locked(s, project, vols)
+        s.commit()
+
+
+def _delete_volumes_locked(s: Session, project: ProjectModel, vols):
+    for v in vols:
+        n = v.name
         if v.instances:
             raise ServerClientError(f"Volume {n} is attached to an instance")
         conf = VolumeConfiguration.model_validate_json(v.configuration)

@@ -183,3 +183,41 @@ def test_external_volume_not_formatted_and_attach_failure_is_volume_error(db):
 
     with session_scope() as s:
         assert shim_volume_specs(s, s.get(JobModel, jid), ["data"])[0]["init_fs"] is False
+
+
+
+def test_volume_attach_waits_for_a_concurrent_delete(db):
+    """A delete holds the volume (volumes lockset) until it commits: an attach arriving while the
+    cloud delete is in progress waits, then re-reads the volume and sees it deleted (the attach
+    path then refuses it) instead of attaching a volume that is being deleted."""
+    import threading
+    import time
+
+    from dstack_amd.server.services import backends as backends_services
+    from dstack_amd.server.services import volumes as volumes_services
+    from dstack_amd.server.services.jobs.volumes import _hold_volume
+
+    with session_scope() as s:
+        vid = _volume(s)
+    deleting = threading.Event()
+    seen = {}
+
+    def slow_delete(_vol):
+        deleting.set()
+        time.sleep(0.3)
+
+    def attach():
+        assert deleting.wait(5)
+        with session_scope() as s:
+            v = s.get(VolumeModel, vid)
+            _hold_volume(s, v)
+            seen["deleted"] = v.deleted
+
+    compute = mock.Mock()
+    compute.delete_volume.side_effect = slow_delete
+    t = threading.Thread(target=attach)
+    t.start()
+    with mock.patch.object(backends_services, "get_project_backend", return_value=compute), session_scope() as s:
+        volumes_services.delete_volumes(s, s.query(ProjectModel).filter_by(name="main").one(), ["data"])
+    t.join(5)
+    assert seen == {"deleted": True}
