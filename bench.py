@@ -2,7 +2,9 @@
 """Headline benchmark: tokens/sec of the Llama-3-8B training task (BASELINE.json metric).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched under
-``torch.distributed.run`` with one rank per GPU (RCCL over xGMI).  W untimed warmup steps, then
+``torch.distributed.run`` with one rank per GPU (RCCL over xGMI).  Started for N>1 WITHOUT a
+launcher (no ``WORLD_SIZE``), it starts ``torch.distributed.run`` itself as a child process; a
+``WORLD_SIZE`` that differs from ``--gpus`` is an error (exit 2), never a silently smaller run.  W untimed warmup steps, then
 exactly K timed steps bracketed by barrier + ``torch.cuda.synchronize()``; the elapsed time is the
 MAX over ranks; rank 0 prints one JSON line.  Every timed step is a full training step: forward,
 backward, ZeRO-1 reduce-scatter, fused AdamW, all-gather.
@@ -45,6 +47,44 @@ def _cold_start(timeout: float = 180.0) -> dict:
         return {"error": str(e)[:300]}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n: int, argv: list) -> int:
+    """``bench.py --gpus N`` (N>1) started without a launcher: run N ranks under
+    ``torch.distributed.run`` as a CHILD process (nothing here has touched the GPU, and no exec
+    replaces this process), forward its output, and return its exit code.  Rank 0's JSON line must
+    report ``n_gpus == N``; anything else is an error, never a silent 1-GPU number."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, DSTACK_AMD_BENCH_CHILD="1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    result = None
+    for line in proc.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        if line.startswith("{"):
+            try:
+                result = json.loads(line)
+            except ValueError:
+                pass
+    rc = proc.wait()
+    if rc != 0:
+        return rc
+    if result is None or result.get("n_gpus") != n:
+        print(f"error: expected a result line with n_gpus={n}, got {result and result.get('n_gpus')}",
+              file=sys.stderr)
+        return 3
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,9 +101,12 @@ def main():
     ap.add_argument("--no-coldstart", action="store_true", help="skip the dstack-apply cold-start half")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_self_launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required", file=sys.stderr)
+        sys.exit(2)
 
     cold = None
     if not args.no_coldstart and int(os.environ.get("RANK", "0")) == 0:
@@ -73,6 +116,9 @@ def main():
 
     env, tr, res = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup, log_every=0,
                        grad_accum=args.grad_accum)
+    if env.world != args.gpus:
+        print(f"error: joined a group of {env.world} ranks, --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     if env.rank == 0:
         import torch
 
@@ -111,9 +157,9 @@ def main():
             out["cold_start"] = {k: cold.get(k) for k in ("running_p50_s", "first_run_s", "runs", "ok", "error")
                                  if cold.get(k) is not None}
         print(json.dumps(out), flush=True)
-    if env.distributed:
-        import torch.distributed as dist
+    import torch.distributed as dist
 
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

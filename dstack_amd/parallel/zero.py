@@ -62,6 +62,7 @@ class ZeroOptimizer:
         group: dist.ProcessGroup | None = None,
         overlap: bool = True,
         overlap_update: bool = True,
+        force_collectives: bool | None = None,
     ):
         self.model = model
         self.lr = lr
@@ -72,7 +73,16 @@ class ZeroOptimizer:
         self.distributed = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
-        self.overlap = overlap and self.world > 1
+        import os
+
+        # debug/validation switch: issue the real reduce-scatter / all-gather even in a 1-rank
+        # group (a valid 1-rank RCCL communicator), so the exact collective code path of an
+        # 8-GPU job -- in-place RS/AG on RCCL's stream, joined from the side stream and the
+        # prefetch hooks -- can run and be checked on a single-GPU box
+        if force_collectives is None:
+            force_collectives = os.environ.get("DSTACK_AMD_ZERO_FORCE_COLLECTIVES", "0") not in ("0", "", "false")
+        self.collectives = self.distributed and (self.world > 1 or force_collectives)
+        self.overlap = overlap and self.collectives
         self.step_count = 0
         # optimizer-in-backward: a bucket whose final gradients are complete is reduce-scattered,
         # updated (AdamW on its shard) and all-gathered on a side stream while backward keeps
@@ -129,8 +139,6 @@ class ZeroOptimizer:
             if used < b.numel:
                 self._pads.append((b.start + used, b.numel - used))
         self._side = None
-        import os
-
         if os.environ.get("DSTACK_AMD_OPT_OVERLAP") is not None:
             overlap_update = os.environ["DSTACK_AMD_OPT_OVERLAP"] not in ("0", "false", "")
         if overlap_update and device.type == "cuda":
@@ -243,12 +251,12 @@ class ZeroOptimizer:
                 b.work.wait()  # the side stream waits for the reduce-scatter
                 b.work = None
             self._adamw(b, self.step_count + 1, self._side_blocks)
-            if self.world > 1:
+            if self.collectives:
                 self._all_gather(b)
         b.updated = True
 
     def _reduce_bucket(self, b: Bucket, async_op: bool):
-        if self.world == 1:
+        if not self.collectives:
             return
         s, n = b.shard_range(self.rank, self.world)
         full = self.flat_grad[b.start : b.start + b.numel]
@@ -305,7 +313,7 @@ class ZeroOptimizer:
         self.step_count += 1
         self._wgen += 1
         pending = [b for b in self.buckets if not b.updated]
-        if self.world > 1:
+        if self.collectives:
             for b in pending:
                 if b.work is None:  # not overlapped (or a param received no grad)
                     self._reduce_bucket(b, async_op=False)
@@ -314,7 +322,7 @@ class ZeroOptimizer:
                     b.work = None
         for b in pending:
             self._adamw(b, self.step_count)
-        if self.world > 1:
+        if self.collectives:
             # gather the updated shards in forward order (buckets are stored in backward order);
             # with prefetch hooks installed the next forward waits per bucket, so the all-gather
             # of later layers overlaps the compute of earlier ones
@@ -324,7 +332,7 @@ class ZeroOptimizer:
             torch.cuda.current_stream().wait_stream(self._side)
         for b in self.buckets:
             b.updated = False
-        if self.world > 1 and not self._prefetch:
+        if self.collectives and not self._prefetch:
             self.wait_params()
 
     def wait_params(self, buckets=None):
@@ -338,7 +346,7 @@ class ZeroOptimizer:
         """Overlap the parameter all-gather with the next forward: each module waits only for
         the buckets holding its own parameters (forward pre-hook); anything not covered by a
         hook is waited for before backward / the next optimizer step."""
-        if self.world == 1:
+        if not self.collectives:
             return
         self._prefetch = True
         for mod in model.modules():

@@ -43,12 +43,17 @@ def init_distributed(backend: str | None = None) -> DistEnv:
     env = DistEnv(rank, world, local_rank)
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
-    if world > 1 and not dist.is_initialized():
+    # DSTACK_AMD_ZERO_FORCE_COLLECTIVES=1 at world 1: a 1-rank RCCL group, so the ZeRO-1
+    # reduce-scatter / all-gather path of a multi-GPU job runs on a single GPU (validation)
+    force = os.environ.get("DSTACK_AMD_ZERO_FORCE_COLLECTIVES", "0") not in ("0", "", "false")
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"  # "nccl" is RCCL on ROCm
         kwargs = {}
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", local_rank)
+        if world == 1 and "MASTER_ADDR" not in os.environ:
+            kwargs.update(store=dist.HashStore(), rank=0, world_size=1)
         dist.init_process_group(backend=backend, **kwargs)
     return env
 

@@ -48,3 +48,25 @@ def test_bench_two_ranks_gloo():
     assert d["n_gpus"] == 2
     assert d["config"]["parallelism"] == "dp2-zero1"
     assert d["config"]["global_batch"] == 4
+
+
+@pytest.mark.slow
+def test_bench_self_launches_ranks_without_a_launcher():
+    """``bench.py --gpus 2`` with no torchrun around it starts the 2 ranks itself (child launcher,
+    gloo on CPU) and reports n_gpus 2 -- never a silent 1-process number."""
+    env = {k: v for k, v in _env().items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["config"]["parallelism"] == "dp2-zero1"
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    env = dict(_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 2
+    assert not _json_lines(r.stdout)
+    assert "WORLD_SIZE=1" in r.stderr

@@ -76,6 +76,7 @@ def test_world_size_mismatch_rejected(tmp_path):
 def _worker(rank, world, port, path, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 8 // world))
     try:
         expect, got = _resume_matches(path)
         q.put((rank, expect, got))
@@ -90,6 +91,7 @@ def _gathered_worker(rank, world, port, path, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 8 // world))
     try:
         tr = _trainer()
         assert tr.opt._prefetch
@@ -117,6 +119,7 @@ def _resume_target_worker(rank, world, port, path, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 8 // world))
     try:
         _, tr1, _ = train_llama.run("llama-tiny", 32, 2, steps=2, warmup=1, log_every=0,
                                     checkpoint_dir=path, save_every=1)
@@ -158,6 +161,19 @@ def test_resume_two_ranks_gloo(tmp_path):
     for _, expect, got in _spawn(_worker, str(tmp_path)):
         assert got == expect
     assert len([f for f in os.listdir(tmp_path / "step-00000002") if f.startswith("optim-rank")]) == 2
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [4, 8])
+def test_resume_many_ranks_gloo(tmp_path, world):
+    """4 and 8 shards (bucket size 64 Ki elements: the shard boundaries fall inside parameters)."""
+    res = _spawn(_worker, str(tmp_path), world=world)
+    assert sorted(r for r, _, _ in res) == list(range(world))
+    for _, expect, got in res:
+        assert got == expect
+    assert len([f for f in os.listdir(tmp_path / "step-00000002") if f.startswith("optim-rank")]) == world
+    for _, ok in _spawn(_gathered_worker, str(tmp_path / "g"), world=world):
+        assert ok
 
 
 @pytest.mark.gpu

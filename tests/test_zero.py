@@ -91,15 +91,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, prefetch=False):
+def _worker(rank, world, port, out_dir, prefetch=False, bucket_numel=1 << 19):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.set_num_threads(2)
+    torch.set_num_threads(max(1, 8 // world))
     base = _model()
     steps = [_batches(2, 2 * world, seed=s) for s in range(2)]
     # each rank takes its slice of every micro-batch
     mine = [[b[rank * 2:(rank + 1) * 2] for b in micro] for micro in steps]
-    model, _ = _zero_steps(base, mine, grad_accum=2, bucket_numel=1 << 19, eps=EPS_DIST, prefetch=prefetch)
+    model, _ = _zero_steps(base, mine, grad_accum=2, bucket_numel=bucket_numel, eps=EPS_DIST, prefetch=prefetch)
     torch.save({k: v.detach() for k, v in model.state_dict().items()}, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.destroy_process_group()
 
@@ -119,6 +119,27 @@ def test_zero_gloo_world2_matches_single_process(tmp_path, prefetch):
     single, _ = _zero_steps(base, steps, grad_accum=2, eps=EPS_DIST)
     for k, v in single.state_dict().items():
         assert (states[0][k] - v).abs().max().item() < 2e-6, k
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [4, 8])
+def test_zero_gloo_many_ranks_uneven_buckets(tmp_path, world):
+    """4 and 8 ranks with a bucket size that is no multiple of anything: buckets hold different
+    numbers of parameters, every bucket is padded to world*64 and each rank's shard boundary falls
+    inside a parameter; all ranks must still end identical and equal the single process."""
+    bucket = (1 << 18) + 12345
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), True, bucket), nprocs=world,
+                       start_method="spawn")
+    states = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    for r in range(1, world):
+        for k in states[0]:
+            assert torch.equal(states[0][k], states[r][k]), (r, k)
+    base = _model()
+    steps = [_batches(2, 2 * world, seed=s) for s in range(2)]
+    single, opt = _zero_steps(base, steps, grad_accum=2, eps=EPS_DIST, bucket_numel=bucket)
+    assert len(opt.buckets) > 2 and len({len(b.params) for b in opt.buckets}) > 1
+    for k, v in single.state_dict().items():
+        assert (states[0][k] - v).abs().max().item() < 5e-6, k
 
 
 @pytest.mark.parametrize("bucket_numel", [1 << 16, 1 << 30])
