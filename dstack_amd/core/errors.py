@@ -29,6 +29,7 @@ class ServerClientErrorCode:
     UNAUTHORIZED = "unauthorized"
     INVALID_REQUEST = "invalid_request"
     BACKEND_NOT_AVAILABLE = "backend_not_available"
+    RESOURCE_BUSY = "resource_busy"
 
 
 class ServerClientError(ServerError):
@@ -75,6 +76,15 @@ class BackendNotAvailable(ServerClientError):
 class RepoDoesNotExistError(ServerClientError):
     code = ServerClientErrorCode.RESOURCE_NOT_EXISTS
     msg = "Repo does not exist"
+
+
+class ResourceBusyError(ServerClientError):
+    """A resource is locked by another operation (a reconciler pass, a concurrent request) for
+    longer than the caller waits: transient, retry (HTTP 409 on the API; background callers retry
+    on their next pass instead of failing the job)."""
+
+    code = ServerClientErrorCode.RESOURCE_BUSY
+    msg = "Resource is being processed, retry"
 
 
 class GatewayError(ServerClientError):

@@ -20,6 +20,7 @@ from dstack_amd import __version__
 from dstack_amd.core.errors import (
     ForbiddenError,
     ResourceNotExistsError,
+    ResourceBusyError,
     ServerClientError,
     UnauthorizedError,
 )
@@ -146,6 +147,10 @@ def register_routes(app: FastAPI):
     @app.exception_handler(ResourceNotExistsError)
     async def _notfound(request: Request, exc: ResourceNotExistsError):
         return _error(400, exc.msg, exc.code)
+
+    @app.exception_handler(ResourceBusyError)
+    async def _busy(request: Request, exc: ResourceBusyError):
+        return _error(409, exc.msg, exc.code)
 
     @app.exception_handler(ServerClientError)
     async def _client_error(request: Request, exc: ServerClientError):

@@ -39,6 +39,7 @@ def claim_and_process(namespace: str, select_ids: Callable[[Session], Iterable],
         if len(ids) >= batch:
             break
         ids += ls.try_add_many([c])
+    done: List = []
     try:
         for item_id in ids:
             try:
@@ -48,6 +49,11 @@ def claim_and_process(namespace: str, select_ids: Callable[[Session], Iterable],
                     process_one(s, item_id)
             except Exception:  # noqa: BLE001
                 logger.exception("%s: processing %s failed", namespace, item_id)
+            finally:
+                # released per item once its transaction ended: a request waiting on this row
+                # (stop/delete under Lockset.hold) does not wait for the rest of the batch
+                ls.remove_many([item_id])
+                done.append(item_id)
     finally:
-        ls.remove_many(ids)
+        ls.remove_many([i for i in ids if i not in done])
     return len(ids) >= batch

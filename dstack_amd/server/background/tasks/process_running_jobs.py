@@ -19,7 +19,7 @@ from sqlalchemy import select
 from sqlalchemy.orm import Session
 
 from dstack_amd.core.backends.base import DSTACK_RUNNER_HTTP_PORT
-from dstack_amd.core.errors import RunnerError, ServerClientError, SSHError
+from dstack_amd.core.errors import ResourceBusyError, RunnerError, ServerClientError, SSHError
 from dstack_amd.core.models.common import NetworkMode
 from dstack_amd.core.models.configurations import ServiceConfiguration
 from dstack_amd.core.models.instances import InstanceStatus
@@ -96,7 +96,8 @@ def _cluster_info(run: RunModel, job: JobModel) -> Optional[ClusterInfo]:
 
 def _attach_volumes(s: Session, run: RunModel, job: JobModel) -> bool:
     """Attach the job's network volumes once its instance is up (``JobRuntimeData.volume_names``
-    records them); a volume error fails the job with ``VOLUME_ERROR``."""
+    records them); a volume error fails the job with ``VOLUME_ERROR``, a volume held by another
+    job's attach transaction is retried on a later pass."""
     from dstack_amd.server.services.jobs import volumes as job_volumes
 
     spec = jobs_services.job_spec(job)
@@ -110,6 +111,10 @@ def _attach_volumes(s: Session, run: RunModel, job: JobModel) -> bool:
         vols = job_volumes.get_job_configured_volumes(s, run.project, spec)
         job_volumes.check_can_attach_job_volumes(vols)
         jrd.volume_names = job_volumes.attach_job_volumes(s, job, inst, vols)
+    except ResourceBusyError as e:
+        logger.info("%s: %s; retrying", job.job_name, e)
+        s.rollback()  # undo a partial attach of this pass (and release its volume locks)
+        return False
     except ServerClientError as e:
         jobs_services.terminate_job(job, JobTerminationReason.VOLUME_ERROR, str(e), delay=False)
         scheduler.wake(scheduler.TERMINATING_JOBS)

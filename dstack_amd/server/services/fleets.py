@@ -28,7 +28,7 @@ from dstack_amd.core.models.fleets import (
 from dstack_amd.core.models.instances import InstanceStatus, RemoteConnectionInfo, SSHKey
 from dstack_amd.core.models.profiles import DEFAULT_FLEET_TERMINATION_IDLE_TIME, Profile
 from dstack_amd.core.models.resources import ResourcesSpec
-from dstack_amd.core.models.runs import Requirements, get_policy_map
+from dstack_amd.core.models.runs import JobStatus, Requirements, get_policy_map
 from dstack_amd.core.models.profiles import SpotPolicy
 from dstack_amd.server.background import scheduler
 from dstack_amd.server.models import FleetModel, InstanceModel, ProjectModel, UserModel
@@ -201,19 +201,42 @@ def delete_fleets(s: Session, project: ProjectModel, names: List[str]):
         if f is None:
             raise ResourceNotExistsError(f"Fleet {name} not found")
         fleets.append(f)
-    with _held(fleets, [i for f in fleets for i in f.instances]):
-        for f in fleets:
-            busy = [i for i in f.instances if i.status == InstanceStatus.BUSY.value]
-            if busy:
-                raise ServerClientError(f"Fleet {f.name} has busy instances; stop the runs first")
-        for f in fleets:
-            for inst in f.instances:
-                if inst.status not in (InstanceStatus.TERMINATING.value, InstanceStatus.TERMINATED.value):
-                    inst.status = InstanceStatus.TERMINATING.value
-                    inst.termination_reason = "fleet deleted"
-            f.status = FleetStatus.TERMINATING.value
-        s.commit()
+    for _attempt in range(5):
+        locked = [i for f in fleets for i in f.instances]
+        with _held(fleets, locked):
+            for f in fleets:
+                s.refresh(f, ["instances"])  # instances added since the lock set was built
+            if {i.id for f in fleets for i in f.instances} != {i.id for i in locked}:
+                s.rollback()
+                continue  # an instance joined a fleet meanwhile: lock the new set and re-check
+            _terminate_fleets_locked(s, fleets)
+            s.commit()
+            break
+    else:
+        from dstack_amd.core.errors import ResourceBusyError
+
+        raise ResourceBusyError("Fleet instances keep changing, retry")
     scheduler.wake(scheduler.INSTANCES, scheduler.FLEETS)
+
+
+def _instance_in_use(inst) -> bool:
+    """BUSY, or holding a job that is not finished (e.g. PROVISIONING for a just-submitted job)."""
+    if inst.status == InstanceStatus.BUSY.value:
+        return True
+    return any(not JobStatus(j.status).is_finished() for j in inst.jobs)
+
+
+def _terminate_fleets_locked(s: Session, fleets):
+    for f in fleets:
+        busy = [i for i in f.instances if _instance_in_use(i)]
+        if busy:
+            raise ServerClientError(f"Fleet {f.name} has busy instances; stop the runs first")
+    for f in fleets:
+        for inst in f.instances:
+            if inst.status not in (InstanceStatus.TERMINATING.value, InstanceStatus.TERMINATED.value):
+                inst.status = InstanceStatus.TERMINATING.value
+                inst.termination_reason = "fleet deleted"
+        f.status = FleetStatus.TERMINATING.value
 
 
 def delete_fleet_instances(s: Session, project: ProjectModel, name: str, instance_nums: List[int]):
@@ -223,7 +246,7 @@ def delete_fleet_instances(s: Session, project: ProjectModel, name: str, instanc
     targets = [i for i in f.instances if i.instance_num in instance_nums]
     with _held([], targets):
         for inst in targets:
-            if inst.status == InstanceStatus.BUSY.value:
+            if _instance_in_use(inst):
                 raise ServerClientError(f"Instance {inst.name} is busy")
         for inst in targets:
             inst.status = InstanceStatus.TERMINATING.value

@@ -20,7 +20,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 from sqlalchemy import delete, insert, select, update
 from sqlalchemy.orm import Session
 
-from dstack_amd.core.errors import ComputeError, ServerClientError
+from dstack_amd.core.errors import ComputeError, ResourceBusyError, ServerClientError
 from dstack_amd.core.models.backends import BACKENDS_WITH_VOLUMES_SUPPORT, BackendType
 from dstack_amd.core.models.runs import JobSpec
 from dstack_amd.core.models.volumes import (
@@ -125,10 +125,12 @@ def _attached_instance_ids(s: Session, v: VolumeModel) -> List:
                           .where(volumes_attachments.c.volume_id == v.id)).scalars())
 
 
-def _hold_volume(s: Session, v: VolumeModel, timeout: float = 10.0):
+def _hold_volume(s: Session, v: VolumeModel, timeout: float = 1.0):
     """Hold ``v`` in the volumes lockset until ``s`` commits, then re-read it: a concurrent
     ``delete_volumes`` (which holds the same lock and commits inside) either finishes first, and the
-    attach sees ``deleted``, or waits and sees the attachment."""
+    attach sees ``deleted``, or waits and sees the attachment.  Contention (another job's attach
+    transaction still holds the volume, e.g. while it talks to its shim) raises
+    ``ResourceBusyError``: the caller retries on its next pass, the job does not fail."""
     import time
 
     from dstack_amd.server.services.locking import lockset, release_at_transaction_end
@@ -145,7 +147,7 @@ def _hold_volume(s: Session, v: VolumeModel, timeout: float = 10.0):
         deadline = time.monotonic() + timeout
         while not ls.add_all_or_nothing([v.id]):
             if time.monotonic() > deadline:
-                raise ServerClientError(f"Volume {v.name} is busy")
+                raise ResourceBusyError(f"Volume {v.name} is busy")
             time.sleep(0.005)
         held.add(v.id)
         release_at_transaction_end(s, ls, [v.id])

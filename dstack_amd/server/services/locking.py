@@ -57,12 +57,15 @@ class Lockset:
 
     @contextlib.contextmanager
     def hold(self, keys: Iterable[Hashable], timeout: float = 30.0) -> Iterator[None]:
-        """Block until all keys are free, hold them for the duration of the block."""
+        """Block until all keys are free, hold them for the duration of the block; a wait longer
+        than ``timeout`` raises ``ResourceBusyError`` (HTTP 409: retry), not a bare 500."""
+        from dstack_amd.core.errors import ResourceBusyError
+
         keys = list(keys)
         deadline = time.monotonic() + timeout
         while not self.add_all_or_nothing(keys):
             if time.monotonic() > deadline:
-                raise TimeoutError(f"timed out waiting for locks {keys}")
+                raise ResourceBusyError(f"Resource is being processed ({len(keys)} lock(s) busy), retry")
             time.sleep(0.005)
         try:
             yield

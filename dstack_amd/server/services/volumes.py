@@ -92,10 +92,12 @@ def delete_volumes(s: Session, project: ProjectModel, names: List[str]):
 
 
 def _delete_volumes_locked(s: Session, project: ProjectModel, vols):
+    # check every volume before deleting any in the cloud: a rejected volume later in the list
+    # must not leave an earlier one deleted in the cloud but ACTIVE in the (rolled back) database
     for v in vols:
-        n = v.name
         if v.instances:
-            raise ServerClientError(f"Volume {n} is attached to an instance")
+            raise ServerClientError(f"Volume {v.name} is attached to an instance")
+    for v in vols:
         conf = VolumeConfiguration.model_validate_json(v.configuration)
         if conf.volume_id is None and v.volume_provisioning_data:
             from dstack_amd.server.services import backends as backends_services

@@ -107,31 +107,45 @@ def create_app(engine: LLMEngine, served_model_name: str, tokenizer=None) -> Fas
         return req, q, _Stream(tok, stop)
 
     async def _drain(req, q, st):
-        """Yields (delta_text, finish_reason or None) until the request finishes."""
+        """Yields (delta_text, finish_reason or None) until the request finishes.  A consumer that
+        goes away early (client disconnect: GeneratorExit / CancelledError in the streaming body or
+        the awaiting handler) aborts the request, so it stops decoding and frees its KV pages."""
         t0 = time.perf_counter()
         first = True
-        while True:
-            token, finished, reason = await q.get()
-            if first and token is not None:
-                state["ttft_sum"] += time.perf_counter() - t0
-                state["ttft_n"] += 1
-                first = False
-            if token is not None:
-                state["gen_tokens"] += 1
-            delta = st.push(token)
-            if st.stopped and not finished:
+        done = False
+        try:
+            while True:
+                token, finished, reason = await q.get()
+                if first and token is not None:
+                    state["ttft_sum"] += time.perf_counter() - t0
+                    state["ttft_n"] += 1
+                    first = False
+                if token is not None:
+                    state["gen_tokens"] += 1
+                delta = st.push(token)
+                if st.stopped and not finished:
+                    engine.abort(req.id)
+                    done = True
+                    yield delta, "stop"
+                    return
+                if finished:
+                    done = True
+                    if reason == "abort":
+                        reason = "stop"
+                    if reason and reason.startswith("error"):
+                        raise HTTPException(500, detail={"message": reason, "type": "server_error"})
+                    yield delta, reason
+                    return
+                if delta:
+                    yield delta, None
+        finally:
+            if not done:
                 engine.abort(req.id)
-                yield delta, "stop"
-                return
-            if finished:
-                if reason == "abort":
-                    reason = "stop"
-                if reason and reason.startswith("error"):
-                    raise HTTPException(500, detail={"message": reason, "type": "server_error"})
-                yield delta, reason
-                return
-            if delta:
-                yield delta, None
+
+    def _abort_all(subs):
+        for _, (req, _q, _st) in subs:
+            if not req.finished:
+                engine.abort(req.id)
 
     def _prompts(body):
         p = body.get("prompt")
@@ -168,25 +182,37 @@ def create_app(engine: LLMEngine, served_model_name: str, tokenizer=None) -> Fas
         n = int(body.get("n") or 1)
         rid = f"cmpl-{uuid.uuid4().hex[:24]}"
         created = int(time.time())
-        subs = []
+        # validate every prompt before submitting any: a 400 for prompt k must not leave prompts
+        # 0..k-1 decoding with no consumer
+        planned = []
         for p in prompts:
             for k in range(n):
                 params = _params(body, len(p), 16)
                 if params.seed is not None and n > 1:
                     params.seed = int(params.seed) + k
+                planned.append((p, params))
+        subs = []
+        try:
+            for p, params in planned:
                 subs.append((p, _submit(p, params, _stop(body))))
+        except BaseException:
+            _abort_all(subs)
+            raise
         want_lp = body.get("logprobs") is not None
 
         if body.get("stream"):
             async def gen():
                 usage = {"prompt_tokens": 0, "completion_tokens": 0}
-                for idx, (p, (req, q, st)) in enumerate(subs):
-                    async for delta, reason in _drain(req, q, st):
-                        ch = {"index": idx, "text": delta, "logprobs": None, "finish_reason": reason}
-                        yield "data: " + json.dumps({"id": rid, "object": "text_completion", "created": created,
-                                                     "model": served_model_name, "choices": [ch]}) + "\n\n"
-                    usage["prompt_tokens"] += len(p)
-                    usage["completion_tokens"] += len(req.output_ids)
+                try:
+                    for idx, (p, (req, q, st)) in enumerate(subs):
+                        async for delta, reason in _drain(req, q, st):
+                            ch = {"index": idx, "text": delta, "logprobs": None, "finish_reason": reason}
+                            yield "data: " + json.dumps({"id": rid, "object": "text_completion", "created": created,
+                                                         "model": served_model_name, "choices": [ch]}) + "\n\n"
+                        usage["prompt_tokens"] += len(p)
+                        usage["completion_tokens"] += len(req.output_ids)
+                finally:
+                    _abort_all(subs)  # the client left mid-stream: later choices were never read
                 if (body.get("stream_options") or {}).get("include_usage"):
                     usage["total_tokens"] = usage["prompt_tokens"] + usage["completion_tokens"]
                     yield "data: " + json.dumps({"id": rid, "object": "text_completion", "created": created,
@@ -196,17 +222,20 @@ def create_app(engine: LLMEngine, served_model_name: str, tokenizer=None) -> Fas
             return StreamingResponse(gen(), media_type="text/event-stream")
 
         choices, pt, ct = [], 0, 0
-        for idx, (p, (req, q, st)) in enumerate(subs):
-            text, reason = "", None
-            async for delta, r in _drain(req, q, st):
-                text += delta
-                reason = r or reason
-            lp = None
-            if want_lp:
-                lp = {"tokens": [tok.decode([t]) for t in req.output_ids], "token_logprobs": list(req.logprobs)}
-            choices.append({"index": idx, "text": text, "logprobs": lp, "finish_reason": reason})
-            pt += len(p)
-            ct += len(req.output_ids)
+        try:
+            for idx, (p, (req, q, st)) in enumerate(subs):
+                text, reason = "", None
+                async for delta, r in _drain(req, q, st):
+                    text += delta
+                    reason = r or reason
+                lp = None
+                if want_lp:
+                    lp = {"tokens": [tok.decode([t]) for t in req.output_ids], "token_logprobs": list(req.logprobs)}
+                choices.append({"index": idx, "text": text, "logprobs": lp, "finish_reason": reason})
+                pt += len(p)
+                ct += len(req.output_ids)
+        finally:
+            _abort_all(subs)
         return {"id": rid, "object": "text_completion", "created": created, "model": served_model_name,
                 "choices": choices, "usage": {"prompt_tokens": pt, "completion_tokens": ct, "total_tokens": pt + ct}}
 

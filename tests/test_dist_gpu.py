@@ -30,11 +30,13 @@ def _train(gpu, steps=3, force=False):
     opt = ZeroOptimizer(m, lr=1e-3, bucket_numel=(1 << 20) + 4096, overlap_update=True, force_collectives=force)
     opt.install_prefetch_hooks(m)
     g = torch.Generator(device=gpu).manual_seed(7)
+    # the same micro-batches every step: the loss must fall (memorisation), not just wander
+    data = [torch.randint(0, cfg.vocab_size, (2, 257), device=gpu, generator=g) for _ in range(GRAD_ACCUM)]
     losses = []
     for _ in range(steps):
         opt.zero_grad()
         for i in range(GRAD_ACCUM):
-            tok = torch.randint(0, cfg.vocab_size, (2, 257), device=gpu, generator=g)
+            tok = data[i]
             opt.sync_grads = i == GRAD_ACCUM - 1
             loss = m.loss(tok[:, :-1], tok[:, 1:])
             (loss / GRAD_ACCUM).backward()

@@ -220,3 +220,50 @@ def test_gateway_capability_and_duplicates(client):
     assert r.status_code == 400 and "not configured" in r.text
     assert client.post("/api/project/main/gateways/delete", json={"names": ["gw"]}).status_code == 400
     assert client.post("/api/project/main/gateways/set_default", json={"name": "gw"}).status_code == 400
+
+
+def test_delete_fleet_refuses_instance_with_unfinished_job(client):
+    """A PROVISIONING instance created for a just-submitted job is in use even though it is not
+    BUSY yet: the fleet delete must not terminate it under the job."""
+    from dstack_amd.server.models import JobModel
+
+    from tests.test_reconcilers import _job, _submit
+
+    _create(client, _ssh(name="prov", hosts=["10.0.0.9"]))
+    with session_scope() as s:
+        rid = _submit(s, {"type": "task", "commands": ["x"]}, name="r-prov")
+        inst = s.query(InstanceModel).one()
+        inst.status = InstanceStatus.PROVISIONING.value
+        j = _job(s, rid)
+        j.instance_id = inst.id
+        j.status = "provisioning"
+    r = client.post("/api/project/main/fleets/delete", json={"names": ["prov"]})
+    assert r.status_code == 400 and "busy" in r.text
+    with session_scope() as s:
+        assert s.query(InstanceModel).one().status == InstanceStatus.PROVISIONING.value
+        s.query(JobModel).one().status = "done"
+    assert client.post("/api/project/main/fleets/delete", json={"names": ["prov"]}).status_code == 200
+
+
+def test_lock_wait_timeout_is_a_409_not_a_500(client):
+    """A request that waits too long for a row a reconciler holds gets 409 'retry', not a 500."""
+    from dstack_amd.server.services import fleets as fleets_services
+    from dstack_amd.server.services.locking import lockset
+
+    _create(client, _ssh(name="held", hosts=["10.0.0.7"]))
+    with session_scope() as s:
+        fid = s.query(FleetModel).filter_by(name="held").one().id
+    orig = fleets_services._held
+
+    def short_held(fleets, instances, timeout=60.0):
+        return orig(fleets, instances, timeout=0.2)
+
+    lockset("fleets").add_all_or_nothing([fid])  # a background pass holds the fleet
+    try:
+        fleets_services._held = short_held
+        r = client.post("/api/project/main/fleets/delete", json={"names": ["held"]})
+    finally:
+        fleets_services._held = orig
+        lockset("fleets").remove_many([fid])
+    assert r.status_code == 409, r.text
+    assert r.json()["detail"][0]["code"] == "resource_busy"

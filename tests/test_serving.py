@@ -8,6 +8,7 @@ run vLLM/TGI containers), so HF's Llama is the oracle for the model math."""
 
 import json
 import math
+import time
 
 import pytest
 import torch
@@ -707,3 +708,73 @@ def test_gpu_rms_norm_fp8_matches_unfused(gpu, with_delta):
     q_ref, s_ref = C.quant_fp8_rows(y_ref)
     torch.testing.assert_close(s, s_ref, rtol=1e-6, atol=0)
     assert (q != q_ref).float().mean().item() < 1e-3
+
+
+def test_api_client_disconnect_aborts_request():
+    """A client that leaves mid-stream aborts its request: decoding stops and the KV pages are
+    freed instead of running to max_tokens with no consumer."""
+    import asyncio
+
+    from dstack_amd.serving.server import create_app
+
+    eng = LLMEngine.from_model("llama-tiny", device="cpu", max_model_len=512, max_batch=4, num_pages=32)
+    app = create_app(eng, served_model_name="llama-tiny")
+    seen = []
+    orig = eng.add_request
+
+    def add_request(*a, **k):
+        r = orig(*a, **k)
+        seen.append(r)
+        return r
+
+    eng.add_request = add_request
+    payload = json.dumps({"model": "llama-tiny", "prompt": [1, 2, 3], "max_tokens": 500, "temperature": 0,
+                          "ignore_eos": True, "stream": True}).encode()
+
+    async def run():
+        got_body = asyncio.Event()
+        state = {"sent_request": False}
+
+        async def receive():
+            if not state["sent_request"]:
+                state["sent_request"] = True
+                return {"type": "http.request", "body": payload, "more_body": False}
+            await got_body.wait()
+            return {"type": "http.disconnect"}
+
+        async def send(msg):
+            if msg["type"] == "http.response.body" and msg.get("body"):
+                got_body.set()
+
+        scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1", "method": "POST",
+                 "scheme": "http", "path": "/v1/completions", "raw_path": b"/v1/completions", "query_string": b"",
+                 "headers": [(b"content-type", b"application/json")], "client": ("127.0.0.1", 1),
+                 "server": ("127.0.0.1", 80), "root_path": ""}
+        await asyncio.wait_for(app(scope, receive, send), 60)
+
+    eng.start()
+    try:
+        asyncio.run(run())
+        deadline = time.time() + 10
+        while time.time() < deadline and (not seen[0].finished or eng.metrics()["running"]):
+            time.sleep(0.02)
+    finally:
+        eng.stop()
+    req = seen[0]
+    assert req.finished and req.finish_reason == "abort"
+    assert len(req.output_ids) < 500
+    assert eng.metrics()["running"] == 0
+
+
+def test_api_completions_rejects_before_submitting_any_prompt(api):
+    """Prompt 2 of 2 too long: a 400, and prompt 1 was never submitted (no orphaned decode)."""
+    before = api.get("/metrics").text
+    r = api.post("/v1/completions", json={"model": "llama-tiny", "prompt": [[1, 2], list(range(1, 300))],
+                                          "max_tokens": 2})
+    assert r.status_code == 400
+    after = api.get("/metrics").text
+
+    def reqs(m):
+        return [ln for ln in m.splitlines() if ln.startswith("dstack_serving_requests_total")][0]
+
+    assert reqs(before) == reqs(after)

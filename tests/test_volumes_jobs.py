@@ -221,3 +221,62 @@ def test_volume_attach_waits_for_a_concurrent_delete(db):
         volumes_services.delete_volumes(s, s.query(ProjectModel).filter_by(name="main").one(), ["data"])
     t.join(5)
     assert seen == {"deleted": True}
+
+
+def test_volume_busy_retries_instead_of_failing_the_job(db):
+    """Another job's attach transaction still holds the volume (e.g. while its shim call is slow):
+    this job is retried on a later pass, not terminated with VOLUME_ERROR."""
+    from dstack_amd.server.background.tasks import process_running_jobs as prj
+    from dstack_amd.server.services import backends as backends_services
+    from dstack_amd.server.services.locking import lockset
+
+    with session_scope() as s:
+        vid = _volume(s)
+        iid = _instance(s)
+        rid = _submit(s, TASK)
+        jid = _provisioning_job(s, rid, iid)
+    compute = mock.Mock()
+    compute.attach_volume.return_value = VolumeAttachmentData(device_name="/dev/sdf")
+    shim = mock.Mock()
+    lockset("volumes").add_all_or_nothing([vid])
+    try:
+        with mock.patch.object(backends_services, "get_project_backend", return_value=compute), \
+                mock.patch.object(prj, "get_shim_client", return_value=shim), session_scope() as s:
+            j = s.get(JobModel, jid)
+            prj._process_provisioning(s, j.run, j)
+    finally:
+        lockset("volumes").remove_many([vid])
+    with session_scope() as s:
+        j = s.get(JobModel, jid)
+        assert j.status == "provisioning" and j.termination_reason is None
+    shim.submit_task.assert_not_called()
+    with mock.patch.object(backends_services, "get_project_backend", return_value=compute), \
+            mock.patch.object(prj, "get_shim_client", return_value=shim), session_scope() as s:
+        j = s.get(JobModel, jid)
+        prj._process_provisioning(s, j.run, j)
+    with session_scope() as s:
+        assert s.get(JobModel, jid).status == "pulling"
+    shim.submit_task.assert_called_once()
+
+
+def test_delete_volumes_checks_all_before_any_cloud_delete(db):
+    """Deleting [v1, v2] with v2 attached: nothing is deleted in the cloud (v1 would otherwise be
+    gone in the cloud yet ACTIVE in the rolled-back database)."""
+    import pytest
+
+    from dstack_amd.core.errors import ServerClientError
+    from dstack_amd.server.services import backends as backends_services
+    from dstack_amd.server.services import volumes as volumes_services
+
+    with session_scope() as s:
+        _volume(s, name="v1")
+        v2 = _volume(s, name="v2")
+        iid = _instance(s)
+        s.execute(volumes_attachments.insert().values(volume_id=v2, instance_id=iid, attachment_data="{}"))
+    compute = mock.Mock()
+    with mock.patch.object(backends_services, "get_project_backend", return_value=compute), session_scope() as s:
+        with pytest.raises(ServerClientError, match="v2 is attached"):
+            volumes_services.delete_volumes(s, s.query(ProjectModel).filter_by(name="main").one(), ["v1", "v2"])
+    compute.delete_volume.assert_not_called()
+    with session_scope() as s:
+        assert not s.query(VolumeModel).filter_by(name="v1").one().deleted
