@@ -12,7 +12,6 @@ from __future__ import annotations
 import base64
 import io
 import os
-import threading
 import time
 from typing import Dict, Iterator, List, Optional
 
@@ -340,6 +339,3 @@ class Client:
             except Exception:  # noqa: BLE001 - ssh-keygen missing: attach just won't work
                 ssh_identity_file = None
         return Client(api, project, ssh_identity_file)
-
-
-_ = threading

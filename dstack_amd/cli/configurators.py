@@ -21,7 +21,7 @@ import yaml
 from dstack_amd.api import Client
 from dstack_amd.cli.utils import confirm_ask, console, fleets_table, plan_table, print_table, status_text
 from dstack_amd.core.errors import CLIError, ConfigurationError
-from dstack_amd.core.models.configurations import PortMapping, ServiceConfiguration
+from dstack_amd.core.models.configurations import PortMapping
 from dstack_amd.core.models.envs import Env
 from dstack_amd.core.models.profiles import CreationPolicy, Profile, ProfilesConfig, SpotPolicy, TerminationPolicy
 from dstack_amd.core.models.repos import LocalRepo, RemoteRepo, Repo, RepoError, VirtualRepo
@@ -534,6 +534,3 @@ def configurator_for(conf_type: str):
         if conf_type in c.TYPES:
             return c()
     raise ConfigurationError(f"unsupported configuration type {conf_type}")
-
-
-_ = (ServiceConfiguration, Dict, List)

@@ -5,7 +5,7 @@ from __future__ import annotations
 
 import sys
 from datetime import datetime, timezone
-from typing import Iterable, List, Optional
+from typing import Iterable, Optional
 
 from rich.console import Console
 from rich.table import Table
@@ -194,6 +194,3 @@ def gateways_table(gateways, verbose: bool = False) -> Table:
 def print_table(t: Table):
     console.print(t)
     console.print()
-
-
-_ = List

@@ -2,10 +2,14 @@
 ``resources.py``; the reference uses boto3).
 
 Covers: RunInstances (on-demand/spot, cloud-init shim bootstrap, root volume size, cluster
-placement group, capacity reservation, security group with SSH), DescribeInstances polling,
-TerminateInstances, placement groups, EBS volumes (create/attach/detach/delete/register) and the
-gateway VM.  Config: ``regions``, ``vpc_name``/``subnet_ids``, ``os_images``; creds:
-``access_key``/``secret_key`` (or the ``AWS_*`` environment).
+placement group, capacity reservations and capacity blocks, tags), VPC selection (default VPC,
+``vpc_name`` tag lookup or ``vpc_ids``, configured ``subnet_ids``, public-IP subnets), one attempt
+per availability zone on no-capacity, EFA network interfaces sized from DescribeInstanceTypes
+(``efa`` / ``efa-only`` cards for RCCL's inter-node RDMA), paginated Describe* calls,
+DescribeInstances polling (private address when ``public_ips: false``), TerminateInstances,
+placement groups, EBS volumes (create/attach/detach/delete/register) and the gateway VM.
+Config: ``regions``, ``vpc_name``/``vpc_ids``/``subnet_ids``, ``public_ips``, ``os_images``,
+``tags``; creds: ``access_key``/``secret_key`` (or the ``AWS_*`` environment).
 """
 
 from __future__ import annotations
@@ -16,7 +20,6 @@ import urllib.parse
 import xml.etree.ElementTree as ET
 from typing import Dict, List, Optional, Tuple
 
-from dstack_amd.core.backends.base import choose_disk_size_mib
 from dstack_amd.core.backends.clouds.common import VMCompute, check_response, cloud_init, sigv4_headers
 from dstack_amd.core.errors import ComputeError, NoCapacityError
 from dstack_amd.core.models.backends import BackendType
@@ -65,75 +68,211 @@ class AWSCompute(VMCompute):
             check_response(r, f"aws {action} {code}")
         return _strip_ns(ET.fromstring(r.text))
 
+    def _paginate(self, region: str, action: str, params: Optional[Dict[str, str]], item_path: str) -> List[ET.Element]:
+        """All items of a paginated Describe* call (follows ``nextToken``)."""
+        items: List[ET.Element] = []
+        token = None
+        for _ in range(100):
+            p = dict(params or {})
+            if token:
+                p["NextToken"] = token
+            root = self._call(region, action, p)
+            items.extend(root.findall(item_path))
+            token = root.findtext("nextToken")
+            if not token:
+                break
+        return items
+
     # ---- helpers ------------------------------------------------------------------------------
     def _image_id(self, region: str, gpu: bool) -> str:
         imgs = self.config.get("os_images") or {}
         key = "amd" if gpu else "cpu"
         if isinstance(imgs.get(key), dict) and imgs[key].get(region):
             return imgs[key][region]
-        root = self._call(region, "DescribeImages", {
+        items = self._paginate(region, "DescribeImages", {
             "Owner.1": UBUNTU_OWNER, "Filter.1.Name": "name",
             "Filter.1.Value.1": "ubuntu/images/hvm-ssd/ubuntu-jammy-22.04-amd64-server-*",
-            "Filter.2.Name": "state", "Filter.2.Value.1": "available"})
-        items = [(i.findtext("creationDate") or "", i.findtext("imageId")) for i in root.iter("item")
-                 if i.findtext("imageId")]
-        if not items:
+            "Filter.2.Name": "state", "Filter.2.Value.1": "available"}, "./imagesSet/item")
+        pairs = [(i.findtext("creationDate") or "", i.findtext("imageId")) for i in items if i.findtext("imageId")]
+        if not pairs:
             raise ComputeError(f"no Ubuntu 22.04 AMI in {region}")
-        return max(items)[1]
+        return max(pairs)[1]
 
-    def _security_group(self, region: str, project: str) -> str:
+    def _vpc_id(self, region: str) -> Optional[str]:
+        """``vpc_ids: {region: vpc-...}`` or ``vpc_name`` (tag Name) from the backend config; None =
+        the region's default VPC (no explicit subnet)."""
+        ids = self.config.get("vpc_ids") or {}
+        if isinstance(ids, dict) and ids.get(region):
+            return ids[region]
+        name = self.config.get("vpc_name")
+        if not name:
+            return None
+        vpcs = self._paginate(region, "DescribeVpcs", {"Filter.1.Name": "tag:Name", "Filter.1.Value.1": name},
+                              "./vpcSet/item")
+        if not vpcs:
+            raise ComputeError(f"no VPC named {name!r} in {region}")
+        return vpcs[0].findtext("vpcId")
+
+    def _subnets(self, region: str, vpc_id: Optional[str], public_ip: bool) -> List[Tuple[str, str]]:
+        """[(subnet id, availability zone)] to try, in AZ order.  Configured ``subnet_ids`` win; in a
+        named VPC public-IP launches use subnets that map public IPs on launch."""
+        conf = self.config.get("subnet_ids")
+        params: Dict[str, str] = {}
+        if isinstance(conf, dict) and conf.get(region):
+            sids = conf[region] if isinstance(conf[region], list) else [conf[region]]
+            for i, sid in enumerate(sids, 1):
+                params[f"SubnetId.{i}"] = sid
+        elif vpc_id is not None:
+            params = {"Filter.1.Name": "vpc-id", "Filter.1.Value.1": vpc_id}
+        else:
+            return []
+        out = []
+        for it in self._paginate(region, "DescribeSubnets", params, "./subnetSet/item"):
+            if vpc_id is not None and "SubnetId.1" not in params and public_ip and \
+                    (it.findtext("mapPublicIpOnLaunch") or "false") != "true":
+                continue
+            out.append((it.findtext("subnetId"), it.findtext("availabilityZone") or ""))
+        if not out:
+            raise ComputeError(f"no usable subnet in {vpc_id or 'the configured subnets'} ({region})")
+        return sorted(out, key=lambda x: x[1])
+
+    def _max_efa_interfaces(self, region: str, instance_type: str) -> int:
+        """EFA network cards of ``instance_type`` (0 when EFA is not supported); the RDMA NICs RCCL's
+        net plugin uses across nodes (reference ``get_maximum_efa_interfaces``)."""
+        try:
+            items = self._paginate(region, "DescribeInstanceTypes", {"InstanceType.1": instance_type},
+                                   "./instanceTypeSet/item")
+        except ComputeError:
+            return 0
+        if not items:
+            return 0
+        net = items[0].find("networkInfo")
+        if net is None or (net.findtext("efaSupported") or "false") != "true":
+            return 0
+        return int(net.findtext("efaInfo/maximumEfaInterfaces") or net.findtext("maximumNetworkCards") or 1)
+
+    def _reservation(self, region: str, reservation_id: str) -> Dict[str, str]:
+        items = self._paginate(region, "DescribeCapacityReservations",
+                               {"CapacityReservationId.1": reservation_id}, "./capacityReservationSet/item")
+        if not items:
+            raise NoCapacityError(f"capacity reservation {reservation_id} not found in {region}")
+        it = items[0]
+        state = it.findtext("state")
+        if state not in ("active", "scheduled"):
+            raise NoCapacityError(f"capacity reservation {reservation_id} is {state}")
+        return {"az": it.findtext("availabilityZone") or "", "type": it.findtext("reservationType") or "default",
+                "instance_type": it.findtext("instanceType") or ""}
+
+    def _security_group(self, region: str, project: str, vpc_id: Optional[str] = None) -> str:
         name = f"dstack_{project}"
-        root = self._call(region, "DescribeSecurityGroups", {"Filter.1.Name": "group-name", "Filter.1.Value.1": name})
+        params = {"Filter.1.Name": "group-name", "Filter.1.Value.1": name}
+        if vpc_id:
+            params.update({"Filter.2.Name": "vpc-id", "Filter.2.Value.1": vpc_id})
+        root = self._call(region, "DescribeSecurityGroups", params)
         gid = root.findtext(".//securityGroupInfo/item/groupId")
         if gid:
             return gid
-        root = self._call(region, "CreateSecurityGroup", {"GroupName": name, "GroupDescription": "dstack-amd"})
+        create = {"GroupName": name, "GroupDescription": "dstack-amd"}
+        if vpc_id:
+            create["VpcId"] = vpc_id
+        root = self._call(region, "CreateSecurityGroup", create)
         gid = root.findtext("groupId")
         self._call(region, "AuthorizeSecurityGroupIngress", {
             "GroupId": gid, "IpPermissions.1.IpProtocol": "tcp", "IpPermissions.1.FromPort": "22",
             "IpPermissions.1.ToPort": "22", "IpPermissions.1.IpRanges.1.CidrIp": "0.0.0.0/0"})
-        # intra-cluster traffic (RCCL/torchrun between nodes of a fleet)
+        # intra-cluster traffic (RCCL/torchrun between nodes of a fleet, EFA needs all-to-all in SG)
         self._call(region, "AuthorizeSecurityGroupIngress", {
             "GroupId": gid, "IpPermissions.1.IpProtocol": "-1",
             "IpPermissions.1.Groups.1.GroupId": gid})
         return gid
 
     # ---- VMCompute hooks ----------------------------------------------------------------------
-    def _launch(self, offer: InstanceOfferWithAvailability, cfg: InstanceConfiguration
-                ) -> Tuple[str, Optional[str], Optional[dict]]:
-        region = offer.region
+    def _run_params(self, offer: InstanceOfferWithAvailability, cfg: InstanceConfiguration, image_id: str,
+                    sg: str, subnet: Optional[str], efa: int, public_ip: bool, capacity_block: bool) -> Dict[str, str]:
         res = offer.instance.resources
         params = {
-            "ImageId": self._image_id(region, bool(res.gpus)), "InstanceType": offer.instance.name,
-            "MinCount": "1", "MaxCount": "1",
+            "ImageId": image_id, "InstanceType": offer.instance.name, "MinCount": "1", "MaxCount": "1",
             "UserData": base64.b64encode(cloud_init(cfg).encode()).decode(),
-            "SecurityGroupId.1": self._security_group(region, cfg.project_name),
             "BlockDeviceMapping.1.DeviceName": "/dev/sda1",
             "BlockDeviceMapping.1.Ebs.VolumeSize": str(max(100, res.disk.size_mib // 1024)),
             "BlockDeviceMapping.1.Ebs.VolumeType": "gp3",
             "TagSpecification.1.ResourceType": "instance",
-            "TagSpecification.1.Tag.1.Key": "Name", "TagSpecification.1.Tag.1.Value": cfg.instance_name,
-            "TagSpecification.1.Tag.2.Key": "dstack_project", "TagSpecification.1.Tag.2.Value": cfg.project_name,
         }
-        if res.spot:
+        tags = {"Name": cfg.instance_name, "owner": "dstack", "dstack_project": cfg.project_name,
+                "dstack_user": cfg.user or "", **(self.config.get("tags") or {})}
+        for i, (k, v) in enumerate(tags.items(), 1):
+            params[f"TagSpecification.1.Tag.{i}.Key"] = k
+            params[f"TagSpecification.1.Tag.{i}.Value"] = str(v)
+        if capacity_block:
+            params["InstanceMarketOptions.MarketType"] = "capacity-block"
+        elif res.spot:
             params["InstanceMarketOptions.MarketType"] = "spot"
             params["InstanceMarketOptions.SpotOptions.SpotInstanceType"] = "one-time"
+            params["InstanceMarketOptions.SpotOptions.InstanceInterruptionBehavior"] = "terminate"
         if cfg.placement_group_name:
             params["Placement.GroupName"] = cfg.placement_group_name
-        if cfg.availability_zone:
-            params["Placement.AvailabilityZone"] = cfg.availability_zone
         if cfg.reservation:
             params["CapacityReservationSpecification.CapacityReservationTarget.CapacityReservationId"] = \
                 cfg.reservation
-        subnets = (self.config.get("subnet_ids") or {}).get(region) if isinstance(self.config.get("subnet_ids"),
-                                                                                 dict) else None
-        if subnets:
-            params["SubnetId"] = subnets
-        root = self._call(region, "RunInstances", params)
-        iid = root.findtext(".//instancesSet/item/instanceId")
-        if not iid:
-            raise ComputeError("RunInstances returned no instance id")
-        return iid, None, {"region": region}
+        if subnet is None:
+            params["SecurityGroupId.1"] = sg  # default VPC: instance-level security group
+            return params
+        # an explicit subnet: interfaces carry subnet + security group (AWS takes one or the other);
+        # EFA cards beyond the first only without a public IP (one interface may associate it)
+        nics = [{"DeviceIndex": "0", "SubnetId": subnet, "SecurityGroupId.1": sg,
+                 "AssociatePublicIpAddress": "true" if public_ip else "false",
+                 "InterfaceType": "efa" if efa > 0 else "interface"}]
+        if efa > 1 and not public_ip:
+            for card in range(1, efa):
+                # p5: every 4th card keeps the IP stack (efa), the rest are RDMA-only (efa-only)
+                kind = "efa" if offer.instance.name.startswith("p5") and card % 4 == 0 else "efa-only"
+                nics.append({"NetworkCardIndex": str(card), "DeviceIndex": "1", "SubnetId": subnet,
+                             "SecurityGroupId.1": sg, "AssociatePublicIpAddress": "false", "InterfaceType": kind})
+        for n, nic in enumerate(nics, 1):
+            for k, v in nic.items():
+                params[f"NetworkInterface.{n}.{k}"] = v
+        return params
+
+    def _launch(self, offer: InstanceOfferWithAvailability, cfg: InstanceConfiguration
+                ) -> Tuple[str, Optional[str], Optional[dict]]:
+        region = offer.region
+        public_ip = bool(self.config.get("public_ips", True))
+        vpc_id = self._vpc_id(region)
+        subnets: List[Tuple[Optional[str], str]] = list(self._subnets(region, vpc_id, public_ip))
+        efa = self._max_efa_interfaces(region, offer.instance.name) if subnets else 0
+        capacity_block = False
+        if cfg.reservation:
+            rsv = self._reservation(region, cfg.reservation)
+            capacity_block = rsv["type"] == "capacity-block"
+            if subnets:
+                subnets = [x for x in subnets if x[1] == rsv["az"]]
+                if not subnets:
+                    raise NoCapacityError(f"no subnet in the reservation's zone {rsv['az']}")
+            elif not cfg.availability_zone:
+                cfg = cfg.model_copy(update={"availability_zone": rsv["az"]})
+        if cfg.availability_zone and subnets:
+            subnets = [x for x in subnets if x[1] == cfg.availability_zone] or subnets
+        image_id = self._image_id(region, bool(offer.instance.resources.gpus))
+        sg = self._security_group(region, cfg.project_name, vpc_id)
+        attempts = subnets or [(None, cfg.availability_zone or "")]
+        tried, last = set(), None
+        for subnet, az in attempts:
+            if az in tried:
+                continue  # one try per zone
+            tried.add(az)
+            params = self._run_params(offer, cfg, image_id, sg, subnet, efa, public_ip, capacity_block)
+            if subnet is None and az:
+                params["Placement.AvailabilityZone"] = az
+            try:
+                root = self._call(region, "RunInstances", params)
+            except NoCapacityError as e:
+                last = e
+                continue
+            iid = root.findtext(".//instancesSet/item/instanceId")
+            if not iid:
+                raise ComputeError("RunInstances returned no instance id")
+            return iid, None, {"region": region, "public_ip": public_ip, "efa_interfaces": efa}
+        raise last or NoCapacityError(f"no capacity for {offer.instance.name} in {region}")
 
     def _describe(self, instance_id: str, region: str, backend_data: dict) -> dict:
         root = self._call(region, "DescribeInstances", {"InstanceId.1": instance_id})
@@ -143,6 +282,9 @@ class AWSCompute(VMCompute):
         state = item.findtext("instanceState/name")
         if state in ("terminated", "shutting-down"):
             return {"status": "terminated"}
+        if backend_data.get("public_ip") is False:  # private subnets: reach it on its VPC address
+            return {"status": state, "hostname": item.findtext("privateIpAddress") if state == "running" else None,
+                    "internal_ip": item.findtext("privateIpAddress")}
         return {"status": state, "hostname": item.findtext("ipAddress") or None,
                 "internal_ip": item.findtext("privateIpAddress")}
 
@@ -242,5 +384,3 @@ class AWSCompute(VMCompute):
                           backend_data: Optional[str] = None) -> None:
         self._terminate(instance_id, configuration.region, {})
 
-
-_ = (choose_disk_size_mib, List)

@@ -30,7 +30,7 @@ import httpx
 
 from dstack_amd.core.backends.base import Compute, get_docker_commands, get_user_data
 from dstack_amd.core.backends.catalog import catalog_offers
-from dstack_amd.core.errors import BackendAuthError, BackendError, ComputeError, NoCapacityError
+from dstack_amd.core.errors import BackendAuthError, ComputeError, NoCapacityError
 from dstack_amd.core.models.instances import (
     InstanceAvailability,
     InstanceConfiguration,
@@ -208,6 +208,3 @@ class OAuthToken:
             tok, ttl = self._fetch()
             self._token, self._exp = tok, time.time() + float(ttl)
         return self._token
-
-
-_ = BackendError

@@ -8,11 +8,9 @@ and reaches pods through one SSH jump pod per backend (NodePort), as in the refe
 
 from __future__ import annotations
 
-import base64
 import json
 import os
-import ssl
-import tempfile
+import time
 from typing import Dict, List, Optional, Tuple
 
 import httpx
@@ -333,6 +331,54 @@ class KubernetesCompute(ContainerCompute):
             if r.status_code not in (200, 202, 404):
                 check_response(r, f"k8s delete {kind}")
 
+    # ---- gateway: pod + LoadBalancer service (reference ``C/backends/kubernetes/compute.py:221-310``) ----
+    def create_gateway(self, configuration):
+        """A ``ubuntu:22.04`` pod running sshd, nginx and the versioned gateway app, exposed by a
+        ``LoadBalancer`` service on 22/80/443.  Needs a cluster with load-balancer support: without
+        an external address after the wait the pod and service are removed and creation fails."""
+        from dstack_amd.core.models.gateways import GatewayProvisioningData
+        from dstack_amd.proxy.gateway.packaging import container_commands
+
+        name = configuration.instance_name.lower().replace("_", "-")[:50]
+        ns = self.namespace
+        cmds = container_commands(configuration.ssh_key_pub)
+        pod = {"apiVersion": "v1", "kind": "Pod",
+               "metadata": {"name": name, "labels": {"app.kubernetes.io/name": name, "dstack/role": "gateway"}},
+               "spec": {"containers": [{"name": "gateway", "image": "ubuntu:22.04", "command": ["/bin/sh"],
+                                        "args": ["-c", " && ".join(cmds)],
+                                        "ports": [{"containerPort": p} for p in (22, 80, 443)]}]}}
+        check_response(self.http.post(self._url(f"/api/v1/namespaces/{ns}/pods"), headers=self._h(), json=pod),
+                       "k8s gateway pod")
+        svc_name = f"{name}-service"
+        svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": svc_name},
+               "spec": {"type": "LoadBalancer", "selector": {"app.kubernetes.io/name": name},
+                        "ports": [{"name": n, "port": p, "targetPort": p}
+                                  for n, p in (("ssh", 22), ("http", 80), ("https", 443))]}}
+        check_response(self.http.post(self._url(f"/api/v1/namespaces/{ns}/services"), headers=self._h(), json=svc),
+                       "k8s gateway service")
+        host = None
+        for _ in range(int(self.config.get("gateway_lb_wait_tries", 60))):
+            r = self.http.get(self._url(f"/api/v1/namespaces/{ns}/services/{svc_name}"), headers=self._h())
+            if r.status_code == 200:
+                ing = (r.json().get("status", {}).get("loadBalancer", {}).get("ingress") or [{}])[0]
+                host = ing.get("hostname") or ing.get("ip")
+                if host:
+                    break
+            time.sleep(float(self.config.get("gateway_lb_wait_s", 5)))
+        if not host:
+            self.terminate_gateway(name, configuration)
+            raise ComputeError("the gateway's LoadBalancer service got no external address "
+                               "(does the cluster support LoadBalancer services?)")
+        return GatewayProvisioningData(instance_id=name, ip_address=host, region=ns,
+                                       backend_data=json.dumps({"ssh_user": "root", "service": svc_name}))
+
+    def terminate_gateway(self, instance_id, configuration, backend_data=None):
+        svc = json.loads(backend_data or "{}").get("service", f"{instance_id}-service")
+        for kind, n in (("services", svc), ("pods", instance_id)):
+            r = self.http.delete(self._url(f"/api/v1/namespaces/{self.namespace}/{kind}/{n}"), headers=self._h())
+            if r.status_code not in (200, 202, 404):
+                check_response(r, f"k8s delete gateway {kind}")
+
 
 def _cpu(v: str) -> int:
     return max(1, int(float(v[:-1]) / 1000) if v.endswith("m") else int(float(v)))
@@ -344,6 +390,3 @@ def _mem_mib(v: str) -> int:
         if v.endswith(u):
             return int(float(v[: -len(u)]) * m)
     return int(float(v) / 2**20)
-
-
-_ = (base64, ssl, tempfile)

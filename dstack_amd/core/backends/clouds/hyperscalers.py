@@ -2,11 +2,16 @@
 azure-mgmt SDK), ``C/backends/gcp/compute.py`` (1378, google-cloud SDK), ``C/backends/oci/compute.py``
 (1181, oci SDK)).
 
-* Azure: OAuth2 client credentials -> one ARM template deployment per VM (public IP + NIC + VM with
-  cloud-init ``customData``); the MI300X path is ``Standard_ND96isr_MI300X_v5``.
-* GCP: service-account JWT (RS256 via OpenSSL) -> ``instances.insert`` with a NAT access config.
-* OCI: HTTP-signature auth (RSA-SHA256 via OpenSSL) -> ``LaunchInstance``; the ``BM.GPU.MI300X.8``
-  bare-metal shape takes up to 20 minutes to boot (the reference's 1200 s timeout).
+* Azure: OAuth2 client credentials -> one ARM template deployment per VM (project NSG + VNet
+  ``dstack-vnet-<region>`` declared idempotently, public IP + NIC + VM with cloud-init
+  ``customData``); the MI300X path is ``Standard_ND96isr_MI300X_v5``.  Gateways: a small VM with its
+  own NSG (22/80/443).
+* GCP: service-account JWT (RS256 via OpenSSL) -> ``instances.insert`` with a NAT access config;
+  gateways (firewall rule on the ``dstack-gateway`` tag) and zonal persistent-disk volumes
+  (create / register / attach / detach / delete, operations awaited).
+* OCI: HTTP-signature auth (RSA-SHA256 via OpenSSL) -> ``LaunchInstance`` with the newest
+  shape-compatible Ubuntu 22.04 image unless one is configured; the ``BM.GPU.MI300X.8`` bare-metal
+  shape takes up to 20 minutes to boot (the reference's 1200 s timeout).
 """
 
 from __future__ import annotations
@@ -17,7 +22,7 @@ import hashlib
 import json
 import time
 import urllib.parse
-from typing import Dict, Optional, Tuple
+from typing import Optional
 
 from dstack_amd.core.backends.clouds.common import (
     OAuthToken,
@@ -60,8 +65,35 @@ class AzureCompute(VMCompute):
         check_response(self.http.put(url, headers=self._h(), json={"location": region}), "azure resource group")
         return rg
 
+    @staticmethod
+    def _rule(name: str, prio: int, port: str) -> dict:
+        return {"name": name, "properties": {"priority": prio, "direction": "Inbound", "access": "Allow",
+                                             "protocol": "Tcp", "sourcePortRange": "*", "destinationPortRange": port,
+                                             "sourceAddressPrefix": "*", "destinationAddressPrefix": "*"}}
+
+    def _network_resources(self, region: str) -> list:
+        """The project network every VM of the region joins, declared in each deployment
+        (idempotent in Incremental mode): an NSG admitting SSH plus all traffic inside the VNet
+        (RCCL/torchrun between nodes), and ``dstack-vnet-<region>`` with subnet ``default``."""
+        nsg = f"dstack-nsg-{region}"
+        rules = [self._rule("ssh", 100, "22"),
+                 {"name": "vnet", "properties": {"priority": 110, "direction": "Inbound", "access": "Allow",
+                                                 "protocol": "*", "sourcePortRange": "*", "destinationPortRange": "*",
+                                                 "sourceAddressPrefix": "VirtualNetwork",
+                                                 "destinationAddressPrefix": "VirtualNetwork"}}]
+        return [
+            {"type": "Microsoft.Network/networkSecurityGroups", "apiVersion": "2023-04-01", "name": nsg,
+             "location": region, "properties": {"securityRules": rules}},
+            {"type": "Microsoft.Network/virtualNetworks", "apiVersion": "2023-04-01", "name": f"dstack-vnet-{region}",
+             "location": region, "dependsOn": [f"[resourceId('Microsoft.Network/networkSecurityGroups', '{nsg}')]"],
+             "properties": {"addressSpace": {"addressPrefixes": ["10.0.0.0/16"]}, "subnets": [
+                 {"name": "default", "properties": {"addressPrefix": "10.0.0.0/20", "networkSecurityGroup": {
+                     "id": f"[resourceId('Microsoft.Network/networkSecurityGroups', '{nsg}')]"}}}]}},
+        ]
+
     def _template(self, name: str, size: str, region: str, user_data: str, disk_gb: int, spot: bool,
-                  public_keys) -> dict:
+                  public_keys, extra_ports=()) -> dict:
+        own_network = not self.config.get("subnet_id")
         subnet = self.config.get("subnet_id") or (
             f"[resourceId('Microsoft.Network/virtualNetworks/subnets', 'dstack-vnet-{region}', 'default')]")
         vm_props = {
@@ -81,14 +113,27 @@ class AzureCompute(VMCompute):
         }
         if spot:
             vm_props.update({"priority": "Spot", "evictionPolicy": "Delete", "billingProfile": {"maxPrice": -1}})
-        res = [
+        nic_deps = [f"[resourceId('Microsoft.Network/publicIPAddresses', '{name}-ip')]"]
+        res = self._network_resources(region) if own_network else []
+        if own_network:
+            nic_deps.append(f"[resourceId('Microsoft.Network/virtualNetworks', 'dstack-vnet-{region}')]")
+        nic_props = {"enableAcceleratedNetworking": True, "ipConfigurations": [{"name": "ipconfig1", "properties": {
+            "subnet": {"id": subnet}, "publicIPAddress": {"id": f"[resourceId('Microsoft.Network/"
+                                                                  f"publicIPAddresses', '{name}-ip')]"}}}]}
+        if extra_ports:  # a gateway: its own NSG on the NIC admits HTTP(S) from anywhere
+            gnsg = f"{name}-nsg"
+            res.append({"type": "Microsoft.Network/networkSecurityGroups", "apiVersion": "2023-04-01", "name": gnsg,
+                        "location": region, "properties": {"securityRules": [
+                            self._rule(f"p{p}", 100 + i, str(p)) for i, p in enumerate((22, *extra_ports))]}})
+            nic_deps.append(f"[resourceId('Microsoft.Network/networkSecurityGroups', '{gnsg}')]")
+            nic_props["networkSecurityGroup"] = {"id": f"[resourceId('Microsoft.Network/networkSecurityGroups', "
+                                                       f"'{gnsg}')]"}
+            nic_props["enableAcceleratedNetworking"] = False
+        res += [
             {"type": "Microsoft.Network/publicIPAddresses", "apiVersion": "2023-04-01", "name": f"{name}-ip",
              "location": region, "sku": {"name": "Standard"}, "properties": {"publicIPAllocationMethod": "Static"}},
             {"type": "Microsoft.Network/networkInterfaces", "apiVersion": "2023-04-01", "name": f"{name}-nic",
-             "location": region, "dependsOn": [f"[resourceId('Microsoft.Network/publicIPAddresses', '{name}-ip')]"],
-             "properties": {"enableAcceleratedNetworking": True, "ipConfigurations": [{"name": "ipconfig1", "properties": {
-                 "subnet": {"id": subnet}, "publicIPAddress": {"id": f"[resourceId('Microsoft.Network/"
-                                                                       f"publicIPAddresses', '{name}-ip')]"}}}]}},
+             "location": region, "dependsOn": nic_deps, "properties": nic_props},
             {"type": "Microsoft.Compute/virtualMachines", "apiVersion": "2023-03-01", "name": name, "location": region,
              "dependsOn": [f"[resourceId('Microsoft.Network/networkInterfaces', '{name}-nic')]"],
              "properties": vm_props},
@@ -126,11 +171,59 @@ class AzureCompute(VMCompute):
     def _terminate(self, instance_id, region, backend_data):
         rg = backend_data.get("resource_group", f"dstack-{region}")
         base = f"{self.ARM}/subscriptions/{self.subscription}/resourceGroups/{rg}/providers"
-        for path, ver in ((f"Microsoft.Compute/virtualMachines/{instance_id}", "2023-03-01"),
-                          (f"Microsoft.Network/publicIPAddresses/{instance_id}-ip", "2023-04-01")):
+        # the VM deletes its OS disk and NIC (deleteOption); the public IP and a gateway's NSG go
+        # after it (Azure refuses to delete an IP still bound to a NIC: the VM delete is awaited)
+        paths = [(f"Microsoft.Compute/virtualMachines/{instance_id}", "2023-03-01"),
+                 (f"Microsoft.Network/publicIPAddresses/{instance_id}-ip", "2023-04-01")]
+        if backend_data.get("gateway"):
+            paths.append((f"Microsoft.Network/networkSecurityGroups/{instance_id}-nsg", "2023-04-01"))
+        for i, (path, ver) in enumerate(paths):
             r = self.http.delete(f"{base}/{path}?api-version={ver}", headers=self._h())
             if r.status_code not in (200, 202, 204, 404):
                 check_response(r, f"azure delete {path}")
+            if i == 0 and r.status_code == 202 and r.headers.get("azure-asyncoperation"):
+                self._await(r.headers["azure-asyncoperation"])
+
+    def _await(self, op_url: str, tries: int = 120, delay: float = 5.0):
+        for _ in range(tries):
+            st = self.http.get(op_url, headers=self._h()).json().get("status", "")
+            if st in ("Succeeded", "Failed", "Canceled"):
+                return st
+            time.sleep(delay)
+        return "Timeout"
+
+    # ---- gateway ------------------------------------------------------------------------------
+    def create_gateway(self, configuration):
+        """A small VM (``Standard_B2s``) with the versioned gateway app, its own NSG admitting
+        22/80/443, and a static public IP (reference ``C/backends/azure/compute.py`` create_gateway)."""
+        from dstack_amd.core.backends.clouds.gateway_boot import gateway_cloud_init
+        from dstack_amd.core.models.gateways import GatewayProvisioningData
+
+        region = configuration.region
+        rg = self._rg(region)
+        name = f"{configuration.instance_name}".replace("_", "-")[:60]
+        tpl = self._template(name, self.config.get("gateway_vm_size", "Standard_B2s"), region,
+                             gateway_cloud_init(configuration), 30, False, [configuration.ssh_key_pub.strip()],
+                             extra_ports=(80, 443))
+        url = (f"{self.ARM}/subscriptions/{self.subscription}/resourcegroups/{rg}/providers/"
+               f"Microsoft.Resources/deployments/{name}?api-version=2021-04-01")
+        check_response(self.http.put(url, headers=self._h(), json={"properties": {"mode": "Incremental",
+                                                                                  "template": tpl}}), "azure gateway")
+        data = {"resource_group": rg, "gateway": True}
+        for _ in range(120):
+            info = self._describe(name, region, data)
+            if info.get("status") == "failed":
+                raise ComputeError(f"azure gateway deployment failed: {info.get('error')}")
+            if info.get("hostname"):
+                return GatewayProvisioningData(instance_id=name, ip_address=info["hostname"], region=region,
+                                               backend_data=json.dumps(data))
+            time.sleep(5)
+        raise ComputeError(f"azure gateway {name} got no public IP")
+
+    def terminate_gateway(self, instance_id, configuration, backend_data=None):
+        data = json.loads(backend_data or "{}")
+        data.setdefault("gateway", True)
+        self._terminate(instance_id, configuration.region, data)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -206,6 +299,139 @@ class GCPCompute(VMCompute):
         if r.status_code != 404:
             check_response(r, "gcp delete")
 
+    def _wait_op(self, r, what: str, tries: int = 120, delay: float = 2.0) -> dict:
+        """Wait for a zonal/global operation returned by a mutating call; raise on its error."""
+        op = r.json()
+        link = op.get("selfLink")
+        for _ in range(tries):
+            if op.get("status") == "DONE":
+                if op.get("error"):
+                    errs = op["error"].get("errors") or [{}]
+                    msg = "; ".join(f"{e.get('code')}: {e.get('message')}" for e in errs)
+                    from dstack_amd.core.errors import NoCapacityError
+
+                    if any("RESOURCE" in (e.get("code") or "") or "STOCKOUT" in (e.get("code") or "") for e in errs):
+                        raise NoCapacityError(f"{what}: {msg}")
+                    raise ComputeError(f"{what}: {msg}")
+                return op
+            if not link:
+                return op
+            time.sleep(delay)
+            op = check_response(self.http.get(link, headers=self._h()), what).json()
+        raise ComputeError(f"{what}: operation did not finish")
+
+    # ---- gateway ------------------------------------------------------------------------------
+    GATEWAY_TAG = "dstack-gateway"
+
+    def _gateway_firewall(self):
+        body = {"name": "dstack-gateway-in-all", "network": self.config.get("vpc", "global/networks/default"),
+                "direction": "INGRESS", "targetTags": [self.GATEWAY_TAG], "sourceRanges": ["0.0.0.0/0"],
+                "allowed": [{"IPProtocol": "tcp", "ports": ["22", "80", "443"]}],
+                "description": "dstack-amd gateways: SSH from the server, HTTP(S) from clients"}
+        r = self.http.post(f"{self.API}/projects/{self.project}/global/firewalls", headers=self._h(), json=body)
+        if r.status_code != 409:  # already exists
+            self._wait_op(check_response(r, "gcp gateway firewall"), "gcp gateway firewall")
+
+    def create_gateway(self, configuration):
+        """An ``e2-small`` VM tagged ``dstack-gateway`` (firewall 22/80/443) running the versioned
+        gateway app; waits for its external IP (reference ``C/backends/gcp/compute.py``)."""
+        from dstack_amd.core.backends.clouds.gateway_boot import gateway_cloud_init
+        from dstack_amd.core.models.gateways import GatewayProvisioningData
+
+        self._gateway_firewall()
+        zone = self._zone(configuration.region)
+        name = configuration.instance_name.lower().replace("_", "-")[:62]
+        body = {
+            "name": name, "machineType": f"zones/{zone}/machineTypes/{self.config.get('gateway_machine_type', 'e2-small')}",
+            "tags": {"items": [self.GATEWAY_TAG]},
+            "disks": [{"boot": True, "autoDelete": True, "initializeParams": {
+                "sourceImage": "projects/ubuntu-os-cloud/global/images/family/ubuntu-2204-lts", "diskSizeGb": "10"}}],
+            "networkInterfaces": [{"network": self.config.get("vpc", "global/networks/default"),
+                                   "accessConfigs": [{"type": "ONE_TO_ONE_NAT", "name": "External NAT"}]}],
+            "metadata": {"items": [{"key": "user-data", "value": gateway_cloud_init(configuration)},
+                                   {"key": "ssh-keys", "value": f"ubuntu:{configuration.ssh_key_pub.strip()}"}]},
+            "labels": {"owner": "dstack", "dstack_project": configuration.project_name.lower(), "role": "gateway"},
+        }
+        r = check_response(self.http.post(f"{self.API}/projects/{self.project}/zones/{zone}/instances",
+                                          headers=self._h(), json=body), "gcp gateway insert")
+        self._wait_op(r, "gcp gateway insert")
+        for _ in range(60):
+            info = self._describe(name, configuration.region, {"zone": zone})
+            if info.get("hostname"):
+                return GatewayProvisioningData(instance_id=name, ip_address=info["hostname"],
+                                               region=configuration.region, availability_zone=zone,
+                                               backend_data=json.dumps({"zone": zone}))
+            time.sleep(5)
+        raise ComputeError(f"gcp gateway {name} got no external IP")
+
+    def terminate_gateway(self, instance_id, configuration, backend_data=None):
+        self._terminate(instance_id, configuration.region, json.loads(backend_data or "{}"))
+
+    # ---- volumes: zonal persistent disks (reference ``C/backends/gcp/compute.py`` volumes) -------
+    def _disk_url(self, zone: str, name: str = "") -> str:
+        return f"{self.API}/projects/{self.project}/zones/{zone}/disks" + (f"/{name}" if name else "")
+
+    @staticmethod
+    def _volume_zone(volume) -> str:
+        pd = volume.provisioning_data
+        return (pd.availability_zone if pd and pd.availability_zone else None) or f"{volume.configuration.region}-a"
+
+    def register_volume(self, volume):
+        from dstack_amd.core.models.volumes import VolumeProvisioningData
+
+        zone = self._zone(volume.configuration.region)
+        r = self.http.get(self._disk_url(zone, volume.configuration.volume_id), headers=self._h())
+        if r.status_code == 404:
+            raise ComputeError(f"disk {volume.configuration.volume_id} not found in {zone}")
+        d = check_response(r, "gcp get disk").json()
+        return VolumeProvisioningData(backend=self.TYPE, volume_id=d["name"], size_gb=int(d.get("sizeGb", 0)),
+                                      availability_zone=zone)
+
+    def create_volume(self, volume):
+        from dstack_amd.core.models.volumes import VolumeProvisioningData
+
+        zone = self._zone(volume.configuration.region)
+        size = int(volume.configuration.size or 100)
+        name = f"{volume.name}-{str(volume.id)[:8]}".lower().replace("_", "-")[:62]
+        body = {"name": name, "sizeGb": str(size), "type": f"zones/{zone}/diskTypes/"
+                f"{self.config.get('volume_disk_type', 'pd-balanced')}",
+                "labels": {"owner": "dstack", "dstack_project": volume.project_name.lower()}}
+        r = check_response(self.http.post(self._disk_url(zone), headers=self._h(), json=body), "gcp create disk")
+        self._wait_op(r, "gcp create disk")
+        return VolumeProvisioningData(backend=self.TYPE, volume_id=name, size_gb=size, availability_zone=zone,
+                                      price=0.10 * size / 730)
+
+    def delete_volume(self, volume):
+        r = self.http.delete(self._disk_url(self._volume_zone(volume), volume.volume_id), headers=self._h())
+        if r.status_code != 404:
+            self._wait_op(check_response(r, "gcp delete disk"), "gcp delete disk")
+
+    def attach_volume(self, volume, instance_id):
+        from dstack_amd.core.models.volumes import VolumeAttachmentData
+
+        zone = self._volume_zone(volume)
+        body = {"source": f"projects/{self.project}/zones/{zone}/disks/{volume.volume_id}",
+                "deviceName": volume.volume_id, "mode": "READ_WRITE", "autoDelete": False}
+        r = check_response(self.http.post(f"{self.API}/projects/{self.project}/zones/{zone}/instances/"
+                                          f"{instance_id}/attachDisk", headers=self._h(), json=body), "gcp attach")
+        self._wait_op(r, "gcp attach disk")
+        # the shim resolves /dev/disk/by-id/google-<device name> (native/shim/volumes.cpp)
+        return VolumeAttachmentData(device_name=volume.volume_id)
+
+    def detach_volume(self, volume, instance_id, force=False):
+        zone = self._volume_zone(volume)
+        r = self.http.post(f"{self.API}/projects/{self.project}/zones/{zone}/instances/{instance_id}/detachDisk"
+                           f"?deviceName={urllib.parse.quote(volume.volume_id)}", headers=self._h())
+        if r.status_code != 404:
+            self._wait_op(check_response(r, "gcp detach"), "gcp detach disk")
+
+    def is_volume_detached(self, volume, instance_id):
+        r = self.http.get(self._disk_url(self._volume_zone(volume), volume.volume_id), headers=self._h())
+        if r.status_code == 404:
+            return True
+        users = check_response(r, "gcp get disk").json().get("users") or []
+        return not any(u.rstrip("/").endswith(f"/instances/{instance_id}") for u in users)
+
 
 # ---------------------------------------------------------------------------------------------
 class OCICompute(VMCompute):
@@ -243,7 +469,7 @@ class OCICompute(VMCompute):
         body = {
             "compartmentId": comp, "availabilityDomain": ads.get(region, f"{region}-AD-1"), "shape": offer.instance.name,
             "displayName": cfg.instance_name,
-            "sourceDetails": {"sourceType": "image", "imageId": (self.config.get("images") or {}).get(region, ""),
+            "sourceDetails": {"sourceType": "image", "imageId": self._image_id(region, comp, offer.instance.name),
                               "bootVolumeSizeInGBs": max(100, offer.instance.resources.disk.size_mib // 1024)},
             "createVnicDetails": {"subnetId": (self.config.get("subnet_ids") or {}).get(region), "assignPublicIp": True},
             "metadata": {"ssh_authorized_keys": "\n".join(cfg.get_public_keys()),
@@ -253,6 +479,20 @@ class OCICompute(VMCompute):
             body["preemptibleInstanceConfig"] = {"preemptionAction": {"type": "TERMINATE", "preserveBootVolume": False}}
         r = check_response(self._signed("POST", region, f"/{self.API_VERSION}/instances", body), "oci launch")
         return r.json()["id"], None, {"compartment": comp}
+
+    def _image_id(self, region: str, compartment: str, shape: str) -> str:
+        """The configured image, else the newest Canonical Ubuntu 22.04 image compatible with the
+        shape (the GPU bare-metal shapes need their own image builds, so the shape filter matters)."""
+        img = (self.config.get("images") or {}).get(region)
+        if img:
+            return img
+        q = urllib.parse.urlencode({"compartmentId": compartment, "operatingSystem": "Canonical Ubuntu",
+                                    "operatingSystemVersion": "22.04", "shape": shape, "sortBy": "TIMECREATED",
+                                    "sortOrder": "DESC", "lifecycleState": "AVAILABLE"})
+        items = check_response(self._signed("GET", region, f"/{self.API_VERSION}/images?{q}"), "oci images").json()
+        if not items:
+            raise ComputeError(f"no Ubuntu 22.04 image for shape {shape} in {region}; set images.{region}")
+        return items[0]["id"]
 
     def _describe(self, instance_id, region, backend_data):
         r = self._signed("GET", region, f"/{self.API_VERSION}/instances/{urllib.parse.quote(instance_id)}")
@@ -274,5 +514,3 @@ class OCICompute(VMCompute):
         if r.status_code not in (200, 204, 404):
             check_response(r, "oci terminate")
 
-
-_ = (Dict, Tuple, ComputeError)

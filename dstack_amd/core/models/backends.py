@@ -41,8 +41,8 @@ BACKENDS_WITH_PLACEMENT_GROUPS_SUPPORT = [BackendType.AWS]
 BACKENDS_WITH_RESERVATION_SUPPORT = [BackendType.AWS]
 BACKENDS_WITH_GATEWAY_SUPPORT = [BackendType.AWS, BackendType.AZURE, BackendType.GCP, BackendType.KUBERNETES,
                                  BackendType.LOCAL]
-BACKENDS_WITH_VOLUMES_SUPPORT = [BackendType.AWS, BackendType.GCP, BackendType.LOCAL, BackendType.RUNPOD,
-                                 BackendType.REMOTE]
+# SSH fleets (remote) have no network-volume API: they use instance mounts (``/host/path:/path``)
+BACKENDS_WITH_VOLUMES_SUPPORT = [BackendType.AWS, BackendType.GCP, BackendType.LOCAL, BackendType.RUNPOD]
 BACKENDS_WITH_PRIVILEGED_SUPPORT = [b for b in BackendType if b not in (BackendType.RUNPOD, BackendType.VASTAI)]
 BACKENDS_WITH_INSTANCE_VOLUMES_SUPPORT = [b for b in BackendType if b not in (BackendType.RUNPOD, BackendType.VASTAI,
                                                                               BackendType.KUBERNETES)]

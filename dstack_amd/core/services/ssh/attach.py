@@ -10,7 +10,6 @@
 
 from __future__ import annotations
 
-import os
 import select
 import socket
 import subprocess
@@ -162,6 +161,3 @@ class RunAttach:
             self._proc = None
             update_ssh_config(self.run_name, None)
             update_ssh_config(f"{self.run_name}-host", None)
-
-
-_ = os

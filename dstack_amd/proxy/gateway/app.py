@@ -188,7 +188,10 @@ def make_app(gw: Gateway) -> FastAPI:
 
     @r.get("/api/healthcheck")
     async def healthcheck():
-        return {"service": "dstack-gateway", "services": len(gw.registry.services)}
+        from dstack_amd import __version__
+
+        # ``version`` is what update.sh and the server's init_gateways compare against
+        return {"service": "dstack-gateway", "version": __version__, "services": len(gw.registry.services)}
 
     @r.post("/api/config")
     async def config(body: ConfigBody):

@@ -25,7 +25,7 @@ from dstack_amd.core.errors import (
     UnauthorizedError,
 )
 from dstack_amd.server import settings
-from dstack_amd.server.db import get_db, migrate, session_scope
+from dstack_amd.server.db import migrate, session_scope
 
 logger = logging.getLogger("dstack_amd.server")
 
@@ -81,6 +81,13 @@ def create_app(start_background: bool = True) -> FastAPI:
 
         token = await run_in_threadpool(init_server_state)
         app.state.admin_token = token
+        if start_background:
+            from dstack_amd.server.services.gateways import init_gateways
+
+            try:
+                await run_in_threadpool(init_gateways)
+            except Exception:  # noqa: BLE001 - gateways must never keep the server from starting
+                logger.exception("gateway init failed")
         sched = None
         if start_background and settings.SERVER_BACKGROUND_PROCESSING_ENABLED:
             from dstack_amd.server.background import start_background_tasks
@@ -220,6 +227,3 @@ def _compatible(client_version: str) -> bool:
         return client_version.split(".")[0] == __version__.split(".")[0]
     except Exception:  # noqa: BLE001
         return True
-
-
-_ = get_db

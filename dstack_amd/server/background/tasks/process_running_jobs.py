@@ -9,7 +9,6 @@ passes.  Every stage is stamped into ``job.timings`` (cold-start instrumentation
 
 from __future__ import annotations
 
-import base64
 import logging
 import time
 from datetime import timedelta
@@ -356,6 +355,3 @@ def _runner_unreachable(job: JobModel, err: str):
         jobs_services.terminate_job(job, JobTerminationReason.INTERRUPTED_BY_NO_CAPACITY,
                                     f"runner unreachable: {err}", delay=False)
         scheduler.wake(scheduler.TERMINATING_JOBS, scheduler.RUNS)
-
-
-_ = base64

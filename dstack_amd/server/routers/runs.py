@@ -6,7 +6,6 @@ from __future__ import annotations
 from typing import List, Optional, Tuple
 
 from fastapi import APIRouter, Depends, Query
-from sqlalchemy import select
 from sqlalchemy.orm import Session
 
 from dstack_amd.core.errors import ResourceNotExistsError, ServerClientError
@@ -17,7 +16,7 @@ from dstack_amd.core.models.runs import Run, RunPlan
 from dstack_amd.core.models.volumes import Volume, VolumePlan, VolumeSpec
 from dstack_amd.server import schemas
 from dstack_amd.server.deps import get_session
-from dstack_amd.server.models import JobModel, ProjectModel, UserModel
+from dstack_amd.server.models import ProjectModel, UserModel
 from dstack_amd.server.security.permissions import authenticated, project_admin, project_manager, project_member
 from dstack_amd.server.services import fleets as fleets_services
 from dstack_amd.server.services import gateways as gateways_services
@@ -345,6 +344,3 @@ def get_job_metrics(run_name: str, replica_num: int = Query(0), job_num: int = Q
         raise ResourceNotExistsError("Job not found")
     job = max(jobs, key=lambda j: j.submission_num)
     return metrics_services.get_job_metrics(s, job, limit)
-
-
-_ = (select, JobModel)

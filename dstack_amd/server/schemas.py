@@ -13,7 +13,7 @@ from dstack_amd.core.models.fleets import FleetSpec
 from dstack_amd.core.models.gateways import GatewayConfiguration
 from dstack_amd.core.models.instances import SSHKey
 from dstack_amd.core.models.profiles import Profile
-from dstack_amd.core.models.runs import ApplyRunPlanInput, Requirements, Run, RunSpec
+from dstack_amd.core.models.runs import ApplyRunPlanInput, Requirements, RunSpec
 from dstack_amd.core.models.users import GlobalRole, ProjectRole
 from dstack_amd.core.models.volumes import VolumeConfiguration
 
@@ -227,7 +227,6 @@ class ListVolumesRequest(_Req):
     only_active: bool = False
 
 
-_ = Run
 
 
 # ---- legacy pools (reference: S/schemas/pools.py, S/schemas/runs.py AddRemoteInstanceRequest) ----

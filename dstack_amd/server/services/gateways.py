@@ -88,14 +88,64 @@ def create_gateway(s: Session, project: ProjectModel, conf: GatewayConfiguration
     return gateway_model_to_gateway(g)
 
 
+def _compute_configuration(g: GatewayModel):
+    from dstack_amd.core.models.gateways import GatewayComputeConfiguration
+
+    conf = GatewayConfiguration.model_validate_json(g.configuration) if g.configuration else None
+    comp = g.gateway_compute
+    if conf is None or comp is None:
+        return None
+    return GatewayComputeConfiguration(project_name=g.project.name, instance_name=g.name, backend=conf.backend,
+                                       region=conf.region, public_ip=conf.public_ip,
+                                       ssh_key_pub=comp.ssh_public_key or "", certificate=conf.certificate)
+
+
+def terminate_gateway_compute(s: Session, g: GatewayModel) -> bool:
+    """Terminate the gateway's VM through its backend (reference
+    ``S/services/gateways/__init__.py:226-255``); ``False`` when the cloud call failed (the gateway
+    row is kept so the user can retry the delete instead of leaking a billed VM)."""
+    comp = g.gateway_compute
+    if comp is None or not comp.active or comp.deleted:
+        return True
+    conf = _compute_configuration(g)
+    if conf is None or conf.backend == BackendType.LOCAL:
+        return True
+    from dstack_amd.server.services import backends as backends_services
+
+    last = None
+    for attempt in range(3):
+        try:
+            compute = backends_services.get_project_backend(s, g.project, conf.backend)
+            logger.info("Deleting gateway compute %s (%s) of %s", comp.instance_id, conf.backend.value, g.name)
+            compute.terminate_gateway(comp.instance_id, conf, comp.backend_data)
+            logger.info("Deleted gateway compute of %s", g.name)
+            return True
+        except Exception as e:  # noqa: BLE001
+            last = e
+            logger.warning("Deleting gateway compute of %s failed (attempt %d): %s", g.name, attempt + 1, e)
+            import time
+
+            time.sleep(0.2 * (attempt + 1))
+    logger.error("Gateway %s kept: its compute %s could not be terminated: %s", g.name, comp.instance_id, last)
+    return False
+
+
 def delete_gateways(s: Session, project: ProjectModel, names: List[str]):
+    gws = []
     for n in names:
         g = get_gateway_by_name(s, project, n)
         if g is None:
             raise ResourceNotExistsError(f"Gateway {n} not found")
+        gws.append(g)
+    failed = []
+    for g in gws:
+        if not terminate_gateway_compute(s, g):
+            failed.append(g.name)
+            continue
         if project.default_gateway_id == g.id:
             project.default_gateway_id = None
         if g.gateway_compute:
+            _drop_tunnel(g)
             g.gateway_compute.active = False
             g.gateway_compute.deleted = True
         local = LocalGatewayProcess._instances.pop(f"{project.name}/{g.name}", None)
@@ -105,6 +155,22 @@ def delete_gateways(s: Session, project: ProjectModel, names: List[str]):
         s.query(RunModel).filter(RunModel.gateway_id == g.id).update({RunModel.gateway_id: None},
                                                                        synchronize_session="fetch")
         s.delete(g)
+    if failed:
+        s.commit()  # the gateways that were terminated stay deleted
+        raise GatewayError(f"Failed to terminate the compute of gateway(s) {', '.join(failed)}; retry the delete")
+
+
+def _drop_tunnel(g: GatewayModel):
+    comp = g.gateway_compute
+    data = json.loads(comp.backend_data or "{}")
+    if data.get("api_url") or not comp.ip_address:
+        return
+    from dstack_amd.core.services.ssh.tunnel import SSHTarget, get_tunnel_pool
+
+    try:
+        get_tunnel_pool().close(SSHTarget(comp.ip_address, data.get("ssh_user", "ubuntu"), int(data.get("ssh_port", 22))))
+    except Exception as e:  # noqa: BLE001
+        logger.debug("closing gateway tunnel: %s", e)
 
 
 def set_default_gateway(s: Session, project: ProjectModel, name: str):
@@ -298,3 +364,141 @@ def provision_gateway(s: Session, g: GatewayModel):
     s.flush()
     g.gateway_compute_id = comp.id
     g.status = GatewayStatus.PROVISIONING.value
+
+
+# ---------------------------------------------------------------------------------------------
+# server start: reconnect, blue/green app update, configure (reference
+# ``S/services/gateways/__init__.py:356-430``)
+# ---------------------------------------------------------------------------------------------
+UPDATE_COOLDOWN_S = 60
+
+
+def _ssh_target(comp: GatewayComputeModel):
+    from dstack_amd.core.services.ssh.tunnel import SSHTarget
+
+    data = json.loads(comp.backend_data or "{}")
+    return SSHTarget(comp.ip_address, data.get("ssh_user", "ubuntu"), int(data.get("ssh_port", 22)))
+
+
+def update_gateway_app(comp: GatewayComputeModel, version: Optional[str] = None, url: Optional[str] = None) -> bool:
+    """Push the server's ``update.sh`` and run the blue/green update to ``version`` on the gateway
+    host over SSH; True when the new app reported healthy (else update.sh rolled back)."""
+    from dstack_amd import __version__
+    from dstack_amd.core.services.ssh.tunnel import get_tunnel_pool
+    from dstack_amd.proxy.gateway import packaging
+
+    version = version or __version__
+    url = url or packaging.package_url(version)
+    pool, target = get_tunnel_pool(), _ssh_target(comp)
+    r = pool.run(target, comp.ssh_private_key, "mkdir -p dstack && cat > dstack/update.sh",
+                 input=packaging.UPDATE_SH.encode(), timeout=60)
+    if r.returncode != 0:
+        raise GatewayError(f"pushing update.sh failed: {r.stderr.decode(errors='replace')[-300:]}")
+    r = pool.run(target, comp.ssh_private_key, packaging.remote_update_command(url, version), timeout=600)
+    out = r.stdout.decode(errors="replace")
+    if "Update successfully completed" in out:
+        logger.info("Gateway %s updated to %s", comp.ip_address, version)
+        return True
+    logger.warning("Gateway %s update to %s failed: %s", comp.ip_address, version, out[-500:])
+    return False
+
+
+def _recently_updated(comp: GatewayComputeModel) -> bool:
+    from datetime import timedelta
+
+    t = comp.app_updated_at
+    if t is None:
+        return False
+    now = get_current_datetime()
+    if t.tzinfo is None:
+        now = now.replace(tzinfo=None)
+    return t > now - timedelta(seconds=UPDATE_COOLDOWN_S)
+
+
+def _restart_local_gateway(s: Session, g: GatewayModel) -> str:
+    """A ``local`` gateway runs as a child of the server: after a server restart it is relaunched
+    on its persisted state (registered services and replicas come back from state-v2.json)."""
+    from dstack_amd.server import settings
+
+    key = f"{g.project.name}/{g.name}"
+    cur = LocalGatewayProcess._instances.get(key)
+    if cur is not None and cur.proc.poll() is None:
+        return "running"
+    proc = LocalGatewayProcess(key, str(settings.SERVER_DIR_PATH / "gateways" / g.project.name / g.name),
+                               settings.SERVER_URL)
+    comp = g.gateway_compute
+    data = json.loads(comp.backend_data or "{}")
+    data.update(api_url=f"http://127.0.0.1:{proc.control_port}", http_port=proc.http_port)
+    comp.backend_data = json.dumps(data)
+    comp.hostname = f"127.0.0.1:{proc.http_port}"
+    return "restarted"
+
+
+def _init_one(gateway_id, skip_update: bool) -> str:
+    from dstack_amd import __version__
+    from dstack_amd.server import settings
+    from dstack_amd.server.db import session_scope
+
+    with session_scope() as s:
+        g = s.get(GatewayModel, gateway_id)
+        if g is None or g.gateway_compute is None:
+            return "gone"
+        if BackendType(g.backend.type) == BackendType.LOCAL:
+            return _restart_local_gateway(s, g)
+        comp = g.gateway_compute
+        try:
+            health = _call(g, "GET", "/api/healthcheck")
+        except Exception as e:  # noqa: BLE001 - an unreachable gateway must not block the server start
+            logger.warning("Failed to connect to gateway %s: %s", comp.ip_address, e)
+            return "unreachable"
+        state = "connected"
+        if health.get("version") != __version__ and not skip_update:
+            if _recently_updated(comp):
+                logger.debug("Skipping gateway %s update: updated recently", comp.ip_address)
+            else:
+                try:
+                    if update_gateway_app(comp):
+                        comp.app_updated_at = get_current_datetime()
+                        state = "updated"
+                    else:
+                        state = "update_failed"
+                except Exception as e:  # noqa: BLE001
+                    logger.warning("Failed to update gateway %s: %s", comp.ip_address, e)
+                    state = "update_failed"
+        try:
+            _call(g, "POST", "/api/config", {"server_url": settings.SERVER_URL})
+        except Exception as e:  # noqa: BLE001
+            logger.warning("Failed to configure gateway %s: %r", comp.ip_address, e)
+        return state
+
+
+def init_gateways(skip_update: Optional[bool] = None) -> dict:
+    """Run at server start (before the reconcilers): every active gateway is reconnected, its app
+    is updated blue/green when it runs another version than the server, and it is re-configured
+    with the server URL; local gateways are relaunched.  Gateways are handled concurrently and a
+    failing one is only logged.  Returns ``{gateway name: state}``."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from dstack_amd.server import settings
+    from dstack_amd.server.db import session_scope
+    from dstack_amd.server.services.locking import db_advisory_lock
+
+    if skip_update is None:
+        skip_update = settings.SKIP_GATEWAY_UPDATE
+    with session_scope() as s:
+        rows = s.execute(select(GatewayModel.id, GatewayModel.name).join(
+            GatewayComputeModel, GatewayModel.gateway_compute_id == GatewayComputeModel.id).where(
+            GatewayComputeModel.active.is_(True), GatewayComputeModel.deleted.is_(False))).all()
+    if not rows:
+        return {}
+    logger.info("Connecting to %d gateway(s)...", len(rows))
+    out = {}
+    with db_advisory_lock(None, "gateway_tunnels"), ThreadPoolExecutor(max_workers=min(8, len(rows))) as ex:
+        futs = {name: ex.submit(_init_one, gid, skip_update) for gid, name in rows}
+        for name, f in futs.items():
+            try:
+                out[name] = f.result()
+            except Exception as e:  # noqa: BLE001
+                logger.warning("gateway %s init failed: %s", name, e)
+                out[name] = "error"
+    return out

@@ -203,6 +203,3 @@ def decode_message(e: LogEvent) -> str:
 def write_job_logs(project: str, run_name: str, job_submission_id: str, pull: dict):
     get_default_log_storage().write_logs(project, run_name, job_submission_id, pull.get("runner_logs") or [],
                                          pull.get("job_logs") or [])
-
-
-_ = os

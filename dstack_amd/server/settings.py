@@ -35,6 +35,8 @@ SERVER_BACKGROUND_PROCESSING_ENABLED = not _env_bool("DSTACK_SERVER_BACKGROUND_P
 # Event-driven scheduling: background tasks are woken on state changes; the interval is only the
 # fallback poll. Set to 0 to reproduce the reference's pure-polling behaviour.
 SERVER_EVENT_DRIVEN = not _env_bool("DSTACK_SERVER_POLLING_ONLY")
+# server start: do not update the app on running gateways (reference DSTACK_SKIP_GATEWAY_UPDATE)
+SKIP_GATEWAY_UPDATE = _env_bool("DSTACK_SKIP_GATEWAY_UPDATE")
 
 SERVER_CLOUDWATCH_LOG_GROUP = os.getenv("DSTACK_SERVER_CLOUDWATCH_LOG_GROUP")
 SERVER_S3_BUCKET = os.getenv("DSTACK_SERVER_S3_BUCKET")

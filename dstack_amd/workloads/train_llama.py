@@ -60,8 +60,17 @@ def init_distributed(backend: str | None = None) -> DistEnv:
 
 class Trainer:
     def __init__(self, model_name: str, seq_len: int, micro_batch: int, device, lr: float = 3e-4,
-                 seed: int = 0, bucket_numel: int = 256 * 1024 * 1024, grad_accum: int = 1):
+                 seed: int = 0, bucket_numel: int = 256 * 1024 * 1024, grad_accum: int = 1,
+                 lr_warmup: int = 0, lr_decay_steps: int = 0, min_lr_ratio: float = 0.1, data_rows: int = 4):
         self.cfg = CONFIGS[model_name]
+        # LR schedule: linear warmup over ``lr_warmup`` optimizer steps, then constant, or cosine
+        # decay to ``min_lr_ratio * lr`` at step ``lr_decay_steps`` when that is set.  A random-init
+        # model hit with the full Adam step at step 1 overshoots (the loss climbs back above
+        # ln(vocab) within a few steps); the warmup is what keeps it descending.
+        self.base_lr = lr
+        self.lr_warmup = lr_warmup
+        self.lr_decay_steps = lr_decay_steps
+        self.min_lr_ratio = min_lr_ratio
         self.seq_len = seq_len
         self.micro_batch = micro_batch
         self.grad_accum = grad_accum
@@ -77,7 +86,7 @@ class Trainer:
         rank = dist.get_rank() if dist.is_initialized() else 0
         g = torch.Generator(device=device).manual_seed(1234 + rank)
         n = micro_batch * (seq_len + 1)
-        self.data = torch.randint(0, self.cfg.vocab_size, (4, n), device=device, generator=g)
+        self.data = torch.randint(0, self.cfg.vocab_size, (data_rows, n), device=device, generator=g)
         self._i = 0
 
     def batch(self):
@@ -85,9 +94,23 @@ class Trainer:
         self._i += 1
         return row[:, :-1], row[:, 1:]
 
+    def lr_at(self, step: int) -> float:
+        """Learning rate of optimizer step ``step`` (1-based)."""
+        import math
+
+        if self.lr_warmup and step <= self.lr_warmup:
+            return self.base_lr * step / self.lr_warmup
+        if self.lr_decay_steps and self.lr_decay_steps > self.lr_warmup:
+            t = min(1.0, (step - self.lr_warmup) / (self.lr_decay_steps - self.lr_warmup))
+            lo = self.min_lr_ratio * self.base_lr
+            return lo + 0.5 * (self.base_lr - lo) * (1 + math.cos(math.pi * t))
+        return self.base_lr
+
     def step(self) -> torch.Tensor:
         """One optimizer step = ``grad_accum`` micro-batches; the gradient reduce-scatter is armed
         only for the last micro-batch so it overlaps that backward."""
+        # set before backward: with optimizer-in-backward AdamW runs per bucket during it
+        self.opt.lr = self.lr_at(self.opt.step_count + 1)
         self.opt.zero_grad()
         total = None
         for i in range(self.grad_accum):
@@ -233,14 +256,16 @@ def _sync(env: DistEnv):
 
 
 def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1,
-        grad_accum: int = 1, checkpoint_dir: str | None = None, save_every: int = 0):
+        grad_accum: int = 1, checkpoint_dir: str | None = None, save_every: int = 0, lr: float = 3e-4,
+        lr_warmup: int = 10, lr_decay_steps: int = 0):
     env = init_distributed()
     device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     from dstack_amd.ops import gemm_tuning
 
     gemm_mode = gemm_tuning.setup(device_index=env.local_rank if device.type == "cuda" else 0)
     t0 = time.time()
-    tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum)
+    tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum, lr=lr, lr_warmup=lr_warmup,
+                 lr_decay_steps=lr_decay_steps)
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
               f"init={time.time()-t0:.1f}s gemm_tuning={gemm_mode}", flush=True)
@@ -290,6 +315,7 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         "max_mem_gb": torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else None,
     }
     result["tflops_per_gpu"] = tok_s / env.world * result["flops_per_token"] / 1e12
+    result["losses"] = [round(x.item(), 4) for x in losses]  # read after the timed region
     result["gemm_tuning"] = gemm_mode
     if env.rank == 0:
         print("[train] result " + json.dumps(result), flush=True)
@@ -309,9 +335,13 @@ def main(argv=None):
                     help="resume from here if it holds a checkpoint (e.g. a dstack volume mount)")
     ap.add_argument("--save-every", type=int, default=0,
                     help="save a checkpoint whenever the optimizer step count is a multiple of N")
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--lr-warmup", type=int, default=10, help="linear LR warmup (optimizer steps)")
+    ap.add_argument("--lr-decay-steps", type=int, default=0, help="cosine decay to 0.1*lr at this step (0: constant)")
     args = ap.parse_args(argv)
     env, tr, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup,
-                     grad_accum=args.grad_accum, checkpoint_dir=args.checkpoint_dir, save_every=args.save_every)
+                     grad_accum=args.grad_accum, checkpoint_dir=args.checkpoint_dir, save_every=args.save_every,
+                     lr=args.lr, lr_warmup=args.lr_warmup, lr_decay_steps=args.lr_decay_steps)
     if args.checkpoint_dir and not (args.save_every and tr.opt.step_count % args.save_every == 0):
         tr.save_checkpoint(args.checkpoint_dir)  # (a step that is a multiple of save_every is saved)
     if env.distributed:

@@ -114,6 +114,18 @@ AmdSmi::AmdSmi() {
     F.procs(socks[s], &np, ph.data());
     for (auto h : ph) handles_.push_back(h);
   }
+  // canonical GPU order = PCI BDF order, whatever order amdsmi reports its handles in: discover(),
+  // xgmi_matrix() and metrics() index the same sorted list, and the sysfs fallback sorts the same
+  // way, so an index means the same physical GPU on every path
+  if (F.bdf) {
+    std::vector<std::pair<std::string, amdsmi_processor_handle>> keyed;
+    for (auto h : handles_) {
+      amdsmi_bdf_t b{};
+      keyed.emplace_back(F.bdf(h, &b) == AMDSMI_STATUS_SUCCESS ? bdf_str(b) : std::string("~"), h);
+    }
+    std::stable_sort(keyed.begin(), keyed.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    for (size_t i = 0; i < keyed.size(); ++i) handles_[i] = keyed[i].second;
+  }
   ok_ = !handles_.empty();
 }
 
@@ -203,7 +215,10 @@ std::vector<AmdGpuMetrics> AmdSmi::metrics() {
 
 std::vector<AmdGpu> discover_amd_gpus_sysfs() {
   std::vector<AmdGpu> out;
-  DIR* d = opendir("/sys/class/drm");
+  // DSTACK_SYSFS_ROOT: a fake /sys tree (tests)
+  const char* root_env = getenv("DSTACK_SYSFS_ROOT");
+  const std::string root = root_env ? root_env : "";
+  DIR* d = opendir((root + "/sys/class/drm").c_str());
   if (!d) return out;
   std::vector<int> renders;
   while (auto* e = readdir(d)) {
@@ -213,7 +228,7 @@ std::vector<AmdGpu> discover_amd_gpus_sysfs() {
   closedir(d);
   std::sort(renders.begin(), renders.end());
   for (int r : renders) {
-    std::string base = "/sys/class/drm/renderD" + std::to_string(r) + "/device/";
+    std::string base = root + "/sys/class/drm/renderD" + std::to_string(r) + "/device/";
     std::string vendor;
     if (!read_file(base + "vendor", vendor) || trim(vendor) != "0x1002") continue;
     AmdGpu g;
@@ -221,7 +236,8 @@ std::vector<AmdGpu> discover_amd_gpus_sysfs() {
     g.drm_render = r;
     g.render_node = "/dev/dri/renderD" + std::to_string(r);
     char target[PATH_MAX];
-    ssize_t n = readlink(("/sys/class/drm/renderD" + std::to_string(r) + "/device").c_str(), target, sizeof target - 1);
+    ssize_t n = readlink((root + "/sys/class/drm/renderD" + std::to_string(r) + "/device").c_str(), target,
+                         sizeof target - 1);
     if (n > 0) {
       target[n] = 0;
       std::string t = target;
@@ -232,9 +248,13 @@ std::vector<AmdGpu> discover_amd_gpus_sysfs() {
     std::string pn;
     if (read_file(base + "product_name", pn)) g.market_name = trim(pn);
     g.name = g.market_name.empty() ? "AMD GPU" : amd_catalog_name(g.market_name);
-    g.numa_node = g.bdf.empty() ? -1 : numa_of_bdf(g.bdf);
+    std::string numa;
+    g.numa_node = read_file(base + "numa_node", numa) ? atoi(numa.c_str()) : -1;
     out.push_back(g);
   }
+  // BDF order (the amdsmi path sorts identically); render-node numbers need not follow the bus
+  std::stable_sort(out.begin(), out.end(), [](const AmdGpu& a, const AmdGpu& b) { return a.bdf < b.bdf; });
+  for (size_t i = 0; i < out.size(); ++i) out[i].index = (int)i;
   return out;
 }
 

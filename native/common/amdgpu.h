@@ -14,7 +14,7 @@
 namespace dsa {
 
 struct AmdGpu {
-  int index = 0;             // enumeration order (== HIP id on the host)
+  int index = 0;             // PCI BDF order on the host (amdsmi and sysfs discovery agree on it)
   std::string name;          // catalog name, e.g. MI355X
   std::string market_name;   // raw amdsmi market name
   std::string arch;          // gfx950

@@ -148,6 +148,9 @@ class DockerDriver : public TaskDriver {
     std::string gl;
     for (size_t k = 0; k < t.gpus.size(); ++k) gl += (k ? "," : "") + std::to_string(t.gpus[k]);
     labels.set("dstack.gpus", gl);
+    std::string rl;
+    for (size_t k = 0; k < t.render_nodes.size(); ++k) rl += (k ? "," : "") + t.render_nodes[k];
+    labels.set("dstack.render_nodes", rl);
     cfg.set("Labels", labels);
     Json hc = Json::object();
     Json binds = Json::array();
@@ -185,17 +188,17 @@ class DockerDriver : public TaskDriver {
       devices.push_back(d);
     };
     if (!t.gpus.empty()) {
+      // /dev/kfd (the compute queue device) + exactly the granted render nodes: the container's
+      // ROCm runtime then enumerates only the job's GPUs, in host BDF order
       add_dev("/dev/kfd");
-      auto gpus = discover_amd_gpus();
-      for (int g : t.gpus)
-        if (g < (int)gpus.size() && !gpus[(size_t)g].render_node.empty()) add_dev(gpus[(size_t)g].render_node);
+      for (auto& rn : t.render_nodes) add_dev(rn);
       Json groups = Json::array();
       groups.push_back("video");
       groups.push_back("render");
       hc.set("GroupAdd", groups);
     }
-    if (path_exists("/dev/infiniband")) {  // RCCL over RoCE/IB (docker.go:1039-1062)
-      add_dev("/dev/infiniband");
+    if (!o_.infiniband_path.empty() && path_exists(o_.infiniband_path)) {  // RCCL over RoCE/IB (docker.go:1039-1062)
+      add_dev(o_.infiniband_path);
       Json ul = Json::array();
       Json m = Json::object();
       m.set("Name", "memlock");
@@ -288,8 +291,12 @@ class DockerDriver : public TaskDriver {
       t.container_name = c["Names"][(size_t)0].str();
       for (auto& g : split(c["Labels"]["dstack.gpus"].str(), ','))
         if (!g.empty()) t.gpus.push_back(atoi(g.c_str()));
+      for (auto& rn : split(c["Labels"]["dstack.render_nodes"].str(), ','))
+        if (!rn.empty()) t.render_nodes.push_back(rn);
       std::string state = c["State"].str();
       t.status = state == "running" ? TaskStatus::Running : TaskStatus::Terminated;
+      // the runner port depends on the network mode (host: fixed; bridge: the published port)
+      if (c["HostConfig"].has("NetworkMode")) t.config.network_mode = c["HostConfig"]["NetworkMode"].str();
       inspect_ports(t);
       out.push_back(t);
     }

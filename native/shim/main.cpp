@@ -21,12 +21,27 @@ namespace dsa {
 static const char* SHIM_VERSION = "0.1.0-mi355x";
 
 Shim::Shim(ShimOptions o, std::unique_ptr<TaskDriver> driver) : opts_(std::move(o)), driver_(std::move(driver)) {
+  // ONE discovery: the lock's indices, the xGMI matrix rows and the render nodes handed to
+  // containers all refer to this snapshot (BDF order, amdgpu.h)
   auto gpus = discover_amd_gpus();
   std::vector<int> numa;
-  for (auto& g : gpus) numa.push_back(g.numa_node);
+  for (auto& g : gpus) {
+    numa.push_back(g.numa_node);
+    inventory_render_.push_back(g.render_node);
+  }
   auto& smi = AmdSmi::instance();
-  gpus_.init((int)gpus.size(), smi.available() ? smi.xgmi_matrix() : std::vector<std::vector<int>>{}, numa);
+  auto xgmi = smi.available() ? smi.xgmi_matrix() : std::vector<std::vector<int>>{};
+  if (xgmi.size() != gpus.size()) xgmi.clear();  // sysfs fallback: no topology, never a mismatched one
+  gpus_.init((int)gpus.size(), xgmi, numa);
   LOGI("shim: driver=%s gpus=%zu", driver_->name(), gpus.size());
+}
+
+std::vector<std::string> Shim::render_nodes_of(const std::vector<int>& idx) const {
+  std::vector<std::string> out;
+  for (int i : idx)
+    if (i >= 0 && i < (int)inventory_render_.size() && !inventory_render_[(size_t)i].empty())
+      out.push_back(inventory_render_[(size_t)i]);
+  return out;
 }
 
 void Shim::restore() {
@@ -94,6 +109,7 @@ void Shim::run_task(std::string id) {
   }
   if (!storage_.get(id, t)) return;
   t.gpus = granted;
+  t.render_nodes = render_nodes_of(granted);
   storage_.update(t);
   if (!t.config.host_ssh_keys.empty() && !t.config.host_ssh_user.empty())
     add_authorized_keys(t.config.host_ssh_user, t.config.host_ssh_keys);

@@ -56,7 +56,11 @@ struct Task {
   std::string termination_reason, termination_message;
   std::string container_name, container_id;
   std::vector<PortMapping> ports;
-  std::vector<int> gpus;  // granted GPU indices (host numbering)
+  std::vector<int> gpus;  // granted GPU indices (host numbering: BDF order, see amdgpu.h)
+  // render nodes of the granted GPUs, resolved from the shim's one discovery snapshot at grant time
+  // (the same snapshot the GPU lock and its xGMI matrix were built from) and kept in the container
+  // labels, so devices never come from a second, possibly differently ordered, discovery
+  std::vector<std::string> render_nodes;
   int runner_port = 0;
   int pid = 0;  // process driver
   int64_t created_ms = 0;
@@ -116,6 +120,7 @@ struct ShimOptions {
   std::string driver = "auto";  // docker | process | auto
   int pull_timeout_s = 20 * 60;
   std::string volumes_root = "/dstack-volumes";
+  std::string infiniband_path = "/dev/infiniband";  // RDMA devices passed through when present
 };
 
 class TaskDriver {
@@ -167,6 +172,8 @@ class Shim {
   const char* driver_name() const { return driver_->name(); }
   GpuLock& gpu_lock() { return gpus_; }
   void restore();
+  // render nodes of host GPU indices, from the discovery snapshot taken at construction
+  std::vector<std::string> render_nodes_of(const std::vector<int>& idx) const;
 
  private:
   void run_task(std::string id);
@@ -174,6 +181,7 @@ class Shim {
   std::unique_ptr<TaskDriver> driver_;
   TaskStorage storage_;
   GpuLock gpus_;
+  std::vector<std::string> inventory_render_;  // index -> /dev/dri/renderD*
   Json host_info_;
   std::mutex hi_mu_;
 };

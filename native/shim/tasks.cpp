@@ -81,6 +81,9 @@ Json Task::to_json() const {
   Json g = Json::array();
   for (int x : gpus) g.push_back(x);
   j.set("gpus", g);
+  Json rn = Json::array();
+  for (auto& r : render_nodes) rn.push_back(r);
+  j.set("render_nodes", rn);
   j.set("runner_port", runner_port);
   Json tj = Json::object();
   for (auto& kv : timings) tj.set(kv.first, (long long)kv.second);

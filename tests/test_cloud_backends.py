@@ -2,6 +2,7 @@
 backends/*``): request shapes, auth/signing, the create -> poll -> terminate flow, capacity errors."""
 
 import base64
+import os
 import json
 import re
 import subprocess
@@ -268,8 +269,14 @@ def test_oci_http_signature(rsa_pem):
         assert auth.startswith('Signature version="1",keyId="ten/usr/fp",algorithm="rsa-sha256"')
         if req.method == "POST":
             assert 'headers="(request-target) date host x-content-sha256 content-type content-length"' in auth
-            assert json.loads(req.content)["shape"] == "BM.GPU.MI300X.8"
+            body = json.loads(req.content)
+            assert body["shape"] == "BM.GPU.MI300X.8"
+            assert body["sourceDetails"]["imageId"] == "ocid1.image.ubuntu"  # looked up, never ""
             return httpx.Response(200, json={"id": "ocid1.instance"})
+        if req.url.path.endswith("/images"):
+            q = dict(urllib.parse.parse_qsl(req.url.query.decode()))
+            assert q["shape"] == "BM.GPU.MI300X.8" and q["operatingSystemVersion"] == "22.04"
+            return httpx.Response(200, json=[{"id": "ocid1.image.ubuntu"}, {"id": "ocid1.image.older"}])
         if "vnicAttachments" in str(req.url):
             return httpx.Response(200, json=[{"vnicId": "v1"}])
         if "/vnics/" in req.url.path:
@@ -369,3 +376,325 @@ def test_registry_image_config_with_token_challenge():
     rc = RegistryClient(_client(handler))
     cfg = rc.get_image_config("rocm/vllm")
     assert cfg.user == "1000:1000" and cfg.entrypoint == ["python3", "-m", "vllm"] and cfg.cmd == ["serve"]
+
+
+def _aws_vpc_handler(calls, capacity_fail_az=None, efa=True, reservation_type="capacity-block"):
+    def handler(req: httpx.Request):
+        form = dict(urllib.parse.parse_qsl(req.content.decode()))
+        a = form["Action"]
+        calls.append(form)
+        if a == "DescribeVpcs":
+            assert form["Filter.1.Value.1"] == "dstack-vpc"
+            return httpx.Response(200, text=_xml("<vpcSet><item><vpcId>vpc-9</vpcId></item></vpcSet>"))
+        if a == "DescribeSubnets":
+            if "NextToken" not in form:  # page 1 of 2
+                return httpx.Response(200, text=_xml(
+                    "<subnetSet><item><subnetId>sn-b</subnetId><availabilityZone>us-east-1b</availabilityZone>"
+                    "<mapPublicIpOnLaunch>false</mapPublicIpOnLaunch></item></subnetSet><nextToken>p2</nextToken>"))
+            return httpx.Response(200, text=_xml(
+                "<subnetSet><item><subnetId>sn-a</subnetId><availabilityZone>us-east-1a</availabilityZone>"
+                "<mapPublicIpOnLaunch>false</mapPublicIpOnLaunch></item></subnetSet>"))
+        if a == "DescribeInstanceTypes":
+            info = ("<networkInfo><efaSupported>true</efaSupported><maximumNetworkCards>32</maximumNetworkCards>"
+                    "<efaInfo><maximumEfaInterfaces>32</maximumEfaInterfaces></efaInfo></networkInfo>") if efa else \
+                "<networkInfo><efaSupported>false</efaSupported></networkInfo>"
+            return httpx.Response(200, text=_xml(f"<instanceTypeSet><item>{info}</item></instanceTypeSet>"))
+        if a == "DescribeCapacityReservations":
+            return httpx.Response(200, text=_xml(
+                "<capacityReservationSet><item><state>active</state><availabilityZone>us-east-1b</availabilityZone>"
+                f"<reservationType>{reservation_type}</reservationType><instanceType>p5.48xlarge</instanceType>"
+                "</item></capacityReservationSet>"))
+        if a == "DescribeImages":
+            return httpx.Response(200, text=_xml("<imagesSet><item><imageId>ami-1</imageId></item></imagesSet>"))
+        if a == "DescribeSecurityGroups":
+            assert form.get("Filter.2.Value.1") == "vpc-9"
+            return httpx.Response(200, text=_xml("<securityGroupInfo><item><groupId>sg-9</groupId></item>"
+                                                 "</securityGroupInfo>"))
+        if a == "RunInstances":
+            if form.get("NetworkInterface.1.SubnetId") == capacity_fail_az:
+                return httpx.Response(500, text=_xml("<Errors><Error><Code>InsufficientInstanceCapacity</Code>"
+                                                     "<Message>no</Message></Error></Errors>"))
+            return httpx.Response(200, text=_xml("<instancesSet><item><instanceId>i-9</instanceId></item>"
+                                                 "</instancesSet>"))
+        if a == "DescribeInstances":
+            return httpx.Response(200, text=_xml("<reservationSet><item><instancesSet><item><instanceState><name>"
+                                                 "running</name></instanceState><ipAddress>3.3.3.3</ipAddress>"
+                                                 "<privateIpAddress>10.9.0.5</privateIpAddress></item></instancesSet>"
+                                                 "</item></reservationSet>"))
+        return httpx.Response(400, text=_xml(f"<Errors><Error><Code>Unexpected{a}</Code></Error></Errors>"))
+    return handler
+
+
+def test_aws_named_vpc_private_efa_cluster_interfaces():
+    """p5.48xlarge in a named VPC without public IPs: all 32 EFA cards requested (every 4th ``efa``,
+    the rest ``efa-only``), subnets from a paginated DescribeSubnets tried one AZ at a time (the first
+    AZ has no capacity), and the host reached on its private address."""
+    calls = []
+    c = compute_class(BackendType.AWS)({"vpc_name": "dstack-vpc", "public_ips": False},
+                                       {"access_key": "AK", "secret_key": "SK"},
+                                       _client(_aws_vpc_handler(calls, capacity_fail_az="sn-a")))
+    offer = _offer(c, "H100:8")
+    assert offer.instance.name == "p5.48xlarge"
+    jpd = c.create_instance(offer, CFG)
+    runs = [f for f in calls if f["Action"] == "RunInstances"]
+    assert [r["NetworkInterface.1.SubnetId"] for r in runs] == ["sn-a", "sn-b"]  # us-east-1a first, then 1b
+    r = runs[-1]
+    assert "SecurityGroupId.1" not in r and r["NetworkInterface.1.SecurityGroupId.1"] == "sg-9"
+    assert r["NetworkInterface.1.InterfaceType"] == "efa" and r["NetworkInterface.1.AssociatePublicIpAddress"] == "false"
+    cards = {int(r[f"NetworkInterface.{n}.NetworkCardIndex"]): r[f"NetworkInterface.{n}.InterfaceType"]
+             for n in range(2, 33)}
+    assert sorted(cards) == list(range(1, 32))
+    assert [k for k, v in cards.items() if v == "efa"] == [4, 8, 12, 16, 20, 24, 28]
+    assert r["TagSpecification.1.Tag.3.Key"] == "dstack_project"
+    c.update_provisioning_data(jpd)
+    assert jpd.hostname == "10.9.0.5"  # private address
+
+
+def test_aws_capacity_block_reservation_pins_zone_and_market():
+    from dstack_amd.core.models.instances import InstanceConfiguration, SSHKey
+
+    calls = []
+    c = compute_class(BackendType.AWS)({"vpc_name": "dstack-vpc"}, {"access_key": "AK", "secret_key": "SK"},
+                                       _client(_aws_vpc_handler(calls, efa=False)))
+    cfg = InstanceConfiguration(project_name="main", instance_name="r-0", user="admin", reservation="cr-123",
+                                ssh_keys=[SSHKey(public="ssh-ed25519 AAAA k")])
+    c2 = compute_class(BackendType.AWS)({"vpc_name": "dstack-vpc", "public_ips": False},
+                                        {"access_key": "AK", "secret_key": "SK"},
+                                        _client(_aws_vpc_handler(calls, efa=False)))
+    c2.create_instance(_offer(c, "H100:8"), cfg)
+    r = [f for f in calls if f["Action"] == "RunInstances"][-1]
+    assert r["InstanceMarketOptions.MarketType"] == "capacity-block"
+    assert r["NetworkInterface.1.SubnetId"] == "sn-b"  # the reservation's zone
+    assert r["CapacityReservationSpecification.CapacityReservationTarget.CapacityReservationId"] == "cr-123"
+    assert r["NetworkInterface.1.InterfaceType"] == "interface"
+
+
+# ---- gateways and volumes on GCP / Azure / Kubernetes --------------------------------------------
+def _gw_conf(backend, region):
+    from dstack_amd.core.models.gateways import GatewayComputeConfiguration
+
+    return GatewayComputeConfiguration(project_name="main", instance_name="gw-1", backend=backend, region=region,
+                                       public_ip=True, ssh_key_pub="ssh-rsa AAA gw")
+
+
+def test_gcp_gateway_firewall_insert_and_terminate(rsa_pem, monkeypatch):
+    monkeypatch.setattr("time.sleep", lambda *_: None)
+    seen = []
+
+    def handler(req):
+        if req.url.host == "oauth2.googleapis.com":
+            return httpx.Response(200, json={"access_token": "G", "expires_in": 3600})
+        seen.append((req.method, req.url.path))
+        if req.url.path.endswith("/global/firewalls"):
+            body = json.loads(req.content)
+            assert body["targetTags"] == ["dstack-gateway"] and body["allowed"][0]["ports"] == ["22", "80", "443"]
+            return httpx.Response(409, json={"error": "exists"})
+        if req.method == "POST" and req.url.path.endswith("/instances"):
+            body = json.loads(req.content)
+            assert body["tags"]["items"] == ["dstack-gateway"] and "e2-small" in body["machineType"]
+            ud = body["metadata"]["items"][0]["value"]
+            assert ud.startswith("#cloud-config") and "dstack_amd-gateway-" in ud
+            return httpx.Response(200, json={"status": "DONE", "selfLink": "https://op/1"})
+        if req.method == "DELETE":
+            return httpx.Response(200, json={"status": "DONE"})
+        return httpx.Response(200, json={"status": "RUNNING", "networkInterfaces": [
+            {"networkIP": "10.1.1.2", "accessConfigs": [{"natIP": "34.2.2.2"}]}]})
+
+    sa = {"client_email": "sa@p.iam.gserviceaccount.com", "private_key": rsa_pem, "project_id": "p"}
+    c = compute_class(BackendType.GCP)({}, {"data": json.dumps(sa)}, _client(handler))
+    gpd = c.create_gateway(_gw_conf(BackendType.GCP, "us-central1"))
+    assert gpd.ip_address == "34.2.2.2" and json.loads(gpd.backend_data)["zone"] == "us-central1-a"
+    c.terminate_gateway(gpd.instance_id, _gw_conf(BackendType.GCP, "us-central1"), gpd.backend_data)
+    assert seen[-1] == ("DELETE", "/compute/v1/projects/p/zones/us-central1-a/instances/gw-1")
+
+
+def test_gcp_persistent_disk_volume_lifecycle(rsa_pem, monkeypatch):
+    import datetime as dt
+    import uuid
+
+    from dstack_amd.core.models.volumes import Volume, VolumeConfiguration, VolumeStatus
+
+    monkeypatch.setattr("time.sleep", lambda *_: None)
+    state = {"users": [], "polls": 0}
+    calls = []
+
+    def handler(req):
+        if req.url.host == "oauth2.googleapis.com":
+            return httpx.Response(200, json={"access_token": "G", "expires_in": 3600})
+        calls.append((req.method, req.url.path + ("?" + req.url.query.decode() if req.url.query else "")))
+        if req.url.host == "op":  # operation polling: RUNNING once, then DONE
+            state["polls"] += 1
+            return httpx.Response(200, json={"status": "DONE"})
+        if req.method == "POST" and req.url.path.endswith("/disks"):
+            body = json.loads(req.content)
+            assert body["sizeGb"] == "200" and body["type"].endswith("diskTypes/pd-balanced")
+            return httpx.Response(200, json={"status": "RUNNING", "selfLink": "https://op/disk"})
+        if req.url.path.endswith("/attachDisk"):
+            body = json.loads(req.content)
+            assert body["deviceName"] == body["source"].rsplit("/", 1)[1]
+            state["users"] = ["https://compute/projects/p/zones/us-central1-a/instances/inst-7"]
+            return httpx.Response(200, json={"status": "DONE"})
+        if "/detachDisk" in req.url.path:
+            state["users"] = []
+            return httpx.Response(200, json={"status": "DONE"})
+        if req.method == "DELETE":
+            return httpx.Response(200, json={"status": "DONE"})
+        return httpx.Response(200, json={"name": "data-x", "sizeGb": "200", "users": state["users"]})
+
+    sa = {"client_email": "sa@p.iam.gserviceaccount.com", "private_key": rsa_pem, "project_id": "p"}
+    c = compute_class(BackendType.GCP)({}, {"data": json.dumps(sa)}, _client(handler))
+    vol = Volume(id=uuid.uuid4(), name="data", project_name="main", external=False, status=VolumeStatus.SUBMITTED,
+                 created_at=dt.datetime.now(dt.timezone.utc),
+                 configuration=VolumeConfiguration(backend=BackendType.GCP, region="us-central1", size=200))
+    vpd = c.create_volume(vol)
+    assert state["polls"] == 1 and vpd.availability_zone == "us-central1-a" and vpd.size_gb == 200
+    vol = vol.model_copy(update={"volume_id": vpd.volume_id, "provisioning_data": vpd})
+    vad = c.attach_volume(vol, "inst-7")
+    assert vad.device_name == vpd.volume_id  # /dev/disk/by-id/google-<device name> on the host
+    assert not c.is_volume_detached(vol, "inst-7")
+    c.detach_volume(vol, "inst-7")
+    assert c.is_volume_detached(vol, "inst-7")
+    c.delete_volume(vol)
+    assert calls[-1][0] == "DELETE" and calls[-1][1].endswith(f"/disks/{vpd.volume_id}")
+
+
+def test_azure_creates_network_and_gateway_with_http_nsg(monkeypatch):
+    monkeypatch.setattr("time.sleep", lambda *_: None)
+    deployed = {}
+
+    def handler(req):
+        if req.url.host == "login.microsoftonline.com":
+            return httpx.Response(200, json={"access_token": "A", "expires_in": 3600})
+        if req.method == "PUT" and "/deployments/" in req.url.path:
+            deployed["tpl"] = json.loads(req.content)["properties"]["template"]
+            return httpx.Response(201, json={})
+        if req.method == "PUT":
+            return httpx.Response(200, json={})
+        if "/deployments/" in req.url.path:
+            return httpx.Response(200, json={"properties": {"provisioningState": "Running"}})
+        if "publicIPAddresses" in req.url.path and req.method == "GET":
+            return httpx.Response(200, json={"properties": {"ipAddress": "20.1.1.1"}})
+        return httpx.Response(200, json={})
+
+    c = compute_class(BackendType.AZURE)({"subscription_id": "sub", "tenant_id": "t"},
+                                         {"client_id": "c", "client_secret": "s"}, _client(handler))
+    gpd = c.create_gateway(_gw_conf(BackendType.AZURE, "eastus"))
+    assert gpd.ip_address == "20.1.1.1"
+    res = {r["type"].split("/")[-1] + ":" + r["name"]: r for r in deployed["tpl"]["resources"]}
+    assert "virtualNetworks:dstack-vnet-eastus" in res and "networkSecurityGroups:dstack-nsg-eastus" in res
+    ports = [r["properties"]["destinationPortRange"] for r in res["networkSecurityGroups:gw-1-nsg"]["properties"]
+             ["securityRules"]]
+    assert ports == ["22", "80", "443"]
+    nic = res["networkInterfaces:gw-1-nic"]
+    assert any("dstack-vnet-eastus" in d for d in nic["dependsOn"]) and "networkSecurityGroup" in nic["properties"]
+    # a VM deployment declares the VNet it joins too (nothing has to pre-exist)
+    c2 = compute_class(BackendType.AZURE)({"subscription_id": "sub", "tenant_id": "t"},
+                                          {"client_id": "c", "client_secret": "s"}, _client(handler))
+    c2.create_instance(_offer(c2, "MI300X:8"), CFG)
+    names = [r["name"] for r in deployed["tpl"]["resources"]]
+    assert "dstack-vnet-eastus" in names or any(n.startswith("dstack-vnet-") for n in names)
+
+
+def _kube_compute(handler, **cfg):
+    kubeconfig = {"data": json.dumps({"current-context": "c", "contexts": [{"name": "c", "context": {
+        "cluster": "k", "user": "u"}}], "clusters": [{"name": "k", "cluster": {"server": "https://k8s.example:6443"}}],
+        "users": [{"name": "u", "user": {"token": "tok"}}]})}
+    return compute_class(BackendType.KUBERNETES)({"kubeconfig": kubeconfig, "gateway_lb_wait_s": 0, **cfg}, {},
+                                                 _client(handler))
+
+
+def test_kubernetes_gateway_pod_and_load_balancer():
+    polls = {"n": 0}
+    created, deleted = [], []
+
+    def handler(req):
+        if req.method == "POST":
+            body = json.loads(req.content)
+            created.append(body)
+            return httpx.Response(201, json=body)
+        if req.method == "DELETE":
+            deleted.append(req.url.path)
+            return httpx.Response(200, json={})
+        polls["n"] += 1
+        ing = [{"hostname": "gw.elb.example"}] if polls["n"] >= 3 else []
+        return httpx.Response(200, json={"status": {"loadBalancer": {"ingress": ing}}})
+
+    c = _kube_compute(handler)
+    gpd = c.create_gateway(_gw_conf(BackendType.KUBERNETES, "default"))
+    assert gpd.ip_address == "gw.elb.example" and json.loads(gpd.backend_data)["ssh_user"] == "root"
+    pod, svc = created
+    script = pod["spec"]["containers"][0]["args"][1]
+    assert "update.sh" in script and script.rstrip().endswith("exec /usr/sbin/sshd -D")
+    assert svc["spec"]["type"] == "LoadBalancer" and [p["port"] for p in svc["spec"]["ports"]] == [22, 80, 443]
+    c.terminate_gateway(gpd.instance_id, _gw_conf(BackendType.KUBERNETES, "default"), gpd.backend_data)
+    assert deleted == ["/api/v1/namespaces/default/services/gw-1-service", "/api/v1/namespaces/default/pods/gw-1"]
+
+
+def test_kubernetes_gateway_without_load_balancer_is_cleaned_up():
+    from dstack_amd.core.errors import ComputeError
+
+    deleted = []
+
+    def handler(req):
+        if req.method == "POST":
+            return httpx.Response(201, json={})
+        if req.method == "DELETE":
+            deleted.append(req.url.path)
+            return httpx.Response(200, json={})
+        return httpx.Response(200, json={"status": {"loadBalancer": {}}})
+
+    c = _kube_compute(handler, gateway_lb_wait_tries=3)
+    with pytest.raises(ComputeError, match="LoadBalancer"):
+        c.create_gateway(_gw_conf(BackendType.KUBERNETES, "default"))
+    assert len(deleted) == 2
+
+
+def test_gateway_scripts_survive_shell_and_cloud_init_quoting(tmp_path):
+    """The scripts reach the host byte for byte: through sh -c (Kubernetes args) and through
+    cloud-init's YAML (runcmd items are JSON-quoted YAML strings)."""
+    import yaml
+
+    from dstack_amd.core.backends.clouds.gateway_boot import gateway_cloud_init
+    from dstack_amd.proxy.gateway import packaging
+
+    for content, path in ((packaging.UPDATE_SH, "update.sh"), (packaging.RESTART_SH, "restart"),
+                          (packaging.SYSTEMD_UNIT, "unit")):
+        cmd = packaging.write_file_command(content, str(tmp_path / path))
+        subprocess.run(["sh", "-c", cmd], check=True)
+        assert (tmp_path / path).read_text() == content
+    ci = yaml.safe_load(gateway_cloud_init(_gw_conf(BackendType.AWS, "us-east-1")))
+    writes = [c for c in ci["runcmd"] if "base64 -d >" in c]
+    assert len(writes) == 2
+    for c in writes:
+        target = c.split("> ", 1)[1].split(" ")[0]
+        local = tmp_path / os.path.basename(target)
+        subprocess.run(["sh", "-c", c.replace(target, str(local))], check=True)
+    assert (tmp_path / "update.sh").read_text() == packaging.UPDATE_SH
+    assert (tmp_path / "dstack-gateway.service").read_text() == packaging.SYSTEMD_UNIT
+
+
+def test_capability_lists_match_implementations():
+    """Every backend advertised for gateways / volumes implements the calls (no base-class
+    NotImplementedError behind an advertised capability)."""
+    from dstack_amd.core.backends.base import Compute
+    from dstack_amd.core.models.backends import BACKENDS_WITH_GATEWAY_SUPPORT, BACKENDS_WITH_VOLUMES_SUPPORT
+
+    def cls_of(bt):
+        if bt == BackendType.LOCAL:
+            from dstack_amd.core.backends.local import LocalCompute
+            return LocalCompute
+        if bt == BackendType.REMOTE:
+            from dstack_amd.core.backends.remote import RemoteCompute
+            return RemoteCompute
+        return compute_class(bt)
+
+    for bt in BACKENDS_WITH_GATEWAY_SUPPORT:
+        if bt == BackendType.LOCAL:
+            continue  # local gateways run in-process (services.gateways.LocalGatewayProcess)
+        cls = cls_of(bt)
+        for m in ("create_gateway", "terminate_gateway"):
+            assert getattr(cls, m) is not getattr(Compute, m), f"{bt.value} advertises gateways without {m}"
+    for bt in BACKENDS_WITH_VOLUMES_SUPPORT:
+        cls = cls_of(bt)
+        for m in ("create_volume", "delete_volume", "register_volume"):
+            assert getattr(cls, m) is not getattr(Compute, m), f"{bt.value} advertises volumes without {m}"

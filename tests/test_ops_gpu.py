@@ -144,6 +144,52 @@ def test_flash_attention(gpu, S, H, KV, causal):
         assert err <= 3e-2 * scale + 2e-2, f"{name}: err {err} (ref max {scale})"
 
 
+def _attn_check(qkv, H, KV, do, causal=True, tol=3e-2):
+    B, S = qkv.shape[:2]
+    D = 128
+    qkv = qkv.detach().requires_grad_()
+    o = ops.attention(qkv, H, KV, causal=causal)
+    xr = qkv.detach().float().requires_grad_()
+    q, k, v = ops.functional.split_qkv(xr, H, KV)
+    orf = ref.attention(q, k, v, causal).reshape(B, S, -1)
+    _close(o, orf, 2e-2, 2e-2)
+    o.backward(do)
+    orf.backward(do.float())
+    g, gr = qkv.grad.view(B, S, H + 2 * KV, D), xr.grad.view(B, S, H + 2 * KV, D)
+    for name, sl in (("dq", slice(0, H)), ("dk", slice(H, H + KV)), ("dv", slice(H + KV, H + 2 * KV))):
+        a, b = g[:, :, sl].float(), gr[:, :, sl]
+        err = (a - b).abs().max().item()
+        scale = b.abs().max().item()
+        rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err <= tol * scale + 2e-2 and rel < 2e-2, f"{name}: err {err} rel {rel} (ref max {scale})"
+
+
+@pytest.mark.parametrize("S", [4096, 8192])
+def test_flash_attention_long_sequence(gpu, S):
+    """The bench shape's sequence length (8192) and 4096, forward + all three gradients."""
+    B, H, KV, D = 1, 8, 2, 128
+    qkv = _rand(B, S, (H + 2 * KV) * D, device=gpu, seed=21)
+    do = _rand(B, S, H * D, device=gpu, seed=22)
+    _attn_check(qkv, H, KV, do)
+
+
+def test_flash_attention_deferred_max_stress_long_seq(gpu):
+    """Scores that grow with the key index across all 8192 keys: every query's running max keeps
+    rising, so the deferred-max path rescales again and again (and the threshold is crossed
+    repeatedly) — the output and gradients must still match the exact softmax."""
+    B, S, H, KV, D = 1, 8192, 4, 1, 128
+    g = torch.Generator(device=gpu).manual_seed(5)
+    u = torch.randn(D, device=gpu, generator=g)
+    u = u / u.norm()
+    x = torch.randn(B, S, H + 2 * KV, D, device=gpu, generator=g) * 0.3
+    ramp = torch.linspace(0, 1, S, device=gpu)
+    x[:, :, :H] += 4.0 * u  # every query points along u
+    x[:, :, H] += (40.0 * ramp)[None, :, None] * u  # key t scores ~ 4*40*t/S/sqrt(128) ≈ 14*t/S ... rising
+    qkv = x.reshape(B, S, -1).to(torch.bfloat16)
+    do = _rand(B, S, H * D, device=gpu, seed=23)
+    _attn_check(qkv, H, KV, do, tol=4e-2)
+
+
 def test_flash_attention_lse_rescale_branch(gpu):
     """Force the online-softmax rescale: a spike key late in the sequence for every query."""
     B, S, H, KV, D = 1, 512, 2, 1, 128
