@@ -200,3 +200,7 @@ class InstanceHealth(CoreModel):
     xgmi_gb_s: Optional[List[List[float]]] = None
     rccl_busbw_gb_s: Optional[float] = None
     message: str = ""
+    sku: Optional[str] = None  # the part the thresholds are relative to (e.g. MI355X)
+    thresholds: Optional[dict] = None  # e.g. {"hbm_tb_s": 4.8, "mfma_bf16_tflops": 1680}
+    ran_at: Optional[float] = None  # unix seconds of the probe run
+    source: Optional[str] = None  # "shim" (async, off the job path) | "runner" (job pre-flight)

@@ -117,6 +117,19 @@ def wake(*names: str):
         _scheduler.wake(*names)
 
 
+def wake_later(delay: float, *names: str):
+    """Wake reconcilers after ``delay`` seconds: a pass that finds an agent not ready yet returns at
+    once and asks to be run again shortly, instead of sleeping inside its claim (which would stall
+    every other row of the batch behind one slow host)."""
+    from dstack_amd.server import settings
+
+    if not (settings.SERVER_EVENT_DRIVEN and _scheduler is not None):
+        return
+    t = threading.Timer(delay, _scheduler.wake, args=names)
+    t.daemon = True
+    t.start()
+
+
 # task names
 SUBMITTED_JOBS = "process_submitted_jobs"
 RUNNING_JOBS = "process_running_jobs"

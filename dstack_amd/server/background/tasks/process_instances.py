@@ -74,15 +74,42 @@ def _process_instance(s: Session, inst_id):
     inst.last_processed_at = get_current_datetime()
 
 
+# SSH-fleet deploys (upload agents, start the shim, wait for host_info: up to minutes per host) run
+# on their own workers, never inside a reconciler claim: the pass that starts one returns at once,
+# and the pass after the deploy finished applies its result.
+_deploy_pool = None
+_deploys: dict = {}
+
+
+def _deploy_executor():
+    global _deploy_pool
+    if _deploy_pool is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _deploy_pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="ssh-deploy")
+    return _deploy_pool
+
+
 def _add_remote(s: Session, inst: InstanceModel):
-    if inst.last_retry_at and get_current_datetime() - inst.last_retry_at < SSH_DEPLOY_RETRY:
-        return
-    inst.last_retry_at = get_current_datetime()
+    fut = _deploys.get(inst.id)
+    if fut is not None and not fut.done():
+        return  # still deploying on its worker
+    if fut is None:
+        if inst.last_retry_at and get_current_datetime() - inst.last_retry_at < SSH_DEPLOY_RETRY:
+            return
+        inst.last_retry_at = get_current_datetime()
+        rci = RemoteConnectionInfo.model_validate_json(inst.remote_connection_info)
+        project = inst.project
+        key = next((k.private for k in rci.ssh_keys if k.private), None) or project.ssh_private_key
+        fut = _deploy_executor().submit(deploy_ssh_instance, rci, project.ssh_public_key, key)
+        _deploys[inst.id] = fut
+        fut.add_done_callback(lambda _f: scheduler.wake(scheduler.INSTANCES))
+        if not fut.done():
+            return
+    _deploys.pop(inst.id, None)
     rci = RemoteConnectionInfo.model_validate_json(inst.remote_connection_info)
-    project = inst.project
-    key = next((k.private for k in rci.ssh_keys if k.private), None) or project.ssh_private_key
     try:
-        host_info = deploy_ssh_instance(rci, project.ssh_public_key, key)
+        host_info = fut.result()
     except Exception as e:  # noqa: BLE001
         logger.warning("instance %s: SSH deploy failed: %s", inst.name, e)
         inst.termination_reason = f"deploy failed: {e}"[:4000]
@@ -115,6 +142,11 @@ def _add_remote(s: Session, inst: InstanceModel):
 
 
 NO_CAPACITY_RETRY = timedelta(minutes=1)
+# GPU health: the shim probes at start; the server re-reads it at most once a minute per instance
+# and asks for a fresh probe when the last one is older than this (only while the host is idle)
+GPU_PROBE_MAX_AGE = timedelta(hours=6)
+GPU_HEALTH_POLL = 60.0
+_health_polled: dict = {}
 MAX_OFFERS_TRIED = 15
 
 
@@ -238,6 +270,7 @@ def _check_provisioning(s: Session, inst: InstanceModel):
         inst.termination_deadline = None
         inst.health_status = None
         inst.unreachable = False
+        refresh_gpu_health(inst, jpd, force=True)
         scheduler.wake(scheduler.RUNNING_JOBS, scheduler.SUBMITTED_JOBS)
         return
     now = get_current_datetime()
@@ -246,6 +279,56 @@ def _check_provisioning(s: Session, inst: InstanceModel):
         inst.status = InstanceStatus.TERMINATING.value
         inst.termination_reason = "provisioning timeout"
         inst.termination_deadline = inst.termination_deadline or now
+
+
+def refresh_gpu_health(inst: InstanceModel, jpd: JobProvisioningData, force: bool = False) -> Optional[str]:
+    """Copy the shim's asynchronous HIP probe result (HBM TB/s, MFMA TFLOPS vs 80 % of the per-SKU
+    baseline) into the instance's health; an unhealthy host is skipped by the scheduler
+    (``pools.filter_pool_instances``).  A stale result is refreshed by asking the shim for a new
+    probe while the host runs no job.  Never on a job's critical path.  Returns the shim state."""
+    import time as _time
+
+    from dstack_amd.core.models.instances import InstanceHealth
+
+    now = _time.monotonic()
+    if not force and now - _health_polled.get(inst.id, -1e9) < GPU_HEALTH_POLL:
+        return None
+    _health_polled[inst.id] = now
+    try:
+        shim = get_shim_client(jpd, inst.project.ssh_private_key)
+        doc = shim.gpu_health()
+    except Exception as e:  # noqa: BLE001 - health is advisory; reachability is judged elsewhere
+        logger.debug("%s: gpu health unavailable: %s", inst.name, e)
+        return None
+    if not isinstance(doc, dict):
+        return None  # a shim without the endpoint
+    state = doc.get("state")
+    res = doc.get("result") or None
+    ran_at = (doc.get("ran_at_ms") or 0) / 1000.0
+    old = json.loads(inst.health_data) if inst.health_data else {}
+    if res and state in ("done", "failed") and ran_at and ran_at != old.get("ran_at"):
+        try:
+            h = InstanceHealth(healthy=bool(res.get("healthy", False)), hbm_tb_s=res.get("hbm_tb_s"),
+                               mfma_bf16_tflops=res.get("mfma_bf16_tflops"), mfma_fp8_tflops=res.get("mfma_fp8_tflops"),
+                               xgmi_gb_s=res.get("xgmi_gb_s"), rccl_busbw_gb_s=res.get("rccl_busbw_gb_s"),
+                               message=res.get("message") or ("" if res.get("healthy") else "GPU health probe failed"),
+                               sku=res.get("sku"), thresholds=res.get("thresholds"), ran_at=ran_at, source="shim")
+        except Exception:  # noqa: BLE001 - a malformed document must not break the pass
+            return state
+        inst.health_data = h.model_dump_json()
+        inst.health_status = None  # (only called with the shim reachable)
+        if not h.healthy:
+            inst.health_status = f"GPU health probe: {h.message}"
+            logger.warning("%s: GPU health probe failed: %s", inst.name, h.message)
+        old = json.loads(inst.health_data)
+    stale = not old.get("ran_at") or _time.time() - old["ran_at"] > GPU_PROBE_MAX_AGE.total_seconds()
+    if stale and state in ("idle", "done", "failed") and (inst.busy_blocks or 0) == 0 and \
+            inst.status == InstanceStatus.IDLE.value:
+        try:
+            state = shim.start_gpu_probe()
+        except Exception as e:  # noqa: BLE001
+            logger.debug("%s: start probe: %s", inst.name, e)
+    return state
 
 
 def _shim_healthy(inst: InstanceModel, jpd: JobProvisioningData) -> bool:
@@ -264,7 +347,10 @@ def _check_instance(s: Session, inst: InstanceModel):
     if healthy:
         inst.unreachable = False
         inst.termination_deadline = None
-        inst.health_status = None
+        gpu = json.loads(inst.health_data) if inst.health_data else {}
+        inst.health_status = None if gpu.get("healthy", True) else f"GPU health probe: {gpu.get('message', '')}"
+        if jpd.dockerized:
+            refresh_gpu_health(inst, jpd)
     else:
         inst.unreachable = True
         inst.health_status = "shim unreachable"

@@ -44,6 +44,11 @@ logger = logging.getLogger(__name__)
 
 ACTIVE = (JobStatus.PROVISIONING.value, JobStatus.PULLING.value, JobStatus.RUNNING.value)
 PROVISIONING_TIMEOUT = timedelta(minutes=20)
+# In-claim wait for an agent that is about to be ready (the process driver starts a task and its
+# runner in ~10 ms): bounded so one slow host delays the rest of its batch by at most this much;
+# after it the pass returns and re-queues the job with wake_later instead of sleeping.
+AGENT_WAIT = 0.1
+AGENT_RECHECK = 0.05
 
 
 def process_running_jobs(batch: int = 5) -> bool:
@@ -205,7 +210,7 @@ def _process_pulling(s: Session, run: RunModel, job: JobModel):
     if jpd.dockerized:
         shim = get_shim_client(jpd, project.ssh_private_key)
         task = None
-        deadline = time.monotonic() + 2.0  # short in-pass wait: the process driver is ready in ms
+        deadline = time.monotonic() + AGENT_WAIT
         while True:
             try:
                 task = shim.get_task(str(job.id))
@@ -230,6 +235,7 @@ def _process_pulling(s: Session, run: RunModel, job: JobModel):
             scheduler.wake(scheduler.TERMINATING_JOBS)
             return
         if task["status"] != "running":
+            scheduler.wake_later(AGENT_RECHECK, scheduler.RUNNING_JOBS)  # pulling an image: check again soon
             return
         job.remove_at = None
         jrd = jobs_services.job_jrd(job)
@@ -237,7 +243,9 @@ def _process_pulling(s: Session, run: RunModel, job: JobModel):
         if task.get("runner_port"):
             ports[DSTACK_RUNNER_HTTP_PORT] = int(task["runner_port"])
         if jrd is not None and jrd.network_mode == NetworkMode.BRIDGE and DSTACK_RUNNER_HTTP_PORT not in ports:
-            return  # bridge network: the runner is reachable only through its published port; not mapped yet
+            # bridge network: the runner is reachable only through its published port; not mapped yet
+            scheduler.wake_later(AGENT_RECHECK, scheduler.RUNNING_JOBS)
+            return
         jobs_services.mark_timing(job, "container_running")
         if jrd is not None:
             jrd.ports = ports or None
@@ -256,12 +264,14 @@ def _submit_to_runner(s: Session, run: RunModel, job: JobModel):
     except SSHError as e:
         logger.info("%s: runner tunnel failed: %s", job.job_name, e)
         return
-    deadline = time.monotonic() + 2.0
+    deadline = time.monotonic() + AGENT_WAIT
     while runner.healthcheck() is None:
         if time.monotonic() > deadline:
             if get_current_datetime() - job.submitted_at > timedelta(seconds=settings.DEFAULT_RUNNER_TIMEOUT):
                 jobs_services.terminate_job(job, JobTerminationReason.WAITING_RUNNER_LIMIT_EXCEEDED, delay=False)
                 scheduler.wake(scheduler.TERMINATING_JOBS)
+            else:
+                scheduler.wake_later(AGENT_RECHECK, scheduler.RUNNING_JOBS)
             return
         time.sleep(0.01)
     run_spec = RunSpec.model_validate_json(run.run_spec)

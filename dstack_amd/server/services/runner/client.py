@@ -77,6 +77,22 @@ class ShimClient:
         if r.status_code not in (200, 404, 409):
             raise RunnerError(f"remove failed: {r.text}")
 
+    def gpu_health(self) -> Optional[dict]:
+        """The shim's latest HIP health-probe state ``{state, started_at_ms, ran_at_ms, result}``
+        (None: a shim without the endpoint)."""
+        r = self.c.get("/api/gpu_health", timeout=5)
+        if r.status_code == 404:
+            return None
+        r.raise_for_status()
+        return r.json()
+
+    def start_gpu_probe(self) -> str:
+        """Ask the shim to (re-)run the probe off the job path: started | running | busy | unavailable."""
+        r = self.c.post("/api/gpu_health/probe", timeout=5)
+        if r.status_code == 404:
+            return "unavailable"
+        return (r.json() or {}).get("state", "unavailable")
+
 
 class RunnerClient:
     def __init__(self, base_url: str):

@@ -231,6 +231,9 @@ std::vector<AmdGpu> discover_amd_gpus_sysfs() {
     std::string base = root + "/sys/class/drm/renderD" + std::to_string(r) + "/device/";
     std::string vendor;
     if (!read_file(base + "vendor", vendor) || trim(vendor) != "0x1002") continue;
+    // only GPUs this process can open: sysfs is host-wide, but a container (or a cgroup device
+    // filter) exposes only some render nodes -- amdsmi lists exactly those, and so must we
+    if (access((root + "/dev/dri/renderD" + std::to_string(r)).c_str(), R_OK | W_OK) != 0) continue;
     AmdGpu g;
     g.index = (int)out.size();
     g.drm_render = r;

@@ -202,12 +202,34 @@ static std::vector<std::vector<double>> xgmi_probe(int ndev, bool quick) {
 }
 
 // rccl_probe.cpp
-std::string rccl_allreduce_probe(int ndev, bool quick, double* best_busbw);
+std::string rccl_allreduce_probe_mp(int nodes, int node_rank, const std::string& master, int port, bool quick,
+                                    double* best_busbw, std::string* err);
+
+// Per-SKU baselines: what THIS probe measures on a healthy part (not the datasheet peaks), so a
+// threshold of min_fraction x baseline flags a GPU running well below its siblings (throttling,
+// a bad HBM stack, a degraded link).  MI355X: profiles/probe_r1q.json (6.05 TB/s copy, 2.10 PF
+// bf16, 4.98 PF fp8).  MI300X-class numbers are scaled from its datasheet ratios.  Unknown parts
+// fall back to absolute floors far below any current Instinct part.
+struct Baseline {
+  const char* sku;
+  double hbm_tb_s, bf16_tflops, fp8_tflops;
+};
+static Baseline baseline_for(int dev) {
+  hipDeviceProp_t p{};
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return {"unknown", 2.5, 600.0, 0.0};
+  const std::string arch = p.gcnArchName;
+  if (arch.rfind("gfx950", 0) == 0) return {"MI355X", 6.0, 2100.0, 4900.0};
+  if (arch.rfind("gfx942", 0) == 0) return {"MI300X", 4.2, 900.0, 1800.0};
+  return {"unknown", 2.5, 600.0, 0.0};
+}
 
 int main(int argc, char** argv) {
   bool quick = false, json = false, want_hbm = false, want_mfma = false, want_xgmi = false, want_rccl = false;
   int only_dev = -1;
-  double min_hbm = 2.0, min_mfma = 500.0;  // TB/s, TFLOPS: well below a healthy MI355X
+  double min_hbm = -1, min_mfma = -1;  // absolute overrides; default: min_fraction x per-SKU baseline
+  double min_fraction = 0.8;
+  int rccl_nodes = 1, node_rank = 0, master_port = 29600;
+  std::string master = "127.0.0.1";
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a == "--quick") quick = true;
@@ -219,8 +241,16 @@ int main(int argc, char** argv) {
     else if (a == "--device" && i + 1 < argc) only_dev = atoi(argv[++i]);
     else if (a == "--min-hbm-tbs" && i + 1 < argc) min_hbm = atof(argv[++i]);
     else if (a == "--min-mfma-tflops" && i + 1 < argc) min_mfma = atof(argv[++i]);
+    else if (a == "--min-fraction" && i + 1 < argc) min_fraction = atof(argv[++i]);
+    else if (a == "--nodes" && i + 1 < argc) rccl_nodes = atoi(argv[++i]);
+    else if (a == "--node-rank" && i + 1 < argc) node_rank = atoi(argv[++i]);
+    else if (a == "--master" && i + 1 < argc) master = argv[++i];
+    else if (a == "--master-port" && i + 1 < argc) master_port = atoi(argv[++i]);
     else {
-      fprintf(stderr, "usage: dstack-probe [--quick] [--json] [--hbm] [--mfma] [--xgmi] [--rccl] [--device N]\n");
+      fprintf(stderr,
+              "usage: dstack-probe [--quick] [--json] [--hbm] [--mfma] [--xgmi] [--rccl] [--device N]\n"
+              "                    [--min-fraction F | --min-hbm-tbs X --min-mfma-tflops Y]\n"
+              "                    [--rccl --nodes N --node-rank R --master HOST --master-port P]\n");
       return 2;
     }
   }
@@ -232,15 +262,29 @@ int main(int argc, char** argv) {
   }
   std::string out = "{";
   bool healthy = true;
+  std::string failing;
   std::vector<int> devs;
   for (int d = 0; d < ndev; ++d)
     if (only_dev < 0 || d == only_dev) devs.push_back(d);
-  char buf[256];
+  char buf[512];
+  const Baseline base = baseline_for(devs[0]);
+  const double thr_hbm = min_hbm >= 0 ? min_hbm : min_fraction * base.hbm_tb_s;
+  const double thr_mfma = min_mfma >= 0 ? min_mfma : min_fraction * base.bf16_tflops;
+  snprintf(buf, sizeof buf,
+           "\"sku\": \"%s\", \"baseline\": {\"hbm_tb_s\": %.2f, \"mfma_bf16_tflops\": %.0f, \"mfma_fp8_tflops\": %.0f}, "
+           "\"thresholds\": {\"hbm_tb_s\": %.2f, \"mfma_bf16_tflops\": %.0f}, ",
+           base.sku, base.hbm_tb_s, base.bf16_tflops, base.fp8_tflops, thr_hbm, thr_mfma);
+  out += buf;
+  auto fail = [&](int dev, const char* what, double v, double thr) {
+    healthy = false;
+    snprintf(buf, sizeof buf, "%sGPU %d %s %.2f < %.2f", failing.empty() ? "" : "; ", dev, what, v, thr);
+    failing += buf;
+  };
   if (want_hbm) {
     out += "\"hbm_tb_s\": [";
     for (size_t k = 0; k < devs.size(); ++k) {
       double v = hbm_probe(devs[k], quick);
-      if (v < min_hbm) healthy = false;
+      if (v < thr_hbm) fail(devs[k], "HBM TB/s", v, thr_hbm);
       snprintf(buf, sizeof buf, "%s%.3f", k ? ", " : "", v);
       out += buf;
     }
@@ -250,7 +294,7 @@ int main(int argc, char** argv) {
     out += "\"mfma_bf16_tflops\": [";
     for (size_t k = 0; k < devs.size(); ++k) {
       double v = mfma_probe(devs[k], quick, false);
-      if (v < min_mfma) healthy = false;
+      if (v < thr_mfma) fail(devs[k], "bf16 TFLOPS", v, thr_mfma);
       snprintf(buf, sizeof buf, "%s%.1f", k ? ", " : "", v);
       out += buf;
     }
@@ -274,14 +318,22 @@ int main(int argc, char** argv) {
     }
     out += "], ";
   }
-  if (want_rccl && ndev > 1 && only_dev < 0) {
+  if (want_rccl && only_dev < 0) {
     double best = 0;
-    out += "\"rccl\": " + rccl_allreduce_probe(ndev, quick, &best) + ", ";
+    std::string err;
+    std::string sweep = rccl_allreduce_probe_mp(rccl_nodes, node_rank, master, master_port, quick, &best, &err);
+    snprintf(buf, sizeof buf, "\"rccl_world\": %d, \"rccl\": ", rccl_nodes * ndev);
+    out += buf + sweep + ", ";
     snprintf(buf, sizeof buf, "\"rccl_busbw_gb_s\": %.1f, ", best);
     out += buf;
+    if (!err.empty()) {
+      healthy = false;
+      failing += (failing.empty() ? "" : "; ") + ("RCCL bootstrap: " + err);
+    }
   }
-  snprintf(buf, sizeof buf, "\"devices\": %d, \"healthy\": %s}", (int)devs.size(), healthy ? "true" : "false");
+  snprintf(buf, sizeof buf, "\"devices\": %d, \"healthy\": %s, ", (int)devs.size(), healthy ? "true" : "false");
   out += buf;
+  out += "\"message\": \"" + failing + "\"}";
   if (json)
     printf("%s\n", out.c_str());
   else

@@ -1,13 +1,15 @@
-// RCCL all-reduce probe across the GPUs of one node (single process, one communicator per GPU via
-// ncclCommInitAll), bf16 sum, message sizes 1 MiB .. 1 GiB.  Reports algbw and busbw
-// (busbw = algbw * 2(n-1)/n, the ring-bound number to compare with one xGMI link, ~153 GB/s).
+// RCCL all-reduce probe, bf16 sum, message sizes 1 MiB .. 1 GiB (256 MiB with --quick): algbw and
+// busbw per size, across the GPUs of one node or, with a TCP-bootstrapped unique id, of all nodes.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 
 #include <string>
+#include <thread>
 #include <vector>
+
+#include "bootstrap.h"
 
 #define HCK(x)                                                                               \
   do {                                                                                       \
@@ -26,11 +28,40 @@
     }                                                                                           \
   } while (0)
 
-std::string rccl_allreduce_probe(int ndev, bool quick, double* best_busbw) {
+// One communicator over every GPU of every node: `nodes` processes (one per node, as the runner
+// starts them), each owning all its local GPUs as ranks node_rank*ndev + d, initialised with
+// ncclCommInitRank from an ncclUniqueId that node 0 creates and serves over TCP (bootstrap.h) --
+// the same unique-id rendezvous a torchrun/RCCL job performs, not ncclCommInitAll's in-process
+// shortcut.  nodes == 1 runs the same path with no network exchange.  busbw = algbw*2(W-1)/W
+// (ring-bound; compare with one xGMI link, ~153 GB/s, intra-node).
+std::string rccl_allreduce_probe_mp(int nodes, int node_rank, const std::string& master, int port, bool quick,
+                                    double* best_busbw, std::string* err) {
+  int ndev = 0;
+  HCK(hipGetDeviceCount(&ndev));
+  const int world = nodes * ndev;
+  ncclUniqueId id;
+  std::thread server;
+  std::string serve_err;
+  if (node_rank == 0) {
+    NCK(ncclGetUniqueId(&id));
+    if (nodes > 1)
+      server = std::thread([&] { serve_err = dsa::bootstrap_serve(port, &id, sizeof id, nodes - 1, 300000); });
+  } else {
+    std::string e = dsa::bootstrap_fetch(master, port, node_rank, &id, sizeof id, 300000);
+    if (!e.empty()) {
+      if (err) *err = e;
+      return "null";
+    }
+  }
   std::vector<ncclComm_t> comms((size_t)ndev);
-  std::vector<int> devs((size_t)ndev);
-  for (int d = 0; d < ndev; ++d) devs[(size_t)d] = d;
-  NCK(ncclCommInitAll(comms.data(), ndev, devs.data()));
+  NCK(ncclGroupStart());
+  for (int d = 0; d < ndev; ++d) {
+    HCK(hipSetDevice(d));
+    NCK(ncclCommInitRank(&comms[(size_t)d], world, id, node_rank * ndev + d));
+  }
+  NCK(ncclGroupEnd());
+  if (server.joinable()) server.join();
+  if (!serve_err.empty() && err) *err = serve_err;
   size_t max_bytes = (quick ? 256ull : 1024ull) << 20;
   std::vector<void*> buf((size_t)ndev);
   std::vector<hipStream_t> st((size_t)ndev);
@@ -73,7 +104,7 @@ std::string rccl_allreduce_probe(int ndev, bool quick, double* best_busbw) {
     HCK(hipEventElapsedTime(&ms, e0, e1));
     double sec = ms * 1e-3 / reps;
     double algbw = bytes / sec / 1e9;
-    double busbw = algbw * 2.0 * (ndev - 1) / ndev;
+    double busbw = world > 1 ? algbw * 2.0 * (world - 1) / world : 0.0;
     if (busbw > *best_busbw) *best_busbw = busbw;
     char b[200];
     snprintf(b, sizeof b, "%s{\"bytes\": %zu, \"time_us\": %.1f, \"algbw_gb_s\": %.1f, \"busbw_gb_s\": %.1f}",

@@ -353,7 +353,11 @@ std::vector<std::pair<std::string, std::string>> Executor::build_env() const {
   return env;
 }
 
-static int run_cmd(const std::vector<std::string>& argv, const std::string& cwd, std::string* output) {
+static int run_cmd(const std::vector<std::string>& argv, const std::string& cwd, std::string* output,
+                   const std::vector<std::pair<std::string, std::string>>* env = nullptr) {
+  std::vector<std::string> env_strs;
+  if (env)
+    for (auto& kv : *env) env_strs.push_back(kv.first + "=" + kv.second);
   int pipefd[2];
   if (pipe(pipefd) != 0) return -1;
   pid_t pid = fork();
@@ -366,6 +370,12 @@ static int run_cmd(const std::vector<std::string>& argv, const std::string& cwd,
     std::vector<char*> a;
     for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
     a.push_back(nullptr);
+    if (env) {
+      std::vector<char*> e;
+      for (auto& s : env_strs) e.push_back(const_cast<char*>(s.c_str()));
+      e.push_back(nullptr);
+      execvpe(a[0], a.data(), e.data());
+    }
     execvp(a[0], a.data());
     _exit(127);
   }
@@ -457,6 +467,50 @@ bool Executor::run_probe() {
     probe_json_ = doc;
   }
   return rc == 0;
+}
+
+// Opt-in RCCL pre-flight for distributed tasks (job env DSTACK_RCCL_PREFLIGHT=1, >1 GPU in the
+// job): every node runs the all-reduce probe with ONE communicator over all GPUs of all nodes,
+// bootstrapped like the job's own RCCL (unique id from the master node over TCP, port MASTER_PORT+1,
+// the job's HIP_VISIBLE_DEVICES / NCCL_SOCKET_IFNAME env), so a broken fabric or a bad GPU fails
+// the job in seconds with the probe's message instead of hanging inside torchrun.
+bool Executor::wants_rccl_preflight() const {
+  const Json& js = submit_body_["job_spec"];
+  std::string v = js["env"]["DSTACK_RCCL_PREFLIGHT"].str("");
+  if (v.empty() || v == "0" || v == "false") return false;
+  const Json& ci = submit_body_["cluster_info"];
+  int nodes = ci["job_ips"].size() > 0 ? (int)ci["job_ips"].size() : (int)js["jobs_per_replica"].as_int(1);
+  int gpus = (int)ci["gpus_per_job"].as_int(0);
+  return v == "force" || nodes * gpus > 1;
+}
+
+bool Executor::run_rccl_preflight(std::string& msg) {
+  if (opts_.probe_binary.empty() || !path_exists(opts_.probe_binary)) {
+    job_logs_.append("[dstack] RCCL pre-flight skipped: no dstack-probe in this container\n");
+    return true;
+  }
+  auto env = build_env();
+  auto get = [&](const std::string& k, const std::string& d) {
+    for (auto& kv : env)
+      if (kv.first == k) return kv.second;
+    return d;
+  };
+  const int port = atoi(get("MASTER_PORT", "29500").c_str()) + 1;
+  std::vector<std::string> argv = {"timeout", "-k", "10", get("DSTACK_RCCL_PREFLIGHT_TIMEOUT", "300"),
+                                   opts_.probe_binary, "--rccl", "--quick", "--json",
+                                   "--nodes", get("DSTACK_NODES_NUM", "1"), "--node-rank", get("DSTACK_NODE_RANK", "0"),
+                                   "--master", get("DSTACK_MASTER_NODE_IP", "127.0.0.1"),
+                                   "--master-port", std::to_string(port)};
+  std::string out;
+  const int64_t t0 = now_millis();
+  int rc = run_cmd(argv, opts_.working_dir, &out, &env);
+  job_logs_.append("[dstack] RCCL pre-flight (" + std::to_string(now_millis() - t0) + " ms, exit " +
+                   std::to_string(rc) + "): " + out + (out.empty() || out.back() != '\n' ? "\n" : ""));
+  if (rc != 0) {
+    msg = rc == 124 || rc == 137 ? "RCCL pre-flight timed out" : "RCCL pre-flight failed (exit " + std::to_string(rc) + ")";
+    return false;
+  }
+  return true;
 }
 
 int Executor::exec_job(std::string& reason, std::string& msg) {
@@ -671,6 +725,8 @@ void Executor::run_thread() {
     add_state("failed", "executor_error", err);
   } else if (submit_body_["job_spec"]["gpu_probe"].as_bool(false) && !run_probe()) {
     add_state("failed", "gpu_health_check_failed", "GPU health probe failed");
+  } else if (wants_rccl_preflight() && !run_rccl_preflight(err)) {
+    add_state("failed", "executor_error", err);
   } else if (stop_requested_) {
     add_state("terminated", "terminated_by_user");
   } else {

@@ -86,6 +86,8 @@ class Executor {
   void rlog(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
   bool setup_repo(std::string& err);
   bool run_probe();
+  bool wants_rccl_preflight() const;
+  bool run_rccl_preflight(std::string& msg);
   int exec_job(std::string& reason, std::string& msg);
 
   RunnerOptions opts_;

@@ -4,12 +4,13 @@
 //   dstack-shim [--log-level N] [--shim-home DIR] [--shim-http-port 10998] [--host 0.0.0.0]
 //               [--runner-binary-path PATH] [--runner-download-url URL] [--probe-binary PATH]
 //               [--runner-http-port 10999] [--runner-ssh-port 10022] [--driver docker|process|auto]
-//               [--privileged] [--service]
+//               [--privileged] [--service] [--no-startup-probe]
 #include <signal.h>
 #include <stdlib.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <thread>
 
 #include "../common/amdgpu.h"
@@ -87,9 +88,79 @@ Json Shim::submit(const Json& cfg, int& http_status) {
   return t.to_json();
 }
 
+std::string Shim::start_gpu_probe() {
+  if (opts_.probe_binary.empty() || !path_exists(opts_.probe_binary) || inventory_render_.empty()) {
+    std::lock_guard<std::mutex> lk(probe_mu_);
+    probe_state_ = "unavailable";
+    return "unavailable";
+  }
+  std::lock_guard<std::mutex> lk(probe_mu_);
+  if (probing_) return "running";
+  // the probe saturates every GPU: never beside a job (its numbers and the job would both suffer)
+  if (gpus_.free_count() != gpus_.total()) return "busy";
+  probing_ = true;
+  probe_state_ = "running";
+  probe_started_ms_ = now_millis();
+  std::thread(&Shim::probe_main, this).detach();
+  return "started";
+}
+
+void Shim::probe_main() {
+  // hold every GPU in the lock for the probe's duration: a task arriving meanwhile waits for it
+  // (wait_for_probe) instead of sharing the GPUs with a bandwidth/MFMA saturation test
+  std::vector<int> all;
+  for (int i = 0; i < gpus_.total(); ++i) all.push_back(i);
+  const bool held = gpus_.lock(all);
+  std::string out;
+  int rc = run_capture({opts_.probe_binary, "--quick", "--json"}, out);
+  if (held) gpus_.release(all);
+  Json doc;
+  for (auto& line : split(out, '\n')) {
+    std::string l = trim(line);
+    if (l.empty() || l[0] != '{') continue;
+    try {
+      doc = Json::parse(l);
+    } catch (...) {
+    }
+  }
+  {
+    std::lock_guard<std::mutex> lk(probe_mu_);
+    probe_ran_ms_ = now_millis();
+    if (doc.is_object()) {
+      probe_doc_ = doc;
+      probe_state_ = "done";
+    } else {
+      probe_state_ = "failed";
+      Json e = Json::object();
+      e.set("healthy", false);
+      e.set("message", "probe exited " + std::to_string(rc) + " without a result: " + out.substr(0, 300));
+      probe_doc_ = e;
+    }
+    probing_ = false;
+  }
+  probe_cv_.notify_all();
+  LOGI("gpu health probe %s in %lld ms", probe_state_.c_str(), (long long)(probe_ran_ms_ - probe_started_ms_));
+}
+
+void Shim::wait_for_probe(int max_ms) {
+  std::unique_lock<std::mutex> lk(probe_mu_);
+  probe_cv_.wait_for(lk, std::chrono::milliseconds(max_ms), [this] { return !probing_; });
+}
+
+Json Shim::gpu_health() {
+  std::lock_guard<std::mutex> lk(probe_mu_);
+  Json j = Json::object();
+  j.set("state", probe_state_);
+  j.set("started_at_ms", (long long)probe_started_ms_);
+  j.set("ran_at_ms", (long long)probe_ran_ms_);
+  j.set("result", probe_doc_.is_object() ? probe_doc_ : Json());
+  return j;
+}
+
 void Shim::run_task(std::string id) {
   Task t;
   if (!storage_.get(id, t)) return;
+  if (t.config.gpu != 0 || !t.config.gpu_indices.empty()) wait_for_probe(120000);
   storage_.set_status(id, TaskStatus::Preparing);
   // GPU grant: explicit indices (server-side xGMI placement) or a count resolved here
   std::vector<int> granted;
@@ -189,6 +260,8 @@ int main(int argc, char** argv) {
   int port = 10998;
   std::string host = "0.0.0.0";
   bool service = false;
+  bool startup_probe = true;
+  if (const char* v = getenv("DSTACK_SHIM_STARTUP_PROBE")) startup_probe = std::string(v) != "0";
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -211,8 +284,19 @@ int main(int argc, char** argv) {
     else if (a == "--volumes-root") o.volumes_root = next();
     else if (a == "--privileged") o.privileged = true;
     else if (a == "--service") service = true;
+    else if (a == "--no-startup-probe") startup_probe = false;
     else if (a == "--version") {
       printf("%s\n", SHIM_VERSION);
+      return 0;
+    } else if (a == "--list-gpus") {  // both discovery paths, for checking they agree (BDF order)
+      Json j = Json::object();
+      Json smi = Json::array(), sys = Json::array();
+      if (AmdSmi::instance().available())
+        for (auto& g : AmdSmi::instance().discover()) smi.push_back(gpu_to_json(g));
+      for (auto& g : discover_amd_gpus_sysfs()) sys.push_back(gpu_to_json(g));
+      j.set("amdsmi", smi);
+      j.set("sysfs", sys);
+      printf("%s\n", j.dump().c_str());
       return 0;
     } else if (a == "--host-info") {  // print host_info.json and exit (used by SSH-fleet deploy)
       printf("%s\n", collect_host_info("/").dump().c_str());
@@ -257,7 +341,17 @@ int main(int argc, char** argv) {
     j.set("driver", shim.driver_name());
     j.set("gpus_free", shim.gpu_lock().free_count());
     j.set("gpus_total", shim.gpu_lock().total());
+    j.set("gpu_health", shim.gpu_health()["state"].str());
     return HttpResponse::json(j);
+  });
+  // GPU health (HIP HBM/MFMA probes, relative per-SKU thresholds): read the latest result, or
+  // start a probe (202; 409 while GPU tasks run)
+  srv.route("GET", "/api/gpu_health", [&](HttpRequest&) { return HttpResponse::json(shim.gpu_health()); });
+  srv.route("POST", "/api/gpu_health/probe", [&](HttpRequest&) {
+    std::string st = shim.start_gpu_probe();
+    Json j = Json::object();
+    j.set("state", st);
+    return HttpResponse::json(j, st == "started" || st == "running" ? 202 : (st == "busy" ? 409 : 200));
   });
   srv.route("GET", "/api/host_info", [&](HttpRequest&) { return HttpResponse::json(shim.host_info()); });
   srv.route("GET", "/api/tasks", [&](HttpRequest&) { return HttpResponse::json(shim.list()); });
@@ -296,6 +390,9 @@ int main(int argc, char** argv) {
   // print the bound port for supervisors that start us with --shim-http-port 0
   printf("DSTACK_SHIM_PORT=%d\n", srv.port());
   fflush(stdout);
+  // first health probe right after start, asynchronously: the server reads it at registration
+  // (GET /api/gpu_health) with no job waiting on it
+  if (startup_probe) shim.start_gpu_probe();
   srv.serve_forever();
   return 0;
 }

@@ -174,14 +174,28 @@ class Shim {
   void restore();
   // render nodes of host GPU indices, from the discovery snapshot taken at construction
   std::vector<std::string> render_nodes_of(const std::vector<int>& idx) const;
+  // GPU health probe (dstack-probe --quick --json), run asynchronously off the job path: at shim
+  // start and on demand.  start_gpu_probe: "started" | "running" | "busy" (GPU tasks hold GPUs)
+  // | "unavailable" (no probe binary or no GPUs)
+  std::string start_gpu_probe();
+  Json gpu_health();
 
  private:
   void run_task(std::string id);
+  void probe_main();
+  // tasks that need GPUs wait (bounded) while the probe owns them
+  void wait_for_probe(int max_ms);
   ShimOptions opts_;
   std::unique_ptr<TaskDriver> driver_;
   TaskStorage storage_;
   GpuLock gpus_;
   std::vector<std::string> inventory_render_;  // index -> /dev/dri/renderD*
+  std::mutex probe_mu_;
+  std::condition_variable probe_cv_;
+  bool probing_ = false;
+  std::string probe_state_ = "idle";  // idle | running | done | failed | unavailable
+  Json probe_doc_;
+  int64_t probe_started_ms_ = 0, probe_ran_ms_ = 0;
   Json host_info_;
   std::mutex hi_mu_;
 };

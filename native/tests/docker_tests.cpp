@@ -410,6 +410,7 @@ int main() {
     const G gs[] = {{128, "0000:f5:00.0", "1"}, {129, "0000:05:00.0", "0"}, {130, "0000:75:00.0", "0"}};
     mkdirs(root + "/sys/class/drm");
     mkdirs(root + "/devices");
+    mkdirs(root + "/dev/dri");
     for (auto& g : gs) {
       std::string dev = root + "/devices/" + g.bdf;
       mkdirs(dev);
@@ -418,7 +419,16 @@ int main() {
       write_file(dev + "/mem_info_vram_total", std::to_string(288ULL << 30) + "\n");
       write_file(dev + "/numa_node", std::string(g.numa) + "\n");
       mkdirs(root + "/sys/class/drm/renderD" + std::to_string(g.render));
+      write_file(root + "/dev/dri/renderD" + std::to_string(g.render), "");
       CHECK(symlink(dev.c_str(), (root + "/sys/class/drm/renderD" + std::to_string(g.render) + "/device").c_str()) == 0);
+    }
+    // a fourth GPU on the host that this process cannot open (not in its container): not listed
+    {
+      std::string dev = root + "/devices/0000:02:00.0";
+      mkdirs(dev);
+      write_file(dev + "/vendor", "0x1002\n");
+      mkdirs(root + "/sys/class/drm/renderD200");
+      CHECK(symlink(dev.c_str(), (root + "/sys/class/drm/renderD200/device").c_str()) == 0);
     }
     setenv("DSTACK_SYSFS_ROOT", root.c_str(), 1);
     auto gpus = discover_amd_gpus_sysfs();

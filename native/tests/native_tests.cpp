@@ -18,6 +18,7 @@
 #include "../common/amdgpu.h"
 #include "../common/json.h"
 #include "../common/net.h"
+#include "../probes/bootstrap.h"
 #include "../runner/executor.h"
 #include "../shim/shim.h"
 
@@ -407,6 +408,44 @@ int main() {
     missing.set("device_name", "dstack-nodisk-xyz");
     CHECK(!prepare_volume(missing, root, hp, err) && err.find("not found") != std::string::npos);
     run_capture({"rm", "-rf", "--", root}, out);
+  });
+
+  run("rccl bootstrap: node 0 serves the unique id to every other node", [] {
+    // stub 128-byte ncclUniqueId; 4 nodes (node 0 + 3 fetchers starting at different times)
+    std::string id(128, '\0');
+    for (size_t i = 0; i < id.size(); ++i) id[i] = (char)(i * 37 + 11);
+    int port = 0;
+    {
+      int s = ::socket(AF_INET, SOCK_STREAM, 0);
+      struct sockaddr_in a{};
+      a.sin_family = AF_INET;
+      ::bind(s, (struct sockaddr*)&a, sizeof a);
+      socklen_t len = sizeof a;
+      getsockname(s, (struct sockaddr*)&a, &len);
+      port = ntohs(a.sin_port);
+      ::close(s);
+    }
+    std::string serve_err = "unset";
+    std::thread server([&] { serve_err = bootstrap_serve(port, id.data(), id.size(), 3, 10000); });
+    std::vector<std::string> got(4), errs(4);
+    std::vector<std::thread> peers;
+    for (int r = 1; r <= 3; ++r)
+      peers.emplace_back([&, r] {
+        std::this_thread::sleep_for(std::chrono::milliseconds(30 * r));
+        std::string buf(128, '\0');
+        errs[(size_t)r] = bootstrap_fetch("127.0.0.1", port, r, &buf[0], buf.size(), 10000);
+        got[(size_t)r] = buf;
+      });
+    for (auto& t : peers) t.join();
+    server.join();
+    CHECK(serve_err.empty());
+    for (int r = 1; r <= 3; ++r) CHECK(errs[(size_t)r].empty() && got[(size_t)r] == id);
+    // a node that never arrives: the server gives up with a clear error instead of hanging
+    std::string e2 = bootstrap_serve(0, id.data(), id.size(), 1, 300);
+    CHECK(e2.find("timed out") != std::string::npos);
+    // nobody serving: the fetch times out too
+    std::string buf(128, '\0');
+    CHECK(!bootstrap_fetch("127.0.0.1", port, 1, &buf[0], buf.size(), 300).empty());
   });
 
   fprintf(stderr, "%d/%d test groups passed\n", g_run - (g_failed ? 1 : 0), g_run);
