@@ -14,9 +14,11 @@ step (default 8 × 1 × 8192).
 Data: synthetic random token ids; weights: random init (no network, no checkpoints).
 
 The orchestration half of the metric (p50 cold start of a task via ``dstack apply``) is measured
-by ``bench_coldstart.py`` (a real server + native shim/runner, 5 sequential task submissions) on
-rank 0 before training, in a child process with its own time limit, and reported in the same JSON
-line as ``cold_start_p50_s`` (submit -> first job output).  ``--no-coldstart`` skips it.
+by ``bench_coldstart.py`` (a real server + native shim/runner) on rank 0 before training, in a
+child process with its own time limit, and reported in the same JSON line as ``cold_start_p50_s``:
+submit -> first job output over 5 runs that each land on a freshly created instance and request
+``MI355X:1`` when the host has a GPU; ``cold_start.warm_start_p50_s`` is the warm-pool number.
+Not included (local backend): VM boot, image pull, container start.  ``--no-coldstart`` skips it.
 """
 
 from __future__ import annotations
@@ -37,7 +39,7 @@ def _cold_start(timeout: float = 180.0) -> dict:
 
     here = os.path.dirname(os.path.abspath(__file__))
     try:
-        r = subprocess.run([sys.executable, os.path.join(here, "bench_coldstart.py"), "--runs", "5"],
+        r = subprocess.run([sys.executable, os.path.join(here, "bench_coldstart.py"), "--runs", "5", "--warm-runs", "4"],
                            capture_output=True, text=True, timeout=timeout, cwd=here)
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
         if lines:
@@ -153,8 +155,12 @@ def main():
             "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu",
         }
         if cold is not None:
+            # fresh-instance p50 (every run on a newly created instance, GPU requested when the
+            # host has one); the warm-pool p50 is a separate field
             out["cold_start_p50_s"] = cold.get("cold_start_p50_s")
-            out["cold_start"] = {k: cold.get(k) for k in ("running_p50_s", "first_run_s", "runs", "ok", "error")
+            out["cold_start"] = {k: cold.get(k) for k in ("cold_running_p50_s", "warm_start_p50_s", "gpu_requested",
+                                                          "fresh_runs", "fresh_ok", "fresh_distinct_instances",
+                                                          "warm_runs", "warm_ok", "excludes", "error")
                                  if cold.get(k) is not None}
         print(json.dumps(out), flush=True)
     import torch.distributed as dist

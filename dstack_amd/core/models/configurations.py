@@ -146,8 +146,17 @@ class _WithCommands(CoreModel):
 class DevEnvironmentConfiguration(ProfileParams, _WithPorts, BaseRunConfiguration):
     type: Literal["dev-environment"] = "dev-environment"
     ide: Literal["vscode"]
-    version: Optional[str] = None
+    version: Optional[str] = Field(None, description="VS Code commit to pre-install the server of (Help > About)")
     init: CommandsList = []
+
+    @field_validator("version")
+    @classmethod
+    def _commit(cls, v):
+        import re
+
+        if v is not None and not re.match(r"^[0-9a-f]{7,40}$", v):
+            raise ValueError("version must be a VS Code commit hash (Help > About), e.g. 1a5daa3a0231a0fbba4f14db7ec463cf99d7768e")
+        return v
 
 
 class TaskConfiguration(ProfileParams, _WithCommands, _WithPorts, BaseRunConfiguration):

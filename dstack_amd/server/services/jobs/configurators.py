@@ -71,22 +71,16 @@ def _duration(v, default: Optional[int]) -> Optional[int]:
     return int(v)
 
 
-def _shell_commands(conf) -> List[str]:
-    cmds: List[str] = list(conf.setup)
+def _shell_commands(conf, run_name: Optional[str] = None) -> List[str]:
     if isinstance(conf, DevEnvironmentConfiguration):
-        cmds += list(conf.init)
-        cmds += [
-            "echo ''",
-            "echo 'To connect: ssh $DSTACK_RUN_NAME  (or open VS Code with the Remote-SSH extension)'",
-            "sleep infinity",
-        ]
-    else:
-        cmds += list(conf.commands)
-    return cmds
+        from dstack_amd.server.services.jobs.ide import dev_environment_commands
+
+        return dev_environment_commands(conf, run_name or "dev")
+    return list(conf.setup) + list(conf.commands)
 
 
-def _build_commands(conf, image_entrypoint: Optional[List[str]] = None) -> List[str]:
-    shell = _shell_commands(conf)
+def _build_commands(conf, image_entrypoint: Optional[List[str]] = None, run_name: Optional[str] = None) -> List[str]:
+    shell = _shell_commands(conf, run_name)
     if conf.entrypoint is not None:
         return shlex.split(conf.entrypoint) + shell
     if shell:
@@ -158,7 +152,8 @@ def get_job_specs_from_run_spec(run_spec: RunSpec, replica_num: int = 0,
         job_name = f"{run_spec.run_name}-{job_num}-{replica_num}"
         specs.append(JobSpec(
             replica_num=replica_num, job_num=job_num, job_name=job_name, jobs_per_replica=nodes,
-            app_specs=_app_specs(conf), user=user, commands=_build_commands(conf, image_entrypoint), env=env,
+            app_specs=_app_specs(conf), user=user, commands=_build_commands(conf, image_entrypoint, run_spec.run_name),
+            env=env,
             home_dir=conf.home_dir, image_name=image, privileged=conf.privileged,
             single_branch=conf.single_branch if conf.single_branch is not None
             else not isinstance(conf, DevEnvironmentConfiguration),
