@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 // which brings a wave under 256 registers: 2 waves per SIMD hide each other's LDS/exp latency.
 // LDS: K|V (64 KiB) + 2-stage Q/dO/lse/delta ring (65 KiB) = 129 KiB -> one workgroup per CU.
 // ================================================================================================
-template <bool CAUSAL>
+template <bool CAUSAL, bool SEED = false>
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
@@ -465,10 +465,21 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const int qlo = qt * 64 + 32 * qh;
     if (!CAUSAL || qlo + 31 >= kw0) {  // some query of my half-tile sees my keys
       f32x16 sc, dpv;
+      // SEED: the row constants start the accumulators (S' = Q.K^T - lse/scale, dP' = dO.V^T -
+      // delta), so p = exp2(scale * S') and dS = p * dP' need no per-element subtractions
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sc[r] = 0.f;
-        dpv[r] = 0.f;
+      for (int rr = 0; rr < 4; ++rr) {
+        const int qi = 32 * qh + 8 * rr + 4 * hf;
+        f4 L = {0.f, 0.f, 0.f, 0.f}, Dl = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (SEED) {
+          L = *reinterpret_cast<const f4*>(ll + qi);
+          Dl = *reinterpret_cast<const f4*>(dl + qi);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sc[4 * rr + i] = SEED ? -L[i] / scale_log2 : 0.f;
+          dpv[4 * rr + i] = SEED ? -Dl[i] : 0.f;
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
@@ -479,15 +490,18 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int qi = 32 * qh + 8 * rr + 4 * hf;
-        const f4 L = *reinterpret_cast<const f4*>(ll + qi);
-        const f4 Dl = *reinterpret_cast<const f4*>(dl + qi);
+        f4 L = {0.f, 0.f, 0.f, 0.f}, Dl = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (!SEED) {
+          L = *reinterpret_cast<const f4*>(ll + qi);
+          Dl = *reinterpret_cast<const f4*>(dl + qi);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * rr + i;
-          float pv = fexp2(fmaf(sc[r], scale_log2, -L[i]));
+          float pv = SEED ? fexp2(sc[r] * scale_log2) : fexp2(fmaf(sc[r], scale_log2, -L[i]));
           if (diag && mykey > qt * 64 + qi + i) pv = 0.f;
           sc[r] = pv;
-          dpv[r] = pv * (dpv[r] - Dl[i]);
+          dpv[r] = SEED ? pv * dpv[r] : pv * (dpv[r] - Dl[i]);
         }
       }
       bf16x8 pb[2], dsb[2];
@@ -537,6 +551,171 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
         }
         *reinterpret_cast<f4*>(dkr + dd) = ok;
         *reinterpret_cast<f4*>(dvr + dd) = ov;
+      }
+  }
+}
+
+// ================================================================================================
+// Backward dK/dV pass, 64 keys per wave: workgroup = 4 waves = 256 keys of one (b, q-head), one
+// wave per SIMD.  Each wave keeps K (and, with VREG, V) of its 64 keys in registers and dK^T / dV^T
+// of those keys in 256 accumulator registers, and sweeps 32-query slices of Q/dO staged in LDS:
+// every Q / dO fragment read from LDS (rows for S and dP, transposed for dV^T and dK^T) feeds the
+// MFMAs of TWO 32-key tiles, so a slice costs 32 KiB of LDS reads for 64 MFMAs per wave (the 8-wave
+// kernel above: 48 KiB for 32) -- MFMA-bound instead of LDS-bound.  With VREG = false, V of the
+// block sits in LDS (64 KiB) and is read as the dP B operand, which frees 64 VGPRs.  Same fp32
+// per-q-head partial output as fa_bwd_dkdv_kernel.
+// ================================================================================================
+template <bool CAUSAL, bool VREG>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv64_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
+    int H, int KVH, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int STAGE = 2 * TILE_BYTES + 512;         // Q (64 rows) | dO (64 rows) | lse | delta
+  constexpr int V_BYTES = VREG ? 0 : 4 * TILE_BYTES;  // V of the 256 keys (four 64-row tiles)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
+  const int NH = H + 2 * KVH;
+  const long rs = (long)NH * HD;
+  const long ors = (long)H * HD;
+  const int bid = blockIdx.x;
+  const int kb = bid / (B * H);  // small kb = most q tiles: heaviest first
+  const int bh = bid % (B * H);
+  const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
+  const bf16_t* base = qkv + (long)b * S * rs;
+  const bf16_t* qp = base + hh * HD;
+  const bf16_t* kp = base + (H + kvh) * HD;
+  const bf16_t* vp = base + (H + KVH + kvh) * HD;
+  const bf16_t* dop = dout + (long)b * S * ors + hh * HD;
+  const float* lp = lse + ((long)b * H + hh) * S;
+  const float* dp = delta + ((long)b * H + hh) * S;
+  const int kb0 = kb * 256, kw0 = kb0 + 64 * w;
+  char* vl = smem;  // (VREG = false) V rows of the block, 4 x 64-row tiles
+  char* ring = smem + V_BYTES;
+
+  bf16x8 kf[2][8];
+  bf16x8 vf[2][VREG ? 8 : 1];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      kf[t][ks] = *reinterpret_cast<const bf16x8*>(kp + (long)(kw0 + 32 * t + l32) * rs + 16 * ks + 8 * hf);
+      if constexpr (VREG)
+        vf[t][ks] = *reinterpret_cast<const bf16x8*>(vp + (long)(kw0 + 32 * t + l32) * rs + 16 * ks + 8 * hf);
+    }
+  if constexpr (!VREG) {
+#pragma unroll
+    for (int h64 = 0; h64 < 4; ++h64)
+      dma_tile64(vp + (long)(kb0 + 64 * h64) * rs, rs, vl + h64 * TILE_BYTES, w, lane);
+  }
+  f32x16 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dk[t][d][r] = 0.f;
+        dv[t][d][r] = 0.f;
+      }
+  const int qt_begin = CAUSAL ? kb0 / 64 : 0;
+  const int nqt = S / 64;
+  auto issue = [&](int qt, char* st) {
+    dma_tile64(qp + (long)qt * 64 * rs, rs, st, w, lane);
+    dma_tile64(dop + (long)qt * 64 * ors, ors, st + TILE_BYTES, w, lane);
+    if (w == 0) dma_f32x64(lp + qt * 64, st + 2 * TILE_BYTES, lane);
+    if (w == 1) dma_f32x64(dp + qt * 64, st + 2 * TILE_BYTES + 256, lane);
+  };
+  issue(qt_begin, ring);
+  wait_dma_and_barrier();
+
+  for (int qt = qt_begin; qt < nqt; ++qt) {
+    const int stage = (qt - qt_begin) & 1;
+    const char* ql = ring + stage * STAGE;
+    const char* dol = ql + TILE_BYTES;
+    const float* ll = reinterpret_cast<const float*>(ql + 2 * TILE_BYTES);
+    const float* dl = ll + 64;
+    if (qt + 1 < nqt) issue(qt + 1, ring + (stage ^ 1) * STAGE);
+#pragma unroll 1  // one slice's temporaries live at a time (256 AGPR accumulators + K/V)
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qlo = qt * 64 + 32 * qs;
+      if (CAUSAL && qlo + 31 < kw0) continue;  // every query of the slice precedes my keys
+      f32x16 sc[2], dpv[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sc[t][r] = 0.f;
+          dpv[t][r] = 0.f;
+        }
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const bf16x8 aq = lds_row(ql, 32 * qs + l32, 2 * ks + hf);
+        const bf16x8 ad = lds_row(dol, 32 * qs + l32, 2 * ks + hf);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          sc[t] = mfma(aq, kf[t][ks], sc[t]);
+          if constexpr (VREG)
+            dpv[t] = mfma(ad, vf[t][ks], dpv[t]);
+          else
+            dpv[t] = mfma(ad, lds_row(vl, 64 * w + 32 * t + l32, 2 * ks + hf), dpv[t]);
+        }
+      }
+      // rows of sc/dpv: q = qlo + (r&3) + 8*(r>>2) + 4*hf ; column (lane) = key kw0 + 32t + l32
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int qi = 32 * qs + 8 * rr + 4 * hf;
+        const f4 L = *reinterpret_cast<const f4*>(ll + qi);
+        const f4 Dl = *reinterpret_cast<const f4*>(dl + qi);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rr + i;
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            float pv = fexp2(fmaf(sc[t][r], scale_log2, -L[i]));
+            if (CAUSAL && qlo < kw0 + 32 * t + 31 && kw0 + 32 * t + l32 > qt * 64 + qi + i) pv = 0.f;
+            sc[t][r] = pv;
+            dpv[t][r] = pv * (dpv[t][r] - Dl[i]);
+          }
+        }
+      }
+      bf16x8 pb[2][2], dsb[2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+          pb[t][k2] = to_bf16x8(sc[t], 8 * k2);
+          dsb[t][k2] = to_bf16x8(dpv[t], 8 * k2);
+        }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+          const bf16x8 at = lds_tr(dol, 32 * qs + 16 * k2, 32 * d, lane);
+          const bf16x8 qtr = lds_tr(ql, 32 * qs + 16 * k2, 32 * d, lane);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            dv[t][d] = mfma(at, pb[t][k2], dv[t][d]);
+            dk[t][d] = mfma(qtr, dsb[t][k2], dk[t][d]);
+          }
+        }
+    }
+    wait_dma_and_barrier();
+  }
+  const float sm = scale_log2 * 0.6931471805599453f;  // softmax scale = scale_log2 * ln2
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int key = kw0 + 32 * t + l32;
+    float* dkr = dkp + (((long)b * S + key) * H + hh) * HD;
+    float* dvr = dvp + (((long)b * S + key) * H + hh) * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int dd = 32 * d + 8 * rr + 4 * hf;
+        *reinterpret_cast<f4*>(dkr + dd) = f4{dk[t][d][4 * rr] * sm, dk[t][d][4 * rr + 1] * sm,
+                                              dk[t][d][4 * rr + 2] * sm, dk[t][d][4 * rr + 3] * sm};
+        *reinterpret_cast<f4*>(dvr + dd) = f4{dv[t][d][4 * rr], dv[t][d][4 * rr + 1], dv[t][d][4 * rr + 2],
+                                              dv[t][d][4 * rr + 3]};
       }
   }
 }
@@ -755,10 +934,13 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   const size_t lds_q = 4 * TILE_BYTES;
   // dK/dV kernel: the 8-wave K/V-resident variant is the default (2.10 vs 2.53 ms for the whole
   // backward at S=8192, same box); DSTACK_AMD_FA_DKDV=4w selects the 4-wave register-resident one
-  static const bool dkdv8 = [] {
+  static const int dkdv_kind = [] {  // 8 = 8-wave (default), 4 = 4-wave, 64 / 65 = 64 keys per wave
     const char* v = getenv("DSTACK_AMD_FA_DKDV");
-    return !(v && std::string(v) == "4w");
+    if (!v) return 8;
+    const std::string s(v);
+    return s == "4w" ? 4 : (s == "64k" ? 64 : (s == "64kv" ? 65 : (s == "seed" ? 9 : 8)));
   }();
+  const bool dkdv8 = dkdv_kind == 8 || dkdv_kind == 9;
   // dQ pass: 8 waves / 256 query rows per workgroup when S % 256 == 0 (DSTACK_AMD_FA_DQ_WAVES=4|8).
   // Whole backward at S=8192, same box, 3 interleaved runs each (tools/gpu_sessions/run_r1t.sh): 4 waves 2.06-2.08
   // ms; 8 waves 2.04-2.07; 8 waves with the dP accumulator seeded with -delta ('row constant')
@@ -770,10 +952,21 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   const int dq_waves = (dq_waves_env == 8 && S % 256 == 0) ? 8 : 4;
 #define DSA_DKDV(C, N)                                                                                 \
   do {                                                                                                 \
-    if (dkdv8)                                                                                         \
+    if (dkdv_kind >= 64 && S % 256 == 0) {                                                             \
+      if (dkdv_kind == 64)                                                                             \
+        fa_bwd_dkdv64_kernel<C, true><<<B * H * (S / 256), 256, 2 * (2 * TILE_BYTES + 512), st>>>(     \
+            (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);         \
+      else                                                                                             \
+        fa_bwd_dkdv64_kernel<C, false><<<B * H * (S / 256), 256, 4 * TILE_BYTES + 2 * (2 * TILE_BYTES + 512), \
+                                         st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, \
+                                               B, S, H, KVH, sl2);                                     \
+    } else if (dkdv_kind == 9) {                                                                      \
+      fa_bwd_dkdv8_kernel<C, true><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(     \
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
+    } else if (dkdv8 || dkdv_kind >= 64) {                                                             \
       fa_bwd_dkdv8_kernel<C><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(          \
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
-    else                                                                                               \
+    } else                                                                                             \
       fa_bwd_dkdv_kernel<C, N><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, \
                                                           delta, dkp, dvp, B, S, H, KVH, sl2);         \
   } while (0)

@@ -7,7 +7,10 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <openssl/err.h>
 #include <openssl/sha.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 #include <poll.h>
 #include <signal.h>
 #include <stdarg.h>
@@ -277,15 +280,32 @@ struct SockReader {
   std::string buf;
   size_t pos = 0;
   int timeout_ms;
+  SSL* ssl = nullptr;
   bool fill() {
     if (pos > 0 && pos == buf.size()) {
       buf.clear();
       pos = 0;
     }
+    char tmp[65536];
+    if (ssl) {
+      // TLS: records already decrypted inside OpenSSL need no poll; otherwise wait for bytes
+      while (true) {
+        if (SSL_pending(ssl) == 0) {
+          struct pollfd p{fd, POLLIN, 0};
+          if (::poll(&p, 1, timeout_ms) <= 0) return false;
+        }
+        int n = SSL_read(ssl, tmp, (int)sizeof tmp);
+        if (n > 0) {
+          buf.append(tmp, (size_t)n);
+          return true;
+        }
+        int e = SSL_get_error(ssl, n);
+        if (e != SSL_ERROR_WANT_READ && e != SSL_ERROR_WANT_WRITE) return false;
+      }
+    }
     struct pollfd p{fd, POLLIN, 0};
     int r = ::poll(&p, 1, timeout_ms);
     if (r <= 0) return false;
-    char tmp[65536];
     ssize_t n = ::recv(fd, tmp, sizeof tmp, 0);
     if (n <= 0) return false;
     buf.append(tmp, (size_t)n);
@@ -682,13 +702,83 @@ static int connect_unix(const std::string& path, std::string& err) {
   return fd;
 }
 
+// ---- TLS (agent downloads from https:// URLs: S3, release servers) ----
+// One client context per process: system CA store (or an explicit CA file), peer and hostname
+// verification on, TLS 1.2+.  The handshake runs on the connected blocking socket.
+struct TlsConn {
+  SSL_CTX* ctx = nullptr;
+  SSL* ssl = nullptr;
+  ~TlsConn() {
+    if (ssl) {
+      SSL_shutdown(ssl);
+      SSL_free(ssl);
+    }
+    if (ctx) SSL_CTX_free(ctx);
+  }
+};
+
+static bool tls_connect(int fd, const HttpClientRequest& req, TlsConn& t, std::string& err) {
+  t.ctx = SSL_CTX_new(TLS_client_method());
+  if (!t.ctx) {
+    err = "TLS: no context";
+    return false;
+  }
+  SSL_CTX_set_min_proto_version(t.ctx, TLS1_2_VERSION);
+  if (!req.insecure) {
+    SSL_CTX_set_verify(t.ctx, SSL_VERIFY_PEER, nullptr);
+    const char* env_ca = getenv("DSTACK_CA_FILE");
+    const std::string ca = !req.ca_file.empty() ? req.ca_file : (env_ca ? env_ca : "");
+    if (!ca.empty() ? SSL_CTX_load_verify_locations(t.ctx, ca.c_str(), nullptr) != 1
+                    : SSL_CTX_set_default_verify_paths(t.ctx) != 1) {
+      err = "TLS: cannot load CA certificates" + (ca.empty() ? std::string() : " from " + ca);
+      return false;
+    }
+  }
+  t.ssl = SSL_new(t.ctx);
+  SSL_set_fd(t.ssl, fd);
+  SSL_set_tlsext_host_name(t.ssl, req.host.c_str());  // SNI
+  if (!req.insecure) SSL_set1_host(t.ssl, req.host.c_str());  // certificate must name the host
+  if (SSL_connect(t.ssl) != 1) {
+    long vr = SSL_get_verify_result(t.ssl);
+    char ebuf[256];
+    ERR_error_string_n(ERR_get_error(), ebuf, sizeof ebuf);
+    err = std::string("TLS handshake with ") + req.host + " failed: " +
+          (vr != X509_V_OK ? X509_verify_cert_error_string(vr) : ebuf);
+    return false;
+  }
+  return true;
+}
+
+static bool tls_send_all(SSL* ssl, const char* p, size_t n) {
+  while (n > 0) {
+    int w = SSL_write(ssl, p, (int)std::min<size_t>(n, 1 << 30));
+    if (w <= 0) return false;
+    p += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
 HttpClientResponse http_request(const HttpClientRequest& req) {
   HttpClientResponse resp;
   int fd = req.unix_socket.empty() ? connect_tcp(req.host, req.port, req.timeout_ms, resp.error)
                                    : connect_unix(req.unix_socket, resp.error);
   if (fd < 0) return resp;
+  TlsConn tls;
+  if (req.tls) {
+    // bounded handshake: the socket is blocking, so give it the request's timeout
+    struct timeval tv{req.timeout_ms / 1000, (req.timeout_ms % 1000) * 1000};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+    if (!tls_connect(fd, req, tls, resp.error)) {
+      ::close(fd);
+      return resp;
+    }
+  }
   std::string out = req.method + " " + req.path + " HTTP/1.1\r\n";
-  out += "Host: " + (req.unix_socket.empty() ? req.host : std::string("docker")) + "\r\n";
+  const bool default_port = req.port == (req.tls ? 443 : 80);
+  out += "Host: " + (req.unix_socket.empty() ? req.host + (default_port ? "" : ":" + std::to_string(req.port))
+                                             : std::string("docker")) + "\r\n";
   bool has_ct = false;
   for (auto& h : req.headers) {
     out += h.first + ": " + h.second + "\r\n";
@@ -697,12 +787,13 @@ HttpClientResponse http_request(const HttpClientRequest& req) {
   if (!req.body.empty() && !has_ct) out += "Content-Type: application/json\r\n";
   out += "Content-Length: " + std::to_string(req.body.size()) + "\r\nConnection: close\r\n\r\n";
   out += req.body;
-  if (!send_all(fd, out.data(), out.size())) {
+  if (!(tls.ssl ? tls_send_all(tls.ssl, out.data(), out.size()) : send_all(fd, out.data(), out.size()))) {
     resp.error = "send failed";
     ::close(fd);
     return resp;
   }
   SockReader rd{fd, {}, 0, req.timeout_ms};
+  rd.ssl = tls.ssl;
   std::string line;
   if (!rd.read_line(line)) {
     resp.error = "no response";
@@ -750,23 +841,62 @@ HttpClientResponse http_request(const HttpClientRequest& req) {
     while (rd.read_some(chunk))
       if (!emit(chunk)) break;
   }
+  if (tls.ssl) {
+    SSL_shutdown(tls.ssl);
+    SSL_free(tls.ssl);
+    tls.ssl = nullptr;
+  }
   ::close(fd);
   if (!resp.error.empty()) resp.status = 0;  // body framing broken: treat as a transport error
   return resp;
 }
 
-HttpClientResponse http_get_url(const std::string& url, int timeout_ms) {
-  HttpClientRequest req;
-  req.timeout_ms = timeout_ms;
+bool parse_url(const std::string& url, HttpClientRequest& req) {
   std::string u = url;
-  if (u.rfind("http://", 0) == 0) u = u.substr(7);
+  if (u.rfind("https://", 0) == 0) {
+    req.tls = true;
+    u = u.substr(8);
+  } else if (u.rfind("http://", 0) == 0) {
+    req.tls = false;
+    u = u.substr(7);
+  } else {
+    return false;
+  }
   auto slash = u.find('/');
   std::string hostport = slash == std::string::npos ? u : u.substr(0, slash);
   req.path = slash == std::string::npos ? "/" : u.substr(slash);
   auto colon = hostport.find(':');
   req.host = colon == std::string::npos ? hostport : hostport.substr(0, colon);
-  req.port = colon == std::string::npos ? 80 : atoi(hostport.c_str() + colon + 1);
-  return http_request(req);
+  req.port = colon == std::string::npos ? (req.tls ? 443 : 80) : atoi(hostport.c_str() + colon + 1);
+  return !req.host.empty();
+}
+
+HttpClientResponse http_get_url(const std::string& url, int timeout_ms, const std::string& ca_file) {
+  std::string cur = url;
+  // follow redirects (release servers and S3 pre-signed URLs answer 301/302/307 with Location)
+  for (int hop = 0; hop < 5; ++hop) {
+    HttpClientRequest req;
+    req.timeout_ms = timeout_ms;
+    req.ca_file = ca_file;
+    if (!parse_url(cur, req)) {
+      HttpClientResponse r;
+      r.error = "unsupported URL: " + cur;
+      return r;
+    }
+    auto r = http_request(req);
+    if ((r.status == 301 || r.status == 302 || r.status == 303 || r.status == 307 || r.status == 308) &&
+        r.headers.count("location")) {
+      std::string loc = r.headers["location"];
+      if (loc.rfind("http", 0) != 0)  // relative: same scheme, host and port
+        loc = std::string(req.tls ? "https://" : "http://") + req.host + ":" + std::to_string(req.port) + loc;
+      cur = loc;
+      continue;
+    }
+    return r;
+  }
+  HttpClientResponse r;
+  r.error = "too many redirects";
+  return r;
 }
 
 }  // namespace dsa

@@ -2,8 +2,8 @@
 //
 // Server: one listener thread, one detached worker thread per connection (keep-alive), a router
 // with {param} path segments, and an in-place upgrade to WebSocket for streaming logs.
-// Client: TCP or unix-socket (Docker Engine API), Content-Length and chunked bodies, optional
-// streaming callback for long-lived chunked responses (image pull progress).
+// Client: TCP, TLS (OpenSSL, verified) or unix-socket (Docker Engine API), Content-Length and chunked
+// bodies, optional streaming callback for long-lived chunked responses (image pull progress).
 #pragma once
 #include <atomic>
 #include <functional>
@@ -144,10 +144,17 @@ struct HttpClientRequest {
   int timeout_ms = 30000;
   // streaming: called with each decoded body chunk; return false to abort
   std::function<bool(const std::string&)> on_chunk;
+  // TLS (https): verified against the system CA store, or ca_file / $DSTACK_CA_FILE; the
+  // certificate must name `host` (SNI + hostname check).  insecure skips verification.
+  bool tls = false;
+  std::string ca_file;
+  bool insecure = false;
 };
 
 HttpClientResponse http_request(const HttpClientRequest& req);
-// http://host:port/path  (no TLS)
-HttpClientResponse http_get_url(const std::string& url, int timeout_ms = 30000);
+// "http[s]://host[:port]/path" -> host, port, path, tls
+bool parse_url(const std::string& url, HttpClientRequest& req);
+// GET http:// or https:// URL, following up to 5 redirects
+HttpClientResponse http_get_url(const std::string& url, int timeout_ms = 30000, const std::string& ca_file = "");
 
 }  // namespace dsa

@@ -322,9 +322,13 @@ int main(int argc, char** argv) {
   if (o.runner_binary.empty()) o.runner_binary = o.home + "/dstack-runner";
   if (!path_exists(o.runner_binary) && !o.runner_download_url.empty()) {  // runner.go:18-109
     LOGI("downloading runner from %s", o.runner_download_url.c_str());
+    // http:// or https:// (verified TLS, redirects followed); written to a temp name and renamed,
+    // so a crash mid-download never leaves a truncated runner behind (runner.go:18-109)
     auto r = http_get_url(o.runner_download_url, 10 * 60 * 1000);
-    if (!r.ok() || !write_file(o.runner_binary, r.body, 0755)) {
+    const std::string tmp = o.runner_binary + ".download";
+    if (!r.ok() || !write_file(tmp, r.body, 0755) || ::rename(tmp.c_str(), o.runner_binary.c_str()) != 0) {
       LOGE("runner download failed: %d %s", r.status, r.error.c_str());
+      ::unlink(tmp.c_str());
       return 1;
     }
   }

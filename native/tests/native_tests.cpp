@@ -18,6 +18,8 @@
 #include "../common/amdgpu.h"
 #include "../common/json.h"
 #include "../common/net.h"
+#include <openssl/ssl.h>
+
 #include "../probes/bootstrap.h"
 #include "../runner/executor.h"
 #include "../shim/shim.h"
@@ -446,6 +448,79 @@ int main() {
     // nobody serving: the fetch times out too
     std::string buf(128, '\0');
     CHECK(!bootstrap_fetch("127.0.0.1", port, 1, &buf[0], buf.size(), 300).empty());
+  });
+
+  run("https download: verified TLS, SNI/hostname, redirect, untrusted CA refused", [] {
+    // a local TLS server with a self-signed certificate for "localhost"; the runner/shim download
+    // path (http_get_url) must fetch through a redirect over TLS, verify against the given CA and
+    // refuse the same server when the CA is not trusted
+    char tmpl[] = "/tmp/tls-test-XXXXXX";
+    std::string dir = mkdtemp(tmpl), out;
+    const std::string key = dir + "/key.pem", cert = dir + "/cert.pem";
+    int rc = run_capture({"openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-subj", "/CN=localhost",
+                          "-addext", "subjectAltName=DNS:localhost", "-days", "1", "-keyout", key, "-out", cert},
+                         out);
+    CHECK(rc == 0);
+    SSL_CTX* ctx = SSL_CTX_new(TLS_server_method());
+    CHECK(SSL_CTX_use_certificate_file(ctx, cert.c_str(), SSL_FILETYPE_PEM) == 1);
+    CHECK(SSL_CTX_use_PrivateKey_file(ctx, key.c_str(), SSL_FILETYPE_PEM) == 1);
+    int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+    struct sockaddr_in a{};
+    a.sin_family = AF_INET;
+    inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+    ::bind(lfd, (struct sockaddr*)&a, sizeof a);
+    ::listen(lfd, 8);
+    socklen_t len = sizeof a;
+    getsockname(lfd, (struct sockaddr*)&a, &len);
+    const int port = ntohs(a.sin_port);
+    std::string blob(300000, '\0');
+    for (size_t i = 0; i < blob.size(); ++i) blob[i] = (char)(i * 131 + 7);
+    std::atomic<int> served{0};
+    std::thread srv([&] {
+      for (int k = 0; k < 3; ++k) {  // redirect, file, and the refused handshake
+        struct pollfd p{lfd, POLLIN, 0};
+        if (::poll(&p, 1, 10000) <= 0) break;
+        int c = ::accept(lfd, nullptr, nullptr);
+        SSL* ssl = SSL_new(ctx);
+        SSL_set_fd(ssl, c);
+        if (SSL_accept(ssl) == 1) {
+          char buf[4096];
+          int n = SSL_read(ssl, buf, sizeof buf - 1);
+          std::string req(buf, n > 0 ? (size_t)n : 0);
+          std::string resp;
+          if (req.rfind("GET /latest/dstack-runner ", 0) == 0)
+            resp = "HTTP/1.1 302 Found\r\nLocation: /v0.1/dstack-runner\r\nContent-Length: 0\r\n\r\n";
+          else if (req.rfind("GET /v0.1/dstack-runner ", 0) == 0 && req.find("Host: localhost:") != std::string::npos)
+            resp = "HTTP/1.1 200 OK\r\nContent-Length: " + std::to_string(blob.size()) + "\r\n\r\n" + blob;
+          else
+            resp = "HTTP/1.1 404 Not Found\r\nContent-Length: 0\r\n\r\n";
+          for (size_t off = 0; off < resp.size();) {
+            int w = SSL_write(ssl, resp.data() + off, (int)(resp.size() - off));
+            if (w <= 0) break;
+            off += (size_t)w;
+          }
+          ++served;
+        }
+        SSL_shutdown(ssl);
+        SSL_free(ssl);
+        ::close(c);
+      }
+    });
+    const std::string url = "https://localhost:" + std::to_string(port) + "/latest/dstack-runner";
+    auto r = http_get_url(url, 10000, cert);
+    CHECK(r.ok() && r.body == blob);
+    auto bad = http_get_url(url, 10000, "/etc/ssl/certs/ca-certificates.crt");  // CA does not know it
+    CHECK(!bad.ok() && bad.error.find("TLS handshake") != std::string::npos);
+    ::shutdown(lfd, SHUT_RDWR);
+    srv.join();
+    ::close(lfd);
+    SSL_CTX_free(ctx);
+    CHECK(served == 2);
+    HttpClientRequest pr;
+    CHECK(parse_url("https://example.com/a/b", pr) && pr.tls && pr.port == 443 && pr.path == "/a/b");
+    CHECK(parse_url("http://h:8080", pr) && !pr.tls && pr.port == 8080 && pr.path == "/");
+    CHECK(!parse_url("ftp://h/x", pr));
+    run_capture({"rm", "-rf", "--", dir}, out);
   });
 
   fprintf(stderr, "%d/%d test groups passed\n", g_run - (g_failed ? 1 : 0), g_run);
