@@ -933,7 +933,10 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   const size_t lds_kv = 2 * (2 * (size_t)dkdv_qt * 256 + 8 * (size_t)dkdv_qt);
   const size_t lds_q = 4 * TILE_BYTES;
   // dK/dV kernel: the 8-wave K/V-resident variant is the default (2.10 vs 2.53 ms for the whole
-  // backward at S=8192, same box); DSTACK_AMD_FA_DKDV=4w selects the 4-wave register-resident one
+  // backward at S=8192, same box); DSTACK_AMD_FA_DKDV=4w selects the 4-wave register-resident one.
+  // Opt-in variants measured slower and kept for A/B only (profiles/fa_dkdv_seed_ab_r4h.txt, 3
+  // interleaved runs, whole backward S=8192): default 675-684 TFLOP/s, 'seed' (row-constant seeded
+  // dK/dV accumulators) 583-592, '64kv' (64 keys per wave, V in registers) 576-581.
   static const int dkdv_kind = [] {  // 8 = 8-wave (default), 4 = 4-wave, 64 / 65 = 64 keys per wave
     const char* v = getenv("DSTACK_AMD_FA_DKDV");
     if (!v) return 8;
