@@ -136,7 +136,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": (res["tokens_per_s"] / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16",
-            "data": "synthetic (uniform random token ids), random-init weights",
+            "data": "synthetic (Zipf unigram + bigram chains, fresh batch every micro-step; "
+                    "workloads/data.py), random-init weights",
             "config": {
                 "model": "Llama-3-8B" if args.model == "llama-3-8b" else args.model,
                 "global_batch": args.micro_batch * args.grad_accum * env.world,
@@ -148,6 +149,8 @@ def main():
             },
             "tflops_per_gpu": round(res["tflops_per_gpu"], 1),
             "final_loss": res["final_loss"],
+            "losses": {"warmup": res.get("warmup_losses"), "timed": res.get("losses"),
+                       "floor": res.get("loss_floor"), "unigram_entropy": res.get("unigram_entropy")},
             "max_mem_gb": res["max_mem_gb"],
             "ops": os.environ.get("DSTACK_AMD_OPS", "hip"),
             "gemm_tuning": res.get("gemm_tuning"),

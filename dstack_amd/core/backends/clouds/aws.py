@@ -15,16 +15,25 @@ Config: ``regions``, ``vpc_name``/``vpc_ids``/``subnet_ids``, ``public_ips``, ``
 from __future__ import annotations
 
 import base64
+import concurrent.futures as cf
+import datetime as _dt
+import json
 import os
 import urllib.parse
 import xml.etree.ElementTree as ET
-from typing import Dict, List, Optional, Tuple
+from dataclasses import replace
+from typing import Dict, List, Optional, Set, Tuple
 
+from dstack_amd.core.backends.catalog import CatalogRow, offline_rows
 from dstack_amd.core.backends.clouds.common import VMCompute, check_response, cloud_init, sigv4_headers
 from dstack_amd.core.errors import ComputeError, NoCapacityError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.gateways import GatewayComputeConfiguration, GatewayProvisioningData
-from dstack_amd.core.models.instances import InstanceConfiguration, InstanceOfferWithAvailability
+from dstack_amd.core.models.instances import (
+    InstanceAvailability,
+    InstanceConfiguration,
+    InstanceOfferWithAvailability,
+)
 from dstack_amd.core.models.placement import PlacementGroup, PlacementGroupProvisioningData
 from dstack_amd.core.models.volumes import Volume, VolumeAttachmentData, VolumeProvisioningData
 
@@ -41,9 +50,21 @@ def _strip_ns(root: ET.Element) -> ET.Element:
     return root
 
 
+def quota_class(instance_name: str, spot: bool) -> str:
+    """EC2 vCPU quota class of an instance type (the ``Class`` dimension of the service quota's
+    usage metric: ``P/OnDemand``, ``G/Spot``, ``Standard/OnDemand``, ...)."""
+    fam = instance_name.split(".")[0].lower()
+    for prefix, cls in (("trn", "Trn"), ("inf", "Inf"), ("dl", "DL"), ("vt", "G"), ("p", "P"), ("g", "G"),
+                        ("x", "X"), ("f", "F")):
+        if fam.startswith(prefix):
+            return f"{cls}/{'Spot' if spot else 'OnDemand'}"
+    return f"Standard/{'Spot' if spot else 'OnDemand'}"
+
+
 class AWSCompute(VMCompute):
     TYPE = BackendType.AWS
     SSH_USER = "ubuntu"
+    CONFIGURABLE_DISK = (1.0, 16384.0)  # EBS gp2/gp3 root volume, GiB
 
     def __init__(self, config: Dict, auth: Dict, client=None):
         super().__init__(config, auth, client)
@@ -82,6 +103,76 @@ class AWSCompute(VMCompute):
             if not token:
                 break
         return items
+
+    # ---- live catalog -------------------------------------------------------------------------
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """Catalog rows checked against the account, per region (reference ``get_offers``,
+        ``aws/compute.py:105-141``): instance types not offered in the region are
+        ``not_available``, types whose vCPU quota class is below the type's vCPUs are ``no_quota``,
+        spot rows take the current lowest spot price over the region's zones."""
+        base = offline_rows(self.TYPE)
+        wanted = self.config.get("regions")
+        regions = sorted({r.location for r in base if not wanted or r.location in wanted})
+        names = sorted({r.instance_name for r in base})
+        with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(regions)))) as ex:
+            info = dict(zip(regions, ex.map(lambda reg: self._region_catalog(reg, names), regions)))
+        out = []
+        for r in base:
+            if r.location not in info:
+                continue
+            offered, spot_prices, quotas = info[r.location]
+            if r.instance_name not in offered:
+                out.append(replace(r, availability=InstanceAvailability.NOT_AVAILABLE))
+                continue
+            price = spot_prices.get(r.instance_name, r.price) if r.spot else r.price
+            quota = quotas.get(quota_class(r.instance_name, r.spot)) if quotas is not None else None
+            avail = InstanceAvailability.NO_QUOTA if quota is not None and quota < r.cpu else \
+                InstanceAvailability.UNKNOWN
+            out.append(replace(r, price=round(price, 6), availability=avail))
+        return out
+
+    def _region_catalog(self, region: str, names: List[str]
+                        ) -> Tuple[Set[str], Dict[str, float], Optional[Dict[str, float]]]:
+        params = {"LocationType": "region", "Filter.1.Name": "instance-type"}
+        for i, n in enumerate(names, 1):
+            params[f"Filter.1.Value.{i}"] = n
+        offered = {it.findtext("instanceType") for it in self._paginate(
+            region, "DescribeInstanceTypeOfferings", params, "./instanceTypeOfferingSet/item")}
+        sp = {"ProductDescription.1": "Linux/UNIX",
+              "StartTime": _dt.datetime.now(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")}
+        for i, n in enumerate(sorted(offered), 1):
+            sp[f"InstanceType.{i}"] = n
+        spot: Dict[str, float] = {}
+        if offered:
+            for it in self._paginate(region, "DescribeSpotPriceHistory", sp, "./spotPriceHistorySet/item"):
+                t, price = it.findtext("instanceType"), float(it.findtext("spotPrice") or "inf")
+                spot[t] = min(price, spot.get(t, price))
+        return offered, spot, self._quotas(region)
+
+    def _quotas(self, region: str) -> Optional[Dict[str, float]]:
+        """vCPU quotas by class from Service Quotas (``None`` when the API is not permitted: the
+        rows then keep ``unknown`` availability, as without quota information)."""
+        url = f"https://servicequotas.{region}.amazonaws.com/"
+        out: Dict[str, float] = {}
+        token = None
+        for _ in range(20):
+            body = json.dumps({"ServiceCode": "ec2", "MaxResults": 100, **({"NextToken": token} if token else {})})
+            headers = sigv4_headers("POST", url, region, "servicequotas", self.access_key, self.secret_key,
+                                    body.encode(), self.session_token, extra_headers={
+                                        "content-type": "application/x-amz-json-1.1",
+                                        "x-amz-target": "ServiceQuotasV20190624.ListServiceQuotas"})
+            r = self.http.post(url, content=body.encode(), headers=headers)
+            if r.status_code >= 400:
+                return None
+            d = r.json()
+            for q in d.get("Quotas") or []:
+                cls = ((q.get("UsageMetric") or {}).get("MetricDimensions") or {}).get("Class")
+                if cls:
+                    out[cls] = float(q.get("Value") or 0)
+            token = d.get("NextToken")
+            if not token:
+                break
+        return out
 
     # ---- helpers ------------------------------------------------------------------------------
     def _image_id(self, region: str, gpu: bool) -> str:

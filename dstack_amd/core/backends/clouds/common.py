@@ -29,7 +29,7 @@ from typing import Dict, List, Optional, Tuple
 import httpx
 
 from dstack_amd.core.backends.base import Compute, get_docker_commands, get_user_data
-from dstack_amd.core.backends.catalog import catalog_offers
+from dstack_amd.core.backends.catalog import CatalogRow, get_catalog_offers
 from dstack_amd.core.errors import BackendAuthError, ComputeError, NoCapacityError
 from dstack_amd.core.models.instances import (
     InstanceAvailability,
@@ -68,7 +68,51 @@ def check_response(r: httpx.Response, what: str) -> httpx.Response:
     return r
 
 
-class VMCompute(Compute):
+class CatalogOffers:
+    """``get_offers`` from the catalog layers (catalog.py): the backend's live listing when it has
+    one (``_fetch_catalog``), else the offline catalog."""
+
+    # ---- offers -------------------------------------------------------------------------------
+    # disk sizes (GB) the cloud lets us choose at launch, for catalog rows without a fixed disk
+    CONFIGURABLE_DISK: Tuple[float, Optional[float]] = (1.0, None)
+
+    def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
+        fetch = self._fetch_catalog if self.has_online_catalog() else None
+        offers = get_catalog_offers(self.TYPE, self.config.get("regions"), requirements, self.CONFIGURABLE_DISK,
+                                    extra_filter=self._offer_filter, fetch=fetch, cache_key=self.catalog_key())
+        avail = self._availability()
+        for o in offers:
+            a = avail.get((o.instance.name, o.region)) if avail else None
+            if a is not None:
+                o.availability = a
+        return offers
+
+    def has_online_catalog(self) -> bool:
+        """True when the backend implements a live listing and it is not switched off
+        (``offline_catalog: true`` in the backend config or ``DSTACK_CATALOG_OFFLINE_ONLY=1``)."""
+        if self.config.get("offline_catalog") or os.getenv("DSTACK_CATALOG_OFFLINE_ONLY") == "1":
+            return False
+        return type(self)._fetch_catalog is not CatalogOffers._fetch_catalog
+
+    def catalog_key(self) -> str:
+        """Online-cache key: backend type + a fingerprint of the credentials / account settings."""
+        ident = json.dumps([self.auth, self.config.get("project_id"), self.config.get("subscription_id")],
+                           sort_keys=True, default=str)
+        return f"{self.TYPE.value}:{hashlib.sha256(ident.encode()).hexdigest()[:16]}"
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """Live listing of the cloud's instance types (price + availability); see catalog.py."""
+        raise NotImplementedError
+
+    def _offer_filter(self, offer: InstanceOfferWithAvailability) -> bool:
+        return True
+
+    def _availability(self) -> Dict[Tuple[str, str], InstanceAvailability]:
+        """Optional extra stock overlay on top of the catalog rows."""
+        return {}
+
+
+class VMCompute(CatalogOffers, Compute):
     """Catalog offers + REST provisioning hooks (``_launch`` / ``_describe`` / ``_terminate``)."""
 
     SSH_USER = "ubuntu"
@@ -79,22 +123,6 @@ class VMCompute(Compute):
         self.config = config or {}
         self.auth = auth or {}
         self.http = client or httpx.Client(timeout=60)
-
-    # ---- offers -------------------------------------------------------------------------------
-    def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
-        offers = catalog_offers(self.TYPE, self.config.get("regions"), requirements)
-        avail = self._availability()
-        out = []
-        for o in offers:
-            a = avail.get((o.instance.name, o.region)) if avail else None
-            if a is not None:
-                o.availability = a
-            out.append(o)
-        return out
-
-    def _availability(self) -> Dict[Tuple[str, str], InstanceAvailability]:
-        """Optional live stock query; the default leaves catalog availability ``unknown``."""
-        return {}
 
     # ---- lifecycle ----------------------------------------------------------------------------
     def create_instance(self, instance_offer: InstanceOfferWithAvailability,

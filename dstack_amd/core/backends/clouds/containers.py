@@ -17,10 +17,11 @@ import httpx
 import yaml
 
 from dstack_amd.core.backends.base import Compute, DSTACK_RUNNER_SSH_PORT
-from dstack_amd.core.backends.catalog import catalog_offers
-from dstack_amd.core.backends.clouds.common import check_response, container_commands
+from dstack_amd.core.backends.catalog import CatalogRow, gpu_row
+from dstack_amd.core.backends.clouds.common import CatalogOffers, check_response, container_commands
 from dstack_amd.core.errors import ComputeError, NoCapacityError
 from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.gpus import normalize_gpu_name
 from dstack_amd.core.models.instances import (
     InstanceAvailability,
     InstanceOfferWithAvailability,
@@ -40,20 +41,56 @@ def _entrypoint(keys: List[str]) -> str:
     return " && ".join(container_commands(keys))
 
 
-class ContainerCompute(Compute):
+class ContainerCompute(CatalogOffers, Compute):
     def __init__(self, config: Dict, auth: Dict, client: Optional[httpx.Client] = None):
         super().__init__()
         self.config, self.auth = config or {}, auth or {}
         self.http = client or httpx.Client(timeout=60)
-
-    def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
-        return catalog_offers(self.TYPE, self.config.get("regions"), requirements)
 
 
 # ---------------------------------------------------------------------------------------------
 class RunpodCompute(ContainerCompute):
     TYPE = BackendType.RUNPOD
     API = "https://api.runpod.io/graphql"
+    CONFIGURABLE_DISK = (10.0, None)
+    GPU_COUNTS = (1, 2, 4, 8)
+    GPU_TYPE_IDS = {"MI300X": "AMD Instinct MI300X OAM"}
+    CATALOG_QUERY = (
+        "query { gpuTypes { id displayName memoryInGb maxGpuCount securePrice secureSpotPrice "
+        "lowestPrice(input: {gpuCount: 1}) { minVcpu minMemory } } "
+        "dataCenters { id listed gpuAvailability { gpuTypeId available stockStatus } } }"
+    )
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """GPU types (secure-cloud on-demand and spot price per GPU, vCPU / RAM per GPU) x data
+        centres' per-type stock; instance name ``<n>x-<GPU>`` as in the offline catalog."""
+        d = self._gql(self.CATALOG_QUERY)
+        types = {t["id"]: t for t in d.get("gpuTypes") or []}
+        wanted = self.config.get("regions")
+        rows = []
+        for dc in d.get("dataCenters") or []:
+            if dc.get("listed") is False or (wanted and dc.get("id") not in wanted):
+                continue
+            for ga in dc.get("gpuAvailability") or []:
+                t = types.get(ga.get("gpuTypeId"))
+                if not t:
+                    continue
+                name = normalize_gpu_name(t.get("displayName") or t["id"])
+                self.GPU_TYPE_IDS = {**self.GPU_TYPE_IDS, name: t["id"]}
+                low = t.get("lowestPrice") or {}
+                ok = bool(ga.get("available")) or (ga.get("stockStatus") or "").lower() in ("high", "medium", "low")
+                for n in self.GPU_COUNTS:
+                    if n > int(t.get("maxGpuCount") or 8):
+                        break
+                    for spot, price in ((False, t.get("securePrice")), (True, t.get("secureSpotPrice"))):
+                        if not price:
+                            continue
+                        rows.append(gpu_row(f"{n}x-{name}", dc["id"], n * float(price),
+                                            n * int(low.get("minVcpu") or 8), n * int(low.get("minMemory") or 32),
+                                            name, n, spot=spot, gpu_memory_gb=t.get("memoryInGb"),
+                                            availability=InstanceAvailability.AVAILABLE if ok
+                                            else InstanceAvailability.NOT_AVAILABLE))
+        return rows
 
     def _gql(self, query: str, variables: Optional[dict] = None) -> dict:
         r = self.http.post(self.API, params={"api_key": self.auth.get("api_key", "")},
@@ -70,7 +107,7 @@ class RunpodCompute(ContainerCompute):
                 project_ssh_private_key: str, volumes: List[Volume]) -> JobProvisioningData:
         res = instance_offer.instance.resources
         keys = [project_ssh_public_key.strip()] + ([run.run_spec.ssh_key_pub.strip()] if run.run_spec.ssh_key_pub else [])
-        gpu_type = {"MI300X": "AMD Instinct MI300X OAM"}.get(res.gpus[0].name, res.gpus[0].name) if res.gpus else None
+        gpu_type = self.GPU_TYPE_IDS.get(res.gpus[0].name, res.gpus[0].name) if res.gpus else None
         inp = {
             "name": f"{run.run_spec.run_name}-{job.job_spec.job_num}", "imageName": _job_image(job),
             "gpuTypeId": gpu_type, "gpuCount": len(res.gpus), "cloudType": "SECURE" if not res.spot else "COMMUNITY",
@@ -141,33 +178,20 @@ class VastAICompute(ContainerCompute):
     def _h(self):
         return {"Authorization": f"Bearer {self.auth.get('api_key', '')}"}
 
-    def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
-        """Live marketplace asks (``/bundles``) when reachable; the catalog otherwise."""
-        try:
-            r = self.http.post(f"{self.API}/bundles/", headers=self._h(),
-                               json={"rentable": {"eq": True}, "rented": {"eq": False}, "order": [["dph_total", "asc"]],
-                                     "limit": 100})
-            asks = r.json().get("offers", []) if r.status_code == 200 else []
-        except httpx.HTTPError:
-            asks = []
-        if not asks:
-            return super().get_offers(requirements)
-        from dstack_amd.core.backends.base import offer_matches
-        from dstack_amd.core.models.gpus import normalize_gpu_name
-        from dstack_amd.core.models.instances import Disk, Gpu, InstanceType, Resources
-
-        out = []
-        for a in asks:
-            name = normalize_gpu_name(a.get("gpu_name", ""))
-            gpus = [Gpu(name=name, memory_mib=int(a.get("gpu_ram", 0))) for _ in range(int(a.get("num_gpus", 0)))]
-            res = Resources(cpus=int(a.get("cpu_cores_effective", 1)), memory_mib=int(a.get("cpu_ram", 0)), gpus=gpus,
-                            spot=False, disk=Disk(size_mib=int(float(a.get("disk_space", 100)) * 1024)))
-            o = InstanceOfferWithAvailability(backend=self.TYPE, instance=InstanceType(name=str(a["id"]), resources=res),
-                                              region=str(a.get("geolocation", "any")), price=float(a["dph_total"]),
-                                              availability=InstanceAvailability.AVAILABLE)
-            if offer_matches(o, requirements):
-                out.append(o)
-        return out
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """Live marketplace asks (``/bundles``): one row per rentable offer, named by its ask id."""
+        r = check_response(self.http.post(f"{self.API}/bundles/", headers=self._h(), json={
+            "rentable": {"eq": True}, "rented": {"eq": False}, "order": [["dph_total", "asc"]], "limit": 500}),
+            "vastai bundles")
+        rows = []
+        for a in r.json().get("offers") or []:
+            n = int(a.get("num_gpus") or 0)
+            rows.append(gpu_row(str(a["id"]), str(a.get("geolocation") or "any"), float(a["dph_total"]),
+                                int(a.get("cpu_cores_effective") or 1), float(a.get("cpu_ram") or 0) / 1024,
+                                a.get("gpu_name") or None, n, disk_gb=float(a.get("disk_space") or 100),
+                                gpu_memory_gb=float(a.get("gpu_ram") or 0) / 1024 or None,
+                                availability=InstanceAvailability.AVAILABLE))
+        return rows
 
     def run_job(self, run, job, instance_offer, project_ssh_public_key, project_ssh_private_key, volumes):
         keys = [project_ssh_public_key.strip()] + ([run.run_spec.ssh_key_pub.strip()] if run.run_spec.ssh_key_pub else [])

@@ -22,8 +22,10 @@ import hashlib
 import json
 import time
 import urllib.parse
-from typing import Optional
+from dataclasses import replace
+from typing import Dict, List, Optional, Tuple
 
+from dstack_amd.core.backends.catalog import CatalogRow, offline_rows
 from dstack_amd.core.backends.clouds.common import (
     OAuthToken,
     VMCompute,
@@ -34,6 +36,7 @@ from dstack_amd.core.backends.clouds.common import (
 )
 from dstack_amd.core.errors import ComputeError
 from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models.instances import InstanceAvailability
 
 
 # ---------------------------------------------------------------------------------------------
@@ -58,6 +61,68 @@ class AzureCompute(VMCompute):
 
     def _h(self):
         return {"Authorization": f"Bearer {self._token.get()}"}
+
+    CONFIGURABLE_DISK = (30.0, 4095.0)  # managed OS disk, GiB
+    RETAIL_PRICES = "https://prices.azure.com/api/retail/prices"
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """Catalog SKUs priced from the public Retail Prices API (Linux pay-as-you-go and Spot
+        meters, every region that sells them) and checked against the subscription's resource-SKU
+        restrictions (``NotAvailableForSubscription`` -> ``no_quota``)."""
+        base = offline_rows(self.TYPE)
+        specs: Dict[str, CatalogRow] = {}
+        for r in base:
+            specs.setdefault(r.instance_name, r)
+        prices = self._retail_prices(sorted(specs))
+        wanted = self.config.get("regions")
+        restricted = self._restricted_skus() if self.subscription else {}
+        out = []
+        for (sku, region, spot), price in sorted(prices.items()):
+            if wanted and region not in wanted:
+                continue
+            avail = InstanceAvailability.NO_QUOTA if region in restricted.get(sku, ()) else InstanceAvailability.UNKNOWN
+            out.append(replace(specs[sku], location=region, spot=spot, price=round(price, 6), availability=avail))
+        return out
+
+    def _retail_prices(self, skus: List[str]) -> Dict[Tuple[str, str, bool], float]:
+        flt = "serviceName eq 'Virtual Machines' and priceType eq 'Consumption' and (" + \
+            " or ".join(f"armSkuName eq '{s}'" for s in skus) + ")"
+        url: Optional[str] = f"{self.RETAIL_PRICES}?{urllib.parse.urlencode({'$filter': flt})}"
+        out: Dict[Tuple[str, str, bool], float] = {}
+        for _ in range(50):
+            if not url:
+                break
+            d = check_response(self.http.get(url), "azure retail prices").json()
+            for it in d.get("Items") or []:
+                name = it.get("skuName") or ""
+                if "Windows" in (it.get("productName") or "") or "Low Priority" in name:
+                    continue
+                if it.get("unitOfMeasure", "1 Hour") != "1 Hour":
+                    continue
+                key = (it.get("armSkuName"), it.get("armRegionName"), "Spot" in name)
+                price = float(it.get("retailPrice") or 0)
+                if price > 0:
+                    out[key] = min(price, out.get(key, price))
+            url = d.get("NextPageLink")
+        return out
+
+    def _restricted_skus(self) -> Dict[str, set]:
+        url = (f"{self.ARM}/subscriptions/{self.subscription}/providers/Microsoft.Compute/skus"
+               "?api-version=2021-07-01")
+        out: Dict[str, set] = {}
+        for _ in range(50):
+            d = check_response(self.http.get(url, headers=self._h()), "azure resource skus").json()
+            for sku in d.get("value") or []:
+                if sku.get("resourceType") != "virtualMachines":
+                    continue
+                for rs in sku.get("restrictions") or []:
+                    if rs.get("reasonCode") == "NotAvailableForSubscription" and rs.get("type") == "Location":
+                        locs = (rs.get("restrictionInfo") or {}).get("locations") or rs.get("values") or []
+                        out.setdefault(sku.get("name"), set()).update(l.lower() for l in locs)
+            url = d.get("nextLink")
+            if not url:
+                break
+        return out
 
     def _rg(self, region: str) -> str:
         rg = (self.config.get("resource_groups") or {}).get(region) or f"dstack-{region}"
@@ -254,12 +319,56 @@ class GCPCompute(VMCompute):
     def _h(self):
         return {"Authorization": f"Bearer {self._token.get()}"}
 
-    def _zone(self, region: str) -> str:
+    CONFIGURABLE_DISK = (10.0, 65536.0)  # persistent boot disk, GB
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """Catalog machine types checked against the project's zones (aggregated
+        ``machineTypes`` list): regions where a type is offered in some zone keep the catalog
+        price (``unknown`` stock), the rest are ``not_available``; zones offering each type are
+        remembered for the launch."""
+        base = offline_rows(self.TYPE)
+        names = sorted({r.instance_name for r in base})
+        flt = " OR ".join(f'(name = "{n}")' for n in names)
+        zones: Dict[Tuple[str, str], List[str]] = {}
+        token = None
+        for _ in range(50):
+            params = {"filter": flt, "maxResults": 500, **({"pageToken": token} if token else {})}
+            d = check_response(self.http.get(f"{self.API}/projects/{self.project}/aggregated/machineTypes",
+                                             params=params, headers=self._h()), "gcp machine types").json()
+            for scope, v in (d.get("items") or {}).items():
+                zone = scope.split("/", 1)[-1]
+                region = zone.rsplit("-", 1)[0]
+                for mt in v.get("machineTypes") or []:
+                    zones.setdefault((mt.get("name"), region), []).append(zone)
+            token = d.get("nextPageToken")
+            if not token:
+                break
+        self._type_zones = {k: sorted(v) for k, v in zones.items()}
+        out = []
+        wanted = self.config.get("regions")
+        specs: Dict[str, List[CatalogRow]] = {}
+        for r in base:
+            specs.setdefault(r.instance_name, []).append(r)
+        for name, rows in specs.items():
+            offered = {reg for (n, reg) in zones if n == name}
+            for spot in sorted({r.spot for r in rows}):
+                proto = next(r for r in rows if r.spot == spot)
+                for region in sorted(offered | {r.location for r in rows if r.spot == spot}):
+                    if wanted and region not in wanted:
+                        continue
+                    out.append(replace(proto, location=region, availability=InstanceAvailability.UNKNOWN
+                                       if region in offered else InstanceAvailability.NOT_AVAILABLE))
+        return out
+
+    def _zone(self, region: str, machine_type: Optional[str] = None) -> str:
         zones = self.config.get("zones") or {}
-        return zones.get(region) or f"{region}-a"
+        if zones.get(region):
+            return zones[region]
+        offered = getattr(self, "_type_zones", {}).get((machine_type, region)) if machine_type else None
+        return offered[0] if offered else f"{region}-a"
 
     def _launch(self, offer, cfg):
-        zone = self._zone(offer.region)
+        zone = self._zone(offer.region, offer.instance.name)
         res = offer.instance.resources
         name = cfg.instance_name.lower().replace("_", "-")[:62]
         body = {

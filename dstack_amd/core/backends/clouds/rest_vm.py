@@ -8,13 +8,22 @@ cloud-init installs ``dstack-shim``.  Vultr is the MI355X/MI325X/MI300X bare-met
 from __future__ import annotations
 
 import base64
+import re
 import uuid
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
+from dstack_amd.core.backends.catalog import CatalogRow, gpu_row
 from dstack_amd.core.backends.clouds.common import OAuthToken, VMCompute, check_response, cloud_init
 from dstack_amd.core.errors import ComputeError
 from dstack_amd.core.models.backends import BackendType
-from dstack_amd.core.models.instances import InstanceConfiguration, InstanceOfferWithAvailability
+from dstack_amd.core.models.gpus import gpu_info, normalize_gpu_name
+from dstack_amd.core.models.instances import (
+    InstanceAvailability,
+    InstanceConfiguration,
+    InstanceOfferWithAvailability,
+)
+
+_AVAILABLE, _NOT_AVAILABLE = InstanceAvailability.AVAILABLE, InstanceAvailability.NOT_AVAILABLE
 
 
 class LambdaCompute(VMCompute):
@@ -23,8 +32,31 @@ class LambdaCompute(VMCompute):
     TYPE = BackendType.LAMBDA
     API = "https://cloud.lambdalabs.com/api/v1"
 
+    REGIONS = ("us-east-1", "us-east-2", "us-west-1", "us-west-2", "us-west-3", "us-south-1", "us-south-2",
+               "us-south-3", "us-midwest-1", "europe-central-1", "asia-northeast-1", "asia-northeast-2",
+               "asia-south-1", "me-west-1")
+
     def _h(self):
         return {"Authorization": f"Bearer {self.auth.get('api_key', '')}"}
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """``GET /instance-types``: price, specs and the regions with capacity right now.  Regions
+        without capacity are listed as ``not_available`` so the plan still shows the type."""
+        r = check_response(self.http.get(f"{self.API}/instance-types", headers=self._h()), "lambda instance-types")
+        rows = []
+        for key, d in (r.json().get("data") or {}).items():
+            it = d.get("instance_type") or {}
+            specs = it.get("specs") or {}
+            m = re.match(r"\s*([A-Za-z0-9]+)[^(]*(?:\((\d+)\s*GB)?", it.get("gpu_description") or "")
+            gpu_name = m.group(1) if m and specs.get("gpus") else None
+            gpu_mem = float(m.group(2)) if m and m.group(2) else None
+            with_capacity = {x.get("name") for x in d.get("regions_with_capacity_available") or []}
+            for loc in sorted(with_capacity | set(self.config.get("regions") or self.REGIONS)):
+                rows.append(gpu_row(it.get("name", key), loc, float(it.get("price_cents_per_hour", 0)) / 100,
+                                    specs.get("vcpus", 0), specs.get("memory_gib", 0), gpu_name,
+                                    specs.get("gpus", 0), disk_gb=specs.get("storage_gib"), gpu_memory_gb=gpu_mem,
+                                    availability=_AVAILABLE if loc in with_capacity else _NOT_AVAILABLE))
+        return rows
 
     def _ensure_key(self, cfg: InstanceConfiguration) -> str:
         name = f"dstack-{cfg.project_name}"
@@ -71,6 +103,61 @@ class VultrCompute(VMCompute):
     def _kind(plan: str) -> str:
         return "bare-metals" if plan.startswith("vbm-") else "instances"
 
+    def _list(self, path: str, key: str) -> List[dict]:
+        out, cursor = [], ""
+        for _ in range(50):
+            params = {"per_page": 500, **({"cursor": cursor} if cursor else {})}
+            d = check_response(self.http.get(f"{self.API}/{path}", params=params, headers=self._h()),
+                               f"vultr {path}").json()
+            out.extend(d.get(key) or [])
+            cursor = ((d.get("meta") or {}).get("links") or {}).get("next") or ""
+            if not cursor:
+                break
+        return out
+
+    @staticmethod
+    def _plan_gpu(plan: dict) -> Tuple[Optional[str], int, Optional[float]]:
+        """GPU model / count / per-GPU memory of a plan: cloud GPU plans carry ``gpu_type`` +
+        ``gpu_vram_gb``; bare metal encodes it in the id (``vbm-256c-2048gb-8-mi355x-gpu``)."""
+        if plan.get("gpu_type"):
+            name = str(plan["gpu_type"]).replace("NVIDIA_", "").replace("AMD_", "").split("_")[0]
+            count = int(plan.get("gpu_count") or 1)
+            vram = float(plan.get("gpu_vram_gb") or 0) / count or None
+            return name, count, vram
+        m = re.search(r"-(\d+)-([a-z0-9]+)-gpu$", plan.get("id", ""))
+        if m:
+            return m.group(2).upper(), int(m.group(1)), None
+        return None, 0, None
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """GPU plans (``/plans?type=vcg``) and bare-metal plans (``/plans-metal``) with their hourly
+        price, and per-region stock from ``/regions/{id}/availability``."""
+        plans = [(p, False) for p in self._list("plans", "plans") if p.get("type") == "vcg" or p.get("gpu_type")]
+        plans += [(p, True) for p in self._list("plans-metal", "plans_metal")]
+        wanted = set(self.config.get("regions") or [])
+        rows, stock = [], {}
+        for plan, metal in plans:
+            gpu_name, count, vram = self._plan_gpu(plan)
+            if not gpu_name and not metal:
+                continue
+            full = gpu_info(normalize_gpu_name(gpu_name)) if gpu_name else None
+            if vram is not None and full is not None and vram < 0.9 * full.memory_gb:
+                continue  # fractional (vGPU) slice of a card
+            price = plan.get("hourly_cost") or round(float(plan.get("monthly_cost", 0)) / 730, 4)
+            for loc in plan.get("locations") or []:
+                if wanted and loc not in wanted:
+                    continue
+                if loc not in stock:
+                    d = check_response(self.http.get(f"{self.API}/regions/{loc}/availability", params={"type": "all"},
+                                                     headers=self._h()), "vultr availability").json()
+                    stock[loc] = set(d.get("available_plans") or [])
+                cpus = plan.get("cpu_threads") or plan.get("cpu_count") or plan.get("vcpu_count") or 0
+                rows.append(gpu_row(plan["id"], loc, float(price), cpus, float(plan.get("ram", 0)) / 1024, gpu_name,
+                                    count, disk_gb=float(plan.get("disk", 0)) * int(plan.get("disk_count") or 1),
+                                    gpu_memory_gb=vram,
+                                    availability=_AVAILABLE if plan["id"] in stock[loc] else _NOT_AVAILABLE))
+        return rows
+
     def _launch(self, offer, cfg):
         kind = self._kind(offer.instance.name)
         body = {"region": offer.region, "plan": offer.instance.name, "label": cfg.instance_name,
@@ -107,14 +194,49 @@ class TensorDockCompute(VMCompute):
     API = "https://marketplace.tensordock.com/api/v0"
     SSH_USER = "user"
 
+    CONFIGURABLE_DISK = (20.0, None)
+    GPU_COUNTS = (1, 2, 4, 8)
+
     def _auth(self):
         return {"api_key": self.auth.get("api_key", ""), "api_token": self.auth.get("api_token", "")}
 
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """Marketplace host nodes (``/client/deploy/hostnodes``): one row per (GPU model, count)
+        that fits a node, CPU / RAM in proportion to the GPUs taken, price = the node's per-unit
+        GPU + vCPU + RAM + 100 GB disk prices.  Instance name ``<gpu model>:<count>:<node id>``."""
+        r = check_response(self.http.get(f"{self.API}/client/deploy/hostnodes"), "tensordock hostnodes")
+        rows = []
+        for node_id, node in (r.json().get("hostnodes") or {}).items():
+            if (node.get("status") or {}).get("online") is False:
+                continue
+            loc = node.get("location") or {}
+            region = "-".join(str(x) for x in (loc.get("country"), loc.get("region"), loc.get("city")) if x)
+            region = region.lower().replace(" ", "") or "any"
+            specs = node.get("specs") or {}
+            cpu, ram, disk = specs.get("cpu") or {}, specs.get("ram") or {}, specs.get("storage") or {}
+            for model, g in (specs.get("gpu") or {}).items():
+                avail = int(g.get("amount") or 0)
+                for n in self.GPU_COUNTS:
+                    if n > avail:
+                        break
+                    cpus = max(1, int(cpu.get("amount", 0)) * n // avail // 2 * 2)
+                    mem = max(1, int(ram.get("amount", 0)) * n // avail)
+                    if int(disk.get("amount", 0)) < 100:
+                        continue
+                    price = (n * float(g.get("price", 0)) + cpus * float(cpu.get("price", 0))
+                             + mem * float(ram.get("price", 0)) + 100 * float(disk.get("price", 0)))
+                    rows.append(gpu_row(f"{model}:{n}:{node_id}", region, price, cpus, mem,
+                                        model.split("-")[0].upper(), n, gpu_memory_gb=g.get("vram"),
+                                        availability=_AVAILABLE))
+        return rows
+
     def _launch(self, offer, cfg):
         res = offer.instance.resources
-        node = offer.instance.name.split(":")[-1] if ":" in offer.instance.name else offer.region
+        parts = offer.instance.name.split(":")
+        node = parts[-1] if len(parts) > 1 else offer.region
+        model = parts[0] if len(parts) == 3 else (res.gpus[0].name.lower() if res.gpus else "")
         data = {**self._auth(), "hostnode": node, "name": cfg.instance_name, "gpu_count": len(res.gpus),
-                "gpu_model": (res.gpus[0].name.lower() if res.gpus else ""), "vcpus": res.cpus,
+                "gpu_model": model, "vcpus": res.cpus,
                 "ram": res.memory_mib // 1024, "storage": res.disk.size_mib // 1024,
                 "external_ports": "{22}", "internal_ports": "{22}", "operating_system": "Ubuntu 22.04 LTS",
                 "cloudinit_script": cloud_init(cfg), "password": uuid.uuid4().hex}
@@ -200,6 +322,43 @@ class DataCrunchCompute(VMCompute):
 
     def _h(self):
         return {"Authorization": f"Bearer {self._token.get()}"}
+
+    CONFIGURABLE_DISK = (50.0, None)
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """``/instance-types`` (on-demand and spot prices, specs) x ``/instance-availability`` per
+        location, on-demand and spot separately."""
+        types = check_response(self.http.get(f"{self.API}/instance-types", headers=self._h()),
+                               "datacrunch instance-types").json()
+        stock: Dict[Tuple[str, bool], set] = {}
+        for spot in (False, True):
+            av = check_response(self.http.get(f"{self.API}/instance-availability",
+                                              params={"is_spot": str(spot).lower()}, headers=self._h()),
+                                "datacrunch availability").json()
+            for loc in av:
+                stock[(loc.get("location_code"), spot)] = set(loc.get("availabilities") or [])
+        locations = sorted({loc for loc, _ in stock} | set(self.config.get("regions") or []))
+        rows = []
+        for t in types:
+            name = t.get("instance_type")
+            gpu = t.get("gpu") or {}
+            desc = re.sub(r"^\d+x\s*", "", gpu.get("description") or "")
+            gpu_name = desc.split()[0] if desc and gpu.get("number_of_gpus") else None
+            gpu_mem = (t.get("gpu_memory") or {}).get("size_in_gigabytes")
+            count = int(gpu.get("number_of_gpus") or 0)
+            for spot in (False, True):
+                price = t.get("spot_price") if spot else t.get("price_per_hour")
+                if price in (None, "", 0, "0"):
+                    continue
+                for loc in locations:
+                    if self.config.get("regions") and loc not in self.config["regions"]:
+                        continue
+                    ok = name in stock.get((loc, spot), set())
+                    rows.append(gpu_row(name, loc, float(price), (t.get("cpu") or {}).get("number_of_cores", 0),
+                                        (t.get("memory") or {}).get("size_in_gigabytes", 0), gpu_name, count,
+                                        spot=spot, gpu_memory_gb=(float(gpu_mem) / count if gpu_mem and count else None),
+                                        availability=_AVAILABLE if ok else _NOT_AVAILABLE))
+        return rows
 
     def _launch(self, offer, cfg):
         r = check_response(self.http.post(f"{self.API}/scripts", headers=self._h(), json={

@@ -163,10 +163,10 @@ def delete_backends(s: Session, project: ProjectModel, names: List[str]):
 
 
 def backend_config_values(body: dict) -> dict:
-    from dstack_amd.core.backends.catalog import CATALOG
+    from dstack_amd.core.backends.catalog import offline_rows
 
     btype = _configurable_type(body)
-    regions = sorted({r for it in CATALOG if it.backend == btype for r in it.regions})
+    regions = sorted({r.location for r in offline_rows(btype)})
     wanted = body.get("regions") or body.get("locations")
     selected = [r for r in regions if not wanted or r in wanted]
     return {"type": btype.value, "default_creds": btype in (BackendType.AWS, BackendType.AZURE, BackendType.GCP,

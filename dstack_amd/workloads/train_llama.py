@@ -22,6 +22,7 @@ import torch.distributed as dist
 
 from dstack_amd.models.llama import CONFIGS, Llama
 from dstack_amd.parallel.zero import ZeroOptimizer
+from dstack_amd.workloads.data import SyntheticLM
 
 
 @dataclass
@@ -61,7 +62,8 @@ def init_distributed(backend: str | None = None) -> DistEnv:
 class Trainer:
     def __init__(self, model_name: str, seq_len: int, micro_batch: int, device, lr: float = 3e-4,
                  seed: int = 0, bucket_numel: int = 256 * 1024 * 1024, grad_accum: int = 1,
-                 lr_warmup: int = 0, lr_decay_steps: int = 0, min_lr_ratio: float = 0.1, data_rows: int = 4):
+                 lr_warmup: int = 0, lr_decay_steps: int = 0, min_lr_ratio: float = 0.1, data: str = "synthetic-lm",
+                 data_rows: int = 4):
         self.cfg = CONFIGS[model_name]
         # LR schedule: linear warmup over ``lr_warmup`` optimizer steps, then constant, or cosine
         # decay to ``min_lr_ratio * lr`` at step ``lr_decay_steps`` when that is set.  A random-init
@@ -84,15 +86,28 @@ class Trainer:
         self.opt = ZeroOptimizer(model, lr=lr, bucket_numel=bucket_numel)
         self.opt.install_prefetch_hooks(model)
         rank = dist.get_rank() if dist.is_initialized() else 0
-        g = torch.Generator(device=device).manual_seed(1234 + rank)
-        n = micro_batch * (seq_len + 1)
-        self.data = torch.randint(0, self.cfg.vocab_size, (data_rows, n), device=device, generator=g)
+        # data: "synthetic-lm" = a fresh structured batch every micro-step (workloads/data.py, the
+        # bench's data); "fixed" = ``data_rows`` uniform-random rows cycled (a memorisation check)
+        self.data_kind = data
+        self.stream = None
+        if data == "synthetic-lm":
+            self.stream = SyntheticLM(self.cfg.vocab_size, seq_len, micro_batch, device, seed=1234 + rank)
+        elif data == "fixed":
+            g = torch.Generator(device=device).manual_seed(1234 + rank)
+            n = micro_batch * (seq_len + 1)
+            self.data = torch.randint(0, self.cfg.vocab_size, (data_rows, n), device=device, generator=g)
+        else:
+            raise ValueError(f"unknown data kind {data!r}")
         self._i = 0
 
     def batch(self):
-        row = self.data[self._i % self.data.shape[0]].view(self.micro_batch, self.seq_len + 1)
+        if self.stream is not None:
+            out = self.stream.batch(self._i)
+        else:
+            row = self.data[self._i % self.data.shape[0]].view(self.micro_batch, self.seq_len + 1)
+            out = row[:, :-1], row[:, 1:]
         self._i += 1
-        return row[:, :-1], row[:, 1:]
+        return out
 
     def lr_at(self, step: int) -> float:
         """Learning rate of optimizer step ``step`` (1-based)."""
@@ -286,8 +301,10 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         if checkpoint_dir and save_every and tr.opt.step_count % save_every == 0:
             tr.save_checkpoint(checkpoint_dir)
 
+    warm_losses = []
     for i in range(warmup):
         loss = tr.step()
+        warm_losses.append(loss.item())
         if env.rank == 0:
             print(f"[train] warmup {i} loss={loss.item():.4f}", flush=True)
         _maybe_save()
@@ -316,6 +333,10 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     }
     result["tflops_per_gpu"] = tok_s / env.world * result["flops_per_token"] / 1e12
     result["losses"] = [round(x.item(), 4) for x in losses]  # read after the timed region
+    result["warmup_losses"] = [round(x, 4) for x in warm_losses]
+    if tr.stream is not None:
+        result["loss_floor"] = round(tr.stream.loss_floor, 4)
+        result["unigram_entropy"] = round(tr.stream.unigram_entropy, 4)
     result["gemm_tuning"] = gemm_mode
     if env.rank == 0:
         print("[train] result " + json.dumps(result), flush=True)

@@ -12,6 +12,10 @@ if ROOT not in sys.path:
 _TMP_HOME = tempfile.mkdtemp(prefix="dstack-amd-tests-")
 os.environ.setdefault("DSTACK_DIR", os.path.join(_TMP_HOME, "dstack"))
 os.environ["DSTACK_SERVER_NO_CLIENT_CONFIG"] = "1"
+# cloud backends plan from the offline catalog unless a test opts into live listings
+# (tests/test_catalog.py); the catalog cache never touches the real ~/.dstack
+os.environ["DSTACK_CATALOG_OFFLINE_ONLY"] = "1"
+os.environ["DSTACK_CATALOG_CACHE_DIR"] = os.path.join(_TMP_HOME, "catalog")
 
 ADMIN_TOKEN = "test-admin-token"
 

@@ -1,0 +1,43 @@
+"""The bench's synthetic token stream (workloads/data.py): deterministic per (seed, index), fresh
+every micro-step, the advertised chain structure and entropy floor."""
+
+import math
+
+import torch
+
+from dstack_amd.workloads.data import SyntheticLM, _A, _B
+
+
+def test_stream_is_deterministic_and_fresh():
+    s = SyntheticLM(32000, 512, 2, "cpu", seed=7)
+    a, b = s.batch(3)
+    assert a.shape == (2, 512) and b.shape == (2, 512)
+    assert torch.equal(a[:, 1:], b[:, :-1])  # targets are the inputs shifted by one
+    assert torch.equal(s.tokens(3), SyntheticLM(32000, 512, 2, "cpu", seed=7).tokens(3))
+    assert not torch.equal(s.tokens(3), s.tokens(4))
+    assert not torch.equal(s.tokens(3), SyntheticLM(32000, 512, 2, "cpu", seed=8).tokens(3))
+    x = s.tokens(0)
+    assert int(x.min()) >= 0 and int(x.max()) < 32000
+
+
+def test_chain_structure_matches_closed_form():
+    V = 128256
+    s = SyntheticLM(V, 4096, 1, "cpu", seed=1, copy_p=0.5)
+    x = s.tokens(0)[0]
+    chained = x[1:] == (_A * x[:-1] + _B) % V
+    assert 0.45 < chained.float().mean().item() < 0.55
+    # tokens that are not chained follow the Zipf head: few distinct ids, far below uniform
+    assert x.unique().numel() < 0.5 * x.numel()
+
+
+def test_loss_floor_and_row_starts():
+    s = SyntheticLM(1000, 64, 4, "cpu", seed=0, zipf_s=1.0, copy_p=0.25)
+    ranks = torch.arange(1, 1001, dtype=torch.float64)
+    q = ranks.reciprocal() / ranks.reciprocal().sum()
+    h = float(-(q * q.log()).sum())
+    assert math.isclose(s.unigram_entropy, h, rel_tol=1e-9)
+    hp = -(0.25 * math.log(0.25) + 0.75 * math.log(0.75))
+    assert math.isclose(s.loss_floor, hp + 0.75 * h, rel_tol=1e-9)
+    assert s.loss_floor < math.log(1000)
+    # every row starts from a fresh sample (no chain crosses rows)
+    assert not bool(s.row_start[1:65].any()) and bool(s.row_start[65])

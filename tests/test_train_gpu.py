@@ -26,7 +26,7 @@ def _train(gpu, ops, monkeypatch):
                                                                       n_layers=4))
     monkeypatch.setenv("DSTACK_AMD_OPS", ops)
     tr = Trainer("llama-3-8b-4l", seq_len=8192, micro_batch=1, device=gpu, lr=3e-4, lr_warmup=WARMUP,
-                 data_rows=1, bucket_numel=64 * 1024 * 1024)
+                 data="fixed", data_rows=1, bucket_numel=64 * 1024 * 1024)
     losses = [tr.step().item() for _ in range(STEPS)]
     del tr
     gc.collect()
