@@ -36,6 +36,7 @@ MIGRATIONS: List[Callable] = [
     _m0001_initial,
     # example of an additive migration kept for databases created before the column existed
     _add_column("jobs", "timings", "TEXT"),
+    _add_column("job_metrics_points", "gpus_extra", "TEXT"),
 ]
 
 

@@ -387,6 +387,8 @@ class JobMetricsPoint(Base):
     gpus_util_percent: Mapped[str] = mapped_column(Text)  # json list
     gpus_power_watts: Mapped[Optional[str]] = mapped_column(Text, nullable=True)  # json list (amdsmi)
     gpus_temperature_c: Mapped[Optional[str]] = mapped_column(Text, nullable=True)
+    # json list of per-GPU dicts: HBM controller activity and xGMI link state / accumulated KiB
+    gpus_extra: Mapped[Optional[str]] = mapped_column(Text, nullable=True)
 
 
 class SecretModel(Base):

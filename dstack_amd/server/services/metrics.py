@@ -1,5 +1,7 @@
 """Job hardware metrics (reference: ``S/services/metrics.py:13-113``): computed from the last two
-``job_metrics_points``; AMD additions: GPU power (W) and temperature (°C) from amdsmi."""
+``job_metrics_points``; AMD additions from amdsmi: GPU power (W), temperature (°C), HBM controller
+activity (%) and xGMI -- links up, and read / write throughput (bytes/s) derived from the
+accumulated per-link traffic counters of consecutive samples."""
 
 from __future__ import annotations
 
@@ -33,6 +35,10 @@ def _calculate(pts: List[JobMetricsPoint]) -> List[Metric]:
     gpus_util: List[List[float]] = []
     gpus_power: List[List[float]] = []
     gpus_temp: List[List[float]] = []
+    gpus_hbm: List[List[float]] = []
+    xgmi_rd: List[List[float]] = []
+    xgmi_wr: List[List[float]] = []
+    xgmi_up: List[List[float]] = []
     for prev, cur in zip(pts, pts[1:]):
         ts.append(_ts(cur.timestamp_micro))
         dt = max(1, cur.timestamp_micro - prev.timestamp_micro)
@@ -48,6 +54,23 @@ def _calculate(pts: List[JobMetricsPoint]) -> List[Metric]:
                 arr.append([])
             for i, v in enumerate(vals):
                 arr[i].append(float(v))
+        ex_prev = json.loads(prev.gpus_extra or "[]")
+        ex_cur = json.loads(cur.gpus_extra or "[]")
+        for i, e in enumerate(ex_cur):
+            for arr in (gpus_hbm, xgmi_rd, xgmi_wr, xgmi_up):
+                while len(arr) <= i:
+                    arr.append([])
+            if e.get("mem_activity_percent") is not None:
+                gpus_hbm[i].append(float(e["mem_activity_percent"]))
+            x = e.get("xgmi")
+            if not x:
+                continue
+            xgmi_up[i].append(float(x.get("links_up", 0)))
+            px = (ex_prev[i].get("xgmi") if i < len(ex_prev) else None) or {}
+            if px:  # counters are cumulative KiB: rate between the two samples (reset -> 0)
+                secs = dt / 1e6
+                xgmi_rd[i].append(max(0.0, (x.get("read_kb", 0) - px.get("read_kb", 0)) * 1024 / secs))
+                xgmi_wr[i].append(max(0.0, (x.get("write_kb", 0) - px.get("write_kb", 0)) * 1024 / secs))
     metrics = [
         Metric(name="cpu_usage_percent", timestamps=ts, values=cpu),
         Metric(name="memory_usage_bytes", timestamps=ts, values=mem),
@@ -62,6 +85,11 @@ def _calculate(pts: List[JobMetricsPoint]) -> List[Metric]:
         metrics.append(Metric(name=f"gpu_power_watts_gpu{i}", timestamps=ts[-len(v):], values=v))
     for i, v in enumerate(gpus_temp):
         metrics.append(Metric(name=f"gpu_temperature_c_gpu{i}", timestamps=ts[-len(v):], values=v))
+    for prefix, series in (("gpu_hbm_activity_percent", gpus_hbm), ("gpu_xgmi_links_up", xgmi_up),
+                           ("gpu_xgmi_read_bytes_per_s", xgmi_rd), ("gpu_xgmi_write_bytes_per_s", xgmi_wr)):
+        for i, v in enumerate(series):
+            if v:
+                metrics.append(Metric(name=f"{prefix}_gpu{i}", timestamps=ts[-len(v):], values=v))
     return metrics
 
 
@@ -77,6 +105,8 @@ def store_metrics_point(s: Session, job: JobModel, m: dict):
         gpus_util_percent=json.dumps([g.get("gpu_util_percent", 0) for g in gpus]),
         gpus_power_watts=json.dumps([g.get("gpu_power_watts", 0) for g in gpus]),
         gpus_temperature_c=json.dumps([g.get("gpu_temperature_c", 0) for g in gpus]),
+        gpus_extra=json.dumps([{"mem_activity_percent": g.get("gpu_mem_activity_percent"), "xgmi": g.get("xgmi")}
+                               for g in gpus]),
     ))
 
 

@@ -45,6 +45,7 @@ def render(s: Session) -> str:
 
     gauge("dstack_job_gpu_util_percent", "Latest GPU utilisation of running jobs (amdsmi)")
     util_lines, mem_lines, cpu_lines, rss_lines = [], [], [], []
+    links_lines, xrd_lines, xwr_lines = [], [], []
     for job in s.execute(select(JobModel).where(JobModel.status == "running")).scalars():
         pt = s.execute(select(JobMetricsPoint).where(JobMetricsPoint.job_id == job.id)
                        .order_by(JobMetricsPoint.timestamp_micro.desc())).scalars().first()
@@ -55,6 +56,14 @@ def render(s: Session) -> str:
             util_lines.append(f'dstack_job_gpu_util_percent{{{lbl},gpu="{i}"}} {u}')
         for i, m in enumerate(json.loads(pt.gpus_memory_usage_bytes or "[]")):
             mem_lines.append(f'dstack_job_gpu_memory_usage_bytes{{{lbl},gpu="{i}"}} {m}')
+        for i, e in enumerate(json.loads(pt.gpus_extra or "[]")):
+            x = (e or {}).get("xgmi")
+            if x:
+                links_lines.append(f'dstack_job_gpu_xgmi_links_up{{{lbl},gpu="{i}"}} {x.get("links_up", 0)}')
+                xrd_lines.append(f'dstack_job_gpu_xgmi_read_bytes_total{{{lbl},gpu="{i}"}} '
+                                 f'{int(x.get("read_kb", 0)) * 1024}')
+                xwr_lines.append(f'dstack_job_gpu_xgmi_write_bytes_total{{{lbl},gpu="{i}"}} '
+                                 f'{int(x.get("write_kb", 0)) * 1024}')
         cpu_lines.append(f"dstack_job_cpu_usage_micro{{{lbl}}} {pt.cpu_usage_micro or 0}")
         rss_lines.append(f"dstack_job_memory_working_set_bytes{{{lbl}}} {pt.memory_working_set_bytes or 0}")
     out += util_lines
@@ -64,6 +73,12 @@ def render(s: Session) -> str:
     out += cpu_lines
     gauge("dstack_job_memory_working_set_bytes", "Latest memory working set of running jobs (cgroup)")
     out += rss_lines
+    gauge("dstack_job_gpu_xgmi_links_up", "xGMI links up per GPU of running jobs (amdsmi)")
+    out += links_lines
+    out.append("# TYPE dstack_job_gpu_xgmi_read_bytes_total counter")
+    out += xrd_lines
+    out.append("# TYPE dstack_job_gpu_xgmi_write_bytes_total counter")
+    out += xwr_lines
 
     from dstack_amd.server.background.scheduler import get_scheduler
 

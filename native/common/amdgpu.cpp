@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cctype>
 #include <cstring>
+#include <limits>
 #include <regex>
 
 #include "net.h"
@@ -31,6 +32,8 @@ typedef amdsmi_status_t (*fn_power)(amdsmi_processor_handle, amdsmi_power_info_t
 typedef amdsmi_status_t (*fn_temp)(amdsmi_processor_handle, amdsmi_temperature_type_t, amdsmi_temperature_metric_t,
                                    int64_t*);
 typedef amdsmi_status_t (*fn_link)(amdsmi_processor_handle, amdsmi_processor_handle, uint64_t*, amdsmi_link_type_t*);
+typedef amdsmi_status_t (*fn_gpu_metrics)(amdsmi_processor_handle, amdsmi_gpu_metrics_t*);
+typedef amdsmi_status_t (*fn_xgmi_status)(amdsmi_processor_handle, amdsmi_xgmi_link_status_t*);
 
 struct Fns {
   fn_init init = nullptr;
@@ -45,6 +48,8 @@ struct Fns {
   fn_power power = nullptr;
   fn_temp temp = nullptr;
   fn_link link = nullptr;
+  fn_gpu_metrics gpu_metrics = nullptr;
+  fn_xgmi_status xgmi_status = nullptr;
 } F;
 
 std::string bdf_str(const amdsmi_bdf_t& b) {
@@ -100,6 +105,8 @@ AmdSmi::AmdSmi() {
   SYM(power, "amdsmi_get_power_info");
   SYM(temp, "amdsmi_get_temp_metric");
   SYM(link, "amdsmi_topo_get_link_type");
+  SYM(gpu_metrics, "amdsmi_get_gpu_metrics_info");
+  SYM(xgmi_status, "amdsmi_get_gpu_xgmi_link_status");
 #undef SYM
   if (!F.init || !F.sockets || !F.procs) return;
   if (F.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return;
@@ -187,6 +194,57 @@ std::vector<std::vector<int>> AmdSmi::xgmi_matrix() {
   return m;
 }
 
+namespace {
+// amdsmi marks fields a device does not report with all-ones
+template <class T>
+bool valid(T v) {
+  return v != std::numeric_limits<T>::max();
+}
+}  // namespace
+
+void fill_xgmi_from(const amdsmi_gpu_metrics_t* gm, const amdsmi_xgmi_link_status_t* ls, AmdGpuMetrics& m) {
+  int links = 0;
+  if (gm) {
+    if (valid(gm->xgmi_link_speed)) m.xgmi_link_speed_gbps = gm->xgmi_link_speed;
+    if (valid(gm->xgmi_link_width)) m.xgmi_link_width = gm->xgmi_link_width;
+    for (int l = 0; l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) {
+      uint64_t r = gm->xgmi_read_data_acc[l], w = gm->xgmi_write_data_acc[l];
+      if (!valid(r) && !valid(w)) continue;
+      r = valid(r) ? r : 0;
+      w = valid(w) ? w : 0;
+      m.xgmi_read_kb_link.push_back(r);
+      m.xgmi_write_kb_link.push_back(w);
+      m.xgmi_read_kb += r;
+      m.xgmi_write_kb += w;
+      links = l + 1;
+    }
+  }
+  if (ls && ls->total_links > 0) {
+    m.xgmi_links_total = (int)std::min<uint32_t>(ls->total_links, AMDSMI_MAX_NUM_XGMI_LINKS);
+    m.xgmi_links_up = 0;
+    for (int l = 0; l < m.xgmi_links_total; ++l) m.xgmi_links_up += ls->status[l] == AMDSMI_XGMI_LINK_UP;
+  } else if (gm) {
+    // older SMU firmware: link state only in gpu_metrics v1.7 (xgmi_link_status)
+    int total = 0, up = 0;
+    for (int l = 0; l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) {
+      if (!valid(gm->xgmi_link_status[l])) continue;
+      ++total;
+      up += gm->xgmi_link_status[l] == AMDSMI_XGMI_LINK_UP;
+    }
+    m.xgmi_links_total = total ? total : links;
+    m.xgmi_links_up = total ? up : 0;
+  }
+}
+
+void AmdSmi::fill_xgmi(void* h, AmdGpuMetrics& m) {
+  amdsmi_gpu_metrics_t gm;
+  memset(&gm, 0xff, sizeof gm);
+  bool have_gm = F.gpu_metrics && F.gpu_metrics(h, &gm) == AMDSMI_STATUS_SUCCESS;
+  amdsmi_xgmi_link_status_t ls{};
+  bool have_ls = F.xgmi_status && F.xgmi_status(h, &ls) == AMDSMI_STATUS_SUCCESS;
+  fill_xgmi_from(have_gm ? &gm : nullptr, have_ls ? &ls : nullptr, m);
+}
+
 std::vector<AmdGpuMetrics> AmdSmi::metrics() {
   std::vector<AmdGpuMetrics> out;
   for (size_t i = 0; i < handles_.size(); ++i) {
@@ -194,7 +252,10 @@ std::vector<AmdGpuMetrics> AmdSmi::metrics() {
     m.index = (int)i;
     auto h = handles_[i];
     amdsmi_engine_usage_t u{};
-    if (F.activity && F.activity(h, &u) == AMDSMI_STATUS_SUCCESS) m.util_percent = u.gfx_activity;
+    if (F.activity && F.activity(h, &u) == AMDSMI_STATUS_SUCCESS) {
+      m.util_percent = u.gfx_activity;
+      if (u.umc_activity != UINT32_MAX) m.mem_activity_percent = u.umc_activity;
+    }
     amdsmi_vram_usage_t vu{};
     if (F.vramusage && F.vramusage(h, &vu) == AMDSMI_STATUS_SUCCESS) {
       m.vram_used_bytes = (uint64_t)vu.vram_used << 20;
@@ -208,6 +269,7 @@ std::vector<AmdGpuMetrics> AmdSmi::metrics() {
     int64_t t = 0;
     if (F.temp && F.temp(h, AMDSMI_TEMPERATURE_TYPE_HOTSPOT, AMDSMI_TEMP_CURRENT, &t) == AMDSMI_STATUS_SUCCESS)
       m.temp_c = (double)t;
+    fill_xgmi(h, m);
     out.push_back(m);
   }
   return out;

@@ -5,6 +5,8 @@
 // Replaces the reference's `docker run amd-smi static --json` + CSV parsing
 // (runner/internal/shim/host/gpu.go:149-196, runner/internal/metrics/metrics.go:172-203).
 #pragma once
+#include <amd_smi/amdsmi.h>
+
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -29,10 +31,20 @@ struct AmdGpu {
 struct AmdGpuMetrics {
   int index = 0;
   double util_percent = 0;
+  double mem_activity_percent = -1;  // UMC (HBM controller) activity, -1 when not reported
   uint64_t vram_used_bytes = 0;
   uint64_t vram_total_bytes = 0;
   double power_w = 0;
   double temp_c = 0;
+  // xGMI (amdsmi gpu_metrics): per-link accumulated traffic (KiB since driver load) and link
+  // state; the server turns two samples into per-GPU xGMI read / write throughput
+  int xgmi_links_total = 0;  // links reported by the device (0: no xGMI data)
+  int xgmi_links_up = 0;
+  int xgmi_link_speed_gbps = 0;  // per-link bitrate (GB/s) as reported by the SMU
+  int xgmi_link_width = 0;
+  uint64_t xgmi_read_kb = 0;  // sum over links
+  uint64_t xgmi_write_kb = 0;
+  std::vector<uint64_t> xgmi_read_kb_link, xgmi_write_kb_link;
 };
 
 class AmdSmi {
@@ -46,6 +58,7 @@ class AmdSmi {
 
  private:
   AmdSmi();
+  void fill_xgmi(void* handle, AmdGpuMetrics& m);
   bool ok_ = false;
   void* lib_ = nullptr;
   std::vector<void*> handles_;
@@ -59,6 +72,10 @@ std::vector<AmdGpu> discover_amd_gpus_sysfs();
 std::vector<AmdGpu> discover_amd_gpus();
 
 Json gpu_to_json(const AmdGpu& g);
+
+// xGMI fields of AmdGpuMetrics from amdsmi gpu_metrics / link status (either may be null;
+// all-ones fields are "not reported")
+void fill_xgmi_from(const amdsmi_gpu_metrics_t* gm, const amdsmi_xgmi_link_status_t* ls, AmdGpuMetrics& m);
 
 // choose `count` GPUs out of `free_idx` maximising xGMI connectivity (fully connected first),
 // preferring one NUMA node; returns empty if impossible

@@ -1,5 +1,6 @@
 // dstack-runner executor implementation (see executor.h).
 #include "executor.h"
+#include "rocprof.h"
 
 #include <arpa/inet.h>
 #include <dirent.h>
@@ -523,15 +524,26 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
     return -1;
   }
   auto env = build_env();
-  // DSTACK_ROCPROF=1: wrap the job in rocprofv3 kernel-trace statistics; the summary is appended
-  // to the job log when the job ends (rocprof counters surfaced in run logs)
-  std::string rocprof_dir;
-  for (auto& kv : env)
-    if (kv.first == "DSTACK_ROCPROF" && (kv.second == "1" || kv.second == "true")) rocprof_dir = opts_.temp_dir + "/rocprof";
-  if (!rocprof_dir.empty()) {
+  // DSTACK_ROCPROF=1: wrap the job in rocprofv3 kernel-trace statistics, plus the hardware
+  // counters of DSTACK_ROCPROF_COUNTERS (validated against the one-pass budget, runner/rocprof.h);
+  // the summaries are appended to the job log when the job ends (rocprof counters in run logs)
+  std::string rocprof_dir, counters_spec;
+  bool want_rocprof = false;
+  for (auto& kv : env) {
+    if (kv.first == "DSTACK_ROCPROF" && (kv.second == "1" || kv.second == "true")) want_rocprof = true;
+    if (kv.first == "DSTACK_ROCPROF_COUNTERS") counters_spec = kv.second;
+  }
+  std::vector<std::string> counters = split_counters(counters_spec);
+  if (!counters.empty()) want_rocprof = true;
+  if (want_rocprof) {
+    rocprof_dir = opts_.temp_dir + "/rocprof";
     mkdirs(rocprof_dir);
-    std::vector<std::string> wrapped = {"rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv",
-                                        "-d", rocprof_dir, "-o", "job", "--"};
+    std::string perr;
+    if (!counters.empty() && !validate_pmc(counters, perr)) {
+      job_logs_.append("[dstack] DSTACK_ROCPROF_COUNTERS ignored: " + perr + "\n");
+      counters.clear();
+    }
+    std::vector<std::string> wrapped = rocprof_argv(rocprof_dir, counters);
     wrapped.insert(wrapped.end(), argv.begin(), argv.end());
     argv = wrapped;
   }
@@ -680,27 +692,21 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
   child_pgid_ = 0;
   int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
   if (!rocprof_dir.empty()) {
-    // surface the kernel statistics in the job log
+    // surface the kernel statistics (and counters) in the job log
     DIR* d = opendir(rocprof_dir.c_str());
-    std::string stats_path;
+    std::string stats_path, counters_path;
     if (d) {
       while (auto* e = readdir(d)) {
         std::string n = e->d_name;
         if (n.find("kernel_stats.csv") != std::string::npos) stats_path = rocprof_dir + "/" + n;
+        if (n.find("counter_collection.csv") != std::string::npos) counters_path = rocprof_dir + "/" + n;
       }
       closedir(d);
     }
     std::string csv;
-    if (!stats_path.empty() && read_file(stats_path, csv)) {
-      std::istringstream ss(csv);
-      std::string line, out = "\n[dstack] rocprofv3 kernel statistics (top 15):\n";
-      int k = 0;
-      while (std::getline(ss, line) && k < 16) {
-        out += "  " + line.substr(0, 240) + "\n";
-        ++k;
-      }
-      job_logs_.append(out);
-    }
+    if (!stats_path.empty() && read_file(stats_path, csv)) job_logs_.append(summarize_kernel_stats(csv, 15));
+    if (!counters_path.empty() && read_file(counters_path, csv))
+      job_logs_.append(summarize_counters(csv, counters, 15));
   }
   if (timed_out) {
     reason = "max_duration_exceeded";

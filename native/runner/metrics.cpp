@@ -1,4 +1,5 @@
-// Runner hardware metrics: cgroup v2/v1 CPU and memory + amdsmi GPU util/VRAM/power/temp.
+// Runner hardware metrics: cgroup v2/v1 CPU and memory + amdsmi GPU util/VRAM/power/temp, HBM
+// controller activity and xGMI link state / accumulated traffic.
 // Reference: runner/internal/metrics/metrics.go:21-256 (nvidia-smi / amd-smi CSV / hl-smi).
 #include <stdlib.h>
 
@@ -60,6 +61,17 @@ Json collect_metrics(const std::vector<int>& gpu_filter) {
       j.set("gpu_util_percent", g.util_percent);
       j.set("gpu_power_watts", g.power_w);
       j.set("gpu_temperature_c", g.temp_c);
+      if (g.mem_activity_percent >= 0) j.set("gpu_mem_activity_percent", g.mem_activity_percent);
+      if (g.xgmi_links_total > 0 || g.xgmi_read_kb || g.xgmi_write_kb) {
+        Json x = Json::object();
+        x.set("links_total", g.xgmi_links_total);
+        x.set("links_up", g.xgmi_links_up);
+        x.set("link_speed_gbps", g.xgmi_link_speed_gbps);
+        x.set("link_width", g.xgmi_link_width);
+        x.set("read_kb", (long long)g.xgmi_read_kb);
+        x.set("write_kb", (long long)g.xgmi_write_kb);
+        j.set("xgmi", x);
+      }
       gpus.push_back(j);
     }
   }

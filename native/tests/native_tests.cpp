@@ -22,6 +22,7 @@
 
 #include "../probes/bootstrap.h"
 #include "../runner/executor.h"
+#include "../runner/rocprof.h"
 #include "../shim/shim.h"
 
 using namespace dsa;
@@ -79,6 +80,67 @@ static void run(const char* name, const std::function<void()>& fn) {
 
 int main() {
   set_log_level(0);
+
+  run("xgmi metrics from amdsmi structs", [] {
+    // all-ones = "not reported" (amdsmi's convention); links 0-3 report traffic, 2 is down
+    amdsmi_gpu_metrics_t gm;
+    memset(&gm, 0xff, sizeof gm);
+    gm.xgmi_link_speed = 32;
+    gm.xgmi_link_width = 16;
+    for (int l = 0; l < 4; ++l) {
+      gm.xgmi_read_data_acc[l] = 1000u * (l + 1);
+      gm.xgmi_write_data_acc[l] = 10u * (l + 1);
+    }
+    amdsmi_xgmi_link_status_t ls{};
+    ls.total_links = 4;
+    for (int l = 0; l < 4; ++l) ls.status[l] = l == 2 ? AMDSMI_XGMI_LINK_DOWN : AMDSMI_XGMI_LINK_UP;
+    AmdGpuMetrics m;
+    fill_xgmi_from(&gm, &ls, m);
+    CHECK(m.xgmi_read_kb == 10000 && m.xgmi_write_kb == 100);
+    CHECK(m.xgmi_read_kb_link.size() == 4 && m.xgmi_read_kb_link[3] == 4000);
+    CHECK(m.xgmi_links_total == 4 && m.xgmi_links_up == 3);
+    CHECK(m.xgmi_link_speed_gbps == 32 && m.xgmi_link_width == 16);
+    // no link-status API: fall back to gpu_metrics' per-link status words
+    for (int l = 0; l < 4; ++l) gm.xgmi_link_status[l] = l == 0 ? AMDSMI_XGMI_LINK_DOWN : AMDSMI_XGMI_LINK_UP;
+    AmdGpuMetrics m2;
+    fill_xgmi_from(&gm, nullptr, m2);
+    CHECK(m2.xgmi_links_total == 4 && m2.xgmi_links_up == 3);
+    // a device without xGMI reports nothing
+    memset(&gm, 0xff, sizeof gm);
+    AmdGpuMetrics m3;
+    fill_xgmi_from(&gm, nullptr, m3);
+    CHECK(m3.xgmi_links_total == 0 && m3.xgmi_read_kb == 0 && m3.xgmi_link_speed_gbps == 0);
+  });
+
+  run("rocprof: one-pass counter budget, argv, csv summaries", [] {
+    std::string err;
+    CHECK(split_counters("SQ_WAVES, TCC_HIT_sum  GRBM_GUI_ACTIVE").size() == 3);
+    CHECK(validate_pmc({"SQ_WAVES", "SQ_INSTS_VALU", "TCC_HIT_sum", "TCC_MISS_sum", "GRBM_GUI_ACTIVE"}, err));
+    CHECK(validate_pmc({"FETCH_SIZE", "TCC_HIT_sum"}, err));  // 3 + 1 TCC
+    CHECK(!validate_pmc({"FETCH_SIZE", "WRITE_SIZE"}, err) && err.find("TCC block needs 5") == 0);
+    CHECK(validate_pmc({"TCC_HIT_sum", "TCC_HIT_avr", "TCC_HIT_max"}, err));  // one counter
+    std::vector<std::string> nine;
+    for (int i = 0; i < 9; ++i) nine.push_back("SQ_C" + std::to_string(i));
+    CHECK(!validate_pmc(nine, err) && err.find("SQ block needs 9") == 0);
+    CHECK(!validate_pmc({"GRBM_A", "GRBM_B", "GRBM_C"}, err));
+    CHECK(!validate_pmc({"MemUnitBusy"}, err));       // derived metric of unknown cost
+    CHECK(!validate_pmc({"SQ_WAVES;rm -rf"}, err));   // names only
+    CHECK(!validate_pmc({}, err));
+    auto a = rocprof_argv("/tmp/p", {"SQ_WAVES"});
+    CHECK(a[0] == "rocprofv3" && a[3] == "--pmc" && a[4] == "SQ_WAVES" && a.back() == "--");
+    CHECK(rocprof_argv("/tmp/p", {})[3] == "--output-format");
+    auto r = parse_csv_record("1,\"k(float*, int)\",\"say \"\"hi\"\"\",3\r");
+    CHECK(r.size() == 4 && r[1] == "k(float*, int)" && r[2] == "say \"hi\"" && r[3] == "3");
+    std::string csv =
+        "Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n"
+        "1,\"a(int)\",SQ_WAVES,10\n2,\"a(int)\",SQ_WAVES,10\n1,\"a(int)\",TCC_HIT_sum,5\n"
+        "3,\"b(int)\",SQ_WAVES,50\n";
+    std::string s = summarize_counters(csv, {"SQ_WAVES", "TCC_HIT_sum"}, 10);
+    CHECK(s.find("b | 1 | 50 | 0") != std::string::npos);
+    CHECK(s.find("a | 2 | 20 | 5") != std::string::npos);
+    CHECK(s.find("b | 1") < s.find("a | 2"));  // ordered by the first counter
+    CHECK(summarize_counters("x,y\n1,2\n", {}, 5).empty());
+  });
 
   run("json roundtrip", [] {
     Json j = Json::parse(R"({"a":1,"b":[true,null,"x\né"],"c":{"d":-2.5e3}})");

@@ -72,6 +72,54 @@ def test_env_and_secrets_interpolation(client, server):
     assert "A=1 S=s3cr3t-value" in _logs(run)
 
 
+_FAKE_ROCPROF = r"""#!/bin/sh
+# stands in for rocprofv3: records the --pmc set, writes the two CSVs the runner summarises, runs
+# the job command
+dir=""; pmc=""
+while [ $# -gt 0 ]; do
+  case "$1" in
+    -d) dir="$2"; shift 2;;
+    --pmc) shift; while [ $# -gt 0 ] && [ "${1#-}" = "$1" ]; do pmc="$pmc $1"; shift; done;;
+    --) shift; break;;
+    *) shift;;
+  esac
+done
+echo "fake-rocprof pmc:$pmc"
+printf '"Name","Calls","TotalDurationNs"\n"gemm_kernel(float*, int)",10,5000\n' > "$dir/job_kernel_stats.csv"
+printf 'Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n1,"gemm_kernel(float*, int)",SQ_WAVES,64\n2,"gemm_kernel(float*, int)",SQ_WAVES,64\n1,"gemm_kernel(float*, int)",GRBM_GUI_ACTIVE,1000\n3,"norm(float*)",SQ_WAVES,8\n' > "$dir/job_counter_collection.csv"
+"$@"
+"""
+
+
+def test_rocprof_counters_in_job_log(client, tmp_path):
+    """DSTACK_ROCPROF_COUNTERS: the runner checks the set against rocprofv3's one-pass budget, adds
+    ``--pmc`` and appends per-kernel counter sums to the job log; an over-budget set is refused
+    with a log line and the job still runs (kernel statistics only)."""
+    from dstack_amd.api import Task
+
+    bin_dir = tmp_path / "bin"
+    bin_dir.mkdir()
+    fake = bin_dir / "rocprofv3"
+    fake.write_text(_FAKE_ROCPROF)
+    fake.chmod(0o755)
+    path = f"{bin_dir}:{os.environ.get('PATH', '/usr/bin:/bin')}"
+    run = client.runs.submit(Task(commands=["echo job-ran"], name="e2e-rocprof",
+                                  env={"PATH": path, "DSTACK_ROCPROF_COUNTERS": "SQ_WAVES,GRBM_GUI_ACTIVE"}))
+    assert run.wait(timeout=60).value == "done"
+    out = _logs(run)
+    assert "fake-rocprof pmc: SQ_WAVES GRBM_GUI_ACTIVE" in out and "job-ran" in out
+    assert "rocprofv3 kernel statistics" in out and "gemm_kernel(float*, int)" in out
+    assert "rocprofv3 counters per kernel" in out
+    assert "gemm_kernel | 2 | 128 | 1000" in out and "norm | 1 | 8 | 0" in out
+    too_many = ",".join(f"SQ_C{i}" for i in range(9))
+    run = client.runs.submit(Task(commands=["echo job-ran"], name="e2e-rocprof-bad",
+                                  env={"PATH": path, "DSTACK_ROCPROF_COUNTERS": too_many}))
+    assert run.wait(timeout=60).value == "done"
+    out = _logs(run)
+    assert "DSTACK_ROCPROF_COUNTERS ignored: SQ block needs 9 counters" in out
+    assert "fake-rocprof pmc:\n" in out.replace("\r", "") and "job-ran" in out
+
+
 def test_stop_long_running(client):
     from dstack_amd.api import Task
 

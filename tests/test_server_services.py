@@ -142,6 +142,35 @@ def test_job_metrics_from_last_points(db):
     assert by_name["gpu_power_watts_gpu1"] == [1000.0]
 
 
+def test_xgmi_and_hbm_metrics(db):
+    """amdsmi xGMI counters are cumulative KiB per GPU: the server reports the rate between two
+    samples, links up, and the HBM controller activity; Prometheus exposes the raw counters."""
+    from dstack_amd.server.services import metrics, prometheus
+
+    def pt(ts, read_kb, write_kb, up):
+        p = _point(ts, 0, [50])
+        p["gpus"][0]["gpu_mem_activity_percent"] = 71
+        p["gpus"][0]["xgmi"] = {"links_total": 7, "links_up": up, "link_speed_gbps": 32, "link_width": 16,
+                                "read_kb": read_kb, "write_kb": write_kb}
+        return p
+
+    with session_scope() as s:
+        job = _job(s)
+        metrics.store_metrics_point(s, job, pt(100, 1_000, 0, 7))
+        metrics.store_metrics_point(s, job, pt(102, 1_000 + 2 * 1024 * 1024, 512, 6))
+        s.flush()
+        by_name = {m.name: m.values for m in metrics.get_job_metrics(s, job).metrics}
+        job.status = "running"
+        s.flush()
+        text = prometheus.render(s)
+    assert by_name["gpu_xgmi_read_bytes_per_s_gpu0"] == [pytest.approx(1024 ** 3)]  # 2 GiB in 2 s
+    assert by_name["gpu_xgmi_write_bytes_per_s_gpu0"] == [pytest.approx(512 * 1024 / 2)]
+    assert by_name["gpu_xgmi_links_up_gpu0"] == [6.0]
+    assert by_name["gpu_hbm_activity_percent_gpu0"] == [71.0]
+    assert 'dstack_job_gpu_xgmi_links_up{run="m1"' in text
+    assert f"dstack_job_gpu_xgmi_read_bytes_total" in text and str((1_000 + 2 * 1024 * 1024) * 1024) in text
+
+
 def test_metrics_ttl_cleanup(db):
     from dstack_amd.server.services import metrics
 
