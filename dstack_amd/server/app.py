@@ -140,7 +140,7 @@ def register_routes(app: FastAPI):
               core.project_backends_router, core.secrets_router, core.repos_router, runs.runs_root,
               runs.runs_router, runs.fleets_root, runs.fleets_router, runs.instances_root, runs.volumes_root,
               runs.volumes_router, runs.gateways_router, runs.logs_router, runs.metrics_router, runs.pools_root,
-              runs.pool_router, proxy.router):
+              runs.pool_router, runs.configs_router, proxy.router):
         app.include_router(r)
 
     @app.exception_handler(UnauthorizedError)

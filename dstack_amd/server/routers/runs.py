@@ -41,6 +41,27 @@ logs_router = APIRouter(prefix="/api/project/{project_name}/logs", tags=["logs"]
 metrics_router = APIRouter(prefix="/api/project/{project_name}/metrics", tags=["metrics"])
 pools_root = APIRouter(prefix="/api/pools", tags=["pools"])
 pool_router = APIRouter(prefix="/api/project/{project_name}/pool", tags=["pools"])
+configs_router = APIRouter(prefix="/api/project/{project_name}/configurations", tags=["configurations"])
+
+
+# ---- configurations ---------------------------------------------------------------------------
+@configs_router.post("/parse")
+def parse_configuration(body: dict, up: UP = Depends(project_member)) -> dict:
+    """YAML text of a run / fleet / volume / gateway configuration -> its validated JSON form (the
+    web UI's ``apply`` page has no YAML parser of its own)."""
+    import yaml
+
+    from dstack_amd.core.models.configurations import parse_apply_configuration
+
+    try:
+        data = yaml.safe_load(body.get("yaml") or "")
+    except yaml.YAMLError as e:
+        raise ServerClientError(f"invalid YAML: {e}")
+    try:
+        conf = parse_apply_configuration(data)
+    except Exception as e:  # noqa: BLE001 -- validation errors go back to the form
+        raise ServerClientError(str(e))
+    return {"type": conf.type, "configuration": conf.model_dump(mode="json", exclude_none=True)}
 
 
 # ---- runs -----------------------------------------------------------------------------------

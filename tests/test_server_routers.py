@@ -235,6 +235,47 @@ def test_web_ui_served(client):
         assert needle in r.text, needle
 
 
+def test_web_ui_apply_and_offers_request_shapes(client):
+    """The UI's apply / offers / fleet pages: YAML -> configurations/parse -> get_plan -> apply with
+    exactly the payloads index.html builds."""
+    html = client.get("/").text
+    for needle in ("configurations/parse", "runs/get_plan", "runs/apply", "fleets/get_plan", "fleets/get",
+                   "spot_policy", "bytes_per_s"):
+        assert needle in html, needle
+    P = "/api/project/main"
+    r = client.post(f"{P}/configurations/parse", json={"yaml": "type: task\nname: ui-run\ncommands: [echo hi]\n"})
+    assert r.status_code == 200, r.text
+    conf = r.json()["configuration"]
+    assert r.json()["type"] == "task" and conf["commands"] == ["echo hi"]
+    run_spec = {"run_name": conf.get("name"), "repo_id": "ui", "repo_data": {"repo_type": "virtual"},
+                "configuration": conf, "ssh_key_pub": ""}
+    plan = client.post(f"{P}/runs/get_plan", json={"run_spec": run_spec, "max_offers": 50})
+    assert plan.status_code == 200, plan.text
+    plan = plan.json()
+    assert plan["job_plans"] and "total_offers" in plan["job_plans"][0]
+    r = client.post(f"{P}/runs/apply", json={"plan": {"run_spec": plan["run_spec"],
+                                                       "current_resource": plan["current_resource"]}, "force": False})
+    assert r.status_code == 200, r.text
+    assert r.json()["run_spec"]["run_name"] == "ui-run"
+    # offers page: a task with gpu / spot policy / max price
+    offers_conf = {"type": "task", "commands": [":"], "spot_policy": "auto", "resources": {"gpu": "MI355X:8"},
+                   "max_price": 100}
+    r = client.post(f"{P}/runs/get_plan", json={"run_spec": {"repo_id": "ui", "repo_data": {"repo_type": "virtual"},
+                                                             "configuration": offers_conf, "ssh_key_pub": ""},
+                                                "max_offers": 200})
+    assert r.status_code == 200, r.text
+    # fleet plan from parsed YAML
+    r = client.post(f"{P}/configurations/parse", json={"yaml": "type: fleet\nname: f1\nnodes: 1\n"})
+    assert r.status_code == 200, r.text
+    r = client.post(f"{P}/fleets/get_plan", json={"spec": {"configuration": r.json()["configuration"]}})
+    assert r.status_code == 200, r.text and "offers" in r.json()
+    # bad YAML / bad configuration -> 400 with the reason
+    r = client.post(f"{P}/configurations/parse", json={"yaml": "type: task\n  bad: [\n"})
+    assert r.status_code == 400 and "invalid YAML" in r.json()["detail"][0]["msg"]
+    r = client.post(f"{P}/configurations/parse", json={"yaml": "type: nonsense\n"})
+    assert r.status_code == 400
+
+
 def test_prometheus_metrics(client):
     _init_virtual_repo(client)
     client.post("/api/project/main/runs/submit", json=_task("prom1"))
