@@ -23,6 +23,8 @@ Design (MI355X-first, not a DDP translation):
 
 from __future__ import annotations
 
+import math
+
 from dataclasses import dataclass, field
 
 import torch
@@ -63,9 +65,16 @@ class ZeroOptimizer:
         overlap: bool = True,
         overlap_update: bool = True,
         force_collectives: bool | None = None,
+        clip_grad_norm: float = 0.0,
     ):
         self.model = model
         self.lr = lr
+        # global gradient-norm clipping (0 = off).  The norm of the whole (averaged) gradient is
+        # known only after backward, so with clipping AdamW runs in step() over every bucket --
+        # the reduce-scatters still overlap backward and the all-gathers the next forward; only
+        # the AdamW update itself leaves the backward's shadow.
+        self.clip_grad_norm = float(clip_grad_norm)
+        self.last_grad_norm: float | None = None
         self.beta1, self.beta2 = betas
         self.eps = eps
         self.weight_decay = weight_decay
@@ -219,17 +228,27 @@ class ZeroOptimizer:
         if b.pending == 0:
             if self.overlap:
                 self._reduce_bucket(b, async_op=True)
-            if self._side is not None:
+            if self._side is not None and not self.clip_grad_norm:
                 self._update_bucket_async(b)
 
-    def _adamw(self, b: Bucket, step: int, max_blocks: int = 0):
+    def _adamw(self, b: Bucket, step: int, max_blocks: int = 0, clip_scale: float = 1.0):
         s, n = b.shard_range(self.rank, self.world)
         i = b.index
         ops.adamw_(self.flat_param[s : s + n], self.flat_grad[s : s + n], self.master[i], self.exp_avg[i],
                    self.exp_avg_sq[i], lr=self.lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
                    weight_decay=self.weight_decay, step=step,
-                   grad_scale=1.0 / self.world,  # the 1/world of the average is fused into AdamW
-                   max_blocks=max_blocks)
+                   # the 1/world of the average (and the clip factor) are fused into AdamW
+                   grad_scale=clip_scale / self.world, max_blocks=max_blocks)
+
+    def _grad_norm(self, buckets) -> float:
+        """L2 norm of the averaged gradient: each rank's reduced shards, summed over ranks."""
+        sq = torch.zeros((), dtype=torch.float32, device=self.flat_grad.device)
+        for b in buckets:
+            s, n = b.shard_range(self.rank, self.world)
+            sq += torch.linalg.vector_norm(self.flat_grad[s : s + n], dtype=torch.float32).square()
+        if self.collectives:
+            dist.all_reduce(sq, group=self.group)
+        return float(sq.sqrt().item()) / self.world
 
     def _all_gather(self, b: Bucket):
         s, n = b.shard_range(self.rank, self.world)
@@ -320,8 +339,14 @@ class ZeroOptimizer:
                 else:
                     b.work.wait()
                     b.work = None
+        clip_scale = 1.0
+        if self.clip_grad_norm:
+            norm = self._grad_norm(self.buckets)
+            self.last_grad_norm = norm
+            if math.isfinite(norm) and norm > self.clip_grad_norm:
+                clip_scale = self.clip_grad_norm / (norm + 1e-6)
         for b in pending:
-            self._adamw(b, self.step_count)
+            self._adamw(b, self.step_count, clip_scale=clip_scale)
         if self.collectives:
             # gather the updated shards in forward order (buckets are stored in backward order);
             # with prefetch hooks installed the next forward waits per bucket, so the all-gather

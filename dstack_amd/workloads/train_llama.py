@@ -63,7 +63,7 @@ class Trainer:
     def __init__(self, model_name: str, seq_len: int, micro_batch: int, device, lr: float = 3e-4,
                  seed: int = 0, bucket_numel: int = 256 * 1024 * 1024, grad_accum: int = 1,
                  lr_warmup: int = 0, lr_decay_steps: int = 0, min_lr_ratio: float = 0.1, data: str = "synthetic-lm",
-                 data_rows: int = 4):
+                 data_rows: int = 4, clip_grad_norm: float = 0.0):
         self.cfg = CONFIGS[model_name]
         # LR schedule: linear warmup over ``lr_warmup`` optimizer steps, then constant, or cosine
         # decay to ``min_lr_ratio * lr`` at step ``lr_decay_steps`` when that is set.  A random-init
@@ -83,7 +83,7 @@ class Trainer:
         model.to(dtype)
         model.init_weights(seed=seed)
         self.model = model
-        self.opt = ZeroOptimizer(model, lr=lr, bucket_numel=bucket_numel)
+        self.opt = ZeroOptimizer(model, lr=lr, bucket_numel=bucket_numel, clip_grad_norm=clip_grad_norm)
         self.opt.install_prefetch_hooks(model)
         rank = dist.get_rank() if dist.is_initialized() else 0
         # data: "synthetic-lm" = a fresh structured batch every micro-step (workloads/data.py, the
@@ -272,7 +272,7 @@ def _sync(env: DistEnv):
 
 def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1,
         grad_accum: int = 1, checkpoint_dir: str | None = None, save_every: int = 0, lr: float = 3e-4,
-        lr_warmup: int = 10, lr_decay_steps: int = 0):
+        lr_warmup: int = 10, lr_decay_steps: int = 0, clip_grad_norm: float = 0.0):
     env = init_distributed()
     device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     from dstack_amd.ops import gemm_tuning
@@ -280,7 +280,7 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     gemm_mode = gemm_tuning.setup(device_index=env.local_rank if device.type == "cuda" else 0)
     t0 = time.time()
     tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum, lr=lr, lr_warmup=lr_warmup,
-                 lr_decay_steps=lr_decay_steps)
+                 lr_decay_steps=lr_decay_steps, clip_grad_norm=clip_grad_norm)
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
               f"init={time.time()-t0:.1f}s gemm_tuning={gemm_mode}", flush=True)
@@ -359,10 +359,12 @@ def main(argv=None):
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--lr-warmup", type=int, default=10, help="linear LR warmup (optimizer steps)")
     ap.add_argument("--lr-decay-steps", type=int, default=0, help="cosine decay to 0.1*lr at this step (0: constant)")
+    ap.add_argument("--clip-grad-norm", type=float, default=0.0, help="global gradient-norm clipping (0: off)")
     args = ap.parse_args(argv)
     env, tr, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup,
                      grad_accum=args.grad_accum, checkpoint_dir=args.checkpoint_dir, save_every=args.save_every,
-                     lr=args.lr, lr_warmup=args.lr_warmup, lr_decay_steps=args.lr_decay_steps)
+                     lr=args.lr, lr_warmup=args.lr_warmup, lr_decay_steps=args.lr_decay_steps,
+                     clip_grad_norm=args.clip_grad_norm)
     if args.checkpoint_dir and not (args.save_every and tr.opt.step_count % args.save_every == 0):
         tr.save_checkpoint(args.checkpoint_dir)  # (a step that is a multiple of save_every is saved)
     if env.distributed:

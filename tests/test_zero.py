@@ -36,8 +36,9 @@ def _batches(n, per, seed=1):
     return [torch.randint(0, CFG.vocab_size, (per, SEQ + 1), generator=g) for _ in range(n)]
 
 
-def _reference_steps(model, steps_batches, grad_accum):
-    """Plain autograd (ops.linear without a sink) + reference AdamW over full parameters."""
+def _reference_steps(model, steps_batches, grad_accum, clip=0.0, norms=None):
+    """Plain autograd (ops.linear without a sink) + reference AdamW over full parameters (with
+    ``clip``: torch's global-norm clipping first)."""
     params = list(model.parameters())
     master = [p.detach().clone().float() for p in params]
     m = [torch.zeros_like(x) for x in master]
@@ -48,6 +49,10 @@ def _reference_steps(model, steps_batches, grad_accum):
         for b in micro:
             loss = model.loss(b[:, :-1], b[:, 1:])
             (loss / grad_accum).backward()
+        if clip:
+            n = torch.nn.utils.clip_grad_norm_(params, clip)
+            if norms is not None:
+                norms.append(float(n))
         with torch.no_grad():
             for i, p in enumerate(params):
                 ref.adamw_(p.data.view(-1), p.grad.reshape(-1), master[i].view(-1), m[i].view(-1), v[i].view(-1),
@@ -55,8 +60,10 @@ def _reference_steps(model, steps_batches, grad_accum):
     return model
 
 
-def _zero_steps(model, steps_batches, grad_accum, bucket_numel=1 << 20, eps=EPS, prefetch=False):
-    opt = ZeroOptimizer(model, lr=LR, betas=BETAS, eps=eps, weight_decay=WD, bucket_numel=bucket_numel)
+def _zero_steps(model, steps_batches, grad_accum, bucket_numel=1 << 20, eps=EPS, prefetch=False, clip=0.0,
+                norms=None):
+    opt = ZeroOptimizer(model, lr=LR, betas=BETAS, eps=eps, weight_decay=WD, bucket_numel=bucket_numel,
+                        clip_grad_norm=clip)
     if prefetch:
         opt.install_prefetch_hooks(model)
     for micro in steps_batches:
@@ -66,6 +73,8 @@ def _zero_steps(model, steps_batches, grad_accum, bucket_numel=1 << 20, eps=EPS,
             loss = model.loss(b[:, :-1], b[:, 1:])
             (loss / grad_accum).backward()
         opt.step()
+        if norms is not None:
+            norms.append(opt.last_grad_norm)
     opt.wait_params()  # prefetch mode leaves the last all-gather in flight for the next forward
     return model, opt
 
@@ -85,13 +94,29 @@ def test_zero_single_process_matches_reference():
     assert all(hasattr(p, "_dsa_grad_sink") for p in zero_model.parameters() if p.dim() == 2)
 
 
+def test_zero_grad_norm_clipping_matches_torch():
+    """clip_grad_norm: the norm of the accumulated gradient (computed from the reduced shards) and
+    the clipped AdamW step equal torch.nn.utils.clip_grad_norm_ + reference AdamW."""
+    base = _model()
+    steps = [_batches(2, 2, seed=s) for s in range(3)]
+    ref_norms, zero_norms = [], []
+    ref_model = _reference_steps(copy.deepcopy(base), steps, grad_accum=2, clip=0.5, norms=ref_norms)
+    zero_model, opt = _zero_steps(copy.deepcopy(base), steps, grad_accum=2, clip=0.5, norms=zero_norms)
+    assert all(n > 0.5 for n in ref_norms)  # clipping is active on every step
+    for a, b in zip(ref_norms, zero_norms):
+        assert abs(a - b) <= 1e-4 * a, (ref_norms, zero_norms)
+    assert _max_diff(ref_model, zero_model) < 2e-5
+    unclipped, _ = _zero_steps(copy.deepcopy(base), steps, grad_accum=2)
+    assert _max_diff(unclipped, zero_model) > 1e-4  # and it changed the trajectory
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, prefetch=False, bucket_numel=1 << 19):
+def _worker(rank, world, port, out_dir, prefetch=False, bucket_numel=1 << 19, clip=0.0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(max(1, 8 // world))
@@ -99,7 +124,8 @@ def _worker(rank, world, port, out_dir, prefetch=False, bucket_numel=1 << 19):
     steps = [_batches(2, 2 * world, seed=s) for s in range(2)]
     # each rank takes its slice of every micro-batch
     mine = [[b[rank * 2:(rank + 1) * 2] for b in micro] for micro in steps]
-    model, _ = _zero_steps(base, mine, grad_accum=2, bucket_numel=bucket_numel, eps=EPS_DIST, prefetch=prefetch)
+    model, _ = _zero_steps(base, mine, grad_accum=2, bucket_numel=bucket_numel, eps=EPS_DIST, prefetch=prefetch,
+                           clip=clip)
     torch.save({k: v.detach() for k, v in model.state_dict().items()}, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.destroy_process_group()
 
@@ -117,6 +143,19 @@ def test_zero_gloo_world2_matches_single_process(tmp_path, prefetch):
     base = _model()
     steps = [_batches(2, 2 * world, seed=s) for s in range(2)]
     single, _ = _zero_steps(base, steps, grad_accum=2, eps=EPS_DIST)
+    for k, v in single.state_dict().items():
+        assert (states[0][k] - v).abs().max().item() < 2e-6, k
+
+
+def test_zero_gloo_world2_clipping_matches_single_process(tmp_path):
+    """The clip norm is all-reduced over ranks' shards: 2 ranks clip exactly like one process."""
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), True, 1 << 19, 0.5), nprocs=world,
+                       start_method="spawn")
+    states = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    base = _model()
+    steps = [_batches(2, 2 * world, seed=s) for s in range(2)]
+    single, _ = _zero_steps(base, steps, grad_accum=2, eps=EPS_DIST, clip=0.5)
     for k, v in single.state_dict().items():
         assert (states[0][k] - v).abs().max().item() < 2e-6, k
 
