@@ -547,12 +547,75 @@ class OCICompute(VMCompute):
     TYPE = BackendType.OCI
     SSH_USER = "ubuntu"
     API_VERSION = "20160918"
+    CONFIGURABLE_DISK = (50.0, 32768.0)  # boot volume, GB
 
     def _host(self, region: str) -> str:
         return f"iaas.{region}.oraclecloud.com"
 
-    def _signed(self, method: str, region: str, path: str, body: Optional[dict] = None):
-        host = self._host(region)
+    def _compartment(self) -> str:
+        return self.config.get("compartment_id") or self.auth.get("tenancy")
+
+    def _availability_domains(self, region: str) -> List[str]:
+        """The tenancy's availability-domain names in ``region`` (tenancy-prefixed, e.g.
+        ``Uocm:US-CHICAGO-1-AD-1``: they cannot be derived from the region name)."""
+        q = urllib.parse.urlencode({"compartmentId": self.auth.get("tenancy") or self._compartment()})
+        r = check_response(self._signed("GET", region, f"/{self.API_VERSION}/availabilityDomains?{q}",
+                                        host=f"identity.{region}.oraclecloud.com"), "oci availability domains")
+        return sorted(d["name"] for d in r.json())
+
+    def _shapes(self, region: str, ad: str) -> List[str]:
+        out, page = [], None
+        for _ in range(50):
+            params = {"compartmentId": self._compartment(), "availabilityDomain": ad, "limit": 100}
+            if page:
+                params["page"] = page
+            r = check_response(self._signed("GET", region, f"/{self.API_VERSION}/shapes?"
+                                            + urllib.parse.urlencode(params)), "oci shapes")
+            out.extend(x.get("shape") for x in r.json())
+            page = r.headers.get("opc-next-page")
+            if not page:
+                break
+        return out
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """Catalog shapes checked against the compartment's shapes per availability domain
+        (``ListShapes``): shapes no AD of a region offers are ``not_available``; the ADs that offer
+        each shape are remembered for the launch."""
+        base = offline_rows(self.TYPE)
+        wanted = self.config.get("regions")
+        regions = sorted(set(wanted or []) | {r.location for r in base if not wanted})
+        names = {r.instance_name for r in base}
+        shape_ads: Dict[Tuple[str, str], List[str]] = {}
+        for region in regions:
+            for ad in self._availability_domains(region):
+                for shape in self._shapes(region, ad):
+                    if shape in names:
+                        shape_ads.setdefault((shape, region), []).append(ad)
+        self._shape_ads = shape_ads
+        specs: Dict[Tuple[str, bool], CatalogRow] = {}
+        for r in base:
+            specs.setdefault((r.instance_name, r.spot), r)
+        out = []
+        for (name, spot), proto in sorted(specs.items()):
+            for region in regions:
+                out.append(replace(proto, location=region, availability=InstanceAvailability.UNKNOWN
+                                   if (name, region) in shape_ads else InstanceAvailability.NOT_AVAILABLE))
+        return out
+
+    def _ad_for(self, region: str, shape: str) -> str:
+        ads = self.config.get("availability_domains") or {}
+        if ads.get(region):
+            return ads[region]
+        offered = getattr(self, "_shape_ads", {}).get((shape, region))
+        if offered:
+            return offered[0]
+        for ad in self._availability_domains(region):
+            if shape in self._shapes(region, ad):
+                return ad
+        raise ComputeError(f"no availability domain of {region} offers {shape}")
+
+    def _signed(self, method: str, region: str, path: str, body: Optional[dict] = None, host: Optional[str] = None):
+        host = host or self._host(region)
         date = email.utils.formatdate(usegmt=True)
         headers = {"date": date, "host": host}
         data = b""
@@ -573,10 +636,10 @@ class OCICompute(VMCompute):
 
     def _launch(self, offer, cfg):
         region = offer.region
-        comp = self.config.get("compartment_id") or self.auth.get("tenancy")
-        ads = self.config.get("availability_domains") or {}
+        comp = self._compartment()
         body = {
-            "compartmentId": comp, "availabilityDomain": ads.get(region, f"{region}-AD-1"), "shape": offer.instance.name,
+            "compartmentId": comp, "availabilityDomain": self._ad_for(region, offer.instance.name),
+            "shape": offer.instance.name,
             "displayName": cfg.instance_name,
             "sourceDetails": {"sourceType": "image", "imageId": self._image_id(region, comp, offer.instance.name),
                               "bootVolumeSizeInGBs": max(100, offer.instance.resources.disk.size_mib // 1024)},

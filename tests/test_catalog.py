@@ -448,6 +448,31 @@ def test_gcp_live_machine_types_and_launch_zone(live, monkeypatch):
     assert "/zones/europe-west4-b/instances" in inserted[0]
 
 
+def test_oci_live_shapes_per_availability_domain(live, monkeypatch):
+    from dstack_amd.core.backends.clouds import hyperscalers
+
+    monkeypatch.setattr(hyperscalers, "rsa_sha256_sign", lambda key, data: b"sig")
+
+    def handler(req):
+        region = req.url.host.split(".")[1]
+        if req.url.path.endswith("/availabilityDomains"):
+            return httpx.Response(200, json=[{"name": f"Xy:{region.upper()}-AD-1"}, {"name": f"Xy:{region.upper()}-AD-2"}])
+        if req.url.path.endswith("/shapes"):
+            q = dict(urllib.parse.parse_qsl(req.url.query.decode()))
+            has = region == "us-chicago-1" and q["availabilityDomain"].endswith("AD-2")
+            if q.get("page") == "p2":
+                return httpx.Response(200, json=[{"shape": "BM.GPU.MI355X.8"}] if has else [])
+            return httpx.Response(200, json=[{"shape": "VM.Standard.E5.Flex"}], headers={"opc-next-page": "p2"})
+        return httpx.Response(404)
+
+    c = compute_class(BackendType.OCI)({"regions": ["us-chicago-1", "eu-frankfurt-1"], "compartment_id": "comp"},
+                                       {"tenancy": "ten", "user": "u", "fingerprint": "fp", "key_content": "k"},
+                                       _client(handler))
+    offers = {o.region: o.availability for o in c.get_offers(_req(gpu="MI355X:8"))}
+    assert offers == {"us-chicago-1": IA.UNKNOWN, "eu-frankfurt-1": IA.NOT_AVAILABLE}
+    assert c._ad_for("us-chicago-1", "BM.GPU.MI355X.8") == "Xy:US-CHICAGO-1-AD-2"
+
+
 def test_live_listing_is_cached_per_credentials(live):
     n = {"calls": 0}
 

@@ -272,7 +272,15 @@ def test_oci_http_signature(rsa_pem):
             body = json.loads(req.content)
             assert body["shape"] == "BM.GPU.MI300X.8"
             assert body["sourceDetails"]["imageId"] == "ocid1.image.ubuntu"  # looked up, never ""
+            # the tenancy's real AD name that offers the shape (not "<region>-AD-1")
+            assert body["availabilityDomain"] == "Uocm:US-CHICAGO-1-AD-2"
             return httpx.Response(200, json={"id": "ocid1.instance"})
+        if req.url.host.startswith("identity.") and req.url.path.endswith("/availabilityDomains"):
+            return httpx.Response(200, json=[{"name": "Uocm:US-CHICAGO-1-AD-1"}, {"name": "Uocm:US-CHICAGO-1-AD-2"}])
+        if req.url.path.endswith("/shapes"):
+            ad = dict(urllib.parse.parse_qsl(req.url.query.decode()))["availabilityDomain"]
+            shapes = ["VM.Standard.E4.Flex"] + (["BM.GPU.MI300X.8"] if ad.endswith("AD-2") else [])
+            return httpx.Response(200, json=[{"shape": x} for x in shapes])
         if req.url.path.endswith("/images"):
             q = dict(urllib.parse.parse_qsl(req.url.query.decode()))
             assert q["shape"] == "BM.GPU.MI300X.8" and q["operatingSystemVersion"] == "22.04"
