@@ -351,6 +351,58 @@ def _gb(v) -> str:
     return "-" if v is None else f"{v / 2**30:.1f}GB"
 
 
+# ---- offer ------------------------------------------------------------------------------------
+def register_offer(sub):
+    p = sub.add_parser("offer", help="List the offers of every configured backend for a resource spec "
+                                     "(live provider listings where the backend has one)")
+    add_project_arg(p)
+    p.add_argument("--gpu", metavar="SPEC", help="GPU spec, e.g. MI355X:8, 192GB..:1.., amd:8")
+    p.add_argument("--cpu", metavar="SPEC")
+    p.add_argument("--memory", metavar="SPEC")
+    p.add_argument("--disk", metavar="SPEC")
+    g = p.add_mutually_exclusive_group()
+    g.add_argument("--spot", dest="spot_policy", action="store_const", const="spot")
+    g.add_argument("--on-demand", dest="spot_policy", action="store_const", const="on-demand")
+    p.add_argument("--max-price", type=float)
+    p.add_argument("-b", "--backend", action="append", dest="backends", metavar="NAME")
+    p.add_argument("-r", "--region", action="append", dest="regions", metavar="NAME")
+    p.add_argument("-n", "--max-offers", type=int, default=50)
+    p.add_argument("--json", action="store_true", help="print the offers as JSON")
+    p.set_defaults(func=cmd_offer)
+
+
+def cmd_offer(args) -> int:
+    import json
+
+    from rich.table import Table
+
+    from dstack_amd.core.models.configurations import parse_run_configuration
+
+    resources = {k: getattr(args, k) for k in ("gpu", "cpu", "memory", "disk") if getattr(args, k)}
+    conf = {"type": "task", "commands": [":"], "resources": resources, "spot_policy": args.spot_policy or "auto"}
+    for k, v in (("max_price", args.max_price), ("backends", args.backends), ("regions", args.regions)):
+        if v:
+            conf[k] = v
+    client = _client(args)
+    plan = client.runs.get_plan(parse_run_configuration(conf), max_offers=args.max_offers)
+    jp = plan.job_plans[0]
+    if args.json:
+        print(json.dumps({"total_offers": jp.total_offers, "max_price": jp.max_price,
+                          "offers": [o.model_dump(mode="json") for o in jp.offers]}, indent=1))
+        return 0
+    t = Table(box=None, header_style="bold")
+    for col in ("#", "BACKEND", "REGION", "INSTANCE", "RESOURCES", "SPOT", "PRICE", "AVAILABILITY"):
+        t.add_column(col, no_wrap=col != "RESOURCES")
+    for i, o in enumerate(jp.offers, 1):
+        r = o.instance.resources
+        t.add_row(str(i), o.backend.value, o.region, o.instance.name, r.pretty_format(), "yes" if r.spot else "no",
+                  f"${o.price:.4g}", o.availability.value)
+    print_table(t)
+    console.print(f"{len(jp.offers)} of {jp.total_offers} offers shown"
+                  + (f", up to ${jp.max_price:.4g}/h" if jp.max_price is not None else ""))
+    return 0
+
+
 # ---- fleet / volume / gateway / pool ----------------------------------------------------------
 def register_fleet(sub):
     p = sub.add_parser("fleet", help="Manage fleets")
@@ -706,5 +758,5 @@ def cmd_run(args) -> int:
 
 
 REGISTRARS = [register_server, register_config, register_init, register_apply, register_delete, register_ps,
-              register_logs, register_stop, register_attach, register_stats, register_fleet, register_volume,
-              register_gateway, register_pool, register_run]
+              register_logs, register_stop, register_attach, register_stats, register_offer, register_fleet,
+              register_volume, register_gateway, register_pool, register_run]

@@ -243,6 +243,26 @@ def test_cli_apply_ps_logs(server, tmp_path):
     assert r.returncode == 5, r.stdout + r.stderr
 
 
+def test_cli_offer(server, tmp_path):
+    """``dstack offer``: every configured backend's offers for a spec (the local backend here)."""
+    import json as _json
+
+    env = dict(os.environ, DSTACK_SERVER_URL=server.url, DSTACK_TOKEN=server.token,
+               DSTACK_DIR=str(tmp_path / "home"), PYTHONPATH=REPO)
+    dstack = [sys.executable, "-m", "dstack_amd"]
+    r = subprocess.run(dstack + ["offer", "--json", "-n", "5"], cwd=tmp_path, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = _json.loads(r.stdout)
+    assert d["total_offers"] >= 1 and d["offers"][0]["backend"] == "local"
+    r = subprocess.run(dstack + ["offer", "--cpu", "1..", "--on-demand"], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "BACKEND" in r.stdout and "offers shown" in r.stdout, r.stdout + r.stderr
+    r = subprocess.run(dstack + ["offer", "--gpu", "MI355X:1024"], cwd=tmp_path, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "0 of 0 offers shown" in r.stdout, r.stdout + r.stderr
+
+
 def test_service_through_local_gateway(tmp_path):
     """Gateway on the server host (built-in data plane): service registered on the gateway,
     replica upstream registered when the job runs, Host-routed request reaches the replica."""
