@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Set, Tuple
 
 from dstack_amd.core.backends.catalog import CatalogRow, offline_rows
 from dstack_amd.core.backends.clouds.common import VMCompute, check_response, cloud_init, sigv4_headers
-from dstack_amd.core.errors import ComputeError, NoCapacityError
+from dstack_amd.core.errors import BackendAuthError, ComputeError, NoCapacityError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.gateways import GatewayComputeConfiguration, GatewayProvisioningData
 from dstack_amd.core.models.instances import (
@@ -103,6 +103,18 @@ class AWSCompute(VMCompute):
             if not token:
                 break
         return items
+
+    def check_credentials(self) -> None:
+        """STS GetCallerIdentity: valid for any credentials that can sign, whatever their policies."""
+        url = "https://sts.amazonaws.com/"
+        body = urllib.parse.urlencode({"Action": "GetCallerIdentity", "Version": "2011-06-15"}).encode()
+        headers = sigv4_headers("POST", url, "us-east-1", "sts", self.access_key, self.secret_key, body,
+                                self.session_token,
+                                extra_headers={"content-type": "application/x-www-form-urlencoded; charset=utf-8"})
+        r = self.http.post(url, content=body, headers=headers)
+        if r.status_code in (400, 401, 403):
+            raise BackendAuthError(f"aws sts: {r.status_code} {r.text[:300]}")
+        check_response(r, "aws sts")
 
     # ---- live catalog -------------------------------------------------------------------------
     def _fetch_catalog(self) -> List[CatalogRow]:

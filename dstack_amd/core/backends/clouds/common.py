@@ -107,6 +107,11 @@ class CatalogOffers:
     def _offer_filter(self, offer: InstanceOfferWithAvailability) -> bool:
         return True
 
+    def check_credentials(self) -> None:
+        """One cheap authenticated call; raises ``BackendAuthError`` when the cloud rejects the
+        credentials (the server refuses to store such a backend).  Default: nothing to check."""
+        return None
+
     def _availability(self) -> Dict[Tuple[str, str], InstanceAvailability]:
         """Optional extra stock overlay on top of the catalog rows."""
         return {}

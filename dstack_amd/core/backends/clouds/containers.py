@@ -19,7 +19,7 @@ import yaml
 from dstack_amd.core.backends.base import Compute, DSTACK_RUNNER_SSH_PORT
 from dstack_amd.core.backends.catalog import CatalogRow, gpu_row
 from dstack_amd.core.backends.clouds.common import CatalogOffers, check_response, container_commands
-from dstack_amd.core.errors import ComputeError, NoCapacityError
+from dstack_amd.core.errors import BackendAuthError, ComputeError, NoCapacityError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.gpus import normalize_gpu_name
 from dstack_amd.core.models.instances import (
@@ -60,6 +60,14 @@ class RunpodCompute(ContainerCompute):
         "lowestPrice(input: {gpuCount: 1}) { minVcpu minMemory } } "
         "dataCenters { id listed gpuAvailability { gpuTypeId available stockStatus } } }"
     )
+
+    def check_credentials(self) -> None:
+        try:
+            self._gql("query { myself { id } }")
+        except ComputeError as e:
+            if any(w in str(e).lower() for w in ("unauthorized", "api key", "forbidden", "authenticated")):
+                raise BackendAuthError(str(e)) from None
+            raise
 
     def _fetch_catalog(self) -> List[CatalogRow]:
         """GPU types (secure-cloud on-demand and spot price per GPU, vCPU / RAM per GPU) x data
@@ -178,6 +186,9 @@ class VastAICompute(ContainerCompute):
     def _h(self):
         return {"Authorization": f"Bearer {self.auth.get('api_key', '')}"}
 
+    def check_credentials(self) -> None:
+        check_response(self.http.get(f"{self.API}/users/current/", headers=self._h()), "vastai user")
+
     def _fetch_catalog(self) -> List[CatalogRow]:
         """Live marketplace asks (``/bundles``): one row per rentable offer, named by its ask id."""
         r = check_response(self.http.post(f"{self.API}/bundles/", headers=self._h(), json={
@@ -251,16 +262,15 @@ class KubernetesCompute(ContainerCompute):
                 "token": user.get("token"), "cert": user.get("client-certificate-data"),
                 "key": user.get("client-key-data")}
 
-    def _client(self) -> httpx.Client:
-        if self.http is not None and not isinstance(self.http, type(None)) and getattr(self, "_http_injected", True):
-            return self.http
-        return self.http
-
     def _h(self):
         return {"Authorization": f"Bearer {self._kube['token']}"} if self._kube.get("token") else {}
 
     def _url(self, path: str) -> str:
         return self._kube["server"].rstrip("/") + path
+
+    def check_credentials(self) -> None:
+        check_response(self.http.get(self._url(f"/api/v1/namespaces/{self.NAMESPACE}"), headers=self._h()),
+                       "kubernetes namespace")
 
     def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
         """One offer per node (allocatable CPU/memory/``amd.com/gpu``)."""

@@ -34,7 +34,7 @@ from dstack_amd.core.backends.clouds.common import (
     cloud_init,
     rsa_sha256_sign,
 )
-from dstack_amd.core.errors import ComputeError
+from dstack_amd.core.errors import BackendAuthError, ComputeError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.instances import InstanceAvailability
 
@@ -52,17 +52,26 @@ class AzureCompute(VMCompute):
         self.tenant = self.config.get("tenant_id") or self.auth.get("tenant_id")
 
     def _fetch_token(self):
-        r = check_response(self.http.post(
+        r = self.http.post(
             f"https://login.microsoftonline.com/{self.tenant}/oauth2/v2.0/token",
             data={"grant_type": "client_credentials", "client_id": self.auth.get("client_id"),
-                  "client_secret": self.auth.get("client_secret"), "scope": f"{self.ARM}/.default"}), "azure token")
-        d = r.json()
+                  "client_secret": self.auth.get("client_secret"), "scope": f"{self.ARM}/.default"})
+        if r.status_code in (400, 401):  # AADSTS errors: unknown tenant / client, bad secret
+            raise BackendAuthError(f"azure token: {r.status_code} {r.text[:300]}")
+        d = check_response(r, "azure token").json()
         return d["access_token"], d.get("expires_in", 3600)
 
     def _h(self):
         return {"Authorization": f"Bearer {self._token.get()}"}
 
     CONFIGURABLE_DISK = (30.0, 4095.0)  # managed OS disk, GiB
+
+    def check_credentials(self) -> None:
+        """Token exchange + read access to the subscription."""
+        r = self.http.get(f"{self.ARM}/subscriptions/{self.subscription}?api-version=2020-01-01", headers=self._h())
+        if r.status_code in (401, 403, 404):
+            raise BackendAuthError(f"azure subscription {self.subscription}: {r.status_code} {r.text[:200]}")
+        check_response(r, "azure subscription")
     RETAIL_PRICES = "https://prices.azure.com/api/retail/prices"
 
     def _fetch_catalog(self) -> List[CatalogRow]:
@@ -310,16 +319,26 @@ class GCPCompute(VMCompute):
         claims = b64url(json.dumps({"iss": self.sa["client_email"], "scope": "https://www.googleapis.com/auth/cloud-platform",
                                     "aud": "https://oauth2.googleapis.com/token", "iat": now, "exp": now + 3600}).encode())
         sig = b64url(rsa_sha256_sign(self.sa["private_key"], f"{header}.{claims}".encode()))
-        r = check_response(self.http.post("https://oauth2.googleapis.com/token", data={
-            "grant_type": "urn:ietf:params:oauth:grant-type:jwt-bearer", "assertion": f"{header}.{claims}.{sig}"}),
-            "gcp token")
-        d = r.json()
+        r = self.http.post("https://oauth2.googleapis.com/token", data={
+            "grant_type": "urn:ietf:params:oauth:grant-type:jwt-bearer", "assertion": f"{header}.{claims}.{sig}"})
+        if r.status_code in (400, 401):  # invalid_grant: unknown / disabled key
+            raise BackendAuthError(f"gcp token: {r.status_code} {r.text[:300]}")
+        d = check_response(r, "gcp token").json()
         return d["access_token"], d.get("expires_in", 3600)
 
     def _h(self):
         return {"Authorization": f"Bearer {self._token.get()}"}
 
     CONFIGURABLE_DISK = (10.0, 65536.0)  # persistent boot disk, GB
+
+    def check_credentials(self) -> None:
+        """Token exchange + the Compute API on the project (403 / 404: no access or no API)."""
+        if not self.sa.get("client_email") or not self.sa.get("private_key"):
+            raise BackendAuthError("gcp: the service-account key needs client_email and private_key")
+        r = self.http.get(f"{self.API}/projects/{self.project}", headers=self._h())
+        if r.status_code in (401, 403, 404):
+            raise BackendAuthError(f"gcp project {self.project}: {r.status_code} {r.text[:200]}")
+        check_response(r, "gcp project")
 
     def _fetch_catalog(self) -> List[CatalogRow]:
         """Catalog machine types checked against the project's zones (aggregated
@@ -554,6 +573,14 @@ class OCICompute(VMCompute):
 
     def _compartment(self) -> str:
         return self.config.get("compartment_id") or self.auth.get("tenancy")
+
+    def check_credentials(self) -> None:
+        region = (self.config.get("regions") or ["us-ashburn-1"])[0]
+        user = urllib.parse.quote(self.auth.get("user", ""))
+        r = self._signed("GET", region, f"/{self.API_VERSION}/users/{user}", host=f"identity.{region}.oraclecloud.com")
+        if r.status_code in (401, 403, 404):
+            raise BackendAuthError(f"oci user: {r.status_code} {r.text[:200]}")
+        check_response(r, "oci user")
 
     def _availability_domains(self, region: str) -> List[str]:
         """The tenancy's availability-domain names in ``region`` (tenancy-prefixed, e.g.

@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Tuple
 
 from dstack_amd.core.backends.catalog import CatalogRow, gpu_row
 from dstack_amd.core.backends.clouds.common import OAuthToken, VMCompute, check_response, cloud_init
-from dstack_amd.core.errors import ComputeError
+from dstack_amd.core.errors import BackendAuthError, ComputeError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.gpus import gpu_info, normalize_gpu_name
 from dstack_amd.core.models.instances import (
@@ -57,6 +57,9 @@ class LambdaCompute(VMCompute):
                                     specs.get("gpus", 0), disk_gb=specs.get("storage_gib"), gpu_memory_gb=gpu_mem,
                                     availability=_AVAILABLE if loc in with_capacity else _NOT_AVAILABLE))
         return rows
+
+    def check_credentials(self) -> None:
+        check_response(self.http.get(f"{self.API}/instance-types", headers=self._h()), "lambda instance-types")
 
     def _ensure_key(self, cfg: InstanceConfiguration) -> str:
         name = f"dstack-{cfg.project_name}"
@@ -102,6 +105,9 @@ class VultrCompute(VMCompute):
     @staticmethod
     def _kind(plan: str) -> str:
         return "bare-metals" if plan.startswith("vbm-") else "instances"
+
+    def check_credentials(self) -> None:
+        check_response(self.http.get(f"{self.API}/account", headers=self._h()), "vultr account")
 
     def _list(self, path: str, key: str) -> List[dict]:
         out, cursor = [], ""
@@ -200,6 +206,11 @@ class TensorDockCompute(VMCompute):
     def _auth(self):
         return {"api_key": self.auth.get("api_key", ""), "api_token": self.auth.get("api_token", "")}
 
+    def check_credentials(self) -> None:
+        r = check_response(self.http.post(f"{self.API}/auth/test", data=self._auth()), "tensordock auth")
+        if not (r.json() or {}).get("success"):
+            raise BackendAuthError(f"tensordock: {r.text[:200]}")
+
     def _fetch_catalog(self) -> List[CatalogRow]:
         """Marketplace host nodes (``/client/deploy/hostnodes``): one row per (GPU model, count)
         that fits a node, CPU / RAM in proportion to the GPUs taken, price = the node's per-unit
@@ -273,6 +284,10 @@ class CudoCompute(VMCompute):
     def _h(self):
         return {"Authorization": f"Bearer {self.auth.get('api_key', '')}"}
 
+    def check_credentials(self) -> None:
+        check_response(self.http.get(f"{self.API}/projects/{self.config.get('project_id', 'default')}",
+                                     headers=self._h()), "cudo project")
+
     def _launch(self, offer, cfg):
         project = self.config.get("project_id", "default")
         res = offer.instance.resources
@@ -314,9 +329,12 @@ class DataCrunchCompute(VMCompute):
         self._token = OAuthToken(self._fetch_token)
 
     def _fetch_token(self):
-        r = check_response(self.http.post(f"{self.API}/oauth2/token", json={
+        r = self.http.post(f"{self.API}/oauth2/token", json={
             "grant_type": "client_credentials", "client_id": self.auth.get("client_id"),
-            "client_secret": self.auth.get("client_secret")}), "datacrunch token")
+            "client_secret": self.auth.get("client_secret")})
+        if r.status_code in (400, 401, 403):
+            raise BackendAuthError(f"datacrunch token: {r.status_code} {r.text[:200]}")
+        check_response(r, "datacrunch token")
         d = r.json()
         return d["access_token"], d.get("expires_in", 3600)
 
@@ -324,6 +342,9 @@ class DataCrunchCompute(VMCompute):
         return {"Authorization": f"Bearer {self._token.get()}"}
 
     CONFIGURABLE_DISK = (50.0, None)
+
+    def check_credentials(self) -> None:
+        self._token.get()  # the client-credentials exchange is the check
 
     def _fetch_catalog(self) -> List[CatalogRow]:
         """``/instance-types`` (on-demand and spot prices, specs) x ``/instance-availability`` per
@@ -399,6 +420,11 @@ class NebiusCompute(VMCompute):
 
     def _h(self):
         return {"Authorization": f"Bearer {self.auth.get('iam_token') or self.auth.get('token', '')}"}
+
+    def check_credentials(self) -> None:
+        check_response(self.http.get(f"{self.API}/instances", params={"folderId": self.config.get("folder_id"),
+                                                                      "pageSize": 1}, headers=self._h()),
+                       "nebius instances")
 
     def _launch(self, offer, cfg):
         res = offer.instance.resources

@@ -30,6 +30,7 @@ class ServerClientErrorCode:
     INVALID_REQUEST = "invalid_request"
     BACKEND_NOT_AVAILABLE = "backend_not_available"
     RESOURCE_BUSY = "resource_busy"
+    INVALID_CREDENTIALS = "invalid_credentials"
 
 
 class ServerClientError(ServerError):
@@ -85,6 +86,14 @@ class ResourceBusyError(ServerClientError):
 
     code = ServerClientErrorCode.RESOURCE_BUSY
     msg = "Resource is being processed, retry"
+
+
+class InvalidCredentialsError(ServerClientError):
+    """Backend credentials the cloud rejected (reference ``BackendInvalidCredentialsError``,
+    ``S/services/backends/configurators/*``)."""
+
+    code = ServerClientErrorCode.INVALID_CREDENTIALS
+    msg = "Invalid credentials"
 
 
 class GatewayError(ServerClientError):

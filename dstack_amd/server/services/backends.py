@@ -117,6 +117,7 @@ def create_backend(s: Session, project: ProjectModel, config: dict) -> BackendMo
     if existing is not None:
         raise ResourceExistsError(f"Backend {btype.value} exists")
     _, cfg, secrets = split_backend_config(config)
+    validate_credentials(btype, cfg, secrets)
     row = BackendModel(id=uuid.uuid4(), project_id=project.id, type=btype.value, config=json.dumps(cfg),
                        auth=json.dumps(secrets))
     s.add(row)
@@ -138,9 +139,45 @@ def update_backend(s: Session, project: ProjectModel, config: dict) -> BackendMo
     if btype == BackendType.KUBERNETES and merged.get("kubeconfig") is None and old_secrets.get("kubeconfig"):
         merged["kubeconfig"] = old_secrets["kubeconfig"]
     _, cfg, secrets = split_backend_config(merged)
+    validate_credentials(btype, cfg, secrets)
     row.config = json.dumps(cfg)
     row.auth = json.dumps(secrets)
     return row
+
+
+def validate_credentials(btype: BackendType, cfg: dict, secrets: dict) -> None:
+    """Reference configurators' credential check: one authenticated call to the cloud.  Rejected
+    credentials fail the request (``InvalidCredentialsError``, HTTP 400); an unreachable API (an
+    air-gapped server, a network blip) does not -- the backend is stored and plans from the
+    offline catalog until the cloud answers.  ``DSTACK_SKIP_BACKEND_VALIDATION=1`` skips it."""
+    import logging
+    import os
+
+    import httpx
+
+    from dstack_amd.core.errors import BackendAuthError, InvalidCredentialsError
+
+    if os.getenv("DSTACK_SKIP_BACKEND_VALIDATION") == "1":
+        return
+    try:
+        from dstack_amd.core.backends.clouds import compute_class
+
+        cls = compute_class(btype)
+        if cls is None:
+            return
+        if btype == BackendType.KUBERNETES and secrets.get("kubeconfig") and not cfg.get("kubeconfig"):
+            cfg = {**cfg, "kubeconfig": secrets["kubeconfig"]}
+        # a short timeout: an air-gapped server must not hold the request for the client's 60 s
+        comp = cls(cfg, secrets, httpx.Client(timeout=float(os.getenv("DSTACK_BACKEND_VALIDATION_TIMEOUT", "15"))))
+        check = getattr(comp, "check_credentials", None)
+        if check is not None:
+            check()
+    except BackendAuthError as e:
+        raise InvalidCredentialsError(f"Invalid {btype.value} credentials: {e}") from None
+    except (httpx.TransportError, OSError) as e:
+        logging.getLogger(__name__).warning("%s credentials not verified (API unreachable: %s)", btype.value, e)
+    except Exception as e:  # noqa: BLE001 -- e.g. a malformed key the signer cannot load
+        raise InvalidCredentialsError(f"Invalid {btype.value} credentials: {e}") from None
 
 
 def _configurable_type(config: dict) -> BackendType:

@@ -36,7 +36,9 @@ SECRET_VALUES = {"s3", "cs", "k", "t", "tok", "s", "apiVersion: v1\n"}
 
 
 @pytest.mark.parametrize("btype", sorted(VALID))
-def test_create_each_backend_secrets_kept_apart(client, btype):
+def test_create_each_backend_secrets_kept_apart(client, btype, monkeypatch):
+    # placeholder credentials: storage / secret separation is under test, not the cloud's verdict
+    monkeypatch.setenv("DSTACK_SKIP_BACKEND_VALIDATION", "1")
     r = client.post("/api/project/main/backends/create", json=VALID[btype])
     assert r.status_code == 200, r.text
     info = client.post(f"/api/project/main/backends/{btype}/config_info").json()
@@ -124,3 +126,75 @@ def test_configured_backend_offers_in_plan(client):
     plan = client.post("/api/project/main/runs/get_plan", json=spec).json()
     offers = plan["job_plans"][0]["offers"]
     assert any(o["backend"] == "vultr" and o["instance"]["resources"]["gpus"][0]["name"] == "MI355X" for o in offers)
+
+
+def test_backend_credentials_validated_on_create(client, monkeypatch):
+    """The cloud's verdict on the credentials decides (reference configurators): rejected -> 400
+    ``invalid_credentials``; unreachable API (air-gapped server) -> stored with a warning."""
+    import httpx
+
+    from dstack_amd.core.backends.clouds import rest_vm
+
+    calls = []
+
+    def fake_get(self, url, **kw):
+        calls.append(url)
+        req = httpx.Request("GET", url)
+        if kw.get("headers", {}).get("Authorization") == "Bearer bad":
+            return httpx.Response(401, text='{"error": "invalid api key"}', request=req)
+        if kw.get("headers", {}).get("Authorization") == "Bearer offline":
+            raise httpx.ConnectError("no route to host", request=req)
+        return httpx.Response(200, json={"data": {}}, request=req)
+
+    monkeypatch.setattr(httpx.Client, "get", fake_get)
+    body = {"type": "lambda", "creds": {"type": "api_key", "api_key": "bad"}}
+    r = client.post("/api/project/main/backends/create", json=body)
+    assert r.status_code == 400 and r.json()["detail"][0]["code"] == "invalid_credentials", r.text
+    assert calls and calls[-1].endswith("/instance-types")
+    body["creds"]["api_key"] = "offline"
+    r = client.post("/api/project/main/backends/create", json=body)
+    assert r.status_code == 200, r.text
+    # update with rejected credentials is refused too, the stored backend stays
+    body["creds"]["api_key"] = "bad"
+    r = client.post("/api/project/main/backends/update", json=body)
+    assert r.status_code == 400
+    body["creds"]["api_key"] = "good"
+    assert client.post("/api/project/main/backends/update", json=body).status_code == 200
+
+
+def test_credential_checks_call_each_cloud():
+    """Each cloud's check_credentials hits an authenticated endpoint and maps 401/403 to an auth
+    error (mock transports)."""
+    import httpx
+
+    from dstack_amd.core.backends.clouds import compute_class
+    from dstack_amd.core.errors import BackendAuthError
+    from dstack_amd.core.models.backends import BackendType
+
+    seen = []
+
+    def deny(req):
+        seen.append(str(req.url))
+        return httpx.Response(401 if "token" not in req.url.path else 400, text="denied")
+
+    client = httpx.Client(transport=httpx.MockTransport(deny))
+    cases = {
+        BackendType.LAMBDA: ({}, {"api_key": "k"}, "/instance-types"),
+        BackendType.VULTR: ({}, {"api_key": "k"}, "/account"),
+        BackendType.DATACRUNCH: ({}, {"client_id": "a", "client_secret": "b"}, "/oauth2/token"),
+        BackendType.CUDO: ({"project_id": "p"}, {"api_key": "k"}, "/projects/p"),
+        BackendType.NEBIUS: ({"folder_id": "f"}, {"iam_token": "t"}, "/instances"),
+        BackendType.VASTAI: ({}, {"api_key": "k"}, "/users/current/"),
+        BackendType.RUNPOD: ({}, {"api_key": "k"}, "graphql"),
+        BackendType.AWS: ({}, {"access_key": "a", "secret_key": "s"}, "sts.amazonaws.com"),
+        BackendType.AZURE: ({"subscription_id": "s", "tenant_id": "t"}, {"client_id": "c", "client_secret": "x"},
+                            "oauth2/v2.0/token"),
+    }
+    for bt, (cfg, auth, needle) in cases.items():
+        c = compute_class(bt)(cfg, auth, client)
+        try:
+            c.check_credentials()
+            raise AssertionError(f"{bt.value}: rejected credentials accepted")
+        except BackendAuthError:
+            pass
+        assert needle in seen[-1], (bt, seen[-1])
