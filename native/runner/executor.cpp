@@ -261,6 +261,34 @@ Json Executor::pull(int64_t since) const {
   return out;
 }
 
+// RDMA devices with at least one ACTIVE port (/sys/class/infiniband/<dev>/ports/<n>/state =
+// "4: ACTIVE"), sorted: the HCAs RCCL should use across nodes (IB, RoCE, AMD AINIC alike)
+std::vector<std::string> active_rdma_devices() {
+  const char* root_env = getenv("DSTACK_SYSFS_ROOT");
+  const std::string base = std::string(root_env ? root_env : "") + "/sys/class/infiniband";
+  std::vector<std::string> out;
+  DIR* d = opendir(base.c_str());
+  if (!d) return out;
+  while (auto* e = readdir(d)) {
+    std::string dev = e->d_name;
+    if (dev == "." || dev == "..") continue;
+    DIR* pd = opendir((base + "/" + dev + "/ports").c_str());
+    if (!pd) continue;
+    bool active = false;
+    while (auto* pe = readdir(pd)) {
+      std::string st;
+      if (pe->d_name[0] != '.' && read_file(base + "/" + dev + "/ports/" + pe->d_name + "/state", st) &&
+          st.find("ACTIVE") != std::string::npos)
+        active = true;
+    }
+    closedir(pd);
+    if (active) out.push_back(dev);
+  }
+  closedir(d);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
 static std::string iface_for_ip(const std::string& ip) {
   struct ifaddrs* ifa = nullptr;
   if (getifaddrs(&ifa) != 0) return "";
@@ -342,6 +370,11 @@ std::vector<std::pair<std::string, std::string>> Executor::build_env() const {
     std::string my_ip = node_rank < (int)ips.size() ? ips[node_rank] : "";
     std::string ifname = my_ip.empty() ? "" : iface_for_ip(my_ip);
     if (!ifname.empty()) set("NCCL_SOCKET_IFNAME", ifname);
+  }
+  if (nodes > 1 && !has("NCCL_IB_HCA")) {
+    std::string hcas;
+    for (auto& dev : active_rdma_devices()) hcas += (hcas.empty() ? "" : ",") + dev;
+    if (!hcas.empty()) set("NCCL_IB_HCA", hcas);
   }
   // secrets (os env < dstack env < secrets < job env)
   for (auto& kv : submit_body_["secrets"].members()) set(kv.first, kv.second.str());

@@ -13,6 +13,9 @@
 
 namespace dsa {
 
+// RDMA devices with an ACTIVE port (NCCL_IB_HCA for multi-node jobs); DSTACK_SYSFS_ROOT for tests
+std::vector<std::string> active_rdma_devices();
+
 // executor states (states.go:3-9)
 enum class ExecState { WaitSubmit, WaitCode, WaitRun, ServeLogs, WaitLogsFinished };
 const char* exec_state_name(ExecState s);

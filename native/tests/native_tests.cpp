@@ -142,6 +142,24 @@ int main() {
     CHECK(summarize_counters("x,y\n1,2\n", {}, 5).empty());
   });
 
+  run("rdma devices with an active port -> NCCL_IB_HCA", [] {
+    char tmpl[] = "/tmp/dsa_ib_XXXXXX";
+    std::string root = mkdtemp(tmpl);
+    auto port = [&](const std::string& dev, int p, const std::string& state) {
+      std::string dir = root + "/sys/class/infiniband/" + dev + "/ports/" + std::to_string(p);
+      mkdirs(dir);
+      write_file(dir + "/state", state + "\n", 0644);
+    };
+    port("mlx5_1", 1, "4: ACTIVE");
+    port("mlx5_0", 1, "1: DOWN");
+    port("mlx5_0", 2, "4: ACTIVE");
+    port("ionic_0", 1, "1: DOWN");
+    setenv("DSTACK_SYSFS_ROOT", root.c_str(), 1);
+    auto devs = active_rdma_devices();
+    unsetenv("DSTACK_SYSFS_ROOT");
+    CHECK(devs.size() == 2 && devs[0] == "mlx5_0" && devs[1] == "mlx5_1");
+  });
+
   run("json roundtrip", [] {
     Json j = Json::parse(R"({"a":1,"b":[true,null,"x\né"],"c":{"d":-2.5e3}})");
     CHECK(j["a"].as_int() == 1);
