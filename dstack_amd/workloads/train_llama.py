@@ -272,7 +272,7 @@ def _sync(env: DistEnv):
 
 def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1,
         grad_accum: int = 1, checkpoint_dir: str | None = None, save_every: int = 0, lr: float = 3e-4,
-        lr_warmup: int = 10, lr_decay_steps: int = 0, clip_grad_norm: float = 0.0):
+        lr_warmup: int = 300, lr_decay_steps: int = 0, clip_grad_norm: float = 0.0):
     env = init_distributed()
     device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     from dstack_amd.ops import gemm_tuning
@@ -357,7 +357,10 @@ def main(argv=None):
     ap.add_argument("--save-every", type=int, default=0,
                     help="save a checkpoint whenever the optimizer step count is a multiple of N")
     ap.add_argument("--lr", type=float, default=3e-4)
-    ap.add_argument("--lr-warmup", type=int, default=10, help="linear LR warmup (optimizer steps)")
+    # 300 warmup steps (1e-6 per step at lr 3e-4): on the bench stream the loss falls 12.56 -> 8.4
+    # in 30 steps; 100 steps gives a noisier curve with excursions back to ~12-14, and global-norm
+    # clipping at 1.0 does not tame them (profiles/lr_sweep_*_r4k.log, loss_{no,}clip_r4n.log)
+    ap.add_argument("--lr-warmup", type=int, default=300, help="linear LR warmup (optimizer steps)")
     ap.add_argument("--lr-decay-steps", type=int, default=0, help="cosine decay to 0.1*lr at this step (0: constant)")
     ap.add_argument("--clip-grad-norm", type=float, default=0.0, help="global gradient-norm clipping (0: off)")
     args = ap.parse_args(argv)
