@@ -1,11 +1,15 @@
 """In-tree builder for the HIP extension ``dstack_amd/ops/_C*.so`` (gfx950 only).
 
 Kernels (``csrc/*.hip``) are compiled by ``hipcc --offload-arch=gfx950`` as plain HIP translation
-units (no torch headers, no hipify); ``csrc/bindings.cpp`` is the only torch-aware file.  Objects
-are rebuilt when their sources or headers change.
+units (no torch headers, no hipify); ``csrc/bindings.cpp`` is the only torch-aware file.  Rebuilds
+are content-addressed, not mtime-based: every object records the SHA-256 of its source, the headers
+and the compile command (``<obj>.sha256``), and the extension records the hash of its objects and
+the link command (``_C.sha256`` next to the ``.so``), so a copied / checked-out tree with fresh
+mtimes is not rebuilt needlessly and an edited source is never missed.
 
     python -m dstack_amd.ops.build            # build
     python -m dstack_amd.ops.build --asm      # also keep .s (register/occupancy audit)
+    python -m dstack_amd.ops.build --check    # exit 1 unless the .so matches the current sources
 """
 
 from __future__ import annotations
@@ -39,11 +43,27 @@ def so_path() -> Path:
     return HERE / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-def _newer(target: Path, deps) -> bool:
-    if not target.exists():
-        return True
-    t = target.stat().st_mtime
-    return any(Path(d).stat().st_mtime > t for d in deps)
+def _digest(files, cmd) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in files:
+        h.update(Path(f).name.encode() + b"\0" + Path(f).read_bytes() + b"\0")
+    h.update("\0".join(cmd).encode())
+    return h.hexdigest()
+
+
+def _stale(target: Path, digest: str) -> bool:
+    stamp = target.with_name(target.name + ".sha256")
+    return not target.exists() or not stamp.exists() or stamp.read_text().strip() != digest
+
+
+def _stamp(target: Path, digest: str) -> None:
+    target.with_name(target.name + ".sha256").write_text(digest + "\n")
+
+
+def so_stamp_path() -> Path:
+    return HERE / "_C.sha256"
 
 
 def _run(cmd):
@@ -53,48 +73,61 @@ def _run(cmd):
     return r.stderr
 
 
-def build(verbose: bool = False, keep_asm: bool = False, force: bool = False) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
-    headers = list(CSRC.glob("*.h"))
+def _plan(keep_asm: bool = False):
+    """[(object, compile command, digest)] and the link command."""
+    headers = sorted(CSRC.glob("*.h"))
     kernels = sorted(CSRC.glob("*.hip"))
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1"]
-    jobs = []
-    objs = []
+    units = []
     for src in kernels:
         obj = BUILD / (src.stem + ".o")
-        objs.append(obj)
-        if force or _newer(obj, [src, *headers]):
-            cmd = [HIPCC, *common, "-c", str(src), "-o", str(obj)]
-            if keep_asm:
-                cmd += ["-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"]
-            jobs.append(cmd)
+        cmd = [HIPCC, *common, "-c", str(src), "-o", str(obj)]
+        if keep_asm:
+            cmd += ["-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"]
+        units.append((obj, cmd, _digest([src, *headers], cmd)))
     inc, lib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     bsrc = CSRC / "bindings.cpp"
     bobj = BUILD / "bindings.o"
-    objs.append(bobj)
-    if force or _newer(bobj, [bsrc]):
-        jobs.append(
-            [
-                "g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-                f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
-                "-DTORCH_API_INCLUDE_EXTENSION_H", *[f"-I{p}" for p in inc], f"-I{py_inc}",
-                "-w", "-c", str(bsrc), "-o", str(bobj),
-            ]
-        )
+    bcmd = [
+        "g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
+        "-DTORCH_API_INCLUDE_EXTENSION_H", *[f"-I{p}" for p in inc], f"-I{py_inc}",
+        "-w", "-c", str(bsrc), "-o", str(bobj),
+    ]
+    units.append((bobj, bcmd, _digest([bsrc], bcmd)))
+    link = [
+        HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *[str(u[0]) for u in units], "-o", str(so_path()),
+        *[f"-L{p}" for p in lib], *[f"-Wl,-rpath,{p}" for p in lib],
+        "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64",
+    ]
+    import hashlib
+
+    so_digest = hashlib.sha256(("\0".join(u[2] for u in units) + "\0" + "\0".join(link)).encode()).hexdigest()
+    return units, link, so_digest
+
+
+def is_current() -> bool:
+    """True when the built extension was linked from exactly the current sources and flags."""
+    so = so_path()
+    _, _, so_digest = _plan()
+    stamp = so_stamp_path()
+    return so.exists() and stamp.exists() and stamp.read_text().strip() == so_digest
+
+
+def build(verbose: bool = False, keep_asm: bool = False, force: bool = False) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    units, link, so_digest = _plan(keep_asm)
+    jobs = [(obj, cmd, d) for obj, cmd, d in units if force or _stale(obj, d)]
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
-        for out in ex.map(_run, jobs):
+        for (obj, _, d), out in zip(jobs, ex.map(lambda j: _run(j[1]), jobs)):
+            _stamp(obj, d)
             if verbose and out:
                 print(out, file=sys.stderr)
     so = so_path()
-    if force or _newer(so, objs):
-        link = [
-            HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(so),
-            *[f"-L{p}" for p in lib], *[f"-Wl,-rpath,{p}" for p in lib],
-            "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-            "-lamdhip64",
-        ]
+    if force or jobs or not is_current():
         _run(link)
+        so_stamp_path().write_text(so_digest + "\n")
     return so
 
 
@@ -103,7 +136,12 @@ def main():
     ap.add_argument("--asm", action="store_true")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", action="store_true")
+    ap.add_argument("--check", action="store_true", help="exit 1 unless the .so matches the current sources")
     a = ap.parse_args()
+    if a.check:
+        ok = is_current()
+        print(f"{so_path()}: {'current' if ok else 'STALE or missing'}")
+        sys.exit(0 if ok else 1)
     print(build(verbose=a.v, keep_asm=a.asm, force=a.force))
 
 

@@ -1,0 +1,34 @@
+"""The HIP extension build is content-addressed (ops/build.py): the digests change with any source,
+header or flag, and a built tree reports itself current."""
+
+import pytest
+
+from dstack_amd.ops import build
+
+
+def test_digest_tracks_content_and_flags(tmp_path):
+    a = tmp_path / "k.hip"
+    a.write_text("__global__ void k() {}\n")
+    d1 = build._digest([a], ["hipcc", "-O3"])
+    assert d1 == build._digest([a], ["hipcc", "-O3"])
+    assert d1 != build._digest([a], ["hipcc", "-O2"])
+    a.write_text("__global__ void k() { }\n")
+    assert d1 != build._digest([a], ["hipcc", "-O3"])
+    obj = tmp_path / "k.o"
+    assert build._stale(obj, d1)
+    obj.write_bytes(b"x")
+    build._stamp(obj, d1)
+    assert not build._stale(obj, d1) and build._stale(obj, d1 + "0")
+
+
+def test_plan_covers_every_kernel_source():
+    units, link, digest = build._plan()
+    srcs = {p.stem for p in build.CSRC.glob("*.hip")} | {"bindings"}
+    assert {u[0].stem for u in units} == srcs
+    assert any("--offload-arch=gfx950" in c for c in units[0][1]) and len(digest) == 64
+
+
+def test_built_extension_is_current():
+    if not build.so_path().exists():
+        pytest.skip("extension not built in this checkout")
+    assert build.is_current(), "the .so does not match the current kernel sources: rebuild"
