@@ -5,6 +5,6 @@ step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; if [ $rc 
 step bench timeout -k 10 500 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_r4o.log 2>&1
 tail -1 gpurun_out/bench_r4o.log | cut -c1-400
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-step prof timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r4o -o run -- python bench.py --steps 3 --warmup 2 --no-coldstart > gpurun_out/prof_r4o.log 2>&1
+step prof timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r4o -o run -- python bench.py --steps 3 --warmup 2 --no-coldstart > gpurun_out/prof_r4o.log 2>&1
 ls gpurun_out/prof_r4o | head
 exit 0
