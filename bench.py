@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--seq-len", type=int, default=8192)
+    # 1 x 8192 tokens per micro-batch: 2 x 8192 (grad-accum 4, same tokens/step, 207 vs 171 GB)
+    # measured 1.2 % slower, interleaved on one box (profiles/ab_microbatch_r4p.txt)
     ap.add_argument("--micro-batch", type=int, default=1)
     # 8 x 8192-token micro-batches per optimizer step: 64k tokens/GPU/step, a 0.5M-token global
     # batch at 8 GPUs (Llama-3 pre-training used 4M+).  It amortises the HBM-bound fp32 AdamW pass
