@@ -328,7 +328,19 @@ def cmd_stats(args) -> int:
             gpus = []
             for i in range(int(vals.get("gpus_detected_num") or 0)):
                 util, used = vals.get(f"gpu_util_percent_gpu{i}"), vals.get(f"gpu_memory_usage_bytes_gpu{i}")
-                gpus.append(f"#{i} {_gb(used)} {util if util is not None else '-'}% util")
+                line = f"#{i} {_gb(used)} {util if util is not None else '-'}% util"
+                power, hbm = vals.get(f"gpu_power_watts_gpu{i}"), vals.get(f"gpu_hbm_activity_percent_gpu{i}")
+                if power is not None:
+                    line += f" {power:.0f}W"
+                if hbm is not None:
+                    line += f" HBM {hbm:.0f}%"
+                rd, wr = vals.get(f"gpu_xgmi_read_bytes_per_s_gpu{i}"), vals.get(f"gpu_xgmi_write_bytes_per_s_gpu{i}")
+                if rd is not None or wr is not None:
+                    line += f" xGMI rd {(rd or 0) / 1e9:.1f} wr {(wr or 0) / 1e9:.1f} GB/s"
+                up = vals.get(f"gpu_xgmi_links_up_gpu{i}")
+                if up is not None:
+                    line += f" ({up:.0f} links up)"
+                gpus.append(line)
             t.add_row(job.job_spec.job_name, f"{cpu}%" if cpu is not None else "-",
                       f"{_gb(mem)}/{_gb(mem_total)}" if mem_total else _gb(mem), "\n".join(gpus) or "-")
         return t
