@@ -45,7 +45,10 @@ constexpr int HD = 128;          // head dim
 // chains, instead of one read -> lgkmcnt(0) -> MFMA per step (which exposes the LDS latency on
 // every MFMA of the phase): 0.702 vs 0.713 ms at S=8192 over three interleaved same-box runs
 // (tools/gpu_sessions/run_r1ze.sh); DSTACK_AMD_FA_FWD_PF=0 selects the old form.
-template <bool CAUSAL, int NW = 4, bool PF = true>
+// PRIO (A/B, DSTACK_AMD_FA_PRIO): 0 = no priority games; 1 = a wave raises its issue priority
+// (s_setprio) for its MFMA phases, so of the two waves on a SIMD the one with matrix work queues
+// it first and the other's softmax VALU fills the gaps; 2 = the softmax phase gets the priority.
+template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
                                                         float* __restrict__ lse, int B, int S,
@@ -98,6 +101,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[t][r] = 0.f;
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(3);
       if constexpr (PF) {
         // step i: key tile t = i & 1, k-slice ks = i >> 1; fragment i + 4 is read while i computes
         bf16x8 kf[4];
@@ -124,6 +128,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
 #pragma unroll
           for (int ks = 0; ks < 8; ++ks) st[t] = mfma(lds_row(kl, 32 * t + l32, 2 * ks + hf), qf[ks], st[t]);
       }
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+      if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(3);
       // only the tile(s) crossing this wave's diagonal need the causal mask (wave-uniform test)
       if (CAUSAL && kv0 + 63 > qw0) {
 #pragma unroll
@@ -166,10 +172,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
       bf16x8 pb[4];
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) pb[s4] = to_bf16x8(st[s4 >> 1], 8 * (s4 & 1));
+      if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
       for (int d = 0; d < 4; ++d)
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) o[d] = mfma(lds_tr(vl, 16 * s4, 32 * d, lane), pb[s4], o[d]);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
     }
     wait_dma_and_barrier();
   }
@@ -884,9 +893,19 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     const char* v = getenv("DSTACK_AMD_FA_FWD_PF");
     return !(v && atoi(v) == 0);
   }();
+  static const int prio = [] {
+    const char* v = getenv("DSTACK_AMD_FA_PRIO");
+    return v ? atoi(v) : 0;
+  }();
   if (waves == 8 && S % 256 == 0) {
     const int grid = B * H * (S / 256);
-    if (causal && pf)
+    if (causal && pf && prio == 1)
+      fa_fwd_kernel<true, 8, true, 1><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2,
+                                                            thr);
+    else if (causal && pf && prio == 2)
+      fa_fwd_kernel<true, 8, true, 2><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2,
+                                                            thr);
+    else if (causal && pf)
       fa_fwd_kernel<true, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2, thr);
     else if (causal)
       fa_fwd_kernel<true, 8, false><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2, thr);
