@@ -48,6 +48,8 @@ constexpr int HD = 128;          // head dim
 // PRIO (A/B, DSTACK_AMD_FA_PRIO): 0 = no priority games; 1 = a wave raises its issue priority
 // (s_setprio) for its MFMA phases, so of the two waves on a SIMD the one with matrix work queues
 // it first and the other's softmax VALU fills the gaps; 2 = the softmax phase gets the priority.
+// Measured (3 interleaved runs, S=8192, profiles/fa_prio_ab_r4r.txt): 0 = 0.641-0.650 ms,
+// 1 = 0.659-0.665, 2 = 0.657-0.658 -- both slower, kept opt-in only.
 template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
