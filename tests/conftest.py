@@ -16,6 +16,44 @@ os.environ["DSTACK_SERVER_NO_CLIENT_CONFIG"] = "1"
 # (tests/test_catalog.py); the catalog cache never touches the real ~/.dstack
 os.environ["DSTACK_CATALOG_OFFLINE_ONLY"] = "1"
 os.environ["DSTACK_CATALOG_CACHE_DIR"] = os.path.join(_TMP_HOME, "catalog")
+# placeholder cloud credentials are not sent to the clouds (tests/test_backends_api.py opts in)
+os.environ["DSTACK_SKIP_BACKEND_VALIDATION"] = "1"
+
+# No test touches the network (the reference runs pytest-socket with --allow-hosts=127.0.0.1):
+# connections and name lookups are limited to loopback and unix sockets in the test process.
+import socket as _socket  # noqa: E402
+
+_LOCAL = {"127.0.0.1", "::1", "localhost", "0.0.0.0", "::", "", None}
+_orig_connect, _orig_connect_ex = _socket.socket.connect, _socket.socket.connect_ex
+_orig_getaddrinfo = _socket.getaddrinfo
+
+
+def _check_addr(sock, addr):
+    if sock.family in (_socket.AF_INET, _socket.AF_INET6) and isinstance(addr, tuple) and addr[0] not in _LOCAL:
+        raise ConnectionRefusedError(f"network access disabled in tests: {addr[0]}")
+
+
+def _guarded_connect(self, addr):
+    _check_addr(self, addr)
+    return _orig_connect(self, addr)
+
+
+def _guarded_connect_ex(self, addr):
+    _check_addr(self, addr)
+    return _orig_connect_ex(self, addr)
+
+
+def _guarded_getaddrinfo(host, *a, **kw):
+    h = host.decode() if isinstance(host, bytes) else host
+    if h not in _LOCAL and not (isinstance(h, str) and h.startswith("127.")):
+        raise _socket.gaierror(_socket.EAI_NONAME, f"name resolution disabled in tests: {h}")
+    return _orig_getaddrinfo(host, *a, **kw)
+
+
+if os.environ.get("DSTACK_TESTS_ALLOW_NETWORK") != "1":
+    _socket.socket.connect = _guarded_connect
+    _socket.socket.connect_ex = _guarded_connect_ex
+    _socket.getaddrinfo = _guarded_getaddrinfo
 
 ADMIN_TOKEN = "test-admin-token"
 

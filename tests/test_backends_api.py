@@ -38,7 +38,7 @@ SECRET_VALUES = {"s3", "cs", "k", "t", "tok", "s", "apiVersion: v1\n"}
 @pytest.mark.parametrize("btype", sorted(VALID))
 def test_create_each_backend_secrets_kept_apart(client, btype, monkeypatch):
     # placeholder credentials: storage / secret separation is under test, not the cloud's verdict
-    monkeypatch.setenv("DSTACK_SKIP_BACKEND_VALIDATION", "1")
+    # (conftest sets DSTACK_SKIP_BACKEND_VALIDATION for every test)
     r = client.post("/api/project/main/backends/create", json=VALID[btype])
     assert r.status_code == 200, r.text
     info = client.post(f"/api/project/main/backends/{btype}/config_info").json()
@@ -133,6 +133,7 @@ def test_backend_credentials_validated_on_create(client, monkeypatch):
     ``invalid_credentials``; unreachable API (air-gapped server) -> stored with a warning."""
     import httpx
 
+    monkeypatch.delenv("DSTACK_SKIP_BACKEND_VALIDATION", raising=False)
     from dstack_amd.core.backends.clouds import rest_vm
 
     calls = []
