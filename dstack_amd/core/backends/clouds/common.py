@@ -78,7 +78,7 @@ class CatalogOffers:
 
     def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
         fetch = self._fetch_catalog if self.has_online_catalog() else None
-        offers = get_catalog_offers(self.TYPE, self.config.get("regions"), requirements, self.CONFIGURABLE_DISK,
+        offers = get_catalog_offers(self.TYPE, self.regions(), requirements, self.CONFIGURABLE_DISK,
                                     extra_filter=self._offer_filter, fetch=fetch, cache_key=self.catalog_key())
         avail = self._availability()
         for o in offers:
@@ -86,6 +86,10 @@ class CatalogOffers:
             if a is not None:
                 o.availability = a
         return offers
+
+    def regions(self) -> Optional[List[str]]:
+        """Configured region filter (``regions``; Azure's configs call them ``locations``)."""
+        return self.config.get("regions") or self.config.get("locations")
 
     def has_online_catalog(self) -> bool:
         """True when the backend implements a live listing and it is not switched off

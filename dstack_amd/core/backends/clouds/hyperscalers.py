@@ -83,7 +83,7 @@ class AzureCompute(VMCompute):
         for r in base:
             specs.setdefault(r.instance_name, r)
         prices = self._retail_prices(sorted(specs))
-        wanted = self.config.get("regions")
+        wanted = self.regions()
         restricted = self._restricted_skus() if self.subscription else {}
         out = []
         for (sku, region, spot), price in sorted(prices.items()):

@@ -416,6 +416,12 @@ def test_azure_live_retail_prices_and_restrictions(live):
     assert offers[("eastus", False)].instance.resources.cpus == 96
 
 
+def test_azure_locations_filter_offers():
+    """Azure configs name their regions ``locations``; they filter the offers like ``regions``."""
+    c = compute_class(BackendType.AZURE)({"locations": ["westus"], "subscription_id": "s", "tenant_id": "t"}, {})
+    assert {o.region for o in c.get_offers(_req(gpu="MI300X:8"))} == {"westus"}
+
+
 def test_gcp_live_machine_types_and_launch_zone(live, monkeypatch):
     from dstack_amd.core.backends.clouds import hyperscalers
 
