@@ -275,6 +275,27 @@ std::vector<AmdGpuMetrics> AmdSmi::metrics() {
   return out;
 }
 
+Json gpu_metrics_to_json(const AmdGpuMetrics& g) {
+  Json j = Json::object();
+  j.set("gpu_memory_usage_bytes", (long long)g.vram_used_bytes);
+  j.set("gpu_memory_total_bytes", (long long)g.vram_total_bytes);
+  j.set("gpu_util_percent", g.util_percent);
+  j.set("gpu_power_watts", g.power_w);
+  j.set("gpu_temperature_c", g.temp_c);
+  if (g.mem_activity_percent >= 0) j.set("gpu_mem_activity_percent", g.mem_activity_percent);
+  if (g.xgmi_links_total > 0 || g.xgmi_read_kb || g.xgmi_write_kb) {
+    Json x = Json::object();
+    x.set("links_total", g.xgmi_links_total);
+    x.set("links_up", g.xgmi_links_up);
+    x.set("link_speed_gbps", g.xgmi_link_speed_gbps);
+    x.set("link_width", g.xgmi_link_width);
+    x.set("read_kb", (long long)g.xgmi_read_kb);
+    x.set("write_kb", (long long)g.xgmi_write_kb);
+    j.set("xgmi", x);
+  }
+  return j;
+}
+
 std::vector<AmdGpu> discover_amd_gpus_sysfs() {
   std::vector<AmdGpu> out;
   // DSTACK_SYSFS_ROOT: a fake /sys tree (tests)

@@ -72,6 +72,8 @@ std::vector<AmdGpu> discover_amd_gpus_sysfs();
 std::vector<AmdGpu> discover_amd_gpus();
 
 Json gpu_to_json(const AmdGpu& g);
+// one GPU's sample in the runner's metrics wire format (gpu_* keys, optional "xgmi" object)
+Json gpu_metrics_to_json(const AmdGpuMetrics& m);
 
 // xGMI fields of AmdGpuMetrics from amdsmi gpu_metrics / link status (either may be null;
 // all-ones fields are "not reported")

@@ -298,6 +298,16 @@ int main(int argc, char** argv) {
       j.set("sysfs", sys);
       printf("%s\n", j.dump().c_str());
       return 0;
+    } else if (a == "--gpu-metrics") {  // one amdsmi sample per GPU (runner wire format), then exit
+      Json arr = Json::array();
+      if (AmdSmi::instance().available())
+        for (auto& m : AmdSmi::instance().metrics()) {
+          Json j = gpu_metrics_to_json(m);
+          j.set("index", m.index);
+          arr.push_back(j);
+        }
+      printf("%s\n", arr.dump().c_str());
+      return 0;
     } else if (a == "--host-info") {  // print host_info.json and exit (used by SSH-fleet deploy)
       printf("%s\n", collect_host_info("/").dump().c_str());
       return 0;
