@@ -98,11 +98,15 @@ class ModelSpec:
     bos_token_id: int | None = None
     eos_token_ids: tuple = ()
     path: str | None = None  # HF checkpoint directory (None: random init)
+    family: str = "llama"  # llama | mistral | qwen2 (same block; qwen2 adds q/k/v biases)
+    qkv_bias: bool = False
 
 
 def load_spec(model: str) -> ModelSpec:
     """``model`` is a built-in config name (``llama-3-8b``, ``llama-3-70b``, …: random weights) or an
-    HF Llama checkpoint directory (``config.json`` + ``*.safetensors``)."""
+    HF checkpoint directory (``config.json`` + ``*.safetensors``) of the Llama block family: Llama
+    2/3/3.x, Mistral (sliding-window models are served up to their window) and Qwen2 / Qwen2.5
+    (q/k/v projection biases)."""
     if model in CONFIGS:
         return ModelSpec(CONFIGS[model], eos_token_ids=())
     cfg_path = os.path.join(model, "config.json")
@@ -112,8 +116,9 @@ def load_spec(model: str) -> ModelSpec:
     with open(cfg_path) as f:
         hf = json.load(f)
     arch = (hf.get("architectures") or ["LlamaForCausalLM"])[0]
-    if hf.get("model_type", "llama") not in ("llama",) and "Llama" not in arch:
-        raise ValueError(f"unsupported architecture {arch} (Llama family only)")
+    family = hf.get("model_type", "llama")
+    if family not in SUPPORTED_FAMILIES:
+        raise ValueError(f"unsupported architecture {arch} (Llama family only: {', '.join(SUPPORTED_FAMILIES)})")
     heads = hf["num_attention_heads"]
     dim = hf["hidden_size"]
     head_dim = hf.get("head_dim") or dim // heads
@@ -122,11 +127,19 @@ def load_spec(model: str) -> ModelSpec:
     # rope: ``rope_theta`` + ``rope_scaling`` (transformers 4.x) or ``rope_parameters`` (5.x)
     rp = hf.get("rope_parameters") or {}
     theta = hf.get("rope_theta", rp.get("rope_theta", 10000.0))
+    max_len = int(hf.get("max_position_embeddings", 8192))
+    # sliding-window attention (Mistral v0.1, Qwen2 with use_sliding_window): up to the window it is
+    # full causal attention, so such a model is served with max_model_len <= window
+    window = hf.get("sliding_window")
+    if window and (family == "mistral" or hf.get("use_sliding_window")):
+        max_len = min(max_len, int(window))
+    if hf.get("hidden_act", "silu") != "silu":
+        raise ValueError(f"unsupported activation {hf.get('hidden_act')} (SwiGLU / silu only)")
     cfg = LlamaConfig(
         name=os.path.basename(os.path.normpath(model)), dim=dim, n_layers=hf["num_hidden_layers"], n_heads=heads,
         n_kv_heads=hf.get("num_key_value_heads", heads), ffn_dim=hf["intermediate_size"],
         vocab_size=hf["vocab_size"], rope_theta=float(theta),
-        norm_eps=float(hf.get("rms_norm_eps", 1e-5)), max_seq_len=int(hf.get("max_position_embeddings", 8192)),
+        norm_eps=float(hf.get("rms_norm_eps", 1e-5)), max_seq_len=max_len,
     )
     rs = hf.get("rope_scaling") or (rp if rp.get("rope_type", "default") != "default" else None)
     scaling = None
@@ -141,7 +154,10 @@ def load_spec(model: str) -> ModelSpec:
     eos = hf.get("eos_token_id")
     eos_ids = tuple(eos) if isinstance(eos, list) else ((eos,) if eos is not None else ())
     return ModelSpec(cfg, scaling, bool(hf.get("tie_word_embeddings", False)), hf.get("bos_token_id"), eos_ids,
-                     path=model)
+                     path=model, family=family, qkv_bias=family == "qwen2")
+
+
+SUPPORTED_FAMILIES = ("llama", "mistral", "qwen2")
 
 
 class ServingLlama:
@@ -210,6 +226,9 @@ class ServingLlama:
                  ffn_norm=self._empty(d), wgu=self._empty(2 * self.F, d), wdown=self._empty(d, self.F))
             for _ in range(cfg.n_layers)
         ]
+        if self.spec.qkv_bias:
+            for L in self.layers:
+                L["bqkv"] = self._empty(self.NH * hd)
 
     # ---- tensor-parallel sharding of full (unsharded) tensors ----
     def _shard(self, kind: str, t: torch.Tensor) -> torch.Tensor:
@@ -254,6 +273,10 @@ class ServingLlama:
             L["wgu"].copy_(torch.cat([self._shard("gate", full[: cfg.ffn_dim]), self._shard("up", full[cfg.ffn_dim :])]))
             L["wo"].copy_(self._shard("wo", draw(f"{i}.wo", (cfg.dim, cfg.n_heads * hd), out_std)))
             L["wdown"].copy_(self._shard("wdown", draw(f"{i}.wdown", (cfg.dim, cfg.ffn_dim), out_std)))
+            if self.spec.qkv_bias:
+                b = draw(f"{i}.bqkv", ((cfg.n_heads + 2 * cfg.n_kv_heads) * hd,), std)
+                bq, bk, bv = b.split([cfg.n_heads * hd, cfg.n_kv_heads * hd, cfg.n_kv_heads * hd])
+                L["bqkv"].copy_(torch.cat([self._shard("q", bq), self._shard("k", bk), self._shard("v", bv)]))
             del full, q, k, v
         return self
 
@@ -303,6 +326,11 @@ class ServingLlama:
                             put(L["wqkv"][(H + KVH) * hd :], t, "v")
                         elif key == "self_attn.o_proj.weight":
                             put(L["wo"], t, "wo")
+                        elif key in ("self_attn.q_proj.bias", "self_attn.k_proj.bias", "self_attn.v_proj.bias") \
+                                and self.spec.qkv_bias:
+                            kind = key.split(".")[1][0]
+                            lo = {"q": 0, "k": H * hd, "v": (H + KVH) * hd}[kind]
+                            put(L["bqkv"][lo : lo + (H if kind == "q" else KVH) * hd], t, kind)
                         elif key == "mlp.gate_proj.weight":
                             put(L["wgu"][:f], t, "gate")
                         elif key == "mlp.up_proj.weight":
@@ -320,6 +348,8 @@ class ServingLlama:
             expected |= {f"model.layers.{i}.{k}.weight" for k in (
                 "input_layernorm", "post_attention_layernorm", "self_attn.q_proj", "self_attn.k_proj",
                 "self_attn.v_proj", "self_attn.o_proj", "mlp.gate_proj", "mlp.up_proj", "mlp.down_proj")}
+            if self.spec.qkv_bias:
+                expected |= {f"model.layers.{i}.self_attn.{p}_proj.bias" for p in "qkv"}
         missing = expected - seen
         if missing:
             raise ValueError(f"checkpoint {path} is missing {len(missing)} tensors, e.g. {sorted(missing)[:3]}")
@@ -504,6 +534,8 @@ class ServingLlama:
             else:
                 x, h = self._add_rms(x, delta, L["attn_norm"], next_w=L["wqkv"])
             qkv = self._mm(h, L["wqkv"]) if isinstance(L["wqkv"], Fp8Weight) else h @ L["wqkv"].t()
+            if "bqkv" in L:
+                qkv = qkv + L["bqkv"]
             sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH,
                                   self.k_scale, self.v_scale)
             o = torch.empty(rows, H * self.D, dtype=x.dtype, device=x.device)
@@ -532,6 +564,8 @@ class ServingLlama:
             else:
                 x, h = self._add_rms(x, delta, L["attn_norm"], next_w=L["wqkv"])
             qkv = self._mm(h, L["wqkv"])
+            if "bqkv" in L:
+                qkv = qkv + L["bqkv"]
             sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH,
                                   self.k_scale, self.v_scale)
             o = sops.paged_decode(qkv, self.k_cache[li], self.v_cache[li], block_tables, ctx_lens, H, KVH, ws=ws,

@@ -81,6 +81,60 @@ def test_checkpoint_loader_rejects_incomplete(tmp_path):
         m.load_hf()
 
 
+def _hf_family_tiny(tmp_path, family):
+    transformers = pytest.importorskip("transformers")
+    common = dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=2,
+                  num_key_value_heads=1, vocab_size=512, max_position_embeddings=1024, rope_theta=1000000.0,
+                  eos_token_id=2, bos_token_id=1)
+    if family == "mistral":
+        cfg = transformers.MistralConfig(head_dim=128, sliding_window=512, **common)
+        cls = transformers.MistralForCausalLM
+    else:
+        cfg = transformers.Qwen2Config(use_sliding_window=False, **common)
+        cls = transformers.Qwen2ForCausalLM
+    torch.manual_seed(0)
+    m = cls(cfg).eval()
+    with torch.no_grad():
+        for name, p in m.named_parameters():
+            if p.dim() == 2:
+                p.normal_(0, 0.08)
+            elif name.endswith("bias"):
+                p.normal_(0, 0.5)  # Qwen2's q/k/v biases: make them matter
+    path = tmp_path / family
+    m.save_pretrained(str(path))
+    return m, str(path)
+
+
+@pytest.mark.parametrize("family", ["mistral", "qwen2"])
+def test_hf_parity_other_llama_block_families(tmp_path, family):
+    """Mistral and Qwen2 (q/k/v biases) checkpoints: greedy decode through the paged engine equals
+    the transformers model; a sliding-window Mistral is capped at its window."""
+    hf, path = _hf_family_tiny(tmp_path, family)
+    spec = load_spec(path)
+    assert spec.family == family and spec.qkv_bias == (family == "qwen2")
+    if family == "mistral":
+        assert spec.cfg.max_seq_len == 512
+    eng = LLMEngine.from_model(path, device="cpu", max_model_len=256, max_batch=4, num_pages=32)
+    prompts = [[1, 5, 9, 33, 7, 100, 2, 45, 61], [1, 300, 301, 302]]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=10, temperature=0, ignore_eos=True))
+    for p, r in zip(prompts, outs):
+        with torch.no_grad():
+            ref = hf.generate(torch.tensor([p]), max_new_tokens=10, do_sample=False, eos_token_id=None,
+                              pad_token_id=0)[0, len(p):].tolist()
+        assert r.output_ids == ref, (family, r.output_ids, ref)
+
+
+def test_qwen2_checkpoint_needs_its_biases(tmp_path):
+    from safetensors.torch import load_file, save_file
+
+    _, path = _hf_family_tiny(tmp_path, "qwen2")
+    sd = load_file(f"{path}/model.safetensors")
+    sd.pop("model.layers.0.self_attn.k_proj.bias")
+    save_file(sd, f"{path}/model.safetensors")
+    with pytest.raises(ValueError, match="missing 1 tensors"):
+        ServingLlama(load_spec(path), "cpu").load_hf()
+
+
 def test_spec_rejects_non_llama(tmp_path):
     (tmp_path / "config.json").write_text(json.dumps({"model_type": "gpt2", "architectures": ["GPT2LMHeadModel"],
                                                       "num_attention_heads": 2, "hidden_size": 256}))
@@ -199,28 +253,33 @@ def _tp_worker(rank, world, port, model, q):
         dist.destroy_process_group()
 
 
-def _hf_tiny_tp(tmp_path):
+def _hf_tiny_tp(tmp_path, family="llama"):
     transformers = pytest.importorskip("transformers")
-    cfg = transformers.LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2,
-                                   num_attention_heads=4, num_key_value_heads=2, vocab_size=512,
-                                   max_position_embeddings=1024, rope_theta=500000.0, head_dim=128)
+    common = dict(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=4,
+                  num_key_value_heads=2, vocab_size=512, max_position_embeddings=1024, rope_theta=500000.0)
+    if family == "qwen2":
+        m_cls, cfg = transformers.Qwen2ForCausalLM, transformers.Qwen2Config(use_sliding_window=False, **common)
+    else:
+        m_cls, cfg = transformers.LlamaForCausalLM, transformers.LlamaConfig(head_dim=128, **common)
     torch.manual_seed(1)
-    m = transformers.LlamaForCausalLM(cfg)
+    m = m_cls(cfg)
     with torch.no_grad():
-        for p in m.parameters():
+        for name, p in m.named_parameters():
             if p.dim() == 2:
                 p.normal_(0, 0.06)
+            elif name.endswith("bias"):
+                p.normal_(0, 0.5)
     m.save_pretrained(str(tmp_path / "hftp"))
     return str(tmp_path / "hftp")
 
 
-@pytest.mark.parametrize("source", ["random", "hf"])
+@pytest.mark.parametrize("source", ["random", "hf", "hf-qwen2"])
 def test_tensor_parallel_matches_single_process(tmp_path, source):
     import torch.multiprocessing as mp
 
     from dstack_amd.server.testing import free_port
 
-    model = "llama-tiny" if source == "random" else _hf_tiny_tp(tmp_path)
+    model = "llama-tiny" if source == "random" else _hf_tiny_tp(tmp_path, "qwen2" if source == "hf-qwen2" else "llama")
     single = LLMEngine.from_model(model, device="cpu", max_model_len=256, max_batch=4, num_pages=24)
     prompts = [[1, 5, 9, 33, 7, 100, 2, 45, 61], [1, 300, 301, 302], list(range(3, 140))]
     want = [r.output_ids for r in single.generate(prompts, SamplingParams(max_tokens=10, temperature=0,
@@ -438,10 +497,11 @@ def test_gpu_sample_kernel(gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_engine_matches_cpu_and_graphs(gpu, tmp_path):
-    """Tiny HF Llama on the HIP path: prefill logits close to the fp32 CPU engine; greedy tokens
-    with and without hipGraphs identical."""
-    hf, path = _hf_tiny(tmp_path)
+@pytest.mark.parametrize("family", ["llama", "qwen2", "mistral"])
+def test_gpu_engine_matches_cpu_and_graphs(gpu, tmp_path, family):
+    """Tiny HF Llama / Qwen2 (biases) / Mistral on the HIP path: greedy tokens with and without
+    hipGraphs identical, first token = the fp32 HF argmax up to bf16 near-ties."""
+    hf, path = _hf_tiny(tmp_path) if family == "llama" else _hf_family_tiny(tmp_path, family)
     prompts = [[1, 5, 9, 33, 7, 100, 2, 45, 61], [1, 300, 301, 302], list(range(1, 200))]
     sp = SamplingParams(max_tokens=20, temperature=0, ignore_eos=True)
     g = LLMEngine.from_model(path, device="cuda", max_model_len=512, max_batch=8, num_pages=64)
