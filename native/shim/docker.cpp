@@ -27,6 +27,10 @@ bool docker_available(const std::string& socket_path) {
 std::string container_bootstrap_script(const ShimOptions& o, const std::vector<std::string>& keys) {
   std::string authorized;
   for (auto& k : keys) authorized += k + "\n";
+  // single-quoted for the shell: a key comment may contain a quote ("alice's laptop")
+  std::string quoted;
+  for (char c : authorized) quoted += c == '\'' ? std::string("'\\''") : std::string(1, c);
+  authorized = quoted;
   std::ostringstream s;
   s << "set -e\n"
     << "export DEBIAN_FRONTEND=noninteractive\n"

@@ -350,6 +350,48 @@ int main() {
     CHECK(msg.find("/dev/kfd") != std::string::npos);
   });
 
+  run("container bootstrap script runs: keys (quotes included), sshd flags, runner exec", [] {
+    ShimOptions o;
+    o.runner_ssh_port = 10022;
+    o.runner_http_port = 10999;
+    std::string script = container_bootstrap_script(o, {"ssh-ed25519 AAAAkey1 alice's laptop", "ssh-rsa AAAAkey2"});
+    char tmpl[] = "/tmp/dsa_boot_XXXXXX";
+    std::string dir = mkdtemp(tmpl);
+    std::string bin = dir + "/bin", home = dir + "/home", log = dir + "/calls.log";
+    mkdirs(bin);
+    mkdirs(home);
+    // stand-ins: sshd / ssh-keygen record their argv; the runner path and /run/sshd are redirected
+    auto stub = [&](const std::string& name) {
+      write_file(bin + "/" + name, "#!/bin/sh\necho \"" + name + " $*\" >> " + log + "\n", 0755);
+    };
+    stub("sshd");
+    stub("ssh-keygen");
+    stub("dstack-runner");
+    auto replace_all = [](std::string s, const std::string& a, const std::string& b) {
+      for (size_t p = s.find(a); p != std::string::npos; p = s.find(a, p + b.size())) s.replace(p, a.size(), b);
+      return s;
+    };
+    script = replace_all(script, "/usr/local/bin/dstack-runner", bin + "/dstack-runner");
+    script = replace_all(script, "/run/sshd", dir + "/run-sshd");
+    write_file(dir + "/boot.sh", script, 0755);
+    std::string cmd = "env -i HOME=" + home + " PATH=" + bin + ":/usr/bin:/bin sh " + dir + "/boot.sh 2>&1";
+    FILE* f = popen(cmd.c_str(), "r");
+    char buf[512];
+    std::string out;
+    while (f && fgets(buf, sizeof buf, f)) out += buf;
+    int rc = f ? pclose(f) : -1;
+    CHECK(rc == 0);
+    std::string keys, calls;
+    read_file(home + "/.ssh/authorized_keys", keys);
+    read_file(log, calls);
+    CHECK(keys == "ssh-ed25519 AAAAkey1 alice's laptop\nssh-rsa AAAAkey2\n");
+    CHECK(calls.find("ssh-keygen -A") != std::string::npos);
+    CHECK(calls.find("sshd -p 10022 -o PermitUserEnvironment=yes -o PasswordAuthentication=no") != std::string::npos);
+    CHECK(calls.find("dstack-runner --log-level") != std::string::npos);
+    CHECK(calls.find("start --http-port 10999 --temp-dir /tmp/runner --home-dir " + home) != std::string::npos);
+    if (rc != 0) fprintf(stderr, "%s\n%s\n", script.c_str(), out.c_str());
+  });
+
   run("docker restore rebuilds tasks and the GPU lock from labels", [] {
     FakeDocker fd([](const Req& r) {
       if (r.method == "GET" && r.target.rfind("/containers/json", 0) == 0) {
