@@ -190,7 +190,7 @@ def get_shim_commands(authorized_keys: List[str], shim_url: str, runner_url: str
 
 def get_user_data(authorized_keys: List[str], shim_url: str, runner_url: str) -> str:
     cmds = get_shim_commands(authorized_keys, shim_url, runner_url)
-    keys = "\n".join(f"  - {k}" for k in authorized_keys)
+    keys = "\n".join(f"  - {json_quote(k)}" for k in authorized_keys)  # a YAML-safe scalar whatever the comment
     runcmd = "\n".join(f"  - {json_quote(c)}" for c in cmds)
     return f"#cloud-config\nssh_authorized_keys:\n{keys}\nruncmd:\n{runcmd}\n"
 
@@ -204,12 +204,14 @@ def json_quote(s: str) -> str:
 def get_docker_commands(authorized_keys: List[str], runner_url: str) -> List[str]:
     """Container-only backends (runpod/vastai/k8s): install sshd and start the runner directly
     (compute.py:334-387)."""
-    keys = "\\n".join(authorized_keys)
+    import shlex
+
+    keys = shlex.quote("".join(k + "\n" for k in authorized_keys))  # comments may hold quotes
     return [
         "export DEBIAN_FRONTEND=noninteractive",
         "(command -v sshd || (apt-get update -qq && apt-get install -yqq openssh-server)) >/dev/null 2>&1",
         "mkdir -p ~/.ssh /run/sshd && chmod 700 ~/.ssh",
-        f"printf '{keys}\\n' >> ~/.ssh/authorized_keys && chmod 600 ~/.ssh/authorized_keys",
+        f"printf '%s' {keys} >> ~/.ssh/authorized_keys && chmod 600 ~/.ssh/authorized_keys",
         f"$(command -v sshd) -p {DSTACK_RUNNER_SSH_PORT} -o PermitUserEnvironment=yes",
         f"curl -fsSL -o /usr/local/bin/dstack-runner '{runner_url}' && chmod +x /usr/local/bin/dstack-runner",
         f"/usr/local/bin/dstack-runner start --http-port {DSTACK_RUNNER_HTTP_PORT} --temp-dir /tmp/runner "

@@ -706,3 +706,26 @@ def test_capability_lists_match_implementations():
         cls = cls_of(bt)
         for m in ("create_volume", "delete_volume", "register_volume"):
             assert getattr(cls, m) is not getattr(Compute, m), f"{bt.value} advertises volumes without {m}"
+
+
+def test_bootstrap_scripts_quote_ssh_keys(tmp_path):
+    """Keys whose comments hold quotes, colons or '#' survive cloud-init YAML and the container
+    bootstrap's shell (reference: compute.py get_user_data / get_docker_commands)."""
+    import subprocess
+
+    import yaml
+
+    from dstack_amd.core.backends.base import get_docker_commands, get_user_data
+
+    keys = ["ssh-ed25519 AAAAone alice's laptop", "ssh-rsa AAAAtwo build: #42 $(touch pwned)"]
+    doc = yaml.safe_load(get_user_data(keys, "https://x/shim", "https://x/runner"))
+    assert doc["ssh_authorized_keys"] == keys
+    cmds = get_docker_commands(keys, "https://x/runner")
+    step = next(c for c in cmds if "authorized_keys" in c and "printf" in c)
+    home = tmp_path / "home"
+    (home / ".ssh").mkdir(parents=True)
+    r = subprocess.run(["sh", "-c", step], env={"HOME": str(home), "PATH": "/usr/bin:/bin"}, cwd=tmp_path,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert (home / ".ssh" / "authorized_keys").read_text() == "".join(k + "\n" for k in keys)
+    assert not (tmp_path / "pwned").exists()
