@@ -448,31 +448,45 @@ class AWSCompute(VMCompute):
 
     # ---- gateway ------------------------------------------------------------------------------
     def create_gateway(self, configuration: GatewayComputeConfiguration) -> GatewayProvisioningData:
+        """A small VM running the gateway package.  ``public_ip: false`` (private gateway): it is
+        launched into the configured VPC's subnets without a public address and served on its
+        private IP (reachable from inside the VPC, e.g. behind an internal load balancer)."""
+        import time
+
         from dstack_amd.core.backends.clouds.gateway_boot import gateway_cloud_init
 
         region = configuration.region
+        public = configuration.public_ip
+        sg = self._gateway_security_group(region, configuration.project_name, self._vpc_id(region))
         params = {"ImageId": self._image_id(region, False), "InstanceType": "t3.small", "MinCount": "1",
                   "MaxCount": "1", "UserData": base64.b64encode(gateway_cloud_init(configuration).encode()).decode(),
-                  "SecurityGroupId.1": self._gateway_security_group(region, configuration.project_name),
                   "TagSpecification.1.ResourceType": "instance", "TagSpecification.1.Tag.1.Key": "Name",
                   "TagSpecification.1.Tag.1.Value": configuration.instance_name}
+        subnets = self._subnets(region, self._vpc_id(region), public)
+        if subnets or not public:
+            if not subnets:
+                raise ComputeError(f"a private gateway needs vpc_name / vpc_ids / subnet_ids for {region}")
+            params.update({"NetworkInterface.1.DeviceIndex": "0", "NetworkInterface.1.SubnetId": subnets[0][0],
+                           "NetworkInterface.1.AssociatePublicIpAddress": "true" if public else "false",
+                           "NetworkInterface.1.SecurityGroupId.1": sg})
+        else:
+            params["SecurityGroupId.1"] = sg
         root = self._call(region, "RunInstances", params)
         iid = root.findtext(".//instancesSet/item/instanceId")
         ip = None
         for _ in range(60):
-            info = self._describe(iid, region, {})
+            info = self._describe(iid, region, {"public_ip": public})
             if info.get("hostname"):
                 ip = info["hostname"]
                 break
-            import time
-
-            time.sleep(5)
+            time.sleep(float(self.config.get("gateway_poll_s", 5)))
         if ip is None:
-            raise ComputeError(f"gateway {iid} got no public IP")
-        return GatewayProvisioningData(instance_id=iid, ip_address=ip, region=region)
+            raise ComputeError(f"gateway {iid} got no {'public' if public else 'private'} IP")
+        return GatewayProvisioningData(instance_id=iid, ip_address=ip, region=region,
+                                       backend_data=json.dumps({"public_ip": public}))
 
-    def _gateway_security_group(self, region: str, project: str) -> str:
-        gid = self._security_group(region, f"{project}_gateway")
+    def _gateway_security_group(self, region: str, project: str, vpc_id: Optional[str] = None) -> str:
+        gid = self._security_group(region, f"{project}_gateway", vpc_id)
         for port in ("80", "443"):
             try:
                 self._call(region, "AuthorizeSecurityGroupIngress", {

@@ -41,6 +41,8 @@ BACKENDS_WITH_PLACEMENT_GROUPS_SUPPORT = [BackendType.AWS]
 BACKENDS_WITH_RESERVATION_SUPPORT = [BackendType.AWS]
 BACKENDS_WITH_GATEWAY_SUPPORT = [BackendType.AWS, BackendType.AZURE, BackendType.GCP, BackendType.KUBERNETES,
                                  BackendType.LOCAL]
+# gateways without a public IP (reached from inside the VPC), reference: AWS only
+BACKENDS_WITH_PRIVATE_GATEWAY_SUPPORT = [BackendType.AWS, BackendType.LOCAL]
 # SSH fleets (remote) have no network-volume API: they use instance mounts (``/host/path:/path``)
 BACKENDS_WITH_VOLUMES_SUPPORT = [BackendType.AWS, BackendType.GCP, BackendType.LOCAL, BackendType.RUNPOD]
 BACKENDS_WITH_PRIVILEGED_SUPPORT = [b for b in BackendType if b not in (BackendType.RUNPOD, BackendType.VASTAI)]

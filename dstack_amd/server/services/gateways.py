@@ -17,7 +17,11 @@ from sqlalchemy import select
 from sqlalchemy.orm import Session
 
 from dstack_amd.core.errors import GatewayError, ResourceExistsError, ResourceNotExistsError, ServerClientError
-from dstack_amd.core.models.backends import BACKENDS_WITH_GATEWAY_SUPPORT, BackendType
+from dstack_amd.core.models.backends import (
+    BACKENDS_WITH_GATEWAY_SUPPORT,
+    BACKENDS_WITH_PRIVATE_GATEWAY_SUPPORT,
+    BackendType,
+)
 from dstack_amd.core.models.gateways import (
     Gateway,
     GatewayConfiguration,
@@ -63,6 +67,8 @@ def get_plan(s: Session, project: ProjectModel, user: UserModel, spec: GatewaySp
 def create_gateway(s: Session, project: ProjectModel, conf: GatewayConfiguration) -> Gateway:
     if conf.backend not in BACKENDS_WITH_GATEWAY_SUPPORT:
         raise ServerClientError(f"Backend {conf.backend.value} does not support gateways")
+    if not conf.public_ip and conf.backend not in BACKENDS_WITH_PRIVATE_GATEWAY_SUPPORT:
+        raise ServerClientError(f"Backend {conf.backend.value} does not support gateways without a public IP")
     if conf.name is None:
         conf.name = generate_name()
     if get_gateway_by_name(s, project, conf.name) is not None:

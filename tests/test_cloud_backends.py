@@ -729,3 +729,53 @@ def test_bootstrap_scripts_quote_ssh_keys(tmp_path):
     assert r.returncode == 0, r.stderr
     assert (home / ".ssh" / "authorized_keys").read_text() == "".join(k + "\n" for k in keys)
     assert not (tmp_path / "pwned").exists()
+
+
+@pytest.mark.parametrize("public", [True, False])
+def test_aws_gateway_public_and_private(public):
+    """AWS gateways: public in the default VPC; ``public_ip: false`` goes into the named VPC's
+    subnet with no public address and is served on its private IP (reference: AWS is the backend
+    with private gateways)."""
+    from dstack_amd.core.models.gateways import GatewayComputeConfiguration
+
+    calls = []
+
+    def handler(req):
+        form = dict(urllib.parse.parse_qsl(req.content.decode()))
+        calls.append(form)
+        a = form["Action"]
+        if a == "DescribeImages":
+            return _ec2x("<imagesSet><item><imageId>ami-1</imageId><creationDate>2024</creationDate></item></imagesSet>")
+        if a == "DescribeSecurityGroups":
+            return _ec2x("<securityGroupInfo><item><groupId>sg-gw</groupId></item></securityGroupInfo>")
+        if a == "AuthorizeSecurityGroupIngress":
+            return _ec2x("<return>true</return>")
+        if a == "DescribeVpcs":
+            return _ec2x("<vpcSet><item><vpcId>vpc-9</vpcId></item></vpcSet>")
+        if a == "DescribeSubnets":
+            return _ec2x("<subnetSet><item><subnetId>subnet-priv</subnetId><availabilityZone>us-east-1a"
+                         "</availabilityZone><mapPublicIpOnLaunch>false</mapPublicIpOnLaunch></item></subnetSet>")
+        if a == "RunInstances":
+            return _ec2x("<instancesSet><item><instanceId>i-gw</instanceId></item></instancesSet>")
+        if a == "DescribeInstances":
+            return _ec2x("<reservationSet><item><instancesSet><item><instanceState><name>running</name></instanceState>"
+                         "<ipAddress>54.1.1.1</ipAddress><privateIpAddress>10.0.3.7</privateIpAddress>"
+                         "</item></instancesSet></item></reservationSet>")
+        return httpx.Response(400, text="<Response><Errors><Error><Code>X</Code></Error></Errors></Response>")
+
+    config = {} if public else {"vpc_name": "inner"}
+    c = compute_class(BackendType.AWS)(config, {"access_key": "a", "secret_key": "s"}, _client(handler))
+    conf = GatewayComputeConfiguration(project_name="main", instance_name="gw-1", backend=BackendType.AWS,
+                                       region="us-east-1", public_ip=public, ssh_key_pub="ssh-rsa AAA gw")
+    gpd = c.create_gateway(conf)
+    run = next(x for x in calls if x["Action"] == "RunInstances")
+    if public:
+        assert gpd.ip_address == "54.1.1.1" and run["SecurityGroupId.1"] == "sg-gw"
+    else:
+        assert gpd.ip_address == "10.0.3.7"
+        assert run["NetworkInterface.1.SubnetId"] == "subnet-priv"
+        assert run["NetworkInterface.1.AssociatePublicIpAddress"] == "false"
+
+
+def _ec2x(body):
+    return httpx.Response(200, text=f'<R xmlns="http://ec2.amazonaws.com/doc/2016-11-15/">{body}</R>')

@@ -269,3 +269,11 @@ def test_gateway_cloud_init_installs_versioned_package():
                                                         region="us-east-1", public_ip=True,
                                                         ssh_key_pub="ssh-rsa AAA x"))
     assert "dstack_amd-gateway-" in ci and "update.sh" in ci and "base64 -d > /etc/systemd/system/dstack-gateway" in ci
+
+
+def test_private_gateway_only_where_supported(client):
+    """``public_ip: false`` is refused up front on backends without private gateways."""
+    body = {"configuration": {"type": "gateway", "name": "gw-priv", "backend": "gcp", "region": "us-central1",
+                              "domain": "gw.example.com", "public_ip": False}}
+    r = client.post("/api/project/main/gateways/create", json=body)
+    assert r.status_code == 400 and "without a public IP" in r.text, r.text
