@@ -87,11 +87,18 @@ class Trainer:
         self.opt.install_prefetch_hooks(model)
         rank = dist.get_rank() if dist.is_initialized() else 0
         # data: "synthetic-lm" = a fresh structured batch every micro-step (workloads/data.py, the
-        # bench's data); "fixed" = ``data_rows`` uniform-random rows cycled (a memorisation check)
+        # bench's data); "tokens:<glob>" = token shards through the native loader (workloads/
+        # tokens.py); "fixed" = ``data_rows`` uniform-random rows cycled (a memorisation check)
         self.data_kind = data
         self.stream = None
         if data == "synthetic-lm":
             self.stream = SyntheticLM(self.cfg.vocab_size, seq_len, micro_batch, device, seed=1234 + rank)
+        elif data.startswith("tokens:"):
+            from dstack_amd.workloads.tokens import TokenShards
+
+            world = dist.get_world_size() if dist.is_initialized() else 1
+            self.stream = TokenShards(data.split(":", 1)[1], seq_len, micro_batch, device, seed=seed, rank=rank,
+                                      world=world, vocab_size=self.cfg.vocab_size)
         elif data == "fixed":
             g = torch.Generator(device=device).manual_seed(1234 + rank)
             n = micro_batch * (seq_len + 1)
@@ -272,7 +279,7 @@ def _sync(env: DistEnv):
 
 def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1,
         grad_accum: int = 1, checkpoint_dir: str | None = None, save_every: int = 0, lr: float = 3e-4,
-        lr_warmup: int = 300, lr_decay_steps: int = 0, clip_grad_norm: float = 0.0):
+        lr_warmup: int = 300, lr_decay_steps: int = 0, clip_grad_norm: float = 0.0, data: str = "synthetic-lm"):
     env = init_distributed()
     device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     from dstack_amd.ops import gemm_tuning
@@ -280,7 +287,7 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     gemm_mode = gemm_tuning.setup(device_index=env.local_rank if device.type == "cuda" else 0)
     t0 = time.time()
     tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum, lr=lr, lr_warmup=lr_warmup,
-                 lr_decay_steps=lr_decay_steps, clip_grad_norm=clip_grad_norm)
+                 lr_decay_steps=lr_decay_steps, clip_grad_norm=clip_grad_norm, data=data)
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
               f"init={time.time()-t0:.1f}s gemm_tuning={gemm_mode}", flush=True)
@@ -334,7 +341,7 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     result["tflops_per_gpu"] = tok_s / env.world * result["flops_per_token"] / 1e12
     result["losses"] = [round(x.item(), 4) for x in losses]  # read after the timed region
     result["warmup_losses"] = [round(x, 4) for x in warm_losses]
-    if tr.stream is not None:
+    if isinstance(tr.stream, SyntheticLM):
         result["loss_floor"] = round(tr.stream.loss_floor, 4)
         result["unigram_entropy"] = round(tr.stream.unigram_entropy, 4)
     result["gemm_tuning"] = gemm_mode
@@ -363,11 +370,13 @@ def main(argv=None):
     ap.add_argument("--lr-warmup", type=int, default=300, help="linear LR warmup (optimizer steps)")
     ap.add_argument("--lr-decay-steps", type=int, default=0, help="cosine decay to 0.1*lr at this step (0: constant)")
     ap.add_argument("--clip-grad-norm", type=float, default=0.0, help="global gradient-norm clipping (0: off)")
+    ap.add_argument("--data", default="synthetic-lm",
+                    help="synthetic-lm (structured synthetic stream) or tokens:<glob>[,<glob>] (token shards)")
     args = ap.parse_args(argv)
     env, tr, _ = run(args.model, args.seq_len, args.micro_batch, args.steps, args.warmup,
                      grad_accum=args.grad_accum, checkpoint_dir=args.checkpoint_dir, save_every=args.save_every,
                      lr=args.lr, lr_warmup=args.lr_warmup, lr_decay_steps=args.lr_decay_steps,
-                     clip_grad_norm=args.clip_grad_norm)
+                     clip_grad_norm=args.clip_grad_norm, data=args.data)
     if args.checkpoint_dir and not (args.save_every and tr.opt.step_count % args.save_every == 0):
         tr.save_checkpoint(args.checkpoint_dir)  # (a step that is a multiple of save_every is saved)
     if env.distributed:
