@@ -150,3 +150,66 @@ class TokenShards:
 def shard_paths_of(spec: str) -> Sequence[str]:
     """``tokens:<glob>[,<glob>...]`` -> shard paths."""
     return expand_paths(spec.split(":", 1)[1] if spec.startswith("tokens:") else spec)
+
+
+def tokenize_to_shards(tokenizer_path: str, inputs: Sequence[str], out_dir: str, shard_tokens: int = 100_000_000,
+                       eos_id: int | None = None, prefix: str = "shard") -> List[str]:
+    """Tokenize text files (one document per line, or whole files with ``--whole-files``) with an
+    HF ``tokenizer.json`` into shards of ``shard_tokens`` tokens (uint16 ids when the vocabulary
+    fits, uint32 otherwise), an end-of-text id between documents.  Returns the shard paths."""
+    from tokenizers import Tokenizer
+
+    tok = Tokenizer.from_file(tokenizer_path)
+    vocab = tok.get_vocab_size()
+    dtype = np.uint16 if vocab <= 65536 else np.uint32
+    os.makedirs(out_dir, exist_ok=True)
+    paths: List[str] = []
+    buf: List[int] = []
+
+    def flush(final=False):
+        while len(buf) >= shard_tokens or (final and buf):
+            chunk, buf[:] = buf[:shard_tokens], buf[shard_tokens:]
+            path = os.path.join(out_dir, f"{prefix}_{len(paths):05d}.bin")
+            write_shard(path, chunk, dtype)
+            paths.append(path)
+
+    for fn in inputs:
+        with open(fn, encoding="utf-8") as f:
+            for line in f:
+                line = line.rstrip("\n")
+                if not line:
+                    continue
+                buf.extend(tok.encode(line).ids)
+                if eos_id is not None:
+                    buf.append(eos_id)
+                if len(buf) >= shard_tokens:
+                    flush()
+    flush(final=True)
+    return paths
+
+
+def main(argv=None):
+    import argparse
+
+    ap = argparse.ArgumentParser(description="token shards for train_llama --data tokens:<glob>")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    t = sub.add_parser("tokenize", help="text files -> token shards")
+    t.add_argument("--tokenizer", required=True, help="HF tokenizer.json")
+    t.add_argument("--out", required=True)
+    t.add_argument("--shard-tokens", type=int, default=100_000_000)
+    t.add_argument("--eos-id", type=int, default=None)
+    t.add_argument("inputs", nargs="+")
+    i = sub.add_parser("info", help="token and window counts of shards")
+    i.add_argument("glob")
+    i.add_argument("--seq-len", type=int, default=8192)
+    a = ap.parse_args(argv)
+    if a.cmd == "tokenize":
+        for p in tokenize_to_shards(a.tokenizer, a.inputs, a.out, a.shard_tokens, a.eos_id):
+            print(p)
+    else:
+        ts = TokenShards(a.glob, a.seq_len, 1, "cpu")
+        print(f"{len(ts.paths)} shards, {ts.num_tokens} tokens, {ts.batches_per_epoch} windows of {a.seq_len}")
+
+
+if __name__ == "__main__":
+    main()

@@ -88,3 +88,22 @@ def test_token_shards_to_gpu_and_train_step(gpu, tmp_path):
     tr = Trainer("llama-tiny", 256, 2, gpu, data=f"tokens:{spec}", lr_warmup=2)
     losses = [tr.step().item() for _ in range(3)]
     assert all(np.isfinite(losses))
+
+
+def test_tokenize_text_to_shards(tmp_path):
+    """Text -> tokenizer.json ids -> shards the loader reads back in order."""
+    from tokenizers import Tokenizer, models, pre_tokenizers
+
+    from dstack_amd.workloads.tokens import main, tokenize_to_shards
+
+    vocab = {w: i for i, w in enumerate(["[UNK]", "<eos>", "the", "mi355x", "trains", "fast", "model"])}
+    tok = Tokenizer(models.WordLevel(vocab, unk_token="[UNK]"))
+    tok.pre_tokenizer = pre_tokenizers.Whitespace()
+    tok.save(str(tmp_path / "tokenizer.json"))
+    (tmp_path / "corpus.txt").write_text("the mi355x trains fast\n\nthe model trains\n" * 50)
+    paths = tokenize_to_shards(str(tmp_path / "tokenizer.json"), [str(tmp_path / "corpus.txt")],
+                               str(tmp_path / "shards"), shard_tokens=120, eos_id=1)
+    assert len(paths) == 4  # 50 * (5 + 4) = 450 tokens
+    data = np.concatenate([np.fromfile(p, dtype=np.uint16, offset=1024) for p in paths])
+    assert data[:9].tolist() == [2, 3, 4, 5, 1, 2, 6, 4, 1]
+    main(["info", str(tmp_path / "shards" / "*.bin"), "--seq-len", "16"])
