@@ -340,14 +340,9 @@ class GCPCompute(VMCompute):
             raise BackendAuthError(f"gcp project {self.project}: {r.status_code} {r.text[:200]}")
         check_response(r, "gcp project")
 
-    def _fetch_catalog(self) -> List[CatalogRow]:
-        """Catalog machine types checked against the project's zones (aggregated
-        ``machineTypes`` list): regions where a type is offered in some zone keep the catalog
-        price (``unknown`` stock), the rest are ``not_available``; zones offering each type are
-        remembered for the launch."""
-        base = offline_rows(self.TYPE)
-        names = sorted({r.instance_name for r in base})
-        flt = " OR ".join(f'(name = "{n}")' for n in names)
+    def _machine_type_zones(self, names) -> Dict[Tuple[str, str], List[str]]:
+        """{(machine type, region): [zones offering it]} from the aggregated machineTypes list."""
+        flt = " OR ".join(f'(name = "{n}")' for n in sorted(names))
         zones: Dict[Tuple[str, str], List[str]] = {}
         token = None
         for _ in range(50):
@@ -362,7 +357,16 @@ class GCPCompute(VMCompute):
             token = d.get("nextPageToken")
             if not token:
                 break
-        self._type_zones = {k: sorted(v) for k, v in zones.items()}
+        return {k: sorted(v) for k, v in zones.items()}
+
+    def _fetch_catalog(self) -> List[CatalogRow]:
+        """Catalog machine types checked against the project's zones (aggregated
+        ``machineTypes`` list): regions where a type is offered in some zone keep the catalog
+        price (``unknown`` stock), the rest are ``not_available``; zones offering each type are
+        remembered for the launch."""
+        base = offline_rows(self.TYPE)
+        zones = self._machine_type_zones({r.instance_name for r in base})
+        self._type_zones = zones
         out = []
         wanted = self.config.get("regions")
         specs: Dict[str, List[CatalogRow]] = {}
@@ -383,7 +387,17 @@ class GCPCompute(VMCompute):
         zones = self.config.get("zones") or {}
         if zones.get(region):
             return zones[region]
-        offered = getattr(self, "_type_zones", {}).get((machine_type, region)) if machine_type else None
+        if not machine_type:
+            return f"{region}-a"
+        known = getattr(self, "_type_zones", None)
+        if known is None or (machine_type, region) not in known:
+            # offers served from the catalog cache (another process, or no live listing): ask once
+            try:
+                found = self._machine_type_zones({machine_type})
+            except Exception:  # noqa: BLE001 -- keep the conventional first zone
+                found = {}
+            self._type_zones = {**(known or {}), **found}
+        offered = self._type_zones.get((machine_type, region))
         return offered[0] if offered else f"{region}-a"
 
     def _launch(self, offer, cfg):

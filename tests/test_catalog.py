@@ -479,6 +479,33 @@ def test_oci_live_shapes_per_availability_domain(live, monkeypatch):
     assert c._ad_for("us-chicago-1", "BM.GPU.MI355X.8") == "Xy:US-CHICAGO-1-AD-2"
 
 
+def test_gcp_launch_finds_zone_without_a_listing(monkeypatch):
+    """Offers from the offline catalog (no live listing in this process): the launch still asks
+    which zone of the region offers the machine type instead of assuming '<region>-a'."""
+    from dstack_amd.core.backends.clouds import hyperscalers
+    from dstack_amd.core.models.instances import InstanceConfiguration, SSHKey
+
+    monkeypatch.setattr(hyperscalers.GCPCompute, "_h", lambda self: {"Authorization": "Bearer t"})
+    inserted = []
+
+    def handler(req):
+        if req.url.path.endswith("/aggregated/machineTypes"):
+            return httpx.Response(200, json={"items": {"zones/us-central1-f": {"machineTypes": [
+                {"name": "a3-highgpu-8g"}]}}})
+        if req.method == "POST":
+            inserted.append(req.url.path)
+            return httpx.Response(200, json={"name": "op"})
+        return httpx.Response(404)
+
+    c = compute_class(BackendType.GCP)({"project_id": "p"}, {"data": json.dumps({"client_email": "x"})},
+                                       _client(handler))
+    offer = next(o for o in c.get_offers(_req(gpu="H100:8")) if o.region == "us-central1")
+    cfg = InstanceConfiguration(project_name="main", instance_name="r-0", user="admin",
+                                ssh_keys=[SSHKey(public="ssh-ed25519 AAAA k")])
+    c.create_instance(offer, cfg)
+    assert "/zones/us-central1-f/instances" in inserted[0]
+
+
 def test_live_listing_is_cached_per_credentials(live):
     n = {"calls": 0}
 
