@@ -3,6 +3,11 @@
 //
 //   dstack-runner [--log-level N] start --http-port 10999 --temp-dir /tmp/runner
 //                 --home-dir /root --working-dir /workflow [--ssh-env] [--probe PATH]
+//                 [--port-file PATH]
+//
+// --http-port 0 binds an ephemeral port; --port-file then receives the bound port (written to a
+// temp file and renamed, so a reader never sees a partial number).  The process shim driver uses
+// this instead of probing for a free port first, which races with every other bind on the host.
 //
 // Lifecycle: wait <= 5 min for /api/submit, run the job, then keep serving until the job's logs
 // were pulled after completion (or 30 s), then exit.
@@ -28,7 +33,8 @@ static const char* VERSION = "0.1.0-mi355x";
 static void usage() {
   fprintf(stderr,
           "usage: dstack-runner [--log-level N] start [--http-port P] [--temp-dir D] [--home-dir D]\n"
-          "                     [--working-dir D] [--ssh-env] [--probe PATH] [--submit-timeout S]\n");
+          "                     [--working-dir D] [--ssh-env] [--probe PATH] [--submit-timeout S]\n"
+          "                     [--port-file PATH]\n");
 }
 
 int main(int argc, char** argv) {
@@ -36,6 +42,7 @@ int main(int argc, char** argv) {
   int submit_timeout_s = 300;
   RunnerOptions opts;
   bool start = false;
+  std::string port_file;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&](const char* name) -> std::string {
@@ -53,6 +60,7 @@ int main(int argc, char** argv) {
     else if (a == "--working-dir") opts.working_dir = next("--working-dir");
     else if (a == "--ssh-env") opts.write_ssh_env = true;
     else if (a == "--probe") opts.probe_binary = next("--probe");
+    else if (a == "--port-file") port_file = next("--port-file");
     else if (a == "--submit-timeout") submit_timeout_s = atoi(next("--submit-timeout").c_str());
     else if (a == "--version") {
       printf("%s\n", VERSION);
@@ -143,6 +151,14 @@ int main(int argc, char** argv) {
     return 1;
   }
   LOGI("dstack-runner %s listening on :%d", VERSION, srv.port());
+  if (!port_file.empty()) {
+    std::string tmp = port_file + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "w");
+    if (!f || fprintf(f, "%d\n", srv.port()) < 0 || fclose(f) != 0 || rename(tmp.c_str(), port_file.c_str()) != 0) {
+      LOGE("cannot write the port file %s", port_file.c_str());
+      return 1;
+    }
+  }
   std::thread server_thread([&] { srv.serve_forever(); });
 
   // lifecycle supervisor

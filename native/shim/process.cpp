@@ -2,13 +2,10 @@
 // Used by the local backend, by bare-metal SSH hosts without a container runtime and by the
 // CPU-only tests.  GPU isolation: the granted GPUs are exported as HIP_VISIBLE_DEVICES (host
 // numbering), so ROCm in the job sees exactly those devices.
-#include <arpa/inet.h>
 #include <fcntl.h>
-#include <netinet/in.h>
 #include <signal.h>
 
 #include <atomic>
-#include <sys/socket.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -21,23 +18,6 @@
 extern char** environ;
 
 namespace dsa {
-
-static int free_tcp_port() {
-  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-  struct sockaddr_in a{};
-  a.sin_family = AF_INET;
-  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-  a.sin_port = 0;
-  if (::bind(fd, (struct sockaddr*)&a, sizeof a) != 0) {
-    ::close(fd);
-    return 0;
-  }
-  socklen_t l = sizeof a;
-  getsockname(fd, (struct sockaddr*)&a, &l);
-  int p = ntohs(a.sin_port);
-  ::close(fd);
-  return p;
-}
 
 // Process-group ids of runner children, readable from a signal handler: when the shim is stopped,
 // process-driver tasks (plain child processes, unlike containers) must not outlive it.
@@ -103,12 +83,10 @@ class ProcessDriver : public TaskDriver {
         if (symlink(ip.c_str(), link.c_str()) != 0) LOGW("mount link %s failed", link.c_str());
       }
     }
-    int port = free_tcp_port();
-    if (port == 0) {
-      reason = "creating_container_error";
-      msg = "no free port for the runner";
-      return false;
-    }
+    // the runner binds an ephemeral port itself and reports it through a file: probing for a free
+    // port here and passing it down would race with every other bind on the host
+    std::string port_file = dir + "/runner.port";
+    unlink(port_file.c_str());
     std::vector<std::string> envs;
     for (char** e = environ; e && *e; ++e) {
       std::string s = *e;
@@ -127,7 +105,7 @@ class ProcessDriver : public TaskDriver {
       envs.push_back("HIP_VISIBLE_DEVICES=-1");  // no GPU granted: hide all devices
     }
     std::vector<std::string> argv = {o_.runner_binary, "--log-level", std::to_string(log_level()), "start",
-                                     "--http-port", std::to_string(port), "--temp-dir", dir + "/tmp",
+                                     "--http-port", "0", "--port-file", port_file, "--temp-dir", dir + "/tmp",
                                      "--home-dir", dir + "/home", "--working-dir", dir + "/workflow"};
     if (!o_.probe_binary.empty()) {
       argv.push_back("--probe");
@@ -160,8 +138,34 @@ class ProcessDriver : public TaskDriver {
     }
     register_child_pgid(pid);
     t.pid = pid;
-    t.runner_port = port;
     t.container_name = "process-" + std::to_string(pid);
+    auto exited = [&]() {
+      int st;
+      if (waitpid(pid, &st, WNOHANG) != pid) return false;
+      unregister_child_pgid(pid);
+      reason = "creating_container_error";
+      msg = "runner exited during startup (see " + log_path + ")";
+      t.pid = 0;
+      return true;
+    };
+    int port = 0;
+    for (int k = 0; k < 1000 && port == 0; ++k) {  // <= 10 s for the runner to bind
+      std::string s;
+      if (read_file(port_file, s)) port = atoi(s.c_str());
+      if (port == 0) {
+        if (exited()) return false;
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      }
+    }
+    if (port == 0) {
+      terminate(t, 1);
+      wait(t);
+      reason = "creating_container_error";
+      msg = "runner did not report its port (see " + log_path + ")";
+      t.pid = 0;
+      return false;
+    }
+    t.runner_port = port;
     t.ports = {PortMapping{o_.runner_http_port, port}};
     // wait until the runner accepts connections so the server's first call succeeds
     for (int k = 0; k < 500; ++k) {
@@ -170,14 +174,7 @@ class ProcessDriver : public TaskDriver {
       r.path = "/api/healthcheck";
       r.timeout_ms = 200;
       if (http_request(r).ok()) break;
-      int st;
-      if (waitpid(pid, &st, WNOHANG) == pid) {
-        unregister_child_pgid(pid);
-        reason = "creating_container_error";
-        msg = "runner exited during startup (see " + log_path + ")";
-        t.pid = 0;
-        return false;
-      }
+      if (exited()) return false;
       std::this_thread::sleep_for(std::chrono::milliseconds(10));
     }
     return true;

@@ -36,6 +36,15 @@ def _logs(run) -> str:
     return b"".join(run.logs()).decode(errors="replace")
 
 
+def _wait(run, timeout: float) -> str:
+    """``run.wait`` that, on a timeout, fails with every job's status and timings."""
+    try:
+        return run.wait(timeout=timeout).value
+    except TimeoutError as e:
+        jobs = [(j.job_spec.job_num, s.status.value, s.timings) for j in run.model.jobs for s in j.job_submissions]
+        pytest.fail(f"{e}; jobs: {jobs}")
+
+
 def test_task_runs_and_streams_logs(client):
     from dstack_amd.api import Task
 
@@ -211,7 +220,7 @@ def test_multinode_task_rendezvous_env(client):
 
     cmd = "echo node=$DSTACK_NODE_RANK/$DSTACK_NODES_NUM master=$DSTACK_MASTER_NODE_IP world=$WORLD_SIZE"
     run = client.runs.submit(Task(commands=[cmd], nodes=2, name="e2e-multinode"))
-    assert run.wait(timeout=90).value == "done"
+    assert _wait(run, 90) == "done"
     outs = sorted(b"".join(run.logs(job_num=j)).decode() for j in (0, 1))
     assert any("node=0/2" in o for o in outs) and any("node=1/2" in o for o in outs)
     assert all("master=" in o and "master= " not in o for o in outs)
