@@ -67,7 +67,7 @@ class Duration(int):
         return core_schema.no_info_plain_validator_function(
             cls.parse,
             json_schema_input_schema=core_schema.union_schema([core_schema.int_schema(), core_schema.str_schema()]),
-            serialization=core_schema.plain_serializer_function_ser_schema(int),
+            serialization=core_schema.plain_serializer_function_ser_schema(int, return_schema=core_schema.int_schema()),
         )
 
 

@@ -114,5 +114,8 @@ class Env:
     def __get_pydantic_core_schema__(cls, source, handler: GetCoreSchemaHandler):
         return core_schema.no_info_plain_validator_function(
             lambda v: v if isinstance(v, Env) else Env(v),
-            serialization=core_schema.plain_serializer_function_ser_schema(lambda e: e.to_json()),
+            json_schema_input_schema=core_schema.union_schema(
+                [core_schema.list_schema(core_schema.str_schema()), core_schema.dict_schema(core_schema.str_schema())]),
+            serialization=core_schema.plain_serializer_function_ser_schema(
+                lambda e: e.to_json(), return_schema=core_schema.dict_schema(core_schema.str_schema())),
         )

@@ -54,7 +54,7 @@ class Memory(float):
         return core_schema.no_info_plain_validator_function(
             cls.parse,
             json_schema_input_schema=core_schema.union_schema([core_schema.float_schema(), core_schema.str_schema()]),
-            serialization=core_schema.plain_serializer_function_ser_schema(float),
+            serialization=core_schema.plain_serializer_function_ser_schema(float, return_schema=core_schema.float_schema()),
         )
 
 
@@ -148,7 +148,9 @@ class ComputeCapability(tuple):
     @classmethod
     def __get_pydantic_core_schema__(cls, source, handler: GetCoreSchemaHandler):
         return core_schema.no_info_plain_validator_function(
-            cls.parse, serialization=core_schema.plain_serializer_function_ser_schema(lambda x: f"{x[0]}.{x[1]}")
+            cls.parse, json_schema_input_schema=core_schema.str_schema(),
+            serialization=core_schema.plain_serializer_function_ser_schema(lambda x: f"{x[0]}.{x[1]}",
+                                                                            return_schema=core_schema.str_schema()),
         )
 
 

@@ -86,7 +86,7 @@ def _token(request: Request) -> Optional[str]:
 
 
 @router.api_route("/proxy/services/{project_name}/{run_name}/{path:path}",
-                  methods=["GET", "POST", "PUT", "PATCH", "DELETE", "OPTIONS", "HEAD"])
+                  methods=["GET", "POST", "PUT", "PATCH", "DELETE", "OPTIONS", "HEAD"], include_in_schema=False)
 async def service_proxy(project_name: str, run_name: str, path: str, request: Request):
     url, meta, status, err = await run_in_threadpool(_resolve, project_name, run_name, _token(request))
     if url is None:

@@ -326,3 +326,89 @@ def test_legacy_get_offers(client):
     assert r.status_code == 200, r.text
     body = r.json()
     assert body["pool_name"] and isinstance(body["instances"], list)
+
+
+# every REST route of the reference server (its ``server/routers/*.py``, prefix + path), so a
+# client of the reference finds each one here
+REFERENCE_ROUTES = [
+    '/api/backends/config_values',
+    '/api/backends/list_types',
+    '/api/fleets/list',
+    '/api/instances/list',
+    '/api/pools/list_instances',
+    '/api/project/{project_name}/backends/create',
+    '/api/project/{project_name}/backends/create_yaml',
+    '/api/project/{project_name}/backends/delete',
+    '/api/project/{project_name}/backends/update',
+    '/api/project/{project_name}/backends/update_yaml',
+    '/api/project/{project_name}/backends/{backend_name}/config_info',
+    '/api/project/{project_name}/backends/{backend_name}/get_yaml',
+    '/api/project/{project_name}/fleets/create',
+    '/api/project/{project_name}/fleets/delete',
+    '/api/project/{project_name}/fleets/delete_instances',
+    '/api/project/{project_name}/fleets/get',
+    '/api/project/{project_name}/fleets/get_plan',
+    '/api/project/{project_name}/fleets/list',
+    '/api/project/{project_name}/gateways/create',
+    '/api/project/{project_name}/gateways/delete',
+    '/api/project/{project_name}/gateways/get',
+    '/api/project/{project_name}/gateways/list',
+    '/api/project/{project_name}/gateways/set_default',
+    '/api/project/{project_name}/gateways/set_wildcard_domain',
+    '/api/project/{project_name}/logs/poll',
+    '/api/project/{project_name}/metrics/job/{run_name}',
+    '/api/project/{project_name}/pool/add_remote',
+    '/api/project/{project_name}/pool/create',
+    '/api/project/{project_name}/pool/delete',
+    '/api/project/{project_name}/pool/list',
+    '/api/project/{project_name}/pool/remove',
+    '/api/project/{project_name}/pool/set_default',
+    '/api/project/{project_name}/pool/show',
+    '/api/project/{project_name}/repos/delete',
+    '/api/project/{project_name}/repos/get',
+    '/api/project/{project_name}/repos/init',
+    '/api/project/{project_name}/repos/list',
+    '/api/project/{project_name}/repos/upload_code',
+    '/api/project/{project_name}/runs/apply',
+    '/api/project/{project_name}/runs/create_instance',
+    '/api/project/{project_name}/runs/delete',
+    '/api/project/{project_name}/runs/get',
+    '/api/project/{project_name}/runs/get_offers',
+    '/api/project/{project_name}/runs/get_plan',
+    '/api/project/{project_name}/runs/stop',
+    '/api/project/{project_name}/runs/submit',
+    '/api/project/{project_name}/secrets/add',
+    '/api/project/{project_name}/secrets/delete',
+    '/api/project/{project_name}/secrets/get',
+    '/api/project/{project_name}/secrets/list',
+    '/api/project/{project_name}/volumes/create',
+    '/api/project/{project_name}/volumes/delete',
+    '/api/project/{project_name}/volumes/get',
+    '/api/project/{project_name}/volumes/list',
+    '/api/projects/create',
+    '/api/projects/delete',
+    '/api/projects/list',
+    '/api/projects/{project_name}/get',
+    '/api/projects/{project_name}/set_members',
+    '/api/runs/list',
+    '/api/server/get_info',
+    '/api/users/create',
+    '/api/users/delete',
+    '/api/users/get_my_user',
+    '/api/users/get_user',
+    '/api/users/list',
+    '/api/users/refresh_token',
+    '/api/users/update',
+    '/api/volumes/list',
+]
+
+
+def test_openapi_schema_covers_reference_routes(client):
+    import re
+
+    r = client.get("/api/openapi.json")
+    assert r.status_code == 200, r.text[:500]
+    norm = lambda p: re.sub(r"\{[^}]+\}", "{}", p)  # noqa: E731
+    ours = {norm(p) for p in r.json()["paths"]}
+    missing = [p for p in REFERENCE_ROUTES if norm(p) not in ours]
+    assert not missing, missing
