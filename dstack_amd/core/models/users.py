@@ -23,6 +23,14 @@ class ProjectRole(str, Enum):
     USER = "user"
 
 
+class UserPermissions(CoreModel):
+    can_create_projects: bool = True
+
+
+class MemberPermissions(CoreModel):
+    can_manage_ssh_fleets: bool = True
+
+
 class User(CoreModel):
     id: uuid.UUID
     username: str
@@ -30,6 +38,7 @@ class User(CoreModel):
     global_role: GlobalRole
     email: Optional[str] = None
     active: bool = True
+    permissions: UserPermissions = UserPermissions()
 
 
 class UserTokenCreds(CoreModel):
@@ -40,13 +49,10 @@ class UserWithCreds(User):
     creds: UserTokenCreds
 
 
-class UserPermissions(CoreModel):
-    can_create_projects: bool = True
-
-
 class Member(CoreModel):
     user: User
     project_role: ProjectRole
+    permissions: MemberPermissions = MemberPermissions()
 
 
 class Project(CoreModel):

@@ -150,14 +150,14 @@ def create_fleet(body: schemas.CreateFleetRequest, up: UP = Depends(project_mana
 @fleets_router.post("/delete")
 def delete_fleets(body: schemas.DeleteFleetsRequest, up: UP = Depends(project_manager),
                   s: Session = Depends(get_session, scope="function")):
-    fleets_services.delete_fleets(s, up[1], body.names)
+    fleets_services.delete_fleets(s, up[1], body.names, up[0])
     return {}
 
 
 @fleets_router.post("/delete_instances")
 def delete_fleet_instances(body: schemas.DeleteFleetInstancesRequest, up: UP = Depends(project_manager),
                            s: Session = Depends(get_session, scope="function")):
-    fleets_services.delete_fleet_instances(s, up[1], body.name, body.instance_nums)
+    fleets_services.delete_fleet_instances(s, up[1], body.name, body.instance_nums, up[0])
     return {}
 
 

@@ -14,6 +14,7 @@
           secret: <base64 32 bytes>
     default_permissions:
       allow_non_admins_create_projects: true
+      allow_non_admins_manage_ssh_fleets: true
 """
 
 from __future__ import annotations
@@ -30,6 +31,7 @@ from dstack_amd.server import settings
 from dstack_amd.server.models import UserModel
 from dstack_amd.server.services import backends as backends_services
 from dstack_amd.server.services import encryption
+from dstack_amd.server.services import permissions as permissions_services
 from dstack_amd.server.services import projects as projects_services
 
 
@@ -42,8 +44,7 @@ class EncryptionConfig(CoreModel):
     keys: List[dict] = []
 
 
-class DefaultPermissions(CoreModel):
-    allow_non_admins_create_projects: bool = True
+DefaultPermissions = permissions_services.DefaultPermissions
 
 
 class ServerConfig(CoreModel):
@@ -60,9 +61,11 @@ class ServerConfigManager:
     def load_config(self) -> bool:
         if not self.path.exists():
             self.config = None
+            permissions_services.set_default_permissions(None)
             return False
         data = yaml.safe_load(self.path.read_text()) or {}
         self.config = ServerConfig.model_validate(data)
+        permissions_services.set_default_permissions(self.config.default_permissions)
         return True
 
     def apply_encryption(self):

@@ -35,6 +35,7 @@ from dstack_amd.server.models import FleetModel, InstanceModel, ProjectModel, Us
 from dstack_amd.server.services import offers as offers_services
 from dstack_amd.server.services import pools as pools_services
 from dstack_amd.server.services.locking import db_advisory_lock, lockset
+from dstack_amd.server.services.permissions import check_can_manage_ssh_fleets
 from dstack_amd.utils.common import generate_name, get_current_datetime
 
 
@@ -131,6 +132,8 @@ def _validate_private_key(key: SSHKey):
 def create_fleet(s: Session, project: ProjectModel, user: UserModel, spec: FleetSpec) -> Fleet:
     conf = spec.configuration
     _validate_fleet_spec(spec)
+    if conf.ssh_config is not None:
+        check_can_manage_ssh_fleets(user, project)
     with db_advisory_lock(s, f"fleet_names_{project.id}"):
         if conf.name is None:
             conf.name = generate_name()
@@ -190,7 +193,13 @@ def create_autocreated_fleet(s: Session, project: ProjectModel, run_name: str, p
     return fleet
 
 
-def delete_fleets(s: Session, project: ProjectModel, names: List[str]):
+def _check_ssh_fleets(user, project: ProjectModel, fleets) -> None:
+    for f in fleets:
+        if FleetSpec.model_validate_json(f.spec).configuration.ssh_config is not None:
+            check_can_manage_ssh_fleets(user, project)
+
+
+def delete_fleets(s: Session, project: ProjectModel, names: List[str], user: Optional[UserModel] = None):
     """Fleets and their instances are held in the background processors' locksets while their
     state is re-read, checked and changed, and committed before release: a job assigned to an
     instance (IDLE -> BUSY) or an instance pass (PROVISIONING -> IDLE) racing the delete can then
@@ -201,6 +210,7 @@ def delete_fleets(s: Session, project: ProjectModel, names: List[str]):
         if f is None:
             raise ResourceNotExistsError(f"Fleet {name} not found")
         fleets.append(f)
+    _check_ssh_fleets(user, project, fleets)
     for _attempt in range(5):
         locked = [i for f in fleets for i in f.instances]
         with _held(fleets, locked):
@@ -239,10 +249,12 @@ def _terminate_fleets_locked(s: Session, fleets):
         f.status = FleetStatus.TERMINATING.value
 
 
-def delete_fleet_instances(s: Session, project: ProjectModel, name: str, instance_nums: List[int]):
+def delete_fleet_instances(s: Session, project: ProjectModel, name: str, instance_nums: List[int],
+                           user: Optional[UserModel] = None):
     f = get_fleet_by_name(s, project, name)
     if f is None:
         raise ResourceNotExistsError(f"Fleet {name} not found")
+    _check_ssh_fleets(user, project, [f])
     targets = [i for i in f.instances if i.instance_num in instance_nums]
     with _held([], targets):
         for inst in targets:

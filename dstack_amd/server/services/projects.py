@@ -13,12 +13,14 @@ from dstack_amd.core.errors import ForbiddenError, ResourceExistsError, Resource
 from dstack_amd.core.models.backends import BackendInfo, BackendType
 from dstack_amd.core.models.users import GlobalRole, Member, Project, ProjectRole
 from dstack_amd.server.models import MemberModel, ProjectModel, UserModel
+from dstack_amd.server.services.permissions import check_can_create_projects, get_member_permissions
 from dstack_amd.server.services.users import get_user_by_name, user_model_to_user
 from dstack_amd.utils.common import generate_rsa_key_pair
 
 
 def project_model_to_project(p: ProjectModel, include_backends: bool = True) -> Project:
-    members = [Member(user=user_model_to_user(m.user), project_role=ProjectRole(m.project_role)) for m in p.members]
+    members = [Member(user=user_model_to_user(m.user), project_role=ProjectRole(m.project_role),
+                      permissions=get_member_permissions(m)) for m in p.members]
     backends = []
     if include_backends:
         # settings only: credentials live in the encrypted auth column and are never returned
@@ -49,6 +51,7 @@ def list_user_projects(s: Session, user: UserModel) -> List[ProjectModel]:
 
 
 def create_project(s: Session, user: UserModel, project_name: str) -> ProjectModel:
+    check_can_create_projects(user)
     if user.global_role != GlobalRole.ADMIN.value:
         owned = s.execute(select(ProjectModel).where(ProjectModel.owner_id == user.id,
                                                      ProjectModel.deleted == False)).scalars().all()  # noqa: E712

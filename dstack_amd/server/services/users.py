@@ -15,8 +15,10 @@ from dstack_amd.utils.common import generate_token, token_hash
 
 
 def user_model_to_user(u: UserModel) -> User:
+    from dstack_amd.server.services.permissions import get_user_permissions
+
     return User(id=u.id, username=u.name, created_at=u.created_at, global_role=GlobalRole(u.global_role),
-                email=u.email, active=u.active)
+                email=u.email, active=u.active, permissions=get_user_permissions(u))
 
 
 def user_model_to_user_with_creds(u: UserModel) -> UserWithCreds:

@@ -412,3 +412,49 @@ def test_openapi_schema_covers_reference_routes(client):
     ours = {norm(p) for p in r.json()["paths"]}
     missing = [p for p in REFERENCE_ROUTES if norm(p) not in ours]
     assert not missing, missing
+
+
+# ---- default permissions (server config.yml) ---------------------------------------------------
+def test_default_permissions_restrict_projects_and_ssh_fleets(client, tmp_path):
+    """``default_permissions`` of the server config: with both switches off a non-admin user can
+    neither create projects nor create/delete SSH fleets, a project admin still manages SSH fleets,
+    and the derived permissions are reported on users and members."""
+    from dstack_amd.server.services import permissions
+    from dstack_amd.server.services.config import ServerConfigManager
+
+    cfg = tmp_path / "config.yml"
+    cfg.write_text("default_permissions:\n  allow_non_admins_create_projects: false\n"
+                   "  allow_non_admins_manage_ssh_fleets: false\n")
+    ServerConfigManager(cfg).load_config()
+    try:
+        u = client.post("/api/users/create", json={"username": "erin"}).json()
+        assert u["permissions"] == {"can_create_projects": False}
+        erin = {"Authorization": f"Bearer {u['creds']['token']}"}
+        r = client.post("/api/projects/create", json={"project_name": "erins"}, headers=erin)
+        assert r.status_code == 403, r.text
+        assert client.post("/api/users/get_my_user").json()["permissions"]["can_create_projects"]
+        r = client.post("/api/projects/main/set_members",
+                        json={"members": [{"username": "admin", "project_role": "admin"},
+                                          {"username": "erin", "project_role": "user"}]})
+        assert r.status_code == 200, r.text
+        members = {m["user"]["username"]: m for m in client.post("/api/projects/main/get").json()["members"]}
+        assert members["erin"]["permissions"] == {"can_manage_ssh_fleets": False}
+        assert members["admin"]["permissions"] == {"can_manage_ssh_fleets": True}
+        key = {"public": "ssh-ed25519 AAAA", "private": "-----BEGIN OPENSSH PRIVATE KEY-----\nx\n"
+                                                       "-----END OPENSSH PRIVATE KEY-----\n"}
+        spec = {"spec": {"configuration": {"type": "fleet", "name": "onprem2",
+                                           "ssh_config": {"user": "ubuntu", "ssh_key": key, "hosts": ["10.0.0.9"]}},
+                         "profile": {"name": "default"}}}
+        assert client.post("/api/project/main/fleets/create", json=spec, headers=erin).status_code == 403
+        assert client.post("/api/project/main/fleets/create", json=spec).status_code == 200
+        r = client.post("/api/project/main/fleets/delete", json={"names": ["onprem2"]}, headers=erin)
+        assert r.status_code == 403
+        # promoted to project admin: allowed
+        client.post("/api/projects/main/set_members",
+                    json={"members": [{"username": "admin", "project_role": "admin"},
+                                      {"username": "erin", "project_role": "admin"}]})
+        r = client.post("/api/project/main/fleets/delete", json={"names": ["onprem2"]}, headers=erin)
+        assert r.status_code == 200, r.text
+    finally:
+        permissions.set_default_permissions(None)
+    assert client.post("/api/projects/create", json={"project_name": "erins"}, headers=erin).status_code == 200
