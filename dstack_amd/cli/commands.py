@@ -573,6 +573,7 @@ def register_pool(sub):
     ap.add_argument("--cpu", help="CPU requirement, e.g. 32..")
     ap.add_argument("--memory", help="Memory requirement, e.g. 256GB..")
     ap.add_argument("--disk", help="Disk requirement, e.g. 500GB..")
+    ap.add_argument("--shared-memory", dest="shared_memory", metavar="SIZE", help="Shared memory size, e.g. 64GB")
     ap.add_argument("--pool", dest="pool_name")
     ap.add_argument("--max-price", type=float)
     ap.add_argument("-b", "--backend", action="append", dest="backends")
@@ -685,6 +686,8 @@ def _pool_requirements(args):
     for k in ("gpu", "cpu", "memory", "disk"):
         if getattr(args, k, None):
             res[k] = getattr(args, k)
+    if getattr(args, "shared_memory", None):
+        res["shm_size"] = args.shared_memory
     spot = SpotPolicy(args.spot_policy) if args.spot_policy else None
     profile = Profile(name="pool-add", backends=args.backends, regions=args.regions, max_price=args.max_price,
                       spot_policy=spot, pool_name=args.pool_name)

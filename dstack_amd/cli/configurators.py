@@ -31,7 +31,8 @@ from dstack_amd.core.models.runs import JobStatus, RunStatus
 # ---- profile arguments (cli/services/profile.py) ----------------------------------------------
 def register_profile_args(parser: argparse.ArgumentParser):
     g = parser.add_argument_group("Profile")
-    g.add_argument("--profile", metavar="NAME", help="Profile from .dstack/profiles.yml")
+    g.add_argument("--profile", metavar="NAME", default=os.getenv("DSTACK_PROFILE"),
+                   help="Profile from .dstack/profiles.yml (default: $DSTACK_PROFILE)")
     g.add_argument("--max-price", type=float, metavar="PRICE", help="Max price per hour, $")
     g.add_argument("--max-duration", metavar="DURATION", help="Max run duration, e.g. 72h or off")
     g.add_argument("-b", "--backend", action="append", dest="backends", metavar="NAME")

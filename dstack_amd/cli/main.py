@@ -25,6 +25,12 @@ def main(argv=None) -> int:
     from dstack_amd.cli.utils import err_console
     from dstack_amd.core.errors import ClientError, CLIError, ConfigurationError, ServerClientError
 
+    import logging
+    import os
+
+    # DSTACK_CLI_LOG_LEVEL=DEBUG shows the client's request log and tracebacks of server errors
+    logging.basicConfig(level=getattr(logging, os.getenv("DSTACK_CLI_LOG_LEVEL", "WARNING").upper(), logging.WARNING),
+                        format="%(levelname)s %(name)s: %(message)s")
     parser = build_parser()
     args = parser.parse_args(argv)
     if not getattr(args, "func", None):

@@ -35,7 +35,8 @@ def configure_logging(level: Optional[str] = None):
     fmt = "%(asctime)s %(levelname)s %(name)s: %(message)s"
     if settings.SERVER_LOG_FORMAT == "json":
         fmt = '{"ts": "%(asctime)s", "level": "%(levelname)s", "logger": "%(name)s", "msg": "%(message)s"}'
-    logging.basicConfig(level=lvl, format=fmt)
+    logging.basicConfig(level=getattr(logging, settings.SERVER_ROOT_LOG_LEVEL, logging.ERROR), format=fmt)
+    logging.getLogger("dstack_amd").setLevel(lvl)
     logging.getLogger("httpx").setLevel(logging.WARNING)
 
 
@@ -48,8 +49,9 @@ def init_server_state(admin_token: Optional[str] = None):
 
     migrate()
     cm = ServerConfigManager()
-    cm.load_config()
-    cm.apply_encryption()
+    if not settings.SERVER_CONFIG_DISABLED:
+        cm.load_config()
+        cm.apply_encryption()
     with session_scope() as s:
         admin = get_or_create_admin_user(s, admin_token or settings.SERVER_ADMIN_TOKEN)
         project = get_or_create_default_project(s, admin, settings.DEFAULT_PROJECT_NAME)
@@ -70,7 +72,8 @@ def init_sentry():
         logger.warning("DSTACK_SENTRY_DSN is set but sentry_sdk is not installed")
         return False
     sentry_sdk.init(dsn=settings.SENTRY_DSN, traces_sample_rate=settings.SENTRY_TRACES_SAMPLE_RATE,
-                    release=__version__)
+                    profiles_sample_rate=settings.SENTRY_PROFILES_SAMPLE_RATE,
+                    environment=settings.SERVER_ENVIRONMENT, release=__version__)
     return True
 
 
@@ -116,13 +119,31 @@ def create_app(start_background: bool = True) -> FastAPI:
 
 
 def _write_client_config(url: str, token: str):
-    """Make the local CLI usable right after `dstack server` (``update_default_project``)."""
-    if os.environ.get("DSTACK_SERVER_NO_CLIENT_CONFIG"):
+    """Make the local CLI usable right after `dstack server` (reference ``update_default_project``):
+    the project becomes the CLI's default when the CLI has none yet; a different default project is
+    replaced only after a confirmation on a terminal, or with ``DSTACK_UPDATE_DEFAULT_PROJECT``;
+    ``DSTACK_DO_NOT_UPDATE_DEFAULT_PROJECT`` never writes."""
+    if os.environ.get("DSTACK_SERVER_NO_CLIENT_CONFIG") or settings.DO_NOT_UPDATE_DEFAULT_PROJECT:
         return
     try:
         from dstack_amd.core.services.configs import ConfigManager
 
         cm = ConfigManager()
+        current = cm.get_project_config()  # the CLI's default project
+        if current is not None and (current.name, current.url, current.token) == (settings.DEFAULT_PROJECT_NAME, url,
+                                                                                   token):
+            return
+        if current is not None and not settings.UPDATE_DEFAULT_PROJECT:
+            import sys
+
+            if not sys.stdin.isatty():
+                logger.info("the CLI's default project is %s at %s; left as is (DSTACK_UPDATE_DEFAULT_PROJECT=1 "
+                            "replaces it)", current.name, current.url)
+                return
+            from rich.prompt import Confirm
+
+            if not Confirm.ask(f"Update the {settings.DEFAULT_PROJECT_NAME} project in the CLI config?"):
+                return
         cm.configure_project(settings.DEFAULT_PROJECT_NAME, url, token, default=True)
         cm.save()
     except Exception as e:  # noqa: BLE001

@@ -158,8 +158,9 @@ def _no_capacity(job: JobModel, msg: str):
 def _runtime_data(inst_offer: InstanceOfferWithAvailability, gpu_indices: Optional[List[int]], spec) -> JobRuntimeData:
     res = inst_offer.instance.resources
     shared = inst_offer.total_blocks > 1
+    bridge = shared or settings.FORCE_BRIDGE_NETWORK  # DSTACK_FORCE_BRIDGE_NETWORK
     return JobRuntimeData(
-        network_mode=NetworkMode.BRIDGE if shared else NetworkMode.HOST,
+        network_mode=NetworkMode.BRIDGE if bridge else NetworkMode.HOST,
         gpu=len(res.gpus) if shared else None, cpu=float(res.cpus) if shared else None,
         memory=(res.memory_mib / 1024) if shared else None, offer=inst_offer, gpu_indices=gpu_indices,
     )

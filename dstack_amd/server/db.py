@@ -71,7 +71,7 @@ def get_db() -> Database:
             from pathlib import Path
 
             Path(settings.DATABASE_URL[len("sqlite:///"):]).parent.mkdir(parents=True, exist_ok=True)
-        _db = Database(settings.DATABASE_URL)
+        _db = Database(settings.DATABASE_URL, echo=settings.SQL_ECHO_ENABLED)
     return _db
 
 

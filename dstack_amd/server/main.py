@@ -18,8 +18,10 @@ def run(host: str = "127.0.0.1", port: int = 3000, log_level: str = "info", toke
 
     from dstack_amd.server.app import configure_logging, create_app
 
+    from dstack_amd.server import settings
+
     configure_logging(log_level)
-    uvicorn.run(create_app(), host=host, port=port, log_level=log_level.lower(), access_log=False,
+    uvicorn.run(create_app(), host=host, port=port, log_level=settings.SERVER_UVICORN_LOG_LEVEL, access_log=False,
                 timeout_graceful_shutdown=5)
 
 

@@ -117,6 +117,7 @@ def create_backend(s: Session, project: ProjectModel, config: dict) -> BackendMo
     if existing is not None:
         raise ResourceExistsError(f"Backend {btype.value} exists")
     _, cfg, secrets = split_backend_config(config)
+    _check_default_creds(secrets)
     validate_credentials(btype, cfg, secrets)
     row = BackendModel(id=uuid.uuid4(), project_id=project.id, type=btype.value, config=json.dumps(cfg),
                        auth=json.dumps(secrets))
@@ -139,10 +140,20 @@ def update_backend(s: Session, project: ProjectModel, config: dict) -> BackendMo
     if btype == BackendType.KUBERNETES and merged.get("kubeconfig") is None and old_secrets.get("kubeconfig"):
         merged["kubeconfig"] = old_secrets["kubeconfig"]
     _, cfg, secrets = split_backend_config(merged)
+    _check_default_creds(secrets)
     validate_credentials(btype, cfg, secrets)
     row.config = json.dumps(cfg)
     row.auth = json.dumps(secrets)
     return row
+
+
+def _check_default_creds(secrets: dict) -> None:
+    """``DSTACK_DEFAULT_CREDS_DISABLED``: ambient credentials (instance role, environment, metadata
+    server) of the machine running the server may not be used by a project's backend."""
+    from dstack_amd.server import settings
+
+    if settings.DEFAULT_CREDS_DISABLED and secrets.get("type") == "default":
+        raise ServerClientError("Default credentials are forbidden by dstack settings")
 
 
 def validate_credentials(btype: BackendType, cfg: dict, secrets: dict) -> None:

@@ -194,8 +194,11 @@ def create_autocreated_fleet(s: Session, project: ProjectModel, run_name: str, p
 
 
 def _check_ssh_fleets(user, project: ProjectModel, fleets) -> None:
+    if user is None:
+        return
     for f in fleets:
-        if FleetSpec.model_validate_json(f.spec).configuration.ssh_config is not None:
+        conf = (json.loads(f.spec or "{}") or {}).get("configuration") or {}
+        if conf.get("ssh_config") is not None:
             check_can_manage_ssh_fleets(user, project)
 
 

@@ -24,7 +24,7 @@ from typing import Deque, Dict, List, Optional, Tuple
 from sqlalchemy import select
 from sqlalchemy.orm import Session
 
-from dstack_amd.core.errors import GatewayError
+from dstack_amd.core.errors import GatewayError, ResourceNotExistsError
 from dstack_amd.core.models.configurations import ServiceConfiguration
 from dstack_amd.core.models.runs import RunSpec, ServiceModelSpec, ServiceSpec
 from dstack_amd.core.models.services import ScalingSpec
@@ -62,10 +62,12 @@ def register_service(s: Session, run: RunModel):
 
         gateway_register_service(s, run)
     else:
-        if conf.scaling is not None and conf.scaling.metric == "rps" and gateway is None and \
-                conf.replicas.min != conf.replicas.max:
-            # the in-server proxy counts requests too, so rps autoscaling works without a gateway
-            pass
+        from dstack_amd.server import settings
+
+        if settings.FORBID_SERVICES_WITHOUT_GATEWAY:
+            raise ResourceNotExistsError("This dstack server forbids services without a gateway. "
+                                         "Please configure a gateway.")
+        # (the in-server proxy counts requests too, so rps autoscaling works without a gateway)
         url = f"/proxy/services/{project.name}/{run.run_name}/"
         model = None
         if conf.model is not None:

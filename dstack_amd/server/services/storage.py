@@ -36,7 +36,9 @@ class S3Storage:
         import httpx
 
         self.bucket = bucket
-        self.region = region or os.getenv("DSTACK_SERVER_S3_BUCKET_REGION") or os.getenv("AWS_REGION", "us-east-1")
+        from dstack_amd.server import settings
+
+        self.region = region or settings.SERVER_BUCKET_REGION or os.getenv("AWS_REGION", "us-east-1")
         self.endpoint = endpoint or f"https://{bucket}.s3.{self.region}.amazonaws.com"
         self.http = client or httpx.Client(timeout=60)
         self.access_key = os.getenv("AWS_ACCESS_KEY_ID", "")
@@ -69,7 +71,7 @@ class S3Storage:
 
 
 def get_default_storage():
-    bucket = os.getenv("DSTACK_SERVER_S3_BUCKET")
+    bucket = os.getenv("DSTACK_SERVER_BUCKET") or os.getenv("DSTACK_SERVER_S3_BUCKET")
     if bucket:
         return S3Storage(bucket)
     d = os.getenv("DSTACK_SERVER_CODE_STORE_DIR")

@@ -42,8 +42,11 @@ def create_user(s: Session, username: str, global_role: GlobalRole = GlobalRole.
     if get_user_by_name(s, username) is not None:
         raise ResourceExistsError(f"User {username} exists")
     token = token or generate_token()
+    from dstack_amd.server import settings
+
     u = UserModel(id=uuid.uuid4(), name=username, token=token, token_hash=token_hash(token),
-                  global_role=global_role.value, email=email, active=active)
+                  global_role=global_role.value, email=email, active=active,
+                  projects_quota=settings.USER_PROJECT_DEFAULT_QUOTA)
     s.add(u)
     s.flush()
     return u

@@ -28,6 +28,13 @@ SERVER_URL = os.getenv("DSTACK_SERVER_URL", f"http://{SERVER_HOST}:{SERVER_PORT}
 SERVER_ADMIN_TOKEN = os.getenv("DSTACK_SERVER_ADMIN_TOKEN")
 SERVER_LOG_LEVEL = os.getenv("DSTACK_SERVER_LOG_LEVEL", "INFO").upper()
 SERVER_LOG_FORMAT = os.getenv("DSTACK_SERVER_LOG_FORMAT", "standard")  # standard | json | rich
+# level of the root logger (third-party libraries); the server's own loggers use SERVER_LOG_LEVEL
+SERVER_ROOT_LOG_LEVEL = os.getenv("DSTACK_SERVER_ROOT_LOG_LEVEL", "ERROR").upper()
+SERVER_UVICORN_LOG_LEVEL = os.getenv("DSTACK_SERVER_UVICORN_LOG_LEVEL", "ERROR").lower()
+SERVER_ENVIRONMENT = os.getenv("DSTACK_SERVER_ENVIRONMENT", "dev")  # reported to Sentry
+# ignore ~/.dstack/server/config.yml entirely (neither read, applied nor created)
+SERVER_CONFIG_DISABLED = os.getenv("DSTACK_SERVER_CONFIG_DISABLED") is not None
+SQL_ECHO_ENABLED = os.getenv("DSTACK_SQL_ECHO_ENABLED") is not None
 
 SERVER_METRICS_TTL_SECONDS = int(os.getenv("DSTACK_SERVER_METRICS_TTL_SECONDS", "3600"))
 SERVER_METRICS_COLLECT_INTERVAL = float(os.getenv("DSTACK_SERVER_METRICS_COLLECT_INTERVAL", "10"))
@@ -39,9 +46,25 @@ SERVER_EVENT_DRIVEN = not _env_bool("DSTACK_SERVER_POLLING_ONLY")
 SKIP_GATEWAY_UPDATE = _env_bool("DSTACK_SKIP_GATEWAY_UPDATE")
 
 SERVER_CLOUDWATCH_LOG_GROUP = os.getenv("DSTACK_SERVER_CLOUDWATCH_LOG_GROUP")
-SERVER_S3_BUCKET = os.getenv("DSTACK_SERVER_S3_BUCKET")
+# code blobs in S3 instead of the database (DSTACK_SERVER_S3_BUCKET is the older name here)
+SERVER_S3_BUCKET = os.getenv("DSTACK_SERVER_BUCKET") or os.getenv("DSTACK_SERVER_S3_BUCKET")
+SERVER_BUCKET_REGION = os.getenv("DSTACK_SERVER_BUCKET_REGION") or os.getenv("DSTACK_SERVER_S3_BUCKET_REGION")
 SENTRY_DSN = os.getenv("DSTACK_SENTRY_DSN")
 SENTRY_TRACES_SAMPLE_RATE = float(os.getenv("DSTACK_SENTRY_TRACES_SAMPLE_RATE", "0.1"))
+SENTRY_PROFILES_SAMPLE_RATE = float(os.getenv("DSTACK_SENTRY_PROFILES_SAMPLE_RATE", "0"))
+
+# backends may not use ambient (instance-role / environment) credentials: `creds: {type: default}`
+DEFAULT_CREDS_DISABLED = os.getenv("DSTACK_DEFAULT_CREDS_DISABLED") is not None
+# projects a new non-admin user may own
+USER_PROJECT_DEFAULT_QUOTA = int(os.getenv("DSTACK_USER_PROJECT_DEFAULT_QUOTA", "10"))
+# services must run behind a gateway (no in-server proxy)
+FORBID_SERVICES_WITHOUT_GATEWAY = os.getenv("DSTACK_FORBID_SERVICES_WITHOUT_GATEWAY") is not None
+# run every job container in bridge networking, also on hosts the job has to itself
+FORCE_BRIDGE_NETWORK = _env_bool("DSTACK_FORCE_BRIDGE_NETWORK")
+# server start: write the default project into the CLI config (~/.dstack/config.yml) always /
+# never; by default only when the CLI config has no default project yet or points to this server
+UPDATE_DEFAULT_PROJECT = os.getenv("DSTACK_UPDATE_DEFAULT_PROJECT") is not None
+DO_NOT_UPDATE_DEFAULT_PROJECT = os.getenv("DSTACK_DO_NOT_UPDATE_DEFAULT_PROJECT") is not None
 
 DEFAULT_PROJECT_NAME = "main"
 LOCAL_BACKEND_ENABLED = _env_bool("DSTACK_LOCAL_BACKEND_ENABLED", True)
@@ -51,7 +74,8 @@ RUNNER_BINARY_PATH = os.getenv("DSTACK_RUNNER_BINARY_PATH")
 RUNNER_DOWNLOAD_URL = os.getenv("DSTACK_RUNNER_DOWNLOAD_URL")
 SHIM_DOWNLOAD_URL = os.getenv("DSTACK_SHIM_DOWNLOAD_URL")
 
-SERVICE_CLIENT_MAX_BODY_SIZE = int(os.getenv("DSTACK_SERVICE_CLIENT_MAX_BODY_SIZE", str(64 * 1024 * 1024)))
+SERVICE_CLIENT_MAX_BODY_SIZE = int(os.getenv("DSTACK_DEFAULT_SERVICE_CLIENT_MAX_BODY_SIZE")
+                                   or os.getenv("DSTACK_SERVICE_CLIENT_MAX_BODY_SIZE") or 64 * 1024 * 1024)
 ACME_SERVER = os.getenv("DSTACK_ACME_SERVER")
 ACME_EAB_KID = os.getenv("DSTACK_ACME_EAB_KID")
 ACME_EAB_HMAC_KEY = os.getenv("DSTACK_ACME_EAB_HMAC_KEY")

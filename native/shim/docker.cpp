@@ -43,7 +43,7 @@ std::string container_bootstrap_script(const ShimOptions& o, const std::vector<s
     << "if command -v sshd >/dev/null 2>&1; then ssh-keygen -A >/dev/null 2>&1 || true; "
     << "$(command -v sshd) -p " << o.runner_ssh_port
     << " -o PermitUserEnvironment=yes -o PasswordAuthentication=no -o PidFile=none || true; fi\n"
-    << "exec /usr/local/bin/dstack-runner --log-level " << log_level() << " start --http-port " << o.runner_http_port
+    << "exec /usr/local/bin/dstack-runner --log-level " << (o.runner_log_level >= 0 ? o.runner_log_level : log_level()) << " start --http-port " << o.runner_http_port
     << " --temp-dir /tmp/runner --home-dir \"$HOME\" --working-dir /workflow --ssh-env"
     << (o.probe_binary.empty() ? "" : " --probe /usr/local/bin/dstack-probe") << "\n";
   return s.str();

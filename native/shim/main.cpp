@@ -4,7 +4,12 @@
 //   dstack-shim [--log-level N] [--shim-home DIR] [--shim-http-port 10998] [--host 0.0.0.0]
 //               [--runner-binary-path PATH] [--runner-download-url URL] [--probe-binary PATH]
 //               [--runner-http-port 10999] [--runner-ssh-port 10022] [--driver docker|process|auto]
-//               [--privileged] [--service] [--no-startup-probe]
+//               [--runner-log-level N] [--privileged] [--service] [--no-startup-probe]
+//
+// Environment defaults (flags override): DSTACK_SHIM_HOME, DSTACK_SHIM_HTTP_PORT,
+// DSTACK_SHIM_LOG_LEVEL, DSTACK_RUNNER_BINARY_PATH, DSTACK_RUNNER_DOWNLOAD_URL,
+// DSTACK_RUNNER_HTTP_PORT, DSTACK_RUNNER_SSH_PORT, DSTACK_RUNNER_LOG_LEVEL,
+// DSTACK_DOCKER_PRIVILEGED, DSTACK_SERVICE_MODE.
 #include <signal.h>
 #include <stdlib.h>
 #include <sys/wait.h>
@@ -262,6 +267,27 @@ int main(int argc, char** argv) {
   bool service = false;
   bool startup_probe = true;
   if (const char* v = getenv("DSTACK_SHIM_STARTUP_PROBE")) startup_probe = std::string(v) != "0";
+  // environment defaults (the reference's EnvVars, main.go:40-124); command-line flags override them
+  auto env = [](const char* name) -> const char* {
+    const char* v = getenv(name);
+    return v && *v ? v : nullptr;
+  };
+  auto env_true = [&](const char* name) {
+    const char* v = env(name);
+    if (!v) return false;
+    std::string s = v;
+    return s == "1" || s == "true" || s == "TRUE" || s == "True" || s == "yes";
+  };
+  if (const char* v = env("DSTACK_SHIM_HOME")) o.home = v;
+  if (const char* v = env("DSTACK_SHIM_HTTP_PORT")) port = atoi(v);
+  if (const char* v = env("DSTACK_SHIM_LOG_LEVEL")) set_log_level(atoi(v));
+  if (const char* v = env("DSTACK_RUNNER_BINARY_PATH")) o.runner_binary = v;
+  if (const char* v = env("DSTACK_RUNNER_DOWNLOAD_URL")) o.runner_download_url = v;
+  if (const char* v = env("DSTACK_RUNNER_HTTP_PORT")) o.runner_http_port = atoi(v);
+  if (const char* v = env("DSTACK_RUNNER_SSH_PORT")) o.runner_ssh_port = atoi(v);
+  if (const char* v = env("DSTACK_RUNNER_LOG_LEVEL")) o.runner_log_level = atoi(v);
+  if (env_true("DSTACK_DOCKER_PRIVILEGED")) o.privileged = true;
+  if (env_true("DSTACK_SERVICE_MODE")) service = true;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -280,6 +306,7 @@ int main(int argc, char** argv) {
     else if (a == "--probe-binary") o.probe_binary = next();
     else if (a == "--runner-http-port") o.runner_http_port = atoi(next().c_str());
     else if (a == "--runner-ssh-port") o.runner_ssh_port = atoi(next().c_str());
+    else if (a == "--runner-log-level") o.runner_log_level = atoi(next().c_str());
     else if (a == "--driver") o.driver = next();
     else if (a == "--volumes-root") o.volumes_root = next();
     else if (a == "--privileged") o.privileged = true;
@@ -316,10 +343,6 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
-  // env fallbacks (main.go:40-124)
-  if (const char* v = getenv("DSTACK_SHIM_HTTP_PORT")) port = atoi(v);
-  if (const char* v = getenv("DSTACK_RUNNER_BINARY_PATH"); v && o.runner_binary.empty()) o.runner_binary = v;
-  if (const char* v = getenv("DSTACK_RUNNER_DOWNLOAD_URL"); v && o.runner_download_url.empty()) o.runner_download_url = v;
   signal(SIGPIPE, SIG_IGN);
   struct sigaction sa{};
   sa.sa_handler = [](int sig) {

@@ -104,7 +104,8 @@ class ProcessDriver : public TaskDriver {
     } else if (t.config.gpu == 0) {
       envs.push_back("HIP_VISIBLE_DEVICES=-1");  // no GPU granted: hide all devices
     }
-    std::vector<std::string> argv = {o_.runner_binary, "--log-level", std::to_string(log_level()), "start",
+    std::vector<std::string> argv = {o_.runner_binary, "--log-level",
+                                     std::to_string(o_.runner_log_level >= 0 ? o_.runner_log_level : log_level()), "start",
                                      "--http-port", "0", "--port-file", port_file, "--temp-dir", dir + "/tmp",
                                      "--home-dir", dir + "/home", "--working-dir", dir + "/workflow"};
     if (!o_.probe_binary.empty()) {

@@ -115,6 +115,7 @@ struct ShimOptions {
   std::string probe_binary;
   int runner_http_port = 10999;
   int runner_ssh_port = 10022;
+  int runner_log_level = -1;  // -1: the shim's own level
   bool privileged = false;
   std::string docker_socket = "/var/run/docker.sock";
   std::string driver = "auto";  // docker | process | auto

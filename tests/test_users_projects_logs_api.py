@@ -54,7 +54,10 @@ def test_deleted_user_loses_access(client):
 
 
 # ---- projects -------------------------------------------------------------------------------------
-def test_project_quota_for_regular_users(client):
+def test_project_quota_for_regular_users(client, monkeypatch):
+    from dstack_amd.server import settings
+
+    monkeypatch.setattr(settings, "USER_PROJECT_DEFAULT_QUOTA", 3)  # DSTACK_USER_PROJECT_DEFAULT_QUOTA
     h = _user(client, "quota")
     for i in range(3):
         assert client.post("/api/projects/create", json={"project_name": f"q{i}"}, headers=h).status_code == 200
