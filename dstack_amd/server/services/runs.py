@@ -241,14 +241,24 @@ def apply_plan(s: Session, project: ProjectModel, user: UserModel, run_spec: Run
     return submit_run(s, project, user, run_spec)
 
 
-_UPDATABLE = {"replicas", "scaling"}
+# an active run is updated in place only when it is a service and nothing but these changed
+# (reference ``S/services/runs.py:_check_can_update_run_spec``): new code and replica-count /
+# autoscaling / prefix-stripping settings; anything else needs the run stopped and resubmitted
+_UPDATABLE_SPEC = {"repo_code_hash", "configuration"}
+_UPDATABLE = {"replicas", "scaling", "strip_prefix"}
+
+
+def _changed(a: dict, b: dict) -> set:
+    return {k for k in set(a) | set(b) if a.get(k) != b.get(k)}
 
 
 def _updatable(old: RunSpec, new: RunSpec) -> bool:
-    a = old.configuration.model_dump(mode="json")
-    b = new.configuration.model_dump(mode="json")
-    diff = {k for k in set(a) | set(b) if a.get(k) != b.get(k)}
-    return diff <= _UPDATABLE
+    if old.configuration.type != "service" or new.configuration.type != "service":
+        return False
+    spec_diff = _changed(old.model_dump(mode="json"), new.model_dump(mode="json"))
+    if not spec_diff <= _UPDATABLE_SPEC:
+        return False
+    return _changed(old.configuration.model_dump(mode="json"), new.configuration.model_dump(mode="json")) <= _UPDATABLE
 
 
 def stop_runs(s: Session, project: ProjectModel, runs_names: List[str], abort: bool):

@@ -174,6 +174,19 @@ def test_apply_with_changed_commands_stops_old_run(client):
     assert r.json()["jobs"][0]["job_spec"]["commands"][-1].endswith("b")
 
 
+def test_in_place_update_rules(client):
+    """Reference ``_check_can_update_run_spec``: only services, and only replicas / scaling /
+    strip_prefix (plus new code); an identical active task is not "updated"."""
+    _repo(client)
+    _submit(client, "svc2", {"type": "service", "commands": ["x"], "port": 8000})
+    plan = lambda name, conf: client.post("/api/project/main/runs/get_plan", json=_spec(name, conf)).json()  # noqa: E731
+    assert plan("svc2", {"type": "service", "commands": ["x"], "port": 8000, "strip_prefix": False})["action"] == "update"
+    assert plan("svc2", {"type": "service", "commands": ["x"], "port": 8001})["action"] == "create"
+    assert plan("svc2", {"type": "service", "commands": ["x"], "port": 8000, "env": {"A": "1"}})["action"] == "create"
+    _submit(client, "tsk", {"type": "task", "commands": ["a"]})
+    assert plan("tsk", {"type": "task", "commands": ["a"]})["action"] == "create"
+
+
 def test_apply_stale_plan_rejected_unless_forced(client):
     _repo(client)
     _submit(client, "svc", {"type": "service", "commands": ["x"], "port": 8000})
