@@ -170,3 +170,12 @@ class URLNotFoundError(ClientError):
 
 class MethodNotAllowedError(ClientError):
     pass
+
+
+class DockerRegistryError(DstackError):
+    """The registry answered, and not with the image's config (unknown image or tag, no access,
+    malformed or oversized config); ``status`` is the HTTP status when there was one."""
+
+    def __init__(self, msg: str = "", status: int = 0):
+        super().__init__(msg)
+        self.status = status

@@ -16,6 +16,8 @@ from typing import Dict, List, Optional, Tuple
 
 import httpx
 
+from dstack_amd.core.errors import DockerRegistryError
+
 MANIFEST_TYPES = ", ".join([
     "application/vnd.docker.distribution.manifest.list.v2+json",
     "application/vnd.oci.image.index.v1+json",
@@ -58,6 +60,9 @@ def parse_image_name(image: str) -> ImageRef:
     return ImageRef(registry, path, digest or tag)
 
 
+MAX_CONFIG_OBJECT_SIZE = 2**22  # 4 MiB, as the reference
+
+
 class RegistryClient:
     def __init__(self, client: Optional[httpx.Client] = None):
         self.http = client or httpx.Client(timeout=30, follow_redirects=True)
@@ -96,19 +101,24 @@ class RegistryClient:
         state: dict = {}
         r = self._get(f"{base}/manifests/{ref.reference}", {"Accept": MANIFEST_TYPES}, auth, state)
         if r.status_code != 200:
-            raise LookupError(f"{image}: manifest {r.status_code}")
+            raise DockerRegistryError(f"manifest of {ref.repository}:{ref.reference}: HTTP {r.status_code}", r.status_code)
         m = r.json()
         if "manifests" in m:  # index: pick linux/amd64
             chosen = next((x for x in m["manifests"] if x.get("platform", {}).get("os") == "linux"
                            and x.get("platform", {}).get("architecture") == "amd64"), m["manifests"][0])
             r = self._get(f"{base}/manifests/{chosen['digest']}", {"Accept": MANIFEST_TYPES}, auth, state)
             if r.status_code != 200:
-                raise LookupError(f"{image}: platform manifest {r.status_code}")
+                raise DockerRegistryError(f"platform manifest: HTTP {r.status_code}", r.status_code)
             m = r.json()
         r = self._get(f"{base}/blobs/{m['config']['digest']}", {}, auth, state)
         if r.status_code != 200:
-            raise LookupError(f"{image}: config blob {r.status_code}")
-        c = r.json().get("config") or {}
+            raise DockerRegistryError(f"config blob: HTTP {r.status_code}", r.status_code)
+        if len(r.content) > MAX_CONFIG_OBJECT_SIZE:
+            raise DockerRegistryError(f"image config object exceeds the size limit of {MAX_CONFIG_OBJECT_SIZE} bytes")
+        try:
+            c = r.json().get("config") or {}
+        except ValueError as e:
+            raise DockerRegistryError(f"malformed image config: {e}") from e
         cfg = ImageConfig(user=c.get("User") or None, entrypoint=c.get("Entrypoint"), cmd=c.get("Cmd"),
                           env=c.get("Env") or [])
         with self._lock:

@@ -167,13 +167,19 @@ def get_job_specs_from_run_spec(run_spec: RunSpec, replica_num: int = 0,
 
 
 def _image_config(conf):
-    """Registry lookup (cached 80 s); offline / private-without-creds images just skip it."""
+    """Registry lookup (cached 80 s).  A registry that answers "no" (unknown image or tag, no
+    access) fails the submission as in the reference (``jobs/configurators/base.py:_get_image_config``);
+    an unreachable registry (an air-gapped server with a local image mirror on the hosts) only skips
+    the lookup, and the image's own entrypoint/user are then not known to the server."""
+    from dstack_amd.core.errors import DockerRegistryError, ServerClientError
     from dstack_amd.server.services.docker import get_image_config
 
     ra = conf.registry_auth
     try:
         return get_image_config(conf.image, ra.username if ra else None, ra.password if ra else None)
-    except Exception:  # noqa: BLE001 - network/registry errors must not block submission
+    except DockerRegistryError as e:
+        raise ServerClientError(f"Error pulling configuration for image {conf.image!r} from the docker registry: {e}")
+    except Exception:  # noqa: BLE001 - registry unreachable: do not block submission
         return None
 
 

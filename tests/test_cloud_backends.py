@@ -386,6 +386,30 @@ def test_registry_image_config_with_token_challenge():
     assert cfg.user == "1000:1000" and cfg.entrypoint == ["python3", "-m", "vllm"] and cfg.cmd == ["serve"]
 
 
+def test_registry_refusal_fails_submission_unreachable_registry_does_not(monkeypatch):
+    """An unknown image (registry answers 404) fails the job spec with a client error, as in the
+    reference; a registry that cannot be reached only skips the lookup."""
+    from dstack_amd.core.errors import DockerRegistryError, ServerClientError
+    from dstack_amd.core.models.configurations import parse_run_configuration
+    from dstack_amd.server.services import docker as docker_mod
+    from dstack_amd.server.services.jobs import configurators
+
+    rc = docker_mod.RegistryClient(_client(lambda req: httpx.Response(404)))
+    with pytest.raises(DockerRegistryError) as ei:
+        rc.get_image_config("rocm/does-not-exist:1")
+    assert ei.value.status == 404
+    conf = parse_run_configuration({"type": "task", "image": "rocm/does-not-exist:1"})
+    monkeypatch.setattr(docker_mod, "_client", rc)
+    with pytest.raises(ServerClientError, match="Error pulling configuration for image"):
+        configurators._image_config(conf)
+
+    def unreachable(req):
+        raise httpx.ConnectError("no route to host")
+
+    monkeypatch.setattr(docker_mod, "_client", docker_mod.RegistryClient(_client(unreachable)))
+    assert configurators._image_config(conf) is None
+
+
 def _aws_vpc_handler(calls, capacity_fail_az=None, efa=True, reservation_type="capacity-block"):
     def handler(req: httpx.Request):
         form = dict(urllib.parse.parse_qsl(req.content.decode()))
