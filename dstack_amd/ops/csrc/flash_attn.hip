@@ -50,7 +50,17 @@ constexpr int HD = 128;          // head dim
 // it first and the other's softmax VALU fills the gaps; 2 = the softmax phase gets the priority.
 // Measured (3 interleaved runs, S=8192, profiles/fa_prio_ab_r4r.txt): 0 = 0.641-0.650 ms,
 // 1 = 0.659-0.665, 2 = 0.657-0.658 -- both slower, kept opt-in only.
-template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0>
+// STAG (A/B, DSTACK_AMD_FA_FWD_STAG=1; NW = 8): the two waves sharing a SIMD (w and w + 4) run the
+// same per-tile program in lockstep -- both in S = K·Q^T, then both in the softmax VALU while the
+// matrix pipe idles, then both in P·V.  With STAG the second half (w >= 4) defers each tile's P·V
+// into the next iteration, ahead of its own S: one wave's softmax then runs beside the other's
+// MFMAs.  V of the previous tile must outlive one more iteration, so the K/V ring is 3 deep
+// (96 KiB of LDS); the deferred P (4 x bf16x8) is carried in registers across the barrier.
+// Measured (3 interleaved runs, S=8192, profiles/fa_stag_ab_r4x.txt): 0.750-0.757 ms vs 0.664-0.673
+// for the lockstep default, identical outputs -- slower, kept opt-in only.  With one barrier per
+// tile the two halves still meet every tile, so the deferred P·V lands on the partner's S phase
+// (matrix beside matrix on one SIMD) instead of beside its softmax.
+template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0, bool STAG = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
                                                         float* __restrict__ lse, int B, int S,
@@ -83,19 +93,36 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
   float m = -INFINITY, lsum = 0.f;
   const int nkv = CAUSAL ? (q0 + QB) / 64 : S / 64;
+  constexpr int NST = STAG ? 3 : 2;          // K/V ring depth
+  const bool late = STAG && w >= NW / 2;     // wave-uniform: this wave defers its P·V by one tile
+  bf16x8 pbp[4];                             // the deferred P of the previous tile (late waves)
+  bool pend = false;
 
   dma_tile64_n<NW>(kp, rs, smem, w, lane);
   dma_tile64_n<NW>(vp, rs, smem + TILE_BYTES, w, lane);
   wait_dma_and_barrier();
 
+  int stg = 0;  // ring slot of tile it
   for (int it = 0; it < nkv; ++it) {
-    const char* kl = smem + (it & 1) * 2 * TILE_BYTES;
+    const char* kl = smem + stg * 2 * TILE_BYTES;
     const char* vl = kl + TILE_BYTES;
+    const int nstg = stg + 1 == NST ? 0 : stg + 1;
     if (it + 1 < nkv) {
-      char* nk = smem + ((it + 1) & 1) * 2 * TILE_BYTES;
+      char* nk = smem + nstg * 2 * TILE_BYTES;
       dma_tile64_n<NW>(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
       dma_tile64_n<NW>(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
     }
+    if constexpr (STAG) {
+      if (late && pend) {  // P·V of the previous tile, whose V is still in its ring slot
+        const char* pv = smem + (stg == 0 ? NST - 1 : stg - 1) * 2 * TILE_BYTES + TILE_BYTES;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) o[d] = mfma(lds_tr(pv, 16 * s4, 32 * d, lane), pbp[s4], o[d]);
+        pend = false;
+      }
+    }
+    stg = nstg;
     const int kv0 = it * 64;
     if (!CAUSAL || kv0 <= qw0 + 31) {
       f32x16 st[2];
@@ -176,13 +203,28 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
       for (int s4 = 0; s4 < 4; ++s4) pb[s4] = to_bf16x8(st[s4 >> 1], 8 * (s4 & 1));
       if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
       if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(3);
+      if (late) {
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
+        for (int s4 = 0; s4 < 4; ++s4) pbp[s4] = pb[s4];
+        pend = true;
+      } else {
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) o[d] = mfma(lds_tr(vl, 16 * s4, 32 * d, lane), pb[s4], o[d]);
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) o[d] = mfma(lds_tr(vl, 16 * s4, 32 * d, lane), pb[s4], o[d]);
+      }
       if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
     }
     wait_dma_and_barrier();
+  }
+  if constexpr (STAG) {
+    if (late && pend) {  // the last tile's deferred P·V (its V was the last DMA: complete, not overwritten)
+      const char* pv = smem + (stg == 0 ? NST - 1 : stg - 1) * 2 * TILE_BYTES + TILE_BYTES;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) o[d] = mfma(lds_tr(pv, 16 * s4, 32 * d, lane), pbp[s4], o[d]);
+    }
   }
 
   lsum += __shfl_xor(lsum, 32, 64);
@@ -899,9 +941,16 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     const char* v = getenv("DSTACK_AMD_FA_PRIO");
     return v ? atoi(v) : 0;
   }();
+  static const bool stag = [] {
+    const char* v = getenv("DSTACK_AMD_FA_FWD_STAG");
+    return v && atoi(v) == 1;
+  }();
   if (waves == 8 && S % 256 == 0) {
     const int grid = B * H * (S / 256);
-    if (causal && pf && prio == 1)
+    if (causal && pf && stag)
+      fa_fwd_kernel<true, 8, true, 0, true><<<grid, 512, 6 * TILE_BYTES, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S,
+                                                                            H, KVH, sl2, thr);
+    else if (causal && pf && prio == 1)
       fa_fwd_kernel<true, 8, true, 1><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2,
                                                             thr);
     else if (causal && pf && prio == 2)
