@@ -37,15 +37,40 @@ def register_server(sub):
     p.add_argument("-p", "--port", type=int, default=int(os.getenv("DSTACK_SERVER_PORT", "3000")))
     p.add_argument("-l", "--log-level", default=os.getenv("DSTACK_SERVER_LOG_LEVEL", "INFO"))
     p.add_argument("--token", default=os.getenv("DSTACK_SERVER_ADMIN_TOKEN"), help="Admin token")
-    p.add_argument("-y", "--yes", action="store_true")
+    p.add_argument("-y", "--yes", action="store_true",
+                   help="Make the server's project the CLI default without asking")
+    p.add_argument("-n", "--no", action="store_true", help="Do not touch the CLI config")
     p.set_defaults(func=cmd_server)
 
 
 def cmd_server(args) -> int:
+    if args.yes:
+        os.environ["DSTACK_UPDATE_DEFAULT_PROJECT"] = "1"
+    if args.no:
+        os.environ["DSTACK_DO_NOT_UPDATE_DEFAULT_PROJECT"] = "1"
+    from dstack_amd.server import settings
     from dstack_amd.server.main import run
 
+    settings.UPDATE_DEFAULT_PROJECT = settings.UPDATE_DEFAULT_PROJECT or args.yes
+    settings.DO_NOT_UPDATE_DEFAULT_PROJECT = settings.DO_NOT_UPDATE_DEFAULT_PROJECT or args.no
     run(args.host, args.port, args.log_level, args.token)
     return 0
+
+
+def _show(args, render) -> int:
+    """Print ``render()`` once, or with ``--watch`` re-render it every second until Ctrl-C."""
+    if not getattr(args, "watch", False):
+        print_table(render())
+        return 0
+    from rich.live import Live
+
+    try:
+        with Live(render(), console=console, refresh_per_second=2) as live:
+            while True:
+                time.sleep(1)
+                live.update(render())
+    except KeyboardInterrupt:
+        return 0
 
 
 # ---- config / init ----------------------------------------------------------------------------
@@ -420,10 +445,12 @@ def register_fleet(sub):
     p = sub.add_parser("fleet", help="Manage fleets")
     add_project_arg(p)
     p.add_argument("-v", "--verbose", action="store_true")
+    p.add_argument("-w", "--watch", action="store_true", help="Update listing in realtime")
     p.set_defaults(func=cmd_fleet_list)
     s = p.add_subparsers(dest="fleet_cmd")
     lp = s.add_parser("list")
     lp.add_argument("-v", "--verbose", action="store_true")
+    lp.add_argument("-w", "--watch", action="store_true", help="Update listing in realtime")
     add_project_arg(lp)
     lp.set_defaults(func=cmd_fleet_list)
     dp = s.add_parser("delete")
@@ -436,8 +463,8 @@ def register_fleet(sub):
 
 def cmd_fleet_list(args) -> int:
     client = _client(args)
-    print_table(fleets_table(client.api.fleets.list(client.project), verbose=getattr(args, "verbose", False)))
-    return 0
+    return _show(args, lambda: fleets_table(client.api.fleets.list(client.project),
+                                            verbose=getattr(args, "verbose", False)))
 
 
 def cmd_fleet_delete(args) -> int:
@@ -456,11 +483,13 @@ def cmd_fleet_delete(args) -> int:
 def register_volume(sub):
     p = sub.add_parser("volume", help="Manage volumes")
     add_project_arg(p)
+    p.add_argument("-w", "--watch", action="store_true", help="Update listing in realtime")
     p.set_defaults(func=cmd_volume_list, verbose=False)
     s = p.add_subparsers(dest="volume_cmd")
     lp = s.add_parser("list")
     add_project_arg(lp)
     lp.add_argument("-v", "--verbose", action="store_true")
+    lp.add_argument("-w", "--watch", action="store_true", help="Update listing in realtime")
     lp.set_defaults(func=cmd_volume_list)
     dp = s.add_parser("delete")
     add_project_arg(dp)
@@ -471,8 +500,7 @@ def register_volume(sub):
 
 def cmd_volume_list(args) -> int:
     client = _client(args)
-    print_table(volumes_table(client.api.volumes.list(client.project)))
-    return 0
+    return _show(args, lambda: volumes_table(client.api.volumes.list(client.project)))
 
 
 def cmd_volume_delete(args) -> int:
@@ -486,11 +514,13 @@ def cmd_volume_delete(args) -> int:
 def register_gateway(sub):
     p = sub.add_parser("gateway", help="Manage gateways")
     add_project_arg(p)
+    p.add_argument("-w", "--watch", action="store_true", help="Update listing in realtime")
     p.set_defaults(func=cmd_gateway_list)
     s = p.add_subparsers(dest="gateway_cmd")
     lp = s.add_parser("list")
     add_project_arg(lp)
     lp.add_argument("-v", "--verbose", action="store_true")
+    lp.add_argument("-w", "--watch", action="store_true", help="Update listing in realtime")
     lp.set_defaults(func=cmd_gateway_list)
     cp = s.add_parser("create")
     add_project_arg(cp)
@@ -515,8 +545,7 @@ def register_gateway(sub):
 
 def cmd_gateway_list(args) -> int:
     client = _client(args)
-    print_table(gateways_table(client.api.gateways.list(client.project)))
-    return 0
+    return _show(args, lambda: gateways_table(client.api.gateways.list(client.project)))
 
 
 def cmd_gateway_create(args) -> int:

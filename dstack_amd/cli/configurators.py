@@ -232,6 +232,20 @@ def validate_gpu_vendor_and_image(conf) -> None:
                                  "(the default image is ROCm-only)")
 
 
+def detect_vscode_version(exe: str = "code") -> Optional[str]:
+    """The commit hash of the local VS Code (second line of ``code --version``), or None."""
+    import subprocess
+
+    try:
+        r = subprocess.run([exe, "--version"], capture_output=True, text=True, timeout=20)
+    except (OSError, subprocess.TimeoutExpired):
+        return None
+    lines = r.stdout.splitlines()
+    if r.returncode != 0 or len(lines) < 2:
+        return None
+    return lines[1].strip() or None
+
+
 # ---- run configurator -------------------------------------------------------------------------
 class RunConfigurator:
     TYPES = ("task", "service", "dev-environment")
@@ -262,6 +276,14 @@ class RunConfigurator:
             conf.ports = merge_ports(conf.ports, [PortMapping.parse(p) for p in args.ports])
         interpolate_registry_auth(conf)
         validate_gpu_vendor_and_image(conf)
+        if getattr(conf, "type", None) == "dev-environment" and conf.ide == "vscode" and conf.version is None:
+            # the IDE server in the container matches the local VS Code (commit hash), so the
+            # desktop client attaches without reinstalling it
+            conf.version = detect_vscode_version()
+            if conf.version is None:
+                console.print("[secondary]Unable to detect the VS Code version and pre-install extensions. "
+                              "Run [code]Shell Command: Install 'code' command in PATH[/] from the VS Code "
+                              "Command Palette to fix it.[/]")
 
     def apply(self, client: Client, conf, conf_path: str, args) -> int:
         self.apply_args(conf, args)

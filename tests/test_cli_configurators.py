@@ -199,3 +199,19 @@ def test_dstack_config_writes_project():
         cfg = yaml.safe_load(f)
     assert cfg["projects"] == [{"default": True, "name": "project", "token": "token",
                                 "url": "http://127.0.0.1:31313"}]
+
+
+def test_dev_environment_pins_local_vscode_version(tmp_path, monkeypatch):
+    """``ide: vscode`` without ``version``: the local VS Code's commit (``code --version`` line 2)
+    is pinned so the container's IDE server matches the desktop client; no ``code``: left unset."""
+    from dstack_amd.core.models.configurations import DevEnvironmentConfiguration
+
+    commit = "1a5daa3a0231a0fbba4f14db7ec463cf99d7768e"
+    code = tmp_path / "code"
+    code.write_text(f"#!/bin/sh\necho 1.97.2\necho {commit}\necho x64\n")
+    code.chmod(0o755)
+    dev = DevEnvironmentConfiguration.model_validate({"type": "dev-environment", "ide": "vscode"})
+    monkeypatch.setenv("PATH", f"{tmp_path}:/usr/bin:/bin")
+    assert _run_args(dev, []).version == commit
+    monkeypatch.setenv("PATH", "/nonexistent")
+    assert _run_args(dev, []).version is None
