@@ -69,6 +69,19 @@ class Run:
             return url if url.startswith("http") else self._api.base_url + url
         return f"{self._api.base_url}/proxy/services/{self._project}/{self.name}/"
 
+    @property
+    def service_model(self) -> Optional["ServiceModel"]:
+        """The OpenAI-compatible model a service publishes (``model:`` in its configuration): its
+        name and the base URL of the model endpoint (in-server ``/proxy/models/<project>`` or the
+        gateway's)."""
+        if not isinstance(self._run.run_spec.configuration, ServiceConfiguration):
+            raise ValueError("The run is not a service")
+        svc = self._run.service
+        if svc is None or svc.model is None:
+            return None
+        url = svc.model.base_url
+        return ServiceModel(svc.model.name, url if url.startswith("http") else self._api.base_url + url)
+
     def _latest_submission(self, replica_num: int = 0, job_num: int = 0):
         for j in self._run.jobs:
             if j.job_spec.replica_num == replica_num and j.job_spec.job_num == job_num:
@@ -149,11 +162,28 @@ class Run:
         return f"<Run '{self.name}' {self.status.value}>"
 
 
+class ServiceModel:
+    def __init__(self, name: str, url: str):
+        self.name = name
+        self.url = url
+
+    def __repr__(self) -> str:
+        return f"<ServiceModel {self.name!r}>"
+
+
 class RunCollection:
     def __init__(self, api: APIClient, project: str, client: "Client"):
         self._api = api
         self._project = project
         self._client = client
+
+    def get_offers(self, profile, requirements):
+        """Offers (pool instances and backends) for a profile + requirements pair."""
+        return self._api.pool.get_offers(self._project, profile, requirements)
+
+    def create_instance(self, profile, requirements):
+        """Provision an instance from the best offer without a run (``dstack pool add``)."""
+        return self._api.pool.create_instance(self._project, profile, requirements)
 
     def _upload(self, repo: Repo) -> Optional[str]:
         buf = io.BytesIO()

@@ -83,3 +83,22 @@ def test_users_and_projects_via_api_client(api):
     assert "team" not in [x.project_name for x in api.projects.list()]
     api.users.delete(["alice"])
     assert "alice" not in [x.username for x in api.users.list()]
+
+
+def test_service_url_and_model_and_offers(dc):
+    from dstack_amd.api import OpenAIChatModel, Service
+    from dstack_amd.core.models.profiles import Profile
+    from dstack_amd.core.models.resources import ResourcesSpec
+    from dstack_amd.core.models.runs import Requirements
+
+    svc = Service(commands=["python3 -m http.server 8000"], port=8000, name="api-svc",
+                  model=OpenAIChatModel(name="llama", format="openai"))
+    run = dc.runs.submit(svc, VirtualRepo())
+    assert run.service_url == "http://testserver/proxy/services/main/api-svc/"
+    m = run.service_model
+    assert m.name == "llama" and m.url == "http://testserver/proxy/models/main"
+    task = dc.runs.submit(Task(commands=["true"], name="api-task"), VirtualRepo())
+    with pytest.raises(ValueError):
+        task.service_model
+    offers = dc.runs.get_offers(Profile(name="p"), Requirements(resources=ResourcesSpec()))
+    assert offers.instances and all(o.backend.value == "local" for o in offers.instances)
