@@ -269,6 +269,40 @@ class RepoCollection:
         except Exception:  # noqa: BLE001
             return False
 
+    def load(self, repo_dir: str, local: bool = False, init: bool = False,
+             git_identity_file: Optional[str] = None, oauth_token: Optional[str] = None) -> Repo:
+        """The repo of a local directory (reference ``RepoCollection.load``).
+
+        ``init=False``: the directory must have been initialised (``dstack init`` or
+        ``load(..., init=True)``), both in the CLI config and on the server.  ``init=True``: a git
+        checkout with a remote becomes a ``RemoteRepo`` (unless ``local``), anything else a
+        ``LocalRepo``; it is initialised in the project and recorded in the CLI config."""
+        from dstack_amd.core.errors import ConfigurationError
+        from dstack_amd.core.models.repos import LocalRepo, RemoteRepo
+        from dstack_amd.core.services.configs import ConfigManager
+
+        cm = ConfigManager()
+        hint = "The repo is not initialized. Run `dstack init` in it or load it with init=True."
+        if not init:
+            rc = cm.get_repo_config(repo_dir)
+            if rc is None:
+                raise ConfigurationError(hint)
+            repo = LocalRepo(repo_dir, rc.repo_id) if rc.repo_type == "local" else RemoteRepo(repo_dir,
+                                                                                              repo_id=rc.repo_id)
+            if not self.is_initialized(repo):
+                raise ConfigurationError(hint)
+            return repo
+        repo: Repo = LocalRepo(repo_dir)
+        if not local:
+            try:
+                repo = RemoteRepo(repo_dir)
+            except Exception:  # noqa: BLE001 - not a git checkout, or no remote: upload the tree
+                repo = LocalRepo(repo_dir)
+        self.init(repo, git_identity_file, oauth_token)
+        key = git_identity_file or str(cm.ensure_ssh_key())
+        cm.save_repo_config(repo_dir, repo.repo_id, "local" if isinstance(repo, LocalRepo) else "remote", key)
+        return repo
+
 
 class FleetCollection:
     def __init__(self, api: APIClient, project: str):

@@ -102,3 +102,19 @@ def test_service_url_and_model_and_offers(dc):
         task.service_model
     offers = dc.runs.get_offers(Profile(name="p"), Requirements(resources=ResourcesSpec()))
     assert offers.instances and all(o.backend.value == "local" for o in offers.instances)
+
+
+def test_repo_collection_load(dc, tmp_path, monkeypatch):
+    from dstack_amd.core.errors import ConfigurationError
+    from dstack_amd.core.models.repos import LocalRepo
+
+    monkeypatch.setenv("DSTACK_DIR", str(tmp_path / "home"))
+    work = tmp_path / "work"
+    work.mkdir()
+    (work / "train.py").write_text("print(1)\n")
+    with pytest.raises(ConfigurationError):
+        dc.repos.load(str(work))
+    repo = dc.repos.load(str(work), init=True)
+    assert isinstance(repo, LocalRepo) and dc.repos.is_initialized(repo)
+    again = dc.repos.load(str(work))
+    assert isinstance(again, LocalRepo) and again.repo_id == repo.repo_id
