@@ -243,3 +243,17 @@ def test_own_example_configurations(path):
         data = yaml.safe_load(f)
     conf = parse_apply_configuration(data)
     assert conf.type == data["type"]
+
+
+def test_configuration_reference_doc_is_current():
+    """docs/reference/dstack.yml.md is generated from the models: regenerate it
+    (``python tools/gen_config_reference.py``) after changing a configuration field."""
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("gen_config_reference",
+                                                  os.path.join(root, "tools", "gen_config_reference.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    with open(os.path.join(root, "docs", "reference", "dstack.yml.md")) as f:
+        assert f.read() == mod.render()
