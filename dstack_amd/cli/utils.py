@@ -155,20 +155,37 @@ def plan_table(plan: RunPlan, max_offers: int = 3) -> Table:
 
 def fleets_table(fleets, verbose: bool = False) -> Table:
     t = Table(box=None, header_style="bold")
-    for col in ("FLEET", "INSTANCE", "BACKEND", "RESOURCES", "PRICE", "STATUS", "CREATED"):
+    cols = ["FLEET", "INSTANCE", "BACKEND", "RESOURCES", "PRICE", "STATUS", "CREATED"]
+    if verbose:
+        cols.append("GPU HEALTH")  # the HIP probe: HBM TB/s, bf16 MFMA TF/s, xGMI / RCCL GB/s
+    for col in cols:
         t.add_column(col, no_wrap=col != "RESOURCES")
     for f in fleets:
         if not f.instances:
-            t.add_row(f.name, "", "", "", "", f.status.value, pretty_date(f.created_at))
+            t.add_row(f.name, "", "", "", "", f.status.value, pretty_date(f.created_at), *([""] if verbose else []))
         for i, inst in enumerate(f.instances):
             res = inst.instance_type.resources.pretty_format() if inst.instance_type else ""
             st = inst.status.value + (" (unreachable)" if inst.unreachable else "")
             if inst.total_blocks and inst.total_blocks > 1:
                 st += f" {inst.busy_blocks}/{inst.total_blocks} busy"
-            t.add_row(f.name if i == 0 else "", str(inst.instance_num),
-                      f"{inst.backend.value if inst.backend else ''} ({inst.region or ''})", res,
-                      f"${inst.price:.4g}" if inst.price is not None else "", st, pretty_date(inst.created))
+            row = [f.name if i == 0 else "", str(inst.instance_num),
+                   f"{inst.backend.value if inst.backend else ''} ({inst.region or ''})", res,
+                   f"${inst.price:.4g}" if inst.price is not None else "", st, pretty_date(inst.created)]
+            if verbose:
+                row.append(health_summary(inst.health))
+            t.add_row(*row)
     return t
+
+
+def health_summary(h) -> str:
+    if not h:
+        return "-"
+    parts = ["ok" if h.get("healthy", True) else f"[red]{h.get('message') or 'unhealthy'}[/]"]
+    for key, unit in (("hbm_tb_s", "TB/s HBM"), ("mfma_bf16_tflops", "TF/s bf16"), ("xgmi_gb_s", "GB/s xGMI"),
+                      ("rccl_busbw_gb_s", "GB/s RCCL")):
+        if h.get(key):
+            parts.append(f"{float(h[key]):.4g} {unit}")
+    return ", ".join(parts)
 
 
 def volumes_table(volumes, verbose: bool = False) -> Table:
