@@ -60,6 +60,10 @@ constexpr int HD = 128;          // head dim
 // for the lockstep default, identical outputs -- slower, kept opt-in only.  With one barrier per
 // tile the two halves still meet every tile, so the deferred P·V lands on the partner's S phase
 // (matrix beside matrix on one SIMD) instead of beside its softmax.
+// PRIO 3 (DSTACK_AMD_FA_HALF_PRIO=1, also for the 8-wave dK/dV and dQ passes): one s_setprio 1 for
+// waves 4-7 at kernel start, no per-phase flips.  Measured (4 interleaved runs, S=8192,
+// profiles/fa_hprio_ab_r4y.txt): forward 0.656-0.670 vs 0.657-0.668 ms, backward 2.018-2.036 vs
+// 2.009-2.053 ms -- within noise, kept opt-in.
 template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0, bool STAG = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
@@ -80,6 +84,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
   const bf16_t* kp = base + (H + kvh) * HD;
   const bf16_t* vp = base + (H + KVH + kvh) * HD;
   const int q0 = qb * QB, qw0 = q0 + 32 * w, myq = qw0 + l32;
+  // PRIO 3: static priority for the second-dispatched half (the arbitration loser of each SIMD pair)
+  if constexpr (PRIO == 3) {
+    if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
 
   bf16x8 qf[8];
 #pragma unroll
@@ -451,7 +459,7 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 // which brings a wave under 256 registers: 2 waves per SIMD hide each other's LDS/exp latency.
 // LDS: K|V (64 KiB) + 2-stage Q/dO/lse/delta ring (65 KiB) = 129 KiB -> one workgroup per CU.
 // ================================================================================================
-template <bool CAUSAL, bool SEED = false>
+template <bool CAUSAL, bool SEED = false, bool HP = false>
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
@@ -461,6 +469,9 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
   constexpr int STAGE = 2 * TILE_BYTES + 512;        // Q (64) | dO (64) | lse | delta
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
   const int g = w & 3, qh = w >> 2, w4 = w & 3;
+  if constexpr (HP) {
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   const int NH = H + 2 * KVH;
   const long rs = (long)NH * HD;
   const long ors = (long)H * HD;
@@ -809,7 +820,7 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __re
 // ================================================================================================
 // Backward dQ pass: workgroup = 128 queries of one (b, q-head); loops over 64-key K/V tiles.
 // ================================================================================================
-template <bool CAUSAL, int NW = 4>
+template <bool CAUSAL, int NW = 4, bool HP = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
                                                            const bf16_t* __restrict__ dout,
                                                            const float* __restrict__ lse,
@@ -822,6 +833,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(con
   const long rs = (long)NH * HD;
   const long ors = (long)H * HD;
   constexpr int QB = 32 * NW;
+  if constexpr (HP) {
+    if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
   const int nqb = S / QB;
   const int bid = blockIdx.x;
   const int qb = CAUSAL ? nqb - 1 - bid / (B * H) : bid / (B * H);
@@ -945,9 +959,16 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     const char* v = getenv("DSTACK_AMD_FA_FWD_STAG");
     return v && atoi(v) == 1;
   }();
+  static const bool half_prio = [] {
+    const char* v = getenv("DSTACK_AMD_FA_HALF_PRIO");
+    return v && atoi(v) == 1;
+  }();
   if (waves == 8 && S % 256 == 0) {
     const int grid = B * H * (S / 256);
-    if (causal && pf && stag)
+    if (causal && pf && half_prio)
+      fa_fwd_kernel<true, 8, true, 3><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2,
+                                                            thr);
+    else if (causal && pf && stag)
       fa_fwd_kernel<true, 8, true, 0, true><<<grid, 512, 6 * TILE_BYTES, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S,
                                                                             H, KVH, sl2, thr);
     else if (causal && pf && prio == 1)
@@ -1023,6 +1044,10 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     return (v && atoi(v) == 4) ? 4 : 8;
   }();
   const int dq_waves = (dq_waves_env == 8 && S % 256 == 0) ? 8 : 4;
+  static const bool half_prio = [] {  // static priority for waves 4-7 (see the forward's PRIO 3)
+    const char* v = getenv("DSTACK_AMD_FA_HALF_PRIO");
+    return v && atoi(v) == 1;
+  }();
 #define DSA_DKDV(C, N)                                                                                 \
   do {                                                                                                 \
     if (dkdv_kind >= 64 && S % 256 == 0) {                                                             \
@@ -1036,6 +1061,9 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     } else if (dkdv_kind == 9) {                                                                      \
       fa_bwd_dkdv8_kernel<C, true><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(     \
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
+    } else if ((dkdv8 || dkdv_kind >= 64) && half_prio) {                                              \
+      fa_bwd_dkdv8_kernel<C, false, true><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>( \
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
     } else if (dkdv8 || dkdv_kind >= 64) {                                                             \
       fa_bwd_dkdv8_kernel<C><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(          \
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
@@ -1046,7 +1074,10 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   if (causal) {
     if (dkdv_qt == 128) DSA_DKDV(true, 4); else DSA_DKDV(true, 2);
     DSA_CHECK(hipGetLastError());
-    if (dq_waves == 8)
+    if (dq_waves == 8 && half_prio)
+      fa_bwd_dq_kernel<true, 8, true><<<B * H * (S / 256), 512, lds_q, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    else if (dq_waves == 8)
       fa_bwd_dq_kernel<true, 8><<<B * H * (S / 256), 512, lds_q, st>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
     else

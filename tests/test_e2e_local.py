@@ -384,7 +384,14 @@ def test_cli_deprecated_run_and_pool(server, tmp_path):
     r = subprocess.run(dstack + ["run", str(proj), "-y"], cwd=tmp_path, env=env, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "via-run" in r.stdout and "deprecated" in r.stdout
+    if "via-run" not in r.stdout:  # tell a lost log line from a CLI streaming race
+        stored = subprocess.run(dstack + ["logs", "e2e-run"], cwd=tmp_path, env=env, capture_output=True, text=True,
+                                timeout=60)
+        diag = subprocess.run(dstack + ["logs", "e2e-run", "-d"], cwd=tmp_path, env=env, capture_output=True,
+                              text=True, timeout=60)
+        pytest.fail(f"apply output lacks the job's line; stored logs: {stored.stdout!r}; runner log tail: "
+                    f"{diag.stdout[-1500:]!r}")
+    assert "deprecated" in r.stdout
     r = subprocess.run(dstack + ["pool", "create", "-n", "cli-pool"], env=env, capture_output=True, text=True,
                        timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr

@@ -305,19 +305,19 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
     variants = {"default": {}, "dkdv4": {"DSTACK_AMD_FA_DKDV": "4w"},
                 "fwd4_dq4": {"DSTACK_AMD_FA_FWD_WAVES": "4", "DSTACK_AMD_FA_DQ_WAVES": "4"},
                 "fwd_pf0": {"DSTACK_AMD_FA_FWD_PF": "0"}, "exact_max": {"DSTACK_AMD_FA_RESCALE_THR": "0"},
-                "fwd_stag": {"DSTACK_AMD_FA_FWD_STAG": "1"}}
+                "fwd_stag": {"DSTACK_AMD_FA_FWD_STAG": "1"}, "half_prio": {"DSTACK_AMD_FA_HALF_PRIO": "1"}}
     out = {}
     for name, extra in variants.items():
         env = dict(os.environ)
         for k in ("DSTACK_AMD_FA_DKDV", "DSTACK_AMD_FA_FWD_WAVES", "DSTACK_AMD_FA_DQ_WAVES", "DSTACK_AMD_FA_FWD_PF",
-                  "DSTACK_AMD_FA_RESCALE_THR", "DSTACK_AMD_FA_FWD_STAG"):
+                  "DSTACK_AMD_FA_RESCALE_THR", "DSTACK_AMD_FA_FWD_STAG", "DSTACK_AMD_FA_HALF_PRIO"):
             env.pop(k, None)
         env.update(extra)
         subprocess.run([sys.executable, "-c", script, str(tmp_path / f"{name}.pt")], env=env, check=True,
                        timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         out[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
     ref_o, ref_g = out["default"]["o"].float(), out["default"]["g"].float()
-    for name in ("dkdv4", "fwd4_dq4", "fwd_pf0", "exact_max", "fwd_stag"):
+    for name in ("dkdv4", "fwd4_dq4", "fwd_pf0", "exact_max", "fwd_stag", "half_prio"):
         o, g = out[name]["o"].float(), out[name]["g"].float()
         assert ((o - ref_o).norm() / ref_o.norm()).item() < 2e-3, name
         assert ((g - ref_g).norm() / ref_g.norm()).item() < 2e-3, name
