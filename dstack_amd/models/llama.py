@@ -118,7 +118,10 @@ class Llama(nn.Module):
         self.param_waiter = None
 
     @torch.no_grad()
-    def init_weights(self, std: float = 0.02, seed: int = 0):
+    def init_weights(self, std: float = 0.02, seed: int = 0, lm_head_std: float | None = None):
+        """Normal(0, std) weights, GPT-2 residual scaling (std / sqrt(2 L)) for the projections
+        that write into the residual stream, unit norms.  ``lm_head_std`` overrides the output
+        head's std (0 = zero-init: uniform logits, an initial loss of exactly ln(vocab))."""
         g = torch.Generator(device=self.embed.device).manual_seed(seed)
         out_std = std / math.sqrt(2 * self.cfg.n_layers)
         for name, p in self.named_parameters():
@@ -128,6 +131,11 @@ class Llama(nn.Module):
                 p.normal_(0.0, out_std, generator=g)
             else:
                 p.normal_(0.0, std, generator=g)
+        if lm_head_std is not None:
+            if lm_head_std == 0:
+                self.lm_head.zero_()
+            else:
+                self.lm_head.normal_(0.0, lm_head_std, generator=g)
 
     def rope_tables(self, seq_len: int, device):
         key = (seq_len, str(device))

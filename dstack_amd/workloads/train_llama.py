@@ -63,7 +63,7 @@ class Trainer:
     def __init__(self, model_name: str, seq_len: int, micro_batch: int, device, lr: float = 3e-4,
                  seed: int = 0, bucket_numel: int = 256 * 1024 * 1024, grad_accum: int = 1,
                  lr_warmup: int = 0, lr_decay_steps: int = 0, min_lr_ratio: float = 0.1, data: str = "synthetic-lm",
-                 data_rows: int = 4, clip_grad_norm: float = 0.0):
+                 data_rows: int = 4, clip_grad_norm: float = 0.0, lm_head_std: float | None = None):
         self.cfg = CONFIGS[model_name]
         # LR schedule: linear warmup over ``lr_warmup`` optimizer steps, then constant, or cosine
         # decay to ``min_lr_ratio * lr`` at step ``lr_decay_steps`` when that is set.  A random-init
@@ -81,7 +81,7 @@ class Trainer:
         with torch.device(device):
             model = Llama(self.cfg)
         model.to(dtype)
-        model.init_weights(seed=seed)
+        model.init_weights(seed=seed, lm_head_std=lm_head_std)
         self.model = model
         self.opt = ZeroOptimizer(model, lr=lr, bucket_numel=bucket_numel, clip_grad_norm=clip_grad_norm)
         self.opt.install_prefetch_hooks(model)

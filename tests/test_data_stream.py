@@ -41,3 +41,20 @@ def test_loss_floor_and_row_starts():
     assert s.loss_floor < math.log(1000)
     # every row starts from a fresh sample (no chain crosses rows)
     assert not bool(s.row_start[1:65].any()) and bool(s.row_start[65])
+
+
+def test_zero_output_head_starts_at_ln_vocab():
+    """``init_weights(lm_head_std=0)``: uniform logits, so the first loss is exactly ln(vocab)."""
+    import math
+
+    import torch
+
+    from dstack_amd.models.llama import CONFIGS, Llama
+
+    cfg = CONFIGS["llama-tiny"]
+    m = Llama(cfg)
+    m.init_weights(seed=1, lm_head_std=0.0)
+    tok = torch.randint(0, cfg.vocab_size, (2, 65), generator=torch.Generator().manual_seed(0))
+    with torch.no_grad():
+        loss = m.loss(tok[:, :-1], tok[:, 1:]).item()
+    assert abs(loss - math.log(cfg.vocab_size)) < 1e-4

@@ -24,10 +24,11 @@ ap.add_argument("--lr", type=float, default=3e-4)
 ap.add_argument("--lr-warmup", type=int, default=100)
 ap.add_argument("--data", default="synthetic-lm")
 ap.add_argument("--clip", type=float, default=0.0, help="global grad-norm clip (ZeroOptimizer clip_grad_norm)")
+ap.add_argument("--lm-head-std", type=float, default=None, help="output head init std (0 = zero-init)")
 a = ap.parse_args()
 CONFIGS["ab"] = dataclasses.replace(CONFIGS["llama-3-8b"], name="ab", n_layers=a.layers)
 tr = Trainer("ab", a.seq_len, 1, torch.device("cuda", 0), lr=a.lr, lr_warmup=a.lr_warmup, grad_accum=a.grad_accum,
-             data=a.data, data_rows=1, clip_grad_norm=a.clip)
+             data=a.data, data_rows=1, clip_grad_norm=a.clip, lm_head_std=a.lm_head_std)
 norms = []
 _orig_step = tr.opt.step
 
@@ -52,4 +53,4 @@ for i in range(a.steps):
     print(f"step {i + 1} loss={losses[-1]} gnorm={norms[-1] if norms else None} t={time.time() - t0:.1f}s",
           flush=True)
 print(json.dumps({"ops": os.environ.get("DSTACK_AMD_OPS", "hip"), "layers": a.layers, "lr": a.lr,
-                  "lr_warmup": a.lr_warmup, "clip": a.clip, "losses": losses, "grad_norms": norms, "step_s": times}), flush=True)
+                  "lr_warmup": a.lr_warmup, "clip": a.clip, "lm_head_std": a.lm_head_std, "losses": losses, "grad_norms": norms, "step_s": times}), flush=True)
