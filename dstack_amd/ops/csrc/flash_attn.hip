@@ -459,11 +459,14 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 // which brings a wave under 256 registers: 2 waves per SIMD hide each other's LDS/exp latency.
 // LDS: K|V (64 KiB) + 2-stage Q/dO/lse/delta ring (65 KiB) = 129 KiB -> one workgroup per CU.
 // ================================================================================================
-template <bool CAUSAL, bool SEED = false, bool HP = false>
+// SPILL: also write dS (bf16, the same values that feed dK) to dsg = [B*H][S queries][S keys] for
+// the recompute-free dQ pass below; keys are stored in the MFMA A-operand order of a 16-key chunk
+// ({0-3, 8-11 | 4-7, 12-15}) so a dQ lane loads its 8 keys as one 16-byte vector.
+template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false>
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
-    int H, int KVH, float scale_log2) {
+    int H, int KVH, float scale_log2, bf16_t* __restrict__ dsg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KV_BYTES = 2 * 128 * 256;            // K (128 rows) | V (128 rows)
   constexpr int STAGE = 2 * TILE_BYTES + 512;        // Q (64) | dO (64) | lse | delta
@@ -573,6 +576,15 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
       for (int k2 = 0; k2 < 2; ++k2) {
         pb[k2] = to_bf16x8(sc, 8 * k2);
         dsb[k2] = to_bf16x8(dpv, 8 * k2);
+      }
+      if constexpr (SPILL) {  // lane = key mykey, register 4*rr+i = query qlo + 8*rr + 4*hf + i
+        const int o = mykey & 15;
+        const int pk = (mykey & ~15) | (((o >> 2) & 1) << 3) | (((o >> 3) & 1) << 2) | (o & 3);
+        bf16_t* drow = dsg + ((long)bh * S + qlo + 4 * hf) * S + pk;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) drow[(long)(8 * rr + i) * S] = f2bf(dpv[4 * rr + i]);
       }
 #pragma unroll
       for (int d = 0; d < 4; ++d)
@@ -924,6 +936,86 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(con
 }
 
 // ================================================================================================
+// Backward dQ pass without recompute: dQ = dS . K with dS read back from the dK/dV pass's spill
+// (fa_bwd_dkdv8_kernel<..., SPILL>): one GEMM per tile instead of three (S, dP, dQ), no Q/dO/lse/
+// delta.  The dS tile is loaded straight into A-operand registers one tile ahead; K tiles go
+// through the same double-buffered LDS ring as fa_bwd_dq_kernel.  Causal: keys > query are zeroed
+// on load (the dK/dV pass never writes fully masked 32x32 sub-tiles).
+// ================================================================================================
+template <bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW) void fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ qkv,
+                                                               const bf16_t* __restrict__ dsg,
+                                                               bf16_t* __restrict__ dqkv, int B, int S, int H,
+                                                               int KVH, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
+  const int NH = H + 2 * KVH;
+  const long rs = (long)NH * HD;
+  constexpr int QB = 32 * NW;
+  const int nqb = S / QB;
+  const int bid = blockIdx.x;
+  const int qb = CAUSAL ? nqb - 1 - bid / (B * H) : bid / (B * H);
+  const int bh = bid % (B * H);
+  const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
+  const bf16_t* kp = qkv + (long)b * S * rs + (H + kvh) * HD;
+  const int q0 = qb * QB, qw0 = q0 + 32 * w, myq = qw0 + l32;
+  const bf16_t* dsr = dsg + ((long)bh * S + myq) * S + 8 * hf;
+  f32x16 dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+  const int nkv = CAUSAL ? (q0 + QB) / 64 : S / 64;
+  const int nmine = CAUSAL ? (qw0 + 31) / 64 + 1 : nkv;  // tiles with kv0 <= qw0 + 31
+  us8 a[4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) a[s4] = *reinterpret_cast<const us8*>(dsr + 16 * s4);
+  dma_tile64_n<NW>(kp, rs, smem, w, lane);
+  wait_dma_and_barrier();
+  for (int it = 0; it < nkv; ++it) {
+    const char* kl = smem + (it & 1) * TILE_BYTES;
+    if (it + 1 < nkv) dma_tile64_n<NW>(kp + (long)(it + 1) * 64 * rs, rs, smem + ((it + 1) & 1) * TILE_BYTES, w, lane);
+    const int kv0 = it * 64;
+    if (it < nmine) {
+      us8 an[4];
+      if (it + 1 < nmine) {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) an[s4] = *reinterpret_cast<const us8*>(dsr + kv0 + 64 + 16 * s4);
+      }
+      if (CAUSAL && kv0 + 63 > qw0) {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int key = kv0 + 16 * s4 + 4 * hf + (j & 3) + 8 * (j >> 2);
+            if (key > myq) a[s4][j] = 0;
+          }
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const bf16x8 av = __builtin_bit_cast(bf16x8, a[s4]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) dq[d] = mfma(av, lds_tr(kl, 16 * s4, 32 * d, lane), dq[d]);
+      }
+      if (it + 1 < nmine) {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) a[s4] = an[s4];
+      }
+    }
+    wait_dma_and_barrier();
+  }
+  const float sm = scale_log2 * 0.6931471805599453f;
+  bf16_t* dqb = dqkv + ((long)b * S + qw0) * rs + hh * HD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qq = (r & 3) + 8 * (r >> 2) + 4 * hf;
+      dqb[(long)qq * rs + 32 * d + l32] = f2bf(dq[d][r] * sm);
+    }
+}
+
+// ================================================================================================
 // launchers
 // ================================================================================================
 static inline bool fa_shape_ok(int S, int H, int KVH, int D) {
@@ -993,9 +1085,24 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
   return hipGetLastError();
 }
 
-// workspace: delta (B*H*S fp32) + dkp + dvp (2 * B*S*H*128 fp32)
+// dS spill for the recompute-free dQ pass (DSTACK_AMD_FA_DQ=ds|recompute): B*H*S*S bf16 of
+// workspace, used while it stays under DSTACK_AMD_FA_DS_MAX_GB (default 16)
+static bool fa_ds_spill(int B, int S, int H) {
+  static const int mode = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DQ");
+    return (v && std::string(v) == "ds") ? 1 : 0;
+  }();
+  static const double max_gb = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DS_MAX_GB");
+    return v ? atof(v) : 16.0;
+  }();
+  return mode == 1 && (double)B * H * S * S * 2 <= max_gb * 1e9;
+}
+
+// workspace: delta (B*H*S fp32) + dkp + dvp (2 * B*S*H*128 fp32) [+ dS spill (B*H*S*S bf16)]
 extern "C" size_t dsa_fa_bwd_workspace(int B, int S, int H) {
-  return (size_t)B * H * S * 4 + 2 * (size_t)B * S * H * HD * 4;
+  return (size_t)B * H * S * 4 + 2 * (size_t)B * S * H * HD * 4 +
+         (fa_ds_spill(B, S, H) ? (size_t)B * H * S * S * 2 : 0);
 }
 
 extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
@@ -1060,18 +1167,44 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
                                                B, S, H, KVH, sl2);                                     \
     } else if (dkdv_kind == 9) {                                                                      \
       fa_bwd_dkdv8_kernel<C, true><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(     \
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr);  \
     } else if ((dkdv8 || dkdv_kind >= 64) && half_prio) {                                              \
       fa_bwd_dkdv8_kernel<C, false, true><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>( \
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr);  \
     } else if (dkdv8 || dkdv_kind >= 64) {                                                             \
       fa_bwd_dkdv8_kernel<C><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(          \
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);           \
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr);  \
     } else                                                                                             \
       fa_bwd_dkdv_kernel<C, N><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, \
                                                           delta, dkp, dvp, B, S, H, KVH, sl2);         \
   } while (0)
-  if (causal) {
+  if (fa_ds_spill(B, S, H)) {  // dK/dV pass writes dS; dQ is one GEMM over the spilled dS
+    bf16_t* dsg = (bf16_t*)(dvp + (size_t)B * S * H * HD);
+    const size_t lds8 = 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512);
+    if (causal)
+      fa_bwd_dkdv8_kernel<true, false, false, true><<<grid, 512, lds8, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, dsg);
+    else
+      fa_bwd_dkdv8_kernel<false, false, false, true><<<grid, 512, lds8, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, dsg);
+    DSA_CHECK(hipGetLastError());
+    const size_t lds_ds = 2 * TILE_BYTES;
+    if (S % 256 == 0) {
+      if (causal)
+        fa_bwd_dq_ds_kernel<true, 8><<<B * H * (S / 256), 512, lds_ds, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv,
+                                                                             B, S, H, KVH, sl2);
+      else
+        fa_bwd_dq_ds_kernel<false, 8><<<B * H * (S / 256), 512, lds_ds, st>>>((const bf16_t*)qkv, dsg,
+                                                                              (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    } else {
+      if (causal)
+        fa_bwd_dq_ds_kernel<true, 4><<<grid, 256, lds_ds, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv, B, S, H,
+                                                                KVH, sl2);
+      else
+        fa_bwd_dq_ds_kernel<false, 4><<<grid, 256, lds_ds, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv, B, S, H,
+                                                                 KVH, sl2);
+    }
+  } else if (causal) {
     if (dkdv_qt == 128) DSA_DKDV(true, 4); else DSA_DKDV(true, 2);
     DSA_CHECK(hipGetLastError());
     if (dq_waves == 8 && half_prio)
