@@ -20,6 +20,7 @@
 //    forward orientation and feeds dS^T as the A operand of dQ = dS·K.  dQ is computed by its own
 //    q-major pass instead of cross-workgroup atomics (deterministic, no atomic-rate floor).
 #include "mfma_tiles.h"
+typedef unsigned short us4 __attribute__((ext_vector_type(4)));
 
 #include <cstdlib>
 #include <string>
@@ -459,9 +460,10 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 // which brings a wave under 256 registers: 2 waves per SIMD hide each other's LDS/exp latency.
 // LDS: K|V (64 KiB) + 2-stage Q/dO/lse/delta ring (65 KiB) = 129 KiB -> one workgroup per CU.
 // ================================================================================================
-// SPILL: also write dS (bf16, the same values that feed dK) to dsg = [B*H][S queries][S keys] for
-// the recompute-free dQ pass below; keys are stored in the MFMA A-operand order of a 16-key chunk
-// ({0-3, 8-11 | 4-7, 12-15}) so a dQ lane loads its 8 keys as one 16-byte vector.
+// SPILL: also write dS^T (bf16, the same values that feed dK) to dsg = [B*H][S keys][S queries]
+// for the recompute-free dQ pass below: a lane owns one key and 4 consecutive queries per register
+// group, so it stores 8 bytes at a time (the [q][key] forms measured 1.40-1.53 ms for this pass
+// with 2-byte stores), and the dQ pass DMAs row-major 64-key tiles and reads them transposed.
 template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false>
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
@@ -577,14 +579,12 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
         pb[k2] = to_bf16x8(sc, 8 * k2);
         dsb[k2] = to_bf16x8(dpv, 8 * k2);
       }
-      if constexpr (SPILL) {  // lane = key mykey, register 4*rr+i = query qlo + 8*rr + 4*hf + i
-        const int o = mykey & 15;
-        const int pk = (mykey & ~15) | (((o >> 2) & 1) << 3) | (((o >> 3) & 1) << 2) | (o & 3);
-        bf16_t* drow = dsg + ((long)bh * S + qlo + 4 * hf) * S + pk;
+      if constexpr (SPILL) {  // lane = key mykey, registers 4*rr+i = queries qlo + 8*rr + 4*hf + i
+        bf16_t* dt = dsg + ((long)bh * S + mykey) * S + qlo + 4 * hf;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) drow[(long)(8 * rr + i) * S] = f2bf(dpv[4 * rr + i]);
+          *reinterpret_cast<us4*>(dt + 8 * rr) =
+              us4{f2bf(dpv[4 * rr]), f2bf(dpv[4 * rr + 1]), f2bf(dpv[4 * rr + 2]), f2bf(dpv[4 * rr + 3])};
       }
 #pragma unroll
       for (int d = 0; d < 4; ++d)
@@ -936,11 +936,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(con
 }
 
 // ================================================================================================
-// Backward dQ pass without recompute: dQ = dS . K with dS read back from the dK/dV pass's spill
+// Backward dQ pass without recompute: dQ = dS . K over the dS^T spilled by the dK/dV pass
 // (fa_bwd_dkdv8_kernel<..., SPILL>): one GEMM per tile instead of three (S, dP, dQ), no Q/dO/lse/
-// delta.  The dS tile is loaded straight into A-operand registers one tile ahead; K tiles go
-// through the same double-buffered LDS ring as fa_bwd_dq_kernel.  Causal: keys > query are zeroed
-// on load (the dK/dV pass never writes fully masked 32x32 sub-tiles).
+// delta.  Per 64-key step a stage holds the K tile and the dS^T tiles (64 keys x 128 queries) of
+// the workgroup's queries, all DMA'd row-major into the swizzled LDS image; the A operand is the
+// transposed read of dS^T, the B operand the transposed read of K.  Causal: keys > query are
+// zeroed after the read (the dK/dV pass never writes fully masked 32x32 sub-tiles).
 // ================================================================================================
 template <bool CAUSAL, int NW>
 __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ qkv,
@@ -951,7 +952,7 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_ds_kernel(const bf16_t* __r
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
   const int NH = H + 2 * KVH;
   const long rs = (long)NH * HD;
-  constexpr int QB = 32 * NW;
+  constexpr int QB = 32 * NW, NT = NW / 4, STG = (1 + NT) * TILE_BYTES;
   const int nqb = S / QB;
   const int bid = blockIdx.x;
   const int qb = CAUSAL ? nqb - 1 - bid / (B * H) : bid / (B * H);
@@ -959,7 +960,7 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_ds_kernel(const bf16_t* __r
   const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
   const bf16_t* kp = qkv + (long)b * S * rs + (H + kvh) * HD;
   const int q0 = qb * QB, qw0 = q0 + 32 * w, myq = qw0 + l32;
-  const bf16_t* dsr = dsg + ((long)bh * S + myq) * S + 8 * hf;
+  const bf16_t* dst = dsg + (long)bh * S * S + q0;  // dS^T rows (keys) of this workgroup's queries
   f32x16 dq[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d)
@@ -967,39 +968,34 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_ds_kernel(const bf16_t* __r
     for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
   const int nkv = CAUSAL ? (q0 + QB) / 64 : S / 64;
   const int nmine = CAUSAL ? (qw0 + 31) / 64 + 1 : nkv;  // tiles with kv0 <= qw0 + 31
-  us8 a[4];
+  auto issue = [&](int it, char* st) {
+    dma_tile64_n<NW>(kp + (long)it * 64 * rs, rs, st, w, lane);
 #pragma unroll
-  for (int s4 = 0; s4 < 4; ++s4) a[s4] = *reinterpret_cast<const us8*>(dsr + 16 * s4);
-  dma_tile64_n<NW>(kp, rs, smem, w, lane);
+    for (int t = 0; t < NT; ++t)
+      dma_tile64_n<NW>(dst + (long)it * 64 * S + 128 * t, S, st + (1 + t) * TILE_BYTES, w, lane);
+  };
+  issue(0, smem);
   wait_dma_and_barrier();
   for (int it = 0; it < nkv; ++it) {
-    const char* kl = smem + (it & 1) * TILE_BYTES;
-    if (it + 1 < nkv) dma_tile64_n<NW>(kp + (long)(it + 1) * 64 * rs, rs, smem + ((it + 1) & 1) * TILE_BYTES, w, lane);
+    const char* kl = smem + (it & 1) * STG;
+    if (it + 1 < nkv) issue(it + 1, smem + ((it + 1) & 1) * STG);
     const int kv0 = it * 64;
     if (it < nmine) {
-      us8 an[4];
-      if (it + 1 < nmine) {
+      const char* dl = kl + (1 + (w >> 2)) * TILE_BYTES;
+      const bool diag = CAUSAL && kv0 + 63 > qw0;
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) an[s4] = *reinterpret_cast<const us8*>(dsr + kv0 + 64 + 16 * s4);
-      }
-      if (CAUSAL && kv0 + 63 > qw0) {
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
+      for (int s4 = 0; s4 < 4; ++s4) {
+        us8 a = __builtin_bit_cast(us8, lds_tr(dl, 16 * s4, 32 * (w & 3), lane));
+        if (diag) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const int key = kv0 + 16 * s4 + 4 * hf + (j & 3) + 8 * (j >> 2);
-            if (key > myq) a[s4][j] = 0;
+            if (key > myq) a[j] = 0;
           }
-      }
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const bf16x8 av = __builtin_bit_cast(bf16x8, a[s4]);
+        }
+        const bf16x8 av = __builtin_bit_cast(bf16x8, a);
 #pragma unroll
         for (int d = 0; d < 4; ++d) dq[d] = mfma(av, lds_tr(kl, 16 * s4, 32 * d, lane), dq[d]);
-      }
-      if (it + 1 < nmine) {
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) a[s4] = an[s4];
       }
     }
     wait_dma_and_barrier();
@@ -1188,20 +1184,20 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
       fa_bwd_dkdv8_kernel<false, false, false, true><<<grid, 512, lds8, st>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, dsg);
     DSA_CHECK(hipGetLastError());
-    const size_t lds_ds = 2 * TILE_BYTES;
+    const size_t lds_ds8 = 2 * 3 * TILE_BYTES, lds_ds4 = 2 * 2 * TILE_BYTES;
     if (S % 256 == 0) {
       if (causal)
-        fa_bwd_dq_ds_kernel<true, 8><<<B * H * (S / 256), 512, lds_ds, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv,
+        fa_bwd_dq_ds_kernel<true, 8><<<B * H * (S / 256), 512, lds_ds8, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv,
                                                                              B, S, H, KVH, sl2);
       else
-        fa_bwd_dq_ds_kernel<false, 8><<<B * H * (S / 256), 512, lds_ds, st>>>((const bf16_t*)qkv, dsg,
+        fa_bwd_dq_ds_kernel<false, 8><<<B * H * (S / 256), 512, lds_ds8, st>>>((const bf16_t*)qkv, dsg,
                                                                               (bf16_t*)dqkv, B, S, H, KVH, sl2);
     } else {
       if (causal)
-        fa_bwd_dq_ds_kernel<true, 4><<<grid, 256, lds_ds, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv, B, S, H,
+        fa_bwd_dq_ds_kernel<true, 4><<<grid, 256, lds_ds4, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv, B, S, H,
                                                                 KVH, sl2);
       else
-        fa_bwd_dq_ds_kernel<false, 4><<<grid, 256, lds_ds, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv, B, S, H,
+        fa_bwd_dq_ds_kernel<false, 4><<<grid, 256, lds_ds4, st>>>((const bf16_t*)qkv, dsg, (bf16_t*)dqkv, B, S, H,
                                                                  KVH, sl2);
     }
   } else if (causal) {
