@@ -120,6 +120,13 @@ class LocalCompute(Compute):
     def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
         shim = LocalShim.get()
         res = host_resources(shim.host_info)
+        g = requirements.resources.gpu if requirements is not None else None
+        if g is not None and res.gpus and not g.count.contains(len(res.gpus)):
+            # the host's shim grants GPU subsets (xGMI-aware lock), so offer as many as the run
+            # allows: `gpu: MI355X:1` or two 2-GPU nodes of a multi-node task fit an 8-GPU host
+            hi = len(res.gpus) if g.count.max is None else min(len(res.gpus), g.count.max)
+            if hi >= max(1, g.count.min or 0):
+                res = res.model_copy(update={"gpus": res.gpus[:hi]})
         offer = InstanceOfferWithAvailability(
             backend=BackendType.LOCAL, instance=InstanceType(name="local", resources=res), region="local",
             price=0.0, availability=InstanceAvailability.AVAILABLE,

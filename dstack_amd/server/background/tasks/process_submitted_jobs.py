@@ -194,7 +194,7 @@ def _assign_pool_instance(s: Session, run: RunModel, job: JobModel, spec, profil
             n_gpus = _gpu_request(spec, shared)
             topo = pools_services.instance_topology(inst)
             gpu_indices = None
-            if n_gpus and topo is not None and topo.gpus:
+            if n_gpus and topo is not None and topo.gpus and inst.backend != BackendType.LOCAL.value:
                 busy = busy_set(inst.busy_gpus)
                 free = [g.index for g in topo.gpus if g.index not in busy]
                 gpu_indices = pick_gpus(topo, free, n_gpus)
@@ -251,7 +251,9 @@ def _create_instance_for_job(s: Session, run: RunModel, job: JobModel, spec, off
     gpu_indices = None
     n_gpus = _gpu_request(spec, offer)
     topo = pools_services.instance_topology(inst)
-    if n_gpus and topo is not None and topo.gpus:
+    # local backend: every local instance is the same host behind ONE shim, whose xGMI-aware lock
+    # arbitrates between them; pinning indices per instance row would hand two jobs the same GPUs
+    if n_gpus and topo is not None and topo.gpus and jpd.backend != BackendType.LOCAL:
         gpu_indices = pick_gpus(topo, [g.index for g in topo.gpus], n_gpus)
         inst.busy_gpus = ",".join(str(x) for x in (gpu_indices or []))
     job.instance_id = inst.id

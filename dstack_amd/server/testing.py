@@ -91,3 +91,44 @@ class ServerProcess:
 
     def __exit__(self, *a):
         self.stop()
+
+
+def fake_amd_sysfs(root, n_gpus: int = 8, product: str = "AMD Instinct MI355X", vram_gib: int = 288,
+                   xgmi: bool = True) -> str:
+    """Build a fake ``/sys`` + ``/dev/dri`` tree of ``n_gpus`` AMD GPUs under ``root`` for the native
+    agents' sysfs discovery (``DSTACK_SYSFS_ROOT``, ``native/common/amdgpu.cpp``): render nodes with
+    vendor/product/VRAM, one PCI device per GPU, and a KFD topology whose io_links (type 11 = xGMI)
+    fully connect the GPUs, as on an 8xMI355X OAM board.  Returns ``root`` as a string."""
+    root = Path(root)
+    nodes = root / "sys" / "class" / "kfd" / "kfd" / "topology" / "nodes"
+    cpu = nodes / "0"
+    cpu.mkdir(parents=True, exist_ok=True)
+    (cpu / "gpu_id").write_text("0\n")
+    (cpu / "properties").write_text("cpu_cores_count 8\nsimd_count 0\n")
+    (root / "dev" / "dri").mkdir(parents=True, exist_ok=True)
+    for i in range(n_gpus):
+        bus = 0x05 + 0x10 * i
+        bdf = f"0000:{bus:02x}:00.0"
+        render = 128 + i
+        dev = root / "sys" / "devices" / "pci0000:00" / bdf
+        dev.mkdir(parents=True, exist_ok=True)
+        (dev / "vendor").write_text("0x1002\n")
+        (dev / "product_name").write_text(product + "\n")
+        (dev / "mem_info_vram_total").write_text(str(vram_gib << 30) + "\n")
+        (dev / "numa_node").write_text(f"{0 if i < n_gpus // 2 or n_gpus == 1 else 1}\n")
+        drm = root / "sys" / "class" / "drm" / f"renderD{render}"
+        drm.mkdir(parents=True, exist_ok=True)
+        if not (drm / "device").exists():
+            os.symlink(dev, drm / "device")
+        (root / "dev" / "dri" / f"renderD{render}").write_text("")
+        node = nodes / str(i + 1)
+        (node / "io_links").mkdir(parents=True, exist_ok=True)
+        (node / "gpu_id").write_text(f"{1000 + i}\n")
+        (node / "properties").write_text(f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+        links = [0] + ([j + 1 for j in range(n_gpus) if j != i] if xgmi else [])
+        for k, to in enumerate(links):
+            ld = node / "io_links" / str(k)
+            ld.mkdir(exist_ok=True)
+            kind = 2 if to == 0 else 11  # PCIe to the CPU node, xGMI to every peer
+            (ld / "properties").write_text(f"type {kind}\nnode_from {i + 1}\nnode_to {to}\nweight 15\n")
+    return str(root)

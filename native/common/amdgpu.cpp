@@ -12,6 +12,7 @@
 #include <cctype>
 #include <cstring>
 #include <limits>
+#include <map>
 #include <regex>
 
 #include "net.h"
@@ -344,7 +345,73 @@ std::vector<AmdGpu> discover_amd_gpus_sysfs() {
   return out;
 }
 
+// KFD topology: /sys/class/kfd/kfd/topology/nodes/<n>/{gpu_id, properties, io_links/<k>/properties}.
+// A GPU node's properties carry "domain" and "location_id" (bus << 8 | device << 3 | function);
+// an io_link of "type 11" (CRAT XGMI) with "node_to" m joins node n to node m directly.
+std::vector<std::vector<int>> xgmi_matrix_sysfs(const std::vector<AmdGpu>& gpus) {
+  const char* root_env = getenv("DSTACK_SYSFS_ROOT");
+  const std::string root = root_env ? root_env : "";
+  const std::string nodes_dir = root + "/sys/class/kfd/kfd/topology/nodes";
+  std::vector<std::vector<int>> m(gpus.size(), std::vector<int>(gpus.size(), 0));
+  auto props = [](const std::string& path) {
+    std::map<std::string, long long> p;
+    std::string s;
+    if (!read_file(path, s)) return p;
+    for (auto& line : split(s, '\n')) {
+      auto sp = line.find(' ');
+      if (sp == std::string::npos) continue;
+      p[line.substr(0, sp)] = atoll(line.c_str() + sp + 1);
+    }
+    return p;
+  };
+  std::map<long long, int> node_to_gpu;  // KFD node id -> index in `gpus`
+  std::vector<long long> gpu_nodes;
+  DIR* d = opendir(nodes_dir.c_str());
+  if (!d) return m;
+  while (auto* e = readdir(d))
+    if (e->d_name[0] >= '0' && e->d_name[0] <= '9') gpu_nodes.push_back(atoll(e->d_name));
+  closedir(d);
+  for (long long n : gpu_nodes) {
+    std::string base = nodes_dir + "/" + std::to_string(n);
+    std::string gid;
+    if (!read_file(base + "/gpu_id", gid) || atoll(gid.c_str()) == 0) continue;  // CPU node
+    auto p = props(base + "/properties");
+    long long loc = p.count("location_id") ? p["location_id"] : -1, dom = p.count("domain") ? p["domain"] : 0;
+    if (loc < 0) continue;
+    char bdf[32];
+    snprintf(bdf, sizeof bdf, "%04llx:%02llx:%02llx.%llx", dom, (loc >> 8) & 0xff, (loc >> 3) & 0x1f, loc & 7);
+    for (size_t i = 0; i < gpus.size(); ++i)
+      if (gpus[i].bdf == bdf) node_to_gpu[n] = (int)i;
+  }
+  for (auto& kv : node_to_gpu) {
+    std::string links = nodes_dir + "/" + std::to_string(kv.first) + "/io_links";
+    DIR* ld = opendir(links.c_str());
+    if (!ld) continue;
+    while (auto* e = readdir(ld)) {
+      if (e->d_name[0] == '.') continue;
+      auto p = props(links + "/" + e->d_name + "/properties");
+      if (!p.count("type") || p["type"] != 11 || !p.count("node_to")) continue;
+      auto it = node_to_gpu.find(p["node_to"]);
+      if (it != node_to_gpu.end() && it->second != kv.second) m[kv.second][it->second] = 1;
+    }
+    closedir(ld);
+  }
+  return m;
+}
+
+static bool sysfs_override() {
+  const char* r = getenv("DSTACK_SYSFS_ROOT");
+  return r && *r;
+}
+
+std::vector<std::vector<int>> xgmi_matrix(const std::vector<AmdGpu>& gpus) {
+  auto& smi = AmdSmi::instance();
+  if (!sysfs_override() && smi.available() && smi.count() == gpus.size()) return smi.xgmi_matrix();
+  return xgmi_matrix_sysfs(gpus);
+}
+
 std::vector<AmdGpu> discover_amd_gpus() {
+  if (sysfs_override()) return discover_amd_gpus_sysfs();  // a fake /sys tree wins over the real devices
   auto& smi = AmdSmi::instance();
   if (smi.available()) {
     auto g = smi.discover();

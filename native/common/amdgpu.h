@@ -51,6 +51,7 @@ class AmdSmi {
  public:
   static AmdSmi& instance();
   bool available() const { return ok_; }
+  size_t count() const { return handles_.size(); }
   std::vector<AmdGpu> discover();
   // xgmi[i][j] = 1 if a direct xGMI link joins GPU i and j (hops == 1), 0 otherwise
   std::vector<std::vector<int>> xgmi_matrix();
@@ -68,8 +69,12 @@ class AmdSmi {
 std::string amd_catalog_name(const std::string& market_name);
 // sysfs-only discovery (no amdsmi): render nodes with vendor 0x1002
 std::vector<AmdGpu> discover_amd_gpus_sysfs();
-// all AMD GPUs on this host (amdsmi, else sysfs)
+// all AMD GPUs on this host (amdsmi, else sysfs; DSTACK_SYSFS_ROOT forces the sysfs path)
 std::vector<AmdGpu> discover_amd_gpus();
+// direct-xGMI adjacency of `gpus` (their order) from the KFD topology's io_links (type 11)
+std::vector<std::vector<int>> xgmi_matrix_sysfs(const std::vector<AmdGpu>& gpus);
+// amdsmi's matrix when it enumerates the same GPUs, else the KFD-topology one
+std::vector<std::vector<int>> xgmi_matrix(const std::vector<AmdGpu>& gpus);
 
 Json gpu_to_json(const AmdGpu& g);
 // one GPU's sample in the runner's metrics wire format (gpu_* keys, optional "xgmi" object)

@@ -56,9 +56,8 @@ Json collect_host_info(const std::string& disk_path) {
   Json topo = Json::object();
   topo.set("gpus", gj);
   Json xg = Json::array();
-  auto& smi = AmdSmi::instance();
-  if (smi.available()) {
-    for (auto& row : smi.xgmi_matrix()) {
+  if (!gpus.empty()) {
+    for (auto& row : xgmi_matrix(gpus)) {
       Json r = Json::array();
       for (int v : row) r.push_back(v);
       xg.push_back(r);

@@ -35,9 +35,8 @@ Shim::Shim(ShimOptions o, std::unique_ptr<TaskDriver> driver) : opts_(std::move(
     numa.push_back(g.numa_node);
     inventory_render_.push_back(g.render_node);
   }
-  auto& smi = AmdSmi::instance();
-  auto xgmi = smi.available() ? smi.xgmi_matrix() : std::vector<std::vector<int>>{};
-  if (xgmi.size() != gpus.size()) xgmi.clear();  // sysfs fallback: no topology, never a mismatched one
+  auto xgmi = xgmi_matrix(gpus);  // amdsmi, else the KFD topology's xGMI io_links
+  if (xgmi.size() != gpus.size()) xgmi.clear();  // never a mismatched topology
   gpus_.init((int)gpus.size(), xgmi, numa);
   LOGI("shim: driver=%s gpus=%zu", driver_->name(), gpus.size());
 }

@@ -23,8 +23,9 @@ def main():
     launch = "python"
     if os.environ.get("E2E_TORCHRUN") == "1":
         # the examples/llama3-8b-train command: torchrun over the rendezvous env the runner exports
-        launch = ("torchrun --nproc-per-node=$DSTACK_GPUS_PER_NODE --master-addr=$DSTACK_MASTER_NODE_IP "
-                  "--master-port=29511")
+        launch = ("torchrun --nnodes=$DSTACK_NODES_NUM --node-rank=$DSTACK_NODE_RANK "
+                  "--nproc-per-node=$DSTACK_GPUS_PER_NODE --master-addr=$DSTACK_MASTER_NODE_IP "
+                  "--master-port=$MASTER_PORT")
     cmd = (f"echo HIP_VISIBLE_DEVICES=$HIP_VISIBLE_DEVICES DSTACK_GPUS_NUM=$DSTACK_GPUS_NUM "
            f"MASTER_ADDR=$DSTACK_MASTER_NODE_IP && cd {ROOT} && "
            f"{launch} bench.py --gpus $DSTACK_GPUS_NUM --steps {steps} --warmup 2 --no-coldstart")
