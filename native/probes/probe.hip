@@ -19,6 +19,8 @@
 #include <string>
 #include <vector>
 
+#include "ranks.h"
+
 #define CK(x)                                                                                    \
   do {                                                                                           \
     hipError_t e_ = (x);                                                                         \
@@ -202,8 +204,9 @@ static std::vector<std::vector<double>> xgmi_probe(int ndev, bool quick) {
 }
 
 // rccl_probe.cpp
-std::string rccl_allreduce_probe_mp(int nodes, int node_rank, const std::string& master, int port, bool quick,
-                                    double* best_busbw, std::string* err);
+std::string rccl_allreduce_probe_mp(int gpus_per_node, int nodes, int node_rank, const std::string& master, int port,
+                                    bool quick, double* best_busbw, int* world_out, std::string* err);
+
 
 // Per-SKU baselines: what THIS probe measures on a healthy part (not the datasheet peaks), so a
 // threshold of min_fraction x baseline flags a GPU running well below its siblings (throttling,
@@ -228,7 +231,7 @@ int main(int argc, char** argv) {
   int only_dev = -1;
   double min_hbm = -1, min_mfma = -1;  // absolute overrides; default: min_fraction x per-SKU baseline
   double min_fraction = 0.8;
-  int rccl_nodes = 1, node_rank = 0, master_port = 29600;
+  int rccl_nodes = 1, node_rank = 0, master_port = 29600, gpus_per_node = 0;
   std::string master = "127.0.0.1";
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -246,15 +249,39 @@ int main(int argc, char** argv) {
     else if (a == "--node-rank" && i + 1 < argc) node_rank = atoi(argv[++i]);
     else if (a == "--master" && i + 1 < argc) master = argv[++i];
     else if (a == "--master-port" && i + 1 < argc) master_port = atoi(argv[++i]);
+    else if (a == "--gpus-per-node" && i + 1 < argc) gpus_per_node = atoi(argv[++i]);
     else {
       fprintf(stderr,
               "usage: dstack-probe [--quick] [--json] [--hbm] [--mfma] [--xgmi] [--rccl] [--device N]\n"
               "                    [--min-fraction F | --min-hbm-tbs X --min-mfma-tflops Y]\n"
-              "                    [--rccl --nodes N --node-rank R --master HOST --master-port P]\n");
+              "                    [--rccl [--gpus-per-node G] --nodes N --node-rank R --master HOST --master-port P]\n");
       return 2;
     }
   }
   if (!want_hbm && !want_mfma && !want_xgmi && !want_rccl) want_hbm = want_mfma = want_xgmi = true;
+  // RCCL first: its one-process-per-GPU ranks are forked before THIS process makes any HIP call
+  std::string rccl_json, rccl_err;
+  if (want_rccl && only_dev < 0) {
+    const int g = gpus_per_node > 0 ? gpus_per_node : dsa::count_gpus_no_hip();
+    if (g <= 0) {
+      rccl_err = "no GPUs visible";
+    } else {
+      double best = 0;
+      int world = 0;
+      std::string sweep = rccl_allreduce_probe_mp(g, rccl_nodes, node_rank, master, master_port, quick, &best, &world,
+                                                  &rccl_err);
+      char b[256];
+      snprintf(b, sizeof b, "\"rccl_world\": %d, \"rccl_gpus_per_node\": %d, \"rccl\": ", world, g);
+      rccl_json = b + sweep + ", ";
+      if (world > 1) {
+        snprintf(b, sizeof b, "\"rccl_busbw_gb_s\": %.1f, ", best);
+        rccl_json += b;
+      } else {
+        rccl_json += "\"rccl_busbw_gb_s\": null, \"rccl_note\": \"world 1: no inter-GPU traffic; bootstrap and "
+                     "communicator check only, not a bandwidth measurement\", ";
+      }
+    }
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     printf("{\"healthy\": false, \"message\": \"no HIP devices\"}\n");
@@ -319,16 +346,12 @@ int main(int argc, char** argv) {
     out += "], ";
   }
   if (want_rccl && only_dev < 0) {
-    double best = 0;
-    std::string err;
-    std::string sweep = rccl_allreduce_probe_mp(rccl_nodes, node_rank, master, master_port, quick, &best, &err);
-    snprintf(buf, sizeof buf, "\"rccl_world\": %d, \"rccl\": ", rccl_nodes * ndev);
-    out += buf + sweep + ", ";
-    snprintf(buf, sizeof buf, "\"rccl_busbw_gb_s\": %.1f, ", best);
-    out += buf;
-    if (!err.empty()) {
+    out += rccl_json;
+    if (!rccl_err.empty()) {
       healthy = false;
-      failing += (failing.empty() ? "" : "; ") + ("RCCL bootstrap: " + err);
+      for (auto& ch : rccl_err)
+        if (ch == '"' || ch == '\\' || ch == '\n') ch = '\'';  // the message is a JSON string
+      failing += (failing.empty() ? "" : "; ") + ("RCCL: " + rccl_err);
     }
   }
   snprintf(buf, sizeof buf, "\"devices\": %d, \"healthy\": %s, ", (int)devs.size(), healthy ? "true" : "false");

@@ -1,15 +1,19 @@
 // RCCL all-reduce probe, bf16 sum, message sizes 1 MiB .. 1 GiB (256 MiB with --quick): algbw and
-// busbw per size, across the GPUs of one node or, with a TCP-bootstrapped unique id, of all nodes.
+// busbw per size, one process per GPU across the GPUs of one node or, with a TCP-bootstrapped
+// unique id, of all nodes.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include <string>
 #include <thread>
 #include <vector>
 
-#include "bootstrap.h"
+#include "ranks.h"
 
 #define HCK(x)                                                                               \
   do {                                                                                       \
@@ -28,98 +32,125 @@
     }                                                                                           \
   } while (0)
 
-// One communicator over every GPU of every node: `nodes` processes (one per node, as the runner
-// starts them), each owning all its local GPUs as ranks node_rank*ndev + d, initialised with
-// ncclCommInitRank from an ncclUniqueId that node 0 creates and serves over TCP (bootstrap.h) --
-// the same unique-id rendezvous a torchrun/RCCL job performs, not ncclCommInitAll's in-process
-// shortcut.  nodes == 1 runs the same path with no network exchange.  busbw = algbw*2(W-1)/W
-// (ring-bound; compare with one xGMI link, ~153 GB/s, intra-node).
-std::string rccl_allreduce_probe_mp(int nodes, int node_rank, const std::string& master, int port, bool quick,
-                                    double* best_busbw, std::string* err) {
-  int ndev = 0;
-  HCK(hipGetDeviceCount(&ndev));
-  const int world = nodes * ndev;
+// One communicator over every GPU of every node, in the job's process layout: one process per GPU
+// (ranks.h forks them before this process touches HIP), global rank node_rank*G + local, every rank
+// calling ncclCommInitRank with the ncclUniqueId that global rank 0 creates and serves over TCP at
+// master:port (bootstrap.h) -- exactly what a `torchrun --nproc-per-node=G` job does through its
+// TCP store, not ncclCommInitAll's or a group-initialised single-process shortcut.
+//
+// Each rank first checks the sum of an fp32 all-reduce (every rank contributes rank+1), then times
+// an in-place bf16 sum sweep (1 MiB .. 1 GiB, 256 MiB with --quick) on its own stream.  The parent
+// takes, per size, the slowest local rank: algbw = bytes / time, busbw = algbw * 2(W-1)/W
+// (ring-bound; compare with one xGMI link, ~153 GB/s, intra-node).  At W == 1 RCCL moves no data
+// between GPUs, so the sweep is reported with busbw null: it proves the bootstrap and the
+// communicator, it is not a bandwidth measurement.
+static std::string rank_body(const dsa::RankCtx& c, const std::string& id_bytes, bool quick) {
   ncclUniqueId id;
-  std::thread server;
-  std::string serve_err;
-  if (node_rank == 0) {
-    NCK(ncclGetUniqueId(&id));
-    if (nodes > 1)
-      server = std::thread([&] { serve_err = dsa::bootstrap_serve(port, &id, sizeof id, nodes - 1, 300000); });
-  } else {
-    std::string e = dsa::bootstrap_fetch(master, port, node_rank, &id, sizeof id, 300000);
-    if (!e.empty()) {
-      if (err) *err = e;
-      return "null";
-    }
-  }
-  std::vector<ncclComm_t> comms((size_t)ndev);
-  NCK(ncclGroupStart());
-  for (int d = 0; d < ndev; ++d) {
-    HCK(hipSetDevice(d));
-    NCK(ncclCommInitRank(&comms[(size_t)d], world, id, node_rank * ndev + d));
-  }
-  NCK(ncclGroupEnd());
-  if (server.joinable()) server.join();
-  if (!serve_err.empty() && err) *err = serve_err;
+  memcpy(&id, id_bytes.data(), sizeof id);
+  HCK(hipSetDevice(c.local));
+  ncclComm_t comm;
+  NCK(ncclCommInitRank(&comm, c.world, id, c.rank));
+  hipStream_t st;
+  HCK(hipStreamCreate(&st));
+  // correctness: sum of (rank + 1) over all ranks, exact in fp32
+  const int nchk = 1024;
+  std::vector<float> h((size_t)nchk, (float)(c.rank + 1));
+  float* dchk = nullptr;
+  HCK(hipMalloc(&dchk, nchk * sizeof(float)));
+  HCK(hipMemcpy(dchk, h.data(), nchk * sizeof(float), hipMemcpyHostToDevice));
+  NCK(ncclAllReduce(dchk, dchk, nchk, ncclFloat32, ncclSum, comm, st));
+  HCK(hipStreamSynchronize(st));
+  HCK(hipMemcpy(h.data(), dchk, nchk * sizeof(float), hipMemcpyDeviceToHost));
+  const float want = (float)c.world * (c.world + 1) / 2.0f;
+  bool ok = true;
+  for (float v : h) ok = ok && v == want;
+  HCK(hipFree(dchk));
   size_t max_bytes = (quick ? 256ull : 1024ull) << 20;
-  std::vector<void*> buf((size_t)ndev);
-  std::vector<hipStream_t> st((size_t)ndev);
-  for (int d = 0; d < ndev; ++d) {
-    HCK(hipSetDevice(d));
-    HCK(hipMalloc(&buf[(size_t)d], max_bytes));
-    HCK(hipMemset(buf[(size_t)d], 0, max_bytes));
-    HCK(hipStreamCreate(&st[(size_t)d]));
-  }
-  std::string out = "[";
-  *best_busbw = 0;
-  bool first = true;
+  void* buf = nullptr;
+  HCK(hipMalloc(&buf, max_bytes));
+  HCK(hipMemset(buf, 0, max_bytes));
+  std::string times = "[";
   for (size_t bytes = 1 << 20; bytes <= max_bytes; bytes *= 4) {
-    size_t count = bytes / 2;  // bf16
-    auto run = [&](int reps) {
-      for (int r = 0; r < reps; ++r) {
-        NCK(ncclGroupStart());
-        for (int d = 0; d < ndev; ++d)
-          NCK(ncclAllReduce(buf[(size_t)d], buf[(size_t)d], count, ncclBfloat16, ncclSum, comms[(size_t)d],
-                            st[(size_t)d]));
-        NCK(ncclGroupEnd());
-      }
-      for (int d = 0; d < ndev; ++d) {
-        HCK(hipSetDevice(d));
-        HCK(hipStreamSynchronize(st[(size_t)d]));
-      }
-    };
-    run(2);
+    const size_t count = bytes / 2;  // bf16
+    for (int r = 0; r < 2; ++r) NCK(ncclAllReduce(buf, buf, count, ncclBfloat16, ncclSum, comm, st));
     const int reps = quick ? 5 : 20;
     hipEvent_t e0, e1;
-    HCK(hipSetDevice(0));
     HCK(hipEventCreate(&e0));
     HCK(hipEventCreate(&e1));
-    HCK(hipEventRecord(e0, st[0]));
-    run(reps);
-    HCK(hipSetDevice(0));
-    HCK(hipEventRecord(e1, st[0]));
+    HCK(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; ++r) NCK(ncclAllReduce(buf, buf, count, ncclBfloat16, ncclSum, comm, st));
+    HCK(hipEventRecord(e1, st));
     HCK(hipEventSynchronize(e1));
     float ms = 0;
     HCK(hipEventElapsedTime(&ms, e0, e1));
-    double sec = ms * 1e-3 / reps;
-    double algbw = bytes / sec / 1e9;
-    double busbw = world > 1 ? algbw * 2.0 * (world - 1) / world : 0.0;
-    if (busbw > *best_busbw) *best_busbw = busbw;
-    char b[200];
-    snprintf(b, sizeof b, "%s{\"bytes\": %zu, \"time_us\": %.1f, \"algbw_gb_s\": %.1f, \"busbw_gb_s\": %.1f}",
-             first ? "" : ", ", bytes, sec * 1e6, algbw, busbw);
-    out += b;
-    first = false;
+    char b[64];
+    snprintf(b, sizeof b, "%s%.2f", times.size() > 1 ? ", " : "", ms * 1e3 / reps);
+    times += b;
     HCK(hipEventDestroy(e0));
     HCK(hipEventDestroy(e1));
   }
-  out += "]";
-  for (int d = 0; d < ndev; ++d) {
-    HCK(hipSetDevice(d));
-    HCK(hipFree(buf[(size_t)d]));
-    HCK(hipStreamDestroy(st[(size_t)d]));
-    ncclCommDestroy(comms[(size_t)d]);
+  times += "]";
+  HCK(hipFree(buf));
+  HCK(hipStreamDestroy(st));
+  ncclCommDestroy(comm);
+  char head[96];
+  snprintf(head, sizeof head, "{\"rank\": %d, \"sum_ok\": %s, \"times_us\": ", c.rank, ok ? "true" : "false");
+  return head + times + "}";
+}
+
+// Numbers of a rank's result line ("times_us": [...]) -- the line is our own fixed format.
+static std::vector<double> parse_times(const std::string& line) {
+  std::vector<double> v;
+  size_t p = line.find("\"times_us\": [");
+  if (p == std::string::npos) return v;
+  p += 13;
+  while (p < line.size() && line[p] != ']') {
+    char* end = nullptr;
+    double x = strtod(line.c_str() + p, &end);
+    if (end == line.c_str() + p) break;
+    v.push_back(x);
+    p = (size_t)(end - line.c_str());
+    while (p < line.size() && (line[p] == ',' || line[p] == ' ')) ++p;
   }
-  return out;
+  return v;
+}
+
+std::string rccl_allreduce_probe_mp(int gpus_per_node, int nodes, int node_rank, const std::string& master, int port,
+                                    bool quick, double* best_busbw, int* world_out, std::string* err) {
+  const int world = nodes * gpus_per_node;
+  *world_out = world;
+  *best_busbw = 0;
+  std::string e;
+  auto results = dsa::run_ranks(
+      gpus_per_node, nodes, node_rank, master, port, sizeof(ncclUniqueId),
+      [](std::string& id) {
+        ncclUniqueId u;
+        if (ncclGetUniqueId(&u) != ncclSuccess) return std::string("ncclGetUniqueId failed");
+        memcpy(&id[0], &u, sizeof u);
+        return std::string();
+      },
+      [quick](const dsa::RankCtx& c, const std::string& id) { return rank_body(c, id, quick); }, 300000, &e);
+  std::vector<double> worst;  // per size: slowest local rank (us)
+  for (auto& r : results) {
+    if (r.line.find("\"sum_ok\": false") != std::string::npos && e.empty())
+      e = "rank " + std::to_string(node_rank * gpus_per_node + r.local) + ": all-reduce sum mismatch";
+    if (r.line.find("\"error\"") != std::string::npos && e.empty()) e = r.line;
+    auto t = parse_times(r.line);
+    if (t.size() > worst.size()) worst.resize(t.size(), 0.0);
+    for (size_t k = 0; k < t.size(); ++k) worst[k] = std::max(worst[k], t[k]);
+  }
+  if (!e.empty() && err) *err = e;
+  std::string out = "[";
+  size_t bytes = 1 << 20;
+  for (size_t k = 0; k < worst.size(); ++k, bytes *= 4) {
+    const double sec = worst[k] * 1e-6;
+    const double algbw = sec > 0 ? bytes / sec / 1e9 : 0.0;
+    const double busbw = world > 1 ? algbw * 2.0 * (world - 1) / world : 0.0;
+    if (busbw > *best_busbw) *best_busbw = busbw;
+    char b[200];
+    snprintf(b, sizeof b, "%s{\"bytes\": %zu, \"time_us\": %.1f, \"algbw_gb_s\": %.1f, \"busbw_gb_s\": %.1f}",
+             k ? ", " : "", bytes, worst[k], algbw, busbw);
+    out += b;
+  }
+  return out + "]";
 }

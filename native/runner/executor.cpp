@@ -505,9 +505,11 @@ bool Executor::run_probe() {
 
 // Opt-in RCCL pre-flight for distributed tasks (job env DSTACK_RCCL_PREFLIGHT=1, >1 GPU in the
 // job): every node runs the all-reduce probe with ONE communicator over all GPUs of all nodes,
-// bootstrapped like the job's own RCCL (unique id from the master node over TCP, port MASTER_PORT+1,
-// the job's HIP_VISIBLE_DEVICES / NCCL_SOCKET_IFNAME env), so a broken fabric or a bad GPU fails
-// the job in seconds with the probe's message instead of hanging inside torchrun.
+// in the job's own process layout -- one process per GPU (DSTACK_GPUS_PER_NODE ranks per node,
+// global rank node_rank*G + local, probes/ranks.h) bootstrapped like the job's RCCL (unique id from
+// global rank 0 over TCP at the master node, port MASTER_PORT+1, the job's HIP_VISIBLE_DEVICES /
+// NCCL_SOCKET_IFNAME env) -- so a broken fabric or a bad GPU fails the job in seconds with the
+// probe's message instead of hanging inside torchrun.
 bool Executor::wants_rccl_preflight() const {
   const Json& js = submit_body_["job_spec"];
   std::string v = js["env"]["DSTACK_RCCL_PREFLIGHT"].str("");
@@ -532,6 +534,7 @@ bool Executor::run_rccl_preflight(std::string& msg) {
   const int port = atoi(get("MASTER_PORT", "29500").c_str()) + 1;
   std::vector<std::string> argv = {"timeout", "-k", "10", get("DSTACK_RCCL_PREFLIGHT_TIMEOUT", "300"),
                                    opts_.probe_binary, "--rccl", "--quick", "--json",
+                                   "--gpus-per-node", get("DSTACK_GPUS_PER_NODE", "0"),
                                    "--nodes", get("DSTACK_NODES_NUM", "1"), "--node-rank", get("DSTACK_NODE_RANK", "0"),
                                    "--master", get("DSTACK_MASTER_NODE_IP", "127.0.0.1"),
                                    "--master-port", std::to_string(port)};
@@ -576,9 +579,16 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
       job_logs_.append("[dstack] DSTACK_ROCPROF_COUNTERS ignored: " + perr + "\n");
       counters.clear();
     }
-    std::vector<std::string> wrapped = rocprof_argv(rocprof_dir, counters);
-    wrapped.insert(wrapped.end(), argv.begin(), argv.end());
-    argv = wrapped;
+    // rocprofv3 goes directly in front of the GPU program (never in front of the job's shell or a
+    // launcher: its preloaded library initialises the GPU in the process it wraps)
+    std::vector<std::string> wrapped;
+    std::string werr;
+    if (rocprof_wrap(argv, rocprof_argv(rocprof_dir, counters), wrapped, werr)) {
+      argv = wrapped;
+    } else {
+      job_logs_.append("[dstack] DSTACK_ROCPROF ignored: " + werr + "; the job runs unprofiled\n");
+      rocprof_dir.clear();
+    }
   }
   std::string wd = opts_.working_dir;
   std::string jwd = js["working_dir"].str();
@@ -724,22 +734,21 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
   close(master);
   child_pgid_ = 0;
   int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
-  if (!rocprof_dir.empty()) {
-    // surface the kernel statistics (and counters) in the job log
+  if (!rocprof_dir.empty()) {  // one pair of CSVs per profiled process (torchrun: one per rank)
+    std::vector<std::string> stats, ctrs;
     DIR* d = opendir(rocprof_dir.c_str());
-    std::string stats_path, counters_path;
     if (d) {
       while (auto* e = readdir(d)) {
-        std::string n = e->d_name;
-        if (n.find("kernel_stats.csv") != std::string::npos) stats_path = rocprof_dir + "/" + n;
-        if (n.find("counter_collection.csv") != std::string::npos) counters_path = rocprof_dir + "/" + n;
+        std::string n = e->d_name, csv;
+        if (n.find("kernel_stats.csv") != std::string::npos && read_file(rocprof_dir + "/" + n, csv))
+          stats.push_back(csv);
+        if (n.find("counter_collection.csv") != std::string::npos && read_file(rocprof_dir + "/" + n, csv))
+          ctrs.push_back(csv);
       }
       closedir(d);
     }
-    std::string csv;
-    if (!stats_path.empty() && read_file(stats_path, csv)) job_logs_.append(summarize_kernel_stats(csv, 15));
-    if (!counters_path.empty() && read_file(counters_path, csv))
-      job_logs_.append(summarize_counters(csv, counters, 15));
+    if (!stats.empty()) job_logs_.append(summarize_kernel_stats(stats, 15));
+    if (!ctrs.empty()) job_logs_.append(summarize_counters(ctrs, counters, 15));
   }
   if (timed_out) {
     reason = "max_duration_exceeded";

@@ -17,16 +17,37 @@ std::vector<std::string> split_counters(const std::string& spec);
 // (their hardware cost is not known here).
 bool validate_pmc(const std::vector<std::string>& counters, std::string& err);
 
-// rocprofv3 argv prefix for the job ("rocprofv3 --kernel-trace --stats [--pmc ...] ... --")
+// rocprofv3 argv prefix for the job ("rocprofv3 --kernel-trace --stats [--pmc ...] ... --"); every
+// profiled process writes <out_dir>/job_<pid>_{kernel_stats,counter_collection}.csv
 std::vector<std::string> rocprof_argv(const std::string& out_dir, const std::vector<std::string>& counters);
+
+// Put rocprofv3 directly in front of the job's GPU program.  rocprofv3's preloaded library
+// initialises the GPU in the process it is given (with --pmc it always does), so whatever follows
+// "--" must be the GPU program itself: a shell, `env`, `timeout` or a launcher there would fork or
+// exec a GPU program from a process that has already touched the GPU.  `rp` is rocprof_argv()'s
+// prefix (ending in "--").
+//  * job = {shell, "-c", script} (how the server runs `commands`): the script's LAST simple command
+//    becomes `[VAR=x ...] exec rocprofv3 ... -- prog args`, so the shell (which never touches the GPU)
+//    execs rocprofv3, which execs the program;
+//  * that command is `torchrun ... script.py` / `python -m torch.distributed.run ...`: each rank
+//    is profiled instead -- `torchrun ... --no-python rocprofv3 ... -- python3 -u script.py`, the
+//    launcher itself stays outside the profiler;
+//  * job = {prog, args...} (an entrypoint without a shell): rocprofv3 ... -- prog args.
+// Anything else -- a last command that is a wrapper (bash, sh, env, timeout, numactl, mpirun, ...),
+// a pipeline, a background job, a compound command, one reached through `||` -- is refused with a
+// reason, and the caller runs the job unprofiled.
+bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::string>& rp,
+                  std::vector<std::string>& out, std::string& err);
 
 // one CSV record (quoted fields with commas / doubled quotes, as rocprofv3 writes kernel names)
 std::vector<std::string> parse_csv_record(const std::string& line);
 
-// job-log text: the top `top` rows of *_kernel_stats.csv
-std::string summarize_kernel_stats(const std::string& csv, int top);
-// job-log text: per kernel, each counter summed over its dispatches (*_counter_collection.csv),
-// kernels ordered by the first counter, top `top`
-std::string summarize_counters(const std::string& csv, const std::vector<std::string>& counters, int top);
+// job-log text: per kernel, calls and time summed over every *_kernel_stats.csv (one per profiled
+// process: torchrun ranks each write their own), top `top` by total time
+std::string summarize_kernel_stats(const std::vector<std::string>& csvs, int top);
+// job-log text: per kernel, each counter summed over its dispatches in every
+// *_counter_collection.csv, kernels ordered by the first counter, top `top`
+std::string summarize_counters(const std::vector<std::string>& csvs, const std::vector<std::string>& counters,
+                               int top);
 
 }  // namespace dsa

@@ -21,6 +21,7 @@
 #include <openssl/ssl.h>
 
 #include "../probes/bootstrap.h"
+#include "../probes/ranks.h"
 #include "../runner/executor.h"
 #include "../runner/rocprof.h"
 #include "../dataloader/tokloader.h"
@@ -136,11 +137,68 @@ int main() {
         "Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n"
         "1,\"a(int)\",SQ_WAVES,10\n2,\"a(int)\",SQ_WAVES,10\n1,\"a(int)\",TCC_HIT_sum,5\n"
         "3,\"b(int)\",SQ_WAVES,50\n";
-    std::string s = summarize_counters(csv, {"SQ_WAVES", "TCC_HIT_sum"}, 10);
+    std::string s = summarize_counters({csv}, {"SQ_WAVES", "TCC_HIT_sum"}, 10);
     CHECK(s.find("b | 1 | 50 | 0") != std::string::npos);
     CHECK(s.find("a | 2 | 20 | 5") != std::string::npos);
     CHECK(s.find("b | 1") < s.find("a | 2"));  // ordered by the first counter
-    CHECK(summarize_counters("x,y\n1,2\n", {}, 5).empty());
+    CHECK(summarize_counters({"x,y\n1,2\n"}, {}, 5).empty());
+    // two processes (torchrun ranks): dispatch ids restart per file, sums add up
+    s = summarize_counters({csv, csv}, {"SQ_WAVES"}, 10);
+    CHECK(s.find("a | 4 | 40") != std::string::npos && s.find("b | 2 | 100") != std::string::npos);
+    std::string ks = "\"Name\",\"Calls\",\"TotalDurationNs\",\"AverageNs\"\n\"gemm(int)\",10,5000,500\n\"norm(int)\",4,1000,250\n";
+    s = summarize_kernel_stats({ks, ks}, 10);
+    CHECK(s.find("2 processes") != std::string::npos);
+    CHECK(s.find("gemm(int) | 20 | 0.010 | 0.50 | 83.33") != std::string::npos);
+    CHECK(s.find("gemm(int)") < s.find("norm(int)"));
+  });
+
+  run("rocprof_wrap: rocprofv3 sits directly in front of the GPU program, never a shell or launcher", [] {
+    const std::vector<std::string> rp = {"rocprofv3", "--kernel-trace", "--", };
+    std::vector<std::string> out;
+    std::string err;
+    auto sh = [](const std::string& script) { return std::vector<std::string>{"/bin/bash", "-c", script}; };
+    // the server's form: commands joined by " && "; the last one is exec'd under the profiler
+    CHECK(rocprof_wrap(sh("pip install x && cd /w && python3 train.py --steps 5"), rp, out, err));
+    CHECK(out.size() == 3 && out[2] == "pip install x && cd /w && exec rocprofv3 --kernel-trace -- python3 train.py --steps 5");
+    // env assignments stay in front of exec (the shell exports them to the program)
+    CHECK(rocprof_wrap(sh("cd /w && FOO=1 BAR='a b' python bench.py"), rp, out, err));
+    CHECK(out[2] == "cd /w && FOO=1 BAR='a b' exec rocprofv3 --kernel-trace -- python bench.py");
+    // an explicit exec is reused; redirections and substitutions stay with the program's words
+    CHECK(rocprof_wrap(sh("exec ./app --n $(nproc) > log 2>&1"), rp, out, err));
+    CHECK(out[2] == "exec rocprofv3 --kernel-trace -- ./app --n $(nproc) > log 2>&1");
+    // torchrun: the launcher stays outside, every rank is profiled
+    CHECK(rocprof_wrap(sh("torchrun --nnodes=$N --nproc-per-node $G --master-addr=$M bench.py --gpus 8"), rp, out,
+                       err));
+    CHECK(out[2] == "exec torchrun --nnodes=$N --nproc-per-node $G --master-addr=$M --no-python rocprofv3 "
+                    "--kernel-trace -- python3 -u bench.py --gpus 8");
+    CHECK(rocprof_wrap(sh("python -m torch.distributed.run --standalone --nproc_per_node=2 t.py"), rp, out, err));
+    CHECK(out[2] == "exec python -m torch.distributed.run --standalone --nproc_per_node=2 --no-python rocprofv3 "
+                    "--kernel-trace -- python3 -u t.py");
+    CHECK(rocprof_wrap(sh("torchrun --no-python --nproc-per-node 2 ./app"), rp, out, err));
+    CHECK(out[2] == "exec torchrun --no-python --nproc-per-node 2 rocprofv3 --kernel-trace -- ./app");
+    // separators inside quotes, comments and a trailing ';' do not split the last command
+    CHECK(rocprof_wrap(sh("echo 'a && b'; python3 x.py \"--tag=c;d\" # run it\n"), rp, out, err));
+    CHECK(out[2].find("exec rocprofv3 --kernel-trace -- python3 x.py") != std::string::npos);
+    // an entrypoint argv without a shell
+    CHECK(rocprof_wrap({"python3", "serve.py"}, rp, out, err));
+    CHECK(out.size() == 5 && out[3] == "python3" && out[4] == "serve.py");
+    // refused: wrappers, shells, pipelines, background jobs, || branches, compound commands
+    for (auto bad : {"cd /w && bash run.sh", "timeout 60 python3 x.py", "env A=1 python3 x.py", "python3 x.py | tee l",
+                     "python3 x.py &", "false || python3 x.py", "for i in 1 2; do python3 x.py; done",
+                     "( python3 x.py )", "numactl -N0 python3 x.py", "mpirun -np 8 ./app", "echo 'unbalanced"}) {
+      err.clear();
+      CHECK(!rocprof_wrap(sh(bad), rp, out, err) && !err.empty());
+    }
+    CHECK(!rocprof_wrap({"/usr/bin/env", "python3", "x.py"}, rp, out, err));
+    CHECK(!rocprof_wrap({"/bin/sh", "run.sh"}, rp, out, err));
+    CHECK(!rocprof_wrap(sh("torchrun --nproc-per-node 2 -m pkg.train"), rp, out, err));
+    // whatever was accepted: the word after "--" is never a shell, env or launcher
+    for (auto ok : {"a && python3 t.py", "torchrun --nproc-per-node=8 t.py", "X=1 ./bin/app"}) {
+      CHECK(rocprof_wrap(sh(ok), rp, out, err));
+      size_t dd = out[2].find(" -- ");
+      std::string after = out[2].substr(dd + 4, out[2].find(' ', dd + 4) - dd - 4);
+      CHECK(after != "bash" && after != "sh" && after != "env" && after != "torchrun" && after != "timeout");
+    }
   });
 
   run("rdma devices with an active port -> NCCL_IB_HCA", [] {
@@ -592,6 +650,90 @@ int main() {
     // nobody serving: the fetch times out too
     std::string buf(128, '\0');
     CHECK(!bootstrap_fetch("127.0.0.1", port, 1, &buf[0], buf.size(), 300).empty());
+  });
+
+  run("rccl ranks: one process per GPU, global rank 0's id reaches every rank of 2 nodes x 3", [] {
+    // the probe's launcher with a stub 128-byte id and a stub rank body (no HIP, no RCCL): node 1
+    // runs in its own process, node 0 here; every rank must get rank 0's id, with the job's global
+    // rank numbering, in its own process.  Not under ThreadSanitizer: it does not support fork() in
+    // a process whose earlier threads it tracked (children report the reused stacks as races); the
+    // plain and ASan builds run it.
+#if defined(__SANITIZE_THREAD__)
+    if (true) return;
+#endif
+    auto free_port = [] {
+      int s = ::socket(AF_INET, SOCK_STREAM, 0);
+      struct sockaddr_in a{};
+      a.sin_family = AF_INET;
+      ::bind(s, (struct sockaddr*)&a, sizeof a);
+      socklen_t len = sizeof a;
+      getsockname(s, (struct sockaddr*)&a, &len);
+      ::close(s);
+      return (int)ntohs(a.sin_port);
+    };
+    const int port = free_port();
+    std::string pat(128, '\0');
+    for (size_t i = 0; i < pat.size(); ++i) pat[i] = (char)(i * 13 + 7);
+    auto make = [&](std::string& id) {
+      id = pat;
+      return std::string();
+    };
+    auto body = [](const RankCtx& c, const std::string& id) {
+      unsigned sum = 0;
+      for (unsigned char ch : id) sum = sum * 31 + ch;
+      return "rank=" + std::to_string(c.rank) + " world=" + std::to_string(c.world) + " local=" +
+             std::to_string(c.local) + " sum=" + std::to_string(sum) + " pid=" + std::to_string(getpid());
+    };
+    unsigned want = 0;
+    for (unsigned char ch : pat) want = want * 31 + ch;
+    const std::string sum_s = " sum=" + std::to_string(want) + " ";
+    pid_t node1 = fork();
+    if (node1 == 0) {
+      std::string e;
+      auto r = run_ranks(3, 2, 1, "127.0.0.1", port, 128, make, body, 10000, &e);
+      bool ok = e.empty() && r.size() == 3;
+      for (int l = 0; l < 3 && ok; ++l)
+        ok = r[(size_t)l].exit_status == 0 &&
+             r[(size_t)l].line.find("rank=" + std::to_string(3 + l) + " world=6 local=" + std::to_string(l)) == 0 &&
+             r[(size_t)l].line.find(sum_s) != std::string::npos;
+      _exit(ok ? 0 : 1);
+    }
+    std::string e;
+    auto r = run_ranks(3, 2, 0, "127.0.0.1", port, 128, make, body, 10000, &e);
+    int st = 0;
+    waitpid(node1, &st, 0);
+    CHECK(WIFEXITED(st) && WEXITSTATUS(st) == 0);
+    CHECK(e.empty() && r.size() == 3);
+    std::set<std::string> pids;
+    for (int l = 0; l < 3; ++l) {
+      CHECK(r[(size_t)l].exit_status == 0);
+      CHECK(r[(size_t)l].line.find("rank=" + std::to_string(l) + " world=6") == 0);
+      CHECK(r[(size_t)l].line.find(sum_s) != std::string::npos);
+      pids.insert(r[(size_t)l].line.substr(r[(size_t)l].line.find("pid=")));
+    }
+    CHECK(pids.size() == 3 && pids.count("pid=" + std::to_string(getpid())) == 0);
+    // world 1: no server, no network, the body still runs
+    auto one = run_ranks(1, 1, 0, "127.0.0.1", free_port(), 128, make, body, 2000, &e);
+    CHECK(one.size() == 1 && one[0].line.find("rank=0 world=1") == 0 && one[0].line.find(sum_s) != std::string::npos);
+    // the second node never arrives: every rank reports a bootstrap error, nothing hangs
+    std::string e2;
+    auto lost = run_ranks(2, 2, 0, "127.0.0.1", free_port(), 128, make, body, 400, &e2);
+    CHECK(!e2.empty() && lost.size() == 2 && lost[0].line.find("bootstrap") != std::string::npos);
+    // a rank that hangs in its body is killed at the deadline
+    std::string e3;
+    auto hung = run_ranks(1, 1, 0, "127.0.0.1", free_port(), 128, make,
+                          [](const RankCtx&, const std::string&) {
+                            sleep(30);
+                            return std::string("late");
+                          },
+                          100, &e3);
+    CHECK(!e3.empty() && hung[0].exit_status == 128 + SIGKILL);
+    // GPU count without HIP: the visible-devices list the shim exports
+    setenv("HIP_VISIBLE_DEVICES", "2,3,5", 1);
+    CHECK(count_gpus_no_hip() == 3);
+    setenv("HIP_VISIBLE_DEVICES", "-1", 1);
+    CHECK(count_gpus_no_hip() == 0);
+    unsetenv("HIP_VISIBLE_DEVICES");
   });
 
   run("https download: verified TLS, SNI/hostname, redirect, untrusted CA refused", [] {

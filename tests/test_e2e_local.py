@@ -82,42 +82,70 @@ def test_env_and_secrets_interpolation(client, server):
 
 
 _FAKE_ROCPROF = r"""#!/bin/sh
-# stands in for rocprofv3: records the --pmc set, writes the two CSVs the runner summarises, runs
-# the job command
-dir=""; pmc=""
+# stands in for rocprofv3: records the --pmc set and the program it was put in front of, writes the
+# two CSVs the runner summarises (one pair per process, -o job_%pid%), then execs the program
+dir=""; pmc=""; out="job"
 while [ $# -gt 0 ]; do
   case "$1" in
     -d) dir="$2"; shift 2;;
+    -o) out="$2"; shift 2;;
     --pmc) shift; while [ $# -gt 0 ] && [ "${1#-}" = "$1" ]; do pmc="$pmc $1"; shift; done;;
     --) shift; break;;
     *) shift;;
   esac
 done
 echo "fake-rocprof pmc:$pmc"
-printf '"Name","Calls","TotalDurationNs"\n"gemm_kernel(float*, int)",10,5000\n' > "$dir/job_kernel_stats.csv"
-printf 'Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n1,"gemm_kernel(float*, int)",SQ_WAVES,64\n2,"gemm_kernel(float*, int)",SQ_WAVES,64\n1,"gemm_kernel(float*, int)",GRBM_GUI_ACTIVE,1000\n3,"norm(float*)",SQ_WAVES,8\n' > "$dir/job_counter_collection.csv"
-"$@"
+echo "fake-rocprof program: $1 rank=${RANK:-none}"
+base="$dir/$(echo "$out" | sed "s/%pid%/$$/")"
+printf '"Name","Calls","TotalDurationNs"\n"gemm_kernel(float*, int)",10,5000\n' > "${base}_kernel_stats.csv"
+printf 'Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n1,"gemm_kernel(float*, int)",SQ_WAVES,64\n2,"gemm_kernel(float*, int)",SQ_WAVES,64\n1,"gemm_kernel(float*, int)",GRBM_GUI_ACTIVE,1000\n3,"norm(float*)",SQ_WAVES,8\n' > "${base}_counter_collection.csv"
+exec "$@"
+"""
+
+# stands in for torchrun: --no-python runs the trailing argv once per local rank (RANK set)
+_FAKE_TORCHRUN = r"""#!/bin/sh
+n=1; nopy=0
+while [ $# -gt 0 ]; do
+  case "$1" in
+    --nproc-per-node) n="$2"; shift 2;;
+    --nproc-per-node=*) n="${1#*=}"; shift;;
+    --no-python) nopy=1; shift;;
+    -*) shift;;
+    *) break;;
+  esac
+done
+[ "$nopy" = 1 ] || { echo "fake-torchrun: rank program not wrapped"; exit 3; }
+i=0
+while [ $i -lt $n ]; do RANK=$i "$@" || exit $?; i=$((i + 1)); done
 """
 
 
-def test_rocprof_counters_in_job_log(client, tmp_path):
-    """DSTACK_ROCPROF_COUNTERS: the runner checks the set against rocprofv3's one-pass budget, adds
-    ``--pmc`` and appends per-kernel counter sums to the job log; an over-budget set is refused
-    with a log line and the job still runs (kernel statistics only)."""
-    from dstack_amd.api import Task
-
+def _fake_bin(tmp_path):
     bin_dir = tmp_path / "bin"
     bin_dir.mkdir()
-    fake = bin_dir / "rocprofv3"
-    fake.write_text(_FAKE_ROCPROF)
-    fake.chmod(0o755)
-    path = f"{bin_dir}:{os.environ.get('PATH', '/usr/bin:/bin')}"
-    run = client.runs.submit(Task(commands=["echo job-ran"], name="e2e-rocprof",
+    for name, text in (("rocprofv3", _FAKE_ROCPROF), ("torchrun", _FAKE_TORCHRUN)):
+        f = bin_dir / name
+        f.write_text(text)
+        f.chmod(0o755)
+    return f"{bin_dir}:{os.environ.get('PATH', '/usr/bin:/bin')}"
+
+
+def test_rocprof_counters_in_job_log(client, tmp_path):
+    """DSTACK_ROCPROF_COUNTERS: the runner checks the set against rocprofv3's one-pass budget, puts
+    rocprofv3 directly in front of the job's program (the shell execs it; never ``-- bash -c``),
+    adds ``--pmc`` and appends per-kernel sums to the job log; an over-budget set is refused with a
+    log line and the job still runs (kernel statistics only)."""
+    from dstack_amd.api import Task
+
+    path = _fake_bin(tmp_path)
+    run = client.runs.submit(Task(commands=["echo setup-ran", "echo job-ran"], name="e2e-rocprof",
                                   env={"PATH": path, "DSTACK_ROCPROF_COUNTERS": "SQ_WAVES,GRBM_GUI_ACTIVE"}))
     assert run.wait(timeout=60).value == "done"
     out = _logs(run)
-    assert "fake-rocprof pmc: SQ_WAVES GRBM_GUI_ACTIVE" in out and "job-ran" in out
-    assert "rocprofv3 kernel statistics" in out and "gemm_kernel(float*, int)" in out
+    assert "fake-rocprof pmc: SQ_WAVES GRBM_GUI_ACTIVE" in out and "job-ran" in out and "setup-ran" in out
+    assert "fake-rocprof program: echo rank=none" in out  # the program itself, not /bin/bash
+    assert out.count("fake-rocprof program:") == 1  # only the last command runs under the profiler
+    assert "rocprofv3 kernel statistics (1 process" in out and "gemm_kernel(float*, int) | 10 |" in out
     assert "rocprofv3 counters per kernel" in out
     assert "gemm_kernel | 2 | 128 | 1000" in out and "norm | 1 | 8 | 0" in out
     too_many = ",".join(f"SQ_C{i}" for i in range(9))
@@ -127,6 +155,48 @@ def test_rocprof_counters_in_job_log(client, tmp_path):
     out = _logs(run)
     assert "DSTACK_ROCPROF_COUNTERS ignored: SQ block needs 9 counters" in out
     assert "fake-rocprof pmc:\n" in out.replace("\r", "") and "job-ran" in out
+
+
+def test_rocprof_per_rank_under_torchrun_and_refusal(client, tmp_path):
+    """A torchrun job is profiled per rank (``torchrun --no-python rocprofv3 ... -- python3 -u
+    script``; the launcher is never under the profiler) and the summaries add up over the ranks'
+    CSVs; a job whose last command is a wrapper (``timeout``) is refused and runs unprofiled."""
+    from dstack_amd.api import Task
+
+    path = _fake_bin(tmp_path)
+    (tmp_path / "t.py").write_text("import os; print('rank-ran', os.environ.get('RANK'))\n")
+    run = client.runs.submit(Task(commands=[f"cd {tmp_path}", "torchrun --nproc-per-node=2 t.py"],
+                                  name="e2e-rocprof-torchrun", env={"PATH": path, "DSTACK_ROCPROF": "1"}))
+    assert run.wait(timeout=60).value == "done", _logs(run)
+    out = _logs(run)
+    assert "fake-rocprof program: python3 rank=0" in out and "fake-rocprof program: python3 rank=1" in out
+    assert "rank-ran 0" in out and "rank-ran 1" in out
+    assert "rocprofv3 kernel statistics (2 processes" in out and "gemm_kernel(float*, int) | 20 |" in out
+    run = client.runs.submit(Task(commands=["timeout 30 echo wrapped-job"], name="e2e-rocprof-refused",
+                                  env={"PATH": path, "DSTACK_ROCPROF": "1"}))
+    assert run.wait(timeout=60).value == "done"
+    out = _logs(run)
+    assert "DSTACK_ROCPROF ignored: the job's last command runs 'timeout'" in out and "wrapped-job" in out
+    assert "fake-rocprof" not in out
+
+
+@pytest.mark.gpu
+def test_rocprof_counters_on_gpu(client):
+    """On the MI355X: the real rocprofv3 with --pmc, put by the runner directly in front of a tiny
+    torch program (the job's shell execs it), and the per-kernel counter rows in the job log."""
+    from dstack_amd.api import GPU, Resources, Task
+
+    prog = "import torch; x = torch.ones(1 << 20, device='cuda'); print('gpu-sum', (x * 2).sum().item())"
+    run = client.runs.submit(Task(commands=["echo before-profiled-step", f'python3 -c "{prog}"'],
+                                  name="e2e-rocprof-gpu", resources=Resources(gpu=GPU(count=1)),
+                                  env={"DSTACK_ROCPROF_COUNTERS": "SQ_WAVES,GRBM_GUI_ACTIVE"}))
+    status = _wait(run, 300)
+    out = _logs(run)
+    print(out[-4000:])
+    assert status == "done", out[-3000:]
+    assert "gpu-sum 2097152.0" in out
+    assert "rocprofv3 kernel statistics (1 process" in out
+    assert "rocprofv3 counters per kernel" in out and "| SQ_WAVES | GRBM_GUI_ACTIVE" in out
 
 
 def test_stop_long_running(client):

@@ -208,11 +208,18 @@ def test_real_probe_relative_thresholds_and_one_rank_rccl():
     assert doc["healthy"] is True and r.returncode == 0, doc
     assert min(doc["hbm_tb_s"]) >= doc["thresholds"]["hbm_tb_s"]
     assert min(doc["mfma_bf16_tflops"]) >= doc["thresholds"]["mfma_bf16_tflops"]
+    # one process per GPU, forked before the probe touches HIP; at world 1 the sweep proves the
+    # bootstrap + communicator + an exact fp32 sum, and is flagged as not a bandwidth measurement
     r = subprocess.run([probe, "--rccl", "--quick", "--json"], capture_output=True, text=True, timeout=180)
     doc = json.loads(r.stdout.strip().splitlines()[-1])
     print(doc)
-    assert r.returncode == 0 and doc["rccl_world"] >= 1 and len(doc["rccl"]) >= 4
+    assert r.returncode == 0 and doc["healthy"] is True, doc
+    assert doc["rccl_world"] == doc["rccl_gpus_per_node"] >= 1 and len(doc["rccl"]) >= 4
     assert all(x["algbw_gb_s"] > 0 for x in doc["rccl"])
+    if doc["rccl_world"] == 1:
+        assert doc["rccl_busbw_gb_s"] is None and "not a bandwidth measurement" in doc["rccl_note"]
+    else:
+        assert doc["rccl_busbw_gb_s"] > 0
 
 
 @pytest.mark.gpu
