@@ -322,7 +322,7 @@ def refresh_gpu_health(inst: InstanceModel, jpd: JobProvisioningData, force: boo
             logger.warning("%s: GPU health probe failed: %s", inst.name, h.message)
         old = json.loads(inst.health_data)
     stale = not old.get("ran_at") or _time.time() - old["ran_at"] > GPU_PROBE_MAX_AGE.total_seconds()
-    if stale and state in ("idle", "done", "failed") and (inst.busy_blocks or 0) == 0 and \
+    if stale and state in ("idle", "done", "failed", "interrupted") and (inst.busy_blocks or 0) == 0 and \
             inst.status == InstanceStatus.IDLE.value:
         try:
             state = shim.start_gpu_probe()

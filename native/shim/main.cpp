@@ -61,7 +61,7 @@ void Shim::restore() {
         if (!storage_.get(id, cur)) return;
         driver_->wait(cur);
         storage_.set_status(id, TaskStatus::Terminated, "container_exited", "");
-        gpus_.release(cur.gpus);
+        release_gpus(cur.gpus);
       }).detach();
     }
   }
@@ -100,9 +100,15 @@ std::string Shim::start_gpu_probe() {
   }
   std::lock_guard<std::mutex> lk(probe_mu_);
   if (probing_) return "running";
-  // the probe saturates every GPU: never beside a job (its numbers and the job would both suffer)
-  if (gpus_.free_count() != gpus_.total()) return "busy";
+  // the probe saturates every GPU: never beside a job.  All GPUs are taken here, under probe_mu_
+  // (tasks grant under the same mutex), so a task either got its GPUs first (-> "busy") or finds
+  // probing_ set and pre-empts the probe -- never a probe running next to a job.
+  std::vector<int> all;
+  for (int i = 0; i < gpus_.total(); ++i) all.push_back(i);
+  if (!gpus_.lock(all)) return "busy";
   probing_ = true;
+  probe_interrupted_ = false;
+  probe_pid_ = -1;
   probe_state_ = "running";
   probe_started_ms_ = now_millis();
   std::thread(&Shim::probe_main, this).detach();
@@ -110,14 +116,42 @@ std::string Shim::start_gpu_probe() {
 }
 
 void Shim::probe_main() {
-  // hold every GPU in the lock for the probe's duration: a task arriving meanwhile waits for it
-  // (wait_for_probe) instead of sharing the GPUs with a bandwidth/MFMA saturation test
-  std::vector<int> all;
-  for (int i = 0; i < gpus_.total(); ++i) all.push_back(i);
-  const bool held = gpus_.lock(all);
+  // the probe runs as its own process group, so a GPU task can kill it (and its children) at once
   std::string out;
-  int rc = run_capture({opts_.probe_binary, "--quick", "--json"}, out);
-  if (held) gpus_.release(all);
+  int rc = -1;
+  int pfd[2];
+  if (pipe(pfd) == 0) {
+    std::vector<std::string> argv = {opts_.probe_binary, "--quick", "--json"};
+    std::vector<char*> a;
+    for (auto& x : argv) a.push_back(const_cast<char*>(x.c_str()));
+    a.push_back(nullptr);
+    pid_t pid = fork();
+    if (pid == 0) {
+      setpgid(0, 0);
+      dup2(pfd[1], 1);
+      close(pfd[0]);
+      close(pfd[1]);
+      execv(a[0], a.data());
+      _exit(127);
+    }
+    close(pfd[1]);
+    if (pid > 0) {
+      bool killed_early = false;
+      {
+        std::lock_guard<std::mutex> lk(probe_mu_);
+        probe_pid_ = pid;
+        killed_early = probe_interrupted_;  // pre-empted before the pid was known
+      }
+      if (killed_early) kill(-pid, SIGKILL), kill(pid, SIGKILL);
+      char buf[4096];
+      ssize_t n;
+      while ((n = read(pfd[0], buf, sizeof buf)) > 0) out.append(buf, (size_t)n);
+      int st = 0;
+      waitpid(pid, &st, 0);
+      rc = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+    }
+    close(pfd[0]);
+  }
   Json doc;
   for (auto& line : split(out, '\n')) {
     std::string l = trim(line);
@@ -129,26 +163,42 @@ void Shim::probe_main() {
   }
   {
     std::lock_guard<std::mutex> lk(probe_mu_);
-    probe_ran_ms_ = now_millis();
-    if (doc.is_object()) {
-      probe_doc_ = doc;
-      probe_state_ = "done";
+    probe_pid_ = -1;
+    std::vector<int> all;
+    for (int i = 0; i < gpus_.total(); ++i) all.push_back(i);
+    gpus_.release(all);  // under probe_mu_: a waiting task grants right after this block
+    if (probe_interrupted_) {
+      probe_state_ = "interrupted";  // the previous result (if any) stays the instance's health
     } else {
-      probe_state_ = "failed";
-      Json e = Json::object();
-      e.set("healthy", false);
-      e.set("message", "probe exited " + std::to_string(rc) + " without a result: " + out.substr(0, 300));
-      probe_doc_ = e;
+      probe_ran_ms_ = now_millis();
+      if (doc.is_object()) {
+        probe_doc_ = doc;
+        probe_state_ = "done";
+      } else {
+        probe_state_ = "failed";
+        Json e = Json::object();
+        e.set("healthy", false);
+        e.set("message", "probe exited " + std::to_string(rc) + " without a result: " + out.substr(0, 300));
+        probe_doc_ = e;
+      }
     }
     probing_ = false;
   }
   probe_cv_.notify_all();
-  LOGI("gpu health probe %s in %lld ms", probe_state_.c_str(), (long long)(probe_ran_ms_ - probe_started_ms_));
+  LOGI("gpu health probe %s in %lld ms", probe_state_.c_str(), (long long)(now_millis() - probe_started_ms_));
 }
 
-void Shim::wait_for_probe(int max_ms) {
-  std::unique_lock<std::mutex> lk(probe_mu_);
-  probe_cv_.wait_for(lk, std::chrono::milliseconds(max_ms), [this] { return !probing_; });
+void Shim::release_gpus(const std::vector<int>& idx) {
+  bool reprobe = false;
+  {
+    std::lock_guard<std::mutex> lk(probe_mu_);
+    gpus_.release(idx);
+    reprobe = probe_interrupted_ && !probing_ && gpus_.free_count() == gpus_.total();
+  }
+  if (reprobe) {
+    LOGI("host idle again: re-running the interrupted GPU health probe");
+    start_gpu_probe();
+  }
 }
 
 Json Shim::gpu_health() {
@@ -164,21 +214,37 @@ Json Shim::gpu_health() {
 void Shim::run_task(std::string id) {
   Task t;
   if (!storage_.get(id, t)) return;
-  if (t.config.gpu != 0 || !t.config.gpu_indices.empty()) wait_for_probe(120000);
   storage_.set_status(id, TaskStatus::Preparing);
-  // GPU grant: explicit indices (server-side xGMI placement) or a count resolved here
+  // GPU grant: explicit indices (server-side xGMI placement) or a count resolved here.  Granted
+  // under probe_mu_, like the probe's own all-GPU lock: a health probe holding the GPUs is
+  // pre-empted (killed; it re-runs when the host is idle) instead of delaying the job behind it.
   std::vector<int> granted;
-  if (!t.config.gpu_indices.empty()) {
-    if (!gpus_.lock(t.config.gpu_indices)) {
-      storage_.set_status(id, TaskStatus::Terminated, "creating_container_error", "requested GPUs are busy");
-      return;
+  if (t.config.gpu != 0 || !t.config.gpu_indices.empty()) {
+    std::unique_lock<std::mutex> lk(probe_mu_);
+    if (probing_) {
+      probe_interrupted_ = true;
+      if (probe_pid_ > 0) {
+        kill(-probe_pid_, SIGKILL);
+        kill(probe_pid_, SIGKILL);
+      }
+      LOGI("task %s pre-empts the running GPU health probe", id.c_str());
+      probe_cv_.wait_for(lk, std::chrono::seconds(30), [this] { return !probing_; });
     }
-    granted = t.config.gpu_indices;
-  } else if (t.config.gpu != 0) {
-    granted = gpus_.acquire(t.config.gpu);
-    if (granted.empty() || (t.config.gpu > 0 && (int)granted.size() != t.config.gpu)) {
-      gpus_.release(granted);
-      storage_.set_status(id, TaskStatus::Terminated, "creating_container_error", "not enough free GPUs");
+    std::string why;
+    if (!t.config.gpu_indices.empty()) {
+      if (gpus_.lock(t.config.gpu_indices)) granted = t.config.gpu_indices;
+      else why = "requested GPUs are busy";
+    } else {
+      granted = gpus_.acquire(t.config.gpu);
+      if (granted.empty() || (t.config.gpu > 0 && (int)granted.size() != t.config.gpu)) {
+        gpus_.release(granted);
+        granted.clear();
+        why = "not enough free GPUs";
+      }
+    }
+    if (!why.empty()) {
+      lk.unlock();
+      storage_.set_status(id, TaskStatus::Terminated, "creating_container_error", why);
       return;
     }
   }
@@ -201,14 +267,14 @@ void Shim::run_task(std::string id) {
   }
   if (!ok) {
     LOGW("task %s failed to start: %s", id.c_str(), msg.c_str());
-    gpus_.release(granted);
+    release_gpus(granted);
     storage_.set_status(id, TaskStatus::Terminated, reason, msg);
     return;
   }
   storage_.set_status(id, TaskStatus::Running);
   LOGI("task %s running (runner port %d, gpus %zu)", id.c_str(), t.runner_port, granted.size());
   driver_->wait(t);
-  gpus_.release(granted);
+  release_gpus(granted);
   storage_.set_status(id, TaskStatus::Terminated, "done_by_runner", "");
   if (!t.config.host_ssh_keys.empty() && !t.config.host_ssh_user.empty())
     remove_authorized_keys(t.config.host_ssh_user, t.config.host_ssh_keys);

@@ -177,15 +177,16 @@ class Shim {
   std::vector<std::string> render_nodes_of(const std::vector<int>& idx) const;
   // GPU health probe (dstack-probe --quick --json), run asynchronously off the job path: at shim
   // start and on demand.  start_gpu_probe: "started" | "running" | "busy" (GPU tasks hold GPUs)
-  // | "unavailable" (no probe binary or no GPUs)
+  // | "unavailable" (no probe binary or no GPUs); a GPU task arriving while it runs pre-empts it
+  // (the probe is killed, state "interrupted") and it runs again once the GPUs are all free
   std::string start_gpu_probe();
   Json gpu_health();
 
  private:
   void run_task(std::string id);
   void probe_main();
-  // tasks that need GPUs wait (bounded) while the probe owns them
-  void wait_for_probe(int max_ms);
+  // GPUs released by a task: re-run a probe that a task interrupted once the host is idle again
+  void release_gpus(const std::vector<int>& idx);
   ShimOptions opts_;
   std::unique_ptr<TaskDriver> driver_;
   TaskStorage storage_;
@@ -193,8 +194,10 @@ class Shim {
   std::vector<std::string> inventory_render_;  // index -> /dev/dri/renderD*
   std::mutex probe_mu_;
   std::condition_variable probe_cv_;
-  bool probing_ = false;
-  std::string probe_state_ = "idle";  // idle | running | done | failed | unavailable
+  bool probing_ = false;             // the probe holds every GPU in gpus_ while this is set
+  pid_t probe_pid_ = -1;             // its process group, so a GPU task can pre-empt it
+  bool probe_interrupted_ = false;   // the last probe was killed for a task: re-probe when idle
+  std::string probe_state_ = "idle";  // idle | running | done | failed | interrupted | unavailable
   Json probe_doc_;
   int64_t probe_started_ms_ = 0, probe_ran_ms_ = 0;
   Json host_info_;

@@ -101,25 +101,73 @@ def test_shim_probes_at_start_and_on_demand(shim):
     assert httpx.get(url + "/api/healthcheck", timeout=2).json()["gpus_free"] == 2
 
 
-def test_gpu_task_waits_for_a_running_probe(shim):
-    """A task asking for GPUs while the probe holds them starts after it, not beside it."""
-    url, _ = shim
+def test_gpu_task_preempts_a_running_probe(shim, tmp_path):
+    """A task asking for GPUs while the probe holds them pre-empts it: the probe is killed (state
+    "interrupted"), the task gets its GPU at once instead of waiting out the probe, and the probe
+    runs again once the host is idle."""
+    url, probe = shim
     _wait_state(url, {"done"})
+    first = httpx.get(url + "/api/gpu_health", timeout=2).json()
+    marker = tmp_path / "probe-finished"
+    runs = tmp_path / "probe-runs"
+    probe.write_text("#!/bin/sh\n"
+                     f"echo run >> {runs}\n"
+                     "sleep 30\n"
+                     f"touch {marker}\n"
+                     f"echo '{json.dumps(GOOD)}'\n")
     assert httpx.post(url + "/api/gpu_health/probe", timeout=2).json()["state"] == "started"
+    deadline = time.time() + 5
+    while not runs.exists() and time.time() < deadline:
+        time.sleep(0.02)
+    assert httpx.get(url + "/api/healthcheck", timeout=2).json()["gpus_free"] == 0
     t0 = time.time()
     r = httpx.post(url + "/api/tasks", json={"id": "t1", "name": "t1", "image_name": "x", "gpu": 1,
                                             "container_ssh_keys": []}, timeout=5)
     assert r.status_code == 200
-    deadline = time.time() + 10
-    while time.time() < deadline:
+    t = {}
+    while time.time() < t0 + 10:
         t = httpx.get(url + "/api/tasks/t1", timeout=2).json()
-        if t["status"] not in ("pending", "preparing"):
+        if t.get("gpus"):
             break
-        time.sleep(0.02)
-    assert t["gpus"] and len(t["gpus"]) == 1, t
-    probe_done = httpx.get(url + "/api/gpu_health", timeout=2).json()["ran_at_ms"] / 1000.0
-    assert probe_done >= t0  # the grant happened only after the probe finished
+        time.sleep(0.01)
+    granted_after = time.time() - t0
+    assert t.get("gpus") and len(t["gpus"]) == 1, t
+    assert granted_after < 1.0, granted_after  # not behind the 30 s probe
+    h = httpx.get(url + "/api/gpu_health", timeout=2).json()
+    assert h["state"] in ("interrupted", "running"), h  # running = already re-probing after the task
+    assert h["ran_at_ms"] == first["ran_at_ms"] or h["state"] == "running"
+    assert not marker.exists()  # killed, never finished
     assert t["render_nodes"] == [["/dev/dri/renderD136", "/dev/dri/renderD128"][t["gpus"][0]]]
+    # the task ends (stand-in runner): the host is idle again and the interrupted probe re-runs
+    deadline = time.time() + 20
+    while time.time() < deadline and runs.read_text().count("run") < 2:
+        time.sleep(0.05)
+    assert runs.read_text().count("run") == 2
+
+
+def test_probe_and_task_never_share_gpus(shim):
+    """Interleaved probe requests and GPU tasks: a probe that finds a GPU in use reports "busy"
+    and never starts beside the job; a task never fails because the probe held the GPUs."""
+    url, _ = shim
+    _wait_state(url, {"done"})
+    states, tasks = [], []
+    for i in range(6):
+        states.append(httpx.post(url + "/api/gpu_health/probe", timeout=2).json()["state"])
+        tid = f"mix{i}"
+        httpx.post(url + "/api/tasks", json={"id": tid, "name": tid, "image_name": "x", "gpu": 1,
+                                            "container_ssh_keys": []}, timeout=5)
+        tasks.append(tid)
+    deadline = time.time() + 20
+    final = {}
+    while time.time() < deadline:
+        final = {tid: httpx.get(url + f"/api/tasks/{tid}", timeout=2).json() for tid in tasks}
+        if all(t["status"] == "terminated" for t in final.values()):
+            break
+        time.sleep(0.05)
+    for t in final.values():
+        assert t.get("termination_message") != "not enough free GPUs", t
+        assert t.get("termination_message") != "requested GPUs are busy", t
+    assert set(states) <= {"started", "running", "busy"}
 
 
 # ---- server side -----------------------------------------------------------------------------
