@@ -287,6 +287,10 @@ class OnlineCache:
         self.ttl = ttl if ttl is not None else float(os.getenv("DSTACK_CATALOG_ONLINE_TTL", 300))
         self.max_stale = max_stale if max_stale is not None else float(os.getenv("DSTACK_CATALOG_MAX_STALE", 86400))
         self.directory = directory
+        # after a failed live fetch the key is not fetched again for this long (serving cached or
+        # offline rows meanwhile): an unreachable API must not stall every plan / scheduler pass
+        self.failure_backoff = min(self.ttl, float(os.getenv("DSTACK_CATALOG_FAILURE_BACKOFF", 60)))
+        self._failed: Dict[str, float] = {}
         self._mem: Dict[str, Tuple[float, List[CatalogRow]]] = {}
         self._locks: Dict[str, threading.Lock] = {}
         self._guard = threading.Lock()
@@ -326,20 +330,32 @@ class OnlineCache:
             if hit and now - hit[0] < self.ttl:
                 self._mem[key] = hit
                 return hit[1]
+            failed_at = self._failed.get(key)
+            if failed_at is not None and now - failed_at < self.failure_backoff:
+                return hit[1] if hit and now - hit[0] < self.max_stale else None  # negative cache
             try:
                 rows = fetch()
             except Exception as e:  # noqa: BLE001 -- any API failure degrades to cached/offline data
+                self._failed[key] = now
                 if hit and now - hit[0] < self.max_stale:
                     logger.warning("catalog: live listing %s failed (%s); serving data %.0fs old", key, e, now - hit[0])
                     return hit[1]
-                logger.warning("catalog: live listing %s failed (%s); using the offline catalog", key, e)
+                logger.warning("catalog: live listing %s failed (%s); using the offline catalog for %.0fs", key, e,
+                               self.failure_backoff)
                 return None
+            self._failed.pop(key, None)
             self._store(key, now, rows)
             return rows
 
 
 _offline = OfflineCatalog()
 _online = OnlineCache()
+
+
+def catalog_fetch_timeout() -> float:
+    """Per-request HTTP timeout (s) of live catalog listings (``DSTACK_CATALOG_FETCH_TIMEOUT``,
+    default 10): a listing feeds a plan, so it must fail fast, unlike a launch call."""
+    return float(os.getenv("DSTACK_CATALOG_FETCH_TIMEOUT", 10))
 
 
 def reset_catalog_state() -> None:

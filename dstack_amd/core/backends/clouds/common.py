@@ -19,6 +19,7 @@ import datetime as _dt
 import hashlib
 import hmac
 import json
+import threading
 import os
 import subprocess
 import tempfile
@@ -29,7 +30,7 @@ from typing import Dict, List, Optional, Tuple
 import httpx
 
 from dstack_amd.core.backends.base import Compute, get_docker_commands, get_user_data
-from dstack_amd.core.backends.catalog import CatalogRow, get_catalog_offers
+from dstack_amd.core.backends.catalog import CatalogRow, catalog_fetch_timeout, get_catalog_offers
 from dstack_amd.core.errors import BackendAuthError, ComputeError, NoCapacityError
 from dstack_amd.core.models.instances import (
     InstanceAvailability,
@@ -68,6 +69,24 @@ def check_response(r: httpx.Response, what: str) -> httpx.Response:
     return r
 
 
+_catalog_fetch = threading.local()
+
+
+def _catalog_timeout_hook(request: httpx.Request) -> None:
+    """httpx request hook: inside a live catalog fetch (this thread), requests get the short catalog
+    timeout instead of the client's launch-sized one."""
+    t = getattr(_catalog_fetch, "timeout", None)
+    if t:
+        request.extensions["timeout"] = httpx.Timeout(t).as_dict()
+
+
+def install_catalog_timeout(client: httpx.Client) -> httpx.Client:
+    hooks = client.event_hooks.get("request", [])
+    if _catalog_timeout_hook not in hooks:
+        client.event_hooks = {**client.event_hooks, "request": [*hooks, _catalog_timeout_hook]}
+    return client
+
+
 class CatalogOffers:
     """``get_offers`` from the catalog layers (catalog.py): the backend's live listing when it has
     one (``_fetch_catalog``), else the offline catalog."""
@@ -77,7 +96,14 @@ class CatalogOffers:
     CONFIGURABLE_DISK: Tuple[float, Optional[float]] = (1.0, None)
 
     def get_offers(self, requirements: Optional[Requirements] = None) -> List[InstanceOfferWithAvailability]:
-        fetch = self._fetch_catalog if self.has_online_catalog() else None
+        fetch = None
+        if self.has_online_catalog():
+            def fetch():
+                _catalog_fetch.timeout = catalog_fetch_timeout()
+                try:
+                    return self._fetch_catalog()
+                finally:
+                    _catalog_fetch.timeout = None
         offers = get_catalog_offers(self.TYPE, self.regions(), requirements, self.CONFIGURABLE_DISK,
                                     extra_filter=self._offer_filter, fetch=fetch, cache_key=self.catalog_key())
         avail = self._availability()
@@ -131,7 +157,7 @@ class VMCompute(CatalogOffers, Compute):
         super().__init__()
         self.config = config or {}
         self.auth = auth or {}
-        self.http = client or httpx.Client(timeout=60)
+        self.http = install_catalog_timeout(client or httpx.Client(timeout=60))
 
     # ---- lifecycle ----------------------------------------------------------------------------
     def create_instance(self, instance_offer: InstanceOfferWithAvailability,

@@ -18,7 +18,12 @@ import yaml
 
 from dstack_amd.core.backends.base import Compute, DSTACK_RUNNER_SSH_PORT
 from dstack_amd.core.backends.catalog import CatalogRow, gpu_row
-from dstack_amd.core.backends.clouds.common import CatalogOffers, check_response, container_commands
+from dstack_amd.core.backends.clouds.common import (
+    CatalogOffers,
+    check_response,
+    container_commands,
+    install_catalog_timeout,
+)
 from dstack_amd.core.errors import BackendAuthError, ComputeError, NoCapacityError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.gpus import normalize_gpu_name
@@ -45,7 +50,7 @@ class ContainerCompute(CatalogOffers, Compute):
     def __init__(self, config: Dict, auth: Dict, client: Optional[httpx.Client] = None):
         super().__init__()
         self.config, self.auth = config or {}, auth or {}
-        self.http = client or httpx.Client(timeout=60)
+        self.http = install_catalog_timeout(client or httpx.Client(timeout=60))
 
 
 # ---------------------------------------------------------------------------------------------

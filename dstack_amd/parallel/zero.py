@@ -74,6 +74,7 @@ class ZeroOptimizer:
         # the reduce-scatters still overlap backward and the all-gathers the next forward; only
         # the AdamW update itself leaves the backward's shadow.
         self.clip_grad_norm = float(clip_grad_norm)
+        self.skipped_steps = 0  # optimizer steps skipped for a non-finite gradient norm (clipping on)
         self.last_grad_norm: float | None = None
         self.beta1, self.beta2 = betas
         self.eps = eps
@@ -341,9 +342,18 @@ class ZeroOptimizer:
                     b.work = None
         clip_scale = 1.0
         if self.clip_grad_norm:
-            norm = self._grad_norm(self.buckets)
+            norm = self._grad_norm(self.buckets)  # all-reduced: every rank sees the same value
             self.last_grad_norm = norm
-            if math.isfinite(norm) and norm > self.clip_grad_norm:
+            if not math.isfinite(norm):
+                # an inf/NaN gradient would poison the fp32 master weights and both moments for
+                # good: skip the update on every rank (the same decision everywhere, so shards and
+                # step counts stay consistent; parameters are unchanged, nothing to all-gather)
+                self.step_count -= 1
+                self.skipped_steps += 1
+                for b in self.buckets:
+                    b.updated = False
+                return
+            if norm > self.clip_grad_norm:
                 clip_scale = self.clip_grad_norm / (norm + 1e-6)
         for b in pending:
             self._adamw(b, self.step_count, clip_scale=clip_scale)

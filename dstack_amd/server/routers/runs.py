@@ -214,6 +214,12 @@ def pool_delete(body: schemas.DeletePoolRequest, up: UP = Depends(project_member
 @pool_router.post("/remove")
 def pool_remove_instance(body: schemas.RemoveInstanceRequest, up: UP = Depends(project_member),
                          s: Session = Depends(get_session, scope="function")):
+    from dstack_amd.server.services.permissions import check_can_manage_ssh_fleets
+
+    pool = pools_services.get_pool(s, up[1], body.pool_name)
+    if pool is not None and any(i.name == body.instance_name and i.backend == "remote" and not i.deleted
+                                for i in pool.instances):
+        check_can_manage_ssh_fleets(up[0], up[1])  # SSH hosts: same rule as SSH fleets
     pools_services.remove_instance(s, up[1], body.pool_name, body.instance_name, body.force)
     return None
 
@@ -221,6 +227,9 @@ def pool_remove_instance(body: schemas.RemoveInstanceRequest, up: UP = Depends(p
 @pool_router.post("/add_remote")
 def pool_add_remote(body: schemas.AddRemoteInstanceRequest, up: UP = Depends(project_member),
                     s: Session = Depends(get_session, scope="function")) -> Instance:
+    from dstack_amd.server.services.permissions import check_can_manage_ssh_fleets
+
+    check_can_manage_ssh_fleets(up[0], up[1])  # an SSH host is an SSH fleet by another door
     if not body.host.strip() or not body.ssh_user.strip() or not body.ssh_keys:
         raise ServerClientError("Host, user or ssh keys are empty")
     return pools_services.add_remote(s, up[1], body.pool_name, body.instance_name, body.instance_network,

@@ -150,6 +150,47 @@ def test_failed_live_listing_falls_back_to_offline(live):
     assert offers and offers[0].availability == IA.UNKNOWN  # the built-in row
 
 
+def test_unreachable_listing_is_fetched_once_per_backoff(live, monkeypatch):
+    """Negative caching: a listing that failed is not fetched again for the backoff period (cached
+    or offline rows meanwhile), so an air-gapped server does not stall every plan on the API; and
+    live listings run with the short catalog timeout, not the client's launch timeout."""
+    timeouts = []
+
+    def handler(r):
+        timeouts.append(r.extensions.get("timeout"))
+        raise httpx.ConnectError("unreachable")
+
+    c = compute_class(BackendType.LAMBDA)({}, {"api_key": "k"}, _client(handler))
+    for _ in range(3):
+        assert c.get_offers(_req(gpu="H100:8"))  # the built-in rows
+    assert len(timeouts) == 1
+    assert timeouts[0]["connect"] == catalog.catalog_fetch_timeout() == 10.0
+    # outside a catalog fetch the same client keeps its own timeout
+    try:
+        c.http.get("https://cloud.lambdalabs.com/api/v1/instances")
+    except httpx.ConnectError:
+        pass
+    assert timeouts[-1]["connect"] != 10.0
+    # after the backoff the listing is tried again
+    monkeypatch.setattr(catalog._online, "failure_backoff", 0.0)
+    c.get_offers(_req(gpu="H100:8"))
+    assert len(timeouts) == 3
+
+
+def test_online_cache_failure_backoff_serves_stale(tmp_path):
+    row = gpu_row("t", "r", 1.0, 1, 1, None, 0)
+    n = {"calls": 0}
+
+    def boom():
+        n["calls"] += 1
+        raise RuntimeError("api down")
+
+    c = OnlineCache(ttl=60, max_stale=3600, directory=tmp_path)
+    c.get("k", lambda: [row])
+    c._mem["k"] = (time.time() - 120, [row])  # expired, still within max_stale
+    assert c.get("k", boom) == [row] and c.get("k", boom) == [row] and n["calls"] == 1
+
+
 def test_offline_only_switch(live, monkeypatch):
     hits = []
     c = compute_class(BackendType.LAMBDA)({"offline_catalog": True}, {"api_key": "k"},

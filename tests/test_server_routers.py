@@ -449,6 +449,15 @@ def test_default_permissions_restrict_projects_and_ssh_fleets(client, tmp_path):
         assert client.post("/api/project/main/fleets/create", json=spec).status_code == 200
         r = client.post("/api/project/main/fleets/delete", json={"names": ["onprem2"]}, headers=erin)
         assert r.status_code == 403
+        # the pool API's SSH-host door is closed by the same rule
+        host = {"host": "10.0.0.10", "port": 22, "ssh_user": "ubuntu", "ssh_keys": [key], "instance_name": "h10"}
+        assert client.post("/api/project/main/pool/add_remote", json=host, headers=erin).status_code == 403
+        r = client.post("/api/project/main/pool/add_remote", json=host)
+        assert r.status_code == 200, r.text
+        pool = client.post("/api/project/main/pool/list").json()[0]["name"]
+        r = client.post("/api/project/main/pool/remove", json={"pool_name": pool, "instance_name": r.json()["name"],
+                                                               "force": True}, headers=erin)
+        assert r.status_code == 403, r.text
         # promoted to project admin: allowed
         client.post("/api/projects/main/set_members",
                     json={"members": [{"username": "admin", "project_role": "admin"},

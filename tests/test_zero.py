@@ -61,16 +61,18 @@ def _reference_steps(model, steps_batches, grad_accum, clip=0.0, norms=None):
 
 
 def _zero_steps(model, steps_batches, grad_accum, bucket_numel=1 << 20, eps=EPS, prefetch=False, clip=0.0,
-                norms=None):
+                norms=None, poison_step=None):
     opt = ZeroOptimizer(model, lr=LR, betas=BETAS, eps=eps, weight_decay=WD, bucket_numel=bucket_numel,
                         clip_grad_norm=clip)
     if prefetch:
         opt.install_prefetch_hooks(model)
-    for micro in steps_batches:
+    for step, micro in enumerate(steps_batches):
         opt.zero_grad()
         for i, b in enumerate(micro):
             opt.sync_grads = i == len(micro) - 1
             loss = model.loss(b[:, :-1], b[:, 1:])
+            if step == poison_step:
+                loss = loss * float("inf")  # every gradient becomes inf/NaN
             (loss / grad_accum).backward()
         opt.step()
         if norms is not None:
@@ -116,17 +118,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, prefetch=False, bucket_numel=1 << 19, clip=0.0):
+def _worker(rank, world, port, out_dir, prefetch=False, bucket_numel=1 << 19, clip=0.0, poison=None, nsteps=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(max(1, 8 // world))
     base = _model()
-    steps = [_batches(2, 2 * world, seed=s) for s in range(2)]
+    steps = [_batches(2, 2 * world, seed=s) for s in range(nsteps)]
     # each rank takes its slice of every micro-batch
     mine = [[b[rank * 2:(rank + 1) * 2] for b in micro] for micro in steps]
-    model, _ = _zero_steps(base, mine, grad_accum=2, bucket_numel=bucket_numel, eps=EPS_DIST, prefetch=prefetch,
-                           clip=clip)
+    # poison = (rank, step): that rank's gradient of that step is inf/NaN
+    model, opt = _zero_steps(base, mine, grad_accum=2, bucket_numel=bucket_numel, eps=EPS_DIST, prefetch=prefetch,
+                             clip=clip, poison_step=poison[1] if poison and poison[0] == rank else None)
     torch.save({k: v.detach() for k, v in model.state_dict().items()}, os.path.join(out_dir, f"rank{rank}.pt"))
+    torch.save({"step_count": opt.step_count, "skipped": opt.skipped_steps}, os.path.join(out_dir, f"opt{rank}.pt"))
     dist.destroy_process_group()
 
 
@@ -155,6 +159,26 @@ def test_zero_gloo_world2_clipping_matches_single_process(tmp_path):
     states = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     base = _model()
     steps = [_batches(2, 2 * world, seed=s) for s in range(2)]
+    single, _ = _zero_steps(base, steps, grad_accum=2, eps=EPS_DIST, clip=0.5)
+    for k, v in single.state_dict().items():
+        assert (states[0][k] - v).abs().max().item() < 2e-6, k
+
+
+def test_zero_gloo_world2_skips_nonfinite_step(tmp_path):
+    """Clipping on, one rank's gradient of step 2 is inf/NaN: the all-reduced norm is non-finite on
+    every rank, so every rank skips that AdamW update (master weights and moments stay clean, the
+    step counter does not advance) -- the result equals one process that never saw step 2."""
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), True, 1 << 19, 0.5, (1, 1), 3),
+                       nprocs=world, start_method="spawn")
+    states = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    for r in range(world):
+        o = torch.load(tmp_path / f"opt{r}.pt", weights_only=True)
+        assert o == {"step_count": 2, "skipped": 1}, o
+    for k in states[0]:
+        assert torch.isfinite(states[0][k]).all() and torch.equal(states[0][k], states[1][k]), k
+    base = _model()
+    steps = [_batches(2, 2 * world, seed=s) for s in (0, 2)]
     single, _ = _zero_steps(base, steps, grad_accum=2, eps=EPS_DIST, clip=0.5)
     for k, v in single.state_dict().items():
         assert (states[0][k] - v).abs().max().item() < 2e-6, k
