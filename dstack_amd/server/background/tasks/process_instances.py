@@ -90,14 +90,33 @@ def _deploy_executor():
     return _deploy_pool
 
 
+# A deploy can take minutes (agent upload, shim start, host_info polling), so it is leased on the
+# instance row: the replica that starts it records itself and the start time while it holds the
+# row (claimed FOR UPDATE on Postgres), and every other replica skips the instance until the lease
+# is older than the deploy deadline -- with several server replicas on one database a host is
+# never deployed twice, and only the owner applies the result (reference: the instance lock held
+# across the deploy, process_instances.py:210-377).
+DEPLOY_LEASE = PROVISIONING_DEADLINE
+
+
 def _add_remote(s: Session, inst: InstanceModel):
+    from dstack_amd.server import settings
+
+    me = settings.SERVER_REPLICA_ID
+    now = get_current_datetime()
     fut = _deploys.get(inst.id)
     if fut is not None and not fut.done():
         return  # still deploying on its worker
     if fut is None:
-        if inst.last_retry_at and get_current_datetime() - inst.last_retry_at < SSH_DEPLOY_RETRY:
+        if inst.deploy_owner and inst.deploy_owner != me and inst.deploy_started_at and \
+                now - inst.deploy_started_at < DEPLOY_LEASE:
+            return  # another replica's deploy is in flight
+        if inst.last_retry_at and now - inst.last_retry_at < SSH_DEPLOY_RETRY:
             return
-        inst.last_retry_at = get_current_datetime()
+        inst.last_retry_at = now
+        inst.deploy_owner = me
+        inst.deploy_started_at = now
+        s.commit()  # the lease is visible to other replicas before the deploy starts
         rci = RemoteConnectionInfo.model_validate_json(inst.remote_connection_info)
         project = inst.project
         key = next((k.private for k in rci.ssh_keys if k.private), None) or project.ssh_private_key
@@ -107,6 +126,10 @@ def _add_remote(s: Session, inst: InstanceModel):
         if not fut.done():
             return
     _deploys.pop(inst.id, None)
+    if inst.deploy_owner not in (None, me):
+        return  # the lease expired and another replica took the host over: its deploy wins
+    inst.deploy_owner = None
+    inst.deploy_started_at = None
     rci = RemoteConnectionInfo.model_validate_json(inst.remote_connection_info)
     try:
         host_info = fut.result()

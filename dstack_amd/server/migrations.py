@@ -37,6 +37,8 @@ MIGRATIONS: List[Callable] = [
     # example of an additive migration kept for databases created before the column existed
     _add_column("jobs", "timings", "TEXT"),
     _add_column("job_metrics_points", "gpus_extra", "TEXT"),
+    _add_column("instances", "deploy_owner", "VARCHAR(100)"),
+    _add_column("instances", "deploy_started_at", "TIMESTAMP"),
 ]
 
 

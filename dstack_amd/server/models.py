@@ -235,6 +235,10 @@ class InstanceModel(Base):
     jobs: Mapped[List["JobModel"]] = relationship(back_populates="instance")
     last_job_processed_at: Mapped[Optional[datetime]] = mapped_column(DateTime, nullable=True)
     volumes: Mapped[List["VolumeModel"]] = relationship(secondary=volumes_attachments, back_populates="instances")
+    # SSH-fleet deploy lease: the server replica running this host's deploy and when it started;
+    # other replicas leave the instance alone until the lease expires (process_instances._add_remote)
+    deploy_owner: Mapped[Optional[str]] = mapped_column(String(100), nullable=True)
+    deploy_started_at: Mapped[Optional[datetime]] = mapped_column(DateTime, nullable=True)
 
 
 class RunModel(Base):

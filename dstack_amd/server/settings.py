@@ -83,3 +83,8 @@ ACME_EAB_HMAC_KEY = os.getenv("DSTACK_ACME_EAB_HMAC_KEY")
 MAX_OFFERS_TRIED = int(os.getenv("DSTACK_SERVER_MAX_OFFERS_TRIED", "15"))
 MAX_PLAN_OFFERS = 50
 DEFAULT_RUNNER_TIMEOUT = 600
+
+
+# identity of this server process among replicas sharing one database (leases such as the SSH-fleet
+# deploy lease record it); fresh per process unless pinned
+SERVER_REPLICA_ID = os.getenv("DSTACK_SERVER_REPLICA_ID") or __import__("uuid").uuid4().hex

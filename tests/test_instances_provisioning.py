@@ -195,3 +195,95 @@ def test_fleet_backend_data_records_placement(db):
         _fleet(s, {"name": "bd", "nodes": 2, "placement": "cluster"})
         assert all(json.loads(i.backend_data)["placement"] == "cluster" for i in _instances(s, "bd"))
     _ = get_current_datetime
+
+
+# ---- SSH-fleet deploys across server replicas ----------------------------------------------------
+HOST_INFO = {"cpus": 128, "memory": 2 << 40, "disk_size": 10 << 40, "addresses": ["10.0.0.5/eth0"],
+             "topology": {"gpus": [{"index": i, "name": "MI355X", "memory_mib": 288 * 1024} for i in range(8)],
+                          "xgmi": [[int(i != j) for j in range(8)] for i in range(8)], "numa": {}, "nics": []}}
+
+
+def _remote_instance(s):
+    from dstack_amd.core.models.instances import SSHKey
+    from dstack_amd.server.services import pools as pools_services
+
+    project = s.query(ProjectModel).filter_by(name="main").one()
+    inst = pools_services.add_remote(s, project, None, "h5", None, None, "10.0.0.5", 22, "ubuntu",
+                                     [SSHKey(public="ssh-ed25519 AAAA", private="k")])
+    return inst.id
+
+
+def test_ssh_deploy_leased_once_across_replicas(db, monkeypatch):
+    """Two server replicas on one database, each with its own in-process deploy futures: the replica
+    that starts a host's deploy leases the instance row, the other skips it (even past the 30 s
+    retry gate), only the owner applies the result, and an expired lease of a dead replica is taken
+    over (reference: the instance lock across the deploy, process_instances.py:210-377)."""
+    import threading
+
+    from dstack_amd.server import settings
+
+    with session_scope() as s:
+        iid = _remote_instance(s)
+    gate, calls = threading.Event(), []
+
+    def fake_deploy(rci, pub, key, **kw):
+        calls.append(rci.host)
+        assert gate.wait(10)
+        return HOST_INFO
+
+    monkeypatch.setattr(pi, "deploy_ssh_instance", fake_deploy)
+
+    def as_replica(name, deploys):
+        monkeypatch.setattr(settings, "SERVER_REPLICA_ID", name)
+        monkeypatch.setattr(pi, "_deploys", deploys)
+
+    a, b = {}, {}
+    as_replica("A", a)
+    with session_scope() as s:
+        pi._add_remote(s, s.get(InstanceModel, iid))
+    with session_scope() as s:
+        inst = s.get(InstanceModel, iid)
+        assert inst.deploy_owner == "A" and inst.status == InstanceStatus.PENDING.value
+        inst.last_retry_at = get_current_datetime() - timedelta(minutes=5)  # past the retry gate
+    as_replica("B", b)
+    for _ in range(3):
+        with session_scope() as s:
+            pi._add_remote(s, s.get(InstanceModel, iid))
+    assert calls == ["10.0.0.5"] and not b  # B never started a second deploy
+    gate.set()
+    a[iid].result(timeout=10)
+    with session_scope() as s:  # B sees the finished deploy's instance still leased: hands off
+        pi._add_remote(s, s.get(InstanceModel, iid))
+        assert s.get(InstanceModel, iid).status == InstanceStatus.PENDING.value
+    as_replica("A", a)
+    with session_scope() as s:
+        pi._add_remote(s, s.get(InstanceModel, iid))
+    with session_scope() as s:
+        inst = s.get(InstanceModel, iid)
+        assert inst.status == InstanceStatus.IDLE.value and inst.total_blocks == 1
+        assert inst.deploy_owner is None and inst.deploy_started_at is None
+    assert len(calls) == 1
+    # a replica that died mid-deploy: its lease expires after the deploy deadline, then another
+    # replica re-deploys the host
+    with session_scope() as s:
+        iid2 = _remote_instance_named(s, "10.0.0.6")
+        inst = s.get(InstanceModel, iid2)
+        inst.deploy_owner = "dead-replica"
+        inst.deploy_started_at = get_current_datetime() - pi.DEPLOY_LEASE - timedelta(seconds=1)
+    as_replica("B", b)
+    with session_scope() as s:
+        pi._add_remote(s, s.get(InstanceModel, iid2))
+    b[iid2].result(timeout=10)
+    assert calls == ["10.0.0.5", "10.0.0.6"]
+    with session_scope() as s:
+        pi._add_remote(s, s.get(InstanceModel, iid2))
+        assert s.get(InstanceModel, iid2).status == InstanceStatus.IDLE.value
+
+
+def _remote_instance_named(s, host):
+    from dstack_amd.core.models.instances import SSHKey
+    from dstack_amd.server.services import pools as pools_services
+
+    project = s.query(ProjectModel).filter_by(name="main").one()
+    return pools_services.add_remote(s, project, None, None, None, None, host, 22, "ubuntu",
+                                     [SSHKey(public="ssh-ed25519 AAAA", private="k")]).id
