@@ -163,8 +163,9 @@ def main():
             # fresh-instance p50 (every run on a newly created instance, GPU requested when the
             # host has one); the warm-pool p50 is a separate field
             out["cold_start_p50_s"] = cold.get("cold_start_p50_s")
-            out["cold_start"] = {k: cold.get(k) for k in ("cold_running_p50_s", "warm_start_p50_s", "gpu_requested",
-                                                          "fresh_runs", "fresh_ok", "fresh_distinct_instances",
+            out["cold_start"] = {k: cold.get(k) for k in ("cold_running_p50_s", "stages_p50_s", "warm_start_p50_s",
+                                                          "gpu_requested", "fresh_agent_per_instance", "fresh_runs",
+                                                          "fresh_ok", "fresh_distinct_instances",
                                                           "warm_runs", "warm_ok", "excludes", "error")
                                  if cold.get(k) is not None}
         print(json.dumps(out), flush=True)

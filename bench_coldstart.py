@@ -9,9 +9,12 @@ timestamps:
 
 Two series, reported separately:
 
-* **fresh** (``cold_start_p50_s``): every run lands on a NEW instance -- the previous run's fleet is
-  deleted and its instance terminated first, so each run goes through offer selection, instance
-  creation, shim registration, GPU grant and runner start.  With a GPU on the host (``--gpu auto``)
+* **fresh** (``cold_start_p50_s``): every run lands on a NEW instance with its OWN freshly started
+  agent -- the previous run's fleet is deleted, its instance terminated and its shim stopped first
+  (local backend in per-instance-agent mode, ``DSTACK_LOCAL_SHIM_PER_INSTANCE=1``), so each run goes
+  through offer selection, instance creation, agent start (``dstack-shim --host-info``, process
+  start, first healthcheck), GPU grant, runner start and the job's first output.  ``stages_p50_s``
+  splits it: offer + instance record, agent start, task/runner start, user command to first log.  With a GPU on the host (``--gpu auto``)
   the task requests ``MI355X:1``, so the xGMI-aware pick, ``HIP_VISIBLE_DEVICES`` and the runner's
   GPU env are in the measured path.
 * **warm** (``warm_start_p50_s``): runs that reuse the idle instance of the previous run (the
@@ -50,7 +53,15 @@ def _sample(run, t0):
     sub = run.model.jobs[0].job_submissions[-1]
     t = sub.timings or {}
     base = t.get("submitted", t0)
+    agent = {}
+    if sub.job_provisioning_data and sub.job_provisioning_data.backend_data:
+        try:
+            agent = json.loads(sub.job_provisioning_data.backend_data).get("agent") or {}
+        except ValueError:
+            agent = {}
     return {
+        "agent": agent,
+        "submit_to_container_running": _d(t, "container_running", base),
         "status": sub.status.value,
         "termination_reason": sub.termination_reason.value if sub.termination_reason else None,
         "message": sub.termination_reason_message,
@@ -86,7 +97,8 @@ def measure_cold_start(runs: int = 5, warm_runs: int = 4, timeout: float = 120.0
 
     use_gpu = _host_has_gpu() if gpu == "auto" else gpu == "yes"
     fresh, warm, errors = [], [], []
-    with ServerProcess() as srv:
+    # one agent per instance: a fresh instance's agent start is inside its job's cold start
+    with ServerProcess(env={"DSTACK_LOCAL_SHIM_PER_INSTANCE": "1"}) as srv:
         client = srv.client()
         for i in range(runs + warm_runs):
             is_fresh = i < runs
@@ -107,14 +119,33 @@ def measure_cold_start(runs: int = 5, warm_runs: int = 4, timeout: float = 120.0
     ok_w = [s for s in warm if s["submit_to_first_log"] is not None]
     med = (lambda xs, k: round(statistics.median([x[k] for x in xs]), 4) if xs else None)
     distinct = len({s["instance"] for s in fresh if s["instance"]})
+
+    def p50(xs):
+        xs = [x for x in xs if x is not None]
+        return round(statistics.median(xs), 4) if xs else None
+
+    agent_s = [s["agent"].get("agent_start_s") for s in ok_f]
+    stages = {
+        "offer_and_instance_s": p50([s["submit_to_provisioned"] - s["agent"].get("agent_start_s", 0.0)
+                                     for s in ok_f if s["submit_to_provisioned"] is not None]),
+        "agent_start_s": p50(agent_s),
+        "agent_host_info_s": p50([s["agent"].get("host_info_s") for s in ok_f]),
+        "task_and_runner_start_s": p50([s["submit_to_running"] - s["submit_to_provisioned"] for s in ok_f
+                                        if s["submit_to_running"] is not None and s["submit_to_provisioned"] is not None]),
+        "command_to_first_log_s": p50([s["submit_to_first_log"] - s["submit_to_running"] for s in ok_f
+                                       if s["submit_to_running"] is not None]),
+    }
     return {
         "cold_start_p50_s": med(ok_f, "submit_to_first_log"),
+        "stages_p50_s": stages,
+        "fresh_agent_per_instance": all(s["agent"] for s in ok_f) and bool(ok_f),
         "cold_running_p50_s": med(ok_f, "submit_to_running"),
         "warm_start_p50_s": med(ok_w, "submit_to_first_log"),
         "gpu_requested": "MI355X:1" if use_gpu else None,
         "fresh_runs": len(fresh), "fresh_ok": len(ok_f), "fresh_distinct_instances": distinct,
         "warm_runs": len(warm), "warm_ok": len(ok_w),
-        "excludes": "VM boot, image pull, container start (local backend, process driver)",
+        "excludes": "VM boot, image pull, container start (local backend, process driver; the agent start "
+                    "of every fresh instance is included)",
         "errors": errors[:5], "fresh": fresh, "warm": warm,
     }
 

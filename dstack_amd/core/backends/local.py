@@ -14,7 +14,7 @@ import os
 import subprocess
 import threading
 import time
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import httpx
 
@@ -36,16 +36,23 @@ from dstack_amd import native_bin
 
 
 class LocalShim:
-    """The single shim process owned by the server for the local backend."""
+    """The single shim process owned by the server for the local backend -- or, with
+    ``DSTACK_LOCAL_SHIM_PER_INSTANCE=1``, one shim per local instance, started by
+    ``create_instance`` and stopped by ``terminate_instance`` like a VM's agent, so a fresh
+    instance's agent start (``--host-info``, process start, first healthcheck) is in the job's
+    cold start (``bench_coldstart.py``).  Per-instance shims do not arbitrate GPUs between each
+    other: the mode is for sequential cold-start measurement, the shared shim for everything else."""
 
     _instance: Optional["LocalShim"] = None
     _lock = threading.Lock()
+    _per_instance: Dict[str, "LocalShim"] = {}
 
     def __init__(self, home: str):
         self.home = home
         self.proc: Optional[subprocess.Popen] = None
         self.port: Optional[int] = None
         self.host_info: dict = {}
+        self.timings: Dict[str, float] = {}  # agent start stages (s) of the last start
 
     @classmethod
     def get(cls) -> "LocalShim":
@@ -67,7 +74,9 @@ class LocalShim:
             if not shim or not runner:
                 raise ComputeError("native agents are not built (make -C native)")
             os.makedirs(self.home, exist_ok=True)
+            t0 = time.perf_counter()
             info = subprocess.run([shim, "--host-info"], capture_output=True, text=True, timeout=60)
+            t_info = time.perf_counter()
             try:
                 self.host_info = json.loads(info.stdout.strip().splitlines()[-1])
             except (ValueError, IndexError):
@@ -83,12 +92,16 @@ class LocalShim:
             if not line.startswith("DSTACK_SHIM_PORT="):
                 raise ComputeError(f"local shim failed to start: {line!r}")
             self.port = int(line.strip().split("=", 1)[1])
+            t_port = time.perf_counter()
             for _ in range(200):
                 try:
                     if httpx.get(f"http://127.0.0.1:{self.port}/api/healthcheck", timeout=1).status_code == 200:
                         break
                 except httpx.HTTPError:
                     time.sleep(0.01)
+            t_ok = time.perf_counter()
+            self.timings = {"host_info_s": round(t_info - t0, 4), "process_start_s": round(t_port - t_info, 4),
+                            "first_healthcheck_s": round(t_ok - t_port, 4), "agent_start_s": round(t_ok - t0, 4)}
 
     def stop(self):
         if self.proc and self.proc.poll() is None:
@@ -143,16 +156,28 @@ class LocalCompute(Compute):
 
     def create_instance(self, instance_offer: InstanceOfferWithAvailability,
                         instance_config: InstanceConfiguration) -> JobProvisioningData:
-        shim = LocalShim.get()
+        instance_id = f"local-{instance_config.instance_name}"
+        data: dict = {}
+        if os.environ.get("DSTACK_LOCAL_SHIM_PER_INSTANCE") == "1":
+            from dstack_amd.server import settings
+
+            shim = LocalShim(str(settings.SERVER_DIR_PATH / "local-shims" / instance_config.instance_name))
+            shim.ensure_started()  # the agent start of a fresh instance
+            LocalShim._per_instance[instance_id] = shim
+            data = {"per_instance_shim": True, "agent": shim.timings}
+        else:
+            shim = LocalShim.get()
         return JobProvisioningData(
             backend=BackendType.LOCAL, instance_type=instance_offer.instance,
-            instance_id=f"local-{instance_config.instance_name}", hostname="127.0.0.1", internal_ip="127.0.0.1",
+            instance_id=instance_id, hostname="127.0.0.1", internal_ip="127.0.0.1",
             region="local", price=0.0, username=os.environ.get("USER", "root"), ssh_port=None, dockerized=True,
-            backend_data=json.dumps({"shim_port": shim.port}),
+            backend_data=json.dumps({"shim_port": shim.port, **data}),
         )
 
     def terminate_instance(self, instance_id: str, region: str, backend_data: Optional[str] = None) -> None:
-        return None  # the local host is never torn down
+        shim = LocalShim._per_instance.pop(instance_id, None)
+        if shim is not None:
+            shim.stop()  # a per-instance agent goes with its instance; the shared one stays
 
     # instance volumes only: a "volume" is a directory under the server dir
     def create_volume(self, volume: Volume) -> VolumeProvisioningData:

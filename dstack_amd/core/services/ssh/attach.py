@@ -112,6 +112,7 @@ class RunAttach:
         self.ports: Dict[int, int] = {}
         self._relays: List[_Relay] = []
         self._proc: Optional[subprocess.Popen] = None
+        self._master = False  # a forwarding master (foreground or ControlPersist'ed) is up
 
     def _remote(self, p: int) -> int:
         if self.jrd is not None and self.jrd.ports:
@@ -144,9 +145,35 @@ class RunAttach:
         for remote, local in mapping.items():
             cmd += ["-L", f"{self.bind}:{local}:localhost:{self._remote(remote)}"]
         cmd.append(self.run_name)
-        self._proc = subprocess.Popen(cmd, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL,
-                                      stderr=subprocess.PIPE)
+        self._proc = self._connect(cmd)
+        self._master = True
         self.ports = mapping
+
+    def _connect(self, cmd: List[str]) -> Optional[subprocess.Popen]:
+        """Start the forwarding master, retrying while the container's sshd is not up yet: the
+        container bootstrap execs the runner first and brings sshd up in the background (possibly
+        after installing it), so the first attach of a fresh job can find the port closed.  With
+        ``ControlPersist`` the client backgrounds the master and exits 0 once connected; a refused
+        or reset connection exits 255 and is retried with backoff until ``DSTACK_ATTACH_TIMEOUT``
+        (default 180 s)."""
+        import os
+        import time
+
+        deadline = time.monotonic() + float(os.getenv("DSTACK_ATTACH_TIMEOUT", 180))
+        delay = 0.5
+        while True:
+            proc = subprocess.Popen(cmd, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+            try:
+                rc = proc.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                return proc  # connected and holding the forwards in the foreground
+            err = (proc.stderr.read() if proc.stderr else b"").decode(errors="replace").strip()
+            if rc == 0:
+                return None  # the persistent master runs in the background
+            if time.monotonic() + delay > deadline:
+                raise SSHError(f"cannot attach to {self.run_name}: ssh exited {rc}: {err[-500:]}")
+            time.sleep(delay)
+            delay = min(delay * 2, 5.0)
 
     def close(self):
         for r in self._relays:
@@ -159,5 +186,10 @@ class RunAttach:
             except subprocess.TimeoutExpired:
                 self._proc.kill()
             self._proc = None
+        if self._master:
+            ctl = ssh_config_path().parent / f"{self.run_name}.control.sock"
+            subprocess.run(["ssh", "-o", f"ControlPath={ctl}", "-O", "exit", self.run_name], capture_output=True,
+                           timeout=10)
+            self._master = False
             update_ssh_config(self.run_name, None)
             update_ssh_config(f"{self.run_name}-host", None)

@@ -491,6 +491,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
   const bf16_t* dop = dout + (long)b * S * ors + hh * HD;
   const float* lp = lse + ((long)b * H + hh) * S;
   const float* dp = delta + ((long)b * H + hh) * S;
+  const __amdgpu_buffer_rsrc_t lrs = make_rsrc(lp, (unsigned)S * 4), drs = make_rsrc(dp, (unsigned)S * 4);
   const int kb0 = kb * 128, kw0 = kb0 + 32 * g, mykey = kw0 + l32;
   char* kl = smem;
   char* vl = smem + 128 * 256;
@@ -518,8 +519,8 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
       dma_tile64(qp + (long)qt * 64 * rs, rs, st, w4, lane);
     else
       dma_tile64(dop + (long)qt * 64 * ors, ors, st + TILE_BYTES, w4, lane);
-    if (w == 0) dma_f32x64(lp + qt * 64, st + 2 * TILE_BYTES, lane);
-    if (w == 4) dma_f32x64(dp + qt * 64, st + 2 * TILE_BYTES + 256, lane);
+    if (w == 0) dma_f32x64_buf(lrs, qt * 64, st + 2 * TILE_BYTES, lane);
+    if (w == 4) dma_f32x64_buf(drs, qt * 64, st + 2 * TILE_BYTES + 256, lane);
   };
   issue(qt_begin, ring);
   wait_dma_and_barrier();
@@ -556,21 +557,30 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
         dpv = mfma(lds_row(dol, 32 * qh + l32, 2 * ks + hf), lds_row(vl, 32 * g + l32, 2 * ks + hf), dpv);
       }
       const bool diag = CAUSAL && qlo < kw0 + 31;
+      // P, then (diagonal tiles only, a wave-uniform branch: 2 of ~64 tiles) the causal mask, then
+      // dS.  Folding the mask into the P loop as a select costs every tile 16 v_cmp + 16 v_cndmask
+      // + 16 s_and; the branch costs the other tiles nothing.
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int qi = 32 * qh + 8 * rr + 4 * hf;
-        f4 L = {0.f, 0.f, 0.f, 0.f}, Dl = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (!SEED) {
-          L = *reinterpret_cast<const f4*>(ll + qi);
-          Dl = *reinterpret_cast<const f4*>(dl + qi);
-        }
+        f4 L = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (!SEED) L = *reinterpret_cast<const f4*>(ll + 32 * qh + 8 * rr + 4 * hf);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          sc[4 * rr + i] = SEED ? fexp2(sc[4 * rr + i] * scale_log2) : fexp2(fmaf(sc[4 * rr + i], scale_log2, -L[i]));
+      }
+      if (__builtin_expect(diag, 0)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (mykey > qt * 64 + 32 * qh + 8 * (r >> 2) + 4 * hf + (r & 3)) sc[r] = 0.f;
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        f4 Dl = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (!SEED) Dl = *reinterpret_cast<const f4*>(dl + 32 * qh + 8 * rr + 4 * hf);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * rr + i;
-          float pv = SEED ? fexp2(sc[r] * scale_log2) : fexp2(fmaf(sc[r], scale_log2, -L[i]));
-          if (diag && mykey > qt * 64 + qi + i) pv = 0.f;
-          sc[r] = pv;
-          dpv[r] = SEED ? pv * dpv[r] : pv * (dpv[r] - Dl[i]);
+          dpv[r] = SEED ? sc[r] * dpv[r] : sc[r] * (dpv[r] - Dl[i]);
         }
       }
       bf16x8 pb[2], dsb[2];

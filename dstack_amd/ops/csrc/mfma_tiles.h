@@ -86,6 +86,22 @@ __device__ __forceinline__ void dma_f32x64(const float* g, char* lds, int lane) 
   __builtin_amdgcn_global_load_lds(GLB1(void, g + lane), LDS3(void, lds), 4, 0, 0);
 }
 
+// Buffer descriptor over `bytes` of a wave-uniform base (readfirstlane'd so the compiler can prove
+// uniformity and keeps it in SGPRs), for LDS-DMA whose per-iteration offset is an SGPR (soffset)
+// and whose per-lane part is one 32-bit voffset: no 64-bit VGPR address pair stays live across a
+// loop (under 256-VGPR pressure such a pair gets spilled, and its reload drains vmcnt).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* p = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// 64 contiguous floats at element `elem0` of the buffer -> LDS (one wave-instruction, 4 B/lane)
+__device__ __forceinline__ void dma_f32x64_buf(__amdgpu_buffer_rsrc_t r, int elem0, char* lds, int lane) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LDS3(void, lds), 4, lane * 4, elem0 * 4, 0, 0);
+}
+
 __device__ __forceinline__ void wait_dma_and_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

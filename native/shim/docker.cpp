@@ -31,18 +31,25 @@ std::string container_bootstrap_script(const ShimOptions& o, const std::vector<s
   std::string quoted;
   for (char c : authorized) quoted += c == '\'' ? std::string("'\\''") : std::string(1, c);
   authorized = quoted;
+  // The runner (the job's critical path) is exec'd at once; sshd -- installed first when the image
+  // lacks it, which can take a minute of package downloads -- comes up in a background subshell.
+  // `dstack attach` retries until it listens (core/services/ssh/attach.py).  The reference installs
+  // and starts sshd synchronously before the runner (runner/internal/shim/docker.go:873-911).
   std::ostringstream s;
   s << "set -e\n"
-    << "export DEBIAN_FRONTEND=noninteractive\n"
-    << "if ! command -v sshd >/dev/null 2>&1; then\n"
-    << "  (apt-get update -qq && apt-get install -y -qq openssh-server) >/dev/null 2>&1 || "
-       "(yum install -y -q openssh-server) >/dev/null 2>&1 || (apk add -q openssh-server) >/dev/null 2>&1 || true\n"
-    << "fi\n"
-    << "mkdir -p ~/.ssh /run/sshd && chmod 700 ~/.ssh\n"
+    << "mkdir -p ~/.ssh && chmod 700 ~/.ssh\n"
     << "printf '%s' '" << authorized << "' >> ~/.ssh/authorized_keys && chmod 600 ~/.ssh/authorized_keys\n"
-    << "if command -v sshd >/dev/null 2>&1; then ssh-keygen -A >/dev/null 2>&1 || true; "
+    << "(\n"
+    << "  export DEBIAN_FRONTEND=noninteractive\n"
+    << "  if ! command -v sshd >/dev/null 2>&1; then\n"
+    << "    (apt-get update -qq && apt-get install -y -qq openssh-server) || (yum install -y -q openssh-server) || "
+       "(apk add -q openssh-server) || true\n"
+    << "  fi\n"
+    << "  mkdir -p /run/sshd\n"
+    << "  if command -v sshd >/dev/null 2>&1; then ssh-keygen -A || true; "
     << "$(command -v sshd) -p " << o.runner_ssh_port
     << " -o PermitUserEnvironment=yes -o PasswordAuthentication=no -o PidFile=none || true; fi\n"
+    << ") </dev/null >/dev/null 2>&1 &\n"
     << "exec /usr/local/bin/dstack-runner --log-level " << (o.runner_log_level >= 0 ? o.runner_log_level : log_level()) << " start --http-port " << o.runner_http_port
     << " --temp-dir /tmp/runner --home-dir \"$HOME\" --working-dir /workflow --ssh-env"
     << (o.probe_binary.empty() ? "" : " --probe /usr/local/bin/dstack-probe") << "\n";

@@ -383,13 +383,66 @@ int main() {
     CHECK(rc == 0);
     std::string keys, calls;
     read_file(home + "/.ssh/authorized_keys", keys);
-    read_file(log, calls);
+    for (int i = 0; i < 100; ++i) {  // sshd starts in the background, after the runner's exec
+      read_file(log, calls);
+      if (calls.find("sshd -p") != std::string::npos) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
     CHECK(keys == "ssh-ed25519 AAAAkey1 alice's laptop\nssh-rsa AAAAkey2\n");
     CHECK(calls.find("ssh-keygen -A") != std::string::npos);
     CHECK(calls.find("sshd -p 10022 -o PermitUserEnvironment=yes -o PasswordAuthentication=no") != std::string::npos);
     CHECK(calls.find("dstack-runner --log-level") != std::string::npos);
     CHECK(calls.find("start --http-port 10999 --temp-dir /tmp/runner --home-dir " + home) != std::string::npos);
     if (rc != 0) fprintf(stderr, "%s\n%s\n", script.c_str(), out.c_str());
+  });
+
+  run("container bootstrap: the runner starts before a missing sshd is installed", [] {
+    // an image without sshd: the stand-in package manager takes 1.5 s and then provides sshd; the
+    // runner must have been exec'd long before that, and sshd must still come up afterwards
+    ShimOptions o;
+    o.runner_ssh_port = 10022;
+    o.runner_http_port = 10999;
+    std::string script = container_bootstrap_script(o, {"ssh-ed25519 AAAAkey1"});
+    char tmpl[] = "/tmp/dsa_boot2_XXXXXX";
+    std::string dir = mkdtemp(tmpl);
+    std::string bin = dir + "/bin", home = dir + "/home", log = dir + "/calls.log";
+    mkdirs(bin);
+    mkdirs(home);
+    auto stamp = [&](const std::string& name) {
+      return "echo \"" + name + " $(date +%s%N)\" >> " + log + "\n";
+    };
+    write_file(bin + "/apt-get",
+               "#!/bin/sh\n" + stamp("apt-get-start") + "[ \"$1\" = update ] && exit 0\nsleep 1.5\n" +
+                   "cat > " + bin + "/sshd <<'EOS'\n#!/bin/sh\n" + stamp("sshd") + "EOS\nchmod +x " + bin + "/sshd\n" +
+                   stamp("apt-get-done"),
+               0755);
+    write_file(bin + "/ssh-keygen", "#!/bin/sh\nexit 0\n", 0755);
+    write_file(bin + "/dstack-runner", "#!/bin/sh\n" + stamp("runner"), 0755);
+    auto replace_all = [](std::string s, const std::string& a, const std::string& b) {
+      for (size_t p = s.find(a); p != std::string::npos; p = s.find(a, p + b.size())) s.replace(p, a.size(), b);
+      return s;
+    };
+    script = replace_all(script, "/usr/local/bin/dstack-runner", bin + "/dstack-runner");
+    script = replace_all(script, "/run/sshd", dir + "/run-sshd");
+    write_file(dir + "/boot.sh", script, 0755);
+    std::string out;
+    int rc = run_capture({"env", "-i", "HOME=" + home, "PATH=" + bin + ":/usr/bin:/bin", "sh", dir + "/boot.sh"}, out);
+    CHECK(rc == 0);
+    std::string calls;
+    for (int i = 0; i < 100; ++i) {  // the background install finishes after the runner
+      read_file(log, calls);
+      if (calls.find("sshd ") != std::string::npos) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    auto at = [&](const std::string& name) {
+      size_t p = calls.find(name + " ");
+      return p == std::string::npos ? -1LL : std::stoll(calls.substr(p + name.size() + 1, 19));
+    };
+    CHECK(at("runner") > 0 && at("apt-get-done") > 0 && at("sshd") > 0);
+    CHECK(at("runner") < at("apt-get-done"));  // the job did not wait for the package install
+    CHECK(at("apt-get-done") - at("runner") > 1000000000LL);
+    CHECK(at("sshd") >= at("apt-get-done"));
+    run_capture({"rm", "-rf", "--", dir}, out);
   });
 
   run("docker restore rebuilds tasks and the GPU lock from labels", [] {

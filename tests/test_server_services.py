@@ -251,3 +251,40 @@ def test_collect_metrics_polls_running_jobs_only(db):
     client.get_metrics.side_effect = AssertionError("finished jobs are not polled")
     with mock.patch.object(process_metrics, "get_runner_client", return_value=client):
         process_metrics.collect_metrics()
+
+
+def test_attach_retries_until_the_container_sshd_is_up(tmp_path, monkeypatch):
+    """The container bootstrap execs the runner first and starts sshd in the background, so the
+    first attach may find the port closed: ssh is retried (exit 255) until it connects (the
+    ControlPersist master exits 0), and gives up with the ssh error after DSTACK_ATTACH_TIMEOUT."""
+    import types
+
+    from dstack_amd.core.errors import SSHError
+    from dstack_amd.core.services.ssh import attach
+
+    monkeypatch.setattr(attach, "ssh_config_path", lambda: tmp_path / "ssh" / "config")
+    bin_dir = tmp_path / "bin"
+    bin_dir.mkdir()
+    count = tmp_path / "count"
+    (bin_dir / "ssh").write_text(
+        "#!/bin/sh\n"
+        f"n=$(cat {count} 2>/dev/null || echo 0); n=$((n + 1)); echo $n > {count}\n"
+        "case \"$*\" in *'-O exit'*) exit 0;; esac\n"
+        "if [ $n -le 2 ]; then echo 'ssh: connect to host 10.0.0.5 port 10022: Connection refused' >&2; exit 255; fi\n"
+        "exit 0\n")
+    (bin_dir / "ssh").chmod(0o755)
+    monkeypatch.setenv("PATH", f"{bin_dir}:/usr/bin:/bin")
+    conf = types.SimpleNamespace(ports=[], type="task")
+    run = types.SimpleNamespace(run_spec=types.SimpleNamespace(run_name="r1", configuration=conf))
+    jpd = types.SimpleNamespace(backend=types.SimpleNamespace(value="aws"), hostname="10.0.0.5", ssh_port=10022,
+                                username="root")
+    sub = types.SimpleNamespace(job_provisioning_data=jpd, job_runtime_data=None)
+    a = attach.RunAttach(run, sub, identity_file=str(tmp_path / "id"))
+    a.open()
+    assert count.read_text().strip() == "3"  # two refusals, then connected
+    a.close()
+    count.write_text("-100")  # every attempt refused
+    monkeypatch.setenv("DSTACK_ATTACH_TIMEOUT", "1")
+    b = attach.RunAttach(run, sub, identity_file=str(tmp_path / "id"))
+    with pytest.raises(SSHError, match="Connection refused"):
+        b.open()
