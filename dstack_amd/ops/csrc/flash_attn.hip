@@ -913,17 +913,24 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(con
         }
       }
       const bool diag = CAUSAL && kv0 + 63 > qw0;
+      // P, the causal mask on diagonal tiles only (a wave-uniform branch, not a per-element select
+      // in every tile: 32 v_cmp + 32 v_cndmask + 31 s_and + the key arithmetic per tile), then dS
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float p = fexp2(fmaf(st[t][r], scale_log2, -L));
-          if (diag) {
-            const int key = kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hf;
-            if (key > myq) p = 0.f;
-          }
-          dpt[t][r] = NW == 8 ? p * dpt[t][r] : p * (dpt[t][r] - Dl);
-        }
+        for (int r = 0; r < 16; ++r) st[t][r] = fexp2(fmaf(st[t][r], scale_log2, -L));
+      if (__builtin_expect(diag, 0)) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hf > myq) st[t][r] = 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          dpt[t][r] = NW == 8 ? st[t][r] * dpt[t][r] : st[t][r] * (dpt[t][r] - Dl);
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const bf16x8 a = to_bf16x8(dpt[s4 >> 1], 8 * (s4 & 1));

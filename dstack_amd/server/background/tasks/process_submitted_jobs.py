@@ -125,11 +125,7 @@ def _master_job(run: RunModel, job: JobModel) -> Optional[JobModel]:
 
 
 def _has_required_instance_mounts(spec) -> bool:
-    """Non-optional instance mounts need a VM backend (a host path to bind); optional ones do not
-    restrict the offers (reference: ``check_run_spec_has_instance_mounts``)."""
-    from dstack_amd.core.models.volumes import InstanceMountPoint
-
-    return any(isinstance(mp, InstanceMountPoint) and not mp.optional for mp in spec.mount_points())
+    return jobs_services.has_required_instance_mounts(spec)
 
 
 def _fleet_can_grow(fleet: FleetModel) -> bool:

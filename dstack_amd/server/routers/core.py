@@ -134,7 +134,7 @@ def list_backend_types() -> List[str]:
 
 
 @backends_router.post("/config_values")
-def backend_config_values(body: dict) -> dict:
+def backend_config_values(body: dict, user: UserModel = Depends(authenticated)) -> dict:
     """Choices for a backend form (reference ``/api/backends/config_values``): the regions the
     catalog knows for the type, with the requested ones (or all) selected; credentials are
     validated when the backend is created."""

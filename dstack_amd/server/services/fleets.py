@@ -287,10 +287,16 @@ def create_instance(s: Session, project: ProjectModel, user: UserModel, profile:
     """Legacy ``runs/create_instance`` (reference: ``S/services/fleets.py`` create_instance): one
     PENDING cloud instance in an auto-created fleet; the instance reconciler provisions it from
     the offers matching ``requirements``."""
+    from dstack_amd.core.models.backends import BACKENDS_WITH_CREATE_INSTANCE_SUPPORT
+
     offers = offers_services.get_offers_by_requirements(s, project, profile, requirements,
                                                         exclude_not_available=True)
+    offers = [(c, o) for c, o in offers
+              if o.backend in BACKENDS_WITH_CREATE_INSTANCE_SUPPORT and o.backend != BackendType.REMOTE]
     if not offers:
-        raise ServerClientError("No offers found for the requirements")
+        raise ServerClientError("Backends do not support create_instance or have no offers for the requirements. "
+                                "Try to select other backends.")
+    best = offers[0][1]
     pool = pools_services.get_or_create_pool_by_name(s, project, profile.pool_name)
     name = f"{profile.name or 'instance'}-{uuid.uuid4().hex[:6]}"
     fleet = create_autocreated_fleet(s, project, name, profile, multinode=False)
@@ -299,6 +305,8 @@ def create_instance(s: Session, project: ProjectModel, user: UserModel, profile:
         profile=profile.model_dump_json(), requirements=requirements.model_dump_json(),
         termination_idle_time=DEFAULT_FLEET_TERMINATION_IDLE_TIME, termination_policy="destroy-after-idle",
         backend_data=json.dumps({"blocks": 1, "placement": None}),
+        # the best offer now; the reconciler provisions from the current offers in the same order
+        backend=best.backend.value, region=best.region, price=best.price, offer=best.model_dump_json(),
     )
     s.flush()
     scheduler.wake(scheduler.INSTANCES)

@@ -151,3 +151,11 @@ def new_job_model(run: RunModel, spec: JobSpec, submission_num: int = 0) -> JobM
     )
     j.timings = json.dumps({"submitted": now.timestamp()})
     return j
+
+
+def has_required_instance_mounts(spec) -> bool:
+    """Non-optional instance mounts need a VM backend (a host path to bind); optional ones do not
+    restrict the offers (reference: ``check_run_spec_has_instance_mounts``)."""
+    from dstack_amd.core.models.volumes import InstanceMountPoint
+
+    return any(isinstance(mp, InstanceMountPoint) and not mp.optional for mp in spec.mount_points())

@@ -114,10 +114,17 @@ def get_member_role(project: ProjectModel, user: UserModel) -> Optional[ProjectR
 
 
 def delete_projects(s: Session, actor: UserModel, names: List[str]):
-    for name in names:
-        p = get_project_or_error(s, name)
-        if actor.global_role != GlobalRole.ADMIN.value and get_member_role(p, actor) != ProjectRole.ADMIN:
-            raise ForbiddenError()
+    """Project admins delete their projects, global admins any; a regular user cannot delete every
+    project they belong to (reference ``services/projects.py:delete_projects``)."""
+    projects = [get_project_or_error(s, name) for name in names]
+    if actor.global_role != GlobalRole.ADMIN.value:
+        for p in projects:
+            if get_member_role(p, actor) != ProjectRole.ADMIN:
+                raise ForbiddenError()
+        own = {p.id for p in list_user_projects(s, actor)}
+        if own and own <= {p.id for p in projects}:
+            raise ServerClientError("Cannot delete the only project")
+    for p in projects:
         p.deleted = True
         p.name = f"_deleted_{p.id.hex[:8]}_{p.name}"[:50]
 

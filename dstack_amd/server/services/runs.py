@@ -169,6 +169,7 @@ def get_plan(s: Session, project: ProjectModel, user: UserModel, run_spec: RunSp
         if profile.creation_policy != CreationPolicy.REUSE:
             backend_offers = offers_services.get_offers_by_requirements(
                 s, project, profile, spec.requirements, multinode=multinode, privileged=spec.privileged,
+                instance_mounts=jobs_services.has_required_instance_mounts(spec),
             )
             offers += [o for _, o in backend_offers]
         job_plans.append(JobPlan(job_spec=spec, offers=offers[:max_offers], total_offers=len(offers),
@@ -194,8 +195,13 @@ def submit_run(s: Session, project: ProjectModel, user: UserModel, run_spec: Run
                 if not RunStatus(existing.status).is_finished():
                     raise ServerClientError(f"Run {run_spec.run_name} is already active")
                 existing.deleted = True
-        repo = (repos_services.get_repo(s, project, run_spec.repo_id) if run_spec.repo_id else None) or \
-            repos_services.get_or_create_virtual_repo(s, project, run_spec.repo_id or "none")
+        repo = repos_services.get_repo(s, project, run_spec.repo_id) if run_spec.repo_id else None
+        if repo is None:
+            # a virtual repo has no code to upload, so it needs no ``repos/init``; a remote or local
+            # one must have been initialised (reference: RepoDoesNotExistError)
+            if run_spec.repo_id and getattr(run_spec.repo_data, "repo_type", "virtual") != "virtual":
+                raise ServerClientError(f"Repo {run_spec.repo_id} does not exist")
+            repo = repos_services.get_or_create_virtual_repo(s, project, run_spec.repo_id or "none")
         now = get_current_datetime()
         conf = run_spec.configuration
         replicas = conf.replicas.min if isinstance(conf, ServiceConfiguration) else 1

@@ -71,7 +71,7 @@ def register_service(s: Session, run: RunModel):
         url = f"/proxy/services/{project.name}/{run.run_name}/"
         model = None
         if conf.model is not None:
-            model = ServiceModelSpec(name=conf.model.name, base_url=f"/proxy/models/{project.name}",
+            model = ServiceModelSpec(name=conf.model.name, base_url=f"/proxy/models/{project.name}/",
                                      type=conf.model.type)
         svc = ServiceSpec(url=url, model=model)
     run.service_spec = svc.model_dump_json()

@@ -96,7 +96,7 @@ def test_service_url_and_model_and_offers(dc):
     run = dc.runs.submit(svc, VirtualRepo())
     assert run.service_url == "http://testserver/proxy/services/main/api-svc/"
     m = run.service_model
-    assert m.name == "llama" and m.url == "http://testserver/proxy/models/main"
+    assert m.name == "llama" and m.url == "http://testserver/proxy/models/main/"
     task = dc.runs.submit(Task(commands=["true"], name="api-task"), VirtualRepo())
     with pytest.raises(ValueError):
         task.service_model

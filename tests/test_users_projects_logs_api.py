@@ -70,6 +70,7 @@ def test_project_quota_for_regular_users(client, monkeypatch):
 def test_project_creator_is_admin_and_can_delete(client):
     h = _user(client, "owner")
     client.post("/api/projects/create", json={"project_name": "mine"}, headers=h)
+    client.post("/api/projects/create", json={"project_name": "spare"}, headers=h)  # not the only one
     got = client.post("/api/projects/mine/get", headers=h).json()
     assert [(m["user"]["username"], m["project_role"]) for m in got["members"]] == [("owner", "admin")]
     other = _user(client, "other")

@@ -12,8 +12,8 @@ for i in 1 2 3; do
   (cd $R && timeout -k 10 200 python tools/bench_attn.py) > $O/new_$i.json 2>>$O/ab.err || exit 1
 done
 cd /tmp && export TMPDIR=/tmp
-(cd $R/.ab_old && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/prof_old -o k -- python3 tools/bench_attn.py) > $O/prof_old.log 2>&1 || exit 1
-(cd $R && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/prof_new -o k -- python3 tools/bench_attn.py) > $O/prof_new.log 2>&1 || exit 1
+(cd $R/.ab_old && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/prof_old -o k -- python3 tools/bench_attn.py) > $R/$O/prof_old.log 2>&1 || exit 1
+(cd $R && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/prof_new -o k -- python3 tools/bench_attn.py) > $R/$O/prof_new.log 2>&1 || exit 1
 cd $R
 for f in $O/*.json; do echo "$f $(cat $f)"; done
 for v in old new; do echo "== $v"; find $O/prof_$v -name "*kernel_stats.csv" -exec grep fa_ {} \; | cut -d, -f1-4; done
