@@ -246,6 +246,17 @@ async def upload_code(request: Request, repo_id: str, up: UP = Depends(project_m
     from dstack_amd.server.db import session_scope
 
     blob = await request.body()
+    ctype = request.headers.get("content-type", "")
+    if ctype.startswith("multipart/form-data"):
+        # the reference client posts the tarball as the multipart field "file"
+        from email.parser import BytesParser
+        from email.policy import HTTP
+
+        msg = BytesParser(policy=HTTP).parsebytes(b"Content-Type: " + ctype.encode() + b"\r\n\r\n" + blob)
+        parts = [p for p in msg.iter_parts() if p.get_param("name", header="content-disposition") == "file"]
+        if not parts:
+            raise ServerClientError("multipart upload without a 'file' field")
+        blob = parts[0].get_payload(decode=True) or b""
     if len(blob) > 64 * 2**20:
         raise ServerClientError("Code blob exceeds 64 MiB; use a remote repo or .dstackignore")
     blob_hash = hashlib.sha256(blob).hexdigest()

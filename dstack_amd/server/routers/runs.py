@@ -16,7 +16,7 @@ from dstack_amd.core.models.runs import Run, RunPlan
 from dstack_amd.core.models.volumes import Volume, VolumePlan, VolumeSpec
 from dstack_amd.server import schemas
 from dstack_amd.server.deps import get_session
-from dstack_amd.server.models import ProjectModel, UserModel
+from dstack_amd.server.models import FleetModel, ProjectModel, UserModel
 from dstack_amd.server.security.permissions import authenticated, project_admin, project_manager, project_member
 from dstack_amd.server.services import fleets as fleets_services
 from dstack_amd.server.services import gateways as gateways_services
@@ -129,7 +129,11 @@ def list_fleets(up: UP = Depends(project_member), s: Session = Depends(get_sessi
 
 @fleets_router.post("/get")
 def get_fleet(body: schemas.GetFleetRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")) -> Fleet:
-    f = fleets_services.get_fleet_by_name(s, up[1], body.name) if body.name else None
+    if body.id is not None:  # by id: deleted fleets too (reference routers/fleets.py get)
+        f = s.get(FleetModel, body.id)
+        f = f if f is not None and f.project_id == up[1].id else None
+    else:
+        f = fleets_services.get_fleet_by_name(s, up[1], body.name) if body.name else None
     if f is None:
         raise ResourceNotExistsError("Fleet not found")
     return fleets_services.fleet_model_to_fleet(f)
@@ -165,20 +169,31 @@ def delete_fleet_instances(body: schemas.DeleteFleetInstancesRequest, up: UP = D
 @instances_root.post("/list")
 def list_instances(body: Optional[schemas.ListInstancesRequest] = None, user: UserModel = Depends(authenticated),
                    s: Session = Depends(get_session, scope="function")) -> List[Instance]:
-    out = []
+    body = body or schemas.ListInstancesRequest()
+    rows = []
     for p in projects_services.list_user_projects(s, user):
-        if body and body.project_names and p.name not in body.project_names:
+        if body.project_names and p.name not in body.project_names:
             continue
-        for inst in pools_services.list_project_instances(s, p, include_terminated=not (body and body.only_active)):
-            if body and body.fleet_ids and inst.fleet_id not in body.fleet_ids:
+        if body.project_name and p.name != body.project_name:
+            continue
+        for inst in pools_services.list_project_instances(s, p, include_terminated=not body.only_active):
+            if body.fleet_ids and inst.fleet_id not in body.fleet_ids:
                 continue
-            out.append(pools_services.instance_model_to_instance(inst))
-    return out[: (body.limit if body else 1000)]
+            if body.pool_name and (inst.pool is None or inst.pool.name != body.pool_name):
+                continue
+            rows.append(inst)
+    # keyset pagination (reference routers/instances.py): order by (created_at, id), newest first
+    rows.sort(key=lambda i: (i.created_at, str(i.id)), reverse=not body.ascending)
+    if body.prev_created_at is not None:
+        key = (body.prev_created_at.replace(tzinfo=None), str(body.prev_id or ""))
+        rows = [i for i in rows if ((i.created_at, str(i.id)) > key if body.ascending else (i.created_at, str(i.id)) < key)]
+    return [pools_services.instance_model_to_instance(i) for i in rows[: body.limit]]
 
 
 @pools_root.post("/list_instances")
-def pools_list_instances(user: UserModel = Depends(authenticated), s: Session = Depends(get_session, scope="function")) -> List[Instance]:
-    return list_instances(None, user, s)
+def pools_list_instances(body: Optional[schemas.ListInstancesRequest] = None, user: UserModel = Depends(authenticated),
+                         s: Session = Depends(get_session, scope="function")) -> List[Instance]:
+    return list_instances(body, user, s)
 
 
 @pool_router.post("/list")

@@ -104,7 +104,13 @@ class ListFleetsRequest(_Req):
 class ListInstancesRequest(_Req):
     project_names: Optional[List[str]] = None
     fleet_ids: Optional[List[UUID]] = None
+    pool_name: Optional[str] = None
+    project_name: Optional[str] = None
     only_active: bool = False
+    # keyset pagination over (created, id), newest first unless ascending
+    prev_created_at: Optional[datetime] = None
+    prev_id: Optional[UUID] = None
+    ascending: bool = False
     limit: int = 1000
 
 
