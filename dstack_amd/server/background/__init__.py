@@ -31,11 +31,16 @@ logger = logging.getLogger(__name__)
 
 
 def process_submitted_gateways() -> bool:
-    from dstack_amd.server.services.gateways import provision_gateway
+    """SUBMITTED gateways get their compute (``provision_gateway``); PROVISIONING ones are connected
+    (``connect_gateway``: RUNNING once the control API answers, FAILED after the deadline)."""
+    from dstack_amd.server.services.gateways import connect_gateway, provision_gateway
 
     with session_scope() as s:
         for g in s.execute(select(GatewayModel).where(GatewayModel.status == GatewayStatus.SUBMITTED.value)).scalars():
             provision_gateway(s, g)
+    with session_scope() as s:
+        for g in s.execute(select(GatewayModel).where(GatewayModel.status == GatewayStatus.PROVISIONING.value)).scalars():
+            connect_gateway(s, g)
     return False
 
 

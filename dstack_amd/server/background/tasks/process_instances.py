@@ -393,8 +393,18 @@ def _check_instance(s: Session, inst: InstanceModel):
                 scheduler.wake(scheduler.INSTANCES)
 
 
+TERMINATION_RETRY_INTERVAL = timedelta(minutes=1)
+TERMINATION_RETRY_MAX = timedelta(minutes=15)
+
+
 def _terminate(s: Session, inst: InstanceModel):
+    """Terminate the cloud instance; a failed call is retried at most once a minute and given up
+    (the instance is marked terminated) 15 minutes after the first failure (reference
+    process_instances ``_terminate``)."""
     jpd = pools_services.instance_jpd(inst)
+    if inst.last_termination_retry_at is not None and \
+            get_current_datetime() - inst.last_termination_retry_at < TERMINATION_RETRY_INTERVAL:
+        return  # too early to retry
     if jpd is not None and jpd.backend not in (BackendType.REMOTE, BackendType.LOCAL):
         try:
             compute = backends_services.get_project_backend(s, inst.project, jpd.backend)
@@ -403,7 +413,7 @@ def _terminate(s: Session, inst: InstanceModel):
             now = get_current_datetime()
             inst.first_termination_retry_at = inst.first_termination_retry_at or now
             inst.last_termination_retry_at = now
-            if now - inst.first_termination_retry_at < timedelta(minutes=15):
+            if now - inst.first_termination_retry_at < TERMINATION_RETRY_MAX:
                 logger.warning("instance %s: terminate failed (will retry): %s", inst.name, e)
                 return
     inst.status = InstanceStatus.TERMINATED.value

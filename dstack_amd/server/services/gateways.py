@@ -322,9 +322,37 @@ def gateway_stats(g: GatewayModel) -> dict:
     return _call(g, "GET", "/api/stats/collect")
 
 
+# a cloud gateway VM boots and starts its app within minutes; one that cannot be reached for this
+# long after its creation is marked FAILED (reference process_gateways: "Failed to connect")
+GATEWAY_CONNECT_DEADLINE = 10 * 60
+
+
+def connect_gateway(s: Session, g: GatewayModel) -> None:
+    """PROVISIONING -> RUNNING once the gateway's control API answers (over the SSH tunnel for a
+    cloud gateway), then its config (server URL, ACME) is pushed; FAILED after the deadline."""
+    try:
+        _call(g, "GET", "/api/healthcheck")
+    except Exception as e:  # noqa: BLE001 - unreachable yet: retried on the next pass
+        created = g.created_at.replace(tzinfo=None) if g.created_at else get_current_datetime()
+        age = (get_current_datetime() - created).total_seconds()
+        if age > GATEWAY_CONNECT_DEADLINE:
+            g.status = GatewayStatus.FAILED.value
+            g.status_message = f"Failed to connect to gateway: {e}"[:1000]
+        return
+    from dstack_amd.server import settings
+
+    try:
+        _call(g, "POST", "/api/config", {"server_url": settings.SERVER_URL})
+    except Exception as e:  # noqa: BLE001 - configuration is re-pushed at server start
+        logger.warning("gateway %s: configure failed: %s", g.name, e)
+    g.status = GatewayStatus.RUNNING.value
+    g.status_message = None
+
+
 def provision_gateway(s: Session, g: GatewayModel):
-    """SUBMITTED -> RUNNING.  ``local`` gateways run in-process on the server host; cloud gateways
-    need the backend's ``create_gateway`` (cloud API)."""
+    """SUBMITTED -> PROVISIONING (-> RUNNING in ``connect_gateway``).  ``local`` gateways run
+    in-process on the server host and are RUNNING at once; cloud gateways need the backend's
+    ``create_gateway`` (cloud API)."""
     conf = GatewayConfiguration.model_validate_json(g.configuration)
     if conf.backend == BackendType.LOCAL:
         from dstack_amd.server import settings
