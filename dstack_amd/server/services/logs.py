@@ -115,65 +115,190 @@ class FileLogStorage(LogStorage):
         return JobSubmissionLogs(logs=events, next_token=next_token)
 
 
+class LogStorageError(Exception):
+    """The log backend cannot be used (bad configuration, missing group, API failure)."""
+
+
 class CloudWatchLogStorage(LogStorage):
-    def __init__(self, group: str, region: Optional[str] = None, client=None):
+    """CloudWatch Logs over its JSON API (SigV4, no SDK), one stream per
+    ``{project}/{run}/{job_submission_id}/{runner|job}``.  Follows the service's PutLogEvents limits
+    (reference ``services/logs.py:CloudWatchLogStorage``): a batch holds at most 10,000 events and
+    1 MiB (message bytes + 26 per event) and spans at most 24 h; events more than 14 days old or 2 h
+    in the future are dropped (both bounds shortened by a 10 min clock-drift margin); a stream that
+    vanished (retention) is re-created and the write retried once."""
+
+    EVENT_MAX_COUNT_IN_BATCH = 10000
+    BATCH_MAX_SIZE = 1048576
+    MESSAGE_MAX_SIZE = 262144
+    MESSAGE_OVERHEAD_SIZE = 26
+    BATCH_MAX_SPAN = 24 * 3600 * 1000
+    CLOCK_DRIFT = 10 * 60 * 1000
+    PAST_EVENT_MAX_DELTA = 14 * 24 * 3600 * 1000 - CLOCK_DRIFT
+    FUTURE_EVENT_MAX_DELTA = 2 * 3600 * 1000 - CLOCK_DRIFT
+    MAX_EMPTY_BACKWARD_PAGES = 10
+
+    def __init__(self, group: str, region: Optional[str] = None, client=None, credentials=None):
         import httpx
 
         self.group = group
         self.region = region or os.getenv("DSTACK_SERVER_CLOUDWATCH_LOG_REGION") or os.getenv("AWS_REGION", "us-east-1")
         self.url = f"https://logs.{self.region}.amazonaws.com/"
+        creds = credentials or (os.getenv("AWS_ACCESS_KEY_ID"), os.getenv("AWS_SECRET_ACCESS_KEY"),
+                                os.getenv("AWS_SESSION_TOKEN"))
+        if not creds[0] or not creds[1]:
+            raise LogStorageError("CloudWatch Logs: no AWS credentials (AWS_ACCESS_KEY_ID / AWS_SECRET_ACCESS_KEY)")
+        self._creds = creds
         self.http = client or httpx.Client(timeout=30)
-        self._streams = set()
+        self._streams: set = set()
+        try:
+            self._call("DescribeLogStreams", {"logGroupName": group, "limit": 1})
+        except _CloudWatchError as e:
+            if e.not_found:
+                raise LogStorageError(f"LogGroup '{group}' does not exist") from e
+            raise LogStorageError(f"CloudWatch Logs error: {e}") from e
 
+    # ---- transport ------------------------------------------------------------------------------
     def _call(self, target: str, body: dict) -> dict:
+        import httpx
+
         from dstack_amd.core.backends.clouds.common import sigv4_headers
 
         data = json.dumps(body).encode()
-        h = sigv4_headers("POST", self.url, self.region, "logs", os.getenv("AWS_ACCESS_KEY_ID", ""),
-                          os.getenv("AWS_SECRET_ACCESS_KEY", ""), data, os.getenv("AWS_SESSION_TOKEN"),
-                          extra_headers={"x-amz-target": f"Logs_20140328.{target}",
-                                         "content-type": "application/x-amz-json-1.1"})
-        r = self.http.post(self.url, content=data, headers=h)
-        if r.status_code >= 400 and "ResourceAlreadyExistsException" not in r.text:
-            raise RuntimeError(f"CloudWatch {target}: {r.status_code} {r.text[:300]}")
+        h = sigv4_headers("POST", self.url, self.region, "logs", self._creds[0], self._creds[1], data,
+                          self._creds[2], extra_headers={"x-amz-target": f"Logs_20140328.{target}",
+                                                         "content-type": "application/x-amz-json-1.1"})
+        try:
+            r = self.http.post(self.url, content=data, headers=h)
+        except httpx.HTTPError as e:
+            raise _CloudWatchError(target, "RequestError", str(e)) from e
+        if r.status_code >= 400:
+            try:
+                err = r.json()
+            except ValueError:
+                err = {}
+            code = str(err.get("__type", "")).rsplit("#", 1)[-1] or f"HTTP{r.status_code}"
+            raise _CloudWatchError(target, code, err.get("message") or r.text[:300])
         return r.json() if r.content else {}
 
     @staticmethod
     def _stream(project, run_name, sub_id, kind):
         return f"{project}/{run_name}/{sub_id}/{kind}"
 
+    # ---- streams --------------------------------------------------------------------------------
+    def _ensure_stream(self, name: str, force: bool = False) -> None:
+        if not force and name in self._streams:
+            return
+        d = self._call("DescribeLogStreams", {"logGroupName": self.group, "logStreamNamePrefix": name})
+        if not any(st.get("logStreamName") == name for st in d.get("logStreams", [])):
+            try:
+                self._call("CreateLogStream", {"logGroupName": self.group, "logStreamName": name})
+            except _CloudWatchError as e:
+                if e.code != "ResourceAlreadyExistsException":
+                    raise
+        self._streams.add(name)
+
+    # ---- write ----------------------------------------------------------------------------------
     def write_logs(self, project, run_name, job_submission_id, runner_logs, job_logs):
         for kind, events in (("runner", runner_logs), ("job", job_logs)):
-            if not events:
-                continue
-            stream = self._stream(project, run_name, job_submission_id, kind)
-            if stream not in self._streams:
-                self._call("CreateLogStream", {"logGroupName": self.group, "logStreamName": stream})
-                self._streams.add(stream)
-            # PutLogEvents: chronological, <= 10k events per batch
-            evs = sorted(events, key=lambda e: int(e["timestamp"]))
-            for i in range(0, len(evs), 10000):
-                self._call("PutLogEvents", {"logGroupName": self.group, "logStreamName": stream, "logEvents": [
-                    {"timestamp": int(e["timestamp"]), "message": e["message"]} for e in evs[i:i + 10000]]})
+            if events:
+                self._write(self._stream(project, run_name, job_submission_id, kind), events)
 
+    def _write(self, stream: str, events: List[dict]) -> None:
+        try:
+            self._ensure_stream(stream)
+            try:
+                self._put(stream, events)
+                return
+            except _CloudWatchError as e:
+                if not e.not_found:
+                    raise
+            self._ensure_stream(stream, force=True)  # deleted by retention: our cache was stale
+            self._put(stream, events)
+        except _CloudWatchError as e:
+            raise LogStorageError(f"CloudWatch Logs error: {e}") from e
+
+    def _put(self, stream: str, events: List[dict]) -> None:
+        ordered = sorted(events, key=lambda e: int(e["timestamp"]))  # stable: runner order within a ms
+        for batch in self.batches(ordered):
+            self._call("PutLogEvents", {"logGroupName": self.group, "logStreamName": stream, "logEvents": batch})
+
+    def batches(self, events: List[dict], now_ms: Optional[int] = None):
+        """Chronological events -> PutLogEvents batches within the service limits."""
+        import time
+
+        now = int(time.time() * 1000) if now_ms is None else now_ms
+        batch: List[dict] = []
+        size = 0
+        first = None
+        for e in events:
+            msg = e.get("message") or ""
+            if not msg:
+                continue
+            ts = int(e["timestamp"])
+            if now - ts > self.PAST_EVENT_MAX_DELTA or ts - now > self.FUTURE_EVENT_MAX_DELTA:
+                continue  # CloudWatch rejects the whole request for one such event
+            msize = len(msg.encode()) + self.MESSAGE_OVERHEAD_SIZE
+            if msize > self.MESSAGE_MAX_SIZE:
+                continue
+            if batch and (ts - first > self.BATCH_MAX_SPAN or size + msize > self.BATCH_MAX_SIZE or
+                          len(batch) >= self.EVENT_MAX_COUNT_IN_BATCH):
+                yield batch
+                batch, size, first = [], 0, None
+            if first is None:
+                first = ts
+            batch.append({"timestamp": ts, "message": msg})
+            size += msize
+        if batch:
+            yield batch
+
+    # ---- read -----------------------------------------------------------------------------------
     def poll_logs(self, project, run_name, job_submission_id, start_time=None, end_time=None, descending=False,
                   limit=1000, diagnose=False) -> JobSubmissionLogs:
-        body = {"logGroupName": self.group, "limit": limit, "startFromHead": not descending,
-                "logStreamName": self._stream(project, run_name, job_submission_id, "runner" if diagnose else "job")}
+        stream = self._stream(project, run_name, job_submission_id, "runner" if diagnose else "job")
+        body = {"logGroupName": self.group, "logStreamName": stream, "limit": limit, "startFromHead": not descending}
         if start_time is not None:
+            # start is inclusive in CloudWatch; callers page with the last timestamp they saw
             body["startTime"] = int(_aware(start_time).timestamp() * 1000) + 1
         if end_time is not None:
             body["endTime"] = int(_aware(end_time).timestamp() * 1000)
         try:
-            d = self._call("GetLogEvents", body)
-        except RuntimeError as e:
-            if "ResourceNotFoundException" in str(e):
+            raw = self._get_events(body)
+        except _CloudWatchError as e:
+            if e.not_found:
                 return JobSubmissionLogs(logs=[])
-            raise
+            raise LogStorageError(f"CloudWatch Logs error: {e}") from e
+        if descending:
+            raw = list(reversed(raw))  # CloudWatch returns chronological order either way
         events = [LogEvent(timestamp=datetime.fromtimestamp(e["timestamp"] / 1000, tz=timezone.utc),
-                           message=e["message"]) for e in d.get("events", [])]
-        next_token = events[-1].timestamp.isoformat() if len(events) == limit else None
+                           message=e["message"]) for e in raw]
+        next_token = events[-1].timestamp.isoformat() if events and len(events) == limit else None
         return JobSubmissionLogs(logs=events, next_token=next_token)
+
+    def _get_events(self, body: dict) -> List[dict]:
+        d = self._call("GetLogEvents", body)
+        events = d.get("events", [])
+        if body["startFromHead"] or events:
+            return events
+        # reading backwards, GetLogEvents may return empty pages before the newest events: follow
+        # nextBackwardToken until events appear or the token stops moving (bounded)
+        token = d.get("nextBackwardToken")
+        for _ in range(self.MAX_EMPTY_BACKWARD_PAGES):
+            d = self._call("GetLogEvents", dict(body, nextToken=token))
+            events = d.get("events", [])
+            if events or d.get("nextBackwardToken") == token:
+                return events
+            token = d.get("nextBackwardToken")
+        return []
+
+
+class _CloudWatchError(Exception):
+    def __init__(self, target: str, code: str, message: str):
+        super().__init__(f"{target}: {code}: {message}")
+        self.code = code
+
+    @property
+    def not_found(self) -> bool:
+        return self.code == "ResourceNotFoundException"
 
 
 def _aware(dt: datetime) -> datetime:
