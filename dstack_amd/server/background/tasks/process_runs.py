@@ -17,6 +17,7 @@ from typing import List, Optional, Set, Tuple
 from sqlalchemy import select
 from sqlalchemy.orm import Session
 
+from dstack_amd.core.errors import ServerClientError
 from dstack_amd.core.models.configurations import ServiceConfiguration
 from dstack_amd.core.models.profiles import RetryEvent
 from dstack_amd.core.models.runs import JobStatus, JobTerminationReason, RunSpec, RunStatus, RunTerminationReason
@@ -176,7 +177,10 @@ def _process_active(s: Session, run: RunModel):
                 s.flush()
                 s.refresh(run)
                 run.desired_replica_count = sum(1 for r in replicas_info if r.active) + diff
-                runs_services.scale_run_replicas(s, run, diff)
+                try:
+                    runs_services.scale_run_replicas(s, run, diff)
+                except ServerClientError as e:  # the scaler's view of active replicas lagged ours
+                    logger.warning("run %s: not scaling by %d: %s", run.run_name, diff, e)
     if run.status != new.value:
         logger.info("run %s: %s -> %s", run.run_name, run.status, new.value)
         run.status = new.value

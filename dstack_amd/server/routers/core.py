@@ -10,7 +10,7 @@ from fastapi import APIRouter, Depends, Request
 from sqlalchemy.orm import Session
 
 from dstack_amd import __version__
-from dstack_amd.core.errors import ForbiddenError, ResourceNotExistsError, ServerClientError
+from dstack_amd.core.errors import ForbiddenError, RepoDoesNotExistError, ResourceNotExistsError, ServerClientError
 from dstack_amd.core.models.repos import RepoHead
 from dstack_amd.core.models.users import GlobalRole, Project, ServerInfo, User, UserWithCreds
 from dstack_amd.server import schemas
@@ -219,9 +219,10 @@ def list_repos(up: UP = Depends(project_member), s: Session = Depends(get_sessio
 
 @repos_router.post("/get")
 def get_repo(body: schemas.GetRepoRequest, up: UP = Depends(project_member), s: Session = Depends(get_session, scope="function")):
-    r = repos_services.get_repo_or_error(s, up[1], body.repo_id)
-    creds = repos_services.get_repo_creds(s, r, up[0].id) if body.include_creds else None
-    return repos_services.repo_model_to_head(r, creds)
+    head = repos_services.get_repo_head(s, up[1], up[0], body.repo_id, body.include_creds)
+    if head is None:
+        raise RepoDoesNotExistError()
+    return head
 
 
 @repos_router.post("/init")

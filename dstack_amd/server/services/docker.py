@@ -15,6 +15,7 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import httpx
+from pydantic import BaseModel, ConfigDict, Field, field_validator
 
 from dstack_amd.core.errors import DockerRegistryError
 
@@ -61,6 +62,71 @@ def parse_image_name(image: str) -> ImageRef:
 
 
 MAX_CONFIG_OBJECT_SIZE = 2**22  # 4 MiB, as the reference
+
+
+# -- registry documents (OCI image-spec manifest.md / config.md; Docker v2 schema 2) -----------
+class _Doc(BaseModel):
+    model_config = ConfigDict(extra="ignore", populate_by_name=True)
+
+
+class Descriptor(_Doc):
+    media_type: Optional[str] = Field(None, alias="mediaType")
+    digest: str
+    size: int = 0
+
+
+class ImageManifest(_Doc):
+    schema_version: int = Field(2, alias="schemaVersion")
+    media_type: Optional[str] = Field(None, alias="mediaType")
+    config: Descriptor
+    layers: List[Descriptor] = []
+
+
+class ImageConfigSection(_Doc):
+    user: Optional[str] = Field(None, alias="User")
+    entrypoint: Optional[List[str]] = Field(None, alias="Entrypoint")
+    cmd: Optional[List[str]] = Field(None, alias="Cmd")
+    env: Optional[List[str]] = Field(None, alias="Env")
+    working_dir: Optional[str] = Field(None, alias="WorkingDir")
+
+    @field_validator("user", mode="before")
+    @classmethod
+    def _empty_user(cls, v):
+        return v or None  # "" means "whatever the runtime defaults to", i.e. unset
+
+
+class ImageConfigObject(_Doc):
+    architecture: Optional[str] = None
+    os: Optional[str] = None
+    config: ImageConfigSection = ImageConfigSection()
+
+    @field_validator("config", mode="before")
+    @classmethod
+    def _null_config(cls, v):
+        return {} if v is None else v  # `"config": null` is legal in the spec
+
+
+def parse_image_manifest(obj: dict) -> ImageManifest:
+    try:
+        return ImageManifest.model_validate(obj)
+    except ValueError as e:
+        raise DockerRegistryError(f"malformed image manifest: {e}") from e
+
+
+def parse_image_config_object(obj: dict) -> ImageConfig:
+    try:
+        c = ImageConfigObject.model_validate(obj).config
+    except ValueError as e:
+        raise DockerRegistryError(f"malformed image config: {e}") from e
+    return ImageConfig(user=c.user, entrypoint=c.entrypoint, cmd=c.cmd, env=c.env or [])
+
+
+def is_valid_docker_volume_target(path: str) -> bool:
+    """A container mount target Docker accepts: absolute, no trailing slash (except ``/``), no NUL
+    (reference: ``S/services/docker.py:155-163``)."""
+    if not path.startswith("/") or "\0" in path:
+        return False
+    return path == "/" or not path.endswith("/")
 
 
 class RegistryClient:
@@ -110,17 +176,17 @@ class RegistryClient:
             if r.status_code != 200:
                 raise DockerRegistryError(f"platform manifest: HTTP {r.status_code}", r.status_code)
             m = r.json()
-        r = self._get(f"{base}/blobs/{m['config']['digest']}", {}, auth, state)
+        digest = parse_image_manifest(m).config.digest
+        r = self._get(f"{base}/blobs/{digest}", {}, auth, state)
         if r.status_code != 200:
             raise DockerRegistryError(f"config blob: HTTP {r.status_code}", r.status_code)
         if len(r.content) > MAX_CONFIG_OBJECT_SIZE:
             raise DockerRegistryError(f"image config object exceeds the size limit of {MAX_CONFIG_OBJECT_SIZE} bytes")
         try:
-            c = r.json().get("config") or {}
+            obj = r.json()
         except ValueError as e:
             raise DockerRegistryError(f"malformed image config: {e}") from e
-        cfg = ImageConfig(user=c.get("User") or None, entrypoint=c.get("Entrypoint"), cmd=c.get("Cmd"),
-                          env=c.get("Env") or [])
+        cfg = parse_image_config_object(obj)
         with self._lock:
             self._cache[key] = (time.time(), cfg)
         return cfg

@@ -62,11 +62,35 @@ def _requirements(conf: FleetConfiguration, profile: Profile) -> Requirements:
                         spot=get_policy_map(profile.spot_policy, SpotPolicy.ONDEMAND), reservation=profile.reservation)
 
 
+def check_ssh_hosts_not_yet_added(s: Session, spec: FleetSpec, current_fleet_id=None) -> None:
+    """An SSH host belongs to at most one active fleet, across every project of the server; the
+    fleet being updated (``current_fleet_id``) may keep its own hosts (reference
+    ``_check_ssh_hosts_not_yet_added``)."""
+    sc = spec.configuration.ssh_config
+    if sc is None or not sc.hosts:
+        return
+    existing = set()
+    rows = s.execute(select(InstanceModel).where(InstanceModel.deleted == False,  # noqa: E712
+                                                 InstanceModel.remote_connection_info.isnot(None),
+                                                 InstanceModel.status != InstanceStatus.TERMINATED.value)).scalars()
+    for inst in rows:
+        if current_fleet_id is not None and inst.fleet_id == current_fleet_id:
+            continue
+        existing.add(RemoteConnectionInfo.model_validate_json(inst.remote_connection_info).host)
+    taken = [h if isinstance(h, str) else h.hostname for h in sc.hosts
+             if (h if isinstance(h, str) else h.hostname) in existing]
+    if taken:
+        raise ServerClientError(f"Instances [{', '.join(taken)}] are already assigned to a fleet.")
+
+
 def get_plan(s: Session, project: ProjectModel, user: UserModel, spec: FleetSpec) -> FleetPlan:
     current = None
+    current_id = None
     if spec.configuration.name:
         f = get_fleet_by_name(s, project, spec.configuration.name)
         current = fleet_model_to_fleet(f) if f else None
+        current_id = f.id if f else None
+    check_ssh_hosts_not_yet_added(s, spec, current_id)
     offers = []
     if spec.configuration.ssh_config is None:
         profile = spec.merged_profile
@@ -134,6 +158,7 @@ def create_fleet(s: Session, project: ProjectModel, user: UserModel, spec: Fleet
     _validate_fleet_spec(spec)
     if conf.ssh_config is not None:
         check_can_manage_ssh_fleets(user, project)
+        check_ssh_hosts_not_yet_added(s, spec)
     with db_advisory_lock(s, f"fleet_names_{project.id}"):
         if conf.name is None:
             conf.name = generate_name()

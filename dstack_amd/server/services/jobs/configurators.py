@@ -14,6 +14,7 @@ from __future__ import annotations
 import shlex
 from typing import Dict, List, Optional
 
+from dstack_amd.core.errors import ServerClientError
 from dstack_amd.core.models.configurations import (
     DevEnvironmentConfiguration,
     PortMapping,
@@ -25,7 +26,7 @@ from dstack_amd.core.models.resources import AcceleratorVendor
 from dstack_amd.core.models.runs import AppSpec, JobSpec, Requirements, Retry, RunSpec, get_policy_map
 from dstack_amd.core.models.unix import UnixUser
 from dstack_amd.core.models.volumes import InstanceMountPoint, VolumeMountPoint
-from dstack_amd.utils.interpolator import VariablesInterpolator
+from dstack_amd.utils.interpolator import InterpolatorError, VariablesInterpolator
 
 DEFAULT_MAX_DURATION_DEV = 6 * 3600
 DEFAULT_AMD_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.7.1"
@@ -97,17 +98,22 @@ def _app_specs(conf) -> List[AppSpec]:
 
 
 def interpolate_job_volumes(volumes, job_num: int):
+    """Per-job mount points: ``${{ dstack.job_num }}`` / ``${{ dstack.node_rank }}`` resolved in volume
+    names and paths; volume names always come out as a list of alternatives (reference:
+    ``S/services/jobs/configurators/base.py`` ``interpolate_job_volumes``). A bad pattern is the
+    user's error (``ServerClientError``)."""
     it = VariablesInterpolator({"dstack": {"job_num": str(job_num), "node_rank": str(job_num)}})
     out = []
     for v in volumes:
-        if isinstance(v, VolumeMountPoint):
-            names = v.name if isinstance(v.name, list) else [v.name]
-            names = [it.interpolate(n) for n in names]
-            out.append(VolumeMountPoint(name=names if isinstance(v.name, list) else names[0],
-                                        path=it.interpolate(v.path)))
-        elif isinstance(v, InstanceMountPoint):
-            out.append(InstanceMountPoint(instance_path=it.interpolate(v.instance_path), path=it.interpolate(v.path),
-                                          optional=v.optional))
+        try:
+            if isinstance(v, VolumeMountPoint):
+                names = v.name if isinstance(v.name, list) else [v.name]
+                out.append(VolumeMountPoint(name=[it.interpolate(n) for n in names], path=it.interpolate(v.path)))
+            elif isinstance(v, InstanceMountPoint):
+                out.append(InstanceMountPoint(instance_path=it.interpolate(v.instance_path),
+                                              path=it.interpolate(v.path), optional=v.optional))
+        except InterpolatorError as e:
+            raise ServerClientError(f"Failed to interpolate volume {v}: {e}") from e
     return out
 
 

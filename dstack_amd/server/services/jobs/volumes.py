@@ -90,6 +90,9 @@ def check_can_attach_job_volumes(volumes: Sequence[Sequence[VolumeModel]]):
             seen.add(br)
             if br[0] not in BACKENDS_WITH_VOLUMES_SUPPORT:
                 raise ServerClientError(f"Backend {br[0].value} does not support volumes")
+    names = [v.name for cands in volumes for v in cands]
+    if len(names) != len(set(names)):
+        raise ServerClientError("Cannot attach the same volume at different mount points")
     if len(volumes) > 1:
         common = set.intersection(*({_backend_region(v) for v in cands} for cands in volumes))
         if not common:

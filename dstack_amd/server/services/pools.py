@@ -199,6 +199,24 @@ def pool_model_to_pool(project: ProjectModel, pool: PoolModel):
                 total_instances=len(insts), available_instances=avail)
 
 
+def generate_instance_name(s: Session, project: ProjectModel, pool_name: Optional[str]) -> str:
+    """A random ``adjective-noun`` name not yet used by a live instance of the pool (reference:
+    ``S/services/pools.py`` ``generate_instance_name``)."""
+    from dstack_amd.utils.common import generate_name
+
+    pool = get_or_create_pool_by_name(s, project, pool_name)
+    taken = {i.name for i in _pool_instances(pool)}
+    name = generate_name()
+    for _ in range(64):
+        if name not in taken:
+            return name
+        name = generate_name()
+    n = 1
+    while f"{name}-{n}" in taken:
+        n += 1
+    return f"{name}-{n}"
+
+
 def list_project_pools(s: Session, project: ProjectModel):
     pools = list(s.execute(select(PoolModel).where(PoolModel.project_id == project.id,
                                                    PoolModel.deleted == False)).scalars())  # noqa: E712
@@ -307,8 +325,7 @@ def add_remote(s: Session, project: ProjectModel, pool_name: Optional[str], inst
                 return instance_model_to_instance(inst)
     pool = get_or_create_pool_by_name(s, project, pool_name)
     if instance_name is None:
-        n = sum(1 for _ in _pool_instances(pool))
-        instance_name = f"{pool.name}-{n}"
+        instance_name = generate_instance_name(s, project, pool.name)
     rci = RemoteConnectionInfo(host=host, port=port, ssh_user=ssh_user, ssh_keys=ssh_keys)
     inst = create_instance_model(
         s, project, pool, name=instance_name, status=InstanceStatus.PENDING, backend=BackendType.REMOTE.value,

@@ -49,6 +49,16 @@ def repo_model_to_head(r: RepoModel, creds: Optional[dict] = None) -> RepoHeadWi
     })
 
 
+def get_repo_head(s: Session, project: ProjectModel, user: UserModel, repo_id: str,
+                  include_creds: bool) -> Optional[RepoHeadWithCreds]:
+    """The repo with the credentials the given user would clone it with: their own, else the
+    repo's legacy shared ones, else none (reference: ``S/services/repos.py`` ``get_repo``)."""
+    r = get_repo(s, project, repo_id)
+    if r is None:
+        return None
+    return repo_model_to_head(r, get_repo_creds(s, r, user.id) if include_creds else None)
+
+
 def list_repos(s: Session, project: ProjectModel) -> List[RepoHead]:
     rows = s.execute(select(RepoModel).where(RepoModel.project_id == project.id)).scalars()
     return [RepoHead.model_validate({"repo_id": r.name, "repo_info": json.loads(r.info)}) for r in rows]
@@ -65,14 +75,18 @@ def init_repo(s: Session, project: ProjectModel, user: UserModel, repo_id: str, 
     else:
         r.info = json.dumps(repo_info)
         r.type = repo_info.get("repo_type", r.type)
+    # the caller's own credentials are added, replaced, or -- when a remote repo is initialised
+    # without them -- removed (reference ``init_repo``: creds are per user)
+    c = s.execute(select(RepoCredsModel).where(RepoCredsModel.repo_id == r.id,
+                                               RepoCredsModel.user_id == user.id)).scalar_one_or_none()
     if repo_creds is not None:
         RemoteRepoCreds.model_validate(repo_creds)
-        c = s.execute(select(RepoCredsModel).where(RepoCredsModel.repo_id == r.id,
-                                                   RepoCredsModel.user_id == user.id)).scalar_one_or_none()
         if c is None:
             s.add(RepoCredsModel(id=uuid.uuid4(), repo_id=r.id, user_id=user.id, creds=json.dumps(repo_creds)))
         else:
             c.creds = json.dumps(repo_creds)
+    elif c is not None and r.type == "remote":
+        s.delete(c)
     return r
 
 

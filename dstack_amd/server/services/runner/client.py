@@ -5,7 +5,8 @@ for remote hosts (``core/services/ssh/tunnel.py``)."""
 from __future__ import annotations
 
 import json
-from typing import Any, Dict, List, Optional
+import re
+from typing import Any, Dict, List, Optional, Tuple
 
 import httpx
 
@@ -20,7 +21,9 @@ REQUEST_TIMEOUT = 15.0
 _clients: Dict[str, httpx.Client] = {}
 
 
-def _client(base_url: str) -> httpx.Client:
+def _client(base_url: str, transport: Optional[httpx.BaseTransport] = None) -> httpx.Client:
+    if transport is not None:  # tests: an in-process transport, never pooled
+        return httpx.Client(base_url=base_url, timeout=REQUEST_TIMEOUT, transport=transport)
     c = _clients.get(base_url)
     if c is None:
         c = httpx.Client(base_url=base_url, timeout=REQUEST_TIMEOUT)
@@ -28,10 +31,75 @@ def _client(base_url: str) -> httpx.Client:
     return c
 
 
+# shim HTTP API generations: 1 = tasks API without the GPU health probe endpoints,
+# 2 = + ``/api/gpu_health`` (probe state, off-path re-probe) and preemption ("interrupted")
+SHIM_LATEST_API_VERSION = 2
+# final shim releases older than this speak API 1 (a shim that reports ``api_version`` wins)
+SHIM_API_V2_MIN_VERSION = (0, 1, 0)
+
+_FINAL_VERSION = re.compile(r"^(\d+)\.(\d+)(?:\.(\d+))?(?:\.\d+)*(?:\+[0-9A-Za-z.]+)?$")
+
+
+def parse_version(value: str) -> Optional[Tuple[int, int, int]]:
+    """``major.minor[.patch[.more]][+local]`` -> ``(major, minor, patch)``; None for anything that
+    is not a final release (pre/dev/rc, major-only build numbers, ``latest``, garbage) -- such
+    agents are local or CI builds and are assumed to speak the latest API
+    (reference: ``S/services/runner/client.py`` ``_parse_version``)."""
+    m = _FINAL_VERSION.match(value or "")
+    if m is None:
+        return None
+    return int(m.group(1)), int(m.group(2)), int(m.group(3) or 0)
+
+
+class ShimHTTPError(RunnerError):
+    """A non-2xx answer from the shim, with the HTTP status kept for callers that branch on it."""
+
+    def __init__(self, status_code: int, message: str):
+        super().__init__(message)
+        self.status_code = status_code
+        self.message = message
+
+    def __repr__(self) -> str:
+        return f"ShimHTTPError({self.status_code})"
+
+
 class ShimClient:
-    def __init__(self, base_url: str):
+    def __init__(self, base_url: str, transport: Optional[httpx.BaseTransport] = None):
         self.base_url = base_url
-        self.c = _client(base_url)
+        self.c = _client(base_url, transport)
+
+    # -- API negotiation ------------------------------------------------------------------
+    def _negotiate(self) -> None:
+        """One healthcheck call fixes the agent's version and API generation for this client."""
+        data = self.healthcheck() or {}
+        self._shim_version = parse_version(str(data.get("version", "")))
+        api = data.get("api_version")
+        if isinstance(api, int):
+            self._api_version = api
+        elif self._shim_version is not None and self._shim_version < SHIM_API_V2_MIN_VERSION:
+            self._api_version = 1
+        else:
+            self._api_version = SHIM_LATEST_API_VERSION
+
+    @property
+    def api_version(self) -> int:
+        if not hasattr(self, "_api_version"):
+            self._negotiate()
+        return self._api_version
+
+    def _request(self, method: str, path: str, **kw) -> httpx.Response:
+        return self.c.request(method, path, **kw)
+
+    @staticmethod
+    def _raise_for_status(r: httpx.Response) -> None:
+        if r.is_success:
+            return
+        kind = "Client" if r.status_code < 500 else "Server"
+        msg = f"{r.status_code} {kind} Error: {r.reason_phrase} for url: {r.url}"
+        body = r.text.strip()
+        if body:
+            msg += f": {body[:500]}"
+        raise ShimHTTPError(r.status_code, msg)
 
     def healthcheck(self) -> Optional[dict]:
         try:
@@ -46,58 +114,62 @@ class ShimClient:
         return r.json()
 
     def submit_task(self, task: dict) -> dict:
-        r = self.c.post("/api/tasks", json=task)
+        """Submit (idempotent: 409 = the task already exists, its current state is returned)."""
+        r = self._request("POST", "/api/tasks", json=task)
         if r.status_code == 409:
             return self.get_task(task["id"])
-        if r.status_code != 200:
-            raise RunnerError(f"shim submit failed: {r.status_code} {r.text}")
+        self._raise_for_status(r)
         return r.json()
 
     def get_task(self, task_id: str) -> Optional[dict]:
-        r = self.c.get(f"/api/tasks/{task_id}")
+        r = self._request("GET", f"/api/tasks/{task_id}")
         if r.status_code == 404:
             return None
-        r.raise_for_status()
+        self._raise_for_status(r)
         return r.json()
 
     def list_tasks(self) -> List[str]:
-        r = self.c.get("/api/tasks")
-        r.raise_for_status()
+        r = self._request("GET", "/api/tasks")
+        self._raise_for_status(r)
         return r.json().get("ids", [])
 
     def terminate_task(self, task_id: str, reason: str = "", message: str = "", timeout: int = 10) -> None:
-        r = self.c.post(f"/api/tasks/{task_id}/terminate",
-                        json={"termination_reason": reason, "termination_message": message, "timeout": timeout},
-                        timeout=timeout + 30)
-        if r.status_code not in (200, 404):
-            raise RunnerError(f"terminate failed: {r.text}")
+        r = self._request("POST", f"/api/tasks/{task_id}/terminate",
+                          json={"termination_reason": reason, "termination_message": message, "timeout": timeout},
+                          timeout=timeout + 30)
+        if r.status_code != 404:
+            self._raise_for_status(r)
 
     def remove_task(self, task_id: str) -> None:
-        r = self.c.post(f"/api/tasks/{task_id}/remove")
-        if r.status_code not in (200, 404, 409):
-            raise RunnerError(f"remove failed: {r.text}")
+        r = self._request("POST", f"/api/tasks/{task_id}/remove")
+        if r.status_code not in (404, 409):
+            self._raise_for_status(r)
 
     def gpu_health(self) -> Optional[dict]:
         """The shim's latest HIP health-probe state ``{state, started_at_ms, ran_at_ms, result}``
-        (None: a shim without the endpoint)."""
-        r = self.c.get("/api/gpu_health", timeout=5)
+        (None: an API-1 shim, which has no probe endpoint)."""
+        if self.api_version < 2:
+            return None
+        r = self._request("GET", "/api/gpu_health", timeout=5)
         if r.status_code == 404:
             return None
-        r.raise_for_status()
+        self._raise_for_status(r)
         return r.json()
 
     def start_gpu_probe(self) -> str:
         """Ask the shim to (re-)run the probe off the job path: started | running | busy | unavailable."""
-        r = self.c.post("/api/gpu_health/probe", timeout=5)
+        if self.api_version < 2:
+            return "unavailable"
+        r = self._request("POST", "/api/gpu_health/probe", timeout=5)
         if r.status_code == 404:
             return "unavailable"
         return (r.json() or {}).get("state", "unavailable")
 
 
 class RunnerClient:
-    def __init__(self, base_url: str):
+    def __init__(self, base_url: str, transport: Optional[httpx.BaseTransport] = None):
         self.base_url = base_url
-        self.c = _client(base_url)
+        self.c = _client(base_url, transport)
 
     def healthcheck(self) -> Optional[dict]:
         try:
@@ -202,4 +274,4 @@ def get_runner_client(jpd: JobProvisioningData, jrd: Optional[JobRuntimeData], p
     return RunnerClient(runner_base_url(jpd, jrd, private_key))
 
 
-__all__ = ["ShimClient", "RunnerClient", "get_shim_client", "get_runner_client", "port_base_url", "SSHError"]
+__all__ = ["ShimClient", "ShimHTTPError", "RunnerClient", "parse_version", "get_shim_client", "get_runner_client", "port_base_url", "SSHError"]

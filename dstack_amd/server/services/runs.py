@@ -140,6 +140,13 @@ def get_run(s: Session, project: ProjectModel, run_name: Optional[str] = None,
 def _validate_run_spec(run_spec: RunSpec):
     if run_spec.run_name is not None and not _RUN_NAME_RE.match(run_spec.run_name):
         raise ServerClientError("Run name must be 2-41 chars of a-z, 0-9 and -, starting with a letter")
+    from dstack_amd.server.services.docker import is_valid_docker_volume_target
+
+    for mp in getattr(run_spec.configuration, "volumes", None) or []:
+        if not is_valid_docker_volume_target(mp.path):
+            raise ServerClientError(f"Invalid volume mount path: {mp.path}")
+        if mp.path == "/workflow" or mp.path.startswith("/workflow/"):
+            raise ServerClientError("Mounting volumes inside /workflow is not supported")
 
 
 def get_plan(s: Session, project: ProjectModel, user: UserModel, run_spec: RunSpec, max_offers: int = 50) -> RunPlan:
@@ -325,34 +332,62 @@ def process_terminating_run(s: Session, run: RunModel):
     scheduler.wake(scheduler.TERMINATING_JOBS)
 
 
+def _replica_importance(jobs: List[JobModel]) -> Optional[int]:
+    """None for an inactive replica (any job terminating or finished), else how costly stopping it
+    is: 0 still submitted, 1 provisioning or pulling, 2 running."""
+    statuses = {JobStatus(j.status) for j in jobs}
+    if JobStatus.TERMINATING in statuses or any(st.is_finished() for st in statuses):
+        return None
+    if JobStatus.SUBMITTED in statuses:
+        return 0
+    if statuses & {JobStatus.PROVISIONING, JobStatus.PULLING}:
+        return 1
+    return 2
+
+
 def scale_run_replicas(s: Session, run: RunModel, replicas_diff: int):
-    """Add replicas (new job models) or terminate the newest ones (``scale_run_replicas``)."""
+    """Scale a service by ``replicas_diff`` replicas (reference ``services/runs.py:scale_run_replicas``).
+
+    Down: the least important active replicas stop first (submitted before provisioning before
+    running; among equals the highest replica number), never below ``replicas.min``.  Up: finished
+    replicas are re-submitted first, then new replica numbers are added, never above ``replicas.max``."""
     if replicas_diff == 0:
         return
     spec = RunSpec.model_validate_json(run.run_spec)
+    conf = spec.configuration
     groups = jobs_services.group_jobs_by_replica_latest(run.jobs)
-    active = {r: js for r, js in groups.items() if not all(JobStatus(j.status).is_finished() for j in js)}
+    active, inactive = [], []
+    for r, js in groups.items():
+        imp = _replica_importance(js)
+        (inactive if imp is None else active).append((imp, r, js))
+    active.sort(key=lambda t: (-t[0], t[1]))  # most important first, then lower replica number
+    lo = conf.replicas.min if isinstance(conf, ServiceConfiguration) else 0
+    hi = conf.replicas.max if isinstance(conf, ServiceConfiguration) else None
     if replicas_diff < 0:
-        for r in sorted(active, reverse=True)[: -replicas_diff]:
-            for j in active[r]:
+        if len(active) + replicas_diff < (lo or 0):
+            raise ServerClientError("Can't scale down below the minimum number of replicas")
+        for _, _, js in reversed(active[replicas_diff:]):
+            for j in js:
+                if JobStatus(j.status).is_finished() or j.status == JobStatus.TERMINATING.value:
+                    continue
                 if j.status == JobStatus.RUNNING.value:
                     jobs_services.stop_runner(s, j)
                 jobs_services.terminate_job(j, JobTerminationReason.SCALED_DOWN)
         scheduler.wake(scheduler.TERMINATING_JOBS)
         return
+    if hi is not None and len(active) + replicas_diff > hi:
+        raise ServerClientError("Can't scale up above the maximum number of replicas")
+    scheduled = 0
+    for _, _, js in sorted(inactive, key=lambda t: t[1]):  # re-run finished replicas first
+        if scheduled == replicas_diff:
+            break
+        retry_run_replica_jobs(s, run, js, only_failed=False)
+        scheduled += 1
     secrets = jobs_services.get_job_secrets(s, run.project)
     next_replica = max(groups.keys(), default=-1) + 1
-    # reuse finished replica slots first
-    finished = sorted(r for r in groups if r not in active)
-    for _ in range(replicas_diff):
-        if finished:
-            r = finished.pop(0)
-            sub = max(j.submission_num for j in groups[r]) + 1
-        else:
-            r, sub = next_replica, 0
-            next_replica += 1
+    for r in range(next_replica, next_replica + replicas_diff - scheduled):
         for js in jobs_services.get_jobs_from_run_spec(spec, r, secrets):
-            s.add(jobs_services.new_job_model(run, js, submission_num=sub))
+            s.add(jobs_services.new_job_model(run, js, submission_num=0))
     s.flush()
     scheduler.wake(scheduler.SUBMITTED_JOBS)
 

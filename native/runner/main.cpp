@@ -28,7 +28,7 @@ Json collect_metrics(const std::vector<int>& gpu_filter);
 
 using namespace dsa;
 
-static const char* VERSION = "0.1.0-mi355x";
+static const char* VERSION = "0.1.0+mi355x";
 
 static void usage() {
   fprintf(stderr,

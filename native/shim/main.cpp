@@ -24,7 +24,7 @@
 
 namespace dsa {
 
-static const char* SHIM_VERSION = "0.1.0-mi355x";
+static const char* SHIM_VERSION = "0.1.0+mi355x";
 
 Shim::Shim(ShimOptions o, std::unique_ptr<TaskDriver> driver) : opts_(std::move(o)), driver_(std::move(driver)) {
   // ONE discovery: the lock's indices, the xGMI matrix rows and the render nodes handed to
@@ -440,6 +440,7 @@ int main(int argc, char** argv) {
     Json j = Json::object();
     j.set("service", "dstack-shim");
     j.set("version", SHIM_VERSION);
+    j.set("api_version", 2);  // 2: tasks + /api/gpu_health (server ShimClient negotiates on this)
     j.set("driver", shim.driver_name());
     j.set("gpus_free", shim.gpu_lock().free_count());
     j.set("gpus_total", shim.gpu_lock().total());
