@@ -9,14 +9,16 @@ and latencies feed the RPS autoscaler.
 
 from __future__ import annotations
 
+import asyncio
 import itertools
 import json
 import time
+from http.cookiejar import CookieJar
 from typing import Dict, List, Optional, Tuple
 
 import httpx
 from fastapi import APIRouter, Request
-from fastapi.responses import JSONResponse, Response, StreamingResponse
+from fastapi.responses import JSONResponse, RedirectResponse, Response, StreamingResponse
 from starlette.concurrency import run_in_threadpool
 from starlette.background import BackgroundTask
 
@@ -32,7 +34,39 @@ from dstack_amd.server.services.users import get_user_by_token
 
 router = APIRouter(tags=["proxy"])
 _rr: Dict[str, itertools.count] = {}
-_client = httpx.AsyncClient(timeout=httpx.Timeout(600, connect=10))
+
+
+class _NoCookies(CookieJar):
+    """The upstream client is shared by every downstream user: it must never remember a
+    ``Set-Cookie`` (that would hand one user's session to the next); cookies travel only in the
+    request/response headers."""
+
+    def extract_cookies(self, response, request):
+        pass
+
+    def set_cookie(self, cookie):
+        pass
+
+
+_clients: Dict[int, httpx.AsyncClient] = {}
+
+
+def _upstream_client() -> httpx.AsyncClient:
+    """One pooled client per event loop (connections are bound to the loop that opened them)."""
+    from dstack_amd.server import settings
+
+    loop = asyncio.get_running_loop()
+    c = _clients.get(id(loop))
+    if c is None or c.is_closed:
+        c = httpx.AsyncClient(timeout=httpx.Timeout(settings.PROXY_UPSTREAM_TIMEOUT, connect=10),
+                              cookies=httpx.Cookies(_NoCookies()), follow_redirects=False)
+        _clients[id(loop)] = c
+    return c
+
+
+# hop-by-hop headers (RFC 9110 7.6.1) are never forwarded; the body length is re-derived
+_HOP = {"connection", "keep-alive", "proxy-authenticate", "proxy-authorization", "te", "trailer",
+        "transfer-encoding", "upgrade"}
 
 
 def _replica_urls(s, run: RunModel, conf: ServiceConfiguration) -> List[str]:
@@ -57,27 +91,29 @@ def _resolve(project_name: str, run_name: str, token: Optional[str]) -> Tuple[Op
     """-> (replica_url, model_dict, status, error)"""
     with session_scope() as s:
         project = get_project_by_name(s, project_name)
+        not_found = f"Service {project_name}/{run_name} not found"
         if project is None:
-            return None, None, 404, "project not found"
+            return None, None, 404, not_found
         run = s.query(RunModel).filter(RunModel.project_id == project.id, RunModel.run_name == run_name,
                                        RunModel.deleted == False).order_by(RunModel.submitted_at.desc()).first()  # noqa
         if run is None or RunStatus(run.status).is_finished():
-            return None, None, 404, "service not found"
+            return None, None, 404, not_found
         spec = RunSpec.model_validate_json(run.run_spec)
         conf = spec.configuration
         if not isinstance(conf, ServiceConfiguration):
-            return None, None, 400, "run is not a service"
+            return None, None, 404, not_found
         if conf.auth:
             user = get_user_by_token(s, token) if token else None
             if user is None or (user.global_role != "admin" and get_member_role(project, user) is None):
-                return None, None, 403, "unauthorized"
+                return None, None, 403, "Access denied"
         urls = _replica_urls(s, run, conf)
         if not urls:
-            return None, None, 503, "no running replicas"
+            return None, None, 503, f"Service {project_name}/{run_name} has no running replicas"
         key = str(run.id)
         n = next(_rr.setdefault(key, itertools.count()))
         model = conf.model.model_dump() if conf.model else None
-        return urls[n % len(urls)], (model | {"run_id": key} if model else {"run_id": key}), 200, ""
+        meta = {"run_id": key, "strip_prefix": conf.strip_prefix}
+        return urls[n % len(urls)], (model | meta if model else meta), 200, ""
 
 
 def _token(request: Request) -> Optional[str]:
@@ -85,30 +121,51 @@ def _token(request: Request) -> Optional[str]:
     return a[7:].strip() if a.lower().startswith("bearer ") else None
 
 
+@router.api_route("/proxy/services/{project_name}/{run_name}", methods=["GET", "HEAD"], include_in_schema=False)
+async def service_root_redirect(project_name: str, run_name: str, request: Request):
+    """``.../run`` -> ``.../run/`` (308 keeps the method), so relative links resolve under the prefix."""
+    url = request.url.replace(path=request.url.path + "/")
+    return RedirectResponse(str(url), status_code=308)
+
+
 @router.api_route("/proxy/services/{project_name}/{run_name}/{path:path}",
                   methods=["GET", "POST", "PUT", "PATCH", "DELETE", "OPTIONS", "HEAD"], include_in_schema=False)
 async def service_proxy(project_name: str, run_name: str, path: str, request: Request):
+    """Forward one request to a replica: original ``Host`` and headers minus hop-by-hop ones, body
+    streamed both ways, status and headers passed through (``Content-Length``/``-Encoding``
+    included -- the body is relayed undecoded), no cookie state kept between users, 504 when the
+    replica does not answer in ``DSTACK_PROXY_UPSTREAM_TIMEOUT``."""
     url, meta, status, err = await run_in_threadpool(_resolve, project_name, run_name, _token(request))
     if url is None:
         return JSONResponse({"detail": err}, status_code=status)
-    with session_scope() as s:
-        run = s.query(RunModel).filter(RunModel.id == meta["run_id"]).first()
-        strip = RunSpec.model_validate_json(run.run_spec).configuration.strip_prefix if run else True
-    target = f"{url}/{path}" if strip else f"{url}/proxy/services/{project_name}/{run_name}/{path}"
+    prefix = f"/proxy/services/{project_name}/{run_name}"
+    target = f"{url}/{path}" if meta["strip_prefix"] else f"{url}{prefix}/{path}"
     if request.url.query:
         target += "?" + request.url.query
-    headers = {k: v for k, v in request.headers.items() if k.lower() not in ("host", "content-length")}
+    # a sized body keeps its Content-Length (streamed, not re-chunked: not every replica server
+    # reads chunked uploads); an unsized one goes chunked
+    headers = [(k, v) for k, v in request.headers.items() if k.lower() not in _HOP]
+    client = _upstream_client()
     start = time.time()
-    req = _client.build_request(request.method, target, headers=headers, content=await request.body())
+    body = request.stream() if request.method not in ("GET", "HEAD", "OPTIONS") else None
+    req = client.build_request(request.method, target, headers=headers, content=body)
     try:
-        upstream = await _client.send(req, stream=True)
+        upstream = await client.send(req, stream=True)
+    except httpx.TimeoutException:
+        return JSONResponse({"detail": "Timed out requesting upstream"}, status_code=504)
     except httpx.HTTPError as e:
-        return JSONResponse({"detail": f"upstream error: {e}"}, status_code=502)
+        return JSONResponse({"detail": f"Error requesting upstream: {e}"}, status_code=502)
     get_request_stats().record(meta["run_id"], time.time() - start)
-    resp_headers = {k: v for k, v in upstream.headers.items()
-                    if k.lower() not in ("content-length", "transfer-encoding", "connection", "content-encoding")}
-    return StreamingResponse(upstream.aiter_raw(), status_code=upstream.status_code, headers=resp_headers,
-                             background=BackgroundTask(upstream.aclose))
+    resp_headers = [(k, v) for k, v in upstream.headers.multi_items() if k.lower() not in _HOP]
+    if request.method == "HEAD" or upstream.status_code in (204, 304):
+        await upstream.aclose()
+        r = Response(status_code=upstream.status_code)
+        r.raw_headers = [(k.lower().encode("latin-1"), v.encode("latin-1")) for k, v in resp_headers]
+        return r
+    r = StreamingResponse(upstream.aiter_raw(), status_code=upstream.status_code,
+                          background=BackgroundTask(upstream.aclose))
+    r.raw_headers = [(k.lower().encode("latin-1"), v.encode("latin-1")) for k, v in resp_headers]
+    return r
 
 
 def _project_models(project_name: str) -> List[dict]:

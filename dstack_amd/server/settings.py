@@ -36,6 +36,9 @@ SERVER_ENVIRONMENT = os.getenv("DSTACK_SERVER_ENVIRONMENT", "dev")  # reported t
 SERVER_CONFIG_DISABLED = os.getenv("DSTACK_SERVER_CONFIG_DISABLED") is not None
 SQL_ECHO_ENABLED = os.getenv("DSTACK_SQL_ECHO_ENABLED") is not None
 
+# in-server service proxy: how long one upstream request may take (LLM generations are long)
+PROXY_UPSTREAM_TIMEOUT = float(os.getenv("DSTACK_PROXY_UPSTREAM_TIMEOUT", "600"))
+
 SERVER_METRICS_TTL_SECONDS = int(os.getenv("DSTACK_SERVER_METRICS_TTL_SECONDS", "3600"))
 SERVER_METRICS_COLLECT_INTERVAL = float(os.getenv("DSTACK_SERVER_METRICS_COLLECT_INTERVAL", "10"))
 SERVER_BACKGROUND_PROCESSING_ENABLED = not _env_bool("DSTACK_SERVER_BACKGROUND_PROCESSING_DISABLED")
