@@ -34,7 +34,7 @@ from dstack_amd.core.backends.clouds.common import (
     cloud_init,
     rsa_sha256_sign,
 )
-from dstack_amd.core.errors import BackendAuthError, ComputeError
+from dstack_amd.core.errors import BackendAuthError, ComputeError, ServerClientError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.instances import InstanceAvailability
 
@@ -589,12 +589,24 @@ class OCICompute(VMCompute):
         return self.config.get("compartment_id") or self.auth.get("tenancy")
 
     def check_credentials(self) -> None:
-        region = (self.config.get("regions") or ["us-ashburn-1"])[0]
+        # the identity API is asked in the key's home region (always subscribed)
+        region = self.auth.get("region") or (self.config.get("regions") or ["us-ashburn-1"])[0]
         user = urllib.parse.quote(self.auth.get("user", ""))
         r = self._signed("GET", region, f"/{self.API_VERSION}/users/{user}", host=f"identity.{region}.oraclecloud.com")
         if r.status_code in (401, 403, 404):
             raise BackendAuthError(f"oci user: {r.status_code} {r.text[:200]}")
         check_response(r, "oci user")
+        # every configured region must be subscribed by the tenancy (else launches fail later)
+        wanted = self.config.get("regions") or []
+        if wanted:
+            tenancy = urllib.parse.quote(self.auth.get("tenancy", ""))
+            r = check_response(self._signed("GET", region, f"/{self.API_VERSION}/tenancies/{tenancy}/regionSubscriptions",
+                                            host=f"identity.{region}.oraclecloud.com"), "oci region subscriptions")
+            subscribed = {x.get("regionName") for x in r.json()}
+            missing = [x for x in wanted if x not in subscribed]
+            if missing:
+                raise ServerClientError(f"Regions {missing} are not subscribed by the OCI tenancy "
+                                        f"(subscribed: {sorted(x for x in subscribed if x)})")
 
     def _availability_domains(self, region: str) -> List[str]:
         """The tenancy's availability-domain names in ``region`` (tenancy-prefixed, e.g.

@@ -139,13 +139,25 @@ def remote_backend_data(shim_port: int = DSTACK_SHIM_HTTP_PORT, direct: bool = F
     return json.dumps({"shim_port": shim_port, "direct": direct})
 
 
-def split_blocks(topo: HostTopology, blocks) -> int:
-    """``blocks: auto`` on an AMD host = one block per GPU; the xGMI-aware allocator then hands
-    out fully-connected subsets (MI355X nodes are all-to-all xGMI, so any subset works)."""
+def auto_blocks(n_gpus: int, cpus: int) -> int:
+    """``blocks: auto`` = as many blocks as the host can be cut into: one per GPU (each block
+    needs at least one CPU, so never more than the CPUs); a CPU-only host, one per CPU (reference
+    ``process_instances`` block rules)."""
+    if n_gpus:
+        return max(1, min(n_gpus, cpus) if cpus else n_gpus)
+    return max(1, cpus)
+
+
+def split_blocks(topo: HostTopology, blocks, cpus: int = 0) -> int:
+    """Blocks of a host: ``auto`` per ``auto_blocks``; an explicit count must divide the GPUs
+    (and CPUs) evenly.  The xGMI-aware allocator hands out fully-connected GPU subsets (MI355X
+    nodes are all-to-all xGMI, so any subset works)."""
     n = len(topo.gpus)
     if blocks == "auto":
-        return max(1, n)
+        return auto_blocks(n, cpus)
     blocks = int(blocks)
     if n and n % blocks != 0:
         raise ProvisioningError(f"{n} GPUs cannot be split into {blocks} blocks")
+    if cpus and cpus % blocks != 0:
+        raise ProvisioningError(f"{cpus} CPUs cannot be split into {blocks} blocks")
     return blocks

@@ -17,7 +17,14 @@ from typing import Optional
 from sqlalchemy import select
 from sqlalchemy.orm import Session
 
-from dstack_amd.core.backends.remote import deploy_ssh_instance, host_info_to_instance_type, remote_backend_data, split_blocks
+from dstack_amd.core.backends.remote import (
+    auto_blocks,
+    deploy_ssh_instance,
+    host_info_to_instance_type,
+    remote_backend_data,
+    split_blocks,
+)
+from dstack_amd.core.errors import ProvisioningError
 from dstack_amd.core.models.backends import BACKENDS_WITH_CREATE_INSTANCE_SUPPORT, BACKENDS_WITH_PLACEMENT_GROUPS_SUPPORT, BackendType
 from dstack_amd.core.models.fleets import InstanceGroupPlacement
 from dstack_amd.core.models.instances import (
@@ -111,6 +118,12 @@ def _add_remote(s: Session, inst: InstanceModel):
         if inst.deploy_owner and inst.deploy_owner != me and inst.deploy_started_at and \
                 now - inst.deploy_started_at < DEPLOY_LEASE:
             return  # another replica's deploy is in flight
+        if now - inst.created_at > TERMINATION_DEADLINE_OFFSET:
+            # never came up in time (unreachable host, bad key, broken agent): give up on it
+            inst.status = InstanceStatus.TERMINATED.value
+            inst.termination_reason = "Provisioning timeout expired"
+            inst.deploy_owner = None
+            return
         if inst.last_retry_at and now - inst.last_retry_at < SSH_DEPLOY_RETRY:
             return
         inst.last_retry_at = now
@@ -146,7 +159,12 @@ def _add_remote(s: Session, inst: InstanceModel):
         inst.termination_reason = f"no address in network {bd.get('network')}"
         inst.status = InstanceStatus.TERMINATED.value
         return
-    total_blocks = split_blocks(topo, bd.get("blocks", 1))
+    try:
+        total_blocks = split_blocks(topo, bd.get("blocks", 1), itype.resources.cpus)
+    except ProvisioningError as e:
+        inst.termination_reason = str(e)
+        inst.status = InstanceStatus.TERMINATED.value
+        return
     jpd = JobProvisioningData(
         backend=BackendType.REMOTE, instance_type=itype, instance_id=inst.name, hostname=rci.host,
         internal_ip=internal_ip or rci.host, region="remote", price=0.0, username=rci.ssh_user, ssh_port=rci.port,
@@ -239,8 +257,8 @@ def _create_instance(s: Session, inst: InstanceModel):
         inst.price = jpd.price
         inst.offer = offer.model_dump_json()
         inst.job_provisioning_data = jpd.model_dump_json()
-        n_gpus = len(offer.instance.resources.gpus)
-        inst.total_blocks = (max(1, n_gpus) if blocks == "auto" else int(blocks))
+        res = offer.instance.resources
+        inst.total_blocks = auto_blocks(len(res.gpus), res.cpus) if blocks == "auto" else int(blocks)
         inst.backend_data = jpd.backend_data
         inst.status = (InstanceStatus.IDLE if jpd.backend == BackendType.LOCAL else InstanceStatus.PROVISIONING).value
         inst.started_at = now

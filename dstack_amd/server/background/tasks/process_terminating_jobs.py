@@ -37,10 +37,10 @@ def _detach_volumes(s: Session, job: JobModel) -> bool:
     from dstack_amd.server.services.jobs.volumes import detach_job_volumes
 
     try:
-        return detach_job_volumes(s, job, job.instance_id, job.remove_at)
+        return detach_job_volumes(s, job, job.used_instance_id, job.volumes_detached_at)
     except Exception as e:  # noqa: BLE001 - a broken backend must not wedge termination forever
         logger.warning("%s: volume detach failed: %s", job.job_name, e)
-        return job.remove_at is not None and get_current_datetime() - job.remove_at > timedelta(minutes=10)
+        return get_current_datetime() - job.volumes_detached_at > timedelta(minutes=10)
 
 
 def _process_job(s: Session, job_id):
@@ -73,11 +73,15 @@ def _process_job(s: Session, job_id):
         from dstack_amd.server.services.services import unregister_replica
 
         unregister_replica(s, run, job)
+    if job.volumes_detached_at is None:
+        # the container is gone: the instance's blocks are freed right away, so a volume stuck in
+        # detaching never holds the host (or its termination); detaching goes on against the
+        # instance the job ran on (``used_instance_id``) -- soft first, forced after stop_duration
+        job.volumes_detached_at = get_current_datetime()
+        jobs_services.release_instance(s, job)
     if not _detach_volumes(s, job):
         job.last_processed_at = get_current_datetime()
-        return  # retried on the next pass (soft detach in progress; forced after stop_duration)
-    jobs_services.release_instance(s, job)
-    job.volumes_detached_at = get_current_datetime()
+        return  # retried on the next pass
     job.status = reason.to_status().value
     job.finished_at = get_current_datetime()
     job.last_processed_at = get_current_datetime()

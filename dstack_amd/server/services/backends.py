@@ -185,6 +185,8 @@ def validate_credentials(btype: BackendType, cfg: dict, secrets: dict) -> None:
             check()
     except BackendAuthError as e:
         raise InvalidCredentialsError(f"Invalid {btype.value} credentials: {e}") from None
+    except ServerClientError:
+        raise  # a configuration the cloud refuses for another reason (e.g. unsubscribed regions)
     except (httpx.TransportError, OSError) as e:
         logging.getLogger(__name__).warning("%s credentials not verified (API unreachable: %s)", btype.value, e)
     except Exception as e:  # noqa: BLE001 -- e.g. a malformed key the signer cannot load
@@ -203,6 +205,22 @@ def _configurable_type(config: dict) -> BackendType:
 
 
 def delete_backends(s: Session, project: ProjectModel, names: List[str]):
+    """Drop backend configurations, refused while any of them still owns live instances or
+    volumes (their cloud resources could no longer be terminated or deleted)."""
+    from dstack_amd.core.models.instances import InstanceStatus
+    from dstack_amd.server.models import InstanceModel, VolumeModel
+
+    busy = s.execute(select(InstanceModel.backend).where(
+        InstanceModel.project_id == project.id, InstanceModel.backend.in_(names),
+        InstanceModel.deleted == False,  # noqa: E712
+        InstanceModel.status != InstanceStatus.TERMINATED.value)).scalars().first()
+    if busy is not None:
+        raise ServerClientError(f"Backend {busy} has active instances. Terminate them before deleting the backend.")
+    for v in s.execute(select(VolumeModel).where(VolumeModel.project_id == project.id,
+                                                 VolumeModel.deleted == False)).scalars():  # noqa: E712
+        if json.loads(v.configuration or "{}").get("backend") in names:
+            raise ServerClientError(f"Backend {json.loads(v.configuration)['backend']} has active volumes. "
+                                    "Delete them before deleting the backend.")
     for n in names:
         row = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
                                                    BackendModel.type == n)).scalar_one_or_none()
@@ -211,9 +229,20 @@ def delete_backends(s: Session, project: ProjectModel, names: List[str]):
 
 
 def backend_config_values(body: dict) -> dict:
+    """Form choices for a backend: with ``creds`` given they are checked against the cloud first
+    (rejected -> ``InvalidCredentialsError``, HTTP 400 ``invalid_credentials``), as the reference's
+    configurators do before offering regions."""
     from dstack_amd.core.backends.catalog import offline_rows
 
     btype = _configurable_type(body)
+    if body.get("creds") is not None:
+        try:
+            _, cfg, secrets = split_backend_config(body)
+        except ValueError:  # a form still being filled in: settings incomplete, creds checkable
+            cfg = {k: v for k, v in body.items() if k not in ("type", "creds")}
+            secrets = dict(body["creds"])
+        _check_default_creds(secrets)
+        validate_credentials(btype, cfg, secrets)
     regions = sorted({r.location for r in offline_rows(btype)})
     wanted = body.get("regions") or body.get("locations")
     selected = [r for r in regions if not wanted or r in wanted]

@@ -64,5 +64,8 @@ def _divisible(offer: InstanceOfferWithAvailability, blocks) -> bool:
 
 
 def _with_blocks(offer: InstanceOfferWithAvailability, blocks) -> InstanceOfferWithAvailability:
-    total = (len(offer.instance.resources.gpus) or 1) if blocks == "auto" else blocks
+    from dstack_amd.core.backends.remote import auto_blocks
+
+    res = offer.instance.resources
+    total = auto_blocks(len(res.gpus), res.cpus) if blocks == "auto" else blocks
     return offer.model_copy(update={"total_blocks": total})

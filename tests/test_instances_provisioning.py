@@ -187,7 +187,26 @@ def test_blocks_offer_helper_keeps_int_blocks():
 
     assert _with_blocks(_offer(gpus=8), 2).total_blocks == 2
     assert _with_blocks(_offer(gpus=8), "auto").total_blocks == 8
-    assert _with_blocks(_offer(gpus=0), "auto").total_blocks == 1
+    assert _with_blocks(_offer(gpus=0), "auto").total_blocks == 128  # CPU host: one block per CPU
+
+
+@pytest.mark.parametrize("cpus,gpus,requested,expected", [
+    (32, 8, 1, 1), (32, 8, 2, 2), (32, 8, 4, 4), (32, 8, "auto", 8), (4, 8, "auto", 4), (8, 8, "auto", 8),
+    (32, 0, 1, 1), (32, 0, 2, 2), (32, 0, 4, 4), (32, 0, "auto", 32),
+], ids=["gpu-no-blocks", "gpu-4-per-block", "gpu-2-per-block", "gpu-auto-max-gpu", "gpu-auto-max-cpu",
+        "gpu-auto-max-cpu-and-gpu", "cpu-no-blocks", "cpu-16-per-block", "cpu-8-per-block", "cpu-auto-max-cpu"])
+def test_block_counts_for_created_and_ssh_instances(cpus, gpus, requested, expected):
+    """Reference ``TestCreateInstance`` / ``TestAddSSHInstance`` block tables: a cloud offer and an
+    SSH host get the same block count for the same shape."""
+    from dstack_amd.core.backends.remote import split_blocks
+    from dstack_amd.core.models.instances import GpuDevice, HostTopology
+    from dstack_amd.server.services.offers import _with_blocks
+
+    o = _offer(gpus=gpus)
+    o.instance.resources.cpus = cpus
+    assert _with_blocks(o, requested).total_blocks == expected
+    topo = HostTopology(gpus=[GpuDevice(index=i, name="MI355X", memory_mib=288 * 1024) for i in range(gpus)])
+    assert split_blocks(topo, requested, cpus) == expected
 
 
 def test_fleet_backend_data_records_placement(db):
@@ -287,3 +306,23 @@ def _remote_instance_named(s, host):
     project = s.query(ProjectModel).filter_by(name="main").one()
     return pools_services.add_remote(s, project, None, None, None, None, host, 22, "ubuntu",
                                      [SSHKey(public="ssh-ed25519 AAAA", private="k")]).id
+
+
+def test_ssh_instance_terminated_when_provisioning_timeout_expired(db, monkeypatch):
+    """(reference ``TestSSHInstanceTerminateProvisionTimeoutExpired``) a pending SSH host that never
+    came up within the deadline is given up without another deploy attempt."""
+    from datetime import timedelta
+
+    from dstack_amd.server.background.tasks import process_instances as pi
+
+    deploys = []
+    monkeypatch.setattr(pi, "deploy_ssh_instance", lambda *a, **k: deploys.append(a) or HOST_INFO)
+    with session_scope() as s:
+        iid = _remote_instance(s)
+        s.get(InstanceModel, iid).created_at = get_current_datetime() - timedelta(days=100)
+    with session_scope() as s:
+        pi._process_instance(s, iid)
+    with session_scope() as s:
+        inst = s.get(InstanceModel, iid)
+        assert inst.status == "terminated" and inst.termination_reason == "Provisioning timeout expired"
+    assert deploys == []

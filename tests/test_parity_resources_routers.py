@@ -130,6 +130,9 @@ def test_ssh_fleet_instance_deletes_need_permission(client):
         r = client.post("/api/project/main/fleets/delete_instances", json={"name": "perm", "instance_nums": [0]},
                         headers=h)
         assert r.status_code == 403
+        # deleting the whole SSH fleet needs the same permission
+        assert client.post("/api/project/main/fleets/delete", json={"names": ["perm"]}, headers=h).status_code == 403
+        assert client.post("/api/project/main/fleets/get", json={"name": "perm"}).json()["status"] != "terminating"
     finally:
         permissions.set_default_permissions(None)
 

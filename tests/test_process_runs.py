@@ -163,3 +163,23 @@ def test_pending_service_resubmits_every_replica(db):
     assert st == RunStatus.SUBMITTED
     assert [(r, n, js) for r, n, js in jobs if js == JobStatus.SUBMITTED.value] == [
         (0, 1, JobStatus.SUBMITTED.value), (1, 1, JobStatus.SUBMITTED.value)]
+
+
+def test_terminating_run_terminates_its_jobs_then_finishes(db):
+    """(reference ``test_terminate_run_jobs``) a run stopped by the user: its running job is moved
+    to TERMINATING with the run's reason mapped; once the job is finished the run is too."""
+    rid = _run(_task(), RunStatus.RUNNING)
+    _set_jobs(rid, JobStatus.RUNNING)
+    with session_scope() as s:
+        run = s.get(RunModel, rid)
+        run.status = RunStatus.TERMINATING.value
+        run.termination_reason = RunTerminationReason.STOPPED_BY_USER.value
+    with mock.patch("dstack_amd.server.services.jobs.stop_runner"):
+        st, reason, jobs = _process(rid)
+    assert st == RunStatus.TERMINATING and jobs == [(0, 0, "terminating")]
+    with session_scope() as s:
+        j = s.query(JobModel).filter_by(run_id=rid).one()
+        assert j.termination_reason == JobTerminationReason.TERMINATED_BY_USER.value
+        j.status = JobStatus.TERMINATED.value
+    st, reason, _ = _process(rid)
+    assert st == RunStatus.TERMINATED and reason == RunTerminationReason.STOPPED_BY_USER.value

@@ -140,11 +140,17 @@ def test_volume_attached_before_shim_submit_and_detached_on_termination(db):
             assert list(s.execute(select(volumes_attachments.c.instance_id)
                                   .where(volumes_attachments.c.volume_id == vid)).scalars()) == [iid]
             jobs_services.terminate_job(j, JobTerminationReason.TERMINATED_BY_USER, delay=False)
-        # soft detach still in progress: the job stays terminating, the instance keeps its blocks
+        # soft detach still in progress: the job stays terminating, but the instance is released
+        # already -- a stuck volume never holds the host (reference test_force_detaches_job_volumes)
         with mock.patch.object(ptj, "get_shim_client", return_value=shim), session_scope() as s:
             ptj._process_job(s, jid)
         with session_scope() as s:
-            assert s.get(JobModel, jid).status == "terminating"
+            j = s.get(JobModel, jid)
+            assert j.status == "terminating" and j.instance_id is None and j.used_instance_id == iid
+            assert j.volumes_detached_at is not None
+            assert s.get(InstanceModel, iid).busy_blocks == 0
+            assert list(s.execute(select(volumes_attachments.c.instance_id)
+                                  .where(volumes_attachments.c.volume_id == vid)).scalars()) == [iid]
         assert compute.detach_volume.call_args.kwargs.get("force") is False
         # past stop_duration + grace: forced detach, then the job finishes
         compute.is_volume_detached.return_value = True
