@@ -5,6 +5,8 @@ from dstack_amd.api._public import (
     BackendCollection,
     Client,
     FleetCollection,
+    PoolCollection,
+    PoolInstance,
     RepoCollection,
     Run,
     RunCollection,
@@ -28,7 +30,7 @@ from dstack_amd.core.services.ssh.ports import PortUsedError
 
 __all__ = [
     "APIClient", "Backend", "BackendCollection", "BackendType", "Client", "ClientError", "ComputeCapability", "DevEnvironment", "Disk",
-    "FleetCollection", "GPU", "LocalRepo", "Memory", "OpenAIChatModel", "PortUsedError", "Range", "RegistryAuth",
+    "FleetCollection", "GPU", "PoolCollection", "PoolInstance", "LocalRepo", "Memory", "OpenAIChatModel", "PortUsedError", "Range", "RegistryAuth",
     "RemoteRepo", "RepoCollection", "Resources", "Run", "RunCollection", "RunStatus", "Scaling", "Service", "Task",
     "TGIChatModel", "VirtualRepo", "VolumeCollection",
 ]

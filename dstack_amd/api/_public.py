@@ -375,6 +375,58 @@ class BackendCollection:
         self._api.backends.delete(self._project, names)
 
 
+class PoolInstance:
+    """One pool of the deprecated pools API (reference ``api/_public/pools.py``)."""
+
+    def __init__(self, api_client: APIClient, pool):
+        self._api = api_client
+        self._pool = pool
+
+    @property
+    def name(self) -> str:
+        return self._pool.name
+
+    @property
+    def default(self) -> bool:
+        return self._pool.default
+
+    @property
+    def total_instances(self) -> int:
+        return self._pool.total_instances
+
+    @property
+    def available_instances(self) -> int:
+        return self._pool.available_instances
+
+    def __repr__(self) -> str:
+        return f"<PoolInstance '{self.name}'>"
+
+    __str__ = __repr__
+
+
+class PoolCollection:
+    """Operations with pools (deprecated in the reference in favour of fleets; kept so old scripts
+    using ``client.pool`` keep working)."""
+
+    def __init__(self, api_client: APIClient, project_name: str):
+        self._api = api_client
+        self._project = project_name
+
+    def list(self) -> List[PoolInstance]:
+        return [PoolInstance(self._api, p) for p in self._api.pool.list(self._project)]
+
+    def show(self, name: Optional[str] = None):
+        """The pool's instances (``None``: the project's default pool)."""
+        return self._api.pool.show(self._project, name)
+
+    def create(self, name: str) -> PoolInstance:
+        self._api.pool.create(self._project, name)
+        return next(p for p in self.list() if p.name == name)
+
+    def delete(self, name: str, force: bool = False):
+        self._api.pool.delete(self._project, name, force)
+
+
 class Client:
     def __init__(self, api_client: APIClient, project_name: str, ssh_identity_file: Optional[str] = None):
         self.api = api_client
@@ -385,6 +437,7 @@ class Client:
         self.fleets = FleetCollection(api_client, project_name)
         self.volumes = VolumeCollection(api_client, project_name)
         self.backends = BackendCollection(api_client, project_name)
+        self.pool = PoolCollection(api_client, project_name)
 
     @staticmethod
     def from_config(project_name: Optional[str] = None, server_url: Optional[str] = None,

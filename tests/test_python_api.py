@@ -118,3 +118,50 @@ def test_repo_collection_load(dc, tmp_path, monkeypatch):
     assert isinstance(repo, LocalRepo) and dc.repos.is_initialized(repo)
     again = dc.repos.load(str(work))
     assert isinstance(again, LocalRepo) and again.repo_id == repo.repo_id
+
+
+def test_pool_collection_legacy_api(dc):
+    """(reference ``api/_public/pools.py``) the deprecated ``client.pool`` still lists, creates,
+    shows and deletes pools."""
+    names = [p.name for p in dc.pool.list()]
+    assert names  # the project's default pool is created on first listing
+    p = dc.pool.create("legacy")
+    assert p.name == "legacy" and repr(p) == "<PoolInstance 'legacy'>" and p.total_instances == 0
+    assert dc.pool.show("legacy").name == "legacy"
+    dc.pool.delete("legacy")
+    assert "legacy" not in [x.name for x in dc.pool.list()]
+
+
+def test_sft_fine_tuning_task_builds_a_runnable_task(dc, tmp_path):
+    """``SFTFineTuningTask`` (reference ``api/huggingface``) is a Task whose commands install the HF
+    stack, unpack the shipped training script and launch it once per GPU with the given options."""
+    import base64
+    import py_compile
+
+    from dstack_amd.api.huggingface import SFTFineTuningTask
+
+    with pytest.raises(ValueError, match="HF_TOKEN"):
+        SFTFineTuningTask(model_name="m", dataset_name="d", env={})
+    t = SFTFineTuningTask(model_name="meta-llama/Llama-3.1-8B", dataset_name="org/sft data", env={"HF_TOKEN": "x"},
+                          lora_r=16, max_steps=10, use_4bit=True, resources={"gpu": "MI355X:8"})
+    assert t.type == "task" and t.sft_args["lora_r"] == 16
+    install, unpack, launch = t.commands
+    assert "trl" in install and "bitsandbytes" in install
+    blob = unpack.split()[1]
+    script = tmp_path / "sft.py"
+    script.write_bytes(base64.b64decode(blob))
+    py_compile.compile(str(script), doraise=True)
+    assert launch.startswith("accelerate launch --num_processes ${DSTACK_GPUS_PER_NODE:-1}")
+    assert "--lora_r 16" in launch and "--max_steps 10" in launch and "'org/sft data'" in launch
+    # the script's CLI accepts exactly what the task passes
+    import importlib.util
+    import shlex
+
+    spec = importlib.util.spec_from_file_location("sft_script", script)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    parsed = mod.parse_args(shlex.split(launch.split("/tmp/dstack_sft_train.py", 1)[1]))
+    assert parsed.lora_r == 16 and parsed.use_4bit is True and parsed.dataset_name == "org/sft data"
+    # and the server accepts it as a run configuration
+    plan = dc.runs.get_plan(t)
+    assert plan.job_plans and plan.job_plans[0].job_spec.commands[-1].endswith(launch)
