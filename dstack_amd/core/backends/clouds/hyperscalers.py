@@ -608,6 +608,106 @@ class OCICompute(VMCompute):
                 raise ServerClientError(f"Regions {missing} are not subscribed by the OCI tenancy "
                                         f"(subscribed: {sorted(x for x in subscribed if x)})")
 
+    # -- network bootstrap (reference ``oci/resources.py:427-690``) -------------------------------
+    # One compartment for everything dstack creates (unless the config names one), and per region a
+    # VCN with an internet gateway, a default route to it, security rules (SSH from anywhere, all
+    # traffic inside the VCN -- RCCL/torch.distributed between nodes use ephemeral ports) and one
+    # regional subnet.  Every step is get-or-create by display name, so it is idempotent and safe to
+    # repeat at launch for regions added later.
+    NET_NAME = "dstack"
+    VCN_CIDR = "10.0.0.0/16"
+    SUBNET_CIDR = "10.0.0.0/18"
+    WAIT_S = 120.0
+    WAIT_POLL_S = 2.0
+
+    def _home_region(self) -> str:
+        return self.auth.get("region") or (self.config.get("regions") or ["us-ashburn-1"])[0]
+
+    def _identity(self, method: str, path: str, body: Optional[dict] = None):
+        region = self._home_region()
+        return self._signed(method, region, f"/{self.API_VERSION}{path}", body,
+                            host=f"identity.{region}.oraclecloud.com")
+
+    def _list_named(self, region: str, kind: str, name: str, **params) -> Optional[dict]:
+        q = urllib.parse.urlencode({**params, "displayName": name})
+        items = check_response(self._signed("GET", region, f"/{self.API_VERSION}/{kind}?{q}"), f"oci list {kind}").json()
+        live = [x for x in items if x.get("lifecycleState") not in ("TERMINATED", "TERMINATING")]
+        return live[0] if live else None
+
+    def _wait_available(self, region: str, kind: str, obj: dict, host: Optional[str] = None) -> dict:
+        deadline = time.time() + self.WAIT_S
+        while obj.get("lifecycleState") not in ("AVAILABLE", "ACTIVE"):
+            if time.time() > deadline:
+                raise ComputeError(f"oci {kind} {obj.get('id')} still {obj.get('lifecycleState')}")
+            time.sleep(self.WAIT_POLL_S)
+            obj = check_response(self._signed("GET", region, f"/{self.API_VERSION}/{kind}/{obj['id']}", host=host),
+                                 f"oci get {kind}").json()
+        return obj
+
+    def ensure_compartment(self) -> str:
+        if self.config.get("compartment_id"):
+            return self.config["compartment_id"]
+        tenancy = self.auth["tenancy"]
+        q = urllib.parse.urlencode({"compartmentId": tenancy, "name": self.NET_NAME, "lifecycleState": "ACTIVE"})
+        found = check_response(self._identity("GET", f"/compartments?{q}"), "oci compartments").json()
+        if found:
+            comp = found[0]
+        else:
+            comp = check_response(self._identity("POST", "/compartments", {
+                "compartmentId": tenancy, "name": self.NET_NAME,
+                "description": "Resources created by dstack"}), "oci create compartment").json()
+            region = self._home_region()
+            comp = self._wait_available(region, "compartments", comp, host=f"identity.{region}.oraclecloud.com")
+        self.config["compartment_id"] = comp["id"]
+        return comp["id"]
+
+    def ensure_network(self, region: str) -> str:
+        """The subnet instances of ``region`` launch into (created on first use)."""
+        comp = self.ensure_compartment()
+        vcn = self._list_named(region, "vcns", f"{self.NET_NAME}-vcn", compartmentId=comp)
+        if vcn is None:
+            vcn = check_response(self._signed("POST", region, f"/{self.API_VERSION}/vcns", {
+                "compartmentId": comp, "cidrBlocks": [self.VCN_CIDR], "displayName": f"{self.NET_NAME}-vcn",
+                "dnsLabel": self.NET_NAME}), "oci create vcn").json()
+        vcn = self._wait_available(region, "vcns", vcn)
+        igw = self._list_named(region, "internetGateways", f"{self.NET_NAME}-igw", compartmentId=comp, vcnId=vcn["id"])
+        if igw is None:
+            igw = check_response(self._signed("POST", region, f"/{self.API_VERSION}/internetGateways", {
+                "compartmentId": comp, "vcnId": vcn["id"], "isEnabled": True,
+                "displayName": f"{self.NET_NAME}-igw"}), "oci create internet gateway").json()
+        igw = self._wait_available(region, "internetGateways", igw)
+        rt_id = vcn["defaultRouteTableId"]
+        rt = check_response(self._signed("GET", region, f"/{self.API_VERSION}/routeTables/{rt_id}"), "oci route table").json()
+        rules = rt.get("routeRules") or []
+        if not any(r.get("destination") == "0.0.0.0/0" for r in rules):
+            check_response(self._signed("PUT", region, f"/{self.API_VERSION}/routeTables/{rt_id}", {"routeRules": rules + [
+                {"destination": "0.0.0.0/0", "destinationType": "CIDR_BLOCK", "networkEntityId": igw["id"]}]}),
+                "oci update route table")
+        sl_id = vcn["defaultSecurityListId"]
+        check_response(self._signed("PUT", region, f"/{self.API_VERSION}/securityLists/{sl_id}", {
+            "ingressSecurityRules": [
+                {"protocol": "6", "source": "0.0.0.0/0", "tcpOptions": {"destinationPortRange": {"min": 22, "max": 22}}},
+                {"protocol": "all", "source": self.VCN_CIDR},
+                {"protocol": "1", "source": "0.0.0.0/0", "icmpOptions": {"type": 3, "code": 4}}],
+            "egressSecurityRules": [{"protocol": "all", "destination": "0.0.0.0/0"}]}), "oci update security list")
+        subnet = self._list_named(region, "subnets", f"{self.NET_NAME}-subnet", compartmentId=comp, vcnId=vcn["id"])
+        if subnet is None:
+            subnet = check_response(self._signed("POST", region, f"/{self.API_VERSION}/subnets", {
+                "compartmentId": comp, "vcnId": vcn["id"], "cidrBlock": self.SUBNET_CIDR,
+                "displayName": f"{self.NET_NAME}-subnet", "dnsLabel": "nodes", "routeTableId": rt_id,
+                "securityListIds": [sl_id], "prohibitPublicIpOnVnic": False}), "oci create subnet").json()
+        subnet = self._wait_available(region, "subnets", subnet)
+        self.config.setdefault("subnet_ids", {})[region] = subnet["id"]
+        return subnet["id"]
+
+    def prepare_config(self) -> dict:
+        """At backend creation: compartment + per-region networks, recorded in the stored config
+        so launches go straight to them (regions without a configured subnet only)."""
+        for region in self.config.get("regions") or [self._home_region()]:
+            if not (self.config.get("subnet_ids") or {}).get(region):
+                self.ensure_network(region)
+        return {"compartment_id": self.config["compartment_id"], "subnet_ids": dict(self.config["subnet_ids"])}
+
     def _availability_domains(self, region: str) -> List[str]:
         """The tenancy's availability-domain names in ``region`` (tenancy-prefixed, e.g.
         ``Uocm:US-CHICAGO-1-AD-1``: they cannot be derived from the region name)."""
@@ -689,6 +789,7 @@ class OCICompute(VMCompute):
 
     def _launch(self, offer, cfg):
         region = offer.region
+        subnet = (self.config.get("subnet_ids") or {}).get(region) or self.ensure_network(region)
         comp = self._compartment()
         body = {
             "compartmentId": comp, "availabilityDomain": self._ad_for(region, offer.instance.name),
@@ -696,7 +797,7 @@ class OCICompute(VMCompute):
             "displayName": cfg.instance_name,
             "sourceDetails": {"sourceType": "image", "imageId": self._image_id(region, comp, offer.instance.name),
                               "bootVolumeSizeInGBs": max(100, offer.instance.resources.disk.size_mib // 1024)},
-            "createVnicDetails": {"subnetId": (self.config.get("subnet_ids") or {}).get(region), "assignPublicIp": True},
+            "createVnicDetails": {"subnetId": subnet, "assignPublicIp": True},
             "metadata": {"ssh_authorized_keys": "\n".join(cfg.get_public_keys()),
                          "user_data": base64.b64encode(cloud_init(cfg).encode()).decode()},
         }

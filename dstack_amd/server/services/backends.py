@@ -119,6 +119,7 @@ def create_backend(s: Session, project: ProjectModel, config: dict) -> BackendMo
     _, cfg, secrets = split_backend_config(config)
     _check_default_creds(secrets)
     validate_credentials(btype, cfg, secrets)
+    cfg = prepare_backend_resources(btype, cfg, secrets)
     row = BackendModel(id=uuid.uuid4(), project_id=project.id, type=btype.value, config=json.dumps(cfg),
                        auth=json.dumps(secrets))
     s.add(row)
@@ -142,6 +143,11 @@ def update_backend(s: Session, project: ProjectModel, config: dict) -> BackendMo
     _, cfg, secrets = split_backend_config(merged)
     _check_default_creds(secrets)
     validate_credentials(btype, cfg, secrets)
+    old_cfg = json.loads(row.config or "{}")
+    for k in ("compartment_id", "subnet_ids"):  # keep what was bootstrapped unless overridden
+        if k in old_cfg and k not in cfg and btype == BackendType.OCI:
+            cfg[k] = old_cfg[k]
+    cfg = prepare_backend_resources(btype, cfg, secrets)
     row.config = json.dumps(cfg)
     row.auth = json.dumps(secrets)
     return row
@@ -191,6 +197,31 @@ def validate_credentials(btype: BackendType, cfg: dict, secrets: dict) -> None:
         logging.getLogger(__name__).warning("%s credentials not verified (API unreachable: %s)", btype.value, e)
     except Exception as e:  # noqa: BLE001 -- e.g. a malformed key the signer cannot load
         raise InvalidCredentialsError(f"Invalid {btype.value} credentials: {e}") from None
+
+
+def prepare_backend_resources(btype: BackendType, cfg: dict, secrets: dict) -> dict:
+    """Cloud-side resources a backend needs before its first launch, created at backend creation
+    and recorded in its stored config (OCI: compartment, VCN, subnet, gateway, routes, security
+    rules).  Skipped with ``DSTACK_SKIP_BACKEND_VALIDATION=1`` (then created lazily at launch); an
+    unreachable API is not an error either -- the launch path creates them idempotently."""
+    import logging
+    import os
+
+    import httpx
+
+    if os.getenv("DSTACK_SKIP_BACKEND_VALIDATION") == "1":
+        return cfg
+    from dstack_amd.core.backends.clouds import compute_class
+
+    cls = compute_class(btype)
+    if cls is None or not hasattr(cls, "prepare_config"):
+        return cfg
+    comp = cls(dict(cfg), secrets, httpx.Client(timeout=30.0))
+    try:
+        return {**cfg, **comp.prepare_config()}
+    except (httpx.TransportError, OSError) as e:
+        logging.getLogger(__name__).warning("%s resources not prepared (API unreachable: %s)", btype.value, e)
+        return cfg
 
 
 def _configurable_type(config: dict) -> BackendType:

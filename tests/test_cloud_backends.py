@@ -274,6 +274,7 @@ def test_oci_http_signature(rsa_pem):
             assert body["sourceDetails"]["imageId"] == "ocid1.image.ubuntu"  # looked up, never ""
             # the tenancy's real AD name that offers the shape (not "<region>-AD-1")
             assert body["availabilityDomain"] == "Uocm:US-CHICAGO-1-AD-2"
+            assert body["createVnicDetails"]["subnetId"] == "ocid1.subnet.pre"  # the configured subnet
             return httpx.Response(200, json={"id": "ocid1.instance"})
         if req.url.host.startswith("identity.") and req.url.path.endswith("/availabilityDomains"):
             return httpx.Response(200, json=[{"name": "Uocm:US-CHICAGO-1-AD-1"}, {"name": "Uocm:US-CHICAGO-1-AD-2"}])
@@ -294,7 +295,9 @@ def test_oci_http_signature(rsa_pem):
     c = compute_class(BackendType.OCI)({"compartment_id": "comp"}, {"tenancy": "ten", "user": "usr",
                                                                       "fingerprint": "fp", "key_content": rsa_pem},
                                        _client(handler))
-    jpd = c.create_instance(_offer(c, "MI300X:8"), CFG)
+    offer = _offer(c, "MI300X:8")
+    c.config["subnet_ids"] = {offer.region: "ocid1.subnet.pre"}
+    jpd = c.create_instance(offer, CFG)
     c.update_provisioning_data(jpd)
     assert jpd.hostname == "140.1.1.1"
 

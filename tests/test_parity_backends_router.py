@@ -76,31 +76,12 @@ def test_config_values_on_valid_credentials(client, cloud_verdict, btype):
     assert r.json()["regions"]["values"] and len(cloud_verdict) == 1
 
 
-def test_oci_backend_not_created_if_regions_not_subscribed(client, monkeypatch):
-    from dstack_amd.core.backends.clouds.hyperscalers import OCICompute
-    from dstack_amd.utils.common import generate_rsa_key_pair
-
-    monkeypatch.delenv("DSTACK_SKIP_BACKEND_VALIDATION", raising=False)
-    asked = []
-
-    def signed(self, method, region, path, body=None, host=None):
-        asked.append((region, path))
-        req = httpx.Request(method, f"https://{host}{path}")
-        if path.endswith("/regionSubscriptions"):
-            return httpx.Response(200, json=[{"regionName": "us-chicago-1"}, {"regionName": "us-ashburn-1"}],
-                                  request=req)
-        return httpx.Response(200, json={"id": "ocid1.user"}, request=req)
-
-    monkeypatch.setattr(OCICompute, "_signed", signed)
-    private, _ = generate_rsa_key_pair()
-    body = json.loads(json.dumps(VALID["oci"]))
-    body["creds"]["key_content"] = private
-    body["regions"] = ["us-chicago-1", "eu-frankfurt-1"]
-    r = client.post("/api/project/main/backends/create", json=body)
+def test_oci_backend_not_created_if_regions_not_subscribed(client, fake_oci):
+    r = client.post("/api/project/main/backends/create", json=_oci_body(["us-chicago-1", "eu-frankfurt-1"]))
     assert r.status_code == 400 and "eu-frankfurt-1" in r.text and "not subscribed" in r.text, r.text
-    assert all(region == "us-chicago-1" for region, _ in asked)  # the key's home region answers
-    body["regions"] = ["us-chicago-1"]
-    assert client.post("/api/project/main/backends/create", json=body).status_code == 200
+    assert {region for _, region, _, _ in fake_oci.calls} == {"us-chicago-1"}  # the key's home region answers
+    assert not [c for c in fake_oci.calls if c[0] == "POST"]  # nothing created for a refused config
+    assert client.post("/api/project/main/backends/create", json=_oci_body(["us-chicago-1"])).status_code == 200
 
 
 def _project_id():
@@ -156,3 +137,119 @@ def test_yaml_create_update_and_get(client):
     assert r.status_code == 200, r.text
     got = yaml.safe_load(client.post("/api/project/main/backends/oci/get_yaml").json()["config_yaml"])
     assert got["type"] == "oci" and got["regions"] == ["us-ashburn-1"] and "creds" not in got
+
+
+class _FakeOCI:
+    """In-memory OCI control plane for the paths the backend uses (identity + core services)."""
+
+    def __init__(self):
+        self.calls = []
+        self.objs = {}  # kind -> list of dicts
+        self.n = 0
+
+    def _store(self, kind, region):
+        key = kind if kind == "compartments" else f"{region}/{kind}"
+        return self.objs.setdefault(key, [])
+
+    def _new(self, kind, body, region, state="PROVISIONING"):
+        self.n += 1
+        obj = {**body, "id": f"ocid1.{kind}.{self.n}", "lifecycleState": state}
+        if kind == "vcns":
+            obj["defaultRouteTableId"] = f"ocid1.rt.{self.n}"
+            obj["defaultSecurityListId"] = f"ocid1.sl.{self.n}"
+            self._store("routeTables", region).append({"id": obj["defaultRouteTableId"], "routeRules": [],
+                                                       "lifecycleState": "AVAILABLE"})
+            self._store("securityLists", region).append({"id": obj["defaultSecurityListId"],
+                                                         "lifecycleState": "AVAILABLE"})
+        self._store(kind, region).append(obj)
+        return obj
+
+    def __call__(self, comp, method, region, path, body=None, host=None):
+        from urllib.parse import parse_qsl, urlsplit
+
+        self.calls.append((method, region, path.split("?")[0], body))
+        u = urlsplit(path)
+        parts = u.path.split("/")[2:]  # drop "" and the API version
+        q = dict(parse_qsl(u.query))
+        req = httpx.Request(method, f"https://{host or 'iaas'}{path}")
+
+        def ok(obj, status=200):
+            return httpx.Response(status, json=obj, request=req)
+
+        kind = parts[0]
+        if kind == "users":
+            return ok({"id": parts[1]})
+        if kind == "tenancies":
+            return ok([{"regionName": "us-chicago-1"}, {"regionName": "us-ashburn-1"}])
+        if method == "GET" and len(parts) == 1:
+            items = self._store(kind, region)
+            name = q.get("displayName") or q.get("name")
+            for o in items:  # every object becomes AVAILABLE after one look
+                o["lifecycleState"] = "ACTIVE" if kind == "compartments" else "AVAILABLE"
+            return ok([o for o in items if name is None or o.get("displayName", o.get("name")) == name])
+        if method == "GET":
+            o = next(o for o in self._store(kind, region) if o["id"] == parts[1])
+            o["lifecycleState"] = "ACTIVE" if kind == "compartments" else "AVAILABLE"
+            return ok(o)
+        if method == "POST" and len(parts) == 1:
+            return ok(self._new(kind, body, region))
+        if method == "PUT":
+            o = next(o for o in self._store(kind, region) if o["id"] == parts[1])
+            o.update(body)
+            return ok(o)
+        raise AssertionError(f"unexpected OCI call {method} {path}")
+
+
+@pytest.fixture
+def fake_oci(monkeypatch):
+    from dstack_amd.core.backends.clouds.hyperscalers import OCICompute
+
+    monkeypatch.delenv("DSTACK_SKIP_BACKEND_VALIDATION", raising=False)
+    monkeypatch.setattr(OCICompute, "WAIT_S", 5.0)
+    monkeypatch.setattr(OCICompute, "WAIT_POLL_S", 0.0)
+    fake = _FakeOCI()
+    monkeypatch.setattr(OCICompute, "_signed", lambda self, *a, **k: fake(self, *a, **k))
+    return fake
+
+
+def _oci_body(regions):
+    from dstack_amd.utils.common import generate_rsa_key_pair
+
+    body = json.loads(json.dumps(VALID["oci"]))
+    body["creds"]["key_content"] = generate_rsa_key_pair()[0]
+    body["regions"] = regions
+    return body
+
+
+def test_oci_backend_creation_bootstraps_the_network(client, fake_oci):
+    """(verdict: OCI network bootstrap; reference ``oci/resources.py:427-690``) creating the backend
+    creates the compartment, and per region the VCN, internet gateway, default route, security
+    rules and a subnet; their ids are stored in the backend's config."""
+    r = client.post("/api/project/main/backends/create", json=_oci_body(["us-chicago-1"]))
+    assert r.status_code == 200, r.text
+    posts = [p for m, _, p, _ in fake_oci.calls if m == "POST"]
+    assert posts == ["/20160918/compartments", "/20160918/vcns", "/20160918/internetGateways", "/20160918/subnets"]
+    objs = {k.split("/")[-1]: v for k, v in fake_oci.objs.items()}  # one region here
+    rt = objs["routeTables"][0]["routeRules"]
+    assert rt == [{"destination": "0.0.0.0/0", "destinationType": "CIDR_BLOCK",
+                   "networkEntityId": objs["internetGateways"][0]["id"]}]
+    ingress = objs["securityLists"][0]["ingressSecurityRules"]
+    assert {"protocol": "all", "source": "10.0.0.0/16"} in ingress  # node-to-node (RCCL) traffic
+    assert any(x.get("tcpOptions", {}).get("destinationPortRange") == {"min": 22, "max": 22} for x in ingress)
+    info = client.post("/api/project/main/backends/oci/config_info").json()
+    assert info["compartment_id"] == fake_oci.objs["compartments"][0]["id"]
+    assert info["subnet_ids"] == {"us-chicago-1": objs["subnets"][0]["id"]}
+
+
+def test_oci_network_bootstrap_is_idempotent_and_lazy_for_new_regions(fake_oci):
+    from dstack_amd.core.backends.clouds.hyperscalers import OCICompute
+
+    auth = {"user": "u", "tenancy": "t", "fingerprint": "f", "region": "us-chicago-1", "key_content": "k"}
+    comp = OCICompute({"regions": ["us-chicago-1"]}, auth, None)
+    first = comp.ensure_network("us-chicago-1")
+    n_posts = sum(1 for m, *_ in fake_oci.calls if m == "POST")
+    again = OCICompute({"regions": ["us-chicago-1"]}, auth, None).ensure_network("us-chicago-1")
+    assert again == first and sum(1 for m, *_ in fake_oci.calls if m == "POST") == n_posts
+    # a region without a recorded subnet gets its own VCN + subnet at launch
+    assert comp.ensure_network("us-ashburn-1") != first
+    assert set(comp.config["subnet_ids"]) == {"us-chicago-1", "us-ashburn-1"}
