@@ -125,10 +125,61 @@ def build(verbose: bool = False, keep_asm: bool = False, force: bool = False) ->
             if verbose and out:
                 print(out, file=sys.stderr)
     so = so_path()
+    linked = False
     if force or jobs or not is_current():
         _run(link)
         so_stamp_path().write_text(so_digest + "\n")
+        linked = True
+    _write_manifest(so, so_digest, [Path(j[0]).stem for j in jobs], [Path(u[0]).stem for u in units], linked)
     return so
+
+
+def manifest_path() -> Path:
+    return so_path().with_name("_C.manifest.json")
+
+
+def _write_manifest(so: Path, so_digest: str, compiled, units, linked: bool):
+    """Build provenance next to the .so: which sources/flags it was linked from (``source_digest``),
+    the binary's own hash, and what this build call compiled versus reused from the
+    content-addressed cache.  ``verify_loaded`` checks it against the library a process mapped."""
+    import datetime
+    import hashlib
+    import json
+    import platform
+
+    prev = {}
+    if manifest_path().exists():
+        try:
+            prev = json.loads(manifest_path().read_text())
+        except ValueError:
+            prev = {}
+    ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.splitlines()
+    m = {
+        "so": so.name, "so_sha256": hashlib.sha256(so.read_bytes()).hexdigest(), "source_digest": so_digest,
+        "arch": ARCH, "hipcc": next((x for x in ver if "HIP version" in x), ver[0] if ver else ""),
+        "units": units, "compiled_now": compiled, "linked_now": linked,
+        "built_at": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds")
+        if (compiled or linked or not prev) else prev.get("built_at"),
+        "built_on": platform.node() if (compiled or linked or not prev) else prev.get("built_on"),
+    }
+    manifest_path().write_text(json.dumps(m, indent=1) + "\n")
+
+
+def verify_loaded(loaded_so: str) -> dict:
+    """Provenance of the extension a process actually loaded: its hash must equal the manifest's,
+    and the manifest's source digest must equal the digest of the kernel sources in this tree --
+    i.e. the running kernels were compiled from exactly these sources.  Raises otherwise."""
+    import hashlib
+    import json
+
+    m = json.loads(manifest_path().read_text())
+    got = hashlib.sha256(Path(loaded_so).read_bytes()).hexdigest()
+    if got != m["so_sha256"]:
+        raise RuntimeError(f"{loaded_so}: binary differs from the build manifest ({got[:12]} vs {m['so_sha256'][:12]})")
+    _, _, digest = _plan()
+    if m["source_digest"] != digest:
+        raise RuntimeError(f"{loaded_so} was built from other kernel sources than this tree's: rebuild")
+    return m
 
 
 def main():

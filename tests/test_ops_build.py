@@ -32,3 +32,26 @@ def test_built_extension_is_current():
     if not build.so_path().exists():
         pytest.skip("extension not built in this checkout")
     assert build.is_current(), "the .so does not match the current kernel sources: rebuild"
+
+
+def test_manifest_records_provenance_and_detects_foreign_binaries(tmp_path, monkeypatch):
+    """The manifest next to the .so ties the binary to the kernel sources of this tree; a binary
+    that is not the one the manifest describes, or a manifest for other sources, is refused."""
+    import json
+    import shutil
+
+    if not build.so_path().exists() or not build.manifest_path().exists():
+        pytest.skip("extension not built in this checkout")
+    m = build.verify_loaded(str(build.so_path()))
+    assert m["arch"] == "gfx950" and set(m["units"]) >= {"flash_attn", "elementwise", "bindings"}
+    fake = tmp_path / "_C.so"
+    shutil.copy(build.so_path(), fake)
+    with open(fake, "ab") as f:
+        f.write(b"\0")
+    with pytest.raises(RuntimeError, match="differs from the build manifest"):
+        build.verify_loaded(str(fake))
+    other = dict(m, source_digest="0" * 64)
+    monkeypatch.setattr(build, "manifest_path", lambda: tmp_path / "m.json")
+    (tmp_path / "m.json").write_text(json.dumps(other))
+    with pytest.raises(RuntimeError, match="other kernel sources"):
+        build.verify_loaded(str(build.so_path()))
