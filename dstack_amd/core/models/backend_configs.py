@@ -275,3 +275,51 @@ def split_backend_config(raw: dict) -> Tuple[str, dict, dict]:
             else:
                 secrets[k] = v
     return btype, data, secrets
+
+
+# ---- form descriptors for the web UI ------------------------------------------------------------
+def _describe(name: str, annotation, required: bool) -> dict:
+    """A small, UI-friendly description of one config field (the JSON schema's $ref/anyOf forms are
+    more than a form renderer needs): str | int | bool | list | map | object | union."""
+    import typing
+
+    origin, args = typing.get_origin(annotation), typing.get_args(annotation)
+    if origin is typing.Annotated:
+        return _describe(name, args[0], required)
+    if origin is Union and type(None) in args:
+        rest = [a for a in args if a is not type(None)]
+        return _describe(name, rest[0] if len(rest) == 1 else Union[tuple(rest)], False)
+    if origin is Union:
+        variants = []
+        for a in args:
+            tf = a.model_fields["type"]
+            variants.append({"type": tf.default, "fields": _model_fields(a)})
+        return {"name": name, "kind": "union", "required": required, "variants": variants}
+    if origin in (list, List):
+        return {"name": name, "kind": "list", "required": required}
+    if origin in (dict, Dict):
+        return {"name": name, "kind": "map", "required": required}
+    if isinstance(annotation, type) and issubclass(annotation, CoreModel):
+        return {"name": name, "kind": "object", "required": required, "fields": _model_fields(annotation)}
+    kind = {bool: "bool", int: "int", float: "float"}.get(annotation, "str")
+    return {"name": name, "kind": kind, "required": required}
+
+
+def _model_fields(cls) -> List[dict]:
+    out = []
+    for n, f in cls.model_fields.items():
+        if n == "type":
+            continue
+        d = _describe(n, f.annotation, f.is_required())
+        if f.description:
+            d["help"] = f.description
+        out.append(d)
+    return out
+
+
+def backend_form_schema() -> Dict[str, List[dict]]:
+    """{backend type: [field descriptor]} for every configurable backend (web UI forms)."""
+    import typing
+
+    union = typing.get_args(typing.get_args(AnyBackendConfig)[0])
+    return {cls.model_fields["type"].default: _model_fields(cls) for cls in union}

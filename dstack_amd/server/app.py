@@ -215,6 +215,19 @@ def register_routes(app: FastAPI):
         """Web UI (single page over the REST API)."""
         return HTMLResponse(ui_index.read_text() if ui_index.exists() else "<h3>dstack-amd</h3>")
 
+    ui_assets = {p.name: p for p in (Path(__file__).parent / "ui" / "js").glob("*.js")}
+
+    @app.get("/ui/js/{name}", include_in_schema=False)
+    def ui_asset(name: str):
+        """The UI's script modules (a fixed whitelist: the files shipped in ``server/ui/js``)."""
+        from fastapi.responses import PlainTextResponse
+
+        p = ui_assets.get(name)
+        if p is None:
+            return PlainTextResponse("not found", status_code=404)
+        return PlainTextResponse(p.read_text(), media_type="text/javascript",
+                                 headers={"Cache-Control": "no-cache"})
+
     @app.get("/metrics", include_in_schema=False)
     def prometheus_metrics():
         """Prometheus exposition (DSTACK_ENABLE_PROMETHEUS_METRICS=0 disables it)."""

@@ -141,6 +141,14 @@ def backend_config_values(body: dict, user: UserModel = Depends(authenticated)) 
     return backends_services.backend_config_values(body)
 
 
+@backends_router.post("/form_schema")
+def backend_form_schema(user: UserModel = Depends(authenticated)) -> dict:
+    """Field descriptors of every configurable backend type (the web UI builds its forms from them)."""
+    from dstack_amd.core.models.backend_configs import backend_form_schema as schema
+
+    return schema()
+
+
 @project_backends_router.post("/create")
 def create_backend(body: dict, up: UP = Depends(project_admin), s: Session = Depends(get_session, scope="function")) -> dict:
     backends_services.create_backend(s, up[1], body)

@@ -1,0 +1,123 @@
+// Projects (members, backends: form built from the server's field descriptors with a credentials
+// check and region picker, or YAML), users, secrets.
+Object.assign(VIEWS, {
+  async projects(name, tab) {
+    if (name) return VIEWS.project(name, tab);
+    const p = await api("/api/projects/list");
+    $("#main").innerHTML = `<h3>Projects</h3>` + table(["project", "owner", "members", "backends"], p.map(x => [esc(x.project_name),
+      esc(x.owner.username), x.members.map(m => `${esc(m.user.username)} (${esc(m.project_role)})`).join(", "), (x.backends || []).map(b => esc(b.name || b)).join(", ")]), true) +
+      `<div class="row"><input id="np" placeholder="new project"><button id="cp">Create</button></div>`;
+    bindRows(p, x => location.hash = "#projects/" + encodeURIComponent(x.project_name));
+    $("#cp").onclick = () => api("/api/projects/create", { project_name: $("#np").value }).then(() => boot()).catch(e => alert(e.message));
+  },
+
+  async project(name, tab = "members") {
+    const p = await api(`/api/projects/${encodeURIComponent(name)}/get`);
+    $("#main").innerHTML = `<h3><a href="#projects" class="muted">projects</a> / ${esc(name)}</h3>
+      <div class="muted">owner ${esc(p.owner.username)} · created ${ago(p.created_at)}</div>
+      ${tabs("ptabs", ["members", "backends", "settings"], tab)}<div id="tab"></div>`;
+    bindTabs("ptabs", t => location.hash = `#projects/${encodeURIComponent(name)}/${t}`);
+    return (PROJECT_TABS[tab] || PROJECT_TABS.members)(p, name);
+  },
+
+  async users(name) {
+    if (name) return VIEWS.user(name);
+    const u = await api("/api/users/list");
+    $("#main").innerHTML = `<h3>Users</h3>` + table(["user", "role", "email", "active", "created", ""], u.map(x => [
+      `<a href="#users/${encodeURIComponent(x.username)}">${esc(x.username)}</a>`, esc(x.global_role), esc(x.email), x.active ? "yes" : "no", ago(x.created_at),
+      `<a data-u="${esc(x.username)}" class="tok muted">[new token]</a> <a data-u="${esc(x.username)}" data-r="${x.global_role === "admin" ? "user" : "admin"}" class="role muted">[make ${x.global_role === "admin" ? "user" : "admin"}]</a> <a data-u="${esc(x.username)}" class="delu muted">[delete]</a>`])) +
+      `<div class="row"><input id="nu" placeholder="username"><input id="ne" placeholder="email (optional)"><select id="nr"><option>user</option><option>admin</option></select><button id="cu">Create</button><span id="tok" class="muted"></span></div>`;
+    $("#cu").onclick = () => api("/api/users/create", { username: $("#nu").value, global_role: $("#nr").value, email: $("#ne").value || null })
+      .then(d => { $("#tok").textContent = "token: " + d.creds.token; }).catch(e => alert(e.message));
+    $$("a.tok").forEach(a => a.onclick = () => api("/api/users/refresh_token", { username: a.dataset.u })
+      .then(d => alert(`new token for ${a.dataset.u}: ${d.creds.token}`)).catch(e => alert(e.message)));
+    $$("a.role").forEach(a => a.onclick = () => act(() => api("/api/users/update", { username: a.dataset.u, global_role: a.dataset.r })));
+    $$("a.delu").forEach(a => a.onclick = () => act(() => api("/api/users/delete", { users: [a.dataset.u] }), `Delete user ${a.dataset.u}?`));
+  },
+  async user(name) {
+    const u = await api("/api/users/get_user", { username: name });
+    const projects = await api("/api/projects/list");
+    const mine = projects.filter(p => p.members.some(m => m.user.username === name));
+    $("#main").innerHTML = `<h3><a href="#users" class="muted">users</a> / ${esc(name)}</h3>` +
+      table(["field", "value"], [["global role", esc(u.global_role)], ["email", esc(u.email || "")], ["active", u.active ? "yes" : "no"], ["created", ago(u.created_at)]]) +
+      `<div class="row"><input id="ue" placeholder="email" value="${esc(u.email || "")}"><label><input type="checkbox" id="ua" ${u.active ? "checked" : ""}> active</label>
+        <button id="us">Save</button></div><h4>Projects</h4>` +
+      table(["project", "role"], mine.map(p => [`<a href="#projects/${encodeURIComponent(p.project_name)}">${esc(p.project_name)}</a>`,
+        esc(p.members.find(m => m.user.username === name).project_role)]));
+    $("#us").onclick = () => act(() => api("/api/users/update", { username: name, global_role: u.global_role, email: $("#ue").value || null, active: $("#ua").checked }));
+  },
+
+  async secrets() {
+    const s = await api(P("secrets/list"));
+    $("#main").innerHTML = `<h3>Secrets <span class="muted">${esc(S.project)}</span></h3>` + table(["name", ""], s.map(x => [esc(x.name), `<a data-s="${esc(x.name)}" class="dels muted">[delete]</a>`])) +
+      `<div class="row"><input id="sn" placeholder="NAME"><input id="sv" placeholder="value" type="password"><button id="sa">Add / update</button></div>
+      <p class="muted">Secrets are interpolated into runs as <code>\${{ secrets.NAME }}</code> and encrypted at rest.</p>`;
+    $("#sa").onclick = () => api(P("secrets/add"), { name: $("#sn").value, value: $("#sv").value }).then(() => route()).catch(e => alert(e.message));
+    $$("a.dels").forEach(a => a.onclick = () => act(() => api(P("secrets/delete"), { secrets_names: [a.dataset.s] }), `Delete secret ${a.dataset.s}?`));
+  },
+});
+
+const PROJECT_TABS = {
+  members(p, name) {
+    const roles = ["admin", "manager", "user"];
+    const memberRow = (u = "", r = "user") => `<div class="row mrow"><input class="mu" value="${esc(u)}" placeholder="username">
+      <select class="mr">${roles.map(x => `<option ${x === r ? "selected" : ""}>${x}</option>`).join("")}</select><a class="muted rm">[remove]</a></div>`;
+    $("#tab").innerHTML = `<div id="members">${p.members.map(m => memberRow(m.user.username, m.project_role)).join("")}</div>
+      <div class="row"><button id="addm">Add member</button><button class="primary" id="savem">Save members</button></div>`;
+    const bindRm = () => $$("a.rm").forEach(a => a.onclick = () => a.closest(".mrow").remove());
+    bindRm();
+    $("#addm").onclick = () => { $("#members").insertAdjacentHTML("beforeend", memberRow()); bindRm(); };
+    $("#savem").onclick = () => act(() => api(`/api/projects/${encodeURIComponent(name)}/set_members`, { members:
+      $$(".mrow").map(r => ({ username: r.querySelector(".mu").value.trim(), project_role: r.querySelector(".mr").value })).filter(m => m.username) }));
+  },
+
+  async backends(p, name) {
+    const B = (x) => `/api/project/${encodeURIComponent(name)}/backends/${x}`;
+    const schema = await api("/api/backends/form_schema");
+    const types = Object.keys(schema).filter(t => t !== "dstack");
+    $("#tab").innerHTML = table(["backend", "settings", ""], (p.backends || []).map(b => [esc(b.name), esc(JSON.stringify(b.config || {})).slice(0, 160),
+        `<a data-b="${esc(b.name)}" class="yb muted">[yaml]</a> <a data-b="${esc(b.name)}" class="delb muted">[delete]</a>`])) +
+      `<h4>Add a backend</h4><div class="row"><select id="bt">${types.map(t => `<option>${esc(t)}</option>`).join("")}</select>
+        <label class="muted"><input type="checkbox" id="asyaml"> as YAML</label></div>
+      <div id="bform"></div><div class="row"><button id="chk">Check credentials & list regions</button><button class="primary" id="addb">Add backend</button>
+        <span id="berr" class="err"></span></div><div id="bregions"></div>`;
+    const renderForm = () => {
+      if ($("#asyaml").checked) {
+        $("#bform").innerHTML = `<textarea id="by" rows="8" cols="70" placeholder="type: vultr&#10;regions: [ewr]&#10;creds:&#10;  type: api_key&#10;  api_key: ..."></textarea>`;
+      } else { $("#bform").innerHTML = formFields(schema[$("#bt").value]); bindForm($("#bform")); }
+      $("#bregions").innerHTML = ""; $("#berr").textContent = "";
+    };
+    const current = () => {
+      const conf = readForm($("#bform"), $("#bt").value);
+      const picked = $$("#bregions input:checked").map(x => x.value);
+      if (picked.length) conf[$("#bt").value === "azure" ? "locations" : "regions"] = picked;
+      return conf;
+    };
+    $("#bt").onchange = renderForm; $("#asyaml").onchange = renderForm; renderForm();
+    $("#chk").onclick = async () => {
+      $("#berr").textContent = ""; $("#bregions").innerHTML = "…";
+      try {
+        const v = await api("/api/backends/config_values", current());
+        $("#bregions").innerHTML = `<p class="muted">credentials ok${v.default_creds ? " · default credentials available" : ""} — regions:</p>` +
+          v.regions.values.map(r => `<label class="chip"><input type="checkbox" value="${esc(r.value)}" ${v.regions.selected.includes(r.value) ? "checked" : ""}> ${esc(r.label)}</label>`).join(" ");
+      } catch (e) { $("#bregions").innerHTML = ""; $("#berr").textContent = e.message; }
+    };
+    $("#addb").onclick = () => act(() => $("#asyaml").checked ? api(B("create_yaml"), { config_yaml: $("#by").value }) : api(B("create"), current()))
+      .then(() => { location.hash = `#projects/${encodeURIComponent(name)}/backends`; });
+    $$("a.delb").forEach(a => a.onclick = () => act(() => api(B("delete"), { backends_names: [a.dataset.b] }), `Delete backend ${a.dataset.b}?`));
+    $$("a.yb").forEach(a => a.onclick = async () => {
+      const y = await api(B(`${encodeURIComponent(a.dataset.b)}/get_yaml`));
+      $("#asyaml").checked = true; renderForm(); $("#by").value = y.config_yaml;
+      $("#addb").textContent = "Update backend";
+      $("#addb").onclick = () => act(() => api(B("update_yaml"), { config_yaml: $("#by").value }));
+    });
+  },
+
+  settings(p, name) {
+    $("#tab").innerHTML = `<h4>Default gateway</h4><p class="muted">Set on the <a href="#gateways">gateways</a> page.</p>
+      <h4>SSH key</h4><pre>${esc(p.ssh_public_key || "(hidden)")}</pre>
+      <h4>Danger zone</h4><button id="delp">Delete project</button>`;
+    $("#delp").onclick = () => act(() => api("/api/projects/delete", { projects_names: [name] }).then(() => { location.hash = "#projects"; return boot(); }),
+      `Delete project ${name} and its runs, fleets and volumes?`);
+  },
+};

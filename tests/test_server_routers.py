@@ -226,19 +226,54 @@ def test_unknown_project(client, path):
     assert client.post(path, json={"run_name": "x"}).status_code in (403, 404, 400)
 
 
+def _ui_text(client):
+    """index.html plus every script module it loads."""
+    import re
+
+    html = client.get("/").text
+    mods = re.findall(r'<script src="(/ui/js/[a-z]+\.js)"', html)
+    assert mods, "no UI modules referenced"
+    parts = [html]
+    for m in mods:
+        r = client.get(m)
+        assert r.status_code == 200 and r.headers["content-type"].startswith("text/javascript"), m
+        parts.append(r.text)
+    return "\n".join(parts)
+
+
 def test_web_ui_served(client):
     r = client.get("/")
-    assert r.status_code == 200 and "dstack-amd" in r.text and "/api/runs/list" in r.text
+    assert r.status_code == 200 and "dstack-amd" in r.text
+    assert client.get("/ui/js/../../app.py").status_code == 404  # only the shipped modules
+    text = _ui_text(client)
+    assert "/api/runs/list" in text
     # management views over the same API: instances, members editor, backends from YAML, metrics charts
     for needle in ("/api/instances/list", "set_members", "backends/${x}", "create_yaml", "metrics/job/", "prev_run_id",
-                   "fleets/delete_instances", "users/refresh_token"):
-        assert needle in r.text, needle
+                   "fleets/delete_instances", "users/refresh_token", "form_schema", "config_values", "descending: true",
+                   "fleet_ids", "job_submissions"):
+        assert needle in text, needle
+
+
+def test_web_ui_calls_only_existing_routes(client):
+    """Every REST path the UI modules call is a route of the app (project-scoped ``P("...")``
+    paths under ``/api/project/{project_name}/``)."""
+    import re
+
+    text = _ui_text(client)
+    routes = set(client.get("/api/openapi.json").json()["paths"])
+    called = set(re.findall(r'P\(["`]([a-z_]+/[a-z_]+)', text)) - {"metrics/job"}  # GET .../metrics/job/{run_name}
+    assert "/api/project/{project_name}/metrics/job/{run_name}" in routes
+    missing = [c for c in called if f"/api/project/{{project_name}}/{c}" not in routes]
+    assert called and not missing, missing
+    absolute = set(re.findall(r'api\(["`](/api/[a-z_/]+)["`]', text))
+    missing = [c for c in absolute if c not in routes]
+    assert absolute and not missing, missing
 
 
 def test_web_ui_apply_and_offers_request_shapes(client):
     """The UI's apply / offers / fleet pages: YAML -> configurations/parse -> get_plan -> apply with
     exactly the payloads index.html builds."""
-    html = client.get("/").text
+    html = _ui_text(client)
     for needle in ("configurations/parse", "runs/get_plan", "runs/apply", "fleets/get_plan", "fleets/get",
                    "spot_policy", "bytes_per_s"):
         assert needle in html, needle
