@@ -188,8 +188,11 @@ def get_shim_commands(authorized_keys: List[str], shim_url: str, runner_url: str
     ]
 
 
-def get_user_data(authorized_keys: List[str], shim_url: str, runner_url: str) -> str:
-    cmds = get_shim_commands(authorized_keys, shim_url, runner_url)
+def get_user_data(authorized_keys: List[str], shim_url: str, runner_url: str,
+                  backend_commands: Optional[List[str]] = None) -> str:
+    """cloud-config: authorized keys, then the cloud's own host setup (``backend_commands``, e.g.
+    opening the VPC subnet in the host firewall), then the shim bootstrap."""
+    cmds = list(backend_commands or []) + get_shim_commands(authorized_keys, shim_url, runner_url)
     keys = "\n".join(f"  - {json_quote(k)}" for k in authorized_keys)  # a YAML-safe scalar whatever the comment
     runcmd = "\n".join(f"  - {json_quote(c)}" for c in cmds)
     return f"#cloud-config\nssh_authorized_keys:\n{keys}\nruncmd:\n{runcmd}\n"

@@ -49,9 +49,9 @@ def agent_urls() -> Tuple[str, str]:
             os.getenv("DSTACK_RUNNER_DOWNLOAD_URL", DEFAULT_RUNNER_URL))
 
 
-def cloud_init(instance_config: InstanceConfiguration) -> str:
+def cloud_init(instance_config: InstanceConfiguration, backend_commands: Optional[List[str]] = None) -> str:
     shim, runner = agent_urls()
-    return get_user_data(instance_config.get_public_keys(), shim, runner)
+    return get_user_data(instance_config.get_public_keys(), shim, runner, backend_commands)
 
 
 def container_commands(authorized_keys: List[str]) -> List[str]:
@@ -204,14 +204,18 @@ class ProvisioningFailed(ComputeError):
 # ---------------------------------------------------------------------------------------------
 # request signing
 # ---------------------------------------------------------------------------------------------
-def rsa_sha256_sign(private_key_pem: str, data: bytes) -> bytes:
-    """RSA PKCS#1 v1.5 / SHA-256 signature with the system ``openssl`` (no crypto wheel needed)."""
+def rsa_sha256_sign(private_key_pem: str, data: bytes, pss: bool = False) -> bytes:
+    """RSA / SHA-256 signature with the system ``openssl`` (no crypto wheel needed): PKCS#1 v1.5, or
+    PSS with a digest-length salt (JWT ``PS256``) when ``pss``."""
     with tempfile.NamedTemporaryFile("w", delete=False, suffix=".pem") as f:
         f.write(private_key_pem)
         key_path = f.name
     try:
         os.chmod(key_path, 0o600)
-        r = subprocess.run(["openssl", "dgst", "-sha256", "-sign", key_path], input=data, capture_output=True)
+        cmd = ["openssl", "dgst", "-sha256", "-sign", key_path]
+        if pss:
+            cmd += ["-sigopt", "rsa_padding_mode:pss", "-sigopt", "rsa_pss_saltlen:-1"]
+        r = subprocess.run(cmd, input=data, capture_output=True)
         if r.returncode != 0:
             raise BackendAuthError(f"openssl signing failed: {r.stderr.decode()[-300:]}")
         return r.stdout

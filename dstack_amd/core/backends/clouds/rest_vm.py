@@ -164,16 +164,39 @@ class VultrCompute(VMCompute):
                                     availability=_AVAILABLE if plan["id"] in stock[loc] else _NOT_AVAILABLE))
         return rows
 
+    def _ensure_vpc(self, region: str) -> dict:
+        """The region's dstack VPC (get or create): every instance and bare-metal node launches
+        into it, so the nodes of a cluster reach each other privately (RCCL bootstrap, torchrun
+        rendezvous) -- the public interface only carries SSH."""
+        name = f"dstack-vpc-{region}"
+        for vpc in self._list("vpcs", "vpcs"):
+            if vpc.get("description") == name and vpc.get("region") in (None, region):
+                return vpc
+        return check_response(self.http.post(f"{self.API}/vpcs", headers=self._h(),
+                                             json={"region": region, "description": name}), "vultr create vpc").json()["vpc"]
+
     def _launch(self, offer, cfg):
         kind = self._kind(offer.instance.name)
+        vpc = self._ensure_vpc(offer.region)
+        subnet = f"{vpc.get('v4_subnet')}/{vpc.get('v4_subnet_mask')}" if vpc.get("v4_subnet") else None
+        # Vultr images ship ufw enabled: let the VPC subnet in (no-op where ufw is absent)
+        host_cmds = [f"command -v ufw >/dev/null && ufw allow from {subnet} && ufw reload || true"] if subnet else []
+        image = self.config.get("images") or {}
         body = {"region": offer.region, "plan": offer.instance.name, "label": cfg.instance_name,
-                "os_id": self.UBUNTU_22_OS_ID, "user_data": base64.b64encode(cloud_init(cfg).encode()).decode(),
-                "tags": ["dstack", cfg.project_name]}
+                "user_data": base64.b64encode(cloud_init(cfg, host_cmds).encode()).decode(),
+                "tags": ["dstack", cfg.project_name], "attach_vpc": [vpc["id"]]}
+        # the OS: Ubuntu 22.04 unless ``images.{instance,bare_metal}`` names an OS id (digits) or a
+        # marketplace image (e.g. a ROCm image for the AMD bare-metal plans)
+        img = str(image.get("bare_metal" if kind == "bare-metals" else "instance") or self.UBUNTU_22_OS_ID)
+        if img.isdigit():
+            body["os_id"] = int(img)
+        else:
+            body["image_id"] = img
         if kind == "instances":
             body["backups"] = "disabled"
         r = check_response(self.http.post(f"{self.API}/{kind}", headers=self._h(), json=body), "vultr create")
         key = "bare_metal" if kind == "bare-metals" else "instance"
-        return r.json()[key]["id"], None, {"kind": kind}
+        return r.json()[key]["id"], None, {"kind": kind, "vpc_id": vpc["id"], "vpc_subnet": subnet}
 
     def _describe(self, instance_id, region, backend_data):
         kind = backend_data.get("kind", "instances")
@@ -184,7 +207,14 @@ class VultrCompute(VMCompute):
         d = d.get("bare_metal") or d.get("instance") or {}
         ip = d.get("main_ip")
         ready = d.get("status") == "active" and ip and ip != "0.0.0.0"
-        return {"status": d.get("status"), "hostname": ip if ready else None, "internal_ip": d.get("internal_ip")}
+        internal = d.get("internal_ip") or None
+        if ready and not internal and backend_data.get("vpc_id"):
+            # the node's address in the dstack VPC is what its cluster peers connect to
+            v = self.http.get(f"{self.API}/{kind}/{instance_id}/vpcs", headers=self._h())
+            if v.status_code == 200:
+                internal = next((x.get("ip_address") for x in v.json().get("vpcs") or []
+                                 if x.get("id") == backend_data["vpc_id"]), None)
+        return {"status": d.get("status"), "hostname": ip if ready else None, "internal_ip": internal}
 
     def _terminate(self, instance_id, region, backend_data):
         kind = backend_data.get("kind", "instances")
@@ -413,13 +443,54 @@ class DataCrunchCompute(VMCompute):
 
 
 class NebiusCompute(VMCompute):
-    """Nebius AI cloud (REST gateway with a static IAM token; the reference's nebius backend)."""
+    """Nebius AI cloud REST gateway (the reference's nebius backend).  Credentials: a service-account
+    authorized key (``service_account`` creds: the key JSON with ``id``, ``service_account_id`` and
+    ``private_key``), exchanged for short-lived IAM tokens with a PS256-signed JWT and cached until
+    shortly before expiry; or a pre-issued IAM token."""
 
     TYPE = BackendType.NEBIUS
     API = "https://compute.api.nebius.cloud/compute/v1"
+    IAM_TOKENS = "https://iam.api.nebius.cloud/iam/v1/tokens"
+
+    def __init__(self, config, auth, client=None):
+        super().__init__(config, auth, client)
+        self._token = OAuthToken(self._exchange_sa_key)
+
+    def _sa_key(self) -> Optional[dict]:
+        import json
+
+        data = self.auth.get("data")
+        if not data:
+            return None
+        try:
+            key = json.loads(data)
+        except ValueError as e:
+            raise BackendAuthError(f"nebius service account key is not JSON: {e}") from None
+        if not all(k in key for k in ("id", "service_account_id", "private_key")):
+            raise BackendAuthError("nebius service account key needs id, service_account_id and private_key")
+        return key
+
+    def _exchange_sa_key(self):
+        import json
+        import time as _time
+
+        from dstack_amd.core.backends.clouds.common import b64url, rsa_sha256_sign
+
+        key = self._sa_key()
+        now = int(_time.time())
+        header = {"typ": "JWT", "alg": "PS256", "kid": key["id"]}
+        claims = {"aud": self.IAM_TOKENS, "iss": key["service_account_id"], "iat": now, "exp": now + 3600}
+        signing_input = f"{b64url(json.dumps(header).encode())}.{b64url(json.dumps(claims).encode())}"
+        sig = rsa_sha256_sign(key["private_key"], signing_input.encode(), pss=True)
+        r = self.http.post(self.IAM_TOKENS, json={"jwt": f"{signing_input}.{b64url(sig)}"})
+        if r.status_code in (400, 401, 403):
+            raise BackendAuthError(f"nebius token exchange: {r.status_code} {r.text[:200]}")
+        d = check_response(r, "nebius token exchange").json()
+        return d["iamToken"], 3600
 
     def _h(self):
-        return {"Authorization": f"Bearer {self.auth.get('iam_token') or self.auth.get('token', '')}"}
+        static = self.auth.get("iam_token") or self.auth.get("token")
+        return {"Authorization": f"Bearer {static or self._token.get()}"}
 
     def check_credentials(self) -> None:
         check_response(self.http.get(f"{self.API}/instances", params={"folderId": self.config.get("folder_id"),

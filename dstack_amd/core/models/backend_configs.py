@@ -165,6 +165,7 @@ class LambdaConfig(_Input):
 class VultrConfig(_Input):
     type: Literal["vultr"] = "vultr"
     regions: Optional[List[str]] = None
+    images: Optional[Dict[str, str]] = None  # {"instance" | "bare_metal": os id or marketplace image id}
     creds: APIKeyCreds
 
 

@@ -111,16 +111,31 @@ def test_aws_capacity_error():
 
 # ---- Vultr (MI355X bare metal) -----------------------------------------------------------------
 def test_vultr_mi355x_bare_metal():
+    """Bare-metal MI355X node: launched into the region's dstack VPC (created once, reused), the
+    host firewall opened to the VPC subnet, and the node's VPC address reported as its internal IP
+    (what cluster peers use for RCCL / torchrun)."""
     state = {"status": "pending"}
+    vpcs, posts = [], []
 
     def handler(req):
         assert req.headers["authorization"] == "Bearer vk"
+        if req.url.path == "/v2/vpcs":
+            if req.method == "POST":
+                body = json.loads(req.content)
+                vpcs.append({"id": "vpc-1", "region": body["region"], "description": body["description"],
+                             "v4_subnet": "10.40.96.0", "v4_subnet_mask": 20})
+                return httpx.Response(201, json={"vpc": vpcs[-1]})
+            return httpx.Response(200, json={"vpcs": vpcs, "meta": {"links": {"next": ""}}})
         if req.method == "POST" and req.url.path == "/v2/bare-metals":
             body = json.loads(req.content)
-            assert body["plan"].endswith("mi355x-gpu")
-            assert "dstack-shim" in base64.b64decode(body["user_data"]).decode()
-            return httpx.Response(202, json={"bare_metal": {"id": "bm-1"}})
-        if req.method == "GET" and req.url.path == "/v2/bare-metals/bm-1":
+            posts.append(body)
+            assert body["plan"].endswith("mi355x-gpu") and body["attach_vpc"] == ["vpc-1"]
+            ud = base64.b64decode(body["user_data"]).decode()
+            assert "dstack-shim" in ud and "ufw allow from 10.40.96.0/20" in ud
+            return httpx.Response(202, json={"bare_metal": {"id": f"bm-{len(posts)}"}})
+        if req.method == "GET" and req.url.path.endswith("/vpcs"):
+            return httpx.Response(200, json={"vpcs": [{"id": "vpc-1", "ip_address": "10.40.96.3"}]})
+        if req.method == "GET" and req.url.path.startswith("/v2/bare-metals/bm-"):
             return httpx.Response(200, json={"bare_metal": {"status": state["status"], "main_ip": "5.5.5.5"}})
         if req.method == "DELETE":
             return httpx.Response(204)
@@ -134,8 +149,43 @@ def test_vultr_mi355x_bare_metal():
     assert jpd.hostname is None  # not active yet
     state["status"] = "active"
     c.update_provisioning_data(jpd)
-    assert jpd.hostname == "5.5.5.5" and jpd.username == "root"
+    assert jpd.hostname == "5.5.5.5" and jpd.username == "root" and jpd.internal_ip == "10.40.96.3"
+    c.create_instance(offer, CFG)  # a second node of the cluster: same VPC, no new one
+    assert len(vpcs) == 1 and [p["attach_vpc"] for p in posts] == [["vpc-1"], ["vpc-1"]]
+    assert posts[0]["os_id"] == 1743
     c.terminate_instance(jpd.instance_id, jpd.region, jpd.backend_data)
+    # a ROCm marketplace image for the bare-metal plans
+    c2 = compute_class(BackendType.VULTR)({"images": {"bare_metal": "amd-rocm"}}, {"api_key": "vk"}, _client(handler))
+    c2.create_instance(offer, CFG)
+    assert posts[-1]["image_id"] == "amd-rocm" and "os_id" not in posts[-1]
+
+
+def test_nebius_service_account_key_exchanged_for_cached_iam_token(rsa_pem):
+    """A service-account authorized key is turned into an IAM token with a PS256 JWT; the token
+    is cached across calls."""
+    exchanges, seen = [], []
+
+    def handler(req):
+        if req.url.host == "iam.api.nebius.cloud":
+            jwt = json.loads(req.content)["jwt"]
+            head, claims, sig = jwt.split(".")
+            pad = lambda x: x + "=" * (-len(x) % 4)  # noqa: E731
+            h = json.loads(base64.urlsafe_b64decode(pad(head)))
+            c = json.loads(base64.urlsafe_b64decode(pad(claims)))
+            assert h == {"typ": "JWT", "alg": "PS256", "kid": "key-1"} and c["iss"] == "sa-1"
+            assert c["aud"].endswith("/iam/v1/tokens") and c["exp"] > c["iat"]
+            assert len(base64.urlsafe_b64decode(pad(sig))) >= 256  # an RSA-2048+ signature
+            exchanges.append(jwt)
+            return httpx.Response(200, json={"iamToken": "t-123", "expiresAt": "2099-01-01T00:00:00Z"})
+        seen.append(req.headers["authorization"])
+        return httpx.Response(200, json={"instances": []})
+
+    key = json.dumps({"id": "key-1", "service_account_id": "sa-1", "private_key": rsa_pem})
+    c = compute_class(BackendType.NEBIUS)({"folder_id": "f"}, {"type": "service_account", "data": key},
+                                          _client(handler))
+    c.check_credentials()
+    c.check_credentials()
+    assert len(exchanges) == 1 and seen == ["Bearer t-123", "Bearer t-123"]
 
 
 # ---- RunPod (MI300X containers) ----------------------------------------------------------------
