@@ -464,11 +464,17 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 // for the recompute-free dQ pass below: a lane owns one key and 4 consecutive queries per register
 // group, so it stores 8 bytes at a time (the [q][key] forms measured 1.40-1.53 ms for this pass
 // with 2-byte stores), and the dQ pass DMAs row-major 64-key tiles and reads them transposed.
-template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false>
+// GQA: one workgroup owns a key block of one KV head and walks the q tiles of every query head of
+// its group (H / KVH heads) in turn, so dK/dV are summed over the group in the accumulators and
+// written once as bf16 straight into dqkv -- no fp32 per-q-head partials in HBM (2 x B*S*H*128*4
+// bytes written and read back) and no reduce kernel.  Grid: B * KVH * S/128 workgroups, each G
+// times longer; K/V are staged into LDS once per block instead of once per query head.
+template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false, bool GQA = false>
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
-    int H, int KVH, float scale_log2, bf16_t* __restrict__ dsg) {
+    int H, int KVH, float scale_log2, bf16_t* __restrict__ dsg, bf16_t* __restrict__ dqkv = nullptr) {
+  static_assert(!(GQA && SPILL), "the dS spill is per query head");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KV_BYTES = 2 * 128 * 256;            // K (128 rows) | V (128 rows)
   constexpr int STAGE = 2 * TILE_BYTES + 512;        // Q (64) | dO (64) | lse | delta
@@ -481,17 +487,18 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
   const long rs = (long)NH * HD;
   const long ors = (long)H * HD;
   const int bid = blockIdx.x;
-  const int kb = bid / (B * H);  // small kb = most q tiles: heaviest first
-  const int bh = bid % (B * H);
-  const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
+  const int G = H / KVH;
+  const int nbh = GQA ? B * KVH : B * H;
+  const int kb = bid / nbh;  // small kb = most q tiles: heaviest first
+  const int bh = bid % nbh;  // (b, q head), or (b, kv head) with GQA
+  const int b = bh / (GQA ? KVH : H);
+  const int kvh = GQA ? bh % KVH : (bh % H) / G;
+  const int h_first = GQA ? kvh * G : bh % H;  // the query head(s) this workgroup walks
+  const int n_heads = GQA ? G : 1;
+  int hh = h_first;
   const bf16_t* base = qkv + (long)b * S * rs;
-  const bf16_t* qp = base + hh * HD;
   const bf16_t* kp = base + (H + kvh) * HD;
   const bf16_t* vp = base + (H + KVH + kvh) * HD;
-  const bf16_t* dop = dout + (long)b * S * ors + hh * HD;
-  const float* lp = lse + ((long)b * H + hh) * S;
-  const float* dp = delta + ((long)b * H + hh) * S;
-  const __amdgpu_buffer_rsrc_t lrs = make_rsrc(lp, (unsigned)S * 4), drs = make_rsrc(dp, (unsigned)S * 4);
   const int kb0 = kb * 128, kw0 = kb0 + 32 * g, mykey = kw0 + l32;
   char* kl = smem;
   char* vl = smem + 128 * 256;
@@ -514,24 +521,43 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     }
   const int qt_begin = CAUSAL ? kb0 / 64 : 0;
   const int nqt = S / 64;
-  auto issue = [&](int qt, char* st) {
+  // GQA walks (query head of the group, q tile) pairs: the next head's first tile is prefetched
+  // under the previous head's last one.  Without GQA this is the plain q-tile loop.
+  const __amdgpu_buffer_rsrc_t lrs0 = make_rsrc(lse + ((long)b * H + h_first) * S, (unsigned)S * 4);
+  const __amdgpu_buffer_rsrc_t drs0 = make_rsrc(delta + ((long)b * H + h_first) * S, (unsigned)S * 4);
+  auto issue = [&](int h, int qt, char* st) {
     if (qh == 0)
-      dma_tile64(qp + (long)qt * 64 * rs, rs, st, w4, lane);
+      dma_tile64(base + h * HD + (long)qt * 64 * rs, rs, st, w4, lane);
     else
-      dma_tile64(dop + (long)qt * 64 * ors, ors, st + TILE_BYTES, w4, lane);
-    if (w == 0) dma_f32x64_buf(lrs, qt * 64, st + 2 * TILE_BYTES, lane);
-    if (w == 4) dma_f32x64_buf(drs, qt * 64, st + 2 * TILE_BYTES + 256, lane);
+      dma_tile64(dout + (long)b * S * ors + h * HD + (long)qt * 64 * ors, ors, st + TILE_BYTES, w4, lane);
+    if constexpr (GQA) {
+      if (w == 0)
+        dma_f32x64_buf(make_rsrc(lse + ((long)b * H + h) * S, (unsigned)S * 4), qt * 64, st + 2 * TILE_BYTES, lane);
+      if (w == 4)
+        dma_f32x64_buf(make_rsrc(delta + ((long)b * H + h) * S, (unsigned)S * 4), qt * 64,
+                       st + 2 * TILE_BYTES + 256, lane);
+    } else {
+      if (w == 0) dma_f32x64_buf(lrs0, qt * 64, st + 2 * TILE_BYTES, lane);
+      if (w == 4) dma_f32x64_buf(drs0, qt * 64, st + 2 * TILE_BYTES + 256, lane);
+    }
   };
-  issue(qt_begin, ring);
+  issue(h_first, qt_begin, ring);
   wait_dma_and_barrier();
 
-  for (int qt = qt_begin; qt < nqt; ++qt) {
-    const int stage = (qt - qt_begin) & 1;
+  const int h_end = h_first + n_heads;
+  int qt = qt_begin, stage = 0;
+  for (;;) {
     const char* ql = ring + stage * STAGE;
     const char* dol = ql + TILE_BYTES;
     const float* ll = reinterpret_cast<const float*>(ql + 2 * TILE_BYTES);
     const float* dl = ll + 64;
-    if (qt + 1 < nqt) issue(qt + 1, ring + (stage ^ 1) * STAGE);
+    int nqt_next = qt + 1, nh = hh;
+    if (GQA && nqt_next == nqt) {
+      nqt_next = qt_begin;
+      ++nh;
+    }
+    const bool more = GQA ? nh < h_end : nqt_next < nqt;
+    if (more) issue(nh, nqt_next, ring + (stage ^ 1) * STAGE);
     const int qlo = qt * 64 + 32 * qh;
     if (!CAUSAL || qlo + 31 >= kw0) {  // some query of my half-tile sees my keys
       f32x16 sc, dpv;
@@ -590,7 +616,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
         dsb[k2] = to_bf16x8(dpv, 8 * k2);
       }
       if constexpr (SPILL) {  // lane = key mykey, registers 4*rr+i = queries qlo + 8*rr + 4*hf + i
-        bf16_t* dt = dsg + ((long)bh * S + mykey) * S + qlo + 4 * hf;
+        bf16_t* dt = dsg + (((long)b * H + hh) * S + mykey) * S + qlo + 4 * hf;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
           *reinterpret_cast<us4*>(dt + 8 * rr) =
@@ -605,6 +631,10 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
         }
     }
     wait_dma_and_barrier();
+    if (!more) break;
+    qt = nqt_next;
+    hh = nh;
+    stage ^= 1;
   }
   // reduce the two q-halves of every key group through LDS (the K/V + ring space is free now):
   // layout [g][dk|dv][d][r][lane] floats -> lane-contiguous, conflict-free
@@ -619,7 +649,26 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
       }
   }
   __syncthreads();
-  if (qh == 0) {
+  if (GQA && qh == 0) {  // the group's sum, bf16, straight into dqkv's K and V slots
+    const float sm = scale_log2 * 0.6931471805599453f;
+    bf16_t* dkr = dqkv + ((long)b * S + mykey) * NH * HD + (H + kvh) * HD;
+    bf16_t* dvr = dkr + KVH * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int dd = 32 * d + 8 * rr + 4 * hf;
+        float ok[4], ov[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rr + i;
+          ok[i] = (dk[d][r] + red[(((g * 2 + 0) * 4 + d) * 16 + r) * 64 + lane]) * sm;
+          ov[i] = dv[d][r] + red[(((g * 2 + 1) * 4 + d) * 16 + r) * 64 + lane];
+        }
+        *reinterpret_cast<us4*>(dkr + dd) = us4{f2bf(ok[0]), f2bf(ok[1]), f2bf(ok[2]), f2bf(ok[3])};
+        *reinterpret_cast<us4*>(dvr + dd) = us4{f2bf(ov[0]), f2bf(ov[1]), f2bf(ov[2]), f2bf(ov[3])};
+      }
+  } else if (qh == 0) {
     const float sm = scale_log2 * 0.6931471805599453f;  // softmax scale = scale_log2 * ln2
     float* dkr = dkp + (((long)b * S + mykey) * H + hh) * HD;
     float* dvr = dvp + (((long)b * S + mykey) * H + hh) * HD;
@@ -1168,6 +1217,13 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     const char* v = getenv("DSTACK_AMD_FA_HALF_PRIO");
     return v && atoi(v) == 1;
   }();
+  // GQA-summed dK/dV (one workgroup per KV head and key block, bf16 written directly, no reduce
+  // kernel): DSTACK_AMD_FA_DKDV_GQA=1
+  static const bool dkdv_gqa_env = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DKDV_GQA");
+    return v && atoi(v) == 1;
+  }();
+  const bool dkdv_gqa = dkdv_gqa_env && dkdv_kind == 8 && !half_prio && !fa_ds_spill(B, S, H);
 #define DSA_DKDV(C, N)                                                                                 \
   do {                                                                                                 \
     if (dkdv_kind >= 64 && S % 256 == 0) {                                                             \
@@ -1184,6 +1240,11 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     } else if ((dkdv8 || dkdv_kind >= 64) && half_prio) {                                              \
       fa_bwd_dkdv8_kernel<C, false, true><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>( \
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr);  \
+    } else if (dkdv_gqa) {                                                                             \
+      fa_bwd_dkdv8_kernel<C, false, false, false, true>                                                \
+          <<<B * KVH * (S / 128), 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(              \
+              (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr, \
+              (bf16_t*)dqkv);                                                                          \
     } else if (dkdv8 || dkdv_kind >= 64) {                                                             \
       fa_bwd_dkdv8_kernel<C><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(          \
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr);  \
@@ -1241,6 +1302,7 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   }
 #undef DSA_DKDV
   DSA_CHECK(hipGetLastError());
+  if (dkdv_gqa) return hipSuccess;  // dK/dV already summed over the group, in dqkv
   const long work = (long)B * S * KVH * (HD / 8);
   int g = (int)((work + 255) / 256);
   if (g > 4096) g = 4096;

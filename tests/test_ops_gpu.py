@@ -286,7 +286,8 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
     forward without the S-phase prefetch (DSTACK_AMD_FA_FWD_PF=0) and the exact running max instead of
     the deferred one (DSTACK_AMD_FA_RESCALE_THR=0), and the staggered forward
     (DSTACK_AMD_FA_FWD_STAG=1), and the recompute-free dQ pass over the dS spilled by the dK/dV
-    pass (DSTACK_AMD_FA_DQ=ds; also at S=1152, its 4-wave dQ form, causal and not).  The switches
+    pass (DSTACK_AMD_FA_DQ=ds; also at S=1152, its 4-wave dQ form, causal and not), and dK/dV summed
+    over the GQA group in one workgroup (DSTACK_AMD_FA_DKDV_GQA=1, causal and not).  The switches
     are read once per process, so each variant runs in a child process."""
     import os
     import subprocess
@@ -305,18 +306,21 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
         "torch.save({'o': o.detach().cpu(), 'g': x.grad.cpu()}, sys.argv[1])\n"
     )
     shape = {"dq_ds_1152": (1152, True), "dq_ds_1152_nc": (1152, False), "default_1152": (1152, True),
-             "default_1152_nc": (1152, False)}
+             "default_1152_nc": (1152, False), "dkdv_gqa_nc": (1024, False), "default_nc": (1024, False)}
     variants = {"default": {}, "dkdv4": {"DSTACK_AMD_FA_DKDV": "4w"},
                 "fwd4_dq4": {"DSTACK_AMD_FA_FWD_WAVES": "4", "DSTACK_AMD_FA_DQ_WAVES": "4"},
                 "fwd_pf0": {"DSTACK_AMD_FA_FWD_PF": "0"}, "exact_max": {"DSTACK_AMD_FA_RESCALE_THR": "0"},
                 "fwd_stag": {"DSTACK_AMD_FA_FWD_STAG": "1"}, "half_prio": {"DSTACK_AMD_FA_HALF_PRIO": "1"},
                 "dq_ds": {"DSTACK_AMD_FA_DQ": "ds"}, "dq_ds_1152": {"DSTACK_AMD_FA_DQ": "ds"},
-                "dq_ds_1152_nc": {"DSTACK_AMD_FA_DQ": "ds"}, "default_1152": {}, "default_1152_nc": {}}
+                "dq_ds_1152_nc": {"DSTACK_AMD_FA_DQ": "ds"}, "default_1152": {}, "default_1152_nc": {},
+                "dkdv_gqa": {"DSTACK_AMD_FA_DKDV_GQA": "1"}, "dkdv_gqa_nc": {"DSTACK_AMD_FA_DKDV_GQA": "1"},
+                "default_nc": {}}
     out = {}
     for name, extra in variants.items():
         env = dict(os.environ)
         for k in ("DSTACK_AMD_FA_DKDV", "DSTACK_AMD_FA_FWD_WAVES", "DSTACK_AMD_FA_DQ_WAVES", "DSTACK_AMD_FA_FWD_PF",
-                  "DSTACK_AMD_FA_RESCALE_THR", "DSTACK_AMD_FA_FWD_STAG", "DSTACK_AMD_FA_HALF_PRIO", "DSTACK_AMD_FA_DQ"):
+                  "DSTACK_AMD_FA_RESCALE_THR", "DSTACK_AMD_FA_FWD_STAG", "DSTACK_AMD_FA_HALF_PRIO", "DSTACK_AMD_FA_DQ",
+                  "DSTACK_AMD_FA_DKDV_GQA"):
             env.pop(k, None)
         env.update(extra)
         sn, causal = shape.get(name, (S, True))
@@ -325,10 +329,12 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
                        timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         out[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
     ref_o, ref_g = out["default"]["o"].float(), out["default"]["g"].float()
-    for name in ("dkdv4", "fwd4_dq4", "fwd_pf0", "exact_max", "fwd_stag", "half_prio", "dq_ds"):
+    for name in ("dkdv4", "fwd4_dq4", "fwd_pf0", "exact_max", "fwd_stag", "half_prio", "dq_ds", "dkdv_gqa"):
         o, g = out[name]["o"].float(), out[name]["g"].float()
         assert ((o - ref_o).norm() / ref_o.norm()).item() < 2e-3, name
         assert ((g - ref_g).norm() / ref_g.norm()).item() < 2e-3, name
+    g, rg = out["dkdv_gqa_nc"]["g"].float(), out["default_nc"]["g"].float()
+    assert ((g - rg).norm() / rg.norm()).item() < 2e-3, "dkdv_gqa_nc"
     for name in ("dq_ds_1152", "dq_ds_1152_nc"):
         ref = out[name.replace("dq_ds", "default")]
         g, rg = out[name]["g"].float(), ref["g"].float()
