@@ -1,25 +1,20 @@
-"""Weight-gradient GEMM layouts at the Llama-3-8B training shapes (T = 8192 tokens per micro-batch):
-dW = G^T X with G [T, M] and X [T, N] token-major, as the forward/backward produce them, against
-the "TN" form the step uses today (both operands transposed to token-contiguous copies first).
-Both forms go through hipBLASLt with TunableOp tuning each shape on first use.  Prints one JSON
-line per shape: ms of each form (the TN time excludes the transposes it needs; ``tn_with_t`` adds
-them)."""
+"""Which operand layout makes the weight-gradient GEMM fast on MI355X?  dW[P,Q] = g[T,P]^T x[T,Q]
+timed as (a) torch.mm(g.t(), x) (both operands reduction-dim-strided, today's path), (b) with g
+pre-transposed (gT[P,T] @ x: NN), (c) both pre-transposed (gT @ xT.t(): both reduction-contiguous),
+plus the cost of a plain transpose copy.  TunableOp tunes the new layouts into a scratch file
+(TUNE=1) so every layout runs its best hipBLASLt solution."""
 import json
 import os
 import sys
 import time
 
-os.environ.setdefault("PYTORCH_TUNABLEOP_ENABLED", "1")
-os.environ.setdefault("PYTORCH_TUNABLEOP_TUNING", "1")
-os.environ.setdefault("PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS", "100")
-os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", "/tmp/wgrad_tunableop.csv")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-SHAPES = {"qkv": (6144, 4096), "o_proj": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
-          "lm_head": (128256, 4096)}
+from dstack_amd.ops import gemm_tuning  # noqa: E402
 
 
-def timeit(fn, iters=20, warm=5):
+def timeit(fn, iters=10, warm=3):
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
@@ -31,26 +26,38 @@ def timeit(fn, iters=20, warm=5):
 
 
 def main():
-    T = int(os.getenv("T", "8192"))
-    only = sys.argv[1:] or list(SHAPES)
-    for name in only:
-        M, N = SHAPES[name]
-        g = torch.randn(T, M, device="cuda", dtype=torch.bfloat16)
-        x = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
-        gt, xt = g.t().contiguous(), x.t().contiguous()
-        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        nt = timeit(lambda: torch.mm(g.t(), x, out=out))          # token-major operands as produced
-        tn = timeit(lambda: torch.mm(gt, xt.t(), out=out))        # token-contiguous copies (today)
-        tr = timeit(lambda: (g.t().contiguous(), x.t().contiguous()))
-        ref = torch.mm(gt, xt.t())
-        err = ((torch.mm(g.t(), x).float() - ref.float()).norm() / ref.float().norm()).item()
-        fl = 2.0 * T * M * N
-        print(json.dumps({"shape": name, "M": M, "N": N, "T": T, "nt_ms": round(nt, 4), "tn_ms": round(tn, 4),
-                          "transposes_ms": round(tr, 4), "tn_with_t_ms": round(tn + tr, 4),
-                          "nt_tflops": round(fl / nt / 1e9, 1), "tn_tflops": round(fl / tn / 1e9, 1),
-                          "rel_diff": err}), flush=True)
-        del g, x, gt, xt, out, ref
+    if os.getenv("TUNE") == "1":
+        import shutil
+        shutil.copy(gemm_tuning.results_path(), "/tmp/wgrad_layouts_tune.csv")
+        os.environ["DSTACK_AMD_GEMM_TUNING_FILE"] = "/tmp/wgrad_layouts_tune.csv"
+        gemm_tuning.setup("tune")
+    else:
+        gemm_tuning.setup("use")
+    dev = torch.device("cuda")
+    T = 8192
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    out = {}
+    for name, (P, Q) in shapes.items():
+        torch.manual_seed(0)
+        g = torch.randn(T, P, device=dev, dtype=torch.bfloat16)
+        x = torch.randn(T, Q, device=dev, dtype=torch.bfloat16)
+        gT = g.t().contiguous()
+        xT = x.t().contiguous()
+        w = torch.empty(P, Q, device=dev, dtype=torch.bfloat16)
+        fl = 2.0 * P * Q * T
+        r = {}
+        r["a_both_strided"] = timeit(lambda: torch.mm(g.t(), x, out=w))
+        r["b_gT_nn"] = timeit(lambda: torch.mm(gT, x, out=w))
+        r["b2_xT"] = timeit(lambda: torch.mm(g.t(), xT.t(), out=w))
+        r["c_both_contig"] = timeit(lambda: torch.mm(gT, xT.t(), out=w))
+        buf = torch.empty_like(gT)
+        r["transpose_g_ms"] = timeit(lambda: buf.copy_(g.t()))
+        res = {k: {"ms": v, "tflops": fl / v / 1e9} if not k.startswith("transpose") else v for k, v in r.items()}
+        out[name] = res
+        print(name, json.dumps(res), flush=True)
+        del g, x, gT, xT, w, buf
         torch.cuda.empty_cache()
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

@@ -15,8 +15,6 @@ for i in 1 2; do  # in the training step (the driver's bench, shorter)
   DSTACK_AMD_FA_DKDV_GQA=0 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/step_base_$i.json 2>>$O/ab.err || exit 1
   DSTACK_AMD_FA_DKDV_GQA=1 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/step_gqa_$i.json 2>>$O/ab.err || exit 1
 done
-timeout -k 10 400 python tools/bench_wgrad_layouts.py qkv o_proj gate_up down > $O/wgrad_layouts.jsonl 2>>$O/ab.err || exit 1
-cat $O/wgrad_layouts.jsonl
 cd /tmp && export TMPDIR=/tmp
 (cd $R && DSTACK_AMD_FA_DKDV_GQA=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_base -o k -- python3 tools/bench_attn.py) > $R/$O/prof_base.log 2>&1 || exit 1
 (cd $R && DSTACK_AMD_FA_DKDV_GQA=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_gqa -o k -- python3 tools/bench_attn.py) > $R/$O/prof_gqa.log 2>&1 || exit 1
