@@ -120,11 +120,13 @@ class Run:
                 self.refresh()
                 continue
             sub = self._latest_submission(replica_num, job_num)
+            rewrite = None if diagnose else self._url_replacer(replica_num, job_num)
             while True:
                 resp = self._api.logs.poll(self._project, self.name, sub.id, start_time=start_time,
                                            diagnose=diagnose, next_token=next_token)
                 for ev in resp.logs:
-                    yield base64.b64decode(ev.message)
+                    chunk = base64.b64decode(ev.message)
+                    yield rewrite(chunk) if rewrite else chunk
                 if resp.next_token and resp.logs:
                     next_token = resp.next_token
                     continue
@@ -138,6 +140,29 @@ class Run:
             self.refresh()
             if self._run.status.is_finished():
                 finished = True  # one more drain pass after termination
+
+    def _url_replacer(self, replica_num: int = 0, job_num: int = 0):
+        """Rewrites the container URLs a job prints: to the forwarded local ports when attached,
+        to the service's public URL for a service (``core.services.logs.URLReplacer``)."""
+        import urllib.parse
+
+        from dstack_amd.core.services.logs import URLReplacer
+
+        job = next((j for j in self._run.jobs if j.job_spec.replica_num == replica_num
+                    and j.job_spec.job_num == job_num), self._run.jobs[0] if self._run.jobs else None)
+        if job is None:
+            return None
+        conf = self._run.run_spec.configuration
+        if self.ports:
+            jpd = job.job_submissions[-1].job_provisioning_data
+            return URLReplacer(ports=self.ports, app_specs=job.job_spec.app_specs or [], hostname="127.0.0.1",
+                               secure=False, ip_address=jpd.hostname if jpd else None)
+        if isinstance(conf, ServiceConfiguration) and self.service_url:
+            u = urllib.parse.urlsplit(self.service_url)
+            secure = u.scheme == "https"
+            return URLReplacer(ports={conf.port.container_port: u.port or (443 if secure else 80)}, app_specs=[],
+                               hostname=u.hostname or "", secure=secure, path_prefix=u.path if u.path != "/" else "")
+        return None
 
     def attach(self, ssh_identity_file: Optional[str] = None, bind_address: str = "127.0.0.1",
                ports_overrides: Optional[Dict[int, int]] = None) -> bool:

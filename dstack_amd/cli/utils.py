@@ -36,18 +36,9 @@ def confirm_ask(prompt: str, default: bool = True) -> bool:
 
 
 def pretty_date(dt: Optional[datetime]) -> str:
-    if dt is None:
-        return "-"
-    if dt.tzinfo is None:
-        dt = dt.replace(tzinfo=timezone.utc)
-    secs = int((datetime.now(timezone.utc) - dt).total_seconds())
-    if secs < 60:
-        return f"{max(secs, 0)} sec ago"
-    if secs < 3600:
-        return f"{secs // 60} min ago"
-    if secs < 86400:
-        return f"{secs // 3600} hour{'s' if secs >= 7200 else ''} ago"
-    return dt.strftime("%Y-%m-%d %H:%M")
+    from dstack_amd.utils.common import pretty_date as _pretty
+
+    return _pretty(dt)
 
 
 def status_text(status: str, error: Optional[str] = None, exit_status: Optional[int] = None) -> str:

@@ -81,10 +81,14 @@ def format_duration(seconds: Optional[int]) -> str:
 
 
 class RegistryAuth(CoreModel):
-    """Credentials for pulling a private Docker image."""
+    """Credentials for pulling a private Docker image (hashable: a cache key of the registry
+    client's image-config cache)."""
 
     username: str
     password: str
+
+    def __hash__(self) -> int:
+        return hash((self.username, self.password))
 
 
 class ApplyAction(str, Enum):

@@ -13,6 +13,7 @@ import hashlib
 import io
 import os
 import re
+import urllib.parse
 import subprocess
 import tarfile
 from abc import ABC, abstractmethod
@@ -212,6 +213,56 @@ def parse_git_url(url: str) -> Dict[str, Optional[str]]:
     return m.groupdict()
 
 
+class GitRepoURL:
+    """A git remote as the run will clone it (reference ``core/models/repos/remote.py``
+    ``GitRepoURL``).  ``ssh://`` URLs and scp-style ``user@host:path`` locations name an SSH host
+    that ``~/.ssh/config`` may alias (HostName / User / Port); an https URL keeps its host, and the
+    SSH form of it takes the user and port the config gives that host."""
+
+    def __init__(self, scheme: str, host: str, path: str, user: Optional[str] = None, port: Optional[int] = None,
+                 ssh_user: Optional[str] = None, ssh_port: Optional[int] = None):
+        self.scheme, self.host, self.path = scheme, host, path.lstrip("/")
+        self.user, self.port = user, port
+        self.ssh_user, self.ssh_port = ssh_user, ssh_port
+
+    @classmethod
+    def parse(cls, url: str, get_ssh_config=None) -> "GitRepoURL":
+        from dstack_amd.utils.ssh import get_ssh_config as _default
+
+        lookup = get_ssh_config or _default
+        url = url.strip()
+        if "://" in url:
+            u = urllib.parse.urlsplit(url)
+            if u.scheme not in ("https", "http", "ssh", "git+ssh") or not u.hostname or not u.path.strip("/"):
+                raise RepoError(f"unsupported git url: {url}")
+            if u.scheme in ("https", "http"):
+                cfg = lookup(u.hostname) or {}
+                return cls(u.scheme, u.hostname, u.path, port=u.port, ssh_user=cfg.get("user"),
+                           ssh_port=int(cfg["port"]) if cfg.get("port") else None)
+            cfg = lookup(u.hostname) or {}
+            port = u.port or (int(cfg["port"]) if cfg.get("port") else None)
+            return cls("ssh", cfg.get("hostname") or u.hostname, u.path, user=u.username or cfg.get("user"),
+                       ssh_user=u.username or cfg.get("user"), ssh_port=port)
+        m = re.match(r"^(?:(?P<user>[^@/:]+)@)?(?P<host>[^:/]+):(?P<path>[^/].*)$", url)
+        if m is None:
+            raise RepoError(f"cannot parse git url: {url}")
+        cfg = lookup(m.group("host")) or {}
+        user = m.group("user") or cfg.get("user")
+        port = int(cfg["port"]) if cfg.get("port") else None
+        return cls("ssh", cfg.get("hostname") or m.group("host"), m.group("path"), user=user, ssh_user=user,
+                   ssh_port=port)
+
+    def as_https(self, oauth_token: Optional[str] = None) -> str:
+        auth = f"anything:{oauth_token}@" if oauth_token else ""
+        port = f":{self.port}" if self.port and self.scheme in ("https", "http") else ""
+        return f"https://{auth}{self.host}{port}/{self.path}"
+
+    def as_ssh(self) -> str:
+        user = self.ssh_user or "git"
+        port = f":{self.ssh_port}" if self.ssh_port else ""
+        return f"ssh://{user}@{self.host}{port}/{self.path}"
+
+
 def _git(repo_dir: str, *args: str) -> str:
     r = subprocess.run(["git", "-C", repo_dir, *args], capture_output=True, text=True)
     if r.returncode != 0:
@@ -237,9 +288,15 @@ class RemoteRepo(Repo):
             head = _git(self.repo_dir, "rev-parse", "HEAD").strip()
         except RepoError:
             head = None
+        try:  # the host the run actually clones from (an ~/.ssh/config alias resolved)
+            g = GitRepoURL.parse(url)
+            r_host, r_user = g.host, g.ssh_user or parts["user"] or ""
+            r_port = g.ssh_port if g.scheme == "ssh" else g.port
+        except RepoError:
+            r_host, r_user, r_port = host, parts["user"] or "", int(parts["port"]) if parts["port"] else None
         self.run_repo_data = RemoteRunRepoData(
-            repo_name=path, repo_host_name=host, repo_port=int(parts["port"]) if parts["port"] else None,
-            repo_user_name=parts["user"] or "", repo_branch=branch, repo_hash=head,
+            repo_name=path, repo_host_name=r_host, repo_port=r_port,
+            repo_user_name=r_user, repo_branch=branch, repo_hash=head,
         )
 
     def diff(self) -> str:

@@ -2,6 +2,7 @@
 
 from __future__ import annotations
 
+import re
 from typing import Optional, Union
 
 from dstack_amd.core.models.common import CoreModel
@@ -15,23 +16,26 @@ class UnixUser(CoreModel):
 
     @classmethod
     def parse(cls, v: str) -> "UnixUser":
-        if not v:
-            raise ValueError("empty user")
+        """``user[:group]``, each a name or a numeric id (reference ``UnixUser.parse``)."""
         parts = v.split(":")
         if len(parts) > 2:
-            raise ValueError(f"invalid user: {v} (expected user[:group])")
+            raise ValueError(f"invalid user: {v!r}: too many parts (expected user[:group])")
         user, group = parts[0], (parts[1] if len(parts) == 2 else None)
-        if not user or (group is not None and not group):
-            raise ValueError(f"invalid user: {v}")
-        if user.startswith("-") or (group or "").startswith("-"):
-            raise ValueError(f"negative uid/gid: {v}")
+        if not user:
+            raise ValueError(f"invalid user: {v!r}: empty user name or id")
+        if group is not None and not group:
+            raise ValueError(f"invalid user: {v!r}: empty group name or id")
         kw: dict = {}
-        if user.isdigit():
+        if re.fullmatch(r"-?\d+", user):
+            if int(user) < 0:
+                raise ValueError(f"invalid user: {v!r}: negative uid")
             kw["uid"] = int(user)
         else:
             kw["username"] = user
-        if group:
-            if group.isdigit():
+        if group is not None:
+            if re.fullmatch(r"-?\d+", group):
+                if int(group) < 0:
+                    raise ValueError(f"invalid user: {v!r}: negative gid")
                 kw["gid"] = int(group)
             else:
                 kw["groupname"] = group

@@ -154,30 +154,109 @@ def get_tunnel_pool() -> TunnelPool:
     return _pool
 
 
-class SSHTunnel:
-    """One-shot tunnel object with the reference's open/close API (used by the CLI attach)."""
+@dataclass(frozen=True)
+class IPSocket:
+    host: str
+    port: int
 
-    def __init__(self, target: SSHTarget, identity_file: str, forwards: List[Tuple[int, str, int]],
-                 control_sock_path: Optional[str] = None):
+    def spec(self) -> str:
+        host = f"[{self.host}]" if ":" in self.host else self.host  # IPv6 literals are bracketed
+        return f"{host}:{self.port}"
+
+
+@dataclass(frozen=True)
+class UnixSocket:
+    path: str
+
+    def spec(self) -> str:
+        return self.path
+
+
+@dataclass(frozen=True)
+class SocketPair:
+    local: object  # IPSocket | UnixSocket
+    remote: object
+
+
+def ports_to_forwarded_sockets(ports: Dict[int, int], bind_local: str = "127.0.0.1") -> List[SocketPair]:
+    """{remote port: local port} -> local-forward socket pairs bound on ``bind_local``."""
+    return [SocketPair(local=IPSocket(bind_local, lp), remote=IPSocket("localhost", rp)) for rp, lp in ports.items()]
+
+
+class SSHTunnel:
+    """One ``ssh -N -f`` master with local (``-L``) and reverse (``-R``) forwards over TCP or unix
+    sockets, addressed later through its control socket (check / exit / exec) -- the CLI's
+    attach.  The identity is a key file path or the key's content (written to a private temp
+    file); ``ssh_config_path`` None means ``-F none`` (the user's config is not consulted)."""
+
+    def __init__(self, target: SSHTarget, identity_file: Optional[str] = None,
+                 forwards: Optional[List[Tuple[int, str, int]]] = None, control_sock_path: Optional[str] = None,
+                 identity_content: Optional[str] = None, options: Optional[Dict[str, str]] = None,
+                 ssh_config_path: Optional[str] = None, forwarded_sockets: Optional[List[SocketPair]] = None,
+                 reverse_forwarded_sockets: Optional[List[SocketPair]] = None, ssh_binary: str = "ssh"):
         self.target = target
+        self.temp_dir = tempfile.TemporaryDirectory(prefix="dstack-tunnel-")
+        if identity_content is not None:
+            identity_file = os.path.join(self.temp_dir.name, "identity")
+            with open(identity_file, "w") as f:
+                f.write(identity_content)
+            os.chmod(identity_file, 0o600)
         self.identity_file = identity_file
-        self.forwards = forwards
-        self.control_sock_path = control_sock_path or os.path.join(tempfile.mkdtemp(), "ctrl")
-        self.proc: Optional[subprocess.Popen] = None
+        self.forwarded_sockets = list(forwarded_sockets or []) + [
+            SocketPair(IPSocket("127.0.0.1", local), IPSocket(host, remote)) for local, host, remote in (forwards or [])]
+        self.reverse_forwarded_sockets = list(reverse_forwarded_sockets or [])
+        self.control_sock_path = control_sock_path or os.path.join(self.temp_dir.name, "control.sock")
+        self.options = dict(options) if options is not None else {
+            "StrictHostKeyChecking": "no", "UserKnownHostsFile": "/dev/null", "LogLevel": "ERROR",
+            "ServerAliveInterval": "30", "ExitOnForwardFailure": "yes", "IdentitiesOnly": "yes"}
+        self.ssh_config_path = ssh_config_path
+        self.ssh = ssh_binary
+
+    @property
+    def destination(self) -> str:
+        return f"{self.target.username}@{self.target.hostname}"
+
+    def open_command(self) -> List[str]:
+        cmd = [self.ssh, "-F", self.ssh_config_path or "none"]
+        if self.identity_file:
+            cmd += ["-i", self.identity_file]
+        cmd += ["-E", os.path.join(self.temp_dir.name, "tunnel.log"), "-N", "-f", "-o", "ControlMaster=auto",
+                "-S", self.control_sock_path]
+        if self.target.port and self.target.port != 22:
+            cmd += ["-p", str(self.target.port)]
+        for k, v in self.options.items():
+            cmd += ["-o", f"{k}={v}"]
+        if self.target.proxy is not None:
+            p = self.target.proxy
+            jump = [self.ssh] + (["-i", self.identity_file] if self.identity_file else []) + [
+                "-W", "%h:%p", "-o", "StrictHostKeyChecking=no", "-o", "UserKnownHostsFile=/dev/null",
+                "-p", str(p.port), f"{p.username}@{p.hostname}"]
+            cmd += ["-o", "ProxyCommand=" + " ".join(jump)]
+        for sp in self.forwarded_sockets:
+            cmd += ["-L", f"{sp.local.spec()}:{sp.remote.spec()}"]
+        for sp in self.reverse_forwarded_sockets:  # -R remote:local
+            cmd += ["-R", f"{sp.remote.spec()}:{sp.local.spec()}"]
+        cmd.append(self.destination)
+        return cmd
+
+    def check_command(self) -> List[str]:
+        return [self.ssh, "-S", self.control_sock_path, "-O", "check", self.destination]
+
+    def close_command(self) -> List[str]:
+        return [self.ssh, "-S", self.control_sock_path, "-O", "exit", self.destination]
+
+    def exec_command(self) -> List[str]:
+        return [self.ssh, "-S", self.control_sock_path, self.destination]
 
     def open(self, timeout: float = 20):
-        cmd = ["ssh", "-f", "-N", "-M", "-S", self.control_sock_path, *_base_opts(self.identity_file, self.target.port),
-               *_proxy_opts(self.target, self.identity_file)]
-        for local, host, remote in self.forwards:
-            cmd += ["-L", f"127.0.0.1:{local}:{host}:{remote}"]
-        cmd.append(f"{self.target.username}@{self.target.hostname}")
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+        r = subprocess.run(self.open_command(), capture_output=True, text=True, timeout=timeout)
         if r.returncode != 0:
-            raise SSHError(r.stderr.strip())
+            log = os.path.join(self.temp_dir.name, "tunnel.log")
+            detail = open(log).read().strip() if os.path.exists(log) else r.stderr.strip()
+            raise SSHError(detail or f"ssh exited with {r.returncode}")
 
     def close(self):
-        subprocess.run(["ssh", "-S", self.control_sock_path, "-O", "exit",
-                        f"{self.target.username}@{self.target.hostname}"], capture_output=True)
+        subprocess.run(self.close_command(), capture_output=True)
 
     def __enter__(self):
         self.open()

@@ -7,6 +7,7 @@ import hashlib
 import ipaddress
 import os
 import random
+import re
 import secrets
 import subprocess
 import tempfile
@@ -28,25 +29,87 @@ def to_aware(dt: Optional[datetime]) -> Optional[datetime]:
 
 
 def pretty_date(dt: Optional[datetime], now: Optional[datetime] = None) -> str:
+    """``now``, ``30 sec ago``, ``1 min ago`` / ``45 mins ago``, ``1 hour ago`` / ``5 hours ago``,
+    ``yesterday``, ``5 days ago``, ``3 weeks ago``, ``3 months ago``, ``1 year ago``; a time in the
+    future is ``""`` (reference ``utils/common.py`` ``pretty_date``)."""
     if dt is None:
         return "-"
-    now = now or get_current_datetime()
-    if dt.tzinfo is not None:
-        dt = dt.astimezone(timezone.utc).replace(tzinfo=None)
-    diff = now - dt
-    s = int(diff.total_seconds())
-    if s < 0:
-        return "now"
-    if s < 60:
-        return f"{s} sec ago"
-    if s < 3600:
-        return f"{s // 60} min ago"
-    if s < 86400:
-        return f"{s // 3600} hour{'s' if s // 3600 > 1 else ''} ago"
-    days = s // 86400
+    now = to_aware(now) if now is not None else datetime.now(timezone.utc)
+    diff = now - to_aware(dt)
+    s, days = int(diff.total_seconds()), diff.days
+    if days < 0:
+        return ""
+    if days == 0:
+        if s < 10:
+            return "now"
+        if s < 60:
+            return f"{s} sec ago"
+        if s < 3600:
+            m = s // 60
+            return f"{m} min{'s' if m > 1 else ''} ago"
+        h = s // 3600
+        return f"{h} hour{'s' if h > 1 else ''} ago"
+    if days == 1:
+        return "yesterday"
     if days < 7:
-        return "yesterday" if days == 1 else f"{days} days ago"
-    return dt.strftime("%b %d, %Y")
+        return f"{days} days ago"
+    for n, unit in ((365, "year"), (30, "month"), (7, "week")):
+        if days >= n:
+            k = days // n
+            return f"{k} {unit}{'s' if k > 1 else ''} ago"
+    return f"{days} days ago"
+
+
+def local_time(dt: datetime) -> str:
+    """``HH:MM`` of ``dt`` (naive values are taken as local time)."""
+    return dt.strftime("%H:%M")
+
+
+_MEMORY_UNITS = {"K": 2**10, "M": 2**20, "G": 2**30, "T": 2**40, "P": 2**50}
+
+
+def parse_memory(memory: str, as_untis: str = "M") -> float:
+    """A Kubernetes-style quantity (``1024Ki``, ``2Gi``, ``512M``) in ``as_untis`` (K|M|G|T)."""
+    m = re.fullmatch(r"\s*([0-9.]+)\s*([KMGTP])?(i)?[Bb]?\s*", memory)
+    if m is None:
+        raise ValueError(f"cannot parse memory quantity {memory!r}")
+    n = float(m.group(1))
+    if m.group(2):
+        n *= _MEMORY_UNITS[m.group(2)] if m.group(3) else 1000 ** ("KMGTP".index(m.group(2)) + 1)
+    return n / _MEMORY_UNITS[as_untis.upper()[0]]
+
+
+def split_chunks(iterable: Iterable[T], chunk_size: int) -> Iterable[List[T]]:
+    """Consecutive lists of at most ``chunk_size`` items (any iterable, generators included)."""
+    if chunk_size < 1:
+        raise ValueError(f"chunk_size must be positive, got {chunk_size}")
+    chunk: List[T] = []
+    for x in iterable:
+        chunk.append(x)
+        if len(chunk) == chunk_size:
+            yield chunk
+            chunk = []
+    if chunk:
+        yield chunk
+
+
+def concat_url_path(a, b):
+    """Join two URL path parts with exactly one ``/`` between them (str or bytes; inner ``//``
+    runs of the parts are kept)."""
+    sep = b"/" if isinstance(a, bytes) else "/"
+    if not b:
+        return a
+    a2 = a[:-1] if a.endswith(sep) else a
+    b2 = b[1:] if b.startswith(sep) else b
+    return a2 + sep + b2
+
+
+def make_proxy_url(server_url: str, proxy_url: str) -> str:
+    """Absolute URL of a service / model endpoint: absolute proxy URLs (gateways) as they are,
+    in-server proxy paths appended to the server URL (keeping its path prefix)."""
+    if "://" in proxy_url:
+        return proxy_url
+    return concat_url_path(server_url.rstrip("/"), proxy_url)
 
 
 def format_pretty_duration(seconds: int) -> str:
@@ -126,7 +189,7 @@ def get_ip_from_network(network: Optional[str], addresses: List[str]) -> Optiona
     ``utils/network.py``); without a network, the first private address."""
     ips = []
     for a in addresses:
-        ip = a.split("/")[0]
+        ip = a.split("/")[0].split("%")[0]  # drop the prefix length / IPv6 zone index
         try:
             ips.append(ipaddress.ip_address(ip))
         except ValueError:
@@ -134,7 +197,7 @@ def get_ip_from_network(network: Optional[str], addresses: List[str]) -> Optiona
     if network:
         net = ipaddress.ip_network(network, strict=False)
         for ip in ips:
-            if ip in net:
+            if ip.version == net.version and ip in net:
                 return str(ip)
         return None
     for ip in ips:
