@@ -105,9 +105,10 @@ def _bearer(request: Request) -> Optional[str]:
 class ReplicaConnections:
     """``ssh -N -L <sock>:localhost:<port>`` per non-direct replica (reference: ServiceConnection)."""
 
-    def __init__(self, sock_dir: Path, identity_file: Optional[str] = None):
+    def __init__(self, sock_dir: Path, identity_file: Optional[str] = None, connect_timeout: float = 20.0):
         self.sock_dir = sock_dir
         self.identity_file = identity_file
+        self.connect_timeout = connect_timeout
         self._procs: Dict[str, subprocess.Popen] = {}
 
     def open(self, rep: Replica) -> Replica:
@@ -126,9 +127,20 @@ class ReplicaConnections:
         if rep.ssh_proxy:
             cmd += ["-J", rep.ssh_proxy]
         cmd.append(rep.ssh_host)
-        self._procs[rep.id] = subprocess.Popen(cmd, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL,
-                                               stderr=subprocess.DEVNULL)
+        proc = subprocess.Popen(cmd, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         _ = host, user_host
+        # the forward is up when its socket exists; an ssh that exits first (bad key, host down) is a
+        # registration error, not a replica that nginx would route to a dead socket
+        deadline = time.time() + self.connect_timeout
+        while not os.path.exists(rep.socket):
+            if proc.poll() is not None:
+                err = proc.stderr.read().decode(errors="ignore").strip() if proc.stderr else ""
+                raise RegistryError(f"cannot connect to replica {rep.id} ({rep.ssh_host}): {err[-300:] or 'ssh exited'}")
+            if time.time() > deadline:
+                proc.kill()
+                raise RegistryError(f"cannot connect to replica {rep.id} ({rep.ssh_host}): timed out")
+            time.sleep(0.05)
+        self._procs[rep.id] = proc
         return rep
 
     def close(self, rep_id: str):
@@ -159,7 +171,10 @@ class Gateway:
         # restore: re-open tunnels and re-render sites from the persisted state
         for svc in self.registry.services.values():
             for rep in svc.replicas.values():
-                self.conns.open(rep)
+                try:
+                    self.conns.open(rep)
+                except RegistryError as e:  # the server re-registers what it still runs
+                    logger.warning("replica %s not reconnected: %s", rep.id, e)
             self._apply_site(svc)
         if nginx is not None:
             for ep in self.registry.entrypoints.values():
@@ -183,7 +198,17 @@ class Gateway:
 
 
 def make_app(gw: Gateway) -> FastAPI:
-    app = FastAPI(title="dstack-amd gateway", docs_url=None, redoc_url=None)
+    from contextlib import asynccontextmanager
+
+    @asynccontextmanager
+    async def lifespan(_app):
+        # state was restored when the Gateway was built (sites re-rendered, replica tunnels reopened);
+        # on shutdown the tunnels and the upstream client go away with the process
+        yield
+        gw.conns.close_all()
+        await gw.http.aclose()
+
+    app = FastAPI(title="dstack-amd gateway", docs_url=None, redoc_url=None, lifespan=lifespan)
     r = APIRouter()
 
     @r.get("/api/healthcheck")
@@ -229,11 +254,18 @@ def make_app(gw: Gateway) -> FastAPI:
         rep = Replica(id=body.job_id, app_port=body.app_port, ssh_host=body.ssh_host, ssh_port=body.ssh_port,
                       ssh_proxy=body.ssh_proxy, internal_ip=body.internal_ip,
                       mode="direct" if body.direct or not body.ssh_host else "ssh")
+        svc = gw.registry.get_service(project, run_name)
+        if svc is None:
+            return JSONResponse({"detail": f"service {project}/{run_name} is not registered"}, status_code=400)
+        if rep.id in svc.replicas:
+            return JSONResponse({"detail": f"replica {rep.id} of {project}/{run_name} is already registered"},
+                                status_code=400)
         try:
-            gw.conns.open(rep)
+            await asyncio.to_thread(gw.conns.open, rep)
             svc = gw.registry.add_replica(project, run_name, rep)
             await asyncio.to_thread(gw._apply_site, svc)
         except RegistryError as e:
+            gw.conns.close(rep.id)
             return JSONResponse({"detail": str(e)}, status_code=400)
         return {}
 

@@ -35,8 +35,8 @@ SERVICE_TEMPLATE = """\
     client_max_body_size {{ client_max_body_size }};
     listen {{ http_port }};
 {% if https %}    listen {{ https_port }} ssl;
-    ssl_certificate /etc/letsencrypt/live/{{ domain }}/fullchain.pem;
-    ssl_certificate_key /etc/letsencrypt/live/{{ domain }}/privkey.pem;
+    ssl_certificate {{ certs_dir }}/{{ domain }}/fullchain.pem;
+    ssl_certificate_key {{ certs_dir }}/{{ domain }}/privkey.pem;
     set $force_https 1;
     if ($scheme = "https") { set $force_https 0; }
     if ($remote_addr = 127.0.0.1) { set $force_https 0; }
@@ -70,8 +70,8 @@ server {
     access_log {{ access_log }} dstack_stat;
     listen {{ http_port }};
 {% if https %}    listen {{ https_port }} ssl;
-    ssl_certificate /etc/letsencrypt/live/{{ domain }}/fullchain.pem;
-    ssl_certificate_key /etc/letsencrypt/live/{{ domain }}/privkey.pem;
+    ssl_certificate {{ certs_dir }}/{{ domain }}/fullchain.pem;
+    ssl_certificate_key {{ certs_dir }}/{{ domain }}/privkey.pem;
 {% endif %}    location / {
         proxy_pass http://127.0.0.1:{{ app_port }}/api/models/{{ project }}/;
         proxy_http_version 1.1;
@@ -95,13 +95,15 @@ class NginxError(RuntimeError):
 class Nginx:
     def __init__(self, conf_dir: str = "/etc/nginx/sites-enabled", access_log: str = "/var/log/nginx/dstack.access.log",
                  app_port: int = 8000, http_port: int = 80, https_port: int = 443, reload_cmd=None,
-                 test_cmd=None):
+                 test_cmd=None, certbot_cmd=None, certs_dir: str = "/etc/letsencrypt/live"):
         self.conf_dir = Path(conf_dir)
         self.access_log = access_log
         self.app_port = app_port
         self.http_port, self.https_port = http_port, https_port
         self.reload_cmd = reload_cmd or ["sudo", "systemctl", "reload", "nginx"]
         self.test_cmd = test_cmd or ["sudo", "nginx", "-t"]
+        self.certbot_cmd = certbot_cmd or ["sudo", "certbot"]
+        self.certs_dir = certs_dir
         self._env = jinja2.Environment(trim_blocks=False, keep_trailing_newline=True)
 
     @staticmethod
@@ -117,12 +119,12 @@ class Nginx:
         return self._env.from_string(SERVICE_TEMPLATE).render(
             name=name, upstreams=ups, domain=svc.domain, access_log=self.access_log,
             client_max_body_size=svc.client_max_body_size, https=svc.https, auth=svc.auth, project=svc.project,
-            app_port=self.app_port, http_port=self.http_port, https_port=self.https_port)
+            app_port=self.app_port, http_port=self.http_port, https_port=self.https_port, certs_dir=self.certs_dir)
 
     def render_entrypoint(self, ep: Entrypoint) -> str:
         return self._env.from_string(ENTRYPOINT_TEMPLATE).render(
             domain=ep.domain, access_log=self.access_log, https=ep.https, project=ep.project,
-            app_port=self.app_port, http_port=self.http_port, https_port=self.https_port)
+            app_port=self.app_port, http_port=self.http_port, https_port=self.https_port, certs_dir=self.certs_dir)
 
     def site_name(self, domain: str) -> str:
         return f"{self.http_port}-{domain}.conf"
@@ -173,9 +175,9 @@ class Nginx:
 
     def obtain_certificate(self, domain: str, acme_server: Optional[str] = None, eab_kid: Optional[str] = None,
                            eab_hmac_key: Optional[str] = None):
-        if os.path.exists(f"/etc/letsencrypt/live/{domain}/fullchain.pem"):
+        if os.path.exists(f"{self.certs_dir}/{domain}/fullchain.pem"):
             return
-        cmd = ["sudo", "certbot", "certonly", "--non-interactive", "--agree-tos", "--register-unsafely-without-email",
+        cmd = [*self.certbot_cmd, "certonly", "--non-interactive", "--agree-tos", "--register-unsafely-without-email",
                "--nginx", "--domain", domain]
         acme_server = acme_server or os.getenv("DSTACK_ACME_SERVER")
         if acme_server:

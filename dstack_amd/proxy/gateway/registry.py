@@ -141,6 +141,8 @@ class Registry:
             svc = self.services.get(f"{project}/{run_name}")
             if svc is None:
                 raise RegistryError(f"service {project}/{run_name} is not registered")
+            if replica.id in svc.replicas:
+                raise RegistryError(f"replica {replica.id} of {project}/{run_name} is already registered")
             svc.replicas[replica.id] = replica
         self.save()
         return svc
@@ -151,6 +153,8 @@ class Registry:
             if svc is None:
                 raise RegistryError(f"service {project}/{run_name} is not registered")
             rep = svc.replicas.pop(replica_id, None)
+            if rep is None:
+                raise RegistryError(f"replica {replica_id} of {project}/{run_name} is not registered")
         self.save()
         return rep
 
