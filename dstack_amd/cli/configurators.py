@@ -56,19 +56,14 @@ def register_profile_args(parser: argparse.ArgumentParser):
     retry.add_argument("--retry-duration", dest="retry_duration", metavar="DURATION")
 
 
-def load_profile(repo_dir: str, name: Optional[str]) -> Optional[Profile]:
-    path = Path(repo_dir) / ".dstack" / "profiles.yml"
-    if not path.exists():
-        if name:
-            raise CLIError(f"profile {name} not found: {path} does not exist")
-        return None
-    cfg = ProfilesConfig.model_validate(yaml.safe_load(path.read_text()) or {"profiles": []})
-    if name:
-        for p in cfg.profiles:
-            if p.name == name:
-                return p
-        raise CLIError(f"profile {name} not found in {path}")
-    return cfg.default()
+def load_profile(repo_dir: str, name: Optional[str]) -> Profile:
+    """Repo profile, then the user's global one, then an empty default (``api.utils.load_profile``)."""
+    from dstack_amd.api.utils import load_profile as _load
+
+    try:
+        return _load(repo_dir, name)
+    except ConfigurationError as e:
+        raise CLIError(str(e)) from e
 
 
 def apply_profile_args(args, profile: Profile):

@@ -18,6 +18,7 @@ import base64
 import concurrent.futures as cf
 import datetime as _dt
 import json
+import logging
 import os
 import urllib.parse
 import xml.etree.ElementTree as ET
@@ -26,7 +27,8 @@ from typing import Dict, List, Optional, Set, Tuple
 
 from dstack_amd.core.backends.catalog import CatalogRow, offline_rows
 from dstack_amd.core.backends.clouds.common import VMCompute, check_response, cloud_init, sigv4_headers
-from dstack_amd.core.errors import BackendAuthError, ComputeError, NoCapacityError
+from dstack_amd.core.backends.clouds.tags import merged_tags
+from dstack_amd.core.errors import BackendAuthError, ComputeError, ComputeResourceNotFoundError, NoCapacityError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.gateways import GatewayComputeConfiguration, GatewayProvisioningData
 from dstack_amd.core.models.instances import (
@@ -36,6 +38,8 @@ from dstack_amd.core.models.instances import (
 )
 from dstack_amd.core.models.placement import PlacementGroup, PlacementGroupProvisioningData
 from dstack_amd.core.models.volumes import Volume, VolumeAttachmentData, VolumeProvisioningData
+
+logger = logging.getLogger(__name__)
 
 API_VERSION = "2016-11-15"
 UBUNTU_OWNER = "099720109477"
@@ -188,18 +192,45 @@ class AWSCompute(VMCompute):
 
     # ---- helpers ------------------------------------------------------------------------------
     def _image_id(self, region: str, gpu: bool) -> str:
+        return self.image_id_and_username(region, gpu)[0]
+
+    def _tag_spec(self, kind: str, base: Dict[str, str]) -> Dict[str, str]:
+        """``TagSpecification.1.*`` query params: dstack's tags plus the config's ``tags``."""
+        out = {"TagSpecification.1.ResourceType": kind}
+        for i, (k, v) in enumerate(merged_tags("aws", base, self.config).items(), 1):
+            out[f"TagSpecification.1.Tag.{i}.Key"] = k
+            out[f"TagSpecification.1.Tag.{i}.Value"] = str(v)
+        return out
+
+    def image_id_and_username(self, region: str, gpu: bool) -> Tuple[str, str]:
+        """(AMI, SSH user) for an instance with or without GPUs.
+
+        ``os_images`` configures them per kind: ``{"cpu": {"name", "owner", "user"}, "amd": {...}}``
+        (name pattern, owner account or ``self``; a kind left out is not launchable), or the
+        older ``{"cpu": {region: ami}, "amd": {...}}`` map. Without ``os_images``: Canonical's Ubuntu
+        22.04 (the ROCm driver comes from the shim's host setup). The newest *available* image wins."""
         imgs = self.config.get("os_images") or {}
         key = "amd" if gpu else "cpu"
-        if isinstance(imgs.get(key), dict) and imgs[key].get(region):
-            return imgs[key][region]
-        items = self._paginate(region, "DescribeImages", {
-            "Owner.1": UBUNTU_OWNER, "Filter.1.Name": "name",
-            "Filter.1.Value.1": "ubuntu/images/hvm-ssd/ubuntu-jammy-22.04-amd64-server-*",
-            "Filter.2.Name": "state", "Filter.2.Value.1": "available"}, "./imagesSet/item")
-        pairs = [(i.findtext("creationDate") or "", i.findtext("imageId")) for i in items if i.findtext("imageId")]
-        if not pairs:
-            raise ComputeError(f"no Ubuntu 22.04 AMI in {region}")
-        return max(pairs)[1]
+        if imgs:
+            spec = imgs.get(key) or (imgs.get("nvidia") if gpu and "amd" not in imgs else None)
+            if not spec:
+                logger.warning("%s image not configured in os_images", key)
+                raise ComputeResourceNotFoundError(f"no {key} image configured in os_images")
+            if "name" not in spec:  # region -> AMI map
+                if spec.get(region):
+                    return spec[region], self.SSH_USER
+                raise ComputeResourceNotFoundError(f"no {key} image configured for {region}")
+            name, owner, user = spec["name"], spec.get("owner") or "self", spec.get("user") or self.SSH_USER
+        else:
+            name, owner, user = "ubuntu/images/hvm-ssd/ubuntu-jammy-22.04-amd64-server-*", UBUNTU_OWNER, self.SSH_USER
+        items = self._paginate(region, "DescribeImages", {"Owner.1": owner, "Filter.1.Name": "name",
+                                                           "Filter.1.Value.1": name}, "./imagesSet/item")
+        avail = [(i.findtext("creationDate") or "", i.findtext("imageId")) for i in items
+                 if i.findtext("imageId") and (i.findtext("imageState") or "available") == "available"]
+        if not avail:
+            logger.warning("image '%s' not found in %s", name, region)
+            raise ComputeResourceNotFoundError(f"image '{name}' (owner {owner}) not found in {region}")
+        return max(avail)[1], user
 
     def _vpc_id(self, region: str) -> Optional[str]:
         """``vpc_ids: {region: vpc-...}`` or ``vpc_name`` (tag Name) from the backend config; None =
@@ -299,13 +330,9 @@ class AWSCompute(VMCompute):
             "BlockDeviceMapping.1.DeviceName": "/dev/sda1",
             "BlockDeviceMapping.1.Ebs.VolumeSize": str(max(100, res.disk.size_mib // 1024)),
             "BlockDeviceMapping.1.Ebs.VolumeType": "gp3",
-            "TagSpecification.1.ResourceType": "instance",
+            **self._tag_spec("instance", {"Name": cfg.instance_name, "owner": "dstack",
+                                          "dstack_project": cfg.project_name, "dstack_user": cfg.user or ""}),
         }
-        tags = {"Name": cfg.instance_name, "owner": "dstack", "dstack_project": cfg.project_name,
-                "dstack_user": cfg.user or "", **(self.config.get("tags") or {})}
-        for i, (k, v) in enumerate(tags.items(), 1):
-            params[f"TagSpecification.1.Tag.{i}.Key"] = k
-            params[f"TagSpecification.1.Tag.{i}.Value"] = str(v)
         if capacity_block:
             params["InstanceMarketOptions.MarketType"] = "capacity-block"
         elif res.spot:
@@ -355,7 +382,7 @@ class AWSCompute(VMCompute):
                 cfg = cfg.model_copy(update={"availability_zone": rsv["az"]})
         if cfg.availability_zone and subnets:
             subnets = [x for x in subnets if x[1] == cfg.availability_zone] or subnets
-        image_id = self._image_id(region, bool(offer.instance.resources.gpus))
+        image_id, ssh_user = self.image_id_and_username(region, bool(offer.instance.resources.gpus))
         sg = self._security_group(region, cfg.project_name, vpc_id)
         attempts = subnets or [(None, cfg.availability_zone or "")]
         tried, last = set(), None
@@ -374,7 +401,7 @@ class AWSCompute(VMCompute):
             iid = root.findtext(".//instancesSet/item/instanceId")
             if not iid:
                 raise ComputeError("RunInstances returned no instance id")
-            return iid, None, {"region": region, "public_ip": public_ip, "efa_interfaces": efa}
+            return iid, None, {"region": region, "public_ip": public_ip, "efa_interfaces": efa, "ssh_user": ssh_user}
         raise last or NoCapacityError(f"no capacity for {offer.instance.name} in {region}")
 
     def _describe(self, instance_id: str, region: str, backend_data: dict) -> dict:
@@ -422,8 +449,8 @@ class AWSCompute(VMCompute):
         zone = getattr(conf, "availability_zone", None) or f"{conf.region}a"
         root = self._call(conf.region, "CreateVolume", {
             "AvailabilityZone": zone, "Size": str(int(conf.size or 100)), "VolumeType": "gp3",
-            "TagSpecification.1.ResourceType": "volume", "TagSpecification.1.Tag.1.Key": "Name",
-            "TagSpecification.1.Tag.1.Value": volume.name})
+            **self._tag_spec("volume", {"Name": volume.name, "owner": "dstack",
+                                        "dstack_project": volume.project_name})})
         return VolumeProvisioningData(volume_id=root.findtext("volumeId"), size_gb=int(root.findtext("size") or 0),
                                       availability_zone=zone, price=0.08 * float(conf.size or 100) / 730)
 
@@ -460,8 +487,8 @@ class AWSCompute(VMCompute):
         sg = self._gateway_security_group(region, configuration.project_name, self._vpc_id(region))
         params = {"ImageId": self._image_id(region, False), "InstanceType": "t3.small", "MinCount": "1",
                   "MaxCount": "1", "UserData": base64.b64encode(gateway_cloud_init(configuration).encode()).decode(),
-                  "TagSpecification.1.ResourceType": "instance", "TagSpecification.1.Tag.1.Key": "Name",
-                  "TagSpecification.1.Tag.1.Value": configuration.instance_name}
+                  **self._tag_spec("instance", {"Name": configuration.instance_name, "owner": "dstack",
+                                                "dstack_project": configuration.project_name, "role": "gateway"})}
         subnets = self._subnets(region, self._vpc_id(region), public)
         if subnets or not public:
             if not subnets:

@@ -165,7 +165,8 @@ class VMCompute(CatalogOffers, Compute):
         instance_id, hostname, backend_data = self._launch(instance_offer, instance_config)
         return JobProvisioningData(
             backend=self.TYPE, instance_type=instance_offer.instance, instance_id=instance_id, hostname=hostname,
-            internal_ip=None, region=instance_offer.region, price=instance_offer.price, username=self.SSH_USER,
+            internal_ip=None, region=instance_offer.region, price=instance_offer.price,
+            username=(backend_data or {}).get("ssh_user") or self.SSH_USER,  # a configured OS image's user
             ssh_port=22, dockerized=self.DOCKERIZED, backend_data=json.dumps(backend_data) if backend_data else None)
 
     def update_provisioning_data(self, provisioning_data: JobProvisioningData, project_ssh_public_key: str = "",

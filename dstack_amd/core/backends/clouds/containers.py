@@ -291,13 +291,8 @@ class KubernetesCompute(ContainerCompute):
         for n in nodes:
             alloc = n.get("status", {}).get("allocatable", {})
             labels = n.get("metadata", {}).get("labels", {})
-            ngpu = int(alloc.get("amd.com/gpu", 0) or 0)
-            gname = labels.get("amd.com/gpu.product-name") or labels.get("beta.amd.com/gpu.product-name") or "MI300X"
-            from dstack_amd.core.models.gpus import normalize_gpu_name
-
-            gname = normalize_gpu_name(gname)
             res = Resources(cpus=_cpu(alloc.get("cpu", "1")), memory_mib=_mem_mib(alloc.get("memory", "0")),
-                            gpus=[Gpu(name=gname, memory_mib=0, vendor="amd") for _ in range(ngpu)], spot=False,
+                            gpus=gpus_from_node_labels(labels, alloc), spot=False,
                             disk=Disk(size_mib=_mem_mib(alloc.get("ephemeral-storage", "100Gi"))))
             o = InstanceOfferWithAvailability(backend=self.TYPE, instance=InstanceType(
                 name=n["metadata"]["name"], resources=res), region=self.namespace, price=0.0,
@@ -417,6 +412,58 @@ class KubernetesCompute(ContainerCompute):
             r = self.http.delete(self._url(f"/api/v1/namespaces/{self.namespace}/{kind}/{n}"), headers=self._h())
             if r.status_code not in (200, 202, 404):
                 check_response(r, f"k8s delete gateway {kind}")
+
+
+# AMD GPU operator's node labeller: PCI device id -> catalog name (when product-name is absent)
+_AMD_DEVICE_IDS = {"75a3": "MI355X", "75a0": "MI350X", "74a5": "MI325X", "74a1": "MI300X", "74a0": "MI300A",
+                   "740c": "MI250X", "740f": "MI210", "738c": "MI100"}
+
+
+def gpus_from_node_labels(labels: dict, allocatable: Optional[dict] = None):
+    """The GPUs a Kubernetes node offers, from its device-plugin resources and node labels (reference
+    ``C/backends/kubernetes/compute.py`` ``_get_gpus_from_node_labels``, which reads NVIDIA's GPU
+    feature discovery labels only).
+
+    AMD first: the count is the allocatable ``amd.com/gpu`` (or the ``amd.com/gpu.count`` label), the
+    model the labeller's ``amd.com/gpu.product-name`` (``AMD_Instinct_MI300X_OAM``) or
+    ``amd.com/gpu.device-id``, the memory ``amd.com/gpu.vram`` (``192G``) or the catalog's. NVIDIA:
+    ``nvidia.com/gpu.count`` + ``nvidia.com/gpu.product`` (``A100-SXM4-80GB``), memory from
+    ``nvidia.com/gpu.memory`` (MiB), the product's ``<n>GB`` suffix or the catalog. A node whose
+    GPU model cannot be told offers no GPUs (it is not guessed)."""
+    import re as _re
+
+    from dstack_amd.core.models.gpus import convert_nvidia_gpu_name, gpu_info, normalize_gpu_name
+    from dstack_amd.core.models.instances import Gpu
+
+    allocatable = allocatable or {}
+    amd_n = int(allocatable.get("amd.com/gpu") or labels.get("amd.com/gpu.count") or 0)
+    if amd_n:
+        product = labels.get("amd.com/gpu.product-name") or labels.get("beta.amd.com/gpu.product-name")
+        name = normalize_gpu_name(product.replace("_", " ")) if product else None
+        if not name:
+            dev = str(labels.get("amd.com/gpu.device-id") or labels.get("beta.amd.com/gpu.device-id") or "").lower()
+            name = _AMD_DEVICE_IDS.get(dev.removeprefix("0x"))
+        if not name:
+            return []
+        vram = _re.fullmatch(r"(\d+)\s*([GM])i?B?", str(labels.get("amd.com/gpu.vram") or ""), _re.I)
+        if vram:
+            mib = int(vram.group(1)) * (1024 if vram.group(2).upper() == "G" else 1)
+        else:
+            info = gpu_info(name)
+            mib = int(info.memory_gb * 1024) if info else 0
+        return [Gpu(name=name, memory_mib=mib, vendor="amd") for _ in range(amd_n)]
+    nv_n = int(labels.get("nvidia.com/gpu.count") or allocatable.get("nvidia.com/gpu") or 0)
+    product = labels.get("nvidia.com/gpu.product")
+    if not nv_n or not product:
+        return []
+    name = convert_nvidia_gpu_name(product.split("-")[0].replace("NVIDIA", "").strip() or product)
+    if labels.get("nvidia.com/gpu.memory"):
+        mib = int(labels["nvidia.com/gpu.memory"])
+    else:
+        m = _re.search(r"(\d+)GB", product, _re.I)
+        info = gpu_info(name)
+        mib = int(m.group(1)) * 1024 if m else (int(info.memory_gb * 1024) if info else 0)
+    return [Gpu(name=name, memory_mib=mib, vendor="nvidia") for _ in range(nv_n)]
 
 
 def _cpu(v: str) -> int:

@@ -18,14 +18,17 @@ from __future__ import annotations
 
 import base64
 import email.utils
+import enum
 import hashlib
 import json
+import re
 import time
 import urllib.parse
-from dataclasses import replace
+from dataclasses import dataclass, replace
 from typing import Dict, List, Optional, Tuple
 
 from dstack_amd.core.backends.catalog import CatalogRow, offline_rows
+from dstack_amd.core.backends.clouds.tags import merged_tags
 from dstack_amd.core.backends.clouds.common import (
     OAuthToken,
     VMCompute,
@@ -36,7 +39,54 @@ from dstack_amd.core.backends.clouds.common import (
 )
 from dstack_amd.core.errors import BackendAuthError, ComputeError, ServerClientError
 from dstack_amd.core.models.backends import BackendType
-from dstack_amd.core.models.instances import InstanceAvailability
+from dstack_amd.core.models.instances import InstanceAvailability, InstanceType
+
+
+class AzureImageVariant(enum.Enum):
+    """Which marketplace image an Azure VM boots (the reference picks among its own prebuilt
+    ``dstack-{,cuda-,grid-}<ver>`` images, ``C/backends/azure/compute.py:342-363``; here the vendor
+    images are used and the shim installs the rest):
+
+    * ``ROCM``: AMD Instinct VMs (``ND*_MI300X_v5``) -> the HPC image with ROCm and the amdgpu driver.
+    * ``NVIDIA``: NVIDIA VMs -> the HPC image with the CUDA driver (``_A10_v5`` GRID VMs included;
+      they need the GRID driver, which the shim's host setup installs).
+    * ``STANDARD``: CPU VMs -> Canonical Ubuntu 22.04.
+
+    ``vm_images`` in the backend config overrides any of them by variant name in lower case
+    (``{"rocm": {"publisher", "offer", "sku", "version"}}``)."""
+
+    ROCM = "rocm"
+    NVIDIA = "nvidia"
+    STANDARD = "standard"
+
+    @classmethod
+    def from_instance_type(cls, instance: InstanceType) -> "AzureImageVariant":
+        gpus = instance.resources.gpus
+        if not gpus:
+            return cls.STANDARD
+        g = gpus[0]
+        vendor = getattr(g.vendor, "value", g.vendor)
+        if vendor == "amd" or "MI300X" in instance.name or g.name.upper().startswith("MI"):
+            return cls.ROCM
+        return cls.NVIDIA
+
+    def image_reference(self, overrides: Optional[dict] = None) -> dict:
+        over = (overrides or {}).get(self.value)
+        if over:
+            return {"version": "latest", **over}
+        return {
+            AzureImageVariant.ROCM: {"publisher": "microsoft-dsvm", "offer": "ubuntu-hpc", "sku": "2204-rocm",
+                                     "version": "latest"},
+            AzureImageVariant.NVIDIA: {"publisher": "microsoft-dsvm", "offer": "ubuntu-hpc", "sku": "2204",
+                                       "version": "latest"},
+            AzureImageVariant.STANDARD: {"publisher": "Canonical", "offer": "0001-com-ubuntu-server-jammy",
+                                         "sku": "22_04-lts-gen2", "version": "latest"},
+        }[self]
+
+
+def gcp_label(value: str) -> str:
+    """A GCP label value from a free-form name: lower case, ``[a-z0-9_-]``, at most 63 characters."""
+    return re.sub(r"[^a-z0-9_\-]", "-", value.lower())[:63]
 
 
 # ---------------------------------------------------------------------------------------------
@@ -166,14 +216,14 @@ class AzureCompute(VMCompute):
         ]
 
     def _template(self, name: str, size: str, region: str, user_data: str, disk_gb: int, spot: bool,
-                  public_keys, extra_ports=()) -> dict:
+                  public_keys, extra_ports=(), image: Optional[dict] = None, tags: Optional[dict] = None) -> dict:
         own_network = not self.config.get("subnet_id")
         subnet = self.config.get("subnet_id") or (
             f"[resourceId('Microsoft.Network/virtualNetworks/subnets', 'dstack-vnet-{region}', 'default')]")
         vm_props = {
             "hardwareProfile": {"vmSize": size},
-            "storageProfile": {"imageReference": {"publisher": "Canonical", "offer": "0001-com-ubuntu-server-jammy",
-                                                  "sku": "22_04-lts-gen2", "version": "latest"},
+            "storageProfile": {"imageReference": image or AzureImageVariant.STANDARD.image_reference(
+                                   self.config.get("vm_images")),
                                "osDisk": {"createOption": "FromImage", "diskSizeGB": disk_gb,
                                           "deleteOption": "Delete"}},
             "osProfile": {"computerName": name[:15], "adminUsername": self.SSH_USER,
@@ -212,6 +262,9 @@ class AzureCompute(VMCompute):
              "dependsOn": [f"[resourceId('Microsoft.Network/networkInterfaces', '{name}-nic')]"],
              "properties": vm_props},
         ]
+        tags = merged_tags("azure", {"owner": "dstack", **(tags or {})}, self.config)
+        for r in res:
+            r["tags"] = tags
         return {"$schema": "https://schema.management.azure.com/schemas/2019-04-01/deploymentTemplate.json#",
                 "contentVersion": "1.0.0.0", "resources": res}
 
@@ -219,9 +272,11 @@ class AzureCompute(VMCompute):
         region = offer.region
         rg = self._rg(region)
         name = cfg.instance_name.replace("_", "-")[:60]
+        image = AzureImageVariant.from_instance_type(offer.instance).image_reference(self.config.get("vm_images"))
         tpl = self._template(name, offer.instance.name, region, cloud_init(cfg),
                              max(100, offer.instance.resources.disk.size_mib // 1024), offer.instance.resources.spot,
-                             cfg.get_public_keys())
+                             cfg.get_public_keys(), image=image,
+                             tags={"dstack_project": cfg.project_name, "dstack_user": cfg.user or ""})
         url = (f"{self.ARM}/subscriptions/{self.subscription}/resourcegroups/{rg}/providers/"
                f"Microsoft.Resources/deployments/{name}?api-version=2021-04-01")
         check_response(self.http.put(url, headers=self._h(), json={"properties": {"mode": "Incremental",
@@ -278,7 +333,8 @@ class AzureCompute(VMCompute):
         name = f"{configuration.instance_name}".replace("_", "-")[:60]
         tpl = self._template(name, self.config.get("gateway_vm_size", "Standard_B2s"), region,
                              gateway_cloud_init(configuration), 30, False, [configuration.ssh_key_pub.strip()],
-                             extra_ports=(80, 443))
+                             extra_ports=(80, 443), tags={"dstack_project": configuration.project_name,
+                                                          "role": "gateway"})
         url = (f"{self.ARM}/subscriptions/{self.subscription}/resourcegroups/{rg}/providers/"
                f"Microsoft.Resources/deployments/{name}?api-version=2021-04-01")
         check_response(self.http.put(url, headers=self._h(), json={"properties": {"mode": "Incremental",
@@ -414,7 +470,8 @@ class GCPCompute(VMCompute):
             "metadata": {"items": [{"key": "user-data", "value": cloud_init(cfg)},
                                    {"key": "ssh-keys", "value": "\n".join(f"{self.SSH_USER}:{k}"
                                                                          for k in cfg.get_public_keys())}]},
-            "labels": {"owner": "dstack", "dstack_project": cfg.project_name.lower()},
+            "labels": merged_tags("gcp", {"owner": "dstack", "dstack_project": gcp_label(cfg.project_name),
+                                          "dstack_user": gcp_label(cfg.user or "")}, self.config),
             "scheduling": {"provisioningModel": "SPOT" if res.spot else "STANDARD",
                            "onHostMaintenance": "TERMINATE" if res.gpus else "MIGRATE",
                            "automaticRestart": False},
@@ -492,7 +549,8 @@ class GCPCompute(VMCompute):
                                    "accessConfigs": [{"type": "ONE_TO_ONE_NAT", "name": "External NAT"}]}],
             "metadata": {"items": [{"key": "user-data", "value": gateway_cloud_init(configuration)},
                                    {"key": "ssh-keys", "value": f"ubuntu:{configuration.ssh_key_pub.strip()}"}]},
-            "labels": {"owner": "dstack", "dstack_project": configuration.project_name.lower(), "role": "gateway"},
+            "labels": merged_tags("gcp", {"owner": "dstack", "dstack_project": gcp_label(configuration.project_name),
+                                          "role": "gateway"}, self.config),
         }
         r = check_response(self.http.post(f"{self.API}/projects/{self.project}/zones/{zone}/instances",
                                           headers=self._h(), json=body), "gcp gateway insert")
@@ -537,7 +595,8 @@ class GCPCompute(VMCompute):
         name = f"{volume.name}-{str(volume.id)[:8]}".lower().replace("_", "-")[:62]
         body = {"name": name, "sizeGb": str(size), "type": f"zones/{zone}/diskTypes/"
                 f"{self.config.get('volume_disk_type', 'pd-balanced')}",
-                "labels": {"owner": "dstack", "dstack_project": volume.project_name.lower()}}
+                "labels": merged_tags("gcp", {"owner": "dstack", "dstack_project": gcp_label(volume.project_name)},
+                                      self.config)}
         r = check_response(self.http.post(self._disk_url(zone), headers=self._h(), json=body), "gcp create disk")
         self._wait_op(r, "gcp create disk")
         return VolumeProvisioningData(backend=self.TYPE, volume_id=name, size_gb=size, availability_zone=zone,
@@ -573,6 +632,64 @@ class GCPCompute(VMCompute):
             return True
         users = check_response(r, "gcp get disk").json().get("users") or []
         return not any(u.rstrip("/").endswith(f"/instances/{instance_id}") for u in users)
+
+
+class ShapesQuota:
+    """Which shapes the compartment may launch where: region -> availability domain -> shape
+    names, as ``ListShapes`` reports per AD (reference ``C/backends/oci/resources.py:72-93``)."""
+
+    def __init__(self, region_ads: Dict[str, Dict[str, set]]):
+        self._by_ad = {ad: set(shapes) for ads in region_ads.values() for ad, shapes in ads.items()}
+        self._by_region = {region: set().union(*ads.values()) if ads else set() for region, ads in region_ads.items()}
+        self._ads = {region: sorted(ads) for region, ads in region_ads.items()}
+
+    def is_within_region_quota(self, shape: str, region: str) -> bool:
+        return shape in self._by_region.get(region, ())
+
+    def is_within_domain_quota(self, shape: str, ad: str) -> bool:
+        return shape in self._by_ad.get(ad, ())
+
+    def domains_for(self, shape: str, region: str) -> List[str]:
+        return [ad for ad in self._ads.get(region, []) if shape in self._by_ad[ad]]
+
+
+@dataclass(frozen=True)
+class SecurityRule:
+    """A security-list rule reduced to what decides its effect, so rules read back from the API
+    (with ids, timestamps, ``isStateless: false`` defaults, options objects) compare equal to the ones
+    dstack wants (reference ``C/backends/oci/resources.py`` ``SecurityRule.from_sdk_rule``)."""
+
+    direction: str  # "INGRESS" | "EGRESS"
+    protocol: str  # "all", "6" (TCP), "17" (UDP), "1" (ICMP)
+    peer: str  # source (ingress) / destination (egress) CIDR
+    peer_type: str = "CIDR_BLOCK"
+    is_stateless: bool = False
+    ports: Optional[Tuple[int, int]] = None
+    icmp: Optional[Tuple[int, Optional[int]]] = None
+
+    @classmethod
+    def from_api(cls, rule: dict, direction: str) -> "SecurityRule":
+        ingress = direction == "INGRESS"
+        opts = rule.get("tcpOptions") or rule.get("udpOptions") or {}
+        rng = opts.get("destinationPortRange")
+        icmp = rule.get("icmpOptions")
+        return cls(direction=direction, protocol=str(rule.get("protocol", "all")),
+                   peer=rule.get("source" if ingress else "destination", ""),
+                   peer_type=rule.get("sourceType" if ingress else "destinationType") or "CIDR_BLOCK",
+                   is_stateless=bool(rule.get("isStateless", False)),
+                   ports=(int(rng["min"]), int(rng["max"])) if rng else None,
+                   icmp=(int(icmp["type"]), icmp.get("code")) if icmp else None)
+
+    def to_api(self) -> dict:
+        ingress = self.direction == "INGRESS"
+        d = {"protocol": self.protocol, ("source" if ingress else "destination"): self.peer,
+             ("sourceType" if ingress else "destinationType"): self.peer_type, "isStateless": self.is_stateless}
+        if self.ports:
+            d["udpOptions" if self.protocol == "17" else "tcpOptions"] = {
+                "destinationPortRange": {"min": self.ports[0], "max": self.ports[1]}}
+        if self.icmp:
+            d["icmpOptions"] = {"type": self.icmp[0], **({"code": self.icmp[1]} if self.icmp[1] is not None else {})}
+        return d
 
 
 # ---------------------------------------------------------------------------------------------
@@ -684,12 +801,7 @@ class OCICompute(VMCompute):
                 {"destination": "0.0.0.0/0", "destinationType": "CIDR_BLOCK", "networkEntityId": igw["id"]}]}),
                 "oci update route table")
         sl_id = vcn["defaultSecurityListId"]
-        check_response(self._signed("PUT", region, f"/{self.API_VERSION}/securityLists/{sl_id}", {
-            "ingressSecurityRules": [
-                {"protocol": "6", "source": "0.0.0.0/0", "tcpOptions": {"destinationPortRange": {"min": 22, "max": 22}}},
-                {"protocol": "all", "source": self.VCN_CIDR},
-                {"protocol": "1", "source": "0.0.0.0/0", "icmpOptions": {"type": 3, "code": 4}}],
-            "egressSecurityRules": [{"protocol": "all", "destination": "0.0.0.0/0"}]}), "oci update security list")
+        self._ensure_security_rules(region, sl_id)
         subnet = self._list_named(region, "subnets", f"{self.NET_NAME}-subnet", compartmentId=comp, vcnId=vcn["id"])
         if subnet is None:
             subnet = check_response(self._signed("POST", region, f"/{self.API_VERSION}/subnets", {
@@ -699,6 +811,30 @@ class OCICompute(VMCompute):
         subnet = self._wait_available(region, "subnets", subnet)
         self.config.setdefault("subnet_ids", {})[region] = subnet["id"]
         return subnet["id"]
+
+    def required_security_rules(self) -> List[SecurityRule]:
+        """SSH from anywhere, everything inside the VCN (RCCL/RDMA between nodes), path-MTU ICMP, any egress."""
+        return [SecurityRule("INGRESS", "6", "0.0.0.0/0", ports=(22, 22)),
+                SecurityRule("INGRESS", "all", self.VCN_CIDR),
+                SecurityRule("INGRESS", "1", "0.0.0.0/0", icmp=(3, 4)),
+                SecurityRule("EGRESS", "all", "0.0.0.0/0")]
+
+    def _ensure_security_rules(self, region: str, sl_id: str) -> bool:
+        """Add the rules dstack needs to the security list, keeping the ones already there;
+        no update when all are present. True when the list was changed."""
+        path = f"/{self.API_VERSION}/securityLists/{sl_id}"
+        cur = check_response(self._signed("GET", region, path), "oci security list").json()
+        have = {"INGRESS": [SecurityRule.from_api(r, "INGRESS") for r in cur.get("ingressSecurityRules") or []],
+                "EGRESS": [SecurityRule.from_api(r, "EGRESS") for r in cur.get("egressSecurityRules") or []]}
+        missing = [r for r in self.required_security_rules() if r not in have[r.direction]]
+        if not missing:
+            return False
+        for r in missing:
+            have[r.direction].append(r)
+        check_response(self._signed("PUT", region, path, {
+            "ingressSecurityRules": [r.to_api() for r in have["INGRESS"]],
+            "egressSecurityRules": [r.to_api() for r in have["EGRESS"]]}), "oci update security list")
+        return True
 
     def prepare_config(self) -> dict:
         """At backend creation: compartment + per-region networks, recorded in the stored config
@@ -737,14 +873,9 @@ class OCICompute(VMCompute):
         base = offline_rows(self.TYPE)
         wanted = self.config.get("regions")
         regions = sorted(set(wanted or []) | {r.location for r in base if not wanted})
-        names = {r.instance_name for r in base}
-        shape_ads: Dict[Tuple[str, str], List[str]] = {}
-        for region in regions:
-            for ad in self._availability_domains(region):
-                for shape in self._shapes(region, ad):
-                    if shape in names:
-                        shape_ads.setdefault((shape, region), []).append(ad)
-        self._shape_ads = shape_ads
+        quota = ShapesQuota({region: {ad: set(self._shapes(region, ad)) for ad in self._availability_domains(region)}
+                             for region in regions})
+        self._quota = quota
         specs: Dict[Tuple[str, bool], CatalogRow] = {}
         for r in base:
             specs.setdefault((r.instance_name, r.spot), r)
@@ -752,14 +883,16 @@ class OCICompute(VMCompute):
         for (name, spot), proto in sorted(specs.items()):
             for region in regions:
                 out.append(replace(proto, location=region, availability=InstanceAvailability.UNKNOWN
-                                   if (name, region) in shape_ads else InstanceAvailability.NOT_AVAILABLE))
+                                   if quota.is_within_region_quota(name, region)
+                                   else InstanceAvailability.NOT_AVAILABLE))
         return out
 
     def _ad_for(self, region: str, shape: str) -> str:
         ads = self.config.get("availability_domains") or {}
         if ads.get(region):
             return ads[region]
-        offered = getattr(self, "_shape_ads", {}).get((shape, region))
+        quota = getattr(self, "_quota", None)
+        offered = quota.domains_for(shape, region) if quota else []
         if offered:
             return offered[0]
         for ad in self._availability_domains(region):

@@ -14,7 +14,7 @@ from __future__ import annotations
 
 from typing import Annotated, Dict, List, Literal, Optional, Tuple, Union
 
-from pydantic import Field, ValidationError
+from pydantic import Field, ValidationError, field_validator
 
 from dstack_amd.core.errors import ServerClientError
 from dstack_amd.core.models.common import CoreModel
@@ -93,6 +93,17 @@ class IAMTokenCreds(_Input):
 
 
 # ---- backend configs ---------------------------------------------------------------------------
+def _check_tags(cloud: str, tags: Optional[Dict[str, str]]) -> Optional[Dict[str, str]]:
+    from dstack_amd.core.backends.clouds.tags import validate_tags
+    from dstack_amd.core.errors import BackendError
+
+    try:
+        validate_tags(cloud, tags)
+    except BackendError as e:
+        raise ValueError(str(e)) from None
+    return tags
+
+
 class AWSOSImage(_Input):
     name: str
     owner: str = "self"
@@ -117,6 +128,8 @@ class AWSConfig(_Input):
     os_images: Optional[AWSOSImages] = None
     creds: Annotated[Union[AccessKeyCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
 
+    _tags = field_validator("tags")(classmethod(lambda cls, v: _check_tags("aws", v)))
+
 
 class AzureConfig(_Input):
     type: Literal["azure"] = "azure"
@@ -129,7 +142,10 @@ class AzureConfig(_Input):
     subnet_id: Optional[str] = None
     public_ips: Optional[bool] = None
     tags: Optional[Dict[str, str]] = None
+    vm_images: Optional[Dict[str, Dict[str, str]]] = None  # AzureImageVariant overrides: rocm/nvidia/standard
     creds: Annotated[Union[ClientCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
+
+    _tags = field_validator("tags")(classmethod(lambda cls, v: _check_tags("azure", v)))
 
 
 class GCPConfig(_Input):
@@ -144,6 +160,8 @@ class GCPConfig(_Input):
     vm_service_account: Optional[str] = None
     tags: Optional[Dict[str, str]] = None
     creds: Annotated[Union[ServiceAccountCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
+
+    _tags = field_validator("tags")(classmethod(lambda cls, v: _check_tags("gcp", v)))
 
 
 class OCIConfig(_Input):

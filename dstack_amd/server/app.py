@@ -26,6 +26,7 @@ from dstack_amd.core.errors import (
 )
 from dstack_amd.server import settings
 from dstack_amd.server.db import migrate, session_scope
+from dstack_amd.server.utils.routers import check_client_server_compatibility
 
 logger = logging.getLogger("dstack_amd.server")
 
@@ -191,10 +192,9 @@ def register_routes(app: FastAPI):
     @app.middleware("http")
     async def log_request(request: Request, call_next):
         start = time.perf_counter()
-        client_version = request.headers.get("x-api-version")
-        if client_version and not _compatible(client_version):
-            return _error(400, f"The client version {client_version} is incompatible with the server {__version__}",
-                          "error")
+        err = check_client_server_compatibility(request.headers.get("x-api-version"), _server_version())
+        if err:
+            return _error(400, err, "error")
         response = await call_next(request)
         logger.debug("%s %s %s %.1f ms", request.method, request.url.path, response.status_code,
                      (time.perf_counter() - start) * 1e3)
@@ -254,10 +254,6 @@ def jsonable_errors(errors):
     return out
 
 
-def _compatible(client_version: str) -> bool:
-    if client_version in ("latest", "0.0.0") or __version__.startswith("0.0"):
-        return True
-    try:
-        return client_version.split(".")[0] == __version__.split(".")[0]
-    except Exception:  # noqa: BLE001
-        return True
+def _server_version() -> Optional[str]:
+    """None for development builds (``0.0.x``): they accept every client."""
+    return None if __version__.startswith("0.0") else __version__

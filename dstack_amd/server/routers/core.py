@@ -3,6 +3,7 @@
 
 from __future__ import annotations
 
+import os
 from typing import List, Tuple
 
 import yaml
@@ -246,6 +247,9 @@ def delete_repos(body: schemas.DeleteReposRequest, up: UP = Depends(project_mana
     return {}
 
 
+CODE_UPLOAD_LIMIT = int(os.environ.get("DSTACK_SERVER_CODE_UPLOAD_LIMIT", 64 * 2**20))
+
+
 @repos_router.post("/upload_code")
 async def upload_code(request: Request, repo_id: str, up: UP = Depends(project_member)):
     import hashlib
@@ -254,7 +258,12 @@ async def upload_code(request: Request, repo_id: str, up: UP = Depends(project_m
 
     from dstack_amd.server.db import session_scope
 
-    blob = await request.body()
+    from dstack_amd.server.utils.common import ajoin_byte_stream_checked
+
+    # the body is read up to the cap (plus multipart framing) and no further
+    blob = await ajoin_byte_stream_checked(request.stream(), CODE_UPLOAD_LIMIT + 2**16)
+    if blob is None:
+        raise ServerClientError(f"Code blob exceeds {CODE_UPLOAD_LIMIT // 2**20} MiB; use a remote repo or .dstackignore")
     ctype = request.headers.get("content-type", "")
     if ctype.startswith("multipart/form-data"):
         # the reference client posts the tarball as the multipart field "file"
@@ -266,8 +275,8 @@ async def upload_code(request: Request, repo_id: str, up: UP = Depends(project_m
         if not parts:
             raise ServerClientError("multipart upload without a 'file' field")
         blob = parts[0].get_payload(decode=True) or b""
-    if len(blob) > 64 * 2**20:
-        raise ServerClientError("Code blob exceeds 64 MiB; use a remote repo or .dstackignore")
+    if len(blob) > CODE_UPLOAD_LIMIT:
+        raise ServerClientError(f"Code blob exceeds {CODE_UPLOAD_LIMIT // 2**20} MiB; use a remote repo or .dstackignore")
     blob_hash = hashlib.sha256(blob).hexdigest()
     project_id = up[1].id
 

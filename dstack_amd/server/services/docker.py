@@ -9,6 +9,7 @@ v2: bearer-token challenge (Docker Hub, GHCR, NGC, ECR-compatible), manifest lis
 
 from __future__ import annotations
 
+import json
 import threading
 import time
 from dataclasses import dataclass
@@ -18,6 +19,7 @@ import httpx
 from pydantic import BaseModel, ConfigDict, Field, field_validator
 
 from dstack_amd.core.errors import DockerRegistryError
+from dstack_amd.server.utils.common import join_byte_stream_checked
 
 MANIFEST_TYPES = ", ".join([
     "application/vnd.docker.distribution.manifest.list.v2+json",
@@ -177,13 +179,16 @@ class RegistryClient:
                 raise DockerRegistryError(f"platform manifest: HTTP {r.status_code}", r.status_code)
             m = r.json()
         digest = parse_image_manifest(m).config.digest
-        r = self._get(f"{base}/blobs/{digest}", {}, auth, state)
-        if r.status_code != 200:
-            raise DockerRegistryError(f"config blob: HTTP {r.status_code}", r.status_code)
-        if len(r.content) > MAX_CONFIG_OBJECT_SIZE:
+        headers = {"Authorization": f"Bearer {state['token']}"} if state.get("token") else {}
+        with self.http.stream("GET", f"{base}/blobs/{digest}", headers=headers,
+                              auth=None if state.get("token") else auth) as r:
+            if r.status_code != 200:
+                raise DockerRegistryError(f"config blob: HTTP {r.status_code}", r.status_code)
+            body = join_byte_stream_checked(r.iter_bytes(), MAX_CONFIG_OBJECT_SIZE)  # stop reading past the cap
+        if body is None:
             raise DockerRegistryError(f"image config object exceeds the size limit of {MAX_CONFIG_OBJECT_SIZE} bytes")
         try:
-            obj = r.json()
+            obj = json.loads(body)
         except ValueError as e:
             raise DockerRegistryError(f"malformed image config: {e}") from e
         cfg = parse_image_config_object(obj)

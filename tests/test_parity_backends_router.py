@@ -159,8 +159,16 @@ class _FakeOCI:
             obj["defaultSecurityListId"] = f"ocid1.sl.{self.n}"
             self._store("routeTables", region).append({"id": obj["defaultRouteTableId"], "routeRules": [],
                                                        "lifecycleState": "AVAILABLE"})
-            self._store("securityLists", region).append({"id": obj["defaultSecurityListId"],
-                                                         "lifecycleState": "AVAILABLE"})
+            self._store("securityLists", region).append({
+                "id": obj["defaultSecurityListId"], "lifecycleState": "AVAILABLE",
+                # OCI's default list: SSH from anywhere, as the API returns it (ids, timestamps, defaults)
+                "ingressSecurityRules": [{"protocol": "6", "source": "0.0.0.0/0", "sourceType": "CIDR_BLOCK",
+                                          "isStateless": False, "id": "r1", "timeCreated": "2024-01-01T00:00:00Z",
+                                          "tcpOptions": {"destinationPortRange": {"min": 22, "max": 22},
+                                                         "sourcePortRange": None}},
+                                         {"protocol": "6", "source": "192.168.0.0/16", "isStateless": False,
+                                          "tcpOptions": {"destinationPortRange": {"min": 9000, "max": 9000}}}],
+                "egressSecurityRules": []})
         self._store(kind, region).append(obj)
         return obj
 
@@ -234,7 +242,11 @@ def test_oci_backend_creation_bootstraps_the_network(client, fake_oci):
     assert rt == [{"destination": "0.0.0.0/0", "destinationType": "CIDR_BLOCK",
                    "networkEntityId": objs["internetGateways"][0]["id"]}]
     ingress = objs["securityLists"][0]["ingressSecurityRules"]
-    assert {"protocol": "all", "source": "10.0.0.0/16"} in ingress  # node-to-node (RCCL) traffic
+    from dstack_amd.core.backends.clouds.hyperscalers import SecurityRule
+
+    rules = [SecurityRule.from_api(x, "INGRESS") for x in ingress]
+    assert SecurityRule("INGRESS", "all", "10.0.0.0/16") in rules  # node-to-node (RCCL) traffic
+    assert SecurityRule("INGRESS", "6", "192.168.0.0/16", ports=(9000, 9000)) in rules  # the user's rule is kept
     assert any(x.get("tcpOptions", {}).get("destinationPortRange") == {"min": 22, "max": 22} for x in ingress)
     info = client.post("/api/project/main/backends/oci/config_info").json()
     assert info["compartment_id"] == fake_oci.objs["compartments"][0]["id"]
@@ -247,9 +259,10 @@ def test_oci_network_bootstrap_is_idempotent_and_lazy_for_new_regions(fake_oci):
     auth = {"user": "u", "tenancy": "t", "fingerprint": "f", "region": "us-chicago-1", "key_content": "k"}
     comp = OCICompute({"regions": ["us-chicago-1"]}, auth, None)
     first = comp.ensure_network("us-chicago-1")
-    n_posts = sum(1 for m, *_ in fake_oci.calls if m == "POST")
+    n_writes = sum(1 for m, *_ in fake_oci.calls if m in ("POST", "PUT"))
     again = OCICompute({"regions": ["us-chicago-1"]}, auth, None).ensure_network("us-chicago-1")
-    assert again == first and sum(1 for m, *_ in fake_oci.calls if m == "POST") == n_posts
+    # nothing created or rewritten the second time (the security rules read back compare equal)
+    assert again == first and sum(1 for m, *_ in fake_oci.calls if m in ("POST", "PUT")) == n_writes
     # a region without a recorded subnet gets its own VCN + subnet at launch
     assert comp.ensure_network("us-ashburn-1") != first
     assert set(comp.config["subnet_ids"]) == {"us-chicago-1", "us-ashburn-1"}

@@ -294,3 +294,52 @@ def test_model_proxy_auth(gw, upstream, monkeypatch, token, status):  # noqa: F8
     r = c.post("/api/models/main/chat/completions", headers=headers,
                json={"model": "llama", "messages": [{"role": "user", "content": "ping"}]})
     assert r.status_code == status
+
+
+class _SSEHandler(__import__("http.server").server.BaseHTTPRequestHandler):
+    """An OpenAI-format replica streaming three chunks and a TGI one streaming tokens."""
+
+    protocol_version = "HTTP/1.1"
+
+    def do_POST(self):
+        req = json.loads(self.rfile.read(int(self.headers.get("content-length", 0))) or b"{}")
+        if self.path == "/v1/chat/completions":
+            events = [json.dumps({"object": "chat.completion.chunk", "model": req["model"],
+                                  "choices": [{"index": 0, "delta": {"content": t}, "finish_reason": None}]})
+                      for t in ("po", "n", "g")] + ["[DONE]"]
+        else:  # TGI /generate_stream
+            toks = [("po", None), ("ng", None), ("<|eot_id|>", {"finish_reason": "eos_token"})]
+            events = [json.dumps({"token": {"text": t}, "details": d}) for t, d in toks]
+        body = "".join(f"data: {e}\n\n" for e in events).encode()
+        self.send_response(200)
+        self.send_header("content-type", "text/event-stream")
+        self.send_header("content-length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+
+    def log_message(self, *a):
+        pass
+
+
+def test_model_proxy_chat_completions_stream(gw):
+    import http.server
+    import threading
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _SSEHandler)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        c = TestClient(make_app(gw))
+        _model_svc(c, srv.server_address[1])
+        _svc(c, run="tgi", options={"openai": {"model": {"name": "llama-tgi", "format": "tgi"}}})
+        _rep(c, srv.server_address[1], run="tgi")
+        for model in ("llama", "llama-tgi"):
+            with c.stream("POST", "/api/models/main/chat/completions",
+                          json={"model": model, "stream": True, "messages": [{"role": "user", "content": "ping"}]}) as r:
+                assert r.status_code == 200 and r.headers["content-type"].startswith("text/event-stream")
+                events = [ln[6:] for ln in r.iter_lines() if ln.startswith("data: ")]
+            assert events[-1] == "[DONE]"
+            chunks = [json.loads(e) for e in events[:-1]]
+            assert "".join(ch["choices"][0]["delta"].get("content", "") for ch in chunks) == "pong"
+            assert all(ch["object"] == "chat.completion.chunk" for ch in chunks)
+    finally:
+        srv.shutdown()
