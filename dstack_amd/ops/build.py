@@ -24,7 +24,8 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
-BUILD = HERE.parent.parent / "build" / "ops"
+ROOT = HERE.parent.parent
+BUILD = ROOT / "build" / "ops"
 ARCH = os.environ.get("DSTACK_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -43,13 +44,19 @@ def so_path() -> Path:
     return HERE / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
+def _portable(cmd) -> str:
+    """A command line with the repository's location factored out: the tree is built here and run
+    from wherever the GPU box unpacks it, and the same sources + flags must give the same digest."""
+    return "\0".join(cmd).replace(str(ROOT), "<repo>")
+
+
 def _digest(files, cmd) -> str:
     import hashlib
 
     h = hashlib.sha256()
     for f in files:
         h.update(Path(f).name.encode() + b"\0" + Path(f).read_bytes() + b"\0")
-    h.update("\0".join(cmd).encode())
+    h.update(_portable(cmd).encode())
     return h.hexdigest()
 
 
@@ -103,7 +110,7 @@ def _plan(keep_asm: bool = False):
     ]
     import hashlib
 
-    so_digest = hashlib.sha256(("\0".join(u[2] for u in units) + "\0" + "\0".join(link)).encode()).hexdigest()
+    so_digest = hashlib.sha256(("\0".join(u[2] for u in units) + "\0" + _portable(link)).encode()).hexdigest()
     return units, link, so_digest
 
 

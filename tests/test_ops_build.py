@@ -55,3 +55,21 @@ def test_manifest_records_provenance_and_detects_foreign_binaries(tmp_path, monk
     (tmp_path / "m.json").write_text(json.dumps(other))
     with pytest.raises(RuntimeError, match="other kernel sources"):
         build.verify_loaded(str(build.so_path()))
+
+
+def test_digests_do_not_depend_on_where_the_tree_lives(tmp_path, monkeypatch):
+    """The GPU box unpacks the tree under another path (and the driver runs smoke() there without
+    building): the same sources and flags must give the same object and extension digests, or the
+    provenance check would reject a current .so."""
+    import shutil
+
+    here = build._plan()
+    moved = tmp_path / "elsewhere" / "repo"
+    shutil.copytree(build.CSRC, moved / "dstack_amd" / "ops" / "csrc")
+    monkeypatch.setattr(build, "ROOT", moved)
+    monkeypatch.setattr(build, "HERE", moved / "dstack_amd" / "ops")
+    monkeypatch.setattr(build, "CSRC", moved / "dstack_amd" / "ops" / "csrc")
+    monkeypatch.setattr(build, "BUILD", moved / "build" / "ops")
+    there = build._plan()
+    assert str(moved) in " ".join(there[1])  # the commands do name the new location...
+    assert [u[2] for u in there[0]] == [u[2] for u in here[0]] and there[2] == here[2]  # ...the digests do not
