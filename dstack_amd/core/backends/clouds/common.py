@@ -224,6 +224,16 @@ def rsa_sha256_sign(private_key_pem: str, data: bytes, pss: bool = False) -> byt
         os.unlink(key_path)
 
 
+def ssh_key_fingerprint(public_key: str) -> str:
+    """OpenSSH ``SHA256:`` fingerprint of a public key line (``type base64 [comment]``): clouds that
+    store account-level keys under free-form names are matched on the key itself, never the name."""
+    import hashlib
+
+    parts = public_key.strip().split()
+    blob = base64.b64decode(parts[1] if len(parts) > 1 else parts[0])
+    return "SHA256:" + base64.b64encode(hashlib.sha256(blob).digest()).decode().rstrip("=")
+
+
 def b64url(b: bytes) -> str:
     return base64.urlsafe_b64encode(b).rstrip(b"=").decode()
 

@@ -13,8 +13,14 @@ import uuid
 from typing import Dict, List, Optional, Tuple
 
 from dstack_amd.core.backends.catalog import CatalogRow, gpu_row
-from dstack_amd.core.backends.clouds.common import OAuthToken, VMCompute, check_response, cloud_init
-from dstack_amd.core.errors import BackendAuthError, ComputeError
+from dstack_amd.core.backends.clouds.common import (
+    OAuthToken,
+    VMCompute,
+    check_response,
+    cloud_init,
+    ssh_key_fingerprint,
+)
+from dstack_amd.core.errors import BackendAuthError, ComputeError, NoCapacityError
 from dstack_amd.core.models.backends import BackendType
 from dstack_amd.core.models.gpus import gpu_info, normalize_gpu_name
 from dstack_amd.core.models.instances import (
@@ -61,22 +67,38 @@ class LambdaCompute(VMCompute):
     def check_credentials(self) -> None:
         check_response(self.http.get(f"{self.API}/instance-types", headers=self._h()), "lambda instance-types")
 
-    def _ensure_key(self, cfg: InstanceConfiguration) -> str:
-        name = f"dstack-{cfg.project_name}"
+    def _ensure_keys(self, cfg: InstanceConfiguration) -> List[str]:
+        """Account SSH keys for the instance's public keys: an account key with the same fingerprint
+        is reused whatever its name, otherwise the key is added as ``dstack-<fingerprint tail>`` (a
+        name per key, so two projects never fight over one name; lambdalabs/compute.py
+        ``_add_project_ssh_key`` names keys by a hash of the key as well)."""
         r = check_response(self.http.get(f"{self.API}/ssh-keys", headers=self._h()), "lambda ssh-keys")
-        if not any(k["name"] == name for k in r.json().get("data", [])):
-            check_response(self.http.post(f"{self.API}/ssh-keys", headers=self._h(),
-                                          json={"name": name, "public_key": cfg.get_public_keys()[0]}),
-                           "lambda add ssh-key")
-        return name
+        have = {}
+        for k in r.json().get("data", []):
+            try:
+                have[ssh_key_fingerprint(k.get("public_key", ""))] = k["name"]
+            except (ValueError, IndexError):
+                continue
+        names = []
+        for pk in cfg.get_public_keys():
+            fp = ssh_key_fingerprint(pk)
+            if fp not in have:
+                name = "dstack-" + re.sub(r"[^A-Za-z0-9]", "", fp.split(":", 1)[1])[-16:]
+                check_response(self.http.post(f"{self.API}/ssh-keys", headers=self._h(),
+                                              json={"name": name, "public_key": pk.strip()}), "lambda add ssh-key")
+                have[fp] = name
+            names.append(have[fp])
+        return list(dict.fromkeys(names))
 
     def _launch(self, offer: InstanceOfferWithAvailability, cfg: InstanceConfiguration
                 ) -> Tuple[str, Optional[str], Optional[dict]]:
         body = {"region_name": offer.region, "instance_type_name": offer.instance.name,
-                "ssh_key_names": [self._ensure_key(cfg)], "name": cfg.instance_name, "quantity": 1,
+                "ssh_key_names": self._ensure_keys(cfg), "name": cfg.instance_name, "quantity": 1,
                 "user_data": cloud_init(cfg)}
-        r = check_response(self.http.post(f"{self.API}/instance-operations/launch", headers=self._h(), json=body),
-                           "lambda launch")
+        r = self.http.post(f"{self.API}/instance-operations/launch", headers=self._h(), json=body)
+        if r.status_code == 400 and "insufficient-capacity" in r.text:
+            raise NoCapacityError(f"lambda: no {offer.instance.name} capacity in {offer.region}")
+        check_response(r, "lambda launch")
         return r.json()["data"]["instance_ids"][0], None, None
 
     def _describe(self, instance_id, region, backend_data) -> dict:
@@ -411,22 +433,50 @@ class DataCrunchCompute(VMCompute):
                                         availability=_AVAILABLE if ok else _NOT_AVAILABLE))
         return rows
 
-    def _launch(self, offer, cfg):
-        r = check_response(self.http.post(f"{self.API}/scripts", headers=self._h(), json={
-            "name": f"{cfg.instance_name}-init", "script": "#!/bin/bash\ncloud-init single --name runcmd || true\n"
-                                                             + _runcmd_script(cloud_init(cfg))}), "datacrunch script")
-        script_id = r.json() if isinstance(r.json(), str) else r.json().get("id")
-        keys = []
+    def _get_or_create_script(self, name: str, script: str) -> str:
+        """A startup script with exactly this content is reused (they are account-level objects;
+        one per launch would pile up), as the reference's ``get_or_create_startup_scrpit``."""
+        r = check_response(self.http.get(f"{self.API}/scripts", headers=self._h()), "datacrunch scripts")
+        for sc in r.json() or []:
+            if sc.get("script") == script:
+                return sc["id"]
+        r = check_response(self.http.post(f"{self.API}/scripts", headers=self._h(), json={"name": name, "script": script}),
+                           "datacrunch script")
+        return r.json() if isinstance(r.json(), str) else r.json().get("id")
+
+    def _get_or_create_keys(self, cfg) -> List[str]:
+        """Account SSH keys matched by fingerprint (datacrunch/api_client.py ``get_or_create_ssh_key``)."""
+        r = check_response(self.http.get(f"{self.API}/sshkeys", headers=self._h()), "datacrunch ssh keys")
+        have = {}
+        for k in r.json() or []:
+            try:
+                have[ssh_key_fingerprint(k.get("key", ""))] = k["id"]
+            except (ValueError, IndexError):
+                continue
+        ids = []
         for pk in cfg.get_public_keys():
-            k = check_response(self.http.post(f"{self.API}/sshkeys", headers=self._h(),
-                                              json={"name": f"dstack-{uuid.uuid4().hex[:8]}", "key": pk}),
-                               "datacrunch ssh key")
-            keys.append(k.json() if isinstance(k.json(), str) else k.json().get("id"))
+            fp = ssh_key_fingerprint(pk)
+            if fp not in have:
+                k = check_response(self.http.post(f"{self.API}/sshkeys", headers=self._h(),
+                                                  json={"name": f"dstack-{cfg.instance_name}.key", "key": pk.strip()}),
+                                   "datacrunch ssh key")
+                have[fp] = k.json() if isinstance(k.json(), str) else k.json().get("id")
+            ids.append(have[fp])
+        return list(dict.fromkeys(ids))
+
+    def _launch(self, offer, cfg):
+        script_id = self._get_or_create_script(
+            f"dstack-{cfg.instance_name}.sh",
+            "#!/bin/bash\ncloud-init single --name runcmd || true\n" + _runcmd_script(cloud_init(cfg)))
+        keys = self._get_or_create_keys(cfg)
         body = {"instance_type": offer.instance.name, "image": "ubuntu-22.04", "hostname": cfg.instance_name,
                 "description": cfg.instance_name, "ssh_key_ids": keys, "location_code": offer.region,
                 "startup_script_id": script_id, "is_spot": offer.instance.resources.spot,
                 "os_volume": {"name": "os", "size": offer.instance.resources.disk.size_mib // 1024}}
-        r = check_response(self.http.post(f"{self.API}/instances", headers=self._h(), json=body), "datacrunch deploy")
+        r = self.http.post(f"{self.API}/instances", headers=self._h(), json=body)
+        if r.status_code == 400 and "not available" in r.text.lower():
+            raise NoCapacityError(f"datacrunch: {offer.instance.name} not available in {offer.region}")
+        check_response(r, "datacrunch deploy")
         iid = r.text.strip().strip('"')
         return iid, None, None
 

@@ -233,19 +233,25 @@ def test_runpod_no_capacity():
 
 
 # ---- Lambda / DataCrunch / Cudo ----------------------------------------------------------------
-def test_lambda_launch_registers_key():
-    keys = []
+def test_lambda_launch_registers_key_once_by_fingerprint():
+    """The instance's key is added under a name derived from its fingerprint; a key already in the
+    account (any name) is reused; an insufficient-capacity answer is a NoCapacityError."""
+    from dstack_amd.core.backends.clouds.common import ssh_key_fingerprint
+
+    keys, launches = [{"name": "someone-elses", "public_key": "ssh-rsa BBBB other"}], []
+    state = {"capacity": True}
 
     def handler(req):
         p = req.url.path
         if p.endswith("/ssh-keys") and req.method == "GET":
-            return httpx.Response(200, json={"data": [{"name": k} for k in keys]})
+            return httpx.Response(200, json={"data": keys})
         if p.endswith("/ssh-keys"):
-            keys.append(json.loads(req.content)["name"])
+            keys.append(json.loads(req.content))
             return httpx.Response(200, json={"data": {}})
         if p.endswith("/launch"):
-            body = json.loads(req.content)
-            assert body["ssh_key_names"] == ["dstack-main"]
+            if not state["capacity"]:
+                return httpx.Response(400, json={"error": {"code": "instance-operations/launch/insufficient-capacity"}})
+            launches.append(json.loads(req.content))
             return httpx.Response(200, json={"data": {"instance_ids": ["L1"]}})
         if p.endswith("/instances/L1"):
             return httpx.Response(200, json={"data": {"status": "active", "ip": "9.9.9.9"}})
@@ -256,12 +262,21 @@ def test_lambda_launch_registers_key():
     c = compute_class(BackendType.LAMBDA)({}, {"api_key": "lk"}, _client(handler))
     jpd = c.create_instance(_offer(c, "H100:8"), CFG)
     c.update_provisioning_data(jpd)
-    assert jpd.hostname == "9.9.9.9" and keys == ["dstack-main"]
+    assert jpd.hostname == "9.9.9.9" and len(keys) == 2
+    added = keys[1]
+    assert added["name"].startswith("dstack-") and ssh_key_fingerprint(added["public_key"]) == \
+        ssh_key_fingerprint(CFG.ssh_keys[0].public)
+    c.create_instance(_offer(c, "H100:8"), CFG)  # same key again: reused, not re-added
+    assert len(keys) == 2 and launches[0]["ssh_key_names"] == launches[1]["ssh_key_names"] == [added["name"]]
     c.terminate_instance("L1", jpd.region)
+    state["capacity"] = False
+    with pytest.raises(NoCapacityError):
+        c.create_instance(_offer(c, "H100:8"), CFG)
 
 
-def test_datacrunch_oauth_token_cached():
-    tokens = []
+def test_datacrunch_oauth_token_cached_and_account_objects_reused():
+    tokens, created = [], []
+    scripts, sshkeys = [], [{"id": "key-0", "name": "mine", "key": CFG.ssh_keys[0].public}]
 
     def handler(req):
         if req.url.path.endswith("/oauth2/token"):
@@ -269,10 +284,20 @@ def test_datacrunch_oauth_token_cached():
             return httpx.Response(200, json={"access_token": "T", "expires_in": 3600})
         assert req.headers["authorization"] == "Bearer T"
         if req.url.path.endswith("/scripts"):
-            return httpx.Response(200, text='"script-1"')
+            if req.method == "GET":
+                return httpx.Response(200, json=scripts)
+            body = json.loads(req.content)
+            scripts.append({"id": f"script-{len(scripts) + 1}", **body})
+            created.append("script")
+            return httpx.Response(200, text=f'"script-{len(scripts)}"')
         if req.url.path.endswith("/sshkeys"):
-            return httpx.Response(200, text='"key-1"')
+            if req.method == "GET":
+                return httpx.Response(200, json=sshkeys)
+            created.append("key")
+            return httpx.Response(200, text='"key-new"')
         if req.url.path.endswith("/instances") and req.method == "POST":
+            body = json.loads(req.content)
+            assert body["ssh_key_ids"] == ["key-0"] and body["startup_script_id"] == "script-1"
             return httpx.Response(200, text='"inst-1"')
         return httpx.Response(200, json={"status": "running", "ip": "1.2.3.4"})
 
@@ -280,7 +305,8 @@ def test_datacrunch_oauth_token_cached():
     jpd = c.create_instance(_offer(c, "H100:8"), CFG)
     c.update_provisioning_data(jpd)
     assert jpd.instance_id == "inst-1" and jpd.hostname == "1.2.3.4"
-    assert len(tokens) == 1
+    c.create_instance(_offer(c, "H100:8"), CFG)  # the same script content and key: both reused
+    assert created == ["script"] and len(tokens) == 1
 
 
 # ---- GCP / OCI signing with a real RSA key ---------------------------------------------------
