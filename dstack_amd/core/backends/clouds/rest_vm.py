@@ -340,17 +340,43 @@ class CudoCompute(VMCompute):
         check_response(self.http.get(f"{self.API}/projects/{self.config.get('project_id', 'default')}",
                                      headers=self._h()), "cudo project")
 
+    def _image(self, res) -> str:
+        """Boot image: ``images`` in the backend config by kind (``amd`` / ``nvidia`` / ``cpu``),
+        else Cudo's NVIDIA driver + Docker image for NVIDIA GPUs and plain Ubuntu 22.04 otherwise
+        (the AMD host setup installs the amdgpu/ROCm user space itself)."""
+        vendor = getattr(res.gpus[0].vendor, "value", res.gpus[0].vendor) if res.gpus else None
+        kind = "cpu" if not res.gpus else ("amd" if vendor == "amd" else "nvidia")
+        over = (self.config.get("images") or {}).get(kind)
+        if over:
+            return over
+        return "ubuntu-2204-nvidia-535-docker-v20240214" if kind == "nvidia" else "ubuntu-2204"
+
+    # Cudo error codes on VM create (cudo/compute.py create_instance)
+    NO_HOSTS, DISK_EXISTS, NETWORK_FULL = 3, 6, 9
+
     def _launch(self, offer, cfg):
+        """``startScript`` is a plain shell script on Cudo (not cloud-config), so the bootstrap's
+        runcmd lines are sent as one; the VM id carries the data centre so that the same instance
+        name can be retried elsewhere; "no hosts available" is a capacity error, the rest fail."""
         project = self.config.get("project_id", "default")
         res = offer.instance.resources
-        vm_id = cfg.instance_name[:60]
+        vm_id = f"{cfg.instance_name}-{offer.region}"[:60]
+        script = "#!/bin/bash\n" + _runcmd_script(cloud_init(cfg))
         body = {"dataCenterId": offer.region, "machineType": offer.instance.name, "vmId": vm_id,
                 "vcpus": res.cpus, "memoryGib": res.memory_mib // 1024, "gpus": len(res.gpus),
-                "bootDiskImageId": "ubuntu-2204-nvidia-535-docker-v20240214" if res.gpus else "ubuntu-2204",
-                "bootDisk": {"sizeGib": res.disk.size_mib // 1024}, "customSshKeys": cfg.get_public_keys(),
-                "startScript": cloud_init(cfg)}
-        check_response(self.http.post(f"{self.API}/projects/{project}/vm", headers=self._h(), json=body),
-                       "cudo create")
+                "bootDiskImageId": self._image(res),
+                "bootDisk": {"storageClass": "STORAGE_CLASS_NETWORK", "sizeGib": res.disk.size_mib // 1024,
+                             "id": f"{vm_id}-disk"},
+                "customSshKeys": cfg.get_public_keys(), "startScript": script}
+        r = self.http.post(f"{self.API}/projects/{project}/vm", headers=self._h(), json=body)
+        if r.status_code >= 400:
+            try:
+                d = r.json()
+            except ValueError:
+                d = {}
+            if d.get("code") == self.NO_HOSTS:
+                raise NoCapacityError(f"cudo: {d.get('message') or 'no hosts available'}")
+            raise ComputeError(f"cudo create: HTTP {r.status_code} {d.get('message') or r.text[:200]}")
         return vm_id, None, {"project": project}
 
     def _describe(self, instance_id, region, backend_data):

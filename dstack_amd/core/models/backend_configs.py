@@ -197,6 +197,7 @@ class CudoConfig(_Input):
     type: Literal["cudo"] = "cudo"
     project_id: str
     regions: Optional[List[str]] = None
+    images: Optional[Dict[str, str]] = None  # boot image id by kind: amd / nvidia / cpu
     creds: APIKeyCreds
 
 

@@ -882,3 +882,37 @@ def test_aws_gateway_public_and_private(public):
 
 def _ec2x(body):
     return httpx.Response(200, text=f'<R xmlns="http://ec2.amazonaws.com/doc/2016-11-15/">{body}</R>')
+
+
+def test_cudo_start_script_is_shell_and_capacity_errors_map():
+    bodies, state = [], {"code": None}
+
+    def handler(req):
+        if req.method == "POST" and req.url.path.endswith("/vm"):
+            if state["code"] is not None:
+                return httpx.Response(400, json={"code": state["code"], "message": "m"})
+            bodies.append(json.loads(req.content))
+            return httpx.Response(200, json={"id": "x"})
+        if "/vms/" in req.url.path and req.method == "GET":
+            return httpx.Response(200, json={"VM": {"state": "ACTIVE", "externalIpAddress": "5.5.5.5",
+                                                   "internalIpAddress": "10.0.0.5"}})
+        return httpx.Response(200, json={})
+
+    c = compute_class(BackendType.CUDO)({"project_id": "p"}, {"api_key": "k"}, _client(handler))
+    offer = _offer(c, "MI300X:4")
+    jpd = c.create_instance(offer, CFG)
+    b = bodies[0]
+    assert b["startScript"].startswith("#!/bin/bash\n") and "#cloud-config" not in b["startScript"]
+    assert "dstack-shim" in b["startScript"] and b["vmId"] == f"run-0-0-{offer.region}"[:60]
+    assert b["customSshKeys"] == [CFG.ssh_keys[0].public]
+    assert b["bootDiskImageId"] == "ubuntu-2204"  # AMD GPUs: not the NVIDIA driver image
+    c.update_provisioning_data(jpd)
+    assert (jpd.hostname, jpd.internal_ip) == ("5.5.5.5", "10.0.0.5")
+    state["code"] = 3
+    with pytest.raises(NoCapacityError):
+        c.create_instance(offer, CFG)
+    state["code"] = 9
+    from dstack_amd.core.errors import ComputeError
+
+    with pytest.raises(ComputeError, match="cudo create"):
+        c.create_instance(offer, CFG)
