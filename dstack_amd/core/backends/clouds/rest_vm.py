@@ -302,7 +302,8 @@ class TensorDockCompute(VMCompute):
                 "gpu_model": model, "vcpus": res.cpus,
                 "ram": res.memory_mib // 1024, "storage": res.disk.size_mib // 1024,
                 "external_ports": "{22}", "internal_ports": "{22}", "operating_system": "Ubuntu 22.04 LTS",
-                "cloudinit_script": cloud_init(cfg), "password": uuid.uuid4().hex}
+                # the form field takes the cloud-config with its newlines escaped (tensordock/api_client.py)
+                "cloudinit_script": cloud_init(cfg).replace("\n", "\\n"), "password": uuid.uuid4().hex}
         r = check_response(self.http.post(f"{self.API}/client/deploy/single", data=data), "tensordock deploy")
         d = r.json()
         if not d.get("success"):

@@ -315,6 +315,8 @@ def test_tensordock_live_listing_and_launch(live):
     jpd = c.create_instance(two, cfg)
     assert launched["hostnode"] == "node-1" and launched["gpu_model"] == "mi300x-oam-192gb"
     assert launched["gpu_count"] == "2" and jpd.ssh_port == 20022
+    script = launched["cloudinit_script"]  # one line, newlines escaped, as the form field expects
+    assert "\n" not in script and script.startswith("#cloud-config\\n") and "dstack-shim" in script
 
 
 def test_runpod_live_listing_feeds_run_job(live):
