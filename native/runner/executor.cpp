@@ -18,6 +18,8 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <stdexcept>
+
 #include <algorithm>
 #include <cstring>
 #include <map>
@@ -100,39 +102,80 @@ std::string resolve_in_path(const std::string& prog, const std::string& path_var
 
 // env interpolation: ${VAR} -> value, $$ -> $
 // ------------------------------------------------------------------------------------------------
+static bool var_start(char c) { return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_'; }
+static bool var_char(char c) { return var_start(c) || (c >= '0' && c <= '9'); }
+
+// ${NAME} expansion of job env values against the environment built so far (env.go
+// interpolateVariables).  Only a well-formed reference is touched: a run of n dollars in front of
+// {NAME} is halved, and an odd run leaves the last dollar to expand the variable ($${A} -> ${A},
+// $$${A} -> $ + value).  Everything else -- bare $NAME, $$ not followed by a reference, ${}, ${!x},
+// ${0x}, an unterminated ${ -- is kept byte for byte, so secrets and passwords containing dollars
+// pass through unchanged.  An unset variable expands to "", as in a shell.  `err` is never set
+// (kept for the callers' signature).
 std::string interpolate_env(const std::string& s, const std::vector<std::pair<std::string, std::string>>& env,
                             std::string* err) {
+  (void)err;
   std::string out;
-  for (size_t i = 0; i < s.size(); ++i) {
+  size_t i = 0;
+  while (i < s.size()) {
     if (s[i] != '$') {
-      out.push_back(s[i]);
+      out.push_back(s[i++]);
       continue;
     }
-    if (i + 1 < s.size() && s[i + 1] == '$') {
-      out.push_back('$');
-      ++i;
+    size_t j = i;
+    while (j < s.size() && s[j] == '$') ++j;
+    const size_t n = j - i;
+    size_t name_end = j + 1;
+    bool ref = j < s.size() && s[j] == '{' && name_end < s.size() && var_start(s[name_end]);
+    if (ref) {
+      while (name_end < s.size() && var_char(s[name_end])) ++name_end;
+      ref = name_end < s.size() && s[name_end] == '}';
+    }
+    if (!ref) {
+      out.append(n, '$');
+      i = j;
       continue;
     }
-    if (i + 1 < s.size() && s[i + 1] == '{') {
-      size_t e = s.find('}', i + 2);
-      if (e == std::string::npos) {
-        if (err) *err = "unterminated ${ in: " + s;
-        return s;
-      }
-      std::string name = s.substr(i + 2, e - i - 2);
-      std::string val;
+    out.append(n / 2, '$');
+    const std::string name = s.substr(j + 1, name_end - j - 1);
+    if (n % 2 == 0) {
+      out += "{" + name + "}";
+    } else {
       for (auto it = env.rbegin(); it != env.rend(); ++it)
         if (it->first == name) {
-          val = it->second;
+          out += it->second;
           break;
         }
-      out += val;
-      i = e;
-      continue;
     }
-    out.push_back('$');
+    i = name_end + 1;
   }
   return out;
+}
+
+// base/rel for the job's working directory (exec.go joinRelPath): "." is the base itself, a
+// relative path may not climb out of it ("..", "a/../.."); an absolute path is taken as is (an
+// image directory such as /workspace -- a superset of the reference, which refuses it).
+bool join_rel_path(const std::string& base, const std::string& rel, std::string& out, std::string& err) {
+  if (!rel.empty() && rel[0] == '/') {
+    out = rel;
+    return true;
+  }
+  std::vector<std::string> parts;
+  for (auto& p : split(rel, '/')) {
+    if (p.empty() || p == ".") continue;
+    if (p == "..") {
+      if (parts.empty()) {
+        err = "working_dir " + rel + " is outside " + base;
+        return false;
+      }
+      parts.pop_back();
+      continue;
+    }
+    parts.push_back(p);
+  }
+  out = base;
+  for (auto& p : parts) out += "/" + p;
+  return true;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -465,6 +508,15 @@ bool Executor::setup_repo(std::string& err) {
       err = "git checkout failed: " + out;
       return false;
     }
+    // the committer identity of the user's local clone (repo_config_name/email), so that commits
+    // made inside the job are attributed as on the laptop (repo.go prepareGit -> SetConfig)
+    for (const char* k : {"name", "email"}) {
+      std::string v = repo[std::string("repo_config_") + k].str();
+      if (!v.empty() && run_cmd({"git", "config", std::string("user.") + k, v}, opts_.working_dir, &out) != 0) {
+        err = std::string("git config user.") + k + " failed: " + out;
+        return false;
+      }
+    }
     if (!blob.empty()) {
       if (run_cmd({"git", "apply", "--whitespace=nowarn", code_path_}, opts_.working_dir, &out) != 0) {
         err = "git apply failed: " + out;
@@ -550,6 +602,54 @@ bool Executor::run_rccl_preflight(std::string& msg) {
   return true;
 }
 
+// The repo's credentials made available to the job itself (executor.go setupCredentials): an SSH
+// clone key as ~/.ssh/id_rsa, an HTTPS token as the GitHub CLI's ~/.config/gh/hosts.yml, so that
+// `git push` / `gh` inside the job work as on the user's machine.  An existing file is never
+// overwritten (the job fails instead); the written file is removed when the job ends.  Returns the
+// path to remove ("" when nothing was written), or sets `err`.
+std::string Executor::setup_credentials(int uid, int gid, std::string& err) {
+  const Json& rs = submit_body_["run_spec"];
+  const Json& repo = rs["repo_data"].is_object() ? rs["repo_data"] : submit_body_["repo_data"];
+  const Json& creds = submit_body_["repo_credentials"];
+  if (repo["repo_type"].str() != "remote" || !creds.is_object()) return "";
+  std::string url = creds["clone_url"].str();
+  bool ssh = url.rfind("ssh://", 0) == 0 || (url.find("://") == std::string::npos && url.find('@') != std::string::npos);
+  std::string path, content;
+  if (ssh) {
+    content = creds["private_key"].str();
+    if (content.empty()) {
+      err = "private key is missing";
+      return "";
+    }
+    path = opts_.home_dir + "/.ssh/id_rsa";
+  } else {
+    std::string token = creds["oauth_token"].str();
+    if (token.empty()) return "";
+    std::string host = url.substr(url.find("://") == std::string::npos ? 0 : url.find("://") + 3);
+    host = host.substr(0, host.find_first_of("/:"));
+    if (host.find('@') != std::string::npos) host = host.substr(host.find('@') + 1);
+    path = opts_.home_dir + "/.config/gh/hosts.yml";
+    content = host + ":\n  oauth_token: \"" + token + "\"\n";
+  }
+  if (path_exists(path)) {
+    err = path + " already exists";
+    return "";
+  }
+  std::string dir = path.substr(0, path.rfind('/'));
+  mkdirs(dir, 0700);
+  if (!write_file(path, content, 0600)) {
+    err = "cannot write " + path;
+    return "";
+  }
+  if (getuid() == 0 && uid >= 0) {  // readable by the job's user, not only by the runner
+    if (chown(dir.c_str(), (uid_t)uid, (gid_t)(gid >= 0 ? gid : -1)) != 0 ||
+        chown(path.c_str(), (uid_t)uid, (gid_t)(gid >= 0 ? gid : -1)) != 0)
+      rlog("cannot chown %s to uid %d", path.c_str(), uid);
+  }
+  rlog("wrote repo credentials to %s", path.c_str());
+  return path;
+}
+
 int Executor::exec_job(std::string& reason, std::string& msg) {
   const Json& js = submit_body_["job_spec"];
   std::vector<std::string> argv;
@@ -590,9 +690,12 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
       rocprof_dir.clear();
     }
   }
-  std::string wd = opts_.working_dir;
-  std::string jwd = js["working_dir"].str();
-  if (!jwd.empty()) wd = jwd[0] == '/' ? jwd : wd + "/" + jwd;
+  std::string wd = opts_.working_dir, wd_err;
+  if (!join_rel_path(opts_.working_dir, js["working_dir"].str(), wd, wd_err)) {
+    reason = "executor_error";
+    msg = wd_err;
+    return -1;
+  }
   mkdirs(wd);
   std::vector<std::string> envs;
   for (auto& kv : env) envs.push_back(kv.first + "=" + kv.second);
@@ -617,6 +720,19 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
       }
     }
   }
+  std::string cred_err;
+  const std::string cred_path = setup_credentials(uid, gid, cred_err);
+  if (!cred_err.empty()) {
+    reason = "executor_error";
+    msg = cred_err;
+    return -1;
+  }
+  struct CredCleanup {  // the written key/token goes when the job does, whatever path it takes
+    std::string p;
+    ~CredCleanup() {
+      if (!p.empty()) unlink(p.c_str());
+    }
+  } cred_cleanup{cred_path};
   // materialise argv/envp (and the resolved executable) before fork(): the runner is
   // multi-threaded (HTTP server), so the child may only make async-signal-safe calls until exec
   std::vector<char*> a, e;
@@ -765,7 +881,7 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
   return code;
 }
 
-void Executor::run_thread() {
+void Executor::run_job_steps() {
   std::string err;
   rlog("setting up repo");
   if (!setup_repo(err)) {
@@ -787,6 +903,22 @@ void Executor::run_thread() {
     else
       add_state("done", "done_by_runner", "", code);
     rlog("job finished: exit_status=%d %s", code, reason.c_str());
+  }
+}
+
+void Executor::run_thread() {
+  // Anything thrown while preparing or running the job fails the job with the error instead of
+  // taking the runner down (the job's logs must still be served): executor.go's recover().
+  try {
+    if (const char* f = getenv("DSTACK_RUNNER_FAULT_INJECT"); f && *f && *f != '0')
+      throw std::runtime_error(std::string("injected fault: ") + f);
+    run_job_steps();
+  } catch (const std::exception& e) {
+    rlog("recovered: %s", e.what());
+    add_state("failed", "executor_error", std::string("recovered: ") + e.what());
+  } catch (...) {
+    rlog("recovered: unknown exception");
+    add_state("failed", "executor_error", "recovered: unknown exception");
   }
   state_ = ExecState::WaitLogsFinished;
   {

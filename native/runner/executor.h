@@ -84,6 +84,8 @@ class Executor {
 
  private:
   void run_thread();
+  void run_job_steps();
+  std::string setup_credentials(int uid, int gid, std::string& err);
   void add_state(const std::string& state, const std::string& reason = "", const std::string& msg = "",
                  int exit_status = -1);
   void rlog(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -109,6 +111,8 @@ class Executor {
   std::mutex fin_mu_;
   std::condition_variable fin_cv_;
 };
+
+bool join_rel_path(const std::string& base, const std::string& rel, std::string& out, std::string& err);
 
 // ${VAR} interpolation with $$ escape (env.go:60-134)
 std::string interpolate_env(const std::string& s, const std::vector<std::pair<std::string, std::string>>& env,

@@ -236,7 +236,7 @@ class DockerDriver : public TaskDriver {
       cfg.set("ExposedPorts", exposed);
     }
     cfg.set("HostConfig", hc);
-    std::string cname = t.config.name.empty() ? t.config.id : t.config.name;
+    std::string cname = unique_container_name(t.config.name.empty() ? t.config.id : t.config.name);
     auto cr = call("POST", "/containers/create?name=" + url_escape(cname), cfg.dump());
     if (!cr.ok()) {
       reason = "creating_container_error";

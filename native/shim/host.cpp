@@ -7,10 +7,12 @@
 #include <pwd.h>
 #include <sys/statvfs.h>
 #include <sys/sysinfo.h>
+#include <openssl/sha.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <fstream>
+#include <set>
 #include <sstream>
 
 #include "../common/amdgpu.h"
@@ -83,36 +85,103 @@ static std::string home_of(const std::string& user) {
   return home ? home : "/root";
 }
 
-static std::string key_body(const std::string& k) {
-  auto parts = split(trim(k), ' ');
-  return parts.size() >= 2 ? parts[0] + " " + parts[1] : trim(k);
+// Tokens of an authorized_keys line: whitespace-separated, double-quoted option values may hold
+// spaces (command="echo hi",no-pty ssh-ed25519 AAAA... comment)
+static std::vector<std::string> key_tokens(const std::string& line) {
+  std::vector<std::string> out;
+  std::string cur;
+  bool quoted = false;
+  for (char c : line) {
+    if (c == '"') quoted = !quoted;
+    if (!quoted && (c == ' ' || c == '\t')) {
+      if (!cur.empty()) out.push_back(cur);
+      cur.clear();
+    } else {
+      cur += c;
+    }
+  }
+  if (!cur.empty()) out.push_back(cur);
+  return out;
 }
 
+static bool is_key_type(const std::string& t) {
+  return t.rfind("ssh-", 0) == 0 || t.rfind("ecdsa-sha2-", 0) == 0 || t.rfind("sk-ssh-", 0) == 0 ||
+         t.rfind("sk-ecdsa-sha2-", 0) == 0;
+}
+
+// The key blob of a public key or an authorized_keys line ("[options] type base64 [comment]"):
+// the bytes its SHA256 fingerprint is taken over, so two lines name the same key exactly when
+// their blobs are equal, whatever their options or comments.  False for a line that holds no
+// well-formed key (the blob must decode and start with its own type string).
+bool public_key_blob(const std::string& line, std::string& blob) {
+  auto t = key_tokens(trim(line));
+  for (size_t i = 0; i + 1 < t.size(); ++i) {
+    if (!is_key_type(t[i])) continue;
+    const std::string& b64 = t[i + 1];
+    if (b64.find_first_not_of("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/=") != std::string::npos)
+      return false;
+    std::string raw = base64_decode(b64);
+    if (raw.size() < 4 + t[i].size()) return false;
+    uint32_t n = ((uint32_t)(uint8_t)raw[0] << 24) | ((uint32_t)(uint8_t)raw[1] << 16) |
+                 ((uint32_t)(uint8_t)raw[2] << 8) | (uint32_t)(uint8_t)raw[3];
+    if (n != t[i].size() || raw.compare(4, n, t[i]) != 0) return false;
+    blob = raw;
+    return true;
+  }
+  return false;
+}
+
+// OpenSSH-style "SHA256:<unpadded base64>" fingerprint, "" for a malformed key
+std::string public_key_fingerprint(const std::string& key) {
+  std::string blob;
+  if (!public_key_blob(key, blob)) return "";
+  unsigned char md[32];
+  SHA256(reinterpret_cast<const unsigned char*>(blob.data()), blob.size(), md);
+  std::string b64 = base64_encode(std::string(reinterpret_cast<char*>(md), sizeof md));
+  while (!b64.empty() && b64.back() == '=') b64.pop_back();
+  return "SHA256:" + b64;
+}
+
+// Add the well-formed keys of `keys` that the file does not hold yet (by key identity: a key
+// already present with other options or another comment is not added twice); other lines are kept
+// byte for byte, a backup of the previous file is left next to it.  Malformed keys are skipped.
 bool add_authorized_keys(const std::string& user, const std::vector<std::string>& keys) {
   std::string dir = home_of(user) + "/.ssh";
   mkdirs(dir, 0700);
   std::string path = dir + "/authorized_keys", content;
   read_file(path, content);
   if (!content.empty()) write_file(path + ".dstack.bak", content, 0600);
+  std::set<std::string> have;
+  for (auto& line : split(content, '\n')) {
+    std::string b;
+    if (public_key_blob(line, b)) have.insert(b);
+  }
   for (auto& k : keys) {
-    if (trim(k).empty()) continue;
-    if (content.find(key_body(k)) != std::string::npos) continue;
+    std::string b;
+    if (!public_key_blob(k, b) || have.count(b)) continue;
+    have.insert(b);
     if (!content.empty() && content.back() != '\n') content += "\n";
     content += trim(k) + "\n";
   }
   return write_file(path, content, 0600);
 }
 
+// Remove every line that holds one of `keys` (with any options / comment); other lines, comments
+// and malformed lines stay.  A missing file is fine.
 bool remove_authorized_keys(const std::string& user, const std::vector<std::string>& keys) {
   std::string path = home_of(user) + "/.ssh/authorized_keys", content;
   if (!read_file(path, content)) return true;
+  std::set<std::string> drop;
+  for (auto& k : keys) {
+    std::string b;
+    if (public_key_blob(k, b)) drop.insert(b);
+  }
   std::string out;
   for (auto& line : split(content, '\n')) {
     if (line.empty()) continue;
-    bool drop = false;
-    for (auto& k : keys)
-      if (key_body(line) == key_body(k)) drop = true;
-    if (!drop) out += line + "\n";
+    std::string b;
+    if (public_key_blob(line, b) && drop.count(b)) continue;
+    out += line + "\n";
   }
   return write_file(path, out, 0600);
 }

@@ -21,6 +21,7 @@ namespace dsa {
 enum class TaskStatus { Pending, Preparing, Pulling, Creating, Running, Terminated };
 const char* task_status_name(TaskStatus s);
 bool task_transition_allowed(TaskStatus from, TaskStatus to);
+std::string unique_container_name(const std::string& base);
 
 struct PortMapping {
   int container = 0;
@@ -104,6 +105,8 @@ class GpuLock {
 
 // ---- host info (host.go, host_info.go) ------------------------------------------------------
 Json collect_host_info(const std::string& disk_path);
+bool public_key_blob(const std::string& line, std::string& blob);
+std::string public_key_fingerprint(const std::string& key);
 bool add_authorized_keys(const std::string& user, const std::vector<std::string>& keys);
 bool remove_authorized_keys(const std::string& user, const std::vector<std::string>& keys);
 

@@ -1,5 +1,6 @@
 // Task model, storage and the xGMI-aware GPU lock (see shim.h).
 #include <algorithm>
+#include <random>
 
 #include "../common/amdgpu.h"
 #include "../common/net.h"
@@ -17,6 +18,20 @@ const char* task_status_name(TaskStatus s) {
     case TaskStatus::Terminated: return "terminated";
   }
   return "unknown";
+}
+
+// Docker container name for a task: the task's name made safe for Docker ([A-Za-z0-9][A-Za-z0-9_.-]*)
+// plus a random suffix, so that a container left behind by an earlier shim (same run name) never
+// makes the create fail with a name conflict (task.go generateUniqueName).  Tasks are found again
+// by their labels, not by name.
+std::string unique_container_name(const std::string& base) {
+  std::string n;
+  for (char c : base) n += (isalnum((unsigned char)c) || c == '_' || c == '.' || c == '-') ? c : '-';
+  if (n.empty() || !isalnum((unsigned char)n[0])) n = "task" + n;
+  static thread_local std::mt19937_64 rng{std::random_device{}()};
+  char suf[9];
+  snprintf(suf, sizeof suf, "%08x", (unsigned)(rng() & 0xffffffffu));
+  return n.substr(0, 200) + "-" + suf;
 }
 
 bool task_transition_allowed(TaskStatus from, TaskStatus to) {
@@ -149,6 +164,7 @@ void GpuLock::init(int n, std::vector<std::vector<int>> xgmi, std::vector<int> n
 
 std::vector<int> GpuLock::acquire(int count) {
   std::lock_guard<std::mutex> lk(mu_);
+  if (count < -1) return {};  // only -1 means "all"; any other negative count is a bad request
   std::vector<int> free_idx;
   for (int k = 0; k < n_; ++k)
     if (!busy_[(size_t)k]) free_idx.push_back(k);

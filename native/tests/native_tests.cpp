@@ -391,8 +391,7 @@ int main() {
     err.clear();
     CHECK(interpolate_env("[${MISSING}]", env, &err) == "[]");  // unset -> empty, as in a shell
     CHECK(err.empty());
-    interpolate_env("${UNTERMINATED", env, &err);
-    CHECK(!err.empty());
+    CHECK(interpolate_env("${UNTERMINATED", env, &err) == "${UNTERMINATED");  // kept as written
   });
 
   run("task status transitions", [] {
@@ -445,6 +444,46 @@ int main() {
     gl.release(a);
     gl.release(b);
     CHECK(gl.acquire(-1).size() == 8);
+  });
+
+  run("gpu lock edges: no GPUs, bad counts, empty and out-of-range lock/release", [&] {
+    GpuLock none;
+    none.init(0, {}, {});
+    CHECK(none.acquire(-1).empty() && none.acquire(1).empty() && none.free_count() == 0);
+    GpuLock gl;
+    gl.init(8, xgmi, numa);
+    CHECK(gl.acquire(-2).empty() && gl.free_count() == 8);  // only -1 means all
+    CHECK(gl.acquire(0).empty() && gl.free_count() == 8);
+    CHECK(gl.acquire(9).empty() && gl.free_count() == 8);   // not enough: nothing granted
+    CHECK(gl.lock({}) && gl.free_count() == 8);            // empty grant: no-op
+    gl.release({});
+    CHECK(!gl.lock({8}) && !gl.lock({-1}) && gl.free_count() == 8);
+    CHECK(!gl.lock({0, 0}) || gl.free_count() == 7);
+  });
+
+  run("task storage: missing ids, every transition, config, unique container names", [] {
+    TaskStorage st;
+    Task out;
+    CHECK(!st.get("nope", out) && !st.set_status("nope", TaskStatus::Preparing) && !st.remove("nope"));
+    const TaskStatus all[] = {TaskStatus::Pending, TaskStatus::Preparing, TaskStatus::Pulling,
+                              TaskStatus::Creating, TaskStatus::Running, TaskStatus::Terminated};
+    int allowed = 0;
+    for (auto a : all)
+      for (auto b : all) allowed += task_transition_allowed(a, b);
+    CHECK(allowed == 4 + 5);  // the 4 forward steps, and Terminated from each of the 5 live states
+    CHECK(!task_transition_allowed(TaskStatus::Terminated, TaskStatus::Terminated));
+    CHECK(!task_transition_allowed(TaskStatus::Running, TaskStatus::Creating));
+    Json j = Json::parse(R"({"id":"t9","name":"run-1-0-0","image_name":"rocm/pytorch","gpu":-1,)"
+                         R"("shm_size":1073741824,"network_mode":"bridge","host_ssh_user":"ubuntu",)"
+                         R"("host_ssh_keys":["k1"],"container_ssh_keys":["k2"]})");
+    TaskConfig c = TaskConfig::from_json(j);
+    CHECK(c.id == "t9" && c.name == "run-1-0-0" && c.image_name == "rocm/pytorch" && c.gpu == -1);
+    CHECK(c.shm_size == (1LL << 30) && c.network_mode == "bridge" && c.host_ssh_user == "ubuntu");
+    CHECK(c.host_ssh_keys == std::vector<std::string>{"k1"} && c.container_ssh_keys == std::vector<std::string>{"k2"});
+    std::string a = unique_container_name("run-1-0-0"), b = unique_container_name("run-1-0-0");
+    CHECK(a != b && a.rfind("run-1-0-0-", 0) == 0 && a.size() == 10 + 8);
+    CHECK(unique_container_name("my run/1").rfind("my-run-1-", 0) == 0);
+    CHECK(unique_container_name("_x").rfind("task_x-", 0) == 0);
   });
 
   run("amd catalog names", [] {
