@@ -128,7 +128,10 @@ class AWSConfig(_Input):
     os_images: Optional[AWSOSImages] = None
     creds: Annotated[Union[AccessKeyCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
 
-    _tags = field_validator("tags")(classmethod(lambda cls, v: _check_tags("aws", v)))
+    @field_validator("tags")
+    @classmethod
+    def _valid_tags(cls, v):
+        return _check_tags("aws", v)
 
 
 class AzureConfig(_Input):
@@ -145,7 +148,10 @@ class AzureConfig(_Input):
     vm_images: Optional[Dict[str, Dict[str, str]]] = None  # AzureImageVariant overrides: rocm/nvidia/standard
     creds: Annotated[Union[ClientCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
 
-    _tags = field_validator("tags")(classmethod(lambda cls, v: _check_tags("azure", v)))
+    @field_validator("tags")
+    @classmethod
+    def _valid_tags(cls, v):
+        return _check_tags("azure", v)
 
 
 class GCPConfig(_Input):
@@ -161,7 +167,10 @@ class GCPConfig(_Input):
     tags: Optional[Dict[str, str]] = None
     creds: Annotated[Union[ServiceAccountCreds, DefaultCreds], Field(discriminator="type")] = DefaultCreds()
 
-    _tags = field_validator("tags")(classmethod(lambda cls, v: _check_tags("gcp", v)))
+    @field_validator("tags")
+    @classmethod
+    def _valid_tags(cls, v):
+        return _check_tags("gcp", v)
 
 
 class OCIConfig(_Input):
