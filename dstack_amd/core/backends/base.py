@@ -188,11 +188,38 @@ def get_shim_commands(authorized_keys: List[str], shim_url: str, runner_url: str
     ]
 
 
+# amdgpu-install release used when a GPU host boots without the kernel driver (the ROCm user space
+# ships in the job's container image; the host only needs amdgpu + /dev/kfd)
+AMDGPU_INSTALL_RELEASE = "6.4"
+AMDGPU_INSTALL_DEB = "amdgpu-install_6.4.60400-1_all.deb"
+# PCI device ids of the Instinct GPUs this build schedules (MI100 .. MI355X), vendor 1002
+AMD_INSTINCT_PCI = "738c|740c|740f|74a0|74a1|74a5|74b5|75a0|75a3"
+
+
+def get_amd_driver_commands(release: str = AMDGPU_INSTALL_RELEASE, deb: str = AMDGPU_INSTALL_DEB) -> List[str]:
+    """Host setup for clouds whose default image has no AMD GPU driver (plain Ubuntu on AWS, GCP,
+    Azure, OCI...): when the host has an Instinct GPU but no ``/dev/kfd``, install the amdgpu DKMS
+    driver with amdgpu-install and load it, before the shim starts (it discovers GPUs through KFD).
+    A no-op on hosts that already have the driver (vendor GPU images, the packer image in
+    ``scripts/packer``) and on CPU hosts.  The reference ships its own VM images instead."""
+    url = f"https://repo.radeon.com/amdgpu-install/{release}/ubuntu/jammy/{deb}"
+    script = (
+        f"if [ ! -e /dev/kfd ] && lspci -nn 2>/dev/null | grep -qiE '1002:({AMD_INSTINCT_PCI})'; then "
+        f"export DEBIAN_FRONTEND=noninteractive; "
+        f"curl -fsSL -o /tmp/amdgpu-install.deb '{url}' && apt-get install -yqq /tmp/amdgpu-install.deb && "
+        f"amdgpu-install -y --usecase=dkms --no-32 && modprobe amdgpu; "
+        f"fi >> /var/log/dstack-amdgpu.log 2>&1"
+    )
+    return [script]
+
+
 def get_user_data(authorized_keys: List[str], shim_url: str, runner_url: str,
                   backend_commands: Optional[List[str]] = None) -> str:
     """cloud-config: authorized keys, then the cloud's own host setup (``backend_commands``, e.g.
-    opening the VPC subnet in the host firewall), then the shim bootstrap."""
-    cmds = list(backend_commands or []) + get_shim_commands(authorized_keys, shim_url, runner_url)
+    opening the VPC subnet in the host firewall), the AMD driver when the image lacks it, then the
+    shim bootstrap."""
+    cmds = (list(backend_commands or []) + get_amd_driver_commands()
+            + get_shim_commands(authorized_keys, shim_url, runner_url))
     keys = "\n".join(f"  - {json_quote(k)}" for k in authorized_keys)  # a YAML-safe scalar whatever the comment
     runcmd = "\n".join(f"  - {json_quote(c)}" for c in cmds)
     return f"#cloud-config\nssh_authorized_keys:\n{keys}\nruncmd:\n{runcmd}\n"

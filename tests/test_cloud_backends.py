@@ -916,3 +916,29 @@ def test_cudo_start_script_is_shell_and_capacity_errors_map():
 
     with pytest.raises(ComputeError, match="cudo create"):
         c.create_instance(offer, CFG)
+
+
+def test_cloud_init_installs_the_amd_driver_only_when_missing(tmp_path):
+    """The bootstrap installs amdgpu (DKMS) before the shim when the host has an Instinct GPU but no
+    /dev/kfd; on CPU hosts (or with the driver present) the step does nothing and succeeds."""
+    from dstack_amd.core.backends.base import get_amd_driver_commands, get_user_data
+
+    ud = get_user_data(["ssh-ed25519 AAAA k"], "https://x/shim", "https://x/runner")
+    lines = [json.loads(line[4:]) for line in ud.splitlines() if line.startswith("  - ") and "amdgpu" in line]
+    assert len(lines) == 1 and "amdgpu-install -y --usecase=dkms" in lines[0]
+    assert ud.index("amdgpu-install") < ud.index("dstack-shim")  # driver first, then the shim
+    # run the step with stand-in tools: lspci reports no AMD GPU -> nothing installed, exit 0
+    bin_dir = tmp_path / "bin"
+    bin_dir.mkdir()
+    (bin_dir / "lspci").write_text("#!/bin/sh\necho '00:02.0 VGA compatible controller [0300]: Intel [8086:46a6]'\n")
+    (bin_dir / "curl").write_text(f"#!/bin/sh\ntouch {tmp_path}/curl-called\nexit 1\n")
+    for f in bin_dir.iterdir():
+        f.chmod(0o755)
+    script = get_amd_driver_commands()[0].replace("/var/log/dstack-amdgpu.log", str(tmp_path / "log"))
+    env = {"PATH": f"{bin_dir}:/usr/bin:/bin"}
+    assert subprocess.run(["bash", "-c", script], env=env).returncode == 0
+    assert not (tmp_path / "curl-called").exists()
+    # an MI355X (1002:75a3) without /dev/kfd -> the installer path runs (the stand-in curl fails it)
+    (bin_dir / "lspci").write_text("#!/bin/sh\necho '05:00.0 Processing accelerators [1200]: AMD [1002:75a3]'\n")
+    subprocess.run(["bash", "-c", script], env=env)
+    assert (tmp_path / "curl-called").exists() or os.path.exists("/dev/kfd")
