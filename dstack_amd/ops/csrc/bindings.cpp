@@ -46,6 +46,13 @@ hipError_t dsa_quant_fp8_rows(const void*, long, void*, long, float*, int, int, 
 bool dsa_gemv_fp8_supported(int, int);
 hipError_t dsa_gemv_fp8(const void*, long, const void*, const float*, void*, long, int, int, int, hipStream_t);
 hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
+bool dsa_gemm_nt_supported(int, int, int);
+hipError_t dsa_gemm_nt(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
+bool dsa_gemm_nt_swiglu_supported(int, int, int);
+hipError_t dsa_gemm_nt_swiglu(const void*, const void*, void*, void*, void*, int, int, int, long, long, hipStream_t);
+bool dsa_gemm_nt_swiglu_bwd_supported(int, int, int);
+hipError_t dsa_gemm_nt_swiglu_bwd(const void*, const void*, const void*, void*, void*, int, int, int, long, long,
+                                  hipStream_t);
 }
 
 namespace {
@@ -365,6 +372,66 @@ torch::Tensor gemv_fp8(torch::Tensor x, torch::Tensor q, torch::Tensor sc) {
   return y;
 }
 
+void check_rows(const torch::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16 && t.dim() == 2, what, ": 2-D bf16 ROCm tensors");
+  TORCH_CHECK(t.stride(1) == 1 && t.stride(0) % 8 == 0, what, ": rows must be contiguous, row stride % 8 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what, ": 16-byte aligned base");
+}
+
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) { return dsa_gemm_nt_supported(M, N, K); }
+
+// out[M][N] (+)= a[M][K] b[N][K]^T  (csrc/gemm_nt.hip)
+void gemm_nt(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool accumulate) {
+  check_rows(a, "gemm_nt");
+  check_rows(b, "gemm_nt");
+  check_rows(out, "gemm_nt");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_nt: shape mismatch");
+  TORCH_CHECK(dsa_gemm_nt_supported(M, N, K), "gemm_nt: M % 256, N % 256, K % 128 must be 0");
+  check(dsa_gemm_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0),
+                    accumulate ? 1 : 0, stream()),
+        "gemm_nt");
+}
+
+bool gemm_nt_swiglu_supported(int64_t T, int64_t F, int64_t K) { return dsa_gemm_nt_swiglu_supported(T, F, K); }
+
+// gu = x w^T (w = [gate; up] [2F][K]) -> (gu [T][2F], a = silu(g) * u [T][F], a^T [F][T])
+std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor x, torch::Tensor w) {
+  check_rows(x, "gemm_nt_swiglu");
+  check_rows(w, "gemm_nt_swiglu");
+  const int64_t T = x.size(0), K = x.size(1), F = w.size(0) / 2;
+  TORCH_CHECK(w.size(1) == K && w.size(0) == 2 * F, "gemm_nt_swiglu: shape mismatch");
+  TORCH_CHECK(dsa_gemm_nt_swiglu_supported(T, F, K), "gemm_nt_swiglu: T % 256, F % 128, K % 128 must be 0");
+  auto gu = torch::empty({T, 2 * F}, x.options());
+  auto a = torch::empty({T, F}, x.options());
+  auto aT = torch::empty({F, T}, x.options());
+  check(dsa_gemm_nt_swiglu(x.data_ptr(), w.data_ptr(), gu.data_ptr(), a.data_ptr(), aT.data_ptr(), T, F, K,
+                           x.stride(0), w.stride(0), stream()),
+        "gemm_nt_swiglu");
+  return {gu, a, aT};
+}
+
+bool gemm_nt_swiglu_bwd_supported(int64_t T, int64_t F, int64_t K) {
+  return dsa_gemm_nt_swiglu_bwd_supported(T, F, K);
+}
+
+// da = dy wdT^T (wdT = W_down^T [F][K]) fused with the SwiGLU backward -> (dgu [T][2F], dgu^T [2F][T])
+std::vector<torch::Tensor> gemm_nt_swiglu_bwd(torch::Tensor dy, torch::Tensor wdT, torch::Tensor gu) {
+  check_rows(dy, "gemm_nt_swiglu_bwd");
+  check_rows(wdT, "gemm_nt_swiglu_bwd");
+  const int64_t T = dy.size(0), K = dy.size(1), F = wdT.size(0);
+  TORCH_CHECK(wdT.size(1) == K, "gemm_nt_swiglu_bwd: shape mismatch");
+  TORCH_CHECK(gu.is_cuda() && gu.scalar_type() == torch::kBFloat16 && gu.is_contiguous() && gu.numel() == T * 2 * F,
+              "gemm_nt_swiglu_bwd: gu must be a contiguous bf16 [T, 2F]");
+  TORCH_CHECK(dsa_gemm_nt_swiglu_bwd_supported(T, F, K), "gemm_nt_swiglu_bwd: T % 256, F % 256, K % 128 must be 0");
+  auto dgu = torch::empty({T, 2 * F}, dy.options());
+  auto dguT = torch::empty({2 * F, T}, dy.options());
+  check(dsa_gemm_nt_swiglu_bwd(dy.data_ptr(), wdT.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), T, F,
+                               K, dy.stride(0), wdT.stride(0), stream()),
+        "gemm_nt_swiglu_bwd");
+  return {dgu, dguT};
+}
+
 // out[P][Q] (+)= a^T b ; a = [T][P], b = [T][Q] (weight gradient dW = dY^T X)
 void gemm_tn(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool accumulate) {
   for (auto* t : {&a, &b, &out}) {
@@ -501,6 +568,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemv_fp8_supported", &gemv_fp8_supported);
   m.def("gemm_tn", &gemm_tn);
   m.def("gemm_tn_supported", &gemm_tn_supported);
+  m.def("gemm_nt", &gemm_nt);
+  m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_swiglu", &gemm_nt_swiglu);
+  m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);
+  m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd);
+  m.def("gemm_nt_swiglu_bwd_supported", &gemm_nt_swiglu_bwd_supported);
   m.def("gemv", &gemv);
   m.def("gemv_supported", &gemv_supported);
   m.def("paged_page_size", &dsa_paged_page_size);

@@ -1,0 +1,608 @@
+// Projection GEMM for CDNA4 (gfx950): C[M][N] (+)= A[M][K] · B[N][K]^T, bf16 in, fp32 accumulate,
+// bf16 out -- the layout of every GEMM of the Llama training step once the weight-gradient and
+// input-gradient operands are token-/reduction-contiguous (ops/functional.py): y = x W^T,
+// dX = dY (W^T)^T, dW = (dY^T)(X^T)^T.  Epilogues fuse the SwiGLU forward into the gate/up GEMM
+// and the SwiGLU backward into the down projection's input-gradient GEMM.
+//
+// Design (one workgroup = one 256x256 output tile, 8 waves = two groups of 4, one workgroup/CU):
+//  * K advances in 64-deep tiles.  Each tile is four 16 KiB "units" in LDS -- A rows 0-127 (a0),
+//    A rows 128-255 (a1), B rows 0-127 (b0), B rows 128-255 (b1) -- filled by LDS-DMA
+//    (global_load_lds_dwordx4, 2 instructions per thread per unit) into a 2-tile ring (128 KiB).
+//    Rows are 128 B; the 16-byte chunk c of row r sits at slot c ^ ((r >> 1) & 7), applied to the
+//    per-lane DMA source address, so every ds_read_b128 fragment read is bank-conflict free.
+//  * Wave (wr, wc) owns output rows {64wr + [0,64)} and {128 + 64wr + [0,64)} (m-subtiles 0/1,
+//    from a0/a1) and columns {32wc + [0,32)} and {128 + 32wc + [0,32)} (n-subtiles 0/1, from
+//    b0/b1): 128x64 per wave, 32 accumulators of mfma_f32_16x16x32_bf16.
+//  * Eight phases per two K-tiles.  A phase = fragment reads + one unit of LDS-DMA, barrier, 16
+//    MFMAs (one 64x32 quadrant x K 64), barrier.  Quadrant order per tile (m,n) = (0,0) (0,1)
+//    (1,0) (1,1): reads 12 / 4 / 8 / 0 ds_read_b128.  Group 1 (waves 4-7) runs one barrier behind
+//    group 0, so on every SIMD one wave issues MFMAs while its partner reads LDS and issues DMA.
+//  * DMA schedule (unit issued per phase, tile t = this iteration's even tile):
+//      P1 a1(t+1)  P2 b0(t+2)  P3 a0(t+2)  P4 b1(t+2) | P5 a1(t+2)  P6 b0(t+3)  P7 a0(t+3)  P8 b1(t+3)
+//    Every unit is restaged only after its last read was retired before a barrier both groups
+//    passed (b0: lgkmcnt(8) after the B reads that P1/P5 issue first).  vmcnt(6) at P4 / P8 leaves
+//    three units in flight and retires exactly the tile read in the next four phases.
+//  * XCD-aware tile order: workgroup ids are dealt round-robin to the 8 XCDs; the logical tile is
+//    remapped so an XCD works on a contiguous, group-M ordered block of tiles that share A rows
+//    and B rows in its L2.
+//  * Operand roles in the MFMA are swapped (B fragment as the "A" operand), so each lane's
+//    accumulator holds 4 consecutive output columns of one row: 8-byte row-contiguous pieces for
+//    the LDS-staged epilogue.
+//
+// The SwiGLU tile maps its 256 columns to gate columns [f0, f0+128) (b0) and up columns
+// [F+f0, F+f0+128) (b1): a lane holds g and u of the same (t, f) in accumulators n and n+2.
+#include <stdlib.h>
+
+#include "mfma_tiles.h"
+
+using namespace dsa;
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short us4 __attribute__((ext_vector_type(4)));
+
+constexpr int NT_BM = 256, NT_BN = 256, NT_BK = 64;
+constexpr int UNIT = 16384;                // one 128 x 64 bf16 unit
+constexpr int BUF = 4 * UNIT;              // a0 | a1 | b0 | b1
+constexpr int EPI_LD = 520;                // epilogue LDS row stride (bytes): 256 bf16 + 8 B pad
+constexpr int NT_LDS = 2 * BUF + 2 * 16384;  // 160 KiB: ring + room for the SwiGLU epilogue
+
+enum Epi { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU = 2, EPI_SWIGLU_BWD = 3 };
+
+struct NTArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* C;      // output (STORE/ACC); gu (SWIGLU); dgu (SWIGLU_BWD)
+  bf16_t* C2;     // a (SWIGLU)
+  bf16_t* C3;     // a^T (SWIGLU); dgu^T (SWIGLU_BWD)
+  const bf16_t* G;  // gu read by SWIGLU_BWD
+  long lda, ldb, ldc;
+  int M, K;
+  int ntn;        // tiles along N
+  int nstride;    // column origin step per n tile (256 plain, 128 SwiGLU)
+  int bsplit;     // offset of the second 128 columns (128 plain, F SwiGLU)
+  int F;          // SwiGLU width (ld of a, columns of gu / 2)
+  int group;      // tile-order group height (tile rows)
+  int wg_per_xcd; // workgroups per XCD (gridDim / 8 when persistent)
+};
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void nt_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N>
+__device__ __forceinline__ void nt_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void nt_lgkmcnt() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Two LDS-DMA instructions of one unit: this wave's 2 KiB piece (16 rows).  The global address is
+// SGPR base + 32-bit per-lane offset (saddr form), the LDS address M0.  Inline asm: the compiler
+// neither drains it (vmcnt(0)) in front of the next ds_read nor counts it; the loop counts by hand.
+__device__ __forceinline__ void nt_dma(const bf16_t* sbase, unsigned v0, unsigned v1, unsigned lds) {
+  unsigned keep;
+  const unsigned lds1 = lds + 1024;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %3\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %3\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "v"(v1), "s"(sbase), "s"(lds), "s"(lds1)
+      : "memory");
+}
+
+__device__ __forceinline__ int nt_xcd_tile(int b, int n) {
+  const int xcd = b & 7, idx = b >> 3, per = n >> 3, rem = n & 7;
+  return xcd * per + (xcd < rem ? xcd : rem) + idx;
+}
+
+__device__ __forceinline__ bf16x8 ldsr(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+
+template <int MS, int NS>
+__device__ __forceinline__ void nt_quadrant(f32x4 (&acc)[2][4][4], const bf16x8 (&af)[4][2],
+                                            const bf16x8 (&bf)[2][2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        acc[MS][mi][2 * NS + n] = mfma16(bf[NS][n][kk], af[mi][kk], acc[MS][mi][2 * NS + n]);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// A fragments of m-subtile MS (unit a_MS of buffer `buf`): 4 row tiles x 2 k halves
+template <int MS>
+__device__ __forceinline__ void nt_read_a(bf16x8 (&af)[4][2], const char* buf, int ra0, int ra1) {
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    af[mi][0] = ldsr(buf + MS * UNIT + mi * 2048 + ra0);
+    af[mi][1] = ldsr(buf + MS * UNIT + mi * 2048 + ra1);
+  }
+}
+
+template <int NS>
+__device__ __forceinline__ void nt_read_b(bf16x8 (&bf)[2][2][2], const char* buf, int rb0, int rb1) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    bf[NS][n][0] = ldsr(buf + (2 + NS) * UNIT + n * 2048 + rb0);
+    bf[NS][n][1] = ldsr(buf + (2 + NS) * UNIT + n * 2048 + rb1);
+  }
+}
+
+}  // namespace
+
+// Tile origin (first row of A/C, first B row of the tile's first 128 columns) of logical tile t.
+__device__ __forceinline__ void nt_tile_origin(const NTArgs& p, int t, int& m0, int& nb0) {
+  const int ntm = p.M / NT_BM;
+  const int in_group = p.group * p.ntn;
+  const int first_m = (t / in_group) * p.group;
+  const int gm = min(ntm - first_m, p.group);
+  m0 = (first_m + (t % in_group) % gm) * NT_BM;
+  nb0 = ((t % in_group) / gm) * p.nstride;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // the plain epilogues store straight from the accumulators while the next tile's prologue DMA
+  // is in flight; the SwiGLU ones stage through LDS (transposed copies) and reload afterwards
+  constexpr bool OVERLAP = EPI == EPI_STORE || EPI == EPI_ACC;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+
+  // --- this workgroup's tiles: XCD x = blockIdx % 8 owns a contiguous slice of the logical tile
+  // order; its workgroups take every (gridDim/8)-th tile of the slice (persistent when the grid is
+  // smaller than the tile count)
+  const int ntiles = (p.M / NT_BM) * p.ntn;
+  const int xcd = blockIdx.x & 7, xj = blockIdx.x >> 3;
+  const int per = ntiles >> 3, rem = ntiles & 7;
+  const int cnt = per + (xcd < rem ? 1 : 0), start = xcd * per + (xcd < rem ? xcd : rem);
+  const int stride = p.wg_per_xcd;
+  int local = xj;
+  if (local >= cnt) return;
+  int m0, nb0;
+  nt_tile_origin(p, start + local, m0, nb0);
+  const int nk = p.K / NT_BK;
+
+  // --- DMA: per-lane source offsets (bytes) of this wave's two 1 KiB pieces of a unit ----------
+  // piece i covers unit rows 16w + 8i + (lane>>3); lane's 16 B slot (lane&7) holds the chunk
+  // (lane&7) ^ (4i + (lane>>4)), the inverse of the read swizzle c ^ ((r>>1)&7).
+  unsigned va[2], vb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * w + 8 * i + (lane >> 3);
+    const int ch = (lane & 7) ^ (4 * i + (lane >> 4));
+    va[i] = (unsigned)((r * p.lda + ch * 8) * 2);
+    vb[i] = (unsigned)((r * p.ldb + ch * 8) * 2);
+  }
+  const unsigned lds0 = (unsigned)(uintptr_t)LDS3(char, smem) + (unsigned)(w * 2048);
+  const bf16_t *a_src0, *a_src1, *b_src0, *b_src1;
+  auto set_src = [&](int tm0, int tnb0) {
+    a_src0 = p.A + (long)tm0 * p.lda;
+    a_src1 = p.A + (long)(tm0 + 128) * p.lda;
+    b_src0 = p.B + (long)tnb0 * p.ldb;
+    b_src1 = p.B + (long)(tnb0 + p.bsplit) * p.ldb;
+  };
+  // units: 0 = a0, 1 = a1, 2 = b0, 3 = b1 of K-tile kt, into ring slot kt & 1
+  auto dma = [&](int unit, int kt) {
+    const unsigned dst = lds0 + (unsigned)((kt & 1) * BUF + unit * UNIT);
+    const long ko = (long)kt * NT_BK;
+    if (unit == 0) nt_dma(a_src0 + ko, va[0], va[1], dst);
+    else if (unit == 1) nt_dma(a_src1 + ko, va[0], va[1], dst);
+    else if (unit == 2) nt_dma(b_src0 + ko, vb[0], vb[1], dst);
+    else nt_dma(b_src1 + ko, vb[0], vb[1], dst);
+  };
+  // K-tile 0 whole and K-tile 1's b0, b1 (its a0, a1 are the first phase's DMA): 12 instructions
+  auto prologue = [&]() {
+    dma(0, 0);
+    dma(1, 0);
+    dma(2, 0);
+    dma(3, 0);
+    dma(2, 1);
+    dma(3, 1);
+  };
+
+  // --- fragment read offsets: row (lane&15) of a 16-row tile, k chunk (lane>>4) (+4 for k 32..63)
+  const int sw = (lane >> 1) & 7;
+  const int c0 = (lane >> 4) ^ sw, c1 = ((lane >> 4) + 4) ^ sw;
+  const int rrow = (lane & 15) * 128;
+  const int ra0 = 64 * wr * 128 + rrow + 16 * c0, ra1 = 64 * wr * 128 + rrow + 16 * c1;
+  const int rb0 = 32 * wc * 128 + rrow + 16 * c0, rb1 = 32 * wc * 128 + rrow + 16 * c1;
+  const char* bufE = smem;
+  const char* bufO = smem + BUF;
+  const int er = lane & 15, ec = 4 * (lane >> 4);
+
+  f32x4 acc[2][4][4];
+  bf16x8 af[4][2], bf[2][2][2];
+
+  set_src(m0, nb0);
+  prologue();
+  nt_vmcnt<4>();
+  nt_barrier();
+
+  while (true) {
+    if (wr == 1) nt_barrier();  // group 1 runs one barrier behind
+    const int next = local + stride;
+    const bool has_next = next < cnt;
+    int m1 = 0, nb1 = 0;
+    if (has_next) nt_tile_origin(p, start + next, m1, nb1);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[a][b][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // Four phases per two K-tiles t (ring slot E) and t+1 (slot O).  A phase: fragment reads and
+    // two units of DMA, all reads retired (lgkmcnt(0)) before the first barrier, 32 MFMAs between
+    // the barriers.  DMA: P1 a0,a1(t+1)->O  P2 b0,b1(t+2)->E  P3 a0,a1(t+2)->E  P4 b0,b1(t+3)->O;
+    // each unit is restaged at least one phase after the phase whose barrier retired its reads.
+    // vmcnt(4) at P2 / P4 keeps two units in flight and retires the tile the next phase reads.
+    // With the plain epilogues the K-tile stream runs on across tiles: the last iteration loads
+    // the next tile's K-tiles 0 and 1, so a tile starts with no prologue.
+    const int niter = nk >> 1;
+    for (int it = 0; it < niter; ++it) {
+      const int t = 2 * it;
+      const bool more = it + 1 < niter;
+      const bool go = more || (OVERLAP && has_next);
+      const int t2 = more ? t + 2 : 0, t3 = more ? t + 3 : 1;
+      // P1: m-subtile 0 of tile t
+      nt_read_b<0>(bf, bufE, rb0, rb1);
+      nt_read_b<1>(bf, bufE, rb0, rb1);
+      nt_read_a<0>(af, bufE, ra0, ra1);
+      dma(0, t + 1);
+      dma(1, t + 1);
+      if (!more && go) set_src(m1, nb1);
+      nt_lgkmcnt<0>();
+      nt_barrier();
+      nt_quadrant<0, 0>(acc, af, bf);
+      nt_quadrant<0, 1>(acc, af, bf);
+      nt_barrier();
+      // P2: m-subtile 1 of tile t; retire tile t+1
+      nt_read_a<1>(af, bufE, ra0, ra1);
+      if (go) {
+        dma(2, t2);
+        dma(3, t2);
+        nt_vmcnt<4>();
+      } else {
+        nt_vmcnt<0>();
+      }
+      nt_lgkmcnt<0>();
+      nt_barrier();
+      nt_quadrant<1, 0>(acc, af, bf);
+      nt_quadrant<1, 1>(acc, af, bf);
+      nt_barrier();
+      // P3: m-subtile 0 of tile t+1
+      nt_read_b<0>(bf, bufO, rb0, rb1);
+      nt_read_b<1>(bf, bufO, rb0, rb1);
+      nt_read_a<0>(af, bufO, ra0, ra1);
+      if (go) {
+        dma(0, t2);
+        dma(1, t2);
+      }
+      nt_lgkmcnt<0>();
+      nt_barrier();
+      nt_quadrant<0, 0>(acc, af, bf);
+      nt_quadrant<0, 1>(acc, af, bf);
+      nt_barrier();
+      // P4: m-subtile 1 of tile t+1; retire tile t+2
+      nt_read_a<1>(af, bufO, ra0, ra1);
+      if (go) {
+        dma(2, t3);
+        dma(3, t3);
+        nt_vmcnt<4>();
+      }
+      nt_lgkmcnt<0>();
+      nt_barrier();
+      nt_quadrant<1, 0>(acc, af, bf);
+      nt_quadrant<1, 1>(acc, af, bf);
+      nt_barrier();
+    }
+    if (wr == 0) nt_barrier();  // re-align the groups
+    if constexpr (!OVERLAP) nt_barrier();  // every wave is past its last fragment read: LDS is free
+
+    // --- epilogue ---------------------------------------------------------------------------------
+    // accumulator (ms, mi, n): tile row 128ms + 64wr + 16mi + (lane&15), tile columns
+    // 128(n>>1) + 32wc + 16(n&1) + 4(lane>>4) + [0,4)
+    if constexpr (OVERLAP) {
+      // bf16 results first (ACC: plus the old C, whose loads the compiler waits for here, before
+      // any DMA is in flight), then the next tile's prologue, then the stores behind it
+      bf16_t* cbase = p.C + (long)(m0 + 64 * wr + er) * p.ldc + nb0 + 32 * wc + ec;
+      us4 o[2][4][4];
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            if constexpr (EPI == EPI_ACC)
+              o[ms][mi][n] = *reinterpret_cast<const us4*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc +
+                                                            (n >> 1) * p.bsplit + 16 * (n & 1));
+          }
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float x = acc[ms][mi][n][j];
+              if constexpr (EPI == EPI_ACC) x += bf2f(o[ms][mi][n][j]);
+              o[ms][mi][n][j] = f2bf(x);
+            }
+      // pin the conversions (and the compiler's waits for the old C) in front of the DMA below
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) asm volatile("" ::"v"(o[ms][mi][n]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            *reinterpret_cast<us4*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + (n >> 1) * p.bsplit +
+                                    16 * (n & 1)) = o[ms][mi][n];
+    } else if constexpr (EPI == EPI_SWIGLU) {
+      // gu tile straight from the accumulators; a = silu(g) * u from the bf16-rounded g, u (what
+      // the backward re-reads from gu), staged through LDS for the row-major and transposed copies
+      bf16_t* gbase = p.C + (long)(m0 + 64 * wr + er) * p.ldc + nb0 + 32 * wc + ec;
+      constexpr int A_LD = 264;            // [256 t][128 f] + 8 B pad
+      char* sa = smem;                      // a, row-major
+      char* sat = smem + 256 * A_LD;        // a^T [128 f][256 t], row stride EPI_LD
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const int r = 128 * ms + 64 * wr + 16 * mi + er;
+            const int c = 32 * wc + 16 * n + ec;
+            us4 g4, u4, o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              g4[j] = f2bf(acc[ms][mi][n][j]);
+              u4[j] = f2bf(acc[ms][mi][n + 2][j]);
+              o[j] = f2bf(silu(bf2f(g4[j])) * bf2f(u4[j]));
+              *reinterpret_cast<bf16_t*>(sat + (c + j) * EPI_LD + 2 * r) = o[j];
+            }
+            bf16_t* gp = gbase + (long)(128 * ms + 16 * mi) * p.ldc + 16 * n;
+            *reinterpret_cast<us4*>(gp) = g4;
+            *reinterpret_cast<us4*>(gp + p.bsplit) = u4;
+            *reinterpret_cast<us4*>(sa + r * A_LD + 2 * c) = o;
+          }
+      nt_barrier();
+      const int f0 = nb0;  // nstride 128: the tile's gate columns
+      // a: 256 rows x 256 B; a wave writes two rows per instruction
+#pragma unroll 4
+      for (int i = 0; i < 16; ++i) {
+        const int r = 16 * i + 2 * w + (lane >> 5), c = 4 * (lane & 31);
+        *reinterpret_cast<us4*>(p.C2 + (long)(m0 + r) * p.F + f0 + c) =
+            *reinterpret_cast<const us4*>(sa + r * A_LD + 2 * c);
+      }
+      // a^T: 128 rows x 512 B
+#pragma unroll 4
+      for (int i = 0; i < 16; ++i) {
+        const int r = 8 * i + w, c = 4 * lane;
+        *reinterpret_cast<us4*>(p.C3 + (long)(f0 + r) * p.M + m0 + c) =
+            *reinterpret_cast<const us4*>(sat + r * EPI_LD + 2 * c);
+      }
+    } else {  // EPI_SWIGLU_BWD: acc = da[t][f] for the tile's 256 f columns (plain column map)
+      // dg = da * u * silu'(g), du = da * silu(g); g, u from gu[t][f], gu[t][F + f]
+      char* sdt = smem;  // dgu^T staging: [256 f][256 t] for gate, then up (two passes)
+      us4 dgv[2][4][4], duv[2][4][4];
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            const int r = 128 * ms + 64 * wr + 16 * mi + er;
+            const int c = 128 * (n >> 1) + 32 * wc + 16 * (n & 1) + ec;
+            const bf16_t* gp = p.G + (long)(m0 + r) * (2L * p.F) + nb0 + c;
+            const us4 g4 = *reinterpret_cast<const us4*>(gp);
+            const us4 u4 = *reinterpret_cast<const us4*>(gp + p.F);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float da = bf2f(f2bf(acc[ms][mi][n][j]));
+              const float g = bf2f(g4[j]), u = bf2f(u4[j]);
+              const float sg = 1.f / (1.f + __expf(-g));
+              const float s = g * sg;
+              dgv[ms][mi][n][j] = f2bf(da * u * (sg + s * (1.f - sg)));
+              duv[ms][mi][n][j] = f2bf(da * s);
+            }
+            bf16_t* dp = p.C + (long)(m0 + r) * (2L * p.F) + nb0 + c;
+            *reinterpret_cast<us4*>(dp) = dgv[ms][mi][n];
+            *reinterpret_cast<us4*>(dp + p.F) = duv[ms][mi][n];
+          }
+      // dgu^T [2F][T]: gate rows nb0 + c, up rows F + nb0 + c; staged transposed per half
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        if (half) nt_barrier();
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+              const int r = 128 * ms + 64 * wr + 16 * mi + er;
+              const int c = 128 * (n >> 1) + 32 * wc + 16 * (n & 1) + ec;
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                *reinterpret_cast<bf16_t*>(sdt + (c + j) * EPI_LD + 2 * r) =
+                    half ? duv[ms][mi][n][j] : dgv[ms][mi][n][j];
+            }
+        nt_barrier();
+#pragma unroll 4
+        for (int i = 0; i < 32; ++i) {
+          const int r = 8 * i + w, c = 4 * lane;
+          *reinterpret_cast<us4*>(p.C3 + (long)(half * p.F + nb0 + r) * p.M + m0 + c) =
+              *reinterpret_cast<const us4*>(sdt + r * EPI_LD + 2 * c);
+        }
+      }
+    }
+    if (!has_next) break;
+    if constexpr (!OVERLAP) {
+      nt_barrier();  // every wave is done with the LDS staging
+      set_src(m1, nb1);
+      prologue();
+      nt_vmcnt<4>();
+      nt_barrier();
+    }
+    local = next;
+    m0 = m1;
+    nb0 = nb1;
+  }
+}
+
+namespace {
+
+bool nt_shape_ok(int M, int N, int K) {
+  return M > 0 && N > 0 && K > 0 && M % NT_BM == 0 && N % NT_BN == 0 && K % (2 * NT_BK) == 0;
+}
+
+int nt_group(int ntm) { return ntm >= 8 ? 8 : ntm; }
+
+int nt_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// One workgroup per CU (128 KiB ring): a grid of min(tiles, CUs rounded down to a multiple of 8)
+// workgroups that loop over their XCD's tiles.
+template <int EPI>
+hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, NT_LDS));
+    attr = true;
+  }
+  const int cap = (nt_cus() / 8) * 8;
+  int grid = tiles;
+  a.wg_per_xcd = 1 << 30;  // one tile per workgroup
+  if (tiles > cap && cap >= 8) {
+    grid = cap;
+    a.wg_per_xcd = cap / 8;
+  }
+  if (const char* g = getenv("DSTACK_AMD_GEMM_NT_GROUP")) a.group = atoi(g) > 0 ? atoi(g) : a.group;
+  gemm_nt_kernel<EPI><<<grid, 512, NT_LDS, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" bool dsa_gemm_nt_supported(int M, int N, int K) { return nt_shape_ok(M, N, K); }
+
+// C[M][N] (+)= A[M][K] B[N][K]^T.  Leading dimensions in elements, multiples of 8 (16-byte rows);
+// every operand must be < 4 GiB from its tile origin (32-bit DMA offsets).
+extern "C" hipError_t dsa_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
+                                  long ldc, int accumulate, hipStream_t st) {
+  if (!nt_shape_ok(M, N, K) || lda % 8 || ldb % 8 || ldc % 4 || lda < K || ldb < K || ldc < N)
+    return hipErrorInvalidValue;
+  if (255L * lda * 2 + 2L * K > 0xffffffffL || 255L * ldb * 2 + 2L * K > 0xffffffffL) return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (bf16_t*)C;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.M = M;
+  a.K = K;
+  a.ntn = N / NT_BN;
+  a.nstride = NT_BN;
+  a.bsplit = 128;
+  a.group = nt_group(M / NT_BM);
+  const int tiles = (M / NT_BM) * (N / NT_BN);
+  return accumulate ? nt_launch<EPI_ACC>(a, tiles, st) : nt_launch<EPI_STORE>(a, tiles, st);
+}
+
+extern "C" bool dsa_gemm_nt_swiglu_supported(int T, int F, int K) {
+  return T % NT_BM == 0 && F % 128 == 0 && K % (2 * NT_BK) == 0 && F > 0 && T > 0;
+}
+
+// gu[T][2F] = X[T][K] Wgu[2F][K]^T (gate rows 0..F-1, up rows F..2F-1), a = silu(g) * u [T][F] and
+// a^T [F][T] from the same tile.
+extern "C" hipError_t dsa_gemm_nt_swiglu(const void* X, const void* W, void* gu, void* a_out, void* aT, int T, int F,
+                                         int K, long ldx, long ldw, hipStream_t st) {
+  if (!dsa_gemm_nt_swiglu_supported(T, F, K) || ldx % 8 || ldw % 8 || ldx < K || ldw < K) return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)X;
+  a.B = (const bf16_t*)W;
+  a.C = (bf16_t*)gu;
+  a.C2 = (bf16_t*)a_out;
+  a.C3 = (bf16_t*)aT;
+  a.lda = ldx;
+  a.ldb = ldw;
+  a.ldc = 2L * F;
+  a.M = T;
+  a.K = K;
+  a.F = F;
+  a.ntn = F / 128;
+  a.nstride = 128;
+  a.bsplit = F;
+  a.group = nt_group(T / NT_BM);
+  return nt_launch<EPI_SWIGLU>(a, (T / NT_BM) * (F / 128), st);
+}
+
+extern "C" bool dsa_gemm_nt_swiglu_bwd_supported(int T, int F, int K) {
+  return T % NT_BM == 0 && F % NT_BN == 0 && K % (2 * NT_BK) == 0 && F > 0 && T > 0;
+}
+
+// da = dY[T][K] WdT[F][K]^T (WdT = W_down^T), fused with the SwiGLU backward against gu [T][2F]:
+// dgu [T][2F] and dgu^T [2F][T].
+extern "C" hipError_t dsa_gemm_nt_swiglu_bwd(const void* dY, const void* WdT, const void* gu, void* dgu, void* dguT,
+                                             int T, int F, int K, long ldy, long ldw, hipStream_t st) {
+  if (!dsa_gemm_nt_swiglu_bwd_supported(T, F, K) || ldy % 8 || ldw % 8 || ldy < K || ldw < K)
+    return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)dY;
+  a.B = (const bf16_t*)WdT;
+  a.C = (bf16_t*)dgu;
+  a.C3 = (bf16_t*)dguT;
+  a.G = (const bf16_t*)gu;
+  a.lda = ldy;
+  a.ldb = ldw;
+  a.ldc = 2L * F;
+  a.M = T;
+  a.K = K;
+  a.F = F;
+  a.ntn = F / NT_BN;
+  a.nstride = NT_BN;
+  a.bsplit = 128;
+  a.group = nt_group(T / NT_BM);
+  return nt_launch<EPI_SWIGLU_BWD>(a, (T / NT_BM) * (F / NT_BN), st);
+}
