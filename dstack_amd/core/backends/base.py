@@ -188,27 +188,54 @@ def get_shim_commands(authorized_keys: List[str], shim_url: str, runner_url: str
     ]
 
 
-# amdgpu-install release used when a GPU host boots without the kernel driver (the ROCm user space
-# ships in the job's container image; the host only needs amdgpu + /dev/kfd)
-AMDGPU_INSTALL_RELEASE = "6.4"
-AMDGPU_INSTALL_DEB = "amdgpu-install_6.4.60400-1_all.deb"
+# amdgpu-install releases used when a GPU host boots without the kernel driver (the ROCm user space
+# ships in the job's container image; the host only needs amdgpu + /dev/kfd).  MI350X/MI355X
+# (gfx950) need the ROCm 7.x driver; the earlier Instinct parts are served by 6.4.
+AMDGPU_INSTALL_RELEASES = {
+    "gfx950": ("7.0", "amdgpu-install_7.0.70000-1_all.deb"),
+    "default": ("6.4", "amdgpu-install_6.4.60400-1_all.deb"),
+}
+AMDGPU_INSTALL_RELEASE, AMDGPU_INSTALL_DEB = AMDGPU_INSTALL_RELEASES["default"]
 # PCI device ids of the Instinct GPUs this build schedules (MI100 .. MI355X), vendor 1002
 AMD_INSTINCT_PCI = "738c|740c|740f|74a0|74a1|74a5|74b5|75a0|75a3"
+AMD_GFX950_PCI = "75a0|75a3"  # MI350X, MI355X
+# written when the bootstrap could not bring up /dev/kfd; the shim reports its text in host_info
+# ("gpu_driver_error") and the server fails the instance's provisioning with it
+AMDGPU_FAILED_MARKER = "/var/lib/dstack/amdgpu-install.failed"
 
 
-def get_amd_driver_commands(release: str = AMDGPU_INSTALL_RELEASE, deb: str = AMDGPU_INSTALL_DEB) -> List[str]:
+def get_amd_driver_commands(releases: Optional[Dict[str, tuple]] = None, marker: str = AMDGPU_FAILED_MARKER,
+                            log: str = "/var/log/dstack-amdgpu.log", os_release: str = "/etc/os-release") -> List[str]:
     """Host setup for clouds whose default image has no AMD GPU driver (plain Ubuntu on AWS, GCP,
     Azure, OCI...): when the host has an Instinct GPU but no ``/dev/kfd``, install the amdgpu DKMS
     driver with amdgpu-install and load it, before the shim starts (it discovers GPUs through KFD).
+
+    * the release follows the detected part (``AMDGPU_INSTALL_RELEASES``: 7.x for gfx950);
+    * the Ubuntu codename comes from ``/etc/os-release`` (jammy, noble, ...), not a fixed one;
+    * the running kernel's headers are installed first (DKMS builds against them);
+    * when ``/dev/kfd`` is still missing afterwards, ``marker`` gets the reason and the log tail,
+      so the host fails provisioning with it instead of registering with zero GPUs.
+
     A no-op on hosts that already have the driver (vendor GPU images, the packer image in
     ``scripts/packer``) and on CPU hosts.  The reference ships its own VM images instead."""
-    url = f"https://repo.radeon.com/amdgpu-install/{release}/ubuntu/jammy/{deb}"
+    rel = dict(AMDGPU_INSTALL_RELEASES, **(releases or {}))
+    new_rel, new_deb = rel["gfx950"]
+    old_rel, old_deb = rel["default"]
     script = (
-        f"if [ ! -e /dev/kfd ] && lspci -nn 2>/dev/null | grep -qiE '1002:({AMD_INSTINCT_PCI})'; then "
-        f"export DEBIAN_FRONTEND=noninteractive; "
-        f"curl -fsSL -o /tmp/amdgpu-install.deb '{url}' && apt-get install -yqq /tmp/amdgpu-install.deb && "
-        f"amdgpu-install -y --usecase=dkms --no-32 && modprobe amdgpu; "
-        f"fi >> /var/log/dstack-amdgpu.log 2>&1"
+        f"if lspci -nn 2>/dev/null | grep -qiE '1002:({AMD_INSTINCT_PCI})' && [ ! -e /dev/kfd ]; then "
+        f"export DEBIAN_FRONTEND=noninteractive; rm -f {marker}; "
+        f"CODENAME=$(. {os_release} 2>/dev/null; echo ${{VERSION_CODENAME:-${{UBUNTU_CODENAME:-jammy}}}}); "
+        f"if lspci -nn | grep -qiE '1002:({AMD_GFX950_PCI})'; then REL={new_rel}; DEB={new_deb}; "
+        f"else REL={old_rel}; DEB={old_deb}; fi; "
+        f"echo \"amdgpu-install $REL for ubuntu/$CODENAME on kernel $(uname -r)\"; "
+        f"apt-get update -qq; apt-get install -yqq \"linux-headers-$(uname -r)\"; "
+        f"curl -fsSL -o /tmp/amdgpu-install.deb \"https://repo.radeon.com/amdgpu-install/$REL/ubuntu/$CODENAME/$DEB\" "
+        f"&& apt-get install -yqq /tmp/amdgpu-install.deb && amdgpu-install -y --usecase=dkms --no-32 "
+        f"&& modprobe amdgpu; "
+        f"if [ ! -e /dev/kfd ]; then mkdir -p $(dirname {marker}); "
+        f"{{ echo \"amdgpu $REL driver install failed on ubuntu/$CODENAME kernel $(uname -r): /dev/kfd missing\"; "
+        f"tail -n 5 {log}; }} > {marker} 2>/dev/null; fi; "
+        f"fi >> {log} 2>&1"
     )
     return [script]
 

@@ -307,6 +307,16 @@ def _check_provisioning(s: Session, inst: InstanceModel):
         except Exception as e:  # noqa: BLE001
             logger.debug("update_provisioning_data: %s", e)
     if jpd.hostname and _shim_healthy(inst, jpd):
+        driver_err = _gpu_driver_error(inst, jpd)
+        if driver_err:
+            # the bootstrap could not load amdgpu (no /dev/kfd): a GPU host without GPUs is a
+            # failed provisioning, with the bootstrap's reason, not an idle CPU host
+            inst.status = InstanceStatus.TERMINATING.value
+            inst.termination_reason = f"GPU driver: {driver_err}"[:1000]
+            inst.health_status = inst.termination_reason
+            inst.termination_deadline = inst.termination_deadline or get_current_datetime()
+            logger.warning("%s: %s", inst.name, inst.termination_reason)
+            return
         inst.status = (InstanceStatus.BUSY if (inst.busy_blocks or 0) > 0 else InstanceStatus.IDLE).value
         inst.termination_deadline = None
         inst.health_status = None
@@ -370,6 +380,20 @@ def refresh_gpu_health(inst: InstanceModel, jpd: JobProvisioningData, force: boo
         except Exception as e:  # noqa: BLE001
             logger.debug("%s: start probe: %s", inst.name, e)
     return state
+
+
+def _gpu_driver_error(inst: InstanceModel, jpd: JobProvisioningData) -> Optional[str]:
+    """The shim's ``gpu_driver_error`` (bootstrap marker) when the offer has GPUs but the host
+    reports none; None otherwise or when host_info is unavailable."""
+    if not jpd.instance_type.resources.gpus:
+        return None
+    try:
+        hi = get_shim_client(jpd, inst.project.ssh_private_key).host_info()
+    except Exception:  # noqa: BLE001 - older shims / transient errors: judged by the probes later
+        return None
+    if not isinstance(hi, dict) or int(hi.get("gpu_count") or 0) > 0:
+        return None
+    return hi.get("gpu_driver_error") or None
 
 
 def _shim_healthy(inst: InstanceModel, jpd: JobProvisioningData) -> bool:

@@ -310,6 +310,8 @@ def _process_running(s: Session, run: RunModel, job: JobModel):
     job.remove_at = None  # runner reachable again: clear the unreachable marker
     if resp.get("gpu_probe") and job.instance is not None:
         _record_gpu_probe(job, resp["gpu_probe"])
+    if resp.get("rccl_preflight") and job.instance is not None:
+        _record_rccl_preflight(job, resp["rccl_preflight"])
     if resp.get("job_logs") or resp.get("runner_logs"):
         logs_services.write_job_logs(run.project.name, run.run_name, str(job.id), resp)
         if resp.get("job_logs"):
@@ -355,6 +357,38 @@ def _record_gpu_probe(job: JobModel, doc: dict):
     if inst.health_data != data:
         inst.health_data = data
         inst.health_status = None if health.healthy else health.message
+
+
+def _record_rccl_preflight(job: JobModel, doc: dict):
+    """The runner ran the RCCL all-reduce pre-flight (DSTACK_RCCL_PREFLIGHT) before a distributed
+    job: its bus bandwidth joins the instance's health, and a failed pre-flight -- or a bus bandwidth
+    under ``DSTACK_RCCL_MIN_BUSBW_GB_S`` (per-link xGMI ring bound ~153 GB/s x links in use) -- marks
+    the host unhealthy, so ``filter_pool_instances`` stops placing jobs on it until the shim's next
+    health probe clears it.  The failing job itself already carries the probe's message."""
+    import os
+
+    from dstack_amd.core.models.instances import InstanceHealth
+
+    inst = job.instance
+    try:
+        old = InstanceHealth.model_validate_json(inst.health_data) if inst.health_data else InstanceHealth()
+    except Exception:  # noqa: BLE001 - an unreadable previous document is replaced
+        old = InstanceHealth()
+    busbw = doc.get("rccl_busbw_gb_s")
+    healthy = bool(doc.get("healthy", True))
+    message = doc.get("message") or ""
+    floor = os.environ.get("DSTACK_RCCL_MIN_BUSBW_GB_S")
+    if healthy and floor and busbw is not None and float(busbw) < float(floor):
+        healthy = False
+        message = f"RCCL bus bandwidth {float(busbw):.1f} GB/s below {float(floor):.1f} GB/s"
+    upd = {"rccl_busbw_gb_s": busbw if busbw is not None else old.rccl_busbw_gb_s}
+    if not healthy:
+        upd.update(healthy=False, message=f"RCCL pre-flight: {message or 'failed'}", source="runner")
+    health = old.model_copy(update=upd)
+    inst.health_data = health.model_dump_json()
+    if not healthy:
+        inst.health_status = health.message
+        logger.warning("%s: %s", inst.name, health.message)
 
 
 def _runner_unreachable(job: JobModel, err: str):

@@ -205,7 +205,7 @@ static std::vector<std::vector<double>> xgmi_probe(int ndev, bool quick) {
 
 // rccl_probe.cpp
 std::string rccl_allreduce_probe_mp(int gpus_per_node, int nodes, int node_rank, const std::string& master, int port,
-                                    bool quick, double* best_busbw, int* world_out, std::string* err);
+                                    bool quick, int timeout_ms, double* best_busbw, int* world_out, std::string* err);
 
 
 // Per-SKU baselines: what THIS probe measures on a healthy part (not the datasheet peaks), so a
@@ -232,6 +232,7 @@ int main(int argc, char** argv) {
   double min_hbm = -1, min_mfma = -1;  // absolute overrides; default: min_fraction x per-SKU baseline
   double min_fraction = 0.8;
   int rccl_nodes = 1, node_rank = 0, master_port = 29600, gpus_per_node = 0;
+  int rccl_timeout_ms = 300000;  // per-rank bootstrap + sweep budget (the runner derives it from its own limit)
   std::string master = "127.0.0.1";
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -250,11 +251,16 @@ int main(int argc, char** argv) {
     else if (a == "--master" && i + 1 < argc) master = argv[++i];
     else if (a == "--master-port" && i + 1 < argc) master_port = atoi(argv[++i]);
     else if (a == "--gpus-per-node" && i + 1 < argc) gpus_per_node = atoi(argv[++i]);
+    else if (a == "--timeout-ms" && i + 1 < argc) {
+      const int t = atoi(argv[++i]);
+      if (t > 0) rccl_timeout_ms = t;
+    }
     else {
       fprintf(stderr,
               "usage: dstack-probe [--quick] [--json] [--hbm] [--mfma] [--xgmi] [--rccl] [--device N]\n"
               "                    [--min-fraction F | --min-hbm-tbs X --min-mfma-tflops Y]\n"
-              "                    [--rccl [--gpus-per-node G] --nodes N --node-rank R --master HOST --master-port P]\n");
+              "                    [--rccl [--gpus-per-node G] --nodes N --node-rank R --master HOST --master-port P\n"
+              "                     [--timeout-ms T]]\n");
       return 2;
     }
   }
@@ -268,8 +274,8 @@ int main(int argc, char** argv) {
     } else {
       double best = 0;
       int world = 0;
-      std::string sweep = rccl_allreduce_probe_mp(g, rccl_nodes, node_rank, master, master_port, quick, &best, &world,
-                                                  &rccl_err);
+      std::string sweep = rccl_allreduce_probe_mp(g, rccl_nodes, node_rank, master, master_port, quick,
+                                                  rccl_timeout_ms, &best, &world, &rccl_err);
       char b[256];
       snprintf(b, sizeof b, "\"rccl_world\": %d, \"rccl_gpus_per_node\": %d, \"rccl\": ", world, g);
       rccl_json = b + sweep + ", ";

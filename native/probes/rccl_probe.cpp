@@ -116,7 +116,7 @@ static std::vector<double> parse_times(const std::string& line) {
 }
 
 std::string rccl_allreduce_probe_mp(int gpus_per_node, int nodes, int node_rank, const std::string& master, int port,
-                                    bool quick, double* best_busbw, int* world_out, std::string* err) {
+                                    bool quick, int timeout_ms, double* best_busbw, int* world_out, std::string* err) {
   const int world = nodes * gpus_per_node;
   *world_out = world;
   *best_busbw = 0;
@@ -129,7 +129,7 @@ std::string rccl_allreduce_probe_mp(int gpus_per_node, int nodes, int node_rank,
         memcpy(&id[0], &u, sizeof u);
         return std::string();
       },
-      [quick](const dsa::RankCtx& c, const std::string& id) { return rank_body(c, id, quick); }, 300000, &e);
+      [quick](const dsa::RankCtx& c, const std::string& id) { return rank_body(c, id, quick); }, timeout_ms, &e);
   std::vector<double> worst;  // per size: slowest local rank (us)
   for (auto& r : results) {
     if (r.line.find("\"sum_ok\": false") != std::string::npos && e.empty())

@@ -296,6 +296,12 @@ Json Executor::pull(int64_t since) const {
       } catch (...) {
       }
     }
+    if (!preflight_json_.empty()) {
+      try {
+        out.set("rccl_preflight", Json::parse(preflight_json_));
+      } catch (...) {
+      }
+    }
   }
   out.set("job_logs", enc(jl));
   out.set("runner_logs", enc(rl));
@@ -584,8 +590,14 @@ bool Executor::run_rccl_preflight(std::string& msg) {
     return d;
   };
   const int port = atoi(get("MASTER_PORT", "29500").c_str()) + 1;
-  std::vector<std::string> argv = {"timeout", "-k", "10", get("DSTACK_RCCL_PREFLIGHT_TIMEOUT", "300"),
+  // the probe's own per-rank deadline ends before the outer `timeout`, so a hung rank is reported
+  // by name ("rank N timed out") instead of as a bare timeout
+  int limit_s = atoi(get("DSTACK_RCCL_PREFLIGHT_TIMEOUT", "300").c_str());
+  if (limit_s < 20) limit_s = 20;
+  const int probe_ms = (limit_s - 15) * 1000 - 5000;  // run_ranks collects up to 5 s past its deadline
+  std::vector<std::string> argv = {"timeout", "-k", "10", std::to_string(limit_s),
                                    opts_.probe_binary, "--rccl", "--quick", "--json",
+                                   "--timeout-ms", std::to_string(probe_ms),
                                    "--gpus-per-node", get("DSTACK_GPUS_PER_NODE", "0"),
                                    "--nodes", get("DSTACK_NODES_NUM", "1"), "--node-rank", get("DSTACK_NODE_RANK", "0"),
                                    "--master", get("DSTACK_MASTER_NODE_IP", "127.0.0.1"),
@@ -595,8 +607,27 @@ bool Executor::run_rccl_preflight(std::string& msg) {
   int rc = run_cmd(argv, opts_.working_dir, &out, &env);
   job_logs_.append("[dstack] RCCL pre-flight (" + std::to_string(now_millis() - t0) + " ms, exit " +
                    std::to_string(rc) + "): " + out + (out.empty() || out.back() != '\n' ? "\n" : ""));
+  // the probe's document (last JSON line): the server records its busbw / verdict as the
+  // instance's health, which the scheduler reads (an unhealthy host gets no new jobs)
+  std::string doc, probe_msg;
+  size_t end = out.find_last_not_of(" \r\n");
+  if (end != std::string::npos) {
+    size_t begin = out.rfind('\n', end);
+    begin = begin == std::string::npos ? 0 : begin + 1;
+    doc = out.substr(begin, end - begin + 1);
+  }
+  if (!doc.empty() && doc[0] == '{') {
+    try {
+      Json d = Json::parse(doc);
+      probe_msg = d["message"].str("");
+      std::lock_guard<std::mutex> lk(states_mu_);
+      preflight_json_ = doc;
+    } catch (...) {
+    }
+  }
   if (rc != 0) {
     msg = rc == 124 || rc == 137 ? "RCCL pre-flight timed out" : "RCCL pre-flight failed (exit " + std::to_string(rc) + ")";
+    if (!probe_msg.empty()) msg += ": " + probe_msg;
     return false;
   }
   return true;
@@ -660,6 +691,12 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
     return -1;
   }
   auto env = build_env();
+  std::string wd = opts_.working_dir, wd_err;
+  if (!join_rel_path(opts_.working_dir, js["working_dir"].str(), wd, wd_err)) {
+    reason = "executor_error";
+    msg = wd_err;
+    return -1;
+  }
   // DSTACK_ROCPROF=1: wrap the job in rocprofv3 kernel-trace statistics, plus the hardware
   // counters of DSTACK_ROCPROF_COUNTERS (validated against the one-pass budget, runner/rocprof.h);
   // the summaries are appended to the job log when the job ends (rocprof counters in run logs)
@@ -683,18 +720,15 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
     // launcher: its preloaded library initialises the GPU in the process it wraps)
     std::vector<std::string> wrapped;
     std::string werr;
-    if (rocprof_wrap(argv, rocprof_argv(rocprof_dir, counters), wrapped, werr)) {
+    std::string path_env = getenv("PATH") ? getenv("PATH") : "/usr/local/bin:/usr/bin:/bin";
+    for (auto& kv : env)
+      if (kv.first == "PATH") path_env = kv.second;
+    if (rocprof_wrap(argv, rocprof_argv(rocprof_dir, counters), wrapped, werr, fs_program_lookup(path_env), wd)) {
       argv = wrapped;
     } else {
       job_logs_.append("[dstack] DSTACK_ROCPROF ignored: " + werr + "; the job runs unprofiled\n");
       rocprof_dir.clear();
     }
-  }
-  std::string wd = opts_.working_dir, wd_err;
-  if (!join_rel_path(opts_.working_dir, js["working_dir"].str(), wd, wd_err)) {
-    reason = "executor_error";
-    msg = wd_err;
-    return -1;
   }
   mkdirs(wd);
   std::vector<std::string> envs;

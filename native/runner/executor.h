@@ -107,6 +107,7 @@ class Executor {
   std::atomic<bool> stop_requested_{false};
   std::atomic<int> child_pgid_{0};
   std::string probe_json_;  // last dstack-probe result (JSON), guarded by states_mu_
+  std::string preflight_json_;  // last RCCL pre-flight document
   mutable std::atomic<bool> pulled_after_finish_{false};
   std::mutex fin_mu_;
   std::condition_variable fin_cv_;

@@ -4,6 +4,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cctype>
@@ -128,6 +130,7 @@ std::string shell_quote(const std::string& w) {
 struct Word {
   std::string text;  // unquoted
   size_t begin = 0;  // offset in the segment
+  size_t end = 0;    // one past its last character
 };
 
 // Top-level command separators of a shell script: "&&", "||", ";", "\n", "|", "&" outside quotes,
@@ -203,14 +206,120 @@ std::vector<Word> split_words(const std::string& s) {
     } else if (c == '\\' && i + 1 < s.size()) {
       cur.text += s[++i];
     } else if (isspace((unsigned char)c)) {
+      cur.end = i;
       out.push_back(cur);
       in = false;
     } else {
       cur.text += c;
     }
   }
-  if (in) out.push_back(cur);
+  if (in) {
+    cur.end = s.size();
+    out.push_back(cur);
+  }
   return out;
+}
+
+// "<<" outside quotes (a heredoc; "<<<" here-strings are single-line and fine)
+bool has_heredoc(const std::string& s) {
+  bool sq = false, dq = false;
+  for (size_t i = 0; i < s.size(); ++i) {
+    const char c = s[i];
+    if (sq) {
+      if (c == '\'') sq = false;
+      continue;
+    }
+    if (c == '\\') {
+      ++i;
+      continue;
+    }
+    if (dq) {
+      if (c == '"') dq = false;
+      continue;
+    }
+    if (c == '\'') sq = true;
+    else if (c == '"') dq = true;
+    else if (c == '<' && i + 1 < s.size() && s[i + 1] == '<') {
+      if (i + 2 < s.size() && s[i + 2] == '<') {
+        i += 2;
+        continue;
+      }
+      return true;
+    }
+  }
+  return false;
+}
+
+bool is_elf(const std::string& h) { return h.size() >= 4 && h.compare(0, 4, "\x7f" "ELF") == 0; }
+
+bool is_python_name(const std::string& p) { return base_name(p).rfind("python", 0) == 0; }
+
+// "#!/usr/bin/env -S python3 -u" -> interpreter "python3", extra {"-u"}.  False without "#!".
+bool parse_shebang(const std::string& head, std::string& interp, std::vector<std::string>& extra) {
+  if (head.size() < 2 || head[0] != '#' || head[1] != '!') return false;
+  const size_t nl = head.find('\n');
+  const std::string line = head.substr(2, nl == std::string::npos ? std::string::npos : nl - 2);
+  std::vector<std::string> toks;
+  for (auto& w : split_words(line)) toks.push_back(w.text);
+  size_t i = 0;
+  if (!toks.empty() && base_name(toks[0]) == "env") {
+    ++i;
+    while (i < toks.size() && (toks[i][0] == '-' || is_assignment(toks[i]))) {
+      if (toks[i] == "-u" || toks[i] == "--unset" || toks[i] == "-C" || toks[i] == "--chdir") ++i;
+      ++i;
+    }
+  }
+  interp = i < toks.size() ? toks[i] : "";
+  extra.assign(toks.begin() + (long)std::min(i + 1, toks.size()), toks.end());
+  return true;
+}
+
+// The program rocprofv3 will start, checked on disk.  OK as is when it is an ELF binary; a "#!"
+// Python script is replaced by its interpreter + the script (`replace`); anything else is refused.
+bool check_program(const std::string& prog, const ProgramLookup& look, const std::string& cwd,
+                   std::vector<std::string>& replace, std::string& err) {
+  replace.clear();
+  if (!look) return true;  // no filesystem view (text-rewrite unit tests)
+  const ProgramInfo pi = look(prog, cwd);
+  if (!pi.found) {
+    err = "cannot find the job's program '" + prog + "' to check that it is not a script";
+    return false;
+  }
+  if (is_elf(pi.head)) return true;
+  std::string interp;
+  std::vector<std::string> extra;
+  if (!parse_shebang(pi.head, interp, extra)) {
+    err = "'" + prog + "' is neither an ELF binary nor a #! script (a shell would run it)";
+    return false;
+  }
+  if (!is_python_name(interp)) {
+    err = "'" + prog + "' is a #! script run by '" + (interp.empty() ? std::string("?") : interp) +
+          "', not by Python";
+    return false;
+  }
+  const ProgramInfo ip = look(interp, cwd);
+  if (!ip.found || !is_elf(ip.head)) {
+    err = "the interpreter '" + interp + "' of '" + prog + "' is not an ELF binary (a shim or wrapper script)";
+    return false;
+  }
+  replace.push_back(interp);
+  replace.insert(replace.end(), extra.begin(), extra.end());
+  replace.push_back(prog);
+  return true;
+}
+
+// the Python a launcher (torchrun, accelerate, deepspeed: console scripts) runs under, from its
+// shebang; "python3" when it cannot be read
+std::string launcher_python(const std::string& launcher, const ProgramLookup& look, const std::string& cwd) {
+  if (!look) return "python3";
+  const ProgramInfo pi = look(launcher, cwd);
+  std::string interp;
+  std::vector<std::string> extra;
+  if (pi.found && parse_shebang(pi.head, interp, extra) && is_python_name(interp)) {
+    const ProgramInfo ip = look(interp, cwd);
+    if (ip.found && is_elf(ip.head)) return interp;
+  }
+  return "python3";
 }
 
 // programs that must never sit between rocprofv3 and the GPU program (they fork/exec it)
@@ -219,7 +328,9 @@ const std::set<std::string>& wrappers() {
       "bash", "sh", "dash", "zsh", "ksh", "env", "timeout", "nohup", "numactl", "taskset", "sudo", "su", "time",
       "nice", "ionice", "stdbuf", "xargs", "chrt", "setsid", "strace", "ltrace", "gdb", "valgrind", "rocprofv3",
       "rocprof", "rocprofv2", "rocprof-compute", "omniperf", "mpirun", "mpiexec", "srun", "accelerate",
-      "deepspeed", "ray", "make", "parallel", "watch", "flock", "script", "tini", "dumb-init"};
+      "deepspeed", "ray", "make", "parallel", "watch", "flock", "script", "tini", "dumb-init", "uv", "uvx",
+      "poetry", "conda", "mamba", "micromamba", "pixi", "pipenv", "hatch", "pdm", "rye", "npx", "nix-shell",
+      "apptainer", "singularity", "docker", "podman", "firejail", "xvfb-run", "catchsegv", "sg", "runuser"};
   return w;
 }
 
@@ -236,8 +347,43 @@ bool torchrun_opt_takes_value(const std::string& o) {
 }
 }  // namespace
 
+ProgramLookup fs_program_lookup(const std::string& path_env) {
+  return [path_env](const std::string& prog, const std::string& cwd) {
+    ProgramInfo pi;
+    auto probe = [&](const std::string& f, bool need_exec) {
+      struct stat st;
+      if (stat(f.c_str(), &st) != 0 || !S_ISREG(st.st_mode)) return false;
+      if (need_exec && access(f.c_str(), X_OK) != 0) return false;
+      pi.found = true;
+      pi.path = f;
+      if (FILE* fp = fopen(f.c_str(), "rb")) {
+        char buf[256];
+        size_t n = fread(buf, 1, sizeof buf, fp);
+        pi.head.assign(buf, n);
+        fclose(fp);
+      }
+      return true;
+    };
+    if (prog.find('/') != std::string::npos) {
+      probe(prog[0] == '/' ? prog : (cwd.empty() ? std::string(".") : cwd) + "/" + prog, false);
+      return pi;
+    }
+    size_t a = 0;
+    while (a <= path_env.size()) {
+      size_t b = path_env.find(':', a);
+      if (b == std::string::npos) b = path_env.size();
+      std::string dir = path_env.substr(a, b - a);
+      if (dir.empty()) dir = ".";
+      if (dir[0] != '/') dir = (cwd.empty() ? std::string(".") : cwd) + "/" + dir;
+      if (probe(dir + "/" + prog, true)) break;
+      a = b + 1;
+    }
+    return pi;
+  };
+}
+
 bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::string>& rp, std::vector<std::string>& out,
-                  std::string& err) {
+                  std::string& err, const ProgramLookup& look, const std::string& cwd) {
   if (job.empty()) {
     err = "empty command";
     return false;
@@ -249,8 +395,12 @@ bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::st
       err = "the job's program '" + prog0 + "' is a launcher/wrapper, not the GPU program";
       return false;
     }
+    std::vector<std::string> rep;
+    if (!check_program(job[0], look, cwd, rep, err)) return false;
     out = rp;
-    out.insert(out.end(), job.begin(), job.end());
+    if (rep.empty()) out.push_back(job[0]);
+    else out.insert(out.end(), rep.begin(), rep.end());
+    out.insert(out.end(), job.begin() + 1, job.end());
     return true;
   }
   // {shell, [-l...]-c, script}: rewrite the script's last simple command
@@ -259,6 +409,10 @@ bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::st
     return false;
   }
   const std::string& script = job[2];
+  if (has_heredoc(script)) {
+    err = "the job script has a heredoc (<<): its body lines are not commands";
+    return false;
+  }
   std::vector<std::pair<size_t, size_t>> segs;
   std::vector<std::string> seps;
   if (!split_script(script, segs, seps)) {
@@ -285,6 +439,18 @@ bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::st
     err = "the job's last command follows '" + seps[(size_t)last - 1] + "' (a pipeline or an || branch)";
     return false;
   }
+  // the directory the last command runs in: `cd DIR` segments before it (a DIR with expansions
+  // makes relative program paths unresolvable)
+  std::string run_cwd = cwd;
+  bool cwd_known = true;
+  for (int k = 0; k < last; ++k) {
+    auto ws = split_words(script.substr(segs[(size_t)k].first, segs[(size_t)k].second - segs[(size_t)k].first));
+    if (ws.empty() || (ws[0].text != "cd" && ws[0].text != "pushd")) continue;
+    const std::string d = ws.size() > 1 ? ws[1].text : std::string("~");
+    if (d.find_first_of("$~`*?") != std::string::npos || d == "-") cwd_known = false;
+    else if (d[0] == '/') run_cwd = d, cwd_known = true;
+    else run_cwd = (run_cwd.empty() ? std::string(".") : run_cwd) + "/" + d;
+  }
   const size_t s0 = segs[(size_t)last].first, s1 = segs[(size_t)last].second;
   const std::string seg = script.substr(s0, s1 - s0);
   auto words = split_words(seg);
@@ -302,16 +468,36 @@ bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::st
     err = "the job's last command is a compound command ('" + first + "')";
     return false;
   }
+  auto check = [&](const std::string& p, std::vector<std::string>& rep) {
+    if (!cwd_known && p.find('/') != std::string::npos && p[0] != '/') {
+      err = "cannot resolve '" + p + "': the script changes to a directory with an expansion first";
+      return false;
+    }
+    return check_program(p, look, run_cwd, rep, err);
+  };
+  auto join = [](const std::vector<std::string>& v) {
+    std::string r;
+    for (size_t i = 0; i < v.size(); ++i) r += (i ? " " : "") + shell_quote(v[i]);
+    return r;
+  };
   const std::string prog = base_name(first);
-  std::string rp_text;
-  for (size_t i = 0; i < rp.size(); ++i) rp_text += (i ? " " : "") + shell_quote(rp[i]);
-  // where the profiler goes in the segment, and what it wraps
-  size_t insert_at = words[w].begin;
-  std::string inserted = "exec " + rp_text + " ";
-  const bool py = prog.rfind("python", 0) == 0;
+  const std::string rp_text = join(rp);
+  const bool py = is_python_name(prog);
+  static const std::set<std::string> py_launchers = {"accelerate", "accelerate.commands.launch",
+                                                      "accelerate.commands.accelerate_cli", "deepspeed",
+                                                      "deepspeed.launcher.runner", "deepspeed.launcher.launch",
+                                                      "torch.distributed.launch"};
   const bool via_module = py && w + 2 < words.size() && words[w + 1].text == "-m" &&
-                          (words[w + 2].text == "torch.distributed.run" || words[w + 2].text == "torch.distributed.launch");
+                          words[w + 2].text == "torch.distributed.run";
+  if (py && w + 2 < words.size() && words[w + 1].text == "-m" && py_launchers.count(words[w + 2].text) &&
+      words[w + 2].text != "torch.distributed.run") {
+    err = "'python -m " + words[w + 2].text + "' is a launcher: run it as torchrun / accelerate launch / deepspeed";
+    return false;
+  }
+  std::string new_seg;
+  bool launcher = false;
   if (prog == "torchrun" || via_module) {
+    launcher = true;
     size_t i = w + (via_module ? 3 : 1);
     bool no_python = false;
     for (; i < words.size(); ++i) {
@@ -328,23 +514,67 @@ bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::st
       err = "torchrun without a training script";
       return false;
     }
-    if (no_python && (wrappers().count(base_name(words[i].text)) || base_name(words[i].text) == "torchrun")) {
-      err = "torchrun --no-python runs '" + words[i].text + "', a launcher/wrapper, not the GPU program";
+    std::string inserted;
+    size_t cut = words[i].begin;
+    if (no_python) {
+      if (wrappers().count(base_name(words[i].text)) || base_name(words[i].text) == "torchrun") {
+        err = "torchrun --no-python runs '" + words[i].text + "', a launcher/wrapper, not the GPU program";
+        return false;
+      }
+      std::vector<std::string> rep;
+      if (!check(words[i].text, rep)) return false;
+      inserted = rp_text + " " + (rep.empty() ? seg.substr(words[i].begin, words[i].end - words[i].begin) : join(rep));
+      cut = words[i].end;
+    } else {
+      // every rank runs under the launcher's own interpreter (its shebang; the python word itself
+      // for `python -m torch.distributed.run`), not whatever "python3" is first on PATH
+      const std::string rank_py = via_module ? words[w].text : launcher_python(first, look, run_cwd);
+      inserted = "--no-python " + rp_text + " " + shell_quote(rank_py) + " -u ";
+    }
+    new_seg = seg.substr(0, words[i].begin) + inserted + seg.substr(no_python ? cut : words[i].begin);
+  } else if (prog == "accelerate" || prog == "deepspeed") {
+    launcher = true;
+    size_t i = w + 1;
+    if (prog == "accelerate") {
+      if (i >= words.size() || words[i].text != "launch") {
+        err = "'accelerate' without 'launch' is not a training launch";
+        return false;
+      }
+      ++i;
+    }
+    size_t script_at = words.size();
+    for (; i < words.size(); ++i) {
+      const std::string& o = words[i].text;
+      if (o == "-m" || o == "--module" || o == "--no_python" || o == "--no-python") {
+        err = prog + " " + o + " cannot be combined with per-rank profiling";
+        return false;
+      }
+      if (!o.empty() && o[0] != '-' && o.size() > 3 && o.compare(o.size() - 3, 3, ".py") == 0) {
+        script_at = i;
+        break;
+      }
+    }
+    if (script_at >= words.size()) {
+      err = prog + " without a training script (*.py)";
       return false;
     }
-    insert_at = words[i].begin;
-    inserted = (no_python ? "" : "--no-python ") + rp_text + (no_python ? " " : " python3 -u ");
+    const std::string rank_py = launcher_python(first, look, run_cwd);
+    new_seg = seg.substr(0, words[script_at].begin) + "--no_python " + rp_text + " " + shell_quote(rank_py) + " -u " +
+              seg.substr(words[script_at].begin);
   } else if (wrappers().count(prog)) {
     err = "the job's last command runs '" + prog + "', a launcher/wrapper, not the GPU program";
     return false;
+  } else {
+    std::vector<std::string> rep;
+    if (!check(first, rep)) return false;
+    const std::string prog_text = rep.empty() ? seg.substr(words[w].begin, words[w].end - words[w].begin) : join(rep);
+    size_t from = words[w].begin;
+    if (w > 0 && words[w - 1].text == "exec") from = words[w - 1].begin;  // "exec prog" -> "exec rocprofv3 ... -- prog"
+    new_seg = seg.substr(0, from) + "exec " + rp_text + " " + prog_text + seg.substr(words[w].end);
   }
-  std::string new_seg = seg.substr(0, insert_at) + inserted + seg.substr(insert_at);
-  if (prog == "torchrun" || via_module) {  // the launcher itself replaces the shell too
+  if (launcher) {  // the launcher itself replaces the shell too
     size_t pw = words[w].begin;
     if (w == 0 || words[w - 1].text != "exec") new_seg = new_seg.substr(0, pw) + "exec " + new_seg.substr(pw);
-  } else if (w > 0 && words[w - 1].text == "exec") {  // "exec prog" -> "exec rocprofv3 ... -- prog"
-    size_t eb = words[w - 1].begin;
-    new_seg = seg.substr(0, eb) + inserted + seg.substr(insert_at);
   }
   out = {job[0], job[1], script.substr(0, s0) + new_seg + script.substr(s1)};
   return true;

@@ -2,6 +2,7 @@
 // DSTACK_ROCPROF_COUNTERS adds hardware counters (--pmc) in the same pass; the summaries are
 // appended to the job log when the job ends (SURVEY §2.I "rocprof counters in run logs").
 #pragma once
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -36,8 +37,27 @@ std::vector<std::string> rocprof_argv(const std::string& out_dir, const std::vec
 // Anything else -- a last command that is a wrapper (bash, sh, env, timeout, numactl, mpirun, ...),
 // a pipeline, a background job, a compound command, one reached through `||` -- is refused with a
 // reason, and the caller runs the job unprofiled.
+//
+// The program after "--" is also checked on disk (`look`): it must be an ELF binary, or a "#!"
+// script whose interpreter is Python (rewritten to `<interpreter> script args`, so the Python
+// binary -- checked to be ELF too -- is what rocprofv3 starts); a shell script, an `env bash`
+// shebang, a pyenv-style shim or a program that cannot be found is refused.  `accelerate launch`
+// and `deepspeed` are profiled per rank like torchrun (`--no_python rocprofv3 ... -- <python> -u
+// script.py`); uv/poetry/conda/pixi/pipenv/hatch runners and `python -m <launcher>` are refused.
+// A script with a heredoc (`<<`) is refused (its body lines are not commands).
+struct ProgramInfo {
+  bool found = false;
+  std::string path;  // resolved file
+  std::string head;  // its first bytes (up to 256)
+};
+// resolve a program word (a path, or a name looked up on PATH) against `cwd`
+using ProgramLookup = std::function<ProgramInfo(const std::string& prog, const std::string& cwd)>;
+// the runner's lookup: `path_env` (the job's PATH) and the real filesystem
+ProgramLookup fs_program_lookup(const std::string& path_env);
+
 bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::string>& rp,
-                  std::vector<std::string>& out, std::string& err);
+                  std::vector<std::string>& out, std::string& err, const ProgramLookup& look,
+                  const std::string& cwd);
 
 // one CSV record (quoted fields with commas / doubled quotes, as rocprofv3 writes kernel names)
 std::vector<std::string> parse_csv_record(const std::string& line);

@@ -2,6 +2,7 @@
 // host_info.go:13-75), authorized_keys editing (authorized_keys.go:16-163) and volume
 // preparation (docker.go prepareVolumes + backends/{aws,gcp}.go device resolution).
 #include <arpa/inet.h>
+#include <stdlib.h>
 #include <dirent.h>
 #include <ifaddrs.h>
 #include <pwd.h>
@@ -12,6 +13,7 @@
 
 #include <algorithm>
 #include <fstream>
+#include <iterator>
 #include <set>
 #include <sstream>
 
@@ -50,6 +52,19 @@ Json collect_host_info(const std::string& disk_path) {
     numa.set(std::to_string(g.index), g.numa_node);
   }
   h.set("gpu_vendor", gpus.empty() ? "" : "amd");
+  // the cloud bootstrap could not bring up the amdgpu driver (core/backends/base.py
+  // get_amd_driver_commands writes the marker): report why, so the server fails the host instead
+  // of registering it with zero GPUs
+  {
+    const char* m = getenv("DSTACK_AMDGPU_MARKER");
+    std::ifstream f(m && *m ? m : "/var/lib/dstack/amdgpu-install.failed");
+    if (f) {
+      std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+      if (text.size() > 2048) text.resize(2048);
+      while (!text.empty() && (text.back() == '\n' || text.back() == ' ')) text.pop_back();
+      if (!text.empty()) h.set("gpu_driver_error", text);
+    }
+  }
   h.set("gpu_count", (long long)gpus.size());
   if (!gpus.empty()) {
     h.set("gpu_name", gpus[0].name);

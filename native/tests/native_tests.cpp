@@ -156,48 +156,93 @@ int main() {
     const std::vector<std::string> rp = {"rocprofv3", "--kernel-trace", "--", };
     std::vector<std::string> out;
     std::string err;
-    auto sh = [](const std::string& script) { return std::vector<std::string>{"/bin/bash", "-c", script}; };
+    // a fake filesystem: names resolve on PATH=/usr/bin, paths against the command's directory
+    const std::string elf = std::string("\x7f") + "ELF\x02\x01";
+    std::map<std::string, std::string> fs = {
+        {"/usr/bin/python3", elf}, {"/usr/bin/python", elf}, {"/opt/venv/bin/python3", elf}, {"/w/app", elf},
+        {"/w/bin/app", elf}, {"/usr/bin/uv", elf},
+        {"/usr/bin/torchrun", "#!/opt/venv/bin/python3\n# -*- coding: utf-8 -*-\n"},
+        {"/usr/bin/accelerate", "#!/usr/bin/python3\n"}, {"/usr/bin/deepspeed", "#!/usr/bin/python3\n"},
+        {"/w/run.sh", "#!/bin/bash\nset -e\n"}, {"/w/train.py", "#!/usr/bin/env python3\nimport torch\n"},
+        {"/w/tool", "echo hi\n"}, {"/shim/python", "#!/usr/bin/env bash\nexec pyenv exec python \"$@\"\n"},
+        {"/w/shimmed.py", "#!/shim/python\n"}, {"/w/unbuf.py", "#!/usr/bin/env -S python3 -u\n"}};
+    ProgramLookup look = [&fs](const std::string& prog, const std::string& cwd) {
+      ProgramInfo pi;
+      std::string f = prog.find('/') == std::string::npos ? "/usr/bin/" + prog
+                      : prog[0] == '/'                     ? prog
+                                                           : cwd + "/" + prog;
+      for (size_t k; (k = f.find("/./")) != std::string::npos;) f.erase(k, 2);
+      auto it = fs.find(f);
+      if (it != fs.end()) pi = ProgramInfo{true, f, it->second};
+      return pi;
+    };
+    auto wrap = [&](const std::string& script, const std::string& cwd = "/w") {
+      err.clear();
+      return rocprof_wrap({"/bin/bash", "-c", script}, rp, out, err, look, cwd);
+    };
     // the server's form: commands joined by " && "; the last one is exec'd under the profiler
-    CHECK(rocprof_wrap(sh("pip install x && cd /w && python3 train.py --steps 5"), rp, out, err));
+    CHECK(wrap("pip install x && cd /w && python3 train.py --steps 5"));
     CHECK(out.size() == 3 && out[2] == "pip install x && cd /w && exec rocprofv3 --kernel-trace -- python3 train.py --steps 5");
     // env assignments stay in front of exec (the shell exports them to the program)
-    CHECK(rocprof_wrap(sh("cd /w && FOO=1 BAR='a b' python bench.py"), rp, out, err));
+    CHECK(wrap("cd /w && FOO=1 BAR='a b' python bench.py"));
     CHECK(out[2] == "cd /w && FOO=1 BAR='a b' exec rocprofv3 --kernel-trace -- python bench.py");
     // an explicit exec is reused; redirections and substitutions stay with the program's words
-    CHECK(rocprof_wrap(sh("exec ./app --n $(nproc) > log 2>&1"), rp, out, err));
+    CHECK(wrap("exec ./app --n $(nproc) > log 2>&1"));
     CHECK(out[2] == "exec rocprofv3 --kernel-trace -- ./app --n $(nproc) > log 2>&1");
-    // torchrun: the launcher stays outside, every rank is profiled
-    CHECK(rocprof_wrap(sh("torchrun --nnodes=$N --nproc-per-node $G --master-addr=$M bench.py --gpus 8"), rp, out,
-                       err));
+    // torchrun: the launcher stays outside, every rank is profiled under torchrun's own Python
+    CHECK(wrap("torchrun --nnodes=$N --nproc-per-node $G --master-addr=$M bench.py --gpus 8"));
     CHECK(out[2] == "exec torchrun --nnodes=$N --nproc-per-node $G --master-addr=$M --no-python rocprofv3 "
-                    "--kernel-trace -- python3 -u bench.py --gpus 8");
-    CHECK(rocprof_wrap(sh("python -m torch.distributed.run --standalone --nproc_per_node=2 t.py"), rp, out, err));
+                    "--kernel-trace -- /opt/venv/bin/python3 -u bench.py --gpus 8");
+    CHECK(wrap("python -m torch.distributed.run --standalone --nproc_per_node=2 t.py"));
     CHECK(out[2] == "exec python -m torch.distributed.run --standalone --nproc_per_node=2 --no-python rocprofv3 "
-                    "--kernel-trace -- python3 -u t.py");
-    CHECK(rocprof_wrap(sh("torchrun --no-python --nproc-per-node 2 ./app"), rp, out, err));
+                    "--kernel-trace -- python -u t.py");
+    CHECK(wrap("torchrun --no-python --nproc-per-node 2 ./app"));
     CHECK(out[2] == "exec torchrun --no-python --nproc-per-node 2 rocprofv3 --kernel-trace -- ./app");
-    // separators inside quotes, comments and a trailing ';' do not split the last command
-    CHECK(rocprof_wrap(sh("echo 'a && b'; python3 x.py \"--tag=c;d\" # run it\n"), rp, out, err));
+    // a #! Python script runs as <interpreter> script (env -S options kept); relative to the cd'd dir
+    CHECK(wrap("cd /w && ./train.py --lr 1", "/"));
+    CHECK(out[2] == "cd /w && exec rocprofv3 --kernel-trace -- python3 ./train.py --lr 1");
+    CHECK(wrap("./unbuf.py"));
+    CHECK(out[2] == "exec rocprofv3 --kernel-trace -- python3 -u ./unbuf.py");
+    CHECK(wrap("X=1 ./bin/app"));
+    CHECK(out[2] == "X=1 exec rocprofv3 --kernel-trace -- ./bin/app");
+    // accelerate / deepspeed: per rank, the launcher outside
+    CHECK(wrap("accelerate launch --num_processes 8 --mixed_precision bf16 train.py --lr 1"));
+    CHECK(out[2] == "exec accelerate launch --num_processes 8 --mixed_precision bf16 --no_python rocprofv3 "
+                    "--kernel-trace -- /usr/bin/python3 -u train.py --lr 1");
+    CHECK(wrap("deepspeed --num_gpus 8 train.py --deepspeed ds.json"));
+    CHECK(out[2] == "exec deepspeed --num_gpus 8 --no_python rocprofv3 --kernel-trace -- /usr/bin/python3 -u "
+                    "train.py --deepspeed ds.json");
+    // here-strings are one line; separators inside quotes, comments and a trailing ';' do not split
+    CHECK(wrap("python3 x.py <<< 'abc'"));
+    CHECK(wrap("echo 'a && b'; python3 x.py \"--tag=c;d\" # run it\n"));
     CHECK(out[2].find("exec rocprofv3 --kernel-trace -- python3 x.py") != std::string::npos);
     // an entrypoint argv without a shell
-    CHECK(rocprof_wrap({"python3", "serve.py"}, rp, out, err));
+    CHECK(rocprof_wrap({"python3", "serve.py"}, rp, out, err, look, "/w"));
     CHECK(out.size() == 5 && out[3] == "python3" && out[4] == "serve.py");
-    // refused: wrappers, shells, pipelines, background jobs, || branches, compound commands
+    CHECK(rocprof_wrap({"./train.py", "--x"}, rp, out, err, look, "/w"));
+    CHECK(out.size() == 6 && out[3] == "python3" && out[4] == "./train.py" && out[5] == "--x");
+    // refused: wrappers, shells, shell scripts, shims, env runners, pipelines, background jobs, ||
+    // branches, compound commands, heredocs, unresolvable or missing programs
     for (auto bad : {"cd /w && bash run.sh", "timeout 60 python3 x.py", "env A=1 python3 x.py", "python3 x.py | tee l",
                      "python3 x.py &", "false || python3 x.py", "for i in 1 2; do python3 x.py; done",
-                     "( python3 x.py )", "numactl -N0 python3 x.py", "mpirun -np 8 ./app", "echo 'unbalanced"}) {
-      err.clear();
-      CHECK(!rocprof_wrap(sh(bad), rp, out, err) && !err.empty());
+                     "( python3 x.py )", "numactl -N0 python3 x.py", "mpirun -np 8 ./app", "echo 'unbalanced",
+                     "./run.sh", "./tool", "./shimmed.py", "uv run python x.py", "poetry run python x.py",
+                     "conda run -n e python x.py", "pixi run python x.py", "python -m accelerate.commands.launch x.py",
+                     "python3 -m deepspeed x.py", "accelerate launch -m pkg.train", "deepspeed --no_python ./app",
+                     "python3 x.py <<EOF\nimport os\nEOF", "cd $HOME && ./app", "nosuch --flag",
+                     "torchrun --nproc-per-node 2 -m pkg.train", "torchrun --no-python ./run.sh"}) {
+      CHECK(!wrap(bad) && !err.empty());
     }
-    CHECK(!rocprof_wrap({"/usr/bin/env", "python3", "x.py"}, rp, out, err));
-    CHECK(!rocprof_wrap({"/bin/sh", "run.sh"}, rp, out, err));
-    CHECK(!rocprof_wrap(sh("torchrun --nproc-per-node 2 -m pkg.train"), rp, out, err));
+    CHECK(!rocprof_wrap({"/usr/bin/env", "python3", "x.py"}, rp, out, err, look, "/w"));
+    CHECK(!rocprof_wrap({"/bin/sh", "run.sh"}, rp, out, err, look, "/w"));
+    CHECK(!rocprof_wrap({"./run.sh"}, rp, out, err, look, "/w"));
     // whatever was accepted: the word after "--" is never a shell, env or launcher
-    for (auto ok : {"a && python3 t.py", "torchrun --nproc-per-node=8 t.py", "X=1 ./bin/app"}) {
-      CHECK(rocprof_wrap(sh(ok), rp, out, err));
+    for (auto ok : {"a && python3 t.py", "torchrun --nproc-per-node=8 t.py", "X=1 ./bin/app", "./train.py"}) {
+      CHECK(wrap(ok));
       size_t dd = out[2].find(" -- ");
       std::string after = out[2].substr(dd + 4, out[2].find(' ', dd + 4) - dd - 4);
-      CHECK(after != "bash" && after != "sh" && after != "env" && after != "torchrun" && after != "timeout");
+      CHECK(after != "bash" && after != "sh" && after != "env" && after != "torchrun" && after != "timeout" &&
+            after.find(".py") == std::string::npos && after.find(".sh") == std::string::npos);
     }
   });
 

@@ -47,8 +47,10 @@ struct JobResult {
 };
 
 // one job through a fresh executor: submit, code blob, run, wait; the last state and all job logs
-static JobResult run_job(const std::string& root, Json body, const std::string& blob = "") {
+static JobResult run_job(const std::string& root, Json body, const std::string& blob = "",
+                         const std::string& probe = "", Json* pull_out = nullptr) {
   RunnerOptions o;
+  o.probe_binary = probe;
   o.temp_dir = root + "/tmp";
   o.home_dir = root + "/home";
   o.working_dir = root + "/wd";
@@ -69,6 +71,7 @@ static JobResult run_job(const std::string& root, Json body, const std::string& 
     r.message = st.back()["termination_message"].str();
     r.exit_status = (int)st.back()["exit_status"].as_int(-1);
   }
+  if (pull_out) *pull_out = p;
   return r;
 }
 
@@ -302,6 +305,54 @@ int main() {
   });
 
   // ---- shim authorized_keys.go ------------------------------------------------------------------
+  run("executor: an RCCL pre-flight failure fails the job with the probe's message before the job runs", [] {
+    // stub dstack-probe: records its argv; node 1 reports a hung rank, node 0 a healthy ring
+    std::string root = tmpdir();
+    std::string probe = root + "/probe.sh";
+    write_file(probe,
+               "#!/bin/sh\necho \"$@\" > " + root + "/probe_args\nrank=0\nwhile [ $# -gt 0 ]; do "
+               "[ \"$1\" = --node-rank ] && rank=$2; shift; done\nif [ \"$rank\" = 1 ]; then echo 'rank 9: waiting'; "
+               "echo '{\"rccl_world\": 16, \"rccl_busbw_gb_s\": null, \"healthy\": false, \"message\": \"RCCL: rank 9 "
+               "timed out\"}'; exit 1; fi\necho '{\"rccl_world\": 16, \"rccl_busbw_gb_s\": 311.5, \"healthy\": true, "
+               "\"message\": \"\"}'\n",
+               0755);
+    auto body = [&](const std::string& rank) {
+      Json b = job({"/bin/sh", "-c", "echo trained"});
+      Json js = b["job_spec"];
+      Json env = Json::object();
+      env.set("DSTACK_RCCL_PREFLIGHT", std::string("force"));
+      env.set("DSTACK_NODE_RANK", rank);
+      env.set("DSTACK_NODES_NUM", std::string("2"));
+      env.set("DSTACK_GPUS_PER_NODE", std::string("8"));
+      env.set("DSTACK_RCCL_PREFLIGHT_TIMEOUT", std::string("60"));
+      js.set("env", env);
+      b.set("job_spec", js);
+      return b;
+    };
+    Json pull;
+    JobResult r = run_job(root + "/n1", body("1"), "", probe, &pull);
+    CHECK(r.state == "failed" && r.reason == "executor_error");
+    CHECK(r.message.find("RCCL pre-flight failed (exit 1): RCCL: rank 9 timed out") == 0);
+    CHECK(r.logs.find("trained") == std::string::npos);  // the job never started
+    CHECK(pull["rccl_preflight"]["healthy"].as_bool(true) == false);
+    // the probe's own deadline ends before the outer timeout (60 s - 15 s - 5 s collect margin)
+    std::string args;
+    CHECK(read_file(root + "/probe_args", args) && args.find("--timeout-ms 40000") != std::string::npos);
+    r = run_job(root + "/n0", body("0"), "", probe, &pull);
+    CHECK(r.state == "done" && r.logs.find("trained") != std::string::npos);
+    CHECK(pull["rccl_preflight"]["rccl_busbw_gb_s"].as_double(0) > 311.0);
+  });
+
+  run("host_info: a failed amdgpu bootstrap (marker file) is reported as gpu_driver_error", [] {
+    std::string root = tmpdir();
+    setenv("DSTACK_AMDGPU_MARKER", (root + "/failed").c_str(), 1);
+    CHECK(!collect_host_info(root).has("gpu_driver_error"));
+    write_file(root + "/failed", "amdgpu 7.0 driver install failed on ubuntu/noble kernel 6.8.0: /dev/kfd missing\n");
+    Json h = collect_host_info(root);
+    CHECK(h["gpu_driver_error"].str() == "amdgpu 7.0 driver install failed on ubuntu/noble kernel 6.8.0: /dev/kfd missing");
+    unsetenv("DSTACK_AMDGPU_MARKER");
+  });
+
   run("authorized_keys: fingerprints and key identity", [] {
     // a real ed25519 public key (generated for this test; the private half was discarded)
     const std::string k1 = "ssh-ed25519 AAAAC3NzaC1lZDI1NTE5AAAAIITSR+i4RoOxF46hsNGCw8yd1/HI82K3pA/ZpvMgvZI/ one@host";

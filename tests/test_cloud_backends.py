@@ -934,11 +934,32 @@ def test_cloud_init_installs_the_amd_driver_only_when_missing(tmp_path):
     (bin_dir / "curl").write_text(f"#!/bin/sh\ntouch {tmp_path}/curl-called\nexit 1\n")
     for f in bin_dir.iterdir():
         f.chmod(0o755)
-    script = get_amd_driver_commands()[0].replace("/var/log/dstack-amdgpu.log", str(tmp_path / "log"))
+    marker, log = tmp_path / "failed", tmp_path / "log"
+    (tmp_path / "os-release").write_text('NAME="Ubuntu"\nVERSION_CODENAME=noble\n')
+    script = get_amd_driver_commands(marker=str(marker), log=str(log), os_release=str(tmp_path / "os-release"))[0]
+    # stand-ins for every tool the installer path calls: no network, no real package manager
+    (bin_dir / "curl").write_text(f"#!/bin/sh\necho \"$@\" >> {tmp_path}/curl-called\nexit 1\n")
+    (bin_dir / "apt-get").write_text(f"#!/bin/sh\necho \"$@\" >> {tmp_path}/apt-called\n")
+    (bin_dir / "uname").write_text("#!/bin/sh\necho 6.8.0-1-test\n")
+    (bin_dir / "modprobe").write_text("#!/bin/sh\nexit 1\n")
+    for f in bin_dir.iterdir():
+        f.chmod(0o755)
     env = {"PATH": f"{bin_dir}:/usr/bin:/bin"}
     assert subprocess.run(["bash", "-c", script], env=env).returncode == 0
-    assert not (tmp_path / "curl-called").exists()
-    # an MI355X (1002:75a3) without /dev/kfd -> the installer path runs (the stand-in curl fails it)
+    assert not (tmp_path / "curl-called").exists() and not marker.exists()
+    if os.path.exists("/dev/kfd"):
+        return  # a GPU box with the driver loaded: the installer path never runs
+    # an MI355X (1002:75a3) without /dev/kfd: the ROCm 7 driver for this Ubuntu's codename, kernel
+    # headers first; the (stand-in) download fails, so the marker carries the reason
     (bin_dir / "lspci").write_text("#!/bin/sh\necho '05:00.0 Processing accelerators [1200]: AMD [1002:75a3]'\n")
     subprocess.run(["bash", "-c", script], env=env)
-    assert (tmp_path / "curl-called").exists() or os.path.exists("/dev/kfd")
+    url = (tmp_path / "curl-called").read_text()
+    assert "amdgpu-install/7.0/ubuntu/noble/amdgpu-install_7.0." in url, url
+    assert "linux-headers-6.8.0-1-test" in (tmp_path / "apt-called").read_text()
+    text = marker.read_text()
+    assert "amdgpu 7.0 driver install failed on ubuntu/noble kernel 6.8.0-1-test: /dev/kfd missing" in text
+    # an MI210 (1002:740f): the 6.4 driver
+    (tmp_path / "curl-called").unlink()
+    (bin_dir / "lspci").write_text("#!/bin/sh\necho '05:00.0 Processing accelerators [1200]: AMD [1002:740f]'\n")
+    subprocess.run(["bash", "-c", script], env=env)
+    assert "amdgpu-install/6.4/ubuntu/noble/amdgpu-install_6.4." in (tmp_path / "curl-called").read_text()

@@ -60,8 +60,11 @@ def _task_yaml(nodes: int, gpus_per_node: int, port: int) -> str:
     conf["resources"]["gpu"] = f"MI355X:{gpus_per_node}"
     conf["resources"].pop("shm_size", None)
     conf.pop("image", None)  # process driver: the host environment is the job's environment
-    conf["env"] = list(conf.get("env", [])) + [f"MASTER_PORT={port}", "OMP_NUM_THREADS=1",
-                                               "PYTHONPATH=" + REPO]
+    # no RCCL on a CPU box: the example's RCCL pre-flight (DSTACK_RCCL_PREFLIGHT=1) is the one
+    # setting dropped here (it is exercised by the runner tests with a stub probe)
+    env = [e for e in conf.get("env", []) if not e.startswith("DSTACK_RCCL_PREFLIGHT=")]
+    assert len(env) == len(conf.get("env", [])) - 1, "the example enables the RCCL pre-flight"
+    conf["env"] = env + [f"MASTER_PORT={port}", "OMP_NUM_THREADS=1", "PYTHONPATH=" + REPO]
     return yaml.safe_dump(conf, sort_keys=False)
 
 

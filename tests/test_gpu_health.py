@@ -311,3 +311,34 @@ def test_gpu_discovery_paths_agree_with_hip_order():
         pr = torch.cuda.get_device_properties(i)
         if hasattr(pr, "pci_bus_id"):
             assert int(smi[i]["bdf"].split(":")[1], 16) == pr.pci_bus_id, (i, smi[i]["bdf"], pr.pci_bus_id)
+
+
+def test_failed_driver_bootstrap_fails_provisioning_with_its_reason(db):
+    """A GPU offer whose host came up without /dev/kfd (the cloud bootstrap's amdgpu install failed,
+    core/backends/base.py marker -> shim host_info ``gpu_driver_error``) is not registered as an
+    idle host with zero GPUs: provisioning fails with the bootstrap's reason."""
+    msg = "amdgpu 7.0 driver install failed on ubuntu/noble kernel 6.8.0-45-generic: /dev/kfd missing"
+
+    class NoDriverShim(FakeShim):
+        def host_info(self):
+            return {"gpu_count": 0, "gpu_vendor": "", "gpu_driver_error": msg}
+
+    with session_scope() as s:
+        iid = _instance(s, status=InstanceStatus.PROVISIONING)
+    with mock.patch.object(pi, "get_shim_client", return_value=NoDriverShim(None)), session_scope() as s:
+        inst = s.get(InstanceModel, iid)
+        pi._check_provisioning(s, inst)
+        assert inst.status == InstanceStatus.TERMINATING.value
+        assert inst.termination_reason == f"GPU driver: {msg}" and inst.health_status == inst.termination_reason
+
+    class DriverOkShim(FakeShim):
+        def host_info(self):  # a marker left from an earlier boot does not matter once GPUs are up
+            return {"gpu_count": 8, "gpu_vendor": "amd", "gpu_driver_error": msg}
+
+    with session_scope() as s:
+        iid = _instance(s, status=InstanceStatus.PROVISIONING)
+    with mock.patch.object(pi, "get_shim_client", return_value=DriverOkShim(_doc(GOOD, time.time()))), \
+            session_scope() as s:
+        inst = s.get(InstanceModel, iid)
+        pi._check_provisioning(s, inst)
+        assert inst.status == InstanceStatus.IDLE.value

@@ -12,6 +12,7 @@ creation failure; non-zero exit; graceful stop; service replica registration."""
 from __future__ import annotations
 
 import itertools
+import json
 from typing import Dict, List, Optional
 from unittest import mock
 
@@ -614,3 +615,72 @@ def test_host_lost_while_pulling_interrupts_job(db):
             (job,) = _jobs(s, rid)
             assert job.status in (JobStatus.TERMINATING.value, JobStatus.FAILED.value)
             assert job.termination_reason == JobTerminationReason.INTERRUPTED_BY_NO_CAPACITY.value
+
+
+class _PreflightRunner(FakeRunner):
+    """Runner of a 2-node job with DSTACK_RCCL_PREFLIGHT: the worker's pre-flight fails (a rank of the
+    all-reduce timed out) before the job starts, the master's passes and keeps the job running."""
+
+    def pull(self, timestamp: int):
+        node = self.submitted["job_spec"].job_num
+        if node == 1:
+            doc = {"rccl_world": 16, "rccl_busbw_gb_s": None, "healthy": False, "message": "RCCL: rank 9 timed out"}
+            st = {"state": "failed", "timestamp": 2, "termination_reason": "executor_error",
+                  "termination_message": "RCCL pre-flight failed (exit 1): RCCL: rank 9 timed out"}
+            return {"job_states": [st], "job_logs": [], "runner_logs": [], "last_updated": 2000,
+                    "rccl_preflight": doc}
+        doc = {"rccl_world": 16, "rccl_busbw_gb_s": 311.5, "healthy": True, "message": ""}
+        st = {"state": "terminated", "timestamp": 3, "termination_reason": "terminated_by_user"} if self.stopped \
+            else {"state": "running", "timestamp": 1}
+        return {"job_states": [st], "job_logs": [], "runner_logs": [], "last_updated": 1000, "rccl_preflight": doc}
+
+
+class _PreflightAgents(Agents):
+    def runner(self, jpd, jrd=None, key=None, *a, **kw):
+        if jpd.hostname not in self.runners:
+            self.runners[jpd.hostname] = _PreflightRunner()
+        return self.runners[jpd.hostname]
+
+
+def test_rccl_preflight_failure_on_one_node_fails_the_replica(db):
+    """A failed RCCL pre-flight on node 1 of a 2-node task fails that job with the probe's message,
+    the run fails (job_failed) and terminates the master's job too; the failing host is marked
+    unhealthy (no new jobs land on it) and the passing host records its bus bandwidth."""
+    agents = _PreflightAgents()
+    with session_scope() as s:
+        ids = [_remote_instance(s, "node-p0")[0], _remote_instance(s, "node-p1")[0]]
+        rid = _submit(s, {"type": "task", "nodes": 2, "commands": ["torchrun train.py"],
+                          "resources": {"gpu": "MI355X:8"}, "env": {"DSTACK_RCCL_PREFLIGHT": "1"}})
+    with agents.patch():
+        status, jobs = _run_to_end(rid, max_ticks=6)
+        # the master's job is stopped through its runner, then removed after the grace delay
+        later = get_current_datetime() + pr.RETRY_DELAY * 4
+        with mock.patch.object(ptj, "get_current_datetime", return_value=later):
+            status, jobs = _run_to_end(rid, max_ticks=3)
+    assert status == RunStatus.FAILED.value, (status, jobs)
+    with session_scope() as s:
+        run = s.get(RunModel, rid)
+        assert run.termination_reason == "job_failed"
+        assert all(r.stopped for r in agents.runners.values() if r.submitted["job_spec"].job_num == 0)
+        by_num = {j.job_num: j for j in _jobs(s, rid)}
+        worker, master = by_num[1], by_num[0]
+        assert worker.status == JobStatus.FAILED.value
+        assert worker.termination_reason == JobTerminationReason.EXECUTOR_ERROR.value
+        assert "rank 9 timed out" in (worker.termination_reason_message or "")
+        assert JobStatus(master.status).is_finished() and master.status != JobStatus.DONE.value
+        insts = [s.get(InstanceModel, i) for i in ids]
+        health = {i.name: json.loads(i.health_data) for i in insts}
+        bad = [i for i in insts if not health[i.name]["healthy"]]
+        good = [i for i in insts if health[i.name]["healthy"]]
+        assert len(bad) == 1 and len(good) == 1
+        assert "rank 9 timed out" in health[bad[0].name]["message"] and "RCCL pre-flight" in bad[0].health_status
+        assert health[good[0].name]["rccl_busbw_gb_s"] == 311.5 and good[0].health_status is None
+        # the scheduler no longer offers the failed host
+        from dstack_amd.core.models.profiles import Profile
+        from dstack_amd.core.models.resources import ResourcesSpec
+        from dstack_amd.core.models.runs import Requirements
+
+        picked = pools_services.filter_pool_instances(insts, Profile(name="p"), Requirements(resources=ResourcesSpec()))
+        assert [i.name for i, _ in picked] == [good[0].name]
+    # the job spec carried the opt-in to the runners
+    assert all(r.submitted["job_spec"].env.get("DSTACK_RCCL_PREFLIGHT") == "1" for r in agents.runners.values())

@@ -32,14 +32,19 @@ def main():
     # hardware metrics: the server polls the runner's /api/metrics (cgroup + amdsmi) every 2 s here
     # E2E_PROBE=1: the shim hands dstack-probe to the runner, which runs the HIP health probes
     # (HBM, bf16/fp8 MFMA) before the job; the result becomes the instance's health
+    # E2E_RCCL_PREFLIGHT=1: the example's RCCL pre-flight, forced for this 1-GPU job (a world of one
+    # rank: bootstrap + communicator + an in-place all-reduce, no link bandwidth)
     probe = os.environ.get("E2E_PROBE") == "1"
+    preflight = os.environ.get("E2E_RCCL_PREFLIGHT") == "1"
     srv_env = {"DSTACK_SERVER_METRICS_COLLECT_INTERVAL": "2"}
-    if probe:
+    if probe or preflight:
         srv_env["DSTACK_LOCAL_GPU_PROBE"] = "1"
+    job_env = {"DSTACK_GPU_PROBE": "1"} if probe else {}
+    if preflight:
+        job_env["DSTACK_RCCL_PREFLIGHT"] = "force"
     with ServerProcess(env=srv_env) as srv:
         client = srv.client()
-        conf = Task(name="llama3-8b-e2e", commands=[cmd], resources=Resources(gpu=GPU(count=1)),
-                    env={"DSTACK_GPU_PROBE": "1"} if probe else {})
+        conf = Task(name="llama3-8b-e2e", commands=[cmd], resources=Resources(gpu=GPU(count=1)), env=job_env)
         t0 = time.time()
         run = client.runs.submit(conf)
         deadline = t0 + float(os.environ.get("E2E_TIMEOUT", "600"))
@@ -76,7 +81,9 @@ def main():
             "hw_metrics_samples": len(samples),
             "hw_metrics_peak": {k: max(x.get(k, 0) for x in samples) for k in (samples[-1] if samples else {})},
         }
-        if probe:
+        if preflight:
+            out["rccl_preflight_log"] = [ln for ln in logs.splitlines() if "RCCL pre-flight" in ln][:1]
+        if probe or preflight:
             insts = client.api.instances.list(["main"])
             out["instance_health"] = [i.health for i in insts]
             out["probe_log"] = [ln for ln in logs.splitlines() if "GPU health probe" in ln][:1]
