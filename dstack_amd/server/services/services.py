@@ -224,12 +224,17 @@ def service_metric_value(s: Session, run: RunModel, conf: ServiceConfiguration) 
         return None
     if conf.scaling.metric == "rps":
         return get_request_stats().rps(run.id)
-    # gpu_util: mean of the latest amdsmi util samples of running jobs (last 2 minutes)
+    # gpu_util: the measured load -- each running job's latest amdsmi util sample of the last
+    # 2 minutes (mean over its GPUs), summed and spread over every running job.  A job without a
+    # recent sample (a replica that just started) counts as idle, so the scaler sizes for the load
+    # it can see: replicas = ceil(sum(util) / target).  No sample at all: no signal, no scaling.
     since = int((time.time() - 120) * 1e6)
     utils: List[float] = []
+    running = 0
     for j in run.jobs:
         if j.status != "running":
             continue
+        running += 1
         pt = s.execute(select(JobMetricsPoint).where(JobMetricsPoint.job_id == j.id,
                                                      JobMetricsPoint.timestamp_micro >= since)
                        .order_by(JobMetricsPoint.timestamp_micro.desc())).scalars().first()
@@ -237,7 +242,7 @@ def service_metric_value(s: Session, run: RunModel, conf: ServiceConfiguration) 
             vals = json.loads(pt.gpus_util_percent or "[]")
             if vals:
                 utils.append(sum(vals) / len(vals))
-    return sum(utils) / len(utils) if utils else None
+    return sum(utils) / running if utils else None
 
 
 def register_replica(s: Session, run: RunModel, job: JobModel):

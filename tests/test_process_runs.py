@@ -183,3 +183,100 @@ def test_terminating_run_terminates_its_jobs_then_finishes(db):
         j.status = JobStatus.TERMINATED.value
     st, reason, _ = _process(rid)
     assert st == RunStatus.TERMINATED and reason == RunTerminationReason.STOPPED_BY_USER.value
+
+
+# ---- gpu_util autoscaling through the DB ---------------------------------------------------------
+def _gpu_util_service():
+    return {"type": "service", "commands": ["serve"], "port": 8000, "replicas": "1..4",
+            "scaling": {"metric": "gpu_util", "target": 70, "scale_up_delay": 60, "scale_down_delay": 300}}
+
+
+def _util_samples(run_id, pct_by_replica, age_s: float = 0.0):
+    """One amdsmi sample (8 GPUs at ``pct``) per running replica, ``age_s`` seconds old (wall clock:
+    the metric reads the last 120 s of JobMetricsPoint rows, as process_metrics writes them)."""
+    import json
+    import time
+    import uuid
+
+    from dstack_amd.server.models import JobMetricsPoint
+
+    ts = int((time.time() - age_s) * 1e6)
+    with session_scope() as s:
+        latest = {}
+        for j in s.query(JobModel).filter_by(run_id=run_id):
+            if j.replica_num not in latest or j.submission_num > latest[j.replica_num].submission_num:
+                latest[j.replica_num] = j
+        for r, pct in pct_by_replica.items():
+            s.add(JobMetricsPoint(id=uuid.uuid4(), job_id=latest[r].id, timestamp_micro=ts, cpu_usage_micro=0,
+                                  memory_usage_bytes=0, memory_working_set_bytes=0,
+                                  gpus_memory_usage_bytes=json.dumps([0] * 8), gpus_util_percent=json.dumps([pct] * 8)))
+
+
+def _process_scaling(run_id, at):
+    from dstack_amd.server.services import services as services_services
+
+    with mock.patch.object(services_services, "get_current_datetime", return_value=at):
+        return _process(run_id, at)
+
+
+def _active_replicas(run_id) -> List[int]:
+    from dstack_amd.server.services import jobs as jobs_services
+
+    with session_scope() as s:
+        run = s.get(RunModel, run_id)
+        groups = jobs_services.group_jobs_by_replica_latest(run.jobs)
+        return sorted(r for r, js in groups.items()
+                      if any(not JobStatus(j.status).is_finished() and j.status != JobStatus.TERMINATING.value
+                             for j in js))
+
+
+def _set_latest_running(run_id):
+    with session_scope() as s:
+        for j in s.query(JobModel).filter_by(run_id=run_id):
+            if j.status == JobStatus.SUBMITTED.value:
+                j.status = JobStatus.RUNNING.value
+                j.job_provisioning_data = JPD
+
+
+def test_gpu_util_autoscaling_through_job_metrics(db):
+    """``scaling: {metric: gpu_util, target: 70}`` end to end at the reconciler level (reference
+    services/services/autoscalers.py:75-108 for the RPS form; gpu_util is this build's amdsmi
+    metric): JobMetricsPoint rows -> service_metric_value (mean util of the running replicas over
+    the last 120 s) -> GPUUtilAutoscaler -> scale_run_replicas.  2 replicas at 95 % -> 3 once the
+    scale-up delay has passed; at 20 % -> 1, not before the scale-down delay."""
+    rid = _run(_gpu_util_service(), RunStatus.RUNNING)
+    with session_scope() as s:
+        runs_services.scale_run_replicas(s, s.get(RunModel, rid), 1)  # 2 replicas
+    _set_latest_running(rid)
+    t0 = get_current_datetime()
+    assert _active_replicas(rid) == [0, 1]
+    # no samples at all: nothing to scale on
+    _process_scaling(rid, t0 + timedelta(minutes=2))
+    assert _active_replicas(rid) == [0, 1]
+    # a stale sample (older than 120 s) is ignored
+    _util_samples(rid, {0: 95.0, 1: 95.0}, age_s=300)
+    _process_scaling(rid, t0 + timedelta(minutes=2))
+    assert _active_replicas(rid) == [0, 1]
+    # hot: ceil(2 * 95 / 70) = 3, but not within the scale-up delay of the last replica start
+    _util_samples(rid, {0: 95.0, 1: 95.0})
+    _process_scaling(rid, t0 + timedelta(seconds=30))
+    assert _active_replicas(rid) == [0, 1]
+    _process_scaling(rid, t0 + timedelta(minutes=2))
+    assert _active_replicas(rid) == [0, 1, 2]
+    with session_scope() as s:
+        assert s.get(RunModel, rid).desired_replica_count == 3
+    _set_latest_running(rid)
+    # one replica without samples does not drag the mean: 0 and 1 at 95 %, 2 unsampled -> stays
+    _process_scaling(rid, t0 + timedelta(minutes=3))
+    assert _active_replicas(rid) == [0, 1, 2]
+    # cold: ceil(3 * 20 / 70) = 1; the scale-down delay (300 s) runs from the newest replica start
+    _util_samples(rid, {0: 20.0, 1: 20.0, 2: 20.0})
+    _process_scaling(rid, get_current_datetime() + timedelta(minutes=2))
+    assert _active_replicas(rid) == [0, 1, 2]
+    _process_scaling(rid, get_current_datetime() + timedelta(minutes=10))
+    assert _active_replicas(rid) == [0]
+    with session_scope() as s:
+        run = s.get(RunModel, rid)
+        stopped = [j for j in run.jobs if j.replica_num in (1, 2)]
+        assert stopped and all(j.termination_reason == JobTerminationReason.SCALED_DOWN.value for j in stopped)
+        assert run.desired_replica_count == 1 and RunStatus(run.status) == RunStatus.RUNNING
