@@ -7,8 +7,9 @@ MI355X-first layout choices:
 * activations stay in [B, S, heads, D] — the HIP flash-attention kernel reads q/k/v as strided views
   of the fused qkv output, no transposes;
 * every elementwise/normalisation step is a fused HIP kernel (``dstack_amd.ops``): residual-add is
-  folded into the next RMSNorm, RoPE is one pass over qkv, SwiGLU one pass over the gate/up output,
-  the loss never materialises fp32 logits.
+  folded into the next RMSNorm, RoPE is one pass over qkv, SwiGLU forward/backward run in the
+  epilogues of the in-tree gate/up and down-projection GEMMs (``ops.swiglu_mlp``), the loss never
+  materialises fp32 logits.
 
 Reference parity: the reference orchestrator ships no model code; its Llama workloads are user
 containers (``examples/fine-tuning/pytorch-distributed/train.dstack.yml``,
@@ -100,8 +101,7 @@ class DecoderLayer(nn.Module):
         o = ops.attention(qkv, cfg.n_heads, cfg.n_kv_heads, causal=True)
         attn_out = ops.linear(o, self.wo)
         x, h = ops.add_rms_norm(x, attn_out, self.ffn_norm, cfg.norm_eps)
-        a = ops.swiglu(ops.linear(h, self.wgu))
-        return x, ops.linear(a, self.wdown)
+        return x, ops.swiglu_mlp(h, self.wgu, self.wdown)
 
 
 class Llama(nn.Module):

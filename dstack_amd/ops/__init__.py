@@ -15,6 +15,7 @@ from dstack_amd.ops.functional import (  # noqa: F401
     rms_norm,
     rope,
     swiglu,
+    swiglu_mlp,
     weight_grad,
 )
 from dstack_amd.ops import _ext  # noqa: F401

@@ -486,7 +486,14 @@ bool nt_shape_ok(int M, int N, int K) {
   return M > 0 && N > 0 && K > 0 && M % NT_BM == 0 && N % NT_BN == 0 && K % (2 * NT_BK) == 0;
 }
 
-int nt_group(int ntm) { return ntm >= 8 ? 8 : ntm; }
+// tile-order group height: an XCD's 32 concurrent tiles are a group x (32 / group) block; taller
+// blocks suit wide outputs, wider blocks tall ones (tools/diag/gemm_group_sweep.sh,
+// profiles/gemm_nt_group_r7d.txt: group 8 for the 8192 x 28672 gate/up GEMM, 4 for the 28672 x 4096
+// weight gradient)
+int nt_group(int ntm, int ntn) {
+  const int g = ntm > 2 * ntn ? 4 : 8;
+  return ntm >= g ? g : ntm;
+}
 
 int nt_cus() {
   static int cus[64] = {0};
@@ -545,7 +552,7 @@ extern "C" hipError_t dsa_gemm_nt(const void* A, const void* B, void* C, int M, 
   a.ntn = N / NT_BN;
   a.nstride = NT_BN;
   a.bsplit = 128;
-  a.group = nt_group(M / NT_BM);
+  a.group = nt_group(M / NT_BM, N / NT_BN);
   const int tiles = (M / NT_BM) * (N / NT_BN);
   return accumulate ? nt_launch<EPI_ACC>(a, tiles, st) : nt_launch<EPI_STORE>(a, tiles, st);
 }
@@ -574,7 +581,7 @@ extern "C" hipError_t dsa_gemm_nt_swiglu(const void* X, const void* W, void* gu,
   a.ntn = F / 128;
   a.nstride = 128;
   a.bsplit = F;
-  a.group = nt_group(T / NT_BM);
+  a.group = nt_group(T / NT_BM, F / 128);
   return nt_launch<EPI_SWIGLU>(a, (T / NT_BM) * (F / 128), st);
 }
 
@@ -603,6 +610,6 @@ extern "C" hipError_t dsa_gemm_nt_swiglu_bwd(const void* dY, const void* WdT, co
   a.ntn = F / NT_BN;
   a.nstride = NT_BN;
   a.bsplit = 128;
-  a.group = nt_group(T / NT_BM);
+  a.group = nt_group(T / NT_BM, F / NT_BN);
   return nt_launch<EPI_SWIGLU_BWD>(a, (T / NT_BM) * (F / NT_BN), st);
 }

@@ -130,6 +130,83 @@ def swiglu(gu: torch.Tensor) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------------------------
+# The SwiGLU MLP with both SwiGLU passes fused into the in-tree GEMM (csrc/gemm_nt.hip)
+# ----------------------------------------------------------------------------------------------
+class _SwiGLUMLP(torch.autograd.Function):
+    """y = (silu(h Wg^T) * (h Wu^T)) Wdown^T with W_gu = [Wg; Wu].
+
+    Forward: one gfx950 GEMM writes gu = h W_gu^T and, from the same tile, a = silu(g) * u and
+    a^T (``gemm_nt_swiglu``: no separate SwiGLU pass re-reading gu); y = a Wdown^T (library GEMM).
+    Backward: the down projection's input gradient da = dy Wdown is computed by the in-tree GEMM
+    with the SwiGLU backward in its epilogue (``gemm_nt_swiglu_bwd``: dgu and dgu^T from the tile,
+    da never reaches HBM); dx = dgu W_gu and the weight gradients (written into the optimizer's
+    flat buffer through ``_dsa_grad_sink``) as in ``_Linear``."""
+
+    @staticmethod
+    def forward(ctx, h, wgu, wdown):
+        C = _ext.require()
+        h2 = _2d(h)
+        gu, a, aT = C.gemm_nt_swiglu(h2, wgu)
+        y = a @ wdown.t()
+        ctx.save_for_backward(h2, gu, aT, wgu, wdown)
+        ctx.hshape = h.shape
+        return y.view(*h.shape[:-1], wdown.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        h2, gu, aT, wgu, wdown = ctx.saved_tensors
+        dy2 = _2d(dy.contiguous())
+        # down projection weight gradient dW = dy^T a  (a^T already written by the forward)
+        gwd = None
+        a_op, b_op = wgrad_operands(dy2, None, xT=aT)
+        sink = getattr(wdown, "_dsa_grad_sink", None)
+        if sink is not None:
+            sink(wdown, a_op, b_op)
+        else:
+            gwd = a_op @ b_op
+        # da = dy Wdown with the SwiGLU backward fused: dgu, dgu^T
+        wdT = _transposed_weight(wdown)
+        if wdT is None:
+            wdT = wdown.t().contiguous()
+        dgu, dguT = C.gemm_nt_swiglu_bwd(dy2, wdT, gu)
+        # dx = dgu W_gu
+        wguT = _transposed_weight(wgu)
+        dx = dgu @ (wguT.t() if wguT is not None else wgu)
+        # gate/up weight gradient dW_gu = dgu^T h  (dgu^T from the fused epilogue)
+        ggu = None
+        a_op, b_op = wgrad_operands(dgu, h2, gT=dguT)
+        sink = getattr(wgu, "_dsa_grad_sink", None)
+        if sink is not None:
+            sink(wgu, a_op, b_op)
+        else:
+            ggu = a_op @ b_op
+        return dx.view(ctx.hshape), ggu, gwd
+
+
+def _mlp_fused_ok(h: torch.Tensor, wgu: torch.Tensor, wdown: torch.Tensor) -> bool:
+    if os.environ.get("DSTACK_AMD_MLP_FUSED", "1") == "0" or _wgrad_mode() != "auto":
+        return False
+    if h.dtype != torch.bfloat16 or wgu.dtype != torch.bfloat16 or wdown.dtype != torch.bfloat16:
+        return False
+    C = _ext.require()
+    T, D = h.numel() // h.shape[-1], h.shape[-1]
+    F = wgu.shape[0] // 2
+    return (tuple(wgu.shape) == (2 * F, D) and tuple(wdown.shape) == (D, F) and wgu.is_contiguous()
+            and wdown.is_contiguous() and C.gemm_nt_swiglu_supported(T, F, D)
+            and C.gemm_nt_swiglu_bwd_supported(T, F, D))
+
+
+def swiglu_mlp(h: torch.Tensor, wgu: torch.Tensor, wdown: torch.Tensor) -> torch.Tensor:
+    """The Llama MLP: ``linear(swiglu(linear(h, wgu)), wdown)``.  On the HIP path both SwiGLU
+    passes live in the epilogues of the in-tree GEMM (``_SwiGLUMLP``); ``DSTACK_AMD_MLP_FUSED=0``
+    (or an untiled shape) keeps the separate kernels."""
+    if _ext.use_hip(h) and _mlp_fused_ok(h, wgu, wdown):
+        return _SwiGLUMLP.apply(h.contiguous(), wgu, wdown)
+    return linear(swiglu(linear(h, wgu)), wdown)
+
+
+# ----------------------------------------------------------------------------------------------
 # RoPE applied to the q and k heads of a fused qkv activation [B, S, (H + 2*KV) * D]
 # ----------------------------------------------------------------------------------------------
 class _RopeQKV(torch.autograd.Function):

@@ -17,6 +17,7 @@ from sqlalchemy import (
     DateTime,
     Float,
     ForeignKey,
+    Index,
     Integer,
     LargeBinary,
     String,
@@ -381,6 +382,8 @@ class PlacementGroupModel(Base):
 
 class JobMetricsPoint(Base):
     __tablename__ = "job_metrics_points"
+    # the newest samples of a job (gpu_util autoscaler, `dstack stats`); migration 6 for older DBs
+    __table_args__ = (Index("ix_job_metrics_points_job_ts", "job_id", "timestamp_micro"),)
     id: Mapped[uuid.UUID] = _id()
     job_id: Mapped[uuid.UUID] = mapped_column(UUIDStr, ForeignKey("jobs.id", ondelete="CASCADE"), index=True)
     timestamp_micro: Mapped[int] = mapped_column(BigInteger)

@@ -536,3 +536,86 @@ def test_linear_dgrad_uses_transposed_weight_per_generation(gpu, monkeypatch):
     monkeypatch.setenv("DSTACK_AMD_DGRAD_WT", "0")
     gx_nn = torch.autograd.grad(ops.linear(x, w), x, g)[0]
     _close(x.grad, gx_nn, 0.05, 1e-2)
+
+
+# ---- in-tree NT GEMM (csrc/gemm_nt.hip) and its SwiGLU epilogues ---------------------------------
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (2304, 9472, 128), (4096, 4352, 384)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_nt_matches_fp32(gpu, M, N, K, accumulate):
+    """C (+)= A B^T against an fp32 matmul; (2304, 9472) and (4096, 4352) have more tiles than CUs
+    (persistent workgroups, XCD slices of unequal size)."""
+    C = _ext.require()
+    a, b = _rand(M, K, device=gpu), _rand(N, K, device=gpu, seed=1)
+    out = _rand(M, N, device=gpu, seed=2) if accumulate else torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    ref_ = (out.float() if accumulate else 0) + a.float() @ b.float().t()
+    C.gemm_nt(a, b, out, accumulate)
+    err = ((out.float() - ref_).norm() / ref_.norm()).item()
+    assert err < 5e-3, err
+
+
+def test_gemm_nt_strided_operands(gpu):
+    """Row strides larger than K / N (views into wider buffers) for A, B and C."""
+    C = _ext.require()
+    M, N, K = 512, 512, 256
+    A = _rand(M, K + 64, device=gpu)[:, 32:32 + K]
+    B = _rand(N, K + 128, device=gpu, seed=1)[:, :K]
+    Cbig = torch.zeros(M, N + 256, device=gpu, dtype=torch.bfloat16)
+    out = Cbig[:, 128:128 + N]
+    C.gemm_nt(A, B, out, False)
+    ref_ = A.float() @ B.float().t()
+    assert ((out.float() - ref_).norm() / ref_.norm()).item() < 5e-3
+    assert Cbig[:, :128].abs().max().item() == 0 and Cbig[:, 128 + N:].abs().max().item() == 0
+
+
+def test_gemm_nt_swiglu_epilogue_matches_fp32(gpu):
+    """gu, a = silu(g) * u and a^T from one GEMM against the fp32 reference (and exactly the
+    separate SwiGLU kernel applied to the same gu)."""
+    C = _ext.require()
+    T, D, F = 1024, 512, 768
+    x, w = _rand(T, D, device=gpu), _rand(2 * F, D, device=gpu, seed=1, scale=0.05)
+    gu, a, aT = C.gemm_nt_swiglu(x, w)
+    gur = x.float() @ w.float().t()
+    assert ((gu.float() - gur).norm() / gur.norm()).item() < 5e-3
+    ar = ref.swiglu(gur)
+    assert ((a.float() - ar).norm() / ar.norm()).item() < 1e-2
+    assert torch.equal(aT, a.t().contiguous())
+    a2, aT2 = C.swiglu_fwd_t(gu)
+    assert torch.equal(a, a2) and torch.equal(aT, aT2)
+
+
+def test_gemm_nt_swiglu_bwd_epilogue_matches_fp32(gpu):
+    C = _ext.require()
+    T, D, F = 1024, 512, 768
+    dy, wdT = _rand(T, D, device=gpu), _rand(F, D, device=gpu, seed=1, scale=0.05)
+    gu = _rand(T, 2 * F, device=gpu, seed=2)
+    dgu, dguT = C.gemm_nt_swiglu_bwd(dy, wdT, gu)
+    gur = gu.float().requires_grad_()
+    da = dy.float() @ wdT.float().t()
+    ref.swiglu(gur).backward(da)
+    assert ((dgu.float() - gur.grad).norm() / gur.grad.norm()).item() < 1e-2
+    assert torch.equal(dguT, dgu.t().contiguous())
+
+
+def test_swiglu_mlp_fused_matches_separate_kernels(gpu, monkeypatch):
+    """ops.swiglu_mlp through the fused GEMM epilogues == linear/swiglu/linear with separate kernels,
+    output and every gradient (no optimizer sinks: the gradients are returned)."""
+    T, D, F = 512, 512, 1024
+    torch.manual_seed(0)
+    h0 = _rand(2, T // 2, D, device=gpu)
+    wgu0 = _rand(2 * F, D, device=gpu, seed=1, scale=0.03)
+    wd0 = _rand(D, F, device=gpu, seed=2, scale=0.03)
+    dy = _rand(2, T // 2, D, device=gpu, seed=3)
+
+    def run():
+        h, wgu, wd = (t.clone().requires_grad_() for t in (h0, wgu0, wd0))
+        y = ops.swiglu_mlp(h, wgu, wd)
+        y.backward(dy)
+        return y.float(), h.grad.float(), wgu.grad.float(), wd.grad.float()
+
+    assert ops.functional._mlp_fused_ok(h0, wgu0, wd0)
+    fused = run()
+    monkeypatch.setenv("DSTACK_AMD_MLP_FUSED", "0")
+    sep = run()
+    for name, a, b in zip(["y", "dh", "dWgu", "dWdown"], fused, sep):
+        rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert rel < 1e-2, f"{name}: rel err {rel}"
