@@ -49,6 +49,7 @@ hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, lon
 bool dsa_gemm_nt_supported(int, int, int);
 hipError_t dsa_gemm_nt(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 bool dsa_gemm_nt_swiglu_supported(int, int, int);
+hipError_t dsa_gemm_nt_trace(const void*, const void*, void*, int, int, int, unsigned long long*, hipStream_t);
 hipError_t dsa_gemm_nt_swiglu(const void*, const void*, void*, void*, void*, int, int, int, long, long, hipStream_t);
 bool dsa_gemm_nt_swiglu_bwd_supported(int, int, int);
 hipError_t dsa_gemm_nt_swiglu_bwd(const void*, const void*, const void*, void*, void*, int, int, int, long, long,
@@ -380,8 +381,12 @@ void check_rows(const torch::Tensor& t, const char* what) {
 
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) { return dsa_gemm_nt_supported(M, N, K); }
 
-// out[M][N] (+)= a[M][K] b[N][K]^T  (csrc/gemm_nt.hip)
+// out[M][N] (+)= a[M][K] b[N][K]^T  (csrc/gemm_nt.hip); mode 2 = timing-only (no stores, diagnostics)
+void gemm_nt_mode(torch::Tensor a, torch::Tensor b, torch::Tensor out, int64_t mode);
 void gemm_nt(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool accumulate) {
+  gemm_nt_mode(a, b, out, accumulate ? 1 : 0);
+}
+void gemm_nt_mode(torch::Tensor a, torch::Tensor b, torch::Tensor out, int64_t mode) {
   check_rows(a, "gemm_nt");
   check_rows(b, "gemm_nt");
   check_rows(out, "gemm_nt");
@@ -389,11 +394,24 @@ void gemm_nt(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool accumulat
   TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_nt: shape mismatch");
   TORCH_CHECK(dsa_gemm_nt_supported(M, N, K), "gemm_nt: M % 256, N % 256, K % 128 must be 0");
   check(dsa_gemm_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0),
-                    accumulate ? 1 : 0, stream()),
+                    (int)mode, stream()),
         "gemm_nt");
 }
 
 bool gemm_nt_swiglu_supported(int64_t T, int64_t F, int64_t K) { return dsa_gemm_nt_swiglu_supported(T, F, K); }
+
+// diagnostic: per-phase s_memtime stamps of workgroup 0 (waves 0 and 4) -> int64 [2, 64]
+torch::Tensor gemm_nt_trace(torch::Tensor a, torch::Tensor b, torch::Tensor out) {
+  check_rows(a, "gemm_nt_trace");
+  check_rows(b, "gemm_nt_trace");
+  check_rows(out, "gemm_nt_trace");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && out.is_contiguous(), "gemm_nt_trace: contiguous operands");
+  auto tr = torch::zeros({2, 64}, a.options().dtype(torch::kInt64));
+  check(dsa_gemm_nt_trace(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.size(0), b.size(0), a.size(1),
+                          reinterpret_cast<unsigned long long*>(tr.data_ptr()), stream()),
+        "gemm_nt_trace");
+  return tr;
+}
 
 // gu = x w^T (w = [gate; up] [2F][K]) -> (gu [T][2F], a = silu(g) * u [T][F], a^T [F][T])
 std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor x, torch::Tensor w) {
@@ -569,8 +587,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn", &gemm_tn);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_nt", &gemm_nt);
+  m.def("gemm_nt_mode", &gemm_nt_mode);
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_swiglu", &gemm_nt_swiglu);
+  m.def("gemm_nt_trace", &gemm_nt_trace);
   m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);
   m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd);
   m.def("gemm_nt_swiglu_bwd_supported", &gemm_nt_swiglu_bwd_supported);

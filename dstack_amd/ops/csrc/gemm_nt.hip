@@ -48,7 +48,9 @@ constexpr int BUF = 4 * UNIT;              // a0 | a1 | b0 | b1
 constexpr int EPI_LD = 520;                // epilogue LDS row stride (bytes): 256 bf16 + 8 B pad
 constexpr int NT_LDS = 2 * BUF + 2 * 16384;  // 160 KiB: ring + room for the SwiGLU epilogue
 
-enum Epi { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU = 2, EPI_SWIGLU_BWD = 3 };
+// EPI_NONE: timing-only build (the accumulators are kept live, nothing is stored): what the
+// epilogue's stores cost (tools/diag, accumulate = 2 in dsa_gemm_nt)
+enum Epi { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU = 2, EPI_SWIGLU_BWD = 3, EPI_NONE = 4 };
 
 struct NTArgs {
   const bf16_t* A;
@@ -65,6 +67,7 @@ struct NTArgs {
   int F;          // SwiGLU width (ld of a, columns of gu / 2)
   int group;      // tile-order group height (tile rows)
   int wg_per_xcd; // workgroups per XCD (gridDim / 8 when persistent)
+  unsigned long long* trace;  // TRACE builds: per-phase s_memtime stamps of workgroup 0
 };
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -117,6 +120,39 @@ __device__ __forceinline__ bf16x8 ldsr(const char* p) { return *reinterpret_cast
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
+// Row-contiguous 16-byte output pieces from two 16-column accumulator tiles x (columns c..c+15)
+// and y (c+16..c+31): a lane of 16-lane row q holds columns 4q..4q+3 of each.  v_permlane16_swap
+// (gfx950) swaps the odd rows of its first operand with the even rows of its second, after which
+// rows 0/2 hold 8 consecutive columns of x, rows 1/3 8 of y: the lane's piece starts at column
+// 16 * (q & 1) + 8 * (q >> 1) of the pair.  One dwordx4 store instead of two dwordx2: the store
+// issue, not bandwidth, bounds an epilogue.
+__device__ __forceinline__ unsigned nt_pk(unsigned short lo, unsigned short hi) {
+  return (unsigned)lo | ((unsigned)hi << 16);
+}
+
+__device__ __forceinline__ us8 nt_pair8(const us4& x, const us4& y) {
+  const auto r0 = __builtin_amdgcn_permlane16_swap(nt_pk(x[0], x[1]), nt_pk(y[0], y[1]), false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(nt_pk(x[2], x[3]), nt_pk(y[2], y[3]), false, false);
+  const unsigned d[4] = {r0[0], r1[0], r0[1], r1[1]};
+  us8 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = (unsigned short)(d[i] & 0xffff);
+    v[2 * i + 1] = (unsigned short)(d[i] >> 16);
+  }
+  return v;
+}
+
+// the same for fp32 accumulators (before rounding): 8 consecutive columns as floats
+__device__ __forceinline__ void nt_pair8f(const f32x4& x, const f32x4& y, float (&o)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[j]), __float_as_uint(y[j]), false, false);
+    o[j] = __uint_as_float(r[0]);
+    o[4 + j] = __uint_as_float(r[1]);
+  }
+}
+
 template <int MS, int NS>
 __device__ __forceinline__ void nt_quadrant(f32x4 (&acc)[2][4][4], const bf16x8 (&af)[4][2],
                                             const bf16x8 (&bf)[2][2][2]) {
@@ -162,14 +198,36 @@ __device__ __forceinline__ void nt_tile_origin(const NTArgs& p, int t, int& m0, 
   nb0 = ((t % in_group) / gm) * p.nstride;
 }
 
-template <int EPI>
+template <int EPI, bool TRACE = false>
 __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // the plain epilogues store straight from the accumulators while the next tile's prologue DMA
   // is in flight; the SwiGLU ones stage through LDS (transposed copies) and reload afterwards
-  constexpr bool OVERLAP = EPI == EPI_STORE || EPI == EPI_ACC;
+  // the plain and SwiGLU-forward epilogues store straight from the accumulators (a^T through the
+  // 32 KiB of LDS above the ring) while the next tile's first K-tiles stream into the ring; the
+  // SwiGLU backward stages whole tiles through LDS and reloads afterwards
+  constexpr bool OVERLAP = EPI == EPI_STORE || EPI == EPI_ACC || EPI == EPI_SWIGLU || EPI == EPI_NONE;
+  // barrier-free epilogues keep the two wave groups staggered across tiles: group 0 stores its
+  // half of the tile while group 1 issues its last MFMAs, group 1 stores while group 0 runs the
+  // next tile's first MFMAs -- the stores take the place of a memory segment of the ping-pong
+  constexpr bool STAGGERED = EPI == EPI_STORE || EPI == EPI_ACC || EPI == EPI_NONE;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;
+  // TRACE: waves 0 and 4 of workgroup 0 stamp every phase boundary of K-iterations 8..11 into
+  // the spare LDS above the ring (ds_write: no VMEM op disturbs the counted vmcnt), copied out at
+  // the end -- where a phase's cycles go (reads, barrier waits, MFMAs)
+  const bool tracer = TRACE && blockIdx.x == 0 && (w == 0 || w == 4);
+  int tcount = 0;
+  auto stamp = [&](int it) {
+    if constexpr (TRACE) {
+      if (tracer && it >= 8 && it < 12) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) reinterpret_cast<unsigned long long*>(smem + 2 * BUF)[(w >> 2) * 64 + tcount] = t;
+        ++tcount;
+      }
+    }
+  };
 
   // --- this workgroup's tiles: XCD x = blockIdx % 8 owns a contiguous slice of the logical tile
   // order; its workgroups take every (gridDim/8)-th tile of the slice (persistent when the grid is
@@ -242,7 +300,9 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   nt_barrier();
 
   while (true) {
-    if (wr == 1) nt_barrier();  // group 1 runs one barrier behind
+    if (!STAGGERED || local == xj) {
+      if (wr == 1) nt_barrier();  // group 1 runs one barrier behind
+    }
     const int next = local + stride;
     const bool has_next = next < cnt;
     int m1 = 0, nb1 = 0;
@@ -268,6 +328,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       const bool go = more || (OVERLAP && has_next);
       const int t2 = more ? t + 2 : 0, t3 = more ? t + 3 : 1;
       // P1: m-subtile 0 of tile t
+      stamp(it);
       nt_read_b<0>(bf, bufE, rb0, rb1);
       nt_read_b<1>(bf, bufE, rb0, rb1);
       nt_read_a<0>(af, bufE, ra0, ra1);
@@ -275,11 +336,15 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       dma(1, t + 1);
       if (!more && go) set_src(m1, nb1);
       nt_lgkmcnt<0>();
+      stamp(it);
       nt_barrier();
+      stamp(it);
       nt_quadrant<0, 0>(acc, af, bf);
       nt_quadrant<0, 1>(acc, af, bf);
+      stamp(it);
       nt_barrier();
       // P2: m-subtile 1 of tile t; retire tile t+1
+      stamp(it);
       nt_read_a<1>(af, bufE, ra0, ra1);
       if (go) {
         dma(2, t2);
@@ -289,11 +354,15 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
         nt_vmcnt<0>();
       }
       nt_lgkmcnt<0>();
+      stamp(it);
       nt_barrier();
+      stamp(it);
       nt_quadrant<1, 0>(acc, af, bf);
       nt_quadrant<1, 1>(acc, af, bf);
+      stamp(it);
       nt_barrier();
       // P3: m-subtile 0 of tile t+1
+      stamp(it);
       nt_read_b<0>(bf, bufO, rb0, rb1);
       nt_read_b<1>(bf, bufO, rb0, rb1);
       nt_read_a<0>(af, bufO, ra0, ra1);
@@ -302,11 +371,15 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
         dma(1, t2);
       }
       nt_lgkmcnt<0>();
+      stamp(it);
       nt_barrier();
+      stamp(it);
       nt_quadrant<0, 0>(acc, af, bf);
       nt_quadrant<0, 1>(acc, af, bf);
+      stamp(it);
       nt_barrier();
       // P4: m-subtile 1 of tile t+1; retire tile t+2
+      stamp(it);
       nt_read_a<1>(af, bufO, ra0, ra1);
       if (go) {
         dma(2, t3);
@@ -314,103 +387,124 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
         nt_vmcnt<4>();
       }
       nt_lgkmcnt<0>();
+      stamp(it);
       nt_barrier();
+      stamp(it);
       nt_quadrant<1, 0>(acc, af, bf);
       nt_quadrant<1, 1>(acc, af, bf);
+      stamp(it);
       nt_barrier();
     }
-    if (wr == 0) nt_barrier();  // re-align the groups
+    if constexpr (TRACE) {
+      if (tracer && lane < 64 && tcount > 0)
+        p.trace[(w >> 2) * 64 + lane] = reinterpret_cast<unsigned long long*>(smem + 2 * BUF)[(w >> 2) * 64 + lane];
+    }
+    if constexpr (!STAGGERED) {
+      if (wr == 0) nt_barrier();  // re-align the groups
+    }
     if constexpr (!OVERLAP) nt_barrier();  // every wave is past its last fragment read: LDS is free
 
     // --- epilogue ---------------------------------------------------------------------------------
     // accumulator (ms, mi, n): tile row 128ms + 64wr + 16mi + (lane&15), tile columns
     // 128(n>>1) + 32wc + 16(n&1) + 4(lane>>4) + [0,4)
-    if constexpr (OVERLAP) {
-      // bf16 results first (ACC: plus the old C, whose loads the compiler waits for here, before
-      // any DMA is in flight), then the next tile's prologue, then the stores behind it
-      bf16_t* cbase = p.C + (long)(m0 + 64 * wr + er) * p.ldc + nb0 + 32 * wc + ec;
-      us4 o[2][4][4];
+    if constexpr (EPI == EPI_NONE) {
 #pragma unroll
       for (int ms = 0; ms < 2; ++ms)
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            if constexpr (EPI == EPI_ACC)
-              o[ms][mi][n] = *reinterpret_cast<const us4*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc +
-                                                            (n >> 1) * p.bsplit + 16 * (n & 1));
-          }
+          for (int n = 0; n < 4; ++n) asm volatile("" ::"v"(acc[ms][mi][n]));
+    } else if constexpr (EPI == EPI_STORE || EPI == EPI_ACC) {
+      // 16-byte pieces: column pair p (n = 2p, 2p+1) of row (ms, mi) -> columns
+      // 128p + 32wc + 16(q&1) + 8(q>>1) .. +8 of the lane's row (q = lane >> 4)
+      const int q = lane >> 4;
+      bf16_t* cbase = p.C + (long)(m0 + 64 * wr + er) * p.ldc + nb0 + 32 * wc + 16 * (q & 1) + 8 * (q >> 1);
+      if constexpr (EPI == EPI_ACC) {
+        us8 old[2][4][2];
 #pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
+        for (int ms = 0; ms < 2; ++ms)
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+          for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-          for (int n = 0; n < 4; ++n)
+            for (int pp = 0; pp < 2; ++pp)
+              old[ms][mi][pp] = *reinterpret_cast<const us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              float x = acc[ms][mi][n][j];
-              if constexpr (EPI == EPI_ACC) x += bf2f(o[ms][mi][n][j]);
-              o[ms][mi][n][j] = f2bf(x);
+        for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+              float v[8];
+              nt_pair8f(acc[ms][mi][2 * pp], acc[ms][mi][2 * pp + 1], v);
+              us8 o;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] + bf2f(old[ms][mi][pp][j]));
+              *reinterpret_cast<us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit) = o;
             }
-      // pin the conversions (and the compiler's waits for the old C) in front of the DMA below
+      } else {
 #pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
+        for (int ms = 0; ms < 2; ++ms)
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+          for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-          for (int n = 0; n < 4; ++n) asm volatile("" ::"v"(o[ms][mi][n]));
-      __builtin_amdgcn_sched_barrier(0);
+            for (int pp = 0; pp < 2; ++pp) {
+              us4 x, y;
 #pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int n = 0; n < 4; ++n)
-            *reinterpret_cast<us4*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + (n >> 1) * p.bsplit +
-                                    16 * (n & 1)) = o[ms][mi][n];
-    } else if constexpr (EPI == EPI_SWIGLU) {
-      // gu tile straight from the accumulators; a = silu(g) * u from the bf16-rounded g, u (what
-      // the backward re-reads from gu), staged through LDS for the row-major and transposed copies
-      bf16_t* gbase = p.C + (long)(m0 + 64 * wr + er) * p.ldc + nb0 + 32 * wc + ec;
-      constexpr int A_LD = 264;            // [256 t][128 f] + 8 B pad
-      char* sa = smem;                      // a, row-major
-      char* sat = smem + 256 * A_LD;        // a^T [128 f][256 t], row stride EPI_LD
-#pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int n = 0; n < 2; ++n) {
-            const int r = 128 * ms + 64 * wr + 16 * mi + er;
-            const int c = 32 * wc + 16 * n + ec;
-            us4 g4, u4, o;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              g4[j] = f2bf(acc[ms][mi][n][j]);
-              u4[j] = f2bf(acc[ms][mi][n + 2][j]);
-              o[j] = f2bf(silu(bf2f(g4[j])) * bf2f(u4[j]));
-              *reinterpret_cast<bf16_t*>(sat + (c + j) * EPI_LD + 2 * r) = o[j];
+              for (int j = 0; j < 4; ++j) {
+                x[j] = f2bf(acc[ms][mi][2 * pp][j]);
+                y[j] = f2bf(acc[ms][mi][2 * pp + 1][j]);
+              }
+              *reinterpret_cast<us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit) = nt_pair8(x, y);
             }
-            bf16_t* gp = gbase + (long)(128 * ms + 16 * mi) * p.ldc + 16 * n;
-            *reinterpret_cast<us4*>(gp) = g4;
-            *reinterpret_cast<us4*>(gp + p.bsplit) = u4;
-            *reinterpret_cast<us4*>(sa + r * A_LD + 2 * c) = o;
-          }
-      nt_barrier();
-      const int f0 = nb0;  // nstride 128: the tile's gate columns
-      // a: 256 rows x 256 B; a wave writes two rows per instruction
-#pragma unroll 4
-      for (int i = 0; i < 16; ++i) {
-        const int r = 16 * i + 2 * w + (lane >> 5), c = 4 * (lane & 31);
-        *reinterpret_cast<us4*>(p.C2 + (long)(m0 + r) * p.F + f0 + c) =
-            *reinterpret_cast<const us4*>(sa + r * A_LD + 2 * c);
       }
-      // a^T: 128 rows x 512 B
-#pragma unroll 4
-      for (int i = 0; i < 16; ++i) {
-        const int r = 8 * i + w, c = 4 * lane;
-        *reinterpret_cast<us4*>(p.C3 + (long)(f0 + r) * p.M + m0 + c) =
-            *reinterpret_cast<const us4*>(sat + r * EPI_LD + 2 * c);
+    } else if constexpr (EPI == EPI_SWIGLU) {
+      // gu and a = silu(g) * u (from the bf16-rounded g, u: what the backward re-reads from gu)
+      // straight from the accumulators; a^T through the spare LDS, one 128-token half at a time
+      const int f0 = nb0;  // nstride 128: the tile's gate columns
+      const int q = lane >> 4;
+      const int pc = 16 * (q & 1) + 8 * (q >> 1);  // the lane's 16-byte piece of a 32-column pair
+      bf16_t* gbase = p.C + (long)(m0 + 64 * wr + er) * p.ldc + f0 + 32 * wc + pc;
+      bf16_t* abase = p.C2 + (long)(m0 + 64 * wr + er) * p.F + f0 + 32 * wc + pc;
+      // a^T half: [128 f][128 t] bf16, 256-byte rows, 16-byte chunk c of row f at c ^ ((f >> 2) & 7)
+      // (the 2-byte transposed writes of lanes 4 f-rows apart land in different banks)
+      char* sat = smem + 2 * BUF;
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms) {
+        us4 o[4][2];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          us4 g4[2], u4[2];
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              g4[n][j] = f2bf(acc[ms][mi][n][j]);
+              u4[n][j] = f2bf(acc[ms][mi][n + 2][j]);
+              o[mi][n][j] = f2bf(silu(bf2f(g4[n][j])) * bf2f(u4[n][j]));
+            }
+          const long ro = (long)(128 * ms + 16 * mi);
+          *reinterpret_cast<us8*>(gbase + ro * p.ldc) = nt_pair8(g4[0], g4[1]);
+          *reinterpret_cast<us8*>(gbase + ro * p.ldc + p.bsplit) = nt_pair8(u4[0], u4[1]);
+          *reinterpret_cast<us8*>(abase + ro * p.F) = nt_pair8(o[mi][0], o[mi][1]);
+        }
+        nt_barrier();  // the previous half's a^T rows have been read
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int f = 32 * wc + 16 * n + ec + j, t = 64 * wr + 16 * mi + er;
+              *reinterpret_cast<bf16_t*>(sat + f * 256 + ((2 * t) ^ (((f >> 2) & 7) << 4))) = o[mi][n][j];
+            }
+        nt_barrier();
+        // 128 rows x 256 B: 16 B per lane, a wave writes 4 rows per instruction
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 32 * i + 4 * w + (lane >> 4), c = 8 * (lane & 15);
+          *reinterpret_cast<us8*>(p.C3 + (long)(f0 + r) * p.M + m0 + 128 * ms + c) =
+              *reinterpret_cast<const us8*>(sat + r * 256 + ((2 * c) ^ (((r >> 2) & 7) << 4)));
+        }
       }
     } else {  // EPI_SWIGLU_BWD: acc = da[t][f] for the tile's 256 f columns (plain column map)
       // dg = da * u * silu'(g), du = da * silu(g); g, u from gu[t][f], gu[t][F + f]
@@ -466,7 +560,12 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
         }
       }
     }
-    if (!has_next) break;
+    if (!has_next) {
+      if constexpr (STAGGERED) {
+        if (wr == 0) nt_barrier();  // equal barrier counts for both groups at exit
+      }
+      break;
+    }
     if constexpr (!OVERLAP) {
       nt_barrier();  // every wave is done with the LDS staging
       set_src(m1, nb1);
@@ -509,11 +608,11 @@ int nt_cus() {
 
 // One workgroup per CU (128 KiB ring): a grid of min(tiles, CUs rounded down to a multiple of 8)
 // workgroups that loop over their XCD's tiles.
-template <int EPI>
+template <int EPI, bool TRACE = false>
 hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI>),
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, TRACE>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, NT_LDS));
     attr = true;
   }
@@ -525,7 +624,7 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
     a.wg_per_xcd = cap / 8;
   }
   if (const char* g = getenv("DSTACK_AMD_GEMM_NT_GROUP")) a.group = atoi(g) > 0 ? atoi(g) : a.group;
-  gemm_nt_kernel<EPI><<<grid, 512, NT_LDS, st>>>(a);
+  gemm_nt_kernel<EPI, TRACE><<<grid, 512, NT_LDS, st>>>(a);
   return hipGetLastError();
 }
 
@@ -554,7 +653,30 @@ extern "C" hipError_t dsa_gemm_nt(const void* A, const void* B, void* C, int M, 
   a.bsplit = 128;
   a.group = nt_group(M / NT_BM, N / NT_BN);
   const int tiles = (M / NT_BM) * (N / NT_BN);
+  if (accumulate == 2) return nt_launch<EPI_NONE>(a, tiles, st);  // timing-only diagnostic
   return accumulate ? nt_launch<EPI_ACC>(a, tiles, st) : nt_launch<EPI_STORE>(a, tiles, st);
+}
+
+// Diagnostic: one plain GEMM with waves 0 and 4 of workgroup 0 stamping every phase boundary of
+// K-iterations 8..11 (s_memtime, 4 per phase) into trace[2][64] (tools/diag/gemm_nt_phases.py).
+extern "C" hipError_t dsa_gemm_nt_trace(const void* A, const void* B, void* C, int M, int N, int K,
+                                        unsigned long long* trace, hipStream_t st) {
+  if (!nt_shape_ok(M, N, K) || K < 24 * NT_BK) return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (bf16_t*)C;
+  a.lda = K;
+  a.ldb = K;
+  a.ldc = N;
+  a.M = M;
+  a.K = K;
+  a.ntn = N / NT_BN;
+  a.nstride = NT_BN;
+  a.bsplit = 128;
+  a.group = nt_group(M / NT_BM, N / NT_BN);
+  a.trace = trace;
+  return nt_launch<EPI_STORE, true>(a, (M / NT_BM) * (N / NT_BN), st);
 }
 
 extern "C" bool dsa_gemm_nt_swiglu_supported(int T, int F, int K) {

@@ -10,6 +10,7 @@
 #   test[=<pytest -k expr>]     pytest -m gpu (optionally a -k selection)
 #   smoke                       __graft_entry__.smoke()
 #   bench[=<steps>]             python bench.py --steps N --warmup 2 (1 GPU)
+#   ab=<steps>:<ENV=a>,<ENV=b>  interleaved same-box A/B of bench.py: a, b, a, b (one env each)
 #   prof[=<steps>]              rocprofv3 --kernel-trace --stats over bench.py -> kernel_stats.csv
 #   pmc=<c1,c2,...>[@<cmd>]     one rocprofv3 --pmc pass (default command: tools/bench_attn.py)
 #   gemm[=<SHAPES>]             tools/bench_gemm_nt.py (in-tree NT GEMM vs hipBLASLt)
@@ -48,6 +49,19 @@ for step in "$@"; do
       fi ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench) run bench 600 python -u bench.py --gpus 1 --steps "${val:-8}" --warmup 2 --no-coldstart || exit 1 ;;
+    ab)
+      steps=${val%%:*}
+      arms=${val#*:}
+      IFS=',' read -r -a envs <<< "$arms"
+      for round in 1 2; do
+        i=0
+        for e in "${envs[@]}"; do
+          i=$((i + 1))
+          # shellcheck disable=SC2086
+          run "ab_${round}_${i}" 600 env $e python -u bench.py --gpus 1 --steps "$steps" --warmup 2 --no-coldstart || exit 1
+          grep -h '"metric"' "$OUT/ab_${round}_${i}.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('[ab]', '$e', d['value'], d['ms_per_step'])" | tee -a "$OUT/ab.txt"
+        done
+      done ;;
     prof)
       run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o k -- \
         python3 -u bench.py --gpus 1 --steps "${val:-5}" --warmup 2 --no-coldstart || exit 1
