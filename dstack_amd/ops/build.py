@@ -122,7 +122,43 @@ def is_current() -> bool:
     return so.exists() and stamp.exists() and stamp.read_text().strip() == so_digest
 
 
+def quick_key() -> str:
+    """A digest of everything the build reads that can be had WITHOUT importing torch: the kernel
+    sources and headers, the torch installation's version file and location, the Python headers'
+    location, the arch and the compiler.  Equal to the manifest's -> the .so is current, and a job
+    whose first command is ``python -m dstack_amd.ops.build`` does not pay a torch import (~2 s)
+    to find that out."""
+    import hashlib
+    import importlib.util
+
+    h = hashlib.sha256()
+    for f in sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("*.hip")) + [CSRC / "bindings.cpp", Path(__file__)]:
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    spec = importlib.util.find_spec("torch")
+    tdir = Path(spec.origin).parent if spec and spec.origin else None
+    h.update(str(tdir).encode())
+    if tdir is not None and (tdir / "version.py").exists():
+        h.update((tdir / "version.py").read_bytes())
+    h.update("\0".join([ARCH, HIPCC, sysconfig.get_paths()["include"], sysconfig.get_config_var("EXT_SUFFIX")]).encode())
+    return h.hexdigest()
+
+
+def _quick_current() -> bool:
+    import hashlib
+    import json
+
+    so = so_path()
+    try:
+        m = json.loads(manifest_path().read_text())
+        return (so.exists() and m.get("quick_key") == quick_key()
+                and hashlib.sha256(so.read_bytes()).hexdigest() == m.get("so_sha256"))
+    except (OSError, ValueError):
+        return False
+
+
 def build(verbose: bool = False, keep_asm: bool = False, force: bool = False) -> Path:
+    if not force and not keep_asm and _quick_current():
+        return so_path()  # nothing changed since the recorded build (no torch import needed)
     BUILD.mkdir(parents=True, exist_ok=True)
     units, link, so_digest = _plan(keep_asm)
     jobs = [(obj, cmd, d) for obj, cmd, d in units if force or _stale(obj, d)]
@@ -168,6 +204,7 @@ def _write_manifest(so: Path, so_digest: str, compiled, units, linked: bool):
         "built_at": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds")
         if (compiled or linked or not prev) else prev.get("built_at"),
         "built_on": platform.node() if (compiled or linked or not prev) else prev.get("built_on"),
+        "quick_key": quick_key(),
     }
     manifest_path().write_text(json.dumps(m, indent=1) + "\n")
 

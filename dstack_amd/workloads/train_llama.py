@@ -10,15 +10,34 @@ Data is synthetic (uniform random token ids) and weights are random-init: there 
 
 from __future__ import annotations
 
-import argparse
-import json
-import os
-import shutil
 import time
-from dataclasses import dataclass
 
-import torch
-import torch.distributed as dist
+_T_IMPORT = time.time()  # before torch: the stage split below starts here
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+import shutil  # noqa: E402
+from dataclasses import dataclass  # noqa: E402
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+_T_TORCH = time.time()
+
+
+def process_start_time() -> float | None:
+    """Wall-clock time this process was exec'd (Linux /proc), so a job's stage split can start
+    from the interpreter launch rather than from the first line of Python."""
+    try:
+        with open("/proc/self/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        start_ticks = int(fields[19])  # field 22 (starttime), counted after the ")" of comm
+        with open("/proc/stat") as f:
+            btime = next(int(ln.split()[1]) for ln in f if ln.startswith("btime"))
+        return btime + start_ticks / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, IndexError, StopIteration):
+        return None
 
 from dstack_amd.models.llama import CONFIGS, Llama
 from dstack_amd.parallel.zero import ZeroOptimizer
@@ -280,14 +299,25 @@ def _sync(env: DistEnv):
 def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log_every: int = 1,
         grad_accum: int = 1, checkpoint_dir: str | None = None, save_every: int = 0, lr: float = 3e-4,
         lr_warmup: int = 300, lr_decay_steps: int = 0, clip_grad_norm: float = 0.0, data: str = "synthetic-lm"):
+    # wall-clock stamps of the task's start-up (rank 0 prints them after the first optimizer step):
+    # process exec -> imports -> rendezvous -> HIP extension -> GEMM selections -> model -> step 1
+    stages = {"proc_start": process_start_time(), "import_start": _T_IMPORT, "torch_imported": _T_TORCH}
     env = init_distributed()
+    stages["dist_ready"] = time.time()
     device = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    if device.type == "cuda":
+        from dstack_amd.ops import _ext
+
+        _ext.require()  # the HIP extension (.so) is mapped here, not at the first kernel
+    stages["extension_loaded"] = time.time()
     from dstack_amd.ops import gemm_tuning
 
     gemm_mode = gemm_tuning.setup(device_index=env.local_rank if device.type == "cuda" else 0)
+    stages["gemm_tuning_loaded"] = time.time()
     t0 = time.time()
     tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum, lr=lr, lr_warmup=lr_warmup,
                  lr_decay_steps=lr_decay_steps, clip_grad_norm=clip_grad_norm, data=data)
+    stages["model_ready"] = time.time()
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "
               f"init={time.time()-t0:.1f}s gemm_tuning={gemm_mode}", flush=True)
@@ -308,10 +338,17 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         if checkpoint_dir and save_every and tr.opt.step_count % save_every == 0:
             tr.save_checkpoint(checkpoint_dir)
 
+    def _first_step_done():
+        if "first_step_done" not in stages:
+            stages["first_step_done"] = time.time()
+            if env.rank == 0:
+                print("[train] stages " + json.dumps(stages), flush=True)
+
     warm_losses = []
     for i in range(warmup):
         loss = tr.step()
         warm_losses.append(loss.item())
+        _first_step_done()
         if env.rank == 0:
             print(f"[train] warmup {i} loss={loss.item():.4f}", flush=True)
         _maybe_save()
@@ -320,6 +357,9 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     losses = []
     for i in range(steps):
         losses.append(tr.step())
+        if i == 0 and "first_step_done" not in stages:
+            losses[-1].item()  # (only when there was no warmup: the stamp needs the step finished)
+            _first_step_done()
         if log_every and env.rank == 0 and (i + 1) % log_every == 0:
             print(f"[train] step {tr.opt.step_count} loss={losses[-1].item():.4f}", flush=True)
         _maybe_save()  # inside the timed loop only when asked for
@@ -345,6 +385,7 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         result["loss_floor"] = round(tr.stream.loss_floor, 4)
         result["unigram_entropy"] = round(tr.stream.unigram_entropy, 4)
     result["gemm_tuning"] = gemm_mode
+    result["stages"] = stages
     if env.rank == 0:
         print("[train] result " + json.dumps(result), flush=True)
     return env, tr, result

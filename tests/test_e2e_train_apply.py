@@ -103,3 +103,24 @@ def test_apply_llama_train_example_dp4(server, tmp_path, nodes, gpus_per_node):
         granted.append(set(line.split("=", 1)[1].strip().split(",")))
     assert all(len(gs) == gpus_per_node for gs in granted)
     assert set().union(*granted) == {"0", "1", "2", "3"}
+
+
+def test_bench_apply_time_to_first_step_and_job_tokens(tmp_path):
+    """bench_apply.py (the BENCH JSON's cold start): the example task through the server on fresh
+    instances, the task's [train] stages line and result line parsed into the stage split and the
+    job's own tokens/s (2 fake GPUs, gloo ranks, tiny model)."""
+    if not _ops_current():
+        pytest.skip("HIP extension not built for the current sources (the example's build step would compile)")
+    sys.path.insert(0, REPO)
+    import bench_apply
+
+    r = bench_apply.measure(gpus=2, runs=2, steps=1, warmup=1, tok_steps=2, tok_warmup=1, fake_gpus=2,
+                            extra_args=CPU_ARGS.replace("--steps 2 --warmup 1", ""), timeout=300)
+    assert not r["errors"], r["errors"]
+    assert r["runs"] == 2 and r["distinct_instances"] == 3 and r["gpu_requested"] == "MI355X:2"
+    st = r["stages_p50_s"]
+    assert all(st[k] is not None and st[k] >= 0 for k in st), st
+    assert r["time_to_first_log_p50_s"] < r["time_to_train_start_p50_s"] < r["time_to_first_step_p50_s"]
+    # the stages tile submit -> first step
+    assert abs(sum(st.values()) - r["time_to_first_step_p50_s"]) < 0.25 * r["time_to_first_step_p50_s"]
+    assert r["job_tokens_per_s"] > 0 and r["job_n_gpus"] == 2 and r["job_steps"] == 2
