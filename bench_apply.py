@@ -40,6 +40,7 @@ _LAUNCHER_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_
                  "DSTACK_AMD_BENCH_CHILD")
 
 STAGES = [  # (name, start stamp, end stamp) -- stamps: server timings + the task's [train] stages
+    # "running": the server has handed the job to the runner; "proc_start": rank 0's exec
     ("control_plane_s", "submitted", "running"),
     ("launch_s", "running", "proc_start"),
     ("imports_s", "proc_start", "torch_imported"),

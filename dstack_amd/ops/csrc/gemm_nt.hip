@@ -68,7 +68,6 @@ struct NTArgs {
   int group;      // tile-order group height (tile rows)
   int wg_per_xcd; // workgroups per XCD (gridDim / 8 when persistent)
   unsigned long long* trace;  // TRACE builds: per-phase s_memtime stamps of workgroup 0
-  int nt_store;   // non-temporal output stores (A/B: DSTACK_AMD_GEMM_NT_NTSTORE)
 };
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -455,11 +454,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
                 x[j] = f2bf(acc[ms][mi][2 * pp][j]);
                 y[j] = f2bf(acc[ms][mi][2 * pp + 1][j]);
               }
-              us8* dst = reinterpret_cast<us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit);
-              if (p.nt_store)
-                __builtin_nontemporal_store(nt_pair8(x, y), dst);
-              else
-                *dst = nt_pair8(x, y);
+              *reinterpret_cast<us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit) = nt_pair8(x, y);
             }
       }
     } else if constexpr (EPI == EPI_SWIGLU) {
@@ -629,7 +624,6 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
     a.wg_per_xcd = cap / 8;
   }
   if (const char* g = getenv("DSTACK_AMD_GEMM_NT_GROUP")) a.group = atoi(g) > 0 ? atoi(g) : a.group;
-  if (const char* n = getenv("DSTACK_AMD_GEMM_NT_NTSTORE")) a.nt_store = atoi(n);
   gemm_nt_kernel<EPI, TRACE><<<grid, 512, NT_LDS, st>>>(a);
   return hipGetLastError();
 }

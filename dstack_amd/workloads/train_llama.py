@@ -28,15 +28,17 @@ _T_TORCH = time.time()
 
 def process_start_time() -> float | None:
     """Wall-clock time this process was exec'd (Linux /proc), so a job's stage split can start
-    from the interpreter launch rather than from the first line of Python."""
+    from the interpreter launch rather than from the first line of Python.  Computed against
+    /proc/uptime (10 ms resolution), not /proc/stat's btime, which is whole seconds."""
     try:
+        now = time.time()
+        with open("/proc/uptime") as f:
+            uptime = float(f.read().split()[0])
         with open("/proc/self/stat") as f:
             fields = f.read().rsplit(")", 1)[1].split()
-        start_ticks = int(fields[19])  # field 22 (starttime), counted after the ")" of comm
-        with open("/proc/stat") as f:
-            btime = next(int(ln.split()[1]) for ln in f if ln.startswith("btime"))
-        return btime + start_ticks / os.sysconf("SC_CLK_TCK")
-    except (OSError, ValueError, IndexError, StopIteration):
+        start_s = int(fields[19]) / os.sysconf("SC_CLK_TCK")  # field 22 (starttime), after the ")" of comm
+        return now - (uptime - start_s)
+    except (OSError, ValueError, IndexError):
         return None
 
 from dstack_amd.models.llama import CONFIGS, Llama

@@ -487,8 +487,10 @@ bool rocprof_wrap(const std::vector<std::string>& job, const std::vector<std::st
                                                       "accelerate.commands.accelerate_cli", "deepspeed",
                                                       "deepspeed.launcher.runner", "deepspeed.launcher.launch",
                                                       "torch.distributed.launch"};
+  // torch.distributed.run, or dstack_amd's torch-free launcher with the same options
   const bool via_module = py && w + 2 < words.size() && words[w + 1].text == "-m" &&
-                          words[w + 2].text == "torch.distributed.run";
+                          (words[w + 2].text == "torch.distributed.run" ||
+                           words[w + 2].text == "dstack_amd.workloads.launch");
   if (py && w + 2 < words.size() && words[w + 1].text == "-m" && py_launchers.count(words[w + 2].text) &&
       words[w + 2].text != "torch.distributed.run") {
     err = "'python -m " + words[w + 2].text + "' is a launcher: run it as torchrun / accelerate launch / deepspeed";

@@ -196,6 +196,9 @@ int main() {
     CHECK(wrap("python -m torch.distributed.run --standalone --nproc_per_node=2 t.py"));
     CHECK(out[2] == "exec python -m torch.distributed.run --standalone --nproc_per_node=2 --no-python rocprofv3 "
                     "--kernel-trace -- python -u t.py");
+    CHECK(wrap("python -m dstack_amd.workloads.launch --nnodes=1 --nproc-per-node 8 bench.py --gpus 8"));
+    CHECK(out[2] == "exec python -m dstack_amd.workloads.launch --nnodes=1 --nproc-per-node 8 --no-python rocprofv3 "
+                    "--kernel-trace -- python -u bench.py --gpus 8");
     CHECK(wrap("torchrun --no-python --nproc-per-node 2 ./app"));
     CHECK(out[2] == "exec torchrun --no-python --nproc-per-node 2 rocprofv3 --kernel-trace -- ./app");
     // a #! Python script runs as <interpreter> script (env -S options kept); relative to the cd'd dir

@@ -52,7 +52,8 @@ def _task_yaml(nodes: int, gpus_per_node: int, port: int) -> str:
     with open(EXAMPLE) as f:
         conf = yaml.safe_load(f)
     cmds = list(conf["commands"])
-    assert cmds[0] == "python -m dstack_amd.ops.build" and "torchrun" in cmds[1] and "bench.py" in cmds[1]
+    assert cmds[0] == "python -m dstack_amd.ops.build" and "dstack_amd.workloads.launch" in cmds[1]
+    assert "bench.py" in cmds[1]
     # the job runs from the repository checkout (the example assumes the repo is the working dir)
     conf["commands"] = [f"cd {REPO}", "echo granted-gpus=$HIP_VISIBLE_DEVICES", cmds[0], cmds[1] + " " + CPU_ARGS]
     conf["name"] = f"llama3-train-{nodes}x{gpus_per_node}"
