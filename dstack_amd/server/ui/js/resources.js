@@ -117,21 +117,59 @@ Object.assign(VIEWS, {
     $("#swd").onclick = () => act(() => api(P("gateways/set_wildcard_domain"), { name, wildcard_domain: $("#wd").value.trim() }));
   },
 
-  async models() {
+  async models(name) {
+    if (name) return VIEWS.model(name);
     const r = await fetch(`/proxy/models/${encodeURIComponent(S.project)}/models`, { headers: { "Authorization": "Bearer " + S.token } }).then(r => r.json());
-    $("#main").innerHTML = `<h3>Models</h3>` + table(["model", "owner"], r.data.map(m => [esc(m.id), esc(m.owned_by)])) +
-      `<h4>Chat</h4><div class="row"><select id="m">${r.data.map(m => `<option>${esc(m.id)}</option>`).join("")}</select>
-       <input id="q" size="60" placeholder="message"><input id="mt" size="5" value="256" title="max tokens"><button class="primary" id="send">Send</button></div><pre id="a"></pre>`;
-    const history = [];
-    $("#send").onclick = async () => {
-      history.push({ role: "user", content: $("#q").value });
-      $("#a").textContent = history.map(m => `${m.role}: ${m.content}`).join("\n\n") + "\n\nassistant: …";
-      const d = await fetch(`/proxy/models/${encodeURIComponent(S.project)}/chat/completions`, { method: "POST",
-        headers: { "Authorization": "Bearer " + S.token, "Content-Type": "application/json" },
-        body: JSON.stringify({ model: $("#m").value, messages: history, max_tokens: +$("#mt").value || 256 }) }).then(r => r.json());
-      const answer = d.choices ? d.choices[0].message.content : JSON.stringify(d, null, 1);
-      history.push({ role: "assistant", content: answer });
-      $("#a").textContent = history.map(m => `${m.role}: ${m.content}`).join("\n\n"); $("#q").value = "";
-    };
+    const runs = await api("/api/runs/list", { project_name: S.project, only_active: true, limit: 100 });
+    const byModel = Object.fromEntries(runs.filter(x => x.service && x.service.model).map(x => [x.service.model.name, x]));
+    $("#main").innerHTML = `<h3>Models</h3>` + table(["model", "owner", "service run", "status", "replicas"], r.data.map(m => {
+      const run = byModel[m.id];
+      return [`<a href="#models/${encodeURIComponent(m.id)}">${esc(m.id)}</a>`, esc(m.owned_by),
+              run ? `<a href="#runs/${encodeURIComponent(run.run_spec.run_name)}">${esc(run.run_spec.run_name)}</a>` : "",
+              run ? st(run.status) : "", run ? String(new Set((run.jobs || []).filter(j => j.job_submissions.at(-1)?.status === "running").map(j => j.job_spec.replica_num)).size) : ""];
+    })) + chatBox(r.data.map(m => m.id));
+    bindChat();
+  },
+
+  async model(name) {
+    // model details: the service run behind it, its replicas, the OpenAI-compatible endpoint, a chat
+    const runs = await api("/api/runs/list", { project_name: S.project, only_active: false, limit: 100 });
+    const run = runs.find(x => x.service && x.service.model && x.service.model.name === name);
+    const m = run ? run.service.model : { name };
+    const base = `${location.origin}/proxy/models/${encodeURIComponent(S.project)}`;
+    const replicas = run ? (run.jobs || []).map(j => { const sub = j.job_submissions.at(-1) || {}; const jpd = sub.job_provisioning_data;
+      return [String(j.job_spec.replica_num), st(sub.status), jpd ? esc(jpd.hostname || "") : "", res(jpd), ago(sub.submitted_at)]; }) : [];
+    const conf = run ? run.run_spec.configuration : {};
+    $("#main").innerHTML = `<h3><a href="#models" class="muted">models</a> / ${esc(name)}</h3>` +
+      table(["field", "value"], [["format", esc(m.format || m.type || "openai")], ["endpoint", `<code>${esc(base)}</code>`],
+        ["service run", run ? `<a href="#runs/${encodeURIComponent(run.run_spec.run_name)}">${esc(run.run_spec.run_name)}</a> ${st(run.status)}` : "<span class=muted>none</span>"],
+        ["service url", run && run.service.url ? `<a href="${esc(run.service.url)}">${esc(run.service.url)}</a>` : ""],
+        ["replicas (min..max)", conf.replicas ? esc(JSON.stringify(conf.replicas)) : "1"],
+        ["scaling", conf.scaling ? `${esc(conf.scaling.metric)} target ${esc(conf.scaling.target)}` : "manual"],
+        ["resources", conf.resources ? esc(yamlish(conf.resources).trim().replace(/\n/g, " ")) : ""]]) +
+      `<h4>Replicas</h4>` + table(["replica", "status", "host", "resources", "submitted"], replicas) +
+      `<h4>Use it</h4><pre>curl ${esc(base)}/chat/completions \\
+  -H "Authorization: Bearer &lt;token&gt;" -H "Content-Type: application/json" \\
+  -d '{"model": "${esc(name)}", "messages": [{"role": "user", "content": "Hello"}]}'</pre>` + chatBox([name]);
+    bindChat();
   },
 });
+
+// OpenAI chat against the project's model proxy (shared by the models list and a model's page)
+function chatBox(models) {
+  return `<h4>Chat</h4><div class="row"><select id="m">${models.map(m => `<option>${esc(m)}</option>`).join("")}</select>
+    <input id="q" size="60" placeholder="message"><input id="mt" size="5" value="256" title="max tokens"><button class="primary" id="send">Send</button></div><pre id="a"></pre>`;
+}
+function bindChat() {
+  const history = [];
+  $("#send").onclick = async () => {
+    history.push({ role: "user", content: $("#q").value });
+    $("#a").textContent = history.map(m => `${m.role}: ${m.content}`).join("\n\n") + "\n\nassistant: …";
+    const d = await fetch(`/proxy/models/${encodeURIComponent(S.project)}/chat/completions`, { method: "POST",
+      headers: { "Authorization": "Bearer " + S.token, "Content-Type": "application/json" },
+      body: JSON.stringify({ model: $("#m").value, messages: history, max_tokens: +$("#mt").value || 256 }) }).then(r => r.json());
+    const answer = d.choices ? d.choices[0].message.content : JSON.stringify(d, null, 1);
+    history.push({ role: "assistant", content: answer });
+    $("#a").textContent = history.map(m => `${m.role}: ${m.content}`).join("\n\n"); $("#q").value = "";
+  };
+}

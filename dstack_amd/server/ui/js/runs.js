@@ -5,7 +5,10 @@ Object.assign(VIEWS, {
   async runs(name, tab) {
     if (name) return VIEWS.run(name, tab);
     const f = JSON.parse(localStorage.getItem("dstack_runs_filter") || '{"active":false,"status":"","type":"","q":"","refresh":true}');
-    const body = (extra = {}) => ({ project_name: S.project, limit: 50, only_active: f.active, ...extra });
+    // list preferences (the reference's table preferences): page size and visible columns
+    const ALL_COLS = ["name", "type", "user", "backend", "resources", "price/h", "cost", "status", "submitted"];
+    const pref = Object.assign({ page: 50, cols: ALL_COLS }, JSON.parse(localStorage.getItem("dstack_runs_prefs") || "{}"));
+    const body = (extra = {}) => ({ project_name: S.project, limit: pref.page, only_active: f.active, ...extra });
     let runs = await api("/api/runs/list", body());
     const shown = () => runs.filter(r => (!f.status || r.status === f.status) && (!f.type || r.run_spec.configuration.type === f.type) &&
       (!f.q || (r.run_spec.run_name + " " + r.user).toLowerCase().includes(f.q.toLowerCase())));
@@ -16,14 +19,22 @@ Object.assign(VIEWS, {
         <select id="fs">${RUN_STATUSES.map(s => `<option value="${s}" ${s === f.status ? "selected" : ""}>${s || "any status"}</option>`).join("")}</select>
         <select id="ft">${["", "task", "service", "dev-environment"].map(s => `<option value="${s}" ${s === f.type ? "selected" : ""}>${s || "any type"}</option>`).join("")}</select>
         <input id="fq" placeholder="name or user" value="${esc(f.q)}"><label><input type="checkbox" id="fr" ${f.refresh ? "checked" : ""}> auto-refresh</label>
-        <a href="#apply" class="muted">+ new run</a></div>` +
-        table(["name", "type", "user", "backend", "resources", "price/h", "cost", "status", "submitted"], rows.map(r => {
+        <a href="#apply" class="muted">+ new run</a> <a id="prefs" class="muted">[preferences]</a></div>
+        <div id="prefbox" class="row" hidden>page size <select id="pg">${[10, 25, 50, 100].map(n => `<option ${n === pref.page ? "selected" : ""}>${n}</option>`).join("")}</select>
+          ${ALL_COLS.map(c => `<label><input type="checkbox" class="pc" value="${c}" ${pref.cols.includes(c) ? "checked" : ""}> ${c}</label>`).join(" ")}</div>` +
+        table(pref.cols, rows.map(r => {
           const j = r.latest_job_submission || {}; const jpd = j.job_provisioning_data;
-          return [esc(r.run_spec.run_name), esc(r.run_spec.configuration.type), esc(r.user), jpd ? esc(jpd.backend) : "", res(jpd),
-                  jpd ? "$" + (+jpd.price).toFixed(2) : "", "$" + (+r.cost || 0).toFixed(2), st(r.status) + (r.error ? ` <span class="err">${esc(r.error)}</span>` : ""), ago(r.submitted_at)];
-        }), true) + (runs.length && runs.length % 50 === 0 ? `<div class="row"><button id="more">Load more</button></div>` : "");
+          const cell = { name: esc(r.run_spec.run_name), type: esc(r.run_spec.configuration.type), user: esc(r.user), backend: jpd ? esc(jpd.backend) : "",
+            resources: res(jpd), "price/h": jpd ? "$" + (+jpd.price).toFixed(2) : "", cost: "$" + (+r.cost || 0).toFixed(2),
+            status: st(r.status) + (r.error ? ` <span class="err">${esc(r.error)}</span>` : ""), submitted: ago(r.submitted_at) };
+          return pref.cols.map(c => cell[c]);
+        }), true) + (runs.length && runs.length % pref.page === 0 ? `<div class="row"><button id="more">Load more</button></div>` : "");
       bindRows(rows, r => location.hash = "#runs/" + encodeURIComponent(r.run_spec.run_name));
       const save = () => localStorage.setItem("dstack_runs_filter", JSON.stringify(f));
+      const savePrefs = () => { localStorage.setItem("dstack_runs_prefs", JSON.stringify(pref)); route(); };
+      $("#prefs").onclick = () => { $("#prefbox").hidden = !$("#prefbox").hidden; };
+      $("#pg").onchange = () => { pref.page = +$("#pg").value; savePrefs(); };
+      $$(".pc").forEach(cb => cb.onchange = () => { pref.cols = ALL_COLS.filter(c => $$(".pc").find(x => x.value === c).checked); savePrefs(); });
       $("#act").onchange = () => { f.active = $("#act").checked; save(); route(); };
       $("#fs").onchange = () => { f.status = $("#fs").value; save(); render(); };
       $("#ft").onchange = () => { f.type = $("#ft").value; save(); render(); };
@@ -39,7 +50,7 @@ Object.assign(VIEWS, {
     if (f.refresh) timers.push(setInterval(async () => {
       if (document.activeElement === $("#fq")) return;
       const fresh = await api("/api/runs/list", body()).catch(() => null);
-      if (fresh && runs.length <= 50) { runs = fresh; render(); }
+      if (fresh && runs.length <= pref.page) { runs = fresh; render(); }
     }, 5000));
   },
 
