@@ -52,6 +52,8 @@ bool dsa_gemm_nt_swiglu_supported(int, int, int);
 hipError_t dsa_gemm_nt_trace(const void*, const void*, void*, int, int, int, unsigned long long*, hipStream_t);
 hipError_t dsa_gemm_nt_swiglu(const void*, const void*, void*, void*, void*, int, int, int, long, long, hipStream_t);
 bool dsa_gemm_nt_swiglu_bwd_supported(int, int, int);
+bool dsa_gemm_km_supported(int, int, int);
+hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 hipError_t dsa_gemm_nt_swiglu_bwd(const void*, const void*, const void*, void*, void*, int, int, int, long, long,
                                   hipStream_t);
 }
@@ -413,8 +415,25 @@ torch::Tensor gemm_nt_trace(torch::Tensor a, torch::Tensor b, torch::Tensor out)
   return tr;
 }
 
-// gu = x w^T (w = [gate; up] [2F][K]) -> (gu [T][2F], a = silu(g) * u [T][F], a^T [F][T])
-std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor x, torch::Tensor w) {
+bool gemm_km_supported(int64_t M, int64_t N, int64_t K) { return dsa_gemm_km_supported(M, N, K); }
+
+// out[M][N] (+)= a[K][M]^T b[K][N]  (csrc/gemm_nt.hip KM form: dW = dY^T X, token-major operands);
+// mode 2 = timing-only
+void gemm_km(torch::Tensor a, torch::Tensor b, torch::Tensor out, int64_t mode) {
+  check_rows(a, "gemm_km");
+  check_rows(b, "gemm_km");
+  check_rows(out, "gemm_km");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "gemm_km: shape mismatch");
+  TORCH_CHECK(dsa_gemm_km_supported(M, N, K), "gemm_km: M % 256, N % 256, K % 128 must be 0");
+  check(dsa_gemm_km(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0),
+                    (int)mode, stream()),
+        "gemm_km");
+}
+
+// gu = x w^T (w = [gate; up] [2F][K]) -> (gu [T][2F], a = silu(g) * u [T][F], a^T [F][T]); with
+// transposed = false a^T is not written (returned empty)
+std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor x, torch::Tensor w, bool transposed) {
   check_rows(x, "gemm_nt_swiglu");
   check_rows(w, "gemm_nt_swiglu");
   const int64_t T = x.size(0), K = x.size(1), F = w.size(0) / 2;
@@ -422,8 +441,8 @@ std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor x, torch::Tensor w) {
   TORCH_CHECK(dsa_gemm_nt_swiglu_supported(T, F, K), "gemm_nt_swiglu: T % 256, F % 128, K % 128 must be 0");
   auto gu = torch::empty({T, 2 * F}, x.options());
   auto a = torch::empty({T, F}, x.options());
-  auto aT = torch::empty({F, T}, x.options());
-  check(dsa_gemm_nt_swiglu(x.data_ptr(), w.data_ptr(), gu.data_ptr(), a.data_ptr(), aT.data_ptr(), T, F, K,
+  auto aT = transposed ? torch::empty({F, T}, x.options()) : torch::empty({0}, x.options());
+  check(dsa_gemm_nt_swiglu(x.data_ptr(), w.data_ptr(), gu.data_ptr(), a.data_ptr(), transposed ? aT.data_ptr() : nullptr, T, F, K,
                            x.stride(0), w.stride(0), stream()),
         "gemm_nt_swiglu");
   return {gu, a, aT};
@@ -434,7 +453,7 @@ bool gemm_nt_swiglu_bwd_supported(int64_t T, int64_t F, int64_t K) {
 }
 
 // da = dy wdT^T (wdT = W_down^T [F][K]) fused with the SwiGLU backward -> (dgu [T][2F], dgu^T [2F][T])
-std::vector<torch::Tensor> gemm_nt_swiglu_bwd(torch::Tensor dy, torch::Tensor wdT, torch::Tensor gu) {
+std::vector<torch::Tensor> gemm_nt_swiglu_bwd(torch::Tensor dy, torch::Tensor wdT, torch::Tensor gu, bool transposed) {
   check_rows(dy, "gemm_nt_swiglu_bwd");
   check_rows(wdT, "gemm_nt_swiglu_bwd");
   const int64_t T = dy.size(0), K = dy.size(1), F = wdT.size(0);
@@ -443,8 +462,8 @@ std::vector<torch::Tensor> gemm_nt_swiglu_bwd(torch::Tensor dy, torch::Tensor wd
               "gemm_nt_swiglu_bwd: gu must be a contiguous bf16 [T, 2F]");
   TORCH_CHECK(dsa_gemm_nt_swiglu_bwd_supported(T, F, K), "gemm_nt_swiglu_bwd: T % 256, F % 256, K % 128 must be 0");
   auto dgu = torch::empty({T, 2 * F}, dy.options());
-  auto dguT = torch::empty({2 * F, T}, dy.options());
-  check(dsa_gemm_nt_swiglu_bwd(dy.data_ptr(), wdT.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), T, F,
+  auto dguT = transposed ? torch::empty({2 * F, T}, dy.options()) : torch::empty({0}, dy.options());
+  check(dsa_gemm_nt_swiglu_bwd(dy.data_ptr(), wdT.data_ptr(), gu.data_ptr(), dgu.data_ptr(), transposed ? dguT.data_ptr() : nullptr, T, F,
                                K, dy.stride(0), wdT.stride(0), stream()),
         "gemm_nt_swiglu_bwd");
   return {dgu, dguT};
@@ -589,10 +608,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt);
   m.def("gemm_nt_mode", &gemm_nt_mode);
   m.def("gemm_nt_supported", &gemm_nt_supported);
-  m.def("gemm_nt_swiglu", &gemm_nt_swiglu);
+  m.def("gemm_nt_swiglu", &gemm_nt_swiglu, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("transposed") = true);
+  m.def("gemm_km", &gemm_km, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("out"), pybind11::arg("mode") = 0);
+  m.def("gemm_km_supported", &gemm_km_supported);
   m.def("gemm_nt_trace", &gemm_nt_trace);
   m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);
-  m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd);
+  m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd, pybind11::arg("dy"), pybind11::arg("wdT"), pybind11::arg("gu"),
+        pybind11::arg("transposed") = true);
   m.def("gemm_nt_swiglu_bwd_supported", &gemm_nt_swiglu_bwd_supported);
   m.def("gemv", &gemv);
   m.def("gemv_supported", &gemv_supported);

@@ -31,6 +31,16 @@
 //
 // The SwiGLU tile maps its 256 columns to gate columns [f0, f0+128) (b0) and up columns
 // [F+f0, F+f0+128) (b1): a lane holds g and u of the same (t, f) in accumulators n and n+2.
+//
+// KM form (weight gradients, C[M][N] (+)= A[K][M]^T B[K][N]: dW = dY^T X with both operands
+// token-major, as the forward and the input gradient leave them -- no transposed copies): the same
+// kernel with the units filled as 64 k-rows x 128 columns (256-byte rows, LDS-DMA from the
+// [K][M] / [K][N] rows) and the fragments read with ds_read_b64_tr_b16 (gfx950's transposed LDS
+// read): two reads of a 4-k x 16-column block give a lane 8 consecutive k of one column, the
+// fragment the row read gives in the NT form.  Chunk c of k-row r sits at c ^ 2((r & 3) | (r & 8) >> 1):
+// a 32-lane half reads 8 rows (4 per 16-lane group, the groups 8 rows apart) x 32 bytes, and the
+// XOR puts them on 8 different 32-byte bank windows.  The XOR depends only on the lane, so the
+// k-half and the 4-row step of a read are immediate offsets; each 16-column block has one address.
 #include <stdlib.h>
 
 #include "mfma_tiles.h"
@@ -50,7 +60,11 @@ constexpr int NT_LDS = 2 * BUF + 2 * 16384;  // 160 KiB: ring + room for the Swi
 
 // EPI_NONE: timing-only build (the accumulators are kept live, nothing is stored): what the
 // epilogue's stores cost (tools/diag, accumulate = 2 in dsa_gemm_nt)
-enum Epi { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU = 2, EPI_SWIGLU_BWD = 3, EPI_NONE = 4 };
+// EPI_SWIGLU_R / EPI_SWIGLU_BWD_R: the SwiGLU epilogues without the transposed copies (a^T, dgu^T),
+// for a step whose weight gradients take the token-major operands (KM form): barrier-free, so the
+// groups stay staggered as in the plain epilogue.
+enum Epi { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU = 2, EPI_SWIGLU_BWD = 3, EPI_NONE = 4, EPI_SWIGLU_R = 5,
+           EPI_SWIGLU_BWD_R = 6 };
 
 struct NTArgs {
   const bf16_t* A;
@@ -186,6 +200,32 @@ __device__ __forceinline__ void nt_read_b(bf16x8 (&bf)[2][2][2], const char* buf
   }
 }
 
+// KM form: the same fragments by transposed reads.  ka[mi] / kb[n]: the lane's byte offset of its
+// 4-k x 16-column block for k-half 0, first 4 rows; +8192 selects k-half 1, +1024 the next 4 rows.
+__device__ __forceinline__ bf16x8 km_frag(const char* p) {
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(bf16x4, p));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS3(bf16x4, p + 1024));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int MS>
+__device__ __forceinline__ void km_read_a(bf16x8 (&af)[4][2], const char* buf, const int (&ka)[4]) {
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    af[mi][0] = km_frag(buf + MS * UNIT + ka[mi]);
+    af[mi][1] = km_frag(buf + MS * UNIT + ka[mi] + 8192);
+  }
+}
+
+template <int NS>
+__device__ __forceinline__ void km_read_b(bf16x8 (&bf)[2][2][2], const char* buf, const int (&kb)[2]) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    bf[NS][n][0] = km_frag(buf + (2 + NS) * UNIT + kb[n]);
+    bf[NS][n][1] = km_frag(buf + (2 + NS) * UNIT + kb[n] + 8192);
+  }
+}
+
 }  // namespace
 
 // Tile origin (first row of A/C, first B row of the tile's first 128 columns) of logical tile t.
@@ -198,7 +238,7 @@ __device__ __forceinline__ void nt_tile_origin(const NTArgs& p, int t, int& m0, 
   nb0 = ((t % in_group) / gm) * p.nstride;
 }
 
-template <int EPI, bool TRACE = false>
+template <int EPI, bool TRACE = false, bool KM = false>
 __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // the plain epilogues store straight from the accumulators while the next tile's prologue DMA
@@ -206,11 +246,11 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   // the plain and SwiGLU-forward epilogues store straight from the accumulators (a^T through the
   // 32 KiB of LDS above the ring) while the next tile's first K-tiles stream into the ring; the
   // SwiGLU backward stages whole tiles through LDS and reloads afterwards
-  constexpr bool OVERLAP = EPI == EPI_STORE || EPI == EPI_ACC || EPI == EPI_SWIGLU || EPI == EPI_NONE;
+  constexpr bool OVERLAP = EPI != EPI_SWIGLU_BWD;
   // barrier-free epilogues keep the two wave groups staggered across tiles: group 0 stores its
   // half of the tile while group 1 issues its last MFMAs, group 1 stores while group 0 runs the
   // next tile's first MFMAs -- the stores take the place of a memory segment of the ping-pong
-  constexpr bool STAGGERED = EPI == EPI_STORE || EPI == EPI_ACC || EPI == EPI_NONE;
+  constexpr bool STAGGERED = EPI != EPI_SWIGLU && EPI != EPI_SWIGLU_BWD;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;
   // TRACE: waves 0 and 4 of workgroup 0 stamp every phase boundary of K-iterations 8..11 into
@@ -249,27 +289,44 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   unsigned va[2], vb[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int r = 16 * w + 8 * i + (lane >> 3);
-    const int ch = (lane & 7) ^ (4 * i + (lane >> 4));
-    va[i] = (unsigned)((r * p.lda + ch * 8) * 2);
-    vb[i] = (unsigned)((r * p.ldb + ch * 8) * 2);
+    if constexpr (KM) {
+      // piece i = k-rows 8w + 4i + (lane >> 4), lane's 16 B slot (lane & 15) holds chunk
+      // (lane & 15) ^ 2((r & 3) | (r & 8) >> 1)
+      const int r = 8 * w + 4 * i + (lane >> 4);
+      const int ch = (lane & 15) ^ (2 * ((r & 3) | ((r >> 1) & 4)));
+      va[i] = (unsigned)((r * p.lda + ch * 8) * 2);
+      vb[i] = (unsigned)((r * p.ldb + ch * 8) * 2);
+    } else {
+      const int r = 16 * w + 8 * i + (lane >> 3);
+      const int ch = (lane & 7) ^ (4 * i + (lane >> 4));
+      va[i] = (unsigned)((r * p.lda + ch * 8) * 2);
+      vb[i] = (unsigned)((r * p.ldb + ch * 8) * 2);
+    }
   }
   const unsigned lds0 = (unsigned)(uintptr_t)LDS3(char, smem) + (unsigned)(w * 2048);
   const bf16_t *a_src0, *a_src1, *b_src0, *b_src1;
   auto set_src = [&](int tm0, int tnb0) {
-    a_src0 = p.A + (long)tm0 * p.lda;
-    a_src1 = p.A + (long)(tm0 + 128) * p.lda;
-    b_src0 = p.B + (long)tnb0 * p.ldb;
-    b_src1 = p.B + (long)(tnb0 + p.bsplit) * p.ldb;
+    if constexpr (KM) {  // the tile's columns of the [K][M] / [K][N] rows
+      a_src0 = p.A + tm0;
+      a_src1 = p.A + tm0 + 128;
+      b_src0 = p.B + tnb0;
+      b_src1 = p.B + tnb0 + p.bsplit;
+    } else {
+      a_src0 = p.A + (long)tm0 * p.lda;
+      a_src1 = p.A + (long)(tm0 + 128) * p.lda;
+      b_src0 = p.B + (long)tnb0 * p.ldb;
+      b_src1 = p.B + (long)(tnb0 + p.bsplit) * p.ldb;
+    }
   };
   // units: 0 = a0, 1 = a1, 2 = b0, 3 = b1 of K-tile kt, into ring slot kt & 1
   auto dma = [&](int unit, int kt) {
     const unsigned dst = lds0 + (unsigned)((kt & 1) * BUF + unit * UNIT);
-    const long ko = (long)kt * NT_BK;
-    if (unit == 0) nt_dma(a_src0 + ko, va[0], va[1], dst);
-    else if (unit == 1) nt_dma(a_src1 + ko, va[0], va[1], dst);
-    else if (unit == 2) nt_dma(b_src0 + ko, vb[0], vb[1], dst);
-    else nt_dma(b_src1 + ko, vb[0], vb[1], dst);
+    const long ka = KM ? (long)kt * NT_BK * p.lda : (long)kt * NT_BK;
+    const long kb = KM ? (long)kt * NT_BK * p.ldb : (long)kt * NT_BK;
+    if (unit == 0) nt_dma(a_src0 + ka, va[0], va[1], dst);
+    else if (unit == 1) nt_dma(a_src1 + ka, va[0], va[1], dst);
+    else if (unit == 2) nt_dma(b_src0 + kb, vb[0], vb[1], dst);
+    else nt_dma(b_src1 + kb, vb[0], vb[1], dst);
   };
   // K-tile 0 whole and K-tile 1's b0, b1 (its a0, a1 are the first phase's DMA): 12 instructions
   auto prologue = [&]() {
@@ -289,10 +346,35 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   const int rb0 = 32 * wc * 128 + rrow + 16 * c0, rb1 = 32 * wc * 128 + rrow + 16 * c1;
   const char* bufE = smem;
   const char* bufO = smem + BUF;
-  const int er = lane & 15, ec = 4 * (lane >> 4);
-
   f32x4 acc[2][4][4];
   bf16x8 af[4][2], bf[2][2][2];
+  const int er = lane & 15, ec = 4 * (lane >> 4);
+  // KM form: lane 4q + p of 16-lane group g addresses k-row 8g + q, columns 16j + 4p .. +3 of
+  // block j (the chunk pair j ^ (q | (g & 1) << 2))
+  int ka[4], kb[2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, x = q | ((g & 1) << 2);
+    const int row = (8 * g + q) * 256 + 8 * pp;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) ka[mi] = row + 32 * ((4 * wr + mi) ^ x);
+#pragma unroll
+    for (int n = 0; n < 2; ++n) kb[n] = row + 32 * ((2 * wc + n) ^ x);
+  }
+  auto read_a0 = [&](const char* buf) {
+    if constexpr (KM) km_read_a<0>(af, buf, ka); else nt_read_a<0>(af, buf, ra0, ra1);
+  };
+  auto read_a1 = [&](const char* buf) {
+    if constexpr (KM) km_read_a<1>(af, buf, ka); else nt_read_a<1>(af, buf, ra0, ra1);
+  };
+  auto read_b = [&](const char* buf) {
+    if constexpr (KM) {
+      km_read_b<0>(bf, buf, kb);
+      km_read_b<1>(bf, buf, kb);
+    } else {
+      nt_read_b<0>(bf, buf, rb0, rb1);
+      nt_read_b<1>(bf, buf, rb0, rb1);
+    }
+  };
 
   set_src(m0, nb0);
   prologue();
@@ -329,9 +411,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       const int t2 = more ? t + 2 : 0, t3 = more ? t + 3 : 1;
       // P1: m-subtile 0 of tile t
       stamp(it);
-      nt_read_b<0>(bf, bufE, rb0, rb1);
-      nt_read_b<1>(bf, bufE, rb0, rb1);
-      nt_read_a<0>(af, bufE, ra0, ra1);
+      read_b(bufE);
+      read_a0(bufE);
       dma(0, t + 1);
       dma(1, t + 1);
       if (!more && go) set_src(m1, nb1);
@@ -345,7 +426,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       nt_barrier();
       // P2: m-subtile 1 of tile t; retire tile t+1
       stamp(it);
-      nt_read_a<1>(af, bufE, ra0, ra1);
+      read_a1(bufE);
       if (go) {
         dma(2, t2);
         dma(3, t2);
@@ -363,9 +444,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       nt_barrier();
       // P3: m-subtile 0 of tile t+1
       stamp(it);
-      nt_read_b<0>(bf, bufO, rb0, rb1);
-      nt_read_b<1>(bf, bufO, rb0, rb1);
-      nt_read_a<0>(af, bufO, ra0, ra1);
+      read_b(bufO);
+      read_a0(bufO);
       if (go) {
         dma(0, t2);
         dma(1, t2);
@@ -380,7 +460,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       nt_barrier();
       // P4: m-subtile 1 of tile t+1; retire tile t+2
       stamp(it);
-      nt_read_a<1>(af, bufO, ra0, ra1);
+      read_a1(bufO);
       if (go) {
         dma(2, t3);
         dma(3, t3);
@@ -457,6 +537,65 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
               *reinterpret_cast<us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit) = nt_pair8(x, y);
             }
       }
+    } else if constexpr (EPI == EPI_SWIGLU_R) {
+      // gu and a straight from the accumulators, no transposed copy
+      const int q = lane >> 4;
+      const int pc = 16 * (q & 1) + 8 * (q >> 1);
+      bf16_t* gbase = p.C + (long)(m0 + 64 * wr + er) * p.ldc + nb0 + 32 * wc + pc;
+      bf16_t* abase = p.C2 + (long)(m0 + 64 * wr + er) * p.F + nb0 + 32 * wc + pc;
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          us4 g4[2], u4[2], o4[2];
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              g4[n][j] = f2bf(acc[ms][mi][n][j]);
+              u4[n][j] = f2bf(acc[ms][mi][n + 2][j]);
+              o4[n][j] = f2bf(silu(bf2f(g4[n][j])) * bf2f(u4[n][j]));
+            }
+          const long ro = (long)(128 * ms + 16 * mi);
+          *reinterpret_cast<us8*>(gbase + ro * p.ldc) = nt_pair8(g4[0], g4[1]);
+          *reinterpret_cast<us8*>(gbase + ro * p.ldc + p.bsplit) = nt_pair8(u4[0], u4[1]);
+          *reinterpret_cast<us8*>(abase + ro * p.F) = nt_pair8(o4[0], o4[1]);
+        }
+    } else if constexpr (EPI == EPI_SWIGLU_BWD_R) {
+      // acc = da[t][f] (plain column map); 16-byte pieces of 8 consecutive f: g, u loaded, dg, du
+      // stored -- dg = da * u * silu'(g), du = da * silu(g), da rounded to bf16 as the unfused path
+      const int q = lane >> 4;
+      const int pc = 32 * wc + 16 * (q & 1) + 8 * (q >> 1);
+      const long rbase = (long)(m0 + 64 * wr + er) * (2L * p.F) + nb0 + pc;
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const long ro = rbase + (long)(128 * ms + 16 * mi) * (2L * p.F);
+          us8 g8[2], u8[2];
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            g8[pp] = *reinterpret_cast<const us8*>(p.G + ro + 128 * pp);
+            u8[pp] = *reinterpret_cast<const us8*>(p.G + ro + 128 * pp + p.F);
+          }
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            float v[8];
+            nt_pair8f(acc[ms][mi][2 * pp], acc[ms][mi][2 * pp + 1], v);
+            us8 dg, du;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float da = bf2f(f2bf(v[j]));
+              const float g = bf2f(g8[pp][j]), u = bf2f(u8[pp][j]);
+              const float sg = 1.f / (1.f + __expf(-g));
+              const float sl = g * sg;
+              dg[j] = f2bf(da * u * (sg + sl * (1.f - sg)));
+              du[j] = f2bf(da * sl);
+            }
+            *reinterpret_cast<us8*>(p.C + ro + 128 * pp) = dg;
+            *reinterpret_cast<us8*>(p.C + ro + 128 * pp + p.F) = du;
+          }
+        }
     } else if constexpr (EPI == EPI_SWIGLU) {
       // gu and a = silu(g) * u (from the bf16-rounded g, u: what the backward re-reads from gu)
       // straight from the accumulators; a^T through the spare LDS, one 128-token half at a time
@@ -608,11 +747,11 @@ int nt_cus() {
 
 // One workgroup per CU (128 KiB ring): a grid of min(tiles, CUs rounded down to a multiple of 8)
 // workgroups that loop over their XCD's tiles.
-template <int EPI, bool TRACE = false>
+template <int EPI, bool TRACE = false, bool KM = false>
 hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, TRACE>),
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, TRACE, KM>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, NT_LDS));
     attr = true;
   }
@@ -624,7 +763,7 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
     a.wg_per_xcd = cap / 8;
   }
   if (const char* g = getenv("DSTACK_AMD_GEMM_NT_GROUP")) a.group = atoi(g) > 0 ? atoi(g) : a.group;
-  gemm_nt_kernel<EPI, TRACE><<<grid, 512, NT_LDS, st>>>(a);
+  gemm_nt_kernel<EPI, TRACE, KM><<<grid, 512, NT_LDS, st>>>(a);
   return hipGetLastError();
 }
 
@@ -693,7 +832,7 @@ extern "C" hipError_t dsa_gemm_nt_swiglu(const void* X, const void* W, void* gu,
   a.B = (const bf16_t*)W;
   a.C = (bf16_t*)gu;
   a.C2 = (bf16_t*)a_out;
-  a.C3 = (bf16_t*)aT;
+  a.C3 = (bf16_t*)aT;  // null: no a^T (EPI_SWIGLU_R)
   a.lda = ldx;
   a.ldb = ldw;
   a.ldc = 2L * F;
@@ -704,6 +843,7 @@ extern "C" hipError_t dsa_gemm_nt_swiglu(const void* X, const void* W, void* gu,
   a.nstride = 128;
   a.bsplit = F;
   a.group = nt_group(T / NT_BM, F / 128);
+  if (!aT) return nt_launch<EPI_SWIGLU_R>(a, (T / NT_BM) * (F / 128), st);
   return nt_launch<EPI_SWIGLU>(a, (T / NT_BM) * (F / 128), st);
 }
 
@@ -733,5 +873,33 @@ extern "C" hipError_t dsa_gemm_nt_swiglu_bwd(const void* dY, const void* WdT, co
   a.nstride = NT_BN;
   a.bsplit = 128;
   a.group = nt_group(T / NT_BM, F / NT_BN);
+  if (!dguT) return nt_launch<EPI_SWIGLU_BWD_R>(a, (T / NT_BM) * (F / NT_BN), st);
   return nt_launch<EPI_SWIGLU_BWD>(a, (T / NT_BM) * (F / NT_BN), st);
+}
+
+extern "C" bool dsa_gemm_km_supported(int M, int N, int K) { return nt_shape_ok(M, N, K); }
+
+// KM form: C[M][N] (+)= A[K][M]^T B[K][N] (weight gradient dW = dY^T X of token-major dY, X).
+// Leading dimensions (row strides of A, B, C) in elements, multiples of 8.
+extern "C" hipError_t dsa_gemm_km(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
+                                  long ldc, int accumulate, hipStream_t st) {
+  if (!nt_shape_ok(M, N, K) || lda % 8 || ldb % 8 || ldc % 4 || lda < M || ldb < N || ldc < N)
+    return hipErrorInvalidValue;
+  if (63L * lda * 2 + 512 > 0xffffffffL || 63L * ldb * 2 + 512 > 0xffffffffL) return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (bf16_t*)C;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.M = M;
+  a.K = K;
+  a.ntn = N / NT_BN;
+  a.nstride = NT_BN;
+  a.bsplit = 128;
+  a.group = nt_group(M / NT_BM, N / NT_BN);
+  const int tiles = (M / NT_BM) * (N / NT_BN);
+  if (accumulate == 2) return nt_launch<EPI_NONE, false, true>(a, tiles, st);
+  return accumulate ? nt_launch<EPI_ACC, false, true>(a, tiles, st) : nt_launch<EPI_STORE, false, true>(a, tiles, st);
 }

@@ -146,46 +146,51 @@ class _SwiGLUMLP(torch.autograd.Function):
     def forward(ctx, h, wgu, wdown):
         C = _ext.require()
         h2 = _2d(h)
-        gu, a, aT = C.gemm_nt_swiglu(h2, wgu)
+        # KM weight gradients take a and dgu token-major: no transposed copies from the epilogues
+        ctx.km = _wgrad_mode() == "km"
+        gu, a, aT = C.gemm_nt_swiglu(h2, wgu, not ctx.km)
         y = a @ wdown.t()
-        ctx.save_for_backward(h2, gu, aT, wgu, wdown)
+        ctx.save_for_backward(h2, gu, a if ctx.km else aT, wgu, wdown)
         ctx.hshape = h.shape
         return y.view(*h.shape[:-1], wdown.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
-        h2, gu, aT, wgu, wdown = ctx.saved_tensors
+        h2, gu, a_or_aT, wgu, wdown = ctx.saved_tensors
         dy2 = _2d(dy.contiguous())
         # down projection weight gradient dW = dy^T a  (a^T already written by the forward)
         gwd = None
-        a_op, b_op = wgrad_operands(dy2, None, xT=aT)
+        if ctx.km:
+            a_op, b_op = wgrad_operands(dy2, a_or_aT)
+        else:
+            a_op, b_op = wgrad_operands(dy2, None, xT=a_or_aT)
         sink = getattr(wdown, "_dsa_grad_sink", None)
         if sink is not None:
             sink(wdown, a_op, b_op)
         else:
-            gwd = a_op @ b_op
+            gwd = mm_into(a_op, b_op)
         # da = dy Wdown with the SwiGLU backward fused: dgu, dgu^T
         wdT = _transposed_weight(wdown)
         if wdT is None:
             wdT = wdown.t().contiguous()
-        dgu, dguT = C.gemm_nt_swiglu_bwd(dy2, wdT, gu)
+        dgu, dguT = C.gemm_nt_swiglu_bwd(dy2, wdT, gu, not ctx.km)
         # dx = dgu W_gu
         wguT = _transposed_weight(wgu)
         dx = dgu @ (wguT.t() if wguT is not None else wgu)
         # gate/up weight gradient dW_gu = dgu^T h  (dgu^T from the fused epilogue)
         ggu = None
-        a_op, b_op = wgrad_operands(dgu, h2, gT=dguT)
+        a_op, b_op = wgrad_operands(dgu, h2, gT=None if ctx.km else dguT)
         sink = getattr(wgu, "_dsa_grad_sink", None)
         if sink is not None:
             sink(wgu, a_op, b_op)
         else:
-            ggu = a_op @ b_op
+            ggu = mm_into(a_op, b_op)
         return dx.view(ctx.hshape), ggu, gwd
 
 
 def _mlp_fused_ok(h: torch.Tensor, wgu: torch.Tensor, wdown: torch.Tensor) -> bool:
-    if os.environ.get("DSTACK_AMD_MLP_FUSED", "1") == "0" or _wgrad_mode() != "auto":
+    if os.environ.get("DSTACK_AMD_MLP_FUSED", "1") == "0" or _wgrad_mode() not in ("auto", "km"):
         return False
     if h.dtype != torch.bfloat16 or wgu.dtype != torch.bfloat16 or wdown.dtype != torch.bfloat16:
         return False
@@ -353,7 +358,7 @@ class _Linear(torch.autograd.Function):
             a, b = wgrad_operands(g2, xs.reshape(-1, xs.shape[-1]), gT=gT)
         sink = getattr(w, "_dsa_grad_sink", None)
         if sink is None:
-            return gx, a @ b
+            return gx, mm_into(a, b)
         sink(w, a, b)
         return gx, None
 
@@ -383,7 +388,32 @@ def _transposed_weight(w: torch.Tensor):
 
 
 def _wgrad_mode() -> str:
+    """How weight gradients dW = g^T x get their operands: ``auto`` (token-contiguous copies made by
+    the HIP transpose kernel or written by the producer, hipBLASLt), ``km`` (both operands left
+    token-major, the in-tree GEMM's KM form: no transposes at all), ``strided`` (token-major,
+    hipBLASLt)."""
     return os.environ.get("DSTACK_AMD_WGRAD", "auto").lower()
+
+
+def mm_into(a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = False) -> torch.Tensor:
+    """``out (+)= a @ b`` for a weight gradient's operands (``wgrad_operands``).  When ``a`` is the
+    transposed view of a token-major [T, P] gradient and ``b`` a token-major [T, Q] input, the
+    in-tree KM-form GEMM runs it (csrc/gemm_nt.hip, ``gemm_km``); other layouts go to the library."""
+    if out is None:
+        out = torch.empty(a.shape[0], b.shape[1], device=a.device, dtype=torch.result_type(a, b))
+    if (a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
+            and _ext.use_hip(a) and a.stride(0) == 1 and b.stride(1) == 1 and out.stride(1) == 1
+            and a.shape[1] == b.shape[0]):
+        C = _ext.require()
+        g = a.t()
+        if (C.gemm_km_supported(a.shape[0], b.shape[1], a.shape[1]) and g.stride(0) % 8 == 0
+                and b.stride(0) % 8 == 0 and out.stride(0) % 8 == 0
+                and all(t.data_ptr() % 16 == 0 for t in (g, b, out))):
+            C.gemm_km(g, b, out, 1 if accumulate else 0)
+            return out
+    if accumulate:
+        return out.addmm_(a, b)
+    return torch.mm(a, b, out=out)
 
 
 def wgrad_operands(g2: torch.Tensor, x2, xT=None, gT=None):
@@ -403,7 +433,7 @@ def wgrad_operands(g2: torch.Tensor, x2, xT=None, gT=None):
     a = g2.t()
     b = xT.t() if xT is not None else x2
     if not (_ext.use_hip(g2) and _wgrad_mode() == "auto"):
-        return a, b
+        return a, b  # "km" (mm_into's in-tree KM GEMM) and "strided" take the token-major views
     C = _ext.require()
     if xT is None and x2.is_contiguous() and C.transpose2d_supported(T, Q):
         b = C.transpose2d(x2).t()

@@ -193,11 +193,8 @@ class ZeroOptimizer:
     def _direct_grad(self, p: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
         """Weight gradient sink for ``ops.linear``: dW = a @ b (a = g^T [P, T], b = x [T, Q], as
         views in whichever layout ``ops.functional.wgrad_operands`` chose) into the flat buffer."""
-        if p._dsa_fresh:
-            torch.mm(a, b, out=p.grad)
-            p._dsa_fresh = False
-        else:
-            p.grad.addmm_(a, b)
+        ops.functional.mm_into(a, b, p.grad, accumulate=not p._dsa_fresh)
+        p._dsa_fresh = False
         self._direct_ok.add(p)
         if self._hooks_on:
             self._on_grad_ready(p)

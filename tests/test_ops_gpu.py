@@ -596,9 +596,56 @@ def test_gemm_nt_swiglu_bwd_epilogue_matches_fp32(gpu):
     assert torch.equal(dguT, dgu.t().contiguous())
 
 
-def test_swiglu_mlp_fused_matches_separate_kernels(gpu, monkeypatch):
+@pytest.mark.parametrize("M,N,K,accumulate", [(256, 256, 128, False), (768, 512, 384, True),
+                                               (2304, 9472, 256, False), (1024, 4352, 1024, True)])
+def test_gemm_km_matches_fp32(gpu, M, N, K, accumulate):
+    """KM form (weight gradient of token-major operands): C (+)= A^T B for A [K][M], B [K][N],
+    fragments by ds_read_b64_tr_b16, against an fp32 matmul."""
+    C = _ext.require()
+    a, b = _rand(K, M, device=gpu), _rand(K, N, device=gpu, seed=1)
+    out = _rand(M, N, device=gpu, seed=2) if accumulate else torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    ref_ = (out.float() if accumulate else 0) + a.float().t() @ b.float()
+    C.gemm_km(a, b, out, 1 if accumulate else 0)
+    err = ((out.float() - ref_).norm() / ref_.norm()).item()
+    assert err < 5e-3, err
+
+
+def test_gemm_km_strided_operands(gpu):
+    """Row strides wider than M / N (views into wider buffers) for A, B and C."""
+    C = _ext.require()
+    M, N, K = 512, 256, 256
+    A = _rand(K, M + 64, device=gpu)[:, 32:32 + M]
+    B = _rand(K, N + 128, device=gpu, seed=1)[:, :N]
+    Cbig = torch.zeros(M, N + 256, device=gpu, dtype=torch.bfloat16)
+    out = Cbig[:, 128:128 + N]
+    C.gemm_km(A, B, out)
+    ref_ = A.float().t() @ B.float()
+    assert ((out.float() - ref_).norm() / ref_.norm()).item() < 5e-3
+    assert Cbig[:, :128].abs().max().item() == 0 and Cbig[:, 128 + N:].abs().max().item() == 0
+
+
+def test_gemm_nt_swiglu_epilogues_without_transposes(gpu):
+    """The barrier-free SwiGLU epilogues (no a^T / dgu^T) write exactly what the transposing ones do."""
+    C = _ext.require()
+    T, D, F = 1024, 512, 768
+    x, w = _rand(T, D, device=gpu), _rand(2 * F, D, device=gpu, seed=1, scale=0.05)
+    gu, a, _ = C.gemm_nt_swiglu(x, w)
+    gu2, a2, aT2 = C.gemm_nt_swiglu(x, w, False)
+    assert torch.equal(gu, gu2) and torch.equal(a, a2) and aT2.numel() == 0
+    dy, wdT = _rand(T, D, device=gpu, seed=3), _rand(F, D, device=gpu, seed=4, scale=0.05)
+    dgu, _ = C.gemm_nt_swiglu_bwd(dy, wdT, gu)
+    dgu2, dguT2 = C.gemm_nt_swiglu_bwd(dy, wdT, gu, False)
+    assert dguT2.numel() == 0
+    # same formulas; the compiler may contract them differently: at most a bf16 rounding apart
+    assert ((dgu.float() - dgu2.float()).norm() / dgu.float().norm()).item() < 1e-3
+
+
+@pytest.mark.parametrize("wgrad", ["auto", "km"])
+def test_swiglu_mlp_fused_matches_separate_kernels(gpu, monkeypatch, wgrad):
     """ops.swiglu_mlp through the fused GEMM epilogues == linear/swiglu/linear with separate kernels,
-    output and every gradient (no optimizer sinks: the gradients are returned)."""
+    output and every gradient (no optimizer sinks: the gradients are returned); ``km``: weight
+    gradients by the in-tree KM-form GEMM on token-major operands, no transposed copies."""
+    monkeypatch.setenv("DSTACK_AMD_WGRAD", wgrad)
     T, D, F = 512, 512, 1024
     torch.manual_seed(0)
     h0 = _rand(2, T // 2, D, device=gpu)
@@ -615,6 +662,7 @@ def test_swiglu_mlp_fused_matches_separate_kernels(gpu, monkeypatch):
     assert ops.functional._mlp_fused_ok(h0, wgu0, wd0)
     fused = run()
     monkeypatch.setenv("DSTACK_AMD_MLP_FUSED", "0")
+    monkeypatch.setenv("DSTACK_AMD_WGRAD", "auto")
     sep = run()
     for name, a, b in zip(["y", "dh", "dWgu", "dWdown"], fused, sep):
         rel = ((a - b).norm() / (b.norm() + 1e-12)).item()

@@ -5,6 +5,11 @@ against the unfused kernels.
 
     python tools/bench_gemm_nt.py                 # all shapes
     SHAPES=fwd_gu,dgrad_gu python tools/bench_gemm_nt.py
+    SHAPES=km python tools/bench_gemm_nt.py        # weight gradients on token-major operands
+
+km: the KM form (dW = dY^T X with dY, X token-major, ``gemm_km``) against hipBLASLt on the same
+operands (its token-major "TT" form) and against what the step did before: transposes of both
+operands (HIP transpose kernel) + hipBLASLt on the token-contiguous layout.
 """
 import json
 import os
@@ -79,6 +84,37 @@ def main():
         print(name, json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
         del a, b, out
         torch.cuda.empty_cache()
+    if not only or "km" in only.split(","):
+        for name in ("wgrad_qkv", "wgrad_o", "wgrad_gu", "wgrad_down"):
+            M, N, K = SHAPES[name]
+            torch.manual_seed(0)
+            g, x = rand(K, M), rand(K, N)  # token-major dY [T][P], X [T][Q]
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            C.gemm_km(g, x, out)
+            ref = g.float().t() @ x.float()
+            err = ((out.float() - ref).norm() / ref.norm()).item()
+            acc = out.clone()
+            C.gemm_km(g, x, acc, 1)
+            err_acc = ((acc.float() - 2 * ref).norm() / (2 * ref).norm()).item()
+            del ref, acc
+            tk, ttt, tnt, ttr = [], [], [], []
+            gT, xT = C.transpose2d(g), C.transpose2d(x)
+            for _ in range(rounds):
+                tk.append(timed(lambda: C.gemm_km(g, x, out), iters))
+                ttt.append(timed(lambda: torch.mm(g.t(), x, out=out), iters))
+                tnt.append(timed(lambda: torch.mm(gT, xT.t(), out=out), iters))
+                ttr.append(timed(lambda: (C.transpose2d(g), C.transpose2d(x)), iters))
+            fl = 2.0 * M * N * K
+            md = statistics.median
+            r = {"M": M, "N": N, "K": K, "km_ms": md(tk), "lib_tt_ms": md(ttt), "lib_nt_ms": md(tnt),
+                 "transposes_ms": md(ttr), "km_tflops": fl / md(tk) / 1e9, "lib_nt_tflops": fl / md(tnt) / 1e9,
+                 "rel_err": err, "rel_err_acc": err_acc,
+                 "speedup_vs_step": (md(tnt) + md(ttr)) / md(tk)}
+            res["km_" + name] = r
+            print("km_" + name, json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}),
+                  flush=True)
+            del g, x, out, gT, xT
+            torch.cuda.empty_cache()
     if not only or "swiglu" in only:
         torch.manual_seed(1)
         x, w = rand(T, D), rand(2 * F, D) * 0.05
@@ -94,6 +130,10 @@ def main():
             tu.append(timed(lambda: C.swiglu_fwd_t(torch.mm(x, w.t())), iters))
         r = {"fused_ms": statistics.median(tf), "unfused_ms": statistics.median(tu), "err_gu": e_gu, "err_a": e_a,
              "err_aT": e_at}
+        gu2, a2, _ = C.gemm_nt_swiglu(x, w, False)
+        r["err_gu_r"] = ((gu2.float() - gu_ref.float()).norm() / gu_ref.float().norm()).item()
+        r["err_a_r"] = ((a2.float() - a_ref.float()).norm() / a_ref.float().norm()).item()
+        r["fused_r_ms"] = statistics.median([timed(lambda: C.gemm_nt_swiglu(x, w, False), iters) for _ in range(rounds)])
         res["swiglu_fwd"] = r
         print("swiglu_fwd", json.dumps(r), flush=True)
         dy, wdT = rand(T, D), rand(F, D) * 0.05
@@ -107,6 +147,10 @@ def main():
             tf.append(timed(lambda: C.gemm_nt_swiglu_bwd(dy, wdT, gu_ref), iters))
             tu.append(timed(lambda: C.swiglu_bwd_t(torch.mm(dy, wdT.t()), gu_ref), iters))
         r = {"fused_ms": statistics.median(tf), "unfused_ms": statistics.median(tu), "err_dgu": e1, "err_dguT": e2}
+        dgu2, _ = C.gemm_nt_swiglu_bwd(dy, wdT, gu_ref, False)
+        r["err_dgu_r"] = ((dgu2.float() - dgu_ref.float()).norm() / dgu_ref.float().norm()).item()
+        r["fused_r_ms"] = statistics.median([timed(lambda: C.gemm_nt_swiglu_bwd(dy, wdT, gu_ref, False), iters)
+                                             for _ in range(rounds)])
         res["swiglu_bwd"] = r
         print("swiglu_bwd", json.dumps(r), flush=True)
     print(json.dumps(res))
