@@ -114,14 +114,14 @@ class _SwiGLU(torch.autograd.Function):
 
 def swiglu(gu: torch.Tensor) -> torch.Tensor:
     """silu(gate) * up of the fused [gate | up] projection.  On the HIP path with token-contiguous
-    weight gradients (``DSTACK_AMD_WGRAD=auto``) the kernel also writes the transposed output,
+    weight gradients (``DSTACK_AMD_WGRAD=transpose``) the kernel also writes the transposed output,
     attached as ``a._dsa_t`` [F, T]: ``linear`` then saves only that copy for the down projection's
     weight gradient (memory-neutral) and backward skips the transpose of ``a``."""
     if _ext.use_hip(gu):
         gu = gu.contiguous()
         T = gu.numel() // gu.shape[-1]
         F = gu.shape[-1] // 2
-        with_t = _wgrad_mode() == "auto" and T % 128 == 0 and F % 64 == 0
+        with_t = _wgrad_mode() == "transpose" and T % 128 == 0 and F % 64 == 0
         a, aT = _SwiGLU.apply(gu, with_t)
         if aT is not None:
             a._dsa_t = aT
@@ -190,7 +190,7 @@ class _SwiGLUMLP(torch.autograd.Function):
 
 
 def _mlp_fused_ok(h: torch.Tensor, wgu: torch.Tensor, wdown: torch.Tensor) -> bool:
-    if os.environ.get("DSTACK_AMD_MLP_FUSED", "1") == "0" or _wgrad_mode() not in ("auto", "km"):
+    if os.environ.get("DSTACK_AMD_MLP_FUSED", "1") == "0" or _wgrad_mode() not in ("transpose", "km"):
         return False
     if h.dtype != torch.bfloat16 or wgu.dtype != torch.bfloat16 or wdown.dtype != torch.bfloat16:
         return False
@@ -388,11 +388,13 @@ def _transposed_weight(w: torch.Tensor):
 
 
 def _wgrad_mode() -> str:
-    """How weight gradients dW = g^T x get their operands: ``auto`` (token-contiguous copies made by
-    the HIP transpose kernel or written by the producer, hipBLASLt), ``km`` (both operands left
-    token-major, the in-tree GEMM's KM form: no transposes at all), ``strided`` (token-major,
-    hipBLASLt)."""
-    return os.environ.get("DSTACK_AMD_WGRAD", "auto").lower()
+    """How weight gradients dW = g^T x get their operands: ``km`` (default: both operands left
+    token-major, the in-tree GEMM's KM form, no transposes at all; +1.0 % tokens/s against
+    ``transpose`` in a same-box A/B, profiles/wgrad_km_ab_r8a.txt), ``transpose`` (``auto``, the
+    previous default: token-contiguous copies made by the HIP transpose kernel or written by the
+    producer, hipBLASLt), ``strided`` (token-major, hipBLASLt)."""
+    m = os.environ.get("DSTACK_AMD_WGRAD", "km").lower()
+    return "transpose" if m == "auto" else m
 
 
 def mm_into(a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = False) -> torch.Tensor:
@@ -432,7 +434,7 @@ def wgrad_operands(g2: torch.Tensor, x2, xT=None, gT=None):
     Q = xT.shape[0] if xT is not None else x2.shape[1]
     a = g2.t()
     b = xT.t() if xT is not None else x2
-    if not (_ext.use_hip(g2) and _wgrad_mode() == "auto"):
+    if not (_ext.use_hip(g2) and _wgrad_mode() == "transpose"):
         return a, b  # "km" (mm_into's in-tree KM GEMM) and "strided" take the token-major views
     C = _ext.require()
     if xT is None and x2.is_contiguous() and C.transpose2d_supported(T, Q):

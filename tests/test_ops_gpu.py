@@ -385,7 +385,7 @@ def test_linear_wgrad_layouts_agree(gpu, T, P, Q, monkeypatch):
     w = _rand(P, Q, device=gpu, seed=10, scale=0.05).requires_grad_()
     g = _rand(T, P, device=gpu, seed=11)
     grads = {}
-    for mode in ("auto", "strided"):
+    for mode in ("auto", "strided", "km"):  # km: the in-tree KM-form GEMM where it tiles the shape
         monkeypatch.setenv("DSTACK_AMD_WGRAD", mode)
         x.grad = w.grad = None
         ops.linear(x, w).backward(g)

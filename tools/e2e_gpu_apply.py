@@ -21,9 +21,11 @@ def main():
 
     steps = os.environ.get("E2E_STEPS", "5")
     launch = "python"
-    if os.environ.get("E2E_TORCHRUN") == "1":
-        # the examples/llama3-8b-train command: torchrun over the rendezvous env the runner exports
-        launch = ("torchrun --nnodes=$DSTACK_NODES_NUM --node-rank=$DSTACK_NODE_RANK "
+    if os.environ.get("E2E_TORCHRUN") == "1" or os.environ.get("E2E_LAUNCH") in ("torchrun", "launch"):
+        # the examples/llama3-8b-train command: one rank per GPU over the rendezvous env the runner
+        # exports, by torchrun or (E2E_LAUNCH=launch, the example's) the torch-free launcher
+        prog = "torchrun" if os.environ.get("E2E_LAUNCH", "torchrun") == "torchrun" else "python -m dstack_amd.workloads.launch"
+        launch = (f"{prog} --nnodes=$DSTACK_NODES_NUM --node-rank=$DSTACK_NODE_RANK "
                   "--nproc-per-node=$DSTACK_GPUS_PER_NODE --master-addr=$DSTACK_MASTER_NODE_IP "
                   "--master-port=$MASTER_PORT")
     cmd = (f"echo HIP_VISIBLE_DEVICES=$HIP_VISIBLE_DEVICES DSTACK_GPUS_NUM=$DSTACK_GPUS_NUM "
@@ -34,14 +36,20 @@ def main():
     # (HBM, bf16/fp8 MFMA) before the job; the result becomes the instance's health
     # E2E_RCCL_PREFLIGHT=1: the example's RCCL pre-flight, forced for this 1-GPU job (a world of one
     # rank: bootstrap + communicator + an in-place all-reduce, no link bandwidth)
+    # E2E_ROCPROF=1: the runner wraps each rank in rocprofv3 (kernel statistics) with the counters
+    # of E2E_ROCPROF_COUNTERS, and appends the per-kernel summaries to the job log
     probe = os.environ.get("E2E_PROBE") == "1"
     preflight = os.environ.get("E2E_RCCL_PREFLIGHT") == "1"
+    rocprof = os.environ.get("E2E_ROCPROF") == "1"
     srv_env = {"DSTACK_SERVER_METRICS_COLLECT_INTERVAL": "2"}
     if probe or preflight:
         srv_env["DSTACK_LOCAL_GPU_PROBE"] = "1"
     job_env = {"DSTACK_GPU_PROBE": "1"} if probe else {}
     if preflight:
         job_env["DSTACK_RCCL_PREFLIGHT"] = "force"
+    if rocprof:
+        job_env["DSTACK_ROCPROF"] = "1"
+        job_env["DSTACK_ROCPROF_COUNTERS"] = os.environ.get("E2E_ROCPROF_COUNTERS", "SQ_WAVES SQ_INSTS_MFMA")
     with ServerProcess(env=srv_env) as srv:
         client = srv.client()
         conf = Task(name="llama3-8b-e2e", commands=[cmd], resources=Resources(gpu=GPU(count=1)), env=job_env)
@@ -83,6 +91,10 @@ def main():
         }
         if preflight:
             out["rccl_preflight_log"] = [ln for ln in logs.splitlines() if "RCCL pre-flight" in ln][:1]
+        if rocprof:
+            lines = logs.splitlines()
+            i = next((k for k, ln in enumerate(lines) if "[dstack] rocprofv3" in ln or "DSTACK_ROCPROF" in ln), None)
+            out["rocprof_log"] = lines[i:i + 40] if i is not None else []
         if probe or preflight:
             insts = client.api.instances.list(["main"])
             out["instance_health"] = [i.health for i in insts]
