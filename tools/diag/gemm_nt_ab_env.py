@@ -24,7 +24,10 @@ def timed(fn, iters=10):
 def main():
     C = _ext.require()
     name, vals = sys.argv[1], sys.argv[2:]
-    for M, N, K in [(8192, 28672, 4096), (8192, 4096, 4096), (28672, 4096, 8192), (8192, 14336, 4096)]:
+    shapes = [(8192, 28672, 4096), (8192, 4096, 4096), (28672, 4096, 8192), (8192, 14336, 4096)]
+    if os.getenv("SHAPES"):  # "M,N,K;M,N,K"
+        shapes = [tuple(int(x) for x in sh.split(",")) for sh in os.environ["SHAPES"].split(";")]
+    for M, N, K in shapes:
         a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
         b = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)

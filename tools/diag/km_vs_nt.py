@@ -34,7 +34,7 @@ def main():
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     res = {}
     for name, fn in (("km", lambda m: C.gemm_km(g, x, out, m)), ("nt", lambda m: C.gemm_nt_mode(gT, xT, out, m))):
-        for mode in (0, 2):
+        for mode in (0, 1, 2):
             ts = [timed(lambda: fn(mode)) for _ in range(int(os.getenv("ROUNDS", "5")))]
             res[f"{name}_mode{mode}_ms"] = round(statistics.median(ts), 4)
     fl = 2.0 * M * N * K

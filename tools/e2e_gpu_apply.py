@@ -57,10 +57,14 @@ def main():
         run = client.runs.submit(conf)
         deadline = t0 + float(os.environ.get("E2E_TIMEOUT", "600"))
         samples = []
+        last_print = time.time()
         while time.time() < deadline:
             run.refresh()
             if run.status.is_finished():
                 break
+            if time.time() - last_print > 20:  # progress for the caller's silence watchdog
+                print(f"[e2e] {time.time() - t0:.0f}s status={run.status.value}", flush=True)
+                last_print = time.time()
             try:
                 jm = client.api.metrics.get_job_metrics("main", run.name, limit=1)
                 cur = {m.name: m.values[-1] for m in jm.metrics if m.values}
