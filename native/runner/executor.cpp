@@ -567,7 +567,11 @@ bool Executor::run_probe() {
 // global rank node_rank*G + local, probes/ranks.h) bootstrapped like the job's RCCL (unique id from
 // global rank 0 over TCP at the master node, port MASTER_PORT+1, the job's HIP_VISIBLE_DEVICES /
 // NCCL_SOCKET_IFNAME env) -- so a broken fabric or a bad GPU fails the job in seconds with the
-// probe's message instead of hanging inside torchrun.
+// probe's message instead of hanging inside torchrun.  By default it runs CONCURRENTLY with the
+// job (DSTACK_RCCL_PREFLIGHT_MODE=concurrent; `blocking` runs it first): on one MI355X the probe
+// takes ~6.7 s (profiles/e2e_rccl_preflight_r8d.txt), all of which would otherwise sit on the
+// job's cold start, while the job spends its first seconds in imports, model init and the first
+// step's compute before its first collective.
 bool Executor::wants_rccl_preflight() const {
   const Json& js = submit_body_["job_spec"];
   std::string v = js["env"]["DSTACK_RCCL_PREFLIGHT"].str("");
@@ -576,6 +580,11 @@ bool Executor::wants_rccl_preflight() const {
   int nodes = ci["job_ips"].size() > 0 ? (int)ci["job_ips"].size() : (int)js["jobs_per_replica"].as_int(1);
   int gpus = (int)ci["gpus_per_job"].as_int(0);
   return v == "force" || nodes * gpus > 1;
+}
+
+bool Executor::preflight_concurrent() const {
+  const std::string m = submit_body_["job_spec"]["env"]["DSTACK_RCCL_PREFLIGHT_MODE"].str("concurrent");
+  return m != "blocking";
 }
 
 bool Executor::run_rccl_preflight(std::string& msg) {
@@ -879,6 +888,11 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
       stop_at = now;
     }
     if (stop_requested_ && stop_at == 0) stop_at = now;
+    if (preflight_state_ == 3 && stop_at == 0) {  // the concurrent RCCL pre-flight failed
+      rlog("RCCL pre-flight failed: stopping job");
+      kill(-pid, SIGTERM);
+      stop_at = now;
+    }
     if (stop_at > 0 && now - stop_at > 10000) kill(-pid, SIGKILL);  // killDelay (executor.go:74)
   }
   close(master);
@@ -904,6 +918,12 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
     reason = "max_duration_exceeded";
     return code;
   }
+  if (preflight_state_ == 3) {
+    reason = "executor_error";
+    std::lock_guard<std::mutex> lk(states_mu_);
+    msg = preflight_err_;
+    return code;
+  }
   if (stop_requested_) {
     reason = "terminated_by_user";
     return code;
@@ -923,13 +943,31 @@ void Executor::run_job_steps() {
     add_state("failed", "executor_error", err);
   } else if (submit_body_["job_spec"]["gpu_probe"].as_bool(false) && !run_probe()) {
     add_state("failed", "gpu_health_check_failed", "GPU health probe failed");
-  } else if (wants_rccl_preflight() && !run_rccl_preflight(err)) {
+  } else if (wants_rccl_preflight() && !preflight_concurrent() && !run_rccl_preflight(err)) {
     add_state("failed", "executor_error", err);
   } else if (stop_requested_) {
     add_state("terminated", "terminated_by_user");
   } else {
+    // concurrent pre-flight: the job starts at once (its imports, model init and first step take
+    // seconds before its first collective) while the probe checks the fabric beside it; a failed
+    // probe stops the job with the probe's message, so a bad fabric still fails the job in
+    // seconds, and a good one costs the job's start-up nothing
+    std::thread preflight;
+    if (wants_rccl_preflight() && preflight_concurrent()) {
+      preflight_state_ = 1;
+      preflight = std::thread([this] {
+        std::string m;
+        const bool ok = run_rccl_preflight(m);
+        if (!ok) {
+          std::lock_guard<std::mutex> lk(states_mu_);
+          preflight_err_ = m;
+        }
+        preflight_state_ = ok ? 2 : 3;
+      });
+    }
     std::string reason, msg;
     int code = exec_job(reason, msg);
+    if (preflight.joinable()) preflight.join();
     if (reason == "max_duration_exceeded" || reason == "terminated_by_user")
       add_state("terminated", reason, msg, code);
     else if (!reason.empty())

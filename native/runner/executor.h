@@ -92,6 +92,7 @@ class Executor {
   bool setup_repo(std::string& err);
   bool run_probe();
   bool wants_rccl_preflight() const;
+  bool preflight_concurrent() const;
   bool run_rccl_preflight(std::string& msg);
   int exec_job(std::string& reason, std::string& msg);
 
@@ -108,6 +109,10 @@ class Executor {
   std::atomic<int> child_pgid_{0};
   std::string probe_json_;  // last dstack-probe result (JSON), guarded by states_mu_
   std::string preflight_json_;  // last RCCL pre-flight document
+  // concurrent pre-flight (DSTACK_RCCL_PREFLIGHT_MODE=concurrent, the default): 0 none, 1 running,
+  // 2 passed, 3 failed (the job is stopped with preflight_err_, guarded by states_mu_)
+  std::atomic<int> preflight_state_{0};
+  std::string preflight_err_;
   mutable std::atomic<bool> pulled_after_finish_{false};
   std::mutex fin_mu_;
   std::condition_variable fin_cv_;

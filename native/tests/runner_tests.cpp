@@ -305,7 +305,7 @@ int main() {
   });
 
   // ---- shim authorized_keys.go ------------------------------------------------------------------
-  run("executor: an RCCL pre-flight failure fails the job with the probe's message before the job runs", [] {
+  run("executor: a blocking RCCL pre-flight failure fails the job with the probe's message before the job runs", [] {
     // stub dstack-probe: records its argv; node 1 reports a hung rank, node 0 a healthy ring
     std::string root = tmpdir();
     std::string probe = root + "/probe.sh";
@@ -316,11 +316,12 @@ int main() {
                "timed out\"}'; exit 1; fi\necho '{\"rccl_world\": 16, \"rccl_busbw_gb_s\": 311.5, \"healthy\": true, "
                "\"message\": \"\"}'\n",
                0755);
-    auto body = [&](const std::string& rank) {
-      Json b = job({"/bin/sh", "-c", "echo trained"});
+    auto body = [&](const std::string& rank, const char* cmd = "echo trained", const char* mode = "blocking") {
+      Json b = job({"/bin/sh", "-c", cmd});
       Json js = b["job_spec"];
       Json env = Json::object();
       env.set("DSTACK_RCCL_PREFLIGHT", std::string("force"));
+      env.set("DSTACK_RCCL_PREFLIGHT_MODE", std::string(mode));
       env.set("DSTACK_NODE_RANK", rank);
       env.set("DSTACK_NODES_NUM", std::string("2"));
       env.set("DSTACK_GPUS_PER_NODE", std::string("8"));
@@ -339,6 +340,40 @@ int main() {
     std::string args;
     CHECK(read_file(root + "/probe_args", args) && args.find("--timeout-ms 40000") != std::string::npos);
     r = run_job(root + "/n0", body("0"), "", probe, &pull);
+    CHECK(r.state == "done" && r.logs.find("trained") != std::string::npos);
+    CHECK(pull["rccl_preflight"]["rccl_busbw_gb_s"].as_double(0) > 311.0);
+  });
+
+  run("executor: the concurrent RCCL pre-flight (default) stops a running job when it fails", [] {
+    // stub probe: node 1 fails after 1 s; the job itself would run for 30 s
+    std::string root = tmpdir();
+    std::string probe = root + "/probe.sh";
+    write_file(probe,
+               "#!/bin/sh\nrank=0\nwhile [ $# -gt 0 ]; do [ \"$1\" = --node-rank ] && rank=$2; shift; done\nsleep 1\n"
+               "if [ \"$rank\" = 1 ]; then echo '{\"healthy\": false, \"message\": \"RCCL: rank 9 timed out\"}'; "
+               "exit 1; fi\necho '{\"rccl_busbw_gb_s\": 311.5, \"healthy\": true, \"message\": \"\"}'\n",
+               0755);
+    auto body = [&](const std::string& rank, const char* cmd) {
+      Json b = job({"/bin/sh", "-c", cmd});
+      Json js = b["job_spec"];
+      Json env = Json::object();
+      env.set("DSTACK_RCCL_PREFLIGHT", std::string("force"));
+      env.set("DSTACK_NODE_RANK", rank);
+      env.set("DSTACK_NODES_NUM", std::string("2"));
+      env.set("DSTACK_GPUS_PER_NODE", std::string("8"));
+      js.set("env", env);
+      b.set("job_spec", js);
+      return b;
+    };
+    Json pull;
+    const int64_t t0 = now_millis();
+    JobResult r = run_job(root + "/n1", body("1", "echo started; sleep 30; echo trained"), "", probe, &pull);
+    CHECK(r.state == "failed" && r.reason == "executor_error");
+    CHECK(r.message.find("RCCL pre-flight failed (exit 1): RCCL: rank 9 timed out") == 0);
+    CHECK(r.logs.find("started") != std::string::npos);  // the job ran beside the probe...
+    CHECK(r.logs.find("trained") == std::string::npos);  // ...and was stopped when it failed
+    CHECK(now_millis() - t0 < 15000);
+    r = run_job(root + "/n0", body("0", "echo trained"), "", probe, &pull);
     CHECK(r.state == "done" && r.logs.find("trained") != std::string::npos);
     CHECK(pull["rccl_preflight"]["rccl_busbw_gb_s"].as_double(0) > 311.0);
   });
