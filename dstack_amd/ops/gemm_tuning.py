@@ -7,7 +7,11 @@ results CSV next to this file; training runs load it with tuning disabled (``mod
 step ever pays for tuning.  The CSV carries TunableOp's validators (ROCm, hipBLASLt, gfx arch);
 on a mismatch PyTorch ignores it and falls back to the default heuristics.
 
-``DSTACK_AMD_GEMM_TUNING`` = ``use`` (default when the file exists) | ``tune`` | ``off``.
+``DSTACK_AMD_GEMM_TUNING`` = ``use`` | ``tune`` | ``off``.  Default: ``off`` for training (since the
+weight gradients moved to the in-tree GEMM, hipBLASLt's own heuristics run the remaining training
+GEMMs as fast as the tuned selections -- 22.70/22.72k vs 22.67/22.65k tokens/s, same box,
+profiles/gemm_tuning_ab_r8h.txt -- and skip TunableOp's ~1 s first-call set-up, which sat on every
+job's start), ``use`` for serving (the tuned fp8 decode GEMMs are up to 2.8x faster).
 """
 
 from __future__ import annotations
@@ -34,7 +38,7 @@ def setup(mode: Optional[str] = None, device_index: int = 0, kind: str = "train"
 
     if not torch.cuda.is_available() or torch.version.hip is None:
         return "off"
-    mode = (mode or os.environ.get("DSTACK_AMD_GEMM_TUNING") or "use").lower()
+    mode = (mode or os.environ.get("DSTACK_AMD_GEMM_TUNING") or ("off" if kind == "train" else "use")).lower()
     arch = torch.cuda.get_device_properties(device_index).gcnArchName.split(":")[0]
     path = results_path(arch, kind)
     tunable = torch.cuda.tunable
@@ -61,6 +65,49 @@ def setup(mode: Optional[str] = None, device_index: int = 0, kind: str = "train"
                          insert_device_ordinal=False)
     tunable.read_file(str(path))
     return "use"
+
+
+def llama_shapes(cfg, tokens: int):
+    """(M, N, K) of every ``a @ b.t()`` library GEMM of a Llama training micro-batch that the
+    in-tree GEMM does not run: the forward projections (qkv, o, down, LM head) and the input
+    gradients through the cached W^T (qkv, o, gate/up, LM head)."""
+    d, hd = cfg.dim, cfg.dim // cfg.n_heads
+    qkv = (cfg.n_heads + 2 * cfg.n_kv_heads) * hd
+    return [(tokens, qkv, d), (tokens, d, d), (tokens, d, cfg.ffn_dim), (tokens, cfg.vocab_size, d),
+            (tokens, d, qkv), (tokens, d, 2 * cfg.ffn_dim), (tokens, d, cfg.vocab_size)]
+
+
+def prewarm(shapes, device):
+    """Start a thread that runs one ``a @ b.t()`` per shape on a side stream, so the library's
+    first-call work -- hipBLASLt's handle and heuristics (0.17 s on the first GEMM of a process), and
+    with ``use`` TunableOp mapping its saved selections onto hipBLASLt's solution list (1.1 s,
+    profiles/first_step_r8b.txt, tools/diag/gemm_first_call.py), plus loading each selected kernel --
+    overlaps the model's initialisation instead of landing in the first forward.  Not while tuning.  Returns the thread (join it
+    before the first step) or None."""
+    import threading
+
+    import torch
+
+    tunable = torch.cuda.tunable
+    if device.type != "cuda" or (tunable.is_enabled() and tunable.tuning_is_enabled()):
+        return None
+    if os.environ.get("DSTACK_AMD_GEMM_PREWARM", "1") == "0":
+        return None
+
+    def work():
+        torch.cuda.set_device(device)
+        st = torch.cuda.Stream(device=device)
+        with torch.cuda.stream(st):
+            for m, n, k in shapes:
+                a = torch.empty(m, k, device=device, dtype=torch.bfloat16)
+                b = torch.empty(n, k, device=device, dtype=torch.bfloat16)
+                torch.mm(a.zero_(), b.zero_().t())
+                del a, b
+        st.synchronize()
+
+    th = threading.Thread(target=work, name="gemm-prewarm", daemon=True)
+    th.start()
+    return th
 
 
 def flush():

@@ -316,9 +316,14 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
 
     gemm_mode = gemm_tuning.setup(device_index=env.local_rank if device.type == "cuda" else 0)
     stages["gemm_tuning_loaded"] = time.time()
+    # the library GEMMs' first-call set-up runs beside the model's initialisation
+    warm = gemm_tuning.prewarm(gemm_tuning.llama_shapes(CONFIGS[model], micro_batch * seq_len), device) \
+        if model in CONFIGS else None
     t0 = time.time()
     tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum, lr=lr, lr_warmup=lr_warmup,
                  lr_decay_steps=lr_decay_steps, clip_grad_norm=clip_grad_norm, data=data)
+    if warm is not None:
+        warm.join()
     stages["model_ready"] = time.time()
     if env.rank == 0:
         print(f"[train] model={model} params={tr.cfg.num_params()/1e9:.2f}B world={env.world} "

@@ -30,7 +30,8 @@ def main():
                   "--master-port=$MASTER_PORT")
     cmd = (f"echo HIP_VISIBLE_DEVICES=$HIP_VISIBLE_DEVICES DSTACK_GPUS_NUM=$DSTACK_GPUS_NUM "
            f"MASTER_ADDR=$DSTACK_MASTER_NODE_IP && cd {ROOT} && "
-           f"{launch} bench.py --gpus $DSTACK_GPUS_NUM --steps {steps} --warmup 2 --no-coldstart")
+           f"{launch} bench.py --gpus $DSTACK_GPUS_NUM --steps {steps} --warmup 2 --no-coldstart "
+           f"{os.environ.get('E2E_ARGS', '').replace(',', ' ')}")  # E2E_ARGS: comma-separated extra bench args
     # hardware metrics: the server polls the runner's /api/metrics (cgroup + amdsmi) every 2 s here
     # E2E_PROBE=1: the shim hands dstack-probe to the runner, which runs the HIP health probes
     # (HBM, bf16/fp8 MFMA) before the job; the result becomes the instance's health
