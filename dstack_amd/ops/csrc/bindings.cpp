@@ -53,6 +53,9 @@ hipError_t dsa_gemm_nt_trace(const void*, const void*, void*, int, int, int, uns
 hipError_t dsa_gemm_nt_swiglu(const void*, const void*, void*, void*, void*, int, int, int, long, long, hipStream_t);
 bool dsa_gemm_nt_swiglu_bwd_supported(int, int, int);
 bool dsa_gemm_km_supported(int, int, int);
+bool dsa_fp8_rows_gemm_supported(int, int, int, int);
+hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
+                             long, long, long, int, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 hipError_t dsa_gemm_nt_swiglu_bwd(const void*, const void*, const void*, void*, void*, int, int, int, long, long,
                                   hipStream_t);
@@ -417,6 +420,46 @@ torch::Tensor gemm_nt_trace(torch::Tensor a, torch::Tensor b, torch::Tensor out)
 
 bool gemm_km_supported(int64_t M, int64_t N, int64_t K) { return dsa_gemm_km_supported(M, N, K); }
 
+bool fp8_rows_gemm_supported(int64_t M, int64_t N, int64_t K, int64_t S) {
+  return dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K, (int)S);
+}
+
+// y[M][N] = bf16(xs[m] ws[n] (xq wq^T)) for a decode batch (M <= 256), e4m3 operands
+// (csrc/fp8_gemm.hip); S > 1 splits K over S workgroups per column block, with fp32 slabs `part`
+// ([S * 256 * N] floats) and tickets `cnt` ([N / 128] int32, zero; left zero)
+torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t S,
+                            torch::Tensor part, torch::Tensor cnt) {
+  for (auto* t : {&xq, &wq}) {
+    TORCH_CHECK(t->is_cuda() && t->element_size() == 1 && t->dim() == 2 && t->stride(1) == 1,
+                "fp8_rows_gemm: 1-byte 2-D operands with contiguous rows");
+    TORCH_CHECK(t->stride(0) % 16 == 0 && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "fp8_rows_gemm: 16-byte aligned rows");
+  }
+  const int64_t M = xq.size(0), K = xq.size(1), N = wq.size(0);
+  TORCH_CHECK(wq.size(1) == K, "fp8_rows_gemm: K mismatch");
+  TORCH_CHECK(xs.is_cuda() && xs.scalar_type() == torch::kFloat32 && xs.is_contiguous() && xs.numel() == M,
+              "fp8_rows_gemm: xs fp32 [M]");
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.is_contiguous() && ws.numel() == N,
+              "fp8_rows_gemm: ws fp32 [N]");
+  TORCH_CHECK(dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K, (int)S),
+              "fp8_rows_gemm: M <= 256, N % 128 == 0, K % (128 S) == 0");
+  float* pp = nullptr;
+  int* cp = nullptr;
+  if (S > 1) {
+    TORCH_CHECK(part.is_cuda() && part.scalar_type() == torch::kFloat32 && part.numel() >= S * 256 * N,
+                "fp8_rows_gemm: part needs S * 256 * N floats");
+    TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == torch::kInt32 && cnt.numel() >= N / 128,
+                "fp8_rows_gemm: cnt needs N / 128 int32");
+    pp = part.data_ptr<float>();
+    cp = cnt.data_ptr<int>();
+  }
+  auto y = torch::empty({M, N}, xq.options().dtype(torch::kBFloat16));
+  check(dsa_fp8_rows_gemm(xq.data_ptr(), xs.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(), pp,
+                          cp, (int)M, (int)N, (int)K, xq.stride(0), wq.stride(0), y.stride(0), (int)S, stream()),
+        "fp8_rows_gemm");
+  return y;
+}
+
 // out[M][N] (+)= a[K][M]^T b[K][N]  (csrc/gemm_nt.hip KM form: dW = dY^T X, token-major operands);
 // mode 2 = timing-only
 void gemm_km(torch::Tensor a, torch::Tensor b, torch::Tensor out, int64_t mode) {
@@ -611,6 +654,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_swiglu", &gemm_nt_swiglu, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("transposed") = true);
   m.def("gemm_km", &gemm_km, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("out"), pybind11::arg("mode") = 0);
   m.def("gemm_km_supported", &gemm_km_supported);
+  m.def("fp8_rows_gemm", &fp8_rows_gemm);
+  m.def("fp8_rows_gemm_supported", &fp8_rows_gemm_supported);
   m.def("gemm_nt_trace", &gemm_nt_trace);
   m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);
   m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd, pybind11::arg("dy"), pybind11::arg("wdT"), pybind11::arg("gu"),
