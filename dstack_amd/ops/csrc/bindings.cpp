@@ -53,9 +53,9 @@ hipError_t dsa_gemm_nt_trace(const void*, const void*, void*, int, int, int, uns
 hipError_t dsa_gemm_nt_swiglu(const void*, const void*, void*, void*, void*, int, int, int, long, long, hipStream_t);
 bool dsa_gemm_nt_swiglu_bwd_supported(int, int, int);
 bool dsa_gemm_km_supported(int, int, int);
-bool dsa_fp8_rows_gemm_supported(int, int, int, int);
-hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
-                             long, long, long, int, hipStream_t);
+bool dsa_fp8_rows_gemm_supported(int, int, int);
+hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, int, int, int, long, long,
+                             long, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 hipError_t dsa_gemm_nt_swiglu_bwd(const void*, const void*, const void*, void*, void*, int, int, int, long, long,
                                   hipStream_t);
@@ -420,15 +420,13 @@ torch::Tensor gemm_nt_trace(torch::Tensor a, torch::Tensor b, torch::Tensor out)
 
 bool gemm_km_supported(int64_t M, int64_t N, int64_t K) { return dsa_gemm_km_supported(M, N, K); }
 
-bool fp8_rows_gemm_supported(int64_t M, int64_t N, int64_t K, int64_t S) {
-  return dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K, (int)S);
+bool fp8_rows_gemm_supported(int64_t M, int64_t N, int64_t K) {
+  return dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K);
 }
 
 // y[M][N] = bf16(xs[m] ws[n] (xq wq^T)) for a decode batch (M <= 256), e4m3 operands
-// (csrc/fp8_gemm.hip); S > 1 splits K over S workgroups per column block, with fp32 slabs `part`
-// ([S * 256 * N] floats) and tickets `cnt` ([N / 128] int32, zero; left zero)
-torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t S,
-                            torch::Tensor part, torch::Tensor cnt) {
+// (csrc/fp8_gemm.hip)
+torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws) {
   for (auto* t : {&xq, &wq}) {
     TORCH_CHECK(t->is_cuda() && t->element_size() == 1 && t->dim() == 2 && t->stride(1) == 1,
                 "fp8_rows_gemm: 1-byte 2-D operands with contiguous rows");
@@ -441,21 +439,10 @@ torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq
               "fp8_rows_gemm: xs fp32 [M]");
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.is_contiguous() && ws.numel() == N,
               "fp8_rows_gemm: ws fp32 [N]");
-  TORCH_CHECK(dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K, (int)S),
-              "fp8_rows_gemm: M <= 256, N % 128 == 0, K % (128 S) == 0");
-  float* pp = nullptr;
-  int* cp = nullptr;
-  if (S > 1) {
-    TORCH_CHECK(part.is_cuda() && part.scalar_type() == torch::kFloat32 && part.numel() >= S * 256 * N,
-                "fp8_rows_gemm: part needs S * 256 * N floats");
-    TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == torch::kInt32 && cnt.numel() >= N / 128,
-                "fp8_rows_gemm: cnt needs N / 128 int32");
-    pp = part.data_ptr<float>();
-    cp = cnt.data_ptr<int>();
-  }
+  TORCH_CHECK(dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K), "fp8_rows_gemm: M <= 256, N % 128, K % 128 == 0");
   auto y = torch::empty({M, N}, xq.options().dtype(torch::kBFloat16));
-  check(dsa_fp8_rows_gemm(xq.data_ptr(), xs.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(), pp,
-                          cp, (int)M, (int)N, (int)K, xq.stride(0), wq.stride(0), y.stride(0), (int)S, stream()),
+  check(dsa_fp8_rows_gemm(xq.data_ptr(), xs.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(),
+                          (int)M, (int)N, (int)K, xq.stride(0), wq.stride(0), y.stride(0), stream()),
         "fp8_rows_gemm");
   return y;
 }

@@ -197,6 +197,9 @@ class ServingLlama:
             _ext.require()
         # DSTACK_AMD_GEMV=0: small decode batches on hipBLASLt too (A/B switch)
         self.gemv = os.environ.get("DSTACK_AMD_GEMV", "1") != "0"
+        # decode-batch fp8 projections (5..256 rows) on the in-tree fp8 GEMM (csrc/fp8_gemm.hip)
+        # instead of hipBLASLt; "lib" keeps hipBLASLt
+        self.fp8_gemm = os.environ.get("DSTACK_AMD_FP8_GEMM", "hip").lower()
         # fp8: norms feeding an fp8 GEMM write e4m3 directly (DSTACK_AMD_FP8_FUSE_NORM=0: separate quant)
         self.fuse_norm_quant = os.environ.get("DSTACK_AMD_FP8_FUSE_NORM", "1") != "0"
         self.cos, self.sin = rope_tables(self.max_model_len + sops.PAGE, self.D, cfg.rope_theta, spec.rope_scaling,
@@ -484,6 +487,10 @@ class ServingLlama:
             if self.gemv and C.gemv_fp8_supported(M, x.shape[1]):
                 return C.gemv_fp8(x, w.q, w.s)
             xq, xs = C.quant_fp8_rows(x)
+        if self.hip and self.fp8_gemm == "hip" and M > 4:
+            y = self._fp8_rows(xq, xs, w)
+            if y is not None:
+                return y
         pad = -M % 16  # hipBLASLt's fp8 GEMM wants every dimension a multiple of 16
         if pad:  # zero rows (e4m3 0x00 = 0.0) with unit scales
             xq = torch.nn.functional.pad(xq, (0, 0, 0, pad))
@@ -491,6 +498,21 @@ class ServingLlama:
         y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), w.q.view(torch.float8_e4m3fn).t(),
                              scale_a=xs.view(-1, 1), scale_b=w.s.view(1, -1), out_dtype=self.dtype)
         return y[:M] if pad else y
+
+    def _fp8_rows(self, xq, xs, w: Fp8Weight):
+        """The in-tree decode fp8 GEMM (64-row batch blocks x 128 weight rows per workgroup) where it
+        beats hipBLASLt (profiles/fp8_decode_gemm_r8j.txt, Llama-3-70B shapes): K <= 8192 and at most
+        256 workgroups, i.e. the qkv and o projections up to 128 rows (1.16-1.19x) and o at 256
+        (1.04x); the gate/up (many column blocks) and the K = 28672 down projection (64 column
+        blocks: hipBLASLt splits K) stay on hipBLASLt."""
+        C = _ext.require()
+        M, K = xq.shape
+        N = w.q.shape[0]
+        if M > 256 or K > 8192 or (N // 128) * ((M + 63) // 64) > 256:
+            return None
+        if xq.stride(0) % 16 or w.q.stride(0) % 16 or not C.fp8_rows_gemm_supported(M, N, K):
+            return None
+        return C.fp8_rows_gemm(xq.view(torch.uint8), xs, w.q.view(torch.uint8), w.s)
 
     def _reduce(self, t):
         """Sum the row-parallel partial outputs of the tensor-parallel ranks (RCCL all-reduce)."""

@@ -669,21 +669,17 @@ def test_swiglu_mlp_fused_matches_separate_kernels(gpu, monkeypatch, wgrad):
         assert rel < 1e-2, f"{name}: rel err {rel}"
 
 
-@pytest.mark.parametrize("M,N,K,S", [(256, 256, 512, 1), (37, 384, 512, 2), (200, 256, 1024, 4), (1, 128, 256, 1)])
-def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K, S):
-    """Decode-batch fp8 GEMM (csrc/fp8_gemm.hip: scaled 16x16x128 f8f6f4 MFMA, split-K with a
-    last-arrival combine) against the fp32 product of the same e4m3 operands and scales."""
+@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (37, 384, 512), (200, 256, 1024), (1, 128, 256), (64, 1024, 384)])
+def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K):
+    """Decode-batch fp8 GEMM (csrc/fp8_gemm.hip: scaled 16x16x128 f8f6f4 MFMA over 64-row batch
+    blocks) against the fp32 product of the same e4m3 operands and scales."""
     C = _ext.require()
-    torch.manual_seed(M + N + K + S)
+    torch.manual_seed(M + N + K)
     x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=gpu, dtype=torch.bfloat16) * 0.05
     xq, xs = ref.quant_fp8_rows(x)
     wq, ws = ref.quant_fp8_rows(w)
-    part = torch.empty(S * 256 * N, device=gpu, dtype=torch.float32)
-    cnt = torch.zeros(N // 128, device=gpu, dtype=torch.int32)
     want = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
-    for _ in range(2):  # the tickets are left zero for the next call
-        y = C.fp8_rows_gemm(xq.view(torch.uint8), xs, wq.view(torch.uint8), ws, S, part, cnt)
-        err = ((y.float() - want).norm() / want.norm()).item()
-        assert err < 1e-2, err
-    assert int(cnt.abs().sum().item()) == 0
+    y = C.fp8_rows_gemm(xq.view(torch.uint8), xs, wq.view(torch.uint8), ws)
+    err = ((y.float() - want).norm() / want.norm()).item()
+    assert err < 1e-2, err

@@ -29,13 +29,6 @@ def timed(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
-def pick_split(N, K):
-    for S in (1, 2, 4, 8):
-        if (N // 128) * S >= 256 and K % (128 * S) == 0:
-            return S
-    return 1
-
-
 def main():
     C = _ext.require()
     gemm_tuning.setup("use", kind="serving")
@@ -50,10 +43,7 @@ def main():
             wq, ws = ref.quant_fp8_rows(w)
             wq = wq.view(torch.uint8)
             del w
-            S = int(os.getenv("SPLIT", "0")) or pick_split(N, K)
-            part = torch.empty(S * 256 * N, device="cuda", dtype=torch.float32)
-            cnt = torch.zeros(N // 128, device="cuda", dtype=torch.int32)
-            ours = lambda: C.fp8_rows_gemm(xq, xs, wq, ws, S, part, cnt)  # noqa: E731
+            ours = lambda: C.fp8_rows_gemm(xq, xs, wq, ws)  # noqa: E731
             pad = -M % 16
             xq_l = torch.nn.functional.pad(xq, (0, 0, 0, pad)) if pad else xq
             xs_l = torch.nn.functional.pad(xs, (0, pad), value=1.0) if pad else xs
@@ -66,14 +56,14 @@ def main():
                 to.append(timed(ours))
                 tl.append(timed(lib))
             wb = N * K
-            r = {"M": M, "N": N, "K": K, "S": S, "ours_us": statistics.median(to) * 1e3,
+            r = {"M": M, "N": N, "K": K, "ours_us": statistics.median(to) * 1e3,
                  "lib_us": statistics.median(tl) * 1e3, "ours_tb_s": wb / statistics.median(to) / 1e9,
                  "lib_tb_s": wb / statistics.median(tl) / 1e9, "rel_diff": err}
             r["speedup"] = r["lib_us"] / r["ours_us"]
             res[f"{name}_m{M}"] = r
             print(f"{name}_m{M}", json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in r.items()}),
                   flush=True)
-            del xq, wq, part, cnt
+            del xq, wq
             torch.cuda.empty_cache()
     print(json.dumps(res))
 
