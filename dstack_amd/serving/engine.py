@@ -165,8 +165,11 @@ class LLMEngine:
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for b in self.buckets[-1:]:
-                self._decode_body(b)  # warm-up: hipBLASLt heuristics, allocator
+            # warm-up of every bucket: each row count may take a different GEMM path (HIP GEMV up to
+            # 4 rows, the in-tree fp8 GEMM, hipBLASLt) and hipBLASLt may not set up a kernel inside
+            # a capture ('operation not permitted when stream is capturing')
+            for b in self.buckets:
+                self._decode_body(b)
         torch.cuda.current_stream(self.device).wait_stream(s)
         pool = torch.cuda.graph_pool_handle()
         self._graph_logits = {}
