@@ -53,9 +53,9 @@ hipError_t dsa_gemm_nt_trace(const void*, const void*, void*, int, int, int, uns
 hipError_t dsa_gemm_nt_swiglu(const void*, const void*, void*, void*, void*, int, int, int, long, long, hipStream_t);
 bool dsa_gemm_nt_swiglu_bwd_supported(int, int, int);
 bool dsa_gemm_km_supported(int, int, int);
-bool dsa_fp8_rows_gemm_supported(int, int, int);
-hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, int, int, int, long, long,
-                             long, hipStream_t);
+bool dsa_fp8_rows_gemm_supported(int, int, int, int, int);
+hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
+                             long, long, long, int, int, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 hipError_t dsa_gemm_nt_swiglu_bwd(const void*, const void*, const void*, void*, void*, int, int, int, long, long,
                                   hipStream_t);
@@ -420,13 +420,15 @@ torch::Tensor gemm_nt_trace(torch::Tensor a, torch::Tensor b, torch::Tensor out)
 
 bool gemm_km_supported(int64_t M, int64_t N, int64_t K) { return dsa_gemm_km_supported(M, N, K); }
 
-bool fp8_rows_gemm_supported(int64_t M, int64_t N, int64_t K) {
-  return dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K);
+bool fp8_rows_gemm_supported(int64_t M, int64_t N, int64_t K, int64_t bm, int64_t S) {
+  return dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K, (int)bm, (int)S);
 }
 
 // y[M][N] = bf16(xs[m] ws[n] (xq wq^T)) for a decode batch (M <= 256), e4m3 operands
-// (csrc/fp8_gemm.hip)
-torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws) {
+// (csrc/fp8_gemm.hip); bm = 64 | 128 batch rows per workgroup; S > 1 splits K, with fp32 slabs
+// `part` (S * 256 * N floats) and tickets `cnt` ((N / 128) * ceil(M / bm) int32, zero; left zero)
+torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t bm,
+                            int64_t S, c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> cnt) {
   for (auto* t : {&xq, &wq}) {
     TORCH_CHECK(t->is_cuda() && t->element_size() == 1 && t->dim() == 2 && t->stride(1) == 1,
                 "fp8_rows_gemm: 1-byte 2-D operands with contiguous rows");
@@ -439,10 +441,24 @@ torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq
               "fp8_rows_gemm: xs fp32 [M]");
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.is_contiguous() && ws.numel() == N,
               "fp8_rows_gemm: ws fp32 [N]");
-  TORCH_CHECK(dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K), "fp8_rows_gemm: M <= 256, N % 128, K % 128 == 0");
+  TORCH_CHECK(dsa_fp8_rows_gemm_supported((int)M, (int)N, (int)K, (int)bm, (int)S),
+              "fp8_rows_gemm: M <= 256, N % 128 == 0, bm 64 | 128, K % (128 S) == 0");
+  float* pp = nullptr;
+  int* cp = nullptr;
+  if (S > 1) {
+    TORCH_CHECK(part.has_value() && cnt.has_value(), "fp8_rows_gemm: split-K needs part and cnt");
+    TORCH_CHECK(part->is_cuda() && part->scalar_type() == torch::kFloat32 && part->numel() >= S * 256 * N,
+                "fp8_rows_gemm: part needs S * 256 * N floats");
+    TORCH_CHECK(cnt->is_cuda() && cnt->scalar_type() == torch::kInt32 &&
+                    cnt->numel() >= (N / 128) * ((M + bm - 1) / bm),
+                "fp8_rows_gemm: cnt needs one int32 per output tile");
+    pp = part->data_ptr<float>();
+    cp = cnt->data_ptr<int>();
+  }
   auto y = torch::empty({M, N}, xq.options().dtype(torch::kBFloat16));
-  check(dsa_fp8_rows_gemm(xq.data_ptr(), xs.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(),
-                          (int)M, (int)N, (int)K, xq.stride(0), wq.stride(0), y.stride(0), stream()),
+  check(dsa_fp8_rows_gemm(xq.data_ptr(), xs.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(), pp,
+                          cp, (int)M, (int)N, (int)K, xq.stride(0), wq.stride(0), y.stride(0), (int)bm, (int)S,
+                          stream()),
         "fp8_rows_gemm");
   return y;
 }
@@ -641,7 +657,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_swiglu", &gemm_nt_swiglu, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("transposed") = true);
   m.def("gemm_km", &gemm_km, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("out"), pybind11::arg("mode") = 0);
   m.def("gemm_km_supported", &gemm_km_supported);
-  m.def("fp8_rows_gemm", &fp8_rows_gemm);
+  m.def("fp8_rows_gemm", &fp8_rows_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),
+        pybind11::arg("ws"), pybind11::arg("bm") = 64, pybind11::arg("split") = 1, pybind11::arg("part") = pybind11::none(),
+        pybind11::arg("cnt") = pybind11::none());
   m.def("fp8_rows_gemm_supported", &fp8_rows_gemm_supported);
   m.def("gemm_nt_trace", &gemm_nt_trace);
   m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);

@@ -3,6 +3,7 @@
 from __future__ import annotations
 
 import os
+import warnings
 
 import torch
 
@@ -303,18 +304,27 @@ def split_qkv(qkv: torch.Tensor, n_heads: int, n_kv_heads: int):
     return x[:, :, :n_heads], x[:, :, n_heads : n_heads + n_kv_heads], x[:, :, n_heads + n_kv_heads :]
 
 
+_ATTN_FALLBACK_WARNED: set = set()
+
+
 def attention(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, causal: bool = True) -> torch.Tensor:
     """Causal GQA attention on the fused projection output; returns [B, S, H*D]."""
     b, s, _ = qkv.shape
     if _ext.use_hip(qkv) and _attn_impl() == "hip":
         d = qkv.shape[-1] // (n_heads + 2 * n_kv_heads)
-        if d != 128 or s % 128 != 0:
-            raise ValueError(f"HIP flash attention needs head_dim 128 and seq_len % 128 == 0 (got head_dim {d}, "
-                             f"seq_len {s}); set DSTACK_AMD_ATTN=sdpa for other shapes")
-        return _FlashAttnQKV.apply(qkv.contiguous(), n_heads, n_kv_heads, causal)
+        if d == 128 and s % 128 == 0:
+            return _FlashAttnQKV.apply(qkv.contiguous(), n_heads, n_kv_heads, causal)
+        # the HIP kernels are tiled for head_dim 128 (Llama-3 8B/70B, Qwen2, Mistral); other shapes
+        # (Llama-3.2 1B/3B: head_dim 64) run PyTorch's SDPA, said once per shape
+        key = (d, s % 128 == 0)
+        if key not in _ATTN_FALLBACK_WARNED:
+            _ATTN_FALLBACK_WARNED.add(key)
+            warnings.warn(f"HIP flash attention is tiled for head_dim 128 and seq_len % 128 == 0 (got head_dim {d}, "
+                          f"seq_len {s}): using PyTorch SDPA for this shape", RuntimeWarning, stacklevel=2)
     q, k, v = split_qkv(qkv, n_heads, n_kv_heads)
     if q.is_cuda:
-        # library attention (PyTorch-ROCm SDPA) — opt-in A/B baseline only (DSTACK_AMD_ATTN=sdpa)
+        # library attention (PyTorch-ROCm SDPA): shapes the HIP kernels do not tile, or the
+        # DSTACK_AMD_ATTN=sdpa A/B baseline
         o = torch.nn.functional.scaled_dot_product_attention(
             q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=causal, enable_gqa=True
         ).transpose(1, 2)

@@ -510,7 +510,7 @@ class ServingLlama:
         N = w.q.shape[0]
         if M > 256 or K > 8192 or (N // 128) * ((M + 63) // 64) > 256:
             return None
-        if xq.stride(0) % 16 or w.q.stride(0) % 16 or not C.fp8_rows_gemm_supported(M, N, K):
+        if xq.stride(0) % 16 or w.q.stride(0) % 16 or not C.fp8_rows_gemm_supported(M, N, K, 64, 1):
             return None
         return C.fp8_rows_gemm(xq.view(torch.uint8), xs, w.q.view(torch.uint8), w.s)
 

@@ -669,10 +669,13 @@ def test_swiglu_mlp_fused_matches_separate_kernels(gpu, monkeypatch, wgrad):
         assert rel < 1e-2, f"{name}: rel err {rel}"
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (37, 384, 512), (200, 256, 1024), (1, 128, 256), (64, 1024, 384)])
-def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K):
-    """Decode-batch fp8 GEMM (csrc/fp8_gemm.hip: scaled 16x16x128 f8f6f4 MFMA over 64-row batch
-    blocks) against the fp32 product of the same e4m3 operands and scales."""
+@pytest.mark.parametrize("M,N,K,bm,split", [(256, 256, 512, 64, 1), (37, 384, 512, 64, 1), (200, 256, 1024, 128, 2),
+                                             (1, 128, 256, 64, 1), (64, 1024, 384, 64, 1), (256, 512, 1024, 128, 1),
+                                             (130, 256, 2048, 128, 4), (256, 1024, 512, 64, 2)])
+def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K, bm, split):
+    """Decode-batch fp8 GEMM (csrc/fp8_gemm.hip: scaled 16x16x128 f8f6f4 MFMA over 64/128-row batch
+    blocks, optional split-K with a last-arrival combine) against the fp32 product of the same
+    e4m3 operands and scales; twice, since the split-K tickets must be left at zero."""
     C = _ext.require()
     torch.manual_seed(M + N + K)
     x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
@@ -680,6 +683,31 @@ def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K):
     xq, xs = ref.quant_fp8_rows(x)
     wq, ws = ref.quant_fp8_rows(w)
     want = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
-    y = C.fp8_rows_gemm(xq.view(torch.uint8), xs, wq.view(torch.uint8), ws)
-    err = ((y.float() - want).norm() / want.norm()).item()
-    assert err < 1e-2, err
+    part = torch.empty(split * 256 * N, device=gpu, dtype=torch.float32)
+    cnt = torch.zeros((N // 128) * ((M + bm - 1) // bm), device=gpu, dtype=torch.int32)
+    for _ in range(2):
+        y = C.fp8_rows_gemm(xq.view(torch.uint8), xs, wq.view(torch.uint8), ws, bm, split, part, cnt)
+        err = ((y.float() - want).norm() / want.norm()).item()
+        assert err < 1e-2, err
+    assert int(cnt.abs().sum().item()) == 0
+
+
+def test_attention_head_dim_64_runs_sdpa_with_a_warning(gpu):
+    """Llama-3.2 1B/3B shapes (head_dim 64) are not tiled by the HIP flash kernels: the op runs
+    PyTorch's SDPA for them (warned once per shape) and matches the fp32 reference, forward and
+    backward."""
+    import warnings as _w
+
+    torch.manual_seed(0)
+    H, KVH, D, S = 8, 2, 64, 256
+    qkv = _rand(1, S, (H + 2 * KVH) * D, device=gpu).requires_grad_()
+    ops.functional._ATTN_FALLBACK_WARNED.discard((D, True))
+    with _w.catch_warnings(record=True) as rec:
+        _w.simplefilter("always")
+        o = ops.attention(qkv, H, KVH)
+    assert any("SDPA" in str(r.message) for r in rec)
+    q, k, v = ops.functional.split_qkv(qkv.detach().float(), H, KVH)
+    want = ref.attention(q, k, v, True).reshape(1, S, -1)
+    assert ((o.float() - want).norm() / want.norm()).item() < 2e-2
+    o.float().square().sum().backward()
+    assert qkv.grad is not None and torch.isfinite(qkv.grad).all()

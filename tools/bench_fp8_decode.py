@@ -43,7 +43,15 @@ def main():
             wq, ws = ref.quant_fp8_rows(w)
             wq = wq.view(torch.uint8)
             del w
-            ours = lambda: C.fp8_rows_gemm(xq, xs, wq, ws)  # noqa: E731
+            variants = {}
+            for bm, sp in ((64, 1), (128, 1), (128, 2), (128, 4), (64, 2)):
+                if not C.fp8_rows_gemm_supported(M, N, K, bm, sp):
+                    continue
+                part = torch.empty(sp * 256 * N, device="cuda", dtype=torch.float32)
+                cnt = torch.zeros((N // 128) * ((M + bm - 1) // bm), device="cuda", dtype=torch.int32)
+                variants[f"bm{bm}s{sp}"] = (lambda bm=bm, sp=sp, part=part, cnt=cnt:
+                                            C.fp8_rows_gemm(xq, xs, wq, ws, bm, sp, part, cnt))
+            ours = variants["bm64s1"]
             pad = -M % 16
             xq_l = torch.nn.functional.pad(xq, (0, 0, 0, pad)) if pad else xq
             xs_l = torch.nn.functional.pad(xs, (0, pad), value=1.0) if pad else xs
@@ -51,15 +59,20 @@ def main():
                                            scale_a=xs_l.view(-1, 1), scale_b=ws.view(1, -1), out_dtype=torch.bfloat16)
             y0, y1 = ours(), lib()[:M]
             err = ((y0.float() - y1.float()).norm() / y1.float().norm()).item()
-            to, tl = [], []
+            to, tl, tv = [], [], {k: [] for k in variants}
             for _ in range(5):
                 to.append(timed(ours))
                 tl.append(timed(lib))
+                for k, fn in variants.items():
+                    tv[k].append(timed(fn))
             wb = N * K
             r = {"M": M, "N": N, "K": K, "ours_us": statistics.median(to) * 1e3,
                  "lib_us": statistics.median(tl) * 1e3, "ours_tb_s": wb / statistics.median(to) / 1e9,
                  "lib_tb_s": wb / statistics.median(tl) / 1e9, "rel_diff": err}
             r["speedup"] = r["lib_us"] / r["ours_us"]
+            r.update({k + "_us": statistics.median(v) * 1e3 for k, v in tv.items()})
+            for k in tv:
+                assert ((variants[k]().float() - y1.float()).norm() / y1.float().norm()).item() < 1e-2, k
             res[f"{name}_m{M}"] = r
             print(f"{name}_m{M}", json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in r.items()}),
                   flush=True)
