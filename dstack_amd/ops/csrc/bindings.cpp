@@ -43,6 +43,7 @@ bool dsa_rmsnorm_fwd_fp8_supported(int, int);
 hipError_t dsa_rmsnorm_fwd_fp8(const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
                                hipStream_t);
 hipError_t dsa_quant_fp8_rows(const void*, long, void*, long, float*, int, int, hipStream_t);
+hipError_t dsa_swiglu_quant_fp8_rows(const void*, long, void*, long, float*, int, int, hipStream_t);
 bool dsa_gemv_fp8_supported(int, int);
 hipError_t dsa_gemv_fp8(const void*, long, const void*, const float*, void*, long, int, int, int, hipStream_t);
 hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
@@ -343,6 +344,22 @@ torch::Tensor gemv(torch::Tensor x, torch::Tensor w) {
 }
 
 // FP8 (e4m3) rows: q [M, K] uint8 (view as float8_e4m3fn) and s [M] fp32, x[m] ~= q[m] * s[m]
+// gu [M, 2F] bf16 -> (q [M, F] e4m3 bytes, s [M] fp32) of bf16(silu(gate) * up), per-row scales
+std::vector<torch::Tensor> swiglu_quant_fp8_rows(torch::Tensor gu) {
+  TORCH_CHECK(gu.is_cuda() && gu.scalar_type() == torch::kBFloat16 && gu.dim() == 2 && gu.stride(1) == 1,
+              "swiglu_quant_fp8_rows: gu must be bf16 [M, 2F] with contiguous rows");
+  TORCH_CHECK(gu.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(gu.data_ptr()) % 16 == 0 && gu.size(1) % 16 == 0,
+              "swiglu_quant_fp8_rows: alignment (2F % 16 == 0)");
+  const int64_t M = gu.size(0), F = gu.size(1) / 2;
+  auto q = torch::empty({M, F}, gu.options().dtype(torch::kUInt8));
+  auto sc = torch::empty({M}, gu.options().dtype(torch::kFloat32));
+  if (M > 0)
+    check(dsa_swiglu_quant_fp8_rows(gu.data_ptr(), gu.stride(0), q.data_ptr(), F, sc.data_ptr<float>(), (int)M,
+                                    (int)F, stream()),
+          "swiglu_quant_fp8_rows");
+  return {q, sc};
+}
+
 std::vector<torch::Tensor> quant_fp8_rows(torch::Tensor x) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.stride(1) == 1,
               "quant_fp8_rows: x must be bf16 [M, K] with contiguous rows");
@@ -661,6 +678,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("ws"), pybind11::arg("bm") = 64, pybind11::arg("split") = 1, pybind11::arg("part") = pybind11::none(),
         pybind11::arg("cnt") = pybind11::none());
   m.def("fp8_rows_gemm_supported", &fp8_rows_gemm_supported);
+  m.def("swiglu_quant_fp8_rows", &swiglu_quant_fp8_rows);
   m.def("gemm_nt_trace", &gemm_nt_trace);
   m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);
   m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd, pybind11::arg("dy"), pybind11::arg("wdT"), pybind11::arg("gu"),

@@ -73,6 +73,51 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restric
   }
 }
 
+// SwiGLU + per-row quantization for the fp8 down projection of a decode step: gu [M][2F] bf16
+// (gate | up) -> q [M][F] e4m3 + s [M], q * s ~= bf16(silu(g) * u) -- the separate swiglu_fwd and
+// quant_rows kernels wrote and re-read the bf16 product.  One workgroup per row: pass 1 takes the
+// row max of the bf16-rounded product, pass 2 recomputes it (the row's gu is L2-resident by then)
+// and writes e4m3.
+__device__ __forceinline__ float silu_q(float g) { return g / (1.f + __expf(-g)); }
+
+__global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __restrict__ gu, long ldg,
+                                                                unsigned char* __restrict__ q, long ldq,
+                                                                float* __restrict__ s, int F) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* gr = gu + (long)row * ldg;
+  auto prod8 = [&](int k, float* a) {
+    float g[8], u[8];
+    unpack8(*reinterpret_cast<const us8*>(gr + k), g);
+    unpack8(*reinterpret_cast<const us8*>(gr + F + k), u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = bf2f(f2bf(silu_q(g[i]) * u[i]));
+  };
+  float amax = 0.f;
+  for (int k = tid * 8; k < F; k += 256 * 8) {
+    float a[8];
+    prod8(k, a);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(a[i]));
+  }
+  amax = wave_max(amax);
+  if ((tid & 63) == 0) red[tid >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float scale = fmaxf(amax, 1e-12f) / E4M3_MAX;
+  const float inv = 1.f / scale;
+  if (tid == 0) s[row] = scale;
+  unsigned char* qr = q + (long)row * ldq;
+  for (int k = tid * 8; k < F; k += 256 * 8) {
+    float a[8];
+    prod8(k, a);
+    unsigned int w0 = f32x4_to_fp8(a[0] * inv, a[1] * inv, a[2] * inv, a[3] * inv);
+    unsigned int w1 = f32x4_to_fp8(a[4] * inv, a[5] * inv, a[6] * inv, a[7] * inv);
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+  }
+}
+
 template <int M, int U>
 __global__ __launch_bounds__(256) void gemv_fp8_kernel(const bf16_t* __restrict__ x, long ldx,
                                                        const unsigned char* __restrict__ W,
@@ -205,6 +250,13 @@ extern "C" hipError_t dsa_quant_fp8_rows(const void* x, long ldx, void* q, long 
                                          hipStream_t st) {
   if (!dsa_quant_fp8_supported(K) || M <= 0) return hipErrorInvalidValue;
   quant_rows_kernel<<<M, 256, 0, st>>>((const bf16_t*)x, ldx, (unsigned char*)q, ldq, s, K);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsa_swiglu_quant_fp8_rows(const void* gu, long ldg, void* q, long ldq, float* s, int M, int F,
+                                                hipStream_t st) {
+  if (F <= 0 || F % 8 || M <= 0) return hipErrorInvalidValue;
+  swiglu_quant_rows_kernel<<<M, 256, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F);
   return hipGetLastError();
 }
 

@@ -531,7 +531,14 @@ class ServingLlama:
     def _mlp_and_attn_out(self, L, x, o):
         """(x + o @ wo^T) -> norm -> SwiGLU MLP; returns (new residual, mlp output)."""
         x, h = self._add_rms(x, self._reduce(self._mm(o, L["wo"])), L["ffn_norm"], next_w=L["wgu"])
-        return x, self._reduce(self._mm(self._swiglu(self._mm(h, L["wgu"])), L["wdown"]))
+        gu = self._mm(h, L["wgu"])
+        wd = L["wdown"]
+        if self.hip and isinstance(wd, Fp8Weight) and not (self.gemv and gu.shape[0] <= 4):
+            # fp8 down projection past the GEMV's rows: SwiGLU and the per-token e4m3 quantization
+            # in one kernel (no bf16 product written and re-read)
+            q, sc = _ext.require().swiglu_quant_fp8_rows(gu if gu.stride(-1) == 1 else gu.contiguous())
+            return x, self._reduce(self._mm_fp8(Fp8Act(q, sc), wd))
+        return x, self._reduce(self._mm(self._swiglu(gu), wd))
 
     # ------------------------------------------------------------------------------------------
     # forward passes

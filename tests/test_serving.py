@@ -838,3 +838,19 @@ def test_api_completions_rejects_before_submitting_any_prompt(api):
         return [ln for ln in m.splitlines() if ln.startswith("dstack_serving_requests_total")][0]
 
     assert reqs(before) == reqs(after)
+
+
+@pytest.mark.gpu
+def test_gpu_swiglu_quant_fp8_rows_matches_separate_kernels(gpu):
+    """The fused SwiGLU + per-row e4m3 quantization equals swiglu_fwd followed by quant_fp8_rows
+    (same bf16-rounded product, same scales, same bytes)."""
+    from dstack_amd.ops import _ext
+
+    C = _ext.require()
+    torch.manual_seed(0)
+    for M, F in ((1, 512), (37, 1024), (256, 3584)):
+        gu = torch.randn(M, 2 * F, device=gpu, dtype=torch.bfloat16) * 2
+        q, s = C.swiglu_quant_fp8_rows(gu)
+        q2, s2 = C.quant_fp8_rows(C.swiglu_fwd(gu))
+        assert torch.equal(s, s2)
+        assert torch.equal(q.view(torch.uint8), q2.view(torch.uint8))
