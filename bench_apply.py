@@ -52,6 +52,25 @@ STAGES = [  # (name, start stamp, end stamp) -- stamps: server timings + the tas
 ]
 
 
+def _free_port_pair() -> int:
+    """A port p with p and p + 1 free on this host (the task's store and its RCCL pre-flight)."""
+    import socket
+
+    for _ in range(50):
+        with socket.socket() as a:
+            a.bind(("127.0.0.1", 0))
+            port = a.getsockname()[1]
+            if port >= 65535:
+                continue
+            with socket.socket() as b:
+                try:
+                    b.bind(("127.0.0.1", port + 1))
+                except OSError:
+                    continue
+            return port
+    return 29611
+
+
 def task_conf(gpus: int, steps: int, warmup: int, extra_args: str, use_gpu: bool, name: str):
     """The example task, as ``dstack apply`` would submit it, run from this checkout."""
     import yaml
@@ -70,7 +89,10 @@ def task_conf(gpus: int, steps: int, warmup: int, extra_args: str, use_gpu: bool
         conf["resources"] = {"gpu": f"MI355X:{gpus}"}
     else:
         conf["resources"] = {"cpu": "1..", "gpu": 0}
-    conf["env"] = list(conf.get("env", [])) + [f"PYTHONPATH={REPO}", "OMP_NUM_THREADS=1"]
+    # a rendezvous port of its own: under the driver's torchrun (bench.py --gpus N) the default
+    # 29500 may be the outer job's store, and the RCCL pre-flight takes the next port too
+    conf["env"] = list(conf.get("env", [])) + [f"PYTHONPATH={REPO}", "OMP_NUM_THREADS=1",
+                                               f"MASTER_PORT={_free_port_pair()}"]
     return parse_run_configuration(conf)
 
 
