@@ -54,6 +54,8 @@ hipError_t dsa_gemm_nt_trace(const void*, const void*, void*, int, int, int, uns
 hipError_t dsa_gemm_nt_swiglu(const void*, const void*, void*, void*, void*, int, int, int, long, long, hipStream_t);
 bool dsa_gemm_nt_swiglu_bwd_supported(int, int, int);
 bool dsa_gemm_km_supported(int, int, int);
+hipError_t dsa_fa_dkdv_trace(const void*, const void*, const float*, const float*, float*, float*, unsigned long long*,
+                             int, int, int, int, float, hipStream_t);
 bool dsa_fp8_rows_gemm_supported(int, int, int, int, int);
 hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
                              long, long, long, int, int, hipStream_t);
@@ -322,6 +324,24 @@ torch::Tensor flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tenso
                    ws.data_ptr(), B, S, H, KVH, D, 1.0f / std::sqrt((float)D), causal ? 1 : 0, stream()),
         "flash_attn_bwd");
   return dqkv;
+}
+
+// diagnostic: per-phase s_memtime stamps of the causal 8-wave dK/dV pass (waves 0 and 4 of
+// workgroup 0, q-tiles 8..11, 5 points each) -> int64 [2, 64]
+torch::Tensor fa_dkdv_trace(torch::Tensor qkv, torch::Tensor dout, torch::Tensor lse, torch::Tensor delta, int64_t H,
+                            int64_t KVH) {
+  check_bf16(qkv, "qkv");
+  check_bf16(dout, "dout");
+  const int B = qkv.size(0), S = qkv.size(1);
+  auto f32 = qkv.options().dtype(torch::kFloat32);
+  auto dkp = torch::empty({B, S, H, 128}, f32), dvp = torch::empty({B, S, H, 128}, f32);
+  auto tr = torch::zeros({2, 64}, qkv.options().dtype(torch::kInt64));
+  const float sl2 = 1.4426950408889634f / std::sqrt(128.f);
+  check(dsa_fa_dkdv_trace(qkv.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                          dkp.data_ptr<float>(), dvp.data_ptr<float>(),
+                          reinterpret_cast<unsigned long long*>(tr.data_ptr()), B, S, (int)H, (int)KVH, sl2, stream()),
+        "fa_dkdv_trace");
+  return tr;
 }
 
 bool gemm_tn_supported(int64_t P, int64_t Q, int64_t T) { return dsa_gemm_tn_supported(P, Q, T); }
@@ -661,6 +681,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("fa_dkdv_trace", &fa_dkdv_trace);
   m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("rms_norm_fp8", &rms_norm_fp8);
   m.def("rms_norm_fp8_supported", &rms_norm_fp8_supported);

@@ -469,7 +469,10 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 // written once as bf16 straight into dqkv -- no fp32 per-q-head partials in HBM (2 x B*S*H*128*4
 // bytes written and read back) and no reduce kernel.  Grid: B * KVH * S/128 workgroups, each G
 // times longer; K/V are staged into LDS once per block instead of once per query head.
-template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false, bool GQA = false>
+// TR (diagnostic, DSTACK_AMD_FA_TRACE=1 through dsa_fa_dkdv_trace): waves 0 and 4 of workgroup 0
+// stamp s_memtime at 5 points of q-tiles 8..11 (tile top, after S/dP, after the softmax / dS math,
+// after dV/dK, after the tile barrier) into the buffer passed as `dsg` -- where a tile's cycles go
+template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false, bool GQA = false, bool TR = false>
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
@@ -545,8 +548,22 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
   wait_dma_and_barrier();
 
   const int h_end = h_first + n_heads;
-  int qt = qt_begin, stage = 0;
+  int qt = qt_begin, stage = 0, tnum = 0;
+  const bool tracer = TR && blockIdx.x == 0 && (w == 0 || w == 4);
+  auto stamp = [&](int k) {
+    if constexpr (TR) {
+      if (tracer && tnum >= 8 && tnum < 12) {
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0)
+          reinterpret_cast<unsigned long long*>(dsg)[(w >> 2) * 64 + (tnum - 8) * 5 + k] = t;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
   for (;;) {
+    stamp(0);
     const char* ql = ring + stage * STAGE;
     const char* dol = ql + TILE_BYTES;
     const float* ll = reinterpret_cast<const float*>(ql + 2 * TILE_BYTES);
@@ -582,6 +599,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
         sc = mfma(lds_row(ql, 32 * qh + l32, 2 * ks + hf), lds_row(kl, 32 * g + l32, 2 * ks + hf), sc);
         dpv = mfma(lds_row(dol, 32 * qh + l32, 2 * ks + hf), lds_row(vl, 32 * g + l32, 2 * ks + hf), dpv);
       }
+      stamp(1);
       const bool diag = CAUSAL && qlo < kw0 + 31;
       // P, then (diagonal tiles only, a wave-uniform branch: 2 of ~64 tiles) the causal mask, then
       // dS.  Folding the mask into the P loop as a select costs every tile 16 v_cmp + 16 v_cndmask
@@ -615,6 +633,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
         pb[k2] = to_bf16x8(sc, 8 * k2);
         dsb[k2] = to_bf16x8(dpv, 8 * k2);
       }
+      stamp(2);
       if constexpr (SPILL) {  // lane = key mykey, registers 4*rr+i = queries qlo + 8*rr + 4*hf + i
         bf16_t* dt = dsg + (((long)b * H + hh) * S + mykey) * S + qlo + 4 * hf;
 #pragma unroll
@@ -630,7 +649,10 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
           dk[d] = mfma(lds_tr(ql, 32 * qh + 16 * k2, 32 * d, lane), dsb[k2], dk[d]);
         }
     }
+    stamp(3);
     wait_dma_and_barrier();
+    stamp(4);
+    ++tnum;
     if (!more) break;
     qt = nqt_next;
     hh = nh;
@@ -1307,5 +1329,17 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   int g = (int)((work + 255) / 256);
   if (g > 4096) g = 4096;
   fa_bwd_reduce_kv_kernel<<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH);
+  return hipGetLastError();
+}
+
+// Diagnostic: one causal dK/dV pass (8-wave kernel) with waves 0 and 4 of workgroup 0 stamping 5
+// points of q-tiles 8..11 (trace [2][64] int64; index (tile - 8) * 5 + point).
+extern "C" hipError_t dsa_fa_dkdv_trace(const void* qkv, const void* dout, const float* lse, const float* delta,
+                                        float* dkp, float* dvp, unsigned long long* trace, int B, int S, int H,
+                                        int KVH, float sl2, hipStream_t st) {
+  if (S % 128) return hipErrorInvalidValue;
+  const size_t lds8 = 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512);
+  fa_bwd_dkdv8_kernel<true, false, false, false, false, true><<<B * H * (S / 128), 512, lds8, st>>>(
+      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, (bf16_t*)trace);
   return hipGetLastError();
 }
