@@ -65,7 +65,9 @@ constexpr int HD = 128;          // head dim
 // waves 4-7 at kernel start, no per-phase flips.  Measured (4 interleaved runs, S=8192,
 // profiles/fa_hprio_ab_r4y.txt): forward 0.656-0.670 vs 0.657-0.668 ms, backward 2.018-2.036 vs
 // 2.009-2.053 ms -- within noise, kept opt-in.
-template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0, bool STAG = false>
+// BUF (DSTACK_AMD_FA_FWD_BUF=1): K/V tiles through buffer descriptors (dma_tile64_buf), which keeps
+// the S phase's LDS-read waits counted instead of lgkmcnt(0).
+template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0, bool STAG = false, bool BUF = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
                                                         float* __restrict__ lse, int B, int S,
@@ -107,8 +109,20 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
   bf16x8 pbp[4];                             // the deferred P of the previous tile (late waves)
   bool pend = false;
 
-  dma_tile64_n<NW>(kp, rs, smem, w, lane);
-  dma_tile64_n<NW>(vp, rs, smem + TILE_BYTES, w, lane);
+  const unsigned kvbytes = (unsigned)(((long)(S - 1) * rs + HD) * 2);
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(kp, kvbytes), vrs = make_rsrc(vp, kvbytes);
+  unsigned kvoff[16 / NW];
+  dma_tile64_offsets<NW>(rs, w, lane, kvoff);
+  auto issue = [&](int t, char* nk) {
+    if constexpr (BUF) {
+      dma_tile64_buf<NW>(krs, kvoff, (int)((long)t * 64 * rs * 2), nk, w);
+      dma_tile64_buf<NW>(vrs, kvoff, (int)((long)t * 64 * rs * 2), nk + TILE_BYTES, w);
+    } else {
+      dma_tile64_n<NW>(kp + (long)t * 64 * rs, rs, nk, w, lane);
+      dma_tile64_n<NW>(vp + (long)t * 64 * rs, rs, nk + TILE_BYTES, w, lane);
+    }
+  };
+  issue(0, smem);
   wait_dma_and_barrier();
 
   int stg = 0;  // ring slot of tile it
@@ -116,11 +130,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
     const char* kl = smem + stg * 2 * TILE_BYTES;
     const char* vl = kl + TILE_BYTES;
     const int nstg = stg + 1 == NST ? 0 : stg + 1;
-    if (it + 1 < nkv) {
-      char* nk = smem + nstg * 2 * TILE_BYTES;
-      dma_tile64_n<NW>(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
-      dma_tile64_n<NW>(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
-    }
+    if (it + 1 < nkv) issue(it + 1, smem + nstg * 2 * TILE_BYTES);
     if constexpr (STAG) {
       if (late && pend) {  // P·V of the previous tile, whose V is still in its ring slot
         const char* pv = smem + (stg == 0 ? NST - 1 : stg - 1) * 2 * TILE_BYTES + TILE_BYTES;
@@ -472,7 +482,12 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 // TR (diagnostic, DSTACK_AMD_FA_TRACE=1 through dsa_fa_dkdv_trace): waves 0 and 4 of workgroup 0
 // stamp s_memtime at 5 points of q-tiles 8..11 (tile top, after S/dP, after the softmax / dS math,
 // after dV/dK, after the tile barrier) into the buffer passed as `dsg` -- where a tile's cycles go
-template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false, bool GQA = false, bool TR = false>
+// PF (DSTACK_AMD_FA_DKDV_PF=1): the S/dP phase keeps the next step's two fragment reads in flight
+// while the current MFMA runs (S and dP alternate, so consecutive MFMAs never share an accumulator),
+// pinned with sched_group_barrier; without it the compiler serialises read -> lgkmcnt(0) -> MFMA
+// for most of the 16 steps.
+template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false, bool GQA = false, bool TR = false,
+          int PF = 0>
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
@@ -528,8 +543,19 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
   // under the previous head's last one.  Without GQA this is the plain q-tile loop.
   const __amdgpu_buffer_rsrc_t lrs0 = make_rsrc(lse + ((long)b * H + h_first) * S, (unsigned)S * 4);
   const __amdgpu_buffer_rsrc_t drs0 = make_rsrc(delta + ((long)b * H + h_first) * S, (unsigned)S * 4);
+  // PF: the Q / dO tiles come through one buffer descriptor per wave (Q for waves 0-3, dO for 4-7)
+  // with 4 loop-invariant 32-bit per-lane offsets and the tile's row offset in an SGPR, instead of
+  // 4 rematerialised 64-bit address pairs per tile (frees ~20 VGPRs for the read pipeline)
+  const long tstride = qh == 0 ? rs : ors;
+  const __amdgpu_buffer_rsrc_t trs =
+      make_rsrc(qh == 0 ? base + h_first * HD : dout + (long)b * S * ors + h_first * HD,
+                (unsigned)(((long)(S - 1) * tstride + HD) * 2));
+  unsigned toff[4];
+  dma_tile64_offsets<4>(tstride, w4, lane, toff);
   auto issue = [&](int h, int qt, char* st) {
-    if (qh == 0)
+    if constexpr (PF && !GQA)
+      dma_tile64_buf<4>(trs, toff, (int)((long)qt * 64 * tstride * 2), st + qh * TILE_BYTES, w4);
+    else if (qh == 0)
       dma_tile64(base + h * HD + (long)qt * 64 * rs, rs, st, w4, lane);
     else
       dma_tile64(dout + (long)b * S * ors + h * HD + (long)qt * 64 * ors, ors, st + TILE_BYTES, w4, lane);
@@ -594,10 +620,42 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
           dpv[4 * rr + i] = SEED ? -Dl[i] : 0.f;
         }
       }
+      if constexpr (PF) {
+        // step i: chain i & 1 (0 = S from Q.K^T, 1 = dP from dO.V^T), k-slice i >> 1
+        auto rd_a = [&](int i) { return lds_row((i & 1) ? dol : ql, 32 * qh + l32, 2 * (i >> 1) + hf); };
+        auto rd_b = [&](int i) { return lds_row((i & 1) ? vl : kl, 32 * g + l32, 2 * (i >> 1) + hf); };
+        constexpr int NB = PF + 1;  // fragment buffers: PF steps in flight + the one computing
+        bf16x8 fa[NB], fb[NB];
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        sc = mfma(lds_row(ql, 32 * qh + l32, 2 * ks + hf), lds_row(kl, 32 * g + l32, 2 * ks + hf), sc);
-        dpv = mfma(lds_row(dol, 32 * qh + l32, 2 * ks + hf), lds_row(vl, 32 * g + l32, 2 * ks + hf), dpv);
+        for (int j = 0; j < PF; ++j) {
+          fa[j] = rd_a(j);
+          fb[j] = rd_b(j);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const bf16x8 a = fa[i % NB], bb = fb[i % NB];
+          if (i + PF < 16) {
+            fa[(i + PF) % NB] = rd_a(i + PF);
+            fb[(i + PF) % NB] = rd_b(i + PF);
+          }
+          if (i & 1)
+            dpv = mfma(a, bb, dpv);
+          else
+            sc = mfma(a, bb, sc);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * PF, 0);
+#pragma unroll
+        for (int i = 0; i < 16 - PF; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, PF, 0);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          sc = mfma(lds_row(ql, 32 * qh + l32, 2 * ks + hf), lds_row(kl, 32 * g + l32, 2 * ks + hf), sc);
+          dpv = mfma(lds_row(dol, 32 * qh + l32, 2 * ks + hf), lds_row(vl, 32 * g + l32, 2 * ks + hf), dpv);
+        }
       }
       stamp(1);
       const bool diag = CAUSAL && qlo < kw0 + 31;
@@ -913,7 +971,10 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __re
 // ================================================================================================
 // Backward dQ pass: workgroup = 128 queries of one (b, q-head); loops over 64-key K/V tiles.
 // ================================================================================================
-template <bool CAUSAL, int NW = 4, bool HP = false>
+// PF > 0 (DSTACK_AMD_FA_DQ_PF): K/V tiles through a buffer descriptor (counted LDS waits, see
+// dma_tile64_buf) and the 32 S/dP fragment reads of a tile kept PF steps ahead of their MFMAs;
+// the default form reads -> lgkmcnt(0) -> MFMA on every step.
+template <bool CAUSAL, int NW = 4, bool HP = false, int PF = 0>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
                                                            const bf16_t* __restrict__ dout,
                                                            const float* __restrict__ lse,
@@ -956,17 +1017,25 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(con
     for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
   const int nkv = CAUSAL ? (q0 + QB) / 64 : S / 64;
 
-  dma_tile64_n<NW>(kp, rs, smem, w, lane);
-  dma_tile64_n<NW>(vp, rs, smem + TILE_BYTES, w, lane);
+  const unsigned kvbytes = (unsigned)(((long)(S - 1) * rs + HD) * 2);
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(kp, kvbytes), vrs = make_rsrc(vp, kvbytes);
+  unsigned kvoff[16 / NW];
+  dma_tile64_offsets<NW>(rs, w, lane, kvoff);
+  auto issue = [&](int t, char* nk) {
+    if constexpr (PF > 0) {
+      dma_tile64_buf<NW>(krs, kvoff, (int)((long)t * 64 * rs * 2), nk, w);
+      dma_tile64_buf<NW>(vrs, kvoff, (int)((long)t * 64 * rs * 2), nk + TILE_BYTES, w);
+    } else {
+      dma_tile64_n<NW>(kp + (long)t * 64 * rs, rs, nk, w, lane);
+      dma_tile64_n<NW>(vp + (long)t * 64 * rs, rs, nk + TILE_BYTES, w, lane);
+    }
+  };
+  issue(0, smem);
   wait_dma_and_barrier();
   for (int it = 0; it < nkv; ++it) {
     const char* kl = smem + (it & 1) * 2 * TILE_BYTES;
     const char* vl = kl + TILE_BYTES;
-    if (it + 1 < nkv) {
-      char* nk = smem + ((it + 1) & 1) * 2 * TILE_BYTES;
-      dma_tile64_n<NW>(kp + (long)(it + 1) * 64 * rs, rs, nk, w, lane);
-      dma_tile64_n<NW>(vp + (long)(it + 1) * 64 * rs, rs, nk + TILE_BYTES, w, lane);
-    }
+    if (it + 1 < nkv) issue(it + 1, smem + ((it + 1) & 1) * 2 * TILE_BYTES);
     const int kv0 = it * 64;
     if (!CAUSAL || kv0 <= qw0 + 31) {
       f32x16 st[2], dpt[2];
@@ -977,11 +1046,39 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(con
           st[t][r] = 0.f;
           dpt[t][r] = NW == 8 ? -Dl : 0.f;  // 8 waves: -delta seeds dP (see the launch note)
         }
+      }
+      if constexpr (PF > 0) {
+        // step i: key sub-tile i >> 4, k-slice (i >> 1) & 7, chain i & 1 (0 = S from K, 1 = dP from V)
+        auto rd = [&](int i) { return lds_row((i & 1) ? vl : kl, 32 * (i >> 4) + l32, 2 * ((i >> 1) & 7) + hf); };
+        constexpr int NB = PF + 1;
+        bf16x8 fr[NB];
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          st[t] = mfma(lds_row(kl, 32 * t + l32, 2 * ks + hf), qf[ks], st[t]);
-          dpt[t] = mfma(lds_row(vl, 32 * t + l32, 2 * ks + hf), df[ks], dpt[t]);
+        for (int j = 0; j < PF; ++j) fr[j] = rd(j);
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          const bf16x8 a = fr[i % NB];
+          if (i + PF < 32) fr[(i + PF) % NB] = rd(i + PF);
+          const int t = i >> 4, ks = (i >> 1) & 7;
+          if (i & 1)
+            dpt[t] = mfma(a, df[ks], dpt[t]);
+          else
+            st[t] = mfma(a, qf[ks], st[t]);
         }
+        __builtin_amdgcn_sched_group_barrier(0x100, PF, 0);
+#pragma unroll
+        for (int i = 0; i < 32 - PF; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, PF, 0);
+      } else {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int ks = 0; ks < 8; ++ks) {
+            st[t] = mfma(lds_row(kl, 32 * t + l32, 2 * ks + hf), qf[ks], st[t]);
+            dpt[t] = mfma(lds_row(vl, 32 * t + l32, 2 * ks + hf), df[ks], dpt[t]);
+          }
       }
       const bool diag = CAUSAL && kv0 + 63 > qw0;
       // P, the causal mask on diagonal tiles only (a wave-uniform branch, not a per-element select
@@ -1139,6 +1236,11 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     const char* v = getenv("DSTACK_AMD_FA_HALF_PRIO");
     return v && atoi(v) == 1;
   }();
+  static const bool fwd_buf_env = [] {
+    const char* v = getenv("DSTACK_AMD_FA_FWD_BUF");
+    return v && atoi(v) == 1;
+  }();
+  const bool fwd_buf = fwd_buf_env && (long)S * (H + 2 * KVH) * HD * 2 < (1L << 31);
   if (waves == 8 && S % 256 == 0) {
     const int grid = B * H * (S / 256);
     if (causal && pf && half_prio)
@@ -1153,6 +1255,9 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     else if (causal && pf && prio == 2)
       fa_fwd_kernel<true, 8, true, 2><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2,
                                                             thr);
+    else if (causal && pf && fwd_buf)
+      fa_fwd_kernel<true, 8, true, 0, false, true><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S,
+                                                                         H, KVH, sl2, thr);
     else if (causal && pf)
       fa_fwd_kernel<true, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2, thr);
     else if (causal)
@@ -1246,6 +1351,20 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     return v && atoi(v) == 1;
   }();
   const bool dkdv_gqa = dkdv_gqa_env && dkdv_kind == 8 && !half_prio && !fa_ds_spill(B, S, H);
+  // S/dP read pipeline of the 8-wave dK/dV pass (DSTACK_AMD_FA_DKDV_PF=0|1|2, default 2).  Whole
+  // backward at S=8192, 3 interleaved runs (profiles/fa_bwd_pf_ab_r8t.txt): PF 0 2.031-2.045 ms,
+  // PF 2 1.959-1.963 ms.  The dQ pass's counterpart (DSTACK_AMD_FA_DQ_PF=1|2) measured no gain.
+  static const int dkdv_pf_env = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DKDV_PF");
+    return v ? atoi(v) : 2;
+  }();
+  // the PF form addresses a Q / dO tile through a buffer descriptor with 32-bit offsets
+  const int dkdv_pf = ((long)S * (H + 2 * KVH) * HD * 2 < (1L << 31)) ? dkdv_pf_env : 0;
+  static const int dq_pf_env = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DQ_PF");
+    return v ? atoi(v) : 0;
+  }();
+  const int dq_pf = ((long)S * (H + 2 * KVH) * HD * 2 < (1L << 31)) ? dq_pf_env : 0;
 #define DSA_DKDV(C, N)                                                                                 \
   do {                                                                                                 \
     if (dkdv_kind >= 64 && S % 256 == 0) {                                                             \
@@ -1267,6 +1386,14 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
           <<<B * KVH * (S / 128), 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(              \
               (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr, \
               (bf16_t*)dqkv);                                                                          \
+    } else if (dkdv_pf == 1 && dkdv_kind == 8) {                                                       \
+      fa_bwd_dkdv8_kernel<C, false, false, false, false, false, 1>                                     \
+          <<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(                             \
+              (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
+    } else if (dkdv_pf >= 2 && dkdv_kind == 8) {                                                       \
+      fa_bwd_dkdv8_kernel<C, false, false, false, false, false, 2>                                     \
+          <<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(                             \
+              (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
     } else if (dkdv8 || dkdv_kind >= 64) {                                                             \
       fa_bwd_dkdv8_kernel<C><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(          \
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr);  \
@@ -1305,6 +1432,15 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     DSA_CHECK(hipGetLastError());
     if (dq_waves == 8 && half_prio)
       fa_bwd_dq_kernel<true, 8, true><<<B * H * (S / 256), 512, lds_q, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    else if (dq_waves == 8 && dq_pf == 1)
+      fa_bwd_dq_kernel<true, 8, false, 1><<<B * H * (S / 256), 512, lds_q, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    else if (dq_waves == 8 && dq_pf == 2)
+      fa_bwd_dq_kernel<true, 8, false, 2><<<B * H * (S / 256), 512, lds_q, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+    else if (dq_waves == 8 && dq_pf >= 3)
+      fa_bwd_dq_kernel<true, 8, false, 4><<<B * H * (S / 256), 512, lds_q, st>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
     else if (dq_waves == 8)
       fa_bwd_dq_kernel<true, 8><<<B * H * (S / 256), 512, lds_q, st>>>(

@@ -81,11 +81,6 @@ __device__ __forceinline__ void dma_tile64_n(const bf16_t* g, long stride, char*
   }
 }
 
-// 64 contiguous floats -> LDS (one wave-instruction, 4 B/lane)
-__device__ __forceinline__ void dma_f32x64(const float* g, char* lds, int lane) {
-  __builtin_amdgcn_global_load_lds(GLB1(void, g + lane), LDS3(void, lds), 4, 0, 0);
-}
-
 // Buffer descriptor over `bytes` of a wave-uniform base (readfirstlane'd so the compiler can prove
 // uniformity and keeps it in SGPRs), for LDS-DMA whose per-iteration offset is an SGPR (soffset)
 // and whose per-lane part is one 32-bit voffset: no 64-bit VGPR address pair stays live across a
@@ -95,6 +90,36 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
   void* p = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// The same tile through a buffer descriptor: the per-lane source offsets (32-bit, swizzle included)
+// are computed once per kernel by dma_tile64_offsets, the tile's row offset is an SGPR byte offset.
+// Besides dropping the per-tile 64-bit address arithmetic, this keeps LDS-read waits counted: the
+// compiler's waitcnt pass counts a FLAT-encoded global_load_lds in lgkmcnt as well as vmcnt, so with
+// one in flight every ds_read consumer gets lgkmcnt(0); a buffer load counts in vmcnt only.
+template <int NW>
+__device__ __forceinline__ void dma_tile64_offsets(long stride, int wave, int lane, unsigned (&off)[16 / NW]) {
+#pragma unroll
+  for (int i = 0; i < 16 / NW; ++i) {
+    const int row = (wave * (16 / NW) + i) * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    off[i] = (unsigned)(((long)row * stride + ch * 8) * 2);
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void dma_tile64_buf(__amdgpu_buffer_rsrc_t r, const unsigned (&off)[16 / NW], int soff,
+                                               char* lds, int wave) {
+  const int so = __builtin_amdgcn_readfirstlane(soff);
+#pragma unroll
+  for (int i = 0; i < 16 / NW; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LDS3(void, lds + (wave * (16 / NW) + i) * 1024), 16, off[i], so, 0,
+                                             0);
+}
+
+// 64 contiguous floats -> LDS (one wave-instruction, 4 B/lane)
+__device__ __forceinline__ void dma_f32x64(const float* g, char* lds, int lane) {
+  __builtin_amdgcn_global_load_lds(GLB1(void, g + lane), LDS3(void, lds), 4, 0, 0);
 }
 
 // 64 contiguous floats at element `elem0` of the buffer -> LDS (one wave-instruction, 4 B/lane)

@@ -287,8 +287,10 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
     the deferred one (DSTACK_AMD_FA_RESCALE_THR=0), and the staggered forward
     (DSTACK_AMD_FA_FWD_STAG=1), and the recompute-free dQ pass over the dS spilled by the dK/dV
     pass (DSTACK_AMD_FA_DQ=ds; also at S=1152, its 4-wave dQ form, causal and not), and dK/dV summed
-    over the GQA group in one workgroup (DSTACK_AMD_FA_DKDV_GQA=1, causal and not).  The switches
-    are read once per process, so each variant runs in a child process."""
+    over the GQA group in one workgroup (DSTACK_AMD_FA_DKDV_GQA=1, causal and not), and the S/dP read
+    pipelines: dK/dV without it or one step ahead (DSTACK_AMD_FA_DKDV_PF=0|1; the default is 2) and the
+    dQ pass's (DSTACK_AMD_FA_DQ_PF=1|2, causal).  The switches are read once per process, so each
+    variant runs in a child process."""
     import os
     import subprocess
     import sys
@@ -306,7 +308,8 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
         "torch.save({'o': o.detach().cpu(), 'g': x.grad.cpu()}, sys.argv[1])\n"
     )
     shape = {"dq_ds_1152": (1152, True), "dq_ds_1152_nc": (1152, False), "default_1152": (1152, True),
-             "default_1152_nc": (1152, False), "dkdv_gqa_nc": (1024, False), "default_nc": (1024, False)}
+             "default_1152_nc": (1152, False), "dkdv_gqa_nc": (1024, False), "default_nc": (1024, False),
+             "dkdv_pf0_nc": (1024, False)}
     variants = {"default": {}, "dkdv4": {"DSTACK_AMD_FA_DKDV": "4w"},
                 "fwd4_dq4": {"DSTACK_AMD_FA_FWD_WAVES": "4", "DSTACK_AMD_FA_DQ_WAVES": "4"},
                 "fwd_pf0": {"DSTACK_AMD_FA_FWD_PF": "0"}, "exact_max": {"DSTACK_AMD_FA_RESCALE_THR": "0"},
@@ -314,13 +317,15 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
                 "dq_ds": {"DSTACK_AMD_FA_DQ": "ds"}, "dq_ds_1152": {"DSTACK_AMD_FA_DQ": "ds"},
                 "dq_ds_1152_nc": {"DSTACK_AMD_FA_DQ": "ds"}, "default_1152": {}, "default_1152_nc": {},
                 "dkdv_gqa": {"DSTACK_AMD_FA_DKDV_GQA": "1"}, "dkdv_gqa_nc": {"DSTACK_AMD_FA_DKDV_GQA": "1"},
-                "default_nc": {}}
+                "default_nc": {}, "dkdv_pf0": {"DSTACK_AMD_FA_DKDV_PF": "0"},
+                "dkdv_pf1": {"DSTACK_AMD_FA_DKDV_PF": "1"}, "dkdv_pf0_nc": {"DSTACK_AMD_FA_DKDV_PF": "0"},
+                "dq_pf1": {"DSTACK_AMD_FA_DQ_PF": "1"}, "dq_pf2": {"DSTACK_AMD_FA_DQ_PF": "2"}}
     out = {}
     for name, extra in variants.items():
         env = dict(os.environ)
         for k in ("DSTACK_AMD_FA_DKDV", "DSTACK_AMD_FA_FWD_WAVES", "DSTACK_AMD_FA_DQ_WAVES", "DSTACK_AMD_FA_FWD_PF",
                   "DSTACK_AMD_FA_RESCALE_THR", "DSTACK_AMD_FA_FWD_STAG", "DSTACK_AMD_FA_HALF_PRIO", "DSTACK_AMD_FA_DQ",
-                  "DSTACK_AMD_FA_DKDV_GQA"):
+                  "DSTACK_AMD_FA_DKDV_GQA", "DSTACK_AMD_FA_DKDV_PF", "DSTACK_AMD_FA_DQ_PF"):
             env.pop(k, None)
         env.update(extra)
         sn, causal = shape.get(name, (S, True))
@@ -329,12 +334,14 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
                        timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         out[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
     ref_o, ref_g = out["default"]["o"].float(), out["default"]["g"].float()
-    for name in ("dkdv4", "fwd4_dq4", "fwd_pf0", "exact_max", "fwd_stag", "half_prio", "dq_ds", "dkdv_gqa"):
+    for name in ("dkdv4", "fwd4_dq4", "fwd_pf0", "exact_max", "fwd_stag", "half_prio", "dq_ds", "dkdv_gqa",
+                 "dkdv_pf0", "dkdv_pf1", "dq_pf1", "dq_pf2"):
         o, g = out[name]["o"].float(), out[name]["g"].float()
         assert ((o - ref_o).norm() / ref_o.norm()).item() < 2e-3, name
         assert ((g - ref_g).norm() / ref_g.norm()).item() < 2e-3, name
-    g, rg = out["dkdv_gqa_nc"]["g"].float(), out["default_nc"]["g"].float()
-    assert ((g - rg).norm() / rg.norm()).item() < 2e-3, "dkdv_gqa_nc"
+    for name in ("dkdv_gqa_nc", "dkdv_pf0_nc"):
+        g, rg = out[name]["g"].float(), out["default_nc"]["g"].float()
+        assert ((g - rg).norm() / rg.norm()).item() < 2e-3, name
     for name in ("dq_ds_1152", "dq_ds_1152_nc"):
         ref = out[name.replace("dq_ds", "default")]
         g, rg = out[name]["g"].float(), ref["g"].float()
