@@ -1475,7 +1475,7 @@ extern "C" hipError_t dsa_fa_dkdv_trace(const void* qkv, const void* dout, const
                                         int KVH, float sl2, hipStream_t st) {
   if (S % 128) return hipErrorInvalidValue;
   const size_t lds8 = 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512);
-  fa_bwd_dkdv8_kernel<true, false, false, false, false, true><<<B * H * (S / 128), 512, lds8, st>>>(
+  fa_bwd_dkdv8_kernel<true, false, false, false, false, true, 2><<<B * H * (S / 128), 512, lds8, st>>>(
       (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, (bf16_t*)trace);
   return hipGetLastError();
 }
