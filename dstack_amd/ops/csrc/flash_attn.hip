@@ -1378,6 +1378,10 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     } else if (dkdv_kind == 9) {                                                                      \
       fa_bwd_dkdv8_kernel<C, true><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(     \
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr);  \
+    } else if ((dkdv8 || dkdv_kind >= 64) && half_prio && dkdv_pf >= 2) {                              \
+      fa_bwd_dkdv8_kernel<C, false, true, false, false, false, 2>                                      \
+          <<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(                             \
+              (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
     } else if ((dkdv8 || dkdv_kind >= 64) && half_prio) {                                              \
       fa_bwd_dkdv8_kernel<C, false, true><<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>( \
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr);  \
