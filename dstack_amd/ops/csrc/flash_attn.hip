@@ -65,7 +65,7 @@ constexpr int HD = 128;          // head dim
 // waves 4-7 at kernel start, no per-phase flips.  Measured (4 interleaved runs, S=8192,
 // profiles/fa_hprio_ab_r4y.txt): forward 0.656-0.670 vs 0.657-0.668 ms, backward 2.018-2.036 vs
 // 2.009-2.053 ms -- within noise, kept opt-in.
-// BUF (DSTACK_AMD_FA_FWD_BUF=1): K/V tiles through buffer descriptors (dma_tile64_buf), which keeps
+// BUF (default; DSTACK_AMD_FA_FWD_BUF=0 turns it off): K/V tiles through buffer descriptors (dma_tile64_buf), which keeps
 // the S phase's LDS-read waits counted instead of lgkmcnt(0).
 template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0, bool STAG = false, bool BUF = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
@@ -971,7 +971,7 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __re
 // ================================================================================================
 // Backward dQ pass: workgroup = 128 queries of one (b, q-head); loops over 64-key K/V tiles.
 // ================================================================================================
-// PF > 0 (DSTACK_AMD_FA_DQ_PF): K/V tiles through a buffer descriptor (counted LDS waits, see
+// PF > 0 (DSTACK_AMD_FA_DQ_PF, default 1): K/V tiles through a buffer descriptor (counted LDS waits, see
 // dma_tile64_buf) and the 32 S/dP fragment reads of a tile kept PF steps ahead of their MFMAs;
 // the default form reads -> lgkmcnt(0) -> MFMA on every step.
 template <bool CAUSAL, int NW = 4, bool HP = false, int PF = 0>
@@ -1236,9 +1236,11 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     const char* v = getenv("DSTACK_AMD_FA_HALF_PRIO");
     return v && atoi(v) == 1;
   }();
+  // K/V through buffer descriptors (DSTACK_AMD_FA_FWD_BUF=0 selects global_load_lds): forward
+  // 0.647-0.663 vs 0.660-0.679 ms, S=8192, 3 interleaved runs (profiles/fa_dq_fwd_ab_r8w.txt)
   static const bool fwd_buf_env = [] {
     const char* v = getenv("DSTACK_AMD_FA_FWD_BUF");
-    return v && atoi(v) == 1;
+    return !(v && atoi(v) == 0);
   }();
   const bool fwd_buf = fwd_buf_env && (long)S * (H + 2 * KVH) * HD * 2 < (1L << 31);
   if (waves == 8 && S % 256 == 0) {
@@ -1360,9 +1362,11 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   }();
   // the PF form addresses a Q / dO tile through a buffer descriptor with 32-bit offsets
   const int dkdv_pf = ((long)S * (H + 2 * KVH) * HD * 2 < (1L << 31)) ? dkdv_pf_env : 0;
+  // dQ pass: DSTACK_AMD_FA_DQ_PF=0|1|2, default 1 (whole backward 1.924-1.946 vs 1.945-1.964 ms;
+  // 2 spills and measured 1.976-2.000, profiles/fa_dq_fwd_ab_r8w.txt)
   static const int dq_pf_env = [] {
     const char* v = getenv("DSTACK_AMD_FA_DQ_PF");
-    return v ? atoi(v) : 0;
+    return v ? atoi(v) : 1;
   }();
   const int dq_pf = ((long)S * (H + 2 * KVH) * HD * 2 < (1L << 31)) ? dq_pf_env : 0;
 #define DSA_DKDV(C, N)                                                                                 \
@@ -1440,11 +1444,8 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     else if (dq_waves == 8 && dq_pf == 1)
       fa_bwd_dq_kernel<true, 8, false, 1><<<B * H * (S / 256), 512, lds_q, st>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
-    else if (dq_waves == 8 && dq_pf == 2)
+    else if (dq_waves == 8 && dq_pf >= 2)
       fa_bwd_dq_kernel<true, 8, false, 2><<<B * H * (S / 256), 512, lds_q, st>>>(
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
-    else if (dq_waves == 8 && dq_pf >= 3)
-      fa_bwd_dq_kernel<true, 8, false, 4><<<B * H * (S / 256), 512, lds_q, st>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
     else if (dq_waves == 8)
       fa_bwd_dq_kernel<true, 8><<<B * H * (S / 256), 512, lds_q, st>>>(

@@ -108,7 +108,7 @@ __device__ __forceinline__ void dma_tile64_offsets(long stride, int wave, int la
 }
 
 template <int NW>
-__device__ __forceinline__ void dma_tile64_buf(__amdgpu_buffer_rsrc_t r, const unsigned (&off)[16 / NW], int soff,
+__device__ __forceinline__ void dma_tile64_buf(__amdgpu_buffer_rsrc_t r, const unsigned* off, int soff,
                                                char* lds, int wave) {
   const int so = __builtin_amdgcn_readfirstlane(soff);
 #pragma unroll
