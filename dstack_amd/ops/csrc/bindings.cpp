@@ -43,7 +43,9 @@ bool dsa_rmsnorm_fwd_fp8_supported(int, int);
 hipError_t dsa_rmsnorm_fwd_fp8(const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
                                hipStream_t);
 hipError_t dsa_quant_fp8_rows(const void*, long, void*, long, float*, int, int, hipStream_t);
-hipError_t dsa_swiglu_quant_fp8_rows(const void*, long, void*, long, float*, int, int, hipStream_t);
+hipError_t dsa_swiglu_quant_fp8_rows(const void*, long, void*, long, float*, int, int, const float*, const float*,
+                                     hipStream_t);
+hipError_t dsa_scale_rows_cols(void*, long, int, int, const float*, const float*, hipStream_t);
 bool dsa_gemv_fp8_supported(int, int);
 hipError_t dsa_gemv_fp8(const void*, long, const void*, const float*, void*, long, int, int, int, hipStream_t);
 hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
@@ -365,19 +367,51 @@ torch::Tensor gemv(torch::Tensor x, torch::Tensor w) {
 
 // FP8 (e4m3) rows: q [M, K] uint8 (view as float8_e4m3fn) and s [M] fp32, x[m] ~= q[m] * s[m]
 // gu [M, 2F] bf16 -> (q [M, F] e4m3 bytes, s [M] fp32) of bf16(silu(gate) * up), per-row scales
-std::vector<torch::Tensor> swiglu_quant_fp8_rows(torch::Tensor gu) {
+// rs / cs (optional, together): gu is the raw product of a tensor-wise-scaled fp8 GEMM; the per-token
+// scale rs [M] and per-output-channel scale cs [2F] are applied before the SwiGLU
+std::vector<torch::Tensor> swiglu_quant_fp8_rows(torch::Tensor gu, c10::optional<torch::Tensor> rs,
+                                                 c10::optional<torch::Tensor> cs) {
   TORCH_CHECK(gu.is_cuda() && gu.scalar_type() == torch::kBFloat16 && gu.dim() == 2 && gu.stride(1) == 1,
               "swiglu_quant_fp8_rows: gu must be bf16 [M, 2F] with contiguous rows");
   TORCH_CHECK(gu.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(gu.data_ptr()) % 16 == 0 && gu.size(1) % 16 == 0,
               "swiglu_quant_fp8_rows: alignment (2F % 16 == 0)");
   const int64_t M = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(rs.has_value() == cs.has_value(), "swiglu_quant_fp8_rows: rs and cs go together");
+  const float* rp = nullptr;
+  const float* cp = nullptr;
+  if (rs.has_value()) {
+    TORCH_CHECK(rs->scalar_type() == torch::kFloat32 && rs->is_contiguous() && rs->numel() == M,
+                "swiglu_quant_fp8_rows: rs must be fp32 [M]");
+    TORCH_CHECK(cs->scalar_type() == torch::kFloat32 && cs->is_contiguous() && cs->numel() == 2 * F &&
+                    reinterpret_cast<uintptr_t>(cs->data_ptr()) % 16 == 0,
+                "swiglu_quant_fp8_rows: cs must be fp32 [2F], 16-byte aligned");
+    rp = rs->data_ptr<float>();
+    cp = cs->data_ptr<float>();
+  }
   auto q = torch::empty({M, F}, gu.options().dtype(torch::kUInt8));
   auto sc = torch::empty({M}, gu.options().dtype(torch::kFloat32));
   if (M > 0)
     check(dsa_swiglu_quant_fp8_rows(gu.data_ptr(), gu.stride(0), q.data_ptr(), F, sc.data_ptr<float>(), (int)M,
-                                    (int)F, stream()),
+                                    (int)F, rp, cp, stream()),
           "swiglu_quant_fp8_rows");
   return {q, sc};
+}
+
+// y [M, N] bf16 (+ row stride) *= rs[:, None] * cs[None, :] in place
+torch::Tensor scale_rows_cols_(torch::Tensor y, torch::Tensor rs, torch::Tensor cs) {
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == torch::kBFloat16 && y.dim() == 2 && y.stride(1) == 1 &&
+                  y.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0 && y.size(1) % 8 == 0,
+              "scale_rows_cols_: y must be bf16 [M, N], contiguous 16-byte-aligned rows, N % 8 == 0");
+  TORCH_CHECK(rs.scalar_type() == torch::kFloat32 && rs.is_contiguous() && rs.numel() == y.size(0),
+              "scale_rows_cols_: rs must be fp32 [M]");
+  TORCH_CHECK(cs.scalar_type() == torch::kFloat32 && cs.is_contiguous() && cs.numel() == y.size(1) &&
+                  reinterpret_cast<uintptr_t>(cs.data_ptr()) % 16 == 0,
+              "scale_rows_cols_: cs must be fp32 [N], 16-byte aligned");
+  if (y.size(0) > 0)
+    check(dsa_scale_rows_cols(y.data_ptr(), y.stride(0), (int)y.size(0), (int)y.size(1), rs.data_ptr<float>(),
+                              cs.data_ptr<float>(), stream()),
+          "scale_rows_cols_");
+  return y;
 }
 
 std::vector<torch::Tensor> quant_fp8_rows(torch::Tensor x) {
@@ -699,7 +733,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("ws"), pybind11::arg("bm") = 64, pybind11::arg("split") = 1, pybind11::arg("part") = pybind11::none(),
         pybind11::arg("cnt") = pybind11::none());
   m.def("fp8_rows_gemm_supported", &fp8_rows_gemm_supported);
-  m.def("swiglu_quant_fp8_rows", &swiglu_quant_fp8_rows);
+  m.def("swiglu_quant_fp8_rows", &swiglu_quant_fp8_rows, py::arg("gu"), py::arg("rs") = py::none(),
+        py::arg("cs") = py::none());
+  m.def("scale_rows_cols_", &scale_rows_cols_);
   m.def("gemm_nt_trace", &gemm_nt_trace);
   m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);
   m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd, pybind11::arg("dy"), pybind11::arg("wdT"), pybind11::arg("gu"),

@@ -80,16 +80,35 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restric
 // and writes e4m3.
 __device__ __forceinline__ float silu_q(float g) { return g / (1.f + __expf(-g)); }
 
+// SCALED: gu is the raw e4m3 x e4m3 product of a tensor-wise-scaled fp8 GEMM (hipBLASLt runs the
+// Llama-3-70B prefill shapes 12-25 % faster with scalar scales than with row-wise ones,
+// profiles/fp8_scaling_modes_r8z.txt); the per-token scale rs[row] and the per-output-channel scale
+// cs[c] of the row-wise form are applied here, on the fp32 values, before the SwiGLU.
+template <bool SCALED>
 __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __restrict__ gu, long ldg,
                                                                 unsigned char* __restrict__ q, long ldq,
-                                                                float* __restrict__ s, int F) {
+                                                                float* __restrict__ s, int F,
+                                                                const float* __restrict__ rs,
+                                                                const float* __restrict__ cs) {
   __shared__ float red[4];
   const int row = blockIdx.x, tid = threadIdx.x;
   const bf16_t* gr = gu + (long)row * ldg;
+  const float r = SCALED ? rs[row] : 1.f;
   auto prod8 = [&](int k, float* a) {
     float g[8], u[8];
     unpack8(*reinterpret_cast<const us8*>(gr + k), g);
     unpack8(*reinterpret_cast<const us8*>(gr + F + k), u);
+    if constexpr (SCALED) {
+      const f4 cg0 = *reinterpret_cast<const f4*>(cs + k), cg1 = *reinterpret_cast<const f4*>(cs + k + 4);
+      const f4 cu0 = *reinterpret_cast<const f4*>(cs + F + k), cu1 = *reinterpret_cast<const f4*>(cs + F + k + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        g[i] = bf2f(f2bf(g[i] * r * cg0[i]));
+        g[4 + i] = bf2f(f2bf(g[4 + i] * r * cg1[i]));
+        u[i] = bf2f(f2bf(u[i] * r * cu0[i]));
+        u[4 + i] = bf2f(f2bf(u[4 + i] * r * cu1[i]));
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = bf2f(f2bf(silu_q(g[i]) * u[i]));
   };
@@ -254,9 +273,42 @@ extern "C" hipError_t dsa_quant_fp8_rows(const void* x, long ldx, void* q, long 
 }
 
 extern "C" hipError_t dsa_swiglu_quant_fp8_rows(const void* gu, long ldg, void* q, long ldq, float* s, int M, int F,
-                                                hipStream_t st) {
-  if (F <= 0 || F % 8 || M <= 0) return hipErrorInvalidValue;
-  swiglu_quant_rows_kernel<<<M, 256, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F);
+                                                const float* rs, const float* cs, hipStream_t st) {
+  if (F <= 0 || F % 8 || M <= 0 || ((rs == nullptr) != (cs == nullptr))) return hipErrorInvalidValue;
+  if (rs)
+    swiglu_quant_rows_kernel<true><<<M, 256, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F, rs, cs);
+  else
+    swiglu_quant_rows_kernel<false><<<M, 256, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F, nullptr,
+                                                       nullptr);
+  return hipGetLastError();
+}
+
+// y[r][c] = bf16(y[r][c] * rs[r] * cs[c]) in place: the row-wise scales of a tensor-wise-scaled fp8
+// GEMM's raw product (see swiglu_quant_rows_kernel).  One workgroup per row, 8 columns per lane.
+__global__ __launch_bounds__(256) void scale_rows_cols_kernel(bf16_t* __restrict__ y, long ldy, int N,
+                                                              const float* __restrict__ rs,
+                                                              const float* __restrict__ cs) {
+  const int row = blockIdx.x;
+  bf16_t* yr = y + (long)row * ldy;
+  const float r = rs[row];
+  for (int c = threadIdx.x * 8; c < N; c += 256 * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const us8*>(yr + c), v);
+    const f4 c0 = *reinterpret_cast<const f4*>(cs + c), c1 = *reinterpret_cast<const f4*>(cs + c + 4);
+    us8 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[i] = f2bf(v[i] * r * c0[i]);
+      o[4 + i] = f2bf(v[4 + i] * r * c1[i]);
+    }
+    *reinterpret_cast<us8*>(yr + c) = o;
+  }
+}
+
+extern "C" hipError_t dsa_scale_rows_cols(void* y, long ldy, int M, int N, const float* rs, const float* cs,
+                                          hipStream_t st) {
+  if (M <= 0 || N <= 0 || N % 8) return hipErrorInvalidValue;
+  scale_rows_cols_kernel<<<M, 256, 0, st>>>((bf16_t*)y, ldy, N, rs, cs);
   return hipGetLastError();
 }
 

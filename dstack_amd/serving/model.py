@@ -202,6 +202,14 @@ class ServingLlama:
         self.fp8_gemm = os.environ.get("DSTACK_AMD_FP8_GEMM", "hip").lower()
         # fp8: norms feeding an fp8 GEMM write e4m3 directly (DSTACK_AMD_FP8_FUSE_NORM=0: separate quant)
         self.fuse_norm_quant = os.environ.get("DSTACK_AMD_FP8_FUSE_NORM", "1") != "0"
+        # fp8 GEMMs of at least this many rows (prefill) run hipBLASLt with scalar scales on the raw
+        # e4m3 operands and apply the row-wise scales afterwards: in the gate/up output's SwiGLU-quant
+        # kernel, or in one in-place pass for o / down (profiles/fp8_scaling_modes_r8z.txt: 12-25 %
+        # faster GEMMs).  DSTACK_AMD_FP8_DEFER_SCALE=0 keeps hipBLASLt's row-wise scaling everywhere.
+        self.fp8_defer_rows = int(os.environ.get("DSTACK_AMD_FP8_DEFER_ROWS", "1024"))
+        if os.environ.get("DSTACK_AMD_FP8_DEFER_SCALE", "1") == "0":
+            self.fp8_defer_rows = 1 << 62
+        self._one = torch.ones((), device=self.device, dtype=torch.float32)
         self.cos, self.sin = rope_tables(self.max_model_len + sops.PAGE, self.D, cfg.rope_theta, spec.rope_scaling,
                                          self.device)
         self.layers: list[dict] = []
@@ -471,10 +479,14 @@ class ServingLlama:
                 return C.gemv(x, w)
         return x @ w.t()
 
-    def _mm_fp8(self, x, w: Fp8Weight):
+    def _mm_fp8(self, x, w: Fp8Weight, defer: str | None = None):
         """``x @ (q * s)^T``: up to 4 rows on the fp8 HIP GEMV (half the weight bytes of the bf16
         one); more rows are quantized per token (HIP) and multiplied by hipBLASLt's fp8 GEMM with
-        row-wise scales (``torch._scaled_mm``)."""
+        row-wise scales (``torch._scaled_mm``).
+
+        ``defer`` (prefill-sized batches, ``fp8_defer_rows``): ``"pass"`` runs the GEMM with scalar
+        scales and applies the row-wise ones in one in-place pass; ``"raw"`` returns
+        ``(raw product, row scales, column scales)`` for a consumer that applies them itself."""
         if isinstance(x, Fp8Act):  # quantized by the fused norm
             xq, xs = x.q, x.s
             M = xq.shape[0]
@@ -491,6 +503,13 @@ class ServingLlama:
             y = self._fp8_rows(xq, xs, w)
             if y is not None:
                 return y
+        if defer is not None and self.hip and M >= self.fp8_defer_rows and M % 16 == 0:
+            raw = torch._scaled_mm(xq.view(torch.float8_e4m3fn), w.q.view(torch.float8_e4m3fn).t(),
+                                   scale_a=self._one, scale_b=self._one, out_dtype=self.dtype)
+            xs1 = xs.reshape(-1).contiguous()
+            if defer == "raw":
+                return raw, xs1, w.s
+            return _ext.require().scale_rows_cols_(raw, xs1, w.s)
         pad = -M % 16  # hipBLASLt's fp8 GEMM wants every dimension a multiple of 16
         if pad:  # zero rows (e4m3 0x00 = 0.0) with unit scales
             xq = torch.nn.functional.pad(xq, (0, 0, 0, pad))
@@ -530,15 +549,28 @@ class ServingLlama:
 
     def _mlp_and_attn_out(self, L, x, o):
         """(x + o @ wo^T) -> norm -> SwiGLU MLP; returns (new residual, mlp output)."""
-        x, h = self._add_rms(x, self._reduce(self._mm(o, L["wo"])), L["ffn_norm"], next_w=L["wgu"])
-        gu = self._mm(h, L["wgu"])
-        wd = L["wdown"]
-        if self.hip and isinstance(wd, Fp8Weight) and not (self.gemv and gu.shape[0] <= 4):
+        wo = L["wo"]
+        ao = self._mm_fp8(o, wo, defer="pass") if isinstance(wo, Fp8Weight) else self._mm(o, wo)
+        x, h = self._add_rms(x, self._reduce(ao), L["ffn_norm"], next_w=L["wgu"])
+        wgu, wd = L["wgu"], L["wdown"]
+        if self.hip and isinstance(wd, Fp8Weight) and isinstance(wgu, Fp8Weight) and not (
+                self.gemv and self._rows(h) <= 4):
             # fp8 down projection past the GEMV's rows: SwiGLU and the per-token e4m3 quantization
-            # in one kernel (no bf16 product written and re-read)
-            q, sc = _ext.require().swiglu_quant_fp8_rows(gu if gu.stride(-1) == 1 else gu.contiguous())
-            return x, self._reduce(self._mm_fp8(Fp8Act(q, sc), wd))
+            # in one kernel (no bf16 product written and re-read); for prefill-sized batches the
+            # gate/up GEMM's row-wise scales are applied inside that kernel too
+            r = self._mm_fp8(h, wgu, defer="raw")
+            C = _ext.require()
+            if isinstance(r, tuple):
+                q, sc = C.swiglu_quant_fp8_rows(r[0], r[1], r[2])
+            else:
+                q, sc = C.swiglu_quant_fp8_rows(r if r.stride(-1) == 1 else r.contiguous())
+            return x, self._reduce(self._mm_fp8(Fp8Act(q, sc), wd, defer="pass"))
+        gu = self._mm(h, wgu)
         return x, self._reduce(self._mm(self._swiglu(gu), wd))
+
+    @staticmethod
+    def _rows(h) -> int:
+        return h.q.shape[0] if isinstance(h, Fp8Act) else h.shape[0]
 
     # ------------------------------------------------------------------------------------------
     # forward passes

@@ -639,6 +639,46 @@ def test_gpu_fp8_engine_tracks_bf16(gpu):
     assert all(len(o.output_ids) == 16 for o in outs)
 
 
+@pytest.mark.gpu
+def test_gpu_fp8_deferred_row_scales_match_rowwise(gpu):
+    """Prefill-sized fp8 GEMMs run with scalar scales on the raw e4m3 operands and apply the
+    row-wise scales afterwards (SwiGLU-quant kernel for gate/up, an in-place pass for o / down).
+    Kernels: bit-identical to scaling in fp32 then rounding.  Model: the extra bf16 rounding of the
+    raw product keeps the prefill logits as close to the bf16 model's as the row-wise path's."""
+    from dstack_amd.ops import _ext
+
+    C = _ext.require()
+    torch.manual_seed(0)
+    for M, F in ((128, 1024), (256, 3584)):
+        raw = torch.randn(M, 2 * F, device=gpu, dtype=torch.bfloat16) * 300
+        rs = torch.rand(M, device=gpu) * 1e-2
+        cs = torch.rand(2 * F, device=gpu) * 1e-2
+        scaled = (raw.float() * rs[:, None] * cs[None, :]).bfloat16()
+        q, s = C.swiglu_quant_fp8_rows(raw, rs, cs)
+        q2, s2 = C.swiglu_quant_fp8_rows(scaled)
+        assert torch.equal(s, s2)
+        assert torch.equal(q.view(torch.uint8), q2.view(torch.uint8))
+        y = raw.clone()
+        C.scale_rows_cols_(y, rs, cs)
+        assert torch.equal(y, scaled)
+    kw = dict(device="cuda", max_model_len=512, max_batch=8, num_pages=64)
+    base = LLMEngine.from_model("llama-tiny", **kw)
+    q8 = LLMEngine.from_model("llama-tiny", quantization="fp8", **kw)
+    n = 384  # past the in-tree decode fp8 GEMM's 256 rows: the hipBLASLt path
+    prompt = torch.arange(1, n + 1, device=gpu)
+    pos = torch.arange(n, dtype=torch.int32, device=gpu)
+    slots = torch.arange(n, dtype=torch.int32, device=gpu)
+    ref_logits = base.model.prefill(prompt, pos, slots, [0], [n]).float()
+    q8.model.fp8_defer_rows = 1 << 62
+    a = q8.model.prefill(prompt, pos, slots, [0], [n]).float()
+    q8.model.fp8_defer_rows = 128
+    b = q8.model.prefill(prompt, pos, slots, [0], [n]).float()
+    cs = torch.nn.functional.cosine_similarity
+    cos_rowwise, cos_deferred = cs(a, ref_logits, dim=-1).item(), cs(b, ref_logits, dim=-1).item()
+    assert cos_deferred > 0.99 and cos_deferred > cos_rowwise - 0.003, (cos_rowwise, cos_deferred)
+    assert cs(a, b, dim=-1).item() > 0.995
+
+
 # ------------------------------------------------------------------------------------------------
 # fp8 (e4m3) KV cache
 # ------------------------------------------------------------------------------------------------
