@@ -41,7 +41,7 @@ hipError_t dsa_gemv(const void*, long, const void*, void*, long, int, int, int, 
 bool dsa_quant_fp8_supported(int);
 bool dsa_rmsnorm_fwd_fp8_supported(int, int);
 hipError_t dsa_rmsnorm_fwd_fp8(const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
-                               hipStream_t);
+                               const float*, const float*, hipStream_t);
 hipError_t dsa_quant_fp8_rows(const void*, long, void*, long, float*, int, int, hipStream_t);
 hipError_t dsa_swiglu_quant_fp8_rows(const void*, long, void*, long, float*, int, int, const float*, const float*,
                                      hipStream_t);
@@ -112,12 +112,27 @@ bool rms_norm_fp8_supported(int64_t rows, int64_t D) { return dsa_rmsnorm_fwd_fp
 
 // (x + delta) -> RMSNorm -> e4m3 [rows, D] (uint8) + per-row scales; returns {h (x + delta, or an
 // empty tensor without delta), q, s}.  Serving decode (rows <= 1024).
+// dr / dc (optional, with delta): delta is a raw fp8 GEMM product whose row-wise scales (dr [rows]
+// per token, dc [D] per output channel) are applied before the residual add
 std::vector<torch::Tensor> rms_norm_fp8(torch::Tensor x, c10::optional<torch::Tensor> delta, torch::Tensor w,
-                                        double eps) {
+                                        double eps, c10::optional<torch::Tensor> dr, c10::optional<torch::Tensor> dc) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   const int rows = x.size(0), D = x.size(1);
-  TORCH_CHECK(dsa_rmsnorm_fwd_fp8_supported(rows, D), "rms_norm_fp8: rows <= 1024, D % 8 == 0, D <= 8192");
+  TORCH_CHECK(dsa_rmsnorm_fwd_fp8_supported(rows, D), "rms_norm_fp8: D % 8 == 0, D <= 8192");
+  TORCH_CHECK(dr.has_value() == dc.has_value() && (!dr.has_value() || delta.has_value()),
+              "rms_norm_fp8: dr and dc go together, with delta");
+  const float* drp = nullptr;
+  const float* dcp = nullptr;
+  if (dr.has_value()) {
+    TORCH_CHECK(dr->scalar_type() == torch::kFloat32 && dr->is_contiguous() && dr->numel() == rows,
+                "rms_norm_fp8: dr must be fp32 [rows]");
+    TORCH_CHECK(dc->scalar_type() == torch::kFloat32 && dc->is_contiguous() && dc->numel() == D &&
+                    reinterpret_cast<uintptr_t>(dc->data_ptr()) % 16 == 0,
+                "rms_norm_fp8: dc must be fp32 [D], 16-byte aligned");
+    drp = dr->data_ptr<float>();
+    dcp = dc->data_ptr<float>();
+  }
   torch::Tensor h;
   if (delta.has_value()) {
     check_bf16(*delta, "delta");
@@ -129,7 +144,7 @@ std::vector<torch::Tensor> rms_norm_fp8(torch::Tensor x, c10::optional<torch::Te
   auto rstd = torch::empty({rows}, x.options().dtype(torch::kFloat32));
   check(dsa_rmsnorm_fwd_fp8(x.data_ptr(), delta.has_value() ? delta->data_ptr() : nullptr, w.data_ptr(),
                             delta.has_value() ? h.data_ptr() : nullptr, q.data_ptr(), qs.data_ptr<float>(),
-                            rstd.data_ptr<float>(), rows, D, (float)eps, stream()),
+                            rstd.data_ptr<float>(), rows, D, (float)eps, drp, dcp, stream()),
         "rms_norm_fp8");
   return {delta.has_value() ? h : torch::Tensor(), q, qs};
 }
@@ -717,7 +732,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("fa_dkdv_trace", &fa_dkdv_trace);
   m.def("quant_fp8_rows", &quant_fp8_rows);
-  m.def("rms_norm_fp8", &rms_norm_fp8);
+  m.def("rms_norm_fp8", &rms_norm_fp8, py::arg("x"), py::arg("delta"), py::arg("w"), py::arg("eps"),
+        py::arg("dr") = py::none(), py::arg("dc") = py::none());
   m.def("rms_norm_fp8_supported", &rms_norm_fp8_supported);
   m.def("gemv_fp8", &gemv_fp8);
   m.def("gemv_fp8_supported", &gemv_fp8_supported);

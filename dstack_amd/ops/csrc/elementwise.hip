@@ -66,7 +66,10 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 // 4 wave sums through LDS.
 // Q (fp8 serving): instead of the bf16 y, write y as e4m3 bytes with one per-row scale
 // (max|y| / 448) to q_out / qs_out — the activation quantization of the next fp8 GEMM fused in.
-template <int NCH, bool ADD, bool Q = false>
+// SC (with ADD): delta is the raw product of a tensor-wise-scaled fp8 GEMM whose row-wise scales
+// dr[row] (per token) and dc[col] (per output channel) are applied here -- rounded to bf16 as the
+// GEMM's own output would be -- before the residual add (fp8 serving prefill, model.py RawScaled)
+template <int NCH, bool ADD, bool Q = false, bool SC = false>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_rowblock_kernel(const bf16_t* __restrict__ x,
                                                                    const bf16_t* __restrict__ delta,
                                                                    const bf16_t* __restrict__ w,
@@ -75,7 +78,9 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_rowblock_kernel(const bf16_t*
                                                                    float* __restrict__ rstd_out,
                                                                    int D, float eps,
                                                                    unsigned char* __restrict__ q_out = nullptr,
-                                                                   float* __restrict__ qs_out = nullptr) {
+                                                                   float* __restrict__ qs_out = nullptr,
+                                                                   const float* __restrict__ dr = nullptr,
+                                                                   const float* __restrict__ dc = nullptr) {
   __shared__ float part[4];
   __shared__ float pmax[4];
   const int tid = threadIdx.x, row = blockIdx.x;
@@ -92,6 +97,15 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_rowblock_kernel(const bf16_t*
       if constexpr (ADD) {
         float d[8];
         unpack8(*reinterpret_cast<const us8*>(delta + base + ch * 8), d);
+        if constexpr (SC) {
+          const float rr = dr[row];
+          const f4 c0 = *reinterpret_cast<const f4*>(dc + ch * 8), c1 = *reinterpret_cast<const f4*>(dc + ch * 8 + 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            d[i] = bf2f(f2bf(d[i] * rr * c0[i]));
+            d[4 + i] = bf2f(f2bf(d[4 + i] * rr * c1[i]));
+          }
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[c][i] = bf2f(f2bf(v[c][i] + d[i]));  // h is stored in bf16
         *reinterpret_cast<us8*>(h_out + base + ch * 8) = pack8(v[c]);
@@ -769,13 +783,20 @@ extern "C" hipError_t dsa_rmsnorm_fwd(const void* x, const void* delta, const vo
   return hipGetLastError();
 }
 
-// (add +) RMSNorm whose output goes straight to e4m3 with per-row scales (fp8 serving, rows <= 1024)
-extern "C" bool dsa_rmsnorm_fwd_fp8_supported(int rows, int D) { return rows > 0 && rows <= 1024 && D % 8 == 0 && D <= 8192; }
+// (add +) RMSNorm whose output goes straight to e4m3 with per-row scales (fp8 serving: decode
+// batches and prefill, one workgroup per row); dr / dc: row-wise scales of a raw fp8 GEMM delta
+extern "C" bool dsa_rmsnorm_fwd_fp8_supported(int rows, int D) { return rows > 0 && D % 8 == 0 && D <= 8192; }
 
 extern "C" hipError_t dsa_rmsnorm_fwd_fp8(const void* x, const void* delta, const void* w, void* h_out, void* q,
-                                          float* qs, float* rstd, int rows, int D, float eps, hipStream_t st) {
-  if (!dsa_rmsnorm_fwd_fp8_supported(rows, D)) return hipErrorInvalidValue;
-  if (delta) {
+                                          float* qs, float* rstd, int rows, int D, float eps, const float* dr,
+                                          const float* dc, hipStream_t st) {
+  if (!dsa_rmsnorm_fwd_fp8_supported(rows, D) || ((dr == nullptr) != (dc == nullptr)) || (dr && !delta))
+    return hipErrorInvalidValue;
+  if (dr) {
+    NCH_DISPATCH_BLK(D, rmsnorm_fwd_rowblock_kernel<NCH, true, true, true><<<rows, 256, 0, st>>>(
+        (const bf16_t*)x, (const bf16_t*)delta, (const bf16_t*)w, (bf16_t*)h_out, nullptr, rstd, D, eps,
+        (unsigned char*)q, qs, dr, dc));
+  } else if (delta) {
     NCH_DISPATCH_BLK(D, rmsnorm_fwd_rowblock_kernel<NCH, true, true><<<rows, 256, 0, st>>>(
         (const bf16_t*)x, (const bf16_t*)delta, (const bf16_t*)w, (bf16_t*)h_out, nullptr, rstd, D, eps,
         (unsigned char*)q, qs));

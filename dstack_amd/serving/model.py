@@ -65,6 +65,27 @@ class Fp8Act:
         self.q, self.s = q, s
 
 
+class RawScaled:
+    """The raw product of a tensor-wise-scaled fp8 GEMM (``raw`` bf16 [M, N]) still owing its
+    row-wise scales: per-token ``rs`` [M] and per-output-channel ``cs`` [N].  The consumer applies
+    them (the fused add + RMSNorm -> e4m3 kernel, or ``materialize``)."""
+
+    __slots__ = ("raw", "rs", "cs")
+
+    def __init__(self, raw: torch.Tensor, rs: torch.Tensor, cs: torch.Tensor):
+        self.raw, self.rs, self.cs = raw, rs, cs
+
+    @property
+    def shape(self):
+        return self.raw.shape
+
+    def rows(self, idx: torch.Tensor) -> "RawScaled":
+        return RawScaled(self.raw[idx], self.rs[idx].contiguous(), self.cs)
+
+    def materialize(self) -> torch.Tensor:
+        return _ext.require().scale_rows_cols_(self.raw, self.rs, self.cs)
+
+
 @dataclass
 class RopeScaling:
     """Llama-3.1 "llama3" RoPE frequency scaling (HF ``rope_scaling``)."""
@@ -455,8 +476,13 @@ class ServingLlama:
     def _add_rms(self, x, delta, w, next_w=None):
         if self.hip:
             if next_w is not None and self._fuse_fp8(x, next_w):
-                h, q, s = _ext.require().rms_norm_fp8(x, delta, w, self.cfg.norm_eps)
+                if isinstance(delta, RawScaled):  # the delta's fp8 GEMM scales applied in the norm
+                    h, q, s = _ext.require().rms_norm_fp8(x, delta.raw, w, self.cfg.norm_eps, delta.rs, delta.cs)
+                else:
+                    h, q, s = _ext.require().rms_norm_fp8(x, delta, w, self.cfg.norm_eps)
                 return h, Fp8Act(q, s)
+            if isinstance(delta, RawScaled):
+                delta = delta.materialize()
             h, y, _ = _ext.require().add_rms_norm_fwd(x, delta, w, self.cfg.norm_eps)
             return h, y
         return ref.add_rms_norm(x, delta, w, self.cfg.norm_eps)
@@ -508,7 +534,7 @@ class ServingLlama:
                                    scale_a=self._one, scale_b=self._one, out_dtype=self.dtype)
             xs1 = xs.reshape(-1).contiguous()
             if defer == "raw":
-                return raw, xs1, w.s
+                return RawScaled(raw, xs1, w.s)
             return _ext.require().scale_rows_cols_(raw, xs1, w.s)
         pad = -M % 16  # hipBLASLt's fp8 GEMM wants every dimension a multiple of 16
         if pad:  # zero rows (e4m3 0x00 = 0.0) with unit scales
@@ -550,7 +576,10 @@ class ServingLlama:
     def _mlp_and_attn_out(self, L, x, o):
         """(x + o @ wo^T) -> norm -> SwiGLU MLP; returns (new residual, mlp output)."""
         wo = L["wo"]
-        ao = self._mm_fp8(o, wo, defer="pass") if isinstance(wo, Fp8Weight) else self._mm(o, wo)
+        # one rank: the o / down GEMMs' row-wise scales travel with the raw product into the next
+        # fused add + RMSNorm; tensor parallel: applied before the all-reduce of the partial sums
+        mode = "raw" if self.tp == 1 else "pass"
+        ao = self._mm_fp8(o, wo, defer=mode) if isinstance(wo, Fp8Weight) else self._mm(o, wo)
         x, h = self._add_rms(x, self._reduce(ao), L["ffn_norm"], next_w=L["wgu"])
         wgu, wd = L["wgu"], L["wdown"]
         if self.hip and isinstance(wd, Fp8Weight) and isinstance(wgu, Fp8Weight) and not (
@@ -560,11 +589,11 @@ class ServingLlama:
             # gate/up GEMM's row-wise scales are applied inside that kernel too
             r = self._mm_fp8(h, wgu, defer="raw")
             C = _ext.require()
-            if isinstance(r, tuple):
-                q, sc = C.swiglu_quant_fp8_rows(r[0], r[1], r[2])
+            if isinstance(r, RawScaled):
+                q, sc = C.swiglu_quant_fp8_rows(r.raw, r.rs, r.cs)
             else:
                 q, sc = C.swiglu_quant_fp8_rows(r if r.stride(-1) == 1 else r.contiguous())
-            return x, self._reduce(self._mm_fp8(Fp8Act(q, sc), wd, defer="pass"))
+            return x, self._reduce(self._mm_fp8(Fp8Act(q, sc), wd, defer=mode))
         gu = self._mm(h, wgu)
         return x, self._reduce(self._mm(self._swiglu(gu), wd))
 
@@ -589,6 +618,15 @@ class ServingLlama:
         for i in range(len(lens)):
             nxt = offsets[i + 1] if i + 1 < len(lens) else rows
             bounds.append((int(offsets[i]), int(nxt) - int(offsets[i])))
+        # consecutive segments of one length attend as one batch (one kernel launch instead of one
+        # per prompt: a 1024-token prompt alone fills 256 workgroups of a 70B layer)
+        groups: list[list[int]] = []
+        for off, n in bounds:
+            g = groups[-1] if groups else None
+            if g is not None and g[1] == n and g[0] + g[1] * g[2] == off:
+                g[2] += 1
+            else:
+                groups.append([off, n, 1])
         for li, L in enumerate(self.layers):
             if delta is None:
                 h = self._rms(x, L["attn_norm"], next_w=L["wqkv"])
@@ -600,16 +638,16 @@ class ServingLlama:
             sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH,
                                   self.k_scale, self.v_scale)
             o = torch.empty(rows, H * self.D, dtype=x.dtype, device=x.device)
-            for off, n in bounds:
-                seg = qkv[off : off + n].view(1, n, -1)
+            for off, n, cnt in groups:
+                seg = qkv[off : off + n * cnt].view(cnt, n, -1)
                 if self.hip:
-                    o[off : off + n] = _ext.require().flash_attn_fwd(seg, H, KVH, True)[0].view(n, -1)
+                    o[off : off + n * cnt] = _ext.require().flash_attn_fwd(seg, H, KVH, True)[0].view(n * cnt, -1)
                 else:
-                    q, k, v = seg.view(1, n, self.NH, self.D).split([H, KVH, KVH], dim=2)
-                    o[off : off + n] = ref.attention(q, k, v, causal=True).reshape(n, -1)
+                    q, k, v = seg.view(cnt, n, self.NH, self.D).split([H, KVH, KVH], dim=2)
+                    o[off : off + n * cnt] = ref.attention(q, k, v, causal=True).reshape(n * cnt, -1)
             x, delta = self._mlp_and_attn_out(L, x, o)
         last = torch.tensor([int(offsets[i]) + int(lens[i]) - 1 for i in range(len(lens))], device=x.device)
-        x, h = self._add_rms(x[last], delta[last], self.norm)
+        x, h = self._add_rms(x[last], delta.rows(last) if isinstance(delta, RawScaled) else delta[last], self.norm)
         return self._logits(h)
 
     @torch.no_grad()

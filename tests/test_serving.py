@@ -642,7 +642,8 @@ def test_gpu_fp8_engine_tracks_bf16(gpu):
 @pytest.mark.gpu
 def test_gpu_fp8_deferred_row_scales_match_rowwise(gpu):
     """Prefill-sized fp8 GEMMs run with scalar scales on the raw e4m3 operands and apply the
-    row-wise scales afterwards (SwiGLU-quant kernel for gate/up, an in-place pass for o / down).
+    row-wise scales afterwards (SwiGLU-quant kernel for gate/up, the fused add + RMSNorm -> e4m3
+    kernel for o / down, or an in-place pass).
     Kernels: bit-identical to scaling in fp32 then rounding.  Model: the extra bf16 rounding of the
     raw product keeps the prefill logits as close to the bf16 model's as the row-wise path's."""
     from dstack_amd.ops import _ext
@@ -661,6 +662,16 @@ def test_gpu_fp8_deferred_row_scales_match_rowwise(gpu):
         y = raw.clone()
         C.scale_rows_cols_(y, rs, cs)
         assert torch.equal(y, scaled)
+    for M, D in ((64, 1024), (2048, 8192)):  # the fused add + RMSNorm -> e4m3 with a raw delta
+        raw = torch.randn(M, D, device=gpu, dtype=torch.bfloat16) * 300
+        rs, cs = torch.rand(M, device=gpu) * 1e-2, torch.rand(D, device=gpu) * 1e-2
+        x = torch.randn(M, D, device=gpu, dtype=torch.bfloat16)
+        w = torch.rand(D, device=gpu, dtype=torch.bfloat16) + 0.5
+        scaled = (raw.float() * rs[:, None] * cs[None, :]).bfloat16()
+        h1, q1, s1 = C.rms_norm_fp8(x, raw, w, 1e-5, rs, cs)
+        h2, q2, s2 = C.rms_norm_fp8(x, scaled, w, 1e-5)
+        assert torch.equal(h1, h2) and torch.equal(s1, s2)
+        assert torch.equal(q1.view(torch.uint8), q2.view(torch.uint8))
     kw = dict(device="cuda", max_model_len=512, max_batch=8, num_pages=64)
     base = LLMEngine.from_model("llama-tiny", **kw)
     q8 = LLMEngine.from_model("llama-tiny", quantization="fp8", **kw)
@@ -788,15 +799,17 @@ def test_gpu_fp8_kv_decode_logits_track_bf16(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rows", [37, 2048])
 @pytest.mark.parametrize("with_delta", [False, True])
-def test_gpu_rms_norm_fp8_matches_unfused(gpu, with_delta):
-    """The fused (add +) RMSNorm -> e4m3 kernel equals RMSNorm followed by the row quantizer."""
+def test_gpu_rms_norm_fp8_matches_unfused(gpu, with_delta, rows):
+    """The fused (add +) RMSNorm -> e4m3 kernel equals RMSNorm followed by the row quantizer
+    (decode batches and, past 1024 rows, prefill, where the unfused norm is the wave-per-row one)."""
     from dstack_amd.ops import _ext
 
     C = _ext.require()
     g = torch.Generator(device=gpu).manual_seed(3)
-    x = torch.randn(37, 8192, device=gpu, generator=g).bfloat16()
-    d = torch.randn(37, 8192, device=gpu, generator=g).bfloat16()
+    x = torch.randn(rows, 8192, device=gpu, generator=g).bfloat16()
+    d = torch.randn(rows, 8192, device=gpu, generator=g).bfloat16()
     w = (torch.rand(8192, device=gpu, generator=g) + 0.5).bfloat16()
     if with_delta:
         h_ref, y_ref, _ = C.add_rms_norm_fwd(x, d, w, 1e-5)
