@@ -67,7 +67,7 @@ constexpr int HD = 128;          // head dim
 // 2.009-2.053 ms -- within noise, kept opt-in.
 // BUF (default; DSTACK_AMD_FA_FWD_BUF=0 turns it off): K/V tiles through buffer descriptors (dma_tile64_buf), which keeps
 // the S phase's LDS-read waits counted instead of lgkmcnt(0).
-template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0, bool STAG = false, bool BUF = false>
+template <bool CAUSAL, int NW = 4, bool PF = true, int PRIO = 0, bool STAG = false, bool BUF = false, int FPD = 4>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
                                                         float* __restrict__ lse, int B, int S,
@@ -152,24 +152,26 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_fwd_kernel(const 
       if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(3);
       if constexpr (PF) {
         // step i: key tile t = i & 1, k-slice ks = i >> 1; fragment i + 4 is read while i computes
-        bf16x8 kf[4];
+        constexpr int PD = BUF ? FPD : 4;  // reads in flight
+        bf16x8 kf[PD];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) kf[i] = lds_row(kl, 32 * (i & 1) + l32, 2 * (i >> 1) + hf);
+        for (int i = 0; i < PD; ++i) kf[i] = lds_row(kl, 32 * (i & 1) + l32, 2 * (i >> 1) + hf);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const bf16x8 a = kf[i & 3];
-          if (i + 4 < 16) kf[i & 3] = lds_row(kl, 32 * ((i + 4) & 1) + l32, 2 * ((i + 4) >> 1) + hf);
+          const bf16x8 a = kf[i % PD];
+          if (i + PD < 16) kf[i % PD] = lds_row(kl, 32 * ((i + PD) & 1) + l32, 2 * ((i + PD) >> 1) + hf);
           st[i & 1] = mfma(a, qf[i >> 1], st[i & 1]);
         }
         // pin the interleave (the scheduler otherwise sinks each read below the MFMAs that free
-        // its register, leaving one read pair in flight): 4 reads, then (MFMA, read) x 12, 4 MFMAs
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        // its register, leaving one read pair in flight): PD reads, then (MFMA, read) x (16 - PD),
+        // PD MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) {
+        for (int i = 0; i < 16 - PD; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, PD, 0);
       } else {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -1243,6 +1245,10 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     return !(v && atoi(v) == 0);
   }();
   const bool fwd_buf = fwd_buf_env && (long)S * (H + 2 * KVH) * HD * 2 < (1L << 31);
+  static const int fwd_pfd = [] {  // S-phase K reads in flight (buffer-DMA form): 4 or 8 (A/B)
+    const char* v = getenv("DSTACK_AMD_FA_FWD_PFD");
+    return (v && atoi(v) == 8) ? 8 : 4;
+  }();
   if (waves == 8 && S % 256 == 0) {
     const int grid = B * H * (S / 256);
     if (causal && pf && half_prio)
@@ -1257,6 +1263,9 @@ extern "C" hipError_t dsa_fa_fwd(const void* qkv, void* out, float* lse, int B, 
     else if (causal && pf && prio == 2)
       fa_fwd_kernel<true, 8, true, 2><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S, H, KVH, sl2,
                                                             thr);
+    else if (causal && pf && fwd_buf && fwd_pfd == 8)
+      fa_fwd_kernel<true, 8, true, 0, false, true, 8><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B,
+                                                                            S, H, KVH, sl2, thr);
     else if (causal && pf && fwd_buf)
       fa_fwd_kernel<true, 8, true, 0, false, true><<<grid, 512, lds, st>>>((const bf16_t*)qkv, (bf16_t*)out, lse, B, S,
                                                                          H, KVH, sl2, thr);
@@ -1398,7 +1407,11 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
       fa_bwd_dkdv8_kernel<C, false, false, false, false, false, 1>                                     \
           <<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(                             \
               (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
-    } else if (dkdv_pf >= 2 && dkdv_kind == 8) {                                                       \
+    } else if (dkdv_pf >= 3 && dkdv_kind == 8) {                                                       \
+      fa_bwd_dkdv8_kernel<C, false, false, false, false, false, 3>                                     \
+          <<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(                             \
+              (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
+    } else if (dkdv_pf == 2 && dkdv_kind == 8) {                                                       \
       fa_bwd_dkdv8_kernel<C, false, false, false, false, false, 2>                                     \
           <<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(                             \
               (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
