@@ -26,6 +26,10 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: the e4m3 projections of --quantization fp8 (torch._scaled_mm, row-wise scales; "
                          "M padded to 16 as the model does; the LM head stays bf16)")
+    ap.add_argument("--scaling", default="row", choices=["row", "tensor"],
+                    help="fp8 scale form: row-wise (decode) or scalar (the deferred-scale prefill GEMMs, "
+                         "model.py RawScaled); TunableOp keys the two separately")
+    ap.add_argument("--weights", default="", help="comma-separated subset of wqkv,wo,wgu,wdown,lm_head")
     args = ap.parse_args()
     import torch
 
@@ -48,13 +52,19 @@ def main():
         for wname, (N, K) in shapes.items():
             if fp8 and wname == "lm_head":
                 continue
+            if args.weights and wname not in args.weights.split(","):
+                continue
             w = torch.randn(N, K, device=dev).to(torch.bfloat16)
             if fp8:
                 w8, sw = w.to(f8), torch.rand(1, N, device=dev) + 0.5
+                if args.scaling == "tensor":
+                    sw = torch.ones((), device=dev)
             for M in sorted({(m + 15) // 16 * 16 for m in buckets} if fp8 else buckets):
                 x = torch.randn(M, K, device=dev).to(torch.bfloat16)
                 if fp8:
                     x8, sx = x.to(f8), torch.rand(M, 1, device=dev) + 0.5
+                    if args.scaling == "tensor":
+                        sx = torch.ones((), device=dev)
 
                     def mm():
                         return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw, out_dtype=torch.bfloat16)
@@ -71,7 +81,7 @@ def main():
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) / it
                 tbs = (N * K * (1 if fp8 else 2) + (M * K + M * N) * 2) / dt / 1e12
-                out.append({"model": name, "w": wname, "dtype": args.dtype, "M": M, "N": N, "K": K,
+                out.append({"model": name, "w": wname, "dtype": args.dtype, "scaling": args.scaling, "M": M, "N": N, "K": K,
                             "us": round(dt * 1e6, 1),
                             "TBps": round(tbs, 2)})
                 print(json.dumps(out[-1]), flush=True)
