@@ -150,7 +150,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         # KM weight gradients take a and dgu token-major: no transposed copies from the epilogues
         ctx.km = _wgrad_mode() == "km"
         gu, a, aT = C.gemm_nt_swiglu(h2, wgu, not ctx.km)
-        y = a @ wdown.t()
+        y = _nt(a, wdown)
         ctx.save_for_backward(h2, gu, a if ctx.km else aT, wgu, wdown)
         ctx.hshape = h.shape
         return y.view(*h.shape[:-1], wdown.shape[0])
@@ -178,7 +178,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         dgu, dguT = C.gemm_nt_swiglu_bwd(dy2, wdT, gu, not ctx.km)
         # dx = dgu W_gu
         wguT = _transposed_weight(wgu)
-        dx = dgu @ (wguT.t() if wguT is not None else wgu)
+        dx = _nt(dgu, wguT) if wguT is not None else dgu @ wgu
         # gate/up weight gradient dW_gu = dgu^T h  (dgu^T from the fused epilogue)
         ggu = None
         a_op, b_op = wgrad_operands(dgu, h2, gT=None if ctx.km else dguT)
@@ -349,7 +349,7 @@ class _Linear(torch.autograd.Function):
         xT = getattr(x, "_dsa_t", None)
         ctx.x_is_t = xT is not None
         ctx.save_for_backward(xT if ctx.x_is_t else x, w)
-        return x @ w.t()
+        return _nt(x, w)
 
     @staticmethod
     def backward(ctx, g):
@@ -357,7 +357,7 @@ class _Linear(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             wt = _transposed_weight(w)
-            gx = g @ (wt.t() if wt is not None else w)
+            gx = _nt(g, wt) if wt is not None else g @ w
         if not ctx.needs_input_grad[1]:
             return gx, None
         g2 = g.reshape(-1, g.shape[-1])
@@ -371,6 +371,23 @@ class _Linear(torch.autograd.Function):
             return gx, mm_into(a, b)
         sink(w, a, b)
         return gx, None
+
+
+def _nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``a @ b.t()`` for a [.., K] activation and a [N, K] weight.  ``DSTACK_AMD_LINEAR_NT=1`` runs it
+    on the in-tree gfx950 GEMM (csrc/gemm_nt.hip) where the shape is tiled; otherwise (and by default:
+    hipBLASLt measured at parity on these shapes) the library GEMM."""
+    if (os.environ.get("DSTACK_AMD_LINEAR_NT") == "1" and _ext.use_hip(a) and a.dtype == torch.bfloat16
+            and b.dtype == torch.bfloat16):
+        a2 = a.reshape(-1, a.shape[-1])
+        C = _ext.require()
+        if (C.gemm_nt_supported(a2.shape[0], b.shape[0], a2.shape[1]) and a2.stride(1) == 1 and b.stride(1) == 1
+                and a2.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+                and a2.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0):
+            out = torch.empty(a2.shape[0], b.shape[0], device=a.device, dtype=a.dtype)
+            C.gemm_nt(a2, b, out, False)
+            return out.view(*a.shape[:-1], b.shape[0])
+    return a @ b.t()
 
 
 def _transposed_weight(w: torch.Tensor):
