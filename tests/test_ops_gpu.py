@@ -403,6 +403,22 @@ def test_linear_wgrad_layouts_agree(gpu, T, P, Q, monkeypatch):
     assert torch.equal(grads["auto"][0], grads["strided"][0])
 
 
+def test_linear_on_in_tree_nt_gemm(gpu, monkeypatch):
+    """DSTACK_AMD_LINEAR_NT=1: the projection's forward (and a tiled shape's input gradient) on the
+    in-tree NT GEMM match the fp32 reference; an untiled shape falls back to the library."""
+    monkeypatch.setenv("DSTACK_AMD_LINEAR_NT", "1")
+    for T, P, Q in ((512, 256, 384), (300, 256, 384)):
+        x = _rand(T, Q, device=gpu, seed=15).requires_grad_()
+        w = _rand(P, Q, device=gpu, seed=16, scale=0.05).requires_grad_()
+        g = _rand(T, P, device=gpu, seed=17)
+        y = ops.linear(x, w)
+        ref_y = x.detach().float() @ w.detach().float().t()
+        assert ((y.float() - ref_y).norm() / ref_y.norm()).item() < 4e-3, (T, P, Q)
+        y.backward(g)
+        ref_gx = g.float() @ w.detach().float()
+        assert ((x.grad.float() - ref_gx).norm() / ref_gx.norm()).item() < 4e-3, (T, P, Q)
+
+
 def test_swiglu_fwd_t_matches(gpu):
     Cx = _ext.require()
     gu = _rand(256, 2 * 192, device=gpu, seed=12)
