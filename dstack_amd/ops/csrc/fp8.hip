@@ -84,7 +84,10 @@ __device__ __forceinline__ float silu_q(float g) { return g / (1.f + __expf(-g))
 // Llama-3-70B prefill shapes 12-25 % faster with scalar scales than with row-wise ones,
 // profiles/fp8_scaling_modes_r8z.txt); the per-token scale rs[row] and the per-output-channel scale
 // cs[c] of the row-wise form are applied here, on the fp32 values, before the SwiGLU.
-template <bool SCALED>
+// NIT > 0: the row's products stay in registers (packed bf16, exact: they are bf16-rounded) between
+// the absmax pass and the quantization pass, so gu (and cs) are read once instead of twice; NIT is
+// the number of 2048-column steps, F <= 2048 * NIT.  NIT = 0: two passes over gu (any F).
+template <bool SCALED, int NIT = 0>
 __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __restrict__ gu, long ldg,
                                                                 unsigned char* __restrict__ q, long ldq,
                                                                 float* __restrict__ s, int F,
@@ -113,11 +116,26 @@ __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __
     for (int i = 0; i < 8; ++i) a[i] = bf2f(f2bf(silu_q(g[i]) * u[i]));
   };
   float amax = 0.f;
-  for (int k = tid * 8; k < F; k += 256 * 8) {
-    float a[8];
-    prod8(k, a);
+  us8 pk[NIT > 0 ? NIT : 1];
+  if constexpr (NIT > 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(a[i]));
+    for (int it = 0; it < NIT; ++it) {
+      const int k = (tid + it * 256) * 8;
+      if (k < F) {
+        float a[8];
+        prod8(k, a);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(a[i]));
+        pk[it] = pack8(a);
+      }
+    }
+  } else {
+    for (int k = tid * 8; k < F; k += 256 * 8) {
+      float a[8];
+      prod8(k, a);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(a[i]));
+    }
   }
   amax = wave_max(amax);
   if ((tid & 63) == 0) red[tid >> 6] = amax;
@@ -127,13 +145,27 @@ __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __
   const float inv = 1.f / scale;
   if (tid == 0) s[row] = scale;
   unsigned char* qr = q + (long)row * ldq;
-  for (int k = tid * 8; k < F; k += 256 * 8) {
-    float a[8];
-    prod8(k, a);
-    unsigned int w0 = f32x4_to_fp8(a[0] * inv, a[1] * inv, a[2] * inv, a[3] * inv);
-    unsigned int w1 = f32x4_to_fp8(a[4] * inv, a[5] * inv, a[6] * inv, a[7] * inv);
-    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-    *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  if constexpr (NIT > 0) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int k = (tid + it * 256) * 8;
+      if (k < F) {
+        float a[8];
+        unpack8(pk[it], a);
+        const unsigned int w0 = f32x4_to_fp8(a[0] * inv, a[1] * inv, a[2] * inv, a[3] * inv);
+        const unsigned int w1 = f32x4_to_fp8(a[4] * inv, a[5] * inv, a[6] * inv, a[7] * inv);
+        *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+      }
+    }
+  } else {
+    for (int k = tid * 8; k < F; k += 256 * 8) {
+      float a[8];
+      prod8(k, a);
+      const unsigned int w0 = f32x4_to_fp8(a[0] * inv, a[1] * inv, a[2] * inv, a[3] * inv);
+      const unsigned int w1 = f32x4_to_fp8(a[4] * inv, a[5] * inv, a[6] * inv, a[7] * inv);
+      *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+    }
   }
 }
 
@@ -275,11 +307,24 @@ extern "C" hipError_t dsa_quant_fp8_rows(const void* x, long ldx, void* q, long 
 extern "C" hipError_t dsa_swiglu_quant_fp8_rows(const void* gu, long ldg, void* q, long ldq, float* s, int M, int F,
                                                 const float* rs, const float* cs, hipStream_t st) {
   if (F <= 0 || F % 8 || M <= 0 || ((rs == nullptr) != (cs == nullptr))) return hipErrorInvalidValue;
-  if (rs)
-    swiglu_quant_rows_kernel<true><<<M, 256, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F, rs, cs);
-  else
-    swiglu_quant_rows_kernel<false><<<M, 256, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F, nullptr,
-                                                       nullptr);
+  // products held in registers for F <= 32768 (Llama-3-70B: F = 28672 -> 14 steps of 2048 columns)
+  const int nit = (F + 2047) / 2048;
+#define DSA_SWQ(SC, N)                                                                                     \
+  swiglu_quant_rows_kernel<SC, N><<<M, 256, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F, \
+                                                     SC ? rs : nullptr, SC ? cs : nullptr)
+#define DSA_SWQ_N(SC)                    \
+  if (nit <= 2) DSA_SWQ(SC, 2);          \
+  else if (nit <= 4) DSA_SWQ(SC, 4);     \
+  else if (nit <= 8) DSA_SWQ(SC, 8);     \
+  else if (nit <= 16) DSA_SWQ(SC, 16);   \
+  else DSA_SWQ(SC, 0);
+  if (rs) {
+    DSA_SWQ_N(true)
+  } else {
+    DSA_SWQ_N(false)
+  }
+#undef DSA_SWQ_N
+#undef DSA_SWQ
   return hipGetLastError();
 }
 

@@ -650,7 +650,7 @@ def test_gpu_fp8_deferred_row_scales_match_rowwise(gpu):
 
     C = _ext.require()
     torch.manual_seed(0)
-    for M, F in ((128, 1024), (256, 3584)):
+    for M, F in ((128, 1024), (256, 3584), (64, 28672)):
         raw = torch.randn(M, 2 * F, device=gpu, dtype=torch.bfloat16) * 300
         rs = torch.rand(M, device=gpu) * 1e-2
         cs = torch.rand(2 * F, device=gpu) * 1e-2
@@ -901,7 +901,7 @@ def test_gpu_swiglu_quant_fp8_rows_matches_separate_kernels(gpu):
 
     C = _ext.require()
     torch.manual_seed(0)
-    for M, F in ((1, 512), (37, 1024), (256, 3584)):
+    for M, F in ((1, 512), (37, 1024), (256, 3584), (16, 14336), (8, 28672), (3, 40960)):
         gu = torch.randn(M, 2 * F, device=gpu, dtype=torch.bfloat16) * 2
         q, s = C.swiglu_quant_fp8_rows(gu)
         q2, s2 = C.quant_fp8_rows(C.swiglu_fwd(gu))
