@@ -42,6 +42,9 @@ __device__ __forceinline__ unsigned int f32x4_to_fp8(float a, float b, float c, 
 }
 
 // one 256-thread workgroup per row; K % 8 == 0
+// NIT > 0: the row stays in registers between the absmax and quantization passes (x read once),
+// K <= 2048 * NIT; NIT = 0: two passes over x (any K)
+template <int NIT = 0>
 __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restrict__ x, long ldx,
                                                          unsigned char* __restrict__ q, long ldq,
                                                          float* __restrict__ s, int K) {
@@ -49,11 +52,26 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restric
   const int row = blockIdx.x, tid = threadIdx.x;
   const bf16_t* xr = x + (long)row * ldx;
   float amax = 0.f;
-  for (int k = tid * 8; k < K; k += 256 * 8) {
-    float v[8];
-    unpack8(*reinterpret_cast<const us8*>(xr + k), v);
+  us8 pk[NIT > 0 ? NIT : 1];
+  if constexpr (NIT > 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+    for (int it = 0; it < NIT; ++it) {
+      const int k = (tid + it * 256) * 8;
+      if (k < K) {
+        pk[it] = *reinterpret_cast<const us8*>(xr + k);
+        float v[8];
+        unpack8(pk[it], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+      }
+    }
+  } else {
+    for (int k = tid * 8; k < K; k += 256 * 8) {
+      float v[8];
+      unpack8(*reinterpret_cast<const us8*>(xr + k), v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+    }
   }
   amax = wave_max(amax);
   if ((tid & 63) == 0) red[tid >> 6] = amax;
@@ -63,21 +81,35 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restric
   const float inv = 1.f / scale;
   if (tid == 0) s[row] = scale;
   unsigned char* qr = q + (long)row * ldq;
-  for (int k = tid * 8; k < K; k += 256 * 8) {
-    float v[8];
-    unpack8(*reinterpret_cast<const us8*>(xr + k), v);
-    unsigned int w0 = f32x4_to_fp8(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
-    unsigned int w1 = f32x4_to_fp8(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv);
-    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-    *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  if constexpr (NIT > 0) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int k = (tid + it * 256) * 8;
+      if (k < K) {
+        float v[8];
+        unpack8(pk[it], v);
+        const unsigned int w0 = f32x4_to_fp8(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+        const unsigned int w1 = f32x4_to_fp8(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv);
+        *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+      }
+    }
+  } else {
+    for (int k = tid * 8; k < K; k += 256 * 8) {
+      float v[8];
+      unpack8(*reinterpret_cast<const us8*>(xr + k), v);
+      const unsigned int w0 = f32x4_to_fp8(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+      const unsigned int w1 = f32x4_to_fp8(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv);
+      *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+    }
   }
 }
 
 // SwiGLU + per-row quantization for the fp8 down projection of a decode step: gu [M][2F] bf16
 // (gate | up) -> q [M][F] e4m3 + s [M], q * s ~= bf16(silu(g) * u) -- the separate swiglu_fwd and
 // quant_rows kernels wrote and re-read the bf16 product.  One workgroup per row: pass 1 takes the
-// row max of the bf16-rounded product, pass 2 recomputes it (the row's gu is L2-resident by then)
-// and writes e4m3.
+// row max of the bf16-rounded product, pass 2 writes e4m3 from the products it kept in registers
+// (F up to 32768; wider rows recompute them from gu).
 __device__ __forceinline__ float silu_q(float g) { return g / (1.f + __expf(-g)); }
 
 // SCALED: gu is the raw e4m3 x e4m3 product of a tensor-wise-scaled fp8 GEMM (hipBLASLt runs the
@@ -300,7 +332,14 @@ extern "C" bool dsa_quant_fp8_supported(int K) { return K > 0 && K % 8 == 0; }
 extern "C" hipError_t dsa_quant_fp8_rows(const void* x, long ldx, void* q, long ldq, float* s, int M, int K,
                                          hipStream_t st) {
   if (!dsa_quant_fp8_supported(K) || M <= 0) return hipErrorInvalidValue;
-  quant_rows_kernel<<<M, 256, 0, st>>>((const bf16_t*)x, ldx, (unsigned char*)q, ldq, s, K);
+  const int nit = (K + 2047) / 2048;
+#define DSA_QR(N) quant_rows_kernel<N><<<M, 256, 0, st>>>((const bf16_t*)x, ldx, (unsigned char*)q, ldq, s, K)
+  if (nit <= 2) DSA_QR(2);
+  else if (nit <= 4) DSA_QR(4);
+  else if (nit <= 8) DSA_QR(8);
+  else if (nit <= 16) DSA_QR(16);
+  else DSA_QR(0);
+#undef DSA_QR
   return hipGetLastError();
 }
 

@@ -580,7 +580,7 @@ def test_fp8_rejects_unknown_quantization():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,K", [(1, 4096), (7, 8192), (256, 4096)])
+@pytest.mark.parametrize("M,K", [(1, 4096), (7, 8192), (256, 4096), (5, 28672), (4, 32768), (2, 1000)])
 def test_gpu_quant_fp8_rows_matches_torch(gpu, M, K):
     """HIP per-row e4m3 quantization: scales equal max|x|/448 and the bytes decode to the same
     values as torch's float8_e4m3fn cast (round to nearest even) up to ties."""
