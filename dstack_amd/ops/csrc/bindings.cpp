@@ -30,7 +30,7 @@ hipError_t dsa_fa_bwd(const void*, const void*, const void*, const float*, void*
                       int, float, int, hipStream_t);
 int dsa_paged_page_size();
 hipError_t dsa_rope_cache_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int,
-                                int, int, float, float, hipStream_t);
+                                int, int, float, float, const float*, const float*, hipStream_t);
 hipError_t dsa_paged_decode(const void*, long, const void*, const void*, const int*, int, const int*, void*, float*,
                             float*, int, int, int, int, int, float, int, float, float, hipStream_t);
 hipError_t dsa_sample(const void*, long, int, int, const float*, const int64_t*, const int*, int*, float*,
@@ -640,10 +640,13 @@ bool check_cache(const torch::Tensor& k, const torch::Tensor& v, int64_t KVH) {
   return fp8;
 }
 
-// rotates q/k of qkv [T, (H+2KVH)*128] in place and writes k, v of each token to its cache slot
+// rotates q/k of qkv [T, (H+2KVH)*128] in place and writes k, v of each token to its cache slot;
+// rs [T] / cs [(H+2KVH)*128] (optional, together): qkv is a raw fp8 GEMM product whose row-wise
+// scales are applied first (and written back for every head)
 void rope_cache_write(torch::Tensor qkv, torch::Tensor positions, torch::Tensor slots, torch::Tensor cos,
                       torch::Tensor sin, torch::Tensor k_cache, torch::Tensor v_cache, int64_t H, int64_t KVH,
-                      double k_scale, double v_scale) {
+                      double k_scale, double v_scale, c10::optional<torch::Tensor> rs,
+                      c10::optional<torch::Tensor> cs) {
   check_bf16(qkv, "qkv");
   check_i32(positions, "positions");
   check_i32(slots, "slots");
@@ -654,9 +657,22 @@ void rope_cache_write(torch::Tensor qkv, torch::Tensor positions, torch::Tensor 
   TORCH_CHECK(cos.scalar_type() == torch::kFloat32 && sin.scalar_type() == torch::kFloat32 && cos.is_contiguous() &&
                   sin.is_contiguous() && cos.size(1) == 64 && sin.sizes() == cos.sizes(),
               "rope tables must be fp32 [max_pos, 64]");
+  TORCH_CHECK(rs.has_value() == cs.has_value(), "rope_cache_write: rs and cs go together");
+  const float* rp = nullptr;
+  const float* cp = nullptr;
+  if (rs.has_value()) {
+    TORCH_CHECK(qkv.is_contiguous(), "rope_cache_write: a raw product must be contiguous");
+    TORCH_CHECK(rs->scalar_type() == torch::kFloat32 && rs->is_contiguous() && rs->numel() == T,
+                "rope_cache_write: rs must be fp32 [T]");
+    TORCH_CHECK(cs->scalar_type() == torch::kFloat32 && cs->is_contiguous() && cs->numel() == (H + 2 * KVH) * 128 &&
+                    reinterpret_cast<uintptr_t>(cs->data_ptr()) % 16 == 0,
+                "rope_cache_write: cs must be fp32 [(H+2KVH)*128], 16-byte aligned");
+    rp = rs->data_ptr<float>();
+    cp = cs->data_ptr<float>();
+  }
   check(dsa_rope_cache_write(qkv.data_ptr(), positions.data_ptr<int>(), slots.data_ptr<int>(), cos.data_ptr<float>(),
                              sin.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(), (int)T, (int)H, (int)KVH,
-                             fp8 ? 1 : 0, (float)k_scale, (float)v_scale, stream()),
+                             fp8 ? 1 : 0, (float)k_scale, (float)v_scale, rp, cp, stream()),
         "rope_cache_write");
 }
 
@@ -760,7 +776,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemv", &gemv);
   m.def("gemv_supported", &gemv_supported);
   m.def("paged_page_size", &dsa_paged_page_size);
-  m.def("rope_cache_write", &rope_cache_write);
+  m.def("rope_cache_write", &rope_cache_write, py::arg("qkv"), py::arg("positions"), py::arg("slots"), py::arg("cos"),
+        py::arg("sin"), py::arg("k_cache"), py::arg("v_cache"), py::arg("H"), py::arg("KVH"), py::arg("k_scale"),
+        py::arg("v_scale"), py::arg("rs") = py::none(), py::arg("cs") = py::none());
   m.def("paged_decode", &paged_decode);
   m.def("sample", &sample);
 }

@@ -75,7 +75,10 @@ __device__ __forceinline__ unsigned char to_fp8(float x) {
 // (= page * PAGE + offset; < 0: padding token, not cached).  One thread = 8 rotation pairs.
 // ------------------------------------------------------------------------------------------------
 // FP8: the cache holds e4m3 bytes of k / k_scale and v / v_scale (same layout, 1 byte per value).
-template <bool FP8>
+// SC: qkv is the raw product of a tensor-wise-scaled fp8 GEMM (serving prefill, model.py RawScaled);
+// the per-token scale rs[t] and per-column scale cs[col] are applied first (rounded to bf16 as the
+// row-wise GEMM's output would be), and the v heads are written back scaled as well.
+template <bool FP8, bool SC = false>
 __global__ __launch_bounds__(256) void rope_cache_write_kernel(bf16_t* __restrict__ qkv,
                                                                const int* __restrict__ positions,
                                                                const int* __restrict__ slots,
@@ -83,7 +86,9 @@ __global__ __launch_bounds__(256) void rope_cache_write_kernel(bf16_t* __restric
                                                                const float* __restrict__ sinT,
                                                                void* __restrict__ k_cache,
                                                                void* __restrict__ v_cache, int T,
-                                                               int H, int KVH, float inv_ks, float inv_vs) {
+                                                               int H, int KVH, float inv_ks, float inv_vs,
+                                                               const float* __restrict__ rs = nullptr,
+                                                               const float* __restrict__ cs = nullptr) {
   constexpr int half = HDIM / 2, cph = half / 8;  // 8 chunks of 8 pairs per head
   const int NH = H + 2 * KVH;
   const size_t total = (size_t)T * NH * cph;
@@ -95,6 +100,28 @@ __global__ __launch_bounds__(256) void rope_cache_write_kernel(bf16_t* __restric
     bf16_t* row = qkv + (size_t)t * NH * HDIM + (size_t)head * HDIM;
     us8 a = *reinterpret_cast<const us8*>(row + c * 8);
     us8 b = *reinterpret_cast<const us8*>(row + half + c * 8);
+    if constexpr (SC) {
+      const float r = rs[t];
+      const float* cc = cs + (size_t)head * HDIM + c * 8;
+      const f4 ca0 = *reinterpret_cast<const f4*>(cc), ca1 = *reinterpret_cast<const f4*>(cc + 4);
+      const f4 cb0 = *reinterpret_cast<const f4*>(cc + half), cb1 = *reinterpret_cast<const f4*>(cc + half + 4);
+      float xa[8], xb[8];
+      unpack8(a, xa);
+      unpack8(b, xb);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        xa[k] = bf2f(f2bf(xa[k] * r * ca0[k]));
+        xa[4 + k] = bf2f(f2bf(xa[4 + k] * r * ca1[k]));
+        xb[k] = bf2f(f2bf(xb[k] * r * cb0[k]));
+        xb[4 + k] = bf2f(f2bf(xb[4 + k] * r * cb1[k]));
+      }
+      a = pack8(xa);
+      b = pack8(xb);
+      if (head >= H + KVH) {  // v heads: the scaled values back in place (q / k: after the rotation)
+        *reinterpret_cast<us8*>(row + c * 8) = a;
+        *reinterpret_cast<us8*>(row + half + c * 8) = b;
+      }
+    }
     if (head < H + KVH) {  // q and k heads rotate
       const int pos = positions[t];
       const f4* cp = reinterpret_cast<const f4*>(cosT + (size_t)pos * half + c * 8);
@@ -511,12 +538,19 @@ extern "C" int dsa_paged_page_size() { return PAGE; }
 extern "C" hipError_t dsa_rope_cache_write(void* qkv, const int* positions, const int* slots,
                                            const float* cosT, const float* sinT, void* k_cache,
                                            void* v_cache, int T, int H, int KVH, int fp8, float k_scale,
-                                           float v_scale, hipStream_t st) {
+                                           float v_scale, const float* rs, const float* cs, hipStream_t st) {
   if (T <= 0) return hipSuccess;
+  if ((rs == nullptr) != (cs == nullptr)) return hipErrorInvalidValue;
   const size_t work = (size_t)T * (H + 2 * KVH) * (HDIM / 16);
   size_t grid = (work + 255) / 256;
   if (grid > 65535 * 4) grid = 65535 * 4;
-  if (fp8)
+  if (rs && fp8)
+    rope_cache_write_kernel<true, true><<<(unsigned)grid, 256, 0, st>>>(
+        (bf16_t*)qkv, positions, slots, cosT, sinT, k_cache, v_cache, T, H, KVH, 1.f / k_scale, 1.f / v_scale, rs, cs);
+  else if (rs)
+    rope_cache_write_kernel<false, true><<<(unsigned)grid, 256, 0, st>>>(
+        (bf16_t*)qkv, positions, slots, cosT, sinT, k_cache, v_cache, T, H, KVH, 1.f, 1.f, rs, cs);
+  else if (fp8)
     rope_cache_write_kernel<true><<<(unsigned)grid, 256, 0, st>>>((bf16_t*)qkv, positions, slots, cosT, sinT,
                                                                   k_cache, v_cache, T, H, KVH, 1.f / k_scale,
                                                                   1.f / v_scale);

@@ -37,13 +37,18 @@ def _is_fp8(cache: torch.Tensor) -> bool:
 # ----------------------------------------------------------------------------------------------
 def rope_cache_write(qkv: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cos: torch.Tensor,
                      sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n_heads: int,
-                     n_kv_heads: int, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
+                     n_kv_heads: int, k_scale: float = 1.0, v_scale: float = 1.0, rs=None, cs=None) -> torch.Tensor:
     """Rotate q and k of ``qkv`` [T, (H + 2*KVH) * 128] in place (token t at ``positions[t]``) and
-    store k/v of every token with ``slots[t] >= 0`` in the cache.  Returns ``qkv``."""
+    store k/v of every token with ``slots[t] >= 0`` in the cache.  Returns ``qkv``.
+
+    ``rs`` [T] / ``cs`` [(H + 2*KVH) * 128]: ``qkv`` is the raw product of a tensor-wise-scaled fp8
+    GEMM; its row-wise scales are applied first, in place for every head."""
     if _ext.use_hip(qkv):
         _ext.require().rope_cache_write(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads,
-                                        k_scale, v_scale)
+                                        k_scale, v_scale, rs, cs)
         return qkv
+    if rs is not None:
+        qkv.copy_((qkv.float() * rs[:, None] * cs[None, :]).to(qkv.dtype))
     return rope_cache_write_ref(qkv, positions, slots, cos, sin, k_cache, v_cache, n_heads, n_kv_heads,
                                 k_scale, v_scale)
 

@@ -632,11 +632,22 @@ class ServingLlama:
                 h = self._rms(x, L["attn_norm"], next_w=L["wqkv"])
             else:
                 x, h = self._add_rms(x, delta, L["attn_norm"], next_w=L["wqkv"])
-            qkv = self._mm(h, L["wqkv"]) if isinstance(L["wqkv"], Fp8Weight) else h @ L["wqkv"].t()
-            if "bqkv" in L:
-                qkv = qkv + L["bqkv"]
-            sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li], H, KVH,
-                                  self.k_scale, self.v_scale)
+            wq = L["wqkv"]
+            if isinstance(wq, Fp8Weight) and "bqkv" not in L:
+                # prefill-sized: the GEMM's row-wise scales are applied by the RoPE / cache-write kernel
+                r = self._mm_fp8(h, wq, defer="raw")
+            else:
+                r = self._mm(h, wq) if isinstance(wq, Fp8Weight) else h @ wq.t()
+            if isinstance(r, RawScaled):
+                qkv = r.raw
+                sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li],
+                                      H, KVH, self.k_scale, self.v_scale, rs=r.rs, cs=r.cs)
+            else:
+                qkv = r
+                if "bqkv" in L:
+                    qkv = qkv + L["bqkv"]
+                sops.rope_cache_write(qkv, positions, slots, self.cos, self.sin, self.k_cache[li], self.v_cache[li],
+                                      H, KVH, self.k_scale, self.v_scale)
             o = torch.empty(rows, H * self.D, dtype=x.dtype, device=x.device)
             for off, n, cnt in groups:
                 seg = qkv[off : off + n * cnt].view(cnt, n, -1)

@@ -467,6 +467,30 @@ def test_gpu_rope_cache_write_kernel(gpu):
     torch.testing.assert_close(vc.float(), vr, atol=1e-6, rtol=0)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cache_dtype", [torch.bfloat16, torch.float8_e4m3fn])
+def test_gpu_rope_cache_write_scaled_raw_product(gpu, cache_dtype):
+    """A raw fp8 GEMM product with its row-wise scales handed to the RoPE / cache-write kernel gives
+    bit-for-bit the qkv (every head, v included) and the cache of the pre-scaled product."""
+    torch.manual_seed(1)
+    dev, H, KVH, T = "cuda", 8, 2, 40
+    cos, sin = sops_rope(dev)
+    W = (H + 2 * KVH) * 128
+    raw = (torch.randn(T, W, device=dev) * 300).to(torch.bfloat16)
+    rs, cs = torch.rand(T, device=dev) * 1e-2, torch.rand(W, device=dev) * 1e-2
+    scaled = (raw.float() * rs[:, None] * cs[None, :]).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=dev, dtype=torch.int32)
+    slots = torch.randperm(4 * 64, device=dev)[:T].int()
+    slots[3] = -1
+    ka, va = sops.alloc_cache(4, KVH, cache_dtype, dev)
+    kb, vb = sops.alloc_cache(4, KVH, cache_dtype, dev)
+    a = sops.rope_cache_write(raw.clone(), pos, slots, cos, sin, ka, va, H, KVH, 0.5, 0.5, rs=rs, cs=cs)
+    b = sops.rope_cache_write(scaled.clone(), pos, slots, cos, sin, kb, vb, H, KVH, 0.5, 0.5)
+    assert torch.equal(a, b)
+    assert torch.equal(ka.view(torch.uint8), kb.view(torch.uint8)) if cache_dtype != torch.bfloat16 else torch.equal(ka, kb)
+    assert torch.equal(va.view(torch.uint8), vb.view(torch.uint8)) if cache_dtype != torch.bfloat16 else torch.equal(va, vb)
+
+
 def sops_rope(dev):
     from dstack_amd.serving.model import rope_tables
 
