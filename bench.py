@@ -13,9 +13,17 @@ Weak scaling: each GPU processes ``--grad-accum`` × ``--micro-batch`` × ``--se
 step (default 8 × 1 × 8192).
 Data: synthetic random token ids; weights: random init (no network, no checkpoints).
 
-The orchestration half of the metric is measured literally, on rank 0 before training, in a
-child process with its own time limit (``bench_apply.py``): a real server (native shim/runner,
-local backend) receives ``examples/llama3-8b-train`` through the API with ``MI355X:N``, the
+The orchestration half of the metric is measured literally, in a child process with its own time
+limit (``bench_apply.py``), at a moment when no rank of this benchmark holds a GPU:
+
+* no launcher (N=1, or N>1 self-launched): in THIS process before any rank exists -- nothing here
+  has touched the GPU yet, and the ranks are started only after the cold start has finished;
+* under an external launcher (the driver's ``torch.distributed.run``): on rank 0 AFTER the timed
+  steps, once every rank has freed its model, optimizer and cached blocks and left the process
+  group (ranks 1..N-1 exit; rank 0 keeps only its idle HIP context), so the applied N-GPU task
+  never shares HBM or xGMI links with the benchmark's own ranks and no collective waits on it.
+
+In it a real server (native shim/runner, local backend) receives ``examples/llama3-8b-train`` through the API with ``MI355X:N``, the
 task's own ``torchrun ... bench.py`` runs, and
 ``cold_start_p50_s`` = submit -> the task's FIRST OPTIMIZER STEP finished, p50 over 3 runs that
 each land on a freshly created instance (``cold_start.stages_p50_s`` splits it: control plane,
@@ -54,18 +62,40 @@ def _child_json(cmd: list, timeout: float) -> dict:
         return {"error": str(e)[:300]}
 
 
-def _cold_start(args, timeout: float = 600.0) -> dict:
+def _cold_start(args) -> dict:
     """The task through ``dstack apply`` (bench_apply.py) and the control-plane-only cold start
-    (bench_coldstart.py)."""
+    (bench_coldstart.py).  ``--coldstart-fake-gpus`` (CPU tests): the agents see that many fake
+    MI355X and the task's ranks run on the CPU over gloo."""
     model_args = (f"--model {args.model} --seq-len {args.seq_len} --micro-batch {args.micro_batch} "
                   f"--grad-accum {args.grad_accum}")
-    apply = _child_json(["bench_apply.py", "--gpus", str(args.gpus), "--runs", "3", "--steps", "1", "--warmup", "1",
-                         "--tok-steps", "5", "--tok-warmup", "2", "--extra-args", model_args], timeout)
+    cmd = ["bench_apply.py", "--gpus", str(args.gpus), "--runs", "3", "--steps", "1", "--warmup", "1",
+           "--tok-steps", "5", "--tok-warmup", "2", "--extra-args", model_args,
+           "--timeout", str(args.coldstart_timeout)]
+    if args.coldstart_fake_gpus:
+        cmd += ["--fake-gpus", str(args.coldstart_fake_gpus)]
+    # 4 task runs, each bounded by --timeout inside; the child as a whole by 4x that
+    apply = _child_json(cmd, 4 * args.coldstart_timeout + 120)
     apply.pop("samples", None)
     cp = _child_json(["bench_coldstart.py", "--runs", "5", "--warm-runs", "4"], 180.0)
     apply["control_plane"] = {k: cp.get(k) for k in ("cold_start_p50_s", "stages_p50_s", "warm_start_p50_s",
                                                       "fresh_ok", "fresh_runs", "error") if cp.get(k) is not None}
     return apply
+
+
+def _merge_cold(out: dict, cold: dict | None) -> dict:
+    """Submit -> first optimizer step of the example task applied through the server, p50 over
+    fresh instances, and the task's own tokens/s, next to the in-process number."""
+    if cold is None:
+        return out
+    out["cold_start_p50_s"] = cold.get("time_to_first_step_p50_s")
+    out["job_tokens_per_s"] = cold.get("job_tokens_per_s")
+    out["cold_start"] = {k: cold.get(k) for k in ("time_to_train_start_p50_s", "time_to_first_log_p50_s",
+                                                  "stages_p50_s", "runs", "distinct_instances",
+                                                  "gpu_requested", "job_ms_per_step", "job_steps",
+                                                  "job_n_gpus", "excludes", "errors", "error",
+                                                  "control_plane", "when")
+                         if cold.get(k) not in (None, [])}
+    return out
 
 
 def _free_port() -> int:
@@ -76,26 +106,30 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _self_launch(n: int, argv: list) -> int:
+def _self_launch(n: int, argv: list, cold: dict | None) -> int:
     """``bench.py --gpus N`` (N>1) started without a launcher: run N ranks under
     ``torch.distributed.run`` as a CHILD process (nothing here has touched the GPU, and no exec
-    replaces this process), forward its output, and return its exit code.  Rank 0's JSON line must
-    report ``n_gpus == N``; anything else is an error, never a silent 1-GPU number."""
+    replaces this process), forward its output, and return its exit code.  The cold start has
+    already run in this process, before any rank existed; it is merged into rank 0's JSON line
+    here.  That line must report ``n_gpus == N``; anything else is an error, never a silent 1-GPU
+    number."""
     import subprocess
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv,
+           "--no-coldstart"]
     env = dict(os.environ, DSTACK_AMD_BENCH_CHILD="1")
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
     result = None
     for line in proc.stdout:
-        sys.stdout.write(line)
-        sys.stdout.flush()
         if line.startswith("{"):
             try:
                 result = json.loads(line)
+                continue  # printed once, with the cold start merged in, after the ranks exit
             except ValueError:
                 pass
+        sys.stdout.write(line)
+        sys.stdout.flush()
     rc = proc.wait()
     if rc != 0:
         return rc
@@ -103,7 +137,26 @@ def _self_launch(n: int, argv: list) -> int:
         print(f"error: expected a result line with n_gpus={n}, got {result and result.get('n_gpus')}",
               file=sys.stderr)
         return 3
+    print(json.dumps(_merge_cold(result, cold)), flush=True)
     return 0
+
+
+def _release_gpu() -> None:
+    """Every rank drops its model, optimizer and cached HBM blocks and leaves the process group
+    (RCCL communicators included), so nothing of the benchmark competes with the cold-start task
+    and no collective or watchdog waits while rank 0 measures it."""
+    import gc
+
+    import torch
+    import torch.distributed as dist
+
+    gc.collect()  # (the caller has dropped its trainer; its hooks form reference cycles)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
@@ -122,18 +175,22 @@ def main():
     # 4 -> 21.49k, 8 -> 21.81k (profiles/ab_r2l_grad_accum.txt)
     ap.add_argument("--grad-accum", type=int, default=8)
     ap.add_argument("--no-coldstart", action="store_true", help="skip the dstack-apply cold-start half")
+    ap.add_argument("--coldstart-timeout", type=float, default=600.0, help="time limit of one applied task run")
+    ap.add_argument("--coldstart-fake-gpus", type=int, default=0, help=argparse.SUPPRESS)  # CPU tests
     args = ap.parse_args()
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(_self_launch(args.gpus, sys.argv[1:]))
+    launched = "WORLD_SIZE" in os.environ
+    cold = None
+    if not launched:
+        # no rank exists and nothing in this process has touched the GPU: the cold start runs now
+        if not args.no_coldstart:
+            cold = dict(_cold_start(args), when="before the benchmark's ranks started")
+        if args.gpus > 1:
+            sys.exit(_self_launch(args.gpus, sys.argv[1:], cold))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required", file=sys.stderr)
         sys.exit(2)
-
-    cold = None
-    if not args.no_coldstart and int(os.environ.get("RANK", "0")) == 0:
-        cold = _cold_start(args)
 
     from dstack_amd.workloads.train_llama import run
 
@@ -142,9 +199,10 @@ def main():
     if env.world != args.gpus:
         print(f"error: joined a group of {env.world} ranks, --gpus {args.gpus}", file=sys.stderr)
         sys.exit(2)
-    if env.rank == 0:
-        import torch
+    import torch
 
+    out = None
+    if env.rank == 0:
         out = {
             "metric": METRIC,
             "value": round(res["tokens_per_s"], 2),
@@ -178,22 +236,14 @@ def main():
             "attn": os.environ.get("DSTACK_AMD_ATTN", "hip"),
             "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu",
         }
-        if cold is not None:
-            # submit -> first optimizer step of the example task applied through the server, p50
-            # over fresh instances; the task's own tokens/s next to the in-process number
-            out["cold_start_p50_s"] = cold.get("time_to_first_step_p50_s")
-            out["job_tokens_per_s"] = cold.get("job_tokens_per_s")
-            out["cold_start"] = {k: cold.get(k) for k in ("time_to_train_start_p50_s", "time_to_first_log_p50_s",
-                                                          "stages_p50_s", "runs", "distinct_instances",
-                                                          "gpu_requested", "job_ms_per_step", "job_steps",
-                                                          "job_n_gpus", "excludes", "errors", "error",
-                                                          "control_plane")
-                                 if cold.get(k) not in (None, [])}
-        print(json.dumps(out), flush=True)
-    import torch.distributed as dist
-
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    del tr
+    _release_gpu()
+    if env.rank != 0:
+        return
+    if launched and not args.no_coldstart:
+        # external launcher: the other ranks have left; the applied task gets the whole node
+        cold = dict(_cold_start(args), when="after the timed steps; benchmark ranks released their GPUs")
+    print(json.dumps(_merge_cold(out, cold)), flush=True)
 
 
 if __name__ == "__main__":

@@ -15,6 +15,7 @@ import time
 _T_IMPORT = time.time()  # before torch: the stage split below starts here
 
 import argparse  # noqa: E402
+import datetime  # noqa: E402
 import json  # noqa: E402
 import os  # noqa: E402
 import shutil  # noqa: E402
@@ -71,7 +72,10 @@ def init_distributed(backend: str | None = None) -> DistEnv:
     if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"  # "nccl" is RCCL on ROCm
-        kwargs = {}
+        # an explicit collective timeout (torch's default is 10 min): a slow first step on a cold
+        # node, a checkpoint save on a shared volume or rank 0 writing results must not trip the
+        # watchdog, while a truly hung peer still fails the job instead of holding the GPUs forever
+        kwargs = {"timeout": datetime.timedelta(seconds=float(os.environ.get("DSTACK_AMD_PG_TIMEOUT_S", "1800")))}
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", local_rank)
         if world == 1 and "MASTER_ADDR" not in os.environ:

@@ -70,3 +70,57 @@ def test_bench_world_size_mismatch_is_an_error():
     assert r.returncode == 2
     assert not _json_lines(r.stdout)
     assert "WORLD_SIZE=1" in r.stderr
+
+
+def _cold_args():
+    return [a for a in ARGS if a != "--no-coldstart"] + ["--coldstart-fake-gpus", "2", "--coldstart-timeout", "240"]
+
+
+def _check_cold(d, n):
+    assert d["n_gpus"] == n and d["config"]["parallelism"] == f"dp{n}-zero1"
+    c = d["cold_start"]
+    assert c["job_n_gpus"] == n and c["runs"] == 3 and c["gpu_requested"] == f"MI355X:{n}", c
+    assert not c.get("errors"), c
+    assert d["cold_start_p50_s"] > 0 and d["job_tokens_per_s"] > 0
+    return c
+
+
+def _skip_without_agents():
+    from dstack_amd.native_bin import runner_path, shim_path
+
+    if not (shim_path() and runner_path()):
+        pytest.skip("native agents not built")
+    from dstack_amd.ops.build import is_current
+
+    if not is_current():
+        pytest.skip("HIP extension not built for the current sources (the example's build step would compile)")
+
+
+@pytest.mark.slow
+def test_bench_self_launched_runs_cold_start_before_ranks_exist():
+    """The driver's N>1 command without a launcher: the parent measures ``dstack apply`` of the
+    example with ``MI355X:2`` (fake GPUs, gloo ranks) BEFORE it starts the benchmark's ranks, then
+    merges that into rank 0's single JSON line."""
+    _skip_without_agents()
+    env = {k: v for k, v in _env().items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *_cold_args()], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    assert _check_cold(lines[0], 2)["when"].startswith("before")
+
+
+@pytest.mark.slow
+def test_bench_under_launcher_runs_cold_start_after_ranks_release():
+    """The driver's exact N>1 form (``torch.distributed.run ... bench.py --gpus 2``, no
+    ``--no-coldstart``): rank 0 runs the cold start only after the timed steps, once both ranks
+    have dropped the trainer and left the process group; rank 1 exits, one JSON line."""
+    _skip_without_agents()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29537", "bench.py", "--gpus", "2", *_cold_args()]
+    r = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    assert _check_cold(lines[0], 2)["when"].startswith("after")
