@@ -35,7 +35,7 @@ from dstack_amd.core.models.instances import (
 from dstack_amd.core.models.runs import Job, JobProvisioningData, Requirements, Run
 from dstack_amd.core.models.volumes import Volume, VolumeProvisioningData
 
-DEFAULT_ROCM_IMAGE = "rocm/pytorch:rocm6.4_ubuntu22.04_py3.10_pytorch_release_2.6.0"
+from dstack_amd.core.models.images import DEFAULT_ROCM_IMAGE  # noqa: E402 - one gfx950-capable image
 
 
 def _job_image(job: Job) -> str:

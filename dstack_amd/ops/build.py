@@ -10,6 +10,7 @@ mtimes is not rebuilt needlessly and an edited source is never missed.
     python -m dstack_amd.ops.build            # build
     python -m dstack_amd.ops.build --asm      # also keep .s (register/occupancy audit)
     python -m dstack_amd.ops.build --check    # exit 1 unless the .so matches the current sources
+    python -m dstack_amd.ops.build --check-toolchain   # hipcc present and able to target gfx950
 """
 
 from __future__ import annotations
@@ -156,12 +157,46 @@ def _quick_current() -> bool:
         return False
 
 
+_PROBE_SRC = "#include <hip/hip_runtime.h>\n__global__ void k(float* p) { p[threadIdx.x] = 1.f; }\n"
+
+
+def check_toolchain() -> str:
+    """hipcc must exist and target gfx950 (ROCm >= 7.0).  Returns the HIP version line; raises a
+    RuntimeError that says what is wrong and what to use instead -- the typical failure is a ROCm 6.x
+    container image on an MI350X/MI355X host, whose compiler has no gfx950 target."""
+    from dstack_amd.core.models.images import DEFAULT_ROCM_IMAGE
+
+    if not Path(HIPCC).exists():
+        raise RuntimeError(f"hipcc not found at {HIPCC}: the HIP kernels need ROCm >= 7.0 for {ARCH} "
+                           f"(set HIPCC, or run in {DEFAULT_ROCM_IMAGE})")
+    ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout
+    line = next((x for x in ver.splitlines() if "HIP version" in x), "HIP version: unknown")
+    import tempfile
+
+    with tempfile.TemporaryDirectory(prefix="dsa_hipcc_") as td:  # (hipcc does not read stdin)
+        src = Path(td) / "probe.hip"
+        src.write_text(_PROBE_SRC)
+        r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-c", str(src), "-o", str(Path(td) / "probe.o")],
+                           capture_output=True, text=True)
+    if r.returncode != 0:
+        rocm = ""
+        info = Path(HIPCC).resolve().parent.parent / ".info" / "version"
+        if info.exists():
+            rocm = f" (ROCm {info.read_text().strip()})"
+        raise RuntimeError(f"{HIPCC}{rocm}, {line.strip()}: cannot compile for --offload-arch={ARCH}; "
+                           f"MI350X/MI355X (gfx950) need ROCm >= 7.0 -- use {DEFAULT_ROCM_IMAGE}.\n"
+                           f"{r.stderr.strip()[-600:]}")
+    return line.strip()
+
+
 def build(verbose: bool = False, keep_asm: bool = False, force: bool = False) -> Path:
     if not force and not keep_asm and _quick_current():
         return so_path()  # nothing changed since the recorded build (no torch import needed)
     BUILD.mkdir(parents=True, exist_ok=True)
     units, link, so_digest = _plan(keep_asm)
     jobs = [(obj, cmd, d) for obj, cmd, d in units if force or _stale(obj, d)]
+    if jobs:
+        check_toolchain()  # a clear message instead of a wall of clang errors
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         for (obj, _, d), out in zip(jobs, ex.map(lambda j: _run(j[1]), jobs)):
             _stamp(obj, d)
@@ -232,12 +267,24 @@ def main():
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", action="store_true")
     ap.add_argument("--check", action="store_true", help="exit 1 unless the .so matches the current sources")
+    ap.add_argument("--check-toolchain", action="store_true", help="only check that hipcc targets gfx950")
     a = ap.parse_args()
+    if a.check_toolchain:
+        try:
+            print(f"{HIPCC}: {check_toolchain()}, --offload-arch={ARCH} ok")
+        except RuntimeError as e:
+            print(f"error: {e}", file=sys.stderr)
+            sys.exit(1)
+        return
     if a.check:
         ok = is_current()
         print(f"{so_path()}: {'current' if ok else 'STALE or missing'}")
         sys.exit(0 if ok else 1)
-    print(build(verbose=a.v, keep_asm=a.asm, force=a.force))
+    try:
+        print(build(verbose=a.v, keep_asm=a.asm, force=a.force))
+    except RuntimeError as e:
+        print(f"error: {e}", file=sys.stderr)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

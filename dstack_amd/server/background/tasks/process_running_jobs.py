@@ -364,7 +364,12 @@ def _record_rccl_preflight(job: JobModel, doc: dict):
     job: its bus bandwidth joins the instance's health, and a failed pre-flight -- or a bus bandwidth
     under ``DSTACK_RCCL_MIN_BUSBW_GB_S`` (per-link xGMI ring bound ~153 GB/s x links in use) -- marks
     the host unhealthy, so ``filter_pool_instances`` stops placing jobs on it until the shim's next
-    health probe clears it.  The failing job itself already carries the probe's message."""
+    health probe clears it.  The failing job itself already carries the probe's message.
+
+    The floor applies to uncontended measurements only: a probe that ran CONCURRENTLY with the
+    job's start-up (the runner's default, ``"mode": "concurrent"`` in its document) shares the GPUs
+    and xGMI links with the job, so its bandwidth is recorded for information and never marks a
+    healthy host bad; an explicit probe failure (a rank hung, a wrong sum) still does."""
     import os
 
     from dstack_amd.core.models.instances import InstanceHealth
@@ -378,7 +383,8 @@ def _record_rccl_preflight(job: JobModel, doc: dict):
     healthy = bool(doc.get("healthy", True))
     message = doc.get("message") or ""
     floor = os.environ.get("DSTACK_RCCL_MIN_BUSBW_GB_S")
-    if healthy and floor and busbw is not None and float(busbw) < float(floor):
+    contended = doc.get("mode") == "concurrent"
+    if healthy and floor and busbw is not None and not contended and float(busbw) < float(floor):
         healthy = False
         message = f"RCCL bus bandwidth {float(busbw):.1f} GB/s below {float(floor):.1f} GB/s"
     upd = {"rccl_busbw_gb_s": busbw if busbw is not None else old.rccl_busbw_gb_s}

@@ -19,6 +19,7 @@ from sqlalchemy.orm import Session
 
 from dstack_amd.core.errors import BackendError, ComputeError, NoCapacityError, ServerClientError
 from dstack_amd.core.models.backends import BackendType
+from dstack_amd.core.models import images
 from dstack_amd.core.models.common import NetworkMode
 from dstack_amd.core.models.instances import InstanceOfferWithAvailability, InstanceStatus
 from dstack_amd.core.models.profiles import DEFAULT_RUN_TERMINATION_IDLE_TIME, CreationPolicy
@@ -101,8 +102,12 @@ def _process_job(s: Session, job_id):
     )
     offers = [(c, o) for c, o in offers if o.backend != BackendType.REMOTE]
     offers = job_volumes.filter_offers_by_volumes(offers, volumes)
+    n_before = len(offers)
+    offers = [(c, o) for c, o in offers if images.offer_supported(spec.image_name, o.instance.resources.gpus)]
     if not offers:
-        _no_capacity(job, "No offers match the requirements")
+        _no_capacity(job, "No offers match the requirements" if not n_before else
+                     f"No offers match the requirements: image {spec.image_name} names a ROCm too old for "
+                     f"the offered GPUs (MI350X/MI355X need ROCm >= 7.0)")
         return
     run_model = runs_services.run_model_to_run(run, include_jobs=False)
     job_obj = Job(job_spec=spec, job_submissions=[jobs_services.job_model_to_job_submission(job)])
@@ -174,7 +179,8 @@ def _assign_pool_instance(s: Session, run: RunModel, job: JobModel, spec, profil
     instances = pools_services.list_project_instances(s, run.project)
     cands = pools_services.filter_pool_instances(instances, profile, spec.requirements, fleet=fleet,
                                                  multinode=multinode, master_jpd=master_jpd)
-    cands = [(i, sh) for i, sh in cands if job_volumes.instance_matches_volumes(i, volumes)]
+    cands = [(i, sh) for i, sh in cands if job_volumes.instance_matches_volumes(i, volumes)
+             and images.offer_supported(spec.image_name, sh.instance.resources.gpus)]
     if not cands:
         return False
     ls = lockset("instances")

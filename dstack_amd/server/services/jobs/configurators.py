@@ -21,6 +21,7 @@ from dstack_amd.core.models.configurations import (
     ServiceConfiguration,
     TaskConfiguration,
 )
+from dstack_amd.core.models.images import DEFAULT_ROCM_IMAGE, check_requested_gpus
 from dstack_amd.core.models.profiles import DEFAULT_STOP_DURATION, ProfileRetry, RetryEvent, SpotPolicy
 from dstack_amd.core.models.resources import AcceleratorVendor
 from dstack_amd.core.models.runs import AppSpec, JobSpec, Requirements, Retry, RunSpec, get_policy_map
@@ -29,7 +30,7 @@ from dstack_amd.core.models.volumes import InstanceMountPoint, VolumeMountPoint
 from dstack_amd.utils.interpolator import InterpolatorError, VariablesInterpolator
 
 DEFAULT_MAX_DURATION_DEV = 6 * 3600
-DEFAULT_AMD_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.7.1"
+DEFAULT_AMD_IMAGE = DEFAULT_ROCM_IMAGE  # ROCm >= 7.0: gfx950 (MI350X/MI355X) support
 DEFAULT_CPU_IMAGE = "python:{python}-slim"
 
 
@@ -139,6 +140,12 @@ def get_job_specs_from_run_spec(run_spec: RunSpec, replica_num: int = 0,
             continue
         env[k] = it.interpolate(str(v), return_missing=True)[0]
     image = conf.image or get_default_image(conf)
+    # an image whose tag names a ROCm older than every requested GPU supports (ROCm 6.x for an
+    # MI355X-only run) can never run: rejected at submission with the image to use instead
+    gpu = conf.resources.gpu
+    bad = check_requested_gpus(image, gpu.name if gpu is not None and (gpu.count.max or 0) > 0 else None)
+    if bad:
+        raise ServerClientError(bad)
     user = UnixUser.parse(conf.user) if conf.user else None
     image_entrypoint = None
     if conf.image and (not _shell_commands(conf) or user is None) and conf.entrypoint is None:

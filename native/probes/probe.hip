@@ -205,7 +205,8 @@ static std::vector<std::vector<double>> xgmi_probe(int ndev, bool quick) {
 
 // rccl_probe.cpp
 std::string rccl_allreduce_probe_mp(int gpus_per_node, int nodes, int node_rank, const std::string& master, int port,
-                                    bool quick, int timeout_ms, double* best_busbw, int* world_out, std::string* err);
+                                    bool quick, int timeout_ms, double* best_busbw, int* world_out, std::string* err,
+                                    int max_mib);
 
 
 // Per-SKU baselines: what THIS probe measures on a healthy part (not the datasheet peaks), so a
@@ -232,6 +233,7 @@ int main(int argc, char** argv) {
   double min_hbm = -1, min_mfma = -1;  // absolute overrides; default: min_fraction x per-SKU baseline
   double min_fraction = 0.8;
   int rccl_nodes = 1, node_rank = 0, master_port = 29600, gpus_per_node = 0;
+  int rccl_max_mib = 0;  // 0: the full sweep
   int rccl_timeout_ms = 300000;  // per-rank bootstrap + sweep budget (the runner derives it from its own limit)
   std::string master = "127.0.0.1";
   for (int i = 1; i < argc; ++i) {
@@ -251,6 +253,7 @@ int main(int argc, char** argv) {
     else if (a == "--master" && i + 1 < argc) master = argv[++i];
     else if (a == "--master-port" && i + 1 < argc) master_port = atoi(argv[++i]);
     else if (a == "--gpus-per-node" && i + 1 < argc) gpus_per_node = atoi(argv[++i]);
+    else if (a == "--max-mib" && i + 1 < argc) rccl_max_mib = atoi(argv[++i]);
     else if (a == "--timeout-ms" && i + 1 < argc) {
       const int t = atoi(argv[++i]);
       if (t > 0) rccl_timeout_ms = t;
@@ -260,7 +263,7 @@ int main(int argc, char** argv) {
               "usage: dstack-probe [--quick] [--json] [--hbm] [--mfma] [--xgmi] [--rccl] [--device N]\n"
               "                    [--min-fraction F | --min-hbm-tbs X --min-mfma-tflops Y]\n"
               "                    [--rccl [--gpus-per-node G] --nodes N --node-rank R --master HOST --master-port P\n"
-              "                     [--timeout-ms T]]\n");
+              "                     [--timeout-ms T] [--max-mib M]]\n");
       return 2;
     }
   }
@@ -275,7 +278,7 @@ int main(int argc, char** argv) {
       double best = 0;
       int world = 0;
       std::string sweep = rccl_allreduce_probe_mp(g, rccl_nodes, node_rank, master, master_port, quick,
-                                                  rccl_timeout_ms, &best, &world, &rccl_err);
+                                                  rccl_timeout_ms, &best, &world, &rccl_err, rccl_max_mib);
       char b[256];
       snprintf(b, sizeof b, "\"rccl_world\": %d, \"rccl_gpus_per_node\": %d, \"rccl\": ", world, g);
       rccl_json = b + sweep + ", ";

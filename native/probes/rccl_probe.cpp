@@ -39,12 +39,14 @@
 // TCP store, not ncclCommInitAll's or a group-initialised single-process shortcut.
 //
 // Each rank first checks the sum of an fp32 all-reduce (every rank contributes rank+1), then times
-// an in-place bf16 sum sweep (1 MiB .. 1 GiB, 256 MiB with --quick) on its own stream.  The parent
+// an in-place bf16 sum sweep (1 MiB .. 1 GiB, 256 MiB with --quick, at most --max-mib: the
+// runner's concurrent pre-flight caps it so the probe takes little HBM and link time beside a
+// starting job) on its own stream.  The parent
 // takes, per size, the slowest local rank: algbw = bytes / time, busbw = algbw * 2(W-1)/W
 // (ring-bound; compare with one xGMI link, ~153 GB/s, intra-node).  At W == 1 RCCL moves no data
 // between GPUs, so the sweep is reported with busbw null: it proves the bootstrap and the
 // communicator, it is not a bandwidth measurement.
-static std::string rank_body(const dsa::RankCtx& c, const std::string& id_bytes, bool quick) {
+static std::string rank_body(const dsa::RankCtx& c, const std::string& id_bytes, bool quick, size_t cap_bytes) {
   ncclUniqueId id;
   memcpy(&id, id_bytes.data(), sizeof id);
   HCK(hipSetDevice(c.local));
@@ -66,6 +68,7 @@ static std::string rank_body(const dsa::RankCtx& c, const std::string& id_bytes,
   for (float v : h) ok = ok && v == want;
   HCK(hipFree(dchk));
   size_t max_bytes = (quick ? 256ull : 1024ull) << 20;
+  if (cap_bytes >= (1u << 20) && cap_bytes < max_bytes) max_bytes = cap_bytes;
   void* buf = nullptr;
   HCK(hipMalloc(&buf, max_bytes));
   HCK(hipMemset(buf, 0, max_bytes));
@@ -116,7 +119,9 @@ static std::vector<double> parse_times(const std::string& line) {
 }
 
 std::string rccl_allreduce_probe_mp(int gpus_per_node, int nodes, int node_rank, const std::string& master, int port,
-                                    bool quick, int timeout_ms, double* best_busbw, int* world_out, std::string* err) {
+                                    bool quick, int timeout_ms, double* best_busbw, int* world_out, std::string* err,
+                                    int max_mib) {
+  const size_t cap_bytes = max_mib > 0 ? (size_t)max_mib << 20 : 0;
   const int world = nodes * gpus_per_node;
   *world_out = world;
   *best_busbw = 0;
@@ -129,7 +134,8 @@ std::string rccl_allreduce_probe_mp(int gpus_per_node, int nodes, int node_rank,
         memcpy(&id[0], &u, sizeof u);
         return std::string();
       },
-      [quick](const dsa::RankCtx& c, const std::string& id) { return rank_body(c, id, quick); }, timeout_ms, &e);
+      [quick, cap_bytes](const dsa::RankCtx& c, const std::string& id) { return rank_body(c, id, quick, cap_bytes); },
+      timeout_ms, &e);
   std::vector<double> worst;  // per size: slowest local rank (us)
   for (auto& r : results) {
     if (r.line.find("\"sum_ok\": false") != std::string::npos && e.empty())

@@ -436,33 +436,59 @@ std::vector<std::pair<std::string, std::string>> Executor::build_env() const {
   return env;
 }
 
+// Every fork of the runner (run_cmd's helpers and the RCCL pre-flight thread, the job's forkpty)
+// happens under this lock, and every descriptor it creates is close-on-exec: the concurrent
+// pre-flight forks from another thread while the job is being started, and a pipe or pty end
+// inherited by the other child would hold that child's EOF open (the probe's output would never
+// end while the job runs, or the job's pty would outlive the job in the probe).
+static std::mutex g_fork_mu;
+
+// Child side, before exec: nothing but 0/1/2 crosses into the new program (async-signal-safe).
+static void close_inherited_fds() {
+  if (close_range(3, ~0U, 0) != 0)
+    for (int fd = 3; fd < 1024; ++fd) close(fd);
+}
+
+// Run argv to completion, collecting stdout+stderr.  `pgid_slot` (optional): the child becomes a
+// process-group leader and its pid is published there while it runs, so another thread can stop
+// the whole group (the concurrent pre-flight when its job ends first).
 static int run_cmd(const std::vector<std::string>& argv, const std::string& cwd, std::string* output,
-                   const std::vector<std::pair<std::string, std::string>>* env = nullptr) {
+                   const std::vector<std::pair<std::string, std::string>>* env = nullptr,
+                   std::atomic<int>* pgid_slot = nullptr) {
   std::vector<std::string> env_strs;
   if (env)
     for (auto& kv : *env) env_strs.push_back(kv.first + "=" + kv.second);
+  std::vector<char*> a, e;
+  for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
+  a.push_back(nullptr);
+  for (auto& s : env_strs) e.push_back(const_cast<char*>(s.c_str()));
+  e.push_back(nullptr);
   int pipefd[2];
-  if (pipe(pipefd) != 0) return -1;
-  pid_t pid = fork();
-  if (pid == 0) {
-    dup2(pipefd[1], 1);
-    dup2(pipefd[1], 2);
-    close(pipefd[0]);
-    close(pipefd[1]);
-    if (!cwd.empty() && chdir(cwd.c_str()) != 0) _exit(127);
-    std::vector<char*> a;
-    for (auto& s : argv) a.push_back(const_cast<char*>(s.c_str()));
-    a.push_back(nullptr);
-    if (env) {
-      std::vector<char*> e;
-      for (auto& s : env_strs) e.push_back(const_cast<char*>(s.c_str()));
-      e.push_back(nullptr);
-      execvpe(a[0], a.data(), e.data());
+  pid_t pid;
+  {
+    std::lock_guard<std::mutex> lk(g_fork_mu);
+    if (pipe2(pipefd, O_CLOEXEC) != 0) return -1;
+    pid = fork();
+    if (pid == 0) {
+      if (pgid_slot) setpgid(0, 0);
+      dup2(pipefd[1], 1);  // (dup2 clears close-on-exec on 1 and 2)
+      dup2(pipefd[1], 2);
+      close_inherited_fds();
+      if (!cwd.empty() && chdir(cwd.c_str()) != 0) _exit(127);
+      if (env) execvpe(a[0], a.data(), e.data());
+      execvp(a[0], a.data());
+      _exit(127);
     }
-    execvp(a[0], a.data());
-    _exit(127);
   }
   close(pipefd[1]);
+  if (pid < 0) {
+    close(pipefd[0]);
+    return -1;
+  }
+  if (pgid_slot) {
+    setpgid(pid, pid);  // (also in the child: whichever runs first, the group exists before a kill)
+    *pgid_slot = pid;
+  }
   char buf[4096];
   ssize_t n;
   while ((n = read(pipefd[0], buf, sizeof buf)) > 0)
@@ -470,6 +496,7 @@ static int run_cmd(const std::vector<std::string>& argv, const std::string& cwd,
   close(pipefd[0]);
   int st = 0;
   waitpid(pid, &st, 0);
+  if (pgid_slot) *pgid_slot = 0;
   return WIFEXITED(st) ? WEXITSTATUS(st) : -1;
 }
 
@@ -587,6 +614,27 @@ bool Executor::preflight_concurrent() const {
   return m != "blocking";
 }
 
+// The job ended (done, failed, stopped, or killed by max_duration) while the concurrent probe still
+// runs: its process group (timeout + probe + one process per GPU) is stopped -- SIGTERM, SIGKILL
+// after 5 s -- so the job's result is reported now, not after the probe's own limit.
+void Executor::stop_preflight() {
+  const int64_t deadline = now_millis() + 5000;
+  bool termed = false;
+  while (preflight_state_ == 1) {
+    const int pg = preflight_pgid_;
+    if (pg > 0) {
+      if (!termed) {
+        job_logs_.append("[dstack] RCCL pre-flight stopped: the job ended first\n");
+        kill(-pg, SIGTERM);
+        termed = true;
+      } else if (now_millis() > deadline) {
+        kill(-pg, SIGKILL);
+      }
+    }
+    usleep(20000);
+  }
+}
+
 bool Executor::run_rccl_preflight(std::string& msg) {
   if (opts_.probe_binary.empty() || !path_exists(opts_.probe_binary)) {
     job_logs_.append("[dstack] RCCL pre-flight skipped: no dstack-probe in this container\n");
@@ -604,8 +652,12 @@ bool Executor::run_rccl_preflight(std::string& msg) {
   int limit_s = atoi(get("DSTACK_RCCL_PREFLIGHT_TIMEOUT", "300").c_str());
   if (limit_s < 20) limit_s = 20;
   const int probe_ms = (limit_s - 15) * 1000 - 5000;  // run_ranks collects up to 5 s past its deadline
+  // concurrent mode: a capped sweep (default 1..64 MiB) so the probe holds little HBM and link
+  // time beside the starting job; blocking mode: the --quick sweep up to 256 MiB
+  const bool concurrent = preflight_concurrent();
+  const std::string max_mib = get("DSTACK_RCCL_PREFLIGHT_MAX_MIB", concurrent ? "64" : "0");
   std::vector<std::string> argv = {"timeout", "-k", "10", std::to_string(limit_s),
-                                   opts_.probe_binary, "--rccl", "--quick", "--json",
+                                   opts_.probe_binary, "--rccl", "--quick", "--json", "--max-mib", max_mib,
                                    "--timeout-ms", std::to_string(probe_ms),
                                    "--gpus-per-node", get("DSTACK_GPUS_PER_NODE", "0"),
                                    "--nodes", get("DSTACK_NODES_NUM", "1"), "--node-rank", get("DSTACK_NODE_RANK", "0"),
@@ -613,8 +665,9 @@ bool Executor::run_rccl_preflight(std::string& msg) {
                                    "--master-port", std::to_string(port)};
   std::string out;
   const int64_t t0 = now_millis();
-  int rc = run_cmd(argv, opts_.working_dir, &out, &env);
-  job_logs_.append("[dstack] RCCL pre-flight (" + std::to_string(now_millis() - t0) + " ms, exit " +
+  int rc = run_cmd(argv, opts_.working_dir, &out, &env, &preflight_pgid_);
+  job_logs_.append(std::string("[dstack] RCCL pre-flight") + (concurrent ? ", concurrent (" : " (") +
+                   std::to_string(now_millis() - t0) + " ms, exit " +
                    std::to_string(rc) + "): " + out + (out.empty() || out.back() != '\n' ? "\n" : ""));
   // the probe's document (last JSON line): the server records its busbw / verdict as the
   // instance's health, which the scheduler reads (an unhealthy host gets no new jobs)
@@ -629,8 +682,10 @@ bool Executor::run_rccl_preflight(std::string& msg) {
     try {
       Json d = Json::parse(doc);
       probe_msg = d["message"].str("");
+      // the server applies its bandwidth floor only to uncontended (blocking) measurements
+      d.set("mode", std::string(concurrent ? "concurrent" : "blocking"));
       std::lock_guard<std::mutex> lk(states_mu_);
-      preflight_json_ = doc;
+      preflight_json_ = d.dump();
     } catch (...) {
     }
   }
@@ -797,6 +852,7 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
   int pipefd[2] = {-1, -1};
   const char* no_pty = getenv("DSTACK_RUNNER_NO_PTY");
   pid_t pid = -1;
+  std::unique_lock<std::mutex> fork_lk(g_fork_mu);
   if (no_pty && *no_pty && *no_pty != '0')
     errno = ENOTSUP;
   else
@@ -804,9 +860,10 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
   if (pid < 0) {
     int pty_errno = errno;
     use_pty = false;
-    if (pipe(pipefd) != 0) {
+    if (pipe2(pipefd, O_CLOEXEC) != 0) {
       reason = "executor_error";
       msg = std::string("forkpty failed: ") + strerror(pty_errno) + "; pipe failed: " + strerror(errno);
+      fork_lk.unlock();
       return -1;
     }
     rlog("forkpty unavailable (%s): using a pipe", strerror(pty_errno));
@@ -814,6 +871,7 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
     if (pid < 0) {
       reason = "executor_error";
       msg = std::string("fork failed: ") + strerror(errno);
+      fork_lk.unlock();
       close(pipefd[0]);
       close(pipefd[1]);
       return -1;
@@ -832,6 +890,7 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
     }
   }
   if (pid == 0) {
+    close_inherited_fds();
     if (chdir(wd.c_str()) != 0) _exit(126);
     if (getuid() == 0 && uid >= 0) {
       if (gid >= 0 && setgid((gid_t)gid) != 0) _exit(126);
@@ -843,6 +902,8 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
     if (write(2, kMsg, sizeof kMsg - 1) < 0) _exit(127);
     _exit(127);
   }
+  if (use_pty) fcntl(master, F_SETFD, FD_CLOEXEC);  // before any other fork can copy it
+  fork_lk.unlock();
   child_pgid_ = pid;  // forkpty()/setsid() make the child a session (and process group) leader
   (void)use_pty;
   add_state("running");
@@ -850,6 +911,8 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
   int64_t max_duration = js["max_duration"].as_int(0);
   int64_t t0 = now_millis(), stop_at = 0;
   bool timed_out = false;
+  bool stopped_by_preflight = false;  // latched while the job runs: a probe failing after the job
+                                      // has exited does not rewrite the job's own result
   char buf[65536];
   int status = 0;
   bool exited = false;
@@ -892,6 +955,7 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
       rlog("RCCL pre-flight failed: stopping job");
       kill(-pid, SIGTERM);
       stop_at = now;
+      stopped_by_preflight = true;
     }
     if (stop_at > 0 && now - stop_at > 10000) kill(-pid, SIGKILL);  // killDelay (executor.go:74)
   }
@@ -918,7 +982,7 @@ int Executor::exec_job(std::string& reason, std::string& msg) {
     reason = "max_duration_exceeded";
     return code;
   }
-  if (preflight_state_ == 3) {
+  if (stopped_by_preflight) {
     reason = "executor_error";
     std::lock_guard<std::mutex> lk(states_mu_);
     msg = preflight_err_;
@@ -967,7 +1031,10 @@ void Executor::run_job_steps() {
     }
     std::string reason, msg;
     int code = exec_job(reason, msg);
-    if (preflight.joinable()) preflight.join();
+    if (preflight.joinable()) {
+      stop_preflight();
+      preflight.join();
+    }
     if (reason == "max_duration_exceeded" || reason == "terminated_by_user")
       add_state("terminated", reason, msg, code);
     else if (!reason.empty())

@@ -94,6 +94,7 @@ class Executor {
   bool wants_rccl_preflight() const;
   bool preflight_concurrent() const;
   bool run_rccl_preflight(std::string& msg);
+  void stop_preflight();
   int exec_job(std::string& reason, std::string& msg);
 
   RunnerOptions opts_;
@@ -112,6 +113,7 @@ class Executor {
   // concurrent pre-flight (DSTACK_RCCL_PREFLIGHT_MODE=concurrent, the default): 0 none, 1 running,
   // 2 passed, 3 failed (the job is stopped with preflight_err_, guarded by states_mu_)
   std::atomic<int> preflight_state_{0};
+  std::atomic<int> preflight_pgid_{0};  // the running probe's process group (0: none)
   std::string preflight_err_;
   mutable std::atomic<bool> pulled_after_finish_{false};
   std::mutex fin_mu_;

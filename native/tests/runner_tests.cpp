@@ -373,9 +373,47 @@ int main() {
     CHECK(r.logs.find("started") != std::string::npos);  // the job ran beside the probe...
     CHECK(r.logs.find("trained") == std::string::npos);  // ...and was stopped when it failed
     CHECK(now_millis() - t0 < 15000);
-    r = run_job(root + "/n0", body("0", "echo trained"), "", probe, &pull);
-    CHECK(r.state == "done" && r.logs.find("trained") != std::string::npos);
-    CHECK(pull["rccl_preflight"]["rccl_busbw_gb_s"].as_double(0) > 311.0);
+    // a healthy probe that ends while the job runs: its document is recorded (mode: concurrent,
+    // capped sweep), and its output reaches the log before the job ends -- the probe's pipe got its
+    // EOF although the job was forked beside it (close-on-exec pipes, forks serialised); repeated,
+    // since the fork race is a matter of timing
+    for (int rep = 0; rep < 4; ++rep) {
+      r = run_job(root + "/n0", body("0", "sleep 2; echo trained"), "", probe, &pull);
+      CHECK(r.state == "done" && r.logs.find("trained") != std::string::npos);
+      CHECK(pull["rccl_preflight"]["rccl_busbw_gb_s"].as_double(0) > 311.0);
+      CHECK(pull["rccl_preflight"]["mode"].str() == "concurrent");
+      const size_t pf = r.logs.find("[dstack] RCCL pre-flight, concurrent");
+      CHECK(pf != std::string::npos && pf < r.logs.find("trained"));
+    }
+  });
+
+  run("executor: a job that ends before the concurrent pre-flight is reported at once, probe stopped", [] {
+    // stub probe: records its argv, then fails after 4 s; the job is done in well under a second
+    std::string root = tmpdir();
+    std::string probe = root + "/probe.sh";
+    write_file(probe,
+               "#!/bin/sh\necho \"$@\" > " + root + "/probe_args\nsleep 4\n"
+               "echo '{\"healthy\": false, \"message\": \"RCCL: rank 3 timed out\"}'; exit 1\n",
+               0755);
+    Json b = job({"/bin/sh", "-c", "sleep 0.5; echo quick"});
+    Json js = b["job_spec"];
+    Json env = Json::object();
+    env.set("DSTACK_RCCL_PREFLIGHT", std::string("force"));
+    env.set("DSTACK_GPUS_PER_NODE", std::string("8"));
+    js.set("env", env);
+    b.set("job_spec", js);
+    Json pull;
+    const int64_t t0 = now_millis();
+    JobResult r = run_job(root + "/n", b, "", probe, &pull);
+    // the job's own result (done), not the probe's later failure, and without waiting for it
+    CHECK(r.state == "done" && r.reason == "done_by_runner");
+    CHECK(r.logs.find("quick") != std::string::npos);
+    CHECK(r.logs.find("RCCL pre-flight stopped: the job ended first") != std::string::npos);
+    CHECK(now_millis() - t0 < 3500);
+    CHECK(!pull["rccl_preflight"].is_object());  // a stopped probe records no health document
+    // the concurrent probe's sweep is capped
+    std::string args;
+    CHECK(read_file(root + "/probe_args", args) && args.find("--max-mib 64") != std::string::npos);
   });
 
   run("host_info: a failed amdgpu bootstrap (marker file) is reported as gpu_driver_error", [] {

@@ -308,17 +308,17 @@ def test_cli_apply_ps_logs(server, tmp_path):
     env = dict(os.environ, DSTACK_SERVER_URL=server.url, DSTACK_TOKEN=server.token,
                DSTACK_DIR=str(tmp_path / "home"), PYTHONPATH=REPO)
     dstack = [sys.executable, "-m", "dstack_amd"]
-    r = subprocess.run(dstack + ["apply", "-y"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
+    r = subprocess.run(dstack + ["apply", "-y"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "cli-says-e2e-cli" in r.stdout and "uploaded-data" in r.stdout
-    r = subprocess.run(dstack + ["ps", "-a"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=60)
+    r = subprocess.run(dstack + ["ps", "-a"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=180)
     assert "e2e-cli" in r.stdout
     r = subprocess.run(dstack + ["logs", "e2e-cli"], cwd=tmp_path, env=env, capture_output=True, text=True,
-                       timeout=60)
+                       timeout=180)
     assert "uploaded-data" in r.stdout
     (tmp_path / "fail.dstack.yml").write_text("type: task\nname: e2e-cli-fail\ncommands: [\"exit 5\"]\n")
     r = subprocess.run(dstack + ["apply", "-y", "-f", "fail.dstack.yml"], cwd=tmp_path, env=env, capture_output=True,
-                       text=True, timeout=120)
+                       text=True, timeout=300)
     assert r.returncode == 5, r.stdout + r.stderr
 
 
@@ -330,15 +330,15 @@ def test_cli_offer(server, tmp_path):
                DSTACK_DIR=str(tmp_path / "home"), PYTHONPATH=REPO)
     dstack = [sys.executable, "-m", "dstack_amd"]
     r = subprocess.run(dstack + ["offer", "--json", "-n", "5"], cwd=tmp_path, env=env, capture_output=True,
-                       text=True, timeout=120)
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     d = _json.loads(r.stdout)
     assert d["total_offers"] >= 1 and d["offers"][0]["backend"] == "local"
     r = subprocess.run(dstack + ["offer", "--cpu", "1..", "--on-demand"], cwd=tmp_path, env=env,
-                       capture_output=True, text=True, timeout=120)
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "BACKEND" in r.stdout and "offers shown" in r.stdout, r.stdout + r.stderr
     r = subprocess.run(dstack + ["offer", "--gpu", "MI355X:1024"], cwd=tmp_path, env=env, capture_output=True,
-                       text=True, timeout=120)
+                       text=True, timeout=300)
     assert r.returncode == 0 and "0 of 0 offers shown" in r.stdout, r.stdout + r.stderr
 
 

@@ -684,3 +684,26 @@ def test_rccl_preflight_failure_on_one_node_fails_the_replica(db):
         assert [i.name for i, _ in picked] == [good[0].name]
     # the job spec carried the opt-in to the runners
     assert all(r.submitted["job_spec"].env.get("DSTACK_RCCL_PREFLIGHT") == "1" for r in agents.runners.values())
+
+
+def test_rccl_preflight_bandwidth_floor_ignores_concurrent_measurements(monkeypatch):
+    """The DSTACK_RCCL_MIN_BUSBW_GB_S floor marks a host unhealthy only for a blocking
+    (uncontended) pre-flight; a concurrent probe shared the GPUs with the job's start-up, so its
+    low number is recorded but the host stays healthy.  A failed probe is unhealthy either way."""
+    from types import SimpleNamespace
+
+    monkeypatch.setenv("DSTACK_RCCL_MIN_BUSBW_GB_S", "200")
+
+    def rec(doc):
+        job = SimpleNamespace(instance=SimpleNamespace(health_data=None, health_status=None, name="h"))
+        prj._record_rccl_preflight(job, doc)
+        return json.loads(job.instance.health_data), job.instance.health_status
+
+    h, st = rec({"rccl_busbw_gb_s": 90.0, "healthy": True, "mode": "concurrent"})
+    assert h["healthy"] and h["rccl_busbw_gb_s"] == 90.0 and st is None
+    h, st = rec({"rccl_busbw_gb_s": 90.0, "healthy": True, "mode": "blocking"})
+    assert not h["healthy"] and "below 200.0" in st
+    h, st = rec({"rccl_busbw_gb_s": 90.0, "healthy": True})  # older runners: treated as blocking
+    assert not h["healthy"]
+    h, st = rec({"rccl_busbw_gb_s": None, "healthy": False, "message": "rank 3 timed out", "mode": "concurrent"})
+    assert not h["healthy"] and "rank 3 timed out" in st
