@@ -104,6 +104,10 @@ def prewarm(shapes, device):
                 torch.mm(a.zero_(), b.zero_().t())
                 del a, b
         st.synchronize()
+        # the caching allocator ties freed blocks to the stream that allocated them: released here,
+        # the side stream's operands (the LM-head pair alone is ~2 x 2 GiB at 8k tokens) would stay
+        # reserved for the whole run, unusable by the default stream's training step
+        torch.cuda.empty_cache()
 
     th = threading.Thread(target=work, name="gemm-prewarm", daemon=True)
     th.start()

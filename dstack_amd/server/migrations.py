@@ -33,6 +33,10 @@ from sqlalchemy import inspect, text
 
 from dstack_amd.server.models import Base
 
+
+class MigrationError(RuntimeError):
+    """An operation that cannot be applied safely to this database (nothing of it was applied)."""
+
 _lock = threading.Lock()
 
 
@@ -115,7 +119,13 @@ class drop_index(Op):
 
 class alter_column_type(Op):
     """``using``: SQL template over ``{col}`` (the quoted column) giving the new value, e.g.
-    ``CAST(trim({col}) AS INTEGER)``; default a plain CAST to ``new_type``."""
+    ``CAST(trim({col}) AS INTEGER)``; default a plain CAST to ``new_type``.
+
+    On SQLite (no ALTER COLUMN) the column is renamed aside, re-added and converted: its NOT NULL
+    and DEFAULT are carried over and its indexes re-created.  Refused there (a table rebuild through
+    ``run_python`` is needed instead): primary-key, foreign-key and inline-UNIQUE columns, and NOT
+    NULL columns without a DEFAULT (SQLite cannot add those).  CHECK constraints that name the
+    column are not carried over."""
 
     def __init__(self, table: str, column: str, new_type: str, using: Optional[str] = None):
         self.table, self.column, self.new_type = table, column, new_type
@@ -127,13 +137,29 @@ class alter_column_type(Op):
             conn.execute(text(f"ALTER TABLE {t} ALTER COLUMN {c} TYPE {self.new_type} "
                               f"USING {self.using.format(col=c)}"))
             return
-        # SQLite: aside, re-add, convert, drop -- indexes re-created on the new column
+        # SQLite: aside, re-add, convert, drop -- constraints carried, indexes re-created
+        info = {r[1]: r for r in conn.execute(text(f"PRAGMA table_info({t})")).fetchall()}
+        if self.column not in info:
+            raise MigrationError(f"{self.table}.{self.column}: no such column")
+        _, _, _, notnull, default, pk = info[self.column]
+        fks = [r for r in conn.execute(text(f"PRAGMA foreign_key_list({t})")).fetchall() if r[3] == self.column]
+        auto_unique = [ix for ix in conn.execute(text(f"PRAGMA index_list({t})")).fetchall()
+                       if ix[1].startswith("sqlite_autoindex_") and
+                       [r[2] for r in conn.execute(text(f"PRAGMA index_info({_q(ix[1])})")).fetchall()] == [self.column]]
+        if pk or fks or auto_unique:
+            what = "primary-key" if pk else "foreign-key" if fks else "UNIQUE"
+            raise MigrationError(f"{self.table}.{self.column}: alter_column_type cannot retype a {what} column on "
+                                 "SQLite; rebuild the table with run_python")
+        if notnull and default is None:
+            raise MigrationError(f"{self.table}.{self.column}: NOT NULL without DEFAULT cannot be re-added on "
+                                 "SQLite; rebuild the table with run_python")
+        decl = self.new_type + (" NOT NULL" if notnull else "") + (f" DEFAULT {default}" if default is not None else "")
         indexes = _indexes_on(conn, self.table, self.column)
         for ix in indexes:
             conn.execute(text(f"DROP INDEX {_q(ix['name'])}"))
         aside = _q(f"_old_{self.column}")
         conn.execute(text(f"ALTER TABLE {t} RENAME COLUMN {c} TO {aside}"))
-        conn.execute(text(f"ALTER TABLE {t} ADD COLUMN {c} {self.new_type}"))
+        conn.execute(text(f"ALTER TABLE {t} ADD COLUMN {c} {decl}"))
         conn.execute(text(f"UPDATE {t} SET {c} = {self.using.format(col=aside)}"))
         conn.execute(text(f"ALTER TABLE {t} DROP COLUMN {aside}"))
         for ix in indexes:

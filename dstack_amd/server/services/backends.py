@@ -111,7 +111,7 @@ def get_project_backend(s: Session, project: ProjectModel, backend_type: Backend
 def create_backend(s: Session, project: ProjectModel, config: dict) -> BackendModel:
     """Validate ``config`` against the backend's model (``core/models/backend_configs.py``) and
     store it: plain settings in ``config``, credentials in the encrypted ``auth`` column."""
-    btype = _configurable_type(config)
+    btype = configurable_type(config)
     existing = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
                                                     BackendModel.type == btype.value)).scalar_one_or_none()
     if existing is not None:
@@ -129,7 +129,7 @@ def create_backend(s: Session, project: ProjectModel, config: dict) -> BackendMo
 
 def update_backend(s: Session, project: ProjectModel, config: dict) -> BackendModel:
     """Replace a backend's settings; credentials omitted from ``config`` keep their stored value."""
-    btype = _configurable_type(config)
+    btype = configurable_type(config)
     row = s.execute(select(BackendModel).where(BackendModel.project_id == project.id,
                                                BackendModel.type == btype.value)).scalar_one_or_none()
     if row is None:
@@ -224,7 +224,7 @@ def prepare_backend_resources(btype: BackendType, cfg: dict, secrets: dict) -> d
         return cfg
 
 
-def _configurable_type(config: dict) -> BackendType:
+def configurable_type(config: dict) -> BackendType:
     try:
         btype = BackendType(config.get("type"))
     except ValueError:
@@ -265,7 +265,7 @@ def backend_config_values(body: dict) -> dict:
     configurators do before offering regions."""
     from dstack_amd.core.backends.catalog import offline_rows
 
-    btype = _configurable_type(body)
+    btype = configurable_type(body)
     if body.get("creds") is not None:
         try:
             _, cfg, secrets = split_backend_config(body)

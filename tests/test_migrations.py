@@ -161,3 +161,29 @@ def test_real_chain_upgrades_a_database_written_before_its_later_steps(tmp_path)
         assert "ix_job_metrics_points_job_ts" in {i["name"] for i in insp.get_indexes("job_metrics_points")}
         row = c.execute(text("SELECT job_id, gpus_util_percent, gpus_extra FROM job_metrics_points")).one()
         assert tuple(row) == ("j1", "[97.0]", None)
+
+
+def test_sqlite_retype_keeps_not_null_and_default_and_refuses_key_columns(tmp_path):
+    """SQLite's rename-aside retype carries NOT NULL and DEFAULT over (a row inserted afterwards
+    without the column still gets the default, a NULL is still refused) and refuses primary-key,
+    foreign-key, inline-UNIQUE and NOT-NULL-without-default columns instead of silently dropping
+    their constraints."""
+    db = Database(f"sqlite:///{tmp_path}/c.db")
+    with db.engine.begin() as c:
+        c.execute(text("CREATE TABLE parents (id INTEGER PRIMARY KEY)"))
+        c.execute(text("CREATE TABLE kids (id INTEGER PRIMARY KEY, n TEXT NOT NULL DEFAULT '7', "
+                       "p INTEGER REFERENCES parents(id), code TEXT UNIQUE, req TEXT NOT NULL)"))
+        c.execute(text("INSERT INTO parents (id) VALUES (1)"))
+        c.execute(text("INSERT INTO kids (id, n, p, code, req) VALUES (1, ' 42 ', 1, 'a', 'x')"))
+        m.alter_column_type("kids", "n", "INTEGER", using="CAST(trim({col}) AS INTEGER)").apply(c)
+        cols = {r[1]: r for r in c.execute(text("PRAGMA table_info(kids)")).fetchall()}
+        assert cols["n"][2] == "INTEGER" and cols["n"][3] == 1 and cols["n"][4] == "'7'"
+        assert c.execute(text("SELECT n FROM kids WHERE id = 1")).scalar() == 42
+        c.execute(text("INSERT INTO kids (id, req) VALUES (2, 'y')"))
+        assert c.execute(text("SELECT n FROM kids WHERE id = 2")).scalar() == 7
+        for col, what in (("id", "primary-key"), ("p", "foreign-key"), ("code", "UNIQUE"),
+                          ("req", "NOT NULL without DEFAULT")):
+            with pytest.raises(m.MigrationError, match=what):
+                m.alter_column_type("kids", col, "INTEGER").apply(c)
+    with db.engine.begin() as c, pytest.raises(Exception):
+        c.execute(text("INSERT INTO kids (id, n, req) VALUES (3, NULL, 'z')"))  # NOT NULL kept

@@ -288,3 +288,85 @@ def test_attach_retries_until_the_container_sshd_is_up(tmp_path, monkeypatch):
     b = attach.RunAttach(run, sub, identity_file=str(tmp_path / "id"))
     with pytest.raises(SSHError, match="Connection refused"):
         b.open()
+
+
+def _apply(m, path, cfg):
+    path.write_text(yaml.safe_dump(cfg))
+    m.load_config()
+    with session_scope() as s:
+        m.apply_config(s, s.query(UserModel).filter_by(name="admin").one())
+
+
+def _backend_types(name):
+    with session_scope() as s:
+        project = s.query(ProjectModel).filter_by(name=name).one()
+        return sorted(b.type for b in s.query(BackendModel).filter_by(project_id=project.id).all())
+
+
+def test_server_config_deletes_unlisted_skips_unchanged_and_survives_a_bad_backend(db, tmp_path, keys, monkeypatch):
+    """Reference ``services/config.py:560-616``: a backend dropped from config.yml is deleted, an
+    unchanged one is not re-validated or rewritten, and one invalid backend is logged and skipped
+    while the valid ones next to it are configured."""
+    from dstack_amd.server.services import backends as backends_services
+    from dstack_amd.server.services.config import ServerConfigManager
+
+    checks = []
+    real = backends_services.validate_credentials
+    monkeypatch.setattr(backends_services, "validate_credentials",
+                        lambda btype, cfg, secrets: (checks.append(btype.value), real(btype, cfg, secrets)))
+    vultr = {"type": "vultr", "creds": {"type": "api_key", "api_key": "VULTR-KEY"}}
+    runpod = {"type": "runpod", "creds": {"type": "api_key", "api_key": "RP-KEY"}}
+    path = tmp_path / "config.yml"
+    m = ServerConfigManager(path)
+    _apply(m, path, {"projects": [{"name": "team", "backends": [vultr, runpod]}]})
+    assert _backend_types("team") == ["runpod", "vultr"] and sorted(checks) == ["runpod", "vultr"]
+    # the same file again: nothing is re-validated (no cloud round-trip per restart) or rewritten
+    checks.clear()
+    _apply(m, path, {"projects": [{"name": "team", "backends": [vultr, runpod]}]})
+    assert checks == []
+    # a changed credential is applied; the unchanged backend is still skipped
+    vultr2 = {"type": "vultr", "creds": {"type": "api_key", "api_key": "VULTR-KEY-2"}}
+    _apply(m, path, {"projects": [{"name": "team", "backends": [vultr2, runpod]}]})
+    assert checks == ["vultr"]
+    # runpod removed from the file -> deleted; an invalid aws entry and an unknown type are skipped
+    bad = [{"type": "aws", "creds": {"type": "access_key"}}, {"type": "no-such-cloud"}]
+    _apply(m, path, {"projects": [{"name": "team", "backends": [vultr2, *bad]}]})
+    assert _backend_types("team") == ["vultr"]
+    with session_scope() as s:
+        project = s.query(ProjectModel).filter_by(name="team").one()
+        (b,) = s.query(BackendModel).filter_by(project_id=project.id).all()
+        assert json.loads(b.auth)["api_key"] == "VULTR-KEY-2"
+
+
+def test_server_config_keeps_unlisted_backend_with_live_instances(db, tmp_path, keys):
+    from dstack_amd.core.models.instances import InstanceStatus
+    from dstack_amd.server.services import pools as pools_services
+    from dstack_amd.server.services.config import ServerConfigManager
+
+    vultr = {"type": "vultr", "creds": {"type": "api_key", "api_key": "VULTR-KEY"}}
+    path = tmp_path / "config.yml"
+    m = ServerConfigManager(path)
+    _apply(m, path, {"projects": [{"name": "team", "backends": [vultr]}]})
+    with session_scope() as s:
+        project = s.query(ProjectModel).filter_by(name="team").one()
+        pool = pools_services.get_or_create_default_pool(s, project)
+        inst = pools_services.create_instance_model(s, project, pool, "vm-1", InstanceStatus.IDLE)
+        inst.backend = "vultr"
+    _apply(m, path, {"projects": [{"name": "team", "backends": []}]})
+    assert _backend_types("team") == ["vultr"]  # logged and kept until its instance is gone
+
+
+def test_server_starts_with_one_invalid_backend_in_config(db, tmp_path, keys, monkeypatch):
+    """``init_server_state`` with a config.yml holding an invalid backend next to a valid one: the
+    server starts and the valid backend is configured (the reference logs and continues)."""
+    from dstack_amd.server import settings
+    from dstack_amd.server.app import init_server_state
+
+    path = tmp_path / "config.yml"
+    path.write_text(yaml.safe_dump({"projects": [{"name": "main", "backends": [
+        {"type": "aws", "creds": {"type": "access_key", "access_key": "AKIA"}},  # no secret_key
+        {"type": "vultr", "creds": {"type": "api_key", "api_key": "VULTR-KEY"}}]}]}))
+    monkeypatch.setattr(settings, "SERVER_CONFIG_FILE_PATH", str(path))
+    monkeypatch.setattr(settings, "SERVER_CONFIG_DISABLED", False)
+    assert init_server_state()
+    assert _backend_types("main") == ["vultr"]
