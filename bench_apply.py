@@ -71,7 +71,7 @@ def _free_port_pair() -> int:
     return 29611
 
 
-def task_conf(gpus: int, steps: int, warmup: int, extra_args: str, use_gpu: bool, name: str):
+def task_conf(gpus: int, steps: int, warmup: int, extra_args: str, use_gpu: bool, name: str, env=()):
     """The example task, as ``dstack apply`` would submit it, run from this checkout."""
     import yaml
 
@@ -93,6 +93,9 @@ def task_conf(gpus: int, steps: int, warmup: int, extra_args: str, use_gpu: bool
     # 29500 may be the outer job's store, and the RCCL pre-flight takes the next port too
     conf["env"] = list(conf.get("env", [])) + [f"PYTHONPATH={REPO}", "OMP_NUM_THREADS=1",
                                                f"MASTER_PORT={_free_port_pair()}"]
+    if env:  # --env overrides (e.g. DSTACK_RCCL_PREFLIGHT=force|0 for the pre-flight A/B)
+        keys = {e.split("=", 1)[0] for e in env}
+        conf["env"] = [e for e in conf["env"] if e.split("=", 1)[0] not in keys] + list(env)
     return parse_run_configuration(conf)
 
 
@@ -134,13 +137,16 @@ def one_run(client, conf, timeout: float) -> dict:
         out["time_to_train_start_s"] = round(stamps["model_ready"] - stamps["submitted"], 4)
     if "first_log" in timings:
         out["time_to_first_log_s"] = round(timings["first_log"] - timings["submitted"], 4)
+    pf = next((ln for ln in logs.splitlines() if ln.startswith("[dstack] RCCL pre-flight")), None)
+    if pf:  # the runner's own line: mode, duration and exit of the probe
+        out["preflight"] = pf[:200]
     if stages is None or (result is None and out["status"] != "done"):
         out["log_tail"] = logs[-2000:]
     return out
 
 
 def measure(gpus: int = 1, runs: int = 3, steps: int = 1, warmup: int = 1, tok_steps: int = 5, tok_warmup: int = 2,
-            extra_args: str = "", timeout: float = 600.0, gpu: str = "auto", fake_gpus: int = 0) -> dict:
+            extra_args: str = "", timeout: float = 600.0, gpu: str = "auto", fake_gpus: int = 0, env=()) -> dict:
     """``fake_gpus`` > 0 (CPU tests): the agents see that many MI355X in a fake sysfs/KFD tree and
     the task's ranks run on the CPU over gloo."""
     for k in _LAUNCHER_ENV:
@@ -166,7 +172,7 @@ def measure(gpus: int = 1, runs: int = 3, steps: int = 1, warmup: int = 1, tok_s
                 errors.append(f"run {i}: previous instance still active")
             tok_run = i == runs
             conf = task_conf(gpus, tok_steps if tok_run else steps, tok_warmup if tok_run else warmup, extra_args,
-                             use_gpu, f"llama3-apply-{i}")
+                             use_gpu, f"llama3-apply-{i}", env)
             s = one_run(client, conf, timeout)
             s["kind"] = "tokens" if tok_run else "cold"
             samples.append(s)
@@ -191,6 +197,28 @@ def measure(gpus: int = 1, runs: int = 3, steps: int = 1, warmup: int = 1, tok_s
     }
 
 
+def _interleaved(a) -> int:
+    """Same-box A/B of task env switches: ``--runs`` rounds, each arm once per round (a fresh
+    server and instance per measurement), p50 of time-to-first-step and of its stages per arm."""
+    arms = [x.strip() for x in a.interleave.split(",") if x.strip()]
+    per = {arm: [] for arm in arms}
+    for _ in range(a.runs):
+        for arm in arms:
+            r = measure(a.gpus, 1, a.steps, a.warmup, 0, 0, a.extra_args, a.timeout, a.gpu, a.fake_gpus,
+                        [*a.env, arm])
+            per[arm].append({"first_step_s": r["stages_p50_s"].get("first_step_s"),
+                             "time_to_first_step_s": r["time_to_first_step_p50_s"], "errors": r["errors"],
+                             "preflight": next((x.get("preflight") for x in r["samples"] if x.get("preflight")),
+                                               None)})
+    p50 = (lambda xs: round(statistics.median(xs), 4) if xs else None)
+    out = {arm: {"first_step_p50_s": p50([x["first_step_s"] for x in v if x["first_step_s"] is not None]),
+                 "time_to_first_step_p50_s": p50([x["time_to_first_step_s"] for x in v
+                                                  if x["time_to_first_step_s"] is not None]),
+                 "samples": v} for arm, v in per.items()}
+    print(json.dumps(out), flush=True)
+    return 0 if all(not x["errors"] for v in per.values() for x in v) else 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,9 +231,14 @@ def main():
     ap.add_argument("--timeout", type=float, default=600)
     ap.add_argument("--gpu", choices=("auto", "yes", "no"), default="auto")
     ap.add_argument("--fake-gpus", type=int, default=0, help="CPU tests: agents see N fake MI355X (gloo ranks)")
+    ap.add_argument("--env", action="append", default=[], help="KEY=VALUE for the task's env (repeatable)")
+    ap.add_argument("--interleave", default="", help="A/B: comma-separated env assignments, one arm each; the "
+                                                     "runs alternate between the arms")
     a = ap.parse_args()
+    if a.interleave:
+        return _interleaved(a)
     r = measure(a.gpus, a.runs, a.steps, a.warmup, a.tok_steps, a.tok_warmup, a.extra_args, a.timeout, a.gpu,
-                a.fake_gpus)
+                a.fake_gpus, a.env)
     print(json.dumps(r), flush=True)
     return 0 if not r["errors"] else 1
 

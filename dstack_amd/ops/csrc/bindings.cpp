@@ -62,6 +62,8 @@ bool dsa_fp8_rows_gemm_supported(int, int, int, int, int);
 hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
                              long, long, long, int, int, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
+hipError_t dsa_gemm_km_f32(const void*, const void*, void*, float*, int, int, int, long, long, long, long, int,
+                           hipStream_t);
 hipError_t dsa_gemm_nt_swiglu_bwd(const void*, const void*, const void*, void*, void*, int, int, int, long, long,
                                   hipStream_t);
 }
@@ -563,6 +565,30 @@ void gemm_km(torch::Tensor a, torch::Tensor b, torch::Tensor out, int64_t mode) 
         "gemm_km");
 }
 
+// weight gradient with an fp32 accumulator acc [M][N]: mode 0 acc = a^T b, 1 acc += a^T b, 2 out (bf16)
+// = acc + a^T b (the last micro-batch, one rounding)
+void gemm_km_f32(torch::Tensor a, torch::Tensor b, torch::Tensor acc, c10::optional<torch::Tensor> out, int64_t mode) {
+  check_rows(a, "gemm_km_f32");
+  check_rows(b, "gemm_km_f32");
+  TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == torch::kFloat32 && acc.dim() == 2 && acc.stride(1) == 1,
+              "gemm_km_f32: acc must be a row-major fp32 CUDA matrix");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && acc.size(0) == M && acc.size(1) == N, "gemm_km_f32: shape mismatch");
+  TORCH_CHECK(dsa_gemm_km_supported(M, N, K), "gemm_km_f32: M % 256, N % 256, K % 128 must be 0");
+  void* o = nullptr;
+  long ldo = 0;
+  if (mode == 2) {
+    TORCH_CHECK(out.has_value(), "gemm_km_f32: mode 2 writes the bf16 `out`");
+    check_rows(*out, "gemm_km_f32");
+    TORCH_CHECK(out->size(0) == M && out->size(1) == N, "gemm_km_f32: out shape mismatch");
+    o = out->data_ptr();
+    ldo = out->stride(0);
+  }
+  check(dsa_gemm_km_f32(a.data_ptr(), b.data_ptr(), o, acc.data_ptr<float>(), M, N, K, a.stride(0), b.stride(0), ldo,
+                        acc.stride(0), (int)mode, stream()),
+        "gemm_km_f32");
+}
+
 // gu = x w^T (w = [gate; up] [2F][K]) -> (gu [T][2F], a = silu(g) * u [T][F], a^T [F][T]); with
 // transposed = false a^T is not written (returned empty)
 std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor x, torch::Tensor w, bool transposed) {
@@ -761,6 +787,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_swiglu", &gemm_nt_swiglu, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("transposed") = true);
   m.def("gemm_km", &gemm_km, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("out"), pybind11::arg("mode") = 0);
   m.def("gemm_km_supported", &gemm_km_supported);
+  m.def("gemm_km_f32", &gemm_km_f32, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("acc"),
+        pybind11::arg("out") = pybind11::none(), pybind11::arg("mode") = 0);
   m.def("fp8_rows_gemm", &fp8_rows_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),
         pybind11::arg("ws"), pybind11::arg("bm") = 64, pybind11::arg("split") = 1, pybind11::arg("part") = pybind11::none(),
         pybind11::arg("cnt") = pybind11::none());

@@ -773,6 +773,266 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
 }
 
 // ================================================================================================
+// Backward dK/dV pass, 8 waves with DECOUPLED halves (DSTACK_AMD_FA_DKDV_DEC=1).
+// Same work split as fa_bwd_dkdv8_kernel (128 keys of one (b, q-head); wave w: keys kb0 + 32*(w&3),
+// query half w>>2 of every 64-query tile), but the two 4-wave halves no longer meet at a workgroup
+// barrier every tile.  A half reads only its own 32 query rows of Q / dO (and K / V, which are
+// resident and read-only after the prologue), so each half now stages its own rows in a ring of its
+// own (2 x [Q 32 rows | dO 32 rows | lse 64 | delta 64] per half) and closes a tile with a 4-wave
+// rendezvous on an LDS counter (each wave: its DMA for the next tile landed and its reads of this
+// one returned -> one lane's ds_add; then it polls until all four have added).  The phase trace of the
+// barrier form (profiles/fa_dkdv_phases_r8s.txt) had both halves in the same phase at once -- the
+// LDS-heavy S/dP reads together, the VALU-only softmax together (matrix pipe idle), and waves 0-3
+// idle ~1,150 ticks per tile at the barrier waiting for waves 4-7.  Decoupled, a half that is ahead
+// keeps going, and `stag` (s_sleep units of 64 clocks, DSTACK_AMD_FA_DKDV_STAG) starts waves 4-7
+// that much later so the halves settle out of phase: one half's softmax beside the other's MFMAs.
+// LDS: K|V 64 KiB + 4 x 16.5 KiB of rings + 2 counters = 130 KiB.  TR: the phase trace (see above).
+// ================================================================================================
+template <bool CAUSAL, bool TR = false, bool EARLY = false>
+__global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8d_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S, int H,
+    int KVH, float scale_log2, int stag, unsigned long long* __restrict__ trace) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KV_BYTES = 2 * 128 * 256;  // K (128 rows) | V (128 rows)
+  constexpr int HT = 32 * 256;             // one half tile: 32 rows x 128 bf16
+  constexpr int HSTAGE = 2 * HT + 512;     // Q half | dO half | lse (64) | delta (64)
+  constexpr int PF = 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
+  const int g = w & 3, qh = w >> 2;
+  const int NH = H + 2 * KVH;
+  const long rs = (long)NH * HD;
+  const long ors = (long)H * HD;
+  const int bid = blockIdx.x;
+  const int kb = bid / (B * H);  // small kb = most q tiles: heaviest first
+  const int bh = bid % (B * H);
+  const int b = bh / H, hh = bh % H, kvh = hh / (H / KVH);
+  const bf16_t* base = qkv + (long)b * S * rs;
+  const bf16_t* kp = base + (H + kvh) * HD;
+  const bf16_t* vp = base + (H + KVH + kvh) * HD;
+  const int kb0 = kb * 128, kw0 = kb0 + 32 * g, mykey = kw0 + l32;
+  char* kl = smem;
+  char* vl = smem + 128 * 256;
+  char* ring = smem + KV_BYTES;  // [stage][half] HSTAGE each
+  unsigned* cnt = reinterpret_cast<unsigned*>(ring + 4 * HSTAGE);
+  {  // K/V of the block: waves 0-3 stage K, waves 4-7 stage V (two 64-row halves each)
+    const bf16_t* src = qh == 0 ? kp : vp;
+    char* dst = qh == 0 ? kl : vl;
+    dma_tile64(src + (long)kb0 * rs, rs, dst, g, lane);
+    dma_tile64(src + (long)(kb0 + 64) * rs, rs, dst + TILE_BYTES, g, lane);
+  }
+  if (tid < 2) cnt[tid] = 0u;
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dk[d][r] = 0.f;
+      dv[d][r] = 0.f;
+    }
+  const int qt_begin = CAUSAL ? kb0 / 64 : 0;
+  const int nqt = S / 64;
+  // this half's 32 rows of Q and dO through buffer descriptors: wave g DMAs rows 8g..8g+7 of each
+  // (two 1 KiB pieces), per-lane offsets loop-invariant, the tile's row offset an SGPR
+  const __amdgpu_buffer_rsrc_t qr = make_rsrc(base + hh * HD, (unsigned)(((long)(S - 1) * rs + HD) * 2));
+  const __amdgpu_buffer_rsrc_t dr =
+      make_rsrc(dout + (long)b * S * ors + hh * HD, (unsigned)(((long)(S - 1) * ors + HD) * 2));
+  const __amdgpu_buffer_rsrc_t lr = make_rsrc(lse + (long)bh * S, (unsigned)S * 4);
+  const __amdgpu_buffer_rsrc_t er = make_rsrc(delta + (long)bh * S, (unsigned)S * 4);
+  unsigned qoff[2], doff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (2 * g + i) * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    qoff[i] = (unsigned)(((long)row * rs + ch * 8) * 2);
+    doff[i] = (unsigned)(((long)row * ors + ch * 8) * 2);
+  }
+  auto issue = [&](int qt, char* st) {  // this half's rows of q tile qt -> its stage `st`
+    const int r0 = qt * 64 + 32 * qh;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, LDS3(void, st + (2 * g + i) * 1024), 16, qoff[i],
+                                               __builtin_amdgcn_readfirstlane((int)((long)r0 * rs * 2)), 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, LDS3(void, st + HT + (2 * g + i) * 1024), 16, doff[i],
+                                               __builtin_amdgcn_readfirstlane((int)((long)r0 * ors * 2)), 0, 0);
+    }
+    if (g == 0) dma_f32x64_buf(lr, qt * 64, st + 2 * HT, lane);        // lse of the whole 64-row tile
+    if (g == 1) dma_f32x64_buf(er, qt * 64, st + 2 * HT + 256, lane);  // delta
+  };
+  issue(qt_begin, ring + qh * HSTAGE);
+  wait_dma_and_barrier();  // K/V, both halves' first tiles and the counters: the one full barrier
+  if (qh == 1)
+    for (int i = 0; i < stag; ++i) __builtin_amdgcn_s_sleep(1);
+  const bool tracer = TR && blockIdx.x == 0 && (w == 0 || w == 4);
+  int qt = qt_begin, stage = 0, tnum = 0;
+  unsigned gen = 0;
+  auto stamp = [&](int k) {
+    if constexpr (TR) {
+      if (tracer && tnum >= 8 && tnum < 12) {
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) trace[qh * 64 + (tnum - 8) * 5 + k] = t;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  for (;;) {
+    stamp(0);
+    const char* ql = ring + (stage * 2 + qh) * HSTAGE;
+    const char* dol = ql + HT;
+    const float* ll = reinterpret_cast<const float*>(ql + 2 * HT) + 32 * qh;
+    const float* dl = ll + 64;
+    const bool more = qt + 1 < nqt;
+    if (more) issue(qt + 1, ring + ((stage ^ 1) * 2 + qh) * HSTAGE);
+    const int qlo = qt * 64 + 32 * qh;
+    if (!CAUSAL || qlo + 31 >= kw0) {  // some query of my half-tile sees my keys
+      f32x16 sc, dpv;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sc[r] = 0.f;
+        dpv[r] = 0.f;
+      }
+      // step i: chain i & 1 (0 = S from Q.K^T, 1 = dP from dO.V^T), k-slice i >> 1; the reads of
+      // step i + PF are issued before the MFMA of step i
+      auto rd_a = [&](int i) { return lds_row((i & 1) ? dol : ql, l32, 2 * (i >> 1) + hf); };
+      auto rd_b = [&](int i) { return lds_row((i & 1) ? vl : kl, 32 * g + l32, 2 * (i >> 1) + hf); };
+      constexpr int NB = PF + 1;
+      bf16x8 fa[NB], fb[NB];
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        fa[j] = rd_a(j);
+        fb[j] = rd_b(j);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const bf16x8 a = fa[i % NB], bb = fb[i % NB];
+        if (i + PF < 16) {
+          fa[(i + PF) % NB] = rd_a(i + PF);
+          fb[(i + PF) % NB] = rd_b(i + PF);
+        }
+        if (i & 1)
+          dpv = mfma(a, bb, dpv);
+        else
+          sc = mfma(a, bb, sc);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * PF, 0);
+#pragma unroll
+      for (int i = 0; i < 16 - PF; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, PF, 0);
+      stamp(1);
+      // the dV/dK operands (transposed dO / Q fragments) do not depend on P or dS: with EARLY the
+      // first d-group is read here and lands under the softmax math, and every later group is read
+      // one group ahead of its MFMAs (without it: 8 reads -> lgkmcnt(0) -> 4 MFMAs per group)
+      bf16x8 gf[2][4];
+      auto rd_g = [&](int d, bf16x8(&f)[4]) {
+        f[0] = lds_tr(dol, 0, 32 * d, lane);
+        f[1] = lds_tr(dol, 16, 32 * d, lane);
+        f[2] = lds_tr(ql, 0, 32 * d, lane);
+        f[3] = lds_tr(ql, 16, 32 * d, lane);
+      };
+      if constexpr (EARLY) rd_g(0, gf[0]);
+      const bool diag = CAUSAL && qlo < kw0 + 31;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const f4 L = *reinterpret_cast<const f4*>(ll + 8 * rr + 4 * hf);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sc[4 * rr + i] = fexp2(fmaf(sc[4 * rr + i], scale_log2, -L[i]));
+      }
+      if (__builtin_expect(diag, 0)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (mykey > qlo + 8 * (r >> 2) + 4 * hf + (r & 3)) sc[r] = 0.f;
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const f4 Dl = *reinterpret_cast<const f4*>(dl + 8 * rr + 4 * hf);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rr + i;
+          dpv[r] = sc[r] * (dpv[r] - Dl[i]);
+        }
+      }
+      bf16x8 pb[2], dsb[2];
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        pb[k2] = to_bf16x8(sc, 8 * k2);
+        dsb[k2] = to_bf16x8(dpv, 8 * k2);
+      }
+      stamp(2);
+      if constexpr (EARLY) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (d + 1 < 4) rd_g(d + 1, gf[(d + 1) & 1]);
+          const bf16x8(&f)[4] = gf[d & 1];
+          dv[d] = mfma(f[0], pb[0], dv[d]);
+          dk[d] = mfma(f[2], dsb[0], dk[d]);
+          dv[d] = mfma(f[1], pb[1], dv[d]);
+          dk[d] = mfma(f[3], dsb[1], dk[d]);
+        }
+      } else {
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int k2 = 0; k2 < 2; ++k2) {
+            dv[d] = mfma(lds_tr(dol, 16 * k2, 32 * d, lane), pb[k2], dv[d]);
+            dk[d] = mfma(lds_tr(ql, 16 * k2, 32 * d, lane), dsb[k2], dk[d]);
+          }
+      }
+    }
+    stamp(3);
+    if (!more) break;
+    // the half's rendezvous: my DMA of the next tile has landed and my reads of this one returned
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    gen += 4;
+    if (lane == 0) __hip_atomic_fetch_add(&cnt[qh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&cnt[qh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen)
+      __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+    stamp(4);
+    ++tnum;
+    ++qt;
+    stage ^= 1;
+  }
+  __syncthreads();  // both halves are done with K/V and their rings: the LDS is reused below
+  // reduce the two q-halves of every key group through LDS: [g][dk|dv][d][r][lane] floats
+  float* red = reinterpret_cast<float*>(smem);
+  if (qh == 1) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        red[(((g * 2 + 0) * 4 + d) * 16 + r) * 64 + lane] = dk[d][r];
+        red[(((g * 2 + 1) * 4 + d) * 16 + r) * 64 + lane] = dv[d][r];
+      }
+  }
+  __syncthreads();
+  if (qh == 0) {
+    const float sm = scale_log2 * 0.6931471805599453f;  // softmax scale = scale_log2 * ln2
+    float* dkr = dkp + (((long)b * S + mykey) * H + hh) * HD;
+    float* dvr = dvp + (((long)b * S + mykey) * H + hh) * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int dd = 32 * d + 8 * rr + 4 * hf;
+        f4 ok, ov;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rr + i;
+          ok[i] = (dk[d][r] + red[(((g * 2 + 0) * 4 + d) * 16 + r) * 64 + lane]) * sm;
+          ov[i] = dv[d][r] + red[(((g * 2 + 1) * 4 + d) * 16 + r) * 64 + lane];
+        }
+        *reinterpret_cast<f4*>(dkr + dd) = ok;
+        *reinterpret_cast<f4*>(dvr + dd) = ov;
+      }
+  }
+}
+
+// ================================================================================================
 // Backward dK/dV pass, 64 keys per wave: workgroup = 4 waves = 256 keys of one (b, q-head), one
 // wave per SIMD.  Each wave keeps K (and, with VREG, V) of its 64 keys in registers and dK^T / dV^T
 // of those keys in 256 accumulator registers, and sweeps 32-query slices of Q/dO staged in LDS:
@@ -1378,9 +1638,28 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     return v ? atoi(v) : 1;
   }();
   const int dq_pf = ((long)S * (H + 2 * KVH) * HD * 2 < (1L << 31)) ? dq_pf_env : 0;
+  // decoupled halves (fa_bwd_dkdv8d_kernel): DSTACK_AMD_FA_DKDV_DEC=1, waves 4-7 started
+  // DSTACK_AMD_FA_DKDV_STAG x 64 clocks late
+  static const int dkdv_dec_env = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DKDV_DEC");
+    return v ? atoi(v) : 0;
+  }();
+  static const int dkdv_stag = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DKDV_STAG");
+    return v ? atoi(v) : 0;
+  }();
+  const bool dkdv_dec = dkdv_dec_env >= 1 && dkdv_kind == 8 && !half_prio && !dkdv_gqa && dkdv_pf >= 2;
+  const size_t lds_dec = 2 * 128 * 256 + 4 * (2 * 32 * 256 + 512) + 16;
 #define DSA_DKDV(C, N)                                                                                 \
   do {                                                                                                 \
-    if (dkdv_kind >= 64 && S % 256 == 0) {                                                             \
+    if (dkdv_dec && dkdv_dec_env == 2) {                                                               \
+      fa_bwd_dkdv8d_kernel<C, false, true><<<grid, 512, lds_dec, st>>>(                                  \
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, dkdv_stag, nullptr); \
+    } else if (dkdv_dec) {                                                                             \
+      fa_bwd_dkdv8d_kernel<C><<<grid, 512, lds_dec, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,  \
+                                                          delta, dkp, dvp, B, S, H, KVH, sl2, dkdv_stag,  \
+                                                          nullptr);                                      \
+    } else if (dkdv_kind >= 64 && S % 256 == 0) {                                                      \
       if (dkdv_kind == 64)                                                                             \
         fa_bwd_dkdv64_kernel<C, true><<<B * H * (S / 256), 256, 2 * (2 * TILE_BYTES + 512), st>>>(     \
             (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2);         \
@@ -1492,6 +1771,18 @@ extern "C" hipError_t dsa_fa_dkdv_trace(const void* qkv, const void* dout, const
                                         float* dkp, float* dvp, unsigned long long* trace, int B, int S, int H,
                                         int KVH, float sl2, hipStream_t st) {
   if (S % 128) return hipErrorInvalidValue;
+  const char* dec = getenv("DSTACK_AMD_FA_DKDV_DEC");
+  if (dec && atoi(dec) >= 1) {  // the decoupled-halves form: stamp 4 is after the half's rendezvous
+    const char* sg = getenv("DSTACK_AMD_FA_DKDV_STAG");
+    const size_t lds_dec = 2 * 128 * 256 + 4 * (2 * 32 * 256 + 512) + 16;
+    if (atoi(dec) == 2)
+      fa_bwd_dkdv8d_kernel<true, true, true><<<B * H * (S / 128), 512, lds_dec, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, sg ? atoi(sg) : 0, trace);
+    else
+      fa_bwd_dkdv8d_kernel<true, true><<<B * H * (S / 128), 512, lds_dec, st>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, sg ? atoi(sg) : 0, trace);
+    return hipGetLastError();
+  }
   const size_t lds8 = 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512);
   fa_bwd_dkdv8_kernel<true, false, false, false, false, true, 2><<<B * H * (S / 128), 512, lds8, st>>>(
       (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, (bf16_t*)trace);

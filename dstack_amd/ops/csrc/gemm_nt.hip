@@ -63,8 +63,11 @@ constexpr int NT_LDS = 2 * BUF + 2 * 16384;  // 160 KiB: ring + room for the Swi
 // EPI_SWIGLU_R / EPI_SWIGLU_BWD_R: the SwiGLU epilogues without the transposed copies (a^T, dgu^T),
 // for a step whose weight gradients take the token-major operands (KM form): barrier-free, so the
 // groups stay staggered as in the plain epilogue.
+// EPI_STORE32 / EPI_ACC32: C is fp32 (an fp32 gradient accumulator: weight gradients summed over
+// micro-batches without a bf16 rounding per micro-batch); EPI_ACC32_BF16: the last micro-batch --
+// the fp32 accumulator F32 (ld ldc32) plus this tile, rounded once, written as bf16 to C.
 enum Epi { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU = 2, EPI_SWIGLU_BWD = 3, EPI_NONE = 4, EPI_SWIGLU_R = 5,
-           EPI_SWIGLU_BWD_R = 6 };
+           EPI_SWIGLU_BWD_R = 6, EPI_STORE32 = 7, EPI_ACC32 = 8, EPI_ACC32_BF16 = 9 };
 
 struct NTArgs {
   const bf16_t* A;
@@ -73,7 +76,9 @@ struct NTArgs {
   bf16_t* C2;     // a (SWIGLU)
   bf16_t* C3;     // a^T (SWIGLU); dgu^T (SWIGLU_BWD)
   const bf16_t* G;  // gu read by SWIGLU_BWD
+  const float* F32;  // fp32 accumulator read by ACC32_BF16
   long lda, ldb, ldc;
+  long ldc32;
   int M, K;
   int ntn;        // tiles along N
   int nstride;    // column origin step per n tile (256 plain, 128 SwiGLU)
@@ -537,6 +542,49 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
               *reinterpret_cast<us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit) = nt_pair8(x, y);
             }
       }
+    } else if constexpr (EPI == EPI_STORE32 || EPI == EPI_ACC32 || EPI == EPI_ACC32_BF16) {
+      // the same 8-column pieces as EPI_STORE, as 8 floats (two 16-byte accesses); old values are
+      // loaded one 128-row half (ms) at a time: 64 VGPRs beside the 128 of the accumulators
+      const int q = lane >> 4;
+      const long col = nb0 + 32 * wc + 16 * (q & 1) + 8 * (q >> 1);
+      const long row = m0 + 64 * wr + er;
+      float* c32 = reinterpret_cast<float*>(p.C) + row * p.ldc + col;
+      const float* o32 = (EPI == EPI_ACC32_BF16 ? p.F32 + row * p.ldc32 + col : c32);
+      const long ldo = EPI == EPI_ACC32_BF16 ? p.ldc32 : p.ldc;
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms) {
+        f4 old[4][2][2];
+        if constexpr (EPI != EPI_STORE32) {
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                old[mi][pp][h] = *reinterpret_cast<const f4*>(o32 + (long)(128 * ms + 16 * mi) * ldo + pp * p.bsplit + 4 * h);
+        }
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            float v[8];
+            nt_pair8f(acc[ms][mi][2 * pp], acc[ms][mi][2 * pp + 1], v);
+            if constexpr (EPI != EPI_STORE32) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += old[mi][pp][j >> 2][j & 3];
+            }
+            if constexpr (EPI == EPI_ACC32_BF16) {
+              us8 o;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+              *reinterpret_cast<us8*>(p.C + row * p.ldc + col + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit) = o;
+            } else {
+              float* dst = c32 + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit;
+              *reinterpret_cast<f4*>(dst) = f4{v[0], v[1], v[2], v[3]};
+              *reinterpret_cast<f4*>(dst + 4) = f4{v[4], v[5], v[6], v[7]};
+            }
+          }
+      }
     } else if constexpr (EPI == EPI_SWIGLU_R) {
       // gu and a straight from the accumulators, no transposed copy
       const int q = lane >> 4;
@@ -878,6 +926,39 @@ extern "C" hipError_t dsa_gemm_nt_swiglu_bwd(const void* dY, const void* WdT, co
 }
 
 extern "C" bool dsa_gemm_km_supported(int M, int N, int K) { return nt_shape_ok(M, N, K); }
+
+// KM form with an fp32 gradient accumulator (weight gradients summed over micro-batches in fp32):
+// mode 0: C32 = A^T B (first micro-batch), 1: C32 += A^T B, 2: C (bf16) = bf16(C32 + A^T B) (last
+// micro-batch: one rounding).  C32 [M][ldc32] fp32, C [M][ldc] bf16 (mode 2 only).
+extern "C" hipError_t dsa_gemm_km_f32(const void* A, const void* B, void* C, float* C32, int M, int N, int K, long lda,
+                                      long ldb, long ldc, long ldc32, int mode, hipStream_t st) {
+  if (!nt_shape_ok(M, N, K) || lda % 8 || ldb % 8 || ldc32 % 4 || lda < M || ldb < N || ldc32 < N || mode < 0 ||
+      mode > 2 || (mode == 2 && (!C || ldc % 8 || ldc < N)))
+    return hipErrorInvalidValue;
+  if (63L * lda * 2 + 512 > 0xffffffffL || 63L * ldb * 2 + 512 > 0xffffffffL) return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.M = M;
+  a.K = K;
+  a.ntn = N / NT_BN;
+  a.nstride = NT_BN;
+  a.bsplit = 128;
+  a.group = nt_group(M / NT_BM, N / NT_BN);
+  const int tiles = (M / NT_BM) * (N / NT_BN);
+  if (mode == 2) {
+    a.C = (bf16_t*)C;
+    a.ldc = ldc;
+    a.F32 = C32;
+    a.ldc32 = ldc32;
+    return nt_launch<EPI_ACC32_BF16, false, true>(a, tiles, st);
+  }
+  a.C = reinterpret_cast<bf16_t*>(C32);
+  a.ldc = ldc32;
+  return mode ? nt_launch<EPI_ACC32, false, true>(a, tiles, st) : nt_launch<EPI_STORE32, false, true>(a, tiles, st);
+}
 
 // KM form: C[M][N] (+)= A[K][M]^T B[K][N] (weight gradient dW = dY^T X of token-major dY, X).
 // Leading dimensions (row strides of A, B, C) in elements, multiples of 8.

@@ -445,6 +445,28 @@ def mm_into(a: torch.Tensor, b: torch.Tensor, out=None, accumulate: bool = False
     return torch.mm(a, b, out=out)
 
 
+def mm_into_f32(a: torch.Tensor, b: torch.Tensor, acc: torch.Tensor, out: torch.Tensor, mode: int) -> None:
+    """Weight gradient ``a @ b`` with an fp32 accumulator ``acc``: mode 0 ``acc = a @ b``, 1
+    ``acc += a @ b``, 2 ``out (bf16) = acc + a @ b`` (the last micro-batch: one rounding).  The
+    in-tree KM GEMM does it in its epilogue (``gemm_km_f32``); other layouts/devices in fp32 torch."""
+    if (a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and _ext.use_hip(a) and a.stride(0) == 1
+            and b.stride(1) == 1 and acc.stride(1) == 1 and a.shape[1] == b.shape[0]):
+        C = _ext.require()
+        g = a.t()
+        if (C.gemm_km_supported(a.shape[0], b.shape[1], a.shape[1]) and g.stride(0) % 8 == 0
+                and b.stride(0) % 8 == 0 and acc.stride(0) % 4 == 0 and out.stride(0) % 8 == 0
+                and all(t.data_ptr() % 16 == 0 for t in (g, b, acc, out))):
+            C.gemm_km_f32(g, b, acc, out if mode == 2 else None, mode)
+            return
+    prod = torch.mm(a.float(), b.float())
+    if mode == 0:
+        acc.copy_(prod)
+    elif mode == 1:
+        acc.add_(prod)
+    else:
+        out.copy_(acc + prod)
+
+
 def wgrad_operands(g2: torch.Tensor, x2, xT=None, gT=None):
     """Operands (a [P, T], b [T, Q]) with dW = a @ b for g2 [T, P] and x2 [T, Q] (or its transpose
     ``xT`` [Q, T] when the producer already wrote it; likewise ``gT`` [P, T] for g2).

@@ -66,6 +66,7 @@ class ZeroOptimizer:
         overlap_update: bool = True,
         force_collectives: bool | None = None,
         clip_grad_norm: float = 0.0,
+        grad_accum_fp32: bool | None = None,
     ):
         self.model = model
         self.lr = lr
@@ -124,12 +125,24 @@ class ZeroOptimizer:
 
         self.flat_param = torch.zeros(self.total_numel, dtype=dtype, device=device)
         self.flat_grad = torch.zeros(self.total_numel, dtype=dtype, device=device)
+        # fp32 accumulation of the GEMM weight gradients over micro-batches (DSTACK_AMD_GRAD_ACCUM_FP32
+        # or ``grad_accum_fp32``): micro-batches 1..n-1 are summed in an fp32 buffer by the weight-
+        # gradient GEMM's epilogue and the last one writes bf16(fp32 sum + its own tile) into
+        # flat_grad -- one rounding per optimizer step instead of one per micro-batch.  The buffer
+        # (4 bytes per parameter) is allocated at the first non-final micro-batch, so runs without
+        # gradient accumulation never hold it.  Norm weights and the embedding accumulate in bf16.
+        if grad_accum_fp32 is None:
+            grad_accum_fp32 = os.environ.get("DSTACK_AMD_GRAD_ACCUM_FP32", "0") not in ("0", "", "false")
+        self.grad_accum_fp32 = bool(grad_accum_fp32) and dtype == torch.bfloat16
+        self.acc32 = None
+        self._offset = {}
         self._bucket_of = {}
         for p, o in layout:
             n = p.numel()
             self.flat_param[o : o + n].copy_(p.detach().reshape(-1))
             p.data = self.flat_param[o : o + n].view_as(p)
             p.grad = self.flat_grad[o : o + n].view_as(p)
+            self._offset[p] = o
         for b in self.buckets:
             for p in b.params:
                 self._bucket_of[p] = b
@@ -190,10 +203,22 @@ class ZeroOptimizer:
         # parameters already counted down in this step's synchronising backward (see _on_grad_ready)
         self._reported = set()
 
+    def _acc32_view(self, p: torch.Tensor) -> torch.Tensor:
+        if self.acc32 is None:
+            self.acc32 = torch.zeros(self.total_numel, dtype=torch.float32, device=self.flat_grad.device)
+        o = self._offset[p]
+        return self.acc32[o : o + p.numel()].view(p.shape)
+
     def _direct_grad(self, p: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
         """Weight gradient sink for ``ops.linear``: dW = a @ b (a = g^T [P, T], b = x [T, Q], as
         views in whichever layout ``ops.functional.wgrad_operands`` chose) into the flat buffer."""
-        ops.functional.mm_into(a, b, p.grad, accumulate=not p._dsa_fresh)
+        if self.grad_accum_fp32 and not (p._dsa_fresh and self.sync_grads):
+            # 0: first of several micro-batches -> fp32; 1: a middle one, fp32 += ; 2: the last one,
+            # bf16(fp32 + this) into flat_grad
+            mode = 2 if self.sync_grads else (0 if p._dsa_fresh else 1)
+            ops.functional.mm_into_f32(a, b, self._acc32_view(p), p.grad, mode)
+        else:
+            ops.functional.mm_into(a, b, p.grad, accumulate=not p._dsa_fresh)
         p._dsa_fresh = False
         self._direct_ok.add(p)
         if self._hooks_on:

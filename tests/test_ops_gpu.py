@@ -289,7 +289,8 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
     pass (DSTACK_AMD_FA_DQ=ds; also at S=1152, its 4-wave dQ form, causal and not), and dK/dV summed
     over the GQA group in one workgroup (DSTACK_AMD_FA_DKDV_GQA=1, causal and not), and the S/dP read
     pipelines: dK/dV without it or one step ahead (DSTACK_AMD_FA_DKDV_PF=0|1; the default is 2) and the
-    dQ pass's (DSTACK_AMD_FA_DQ_PF=1|2, causal).  The switches are read once per process, so each
+    dQ pass's (DSTACK_AMD_FA_DQ_PF=1|2, causal), and the dK/dV pass with decoupled halves
+    (DSTACK_AMD_FA_DKDV_DEC=1, with and without a stagger; bit-identical to the barrier form).  The switches are read once per process, so each
     variant runs in a child process."""
     import os
     import subprocess
@@ -309,7 +310,7 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
     )
     shape = {"dq_ds_1152": (1152, True), "dq_ds_1152_nc": (1152, False), "default_1152": (1152, True),
              "default_1152_nc": (1152, False), "dkdv_gqa_nc": (1024, False), "default_nc": (1024, False),
-             "dkdv_pf0_nc": (1024, False)}
+             "dkdv_pf0_nc": (1024, False), "dkdv_dec_nc": (1024, False), "dkdv_dec_1152": (1152, True)}
     variants = {"default": {}, "dkdv4": {"DSTACK_AMD_FA_DKDV": "4w"},
                 "fwd4_dq4": {"DSTACK_AMD_FA_FWD_WAVES": "4", "DSTACK_AMD_FA_DQ_WAVES": "4"},
                 "fwd_pf0": {"DSTACK_AMD_FA_FWD_PF": "0"}, "exact_max": {"DSTACK_AMD_FA_RESCALE_THR": "0"},
@@ -319,13 +320,18 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
                 "dkdv_gqa": {"DSTACK_AMD_FA_DKDV_GQA": "1"}, "dkdv_gqa_nc": {"DSTACK_AMD_FA_DKDV_GQA": "1"},
                 "default_nc": {}, "dkdv_pf0": {"DSTACK_AMD_FA_DKDV_PF": "0"},
                 "dkdv_pf1": {"DSTACK_AMD_FA_DKDV_PF": "1"}, "dkdv_pf0_nc": {"DSTACK_AMD_FA_DKDV_PF": "0"},
-                "dq_pf1": {"DSTACK_AMD_FA_DQ_PF": "1"}, "dq_pf2": {"DSTACK_AMD_FA_DQ_PF": "2"}}
+                "dq_pf1": {"DSTACK_AMD_FA_DQ_PF": "1"}, "dq_pf2": {"DSTACK_AMD_FA_DQ_PF": "2"},
+                "dkdv_dec": {"DSTACK_AMD_FA_DKDV_DEC": "1"},
+                "dkdv_dec_stag": {"DSTACK_AMD_FA_DKDV_DEC": "1", "DSTACK_AMD_FA_DKDV_STAG": "24"},
+                "dkdv_dec_nc": {"DSTACK_AMD_FA_DKDV_DEC": "1"}, "dkdv_dec_1152": {"DSTACK_AMD_FA_DKDV_DEC": "1"},
+                "dkdv_dec_early": {"DSTACK_AMD_FA_DKDV_DEC": "2"}}
     out = {}
     for name, extra in variants.items():
         env = dict(os.environ)
         for k in ("DSTACK_AMD_FA_DKDV", "DSTACK_AMD_FA_FWD_WAVES", "DSTACK_AMD_FA_DQ_WAVES", "DSTACK_AMD_FA_FWD_PF",
                   "DSTACK_AMD_FA_RESCALE_THR", "DSTACK_AMD_FA_FWD_STAG", "DSTACK_AMD_FA_HALF_PRIO", "DSTACK_AMD_FA_DQ",
-                  "DSTACK_AMD_FA_DKDV_GQA", "DSTACK_AMD_FA_DKDV_PF", "DSTACK_AMD_FA_DQ_PF"):
+                  "DSTACK_AMD_FA_DKDV_GQA", "DSTACK_AMD_FA_DKDV_PF", "DSTACK_AMD_FA_DQ_PF", "DSTACK_AMD_FA_DKDV_DEC",
+                  "DSTACK_AMD_FA_DKDV_STAG"):
             env.pop(k, None)
         env.update(extra)
         sn, causal = shape.get(name, (S, True))
@@ -335,13 +341,18 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
         out[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
     ref_o, ref_g = out["default"]["o"].float(), out["default"]["g"].float()
     for name in ("dkdv4", "fwd4_dq4", "fwd_pf0", "exact_max", "fwd_stag", "half_prio", "dq_ds", "dkdv_gqa",
-                 "dkdv_pf0", "dkdv_pf1", "dq_pf1", "dq_pf2"):
+                 "dkdv_pf0", "dkdv_pf1", "dq_pf1", "dq_pf2", "dkdv_dec", "dkdv_dec_stag"):
         o, g = out[name]["o"].float(), out[name]["g"].float()
         assert ((o - ref_o).norm() / ref_o.norm()).item() < 2e-3, name
         assert ((g - ref_g).norm() / ref_g.norm()).item() < 2e-3, name
-    for name in ("dkdv_gqa_nc", "dkdv_pf0_nc"):
+    for name in ("dkdv_gqa_nc", "dkdv_pf0_nc", "dkdv_dec_nc"):
         g, rg = out[name]["g"].float(), out["default_nc"]["g"].float()
         assert ((g - rg).norm() / rg.norm()).item() < 2e-3, name
+    # the decoupled dK/dV computes exactly what the barrier form does: identical gradients
+    assert torch.equal(out["dkdv_dec"]["g"], out["default"]["g"])
+    assert torch.equal(out["dkdv_dec_stag"]["g"], out["default"]["g"])
+    assert torch.equal(out["dkdv_dec_early"]["g"], out["default"]["g"])
+    assert torch.equal(out["dkdv_dec_1152"]["g"], out["default_1152"]["g"])
     for name in ("dq_ds_1152", "dq_ds_1152_nc"):
         ref = out[name.replace("dq_ds", "default")]
         g, rg = out[name]["g"].float(), ref["g"].float()
@@ -631,6 +642,55 @@ def test_gemm_km_matches_fp32(gpu, M, N, K, accumulate):
     C.gemm_km(a, b, out, 1 if accumulate else 0)
     err = ((out.float() - ref_).norm() / ref_.norm()).item()
     assert err < 5e-3, err
+
+
+@pytest.mark.parametrize("M,N", [(1024, 4096), (4096, 1024)])
+def test_gemm_km_grad_accumulation_8_micro_batches_k8192(gpu, M, N):
+    """Weight gradients over 8 micro-batches of 8192 tokens (the bench's step): the bf16 path
+    (gemm_km, accumulate=1 seven times, a bf16 rounding per micro-batch) and the fp32-accumulator
+    path (gemm_km_f32: modes 0, 1 x 6, 2 -- one rounding), both against the fp32 sum of the eight
+    fp32 products.  The fp32 path must be at the single-rounding level and below the bf16 path."""
+    C = _ext.require()
+    K, n = 8192, 8
+    ref_ = torch.zeros(M, N, device=gpu, dtype=torch.float32)
+    out16 = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    out32 = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    acc = torch.empty(M, N, device=gpu, dtype=torch.float32)
+    for i in range(n):
+        # dY-like operands: scaled by 1/n, as the bench's loss / grad_accum does
+        a = _rand(K, M, device=gpu, seed=10 + i, scale=1.0 / n)
+        b = _rand(K, N, device=gpu, seed=100 + i)
+        ref_ += a.float().t() @ b.float()
+        C.gemm_km(a, b, out16, 1 if i else 0)
+        C.gemm_km_f32(a, b, acc, out32 if i == n - 1 else None, 2 if i == n - 1 else (1 if i else 0))
+    e16 = ((out16.float() - ref_).norm() / ref_.norm()).item()
+    e32 = ((out32.float() - ref_).norm() / ref_.norm()).item()
+    one = ((ref_.bfloat16().float() - ref_).norm() / ref_.norm()).item()  # one bf16 rounding
+    print(f"rel err bf16-accumulated {e16:.3e}, fp32-accumulated {e32:.3e}, one rounding {one:.3e}")
+    assert e32 < 1.2 * one + 1e-5, (e32, one)
+    assert e32 < e16, (e32, e16)
+    assert e16 < 8e-3, e16
+
+
+def test_gemm_km_f32_modes_and_strides(gpu):
+    """gemm_km_f32 mode 0 stores fp32, mode 1 adds, mode 2 writes bf16(acc + product) into a strided
+    bf16 view without touching its neighbours; the accumulator may be a strided fp32 view too."""
+    C = _ext.require()
+    M, N, K = 512, 256, 256
+    a, b = _rand(K, M, device=gpu), _rand(K, N, device=gpu, seed=1)
+    prod = a.float().t() @ b.float()
+    big = torch.zeros(M, N + 128, device=gpu, dtype=torch.float32)
+    acc = big[:, 64:64 + N]
+    C.gemm_km_f32(a, b, acc, None, 0)
+    assert ((acc - prod).norm() / prod.norm()).item() < 1e-5
+    C.gemm_km_f32(a, b, acc, None, 1)
+    assert ((acc - 2 * prod).norm() / prod.norm()).item() < 2e-5
+    assert big[:, :64].abs().max().item() == 0 and big[:, 64 + N:].abs().max().item() == 0
+    obig = torch.zeros(M, N + 256, device=gpu, dtype=torch.bfloat16)
+    out = obig[:, 128:128 + N]
+    C.gemm_km_f32(a, b, acc, out, 2)
+    assert ((out.float() - 3 * prod).norm() / (3 * prod).norm()).item() < 3e-3
+    assert obig[:, :128].abs().max().item() == 0 and obig[:, 128 + N:].abs().max().item() == 0
 
 
 def test_gemm_km_strided_operands(gpu):

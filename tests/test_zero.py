@@ -249,3 +249,40 @@ def test_bucket_completes_once_after_all_its_gradients():
     for i, seen_ids in completions:
         assert {id(p) for p in opt.buckets[i].params} <= seen_ids, f"bucket {i} completed early"
     assert all(b.pending == 0 for b in opt.buckets)
+
+
+def test_mm_into_f32_fallback_modes():
+    """The fp32 gradient-accumulator contract on the torch fallback (the HIP path is
+    test_ops_gpu.py::test_gemm_km_f32_modes_and_strides): 0 stores, 1 adds, 2 writes bf16(acc + a@b)."""
+    import torch
+
+    from dstack_amd.ops import functional as F
+
+    g = torch.Generator().manual_seed(0)
+    a = torch.randn(64, 32, generator=g).bfloat16()
+    b = torch.randn(32, 48, generator=g).bfloat16()
+    acc = torch.zeros(64, 48)
+    out = torch.zeros(64, 48, dtype=torch.bfloat16)
+    prod = a.float() @ b.float()
+    F.mm_into_f32(a, b, acc, out, 0)
+    assert torch.allclose(acc, prod) and out.abs().max() == 0
+    F.mm_into_f32(a, b, acc, out, 1)
+    assert torch.allclose(acc, 2 * prod)
+    F.mm_into_f32(a, b, acc, out, 2)
+    assert torch.equal(out, (2 * prod + prod).bfloat16())
+
+
+def test_zero_grad_accum_fp32_only_for_bf16_params(monkeypatch):
+    import torch
+    import torch.nn as nn
+
+    from dstack_amd.parallel.zero import ZeroOptimizer
+
+    monkeypatch.setenv("DSTACK_AMD_GRAD_ACCUM_FP32", "1")
+    m32 = nn.Linear(64, 64, bias=False)
+    assert not ZeroOptimizer(m32).grad_accum_fp32  # fp32 params: nothing to gain
+    m16 = nn.Linear(64, 64, bias=False).to(torch.bfloat16)
+    opt = ZeroOptimizer(m16)
+    assert opt.grad_accum_fp32 and opt.acc32 is None  # allocated at the first non-final micro-batch
+    w = next(m16.parameters())
+    assert opt._acc32_view(w).shape == w.shape and opt.acc32.dtype == torch.float32
