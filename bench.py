@@ -150,10 +150,14 @@ def _release_gpu() -> None:
     import torch
     import torch.distributed as dist
 
-    gc.collect()  # (the caller has dropped its trainer; its hooks form reference cycles)
+    gc.collect()  # (the caller has closed and dropped its trainer)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+        held = torch.cuda.memory_allocated() / 2**30
+        if held > 1.0:  # the cold-start task needs the GPUs: say so if this rank could not let go
+            print(f"[bench] warning: {held:.1f} GiB still allocated after releasing the trainer", file=sys.stderr,
+                  flush=True)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
@@ -236,6 +240,7 @@ def main():
             "attn": os.environ.get("DSTACK_AMD_ATTN", "hip"),
             "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu",
         }
+    tr.close()  # the optimizer's autograd hooks pin model and buffers from the C++ side
     del tr
     _release_gpu()
     if env.rank != 0:

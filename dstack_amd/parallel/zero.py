@@ -417,6 +417,28 @@ class ZeroOptimizer:
             buckets = self._buckets_of(own)
             self._hooks.append(mod.register_forward_pre_hook(lambda m, a, _b=buckets: self.wait_params(_b)))
 
+    def close(self):
+        """Detach from the model so that the optimizer, its flat buffers and the model can be
+        freed: the post-accumulate-grad and forward pre-hooks are held by the autograd engine's C++
+        side (a reference cycle Python's gc cannot see through), and the per-parameter sinks point
+        back at this object.  Waits for in-flight side-stream work first."""
+        self.wait_params()
+        if self._side is not None:
+            self._side.synchronize()
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        for b in self.buckets:
+            for p in b.params:
+                for a in ("_dsa_grad_sink", "_dsa_grad_writer", "_dsa_wgen", "_dsa_wt", "_dsa_fresh"):
+                    if hasattr(p, a):
+                        delattr(p, a)
+                p.grad = None
+        for mod in self.model.modules():
+            if getattr(mod, "param_waiter", None) is not None:
+                mod.param_waiter = None
+        self.acc32 = None
+
     def _buckets_of(self, params):
         return [self.buckets[i] for i in sorted({self._bucket_of[p].index for p in params})]
 

@@ -141,6 +141,13 @@ class Trainer:
         self._i += 1
         return out
 
+    def close(self):
+        """Release the GPU memory of the model and optimizer (see ZeroOptimizer.close): after
+        this, dropping the trainer frees its tensors and ``torch.cuda.empty_cache`` returns them."""
+        self.opt.close()
+        self.stream = None
+        self.data = None
+
     def lr_at(self, step: int) -> float:
         """Learning rate of optimizer step ``step`` (1-based)."""
         import math

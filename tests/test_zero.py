@@ -286,3 +286,29 @@ def test_zero_grad_accum_fp32_only_for_bf16_params(monkeypatch):
     assert opt.grad_accum_fp32 and opt.acc32 is None  # allocated at the first non-final micro-batch
     w = next(m16.parameters())
     assert opt._acc32_view(w).shape == w.shape and opt.acc32.dtype == torch.float32
+
+
+def test_trainer_close_frees_model_and_optimizer(monkeypatch):
+    """With collectives or optimizer-in-backward, ZeroOptimizer's autograd hooks are held from the
+    C++ side of the engine: a dropped trainer stays alive (on a GPU: every byte of the model and its
+    optimizer, which is what made the 1-GPU cold start under a launcher OOM).  Trainer.close()
+    detaches it so that it is freed."""
+    import gc
+    import weakref
+
+    import torch.distributed as dist
+
+    from dstack_amd.workloads.train_llama import run
+
+    monkeypatch.setenv("DSTACK_AMD_ZERO_FORCE_COLLECTIVES", "1")  # a 1-rank gloo group: hooks on
+    env, tr, _ = run("llama-tiny", 64, 1, 1, 0, log_every=0, grad_accum=2)
+    try:
+        assert tr.opt._hooks
+        wm, wo = weakref.ref(tr.model), weakref.ref(tr.opt)
+        tr.close()
+        del tr
+        gc.collect()
+        assert wm() is None and wo() is None
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
