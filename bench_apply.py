@@ -93,9 +93,9 @@ def task_conf(gpus: int, steps: int, warmup: int, extra_args: str, use_gpu: bool
     # 29500 may be the outer job's store, and the RCCL pre-flight takes the next port too
     conf["env"] = list(conf.get("env", [])) + [f"PYTHONPATH={REPO}", "OMP_NUM_THREADS=1",
                                                f"MASTER_PORT={_free_port_pair()}"]
-    if env:  # --env overrides (e.g. DSTACK_RCCL_PREFLIGHT=force|0 for the pre-flight A/B)
-        keys = {e.split("=", 1)[0] for e in env}
-        conf["env"] = [e for e in conf["env"] if e.split("=", 1)[0] not in keys] + list(env)
+    if env:  # --env overrides (e.g. DSTACK_RCCL_PREFLIGHT=force|0 for the pre-flight A/B); the last wins
+        last = {e.split("=", 1)[0]: e for e in env}
+        conf["env"] = [e for e in conf["env"] if e.split("=", 1)[0] not in last] + list(last.values())
     return parse_run_configuration(conf)
 
 
@@ -126,7 +126,7 @@ def one_run(client, conf, timeout: float) -> dict:
     stages, result = _parse_logs(logs)
     stamps = dict(timings)
     if stages:
-        stamps.update({k: v for k, v in stages.items() if v is not None})
+        stamps.update({k: v for k, v in stages.items() if isinstance(v, (int, float))})
     out = {"status": sub.status.value, "instance": sub.job_provisioning_data.instance_id if sub.job_provisioning_data else None,
            "stages_s": {}, "job_result": result}
     for name, a, b in STAGES:
@@ -137,6 +137,8 @@ def one_run(client, conf, timeout: float) -> dict:
         out["time_to_train_start_s"] = round(stamps["model_ready"] - stamps["submitted"], 4)
     if "first_log" in timings:
         out["time_to_first_log_s"] = round(timings["first_log"] - timings["submitted"], 4)
+    if stages and stages.get("first_step_split"):
+        out["first_step_split"] = stages["first_step_split"]
     pf = next((ln for ln in logs.splitlines() if ln.startswith("[dstack] RCCL pre-flight")), None)
     if pf:  # the runner's own line: mode, duration and exit of the probe
         out["preflight"] = pf[:200]
@@ -146,7 +148,8 @@ def one_run(client, conf, timeout: float) -> dict:
 
 
 def measure(gpus: int = 1, runs: int = 3, steps: int = 1, warmup: int = 1, tok_steps: int = 5, tok_warmup: int = 2,
-            extra_args: str = "", timeout: float = 600.0, gpu: str = "auto", fake_gpus: int = 0, env=()) -> dict:
+            extra_args: str = "", timeout: float = 600.0, gpu: str = "auto", fake_gpus: int = 0, env=(),
+            local_probe: bool = False) -> dict:
     """``fake_gpus`` > 0 (CPU tests): the agents see that many MI355X in a fake sysfs/KFD tree and
     the task's ranks run on the CPU over gloo."""
     for k in _LAUNCHER_ENV:
@@ -155,6 +158,8 @@ def measure(gpus: int = 1, runs: int = 3, steps: int = 1, warmup: int = 1, tok_s
     from dstack_amd.server.testing import ServerProcess
 
     srv_env = {"DSTACK_LOCAL_SHIM_PER_INSTANCE": "1"}
+    if local_probe:  # the shim hands dstack-probe to the runner (the example's RCCL pre-flight runs)
+        srv_env["DSTACK_LOCAL_GPU_PROBE"] = "1"
     if fake_gpus:
         import tempfile
 
@@ -205,11 +210,13 @@ def _interleaved(a) -> int:
     for _ in range(a.runs):
         for arm in arms:
             r = measure(a.gpus, 1, a.steps, a.warmup, 0, 0, a.extra_args, a.timeout, a.gpu, a.fake_gpus,
-                        [*a.env, arm])
-            per[arm].append({"first_step_s": r["stages_p50_s"].get("first_step_s"),
+                        [*a.env, arm], a.local_probe)
+            per[arm].append({"first_step_s": r["stages_p50_s"].get("first_step_s"), "stages_s": r["stages_p50_s"],
                              "time_to_first_step_s": r["time_to_first_step_p50_s"], "errors": r["errors"],
                              "preflight": next((x.get("preflight") for x in r["samples"] if x.get("preflight")),
-                                               None)})
+                                               None),
+                             "first_step_split": next((x.get("first_step_split") for x in r["samples"]
+                                                       if x.get("first_step_split")), None)})
     p50 = (lambda xs: round(statistics.median(xs), 4) if xs else None)
     out = {arm: {"first_step_p50_s": p50([x["first_step_s"] for x in v if x["first_step_s"] is not None]),
                  "time_to_first_step_p50_s": p50([x["time_to_first_step_s"] for x in v
@@ -232,13 +239,14 @@ def main():
     ap.add_argument("--gpu", choices=("auto", "yes", "no"), default="auto")
     ap.add_argument("--fake-gpus", type=int, default=0, help="CPU tests: agents see N fake MI355X (gloo ranks)")
     ap.add_argument("--env", action="append", default=[], help="KEY=VALUE for the task's env (repeatable)")
+    ap.add_argument("--local-probe", action="store_true", help="hand dstack-probe to the runner (pre-flight runs)")
     ap.add_argument("--interleave", default="", help="A/B: comma-separated env assignments, one arm each; the "
                                                      "runs alternate between the arms")
     a = ap.parse_args()
     if a.interleave:
         return _interleaved(a)
     r = measure(a.gpus, a.runs, a.steps, a.warmup, a.tok_steps, a.tok_warmup, a.extra_args, a.timeout, a.gpu,
-                a.fake_gpus, a.env)
+                a.fake_gpus, a.env, a.local_probe)
     print(json.dumps(r), flush=True)
     return 0 if not r["errors"] else 1
 

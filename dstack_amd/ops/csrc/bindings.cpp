@@ -62,6 +62,8 @@ bool dsa_fp8_rows_gemm_supported(int, int, int, int, int);
 hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
                              long, long, long, int, int, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
+hipError_t dsa_synthetic_tokens(const double*, const int64_t*, const int64_t*, const int64_t*, int64_t*, int64_t*,
+                                uint64_t, float, int, int, int, hipStream_t);
 hipError_t dsa_gemm_km_f32(const void*, const void*, void*, float*, int, int, int, long, long, long, long, int,
                            hipStream_t);
 hipError_t dsa_gemm_nt_swiglu_bwd(const void*, const void*, const void*, void*, void*, int, int, int, long, long,
@@ -589,6 +591,22 @@ void gemm_km_f32(torch::Tensor a, torch::Tensor b, torch::Tensor acc, c10::optio
         "gemm_km_f32");
 }
 
+// the bench's synthetic token stream (workloads/data.py, csrc/data.hip): out [n] int64, ws [n] int64
+void synthetic_tokens(torch::Tensor cdf, torch::Tensor perm, torch::Tensor pow_a, torch::Tensor geo_b,
+                      torch::Tensor out, torch::Tensor ws, int64_t key, double copy_p, int64_t row_len) {
+  TORCH_CHECK(cdf.is_cuda() && cdf.scalar_type() == torch::kFloat64 && cdf.is_contiguous(), "synthetic_tokens: cdf");
+  for (auto* t : {&perm, &pow_a, &geo_b, &out, &ws})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt64 && t->is_contiguous(),
+                "synthetic_tokens: int64 CUDA tensors expected");
+  const int64_t n = out.numel(), V = cdf.numel();
+  TORCH_CHECK(perm.numel() == V && ws.numel() >= n && pow_a.numel() > n && geo_b.numel() > n,
+              "synthetic_tokens: shape mismatch");
+  check(dsa_synthetic_tokens(cdf.data_ptr<double>(), perm.data_ptr<int64_t>(), pow_a.data_ptr<int64_t>(),
+                             geo_b.data_ptr<int64_t>(), out.data_ptr<int64_t>(), ws.data_ptr<int64_t>(), (uint64_t)key,
+                             (float)copy_p, (int)n, (int)row_len, (int)V, stream()),
+        "synthetic_tokens");
+}
+
 // gu = x w^T (w = [gate; up] [2F][K]) -> (gu [T][2F], a = silu(g) * u [T][F], a^T [F][T]); with
 // transposed = false a^T is not written (returned empty)
 std::vector<torch::Tensor> gemm_nt_swiglu(torch::Tensor x, torch::Tensor w, bool transposed) {
@@ -787,6 +805,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_swiglu", &gemm_nt_swiglu, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("transposed") = true);
   m.def("gemm_km", &gemm_km, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("out"), pybind11::arg("mode") = 0);
   m.def("gemm_km_supported", &gemm_km_supported);
+  m.def("synthetic_tokens", &synthetic_tokens);
   m.def("gemm_km_f32", &gemm_km_f32, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("acc"),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("mode") = 0);
   m.def("fp8_rows_gemm", &fp8_rows_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),

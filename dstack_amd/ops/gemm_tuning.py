@@ -77,13 +77,14 @@ def llama_shapes(cfg, tokens: int):
             (tokens, d, qkv), (tokens, d, 2 * cfg.ffn_dim), (tokens, d, cfg.vocab_size)]
 
 
-def prewarm(shapes, device):
+def prewarm(shapes, device, extra=None):
     """Start a thread that runs one ``a @ b.t()`` per shape on a side stream, so the library's
     first-call work -- hipBLASLt's handle and heuristics (0.17 s on the first GEMM of a process), and
     with ``use`` TunableOp mapping its saved selections onto hipBLASLt's solution list (1.1 s,
     profiles/first_step_r8b.txt, tools/diag/gemm_first_call.py), plus loading each selected kernel --
-    overlaps the model's initialisation instead of landing in the first forward.  Not while tuning.  Returns the thread (join it
-    before the first step) or None."""
+    overlaps the model's initialisation instead of landing in the first forward.  Not while tuning.  ``extra`` (a
+    callable) runs on the same thread afterwards: the first use of the data pipeline's kernels.  Returns the thread
+    (join it before the first step) or None."""
     import threading
 
     import torch
@@ -91,7 +92,7 @@ def prewarm(shapes, device):
     tunable = torch.cuda.tunable
     if device.type != "cuda" or (tunable.is_enabled() and tunable.tuning_is_enabled()):
         return None
-    if os.environ.get("DSTACK_AMD_GEMM_PREWARM", "1") == "0":
+    if os.environ.get("DSTACK_AMD_GEMM_PREWARM", "1") == "0" and not float(os.environ.get("DSTACK_AMD_ACT_POOL_GB", "0") or 0):
         return None
 
     def work():
@@ -108,6 +109,16 @@ def prewarm(shapes, device):
         # the side stream's operands (the LM-head pair alone is ~2 x 2 GiB at 8k tokens) would stay
         # reserved for the whole run, unusable by the default stream's training step
         torch.cuda.empty_cache()
+        # DSTACK_AMD_ACT_POOL_GB: reserve the first step's activation memory here, beside model
+        # init, as one default-stream segment the caching allocator then splits (the first forward
+        # otherwise grows the pool with hipMalloc calls inside the timed-to-first-step path)
+        gb = float(os.environ.get("DSTACK_AMD_ACT_POOL_GB", "0") or 0)
+        if gb > 0:
+            pool = torch.empty(int(gb * 2**30), dtype=torch.uint8, device=device)
+            del pool
+        if extra is not None:
+            extra()
+            torch.cuda.current_stream(device).synchronize()
 
     th = threading.Thread(target=work, name="gemm-prewarm", daemon=True)
     th.start()

@@ -131,6 +131,8 @@ class Trainer:
         else:
             raise ValueError(f"unknown data kind {data!r}")
         self._i = 0
+        self.trace_next_step = False
+        self.last_split = None
 
     def batch(self):
         if self.stream is not None:
@@ -165,15 +167,34 @@ class Trainer:
         only for the last micro-batch so it overlaps that backward."""
         # set before backward: with optimizer-in-backward AdamW runs per bucket during it
         self.opt.lr = self.lr_at(self.opt.step_count + 1)
+        trace = self.trace_next_step  # diagnostic: synchronised split of this step (first_step_split)
+        self.trace_next_step = False
+        split = {"batch": 0.0, "fwd": 0.0, "bwd": 0.0, "opt": 0.0}
+
+        def mark(k, t0):
+            if trace:
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize(self.device)
+                split[k] += time.time() - t0
+            return time.time()
+
         self.opt.zero_grad()
         total = None
         for i in range(self.grad_accum):
+            t0 = time.time()
             tokens, targets = self.batch()
+            t0 = mark("batch", t0)
             self.opt.sync_grads = i == self.grad_accum - 1
             loss = self.model.loss(tokens, targets)
+            t0 = mark("fwd", t0)
             (loss / self.grad_accum if self.grad_accum > 1 else loss).backward()
+            mark("bwd", t0)
             total = loss.detach() if total is None else total + loss.detach()
+        t0 = time.time()
         self.opt.step()
+        if trace:
+            mark("opt", t0)
+            self.last_split = {k: round(v, 4) for k, v in split.items()}
         return total / self.grad_accum
 
     # ---- checkpoints: safetensors, one optimizer shard per rank, written to a directory that is
@@ -356,9 +377,15 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
         if checkpoint_dir and save_every and tr.opt.step_count % save_every == 0:
             tr.save_checkpoint(checkpoint_dir)
 
+    # DSTACK_AMD_FIRST_STEP_SPLIT=1: the first step synchronises around its batches / forwards /
+    # backwards / optimizer step and reports the sums (diagnostic: it slows that step slightly)
+    tr.trace_next_step = os.environ.get("DSTACK_AMD_FIRST_STEP_SPLIT", "0") == "1"
+
     def _first_step_done():
         if "first_step_done" not in stages:
             stages["first_step_done"] = time.time()
+            if tr.last_split is not None:
+                stages["first_step_split"] = tr.last_split
             if env.rank == 0:
                 print("[train] stages " + json.dumps(stages), flush=True)
 

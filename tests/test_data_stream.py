@@ -58,3 +58,20 @@ def test_zero_output_head_starts_at_ln_vocab():
     with torch.no_grad():
         loss = m.loss(tok[:, :-1], tok[:, 1:]).item()
     assert abs(loss - math.log(cfg.vocab_size)) < 1e-4
+
+
+def test_splitmix64_matches_uint64_arithmetic():
+    """The int64 torch form of splitmix64 (wrap-around multiply, logical shifts) equals the uint64
+    definition that ops/csrc/data.hip computes."""
+    from dstack_amd.workloads.data import _splitmix64
+
+    def ref(z):
+        m = (1 << 64) - 1
+        z = (z + 0x9E3779B97F4A7C15) & m
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+        return z ^ (z >> 31)
+
+    xs = [0, 1, 2, 12345, (1 << 40) + 7, (1 << 62) + 3, (1 << 63) - 1]
+    got = _splitmix64(torch.tensor(xs, dtype=torch.int64)).tolist()
+    assert [g & ((1 << 64) - 1) for g in got] == [ref(x) for x in xs]

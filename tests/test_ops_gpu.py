@@ -794,3 +794,16 @@ def test_attention_head_dim_64_runs_sdpa_with_a_warning(gpu):
     assert ((o.float() - want).norm() / want.norm()).item() < 2e-2
     o.float().square().sum().backward()
     assert qkv.grad is not None and torch.isfinite(qkv.grad).all()
+
+
+@pytest.mark.parametrize("mb,S", [(1, 8192), (2, 1023), (1, 64)])
+def test_synthetic_tokens_kernel_matches_cpu_reference(gpu, mb, S):
+    """The bench's data stream generated by the HIP kernel (csrc/data.hip) is bit-identical to the
+    torch definition on the CPU (workloads/data.py), for several (seed, index) keys."""
+    from dstack_amd.workloads.data import SyntheticLM
+
+    V = 128256
+    g, c = SyntheticLM(V, S, mb, gpu, seed=3), SyntheticLM(V, S, mb, "cpu", seed=3)
+    for index in (0, 1, 17, 1 << 40):
+        a, b = g.tokens(index).cpu(), c.tokens(index)
+        assert a.shape == (mb, S + 1) and torch.equal(a, b), index
