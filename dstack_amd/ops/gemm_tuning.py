@@ -39,12 +39,16 @@ def setup(mode: Optional[str] = None, device_index: int = 0, kind: str = "train"
     if not torch.cuda.is_available() or torch.version.hip is None:
         return "off"
     mode = (mode or os.environ.get("DSTACK_AMD_GEMM_TUNING") or ("off" if kind == "train" else "use")).lower()
-    arch = torch.cuda.get_device_properties(device_index).gcnArchName.split(":")[0]
-    path = results_path(arch, kind)
     tunable = torch.cuda.tunable
     if mode == "off":
-        tunable.enable(False)
+        # TunableOp is off unless PYTORCH_TUNABLEOP_ENABLED says otherwise; touching it (86-140 ms:
+        # its context is created on first use) or the device properties (106-124 ms on first call)
+        # sat on every job's start-up path (tools/diag/init_split.py, profiles/init_split_r9n.txt)
+        if os.environ.get("PYTORCH_TUNABLEOP_ENABLED", "0") not in ("0", ""):
+            tunable.enable(False)
         return "off"
+    arch = torch.cuda.get_device_properties(device_index).gcnArchName.split(":")[0]
+    path = results_path(arch, kind)
     if mode == "tune":
         path.parent.mkdir(parents=True, exist_ok=True)
         tunable.enable(True)

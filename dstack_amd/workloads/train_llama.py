@@ -103,9 +103,16 @@ class Trainer:
         self.grad_accum = grad_accum
         self.device = device
         dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
-        with torch.device(device):
-            model = Llama(self.cfg)
-        model.to(dtype)
+        # parameters allocated in their final dtype: constructing in fp32 and converting allocated
+        # and copied twice the model (27-66 ms of the start-up, profiles/init_split_r9n.txt)
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(dtype)
+        try:
+            with torch.device(device):
+                model = Llama(self.cfg)
+        finally:
+            torch.set_default_dtype(prev)
+        model.to(dtype)  # (a no-op unless a submodule pins its own dtype)
         model.init_weights(seed=seed, lm_head_std=lm_head_std)
         self.model = model
         self.opt = ZeroOptimizer(model, lr=lr, bucket_numel=bucket_numel, clip_grad_norm=clip_grad_norm)
@@ -354,7 +361,10 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     t0 = time.time()
     tr = Trainer(model, seq_len, micro_batch, device, grad_accum=grad_accum, lr=lr, lr_warmup=lr_warmup,
                  lr_decay_steps=lr_decay_steps, clip_grad_norm=clip_grad_norm, data=data)
-    if warm is not None:
+    # DSTACK_AMD_PREWARM_JOIN=late: the first step starts while the prewarm thread still loads the
+    # later (backward) GEMMs' kernels; joined after the first step instead of before it
+    late_join = os.environ.get("DSTACK_AMD_PREWARM_JOIN", "early") == "late"
+    if warm is not None and not late_join:
         warm.join()
     stages["model_ready"] = time.time()
     if env.rank == 0:
@@ -382,6 +392,8 @@ def run(model: str, seq_len: int, micro_batch: int, steps: int, warmup: int, log
     tr.trace_next_step = os.environ.get("DSTACK_AMD_FIRST_STEP_SPLIT", "0") == "1"
 
     def _first_step_done():
+        if warm is not None and late_join:
+            warm.join()
         if "first_step_done" not in stages:
             stages["first_step_done"] = time.time()
             if tr.last_split is not None:
