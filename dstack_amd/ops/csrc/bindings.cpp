@@ -62,6 +62,7 @@ bool dsa_fp8_rows_gemm_supported(int, int, int, int, int);
 hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
                              long, long, long, int, int, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
+hipError_t dsa_cu_hog(int, int, int, double, int*, hipStream_t);
 hipError_t dsa_synthetic_tokens(const double*, const int64_t*, const int64_t*, const int64_t*, int64_t*, int64_t*,
                                 uint64_t, float, int, int, int, hipStream_t);
 hipError_t dsa_gemm_km_f32(const void*, const void*, void*, float*, int, int, int, long, long, long, long, int,
@@ -591,6 +592,12 @@ void gemm_km_f32(torch::Tensor a, torch::Tensor b, torch::Tensor acc, c10::optio
         "gemm_km_f32");
 }
 
+// diagnostic: hold `blocks` workgroup slots for `us` microseconds on the current stream
+void cu_hog(int64_t blocks, int64_t threads, int64_t lds_bytes, double us, torch::Tensor sink) {
+  TORCH_CHECK(sink.is_cuda() && sink.scalar_type() == torch::kInt32, "cu_hog: int32 CUDA sink");
+  check(dsa_cu_hog((int)blocks, (int)threads, (int)lds_bytes, us, sink.data_ptr<int>(), stream()), "cu_hog");
+}
+
 // the bench's synthetic token stream (workloads/data.py, csrc/data.hip): out [n] int64, ws [n] int64
 void synthetic_tokens(torch::Tensor cdf, torch::Tensor perm, torch::Tensor pow_a, torch::Tensor geo_b,
                       torch::Tensor out, torch::Tensor ws, int64_t key, double copy_p, int64_t row_len) {
@@ -806,6 +813,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_km", &gemm_km, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("out"), pybind11::arg("mode") = 0);
   m.def("gemm_km_supported", &gemm_km_supported);
   m.def("synthetic_tokens", &synthetic_tokens);
+  m.def("cu_hog", &cu_hog);
   m.def("gemm_km_f32", &gemm_km_f32, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("acc"),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("mode") = 0);
   m.def("fp8_rows_gemm", &fp8_rows_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),

@@ -933,3 +933,32 @@ extern "C" hipError_t dsa_adamw(void* param, const void* grad, float* master, fl
       (bf16_t*)param, (const bf16_t*)grad, master, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------
+// Diagnostic: occupy `blocks` workgroup slots (threads x LDS bytes each) for `us` microseconds of
+// wall clock (s_memrealtime, 100 MHz), the way a collective's kernel holds CUs beside compute
+// (tools/diag/cu_hog.py: what a persistent GEMM pays when some CUs are taken).  Every wave exits
+// when the time is up.
+// ------------------------------------------------------------------------------------------------
+__global__ void cu_hog_kernel(unsigned long long ticks, int* sink) {
+  extern __shared__ int hog_lds[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int acc = threadIdx.x;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    hog_lds[threadIdx.x & 255] = acc;
+    acc += hog_lds[(threadIdx.x + 1) & 255];
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (acc == 0x7fffffff) sink[0] = acc;  // keep the loop; practically never true
+}
+
+extern "C" hipError_t dsa_cu_hog(int blocks, int threads, int lds_bytes, double us, int* sink, hipStream_t st) {
+  if (blocks <= 0 || threads <= 0 || threads > 1024 || lds_bytes < 1024 || lds_bytes > 160 * 1024 || us <= 0 ||
+      us > 1e6)
+    return hipErrorInvalidValue;
+  if (lds_bytes > 64 * 1024)
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&cu_hog_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
+  cu_hog_kernel<<<blocks, threads, lds_bytes, st>>>((unsigned long long)(us * 100.0), sink);
+  return hipGetLastError();
+}

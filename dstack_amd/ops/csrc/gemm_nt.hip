@@ -43,6 +43,8 @@
 // k-half and the 4-row step of a read are immediate offsets; each 16-column block has one address.
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "mfma_tiles.h"
 
 using namespace dsa;
@@ -86,6 +88,8 @@ struct NTArgs {
   int F;          // SwiGLU width (ld of a, columns of gu / 2)
   int group;      // tile-order group height (tile rows)
   int wg_per_xcd; // workgroups per XCD (gridDim / 8 when persistent)
+  int* queue;     // dynamic tile order (persistent grids): [0..7] per-XCD tile counters, [8] exited
+                  // workgroups (the last one re-zeroes the slot); null: the static order
   unsigned long long* trace;  // TRACE builds: per-phase s_memtime stamps of workgroup 0
 };
 
@@ -282,8 +286,37 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   const int per = ntiles >> 3, rem = ntiles & 7;
   const int cnt = per + (xcd < rem ? 1 : 0), start = xcd * per + (xcd < rem ? xcd : rem);
   const int stride = p.wg_per_xcd;
-  int local = xj;
-  if (local >= cnt) return;
+  // Dynamic tile order (p.queue): instead of every (wg_per_xcd)-th tile of its XCD's slice, a
+  // workgroup claims the slice's next tile from a per-XCD counter, one tile ahead (the claim for
+  // tile i+2 is made at the top of tile i and read at its end, many barriers later, through two
+  // LDS slots at the top of the 160 KiB that the plain / barrier-free epilogues never touch).
+  // With some CUs held by a concurrent kernel -- RCCL's reduce-scatter / all-gather blocks beside
+  // ZeRO-1's backward, the side-stream AdamW -- the static order waits for the late workgroups'
+  // share; claimed tiles go to whoever is free (tools/diag/cu_hog.py).
+  int* const q = p.queue;
+  volatile int* qslot = reinterpret_cast<volatile int*>(smem + NT_LDS - 64);
+  int local = xj, next = xj + stride, par = 0;
+  if (q) {
+    if (w == 0 && lane == 0) {
+      const int a0 = atomicAdd(q + xcd, 1);
+      qslot[0] = a0;
+      qslot[1] = a0 < cnt ? atomicAdd(q + xcd, 1) : cnt;
+    }
+    __syncthreads();
+    local = __builtin_amdgcn_readfirstlane(qslot[0]);  // (uniform: the DMA bases are SGPRs)
+    next = __builtin_amdgcn_readfirstlane(qslot[1]);
+    __syncthreads();
+  }
+  auto leave = [&]() {  // the last workgroup to leave re-zeroes the counters for the slot's next use
+    if (q && w == 0 && lane == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) q[i] = 0;
+    }
+  };
+  if (local >= cnt) {
+    leave();
+    return;
+  }
   int m0, nb0;
   nt_tile_origin(p, start + local, m0, nb0);
   const int nk = p.K / NT_BK;
@@ -390,8 +423,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     if (!STAGGERED || local == xj) {
       if (wr == 1) nt_barrier();  // group 1 runs one barrier behind
     }
-    const int next = local + stride;
     const bool has_next = next < cnt;
+    if (q && w == 0 && lane == 0) qslot[par] = has_next ? atomicAdd(q + xcd, 1) : cnt;  // the tile after next
     int m1 = 0, nb1 = 0;
     if (has_next) nt_tile_origin(p, start + next, m1, nb1);
 #pragma unroll
@@ -751,6 +784,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       if constexpr (STAGGERED) {
         if (wr == 0) nt_barrier();  // equal barrier counts for both groups at exit
       }
+      leave();
       break;
     }
     if constexpr (!OVERLAP) {
@@ -761,6 +795,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       nt_barrier();
     }
     local = next;
+    next = q ? __builtin_amdgcn_readfirstlane(qslot[par]) : next + stride;
+    par ^= 1;
     m0 = m1;
     nb0 = nb1;
   }
@@ -795,6 +831,30 @@ int nt_cus() {
 
 // One workgroup per CU (128 KiB ring): a grid of min(tiles, CUs rounded down to a multiple of 8)
 // workgroups that loop over their XCD's tiles.
+// Dynamic-order counter slots: one 64-byte slot per launch from a ring per device, zeroed once; a
+// launch's last workgroup re-zeroes its slot, which is reused 1024 launches later.
+constexpr int NT_QSLOTS = 1024;
+int* nt_queue_slot(hipStream_t st) {
+  static int* ring[64] = {nullptr};
+  static std::atomic<unsigned> seq[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (!ring[dev]) {
+    int* r = nullptr;
+    if (hipMalloc(&r, NT_QSLOTS * 64) != hipSuccess) return nullptr;
+    if (hipMemset(r, 0, NT_QSLOTS * 64) != hipSuccess) return nullptr;
+    ring[dev] = r;
+  }
+  return ring[dev] + (seq[dev].fetch_add(1) % NT_QSLOTS) * 16;
+}
+
+// EPIs whose epilogue stages through LDS (the SwiGLU forms with transposed copies) keep the
+// static order: the dynamic order's broadcast slots sit at the top of the LDS they use.
+template <int EPI>
+constexpr bool nt_dynamic_ok() { return EPI != EPI_SWIGLU && EPI != EPI_SWIGLU_BWD; }
+
 template <int EPI, bool TRACE = false, bool KM = false>
 hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
   static bool attr = false;
@@ -806,9 +866,21 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
   const int cap = (nt_cus() / 8) * 8;
   int grid = tiles;
   a.wg_per_xcd = 1 << 30;  // one tile per workgroup
-  if (tiles > cap && cap >= 8) {
+  // DSTACK_AMD_GEMM_NT_PERSISTENT=0: one workgroup per tile even when the tiles outnumber the CUs
+  // (A/B against CUs held by a concurrent kernel, tools/diag/cu_hog.py)
+  static const bool persistent = [] {
+    const char* v = getenv("DSTACK_AMD_GEMM_NT_PERSISTENT");
+    return !(v && atoi(v) == 0);
+  }();
+  // DSTACK_AMD_GEMM_NT_DYNAMIC=1: claimed (dynamic) tile order; 0 (default): the static order
+  static const bool dynamic = [] {
+    const char* v = getenv("DSTACK_AMD_GEMM_NT_DYNAMIC");
+    return v && atoi(v) == 1;
+  }();
+  if (persistent && tiles > cap && cap >= 8) {
     grid = cap;
     a.wg_per_xcd = cap / 8;
+    if (dynamic && !TRACE && nt_dynamic_ok<EPI>()) a.queue = nt_queue_slot(st);
   }
   if (const char* g = getenv("DSTACK_AMD_GEMM_NT_GROUP")) a.group = atoi(g) > 0 ? atoi(g) : a.group;
   gemm_nt_kernel<EPI, TRACE, KM><<<grid, 512, NT_LDS, st>>>(a);

@@ -630,6 +630,49 @@ def test_gemm_nt_swiglu_bwd_epilogue_matches_fp32(gpu):
     assert torch.equal(dguT, dgu.t().contiguous())
 
 
+# the step's own reduction lengths (K = 4096 model dim, 14336 FFN dim, 8192 tokens for the weight
+# gradients): the unit tests above stop at K <= 1024; long K exercises the ring's steady state and
+# the accumulation error over many K-tiles
+@pytest.mark.parametrize("M,N,K", [(2048, 4096, 4096), (1024, 4096, 14336)])
+def test_gemm_nt_long_k_matches_fp32(gpu, M, N, K):
+    C = _ext.require()
+    a, b = _rand(M, K, device=gpu, scale=0.5), _rand(N, K, device=gpu, seed=1, scale=0.5)
+    out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    C.gemm_nt(a, b, out, False)
+    ref_ = a.float() @ b.float().t()
+    assert ((out.float() - ref_).norm() / ref_.norm()).item() < 5e-3
+
+
+def test_gemm_nt_swiglu_epilogues_long_k(gpu):
+    """The fused MLP epilogues at the step's K: gate/up (K = 4096) with SwiGLU, and the down
+    projection's input gradient (K = 4096, F = 14336 columns) with the SwiGLU backward."""
+    C = _ext.require()
+    T, D, F = 1024, 4096, 1792
+    x, w = _rand(T, D, device=gpu), _rand(2 * F, D, device=gpu, seed=1, scale=0.02)
+    gu, a, _ = C.gemm_nt_swiglu(x, w, False)
+    gur = x.float() @ w.float().t()
+    assert ((gu.float() - gur).norm() / gur.norm()).item() < 5e-3
+    ar = ref.swiglu(gur)
+    assert ((a.float() - ar).norm() / ar.norm()).item() < 1e-2
+    dy, wdT = _rand(T, D, device=gpu, seed=3), _rand(F, D, device=gpu, seed=4, scale=0.02)
+    dgu, _ = C.gemm_nt_swiglu_bwd(dy, wdT, gu, False)
+    g2 = gu.float().requires_grad_()
+    ref.swiglu(g2).backward(dy.float() @ wdT.float().t())
+    assert ((dgu.float() - g2.grad).norm() / g2.grad.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("M,N", [(4096, 4096), (4096, 14336)])
+def test_gemm_km_k8192_matches_fp32(gpu, M, N):
+    """Weight gradients at the bench's 8192 tokens per micro-batch (KM form, ds_read_b64_tr_b16)."""
+    C = _ext.require()
+    K = 8192
+    a, b = _rand(K, M, device=gpu, scale=0.5), _rand(K, N, device=gpu, seed=1, scale=0.5)
+    out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    C.gemm_km(a, b, out, 0)
+    ref_ = a.float().t() @ b.float()
+    assert ((out.float() - ref_).norm() / ref_.norm()).item() < 5e-3
+
+
 @pytest.mark.parametrize("M,N,K,accumulate", [(256, 256, 128, False), (768, 512, 384, True),
                                                (2304, 9472, 256, False), (1024, 4352, 1024, True)])
 def test_gemm_km_matches_fp32(gpu, M, N, K, accumulate):
