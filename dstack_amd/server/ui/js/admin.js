@@ -1,5 +1,6 @@
-// Projects (members, backends: form built from the server's field descriptors with a credentials
-// check and region picker, or YAML), users, secrets.
+// Projects (members with user suggestions, backends: form built from the server's field descriptors
+// with a credentials check and region picker, or YAML; the project's gateways; the CLI set-up
+// command), users, secrets.
 Object.assign(VIEWS, {
   async projects(name, tab) {
     if (name) return VIEWS.project(name, tab);
@@ -15,7 +16,7 @@ Object.assign(VIEWS, {
     const p = await api(`/api/projects/${encodeURIComponent(name)}/get`);
     $("#main").innerHTML = `<h3><a href="#projects" class="muted">projects</a> / ${esc(name)}</h3>
       <div class="muted">owner ${esc(p.owner.username)} · created ${ago(p.created_at)}</div>
-      ${tabs("ptabs", ["members", "backends", "settings"], tab)}<div id="tab"></div>`;
+      ${tabs("ptabs", ["members", "backends", "gateways", "cli", "settings"], tab)}<div id="tab"></div>`;
     bindTabs("ptabs", t => location.hash = `#projects/${encodeURIComponent(name)}/${t}`);
     return (PROJECT_TABS[tab] || PROJECT_TABS.members)(p, name);
   },
@@ -60,10 +61,12 @@ Object.assign(VIEWS, {
 const PROJECT_TABS = {
   members(p, name) {
     const roles = ["admin", "manager", "user"];
-    const memberRow = (u = "", r = "user") => `<div class="row mrow"><input class="mu" value="${esc(u)}" placeholder="username">
+    const memberRow = (u = "", r = "user") => `<div class="row mrow"><input class="mu" list="known-users" value="${esc(u)}" placeholder="username">
       <select class="mr">${roles.map(x => `<option ${x === r ? "selected" : ""}>${x}</option>`).join("")}</select><a class="muted rm">[remove]</a></div>`;
-    $("#tab").innerHTML = `<div id="members">${p.members.map(m => memberRow(m.user.username, m.project_role)).join("")}</div>
+    $("#tab").innerHTML = `<datalist id="known-users"></datalist><div id="members">${p.members.map(m => memberRow(m.user.username, m.project_role)).join("")}</div>
       <div class="row"><button id="addm">Add member</button><button class="primary" id="savem">Save members</button></div>`;
+    // user suggestions (admins can list users; others type the name)
+    api("/api/users/list").then(us => { $("#known-users").innerHTML = us.map(u => `<option value="${esc(u.username)}">`).join(""); }).catch(() => {});
     const bindRm = () => $$("a.rm").forEach(a => a.onclick = () => a.closest(".mrow").remove());
     bindRm();
     $("#addm").onclick = () => { $("#members").insertAdjacentHTML("beforeend", memberRow()); bindRm(); };
@@ -111,6 +114,39 @@ const PROJECT_TABS = {
       $("#addb").textContent = "Update backend";
       $("#addb").onclick = () => act(() => api(B("update_yaml"), { config_yaml: $("#by").value }));
     });
+  },
+
+  async gateways(p, name) {
+    // the project's gateways (service endpoints with TLS and autoscaling), default first; a new one
+    // from a short form (the full configuration is on the apply page)
+    const G = (x) => `/api/project/${encodeURIComponent(name)}/gateways/${x}`;
+    const gws = await api(G("list"));
+    const backends = (p.backends || []).map(b => b.name || b);
+    $("#tab").innerHTML = table(["gateway", "backend / region", "hostname", "wildcard domain", "default", "status", ""], gws.map(g => [
+        `<a href="#gateways/${encodeURIComponent(g.name)}">${esc(g.name)}</a>`, `${esc(g.backend)} / ${esc(g.region)}`, esc(g.hostname || ""),
+        esc(g.wildcard_domain || ""), g.default ? "yes" : `<a data-g="${esc(g.name)}" class="defg muted">[make default]</a>`, st(g.status),
+        `<a data-g="${esc(g.name)}" class="delg muted">[delete]</a>`])) +
+      `<h4>Add a gateway</h4><div class="row"><input id="gn" placeholder="name"><select id="gb">${backends.map(b => `<option>${esc(b)}</option>`).join("")}</select>
+        <input id="gr" placeholder="region"><input id="gd" placeholder="*.example.com domain (optional)"><label><input type="checkbox" id="gdef"> default</label>
+        <button class="primary" id="gadd">Create</button><span id="gerr" class="err"></span></div>`;
+    $$("a.defg").forEach(a => a.onclick = () => act(() => api(G("set_default"), { name: a.dataset.g })));
+    $$("a.delg").forEach(a => a.onclick = () => act(() => api(G("delete"), { names: [a.dataset.g] }), `Delete gateway ${a.dataset.g}?`));
+    $("#gadd").onclick = async () => {
+      const configuration = { type: "gateway", name: $("#gn").value.trim() || null, backend: $("#gb").value, region: $("#gr").value.trim(),
+                              default: $("#gdef").checked };
+      if ($("#gd").value.trim()) configuration.domain = $("#gd").value.trim();
+      try { await api(G("create"), { configuration }); route(); } catch (e) { $("#gerr").textContent = e.message; }
+    };
+  },
+
+  async cli(p, name) {
+    // the CLI / Python API set-up for this project: the same server URL and the signed-in user's token
+    const url = location.origin;
+    const cmd = `dstack config --url ${url} --project ${name} --token ${S.token}`;
+    $("#tab").innerHTML = `<p class="muted">Run this to point the CLI at this project (it writes ~/.dstack/config.yml):</p>
+      <pre id="clicmd">${esc(cmd)}</pre><div class="row"><button id="copy">Copy</button><span id="copied" class="muted"></span></div>
+      <p class="muted">Python API:</p><pre>${esc(`from dstack_amd.api import Client\nclient = Client.from_config(project_name="${name}")\nprint([r.name for r in client.runs.list()])`)}</pre>`;
+    $("#copy").onclick = () => navigator.clipboard.writeText(cmd).then(() => { $("#copied").textContent = "copied"; }).catch(e => alert(e.message));
   },
 
   settings(p, name) {

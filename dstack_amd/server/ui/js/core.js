@@ -1,6 +1,7 @@
 // dstack-amd web UI core: REST client, router, shared widgets (tables, tabs, charts, forms).
-// Views register themselves in VIEWS (one module per area: runs.js, fleets.js, resources.js, admin.js).
-const PAGES = ["runs", "apply", "offers", "fleets", "instances", "volumes", "gateways", "models", "projects", "users", "secrets"];
+// Views register themselves in VIEWS (one module per area: dashboard.js, runs.js, fleets.js, resources.js,
+// admin.js).
+const PAGES = ["home", "runs", "apply", "offers", "fleets", "instances", "volumes", "gateways", "models", "projects", "users", "secrets"];
 const S = { token: localStorage.getItem("dstack_token"), project: localStorage.getItem("dstack_project") || "main", me: null };
 const VIEWS = {};
 const $ = (s) => document.querySelector(s);
@@ -46,9 +47,9 @@ async function boot() {
 
 function route() {
   clearTimers();
-  const [page, ...args] = (location.hash.slice(1) || "runs").split("/");
+  const [page, ...args] = (location.hash.slice(1) || "home").split("/");
   $("#nav").innerHTML = PAGES.map(p => `<a href="#${p}" class="${p === page ? "active" : ""}">${p}</a>`).join("") + `<a onclick="logout()">sign out</a>`;
-  (VIEWS[page] || VIEWS.runs)(...args.map(decodeURIComponent)).catch(e => $("#main").innerHTML = `<p class="err">${esc(e.message)}</p>`);
+  (VIEWS[page] || VIEWS.home)(...args.map(decodeURIComponent)).catch(e => $("#main").innerHTML = `<p class="err">${esc(e.message)}</p>`);
 }
 
 // ---- widgets ---------------------------------------------------------------------------------

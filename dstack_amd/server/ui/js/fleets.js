@@ -22,7 +22,7 @@ Object.assign(VIEWS, {
       return [esc(f.name), conf.ssh_config ? "ssh" : "cloud", live.length, gpus, `${busy}/${blocks}`,
               [...new Set(live.map(i => i.backend))].map(esc).join(", "), st(f.status), ago(f.created_at)];
     });
-    $("#main").innerHTML = `<h3>Fleets</h3><div class="row"><a href="#apply" class="muted">+ new fleet (YAML)</a></div>` +
+    $("#main").innerHTML = `<h3>Fleets</h3><div class="row"><a href="#newfleet" class="muted">+ add SSH hosts</a> <a href="#apply" class="muted">+ new fleet (YAML)</a></div>` +
       table(["fleet", "kind", "instances", "GPUs", "busy blocks", "backends", "status", "created"], rows, true);
     bindRows(fleets, f => location.hash = "#fleets/" + encodeURIComponent(f.name));
   },

@@ -250,7 +250,10 @@ def test_web_ui_served(client):
     # management views over the same API: instances, members editor, backends from YAML, metrics charts
     for needle in ("/api/instances/list", "set_members", "backends/${x}", "create_yaml", "metrics/job/", "prev_run_id",
                    "fleets/delete_instances", "users/refresh_token", "form_schema", "config_values", "descending: true",
-                   "fleet_ids", "job_submissions"):
+                   "fleet_ids", "job_submissions",
+                   # overview, SSH-fleet form, project gateways / CLI tabs, member suggestions
+                   "home()", "newfleet()", 'P("fleets/get_plan")', 'P("fleets/create")', "dstack config --url",
+                   'G("set_default")', "known-users"):
         assert needle in text, needle
 
 
