@@ -380,12 +380,13 @@ def test_service_through_local_gateway(tmp_path):
         assert body is not None and "Directory listing" in body
 
 
+@pytest.mark.timeout(1600)  # a sanitizer build from scratch beside a loaded parallel run
 @pytest.mark.parametrize("target", ["test", "test-tsan", "test-asan"])
 def test_native_unit_tests(target):
     """C++ unit tests of the agents (JSON, log history, xGMI placement, GPU lock, HTTP), plain and
     under ThreadSanitizer / AddressSanitizer+UBSan (host code; the Go reference runs -race)."""
     r = subprocess.run(["make", "-C", os.path.join(REPO, "native"), target], capture_output=True, text=True,
-                       timeout=600)
+                       timeout=1500)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
