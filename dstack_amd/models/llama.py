@@ -96,9 +96,7 @@ class DecoderLayer(nn.Module):
             h = ops.rms_norm(x, self.attn_norm, cfg.norm_eps)
         else:
             x, h = ops.add_rms_norm(x, delta, self.attn_norm, cfg.norm_eps)
-        qkv = ops.linear(h, self.wqkv)
-        qkv = ops.rope(qkv, cos, sin, cfg.n_heads + cfg.n_kv_heads, hd)
-        o = ops.attention(qkv, cfg.n_heads, cfg.n_kv_heads, causal=True)
+        o = ops.qkv_rope_attention(h, self.wqkv, cos, sin, cfg.n_heads, cfg.n_kv_heads)
         attn_out = ops.linear(o, self.wo)
         x, h = ops.add_rms_norm(x, attn_out, self.ffn_norm, cfg.norm_eps)
         return x, ops.swiglu_mlp(h, self.wgu, self.wdown)

@@ -9,8 +9,8 @@ a training job (``python -m dstack_amd.ops.build``) -- does not import torch whe
 already current.
 """
 
-_OPS = ("adamw_", "add_rms_norm", "attention", "cross_entropy", "embedding", "linear", "rms_norm", "rope",
-        "swiglu", "swiglu_mlp", "weight_grad")
+_OPS = ("adamw_", "add_rms_norm", "attention", "cross_entropy", "embedding", "linear", "qkv_rope_attention",
+        "rms_norm", "rope", "swiglu", "swiglu_mlp", "weight_grad")
 
 
 def __getattr__(name):

@@ -27,7 +27,7 @@ hipError_t dsa_embedding_bwd(const void*, const int64_t*, const int64_t*, void*,
 hipError_t dsa_fa_fwd(const void*, void*, float*, int, int, int, int, int, float, int, hipStream_t);
 size_t dsa_fa_bwd_workspace(int, int, int);
 hipError_t dsa_fa_bwd(const void*, const void*, const void*, const float*, void*, void*, int, int, int, int,
-                      int, float, int, hipStream_t);
+                      int, float, int, const float*, const float*, hipStream_t);
 int dsa_paged_page_size();
 hipError_t dsa_rope_cache_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int,
                                 int, int, float, float, const float*, const float*, hipStream_t);
@@ -51,6 +51,9 @@ hipError_t dsa_gemv_fp8(const void*, long, const void*, const float*, void*, lon
 hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 bool dsa_gemm_nt_supported(int, int, int);
 hipError_t dsa_gemm_nt(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
+bool dsa_gemm_nt_rope_supported(int, int, int, int, int);
+hipError_t dsa_gemm_nt_rope(const void*, const void*, void*, const float*, const float*, int, int, int, long, long,
+                            long, int, int, hipStream_t);
 bool dsa_gemm_nt_swiglu_supported(int, int, int);
 hipError_t dsa_gemm_nt_trace(const void*, const void*, void*, int, int, int, unsigned long long*, hipStream_t);
 hipError_t dsa_gemm_nt_swiglu(const void*, const void*, void*, void*, void*, int, int, int, long, long, hipStream_t);
@@ -333,17 +336,31 @@ std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor qkv, int64_t H, int64_t 
   return {out, lse};
 }
 
+// rope_cos / rope_sin ([>= S, 64] fp32, optional): q and k of `qkv` were rotated by RoPE; the
+// returned gradient is w.r.t. the unrotated projection (the RoPE backward fused in)
 torch::Tensor flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H,
-                             int64_t KVH, bool causal) {
+                             int64_t KVH, bool causal, c10::optional<torch::Tensor> rope_cos,
+                             c10::optional<torch::Tensor> rope_sin) {
   check_bf16(dout, "dout");
   check_bf16(qkv, "qkv");
   check_bf16(out, "out");
   const int B = qkv.size(0), S = qkv.size(1);
   const int D = qkv.size(2) / (H + 2 * KVH);
+  const float *rc = nullptr, *rs = nullptr;
+  TORCH_CHECK(rope_cos.has_value() == rope_sin.has_value(), "flash_attn_bwd: rope_cos and rope_sin go together");
+  if (rope_cos.has_value()) {
+    for (const auto& t : {*rope_cos, *rope_sin}) {
+      TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous() && t.dim() == 2 &&
+                      t.size(0) >= S && t.size(1) == D / 2,
+                  "flash_attn_bwd: rope tables must be contiguous fp32 [>= S, head_dim / 2]");
+    }
+    rc = rope_cos->data_ptr<float>();
+    rs = rope_sin->data_ptr<float>();
+  }
   auto dqkv = torch::empty_like(qkv);
   auto ws = torch::empty({(int64_t)dsa_fa_bwd_workspace(B, S, H)}, qkv.options().dtype(torch::kUInt8));
   check(dsa_fa_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), dqkv.data_ptr(),
-                   ws.data_ptr(), B, S, H, KVH, D, 1.0f / std::sqrt((float)D), causal ? 1 : 0, stream()),
+                   ws.data_ptr(), B, S, H, KVH, D, 1.0f / std::sqrt((float)D), causal ? 1 : 0, rc, rs, stream()),
         "flash_attn_bwd");
   return dqkv;
 }
@@ -495,6 +512,32 @@ void gemm_nt_mode(torch::Tensor a, torch::Tensor b, torch::Tensor out, int64_t m
 }
 
 bool gemm_nt_swiglu_supported(int64_t T, int64_t F, int64_t K) { return dsa_gemm_nt_swiglu_supported(T, F, K); }
+
+bool gemm_nt_rope_supported(int64_t M, int64_t N, int64_t K, int64_t S, int64_t rot_cols) {
+  return dsa_gemm_nt_rope_supported(M, N, K, S, rot_cols);
+}
+
+// qkv[M][N] = a[M][K] w[N][K]^T with RoPE (rotate-half, head_dim 128) on columns [0, rot_cols), in
+// the GEMM's epilogue before the bf16 rounding; row m is position m % S (csrc/gemm_nt.hip EPI_ROPE)
+torch::Tensor gemm_nt_rope(torch::Tensor a, torch::Tensor w, torch::Tensor cos, torch::Tensor sin, int64_t S,
+                           int64_t rot_cols) {
+  check_rows(a, "gemm_nt_rope");
+  check_rows(w, "gemm_nt_rope");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm_nt_rope: shape mismatch");
+  for (const auto& t : {cos, sin}) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous() && t.dim() == 2 &&
+                    t.size(0) >= S && t.size(1) == 64,
+                "gemm_nt_rope: rope tables must be contiguous fp32 [>= S, 64]");
+  }
+  TORCH_CHECK(dsa_gemm_nt_rope_supported(M, N, K, S, rot_cols),
+              "gemm_nt_rope: M % S == 0, S % 256, N % 256, K % 128 must be 0, rot_cols % 128 == 0");
+  auto out = torch::empty({M, N}, a.options());
+  check(dsa_gemm_nt_rope(a.data_ptr(), w.data_ptr(), out.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                         M, N, K, a.stride(0), w.stride(0), out.stride(0), S, rot_cols, stream()),
+        "gemm_nt_rope");
+  return out;
+}
 
 // diagnostic: per-phase s_memtime stamps of workgroup 0 (waves 0 and 4) -> int64 [2, 64]
 torch::Tensor gemm_nt_trace(torch::Tensor a, torch::Tensor b, torch::Tensor out) {
@@ -796,7 +839,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw", &adamw);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
-  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"),
+        py::arg("H"), py::arg("KVH"), py::arg("causal"), py::arg("rope_cos") = py::none(),
+        py::arg("rope_sin") = py::none());
   m.def("fa_dkdv_trace", &fa_dkdv_trace);
   m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("rms_norm_fp8", &rms_norm_fp8, py::arg("x"), py::arg("delta"), py::arg("w"), py::arg("eps"),
@@ -824,6 +869,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cs") = py::none());
   m.def("scale_rows_cols_", &scale_rows_cols_);
   m.def("gemm_nt_trace", &gemm_nt_trace);
+  m.def("gemm_nt_rope", &gemm_nt_rope);
+  m.def("gemm_nt_rope_supported", &gemm_nt_rope_supported);
   m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);
   m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd, pybind11::arg("dy"), pybind11::arg("wdT"), pybind11::arg("gu"),
         pybind11::arg("transposed") = true);

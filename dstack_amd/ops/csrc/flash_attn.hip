@@ -1230,6 +1230,62 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __re
   }
 }
 
+// the same with the RoPE backward fused into dk: a thread sums 8 dims d and their partners d + 64
+// of one (b, s, kv-head) and writes the gradient w.r.t. the unrotated k (cos / sin [S][64])
+__global__ __launch_bounds__(256) void fa_bwd_reduce_kv_rope_kernel(const float* __restrict__ dkp,
+                                                                    const float* __restrict__ dvp,
+                                                                    bf16_t* __restrict__ dqkv, int B, int S,
+                                                                    int H, int KVH,
+                                                                    const float* __restrict__ rcos,
+                                                                    const float* __restrict__ rsin) {
+  const int G = H / KVH;
+  const long total = (long)B * S * KVH * (HD / 16);
+  const long NHD = (long)(H + 2 * KVH) * HD;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % (HD / 16));
+    const long r = i / (HD / 16);
+    const int kvh = (int)(r % KVH);
+    const long bs = r / KVH;
+    float ak[2][8], av[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ak[h][j] = av[h][j] = 0.f;
+    for (int g = 0; g < G; ++g) {
+      const long src = (bs * H + kvh * G + g) * HD + c * 8;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f4* pk = reinterpret_cast<const f4*>(dkp + src + 64 * h);
+        const f4* pv = reinterpret_cast<const f4*>(dvp + src + 64 * h);
+        const f4 k0 = pk[0], k1 = pk[1], v0 = pv[0], v1 = pv[1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ak[h][j] += k0[j];
+          ak[h][4 + j] += k1[j];
+          av[h][j] += v0[j];
+          av[h][4 + j] += v1[j];
+        }
+      }
+    }
+    const long t = (bs % S) * (HD / 2) + c * 8;
+    const f4 c0 = *reinterpret_cast<const f4*>(rcos + t), c1 = *reinterpret_cast<const f4*>(rcos + t + 4);
+    const f4 s0 = *reinterpret_cast<const f4*>(rsin + t), s1 = *reinterpret_cast<const f4*>(rsin + t + 4);
+    const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+    const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    float o1[8], o2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = ak[0][j] * cs[j] + ak[1][j] * sn[j];
+      o2[j] = ak[1][j] * cs[j] - ak[0][j] * sn[j];
+    }
+    bf16_t* row = dqkv + bs * NHD;
+    *reinterpret_cast<us8*>(row + (H + kvh) * HD + c * 8) = pack8(o1);
+    *reinterpret_cast<us8*>(row + (H + kvh) * HD + 64 + c * 8) = pack8(o2);
+    *reinterpret_cast<us8*>(row + (H + KVH + kvh) * HD + c * 8) = pack8(av[0]);
+    *reinterpret_cast<us8*>(row + (H + KVH + kvh) * HD + 64 + c * 8) = pack8(av[1]);
+  }
+}
+
 // ================================================================================================
 // Backward dQ pass: workgroup = 128 queries of one (b, q-head); loops over 64-key K/V tiles.
 // ================================================================================================
@@ -1242,7 +1298,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(con
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta,
                                                            bf16_t* __restrict__ dqkv, int B, int S,
-                                                           int H, int KVH, float scale_log2) {
+                                                           int H, int KVH, float scale_log2,
+                                                           const float* __restrict__ rcos,
+                                                           const float* __restrict__ rsin) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, l32 = lane & 31;
   const int NH = H + 2 * KVH;
@@ -1373,6 +1431,22 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fa_bwd_dq_kernel(con
   // dq accumulator: column (lane) = d within block, rows q = (r&3) + 8*(r>>2) + 4*hf (wave-local)
   const float sm = scale_log2 * 0.6931471805599453f;
   bf16_t* dqb = dqkv + ((long)b * S + qw0) * rs + hh * HD;
+  if (rcos != nullptr) {
+    // RoPE backward fused (the forward rotated q in the qkv GEMM's epilogue): the gradient w.r.t.
+    // the unrotated q, g1 c + g2 s / g2 c - g1 s for the pair (d, d + 64) = accumulators d, d + 2
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qq = (r & 3) + 8 * (r >> 2) + 4 * hf;
+        const long t = (long)(qw0 + qq) * (HD / 2) + 32 * d + l32;
+        const float c = rcos[t], sn = rsin[t];
+        const float g1 = dq[d][r] * sm, g2 = dq[d + 2][r] * sm;
+        dqb[(long)qq * rs + 32 * d + l32] = f2bf(g1 * c + g2 * sn);
+        dqb[(long)qq * rs + 64 + 32 * d + l32] = f2bf(g2 * c - g1 * sn);
+      }
+    return;
+  }
 #pragma unroll
   for (int d = 0; d < 4; ++d)
 #pragma unroll
@@ -1565,9 +1639,16 @@ extern "C" size_t dsa_fa_bwd_workspace(int B, int S, int H) {
          (fa_ds_spill(B, S, H) ? (size_t)B * H * S * S * 2 : 0);
 }
 
+extern "C" hipError_t dsa_rope_qkv(const void* in, void* out, const float* cosT, const float* sinT, int rows, int S,
+                                   int NH, int n_rot, int D, int inverse, hipStream_t st);
+
+// rcos / rsin (nullable, [S][64] fp32): q and k were rotated by RoPE after the projection (the qkv
+// GEMM's epilogue); dqkv is then the gradient w.r.t. the unrotated projection -- fused into the dQ
+// epilogue and the dK reduction on the default path, an in-place pass on the others.
 extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
                                  void* dqkv, void* workspace, int B, int S, int H, int KVH, int D,
-                                 float scale, int causal, hipStream_t st) {
+                                 float scale, int causal, const float* rcos, const float* rsin,
+                                 hipStream_t st) {
   if (!fa_shape_ok(S, H, KVH, D)) return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
   float* delta = (float*)workspace;
@@ -1622,6 +1703,13 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     return v && atoi(v) == 1;
   }();
   const bool dkdv_gqa = dkdv_gqa_env && dkdv_kind == 8 && !half_prio && !fa_ds_spill(B, S, H);
+  const bool rope_fused = rcos != nullptr && !dkdv_gqa && !fa_ds_spill(B, S, H);
+  const float* rq = rope_fused ? rcos : nullptr;
+  const float* rsq = rope_fused ? rsin : nullptr;
+  auto rope_after = [&]() -> hipError_t {  // the paths without the fused RoPE backward
+    if (rcos == nullptr || rope_fused) return hipSuccess;
+    return dsa_rope_qkv(dqkv, dqkv, rcos, rsin, B * S, S, H + 2 * KVH, H + KVH, HD, 1, st);
+  };
   // S/dP read pipeline of the 8-wave dK/dV pass (DSTACK_AMD_FA_DKDV_PF=0|1|2, default 2).  Whole
   // backward at S=8192, 3 interleaved runs (profiles/fa_bwd_pf_ab_r8t.txt): PF 0 2.031-2.045 ms,
   // PF 2 1.959-1.963 ms.  The dQ pass's counterpart (DSTACK_AMD_FA_DQ_PF=1|2) measured no gain.
@@ -1732,37 +1820,45 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     DSA_CHECK(hipGetLastError());
     if (dq_waves == 8 && half_prio)
       fa_bwd_dq_kernel<true, 8, true><<<B * H * (S / 256), 512, lds_q, st>>>(
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else if (dq_waves == 8 && dq_pf == 1)
       fa_bwd_dq_kernel<true, 8, false, 1><<<B * H * (S / 256), 512, lds_q, st>>>(
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else if (dq_waves == 8 && dq_pf >= 2)
       fa_bwd_dq_kernel<true, 8, false, 2><<<B * H * (S / 256), 512, lds_q, st>>>(
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else if (dq_waves == 8)
       fa_bwd_dq_kernel<true, 8><<<B * H * (S / 256), 512, lds_q, st>>>(
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else
       fa_bwd_dq_kernel<true><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta,
-                                                       (bf16_t*)dqkv, B, S, H, KVH, sl2);
+                                                       (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
   } else {
     if (dkdv_qt == 128) DSA_DKDV(false, 4); else DSA_DKDV(false, 2);
     DSA_CHECK(hipGetLastError());
     if (dq_waves == 8)
       fa_bwd_dq_kernel<false, 8><<<B * H * (S / 256), 512, lds_q, st>>>(
-          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+          (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else
       fa_bwd_dq_kernel<false><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse,
-                                                        delta, (bf16_t*)dqkv, B, S, H, KVH, sl2);
+                                                        delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
   }
 #undef DSA_DKDV
   DSA_CHECK(hipGetLastError());
-  if (dkdv_gqa) return hipSuccess;  // dK/dV already summed over the group, in dqkv
+  if (dkdv_gqa) return rope_after();  // dK/dV already summed over the group, in dqkv
+  if (rope_fused) {
+    const long work = (long)B * S * KVH * (HD / 16);
+    int g = (int)((work + 255) / 256);
+    if (g > 4096) g = 4096;
+    fa_bwd_reduce_kv_rope_kernel<<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH, rcos, rsin);
+    return hipGetLastError();
+  }
   const long work = (long)B * S * KVH * (HD / 8);
   int g = (int)((work + 255) / 256);
   if (g > 4096) g = 4096;
   fa_bwd_reduce_kv_kernel<<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH);
-  return hipGetLastError();
+  DSA_CHECK(hipGetLastError());
+  return rope_after();
 }
 
 // Diagnostic: one causal dK/dV pass (8-wave kernel) with waves 0 and 4 of workgroup 0 stamping 5

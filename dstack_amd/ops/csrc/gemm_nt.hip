@@ -68,8 +68,13 @@ constexpr int NT_LDS = 2 * BUF + 2 * 16384;  // 160 KiB: ring + room for the Swi
 // EPI_STORE32 / EPI_ACC32: C is fp32 (an fp32 gradient accumulator: weight gradients summed over
 // micro-batches without a bf16 rounding per micro-batch); EPI_ACC32_BF16: the last micro-batch --
 // the fp32 accumulator F32 (ld ldc32) plus this tile, rounded once, written as bf16 to C.
+// EPI_ROPE: the qkv projection with RoPE (rotate-half, head_dim 128) applied to the fp32
+// accumulators of the first `rcols` columns (the q and k heads) before the one rounding to bf16.
+// The tile's 256 columns are two heads; unit b0 takes dims 0-63 of both, b1 dims 64-127 (the B
+// rows of the second 64 unit rows come from 64 rows further on), so a lane's accumulators n and
+// n + 2 are the rotated pair (d, d + 64) of one row and head.
 enum Epi { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU = 2, EPI_SWIGLU_BWD = 3, EPI_NONE = 4, EPI_SWIGLU_R = 5,
-           EPI_SWIGLU_BWD_R = 6, EPI_STORE32 = 7, EPI_ACC32 = 8, EPI_ACC32_BF16 = 9 };
+           EPI_SWIGLU_BWD_R = 6, EPI_STORE32 = 7, EPI_ACC32 = 8, EPI_ACC32_BF16 = 9, EPI_ROPE = 10 };
 
 struct NTArgs {
   const bf16_t* A;
@@ -79,6 +84,10 @@ struct NTArgs {
   bf16_t* C3;     // a^T (SWIGLU); dgu^T (SWIGLU_BWD)
   const bf16_t* G;  // gu read by SWIGLU_BWD
   const float* F32;  // fp32 accumulator read by ACC32_BF16
+  const float* rcos;  // ROPE: cos / sin tables [S][64] fp32
+  const float* rsin;
+  int rS;             // ROPE: sequence length (row % rS = position)
+  int rcols;          // ROPE: columns [0, rcols) are rotated (multiple of 128)
   long lda, ldb, ldc;
   long ldc32;
   int M, K;
@@ -337,8 +346,10 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     } else {
       const int r = 16 * w + 8 * i + (lane >> 3);
       const int ch = (lane & 7) ^ (4 * i + (lane >> 4));
+      // ROPE: unit rows 64-127 are the B rows 128-191 past the unit's origin (the second head)
+      const int rb = (EPI == EPI_ROPE && r >= 64) ? r + 64 : r;
       va[i] = (unsigned)((r * p.lda + ch * 8) * 2);
-      vb[i] = (unsigned)((r * p.ldb + ch * 8) * 2);
+      vb[i] = (unsigned)((rb * p.ldb + ch * 8) * 2);
     }
   }
   const unsigned lds0 = (unsigned)(uintptr_t)LDS3(char, smem) + (unsigned)(w * 2048);
@@ -575,6 +586,45 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
               *reinterpret_cast<us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + pp * p.bsplit) = nt_pair8(x, y);
             }
       }
+    } else if constexpr (EPI == EPI_ROPE) {
+      // unit column u = 32wc + 16(n&1) + 4q + j of b0 (b1) is dim 32(wc&1) + 16(n&1) + 4q + j (+64)
+      // of head nb0/128 + (wc>>1); the 8-column pieces of EPI_STORE land at
+      // nb0 + 128(wc>>1) + 32(wc&1) + 16(q&1) + 8(q>>1), the b1 piece 64 columns on
+      const int q = lane >> 4;
+      const int hcol = nb0 + 128 * (wc >> 1);
+      if (hcol < p.rcols) {  // wave-uniform: q / k heads rotate, v heads pass through
+        const int pos0 = m0 % p.rS + 64 * wr + er;
+        const int d0 = 32 * (wc & 1) + 4 * q;
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            const long t = (long)(pos0 + 128 * ms + 16 * mi) * 64 + d0;
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+              const f4 c = *reinterpret_cast<const f4*>(p.rcos + t + 16 * n);
+              const f4 sn = *reinterpret_cast<const f4*>(p.rsin + t + 16 * n);
+              const f32x4 x1 = acc[ms][mi][n], x2 = acc[ms][mi][n + 2];
+              acc[ms][mi][n] = x1 * c - x2 * sn;
+              acc[ms][mi][n + 2] = x2 * c + x1 * sn;
+            }
+          }
+      }
+      bf16_t* cbase = p.C + (long)(m0 + 64 * wr + er) * p.ldc + hcol + 32 * (wc & 1) + 16 * (q & 1) + 8 * (q >> 1);
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            us4 x, y;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              x[j] = f2bf(acc[ms][mi][2 * pp][j]);
+              y[j] = f2bf(acc[ms][mi][2 * pp + 1][j]);
+            }
+            *reinterpret_cast<us8*>(cbase + (long)(128 * ms + 16 * mi) * p.ldc + 64 * pp) = nt_pair8(x, y);
+          }
     } else if constexpr (EPI == EPI_STORE32 || EPI == EPI_ACC32 || EPI == EPI_ACC32_BF16) {
       // the same 8-column pieces as EPI_STORE, as 8 floats (two 16-byte accesses); old values are
       // loaded one 128-row half (ms) at a time: 64 VGPRs beside the 128 of the accumulators
@@ -914,6 +964,40 @@ extern "C" hipError_t dsa_gemm_nt(const void* A, const void* B, void* C, int M, 
   const int tiles = (M / NT_BM) * (N / NT_BN);
   if (accumulate == 2) return nt_launch<EPI_NONE>(a, tiles, st);  // timing-only diagnostic
   return accumulate ? nt_launch<EPI_ACC>(a, tiles, st) : nt_launch<EPI_STORE>(a, tiles, st);
+}
+
+// qkv = A[M][K] B[N][K]^T with RoPE on the columns [0, rot_cols) (head_dim 128, rotate-half, fp32
+// tables cos / sin [>= S][64]), rounded once to bf16.  Row m is position m % S.
+extern "C" bool dsa_gemm_nt_rope_supported(int M, int N, int K, int S, int rot_cols) {
+  return nt_shape_ok(M, N, K) && S > 0 && S % NT_BM == 0 && M % S == 0 && rot_cols % 128 == 0 &&
+         rot_cols <= N;
+}
+
+extern "C" hipError_t dsa_gemm_nt_rope(const void* A, const void* B, void* C, const float* cosT, const float* sinT,
+                                       int M, int N, int K, long lda, long ldb, long ldc, int S, int rot_cols,
+                                       hipStream_t st) {
+  if (!dsa_gemm_nt_rope_supported(M, N, K, S, rot_cols) || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K ||
+      ldc < N)
+    return hipErrorInvalidValue;
+  if (255L * lda * 2 + 2L * K > 0xffffffffL || 255L * ldb * 2 + 2L * K > 0xffffffffL) return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (bf16_t*)C;
+  a.rcos = cosT;
+  a.rsin = sinT;
+  a.rS = S;
+  a.rcols = rot_cols;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.M = M;
+  a.K = K;
+  a.ntn = N / NT_BN;
+  a.nstride = NT_BN;
+  a.bsplit = 64;  // b1 = dims 64-127 of the tile's two heads
+  a.group = nt_group(M / NT_BM, N / NT_BN);
+  return nt_launch<EPI_ROPE>(a, (M / NT_BM) * (N / NT_BN), st);
 }
 
 // Diagnostic: one plain GEMM with waves 0 and 4 of workgroup 0 stamping every phase boundary of

@@ -294,6 +294,69 @@ class _FlashAttnQKV(torch.autograd.Function):
         return dqkv, None, None, None
 
 
+class _QKVRopeAttn(torch.autograd.Function):
+    """o = attention(rope(h Wqkv^T)) with both RoPE passes fused away: the forward rotates q and k
+    in the in-tree qkv GEMM's epilogue (``gemm_nt_rope``, fp32 accumulators rotated before the one
+    bf16 rounding), the backward hands the tables to the flash-attention backward, whose dQ epilogue
+    and dK reduction write the gradient w.r.t. the unrotated projection.  No ``rope_qkv_kernel``
+    pass (a full read + write of qkv) in either direction.  Weight and input gradients as in
+    ``_Linear`` (the weight gradient through ``_dsa_grad_sink``)."""
+
+    @staticmethod
+    def forward(ctx, h, wqkv, cos, sin, n_heads, n_kv_heads):
+        C = _ext.require()
+        b, s, _ = h.shape
+        h2 = _2d(h)
+        qkv = C.gemm_nt_rope(h2, wqkv, cos, sin, s, (n_heads + n_kv_heads) * 128).view(b, s, -1)
+        o, lse = C.flash_attn_fwd(qkv, n_heads, n_kv_heads, True)
+        ctx.save_for_backward(h2, wqkv, qkv, o, lse, cos, sin)
+        ctx.meta = (n_heads, n_kv_heads, h.shape)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        C = _ext.require()
+        h2, wqkv, qkv, o, lse, cos, sin = ctx.saved_tensors
+        n_heads, n_kv_heads, hshape = ctx.meta
+        dqkv = C.flash_attn_bwd(do.contiguous(), qkv, o, lse, n_heads, n_kv_heads, True, cos, sin)
+        g2 = dqkv.view(-1, dqkv.shape[-1])
+        wt = _transposed_weight(wqkv)
+        dh = _nt(g2, wt) if wt is not None else g2 @ wqkv
+        a, b = wgrad_operands(g2, h2)
+        sink = getattr(wqkv, "_dsa_grad_sink", None)
+        gw = None
+        if sink is None:
+            gw = mm_into(a, b)
+        else:
+            sink(wqkv, a, b)
+        return dh.view(hshape), gw, None, None, None, None
+
+
+def _qkv_rope_ok(h: torch.Tensor, wqkv: torch.Tensor, cos: torch.Tensor, n_heads: int, n_kv_heads: int) -> bool:
+    if os.environ.get("DSTACK_AMD_QKV_ROPE", "1") == "0" or _attn_impl() != "hip":
+        return False
+    if h.dtype != torch.bfloat16 or wqkv.dtype != torch.bfloat16 or not (h.is_contiguous() and wqkv.is_contiguous()):
+        return False
+    if h.dim() != 3 or wqkv.shape[0] != (n_heads + 2 * n_kv_heads) * 128 or cos.dtype != torch.float32:
+        return False
+    C = _ext.require()
+    b, s, d = h.shape
+    return s % 256 == 0 and C.gemm_nt_rope_supported(b * s, wqkv.shape[0], d, s, (n_heads + n_kv_heads) * 128)
+
+
+def qkv_rope_attention(h: torch.Tensor, wqkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_heads: int,
+                       n_kv_heads: int) -> torch.Tensor:
+    """Causal GQA attention of the Llama block: ``attention(rope(linear(h, wqkv)))``, [B, S, H*D].
+    On the HIP path with head_dim 128 and S % 256 == 0 the RoPE passes are fused into the qkv GEMM
+    and the attention backward (``_QKVRopeAttn``; ``DSTACK_AMD_QKV_ROPE=0`` keeps the separate
+    kernels)."""
+    if _ext.use_hip(h) and _qkv_rope_ok(h, wqkv, cos, n_heads, n_kv_heads):
+        return _QKVRopeAttn.apply(h, wqkv, cos.contiguous(), sin.contiguous(), n_heads, n_kv_heads)
+    hd = wqkv.shape[0] // (n_heads + 2 * n_kv_heads)
+    qkv = rope(linear(h, wqkv), cos, sin, n_heads + n_kv_heads, hd)
+    return attention(qkv, n_heads, n_kv_heads, causal=True)
+
+
 def _attn_impl() -> str:
     return os.environ.get("DSTACK_AMD_ATTN", "hip").lower()
 

@@ -850,3 +850,61 @@ def test_synthetic_tokens_kernel_matches_cpu_reference(gpu, mb, S):
     for index in (0, 1, 17, 1 << 40):
         a, b = g.tokens(index).cpu(), c.tokens(index)
         assert a.shape == (mb, S + 1) and torch.equal(a, b), index
+
+
+def _qkv_rope_ref(h, w, cos, sin, H, KV):
+    """fp32 reference of rope(h W^T) on the q and k heads (head_dim 128)."""
+    B, S, _ = h.shape
+    x = (h.reshape(B * S, -1) @ w.t()).view(B, S, H + 2 * KV, 128)
+    return torch.cat([ref.apply_rope(x[:, :, : H + KV], cos, sin), x[:, :, H + KV :]], 2).reshape(B, S, -1)
+
+
+@pytest.mark.parametrize("B,S,K,H,KV", [(2, 256, 512, 4, 2), (1, 1024, 4096, 32, 8), (1, 8192, 256, 2, 1)])
+def test_gemm_nt_rope_epilogue_matches_fp32(gpu, B, S, K, H, KV):
+    """The qkv GEMM with RoPE in its epilogue (EPI_ROPE: b1 unit = dims 64-127 of the tile's two
+    heads) against fp32 matmul + rotate-half; (1, 8192, ...) reaches the last positions."""
+    C = _ext.require()
+    N = (H + 2 * KV) * 128
+    h = _rand(B, S, K, device=gpu)
+    w = _rand(N, K, device=gpu, seed=1, scale=K ** -0.5)
+    cos, sin = ref.rope_cos_sin(S, 128, 500000.0, gpu)
+    assert C.gemm_nt_rope_supported(B * S, N, K, S, (H + KV) * 128)
+    out = C.gemm_nt_rope(h.view(B * S, K), w, cos, sin, S, (H + KV) * 128).view(B, S, N)
+    exp = _qkv_rope_ref(h.float(), w.float(), cos, sin, H, KV)
+    _close(out, exp, 3e-2, 1e-2)
+    # v heads are the plain product
+    _close(out[..., (H + KV) * 128:], (h.float().view(B * S, K) @ w.float().t()).view(B, S, N)[..., (H + KV) * 128:],
+           3e-2, 1e-2)
+
+
+@pytest.mark.parametrize("B,S,D,H,KV", [(2, 256, 512, 4, 2), (1, 8192, 1024, 8, 2)])
+def test_qkv_rope_attention_fused_matches_fp32(gpu, monkeypatch, B, S, D, H, KV):
+    """attention(rope(h Wqkv^T)) with both RoPE passes fused (GEMM epilogue forward, dQ epilogue and
+    dK reduction backward) against fp32 autograd, and against the separate-kernel path."""
+    monkeypatch.delenv("DSTACK_AMD_QKV_ROPE", raising=False)
+    N = (H + 2 * KV) * 128
+    h = _rand(B, S, D, device=gpu).requires_grad_()
+    w = _rand(N, D, device=gpu, seed=1, scale=D ** -0.5).requires_grad_()
+    cos, sin = ref.rope_cos_sin(S, 128, 500000.0, gpu)
+    assert ops.functional._qkv_rope_ok(h, w, cos, H, KV)
+    o = ops.qkv_rope_attention(h, w, cos, sin, H, KV)
+    do = _rand(B, S, H * 128, device=gpu, seed=3)
+    o.backward(do)
+    hr, wr = h.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    q, k, v = ops.functional.split_qkv(_qkv_rope_ref(hr, wr, cos, sin, H, KV), H, KV)
+    orf = ref.attention(q, k, v, True).reshape(B, S, -1)
+    orf.backward(do.float())
+    _close(o, orf, 2e-2, 2e-2)
+    for name, a, b in (("dh", h.grad, hr.grad), ("dw", w.grad, wr.grad)):
+        a = a.float()
+        rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert rel < 2e-2, f"{name}: rel {rel}"
+    # the unfused path (GEMM, rope_qkv, attention, inverse rope_qkv) agrees closely
+    monkeypatch.setenv("DSTACK_AMD_QKV_ROPE", "0")
+    h2, w2 = h.detach().clone().requires_grad_(), w.detach().clone().requires_grad_()
+    o2 = ops.qkv_rope_attention(h2, w2, cos, sin, H, KV)
+    o2.backward(do)
+    for name, a, b in (("o", o, o2), ("dh", h.grad, h2.grad), ("dw", w.grad, w2.grad)):
+        a, b = a.float(), b.float()
+        rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert rel < 1e-2, f"fused vs unfused {name}: rel {rel}"
