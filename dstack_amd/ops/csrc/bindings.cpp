@@ -52,6 +52,12 @@ hipError_t dsa_gemm_tn(const void*, const void*, void*, int, int, int, long, lon
 bool dsa_gemm_nt_supported(int, int, int);
 hipError_t dsa_gemm_nt(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 bool dsa_gemm_nt_rope_supported(int, int, int, int, int);
+bool dsa_gemm_nt_f8_supported(int, int, int);
+bool dsa_gemm_nt_f8_swiglu_supported(int, int, int);
+hipError_t dsa_gemm_nt_f8_swiglu(const void*, const void*, void*, float*, const float*, const float*, int, int, int,
+                                 long, long, hipStream_t);
+hipError_t dsa_quant_fp8_rows_pmax(const void*, long, const float*, int, void*, long, float*, int, int, hipStream_t);
+hipError_t dsa_gemm_nt_f8(const void*, const void*, void*, int, int, int, long, long, long, hipStream_t);
 hipError_t dsa_gemm_nt_rope(const void*, const void*, void*, const float*, const float*, int, int, int, long, long,
                             long, int, int, hipStream_t);
 bool dsa_gemm_nt_swiglu_supported(int, int, int);
@@ -513,6 +519,54 @@ void gemm_nt_mode(torch::Tensor a, torch::Tensor b, torch::Tensor out, int64_t m
 
 bool gemm_nt_swiglu_supported(int64_t T, int64_t F, int64_t K) { return dsa_gemm_nt_swiglu_supported(T, F, K); }
 
+bool gemm_nt_f8_supported(int64_t M, int64_t N, int64_t K) { return dsa_gemm_nt_f8_supported(M, N, K); }
+
+// out[M][N] = bf16(a[M][K] w[N][K]^T) for e4m3 a / w (uint8 or float8_e4m3fn storage), unscaled
+void gemm_nt_f8(torch::Tensor a, torch::Tensor w, torch::Tensor out) {
+  for (const auto& t : {a, w}) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.element_size() == 1,
+                "gemm_nt_f8: operands must be 2-D row-major 1-byte (e4m3) tensors");
+  }
+  check_rows(out, "gemm_nt_f8");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_nt_f8: shape mismatch");
+  TORCH_CHECK(dsa_gemm_nt_f8_supported(M, N, K), "gemm_nt_f8: M % 256, N % 256, K % 256 must be 0");
+  check(dsa_gemm_nt_f8(a.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), w.stride(0), out.stride(0),
+                       stream()),
+        "gemm_nt_f8");
+}
+
+bool gemm_nt_f8_swiglu_supported(int64_t M, int64_t F, int64_t K) { return dsa_gemm_nt_f8_swiglu_supported(M, F, K); }
+
+// Serving fp8 gate/up + SwiGLU + per-token e4m3 quantization: x [M][K] e4m3 with row scales xs [M],
+// w [2F][K] e4m3 (gate rows then up rows) with per-output-channel scales ws [2F] ->
+// (q [M][F] e4m3, s [M]) -- what swiglu_quant_fp8_rows(raw, xs, ws) gives for the raw product,
+// with a = silu(g) u (bf16) as the only intermediate in HBM.  Also returns a (diagnostics).
+std::vector<torch::Tensor> gemm_nt_f8_swiglu_quant(torch::Tensor x, torch::Tensor w, torch::Tensor xs,
+                                                   torch::Tensor ws) {
+  for (const auto& t : {x, w}) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.element_size() == 1,
+                "gemm_nt_f8_swiglu_quant: operands must be 2-D row-major e4m3 tensors");
+  }
+  const int64_t M = x.size(0), K = x.size(1), F = w.size(0) / 2;
+  TORCH_CHECK(w.size(1) == K && w.size(0) == 2 * F, "gemm_nt_f8_swiglu_quant: shape mismatch");
+  TORCH_CHECK(xs.scalar_type() == torch::kFloat32 && xs.is_contiguous() && xs.numel() == M &&
+                  ws.scalar_type() == torch::kFloat32 && ws.is_contiguous() && ws.numel() == 2 * F,
+              "gemm_nt_f8_swiglu_quant: fp32 scales xs [M], ws [2F]");
+  TORCH_CHECK(dsa_gemm_nt_f8_swiglu_supported(M, F, K), "gemm_nt_f8_swiglu_quant: M % 256, F % 128, K % 256 must be 0");
+  auto a = torch::empty({M, F}, x.options().dtype(torch::kBFloat16));
+  auto pmax = torch::empty({M, F / 32}, x.options().dtype(torch::kFloat32));
+  auto q = torch::empty({M, F}, x.options().dtype(torch::kUInt8));
+  auto s = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  check(dsa_gemm_nt_f8_swiglu(x.data_ptr(), w.data_ptr(), a.data_ptr(), pmax.data_ptr<float>(), xs.data_ptr<float>(),
+                              ws.data_ptr<float>(), M, F, K, x.stride(0), w.stride(0), stream()),
+        "gemm_nt_f8_swiglu");
+  check(dsa_quant_fp8_rows_pmax(a.data_ptr(), F, pmax.data_ptr<float>(), F / 32, q.data_ptr(), F,
+                                s.data_ptr<float>(), M, F, stream()),
+        "quant_fp8_rows_pmax");
+  return {q, s, a};
+}
+
 bool gemm_nt_rope_supported(int64_t M, int64_t N, int64_t K, int64_t S, int64_t rot_cols) {
   return dsa_gemm_nt_rope_supported(M, N, K, S, rot_cols);
 }
@@ -870,6 +924,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_rows_cols_", &scale_rows_cols_);
   m.def("gemm_nt_trace", &gemm_nt_trace);
   m.def("gemm_nt_rope", &gemm_nt_rope);
+  m.def("gemm_nt_f8", &gemm_nt_f8);
+  m.def("gemm_nt_f8_supported", &gemm_nt_f8_supported);
+  m.def("gemm_nt_f8_swiglu_quant", &gemm_nt_f8_swiglu_quant);
+  m.def("gemm_nt_f8_swiglu_supported", &gemm_nt_f8_swiglu_supported);
   m.def("gemm_nt_rope_supported", &gemm_nt_rope_supported);
   m.def("gemm_nt_swiglu_supported", &gemm_nt_swiglu_supported);
   m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd, pybind11::arg("dy"), pybind11::arg("wdT"), pybind11::arg("gu"),

@@ -327,7 +327,44 @@ __global__ __launch_bounds__(256) void gemv_fp8_rows_kernel(const bf16_t* __rest
 
 }  // namespace
 
+// Row quantizer whose row max comes precomputed as P partial maxima per row (pmax [M][P], written by
+// the fp8 gate/up GEMM's SwiGLU epilogue): one pass over x instead of two (or a register-held row).
+// Same scale and rounding as quant_rows_kernel.
+__global__ __launch_bounds__(256) void quant_rows_pmax_kernel(const bf16_t* __restrict__ x, long ldx,
+                                                              const float* __restrict__ pmax, int P,
+                                                              unsigned char* __restrict__ q, long ldq,
+                                                              float* __restrict__ s, int K) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  float amax = 0.f;
+  for (int i = tid; i < P; i += 256) amax = fmaxf(amax, pmax[(long)row * P + i]);
+  amax = wave_max(amax);
+  if ((tid & 63) == 0) red[tid >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float scale = fmaxf(amax, 1e-12f) / E4M3_MAX;
+  const float inv = 1.f / scale;
+  if (tid == 0) s[row] = scale;
+  const bf16_t* xr = x + (long)row * ldx;
+  unsigned char* qr = q + (long)row * ldq;
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  for (int k = tid * 8; k < K; k += 256 * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const us8*>(xr + k), v);
+    const unsigned int w0 = f32x4_to_fp8(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+    const unsigned int w1 = f32x4_to_fp8(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv);
+    *reinterpret_cast<u2*>(qr + k) = u2{w0, w1};
+  }
+}
+
 extern "C" bool dsa_quant_fp8_supported(int K) { return K > 0 && K % 8 == 0; }
+
+extern "C" hipError_t dsa_quant_fp8_rows_pmax(const void* x, long ldx, const float* pmax, int P, void* q, long ldq,
+                                              float* s, int M, int K, hipStream_t st) {
+  if (!dsa_quant_fp8_supported(K) || M <= 0 || P <= 0) return hipErrorInvalidValue;
+  quant_rows_pmax_kernel<<<M, 256, 0, st>>>((const bf16_t*)x, ldx, pmax, P, (unsigned char*)q, ldq, s, K);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t dsa_quant_fp8_rows(const void* x, long ldx, void* q, long ldq, float* s, int M, int K,
                                          hipStream_t st) {

@@ -74,7 +74,12 @@ constexpr int NT_LDS = 2 * BUF + 2 * 16384;  // 160 KiB: ring + room for the Swi
 // rows of the second 64 unit rows come from 64 rows further on), so a lane's accumulators n and
 // n + 2 are the rotated pair (d, d + 64) of one row and head.
 enum Epi { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU = 2, EPI_SWIGLU_BWD = 3, EPI_NONE = 4, EPI_SWIGLU_R = 5,
-           EPI_SWIGLU_BWD_R = 6, EPI_STORE32 = 7, EPI_ACC32 = 8, EPI_ACC32_BF16 = 9, EPI_ROPE = 10 };
+           EPI_SWIGLU_BWD_R = 6, EPI_STORE32 = 7, EPI_ACC32 = 8, EPI_ACC32_BF16 = 9, EPI_ROPE = 10,
+           EPI_SWIGLU_F8 = 11 };
+// EPI_SWIGLU_F8 (F8 only): the serving engine's fp8 gate/up projection -- the SwiGLU tile map of
+// EPI_SWIGLU over raw e4m3 products, the row-wise scales srow[m] scol[n] applied in the epilogue,
+// a = silu(g) u written as bf16 [M][F] (C2) and each wave's per-row max |a| over its 32 columns as
+// pmax[m][F / 32] for the one-pass row quantizer that follows (no [M][2F] product in HBM).
 
 struct NTArgs {
   const bf16_t* A;
@@ -88,6 +93,9 @@ struct NTArgs {
   const float* rsin;
   int rS;             // ROPE: sequence length (row % rS = position)
   int rcols;          // ROPE: columns [0, rcols) are rotated (multiple of 128)
+  const float* srow;  // SWIGLU_F8: per-row (token) and per-output-channel scales, partial maxima
+  const float* scol;
+  float* pmax;
   long lda, ldb, ldc;
   long ldc32;
   int M, K;
@@ -185,6 +193,9 @@ __device__ __forceinline__ void nt_pair8f(const f32x4& x, const f32x4& y, float 
   }
 }
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
 template <int MS, int NS>
 __device__ __forceinline__ void nt_quadrant(f32x4 (&acc)[2][4][4], const bf16x8 (&af)[4][2],
                                             const bf16x8 (&bf)[2][2][2]) {
@@ -197,6 +208,46 @@ __device__ __forceinline__ void nt_quadrant(f32x4 (&acc)[2][4][4], const bf16x8 
       for (int n = 0; n < 2; ++n)
         acc[MS][mi][2 * NS + n] = mfma16(bf[NS][n][kk], af[mi][kk], acc[MS][mi][2 * NS + n]);
   __builtin_amdgcn_s_setprio(0);
+}
+
+// F8: one v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales: the fp8 rate) per accumulator, the
+// two bf16 MFMAs' cycles for twice the k.  The fragments are read straight into 32-byte operands
+// (nt_read_a8 / nt_read_b8: chunks g and g + 4 of the 128-byte row; A and B take the same chunk
+// order, so the product runs over a permutation of k -- the same sum).
+template <int MS, int NS>
+__device__ __forceinline__ void nt_quadrant8(f32x4 (&acc)[2][4][4], const i32x8 (&af)[4], const i32x8 (&bf)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      acc[MS][mi][2 * NS + n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[NS][n], af[mi], acc[MS][mi][2 * NS + n],
+                                                                               0, 0, 0, 127, 0, 127);
+  // pin the MFMAs into this phase: without the use, the compiler sinks them past the phase's
+  // barrier into later phases, where their fragments stay live beside the next ones (spills)
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[MS][mi][2 * NS + n]));
+  __builtin_amdgcn_s_setprio(0);
+}
+
+__device__ __forceinline__ i32x8 ldsr8(const char* p0, const char* p1) {
+  const i32x4 a = *reinterpret_cast<const i32x4*>(p0), b = *reinterpret_cast<const i32x4*>(p1);
+  return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+template <int MS>
+__device__ __forceinline__ void nt_read_a8(i32x8 (&af)[4], const char* buf, int ra0, int ra1) {
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) af[mi] = ldsr8(buf + MS * UNIT + mi * 2048 + ra0, buf + MS * UNIT + mi * 2048 + ra1);
+}
+
+template <int NS>
+__device__ __forceinline__ void nt_read_b8(i32x8 (&bf)[2][2], const char* buf, int rb0, int rb1) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+    bf[NS][n] = ldsr8(buf + (2 + NS) * UNIT + n * 2048 + rb0, buf + (2 + NS) * UNIT + n * 2048 + rb1);
 }
 
 // A fragments of m-subtile MS (unit a_MS of buffer `buf`): 4 row tiles x 2 k halves
@@ -256,7 +307,10 @@ __device__ __forceinline__ void nt_tile_origin(const NTArgs& p, int t, int& m0, 
   nb0 = ((t % in_group) / gm) * p.nstride;
 }
 
-template <int EPI, bool TRACE = false, bool KM = false>
+// F8: A and B are e4m3 bytes addressed as bf16 pairs (lda, ldb, K in 2-byte units): the K-tile
+// of 64 "elements" is the same 128-byte row piece, so the DMA ring, the swizzle and the fragment
+// reads are unchanged; only the MFMA differs (nt_quadrant).
+template <int EPI, bool TRACE = false, bool KM = false, bool F8 = false>
 __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // the plain epilogues store straight from the accumulators while the next tile's prologue DMA
@@ -409,22 +463,35 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
 #pragma unroll
     for (int n = 0; n < 2; ++n) kb[n] = row + 32 * ((2 * wc + n) ^ x);
   }
+  i32x8 af8[4], bf8[2][2];  // F8 fragments
   auto read_a0 = [&](const char* buf) {
-    if constexpr (KM) km_read_a<0>(af, buf, ka); else nt_read_a<0>(af, buf, ra0, ra1);
+    if constexpr (KM) km_read_a<0>(af, buf, ka);
+    else if constexpr (F8) nt_read_a8<0>(af8, buf, ra0, ra1);
+    else nt_read_a<0>(af, buf, ra0, ra1);
   };
   auto read_a1 = [&](const char* buf) {
-    if constexpr (KM) km_read_a<1>(af, buf, ka); else nt_read_a<1>(af, buf, ra0, ra1);
+    if constexpr (KM) km_read_a<1>(af, buf, ka);
+    else if constexpr (F8) nt_read_a8<1>(af8, buf, ra0, ra1);
+    else nt_read_a<1>(af, buf, ra0, ra1);
   };
   auto read_b = [&](const char* buf) {
     if constexpr (KM) {
       km_read_b<0>(bf, buf, kb);
       km_read_b<1>(bf, buf, kb);
+    } else if constexpr (F8) {
+      nt_read_b8<0>(bf8, buf, rb0, rb1);
+      nt_read_b8<1>(bf8, buf, rb0, rb1);
     } else {
       nt_read_b<0>(bf, buf, rb0, rb1);
       nt_read_b<1>(bf, buf, rb0, rb1);
     }
   };
 
+#define NT_QUAD(MS, NS)                                  \
+  do {                                                   \
+    if constexpr (F8) nt_quadrant8<MS, NS>(acc, af8, bf8); \
+    else nt_quadrant<MS, NS>(acc, af, bf);               \
+  } while (0)
   set_src(m0, nb0);
   prologue();
   nt_vmcnt<4>();
@@ -469,8 +536,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       stamp(it);
       nt_barrier();
       stamp(it);
-      nt_quadrant<0, 0>(acc, af, bf);
-      nt_quadrant<0, 1>(acc, af, bf);
+      NT_QUAD(0, 0);
+      NT_QUAD(0, 1);
       stamp(it);
       nt_barrier();
       // P2: m-subtile 1 of tile t; retire tile t+1
@@ -487,8 +554,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       stamp(it);
       nt_barrier();
       stamp(it);
-      nt_quadrant<1, 0>(acc, af, bf);
-      nt_quadrant<1, 1>(acc, af, bf);
+      NT_QUAD(1, 0);
+      NT_QUAD(1, 1);
       stamp(it);
       nt_barrier();
       // P3: m-subtile 0 of tile t+1
@@ -503,8 +570,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       stamp(it);
       nt_barrier();
       stamp(it);
-      nt_quadrant<0, 0>(acc, af, bf);
-      nt_quadrant<0, 1>(acc, af, bf);
+      NT_QUAD(0, 0);
+      NT_QUAD(0, 1);
       stamp(it);
       nt_barrier();
       // P4: m-subtile 1 of tile t+1; retire tile t+2
@@ -519,8 +586,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       stamp(it);
       nt_barrier();
       stamp(it);
-      nt_quadrant<1, 0>(acc, af, bf);
-      nt_quadrant<1, 1>(acc, af, bf);
+      NT_QUAD(1, 0);
+      NT_QUAD(1, 1);
       stamp(it);
       nt_barrier();
     }
@@ -692,6 +759,41 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
           *reinterpret_cast<us8*>(gbase + ro * p.ldc + p.bsplit) = nt_pair8(u4[0], u4[1]);
           *reinterpret_cast<us8*>(abase + ro * p.F) = nt_pair8(o4[0], o4[1]);
         }
+    } else if constexpr (EPI == EPI_SWIGLU_F8) {
+      // acc n / n + 2 = raw g / u of (row, f); the deferred-scale SwiGLU-quant's arithmetic
+      // (swiglu_quant_rows_kernel<SCALED>): bf16(raw) * rs * cs -> bf16, a = bf16(silu(g) u)
+      const int q = lane >> 4;
+      const int f0 = nb0 + 32 * wc;  // this wave's 32 columns of the F outputs
+      bf16_t* abase = p.C2 + (long)(m0 + 64 * wr + er) * p.F + f0 + 16 * (q & 1) + 8 * (q >> 1);
+      f4 cg[2], cu[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        cg[n] = *reinterpret_cast<const f4*>(p.scol + f0 + 16 * n + 4 * q);
+        cu[n] = *reinterpret_cast<const f4*>(p.scol + p.F + f0 + 16 * n + 4 * q);
+      }
+      const int P = p.F / 32;
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const int row = m0 + 128 * ms + 64 * wr + 16 * mi + er;
+          const float r = p.srow[row];
+          us4 o4[2];
+          float am = 0.f;
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float g = bf2f(f2bf(bf2f(f2bf(acc[ms][mi][n][j])) * r * cg[n][j]));
+              const float u = bf2f(f2bf(bf2f(f2bf(acc[ms][mi][n + 2][j])) * r * cu[n][j]));
+              o4[n][j] = f2bf(silu(g) * u);
+              am = fmaxf(am, fabsf(bf2f(o4[n][j])));
+            }
+          *reinterpret_cast<us8*>(abase + (long)(128 * ms + 16 * mi) * p.F) = nt_pair8(o4[0], o4[1]);
+          am = fmaxf(am, __shfl_xor(am, 16));
+          am = fmaxf(am, __shfl_xor(am, 32));
+          if (q == 0) p.pmax[(long)row * P + f0 / 32] = am;
+        }
     } else if constexpr (EPI == EPI_SWIGLU_BWD_R) {
       // acc = da[t][f] (plain column map); 16-byte pieces of 8 consecutive f: g, u loaded, dg, du
       // stored -- dg = da * u * silu'(g), du = da * silu(g), da rounded to bf16 as the unfused path
@@ -852,6 +954,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   }
 }
 
+#undef NT_QUAD
+
 namespace {
 
 bool nt_shape_ok(int M, int N, int K) {
@@ -905,11 +1009,11 @@ int* nt_queue_slot(hipStream_t st) {
 template <int EPI>
 constexpr bool nt_dynamic_ok() { return EPI != EPI_SWIGLU && EPI != EPI_SWIGLU_BWD; }
 
-template <int EPI, bool TRACE = false, bool KM = false>
+template <int EPI, bool TRACE = false, bool KM = false, bool F8 = false>
 hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, TRACE, KM>),
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, TRACE, KM, F8>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, NT_LDS));
     attr = true;
   }
@@ -933,7 +1037,7 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
     if (dynamic && !TRACE && nt_dynamic_ok<EPI>()) a.queue = nt_queue_slot(st);
   }
   if (const char* g = getenv("DSTACK_AMD_GEMM_NT_GROUP")) a.group = atoi(g) > 0 ? atoi(g) : a.group;
-  gemm_nt_kernel<EPI, TRACE, KM><<<grid, 512, NT_LDS, st>>>(a);
+  gemm_nt_kernel<EPI, TRACE, KM, F8><<<grid, 512, NT_LDS, st>>>(a);
   return hipGetLastError();
 }
 
@@ -964,6 +1068,64 @@ extern "C" hipError_t dsa_gemm_nt(const void* A, const void* B, void* C, int M, 
   const int tiles = (M / NT_BM) * (N / NT_BN);
   if (accumulate == 2) return nt_launch<EPI_NONE>(a, tiles, st);  // timing-only diagnostic
   return accumulate ? nt_launch<EPI_ACC>(a, tiles, st) : nt_launch<EPI_STORE>(a, tiles, st);
+}
+
+// C[M][N] = bf16(A[M][K] B[N][K]^T) for e4m3 A and B (row strides lda / ldb in bytes, K in
+// bytes): the raw product, no scales (the serving engine applies the row-wise scales in the
+// consumer kernels, serving/model.py).  Same tiles and schedule as the bf16 GEMM.
+extern "C" bool dsa_gemm_nt_f8_supported(int M, int N, int K) { return K % 2 == 0 && nt_shape_ok(M, N, K / 2); }
+
+extern "C" hipError_t dsa_gemm_nt_f8(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
+                                     long ldc, hipStream_t st) {
+  if (!dsa_gemm_nt_f8_supported(M, N, K) || lda % 16 || ldb % 16 || ldc % 8 || lda < K || ldb < K || ldc < N)
+    return hipErrorInvalidValue;
+  if (255L * lda + K > 0xffffffffL || 255L * ldb + K > 0xffffffffL) return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (bf16_t*)C;
+  a.lda = lda / 2;
+  a.ldb = ldb / 2;
+  a.ldc = ldc;
+  a.M = M;
+  a.K = K / 2;
+  a.ntn = N / NT_BN;
+  a.nstride = NT_BN;
+  a.bsplit = 128;
+  a.group = nt_group(M / NT_BM, N / NT_BN);
+  return nt_launch<EPI_STORE, false, false, true>(a, (M / NT_BM) * (N / NT_BN), st);
+}
+
+// Serving fp8 gate/up with the SwiGLU in the epilogue: X [M][K] e4m3 (ldx bytes), W [2F][K] e4m3
+// (gate rows, then up rows; ldw bytes), rs [M] / cs [2F] the row-wise scales; writes a [M][F] bf16
+// and pmax [M][F / 32] (per-row partial max |a|, for quant_rows_pmax).
+extern "C" bool dsa_gemm_nt_f8_swiglu_supported(int M, int F, int K) {
+  return M > 0 && F > 0 && M % NT_BM == 0 && F % 128 == 0 && K % (4 * NT_BK) == 0;
+}
+
+extern "C" hipError_t dsa_gemm_nt_f8_swiglu(const void* X, const void* W, void* a_out, float* pmax, const float* rs,
+                                            const float* cs, int M, int F, int K, long ldx, long ldw,
+                                            hipStream_t st) {
+  if (!dsa_gemm_nt_f8_swiglu_supported(M, F, K) || ldx % 16 || ldw % 16 || ldx < K || ldw < K)
+    return hipErrorInvalidValue;
+  if (255L * ldx + K > 0xffffffffL || 255L * ldw + K > 0xffffffffL) return hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)X;
+  a.B = (const bf16_t*)W;
+  a.C2 = (bf16_t*)a_out;
+  a.srow = rs;
+  a.scol = cs;
+  a.pmax = pmax;
+  a.lda = ldx / 2;
+  a.ldb = ldw / 2;
+  a.M = M;
+  a.K = K / 2;
+  a.F = F;
+  a.ntn = F / 128;
+  a.nstride = 128;
+  a.bsplit = F;
+  a.group = nt_group(M / NT_BM, F / 128);
+  return nt_launch<EPI_SWIGLU_F8, false, false, true>(a, (M / NT_BM) * (F / 128), st);
 }
 
 // qkv = A[M][K] B[N][K]^T with RoPE on the columns [0, rot_cols) (head_dim 128, rotate-half, fp32

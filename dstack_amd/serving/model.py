@@ -221,6 +221,12 @@ class ServingLlama:
         # decode-batch fp8 projections (5..256 rows) on the in-tree fp8 GEMM (csrc/fp8_gemm.hip)
         # instead of hipBLASLt; "lib" keeps hipBLASLt
         self.fp8_gemm = os.environ.get("DSTACK_AMD_FP8_GEMM", "hip").lower()
+        # DSTACK_AMD_FP8_SWIGLU_GEMM=1: fp8 gate/up for batches of a multiple of 256 rows on the
+        # in-tree 256x256 GEMM with the SwiGLU and the row-wise scales in its epilogue
+        # (csrc/gemm_nt.hip EPI_SWIGLU_F8) and a one-pass row quantizer after it -- bit-identical
+        # output, but 0.99x (16384 rows) / 0.95x (256 rows) the hipBLASLt + SwiGLU-quant pair
+        # (profiles/fp8_swiglu_gemm_r7c.txt), so off by default
+        self.fp8_swiglu_gemm = os.environ.get("DSTACK_AMD_FP8_SWIGLU_GEMM", "0") == "1"
         # fp8: norms feeding an fp8 GEMM write e4m3 directly (DSTACK_AMD_FP8_FUSE_NORM=0: separate quant)
         self.fuse_norm_quant = os.environ.get("DSTACK_AMD_FP8_FUSE_NORM", "1") != "0"
         # fp8 GEMMs of at least this many rows (prefill) run hipBLASLt with scalar scales on the raw
@@ -587,8 +593,11 @@ class ServingLlama:
             # fp8 down projection past the GEMV's rows: SwiGLU and the per-token e4m3 quantization
             # in one kernel (no bf16 product written and re-read); for prefill-sized batches the
             # gate/up GEMM's row-wise scales are applied inside that kernel too
-            r = self._mm_fp8(h, wgu, defer="raw")
             C = _ext.require()
+            fused = self._swiglu_gemm_fp8(h, wgu)
+            if fused is not None:
+                return x, self._reduce(self._mm_fp8(fused, wd, defer=mode))
+            r = self._mm_fp8(h, wgu, defer="raw")
             if isinstance(r, RawScaled):
                 q, sc = C.swiglu_quant_fp8_rows(r.raw, r.rs, r.cs)
             else:
@@ -596,6 +605,27 @@ class ServingLlama:
             return x, self._reduce(self._mm_fp8(Fp8Act(q, sc), wd, defer=mode))
         gu = self._mm(h, wgu)
         return x, self._reduce(self._mm(self._swiglu(gu), wd))
+
+    def _swiglu_gemm_fp8(self, h, wgu: Fp8Weight):
+        """SwiGLU(h @ Wgu^T) quantized per token to e4m3 (an ``Fp8Act`` for the down projection) by
+        the in-tree fp8 GEMM with the SwiGLU in its epilogue, or None where it does not apply
+        (rows not a multiple of 256, untiled shapes, ``DSTACK_AMD_FP8_SWIGLU_GEMM=0``)."""
+        if not (self.hip and self.fp8_swiglu_gemm):
+            return None
+        C = _ext.require()
+        rows, K = (h.q.shape if isinstance(h, Fp8Act) else h.shape)
+        F = wgu.q.shape[0] // 2
+        if rows % 256 or not C.gemm_nt_f8_swiglu_supported(rows, F, K) or wgu.q.stride(0) % 16:
+            return None
+        if isinstance(h, Fp8Act):
+            xq, xs = h.q, h.s
+        else:
+            xq, xs = C.quant_fp8_rows(h if h.stride(-1) == 1 and h.stride(0) % 8 == 0 else h.contiguous())
+        if xq.stride(-1) != 1 or xq.stride(0) % 16:
+            return None
+        q, sc, _ = C.gemm_nt_f8_swiglu_quant(xq.view(torch.uint8), wgu.q.view(torch.uint8),
+                                              xs.reshape(-1).contiguous(), wgu.s.reshape(-1).contiguous())
+        return Fp8Act(q, sc)
 
     @staticmethod
     def _rows(h) -> int:

@@ -908,3 +908,20 @@ def test_qkv_rope_attention_fused_matches_fp32(gpu, monkeypatch, B, S, D, H, KV)
         a, b = a.float(), b.float()
         rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert rel < 1e-2, f"fused vs unfused {name}: rel {rel}"
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 1024), (256, 512, 8192), (768, 256, 28672 // 4)])
+def test_gemm_nt_f8_matches_fp32(gpu, M, N, K):
+    """The e4m3 form of the 256x256 GEMM (scaled 16x16x128 MFMA, raw product) against the fp32
+    product of the same e4m3 values."""
+    C = _ext.require()
+    assert C.gemm_nt_f8_supported(M, N, K)
+    g = torch.Generator(device=gpu).manual_seed(5)
+    a = (torch.randn(M, K, device=gpu, generator=g) * 2).to(torch.float8_e4m3fn)
+    w = (torch.randn(N, K, device=gpu, generator=g) * 2).to(torch.float8_e4m3fn)
+    out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    C.gemm_nt_f8(a.view(torch.uint8), w.view(torch.uint8), out)
+    exp = a.float() @ w.float().t()
+    rel = ((out.float() - exp).norm() / exp.norm()).item()
+    assert rel < 5e-3, rel
+    _close(out, exp, 0.0, 1e-2)

@@ -714,6 +714,49 @@ def test_gpu_fp8_deferred_row_scales_match_rowwise(gpu):
     assert cs(a, b, dim=-1).item() > 0.995
 
 
+@pytest.mark.gpu
+def test_gpu_fp8_swiglu_gemm_matches_deferred_kernels(gpu):
+    """The fp8 gate/up GEMM with the SwiGLU and the row-wise scales in its epilogue plus the
+    one-pass row quantizer (csrc/gemm_nt.hip EPI_SWIGLU_F8, fp8.hip quant_rows_pmax) against
+    hipBLASLt's raw product fed to the deferred-scale SwiGLU-quant kernel; and the fp8 engine's
+    prefill logits with the fused path on and off."""
+    from dstack_amd.ops import _ext
+    from dstack_amd.ops import reference as ref
+
+    C = _ext.require()
+    torch.manual_seed(0)
+    one = torch.ones((), device=gpu)
+    for M, F, K in ((256, 1024, 512), (512, 3584, 8192)):
+        assert C.gemm_nt_f8_swiglu_supported(M, F, K)
+        x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+        w = torch.randn(2 * F, K, device=gpu, dtype=torch.bfloat16) * 0.02
+        xq, xs = C.quant_fp8_rows(x)
+        wq, ws = ref.quant_fp8_rows(w)
+        xs = xs.reshape(-1).contiguous()
+        raw = torch._scaled_mm(xq.view(torch.float8_e4m3fn), wq.t(), scale_a=one, scale_b=one,
+                               out_dtype=torch.bfloat16)
+        q_ref, s_ref = C.swiglu_quant_fp8_rows(raw, xs, ws)
+        q, s, a = C.gemm_nt_f8_swiglu_quant(xq.view(torch.uint8), wq.view(torch.uint8), xs, ws)
+        assert torch.allclose(s, s_ref, rtol=1e-3, atol=0), (s - s_ref).abs().max().item()
+        same = (q.view(torch.uint8) == q_ref.view(torch.uint8)).float().mean().item()
+        assert same > 0.999, same
+        deq, deq_ref = q.view(torch.float8_e4m3fn).float() * s[:, None], q_ref.view(torch.float8_e4m3fn).float() * s_ref[:, None]
+        assert ((deq - deq_ref).norm() / deq_ref.norm()).item() < 1e-2
+        exp = ref.swiglu((raw.float() * xs[:, None] * ws[None, :]).bfloat16().float())
+        assert ((a.float() - exp).norm() / exp.norm()).item() < 1e-2
+    kw = dict(device="cuda", max_model_len=1024, max_batch=8, num_pages=64)
+    q8 = LLMEngine.from_model("llama-tiny", quantization="fp8", **kw)
+    n = 512  # a multiple of 256 rows: the fused gate/up path
+    prompt = torch.arange(1, n + 1, device=gpu)
+    pos = torch.arange(n, dtype=torch.int32, device=gpu)
+    slots = torch.arange(n, dtype=torch.int32, device=gpu)
+    q8.model.fp8_swiglu_gemm = False
+    a = q8.model.prefill(prompt, pos, slots, [0], [n]).float()
+    q8.model.fp8_swiglu_gemm = True
+    b = q8.model.prefill(prompt, pos, slots, [0], [n]).float()
+    assert torch.nn.functional.cosine_similarity(a, b, dim=-1).item() > 0.999
+
+
 # ------------------------------------------------------------------------------------------------
 # fp8 (e4m3) KV cache
 # ------------------------------------------------------------------------------------------------
