@@ -48,6 +48,29 @@ Object.assign(VIEWS, {
     $("#us").onclick = () => act(() => api("/api/users/update", { username: name, global_role: u.global_role, email: $("#ue").value || null, active: $("#ua").checked }));
   },
 
+  async account() {
+    // the signed-in user's own page (the reference's user settings): role, token (shown on demand,
+    // copy, refresh), projects and roles
+    const me = await api("/api/users/get_my_user");
+    const projects = await api("/api/projects/list");
+    const mine = projects.filter(p => p.members.some(m => m.user.username === me.username));
+    $("#main").innerHTML = `<h3>Account <span class="muted">${esc(me.username)}</span></h3>` +
+      table(["field", "value"], [["global role", esc(me.global_role)], ["email", esc(me.email || "")], ["created", ago(me.created_at)],
+        ["token", `<code id="mytok">••••••••</code> <a id="showtok" class="muted">[show]</a> <a id="copytok" class="muted">[copy]</a>`]]) +
+      `<div class="row"><button id="reftok">Refresh token</button><span class="muted">the old token stops working; the CLI config needs the new one</span></div>
+      <h4>Projects</h4>` + table(["project", "role", "owner"], mine.map(p => [`<a href="#projects/${encodeURIComponent(p.project_name)}">${esc(p.project_name)}</a>`,
+        esc(p.members.find(m => m.user.username === me.username).project_role), esc(p.owner.username)])) +
+      `<div class="row"><a onclick="logout()" class="muted">sign out</a></div>`;
+    const token = () => me.creds?.token || S.token;
+    $("#showtok").onclick = () => { $("#mytok").textContent = token(); };
+    $("#copytok").onclick = () => navigator.clipboard?.writeText(token());
+    $("#reftok").onclick = () => act(async () => {
+      const d = await api("/api/users/refresh_token", { username: me.username });
+      S.token = d.creds.token; localStorage.setItem("dstack_token", S.token);
+      alert("new token: " + S.token);
+    }, "Refresh your token?");
+  },
+
   async secrets() {
     const s = await api(P("secrets/list"));
     $("#main").innerHTML = `<h3>Secrets <span class="muted">${esc(S.project)}</span></h3>` + table(["name", ""], s.map(x => [esc(x.name), `<a data-s="${esc(x.name)}" class="dels muted">[delete]</a>`])) +

@@ -37,7 +37,7 @@ function login() {
 
 async function boot() {
   S.me = await api("/api/users/get_my_user");
-  $("#who").textContent = S.me.username + (S.me.global_role === "admin" ? " (admin)" : "");
+  $("#who").innerHTML = `<a href="#account" class="muted">${esc(S.me.username)}${S.me.global_role === "admin" ? " (admin)" : ""}</a>`;
   const projects = await api("/api/projects/list");
   if (!projects.find(p => p.project_name === S.project) && projects.length) S.project = projects[0].project_name;
   $("#project").innerHTML = projects.map(p => `<option ${p.project_name === S.project ? "selected" : ""}>${esc(p.project_name)}</option>`).join("");

@@ -22,9 +22,15 @@ Object.assign(VIEWS, {
       return [esc(f.name), conf.ssh_config ? "ssh" : "cloud", live.length, gpus, `${busy}/${blocks}`,
               [...new Set(live.map(i => i.backend))].map(esc).join(", "), st(f.status), ago(f.created_at)];
     });
-    $("#main").innerHTML = `<h3>Fleets</h3><div class="row"><a href="#newfleet" class="muted">+ add SSH hosts</a> <a href="#apply" class="muted">+ new fleet (YAML)</a></div>` +
-      table(["fleet", "kind", "instances", "GPUs", "busy blocks", "backends", "status", "created"], rows, true);
+    $("#main").innerHTML = `<h3>Fleets</h3><div class="row"><a href="#newfleet" class="muted">+ add SSH hosts</a> <a href="#apply" class="muted">+ new fleet (YAML)</a>
+        <button id="fdel" disabled>Delete selected</button></div>` +
+      table(["", "fleet", "kind", "instances", "GPUs", "busy blocks", "backends", "status", "created"],
+            rows.map((r, i) => [`<input type="checkbox" class="fsel" value="${esc(fleets[i].name)}">`, ...r]), true);
     bindRows(fleets, f => location.hash = "#fleets/" + encodeURIComponent(f.name));
+    const picked = () => $$(".fsel").filter(c => c.checked).map(c => c.value);
+    $$(".fsel").forEach(c => { c.onclick = (e) => e.stopPropagation(); c.onchange = () => { $("#fdel").disabled = !picked().length; }; });
+    $("#fdel").onclick = () => act(() => api(P("fleets/delete"), { names: picked() }),
+      `Delete fleet(s) ${picked().join(", ")} and terminate their instances?`);
   },
 
   async fleet(name, tab = "instances") {

@@ -10,6 +10,7 @@ Object.assign(VIEWS, {
     const pref = Object.assign({ page: 50, cols: ALL_COLS }, JSON.parse(localStorage.getItem("dstack_runs_prefs") || "{}"));
     const body = (extra = {}) => ({ project_name: S.project, limit: pref.page, only_active: f.active, ...extra });
     let runs = await api("/api/runs/list", body());
+    const sel = new Set();  // selected run names (kept across refreshes)
     const shown = () => runs.filter(r => (!f.status || r.status === f.status) && (!f.type || r.run_spec.configuration.type === f.type) &&
       (!f.q || (r.run_spec.run_name + " " + r.user).toLowerCase().includes(f.q.toLowerCase())));
     const render = () => {
@@ -20,16 +21,38 @@ Object.assign(VIEWS, {
         <select id="ft">${["", "task", "service", "dev-environment"].map(s => `<option value="${s}" ${s === f.type ? "selected" : ""}>${s || "any type"}</option>`).join("")}</select>
         <input id="fq" placeholder="name or user" value="${esc(f.q)}"><label><input type="checkbox" id="fr" ${f.refresh ? "checked" : ""}> auto-refresh</label>
         <a href="#apply" class="muted">+ new run</a> <a id="prefs" class="muted">[preferences]</a></div>
+        <div class="row"><span class="muted" id="nsel">0 selected</span><button id="bstop" disabled>Stop</button>
+          <button id="babort" disabled>Abort</button><button id="bdel" disabled>Delete</button></div>
         <div id="prefbox" class="row" hidden>page size <select id="pg">${[10, 25, 50, 100].map(n => `<option ${n === pref.page ? "selected" : ""}>${n}</option>`).join("")}</select>
           ${ALL_COLS.map(c => `<label><input type="checkbox" class="pc" value="${c}" ${pref.cols.includes(c) ? "checked" : ""}> ${c}</label>`).join(" ")}</div>` +
-        table(pref.cols, rows.map(r => {
+        table([`<input type="checkbox" id="selall">`, ...pref.cols], rows.map(r => {
           const j = r.latest_job_submission || {}; const jpd = j.job_provisioning_data;
           const cell = { name: esc(r.run_spec.run_name), type: esc(r.run_spec.configuration.type), user: esc(r.user), backend: jpd ? esc(jpd.backend) : "",
             resources: res(jpd), "price/h": jpd ? "$" + (+jpd.price).toFixed(2) : "", cost: "$" + (+r.cost || 0).toFixed(2),
             status: st(r.status) + (r.error ? ` <span class="err">${esc(r.error)}</span>` : ""), submitted: ago(r.submitted_at) };
-          return pref.cols.map(c => cell[c]);
+          return [`<input type="checkbox" class="rsel" value="${esc(r.run_spec.run_name)}" ${sel.has(r.run_spec.run_name) ? "checked" : ""}>`,
+                  ...pref.cols.map(c => cell[c])];
         }), true) + (runs.length && runs.length % pref.page === 0 ? `<div class="row"><button id="more">Load more</button></div>` : "");
       bindRows(rows, r => location.hash = "#runs/" + encodeURIComponent(r.run_spec.run_name));
+      // bulk actions over the selected runs (the reference's run list: stop / abort / delete)
+      const FINISHED = ["done", "failed", "terminated", "aborted"];
+      const picked = () => runs.filter(r => sel.has(r.run_spec.run_name));
+      const sync = () => {
+        const p = picked();
+        $("#nsel").textContent = `${p.length} selected`;
+        $("#bstop").disabled = $("#babort").disabled = !p.some(r => !FINISHED.includes(r.status));
+        $("#bdel").disabled = !p.length || !p.every(r => FINISHED.includes(r.status));
+      };
+      $$(".rsel").forEach(cb => { cb.onclick = (e) => e.stopPropagation();
+        cb.onchange = () => { cb.checked ? sel.add(cb.value) : sel.delete(cb.value); sync(); }; });
+      $("#selall").onclick = (e) => e.stopPropagation();
+      $("#selall").onchange = () => { rows.forEach(r => $("#selall").checked ? sel.add(r.run_spec.run_name) : sel.delete(r.run_spec.run_name)); render(); };
+      const bulk = (body, path, q) => act(() => api(P(path), { runs_names: picked().map(r => r.run_spec.run_name), ...body })
+        .then(() => sel.clear()), q);
+      $("#bstop").onclick = () => bulk({ abort: false }, "runs/stop");
+      $("#babort").onclick = () => bulk({ abort: true }, "runs/stop", `Abort ${picked().length} run(s)?`);
+      $("#bdel").onclick = () => bulk({}, "runs/delete", `Delete ${picked().length} run(s)?`);
+      sync();
       const save = () => localStorage.setItem("dstack_runs_filter", JSON.stringify(f));
       const savePrefs = () => { localStorage.setItem("dstack_runs_prefs", JSON.stringify(pref)); route(); };
       $("#prefs").onclick = () => { $("#prefbox").hidden = !$("#prefbox").hidden; };
@@ -50,7 +73,7 @@ Object.assign(VIEWS, {
     if (f.refresh) timers.push(setInterval(async () => {
       if (document.activeElement === $("#fq")) return;
       const fresh = await api("/api/runs/list", body()).catch(() => null);
-      if (fresh && runs.length <= pref.page) { runs = fresh; render(); }
+      if (fresh && runs.length <= pref.page && !document.activeElement?.classList.contains("rsel")) { runs = fresh; render(); }
     }, 5000));
   },
 
@@ -63,7 +86,7 @@ Object.assign(VIEWS, {
       ${r.service ? `<span class="muted">service: <a href="${esc(r.service.url)}">${esc(r.service.url)}</a>${r.service.model ? ` · model ${esc(r.service.model.name)} at ${esc(r.service.model.base_url)}` : ""}</span>` : ""}
       <span class="muted">${esc(conf.type)} · by ${esc(r.user)} · submitted ${ago(r.submitted_at)} · cost $${(+r.cost || 0).toFixed(2)}
       ${r.termination_reason ? " · reason: " + esc(r.termination_reason) : ""}</span>${r.error ? `<span class="err">${esc(r.error)}</span>` : ""}</div>
-      ${tabs("rtabs", ["overview", "logs", "metrics", "configuration"], tab)}<div id="tab"></div>`;
+      ${tabs("rtabs", ["overview", "jobs", "logs", "metrics", "configuration"], tab)}<div id="tab"></div>`;
     bindTabs("rtabs", t => location.hash = `#runs/${encodeURIComponent(name)}/${t}`);
     if (finished) $("#del").onclick = () => act(() => api(P("runs/delete"), { runs_names: [name] }).then(() => location.hash = "#runs"), `Delete ${name}?`);
     else {
@@ -100,6 +123,27 @@ const RUN_TABS = {
     if (ports.length) html += `<div class="muted">ports: ${esc(ports.join(", "))}</div>`;
     $("#tab").innerHTML = html;
     if (!["done", "failed", "terminated"].includes(r.status)) timers.push(setInterval(() => { if (location.hash.endsWith("/overview") || location.hash === "#runs/" + encodeURIComponent(name)) route(); }, 5000));
+  },
+
+  jobs(r) {
+    // one section per job: what it runs (image, commands, env names, requirements) and where its
+    // latest submission landed (instance, GPUs, ports, volumes), the full specs on demand
+    $("#tab").innerHTML = r.jobs.map((j, i) => {
+      const spec = j.job_spec, sub = j.job_submissions.at(-1) || {}, jpd = sub.job_provisioning_data, jrd = sub.job_runtime_data || {};
+      const req = spec.requirements || {};
+      return `<h4>${esc(jobLabel(j))} ${st(sub.status)}</h4>` + table(["field", "value"], [
+        ["image", esc(spec.image_name || "")], ["commands", `<pre>${esc((spec.commands || []).join("\n"))}</pre>`],
+        ["working dir", esc(spec.working_dir || "")], ["env", esc(Object.keys(spec.env || {}).join(", "))],
+        ["requirements", esc(yamlish(req.resources || req).trim().replace(/\n/g, " "))],
+        ["max duration", spec.max_duration ? dur(spec.max_duration) : "-"], ["retry", esc(JSON.stringify(spec.retry || null))],
+        ["instance", jpd ? `${esc(jpd.backend)}/${esc(jpd.region)} ${esc(jpd.instance_id || "")} ${esc(jpd.hostname || "")}` : ""],
+        ["resources", res(jpd)], ["GPU indices", esc((jrd.gpu_indices || []).join(","))],
+        ["ports", esc(Object.entries(jrd.ports || {}).map(([c, h]) => `${c}→${h}`).join(", "))],
+        ["volumes", esc((jrd.volume_names || spec.volumes || []).map(v => typeof v === "string" ? v : v.name || JSON.stringify(v)).join(", "))],
+        ["submissions", String(j.job_submissions.length)]]) +
+        `<details><summary class="muted">job spec (JSON)</summary><pre>${esc(JSON.stringify(spec, null, 1))}</pre></details>` +
+        `<details><summary class="muted">latest submission (JSON)</summary><pre>${esc(JSON.stringify(sub, null, 1))}</pre></details>`;
+    }).join("");
   },
 
   async logs(r, name) {

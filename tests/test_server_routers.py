@@ -253,7 +253,10 @@ def test_web_ui_served(client):
                    "fleet_ids", "job_submissions",
                    # overview, SSH-fleet form, project gateways / CLI tabs, member suggestions
                    "home()", "newfleet()", 'P("fleets/get_plan")', 'P("fleets/create")', "dstack config --url",
-                   'G("set_default")', "known-users"):
+                   'G("set_default")', "known-users",
+                   # bulk run / fleet actions, a run's jobs tab, the signed-in user's account page
+                   '"runs/stop"', '"runs/delete"', "runs_names: picked()", "fleets/delete\"), { names: picked()", "jobs(r)",
+                   "account()", '"/api/users/get_my_user"'):
         assert needle in text, needle
 
 
