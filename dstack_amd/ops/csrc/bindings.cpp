@@ -53,6 +53,7 @@ bool dsa_gemm_nt_supported(int, int, int);
 hipError_t dsa_gemm_nt(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 bool dsa_gemm_nt_rope_supported(int, int, int, int, int);
 bool dsa_gemm_nt_f8_supported(int, int, int);
+void dsa_gemm_nt_set_grid(int);
 bool dsa_gemm_nt_f8_swiglu_supported(int, int, int);
 hipError_t dsa_gemm_nt_f8_swiglu(const void*, const void*, void*, float*, const float*, const float*, int, int, int,
                                  long, long, hipStream_t);
@@ -925,6 +926,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_trace", &gemm_nt_trace);
   m.def("gemm_nt_rope", &gemm_nt_rope);
   m.def("gemm_nt_f8", &gemm_nt_f8);
+  m.def("gemm_nt_set_grid", [](int64_t mode) { dsa_gemm_nt_set_grid((int)mode); },
+        "in-tree GEMM grid form: -1 environment default, 0 one workgroup per tile, 1 persistent");
   m.def("gemm_nt_f8_supported", &gemm_nt_f8_supported);
   m.def("gemm_nt_f8_swiglu_quant", &gemm_nt_f8_swiglu_quant);
   m.def("gemm_nt_f8_swiglu_supported", &gemm_nt_f8_swiglu_supported);

@@ -1009,6 +1009,14 @@ int* nt_queue_slot(hipStream_t st) {
 template <int EPI>
 constexpr bool nt_dynamic_ok() { return EPI != EPI_SWIGLU && EPI != EPI_SWIGLU_BWD; }
 
+// Grid form chosen at run time (dsa_gemm_nt_set_grid): -1 = DSTACK_AMD_GEMM_NT_PERSISTENT (default
+// persistent), 0 = one workgroup per tile, 1 = persistent.  The trainer picks the per-tile grid for
+// the micro-batch whose backward runs beside RCCL's reduce-scatter / all-gather: a collective's
+// workgroups hold CUs, and a persistent grid's workgroups on those CUs then start only when the
+// collective ends (tools/diag/cu_hog.py, profiles/cu_hog_*_r9q.txt: 1.53 -> 2.31 ms for the
+// gate/up GEMM beside 32 held CUs, 1.72 per tile).
+std::atomic<int> g_nt_grid{-1};
+
 template <int EPI, bool TRACE = false, bool KM = false, bool F8 = false>
 hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
   static bool attr = false;
@@ -1031,7 +1039,8 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
     const char* v = getenv("DSTACK_AMD_GEMM_NT_DYNAMIC");
     return v && atoi(v) == 1;
   }();
-  if (persistent && tiles > cap && cap >= 8) {
+  const int mode = g_nt_grid.load(std::memory_order_relaxed);
+  if ((mode >= 0 ? mode == 1 : persistent) && tiles > cap && cap >= 8) {
     grid = cap;
     a.wg_per_xcd = cap / 8;
     if (dynamic && !TRACE && nt_dynamic_ok<EPI>()) a.queue = nt_queue_slot(st);
@@ -1044,6 +1053,9 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
 }  // namespace
 
 extern "C" bool dsa_gemm_nt_supported(int M, int N, int K) { return nt_shape_ok(M, N, K); }
+
+// -1: the environment's default grid form, 0: one workgroup per tile, 1: persistent (see g_nt_grid)
+extern "C" void dsa_gemm_nt_set_grid(int mode) { g_nt_grid.store(mode < 0 ? -1 : (mode ? 1 : 0)); }
 
 // C[M][N] (+)= A[M][K] B[N][K]^T.  Leading dimensions in elements, multiples of 8 (16-byte rows);
 // every operand must be < 4 GiB from its tile origin (32-bit DMA offsets).

@@ -84,6 +84,15 @@ def init_distributed(backend: str | None = None) -> DistEnv:
     return env
 
 
+def _gemm_grid(mode: int) -> None:
+    """Set the in-tree GEMM's grid form (-1 default, 0 per tile, 1 persistent) if the extension is
+    loaded (host-side setting, read at each launch)."""
+    from dstack_amd.ops import _ext
+
+    if _ext.available():
+        _ext.require().gemm_nt_set_grid(mode)
+
+
 class Trainer:
     def __init__(self, model_name: str, seq_len: int, micro_batch: int, device, lr: float = 3e-4,
                  seed: int = 0, bucket_numel: int = 256 * 1024 * 1024, grad_accum: int = 1,
@@ -140,6 +149,14 @@ class Trainer:
         self._i = 0
         self.trace_next_step = False
         self.last_split = None
+        # grid form of the in-tree GEMM for the last micro-batch, whose backward runs beside the
+        # reduce-scatter / AdamW / all-gather (DSTACK_AMD_GEMM_GRID_LAST = tile | persistent | auto):
+        # auto = one workgroup per tile when there are collectives (a persistent grid waits for the
+        # CUs the collective's workgroups hold), the default form otherwise
+        mode = os.environ.get("DSTACK_AMD_GEMM_GRID_LAST", "auto").lower()
+        self._last_grid = {"tile": 0, "persistent": 1}.get(mode)
+        if mode == "auto":
+            self._last_grid = 0 if self.opt.collectives else None
 
     def batch(self):
         if self.stream is not None:
@@ -187,6 +204,7 @@ class Trainer:
 
         self.opt.zero_grad()
         total = None
+        grid = _gemm_grid if self._last_grid is not None and self.device.type == "cuda" else None
         for i in range(self.grad_accum):
             t0 = time.time()
             tokens, targets = self.batch()
@@ -194,7 +212,13 @@ class Trainer:
             self.opt.sync_grads = i == self.grad_accum - 1
             loss = self.model.loss(tokens, targets)
             t0 = mark("fwd", t0)
-            (loss / self.grad_accum if self.grad_accum > 1 else loss).backward()
+            if grid is not None and self.opt.sync_grads:
+                grid(self._last_grid)
+            try:
+                (loss / self.grad_accum if self.grad_accum > 1 else loss).backward()
+            finally:
+                if grid is not None and self.opt.sync_grads:
+                    grid(-1)
             mark("bwd", t0)
             total = loss.detach() if total is None else total + loss.detach()
         t0 = time.time()

@@ -312,3 +312,30 @@ def test_trainer_close_frees_model_and_optimizer(monkeypatch):
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def test_trainer_picks_gemm_grid_for_the_communicating_micro_batch(monkeypatch):
+    """DSTACK_AMD_GEMM_GRID_LAST: auto = the per-tile GEMM grid for the last micro-batch only when
+    the optimizer runs collectives (a persistent grid waits for CUs held by RCCL's workgroups);
+    tile / persistent force it; the setting is restored after the backward."""
+    from dstack_amd.workloads import train_llama
+    from dstack_amd.workloads.train_llama import Trainer
+
+    calls = []
+    monkeypatch.setattr(train_llama, "_gemm_grid", lambda m: calls.append(m))
+    for env, want in (("auto", None), ("tile", 0), ("persistent", 1)):
+        monkeypatch.setenv("DSTACK_AMD_GEMM_GRID_LAST", env)
+        tr = Trainer("llama-tiny", 32, 2, torch.device("cpu"), grad_accum=3)
+        assert tr._last_grid == want, env
+        tr.close()
+    # on CPU no grid is ever set (the switch is for the GPU GEMM); with collectives it would be
+    monkeypatch.setenv("DSTACK_AMD_GEMM_GRID_LAST", "tile")
+    tr = Trainer("llama-tiny", 32, 2, torch.device("cpu"), grad_accum=3)
+    tr.step()
+    assert calls == []
+    tr.device = torch.device("cuda")  # exercise the switch logic without a GPU: only the grid calls
+    monkeypatch.setattr(tr.model, "loss", lambda tok, tgt: (tr.model.embed.float().sum() * 0.0) + 1.0)
+    tr.opt.step = lambda: None
+    tr.step()
+    assert calls == [0, -1]
+    tr.close()
