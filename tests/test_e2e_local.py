@@ -50,7 +50,7 @@ def test_task_runs_and_streams_logs(client):
 
     run = client.runs.submit(Task(commands=["echo hello-$DSTACK_RUN_NAME", "echo rank=$DSTACK_NODE_RANK"],
                                   name="e2e-hello"))
-    assert run.wait(timeout=60).value == "done"
+    assert run.wait(timeout=180).value == "done"
     out = _logs(run)
     assert "hello-e2e-hello" in out and "rank=0" in out
     sub = run.model.jobs[0].job_submissions[-1]
@@ -64,7 +64,7 @@ def test_task_failure_exit_code(client):
     from dstack_amd.api import Task
 
     run = client.runs.submit(Task(commands=["echo about-to-fail", "exit 7"], name="e2e-fail"))
-    assert run.wait(timeout=60).value == "failed"
+    assert run.wait(timeout=180).value == "failed"
     sub = run.model.jobs[0].job_submissions[-1]
     assert sub.exit_status == 7
     assert sub.termination_reason.value == "container_exited_with_error"
@@ -77,7 +77,7 @@ def test_env_and_secrets_interpolation(client, server):
     client.api.secrets.create_or_update("main", "MY_SECRET", "s3cr3t-value")
     run = client.runs.submit(Task(commands=["echo A=$A S=$S"], env={"A": "1", "S": "${{ secrets.MY_SECRET }}"},
                                   name="e2e-env"))
-    assert run.wait(timeout=60).value == "done"
+    assert run.wait(timeout=180).value == "done"
     assert "A=1 S=s3cr3t-value" in _logs(run)
 
 
@@ -140,7 +140,7 @@ def test_rocprof_counters_in_job_log(client, tmp_path):
     path = _fake_bin(tmp_path)
     run = client.runs.submit(Task(commands=["echo setup-ran", "echo job-ran"], name="e2e-rocprof",
                                   env={"PATH": path, "DSTACK_ROCPROF_COUNTERS": "SQ_WAVES,GRBM_GUI_ACTIVE"}))
-    assert run.wait(timeout=60).value == "done"
+    assert run.wait(timeout=180).value == "done"
     out = _logs(run)
     assert "fake-rocprof pmc: SQ_WAVES GRBM_GUI_ACTIVE" in out and "job-ran" in out and "setup-ran" in out
     assert "fake-rocprof program: echo rank=none" in out  # the program itself, not /bin/bash
@@ -151,7 +151,7 @@ def test_rocprof_counters_in_job_log(client, tmp_path):
     too_many = ",".join(f"SQ_C{i}" for i in range(9))
     run = client.runs.submit(Task(commands=["echo job-ran"], name="e2e-rocprof-bad",
                                   env={"PATH": path, "DSTACK_ROCPROF_COUNTERS": too_many}))
-    assert run.wait(timeout=60).value == "done"
+    assert run.wait(timeout=180).value == "done"
     out = _logs(run)
     assert "DSTACK_ROCPROF_COUNTERS ignored: SQ block needs 9 counters" in out
     assert "fake-rocprof pmc:\n" in out.replace("\r", "") and "job-ran" in out
@@ -167,14 +167,14 @@ def test_rocprof_per_rank_under_torchrun_and_refusal(client, tmp_path):
     (tmp_path / "t.py").write_text("import os; print('rank-ran', os.environ.get('RANK'))\n")
     run = client.runs.submit(Task(commands=[f"cd {tmp_path}", "torchrun --nproc-per-node=2 t.py"],
                                   name="e2e-rocprof-torchrun", env={"PATH": path, "DSTACK_ROCPROF": "1"}))
-    assert run.wait(timeout=60).value == "done", _logs(run)
+    assert run.wait(timeout=180).value == "done", _logs(run)
     out = _logs(run)
     assert "fake-rocprof program: python3 rank=0" in out and "fake-rocprof program: python3 rank=1" in out
     assert "rank-ran 0" in out and "rank-ran 1" in out
     assert "rocprofv3 kernel statistics (2 processes" in out and "gemm_kernel(float*, int) | 20 |" in out
     run = client.runs.submit(Task(commands=["timeout 30 echo wrapped-job"], name="e2e-rocprof-refused",
                                   env={"PATH": path, "DSTACK_ROCPROF": "1"}))
-    assert run.wait(timeout=60).value == "done"
+    assert run.wait(timeout=180).value == "done"
     out = _logs(run)
     assert "DSTACK_ROCPROF ignored: the job's last command runs 'timeout'" in out and "wrapped-job" in out
     assert "fake-rocprof" not in out
@@ -207,7 +207,7 @@ def test_stop_long_running(client):
     while "started" not in _logs(run) and time.time() < deadline:
         time.sleep(0.2)
     run.stop(abort=False)
-    st = run.wait(timeout=60)
+    st = run.wait(timeout=180)
     assert st.value in ("terminated", "aborted", "done")
     assert run.model.jobs[0].job_submissions[-1].termination_reason.value in (
         "terminated_by_user", "aborted_by_user")
@@ -221,7 +221,7 @@ def test_local_repo_code_upload(client, tmp_path):
     (tmp_path / ".gitignore").write_text("ignored.txt\n")
     (tmp_path / "ignored.txt").write_text("nope")
     run = client.runs.submit(Task(commands=["python3 train.py", "ls"], name="e2e-repo"), repo=LocalRepo(str(tmp_path)))
-    assert run.wait(timeout=60).value == "done"
+    assert run.wait(timeout=180).value == "done"
     out = _logs(run)
     assert "training-script-ran 42" in out
     assert "ignored.txt" not in out
@@ -246,7 +246,7 @@ def test_service_through_in_server_proxy(client, server):
             pass
         time.sleep(0.3)
     run.stop(abort=True)
-    run.wait(timeout=60)
+    run.wait(timeout=180)
     assert body is not None and "Directory listing" in body
 
 
@@ -279,7 +279,7 @@ def test_llm_service_through_model_proxy(client, server):
             time.sleep(0.5)
     finally:
         run.stop(abort=True)
-        run.wait(timeout=60)
+        run.wait(timeout=180)
     assert body is not None, _logs(run)[-2000:]
     assert body["choices"][0]["message"]["role"] == "assistant"
     assert 1 <= body["usage"]["completion_tokens"] <= 4
@@ -375,7 +375,7 @@ def test_service_through_local_gateway(tmp_path):
                 pass
             time.sleep(0.3)
         run.stop(abort=True)
-        run.wait(timeout=60)
+        run.wait(timeout=180)
         c.api.gateways.delete("main", ["gw"])
         assert body is not None and "Directory listing" in body
 
