@@ -107,6 +107,7 @@ struct NTArgs {
   int wg_per_xcd; // workgroups per XCD (gridDim / 8 when persistent)
   int* queue;     // dynamic tile order (persistent grids): [0..7] per-XCD tile counters, [8] exited
                   // workgroups (the last one re-zeroes the slot); null: the static order
+  float* split_ws;  // split remainder (persistent grids): fp32 partial tiles [8 * wg_per_xcd / 2][2][65536]
   unsigned long long* trace;  // TRACE builds: per-phase s_memtime stamps of workgroup 0
 };
 
@@ -297,6 +298,12 @@ __device__ __forceinline__ void km_read_b(bf16x8 (&bf)[2][2][2], const char* buf
 
 }  // namespace
 
+// the epilogues gemm_nt_split_fixup implements (the plain and fp32-accumulator ones)
+template <int EPI>
+constexpr bool nt_split_ok() {
+  return EPI == EPI_STORE || EPI == EPI_ACC || EPI == EPI_STORE32 || EPI == EPI_ACC32 || EPI == EPI_ACC32_BF16;
+}
+
 // Tile origin (first row of A/C, first B row of the tile's first 128 columns) of logical tile t.
 __device__ __forceinline__ void nt_tile_origin(const NTArgs& p, int t, int& m0, int& nb0) {
   const int ntm = p.M / NT_BM;
@@ -349,6 +356,22 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   const int per = ntiles >> 3, rem = ntiles & 7;
   const int cnt = per + (xcd < rem ? 1 : 0), start = xcd * per + (xcd < rem ? xcd : rem);
   const int stride = p.wg_per_xcd;
+  const int nk = p.K / NT_BK;
+  // Split remainder: a persistent grid runs ceil(cnt / stride) rounds per XCD; when the last round
+  // holds r <= stride / 2 tiles, those tiles are split into two K halves (units), so the last round
+  // takes half a tile's time on every workgroup instead of a whole one on half of them (the qkv
+  // weight gradient: 384 tiles = 1.5 rounds; the down projection's: 3.5).  Unit u < full is tile u;
+  // unit full + 2 s + h is half h of tile full + s; both halves store fp32 accumulators, and
+  // gemm_nt_split_fixup combines them and runs the epilogue.
+  const int rx = cnt % stride;
+  const bool split = nt_split_ok<EPI>() && !TRACE && p.split_ws != nullptr && rx > 0 && 2 * rx <= stride &&
+                     (nk & 3) == 0;
+  const int full = cnt - (split ? rx : 0);
+  const int ucnt = split ? full + 2 * rx : cnt;
+  auto utile = [&](int u) { return u < full ? u : full + ((u - full) >> 1); };
+  auto uhalf = [&](int u) { return u < full ? -1 : ((u - full) & 1); };
+  auto ukb = [&](int u) { return uhalf(u) == 1 ? (nk >> 1) : 0; };
+  auto uke = [&](int u) { return uhalf(u) == 0 ? (nk >> 1) : nk; };
   // Dynamic tile order (p.queue): instead of every (wg_per_xcd)-th tile of its XCD's slice, a
   // workgroup claims the slice's next tile from a per-XCD counter, one tile ahead (the claim for
   // tile i+2 is made at the top of tile i and read at its end, many barriers later, through two
@@ -376,13 +399,12 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
       for (int i = 0; i < 9; ++i) q[i] = 0;
     }
   };
-  if (local >= cnt) {
+  if (local >= ucnt) {
     leave();
     return;
   }
   int m0, nb0;
-  nt_tile_origin(p, start + local, m0, nb0);
-  const int nk = p.K / NT_BK;
+  nt_tile_origin(p, start + utile(local), m0, nb0);
 
   // --- DMA: per-lane source offsets (bytes) of this wave's two 1 KiB pieces of a unit ----------
   // piece i covers unit rows 16w + 8i + (lane>>3); lane's 16 B slot (lane&7) holds the chunk
@@ -432,13 +454,13 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     else nt_dma(b_src1 + kb, vb[0], vb[1], dst);
   };
   // K-tile 0 whole and K-tile 1's b0, b1 (its a0, a1 are the first phase's DMA): 12 instructions
-  auto prologue = [&]() {
-    dma(0, 0);
-    dma(1, 0);
-    dma(2, 0);
-    dma(3, 0);
-    dma(2, 1);
-    dma(3, 1);
+  auto prologue = [&](int k0) {
+    dma(0, k0);
+    dma(1, k0);
+    dma(2, k0);
+    dma(3, k0);
+    dma(2, k0 + 1);
+    dma(3, k0 + 1);
   };
 
   // --- fragment read offsets: row (lane&15) of a 16-row tile, k chunk (lane>>4) (+4 for k 32..63)
@@ -493,7 +515,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     else nt_quadrant<MS, NS>(acc, af, bf);               \
   } while (0)
   set_src(m0, nb0);
-  prologue();
+  prologue(ukb(local));
   nt_vmcnt<4>();
   nt_barrier();
 
@@ -501,10 +523,11 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     if (!STAGGERED || local == xj) {
       if (wr == 1) nt_barrier();  // group 1 runs one barrier behind
     }
-    const bool has_next = next < cnt;
+    const bool has_next = next < ucnt;
     if (q && w == 0 && lane == 0) qslot[par] = has_next ? atomicAdd(q + xcd, 1) : cnt;  // the tile after next
     int m1 = 0, nb1 = 0;
-    if (has_next) nt_tile_origin(p, start + next, m1, nb1);
+    if (has_next) nt_tile_origin(p, start + utile(next), m1, nb1);
+    const int kbn = has_next ? ukb(next) : 0;  // the next unit's first K-tile
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -519,12 +542,13 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     // vmcnt(4) at P2 / P4 keeps two units in flight and retires the tile the next phase reads.
     // With the plain epilogues the K-tile stream runs on across tiles: the last iteration loads
     // the next tile's K-tiles 0 and 1, so a tile starts with no prologue.
-    const int niter = nk >> 1;
+    const int kb0 = ukb(local);
+    const int niter = (uke(local) - kb0) >> 1;
     for (int it = 0; it < niter; ++it) {
-      const int t = 2 * it;
+      const int t = kb0 + 2 * it;
       const bool more = it + 1 < niter;
       const bool go = more || (OVERLAP && has_next);
-      const int t2 = more ? t + 2 : 0, t3 = more ? t + 3 : 1;
+      const int t2 = more ? t + 2 : kbn, t3 = more ? t + 3 : kbn + 1;
       // P1: m-subtile 0 of tile t
       stamp(it);
       read_b(bufE);
@@ -600,6 +624,22 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     }
     if constexpr (!OVERLAP) nt_barrier();  // every wave is past its last fragment read: LDS is free
 
+    // --- split remainder: each K half stores its fp32 accumulators; gemm_nt_split_fixup (launched
+    // right after on the same stream) adds the two halves and runs the epilogue for those tiles.
+    // (Waiting for the partner inside this kernel put the accumulators of two code paths through
+    // one epilogue and the register allocator spilled them on every tile.)
+    const int khalf = split ? uhalf(local) : -1;
+    if (khalf >= 0) {
+      // slot (XCD, split tile, half): wave w's 32 accumulators as lane-interleaved 16-byte pieces
+      const int slot = 2 * (xcd * (stride >> 1) + ((local - full) >> 1)) + khalf;
+      float* wsp = p.split_ws + (long)slot * 65536 + w * 8192 + 4 * lane;
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) *reinterpret_cast<f32x4*>(wsp + ((ms * 4 + mi) * 4 + n) * 256) = acc[ms][mi][n];
+    } else {
     // --- epilogue ---------------------------------------------------------------------------------
     // accumulator (ms, mi, n): tile row 128ms + 64wr + 16mi + (lane&15), tile columns
     // 128(n>>1) + 32wc + 16(n&1) + 4(lane>>4) + [0,4)
@@ -932,6 +972,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
         }
       }
     }
+    }  // khalf < 0 (the epilogue)
     if (!has_next) {
       if constexpr (STAGGERED) {
         if (wr == 0) nt_barrier();  // equal barrier counts for both groups at exit
@@ -942,7 +983,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     if constexpr (!OVERLAP) {
       nt_barrier();  // every wave is done with the LDS staging
       set_src(m1, nb1);
-      prologue();
+      prologue(kbn);
       nt_vmcnt<4>();
       nt_barrier();
     }
@@ -955,6 +996,62 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
 }
 
 #undef NT_QUAD
+
+// The epilogue of the split tiles: block b = (XCD, split tile s) adds the two K halves' fp32
+// accumulators (stored by the main kernel's threads in their accumulator layout) and writes the
+// tile as that EPI does.  Threads keep the main kernel's roles, so the piece a thread reads is the
+// accumulator f32x4 (ms, mi, n) of wave w: tile row 128 ms + 64 wr + 16 mi + (lane & 15), columns
+// 4 (lane >> 4) + [0, 4) of column block (n >> 1) * bsplit + 32 wc + 16 (n & 1).
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_nt_split_fixup(NTArgs p) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3;
+  const int half_w = p.wg_per_xcd >> 1;
+  const int xcd = blockIdx.x / half_w, sidx = blockIdx.x % half_w;
+  const int ntiles = (p.M / NT_BM) * p.ntn;
+  const int per = ntiles >> 3, rem = ntiles & 7;
+  const int cnt = per + (xcd < rem ? 1 : 0), start = xcd * per + (xcd < rem ? xcd : rem);
+  const int rx = cnt % p.wg_per_xcd;
+  if (!(rx > 0 && 2 * rx <= p.wg_per_xcd) || sidx >= rx) return;  // the main kernel's `split`
+  int m0, nb0;
+  nt_tile_origin(p, start + (cnt - rx) + sidx, m0, nb0);
+  const int slot = 2 * blockIdx.x;
+  const float* w0 = p.split_ws + (long)slot * 65536 + w * 8192 + 4 * lane;
+  const float* w1 = w0 + 65536;
+  const int er = lane & 15, ec = 4 * (lane >> 4);
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int idx = ((ms * 4 + mi) * 4 + n) * 256;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(w0 + idx) + *reinterpret_cast<const f32x4*>(w1 + idx);
+        const long row = m0 + 128 * ms + 64 * wr + 16 * mi + er;
+        const long col = nb0 + (n >> 1) * (long)p.bsplit + 32 * wc + 16 * (n & 1) + ec;
+        if constexpr (EPI == EPI_STORE || EPI == EPI_ACC) {
+          bf16_t* c = p.C + row * p.ldc + col;
+          us4 o;
+          if constexpr (EPI == EPI_ACC) {
+            const us4 old = *reinterpret_cast<const us4*>(c);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j] + bf2f(old[j]));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+          }
+          *reinterpret_cast<us4*>(c) = o;
+        } else if constexpr (EPI == EPI_STORE32 || EPI == EPI_ACC32) {
+          float* c = reinterpret_cast<float*>(p.C) + row * p.ldc + col;
+          *reinterpret_cast<f32x4*>(c) = EPI == EPI_ACC32 ? v + *reinterpret_cast<const f32x4*>(c) : v;
+        } else if constexpr (EPI == EPI_ACC32_BF16) {
+          const f32x4 o32 = *reinterpret_cast<const f32x4*>(p.F32 + row * p.ldc32 + col) + v;
+          us4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(o32[j]);
+          *reinterpret_cast<us4*>(p.C + row * p.ldc + col) = o;
+        }
+      }
+}
 
 namespace {
 
@@ -1004,10 +1101,34 @@ int* nt_queue_slot(hipStream_t st) {
   return ring[dev] + (seq[dev].fetch_add(1) % NT_QSLOTS) * 16;
 }
 
+// Split-remainder workspaces (see the kernel's `split`): a ring of NT_SPLIT_RING per device, one per
+// launch in turn (the launches of one stream are ordered; concurrent launches on other streams take
+// the other entry).  Not under stream capture (no allocation there).
+constexpr int NT_SPLIT_RING = 2;
+float* nt_split_slot(hipStream_t st, int slots) {
+  static float* ring[64][NT_SPLIT_RING] = {{nullptr}};
+  static int have[64][NT_SPLIT_RING] = {{0}};
+  static std::atomic<unsigned> seq[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  const int i = (int)(seq[dev].fetch_add(1) % NT_SPLIT_RING);
+  if (have[dev][i] < slots) {
+    float* w = nullptr;
+    if (hipMalloc(&w, (size_t)slots * 2 * 65536 * sizeof(float)) != hipSuccess) return nullptr;
+    if (ring[dev][i]) (void)hipFree(ring[dev][i]);  // (hipFree synchronises the device)
+    ring[dev][i] = w;
+    have[dev][i] = slots;
+  }
+  return ring[dev][i];
+}
+
 // EPIs whose epilogue stages through LDS (the SwiGLU forms with transposed copies) keep the
 // static order: the dynamic order's broadcast slots sit at the top of the LDS they use.
 template <int EPI>
 constexpr bool nt_dynamic_ok() { return EPI != EPI_SWIGLU && EPI != EPI_SWIGLU_BWD; }
+
 
 // Grid form chosen at run time (dsa_gemm_nt_set_grid): -1 = DSTACK_AMD_GEMM_NT_PERSISTENT (default
 // persistent), 0 = one workgroup per tile, 1 = persistent.  The trainer picks the per-tile grid for
@@ -1044,9 +1165,22 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
     grid = cap;
     a.wg_per_xcd = cap / 8;
     if (dynamic && !TRACE && nt_dynamic_ok<EPI>()) a.queue = nt_queue_slot(st);
+    // DSTACK_AMD_GEMM_NT_SPLIT=0: keep the last round's tiles whole
+    static const bool split_env = [] {
+      const char* v = getenv("DSTACK_AMD_GEMM_NT_SPLIT");
+      return !(v && atoi(v) == 0);
+    }();
+    const int per_xcd = (tiles + 7) / 8, rx = per_xcd % a.wg_per_xcd;
+    if (split_env && !a.queue && !TRACE && nt_split_ok<EPI>() && rx > 0 && 2 * rx <= a.wg_per_xcd &&
+        (a.K / NT_BK) % 4 == 0)
+      a.split_ws = nt_split_slot(st, 8 * (a.wg_per_xcd / 2));
   }
   if (const char* g = getenv("DSTACK_AMD_GEMM_NT_GROUP")) a.group = atoi(g) > 0 ? atoi(g) : a.group;
   gemm_nt_kernel<EPI, TRACE, KM, F8><<<grid, 512, NT_LDS, st>>>(a);
+  if (a.split_ws) {
+    DSA_CHECK(hipGetLastError());
+    gemm_nt_split_fixup<EPI><<<8 * (a.wg_per_xcd / 2), 512, 0, st>>>(a);
+  }
   return hipGetLastError();
 }
 
