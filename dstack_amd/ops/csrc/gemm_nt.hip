@@ -108,6 +108,7 @@ struct NTArgs {
   int* queue;     // dynamic tile order (persistent grids): [0..7] per-XCD tile counters, [8] exited
                   // workgroups (the last one re-zeroes the slot); null: the static order
   float* split_ws;  // split remainder (persistent grids): fp32 partial tiles [8 * wg_per_xcd / 2][2][65536]
+  int* split_cnt;   // one ticket counter per split tile, zero between launches
   unsigned long long* trace;  // TRACE builds: per-phase s_memtime stamps of workgroup 0
 };
 
@@ -298,7 +299,7 @@ __device__ __forceinline__ void km_read_b(bf16x8 (&bf)[2][2][2], const char* buf
 
 }  // namespace
 
-// the epilogues gemm_nt_split_fixup implements (the plain and fp32-accumulator ones)
+// the epilogues the split-remainder path runs (the plain and fp32-accumulator ones)
 template <int EPI>
 constexpr bool nt_split_ok() {
   return EPI == EPI_STORE || EPI == EPI_ACC || EPI == EPI_STORE32 || EPI == EPI_ACC32 || EPI == EPI_ACC32_BF16;
@@ -361,8 +362,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
   // holds r <= stride / 2 tiles, those tiles are split into two K halves (units), so the last round
   // takes half a tile's time on every workgroup instead of a whole one on half of them (the qkv
   // weight gradient: 384 tiles = 1.5 rounds; the down projection's: 3.5).  Unit u < full is tile u;
-  // unit full + 2 s + h is half h of tile full + s; both halves store fp32 accumulators, and
-  // gemm_nt_split_fixup combines them and runs the epilogue.
+  // unit full + 2 s + h is half h of tile full + s (see the split-remainder block after the loop).
   const int rx = cnt % stride;
   const bool split = nt_split_ok<EPI>() && !TRACE && p.split_ws != nullptr && rx > 0 && 2 * rx <= stride &&
                      (nk & 3) == 0;
@@ -624,22 +624,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     }
     if constexpr (!OVERLAP) nt_barrier();  // every wave is past its last fragment read: LDS is free
 
-    // --- split remainder: each K half stores its fp32 accumulators; gemm_nt_split_fixup (launched
-    // right after on the same stream) adds the two halves and runs the epilogue for those tiles.
-    // (Waiting for the partner inside this kernel put the accumulators of two code paths through
-    // one epilogue and the register allocator spilled them on every tile.)
-    const int khalf = split ? uhalf(local) : -1;
-    if (khalf >= 0) {
-      // slot (XCD, split tile, half): wave w's 32 accumulators as lane-interleaved 16-byte pieces
-      const int slot = 2 * (xcd * (stride >> 1) + ((local - full) >> 1)) + khalf;
-      float* wsp = p.split_ws + (long)slot * 65536 + w * 8192 + 4 * lane;
-#pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) *reinterpret_cast<f32x4*>(wsp + ((ms * 4 + mi) * 4 + n) * 256) = acc[ms][mi][n];
-    } else {
+    // --- epilogue (a lambda: the split-remainder path below runs it from its own branch) ---------
+    auto run_epilogue = [&]() {
     // --- epilogue ---------------------------------------------------------------------------------
     // accumulator (ms, mi, n): tile row 128ms + 64wr + 16mi + (lane&15), tile columns
     // 128(n>>1) + 32wc + 16(n&1) + 4(lane>>4) + [0,4)
@@ -972,10 +958,68 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
         }
       }
     }
-    }  // khalf < 0 (the epilogue)
+    };  // run_epilogue
+    // --- split remainder: both K halves of a last-round tile store their fp32 accumulators; the
+    // half that takes the tile's ticket second adds the other's and runs the epilogue (no waiting
+    // on a partner).  The epilogue is inlined once per branch: a single copy reached by both the
+    // plain and the combined accumulators made the register allocator spill them on every tile.
+    bool aligned = false;
+    if constexpr (nt_split_ok<EPI>()) {
+      const int khalf = split ? uhalf(local) : -1;
+      if (khalf >= 0) {
+        if constexpr (STAGGERED) {
+          if (wr == 0) nt_barrier();  // group 1 has finished its last phase: both groups aligned
+        }
+        aligned = true;
+        const int pair = xcd * (stride >> 1) + ((local - full) >> 1);
+        float* mine = p.split_ws + (long)(2 * pair + khalf) * 65536 + w * 8192 + 4 * lane;
+        const float* other = p.split_ws + (long)(2 * pair + (khalf ^ 1)) * 65536 + w * 8192 + 4 * lane;
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+              *reinterpret_cast<f32x4*>(mine + ((ms * 4 + mi) * 4 + n) * 256) = acc[ms][mi][n];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        nt_barrier();  // every wave's partial is stored
+        volatile int* tslot = reinterpret_cast<volatile int*>(smem + NT_LDS - 64);
+        if (w == 0 && lane == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const int t = __hip_atomic_fetch_add(p.split_cnt + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (t == 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(p.split_cnt + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+          }
+          tslot[2] = t;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the broadcast lands before the barrier
+        }
+        nt_barrier();
+        if (tslot[2] == 1) {
+          // 4 pieces at a time (the compiler would issue all 32 loads first: 128 more VGPRs)
+#pragma unroll
+          for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+              for (int n = 0; n < 4; ++n)
+                acc[ms][mi][n] += *reinterpret_cast<const f32x4*>(other + ((ms * 4 + mi) * 4 + n) * 256);
+#pragma unroll
+              for (int n = 0; n < 4; ++n) asm volatile("" : "+v"(acc[ms][mi][n])::"memory");
+            }
+          run_epilogue();
+        }
+      } else {
+        run_epilogue();
+      }
+    } else {
+      run_epilogue();
+    }
     if (!has_next) {
       if constexpr (STAGGERED) {
-        if (wr == 0) nt_barrier();  // equal barrier counts for both groups at exit
+        if (wr == 0 && !aligned) nt_barrier();  // equal barrier counts for both groups at exit
       }
       leave();
       break;
@@ -996,62 +1040,6 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
 }
 
 #undef NT_QUAD
-
-// The epilogue of the split tiles: block b = (XCD, split tile s) adds the two K halves' fp32
-// accumulators (stored by the main kernel's threads in their accumulator layout) and writes the
-// tile as that EPI does.  Threads keep the main kernel's roles, so the piece a thread reads is the
-// accumulator f32x4 (ms, mi, n) of wave w: tile row 128 ms + 64 wr + 16 mi + (lane & 15), columns
-// 4 (lane >> 4) + [0, 4) of column block (n >> 1) * bsplit + 32 wc + 16 (n & 1).
-template <int EPI>
-__global__ __launch_bounds__(512) void gemm_nt_split_fixup(NTArgs p) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3;
-  const int half_w = p.wg_per_xcd >> 1;
-  const int xcd = blockIdx.x / half_w, sidx = blockIdx.x % half_w;
-  const int ntiles = (p.M / NT_BM) * p.ntn;
-  const int per = ntiles >> 3, rem = ntiles & 7;
-  const int cnt = per + (xcd < rem ? 1 : 0), start = xcd * per + (xcd < rem ? xcd : rem);
-  const int rx = cnt % p.wg_per_xcd;
-  if (!(rx > 0 && 2 * rx <= p.wg_per_xcd) || sidx >= rx) return;  // the main kernel's `split`
-  int m0, nb0;
-  nt_tile_origin(p, start + (cnt - rx) + sidx, m0, nb0);
-  const int slot = 2 * blockIdx.x;
-  const float* w0 = p.split_ws + (long)slot * 65536 + w * 8192 + 4 * lane;
-  const float* w1 = w0 + 65536;
-  const int er = lane & 15, ec = 4 * (lane >> 4);
-#pragma unroll
-  for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int idx = ((ms * 4 + mi) * 4 + n) * 256;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(w0 + idx) + *reinterpret_cast<const f32x4*>(w1 + idx);
-        const long row = m0 + 128 * ms + 64 * wr + 16 * mi + er;
-        const long col = nb0 + (n >> 1) * (long)p.bsplit + 32 * wc + 16 * (n & 1) + ec;
-        if constexpr (EPI == EPI_STORE || EPI == EPI_ACC) {
-          bf16_t* c = p.C + row * p.ldc + col;
-          us4 o;
-          if constexpr (EPI == EPI_ACC) {
-            const us4 old = *reinterpret_cast<const us4*>(c);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j] + bf2f(old[j]));
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
-          }
-          *reinterpret_cast<us4*>(c) = o;
-        } else if constexpr (EPI == EPI_STORE32 || EPI == EPI_ACC32) {
-          float* c = reinterpret_cast<float*>(p.C) + row * p.ldc + col;
-          *reinterpret_cast<f32x4*>(c) = EPI == EPI_ACC32 ? v + *reinterpret_cast<const f32x4*>(c) : v;
-        } else if constexpr (EPI == EPI_ACC32_BF16) {
-          const f32x4 o32 = *reinterpret_cast<const f32x4*>(p.F32 + row * p.ldc32 + col) + v;
-          us4 o;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = f2bf(o32[j]);
-          *reinterpret_cast<us4*>(p.C + row * p.ldc + col) = o;
-        }
-      }
-}
 
 namespace {
 
@@ -1103,25 +1091,36 @@ int* nt_queue_slot(hipStream_t st) {
 
 // Split-remainder workspaces (see the kernel's `split`): a ring of NT_SPLIT_RING per device, one per
 // launch in turn (the launches of one stream are ordered; concurrent launches on other streams take
-// the other entry).  Not under stream capture (no allocation there).
+// the other entry): fp32 partials and one ticket counter per split tile (zeroed once; the second
+// arriver re-zeroes it).  Not under stream capture (no allocation there).
 constexpr int NT_SPLIT_RING = 2;
-float* nt_split_slot(hipStream_t st, int slots) {
-  static float* ring[64][NT_SPLIT_RING] = {{nullptr}};
+bool nt_split_slot(hipStream_t st, int pairs, float** ws, int** cnt) {
+  static float* wring[64][NT_SPLIT_RING] = {{nullptr}};
+  static int* cring[64][NT_SPLIT_RING] = {{nullptr}};
   static int have[64][NT_SPLIT_RING] = {{0}};
   static std::atomic<unsigned> seq[64];
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
   const int i = (int)(seq[dev].fetch_add(1) % NT_SPLIT_RING);
-  if (have[dev][i] < slots) {
+  if (have[dev][i] < pairs) {
     float* w = nullptr;
-    if (hipMalloc(&w, (size_t)slots * 2 * 65536 * sizeof(float)) != hipSuccess) return nullptr;
-    if (ring[dev][i]) (void)hipFree(ring[dev][i]);  // (hipFree synchronises the device)
-    ring[dev][i] = w;
-    have[dev][i] = slots;
+    int* c = nullptr;
+    if (hipMalloc(&w, (size_t)pairs * 2 * 65536 * sizeof(float)) != hipSuccess) return false;
+    if (hipMalloc(&c, (size_t)pairs * sizeof(int)) != hipSuccess || hipMemset(c, 0, (size_t)pairs * sizeof(int)) != hipSuccess) {
+      (void)hipFree(w);
+      return false;
+    }
+    if (wring[dev][i]) (void)hipFree(wring[dev][i]);  // (hipFree synchronises the device)
+    if (cring[dev][i]) (void)hipFree(cring[dev][i]);
+    wring[dev][i] = w;
+    cring[dev][i] = c;
+    have[dev][i] = pairs;
   }
-  return ring[dev][i];
+  *ws = wring[dev][i];
+  *cnt = cring[dev][i];
+  return true;
 }
 
 // EPIs whose epilogue stages through LDS (the SwiGLU forms with transposed copies) keep the
@@ -1173,14 +1172,10 @@ hipError_t nt_launch(NTArgs a, int tiles, hipStream_t st) {
     const int per_xcd = (tiles + 7) / 8, rx = per_xcd % a.wg_per_xcd;
     if (split_env && !a.queue && !TRACE && nt_split_ok<EPI>() && rx > 0 && 2 * rx <= a.wg_per_xcd &&
         (a.K / NT_BK) % 4 == 0)
-      a.split_ws = nt_split_slot(st, 8 * (a.wg_per_xcd / 2));
+      if (!nt_split_slot(st, 8 * (a.wg_per_xcd / 2), &a.split_ws, &a.split_cnt)) a.split_ws = nullptr;
   }
   if (const char* g = getenv("DSTACK_AMD_GEMM_NT_GROUP")) a.group = atoi(g) > 0 ? atoi(g) : a.group;
   gemm_nt_kernel<EPI, TRACE, KM, F8><<<grid, 512, NT_LDS, st>>>(a);
-  if (a.split_ws) {
-    DSA_CHECK(hipGetLastError());
-    gemm_nt_split_fixup<EPI><<<8 * (a.wg_per_xcd / 2), 512, 0, st>>>(a);
-  }
   return hipGetLastError();
 }
 
