@@ -823,38 +823,44 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(NTArgs p) {
     } else if constexpr (EPI == EPI_SWIGLU_BWD_R) {
       // acc = da[t][f] (plain column map); 16-byte pieces of 8 consecutive f: g, u loaded, dg, du
       // stored -- dg = da * u * silu'(g), du = da * silu(g), da rounded to bf16 as the unfused path
+      // g, u of row group i + 1 are loaded while group i is computed and stored (two register
+      // sets of 16 VGPRs): each group's load latency was exposed, 8 times per tile
       const int q = lane >> 4;
       const int pc = 32 * wc + 16 * (q & 1) + 8 * (q >> 1);
       const long rbase = (long)(m0 + 64 * wr + er) * (2L * p.F) + nb0 + pc;
+      us8 g8[2][2], u8[2][2];
+      auto load_gu = [&](int i, int b) {
+        const long ro = rbase + (long)(128 * (i >> 2) + 16 * (i & 3)) * (2L * p.F);
 #pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const long ro = rbase + (long)(128 * ms + 16 * mi) * (2L * p.F);
-          us8 g8[2], u8[2];
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp) {
-            g8[pp] = *reinterpret_cast<const us8*>(p.G + ro + 128 * pp);
-            u8[pp] = *reinterpret_cast<const us8*>(p.G + ro + 128 * pp + p.F);
-          }
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp) {
-            float v[8];
-            nt_pair8f(acc[ms][mi][2 * pp], acc[ms][mi][2 * pp + 1], v);
-            us8 dg, du;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float da = bf2f(f2bf(v[j]));
-              const float g = bf2f(g8[pp][j]), u = bf2f(u8[pp][j]);
-              const float sg = 1.f / (1.f + __expf(-g));
-              const float sl = g * sg;
-              dg[j] = f2bf(da * u * (sg + sl * (1.f - sg)));
-              du[j] = f2bf(da * sl);
-            }
-            *reinterpret_cast<us8*>(p.C + ro + 128 * pp) = dg;
-            *reinterpret_cast<us8*>(p.C + ro + 128 * pp + p.F) = du;
-          }
+        for (int pp = 0; pp < 2; ++pp) {
+          g8[b][pp] = *reinterpret_cast<const us8*>(p.G + ro + 128 * pp);
+          u8[b][pp] = *reinterpret_cast<const us8*>(p.G + ro + 128 * pp + p.F);
         }
+      };
+      load_gu(0, 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int ms = i >> 2, mi = i & 3, b = i & 1;
+        if (i + 1 < 8) load_gu(i + 1, b ^ 1);
+        const long ro = rbase + (long)(128 * ms + 16 * mi) * (2L * p.F);
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          float v[8];
+          nt_pair8f(acc[ms][mi][2 * pp], acc[ms][mi][2 * pp + 1], v);
+          us8 dg, du;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float da = bf2f(f2bf(v[j]));
+            const float g = bf2f(g8[b][pp][j]), u = bf2f(u8[b][pp][j]);
+            const float sg = 1.f / (1.f + __expf(-g));
+            const float sl = g * sg;
+            dg[j] = f2bf(da * u * (sg + sl * (1.f - sg)));
+            du[j] = f2bf(da * sl);
+          }
+          *reinterpret_cast<us8*>(p.C + ro + 128 * pp) = dg;
+          *reinterpret_cast<us8*>(p.C + ro + 128 * pp + p.F) = du;
+        }
+      }
     } else if constexpr (EPI == EPI_SWIGLU) {
       // gu and a = silu(g) * u (from the bf16-rounded g, u: what the backward re-reads from gu)
       // straight from the accumulators; a^T through the spare LDS, one 128-token half at a time
