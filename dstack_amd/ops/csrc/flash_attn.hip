@@ -488,8 +488,11 @@ __global__ __launch_bounds__(256, DKDV_WAVES_PER_SIMD) void fa_bwd_dkdv_kernel(
 // while the current MFMA runs (S and dP alternate, so consecutive MFMAs never share an accumulator),
 // pinned with sched_group_barrier; without it the compiler serialises read -> lgkmcnt(0) -> MFMA
 // for most of the 16 steps.
+// P16 (DSTACK_AMD_FA_DKDV_BF16, default on): the per-query-head dK/dV partials go to HBM as bf16 (the
+// layout flash-attention 2 uses for its GQA expansion: per-head bf16 partials, summed in fp32 by the
+// group reduction), halving the 2 x B*S*H*128 partial bytes written here and read back by the reduce.
 template <bool CAUSAL, bool SEED = false, bool HP = false, bool SPILL = false, bool GQA = false, bool TR = false,
-          int PF = 0>
+          int PF = 0, bool P16 = false>
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dkp, float* __restrict__ dvp, int B, int S,
@@ -752,8 +755,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
       }
   } else if (qh == 0) {
     const float sm = scale_log2 * 0.6931471805599453f;  // softmax scale = scale_log2 * ln2
-    float* dkr = dkp + (((long)b * S + mykey) * H + hh) * HD;
-    float* dvr = dvp + (((long)b * S + mykey) * H + hh) * HD;
+    const long row = (((long)b * S + mykey) * H + hh) * HD;
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
@@ -766,8 +768,15 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8_kernel(
           ok[i] = (dk[d][r] + red[(((g * 2 + 0) * 4 + d) * 16 + r) * 64 + lane]) * sm;
           ov[i] = dv[d][r] + red[(((g * 2 + 1) * 4 + d) * 16 + r) * 64 + lane];
         }
-        *reinterpret_cast<f4*>(dkr + dd) = ok;
-        *reinterpret_cast<f4*>(dvr + dd) = ov;
+        if constexpr (P16) {
+          *reinterpret_cast<us4*>(reinterpret_cast<bf16_t*>(dkp) + row + dd) =
+              us4{f2bf(ok[0]), f2bf(ok[1]), f2bf(ok[2]), f2bf(ok[3])};
+          *reinterpret_cast<us4*>(reinterpret_cast<bf16_t*>(dvp) + row + dd) =
+              us4{f2bf(ov[0]), f2bf(ov[1]), f2bf(ov[2]), f2bf(ov[3])};
+        } else {
+          *reinterpret_cast<f4*>(dkp + row + dd) = ok;
+          *reinterpret_cast<f4*>(dvp + row + dd) = ov;
+        }
       }
   }
 }
@@ -1012,8 +1021,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8d_kernel(
   __syncthreads();
   if (qh == 0) {
     const float sm = scale_log2 * 0.6931471805599453f;  // softmax scale = scale_log2 * ln2
-    float* dkr = dkp + (((long)b * S + mykey) * H + hh) * HD;
-    float* dvr = dvp + (((long)b * S + mykey) * H + hh) * HD;
+    const long row = (((long)b * S + mykey) * H + hh) * HD;
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
@@ -1026,8 +1034,8 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkdv8d_kernel(
           ok[i] = (dk[d][r] + red[(((g * 2 + 0) * 4 + d) * 16 + r) * 64 + lane]) * sm;
           ov[i] = dv[d][r] + red[(((g * 2 + 1) * 4 + d) * 16 + r) * 64 + lane];
         }
-        *reinterpret_cast<f4*>(dkr + dd) = ok;
-        *reinterpret_cast<f4*>(dvr + dd) = ov;
+        *reinterpret_cast<f4*>(dkp + row + dd) = ok;
+        *reinterpret_cast<f4*>(dvp + row + dd) = ov;
       }
   }
 }
@@ -1197,7 +1205,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv64_kernel(
   }
 }
 
-// sum the per-q-head fp32 partials over each GQA group -> bf16 dk/dv inside dqkv
+// sum the per-q-head fp32 (P16: bf16) partials over each GQA group -> bf16 dk/dv inside dqkv
+template <bool P16 = false>
 __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __restrict__ dkp,
                                                                const float* __restrict__ dvp,
                                                                bf16_t* __restrict__ dqkv, int B,
@@ -1213,15 +1222,26 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __re
     float ak[8] = {0, 0, 0, 0, 0, 0, 0, 0}, av[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int g = 0; g < G; ++g) {
       const long src = (bs * H + kvh * G + g) * HD + c * 8;
-      const f4* pk = reinterpret_cast<const f4*>(dkp + src);
-      const f4* pv = reinterpret_cast<const f4*>(dvp + src);
-      const f4 k0 = pk[0], k1 = pk[1], v0 = pv[0], v1 = pv[1];
+      if constexpr (P16) {
+        float k8[8], v8[8];
+        unpack8(*reinterpret_cast<const us8*>(reinterpret_cast<const bf16_t*>(dkp) + src), k8);
+        unpack8(*reinterpret_cast<const us8*>(reinterpret_cast<const bf16_t*>(dvp) + src), v8);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        ak[j] += k0[j];
-        ak[4 + j] += k1[j];
-        av[j] += v0[j];
-        av[4 + j] += v1[j];
+        for (int j = 0; j < 8; ++j) {
+          ak[j] += k8[j];
+          av[j] += v8[j];
+        }
+      } else {
+        const f4* pk = reinterpret_cast<const f4*>(dkp + src);
+        const f4* pv = reinterpret_cast<const f4*>(dvp + src);
+        const f4 k0 = pk[0], k1 = pk[1], v0 = pv[0], v1 = pv[1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ak[j] += k0[j];
+          ak[4 + j] += k1[j];
+          av[j] += v0[j];
+          av[4 + j] += v1[j];
+        }
       }
     }
     bf16_t* row = dqkv + bs * NHD;
@@ -1232,6 +1252,7 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_kernel(const float* __re
 
 // the same with the RoPE backward fused into dk: a thread sums 8 dims d and their partners d + 64
 // of one (b, s, kv-head) and writes the gradient w.r.t. the unrotated k (cos / sin [S][64])
+template <bool P16 = false>  // P16: the partials are bf16 (fa_bwd_dkdv8_kernel<..., P16>)
 __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_rope_kernel(const float* __restrict__ dkp,
                                                                     const float* __restrict__ dvp,
                                                                     bf16_t* __restrict__ dqkv, int B, int S,
@@ -1255,15 +1276,26 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kv_rope_kernel(const float*
       const long src = (bs * H + kvh * G + g) * HD + c * 8;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f4* pk = reinterpret_cast<const f4*>(dkp + src + 64 * h);
-        const f4* pv = reinterpret_cast<const f4*>(dvp + src + 64 * h);
-        const f4 k0 = pk[0], k1 = pk[1], v0 = pv[0], v1 = pv[1];
+        if constexpr (P16) {
+          float k8[8], v8[8];
+          unpack8(*reinterpret_cast<const us8*>(reinterpret_cast<const bf16_t*>(dkp) + src + 64 * h), k8);
+          unpack8(*reinterpret_cast<const us8*>(reinterpret_cast<const bf16_t*>(dvp) + src + 64 * h), v8);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          ak[h][j] += k0[j];
-          ak[h][4 + j] += k1[j];
-          av[h][j] += v0[j];
-          av[h][4 + j] += v1[j];
+          for (int j = 0; j < 8; ++j) {
+            ak[h][j] += k8[j];
+            av[h][j] += v8[j];
+          }
+        } else {
+          const f4* pk = reinterpret_cast<const f4*>(dkp + src + 64 * h);
+          const f4* pv = reinterpret_cast<const f4*>(dvp + src + 64 * h);
+          const f4 k0 = pk[0], k1 = pk[1], v0 = pv[0], v1 = pv[1];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ak[h][j] += k0[j];
+            ak[h][4 + j] += k1[j];
+            av[h][j] += v0[j];
+            av[h][4 + j] += v1[j];
+          }
         }
       }
     }
@@ -1737,6 +1769,13 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     return v ? atoi(v) : 0;
   }();
   const bool dkdv_dec = dkdv_dec_env >= 1 && dkdv_kind == 8 && !half_prio && !dkdv_gqa && dkdv_pf >= 2;
+  // bf16 per-query-head dK/dV partials (DSTACK_AMD_FA_DKDV_BF16=1|0): the default 8-wave PF-2 pass only
+  static const bool dkdv_bf16_env = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DKDV_BF16");
+    return v ? atoi(v) == 1 : true;
+  }();
+  const bool p16 = dkdv_bf16_env && dkdv_kind == 8 && dkdv_pf == 2 && !dkdv_dec && !half_prio && !dkdv_gqa &&
+                   !fa_ds_spill(B, S, H);
   const size_t lds_dec = 2 * 128 * 256 + 4 * (2 * 32 * 256 + 512) + 16;
 #define DSA_DKDV(C, N)                                                                                 \
   do {                                                                                                 \
@@ -1776,6 +1815,10 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
               (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
     } else if (dkdv_pf >= 3 && dkdv_kind == 8) {                                                       \
       fa_bwd_dkdv8_kernel<C, false, false, false, false, false, 3>                                     \
+          <<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(                             \
+              (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
+    } else if (p16) {                                                                                  \
+      fa_bwd_dkdv8_kernel<C, false, false, false, false, false, 2, true>                               \
           <<<grid, 512, 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512), st>>>(                             \
               (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dkp, dvp, B, S, H, KVH, sl2, nullptr); \
     } else if (dkdv_pf == 2 && dkdv_kind == 8) {                                                       \
@@ -1850,13 +1893,19 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
     const long work = (long)B * S * KVH * (HD / 16);
     int g = (int)((work + 255) / 256);
     if (g > 4096) g = 4096;
-    fa_bwd_reduce_kv_rope_kernel<<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH, rcos, rsin);
+    if (p16)
+      fa_bwd_reduce_kv_rope_kernel<true><<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH, rcos, rsin);
+    else
+      fa_bwd_reduce_kv_rope_kernel<false><<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH, rcos, rsin);
     return hipGetLastError();
   }
   const long work = (long)B * S * KVH * (HD / 8);
   int g = (int)((work + 255) / 256);
   if (g > 4096) g = 4096;
-  fa_bwd_reduce_kv_kernel<<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH);
+  if (p16)
+    fa_bwd_reduce_kv_kernel<true><<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH);
+  else
+    fa_bwd_reduce_kv_kernel<false><<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH);
   DSA_CHECK(hipGetLastError());
   return rope_after();
 }

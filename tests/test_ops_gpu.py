@@ -290,8 +290,10 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
     over the GQA group in one workgroup (DSTACK_AMD_FA_DKDV_GQA=1, causal and not), and the S/dP read
     pipelines: dK/dV without it or one step ahead (DSTACK_AMD_FA_DKDV_PF=0|1; the default is 2) and the
     dQ pass's (DSTACK_AMD_FA_DQ_PF=1|2, causal), and the dK/dV pass with decoupled halves
-    (DSTACK_AMD_FA_DKDV_DEC=1, with and without a stagger; bit-identical to the barrier form).  The switches are read once per process, so each
-    variant runs in a child process."""
+    (DSTACK_AMD_FA_DKDV_DEC=1, with and without a stagger; bit-identical to the barrier form with fp32
+    partials), and the default pass with fp32 instead of bf16 per-query-head dK/dV partials
+    (DSTACK_AMD_FA_DKDV_BF16=0).  The switches are read once per process, so each variant runs in a
+    child process."""
     import os
     import subprocess
     import sys
@@ -310,7 +312,8 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
     )
     shape = {"dq_ds_1152": (1152, True), "dq_ds_1152_nc": (1152, False), "default_1152": (1152, True),
              "default_1152_nc": (1152, False), "dkdv_gqa_nc": (1024, False), "default_nc": (1024, False),
-             "dkdv_pf0_nc": (1024, False), "dkdv_dec_nc": (1024, False), "dkdv_dec_1152": (1152, True)}
+             "dkdv_pf0_nc": (1024, False), "dkdv_dec_nc": (1024, False), "dkdv_dec_1152": (1152, True),
+             "p32_1152": (1152, True), "p32_nc": (1024, False)}
     variants = {"default": {}, "dkdv4": {"DSTACK_AMD_FA_DKDV": "4w"},
                 "fwd4_dq4": {"DSTACK_AMD_FA_FWD_WAVES": "4", "DSTACK_AMD_FA_DQ_WAVES": "4"},
                 "fwd_pf0": {"DSTACK_AMD_FA_FWD_PF": "0"}, "exact_max": {"DSTACK_AMD_FA_RESCALE_THR": "0"},
@@ -324,14 +327,16 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
                 "dkdv_dec": {"DSTACK_AMD_FA_DKDV_DEC": "1"},
                 "dkdv_dec_stag": {"DSTACK_AMD_FA_DKDV_DEC": "1", "DSTACK_AMD_FA_DKDV_STAG": "24"},
                 "dkdv_dec_nc": {"DSTACK_AMD_FA_DKDV_DEC": "1"}, "dkdv_dec_1152": {"DSTACK_AMD_FA_DKDV_DEC": "1"},
-                "dkdv_dec_early": {"DSTACK_AMD_FA_DKDV_DEC": "2"}}
+                "dkdv_dec_early": {"DSTACK_AMD_FA_DKDV_DEC": "2"},
+                "p32": {"DSTACK_AMD_FA_DKDV_BF16": "0"}, "p32_1152": {"DSTACK_AMD_FA_DKDV_BF16": "0"},
+                "p32_nc": {"DSTACK_AMD_FA_DKDV_BF16": "0"}}
     out = {}
     for name, extra in variants.items():
         env = dict(os.environ)
         for k in ("DSTACK_AMD_FA_DKDV", "DSTACK_AMD_FA_FWD_WAVES", "DSTACK_AMD_FA_DQ_WAVES", "DSTACK_AMD_FA_FWD_PF",
                   "DSTACK_AMD_FA_RESCALE_THR", "DSTACK_AMD_FA_FWD_STAG", "DSTACK_AMD_FA_HALF_PRIO", "DSTACK_AMD_FA_DQ",
                   "DSTACK_AMD_FA_DKDV_GQA", "DSTACK_AMD_FA_DKDV_PF", "DSTACK_AMD_FA_DQ_PF", "DSTACK_AMD_FA_DKDV_DEC",
-                  "DSTACK_AMD_FA_DKDV_STAG"):
+                  "DSTACK_AMD_FA_DKDV_STAG", "DSTACK_AMD_FA_DKDV_BF16"):
             env.pop(k, None)
         env.update(extra)
         sn, causal = shape.get(name, (S, True))
@@ -339,20 +344,31 @@ def test_flash_attention_kernel_variants_agree(gpu, tmp_path):
                        env=env, check=True,
                        timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         out[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
-    ref_o, ref_g = out["default"]["o"].float(), out["default"]["g"].float()
+    # the variants keep fp32 dK/dV partials: they are compared with the default pass in that form
+    ref_o, ref_g = out["p32"]["o"].float(), out["p32"]["g"].float()
     for name in ("dkdv4", "fwd4_dq4", "fwd_pf0", "exact_max", "fwd_stag", "half_prio", "dq_ds", "dkdv_gqa",
                  "dkdv_pf0", "dkdv_pf1", "dq_pf1", "dq_pf2", "dkdv_dec", "dkdv_dec_stag"):
         o, g = out[name]["o"].float(), out[name]["g"].float()
         assert ((o - ref_o).norm() / ref_o.norm()).item() < 2e-3, name
         assert ((g - ref_g).norm() / ref_g.norm()).item() < 2e-3, name
     for name in ("dkdv_gqa_nc", "dkdv_pf0_nc", "dkdv_dec_nc"):
-        g, rg = out[name]["g"].float(), out["default_nc"]["g"].float()
+        g, rg = out[name]["g"].float(), out["p32_nc"]["g"].float()
         assert ((g - rg).norm() / rg.norm()).item() < 2e-3, name
-    # the decoupled dK/dV computes exactly what the barrier form does: identical gradients
-    assert torch.equal(out["dkdv_dec"]["g"], out["default"]["g"])
-    assert torch.equal(out["dkdv_dec_stag"]["g"], out["default"]["g"])
-    assert torch.equal(out["dkdv_dec_early"]["g"], out["default"]["g"])
-    assert torch.equal(out["dkdv_dec_1152"]["g"], out["default_1152"]["g"])
+    # bf16 partials (the default): one more bf16 rounding of each per-head partial before the
+    # group sum, as flash-attention 2 stores its GQA partials
+    for name, ref in (("default", "p32"), ("default_nc", "p32_nc"), ("default_1152", "p32_1152")):
+        g, rg = out[name]["g"].float(), out[ref]["g"].float()
+        assert ((g - rg).norm() / rg.norm()).item() < 4e-3, name
+    # the decoupled dK/dV computes exactly what the barrier form does (both with fp32 partials):
+    # identical gradients
+    assert torch.equal(out["dkdv_dec"]["g"], out["p32"]["g"])
+    assert torch.equal(out["dkdv_dec_stag"]["g"], out["p32"]["g"])
+    assert torch.equal(out["dkdv_dec_early"]["g"], out["p32"]["g"])
+    assert torch.equal(out["dkdv_dec_1152"]["g"], out["p32_1152"]["g"])
+    # bf16 partials change only the K and V gradient columns, by at most a bf16 rounding of a partial
+    qcols = H * D
+    assert torch.equal(out["p32"]["g"][..., :qcols], out["default"]["g"][..., :qcols])
+    assert not torch.equal(out["p32"]["g"], out["default"]["g"])
     for name in ("dq_ds_1152", "dq_ds_1152_nc"):
         ref = out[name.replace("dq_ds", "default")]
         g, rg = out[name]["g"].float(), ref["g"].float()
