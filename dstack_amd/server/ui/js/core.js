@@ -1,7 +1,7 @@
 // dstack-amd web UI core: REST client, router, shared widgets (tables, tabs, charts, forms).
 // Views register themselves in VIEWS (one module per area: dashboard.js, runs.js, fleets.js, resources.js,
-// admin.js).
-const PAGES = ["home", "runs", "apply", "offers", "fleets", "instances", "volumes", "gateways", "models", "projects", "users", "secrets"];
+// admin.js, forms.js).
+const PAGES = ["home", "runs", "new", "apply", "offers", "fleets", "instances", "volumes", "gateways", "models", "projects", "users", "secrets"];
 const S = { token: localStorage.getItem("dstack_token"), project: localStorage.getItem("dstack_project") || "main", me: null };
 const VIEWS = {};
 const $ = (s) => document.querySelector(s);

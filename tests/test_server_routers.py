@@ -1,6 +1,8 @@
 """REST API tests against an in-memory server (reference test strategy: ``src/tests/_internal/
 server/routers/test_*.py`` — TestClient + real DB, background tasks driven explicitly)."""
 
+import json
+
 import pytest
 
 from tests.conftest import ADMIN_TOKEN
@@ -315,6 +317,75 @@ def test_web_ui_apply_and_offers_request_shapes(client):
     assert r.status_code == 400 and "invalid YAML" in r.json()["detail"][0]["msg"]
     r = client.post(f"{P}/configurations/parse", json={"yaml": "type: nonsense\n"})
     assert r.status_code == 400
+
+
+def _form_yaml(kind, vals):
+    """YAML the UI's configuration forms produce (forms.js buildConfiguration + core.js yamlish), run
+    under node with the browser globals stubbed."""
+    import json
+    import os
+    import shutil
+    import subprocess
+
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node is not installed")
+    major = int(subprocess.run([node, "--version"], capture_output=True, text=True).stdout.strip().lstrip("v").split(".")[0])
+    if major < 12:
+        pytest.skip(f"node {major} is too old")
+    # node 12-15 (this image ships 12): ?? and ?. behind V8 flags; the one ??= of core.js spelled out
+    # and Array.prototype.at polyfilled -- what browsers run natively
+    flags = ["--harmony-nullish", "--harmony-optional-chaining"] if major < 16 else []
+    ui = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dstack_amd", "server", "ui", "js")
+    src = {m: open(os.path.join(ui, m)).read().replace("o[k] ??= {}", "(o[k] = o[k] ?? {})") for m in ("core.js", "forms.js")}
+    script = (
+        "const vm = require('vm');"
+        "if (!Array.prototype.at) Array.prototype.at = function (i) { return this[i < 0 ? this.length + i : i]; };"
+        "globalThis.localStorage = {getItem: () => null, setItem() {}};"
+        "globalThis.document = {querySelector: () => null, querySelectorAll: () => []};"
+        f"vm.runInThisContext({json.dumps(src['core.js'])});"
+        f"vm.runInThisContext({json.dumps(src['forms.js'])});"
+        f"process.stdout.write(vm.runInThisContext('yamlish(buildConfiguration(' + JSON.stringify({json.dumps(kind)}) + ', ' + "
+        f"JSON.stringify({json.dumps(vals)}) + ')).trimStart()'));"
+    )
+    return subprocess.run([node, *flags, "-e", script], check=True, capture_output=True, text=True, timeout=60).stdout
+
+
+def test_web_ui_forms_produce_configurations_the_server_accepts(client):
+    """forms.js: each kind's form values -> YAML that configurations/parse accepts with the intended
+    fields, and (runs, fleets) a plan from it."""
+    P = "/api/project/main"
+    cases = {
+        "task": ({"name": "form-task", "commands": ["echo 1", "python -c 'print(2)'"], "gpu": "MI355X:8", "nodes": 2,
+                  "env": ["HF_TOKEN", "NCCL_DEBUG=INFO"], "max_duration": "72h", "spot_policy": "auto"},
+                 {"nodes": 2, "commands": ["echo 1", "python -c 'print(2)'"]}),
+        "service": ({"name": "form-svc", "commands": ["vllm serve m --port 8000"], "port": 8000, "gpu": "MI355X:8",
+                     "replicas": "1..4", "scaling_metric": "rps", "scaling_target": 10.0, "model": "meta-llama/Meta-Llama-3-70B"},
+                    {"port": 8000}),
+        "dev-environment": ({"name": "form-dev", "ide": "vscode", "gpu": "MI355X:1", "init": ["pip install x"]}, {"ide": "vscode"}),
+        "fleet": ({"name": "form-fleet", "nodes": "0..4", "gpu": "MI355X:8", "placement": "cluster", "idle_duration": "30m"},
+                  {"placement": "cluster"}),
+        "volume": ({"name": "form-vol", "backend": "aws", "region": "us-east-1", "size": "500GB"}, {"region": "us-east-1"}),
+    }
+    for kind, (vals, expect) in cases.items():
+        text = _form_yaml(kind, vals)
+        r = client.post(f"{P}/configurations/parse", json={"yaml": text})
+        assert r.status_code == 200, (kind, text, r.text)
+        conf = r.json()["configuration"]
+        assert r.json()["type"] == kind and conf["name"] == vals["name"], (kind, conf)
+        for k, v in expect.items():
+            got = conf[k]
+            assert got == v or (isinstance(got, dict) and got.get("container_port") == v), (kind, k, got)
+        if kind in ("task", "service", "dev-environment"):
+            assert "MI355X" in json.dumps(conf["resources"]), conf["resources"]
+            run_spec = {"run_name": conf["name"], "repo_id": "ui", "repo_data": {"repo_type": "virtual"},
+                        "configuration": conf, "ssh_key_pub": ""}
+            r = client.post(f"{P}/runs/get_plan", json={"run_spec": run_spec, "max_offers": 5})
+            assert r.status_code == 200, (kind, r.text)
+        elif kind == "fleet":
+            assert conf["nodes"]["min"] == 0 and conf["nodes"]["max"] == 4, conf["nodes"]
+            r = client.post(f"{P}/fleets/get_plan", json={"spec": {"configuration": conf}})
+            assert r.status_code == 200, r.text
 
 
 def test_prometheus_metrics(client):
