@@ -23,6 +23,7 @@
 typedef unsigned short us4 __attribute__((ext_vector_type(4)));
 
 #include <cstdlib>
+#include <mutex>
 #include <string>
 
 using namespace dsa;
@@ -1677,6 +1678,32 @@ extern "C" hipError_t dsa_rope_qkv(const void* in, void* out, const float* cosT,
 // rcos / rsin (nullable, [S][64] fp32): q and k were rotated by RoPE after the projection (the qkv
 // GEMM's epilogue); dqkv is then the gradient w.r.t. the unrotated projection -- fused into the dQ
 // epilogue and the dK reduction on the default path, an in-place pass on the others.
+// The dQ pass on a second stream of the same device (DSTACK_AMD_FA_DQ_STREAM=1): it depends only on
+// the delta pass, like the dK/dV pass, so the two can share the CUs -- the workgroups of one fill
+// what the other's causal tail leaves idle.  The side stream is non-blocking (no implicit sync with
+// the legacy default stream); the caller's stream waits for it before anything reads dqkv.
+namespace {
+struct FaSide {
+  hipStream_t s = nullptr;
+  hipEvent_t ready = nullptr, done = nullptr;
+};
+FaSide* fa_side() {
+  static std::mutex mu;
+  static FaSide sides[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  FaSide& f = sides[dev];
+  if (f.s == nullptr) {
+    if (hipStreamCreateWithFlags(&f.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&f.ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+  }
+  return &f;
+}
+}  // namespace
+
 extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
                                  void* dqkv, void* workspace, int B, int S, int H, int KVH, int D,
                                  float scale, int causal, const float* rcos, const float* rsin,
@@ -1832,6 +1859,13 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
       fa_bwd_dkdv_kernel<C, N><<<grid, 256, lds_kv, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, \
                                                           delta, dkp, dvp, B, S, H, KVH, sl2);         \
   } while (0)
+  static const bool dq_stream_env = [] {
+    const char* v = getenv("DSTACK_AMD_FA_DQ_STREAM");
+    return v && atoi(v) == 1;
+  }();
+  FaSide* side = nullptr;  // set when the causal dQ pass runs on the side stream
+  // the caller's stream waits for the side stream's dQ pass before anything after this call
+  auto join = [&]() -> hipError_t { return side ? hipStreamWaitEvent(st, side->done, 0) : hipSuccess; };
   if (fa_ds_spill(B, S, H)) {  // dK/dV pass writes dS; dQ is one GEMM over the spilled dS
     bf16_t* dsg = (bf16_t*)(dvp + (size_t)B * S * H * HD);
     const size_t lds8 = 2 * 128 * 256 + 2 * (2 * TILE_BYTES + 512);
@@ -1859,23 +1893,30 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
                                                                  KVH, sl2);
     }
   } else if (causal) {
+    hipStream_t qs = st;  // the dQ pass's stream
+    if (dq_stream_env && (side = fa_side()) != nullptr) {
+      DSA_CHECK(hipEventRecord(side->ready, st));  // after the delta pass
+      DSA_CHECK(hipStreamWaitEvent(side->s, side->ready, 0));
+      qs = side->s;
+    }
     if (dkdv_qt == 128) DSA_DKDV(true, 4); else DSA_DKDV(true, 2);
     DSA_CHECK(hipGetLastError());
     if (dq_waves == 8 && half_prio)
-      fa_bwd_dq_kernel<true, 8, true><<<B * H * (S / 256), 512, lds_q, st>>>(
+      fa_bwd_dq_kernel<true, 8, true><<<B * H * (S / 256), 512, lds_q, qs>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else if (dq_waves == 8 && dq_pf == 1)
-      fa_bwd_dq_kernel<true, 8, false, 1><<<B * H * (S / 256), 512, lds_q, st>>>(
+      fa_bwd_dq_kernel<true, 8, false, 1><<<B * H * (S / 256), 512, lds_q, qs>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else if (dq_waves == 8 && dq_pf >= 2)
-      fa_bwd_dq_kernel<true, 8, false, 2><<<B * H * (S / 256), 512, lds_q, st>>>(
+      fa_bwd_dq_kernel<true, 8, false, 2><<<B * H * (S / 256), 512, lds_q, qs>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else if (dq_waves == 8)
-      fa_bwd_dq_kernel<true, 8><<<B * H * (S / 256), 512, lds_q, st>>>(
+      fa_bwd_dq_kernel<true, 8><<<B * H * (S / 256), 512, lds_q, qs>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
     else
-      fa_bwd_dq_kernel<true><<<grid, 256, lds_q, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta,
+      fa_bwd_dq_kernel<true><<<grid, 256, lds_q, qs>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta,
                                                        (bf16_t*)dqkv, B, S, H, KVH, sl2, rq, rsq);
+    if (side != nullptr) DSA_CHECK(hipEventRecord(side->done, qs));
   } else {
     if (dkdv_qt == 128) DSA_DKDV(false, 4); else DSA_DKDV(false, 2);
     DSA_CHECK(hipGetLastError());
@@ -1888,7 +1929,10 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   }
 #undef DSA_DKDV
   DSA_CHECK(hipGetLastError());
-  if (dkdv_gqa) return rope_after();  // dK/dV already summed over the group, in dqkv
+  if (dkdv_gqa) {  // dK/dV already summed over the group, in dqkv
+    DSA_CHECK(join());
+    return rope_after();
+  }
   if (rope_fused) {
     const long work = (long)B * S * KVH * (HD / 16);
     int g = (int)((work + 255) / 256);
@@ -1897,7 +1941,8 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
       fa_bwd_reduce_kv_rope_kernel<true><<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH, rcos, rsin);
     else
       fa_bwd_reduce_kv_rope_kernel<false><<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH, rcos, rsin);
-    return hipGetLastError();
+    DSA_CHECK(hipGetLastError());
+    return join();
   }
   const long work = (long)B * S * KVH * (HD / 8);
   int g = (int)((work + 255) / 256);
@@ -1907,6 +1952,7 @@ extern "C" hipError_t dsa_fa_bwd(const void* qkv, const void* out, const void* d
   else
     fa_bwd_reduce_kv_kernel<false><<<g, 256, 0, st>>>(dkp, dvp, (bf16_t*)dqkv, B, S, H, KVH);
   DSA_CHECK(hipGetLastError());
+  DSA_CHECK(join());
   return rope_after();
 }
 
