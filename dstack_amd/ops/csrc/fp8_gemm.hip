@@ -27,6 +27,8 @@
 //    exhaustively over the XOR-linear swizzles of the row's low 4 bits).
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "mfma_tiles.h"
 
 using namespace dsa;
@@ -158,8 +160,11 @@ __global__ __launch_bounds__(512, 2) void fp8_rows_gemm_kernel(F8Args p) {
   if (nsteps > 1) issue(1);
   for (int t = 0; t < nsteps; ++t) {
     if (t + 1 < nsteps) f8_vmcnt<NP>(); else f8_vmcnt<0>();  // step t landed (this wave's pieces)
+    // ... and every wave's: a bare s_barrier (__syncthreads() is also a fence, for which the compiler
+    // drained vmcnt to 0 here -- the ring then never had a step in flight across the barrier)
     __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();                                           // ... and every wave's
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     if (t + 2 < nsteps) issue(t + 2);  // into the slot step t-1 read: every wave is past it
     const char* st = smem + (t % F8_NSTAGE) * STAGE;
     i32x8 wf[CB], xf[2];
@@ -262,5 +267,275 @@ extern "C" hipError_t dsa_fp8_rows_gemm(const void* X, const float* xs, const vo
     fp8_rows_gemm_kernel<64><<<grid, 512, F8_NSTAGE * f8_stage<64>(), st>>>(a);
   else
     fp8_rows_gemm_kernel<128><<<grid, 512, F8_NSTAGE * f8_stage<128>(), st>>>(a);
+  return hipGetLastError();
+}
+
+// ================================================================================================
+// Weight-streaming decode GEMM for 128 < M <= 256 token rows (fp8_stream_gemm): the weights never
+// touch LDS.  fp8_rows_gemm above stages both operands through LDS, and each CU pulls 1.5-3x the
+// weight bytes into it; the 256x256 e4m3 tile (gemm_nt_f8) keeps one 64 KiB K-step (activations +
+// weights) in flight per CU and waits ~2 us for each, i.e. ~3.6 TB/s at gate/up.  Here:
+//  * a workgroup = 4 waves (one per SIMD) x 64 weight rows x all 256 token rows x a K slice; the
+//    256 x 64 fp32 accumulators of a wave fill its 256 accumulation registers;
+//  * each wave loads ITS 64 weight rows straight from HBM into VGPRs (nontemporal: read once) as the
+//    MFMA A operands, two K-steps ahead (3 live register sets, 96 VGPRs) -- no LDS, nothing shared;
+//  * the activations (256 x 128 B per K-step, L2-resident: every workgroup reads them) are LDS-DMA'd
+//    into a 4-slot ring (128 KiB) two steps ahead, one barrier per step; every wave reads all 16
+//    token blocks of a step from LDS (the f8_swz swizzle: conflict-free fragment reads);
+//  * v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales): a lane's accumulator holds 4 consecutive
+//    output columns (weight rows) of one token row, so the epilogue stores 8-byte bf16 pieces;
+//  * S > 1 splits K: fp32 partials [S][M][N] and fp8_stream_reduce_kernel adds them with the scales.
+// In flight per CU: 2 K-steps x 4 waves x 64 rows x 128 B = 64 KiB of weights, against 32 KiB of
+// weights (+ 32 KiB of activations) for the LDS-staged 256x256 tile -- the Little's-law term that
+// bounds an HBM stream at this grid size.  LDS fragment reads: 4 bytes per weight byte (a 16-row
+// wave, measured first, read 16 and was LDS-bound at 0.8x hipBLASLt).
+// ================================================================================================
+namespace {
+constexpr int FS_NX = 4;                   // activation ring slots
+constexpr int FS_XT = F8_MAXM * F8_BK;     // one slot: 256 token rows x 128 B = 32 KiB
+
+struct FSArgs {
+  const uint8_t* X;
+  const float* xs;
+  const uint8_t* W;
+  const float* ws;
+  bf16_t* Y;
+  float* part;  // [S][M][N] fp32 (S > 1)
+  long ldx, ldw, ldy;
+  int M, N, K, S;
+};
+
+template <int N>
+__device__ __forceinline__ void fs_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// a bare workgroup barrier: __syncthreads() is a release/acquire fence as well, for which the compiler
+// drains vmcnt to 0 before the s_barrier -- every prefetch in flight would be waited for each step
+__device__ __forceinline__ void fs_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+}  // namespace
+
+// (device functions rather than lambdas of the kernel template: a lambda using these builtins made
+// the host pass drop the template's launch stub -- an undefined symbol at load time)
+template <int XP, int NWV>
+__device__ __forceinline__ void fs_issue_x(__amdgpu_buffer_rsrc_t xrs, const unsigned (&xoff)[XP], char* slot, int so,
+                                           int w) {
+#pragma unroll
+  for (int i = 0; i < XP; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, LDS3(void, slot + (w + NWV * i) * 1024), 16, xoff[i], so, 0, 0);
+}
+template <int NF>
+__device__ __forceinline__ void fs_load_w(__amdgpu_buffer_rsrc_t wrs, const unsigned (&woff)[NF], int so,
+                                          i32x8 (&dst)[NF]) {
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)woff[f], so, 2);  // 2: nontemporal
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)woff[f] + 16, so, 2);
+    dst[f] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+  }
+}
+
+// NWV waves x NF 16-row weight fragments per wave (a workgroup: 16 NWV NF weight rows); D: prefetch
+// distance in K-steps for activations and weights
+template <int NWV, int NF, int D>
+__global__ __launch_bounds__(64 * NWV, 1) void fp8_stream_gemm_kernel(FSArgs p) {
+  constexpr int NSET = 4;               // weight register sets = the unroll factor (D + 1 live)
+  constexpr int XP = 32 / NWV;          // X pieces (1 KiB) per wave per step
+  constexpr int OPS = XP + 2 * NF;      // vector-memory ops per wave per step
+  constexpr int WAIT = (D - 1) * OPS;   // issued after W(t): X(t+1), W(t+1), ..., X(t+D-1), W(t+D-1)
+  static_assert(D >= 1 && D + 1 <= NSET, "D + 1 weight sets live");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = (blockIdx.x * NWV + w) * 16 * NF;  // this wave's first weight row
+  const int ks = p.K / p.S, nsteps = ks / F8_BK;
+  const long k0 = (long)blockIdx.y * ks;
+
+  // --- activation DMA: 32 pieces of 1 KiB (8 token rows x 128 B) per step, XP per wave ------------
+  const __amdgpu_buffer_rsrc_t xrs = make_rsrc(p.X, (unsigned)((long)(p.M - 1) * p.ldx + p.K));
+  unsigned xoff[XP];
+#pragma unroll
+  for (int i = 0; i < XP; ++i) {
+    const int piece = w + NWV * i, row = 8 * piece + (lane >> 3);
+    const int ch = (lane & 7) ^ f8_swz(row & 15);
+    const int srow = row < p.M ? row : p.M - 1;  // rows past M re-read the last real row (not stored)
+    xoff[i] = (unsigned)((long)srow * p.ldx + ch * 16);
+  }
+  auto issue_x = [&](int t) {
+    fs_issue_x<XP, NWV>(xrs, xoff, smem + (t & (FS_NX - 1)) * FS_XT,
+                        __builtin_amdgcn_readfirstlane((int)(k0 + (long)t * F8_BK)), w);
+  };
+  // --- weights: rows n0 + 16 f + r, bytes [32 g, 32 g + 32) of the K-step, through a buffer
+  // descriptor (one 32-bit offset per fragment, the step in an SGPR: 64-bit row pointers spilled),
+  // nontemporal (read once: the weights must not evict the activations from L2)
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(p.W, (unsigned)((long)(p.N - 1) * p.ldw + p.K));
+  unsigned woff[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) woff[f] = (unsigned)((long)(n0 + 16 * f + r) * p.ldw + k0 + 32 * g);
+  auto load_w = [&](int t, i32x8 (&dst)[NF]) {
+    fs_load_w<NF>(wrs, woff, __builtin_amdgcn_readfirstlane(t * F8_BK), dst);
+  };
+
+  f32x4 acc[16][NF];
+#pragma unroll
+  for (int tb = 0; tb < 16; ++tb)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[tb][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int sw = f8_swz(r), c0 = ((2 * g) ^ sw) * 16, c1 = ((2 * g + 1) ^ sw) * 16;
+
+  // prologue in the order the waits count: X(0) W(0) ... X(D-1) W(D-1)
+  i32x8 wf[NSET][NF];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    issue_x(j);
+    load_w(j, wf[j]);
+  }
+  // one K-step on weight set J; ISSUE: it issues X(t+3), W(t+3); WN: the vmcnt it may leave
+  // outstanding (all compile-time: no branch inside a step, where a branch made the compiler copy
+  // the accumulators)
+  auto step = [&](int t, auto J, auto ISSUE, auto WN) {
+    constexpr int j = decltype(J)::value;
+    fs_vmcnt<decltype(WN)::value>();  // this wave's X(t) and W(t) have landed
+    fs_barrier();                      // every wave's X(t); every wave is past step t-1 (its X slot is free)
+    if constexpr (decltype(ISSUE)::value) {
+      issue_x(t + D);
+      load_w(t + D, wf[(j + D) % NSET]);  // a set no live step uses (D + 1 of the 4 are live)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const char* st = smem + (t & (FS_NX - 1)) * FS_XT + r * F8_BK;
+    // token-block fragments two blocks ahead of their MFMAs (3 buffers), the interleave pinned
+    i32x8 xf[3];
+    xf[0] = f8_frag(st + c0, st + c1);
+    xf[1] = f8_frag(st + 2048 + c0, st + 2048 + c1);
+#pragma unroll
+    for (int tb = 0; tb < 16; ++tb) {
+      if (tb + 2 < 16) xf[(tb + 2) % 3] = f8_frag(st + (tb + 2) * 2048 + c0, st + (tb + 2) * 2048 + c1);
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+        acc[tb][f] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[j][f], xf[tb % 3], acc[tb][f], 0, 0, 0, 127,
+                                                                      0, 127);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // blocks 0, 1: 2 ds_read_b128 each
+#pragma unroll
+    for (int tb = 0; tb < 14; ++tb) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // block tb + 2
+      __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);  // block tb's MFMAs
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * NF, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using W0 = std::integral_constant<int, 0>;
+  using WF = std::integral_constant<int, WAIT>;
+  // every group but the last: full issue, WAIT outstanding
+  const int last = nsteps - NSET;
+  for (int t0 = 0; t0 < last; t0 += NSET) {
+    step(t0 + 0, std::integral_constant<int, 0>{}, T{}, WF{});
+    step(t0 + 1, std::integral_constant<int, 1>{}, T{}, WF{});
+    step(t0 + 2, std::integral_constant<int, 2>{}, T{}, WF{});
+    step(t0 + 3, std::integral_constant<int, 3>{}, T{}, WF{});
+  }
+  // the last group (t = nsteps - 4 + j): steps with j + D < 4 still issue (up to step nsteps - 1)
+  // and wait as usual; the rest drain
+  step(last + 0, std::integral_constant<int, 0>{}, std::bool_constant<(0 + D < NSET)>{},
+       std::integral_constant<int, (0 + D < NSET) ? WAIT : 0>{});
+  step(last + 1, std::integral_constant<int, 1>{}, std::bool_constant<(1 + D < NSET)>{},
+       std::integral_constant<int, (1 + D < NSET) ? WAIT : 0>{});
+  step(last + 2, std::integral_constant<int, 2>{}, std::bool_constant<(2 + D < NSET)>{},
+       std::integral_constant<int, (2 + D < NSET) ? WAIT : 0>{});
+  step(last + 3, std::integral_constant<int, 3>{}, F{}, W0{});
+
+  // --- epilogue: lane holds C[n = 4 g + e][m = r] of each (token block, fragment) ------------------
+  if (p.S > 1) {
+    float* part = p.part + (long)blockIdx.y * p.M * p.N;
+#pragma unroll
+    for (int tb = 0; tb < 16; ++tb) {
+      const int m = 16 * tb + r;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+        *reinterpret_cast<f32x4*>(part + (long)m * p.N + n0 + 16 * f + 4 * g) = acc[tb][f];
+    }
+    return;
+  }
+  f32x4 wsc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) wsc[f] = *reinterpret_cast<const f32x4*>(p.ws + n0 + 16 * f + 4 * g);
+#pragma unroll
+  for (int tb = 0; tb < 16; ++tb) {
+    const int m = 16 * tb + r;
+    if (m >= p.M) continue;
+    const float xsc = p.xs[m];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      unsigned short o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[tb][f][e] * xsc * wsc[f][e]);
+      *reinterpret_cast<uint2*>(p.Y + (long)m * p.ldy + n0 + 16 * f + 4 * g) =
+          uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
+    }
+  }
+}
+
+// y[m][n] = bf16(xs[m] ws[n] sum_s part[s][m][n]), 4 columns per thread
+__global__ __launch_bounds__(256) void fp8_stream_reduce_kernel(const float* __restrict__ part,
+                                                                const float* __restrict__ xs,
+                                                                const float* __restrict__ ws, bf16_t* __restrict__ Y,
+                                                                int M, int N, long ldy, int S) {
+  const long n4 = N / 4, total = (long)M * n4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int m = (int)(i / n4), n = (int)(i % n4) * 4;
+    f32x4 a = *reinterpret_cast<const f32x4*>(part + (long)m * N + n);
+    for (int s2 = 1; s2 < S; ++s2) a += *reinterpret_cast<const f32x4*>(part + ((long)s2 * M + m) * N + n);
+    const float xsc = xs[m];
+    const f32x4 wsv = *reinterpret_cast<const f32x4*>(ws + n);
+    unsigned short o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf(a[e] * xsc * wsv[e]);
+    *reinterpret_cast<uint2*>(Y + (long)m * ldy + n) =
+        uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
+  }
+}
+
+extern "C" bool dsa_fp8_stream_gemm_supported(int M, int N, int K, int rw, int S) {
+  // rw weight rows per wave: 64 (4 waves: 256 per workgroup) or 32 (8 waves: 256 per workgroup);
+  // each K slice whole groups of 4 K-steps
+  return M > 0 && M <= F8_MAXM && (rw == 64 || rw == 32) && N > 0 && N % 256 == 0 && S >= 1 && K > 0 &&
+         K % (4 * F8_BK * S) == 0;
+}
+
+// Y[M][N] = bf16(xs[m] ws[n] X W^T) with X [M][K] e4m3 (ldx bytes), W [N][K] e4m3 (ldw bytes); rw weight
+// rows per wave (64 | 32); S > 1: `part` holds S * M * N floats
+extern "C" hipError_t dsa_fp8_stream_gemm(const void* X, const float* xs, const void* W, const float* ws, void* Y,
+                                          float* part, int M, int N, int K, long ldx, long ldw, long ldy, int rw,
+                                          int S, hipStream_t st) {
+  if (!dsa_fp8_stream_gemm_supported(M, N, K, rw, S) || ldx % 16 || ldw % 16 || ldy % 4 || ldx < K || ldw < K ||
+      ldy < N)
+    return hipErrorInvalidValue;
+  if (S > 1 && part == nullptr) return hipErrorInvalidValue;
+  if ((long)(M - 1) * ldx + K > 0xffffffffL) return hipErrorInvalidValue;  // X through a 32-bit buffer range
+  static bool attr = false;
+  if (!attr) {
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fp8_stream_gemm_kernel<4, 4, 3>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fp8_stream_gemm_kernel<8, 2, 2>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
+    attr = true;
+  }
+  FSArgs a{(const uint8_t*)X, xs, (const uint8_t*)W, ws, (bf16_t*)Y, part, ldx, ldw, ldy, M, N, K, S};
+  if (rw == 64)
+    fp8_stream_gemm_kernel<4, 4, 3><<<dim3(N / 256, S), 256, FS_NX * FS_XT, st>>>(a);
+  else
+    fp8_stream_gemm_kernel<8, 2, 2><<<dim3(N / 256, S), 512, FS_NX * FS_XT, st>>>(a);
+  DSA_CHECK(hipGetLastError());
+  if (S > 1) {
+    const long work = (long)M * (N / 4);
+    const int g = (int)((work + 255) / 256 < 4096 ? (work + 255) / 256 : 4096);
+    fp8_stream_reduce_kernel<<<g, 256, 0, st>>>(part, xs, ws, (bf16_t*)Y, M, N, ldy, S);
+  }
   return hipGetLastError();
 }

@@ -1,0 +1,71 @@
+"""Llama-3-70B decode projections at a batch of 256 rows: the weight-streaming fp8 GEMM
+(csrc/fp8_gemm.hip fp8_stream_gemm, split-K variants) against hipBLASLt's row-scaled fp8 GEMM with
+the serving engine's tuned selections (torch._scaled_mm) and the LDS-staged in-tree form
+(fp8_rows_gemm).  One JSON line per shape.
+
+    python tools/bench_fp8_stream.py        # ROWS=256 (comma list)
+"""
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from dstack_amd.ops import _ext, gemm_tuning  # noqa: E402
+from dstack_amd.ops import reference as ref  # noqa: E402
+
+SHAPES = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672)}
+
+
+def timed(fn, iters=50):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    C = _ext.require()
+    gemm_tuning.setup("use", kind="serving")
+    for M in [int(m) for m in os.getenv("ROWS", "256").split(",")]:
+        for name, (N, K) in SHAPES.items():
+            torch.manual_seed(0)
+            x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+            w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+            xq, xs = C.quant_fp8_rows(x)
+            wq, ws = ref.quant_fp8_rows(w)
+            wq = wq.view(torch.uint8)
+            del w
+            lib = lambda: torch._scaled_mm(xq.view(torch.float8_e4m3fn), wq.view(torch.float8_e4m3fn).t(),  # noqa: E731
+                                           scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1), out_dtype=torch.bfloat16)
+            ref_y = lib().float()
+            cands = {"lib": lib}
+            for rw in (64, 32):
+                for sp in (1, 2, 4, 7, 8):
+                    if C.fp8_stream_gemm_supported(M, N, K, rw, sp):
+                        cands[f"stream_r{rw}_s{sp}"] = (lambda sp=sp, rw=rw: C.fp8_stream_gemm(xq, xs, wq, ws, rw, sp))
+            if C.fp8_rows_gemm_supported(M, N, K, 64, 1):
+                cands["rows_bm64"] = lambda: C.fp8_rows_gemm(xq, xs, wq, ws, 64, 1)
+            out = {"shape": name, "M": M, "N": N, "K": K}
+            for k, fn in cands.items():
+                err = ((fn().float() - ref_y).norm() / ref_y.norm()).item()
+                assert err < 1e-2, (k, err)
+                t = statistics.median(timed(fn) for _ in range(5))
+                out[k + "_us"] = round(t, 2)
+                out[k + "_tb_s"] = round(N * K / t / 1e6, 3)
+            best = min((v, k) for k, v in out.items() if k.endswith("_us") and k.startswith("stream"))
+            out["best_stream"] = best[1][:-3]
+            out["speedup_vs_lib"] = round(out["lib_us"] / best[0], 3)
+            print(json.dumps(out), flush=True)
+            del xq, wq
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
