@@ -197,9 +197,19 @@ def build(verbose: bool = False, keep_asm: bool = False, force: bool = False) ->
     jobs = [(obj, cmd, d) for obj, cmd, d in units if force or _stale(obj, d)]
     if jobs:
         check_toolchain()  # a clear message instead of a wall of clang errors
+    # a unit's stamp is dropped before it compiles and written by the worker right after it succeeds:
+    # when another unit fails, a unit that compiled must not keep the stamp of its PREVIOUS sources
+    # (reverting those sources would then reuse the new object under the old stamp)
+    for obj, _, _ in jobs:
+        obj.with_name(obj.name + ".sha256").unlink(missing_ok=True)
+
+    def compile_unit(j):
+        out = _run(j[1])
+        _stamp(j[0], j[2])
+        return out
+
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
-        for (obj, _, d), out in zip(jobs, ex.map(lambda j: _run(j[1]), jobs)):
-            _stamp(obj, d)
+        for out in ex.map(compile_unit, jobs):
             if verbose and out:
                 print(out, file=sys.stderr)
     so = so_path()

@@ -21,6 +21,35 @@ def test_digest_tracks_content_and_flags(tmp_path):
     assert not build._stale(obj, d1) and build._stale(obj, d1 + "0")
 
 
+def test_failed_build_leaves_no_stale_stamp(tmp_path, monkeypatch):
+    """When one unit fails to compile, a unit that compiled in the same call carries the stamp of its
+    NEW sources (or none) -- never the stamp of the previous ones, under which a revert of those
+    sources would reuse the new object."""
+    a_obj, b_obj = tmp_path / "a.o", tmp_path / "b.o"
+    a_obj.write_bytes(b"old a")
+    b_obj.write_bytes(b"old b")
+    build._stamp(a_obj, "old-a")
+    build._stamp(b_obj, "old-b")
+    units = [(a_obj, ["cc", "a"], "new-a"), (b_obj, ["cc", "b"], "new-b")]
+
+    def run(cmd):
+        if cmd[1] == "b":
+            raise RuntimeError("compile failed: b")
+        a_obj.write_bytes(b"new a")
+        return ""
+
+    monkeypatch.setattr(build, "_quick_current", lambda: False)
+    monkeypatch.setattr(build, "_plan", lambda keep_asm=False: (units, ["ld"], "so"))
+    monkeypatch.setattr(build, "_run", run)
+    monkeypatch.setattr(build, "check_toolchain", lambda: "hipcc")
+    monkeypatch.setattr(build, "BUILD", tmp_path)
+    with pytest.raises(RuntimeError, match="compile failed: b"):
+        build.build()
+    assert not build._stale(a_obj, "new-a")  # compiled: stamped with its new digest
+    assert build._stale(a_obj, "old-a")
+    assert build._stale(b_obj, "old-b") and build._stale(b_obj, "new-b")  # failed: no stamp at all
+
+
 def test_plan_covers_every_kernel_source():
     units, link, digest = build._plan()
     srcs = {p.stem for p in build.CSRC.glob("*.hip")} | {"bindings"}
