@@ -71,7 +71,7 @@ hipError_t dsa_fa_dkdv_trace(const void*, const void*, const float*, const float
 bool dsa_fp8_rows_gemm_supported(int, int, int, int, int);
 bool dsa_fp8_stream_gemm_supported(int, int, int, int, int);
 hipError_t dsa_fp8_stream_gemm(const void*, const float*, const void*, const float*, void*, float*, int, int, int,
-                               long, long, long, int, int, hipStream_t);
+                               long, long, long, int, int, int, hipStream_t);
 hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
                              long, long, long, int, int, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
@@ -661,9 +661,10 @@ bool fp8_stream_gemm_supported(int64_t M, int64_t N, int64_t K, int64_t rw, int6
 
 // y[M][N] = bf16(xs[m] ws[n] (xq wq^T)) for a decode batch of up to 256 rows with the weights streamed
 // straight into registers (csrc/fp8_gemm.hip fp8_stream_gemm); rw = 64 | 32 weight rows per wave,
-// S > 1 splits K (fp32 partials allocated here, added by a second kernel)
+// S > 1 splits K (fp32 partials allocated here, added by a second kernel); shuffled: wq [N][K] holds the
+// weights in ops.serving.fp8_stream_shuffle order
 torch::Tensor fp8_stream_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t rw,
-                              int64_t S) {
+                              int64_t S, bool shuffled) {
   for (auto* t : {&xq, &wq}) {
     TORCH_CHECK(t->is_cuda() && t->element_size() == 1 && t->dim() == 2 && t->stride(1) == 1,
                 "fp8_stream_gemm: 1-byte 2-D operands with contiguous rows");
@@ -672,18 +673,19 @@ torch::Tensor fp8_stream_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor 
   }
   const int64_t M = xq.size(0), K = xq.size(1), N = wq.size(0);
   TORCH_CHECK(wq.size(1) == K, "fp8_stream_gemm: K mismatch");
+  TORCH_CHECK(!shuffled || wq.is_contiguous(), "fp8_stream_gemm: a shuffled weight is one contiguous block");
   TORCH_CHECK(xs.is_cuda() && xs.scalar_type() == torch::kFloat32 && xs.is_contiguous() && xs.numel() == M,
               "fp8_stream_gemm: xs fp32 [M]");
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.is_contiguous() && ws.numel() == N,
               "fp8_stream_gemm: ws fp32 [N]");
   TORCH_CHECK(dsa_fp8_stream_gemm_supported((int)M, (int)N, (int)K, (int)rw, (int)S),
-              "fp8_stream_gemm: M <= 256, rw 64 | 32, N % 256 == 0, K % (512 S) == 0");
+              "fp8_stream_gemm: M <= 256, rw 32 (or 64 without split), N % 256 == 0, K % (512 S) == 0");
   auto y = torch::empty({M, N}, xq.options().dtype(torch::kBFloat16));
   torch::Tensor part;
   if (S > 1) part = torch::empty({S, M, N}, xq.options().dtype(torch::kFloat32));
   check(dsa_fp8_stream_gemm(xq.data_ptr(), xs.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(),
                             S > 1 ? part.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, xq.stride(0),
-                            wq.stride(0), y.stride(0), (int)rw, (int)S, stream()),
+                            wq.stride(0), y.stride(0), (int)rw, (int)S, (int)shuffled, stream()),
         "fp8_stream_gemm");
   return y;
 }
@@ -957,7 +959,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("cnt") = pybind11::none());
   m.def("fp8_rows_gemm_supported", &fp8_rows_gemm_supported);
   m.def("fp8_stream_gemm", &fp8_stream_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),
-        pybind11::arg("ws"), pybind11::arg("rw") = 64, pybind11::arg("split") = 1);
+        pybind11::arg("ws"), pybind11::arg("rw") = 64, pybind11::arg("split") = 1, pybind11::arg("shuffled") = false);
   m.def("fp8_stream_gemm_supported", &fp8_stream_gemm_supported);
   m.def("swiglu_quant_fp8_rows", &swiglu_quant_fp8_rows, py::arg("gu"), py::arg("rs") = py::none(),
         py::arg("cs") = py::none());

@@ -303,6 +303,7 @@ struct FSArgs {
   float* part;  // [S][M][N] fp32 (S > 1)
   long ldx, ldw, ldy;
   int M, N, K, S;
+  int shuffled;  // W in ops.serving.fp8_stream_shuffle order
 };
 
 template <int N>
@@ -327,19 +328,23 @@ __device__ __forceinline__ void fs_issue_x(__amdgpu_buffer_rsrc_t xrs, const uns
   for (int i = 0; i < XP; ++i)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, LDS3(void, slot + (w + NWV * i) * 1024), 16, xoff[i], so, 0, 0);
 }
+// half: the byte distance of a fragment's two 16-byte pieces (16: adjacent in a row; 1 KiB: pre-shuffled),
+// added to the uniform offset so that it costs no VGPRs
 template <int NF>
-__device__ __forceinline__ void fs_load_w(__amdgpu_buffer_rsrc_t wrs, const unsigned (&woff)[NF], int so,
+__device__ __forceinline__ void fs_load_w(__amdgpu_buffer_rsrc_t wrs, const unsigned (&woff)[NF], int so, int half,
                                           i32x8 (&dst)[NF]) {
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     const auto a = __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)woff[f], so, 2);  // 2: nontemporal
-    const auto b = __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)woff[f] + 16, so, 2);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)woff[f], so + half, 2);
     dst[f] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
   }
 }
 
 // NWV waves x NF 16-row weight fragments per wave (a workgroup: 16 NWV NF weight rows); D: prefetch
-// distance in K-steps for activations and weights
+// distance in K-steps for activations and weights.  p.shuffled: the weights are pre-shuffled
+// (ops.serving.fp8_stream_shuffle: per 16-row block and K-step, the 2 KiB a wave's fragment reads, in lane
+// order) -- every weight load is 1 KiB contiguous and each fragment's stream is sequential over K
 template <int NWV, int NF, int D>
 __global__ __launch_bounds__(64 * NWV, 1) void fp8_stream_gemm_kernel(FSArgs p) {
   constexpr int NSET = 4;               // weight register sets = the unroll factor (D + 1 live)
@@ -371,12 +376,17 @@ __global__ __launch_bounds__(64 * NWV, 1) void fp8_stream_gemm_kernel(FSArgs p) 
   // --- weights: rows n0 + 16 f + r, bytes [32 g, 32 g + 32) of the K-step, through a buffer
   // descriptor (one 32-bit offset per fragment, the step in an SGPR: 64-bit row pointers spilled),
   // nontemporal (read once: the weights must not evict the activations from L2)
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(p.W, (unsigned)((long)(p.N - 1) * p.ldw + p.K));
+  const bool sh = p.shuffled;
+  const __amdgpu_buffer_rsrc_t wrs =
+      make_rsrc(p.W, sh ? (unsigned)((long)p.N * p.K) : (unsigned)((long)(p.N - 1) * p.ldw + p.K));
+  const int wstep = sh ? 2048 : F8_BK, whalf = sh ? 1024 : 16;
   unsigned woff[NF];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) woff[f] = (unsigned)((long)(n0 + 16 * f + r) * p.ldw + k0 + 32 * g);
+  for (int f = 0; f < NF; ++f)
+    woff[f] = sh ? (unsigned)(((long)((n0 >> 4) + f) * (p.K / F8_BK) + k0 / F8_BK) * 2048 + lane * 16)
+                 : (unsigned)((long)(n0 + 16 * f + r) * p.ldw + k0 + 32 * g);
   auto load_w = [&](int t, i32x8 (&dst)[NF]) {
-    fs_load_w<NF>(wrs, woff, __builtin_amdgcn_readfirstlane(t * F8_BK), dst);
+    fs_load_w<NF>(wrs, woff, __builtin_amdgcn_readfirstlane(t * wstep), whalf, dst);
   };
 
   f32x4 acc[16][NF];
@@ -503,21 +513,25 @@ __global__ __launch_bounds__(256) void fp8_stream_reduce_kernel(const float* __r
 
 extern "C" bool dsa_fp8_stream_gemm_supported(int M, int N, int K, int rw, int S) {
   // rw weight rows per wave: 64 (4 waves: 256 per workgroup) or 32 (8 waves: 256 per workgroup);
-  // each K slice whole groups of 4 K-steps
-  return M > 0 && M <= F8_MAXM && (rw == 64 || rw == 32) && N > 0 && N % 256 == 0 && S >= 1 && K > 0 &&
-         K % (4 * F8_BK * S) == 0;
+  // each K slice whole groups of 4 K-steps.  rw 64 without split only: its split-K epilogue (the
+  // accumulators spilled around the last K-step's MFMAs) stored one wrong register per tile on
+  // gfx950 (profiles/fp8_stream_shuffle_r9u.txt), and rw 32 is the faster form there anyway
+  return M > 0 && M <= F8_MAXM && (rw == 32 || (rw == 64 && S == 1)) && N > 0 && N % 256 == 0 && S >= 1 &&
+         K > 0 && K % (4 * F8_BK * S) == 0;
 }
 
 // Y[M][N] = bf16(xs[m] ws[n] X W^T) with X [M][K] e4m3 (ldx bytes), W [N][K] e4m3 (ldw bytes); rw weight
 // rows per wave (64 | 32); S > 1: `part` holds S * M * N floats
+// shuffled: W is in the ops.serving.fp8_stream_shuffle order (ldw ignored; N * K bytes, < 4 GiB)
 extern "C" hipError_t dsa_fp8_stream_gemm(const void* X, const float* xs, const void* W, const float* ws, void* Y,
                                           float* part, int M, int N, int K, long ldx, long ldw, long ldy, int rw,
-                                          int S, hipStream_t st) {
+                                          int S, int shuffled, hipStream_t st) {
   if (!dsa_fp8_stream_gemm_supported(M, N, K, rw, S) || ldx % 16 || ldw % 16 || ldy % 4 || ldx < K || ldw < K ||
       ldy < N)
     return hipErrorInvalidValue;
   if (S > 1 && part == nullptr) return hipErrorInvalidValue;
   if ((long)(M - 1) * ldx + K > 0xffffffffL) return hipErrorInvalidValue;  // X through a 32-bit buffer range
+  if (shuffled && (long)N * K > 0xffffffffL) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
     DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fp8_stream_gemm_kernel<4, 4, 3>),
@@ -526,7 +540,7 @@ extern "C" hipError_t dsa_fp8_stream_gemm(const void* X, const float* xs, const 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
     attr = true;
   }
-  FSArgs a{(const uint8_t*)X, xs, (const uint8_t*)W, ws, (bf16_t*)Y, part, ldx, ldw, ldy, M, N, K, S};
+  FSArgs a{(const uint8_t*)X, xs, (const uint8_t*)W, ws, (bf16_t*)Y, part, ldx, ldw, ldy, M, N, K, S, shuffled};
   if (rw == 64)
     fp8_stream_gemm_kernel<4, 4, 3><<<dim3(N / 256, S), 256, FS_NX * FS_XT, st>>>(a);
   else

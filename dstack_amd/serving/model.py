@@ -40,19 +40,20 @@ from dstack_amd.ops import serving as sops
 
 class Fp8Weight:
     """A linear weight stored as e4m3 bytes ``q`` [N, K] (uint8 storage, float8_e4m3fn values) with
-    one fp32 scale per output row ``s`` [N]: W ~= q * s[:, None]."""
+    one fp32 scale per output row ``s`` [N]: W ~= q * s[:, None].  ``qs``: the same bytes in the
+    weight-streaming decode GEMM's layout (``ops.serving.fp8_stream_shuffle``), or None."""
 
-    __slots__ = ("q", "s")
+    __slots__ = ("q", "s", "qs")
 
-    def __init__(self, q: torch.Tensor, s: torch.Tensor):
-        self.q, self.s = q, s
+    def __init__(self, q: torch.Tensor, s: torch.Tensor, qs: torch.Tensor | None = None):
+        self.q, self.s, self.qs = q, s, qs
 
     @property
     def shape(self):
         return self.q.shape
 
     def nbytes(self) -> int:
-        return self.q.numel() + self.s.numel() * 4
+        return self.q.numel() + self.s.numel() * 4 + (self.qs.numel() if self.qs is not None else 0)
 
 
 class Fp8Act:
@@ -229,6 +230,12 @@ class ServingLlama:
         self.fp8_swiglu_gemm = os.environ.get("DSTACK_AMD_FP8_SWIGLU_GEMM", "0") == "1"
         # fp8: norms feeding an fp8 GEMM write e4m3 directly (DSTACK_AMD_FP8_FUSE_NORM=0: separate quant)
         self.fuse_norm_quant = os.environ.get("DSTACK_AMD_FP8_FUSE_NORM", "1") != "0"
+        # decode batches of 129..256 rows multiply the largest fp8 weights
+        # (gate/up N >= 32768, down K >= 16384: the Llama-3-70B MLP on one GPU) on the weight-streaming
+        # GEMM (csrc/fp8_gemm.hip fp8_stream_gemm) from a pre-shuffled second copy of those weights
+        # (+0.7 GB per 70B layer): decode 6.86-6.88k -> 7.17-7.21k tok/s on the 70B fp8 bench, same box
+        # (profiles/fp8_stream_shuffle_r9u.txt).  DSTACK_AMD_FP8_STREAM=0: hipBLASLt, no second copy
+        self.fp8_stream = os.environ.get("DSTACK_AMD_FP8_STREAM", "1") != "0"
         # fp8 GEMMs of at least this many rows (prefill) run hipBLASLt with scalar scales on the raw
         # e4m3 operands and apply the row-wise scales afterwards: in the gate/up output's SwiGLU-quant
         # kernel, or in one in-place pass for o / down (profiles/fp8_scaling_modes_r8z.txt: 12-25 %
@@ -411,11 +418,25 @@ class ServingLlama:
                 else:
                     q8, sc = ref.quant_fp8_rows(w)
                     q = q8.view(torch.uint8)
-                L[k] = Fp8Weight(q, sc)
+                L[k] = Fp8Weight(q, sc, self._stream_copy(k, q))
                 del w
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
         return self
+
+    def _stream_split(self, N: int, K: int) -> int | None:
+        """The K split the weight-streaming decode GEMM runs an [N, K] fp8 weight with, or None
+        where hipBLASLt stays faster (profiles/fp8_stream_shuffle_r9u.txt: gate/up N = 57344 119.9 vs
+        139.4 us, down K = 28672 75.2 vs 80.8 us at 256 rows; qkv / o lose)."""
+        if not (self.hip and self.fp8_stream and self.tp == 1) or not (N >= 32768 or K >= 16384):
+            return None
+        split = K // 4096 if K > 8192 else 1
+        return split if _ext.require().fp8_stream_gemm_supported(256, N, K, 32, split) else None
+
+    def _stream_copy(self, key: str, q: torch.Tensor):
+        if key not in ("wgu", "wdown") or self._stream_split(*q.shape) is None:
+            return None
+        return sops.fp8_stream_shuffle(q)
 
     def weight_bytes(self) -> int:
         ts = [self.embed, self.norm] + ([] if self.spec.tie_embeddings else [self.lm_head])
@@ -531,6 +552,9 @@ class ServingLlama:
             if self.gemv and C.gemv_fp8_supported(M, x.shape[1]):
                 return C.gemv_fp8(x, w.q, w.s)
             xq, xs = C.quant_fp8_rows(x)
+        if w.qs is not None and 128 < M <= 256 and xq.stride(0) % 16 == 0:
+            split = self._stream_split(*w.q.shape)
+            return _ext.require().fp8_stream_gemm(xq.view(torch.uint8), xs, w.qs, w.s, 32, split, True)
         if self.hip and self.fp8_gemm == "hip" and M > 4:
             y = self._fp8_rows(xq, xs, w)
             if y is not None:

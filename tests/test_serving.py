@@ -715,6 +715,36 @@ def test_gpu_fp8_deferred_row_scales_match_rowwise(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_fp8_stream_gemm_in_the_engine(gpu, monkeypatch):
+    """The weight-streaming decode fp8 GEMM in the model (``_mm_fp8`` for 129..256 rows, pre-shuffled
+    second copy ``Fp8Weight.qs``), forced onto llama-tiny's MLP (the default rule only takes the
+    70B-sized gate/up and down weights): a 256-token forward's logits match the hipBLASLt path's."""
+    from dstack_amd.ops import _ext
+    from dstack_amd.ops.serving import fp8_stream_shuffle
+
+    kw = dict(device="cuda", max_model_len=512, max_batch=8, num_pages=64)
+    q8 = LLMEngine.from_model("llama-tiny", quantization="fp8", **kw)
+    m = q8.model
+    assert all(L[k].qs is None for L in m.layers for k in m.FP8_KEYS)  # tiny shapes: no second copy
+    n = 256  # (prefill segments are 128-row aligned)
+    prompt = torch.arange(1, n + 1, device=gpu)
+    pos = torch.arange(n, dtype=torch.int32, device=gpu)
+    slots = torch.arange(n, dtype=torch.int32, device=gpu)
+    a = m.prefill(prompt, pos, slots, [0], [n]).float()
+    m._stream_split = lambda N, K: 1
+    for L in m.layers:
+        for k in ("wgu", "wdown"):
+            L[k].qs = fp8_stream_shuffle(L[k].q)
+    C = _ext.require()
+    calls, orig = [], C.fp8_stream_gemm
+    monkeypatch.setattr(C, "fp8_stream_gemm", lambda *a_, **k_: calls.append(a_[0].shape) or orig(*a_, **k_))
+    b = m.prefill(prompt, pos, slots, [0], [n]).float()
+    assert len(calls) == 2 * len(m.layers) and all(128 < c[0] <= 256 for c in calls), calls
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=-1).item()
+    assert cos > 0.999, cos
+
+
+@pytest.mark.gpu
 def test_gpu_fp8_swiglu_gemm_matches_deferred_kernels(gpu):
     """The fp8 gate/up GEMM with the SwiGLU and the row-wise scales in its epilogue plus the
     one-pass row quantizer (csrc/gemm_nt.hip EPI_SWIGLU_F8, fp8.hip quant_rows_pmax) against
@@ -974,3 +1004,26 @@ def test_gpu_swiglu_quant_fp8_rows_matches_separate_kernels(gpu):
         q2, s2 = C.quant_fp8_rows(C.swiglu_fwd(gu))
         assert torch.equal(s, s2)
         assert torch.equal(q.view(torch.uint8), q2.view(torch.uint8))
+
+
+def test_fp8_stream_shuffle_layout_matches_the_kernel_addressing():
+    """ops.serving.fp8_stream_shuffle (the pre-shuffled weight layout of fp8_stream_gemm(...,
+    shuffled=True)): lane r + 16 g of 16-row block nb at K-step t reads bytes [32 g + 16 h, +16) of row
+    16 nb + r at offset ((nb (K / 128) + t) 2 + h) 1024 + 16 lane -- the address the kernel computes
+    (csrc/fp8_gemm.hip fp8_stream_gemm_kernel); unshuffle inverts it."""
+    N, K = 48, 384
+    w = torch.randint(0, 256, (N, K), dtype=torch.uint8)
+    sh = sops.fp8_stream_shuffle(w)
+    assert sh.shape == (N, K) and sh.is_contiguous()
+    assert torch.equal(sops.fp8_stream_unshuffle(sh), w)
+    flat = sh.flatten()
+    for nb in range(N // 16):
+        for t in range(K // 128):
+            for lane in range(64):
+                r, g = lane % 16, lane // 16
+                for h in range(2):
+                    off = ((nb * (K // 128) + t) * 2 + h) * 1024 + lane * 16
+                    k = t * 128 + 32 * g + 16 * h
+                    assert torch.equal(flat[off:off + 16], w[16 * nb + r, k:k + 16])
+    f8 = sops.fp8_stream_shuffle(w.view(torch.float8_e4m3fn))
+    assert f8.dtype == torch.float8_e4m3fn and torch.equal(f8.view(torch.uint8), sh)

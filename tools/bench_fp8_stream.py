@@ -1,5 +1,5 @@
 """Llama-3-70B decode projections at a batch of 256 rows: the weight-streaming fp8 GEMM
-(csrc/fp8_gemm.hip fp8_stream_gemm, split-K variants) against hipBLASLt's row-scaled fp8 GEMM with
+(csrc/fp8_gemm.hip fp8_stream_gemm, split-K variants, row-major or pre-shuffled weights) against hipBLASLt's row-scaled fp8 GEMM with
 the serving engine's tuned selections (torch._scaled_mm) and the LDS-staged in-tree form
 (fp8_rows_gemm).  One JSON line per shape.
 
@@ -15,6 +15,7 @@ import torch  # noqa: E402
 
 from dstack_amd.ops import _ext, gemm_tuning  # noqa: E402
 from dstack_amd.ops import reference as ref  # noqa: E402
+from dstack_amd.ops.serving import fp8_stream_shuffle  # noqa: E402
 
 SHAPES = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672)}
 
@@ -46,16 +47,21 @@ def main():
                                            scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1), out_dtype=torch.bfloat16)
             ref_y = lib().float()
             cands = {"lib": lib}
+            wsh = fp8_stream_shuffle(wq)
             for rw in (64, 32):
                 for sp in (1, 2, 4, 7, 8):
                     if C.fp8_stream_gemm_supported(M, N, K, rw, sp):
                         cands[f"stream_r{rw}_s{sp}"] = (lambda sp=sp, rw=rw: C.fp8_stream_gemm(xq, xs, wq, ws, rw, sp))
+                        cands[f"stream_sh_r{rw}_s{sp}"] = (
+                            lambda sp=sp, rw=rw: C.fp8_stream_gemm(xq, xs, wsh, ws, rw, sp, True))
             if C.fp8_rows_gemm_supported(M, N, K, 64, 1):
                 cands["rows_bm64"] = lambda: C.fp8_rows_gemm(xq, xs, wq, ws, 64, 1)
             out = {"shape": name, "M": M, "N": N, "K": K}
             for k, fn in cands.items():
                 err = ((fn().float() - ref_y).norm() / ref_y.norm()).item()
-                assert err < 1e-2, (k, err)
+                if not err < 1e-2:  # reported, not timed
+                    out[k + "_rel_err"] = err
+                    continue
                 t = statistics.median(timed(fn) for _ in range(5))
                 out[k + "_us"] = round(t, 2)
                 out[k + "_tb_s"] = round(N * K / t / 1e6, 3)
@@ -63,7 +69,7 @@ def main():
             out["best_stream"] = best[1][:-3]
             out["speedup_vs_lib"] = round(out["lib_us"] / best[0], 3)
             print(json.dumps(out), flush=True)
-            del xq, wq
+            del xq, wq, wsh
             torch.cuda.empty_cache()
 
 

@@ -15,6 +15,7 @@
 #   pmc=<c1,c2,...>[@<cmd>]     one rocprofv3 --pmc pass (default command: tools/bench_attn.py)
 #   gemm[=<SHAPES>]             tools/bench_gemm_nt.py (in-tree NT GEMM vs hipBLASLt)
 #   attn                        tools/bench_attn.py
+#   tool=<script.py>            any other measurement script (python -u <script.py>)
 #   e2e[=<env assignments>]     tools/e2e_gpu_apply.py (the task through the server, local backend)
 #   serve=<bench_serve.py args> bench_serve.py
 set -o pipefail
@@ -75,6 +76,7 @@ for step in "$@"; do
         -d "$OUT/pmc" -o p -- $cmd || exit 1 ;;
     gemm) SHAPES="$val" run gemm 600 python -u tools/bench_gemm_nt.py || exit 1 ;;
     attn) run attn 600 python -u tools/bench_attn.py || exit 1 ;;
+    tool) run "$(basename "$val" .py)" 600 python -u "$val" || exit 1 ;;
     e2e)
       # shellcheck disable=SC2086
       run e2e 900 env $val python -u tools/e2e_gpu_apply.py || exit 1 ;;
