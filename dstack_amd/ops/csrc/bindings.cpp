@@ -661,10 +661,10 @@ bool fp8_stream_gemm_supported(int64_t M, int64_t N, int64_t K, int64_t rw, int6
 
 // y[M][N] = bf16(xs[m] ws[n] (xq wq^T)) for a decode batch of up to 256 rows with the weights streamed
 // straight into registers (csrc/fp8_gemm.hip fp8_stream_gemm); rw = 64 | 32 weight rows per wave,
-// S > 1 splits K (fp32 partials allocated here, added by a second kernel); shuffled: wq [N][K] holds the
-// weights in ops.serving.fp8_stream_shuffle order
+// S > 1 splits K (fp32 partials allocated here, added by a second kernel); shuffled 1 | 2: wq [N][K] holds
+// the weights in ops.serving.fp8_stream_shuffle(wq, group=16 | 256) order
 torch::Tensor fp8_stream_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t rw,
-                              int64_t S, bool shuffled) {
+                              int64_t S, int64_t shuffled) {
   for (auto* t : {&xq, &wq}) {
     TORCH_CHECK(t->is_cuda() && t->element_size() == 1 && t->dim() == 2 && t->stride(1) == 1,
                 "fp8_stream_gemm: 1-byte 2-D operands with contiguous rows");
@@ -673,7 +673,8 @@ torch::Tensor fp8_stream_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor 
   }
   const int64_t M = xq.size(0), K = xq.size(1), N = wq.size(0);
   TORCH_CHECK(wq.size(1) == K, "fp8_stream_gemm: K mismatch");
-  TORCH_CHECK(!shuffled || wq.is_contiguous(), "fp8_stream_gemm: a shuffled weight is one contiguous block");
+  TORCH_CHECK(shuffled >= 0 && shuffled <= 2 && (!shuffled || wq.is_contiguous()),
+              "fp8_stream_gemm: shuffled 0 | 1 | 2, a shuffled weight one contiguous block");
   TORCH_CHECK(xs.is_cuda() && xs.scalar_type() == torch::kFloat32 && xs.is_contiguous() && xs.numel() == M,
               "fp8_stream_gemm: xs fp32 [M]");
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.is_contiguous() && ws.numel() == N,
@@ -959,7 +960,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("cnt") = pybind11::none());
   m.def("fp8_rows_gemm_supported", &fp8_rows_gemm_supported);
   m.def("fp8_stream_gemm", &fp8_stream_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),
-        pybind11::arg("ws"), pybind11::arg("rw") = 64, pybind11::arg("split") = 1, pybind11::arg("shuffled") = false);
+        pybind11::arg("ws"), pybind11::arg("rw") = 64, pybind11::arg("split") = 1, pybind11::arg("shuffled") = 0);
   m.def("fp8_stream_gemm_supported", &fp8_stream_gemm_supported);
   m.def("swiglu_quant_fp8_rows", &swiglu_quant_fp8_rows, py::arg("gu"), py::arg("rs") = py::none(),
         py::arg("cs") = py::none());

@@ -303,7 +303,7 @@ struct FSArgs {
   float* part;  // [S][M][N] fp32 (S > 1)
   long ldx, ldw, ldy;
   int M, N, K, S;
-  int shuffled;  // W in ops.serving.fp8_stream_shuffle order
+  int shuffled;  // W in ops.serving.fp8_stream_shuffle order: 0 row-major, 1 per 16-row block, 2 per 256 rows
 };
 
 template <int N>
@@ -328,6 +328,22 @@ __device__ __forceinline__ void fs_issue_x(__amdgpu_buffer_rsrc_t xrs, const uns
   for (int i = 0; i < XP; ++i)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, LDS3(void, slot + (w + NWV * i) * 1024), 16, xoff[i], so, 0, 0);
 }
+// 7 waves (XP = 5 pieces, the last ones loaded twice -- identical bytes to one slot): the offsets are
+// recomputed at every issue from the lane id behind an opaque move (kept live, 5 offsets spilled in
+// the main loop)
+template <int XP, int NWV>
+__device__ __forceinline__ void fs_issue_x_rc(__amdgpu_buffer_rsrc_t xrs, char* slot, int so, int w, int M, long ldx) {
+  int lane = __lane_id();
+  asm volatile("" : "+v"(lane));
+#pragma unroll
+  for (int i = 0; i < XP; ++i) {
+    const int piece = min(w + NWV * i, 31), row = 8 * piece + (lane >> 3);
+    const int ch = (lane & 7) ^ f8_swz(row & 15);
+    const int srow = row < M ? row : M - 1;  // rows past M re-read the last real row (not stored)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, LDS3(void, slot + piece * 1024), 16,
+                                             (unsigned)((long)srow * ldx + ch * 16), so, 0, 0);
+  }
+}
 // half: the byte distance of a fragment's two 16-byte pieces (16: adjacent in a row; 1 KiB: pre-shuffled),
 // added to the uniform offset so that it costs no VGPRs
 template <int NF>
@@ -348,7 +364,7 @@ __device__ __forceinline__ void fs_load_w(__amdgpu_buffer_rsrc_t wrs, const unsi
 template <int NWV, int NF, int D>
 __global__ __launch_bounds__(64 * NWV, 1) void fp8_stream_gemm_kernel(FSArgs p) {
   constexpr int NSET = 4;               // weight register sets = the unroll factor (D + 1 live)
-  constexpr int XP = 32 / NWV;          // X pieces (1 KiB) per wave per step
+  constexpr int XP = (32 + NWV - 1) / NWV;  // X pieces (1 KiB) per wave per step
   constexpr int OPS = XP + 2 * NF;      // vector-memory ops per wave per step
   constexpr int WAIT = (D - 1) * OPS;   // issued after W(t): X(t+1), W(t+1), ..., X(t+D-1), W(t+D-1)
   static_assert(D >= 1 && D + 1 <= NSET, "D + 1 weight sets live");
@@ -361,30 +377,42 @@ __global__ __launch_bounds__(64 * NWV, 1) void fp8_stream_gemm_kernel(FSArgs p) 
 
   // --- activation DMA: 32 pieces of 1 KiB (8 token rows x 128 B) per step, XP per wave ------------
   const __amdgpu_buffer_rsrc_t xrs = make_rsrc(p.X, (unsigned)((long)(p.M - 1) * p.ldx + p.K));
-  unsigned xoff[XP];
+  unsigned xoff[32 % NWV ? 1 : XP];
+  if constexpr (32 % NWV == 0) {
 #pragma unroll
-  for (int i = 0; i < XP; ++i) {
-    const int piece = w + NWV * i, row = 8 * piece + (lane >> 3);
-    const int ch = (lane & 7) ^ f8_swz(row & 15);
-    const int srow = row < p.M ? row : p.M - 1;  // rows past M re-read the last real row (not stored)
-    xoff[i] = (unsigned)((long)srow * p.ldx + ch * 16);
+    for (int i = 0; i < XP; ++i) {
+      const int piece = w + NWV * i, row = 8 * piece + (lane >> 3);
+      const int ch = (lane & 7) ^ f8_swz(row & 15);
+      const int srow = row < p.M ? row : p.M - 1;  // rows past M re-read the last real row (not stored)
+      xoff[i] = (unsigned)((long)srow * p.ldx + ch * 16);
+    }
   }
   auto issue_x = [&](int t) {
-    fs_issue_x<XP, NWV>(xrs, xoff, smem + (t & (FS_NX - 1)) * FS_XT,
-                        __builtin_amdgcn_readfirstlane((int)(k0 + (long)t * F8_BK)), w);
+    const int so = __builtin_amdgcn_readfirstlane((int)(k0 + (long)t * F8_BK));
+    if constexpr (32 % NWV == 0)
+      fs_issue_x<XP, NWV>(xrs, xoff, smem + (t & (FS_NX - 1)) * FS_XT, so, w);
+    else
+      fs_issue_x_rc<XP, NWV>(xrs, smem + (t & (FS_NX - 1)) * FS_XT, so, w, p.M, p.ldx);
   };
   // --- weights: rows n0 + 16 f + r, bytes [32 g, 32 g + 32) of the K-step, through a buffer
   // descriptor (one 32-bit offset per fragment, the step in an SGPR: 64-bit row pointers spilled),
   // nontemporal (read once: the weights must not evict the activations from L2)
-  const bool sh = p.shuffled;
+  // shuffled 1: a 16-row block's 2 KiB pieces consecutive over K; 2: the GB blocks of a workgroup's rows
+  // side by side per K-step (GB x 2 KiB contiguous per workgroup and step)
+  constexpr int GB = NWV * NF;
+  const int sh = p.shuffled;
   const __amdgpu_buffer_rsrc_t wrs =
       make_rsrc(p.W, sh ? (unsigned)((long)p.N * p.K) : (unsigned)((long)(p.N - 1) * p.ldw + p.K));
-  const int wstep = sh ? 2048 : F8_BK, whalf = sh ? 1024 : 16;
+  const int wstep = sh == 2 ? GB * 2048 : sh ? 2048 : F8_BK, whalf = sh ? 1024 : 16;
+  const long ksteps = p.K / F8_BK;
   unsigned woff[NF];
 #pragma unroll
-  for (int f = 0; f < NF; ++f)
-    woff[f] = sh ? (unsigned)(((long)((n0 >> 4) + f) * (p.K / F8_BK) + k0 / F8_BK) * 2048 + lane * 16)
-                 : (unsigned)((long)(n0 + 16 * f + r) * p.ldw + k0 + 32 * g);
+  for (int f = 0; f < NF; ++f) {
+    const int blk = (n0 >> 4) + f;  // 16-row block
+    woff[f] = sh == 2 ? (unsigned)((((long)(blk / GB) * ksteps + k0 / F8_BK) * GB + blk % GB) * 2048 + lane * 16)
+              : sh    ? (unsigned)(((long)blk * ksteps + k0 / F8_BK) * 2048 + lane * 16)
+                      : (unsigned)((long)(n0 + 16 * f + r) * p.ldw + k0 + 32 * g);
+  }
   auto load_w = [&](int t, i32x8 (&dst)[NF]) {
     fs_load_w<NF>(wrs, woff, __builtin_amdgcn_readfirstlane(t * wstep), whalf, dst);
   };
@@ -416,25 +444,26 @@ __global__ __launch_bounds__(64 * NWV, 1) void fp8_stream_gemm_kernel(FSArgs p) 
     }
     __builtin_amdgcn_sched_barrier(0);
     const char* st = smem + (t & (FS_NX - 1)) * FS_XT + r * F8_BK;
-    // token-block fragments two blocks ahead of their MFMAs (3 buffers), the interleave pinned
-    i32x8 xf[3];
-    xf[0] = f8_frag(st + c0, st + c1);
-    xf[1] = f8_frag(st + 2048 + c0, st + 2048 + c1);
+    // token-block fragments LA = 2 blocks ahead of their MFMAs (3 buffers), the interleave pinned
+    constexpr int LA = 2;
+    i32x8 xf[LA + 1];
+#pragma unroll
+    for (int i = 0; i < LA; ++i) xf[i] = f8_frag(st + i * 2048 + c0, st + i * 2048 + c1);
 #pragma unroll
     for (int tb = 0; tb < 16; ++tb) {
-      if (tb + 2 < 16) xf[(tb + 2) % 3] = f8_frag(st + (tb + 2) * 2048 + c0, st + (tb + 2) * 2048 + c1);
+      if (tb + LA < 16) xf[(tb + LA) % (LA + 1)] = f8_frag(st + (tb + LA) * 2048 + c0, st + (tb + LA) * 2048 + c1);
 #pragma unroll
       for (int f = 0; f < NF; ++f)
-        acc[tb][f] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[j][f], xf[tb % 3], acc[tb][f], 0, 0, 0, 127,
-                                                                      0, 127);
+        acc[tb][f] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[j][f], xf[tb % (LA + 1)], acc[tb][f], 0, 0, 0,
+                                                                      127, 0, 127);
     }
-    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // blocks 0, 1: 2 ds_read_b128 each
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * LA, 0);  // the first LA blocks: 2 ds_read_b128 each
 #pragma unroll
-    for (int tb = 0; tb < 14; ++tb) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // block tb + 2
+    for (int tb = 0; tb < 16 - LA; ++tb) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // block tb + LA
       __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);  // block tb's MFMAs
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * NF, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, LA * NF, 0);
     __builtin_amdgcn_sched_barrier(0);
   };
   using T = std::true_type;
@@ -512,16 +541,18 @@ __global__ __launch_bounds__(256) void fp8_stream_reduce_kernel(const float* __r
 }
 
 extern "C" bool dsa_fp8_stream_gemm_supported(int M, int N, int K, int rw, int S) {
-  // rw weight rows per wave: 64 (4 waves: 256 per workgroup) or 32 (8 waves: 256 per workgroup);
-  // each K slice whole groups of 4 K-steps.  rw 64 without split only: its split-K epilogue (the
-  // accumulators spilled around the last K-step's MFMAs) stored one wrong register per tile on
-  // gfx950 (profiles/fp8_stream_shuffle_r9u.txt), and rw 32 is the faster form there anyway
-  return M > 0 && M <= F8_MAXM && (rw == 32 || (rw == 64 && S == 1)) && N > 0 && N % 256 == 0 && S >= 1 &&
-         K > 0 && K % (4 * F8_BK * S) == 0;
+  // rw weight rows per wave: 64 (4 waves: 256 per workgroup), 32 (8 waves: 256 per workgroup) or 28
+  // (7 waves x 32 rows: 224 per workgroup, e.g. 256 workgroups for the 70B gate/up); each K slice whole
+  // groups of 4 K-steps.  rw 64 without split only: its split-K epilogue (the accumulators spilled
+  // around the last K-step's MFMAs) stored one wrong register per tile on gfx950
+  // (profiles/fp8_stream_shuffle_r9u.txt), and rw 32 is the faster form there anyway
+  const int wgr = rw == 28 ? 224 : 256;
+  return M > 0 && M <= F8_MAXM && (rw == 32 || rw == 28 || (rw == 64 && S == 1)) && N > 0 && N % wgr == 0 &&
+         S >= 1 && K > 0 && K % (4 * F8_BK * S) == 0;
 }
 
 // Y[M][N] = bf16(xs[m] ws[n] X W^T) with X [M][K] e4m3 (ldx bytes), W [N][K] e4m3 (ldw bytes); rw weight
-// rows per wave (64 | 32); S > 1: `part` holds S * M * N floats
+// rows per wave (64 | 32 | 28: 7 waves); S > 1: `part` holds S * M * N floats
 // shuffled: W is in the ops.serving.fp8_stream_shuffle order (ldw ignored; N * K bytes, < 4 GiB)
 extern "C" hipError_t dsa_fp8_stream_gemm(const void* X, const float* xs, const void* W, const float* ws, void* Y,
                                           float* part, int M, int N, int K, long ldx, long ldw, long ldy, int rw,
@@ -538,11 +569,15 @@ extern "C" hipError_t dsa_fp8_stream_gemm(const void* X, const float* xs, const 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
     DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fp8_stream_gemm_kernel<8, 2, 2>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fp8_stream_gemm_kernel<7, 2, 2>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
     attr = true;
   }
   FSArgs a{(const uint8_t*)X, xs, (const uint8_t*)W, ws, (bf16_t*)Y, part, ldx, ldw, ldy, M, N, K, S, shuffled};
   if (rw == 64)
     fp8_stream_gemm_kernel<4, 4, 3><<<dim3(N / 256, S), 256, FS_NX * FS_XT, st>>>(a);
+  else if (rw == 28)
+    fp8_stream_gemm_kernel<7, 2, 2><<<dim3(N / 224, S), 448, FS_NX * FS_XT, st>>>(a);
   else
     fp8_stream_gemm_kernel<8, 2, 2><<<dim3(N / 256, S), 512, FS_NX * FS_XT, st>>>(a);
   DSA_CHECK(hipGetLastError());

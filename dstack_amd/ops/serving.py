@@ -182,21 +182,26 @@ def sample_ref(logits, temps, seeds, steps):
 # ----------------------------------------------------------------------------------------------
 # Decode-GEMM weight layout
 # ----------------------------------------------------------------------------------------------
-def fp8_stream_shuffle(wq: torch.Tensor) -> torch.Tensor:
-    """The weight layout of ``fp8_stream_gemm(..., shuffled=True)`` (``csrc/fp8_gemm.hip``): for each
+def fp8_stream_shuffle(wq: torch.Tensor, group: int = 16) -> torch.Tensor:
+    """The weight layout of ``fp8_stream_gemm(..., shuffled=1 | 2)`` (``csrc/fp8_gemm.hip``): for each
     block of 16 weight rows and each 128-byte K-step, the 2 KiB that one MFMA fragment of a wave
     reads, in lane order -- half h (16 bytes of 32) of lane ``r + 16 g`` (row r, bytes 32 g .. 32 g + 32)
-    at ``h * 1024 + lane * 16``.  Every weight load of the kernel is then 1 KiB contiguous and each
-    16-row block's stream runs sequentially over K.  ``wq`` [N][K] 1-byte, N % 16 == 0, K % 128 == 0;
-    returns a contiguous [N][K] tensor of the same dtype (done once, when the weights are loaded)."""
+    at ``h * 1024 + lane * 16``.  Every weight load of the kernel is then 1 KiB contiguous.
+    ``group`` 16 (shuffled=1): a block's pieces run consecutively over K; the workgroup's rows
+    (shuffled=2: 256, or 224 for the 7-wave form): per K-step the blocks of one workgroup sit side
+    by side (group x 128 bytes contiguous per workgroup and step).  ``wq`` [N][K] 1-byte, N % group == 0, K % 128 == 0; returns a contiguous
+    [N][K] tensor of the same dtype (done once, when the weights are loaded)."""
     N, K = wq.shape
-    assert N % 16 == 0 and K % 128 == 0 and wq.element_size() == 1, (tuple(wq.shape), wq.dtype)
-    b = wq.view(torch.uint8).reshape(N // 16, 16, K // 128, 4, 2, 16)  # (nb, r, t, g, h, byte)
-    return b.permute(0, 2, 4, 3, 1, 5).contiguous().view(N, K).view(wq.dtype)
+    assert group % 16 == 0 and N % group == 0 and K % 128 == 0 and wq.element_size() == 1, (
+        tuple(wq.shape), wq.dtype, group)
+    nb = group // 16
+    b = wq.view(torch.uint8).reshape(N // group, nb, 16, K // 128, 4, 2, 16)  # (grp, blk, r, t, g, h, byte)
+    return b.permute(0, 3, 1, 5, 4, 2, 6).contiguous().view(N, K).view(wq.dtype)
 
 
-def fp8_stream_unshuffle(ws: torch.Tensor) -> torch.Tensor:
+def fp8_stream_unshuffle(ws: torch.Tensor, group: int = 16) -> torch.Tensor:
     """Inverse of :func:`fp8_stream_shuffle` (tests)."""
     N, K = ws.shape
-    b = ws.view(torch.uint8).reshape(N // 16, K // 128, 2, 4, 16, 16)  # (nb, t, h, g, r, byte)
-    return b.permute(0, 4, 1, 3, 2, 5).contiguous().view(N, K).view(ws.dtype)
+    nb = group // 16
+    b = ws.view(torch.uint8).reshape(N // group, K // 128, nb, 2, 4, 16, 16)  # (grp, t, blk, h, g, r, byte)
+    return b.permute(0, 2, 5, 1, 4, 3, 6).contiguous().view(N, K).view(ws.dtype)

@@ -236,6 +236,7 @@ class ServingLlama:
         # (+0.7 GB per 70B layer): decode 6.86-6.88k -> 7.17-7.21k tok/s on the 70B fp8 bench, same box
         # (profiles/fp8_stream_shuffle_r9u.txt).  DSTACK_AMD_FP8_STREAM=0: hipBLASLt, no second copy
         self.fp8_stream = os.environ.get("DSTACK_AMD_FP8_STREAM", "1") != "0"
+        self.fp8_stream_layout = int(os.environ.get("DSTACK_AMD_FP8_STREAM_LAYOUT", "2"))  # 1 | 2 (fp8_stream_shuffle)
         # fp8 GEMMs of at least this many rows (prefill) run hipBLASLt with scalar scales on the raw
         # e4m3 operands and apply the row-wise scales afterwards: in the gate/up output's SwiGLU-quant
         # kernel, or in one in-place pass for o / down (profiles/fp8_scaling_modes_r8z.txt: 12-25 %
@@ -424,19 +425,23 @@ class ServingLlama:
             torch.cuda.empty_cache()
         return self
 
-    def _stream_split(self, N: int, K: int) -> int | None:
-        """The K split the weight-streaming decode GEMM runs an [N, K] fp8 weight with, or None
-        where hipBLASLt stays faster (profiles/fp8_stream_shuffle_r9u.txt: gate/up N = 57344 119.9 vs
-        139.4 us, down K = 28672 75.2 vs 80.8 us at 256 rows; qkv / o lose)."""
+    def _stream_cfg(self, N: int, K: int) -> tuple[int, int] | None:
+        """(weight rows per wave, K split) the weight-streaming decode GEMM runs an [N, K] fp8 weight
+        with, or None where hipBLASLt stays faster (profiles/fp8_stream_shuffle_r9u.txt: gate/up
+        N = 57344 and down K = 28672 at 256 rows win; qkv / o lose).  The 8-wave form (32 rows per
+        wave, 256 per workgroup): the 7-wave one, whose 224-row workgroups cover all 256 CUs at the
+        70B gate/up, measured no faster (117.5 vs 116.2 us, profiles/fp8_stream_shuffle_r9x.txt)."""
         if not (self.hip and self.fp8_stream and self.tp == 1) or not (N >= 32768 or K >= 16384):
             return None
         split = K // 4096 if K > 8192 else 1
-        return split if _ext.require().fp8_stream_gemm_supported(256, N, K, 32, split) else None
+        return (32, split) if _ext.require().fp8_stream_gemm_supported(256, N, K, 32, split) else None
 
     def _stream_copy(self, key: str, q: torch.Tensor):
-        if key not in ("wgu", "wdown") or self._stream_split(*q.shape) is None:
+        cfg = self._stream_cfg(*q.shape) if key in ("wgu", "wdown") else None
+        if cfg is None:
             return None
-        return sops.fp8_stream_shuffle(q)
+        group = 16 if self.fp8_stream_layout == 1 else (224 if cfg[0] == 28 else 256)
+        return sops.fp8_stream_shuffle(q, group)
 
     def weight_bytes(self) -> int:
         ts = [self.embed, self.norm] + ([] if self.spec.tie_embeddings else [self.lm_head])
@@ -553,8 +558,8 @@ class ServingLlama:
                 return C.gemv_fp8(x, w.q, w.s)
             xq, xs = C.quant_fp8_rows(x)
         if w.qs is not None and 128 < M <= 256 and xq.stride(0) % 16 == 0:
-            split = self._stream_split(*w.q.shape)
-            return _ext.require().fp8_stream_gemm(xq.view(torch.uint8), xs, w.qs, w.s, 32, split, True)
+            rw, split = self._stream_cfg(*w.q.shape)
+            return _ext.require().fp8_stream_gemm(xq.view(torch.uint8), xs, w.qs, w.s, rw, split, self.fp8_stream_layout)
         if self.hip and self.fp8_gemm == "hip" and M > 4:
             y = self._fp8_rows(xq, xs, w)
             if y is not None:

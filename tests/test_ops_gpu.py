@@ -837,20 +837,21 @@ def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K, bm, split):
     assert int(cnt.abs().sum().item()) == 0
 
 
-@pytest.mark.parametrize("shuffled", [False, True])
-@pytest.mark.parametrize("rw", [64, 32])
+@pytest.mark.parametrize("shuffled", [0, 1, 2])
+@pytest.mark.parametrize("rw", [64, 32, 28])
 @pytest.mark.parametrize("M,N,K,split", [(256, 256, 512, 1), (256, 1024, 2048, 1), (200, 256, 2048, 2),
-                                         (129, 512, 4096, 4), (256, 512, 8192, 1), (256, 256, 7168, 7)])
+                                         (129, 512, 4096, 4), (256, 512, 8192, 1), (256, 256, 7168, 7),
+                                         (256, 448, 2048, 1), (200, 672, 4096, 2)])
 def test_fp8_stream_gemm_matches_fp32(gpu, M, N, K, split, rw, shuffled):
     """Weight-streaming decode fp8 GEMM (csrc/fp8_gemm.hip fp8_stream_gemm: each wave's weight rows
-    straight into registers two K-steps ahead, activations through an LDS ring; 4 waves x 64 rows or
-    8 waves x 32 rows; optional split-K with a separate reduce; the weights row-major or pre-shuffled
-    by ops.serving.fp8_stream_shuffle) against the fp32 product of the same e4m3 operands and row-wise
+    straight into registers two K-steps ahead, activations through an LDS ring; 4 waves x 64 rows,
+    8 waves x 32 rows or 7 x 32; optional split-K with a separate reduce; the weights row-major or pre-shuffled
+    by ops.serving.fp8_stream_shuffle in 16-row blocks or 256-row groups) against the fp32 product of the same e4m3 operands and row-wise
     scales; padded token rows (M < 256) must not be stored."""
     from dstack_amd.ops.serving import fp8_stream_shuffle
 
     C = _ext.require()
-    if rw == 64 and split > 1:  # not offered (see dsa_fp8_stream_gemm_supported)
+    if (rw == 64 and split > 1) or N % (224 if rw == 28 else 256):  # not offered (dsa_fp8_stream_gemm_supported)
         assert not C.fp8_stream_gemm_supported(M, N, K, rw, split)
         return
     assert C.fp8_stream_gemm_supported(M, N, K, rw, split)
@@ -860,7 +861,7 @@ def test_fp8_stream_gemm_matches_fp32(gpu, M, N, K, split, rw, shuffled):
     xq, xs = ref.quant_fp8_rows(x)
     wq, ws = ref.quant_fp8_rows(w)
     want = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
-    wk = fp8_stream_shuffle(wq) if shuffled else wq
+    wk = fp8_stream_shuffle(wq, {1: 16, 2: 224 if rw == 28 else 256}[shuffled]) if shuffled else wq
     for _ in range(2):
         y = C.fp8_stream_gemm(xq.view(torch.uint8), xs, wk.view(torch.uint8), ws, rw, split, shuffled)
         assert y.shape == (M, N)

@@ -731,10 +731,10 @@ def test_gpu_fp8_stream_gemm_in_the_engine(gpu, monkeypatch):
     pos = torch.arange(n, dtype=torch.int32, device=gpu)
     slots = torch.arange(n, dtype=torch.int32, device=gpu)
     a = m.prefill(prompt, pos, slots, [0], [n]).float()
-    m._stream_split = lambda N, K: 1
+    m._stream_cfg = lambda N, K: (32, 1)
     for L in m.layers:
         for k in ("wgu", "wdown"):
-            L[k].qs = fp8_stream_shuffle(L[k].q)
+            L[k].qs = fp8_stream_shuffle(L[k].q, 16 if m.fp8_stream_layout == 1 else 256)
     C = _ext.require()
     calls, orig = [], C.fp8_stream_gemm
     monkeypatch.setattr(C, "fp8_stream_gemm", lambda *a_, **k_: calls.append(a_[0].shape) or orig(*a_, **k_))
@@ -1007,23 +1007,29 @@ def test_gpu_swiglu_quant_fp8_rows_matches_separate_kernels(gpu):
 
 
 def test_fp8_stream_shuffle_layout_matches_the_kernel_addressing():
-    """ops.serving.fp8_stream_shuffle (the pre-shuffled weight layout of fp8_stream_gemm(...,
-    shuffled=True)): lane r + 16 g of 16-row block nb at K-step t reads bytes [32 g + 16 h, +16) of row
-    16 nb + r at offset ((nb (K / 128) + t) 2 + h) 1024 + 16 lane -- the address the kernel computes
-    (csrc/fp8_gemm.hip fp8_stream_gemm_kernel); unshuffle inverts it."""
-    N, K = 48, 384
+    """ops.serving.fp8_stream_shuffle (the pre-shuffled weight layouts of fp8_stream_gemm(...,
+    shuffled=1 | 2)): lane r + 16 g of 16-row block nb at K-step t reads bytes [32 g + 16 h, +16) of row
+    16 nb + r at the offset the kernel computes (csrc/fp8_gemm.hip fp8_stream_gemm_kernel) for 16-row
+    blocks and for 256-row groups; unshuffle inverts it."""
+    N, K = 1792, 384
     w = torch.randint(0, 256, (N, K), dtype=torch.uint8)
-    sh = sops.fp8_stream_shuffle(w)
-    assert sh.shape == (N, K) and sh.is_contiguous()
-    assert torch.equal(sops.fp8_stream_unshuffle(sh), w)
-    flat = sh.flatten()
-    for nb in range(N // 16):
-        for t in range(K // 128):
-            for lane in range(64):
-                r, g = lane % 16, lane // 16
-                for h in range(2):
-                    off = ((nb * (K // 128) + t) * 2 + h) * 1024 + lane * 16
-                    k = t * 128 + 32 * g + 16 * h
-                    assert torch.equal(flat[off:off + 16], w[16 * nb + r, k:k + 16])
-    f8 = sops.fp8_stream_shuffle(w.view(torch.float8_e4m3fn))
+    ks = K // 128
+    for group in (16, 256, 224):
+        sh = sops.fp8_stream_shuffle(w, group)
+        assert sh.shape == (N, K) and sh.is_contiguous()
+        assert torch.equal(sops.fp8_stream_unshuffle(sh, group), w)
+        flat = sh.flatten()
+        for nb in range(0, N // 16, 5):
+            for t in range(ks):
+                for lane in range(0, 64, 3):
+                    r, g = lane % 16, lane // 16
+                    for h in range(2):
+                        if group == 16:
+                            off = ((nb * ks + t) * 2 + h) * 1024 + lane * 16
+                        else:  # the gb blocks of a workgroup's rows side by side per K-step
+                            gb = group // 16
+                            off = (((nb // gb) * ks + t) * gb + nb % gb) * 2048 + h * 1024 + lane * 16
+                        k = t * 128 + 32 * g + 16 * h
+                        assert torch.equal(flat[off:off + 16], w[16 * nb + r, k:k + 16])
+    f8 = sops.fp8_stream_shuffle(w.view(torch.float8_e4m3fn), 224)
     assert f8.dtype == torch.float8_e4m3fn and torch.equal(f8.view(torch.uint8), sh)

@@ -47,13 +47,20 @@ def main():
                                            scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1), out_dtype=torch.bfloat16)
             ref_y = lib().float()
             cands = {"lib": lib}
-            wsh = fp8_stream_shuffle(wq)
-            for rw in (64, 32):
+            wsh = {(1, 0): fp8_stream_shuffle(wq, 16)}
+            for g in (256, 224):
+                if N % g == 0:
+                    wsh[(2, g)] = fp8_stream_shuffle(wq, g)
+            for rw in (64, 32, 28):
+                g = 224 if rw == 28 else 256
                 for sp in (1, 2, 4, 7, 8):
                     if C.fp8_stream_gemm_supported(M, N, K, rw, sp):
-                        cands[f"stream_r{rw}_s{sp}"] = (lambda sp=sp, rw=rw: C.fp8_stream_gemm(xq, xs, wq, ws, rw, sp))
-                        cands[f"stream_sh_r{rw}_s{sp}"] = (
-                            lambda sp=sp, rw=rw: C.fp8_stream_gemm(xq, xs, wsh, ws, rw, sp, True))
+                        if rw != 28:
+                            cands[f"stream_r{rw}_s{sp}"] = (
+                                lambda sp=sp, rw=rw: C.fp8_stream_gemm(xq, xs, wq, ws, rw, sp))
+                        for m, key in ((1, (1, 0)), (2, (2, g))):
+                            cands[f"stream_sh{m}_r{rw}_s{sp}"] = (
+                                lambda sp=sp, rw=rw, m=m, key=key: C.fp8_stream_gemm(xq, xs, wsh[key], ws, rw, sp, m))
             if C.fp8_rows_gemm_supported(M, N, K, 64, 1):
                 cands["rows_bm64"] = lambda: C.fp8_rows_gemm(xq, xs, wq, ws, 64, 1)
             out = {"shape": name, "M": M, "N": N, "K": K}
