@@ -436,6 +436,13 @@ class ServingLlama:
         split = K // 4096 if K > 8192 else 1
         return (32, split) if _ext.require().fp8_stream_gemm_supported(256, N, K, 32, split) else None
 
+    @staticmethod
+    def _stream_min_rows(split: int) -> int:
+        """Fewest rows the streaming GEMM is used for (its time barely depends on the rows; hipBLASLt's
+        does): the unsplit gate/up wins from 160 rows on (111 vs 123 us), the split-K down projection
+        only from 224 (71 vs 77 us; at 192, 68 vs 67), profiles/fp8_stream_rows_r9z.txt."""
+        return 129 if split == 1 else 224
+
     def _stream_copy(self, key: str, q: torch.Tensor):
         cfg = self._stream_cfg(*q.shape) if key in ("wgu", "wdown") else None
         if cfg is None:
@@ -557,9 +564,11 @@ class ServingLlama:
             if self.gemv and C.gemv_fp8_supported(M, x.shape[1]):
                 return C.gemv_fp8(x, w.q, w.s)
             xq, xs = C.quant_fp8_rows(x)
-        if w.qs is not None and 128 < M <= 256 and xq.stride(0) % 16 == 0:
+        if w.qs is not None and M <= 256 and xq.stride(0) % 16 == 0:
             rw, split = self._stream_cfg(*w.q.shape)
-            return _ext.require().fp8_stream_gemm(xq.view(torch.uint8), xs, w.qs, w.s, rw, split, self.fp8_stream_layout)
+            if M >= self._stream_min_rows(split):
+                return _ext.require().fp8_stream_gemm(xq.view(torch.uint8), xs, w.qs, w.s, rw, split,
+                                                      self.fp8_stream_layout)
         if self.hip and self.fp8_gemm == "hip" and M > 4:
             y = self._fp8_rows(xq, xs, w)
             if y is not None:

@@ -3,7 +3,7 @@
 the serving engine's tuned selections (torch._scaled_mm) and the LDS-staged in-tree form
 (fp8_rows_gemm).  One JSON line per shape.
 
-    python tools/bench_fp8_stream.py        # ROWS=256 (comma list)
+    python tools/bench_fp8_stream.py        # ROWS=256 (comma list), MODEL=8b for the Llama-3-8B shapes
 """
 import json
 import os
@@ -18,6 +18,8 @@ from dstack_amd.ops import reference as ref  # noqa: E402
 from dstack_amd.ops.serving import fp8_stream_shuffle  # noqa: E402
 
 SHAPES = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672)}
+if os.getenv("MODEL") == "8b":  # Llama-3-8B projections
+    SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
 
 
 def timed(fn, iters=50):
