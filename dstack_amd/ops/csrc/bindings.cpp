@@ -71,7 +71,7 @@ hipError_t dsa_fa_dkdv_trace(const void*, const void*, const float*, const float
 bool dsa_fp8_rows_gemm_supported(int, int, int, int, int);
 bool dsa_fp8_stream_gemm_supported(int, int, int, int, int);
 hipError_t dsa_fp8_stream_gemm(const void*, const float*, const void*, const float*, void*, float*, int, int, int,
-                               long, long, long, int, int, int, hipStream_t);
+                               long, long, long, int, int, int, int, hipStream_t);
 hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
                              long, long, long, int, int, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
@@ -664,7 +664,7 @@ bool fp8_stream_gemm_supported(int64_t M, int64_t N, int64_t K, int64_t rw, int6
 // S > 1 splits K (fp32 partials allocated here, added by a second kernel); shuffled 1 | 2: wq [N][K] holds
 // the weights in ops.serving.fp8_stream_shuffle(wq, group=16 | 256) order
 torch::Tensor fp8_stream_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t rw,
-                              int64_t S, int64_t shuffled) {
+                              int64_t S, int64_t shuffled, int64_t depth) {
   for (auto* t : {&xq, &wq}) {
     TORCH_CHECK(t->is_cuda() && t->element_size() == 1 && t->dim() == 2 && t->stride(1) == 1,
                 "fp8_stream_gemm: 1-byte 2-D operands with contiguous rows");
@@ -686,7 +686,7 @@ torch::Tensor fp8_stream_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor 
   if (S > 1) part = torch::empty({S, M, N}, xq.options().dtype(torch::kFloat32));
   check(dsa_fp8_stream_gemm(xq.data_ptr(), xs.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(),
                             S > 1 ? part.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, xq.stride(0),
-                            wq.stride(0), y.stride(0), (int)rw, (int)S, (int)shuffled, stream()),
+                            wq.stride(0), y.stride(0), (int)rw, (int)S, (int)shuffled, (int)depth, stream()),
         "fp8_stream_gemm");
   return y;
 }
@@ -960,7 +960,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("cnt") = pybind11::none());
   m.def("fp8_rows_gemm_supported", &fp8_rows_gemm_supported);
   m.def("fp8_stream_gemm", &fp8_stream_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),
-        pybind11::arg("ws"), pybind11::arg("rw") = 64, pybind11::arg("split") = 1, pybind11::arg("shuffled") = 0);
+        pybind11::arg("ws"), pybind11::arg("rw") = 64, pybind11::arg("split") = 1, pybind11::arg("shuffled") = 0,
+        pybind11::arg("depth") = 2);
   m.def("fp8_stream_gemm_supported", &fp8_stream_gemm_supported);
   m.def("swiglu_quant_fp8_rows", &swiglu_quant_fp8_rows, py::arg("gu"), py::arg("rs") = py::none(),
         py::arg("cs") = py::none());

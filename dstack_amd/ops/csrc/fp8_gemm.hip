@@ -321,7 +321,9 @@ __device__ __forceinline__ void fs_barrier() {
 
 // (device functions rather than lambdas of the kernel template: a lambda using these builtins made
 // the host pass drop the template's launch stub -- an undefined symbol at load time)
-template <int XP, int NWV>
+// (TAG: the calling kernel's prefetch depth -- one specialization per kernel; the host pass rejected a
+// second kernel template calling an already-used specialization, "substitution failure")
+template <int XP, int NWV, int TAG>
 __device__ __forceinline__ void fs_issue_x(__amdgpu_buffer_rsrc_t xrs, const unsigned (&xoff)[XP], char* slot, int so,
                                            int w) {
 #pragma unroll
@@ -390,7 +392,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void fp8_stream_gemm_kernel(FSArgs p) 
   auto issue_x = [&](int t) {
     const int so = __builtin_amdgcn_readfirstlane((int)(k0 + (long)t * F8_BK));
     if constexpr (32 % NWV == 0)
-      fs_issue_x<XP, NWV>(xrs, xoff, smem + (t & (FS_NX - 1)) * FS_XT, so, w);
+      fs_issue_x<XP, NWV, D>(xrs, xoff, smem + (t & (FS_NX - 1)) * FS_XT, so, w);
     else
       fs_issue_x_rc<XP, NWV>(xrs, smem + (t & (FS_NX - 1)) * FS_XT, so, w, p.M, p.ldx);
   };
@@ -552,17 +554,19 @@ extern "C" bool dsa_fp8_stream_gemm_supported(int M, int N, int K, int rw, int S
 }
 
 // Y[M][N] = bf16(xs[m] ws[n] X W^T) with X [M][K] e4m3 (ldx bytes), W [N][K] e4m3 (ldw bytes); rw weight
-// rows per wave (64 | 32 | 28: 7 waves); S > 1: `part` holds S * M * N floats
+// rows per wave (64 | 32 | 28: 7 waves); S > 1: `part` holds S * M * N floats; depth: weight / activation
+// prefetch distance in K-steps for rw 32 (2, or 3: 4 weight register sets live; rw 64 runs 3, rw 28 2)
 // shuffled: W is in the ops.serving.fp8_stream_shuffle order (ldw ignored; N * K bytes, < 4 GiB)
 extern "C" hipError_t dsa_fp8_stream_gemm(const void* X, const float* xs, const void* W, const float* ws, void* Y,
                                           float* part, int M, int N, int K, long ldx, long ldw, long ldy, int rw,
-                                          int S, int shuffled, hipStream_t st) {
+                                          int S, int shuffled, int depth, hipStream_t st) {
   if (!dsa_fp8_stream_gemm_supported(M, N, K, rw, S) || ldx % 16 || ldw % 16 || ldy % 4 || ldx < K || ldw < K ||
       ldy < N)
     return hipErrorInvalidValue;
   if (S > 1 && part == nullptr) return hipErrorInvalidValue;
   if ((long)(M - 1) * ldx + K > 0xffffffffL) return hipErrorInvalidValue;  // X through a 32-bit buffer range
   if (shuffled && (long)N * K > 0xffffffffL) return hipErrorInvalidValue;
+  if (depth != 2 && !(depth == 3 && rw == 32)) return hipErrorInvalidValue;  // weight prefetch distance in K-steps
   static bool attr = false;
   if (!attr) {
     DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fp8_stream_gemm_kernel<4, 4, 3>),
@@ -571,6 +575,8 @@ extern "C" hipError_t dsa_fp8_stream_gemm(const void* X, const float* xs, const 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
     DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fp8_stream_gemm_kernel<7, 2, 2>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
+    DSA_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fp8_stream_gemm_kernel<8, 2, 3>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, FS_NX * FS_XT));
     attr = true;
   }
   FSArgs a{(const uint8_t*)X, xs, (const uint8_t*)W, ws, (bf16_t*)Y, part, ldx, ldw, ldy, M, N, K, S, shuffled};
@@ -578,6 +584,8 @@ extern "C" hipError_t dsa_fp8_stream_gemm(const void* X, const float* xs, const 
     fp8_stream_gemm_kernel<4, 4, 3><<<dim3(N / 256, S), 256, FS_NX * FS_XT, st>>>(a);
   else if (rw == 28)
     fp8_stream_gemm_kernel<7, 2, 2><<<dim3(N / 224, S), 448, FS_NX * FS_XT, st>>>(a);
+  else if (depth == 3)
+    fp8_stream_gemm_kernel<8, 2, 3><<<dim3(N / 256, S), 512, FS_NX * FS_XT, st>>>(a);
   else
     fp8_stream_gemm_kernel<8, 2, 2><<<dim3(N / 256, S), 512, FS_NX * FS_XT, st>>>(a);
   DSA_CHECK(hipGetLastError());

@@ -862,8 +862,8 @@ def test_fp8_stream_gemm_matches_fp32(gpu, M, N, K, split, rw, shuffled):
     wq, ws = ref.quant_fp8_rows(w)
     want = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
     wk = fp8_stream_shuffle(wq, {1: 16, 2: 224 if rw == 28 else 256}[shuffled]) if shuffled else wq
-    for _ in range(2):
-        y = C.fp8_stream_gemm(xq.view(torch.uint8), xs, wk.view(torch.uint8), ws, rw, split, shuffled)
+    for depth in ([2, 3] if rw == 32 else [2]):
+        y = C.fp8_stream_gemm(xq.view(torch.uint8), xs, wk.view(torch.uint8), ws, rw, split, shuffled, depth)
         assert y.shape == (M, N)
         err = ((y.float() - want).norm() / want.norm()).item()
         assert err < 1e-2, err

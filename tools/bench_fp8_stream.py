@@ -63,6 +63,9 @@ def main():
                         for m, key in ((1, (1, 0)), (2, (2, g))):
                             cands[f"stream_sh{m}_r{rw}_s{sp}"] = (
                                 lambda sp=sp, rw=rw, m=m, key=key: C.fp8_stream_gemm(xq, xs, wsh[key], ws, rw, sp, m))
+                        if rw == 32:  # weights three K-steps ahead
+                            cands[f"stream_sh2d3_r{rw}_s{sp}"] = (
+                                lambda sp=sp, key=(2, g): C.fp8_stream_gemm(xq, xs, wsh[key], ws, 32, sp, 2, 3))
             if C.fp8_rows_gemm_supported(M, N, K, 64, 1):
                 cands["rows_bm64"] = lambda: C.fp8_rows_gemm(xq, xs, wq, ws, 64, 1)
             out = {"shape": name, "M": M, "N": N, "K": K}
