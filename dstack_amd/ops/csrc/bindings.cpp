@@ -73,7 +73,7 @@ bool dsa_fp8_stream_gemm_supported(int, int, int, int, int);
 hipError_t dsa_fp8_stream_gemm(const void*, const float*, const void*, const float*, void*, float*, int, int, int,
                                long, long, long, int, int, int, int, hipStream_t);
 hipError_t dsa_fp8_rows_gemm(const void*, const float*, const void*, const float*, void*, float*, int*, int, int, int,
-                             long, long, long, int, int, hipStream_t);
+                             long, long, long, int, int, int, hipStream_t);
 hipError_t dsa_gemm_km(const void*, const void*, void*, int, int, int, long, long, long, int, hipStream_t);
 hipError_t dsa_cu_hog(int, int, int, double, int*, hipStream_t);
 hipError_t dsa_synthetic_tokens(const double*, const int64_t*, const int64_t*, const int64_t*, int64_t*, int64_t*,
@@ -618,9 +618,11 @@ bool fp8_rows_gemm_supported(int64_t M, int64_t N, int64_t K, int64_t bm, int64_
 
 // y[M][N] = bf16(xs[m] ws[n] (xq wq^T)) for a decode batch (M <= 256), e4m3 operands
 // (csrc/fp8_gemm.hip); bm = 64 | 128 batch rows per workgroup; S > 1 splits K, with fp32 slabs
-// `part` (S * 256 * N floats) and tickets `cnt` ((N / 128) * ceil(M / bm) int32, zero; left zero)
+// `part` (S * 256 * N floats) and tickets `cnt` ((N / 128) * ceil(M / bm) int32, zero; left zero);
+// wimg: wq holds ops.serving.fp8_rows_shuffle(w), the weights as per-tile LDS images
 torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t bm,
-                            int64_t S, c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> cnt) {
+                            int64_t S, c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> cnt,
+                            bool wimg) {
   for (auto* t : {&xq, &wq}) {
     TORCH_CHECK(t->is_cuda() && t->element_size() == 1 && t->dim() == 2 && t->stride(1) == 1,
                 "fp8_rows_gemm: 1-byte 2-D operands with contiguous rows");
@@ -629,6 +631,7 @@ torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq
   }
   const int64_t M = xq.size(0), K = xq.size(1), N = wq.size(0);
   TORCH_CHECK(wq.size(1) == K, "fp8_rows_gemm: K mismatch");
+  TORCH_CHECK(!wimg || wq.is_contiguous(), "fp8_rows_gemm: an LDS-image weight is one contiguous block");
   TORCH_CHECK(xs.is_cuda() && xs.scalar_type() == torch::kFloat32 && xs.is_contiguous() && xs.numel() == M,
               "fp8_rows_gemm: xs fp32 [M]");
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.is_contiguous() && ws.numel() == N,
@@ -650,7 +653,7 @@ torch::Tensor fp8_rows_gemm(torch::Tensor xq, torch::Tensor xs, torch::Tensor wq
   auto y = torch::empty({M, N}, xq.options().dtype(torch::kBFloat16));
   check(dsa_fp8_rows_gemm(xq.data_ptr(), xs.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(), pp,
                           cp, (int)M, (int)N, (int)K, xq.stride(0), wq.stride(0), y.stride(0), (int)bm, (int)S,
-                          stream()),
+                          (int)wimg, stream()),
         "fp8_rows_gemm");
   return y;
 }
@@ -957,7 +960,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("out") = pybind11::none(), pybind11::arg("mode") = 0);
   m.def("fp8_rows_gemm", &fp8_rows_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),
         pybind11::arg("ws"), pybind11::arg("bm") = 64, pybind11::arg("split") = 1, pybind11::arg("part") = pybind11::none(),
-        pybind11::arg("cnt") = pybind11::none());
+        pybind11::arg("cnt") = pybind11::none(), pybind11::arg("wimg") = false);
   m.def("fp8_rows_gemm_supported", &fp8_rows_gemm_supported);
   m.def("fp8_stream_gemm", &fp8_stream_gemm, pybind11::arg("xq"), pybind11::arg("xs"), pybind11::arg("wq"),
         pybind11::arg("ws"), pybind11::arg("rw") = 64, pybind11::arg("split") = 1, pybind11::arg("shuffled") = 0,

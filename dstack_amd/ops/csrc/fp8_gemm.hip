@@ -57,6 +57,7 @@ struct F8Args {
   int* cnt;      // one ticket per output tile, zero between launches (S > 1)
   long ldx, ldw, ldy;
   int M, N, K, S;
+  int wimg;      // W stored as LDS images (ops.serving.fp8_rows_shuffle): 16 KiB per 128-row tile and K-step
 };
 __device__ __forceinline__ int f8_swz(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 2); }
 
@@ -70,7 +71,7 @@ __device__ __forceinline__ void f8_dma(const uint8_t* sbase, unsigned voff, unsi
       "global_load_lds_dwordx4 %1, %2\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds)
+      : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds))  // (uniform; kept in an SGPR)
       : "memory");
 }
 
@@ -131,18 +132,21 @@ __global__ __launch_bounds__(512, 2) void fp8_rows_gemm_kernel(F8Args p) {
       const int piece = w + 8 * (i - XP);
       const int row = 8 * piece + (lane >> 3);
       const int ch = (lane & 7) ^ f8_swz(row & 15);
-      voff[i] = (unsigned)((long)row * p.ldw + ch * 16);
+      // LDS-image weights: the piece's 1 KiB is contiguous, already in the swizzled LDS order
+      voff[i] = p.wimg ? (unsigned)(piece * 1024 + lane * 16) : (unsigned)((long)row * p.ldw + ch * 16);
       ldsoff[i] = (unsigned)(XT + piece * 1024);
     }
   }
   const unsigned lds0 = (unsigned)(uintptr_t)LDS3(char, smem);
   const uint8_t* xbase = p.X + (long)split * ks;
-  const uint8_t* wbase = p.W + (long)n0 * p.ldw + (long)split * ks;
+  const uint8_t* wbase = p.wimg ? p.W + ((long)nb * (p.K / F8_BK) + (long)split * nsteps) * (F8_BN * F8_BK)
+                                : p.W + (long)n0 * p.ldw + (long)split * ks;
+  const long wstep = p.wimg ? F8_BN * F8_BK : F8_BK;
   auto issue = [&](int step) {
     const unsigned slot = lds0 + (unsigned)((step % F8_NSTAGE) * STAGE);
-    const long ko = (long)step * F8_BK;
+    const long ko = (long)step * F8_BK, kw = (long)step * wstep;
 #pragma unroll
-    for (int i = 0; i < NP; ++i) f8_dma(i < XP ? xbase + ko : wbase + ko, voff[i], slot + ldsoff[i]);
+    for (int i = 0; i < NP; ++i) f8_dma(i < XP ? xbase + ko : wbase + kw, voff[i], slot + ldsoff[i]);
   };
 
   // --- fragment read offsets: row (lane & 15) of a 16-row block, k chunk pair g = lane >> 4 ----
@@ -244,10 +248,11 @@ extern "C" bool dsa_fp8_rows_gemm_supported(int M, int N, int K, int bm, int S) 
 // Y[M][N] = bf16(xs[m] ws[n] X W^T); X [M][K] e4m3 (row stride ldx bytes), W [N][K] e4m3 (ldw
 // bytes), Y bf16 (ldy elements).  bm: batch rows per workgroup (64 or 128).  S > 1 splits K over
 // S workgroups per output tile: `part` holds S * 256 * N floats and `cnt` one int per output tile
-// ((N / 128) * ceil(M / bm)), zero on the first call (each call leaves them zero).
+// ((N / 128) * ceil(M / bm)), zero on the first call (each call leaves them zero).  wimg: W holds
+// ops.serving.fp8_rows_shuffle(w) (per 128-row tile and K-step the 16 KiB LDS image; ldw ignored).
 extern "C" hipError_t dsa_fp8_rows_gemm(const void* X, const float* xs, const void* W, const float* ws, void* Y,
                                         float* part, int* cnt, int M, int N, int K, long ldx, long ldw, long ldy,
-                                        int bm, int S, hipStream_t st) {
+                                        int bm, int S, int wimg, hipStream_t st) {
   if (!dsa_fp8_rows_gemm_supported(M, N, K, bm, S) || ldx % 16 || ldw % 16 || ldy % 4 || ldx < K || ldw < K ||
       ldy < N)
     return hipErrorInvalidValue;
@@ -261,7 +266,7 @@ extern "C" hipError_t dsa_fp8_rows_gemm(const void* X, const float* xs, const vo
                                   hipFuncAttributeMaxDynamicSharedMemorySize, F8_NSTAGE * f8_stage<128>()));
     attr = true;
   }
-  F8Args a{(const uint8_t*)X, xs, (const uint8_t*)W, ws, (bf16_t*)Y, part, cnt, ldx, ldw, ldy, M, N, K, S};
+  F8Args a{(const uint8_t*)X, xs, (const uint8_t*)W, ws, (bf16_t*)Y, part, cnt, ldx, ldw, ldy, M, N, K, S, wimg};
   const dim3 grid((N / F8_BN) * ((M + bm - 1) / bm), S);
   if (bm == 64)
     fp8_rows_gemm_kernel<64><<<grid, 512, F8_NSTAGE * f8_stage<64>(), st>>>(a);

@@ -205,3 +205,23 @@ def fp8_stream_unshuffle(ws: torch.Tensor, group: int = 16) -> torch.Tensor:
     nb = group // 16
     b = ws.view(torch.uint8).reshape(N // group, K // 128, nb, 2, 4, 16, 16)  # (grp, t, blk, h, g, r, byte)
     return b.permute(0, 2, 5, 1, 4, 3, 6).contiguous().view(N, K).view(ws.dtype)
+
+
+def _f8_swz(r: torch.Tensor) -> torch.Tensor:
+    """The 16-byte-chunk XOR swizzle of the fp8 GEMMs' LDS tiles (csrc/fp8_gemm.hip f8_swz)."""
+    return ((r >> 1) & 1) | (((r >> 3) & 1) << 2)
+
+
+def fp8_rows_shuffle(wq: torch.Tensor) -> torch.Tensor:
+    """The weight layout of ``fp8_rows_gemm(..., wimg=True)``: per 128-row tile and 128-byte K-step
+    the 16 KiB image the kernel's LDS holds -- row r's 16-byte chunk c at ``r * 128 + c * 16`` is the
+    row's chunk ``c ^ f8_swz(r % 16)`` -- so every weight DMA of the kernel reads 1 KiB contiguous and
+    a tile's stream is sequential over K.  ``wq`` [N][K] 1-byte, N % 128 == 0, K % 128 == 0; returns a
+    contiguous [N][K] tensor of the same dtype."""
+    N, K = wq.shape
+    assert N % 128 == 0 and K % 128 == 0 and wq.element_size() == 1, (tuple(wq.shape), wq.dtype)
+    b = wq.view(torch.uint8).reshape(N // 128, 128, K // 128, 8, 16).permute(0, 2, 1, 3, 4)  # (nb, t, r, c, byte)
+    r = torch.arange(128, device=wq.device)
+    src = torch.arange(8, device=wq.device)[None, :] ^ _f8_swz(r % 16)[:, None]  # [r, c] -> source chunk
+    idx = src.view(1, 1, 128, 8, 1).expand(N // 128, K // 128, 128, 8, 16)
+    return torch.gather(b, 3, idx).contiguous().view(N, K).view(wq.dtype)

@@ -817,10 +817,14 @@ def test_swiglu_mlp_fused_matches_separate_kernels(gpu, monkeypatch, wgrad):
 @pytest.mark.parametrize("M,N,K,bm,split", [(256, 256, 512, 64, 1), (37, 384, 512, 64, 1), (200, 256, 1024, 128, 2),
                                              (1, 128, 256, 64, 1), (64, 1024, 384, 64, 1), (256, 512, 1024, 128, 1),
                                              (130, 256, 2048, 128, 4), (256, 1024, 512, 64, 2)])
-def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K, bm, split):
+@pytest.mark.parametrize("wimg", [False, True])
+def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K, bm, split, wimg):
     """Decode-batch fp8 GEMM (csrc/fp8_gemm.hip: scaled 16x16x128 f8f6f4 MFMA over 64/128-row batch
-    blocks, optional split-K with a last-arrival combine) against the fp32 product of the same
-    e4m3 operands and scales; twice, since the split-K tickets must be left at zero."""
+    blocks, optional split-K with a last-arrival combine; weights row-major or as per-tile LDS images,
+    ops.serving.fp8_rows_shuffle) against the fp32 product of the same e4m3 operands and scales;
+    twice, since the split-K tickets must be left at zero."""
+    from dstack_amd.ops.serving import fp8_rows_shuffle
+
     C = _ext.require()
     torch.manual_seed(M + N + K)
     x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
@@ -830,8 +834,9 @@ def test_fp8_rows_gemm_matches_fp32(gpu, M, N, K, bm, split):
     want = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
     part = torch.empty(split * 256 * N, device=gpu, dtype=torch.float32)
     cnt = torch.zeros((N // 128) * ((M + bm - 1) // bm), device=gpu, dtype=torch.int32)
+    wk = fp8_rows_shuffle(wq) if wimg else wq
     for _ in range(2):
-        y = C.fp8_rows_gemm(xq.view(torch.uint8), xs, wq.view(torch.uint8), ws, bm, split, part, cnt)
+        y = C.fp8_rows_gemm(xq.view(torch.uint8), xs, wk.view(torch.uint8), ws, bm, split, part, cnt, wimg)
         err = ((y.float() - want).norm() / want.norm()).item()
         assert err < 1e-2, err
     assert int(cnt.abs().sum().item()) == 0

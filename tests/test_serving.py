@@ -1033,3 +1033,21 @@ def test_fp8_stream_shuffle_layout_matches_the_kernel_addressing():
                         assert torch.equal(flat[off:off + 16], w[16 * nb + r, k:k + 16])
     f8 = sops.fp8_stream_shuffle(w.view(torch.float8_e4m3fn), 224)
     assert f8.dtype == torch.float8_e4m3fn and torch.equal(f8.view(torch.uint8), sh)
+
+
+def test_fp8_rows_shuffle_layout_is_the_kernels_lds_image():
+    """ops.serving.fp8_rows_shuffle (fp8_rows_gemm(..., wimg=True)): per 128-row tile and K-step the
+    1 KiB DMA piece p holds, at lane * 16, row 8 p + lane // 8's chunk (lane % 8) ^ f8_swz(row % 16) --
+    what the kernel's row-major DMA writes to LDS (csrc/fp8_gemm.hip fp8_rows_gemm_kernel)."""
+    N, K = 256, 384
+    w = torch.randint(0, 256, (N, K), dtype=torch.uint8)
+    img = sops.fp8_rows_shuffle(w).flatten()
+    swz = lambda r: ((r >> 1) & 1) | (((r >> 3) & 1) << 2)  # noqa: E731
+    ks = K // 128
+    for nb in range(N // 128):
+        for t in range(ks):
+            for piece in range(16):
+                for lane in range(0, 64, 5):
+                    row, off = 8 * piece + (lane >> 3), (nb * ks + t) * 16384 + piece * 1024 + lane * 16
+                    ch = (lane & 7) ^ swz(row & 15)
+                    assert torch.equal(img[off:off + 16], w[nb * 128 + row, t * 128 + ch * 16:t * 128 + ch * 16 + 16])

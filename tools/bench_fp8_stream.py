@@ -15,7 +15,7 @@ import torch  # noqa: E402
 
 from dstack_amd.ops import _ext, gemm_tuning  # noqa: E402
 from dstack_amd.ops import reference as ref  # noqa: E402
-from dstack_amd.ops.serving import fp8_stream_shuffle  # noqa: E402
+from dstack_amd.ops.serving import fp8_rows_shuffle, fp8_stream_shuffle  # noqa: E402
 
 SHAPES = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672)}
 if os.getenv("MODEL") == "8b":  # Llama-3-8B projections
@@ -67,7 +67,11 @@ def main():
                             cands[f"stream_sh2d3_r{rw}_s{sp}"] = (
                                 lambda sp=sp, key=(2, g): C.fp8_stream_gemm(xq, xs, wsh[key], ws, 32, sp, 2, 3))
             if C.fp8_rows_gemm_supported(M, N, K, 64, 1):
+                wimg = fp8_rows_shuffle(wq)
                 cands["rows_bm64"] = lambda: C.fp8_rows_gemm(xq, xs, wq, ws, 64, 1)
+                cands["rows_img_bm64"] = lambda: C.fp8_rows_gemm(xq, xs, wimg, ws, 64, 1, None, None, True)
+                if C.fp8_rows_gemm_supported(M, N, K, 128, 1):
+                    cands["rows_img_bm128"] = lambda: C.fp8_rows_gemm(xq, xs, wimg, ws, 128, 1, None, None, True)
             out = {"shape": name, "M": M, "N": N, "K": K}
             for k, fn in cands.items():
                 err = ((fn().float() - ref_y).norm() / ref_y.norm()).item()
@@ -78,6 +82,7 @@ def main():
                 out[k + "_us"] = round(t, 2)
                 out[k + "_tb_s"] = round(N * K / t / 1e6, 3)
             best = min((v, k) for k, v in out.items() if k.endswith("_us") and k.startswith("stream"))
+            wimg = None
             out["best_stream"] = best[1][:-3]
             out["speedup_vs_lib"] = round(out["lib_us"] / best[0], 3)
             print(json.dumps(out), flush=True)
