@@ -23,6 +23,7 @@ MI355X-first layout (contrast: the reference runs vLLM/TGI containers for servic
 from __future__ import annotations
 
 import json
+import logging
 import math
 import os
 import zlib
@@ -36,6 +37,8 @@ from dstack_amd.models.llama import CONFIGS, LlamaConfig
 from dstack_amd.ops import _ext
 from dstack_amd.ops import reference as ref
 from dstack_amd.ops import serving as sops
+
+logger = logging.getLogger(__name__)
 
 
 class Fp8Weight:
@@ -419,11 +422,29 @@ class ServingLlama:
                 else:
                     q8, sc = ref.quant_fp8_rows(w)
                     q = q8.view(torch.uint8)
-                L[k] = Fp8Weight(q, sc, self._stream_copy(k, q))
+                L[k] = Fp8Weight(q, sc)
                 del w
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
+        self._add_stream_copies()
         return self
+
+    def _add_stream_copies(self, reserve_bytes: int = 32 << 30):
+        """The pre-shuffled second copies of the weights the streaming decode GEMM takes
+        (``_stream_cfg``), when they fit with ``reserve_bytes`` of HBM left for the KV cache and
+        workspaces; otherwise none (logged) and those GEMMs stay on hipBLASLt."""
+        todo = [(L, k) for L in self.layers for k in ("wgu", "wdown")
+                if isinstance(L.get(k), Fp8Weight) and L[k].qs is None and self._stream_cfg(*L[k].q.shape)]
+        if not todo:
+            return
+        need = sum(L[k].q.numel() for L, k in todo)
+        free, _ = torch.cuda.mem_get_info(self.device)
+        if free - need < reserve_bytes:
+            logger.warning("fp8 streaming decode GEMM off: its weight copies (%.1f GB) would leave %.1f GB of HBM",
+                           need / 1e9, (free - need) / 1e9)
+            return
+        for L, k in todo:
+            L[k].qs = self._stream_copy(k, L[k].q)
 
     def _stream_cfg(self, N: int, K: int) -> tuple[int, int] | None:
         """(weight rows per wave, K split) the weight-streaming decode GEMM runs an [N, K] fp8 weight

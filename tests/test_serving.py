@@ -732,9 +732,13 @@ def test_gpu_fp8_stream_gemm_in_the_engine(gpu, monkeypatch):
     slots = torch.arange(n, dtype=torch.int32, device=gpu)
     a = m.prefill(prompt, pos, slots, [0], [n]).float()
     m._stream_cfg = lambda N, K: (32, 1)
+    m._add_stream_copies(reserve_bytes=1 << 62)  # no room left: no copies, hipBLASLt stays
+    assert all(L[k].qs is None for L in m.layers for k in m.FP8_KEYS)
+    m._add_stream_copies(reserve_bytes=0)
     for L in m.layers:
         for k in ("wgu", "wdown"):
-            L[k].qs = fp8_stream_shuffle(L[k].q, 16 if m.fp8_stream_layout == 1 else 256)
+            group = 16 if m.fp8_stream_layout == 1 else 256
+            assert torch.equal(L[k].qs.view(torch.uint8), fp8_stream_shuffle(L[k].q, group).view(torch.uint8))
     C = _ext.require()
     calls, orig = [], C.fp8_stream_gemm
     monkeypatch.setattr(C, "fp8_stream_gemm", lambda *a_, **k_: calls.append(a_[0].shape) or orig(*a_, **k_))
