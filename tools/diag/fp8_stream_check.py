@@ -1,4 +1,4 @@
-"""Where a weight-streaming fp8 GEMM result goes wrong: for each (rows, N, K, split, rw, shuffled) case
+"""Where a weight-streaming fp8 GEMM result goes wrong: for each (rows, N, K, split, rw, shuffled 0|1|2) case
 prints the relative error, the count of non-finite outputs and the first bad rows / column blocks.
 CASES="200,256,2048,2,64,0;..." python tools/diag/fp8_stream_check.py"""
 import os
@@ -22,8 +22,8 @@ for case in cases.split(";"):
     xq, xs = ref.quant_fp8_rows(x)
     wq, ws = ref.quant_fp8_rows(w)
     want = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
-    wk = fp8_stream_shuffle(wq) if sh else wq
-    y = C.fp8_stream_gemm(xq.view(torch.uint8), xs, wk.view(torch.uint8), ws, rw, S, bool(sh)).float()
+    wk = fp8_stream_shuffle(wq, {1: 16, 2: 224 if rw == 28 else 256}[sh]) if sh else wq
+    y = C.fp8_stream_gemm(xq.view(torch.uint8), xs, wk.view(torch.uint8), ws, rw, S, sh).float()
     torch.cuda.synchronize()
     bad = ~torch.isfinite(y)
     d = (y - want).abs()
