@@ -119,13 +119,15 @@ __device__ __forceinline__ float silu_q(float g) { return g / (1.f + __expf(-g))
 // NIT > 0: the row's products stay in registers (packed bf16, exact: they are bf16-rounded) between
 // the absmax pass and the quantization pass, so gu (and cs) are read once instead of twice; NIT is
 // the number of 2048-column steps, F <= 2048 * NIT.  NIT = 0: two passes over gu (any F).
-template <bool SCALED, int NIT = 0>
-__global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __restrict__ gu, long ldg,
+// BS: threads per row (256, or 1024 for decode-sized M: one workgroup per row leaves a 256-row batch
+// with 4 waves per CU, too few loads in flight to stream the row at HBM rate)
+template <bool SCALED, int NIT = 0, int BS = 256>
+__global__ __launch_bounds__(BS) void swiglu_quant_rows_kernel(const bf16_t* __restrict__ gu, long ldg,
                                                                 unsigned char* __restrict__ q, long ldq,
                                                                 float* __restrict__ s, int F,
                                                                 const float* __restrict__ rs,
                                                                 const float* __restrict__ cs) {
-  __shared__ float red[4];
+  __shared__ float red[BS / 64];
   const int row = blockIdx.x, tid = threadIdx.x;
   const bf16_t* gr = gu + (long)row * ldg;
   const float r = SCALED ? rs[row] : 1.f;
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __
   if constexpr (NIT > 0) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int k = (tid + it * 256) * 8;
+      const int k = (tid + it * BS) * 8;
       if (k < F) {
         float a[8];
         prod8(k, a);
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __
       }
     }
   } else {
-    for (int k = tid * 8; k < F; k += 256 * 8) {
+    for (int k = tid * 8; k < F; k += BS * 8) {
       float a[8];
       prod8(k, a);
 #pragma unroll
@@ -172,7 +174,9 @@ __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __
   amax = wave_max(amax);
   if ((tid & 63) == 0) red[tid >> 6] = amax;
   __syncthreads();
-  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  amax = red[0];
+#pragma unroll
+  for (int i = 1; i < BS / 64; ++i) amax = fmaxf(amax, red[i]);
   const float scale = fmaxf(amax, 1e-12f) / E4M3_MAX;
   const float inv = 1.f / scale;
   if (tid == 0) s[row] = scale;
@@ -181,7 +185,7 @@ __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __
   if constexpr (NIT > 0) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int k = (tid + it * 256) * 8;
+      const int k = (tid + it * BS) * 8;
       if (k < F) {
         float a[8];
         unpack8(pk[it], a);
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(256) void swiglu_quant_rows_kernel(const bf16_t* __
       }
     }
   } else {
-    for (int k = tid * 8; k < F; k += 256 * 8) {
+    for (int k = tid * 8; k < F; k += BS * 8) {
       float a[8];
       prod8(k, a);
       const unsigned int w0 = f32x4_to_fp8(a[0] * inv, a[1] * inv, a[2] * inv, a[3] * inv);
@@ -383,17 +387,20 @@ extern "C" hipError_t dsa_quant_fp8_rows(const void* x, long ldx, void* q, long 
 extern "C" hipError_t dsa_swiglu_quant_fp8_rows(const void* gu, long ldg, void* q, long ldq, float* s, int M, int F,
                                                 const float* rs, const float* cs, hipStream_t st) {
   if (F <= 0 || F % 8 || M <= 0 || ((rs == nullptr) != (cs == nullptr))) return hipErrorInvalidValue;
-  // products held in registers for F <= 32768 (Llama-3-70B: F = 28672 -> 14 steps of 2048 columns)
-  const int nit = (F + 2047) / 2048;
-#define DSA_SWQ(SC, N)                                                                                     \
-  swiglu_quant_rows_kernel<SC, N><<<M, 256, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F, \
-                                                     SC ? rs : nullptr, SC ? cs : nullptr)
-#define DSA_SWQ_N(SC)                    \
-  if (nit <= 2) DSA_SWQ(SC, 2);          \
-  else if (nit <= 4) DSA_SWQ(SC, 4);     \
-  else if (nit <= 8) DSA_SWQ(SC, 8);     \
-  else if (nit <= 16) DSA_SWQ(SC, 16);   \
-  else DSA_SWQ(SC, 0);
+  // products held in registers for F <= 32768 (Llama-3-70B: F = 28672 -> 14 steps of 2048 columns);
+  // decode-sized batches (M <= 512) run 1024 threads per row (4 steps of 8192 columns)
+  const int nit = (F + 2047) / 2048, nit4 = (F + 8191) / 8192;
+#define DSA_SWQ(SC, N, BS)                                                                        \
+  swiglu_quant_rows_kernel<SC, N, BS><<<M, BS, 0, st>>>((const bf16_t*)gu, ldg, (unsigned char*)q, ldq, s, F, \
+                                                        SC ? rs : nullptr, SC ? cs : nullptr)
+#define DSA_SWQ_N(SC)                                  \
+  if (M <= 512 && nit4 <= 2) DSA_SWQ(SC, 2, 1024);     \
+  else if (M <= 512 && nit4 <= 4) DSA_SWQ(SC, 4, 1024); \
+  else if (nit <= 2) DSA_SWQ(SC, 2, 256);              \
+  else if (nit <= 4) DSA_SWQ(SC, 4, 256);              \
+  else if (nit <= 8) DSA_SWQ(SC, 8, 256);              \
+  else if (nit <= 16) DSA_SWQ(SC, 16, 256);            \
+  else DSA_SWQ(SC, 0, 256);
   if (rs) {
     DSA_SWQ_N(true)
   } else {

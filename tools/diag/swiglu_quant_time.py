@@ -1,0 +1,29 @@
+"""SwiGLU + per-row e4m3 quantization of a decode step's gate/up product (Llama-3-70B: 256 rows x
+2 x 28672), timed with events, scaled and unscaled forms; one JSON line."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+from dstack_amd.ops import _ext  # noqa: E402
+
+C = _ext.require()
+M, F = int(os.getenv("ROWS", "256")), int(os.getenv("F", "28672"))
+gu = torch.randn(M, 2 * F, device="cuda", dtype=torch.bfloat16)
+rs, cs = torch.rand(M, device="cuda") + 0.5, torch.rand(2 * F, device="cuda") + 0.5
+out = {"M": M, "F": F}
+for name, fn in (("unscaled", lambda: C.swiglu_quant_fp8_rows(gu)), ("scaled", lambda: C.swiglu_quant_fp8_rows(gu, rs, cs))):
+    for _ in range(10):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(200):
+        fn()
+    b.record()
+    b.synchronize()
+    us = a.elapsed_time(b) / 200 * 1e3
+    out[name + "_us"] = round(us, 2)
+    out[name + "_tb_s"] = round((M * 2 * F * 2 + M * F) / us / 1e6, 2)
+print(json.dumps(out), flush=True)
