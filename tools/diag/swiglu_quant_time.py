@@ -1,5 +1,6 @@
 """SwiGLU + per-row e4m3 quantization of a decode step's gate/up product (Llama-3-70B: 256 rows x
-2 x 28672), timed with events, scaled and unscaled forms; one JSON line."""
+2 x 28672), scaled and unscaled forms, and the fused add + RMSNorm -> e4m3 (256 x 8192), timed with
+events; one JSON line."""
 import json
 import os
 import sys
@@ -14,7 +15,11 @@ M, F = int(os.getenv("ROWS", "256")), int(os.getenv("F", "28672"))
 gu = torch.randn(M, 2 * F, device="cuda", dtype=torch.bfloat16)
 rs, cs = torch.rand(M, device="cuda") + 0.5, torch.rand(2 * F, device="cuda") + 0.5
 out = {"M": M, "F": F}
-for name, fn in (("unscaled", lambda: C.swiglu_quant_fp8_rows(gu)), ("scaled", lambda: C.swiglu_quant_fp8_rows(gu, rs, cs))):
+D = int(os.getenv("D", "8192"))
+x, dl = torch.randn(M, D, device="cuda", dtype=torch.bfloat16), torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+wn = torch.rand(D, device="cuda", dtype=torch.bfloat16) + 0.5
+for name, fn in (("unscaled", lambda: C.swiglu_quant_fp8_rows(gu)), ("scaled", lambda: C.swiglu_quant_fp8_rows(gu, rs, cs)),
+                 ("add_rmsnorm_fp8", lambda: C.rms_norm_fp8(x, dl, wn, 1e-5))):
     for _ in range(10):
         fn()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -25,5 +30,6 @@ for name, fn in (("unscaled", lambda: C.swiglu_quant_fp8_rows(gu)), ("scaled", l
     b.synchronize()
     us = a.elapsed_time(b) / 200 * 1e3
     out[name + "_us"] = round(us, 2)
-    out[name + "_tb_s"] = round((M * 2 * F * 2 + M * F) / us / 1e6, 2)
+    nbytes = M * D * 2 * 3 + M * D if name == "add_rmsnorm_fp8" else M * 2 * F * 2 + M * F
+    out[name + "_tb_s"] = round(nbytes / us / 1e6, 2)
 print(json.dumps(out), flush=True)
