@@ -19,7 +19,7 @@ D = int(os.getenv("D", "8192"))
 x, dl = torch.randn(M, D, device="cuda", dtype=torch.bfloat16), torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
 wn = torch.rand(D, device="cuda", dtype=torch.bfloat16) + 0.5
 for name, fn in (("unscaled", lambda: C.swiglu_quant_fp8_rows(gu)), ("scaled", lambda: C.swiglu_quant_fp8_rows(gu, rs, cs)),
-                 ("add_rmsnorm_fp8", lambda: C.rms_norm_fp8(x, dl, wn, 1e-5))):
+                 ("add_rmsnorm_fp8", lambda: C.rms_norm_fp8(x, dl, wn, 1e-5)), ("quant_rows", lambda: C.quant_fp8_rows(x))):
     for _ in range(10):
         fn()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -30,6 +30,6 @@ for name, fn in (("unscaled", lambda: C.swiglu_quant_fp8_rows(gu)), ("scaled", l
     b.synchronize()
     us = a.elapsed_time(b) / 200 * 1e3
     out[name + "_us"] = round(us, 2)
-    nbytes = M * D * 2 * 3 + M * D if name == "add_rmsnorm_fp8" else M * 2 * F * 2 + M * F
+    nbytes = {"add_rmsnorm_fp8": M * D * 2 * 3 + M * D, "quant_rows": M * D * 3}.get(name, M * 2 * F * 2 + M * F)
     out[name + "_tb_s"] = round(nbytes / us / 1e6, 2)
 print(json.dumps(out), flush=True)
